@@ -1,0 +1,252 @@
+/*
+ * lbt_dfxp.h -- C-ABI of the MI355X (gfx950) dynamic-fixed-point (DFXP) training hot path.
+ *
+ * Every entry point is stream-ordered (the last argument is a hipStream_t passed as void*),
+ * takes caller-owned DEVICE pointers, allocates nothing and never synchronises, so a caller
+ * may capture any sequence of calls into a HIP graph. Return value: 0 on success, otherwise
+ * a hipError_t code or one of the LBT_E* argument errors below.
+ *
+ * The reference (freudh/lbt) is TensorFlow-1 Python; it has no native FFI. Each entry point
+ * replaces the TF op sequence named in its comment (file:line in the reference tree), i.e.
+ * it is what a ctypes / cffi binding of the reference's quantiser and layers would bind
+ * (see INTEGRATION.md).
+ *
+ * Conventions
+ *   - Activations / gradients: NHWC, fp32 or integer codes. Weights: HWIO fp32 master copy.
+ *   - A DFXP tensor is (integer codes q, shared exponent e): value = q * 2^-e with
+ *     e = bits - I - 1, I = "integer_bits" held per quantiser slot in device memory.
+ *   - Quantiser slots live in three device arrays owned by the caller:
+ *       exps[slot]      int32  integer bits I (dynamic_fixed_point.py:27,34 "integer_bits")
+ *       counts[(slot*LBT_NSHARD + shard)*2 + {0,1}]  int32
+ *                              #(x*m >= L or x*m < -L), #(x*m >= L/2 or x*m < -L/2)
+ *                              (the numerators of overflow_rate, dynamic_fixed_point.py:48-67)
+ *       step[0]         uint64 training-step counter (noise counter)
+ *   - Stochastic-rounding noise: Philox4x32-10, counter (i>>2, qid, step_lo, step_hi),
+ *     key (seed_lo, seed_hi), u = (r[i&3] >> 8) * 2^-24, i = element index modulo
+ *     prod(shape[1:]) -- the reference's tf.random_uniform(X.shape[1:]) broadcast over dim 0
+ *     (dynamic_fixed_point.py:36).
+ */
+#ifndef LBT_DFXP_H
+#define LBT_DFXP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBT_OK 0
+#define LBT_EINVAL 1001  /* unsupported shape / argument combination */
+
+/* Reduction outputs (overflow counters, per-channel integer sums) are SHARDED: a kernel adds
+ * its per-workgroup partial into shard (workgroup id % LBT_NSHARD) so that thousands of
+ * workgroups never serialise on one address; consumers sum the shards.                  */
+#define LBT_NSHARD 32
+
+/* Output encodings of a quantiser. */
+enum {
+  LBT_OUT_I8 = 0,     /* signed codes, bits <= 8                                     */
+  LBT_OUT_U8OFF = 1,  /* unsigned 9-bit codes q in [0,255] stored as int8 (q - 128)  */
+  LBT_OUT_I16 = 2,    /* signed codes, bits <= 16                                    */
+  LBT_OUT_F32 = 3     /* dequantised fake-quant value q * 2^-e (the reference's STE output) */
+};
+
+/* One quantiser: where its exponent / counters live and how it rounds. */
+typedef struct lbt_qdesc {
+  const int32_t* exps;   /* device [slots]                                   */
+  int32_t* counts;       /* device [slots][LBT_NSHARD][2]; NULL = no stats   */
+  const uint64_t* step;  /* device [1]                                       */
+  uint64_t seed;         /* noise key                                        */
+  uint32_t qid;          /* noise stream id (crc32 of the range variable)    */
+  int32_t slot;
+  int32_t bits;          /* total bits incl. sign, 2..16                     */
+  int32_t stochastic;    /* 1: floor(x*m + u)  0: round-half-even(x*m)       */
+} lbt_qdesc;
+
+/* Convolution geometry, TF padding already resolved into (top,bottom,left,right). */
+typedef struct lbt_conv_desc {
+  int32_t N, H, W, Cin, Cout, KH, KW, SH, SW, PT, PB, PL, PR, Ho, Wo;
+} lbt_conv_desc;
+
+/* ---------------------------------------------------------------- quantiser ---------- */
+
+/* weight_quantization + the overflow statistics of update_range
+ * (dynamic_fixed_point.py:4-45 / :48-67).  x is [rows, inner] fp32 (inner = prod(shape[1:])).
+ * out is written in `out_kind` encoding, same element order as x.  If chsum != NULL the
+ * per-channel integer sums S1[c] = sum q, S2[c] = sum q^2 over all elements with channel
+ * c = index % C are ADDED to the sharded int64 buffer chsum[LBT_NSHARD][2C] (S1 at [0,C),
+ * S2 at [C,2C) of a shard).  All "chsum"/"sums" buffers below use that sharded layout.   */
+int lbt_dfxp_quantize(const float* x, void* out, int out_kind, int64_t rows, int64_t inner,
+                      lbt_qdesc q, int64_t* chsum, int32_t C, void* stream);
+
+/* update_range for every slot (dynamic_fixed_point.py:70-94):
+ *   c = sum over shards; r1 = c1/n[s], r2 = c2/n[s] (fp32), delta = r1 > t ? +1 : (r2 <= t ? -1 : 0)
+ *   I <- clamp(I + delta, bits-31, bits-1); counts zeroed; step[0] += 1.
+ * Slots with nelem <= 0 (not fed this step) are left untouched.                          */
+int lbt_dfxp_range_update(int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
+                          const float* nelem, int32_t nslots, uint64_t* step, void* stream);
+
+/* Quantise a conv / dense weight (HWIO fp32, noise over shape[1:] = [KW,Cin,Cout]) into the
+ * layouts the GEMM kernels consume (any output may be NULL):
+ *   w_hwio  int8 [KH][KW][Cin][Cout]       (generic kernels)
+ *   wf      int8 [Cout][ksf*16]            fwd B operand, k = (tap, ci), zero padded to ksf*16
+ *   wd      int8 [Cin][ksd*16]             dgrad B operand, k = (tap, co)
+ *   colsum  int32 [Cout]  sum_k w[k][co]   (offset-input correction)                      */
+int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, int32_t Cin, int32_t Cout,
+                             lbt_qdesc q, int8_t* w_hwio, int8_t* wf, int32_t ksf, int8_t* wd,
+                             int32_t ksd, int32_t* colsum, void* stream);
+
+/* ---------------------------------------------------------------- integer GEMMs ------ */
+
+/* Conv2d_q forward y = conv(Xq, Wq) (dynamic_fixed_point.py:287-291, tf.nn.conv2d) as an
+ * int8 implicit GEMM on v_mfma_i32_16x16x64_i8.  xq: NHWC int8 codes (x_u8off: unsigned
+ * 9-bit offset encoding, else signed 8-bit); wf/wcolsum from lbt_dfxp_quantize_weight.
+ * Epilogue: acc -> fp32 * 2^-(ex+ew); written to y (fp32 NHWC) if y != NULL and/or
+ * quantised with qout into yq (int8 NHWC) with per-channel sums into ychsum.
+ * Requires Cin % 16 == 0 and Cout % 16 == 0.                                               */
+int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf,
+                    const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw,
+                    float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream);
+
+/* Conv2d_q backward dX = tf.gradients(y, X, gradq) (dynamic_fixed_point.py:305): int8
+ * implicit GEMM over (tap, co) of the quantised grad.  dx (fp32 NHWC [N,H,W,Cin]) =
+ * acc * 2^-(eg+ew) (+ add_src[e] if add_src != NULL).  Requires Cin%16 == 0, Cout%16 == 0. */
+int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                      lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
+
+/* Conv2d_q backward dW = tf.gradients(y, W, gradq) (dynamic_fixed_point.py:302), pass 1:
+ * int32 partial sums over `nsplit` pixel ranges into slab [nsplit][KH*KW][Cin][Cout]
+ * (x_u8off: xq in the unsigned-9-bit offset encoding; the offset is undone in pass 2).       */
+int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t* gq, lbt_conv_desc d,
+                      int32_t* slab, int32_t nsplit, void* stream);
+
+/* pass 2: dW = float(sum_split slab + 128*x_u8off*gcolsum[co]) * 2^-(ex+eg) + wd2 * W,
+ * written HWIO into dw (wd2 = 2*weight_decay as fp32, the "+ 2*wd*W" of :302).
+ * gcolsum is the sharded per-channel sum buffer [LBT_NSHARD][2*Cout] of the grad codes.   */
+int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_t K, int32_t Cout,
+                          int32_t x_u8off, const int64_t* gcolsum, lbt_qdesc qx, lbt_qdesc qg,
+                          const float* w, float wd2, float* dw, void* stream);
+
+/* Generic (any-shape) integer conv on the VALU, for signed 9-bit inputs and channel counts
+ * that are not multiples of 16 (conv1 3->16, Dense_q as a 1x1 conv).  x codes are int16 when
+ * x_i16 != 0, else int8; w is int8 HWIO; g is int8.                                        */
+int lbt_conv_fwd_generic(const void* xq, int32_t x_i16, const int8_t* w_hwio, lbt_conv_desc d,
+                         lbt_qdesc qx, lbt_qdesc qw, float* y, void* stream);
+int lbt_conv_dgrad_generic(const int8_t* gq, const int8_t* w_hwio, lbt_conv_desc d,
+                           lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
+int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
+                           int32_t* slab, int32_t nsplit, void* stream);
+
+/* ---------------------------------------------------------------- batch norm -------- */
+
+/* The statistics of one Normalization_q (dynamic_fixed_point.py:584-616): its input codes q
+ * (quantiser qn), the sharded integer sums S1 = sum q, S2 = sum q^2 per channel (chsum,
+ * [LBT_NSHARD][2C], produced by the quantiser or by the conv epilogue), n elements/channel.
+ * Moments (biased, as tf.nn.moments): mu = S1*s/n, var = S2*s^2/n - mu^2 in double,
+ * sigma = sqrtf((float)var + eps).  The first workgroup writes ms = [mu[C], sigma[C]] and,
+ * if run_mean != NULL, the running averages avg = momentum*avg + one_minus_momentum*x
+ * (:601-612).                                                                              */
+typedef struct lbt_bn_norm {
+  const int8_t* q; lbt_qdesc qn; const int64_t* chsum; int64_t n;
+  float eps, momentum, one_minus_momentum;
+  float* ms; float* run_mean; float* run_var;
+} lbt_bn_norm;
+
+/* One branch of the forward element chain:
+ *   v = xin[e]                          if nrm.q == NULL
+ *     = ((float)q*s - mu) / sigma       else                          (Normalization_q :616)
+ *   if qr.bits: R = Q(v, qr) -> rout; v = ((float)R*sr)*gb[c] + gb[C+c]  (Rescale_q :677-683)
+ * gb = [gamma_q[C], beta_q[C]] dequantised (lbt_dfxp_quantize with LBT_OUT_F32).           */
+typedef struct lbt_chain_branch {
+  lbt_bn_norm nrm; const float* xin;
+  lbt_qdesc qr; int8_t* rout; const float* gb;
+} lbt_chain_branch;
+
+/* Forward element chain over [rows, inner] (inner = H*W*C, channel = index % C):
+ *   v = b1 (+ b2 if has_b2) (+ res[e] if res) ; if relu: v = max(0, v)
+ *   (ResidualBlock_q :858-863: relu(y1 + y2))
+ *   y = v (fp32, if y != NULL); o1 = Q(v, qo1) and o2 = Q(v, qo2) in o*_kind if != NULL
+ *   (the next layers' input quantisers, e.g. Conv2d_q X at bits+1 in LBT_OUT_U8OFF).        */
+typedef struct lbt_chain_fwd {
+  lbt_chain_branch b1, b2; int32_t has_b2;
+  const float* res; int32_t relu;
+  float* y;
+  void* o1; int32_t o1_kind; lbt_qdesc qo1;
+  void* o2; int32_t o2_kind; lbt_qdesc qo2;
+  int64_t rows, inner; int32_t C;
+} lbt_chain_fwd;
+int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream);
+
+/* Backward pass A of one BN (Rescale_q.backward :686-691, then the first half of
+ * Normalization_q.backward :620-623) on the masked incoming gradient g':
+ *   if qrg.bits: G2 = Q(g', qrg); sums[0:C) += G2*R, sums[C:2C) += G2; d = ((float)G2*sg2)*gamma_q
+ *   else         d = g'
+ *   if qng.bits: G = Q(d, qng) -> gout (int8); sums[2C:3C) += G, sums[3C:4C) += G*qn_codes
+ *   else         dout = d (fp32)
+ * sums is sharded [LBT_NSHARD][4C].                                                         */
+typedef struct lbt_bwd_branch {
+  lbt_qdesc qrg; const int8_t* R; lbt_qdesc qr; const float* gb;
+  lbt_qdesc qng; const int8_t* qn_codes;
+  int8_t* gout; float* dout; int64_t* sums;
+} lbt_bwd_branch;
+
+/* g' = g * mask, mask = (y_mask[e] > 0) if y_mask (ReLU_q backward, TF _MaximumGrad), or the
+ * recomputed branch-1 Rescale_q output ((float)R*sr*gamma_q + beta_q > 0) if mask_from_r,
+ * else 1.  gmask_out = g' (the identity-shortcut gradient) if != NULL.  Both branches see
+ * the same g' (ResidualBlock_q.backward :865-869).                                         */
+typedef struct lbt_chain_bwd_a {
+  const float* g; const float* y_mask; int32_t mask_from_r;
+  float* gmask_out;
+  lbt_bwd_branch b1, b2; int32_t has_b2;
+  int64_t rows, inner; int32_t C;
+} lbt_chain_bwd_a;
+int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream);
+
+/* Pass B (the rest of Normalization_q.backward): with SG = sum G, SGQ = sum G*q from pass A,
+ *   mg = sg*SG/n, mgx = sg*(s*SGQ - mu*SG)/(n*sigma)   (double -> fp32)
+ *   dx = (((float)G*sg - mg) - xhat*mgx) / sigma,  xhat = ((float)q*s - mu)/sigma
+ * Outputs dx (fp32) if != NULL and/or gq = Q(dx, qo) (int8, the next Conv2d_q grad
+ * quantiser) with sharded per-channel sums of gq into gcolsum [LBT_NSHARD][2C].           */
+typedef struct lbt_chain_bwd_b {
+  const int8_t* G; lbt_qdesc qng; const int8_t* qn_codes; lbt_qdesc qn; const float* ms;
+  const int64_t* sums; int64_t n;
+  float* dx; int8_t* gq; lbt_qdesc qo; int64_t* gcolsum;
+  int64_t rows, inner; int32_t C;
+} lbt_chain_bwd_b;
+int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream);
+
+/* Rescale_q parameter gradients (:689-690) from pass-A sums:
+ * dgamma = (float)((double)sum(G2*R) * sg2*sr) + wd2*gamma,  dbeta = (float)((double)sum G2 * sg2). */
+int lbt_bn_param_grads(const int64_t* sums, int32_t C, lbt_qdesc qrg, lbt_qdesc qr,
+                       const float* gamma, float wd2, float* dgamma, float* dbeta, void* stream);
+
+/* ---------------------------------------------------------------- glue ---------------- */
+
+/* ReLU_q forward (:986, tf.maximum(0,x)) and backward (TF _MaximumGrad: g where x > 0). */
+int lbt_relu_fwd(const float* x, float* y, int64_t n, void* stream);
+int lbt_relu_bwd(const float* g, const float* x, float* dx, int64_t n, void* stream);
+/* elementwise a + b (ResidualBlock_q :862 / :869). */
+int lbt_add(const float* a, const float* b, float* y, int64_t n, void* stream);
+/* AvgPool_q over the whole HxW map (:1017): y[n,c] = (sequential fp32 sum) * (1/(H*W)). */
+int lbt_avgpool_fwd(const float* x, float* y, int32_t N, int32_t HW, int32_t C, void* stream);
+int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW, int32_t C, void* stream);
+/* mean sparse softmax cross-entropy (models.py:30-32) -> loss[0] (fp32, device), dz = d loss / d z. */
+int lbt_softmax_xent(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss,
+                     float* dz, void* stream);
+/* MomentumOptimizer.apply_gradients (trainer.py:81-82): a = mu*a + g*gscale; w -= lr*a. */
+int lbt_sgd_momentum(float* w, float* a, const float* g, int64_t n, float lr, float mu,
+                     float gscale, void* stream);
+
+/* Conv2d_q / Dense_q bias (use_bias=True, dynamic_fixed_point.py:198-201,293-296,390-393):
+ * y[e] += bq[e % C] (bq dequantised by lbt_dfxp_quantize), and db[c] = sum_e gq * 2^-eg from
+ * the grad quantiser's sharded per-channel sums chsum [LBT_NSHARD][2C] (:209, :459).       */
+int lbt_bias_add(float* y, const float* bq, int64_t n, int32_t C, void* stream);
+int lbt_bias_grad(const int64_t* chsum, int32_t C, lbt_qdesc qg, float* db, void* stream);
+
+/* ABI version for the Python loader. */
+int lbt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LBT_DFXP_H */

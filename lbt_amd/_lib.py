@@ -1,0 +1,142 @@
+"""ctypes binding of ``include/lbt_dfxp.h`` -- the C-ABI of the gfx950 DFXP kernels.
+
+This is the only place Python touches the native library. There is no CPU fallback: if
+``liblbt_dfxp.so`` is missing or fails to load, every op raises. ``torch`` is imported first
+so that the HIP runtime the library binds to (``libamdhip64.so.7``) is the one PyTorch-ROCm
+already loaded -- device pointers and streams are then shared with torch.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime before the kernels library)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblbt_dfxp.so")
+
+NSHARD = 32
+OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
+ABI_VERSION = 1
+
+c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
+    ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
+
+
+class QDesc(ctypes.Structure):
+    _fields_ = [("exps", c_void_p), ("counts", c_void_p), ("step", c_void_p), ("seed", c_uint64),
+                ("qid", c_uint32), ("slot", c_int32), ("bits", c_int32), ("stochastic", c_int32)]
+
+
+NO_Q = QDesc()  # bits == 0: inactive quantiser
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("N", "H", "W", "Cin", "Cout", "KH", "KW", "SH", "SW",
+                                       "PT", "PB", "PL", "PR", "Ho", "Wo")]
+
+
+class BnNorm(ctypes.Structure):
+    _fields_ = [("q", c_void_p), ("qn", QDesc), ("chsum", c_void_p), ("n", c_int64),
+                ("eps", c_float), ("momentum", c_float), ("one_minus_momentum", c_float),
+                ("ms", c_void_p), ("run_mean", c_void_p), ("run_var", c_void_p)]
+
+
+class ChainBranch(ctypes.Structure):
+    _fields_ = [("nrm", BnNorm), ("xin", c_void_p), ("qr", QDesc), ("rout", c_void_p), ("gb", c_void_p)]
+
+
+class ChainFwd(ctypes.Structure):
+    _fields_ = [("b1", ChainBranch), ("b2", ChainBranch), ("has_b2", c_int32),
+                ("res", c_void_p), ("relu", c_int32), ("y", c_void_p),
+                ("o1", c_void_p), ("o1_kind", c_int32), ("qo1", QDesc),
+                ("o2", c_void_p), ("o2_kind", c_int32), ("qo2", QDesc),
+                ("rows", c_int64), ("inner", c_int64), ("C", c_int32)]
+
+
+class BwdBranch(ctypes.Structure):
+    _fields_ = [("qrg", QDesc), ("R", c_void_p), ("qr", QDesc), ("gb", c_void_p),
+                ("qng", QDesc), ("qn_codes", c_void_p), ("gout", c_void_p), ("dout", c_void_p),
+                ("sums", c_void_p)]
+
+
+class ChainBwdA(ctypes.Structure):
+    _fields_ = [("g", c_void_p), ("y_mask", c_void_p), ("mask_from_r", c_int32), ("gmask_out", c_void_p),
+                ("b1", BwdBranch), ("b2", BwdBranch), ("has_b2", c_int32),
+                ("rows", c_int64), ("inner", c_int64), ("C", c_int32)]
+
+
+class ChainBwdB(ctypes.Structure):
+    _fields_ = [("G", c_void_p), ("qng", QDesc), ("qn_codes", c_void_p), ("qn", QDesc), ("ms", c_void_p),
+                ("sums", c_void_p), ("n", c_int64),
+                ("dx", c_void_p), ("gq", c_void_p), ("qo", QDesc), ("gcolsum", c_void_p),
+                ("rows", c_int64), ("inner", c_int64), ("C", c_int32)]
+
+
+_P = c_void_p
+_SIGS = {
+    "lbt_abi_version": [],
+    "lbt_dfxp_quantize": [_P, _P, c_int32, c_int64, c_int64, QDesc, _P, c_int32, _P],
+    "lbt_dfxp_range_update": [_P, _P, _P, _P, _P, c_int32, _P, _P],
+    "lbt_dfxp_quantize_weight": [_P, c_int32, c_int32, c_int32, c_int32, QDesc, _P, _P, c_int32, _P, c_int32,
+                                 _P, _P],
+    "lbt_conv_fwd_i8": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
+    "lbt_conv_dgrad_i8": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
+    "lbt_conv_wgrad_i8": [_P, c_int32, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_wgrad_reduce": [_P, c_int32, c_int32, c_int32, c_int32, _P, QDesc, QDesc, _P, c_float, _P, _P],
+    "lbt_conv_fwd_generic": [_P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
+    "lbt_conv_dgrad_generic": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, _P],
+    "lbt_conv_wgrad_generic": [_P, c_int32, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_bn_chain_fwd": [_P, _P],
+    "lbt_bn_chain_bwd_a": [_P, _P],
+    "lbt_bn_chain_bwd_b": [_P, _P],
+    "lbt_bn_param_grads": [_P, c_int32, QDesc, QDesc, _P, c_float, _P, _P, _P],
+    "lbt_relu_fwd": [_P, _P, c_int64, _P],
+    "lbt_relu_bwd": [_P, _P, _P, c_int64, _P],
+    "lbt_add": [_P, _P, _P, c_int64, _P],
+    "lbt_avgpool_fwd": [_P, _P, c_int32, c_int32, c_int32, _P],
+    "lbt_avgpool_bwd": [_P, _P, c_int32, c_int32, c_int32, _P],
+    "lbt_softmax_xent": [_P, _P, c_int32, c_int32, _P, _P, _P],
+    "lbt_sgd_momentum": [_P, _P, _P, c_int64, c_float, c_float, c_float, _P],
+    "lbt_bias_add": [_P, _P, c_int64, c_int32, _P],
+    "lbt_bias_grad": [_P, c_int32, QDesc, _P, _P],
+}
+EXPORTED = sorted(_SIGS)
+
+_lib = None
+
+
+class LbtError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load (once) and type the native library. Raises if it is missing -- no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError("lbt_amd native library not built: %s (run `python -m lbt_amd._build`)" % path)
+    lib = ctypes.CDLL(path)
+    for name, argtypes in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int32
+    if lib.lbt_abi_version() != ABI_VERSION:
+        raise ImportError("lbt_amd ABI mismatch: library %d, bindings %d" % (lib.lbt_abi_version(), ABI_VERSION))
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke a C-ABI entry point; raise LbtError on a non-zero status."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise LbtError("%s failed with status %d%s" % (name, rc, " (LBT_EINVAL)" if rc == 1001 else ""))
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -1,0 +1,471 @@
+// bn.hip -- BatchNorm_q = Normalization_q + Rescale_q (dynamic_fixed_point.py:539-743) and the
+// ReLU / residual glue around it, as element chains fused with the neighbouring DFXP quantisers.
+//
+// All three kernels are HBM-bound element passes over [rows, inner] (inner = H*W*C): each
+// thread owns 4 consecutive elements of one row (one channel quad, one Philox call per
+// quantiser, reused over `rpt` rows of the batch since the noise is shared over dim 0) and
+// reads / writes them with 4- or 16-byte vector accesses.  Per-channel statistics are exact
+// integer sums (moments of the quantised input; G*R, G, G*q for the backward), reduced
+// wave -> LDS -> one atomic per workgroup into a shard, so they are deterministic and
+// independent of the launch geometry.
+#include "dfxp_device.h"
+
+using namespace lbt;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+LBT_DEV void load4_i8(const int8_t* p, int64_t i, int v[4]) {
+  const char4 c = *reinterpret_cast<const char4*>(p + i);
+  v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
+}
+LBT_DEV void load4_f32(const float* p, int64_t i, float v[4]) {
+  const float4 c = *reinterpret_cast<const float4*>(p + i);
+  v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
+}
+LBT_DEV void store4_i8(int8_t* p, int64_t i, const int v[4], int off) {
+  char4 c;
+  c.x = (int8_t)(v[0] - off); c.y = (int8_t)(v[1] - off); c.z = (int8_t)(v[2] - off); c.w = (int8_t)(v[3] - off);
+  *reinterpret_cast<char4*>(p + i) = c;
+}
+LBT_DEV void store4_f32(float* p, int64_t i, const float v[4]) {
+  *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+}
+LBT_DEV void store4_code(void* out, int kind, int64_t i, const int c[4], float inv_m) {
+  if (kind == LBT_OUT_I8) {
+    store4_i8((int8_t*)out, i, c, 0);
+  } else if (kind == LBT_OUT_U8OFF) {
+    int t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = c[k] < 0 ? 0 : c[k];
+    store4_i8((int8_t*)out, i, t, 128);
+  } else if (kind == LBT_OUT_I16) {
+    short4 s; s.x = (short)c[0]; s.y = (short)c[1]; s.z = (short)c[2]; s.w = (short)c[3];
+    *reinterpret_cast<short4*>((int16_t*)out + i) = s;
+  } else {
+    float f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = (float)c[k] * inv_m;
+    store4_f32((float*)out, i, f);
+  }
+}
+
+LBT_DEV Noise4 noise_for(const lbt_qdesc& q, const QState& s, int64_t g) {
+  Noise4 n = {{0.f, 0.f, 0.f, 0.f}};
+  if (s.active && q.stochastic) n = noise4((uint64_t)g, q.qid, s.step, q.seed);
+  return n;
+}
+
+// Sum a sharded [LBT_NSHARD][stride] int64 buffer's first n entries into LDS tmp[n].
+LBT_DEV void sum_shards(const int64_t* src, int n, int stride, long long* tmp) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    long long s = 0;
+    for (int k = 0; k < LBT_NSHARD; ++k) s += src[(int64_t)k * stride + i];
+    tmp[i] = s;
+  }
+}
+
+// Normalization_q moments from the exact integer sums -> mu / sigma in LDS (and ms / running
+// stats from the first workgroup).
+LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long long* tmp) {
+  sum_shards(b.chsum, 2 * C, 2 * C, tmp);
+  __syncthreads();
+  const double s = ldexp(1.0, -frac_exp(b.qn));
+  const bool writer = blockIdx.x == 0 && blockIdx.y == 0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const double mean_d = (double)tmp[c] * s / (double)b.n;
+    const double var_d = (double)tmp[C + c] * (s * s) / (double)b.n - mean_d * mean_d;
+    const float m = (float)mean_d, v = (float)var_d;
+    const float sigma = sqrtf(v + b.eps);
+    mu[c] = m;
+    sg[c] = sigma;
+    if (writer) {
+      if (b.ms) { b.ms[c] = m; b.ms[C + c] = sigma; }
+      if (b.run_mean) {
+        b.run_mean[c] = b.momentum * b.run_mean[c] + b.one_minus_momentum * m;
+        b.run_var[c] = b.momentum * b.run_var[c] + b.one_minus_momentum * v;
+      }
+    }
+  }
+}
+
+// ============================================================================ forward chain
+struct BranchState {
+  QState qn, qr;
+  float sn, sr;
+};
+
+__global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, int rpt) {
+  extern __shared__ float shf[];  // per branch: mu, sigma, gq, bq [C each]; then long long tmp[2C]
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const int C = a.C;
+  float* P1 = shf;
+  float* P2 = shf + 4 * C;
+  long long* tmp = reinterpret_cast<long long*>(shf + 8 * C);
+  const lbt_chain_branch* br[2] = {&a.b1, &a.b2};
+  const int nb = a.has_b2 ? 2 : 1;
+  BranchState bs[2];
+  for (int b = 0; b < nb; ++b) {
+    const lbt_chain_branch& B = *br[b];
+    float* P = b ? P2 : P1;
+    bs[b].qr = qstate(B.qr);
+    bs[b].sr = bs[b].qr.active ? bs[b].qr.inv_m : 0.f;
+    if (B.nrm.q) {
+      bs[b].qn = qstate(B.nrm.qn);
+      bs[b].sn = bs[b].qn.inv_m;
+      bn_moments(B.nrm, C, P, P + C, tmp);
+      __syncthreads();
+    } else {
+      bs[b].qn.active = 0;
+      bs[b].sn = 0.f;
+    }
+    if (bs[b].qr.active)
+      for (int c = threadIdx.x; c < C; c += kThreads) { P[2 * C + c] = B.gb[c]; P[3 * C + c] = B.gb[C + c]; }
+  }
+  __syncthreads();
+  const QState so1 = qstate(a.qo1), so2 = qstate(a.qo2);
+  const bool o1 = a.o1 && so1.active, o2 = a.o2 && so2.active;
+  int ov[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};  // qr1, qr2, qo1, qo2
+
+  const int64_t groups = a.inner >> 2;
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (g < groups) {
+    const int c0 = (int)((g << 2) % C);
+    Noise4 nr[2], no1, no2;
+    for (int b = 0; b < nb; ++b) nr[b] = noise_for(br[b]->qr, bs[b].qr, g);
+    no1 = noise_for(a.qo1, so1, g);
+    no2 = noise_for(a.qo2, so2, g);
+    const int64_t r0 = (int64_t)blockIdx.y * rpt;
+    const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+    for (int64_t r = r0; r < rend; ++r) {
+      const int64_t e = r * a.inner + (g << 2);
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < nb; ++b) {
+        const lbt_chain_branch& B = *br[b];
+        const float* P = b ? P2 : P1;
+        float t[4];
+        if (B.nrm.q) {
+          int q[4];
+          load4_i8(B.nrm.q, e, q);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float x1 = (float)q[k] * bs[b].sn;
+            const float x2 = x1 - P[c0 + k];
+            t[k] = x2 / P[C + c0 + k];
+          }
+        } else {
+          load4_f32(B.xin, e, t);
+        }
+        if (bs[b].qr.active) {
+          int R[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            R[k] = quant1(bs[b].qr, B.qr.stochastic, t[k], nr[b].u[k], ov[b][0], ov[b][1]);
+            const float xr = (float)R[k] * bs[b].sr;
+            const float m1 = xr * P[2 * C + c0 + k];
+            t[k] = m1 + P[3 * C + c0 + k];
+          }
+          if (B.rout) store4_i8(B.rout, e, R, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = b ? v[k] + t[k] : t[k];
+      }
+      if (a.res) {
+        float rr[4];
+        load4_f32(a.res, e, rr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = v[k] + rr[k];
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+      }
+      if (a.y) store4_f32(a.y, e, v);
+      if (o1) {
+        int c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = quant1(so1, a.qo1.stochastic, v[k], no1.u[k], ov[2][0], ov[2][1]);
+        store4_code(a.o1, a.o1_kind, e, c, so1.inv_m);
+      }
+      if (o2) {
+        int c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = quant1(so2, a.qo2.stochastic, v[k], no2.u[k], ov[3][0], ov[3][1]);
+        store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
+      }
+    }
+  }
+  if (bs[0].qr.active) block_flush_counts(a.b1.qr, ov[0][0], ov[0][1], sh_cnt);
+  if (nb > 1 && bs[1].qr.active) block_flush_counts(a.b2.qr, ov[1][0], ov[1][1], sh_cnt);
+  if (o1) block_flush_counts(a.qo1, ov[2][0], ov[2][1], sh_cnt);
+  if (o2) block_flush_counts(a.qo2, ov[3][0], ov[3][1], sh_cnt);
+}
+
+// ============================================================================ backward pass A
+__global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a, int rpt) {
+  extern __shared__ float shf[];  // per branch: gq, bq [C]; then long long sums[2][4C]
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const int C = a.C;
+  long long* S = reinterpret_cast<long long*>(shf + 4 * C);  // [2][4C]
+  const lbt_bwd_branch* br[2] = {&a.b1, &a.b2};
+  const int nb = a.has_b2 ? 2 : 1;
+  QState qrg[2], qng[2], qr[2];
+  for (int b = 0; b < nb; ++b) {
+    const lbt_bwd_branch& B = *br[b];
+    qrg[b] = qstate(B.qrg);
+    qng[b] = qstate(B.qng);
+    qr[b] = qstate(B.qr);
+    if (B.gb)
+      for (int c = threadIdx.x; c < C; c += kThreads) { shf[b * 2 * C + c] = B.gb[c]; shf[b * 2 * C + C + c] = B.gb[C + c]; }
+  }
+  for (int i = threadIdx.x; i < 8 * C; i += kThreads) S[i] = 0;
+  __syncthreads();
+  int ov[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};  // qrg1, qng1, qrg2, qng2
+  const int64_t groups = a.inner >> 2;
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (g < groups) {
+    const int c0 = (int)((g << 2) % C);
+    Noise4 nrg[2], nng[2];
+    for (int b = 0; b < nb; ++b) {
+      nrg[b] = noise_for(br[b]->qrg, qrg[b], g);
+      nng[b] = noise_for(br[b]->qng, qng[b], g);
+    }
+    int acc[2][4][4];  // [branch][sum][k]
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[b][s][k] = 0;
+    const int64_t r0 = (int64_t)blockIdx.y * rpt;
+    const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+    for (int64_t r = r0; r < rend; ++r) {
+      const int64_t e = r * a.inner + (g << 2);
+      float gv[4];
+      load4_f32(a.g, e, gv);
+      int R1[4] = {0, 0, 0, 0};
+      if (a.b1.R) load4_i8(a.b1.R, e, R1);
+      if (a.y_mask) {
+        float ym[4];
+        load4_f32(a.y_mask, e, ym);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gv[k] = ym[k] > 0.f ? gv[k] : 0.f;
+      } else if (a.mask_from_r) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float xr = (float)R1[k] * qr[0].inv_m;
+          const float m1 = xr * shf[c0 + k];
+          const float yv = m1 + shf[C + c0 + k];
+          gv[k] = yv > 0.f ? gv[k] : 0.f;
+        }
+      }
+      if (a.gmask_out) store4_f32(a.gmask_out, e, gv);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (b >= nb) break;
+        const lbt_bwd_branch& B = *br[b];
+        float d[4] = {gv[0], gv[1], gv[2], gv[3]};
+        if (qrg[b].active) {
+          int R[4];
+          if (b == 0) { R[0] = R1[0]; R[1] = R1[1]; R[2] = R1[2]; R[3] = R1[3]; }
+          else load4_i8(B.R, e, R);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int G2 = quant1(qrg[b], B.qrg.stochastic, d[k], nrg[b].u[k], ov[2 * b][0], ov[2 * b][1]);
+            acc[b][0][k] += G2 * R[k];
+            acc[b][1][k] += G2;
+            const float gh = (float)G2 * qrg[b].inv_m;
+            d[k] = gh * shf[b * 2 * C + c0 + k];
+          }
+        }
+        if (qng[b].active) {
+          int G[4], qn[4];
+          load4_i8(B.qn_codes, e, qn);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            G[k] = quant1(qng[b], B.qng.stochastic, d[k], nng[b].u[k], ov[2 * b + 1][0], ov[2 * b + 1][1]);
+            acc[b][2][k] += G[k];
+            acc[b][3][k] += G[k] * qn[k];
+          }
+          store4_i8(B.gout, e, G, 0);
+        } else if (B.dout) {
+          store4_f32(B.dout, e, d);
+        }
+      }
+    }
+    for (int b = 0; b < nb; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (acc[b][s][k])
+            atomicAdd((unsigned long long*)&S[b * 4 * C + s * C + c0 + k], (unsigned long long)(long long)acc[b][s][k]);
+  }
+  for (int b = 0; b < nb; ++b) {
+    if (qrg[b].active) block_flush_counts(br[b]->qrg, ov[2 * b][0], ov[2 * b][1], sh_cnt);
+    if (qng[b].active) block_flush_counts(br[b]->qng, ov[2 * b + 1][0], ov[2 * b + 1][1], sh_cnt);
+  }
+  __syncthreads();
+  for (int b = 0; b < nb; ++b)
+    if (br[b]->sums) block_flush_sums(S + b * 4 * C, 4 * C, br[b]->sums, 4 * C);
+}
+
+// ============================================================================ backward pass B
+__global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a, int rpt) {
+  extern __shared__ float shf[];  // mu, sigma, mg, mgx [C]; then long long tmp[2C] / colsum[2C]
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const int C = a.C;
+  float* mu = shf;
+  float* sg = shf + C;
+  float* mg = shf + 2 * C;
+  float* mgx = shf + 3 * C;
+  long long* tmp = reinterpret_cast<long long*>(shf + 4 * C);
+  // SG at sums[2C:3C), SGQ at sums[3C:4C) of each shard
+  for (int i = threadIdx.x; i < 2 * C; i += kThreads) {
+    long long s = 0;
+    for (int k = 0; k < LBT_NSHARD; ++k) s += a.sums[(int64_t)k * 4 * C + 2 * C + i];
+    tmp[i] = s;
+  }
+  __syncthreads();
+  const QState sgq = qstate(a.qng), sn = qstate(a.qn), so = qstate(a.qo);
+  {
+    const double s = (double)sn.inv_m, g = (double)sgq.inv_m, n = (double)a.n;
+    for (int c = threadIdx.x; c < C; c += kThreads) {
+      const float m = a.ms[c], sig = a.ms[C + c];
+      mu[c] = m;
+      sg[c] = sig;
+      const double SG = (double)tmp[c], SGQ = (double)tmp[C + c];
+      mg[c] = (float)(g * SG / n);
+      mgx[c] = (float)(g * (s * SGQ - (double)m * SG) / (n * (double)sig));
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += kThreads) tmp[i] = 0;
+  __syncthreads();
+  const bool want_q = a.gq && so.active;
+  int ov1 = 0, ov2 = 0;
+  const int64_t groups = a.inner >> 2;
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (g < groups) {
+    const int c0 = (int)((g << 2) % C);
+    const Noise4 no = noise_for(a.qo, so, g);
+    int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+    const int64_t r0 = (int64_t)blockIdx.y * rpt;
+    const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+    for (int64_t r = r0; r < rend; ++r) {
+      const int64_t e = r * a.inner + (g << 2);
+      int G[4], q[4];
+      load4_i8(a.G, e, G);
+      load4_i8(a.qn_codes, e, q);
+      float dx[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c0 + k;
+        const float x1 = (float)q[k] * sn.inv_m;
+        const float x2 = x1 - mu[c];
+        const float xh = x2 / sg[c];
+        const float gh = (float)G[k] * sgq.inv_m;
+        const float t1 = gh - mg[c];
+        const float t2 = xh * mgx[c];
+        dx[k] = (t1 - t2) / sg[c];
+      }
+      if (a.dx) store4_f32(a.dx, e, dx);
+      if (want_q) {
+        int c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          c[k] = quant1(so, a.qo.stochastic, dx[k], no.u[k], ov1, ov2);
+          s1[k] += c[k];
+          s2[k] += c[k] * c[k];
+        }
+        store4_i8(a.gq, e, c, 0);
+      }
+    }
+    if (want_q && a.gcolsum) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (s1[k]) atomicAdd((unsigned long long*)&tmp[c0 + k], (unsigned long long)(long long)s1[k]);
+        if (s2[k]) atomicAdd((unsigned long long*)&tmp[C + c0 + k], (unsigned long long)(long long)s2[k]);
+      }
+    }
+  }
+  if (want_q) block_flush_counts(a.qo, ov1, ov2, sh_cnt);
+  if (want_q && a.gcolsum) {
+    __syncthreads();
+    block_flush_sums(tmp, 2 * C, a.gcolsum, 2 * C);
+  }
+}
+
+__global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
+                                   float wd2, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  long long sgr = 0, sg = 0;
+  for (int k = 0; k < LBT_NSHARD; ++k) {
+    sgr += sums[(int64_t)k * 4 * C + c];
+    sg += sums[(int64_t)k * 4 * C + C + c];
+  }
+  const double g2 = ldexp(1.0, -frac_exp(qrg)), r = ldexp(1.0, -frac_exp(qr));
+  const float a = (float)((double)sgr * (g2 * r));
+  const float b = wd2 * gamma[c];
+  dgamma[c] = a + b;
+  dbeta[c] = (float)((double)sg * g2);
+}
+
+// grid over [groups, rows/rpt] with >= ~2048 workgroups
+bool grid_for(int64_t rows, int64_t inner, dim3& grid, int& rpt) {
+  const int64_t groups = inner / 4;
+  const int64_t gblocks = (groups + kThreads - 1) / kThreads;
+  int64_t r = (gblocks * rows) / 2048;
+  if (r < 1) r = 1;
+  if (r > 64) r = 64;
+  const int64_t yb = (rows + r - 1) / r;
+  if (gblocks > 0x7fffffff || yb > 65535) return false;
+  grid = dim3((unsigned)gblocks, (unsigned)yb);
+  rpt = (int)r;
+  return true;
+}
+
+bool shape_ok(int64_t rows, int64_t inner, int C) {
+  return rows > 0 && inner > 0 && C > 0 && C % 4 == 0 && inner % C == 0 && inner % 4 == 0;
+}
+
+}  // namespace
+
+extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
+  if (!shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;
+  dim3 grid;
+  int rpt;
+  if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
+  const size_t shm = sizeof(float) * 8 * a->C + sizeof(long long) * 2 * a->C;
+  hipLaunchKernelGGL(chain_fwd_kernel, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream) {
+  if (!shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;
+  dim3 grid;
+  int rpt;
+  if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
+  const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 8 * a->C;
+  hipLaunchKernelGGL(chain_bwd_a_kernel, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream) {
+  if (!shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;
+  dim3 grid;
+  int rpt;
+  if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
+  const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 2 * a->C;
+  hipLaunchKernelGGL(chain_bwd_b_kernel, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_bn_param_grads(const int64_t* sums, int32_t C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
+                                  float wd2, float* dgamma, float* dbeta, void* stream) {
+  hipLaunchKernelGGL(param_grads_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, C, qrg, qr,
+                     gamma, wd2, dgamma, dbeta);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,190 @@
+// conv_generic.hip -- any-shape integer convolution on the VALU (int32 accumulation).
+//
+// Used where the MFMA implicit GEMM does not apply:
+//   * signed 9-bit inputs (ResNet conv1 reads the image, quantised at bits+1 = 9 bits,
+//     dynamic_fixed_point.py:287-288 -- int8 MFMA is signed x signed 8-bit);
+//   * channel counts that are not multiples of 16 (conv1 Cin=3, Dense_q 64->10 run as a
+//     1x1 conv on [B,1,1,C], custom.py's MNIST convs).
+// Exact integer arithmetic, so results are bit-identical to the MFMA path and the oracle.
+#include "dfxp_device.h"
+
+using namespace lbt;
+
+namespace {
+
+template <typename TX>
+__global__ __launch_bounds__(256) void conv_fwd_generic_kernel(const TX* __restrict__ x, const int8_t* __restrict__ w,
+                                                              lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw,
+                                                              float* __restrict__ y) {
+  const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qw)));
+  const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cout;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int co = (int)(i % d.Cout);
+  int64_t m = i / d.Cout;
+  const int ow = (int)(m % d.Wo);
+  m /= d.Wo;
+  const int oh = (int)(m % d.Ho);
+  const int n = (int)(m / d.Ho);
+  int acc = 0;
+  for (int kh = 0; kh < d.KH; ++kh) {
+    const int ih = oh * d.SH + kh - d.PT;
+    if ((unsigned)ih >= (unsigned)d.H) continue;
+    for (int kw = 0; kw < d.KW; ++kw) {
+      const int iw = ow * d.SW + kw - d.PL;
+      if ((unsigned)iw >= (unsigned)d.W) continue;
+      const TX* xp = x + (((int64_t)n * d.H + ih) * d.W + iw) * d.Cin;
+      const int8_t* wp = w + ((int64_t)(kh * d.KW + kw) * d.Cin) * d.Cout + co;
+      for (int ci = 0; ci < d.Cin; ++ci) acc += (int)xp[ci] * (int)wp[(int64_t)ci * d.Cout];
+    }
+  }
+  y[i] = (float)acc * scale;
+}
+
+__global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const int8_t* __restrict__ g,
+                                                                const int8_t* __restrict__ w, lbt_conv_desc d,
+                                                                lbt_qdesc qg, lbt_qdesc qw, float* __restrict__ dx,
+                                                                const float* __restrict__ add_src) {
+  const float scale = ldexpf(1.0f, -(frac_exp(qg) + frac_exp(qw)));
+  const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int ci = (int)(i % d.Cin);
+  int64_t m = i / d.Cin;
+  const int iw = (int)(m % d.W);
+  m /= d.W;
+  const int ih = (int)(m % d.H);
+  const int n = (int)(m / d.H);
+  int acc = 0;
+  for (int kh = 0; kh < d.KH; ++kh) {
+    const int ny = ih + d.PT - kh;
+    if (ny < 0 || ny % d.SH) continue;
+    const int oh = ny / d.SH;
+    if (oh >= d.Ho) continue;
+    for (int kw = 0; kw < d.KW; ++kw) {
+      const int nx = iw + d.PL - kw;
+      if (nx < 0 || nx % d.SW) continue;
+      const int ow = nx / d.SW;
+      if (ow >= d.Wo) continue;
+      const int8_t* gp = g + (((int64_t)n * d.Ho + oh) * d.Wo + ow) * d.Cout;
+      const int8_t* wp = w + ((int64_t)(kh * d.KW + kw) * d.Cin + ci) * d.Cout;
+      for (int co = 0; co < d.Cout; ++co) acc += (int)gp[co] * (int)wp[co];
+    }
+  }
+  const float v = (float)acc * scale;
+  dx[i] = add_src ? v + add_src[i] : v;
+}
+
+// grid = nsplit blocks; block b reduces pixels [b*per, (b+1)*per) in chunks of kChunk staged in
+// LDS (im2col patch of X and the G rows), every thread owning (k, co) outputs.
+constexpr int kChunk = 32;
+template <typename TX>
+__global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __restrict__ x, const int8_t* __restrict__ g,
+                                                                lbt_conv_desc d, int32_t* __restrict__ slab,
+                                                                int64_t P, int nsplit) {
+  extern __shared__ int16_t sh[];  // Xs[kChunk][K] then Gs[kChunk][Cout]
+  const int K = d.KH * d.KW * d.Cin;
+  int16_t* Xs = sh;
+  int16_t* Gs = sh + kChunk * K;
+  const int64_t per = (P + nsplit - 1) / nsplit;
+  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p1 = p0 + per < P ? p0 + per : P;
+  const int nout = K * d.Cout;
+  constexpr int kMaxOut = 16;  // outputs per thread (K*Cout <= 4096)
+  int acc[kMaxOut];
+#pragma unroll
+  for (int j = 0; j < kMaxOut; ++j) acc[j] = 0;
+  const int64_t HWo = (int64_t)d.Ho * d.Wo;
+  for (int64_t c0 = p0; c0 < p1; c0 += kChunk) {
+    const int cn = (int)(p1 - c0 < kChunk ? p1 - c0 : kChunk);
+    for (int t = threadIdx.x; t < kChunk * K; t += blockDim.x) {
+      const int pl = t / K, k = t - pl * K;
+      int v = 0;
+      if (pl < cn) {
+        const int64_t p = c0 + pl;
+        const int n = (int)(p / HWo);
+        const int64_t rem = p - (int64_t)n * HWo;
+        const int oh = (int)(rem / d.Wo), ow = (int)(rem - (int64_t)oh * d.Wo);
+        const int tap = k / d.Cin, ci = k - tap * d.Cin;
+        const int kh = tap / d.KW, kw = tap - kh * d.KW;
+        const int ih = oh * d.SH + kh - d.PT, iw = ow * d.SW + kw - d.PL;
+        if ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W)
+          v = (int)x[(((int64_t)n * d.H + ih) * d.W + iw) * d.Cin + ci];
+      }
+      Xs[t] = (int16_t)v;
+    }
+    for (int t = threadIdx.x; t < kChunk * d.Cout; t += blockDim.x) {
+      const int pl = t / d.Cout, co = t - pl * d.Cout;
+      Gs[t] = pl < cn ? (int16_t)g[(c0 + pl) * d.Cout + co] : (int16_t)0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kMaxOut; ++j) {
+      const int o = threadIdx.x + j * blockDim.x;
+      if (o < nout) {
+        const int k = o / d.Cout, co = o - k * d.Cout;
+        int a = acc[j];
+        for (int pl = 0; pl < kChunk; ++pl) a += (int)Xs[pl * K + k] * (int)Gs[pl * d.Cout + co];
+        acc[j] = a;
+      }
+    }
+    __syncthreads();
+  }
+  int32_t* dst = slab + (int64_t)blockIdx.x * nout;
+#pragma unroll
+  for (int j = 0; j < kMaxOut; ++j) {
+    const int o = threadIdx.x + j * blockDim.x;
+    if (o < nout) dst[o] = acc[j];
+  }
+}
+
+bool desc_ok(const lbt_conv_desc& d) {
+  return d.N > 0 && d.H > 0 && d.W > 0 && d.KH > 0 && d.KW > 0 && d.SH > 0 && d.SW > 0 && d.Ho > 0 &&
+         d.Wo > 0 && d.Cin > 0 && d.Cout > 0;
+}
+
+}  // namespace
+
+extern "C" int lbt_conv_fwd_generic(const void* xq, int32_t x_i16, const int8_t* w_hwio, lbt_conv_desc d,
+                                    lbt_qdesc qx, lbt_qdesc qw, float* y, void* stream) {
+  if (!desc_ok(d)) return LBT_EINVAL;
+  const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cout;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  if (x_i16)
+    hipLaunchKernelGGL(conv_fwd_generic_kernel<int16_t>, dim3(blocks), dim3(256), 0, st, (const int16_t*)xq, w_hwio, d,
+                       qx, qw, y);
+  else
+    hipLaunchKernelGGL(conv_fwd_generic_kernel<int8_t>, dim3(blocks), dim3(256), 0, st, (const int8_t*)xq, w_hwio, d,
+                       qx, qw, y);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_conv_dgrad_generic(const int8_t* gq, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qg,
+                                      lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
+  if (!desc_ok(d)) return LBT_EINVAL;
+  const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL(conv_dgrad_generic_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, gq, w_hwio, d, qg,
+                     qw, dx, add_src);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
+                                      int32_t* slab, int32_t nsplit, void* stream) {
+  if (!desc_ok(d) || nsplit <= 0) return LBT_EINVAL;
+  const int K = d.KH * d.KW * d.Cin;
+  if ((int64_t)K * d.Cout > 16 * 256) return LBT_EINVAL;
+  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
+  if ((P + nsplit - 1) / nsplit > 8192) return LBT_EINVAL;  // int32 partial bound for 9-bit x 8-bit
+  const size_t shm = sizeof(int16_t) * kChunk * (K + d.Cout);
+  if (shm > 64 * 1024) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (x_i16)
+    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int16_t>, dim3(nsplit), dim3(256), shm, st, (const int16_t*)xq, gq, d,
+                       slab, P, nsplit);
+  else
+    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int8_t>, dim3(nsplit), dim3(256), shm, st, (const int8_t*)xq, gq, d,
+                       slab, P, nsplit);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,376 @@
+// conv_mfma.hip -- int8 implicit-GEMM convolution on gfx950 v_mfma_i32_16x16x64_i8.
+//
+//  lbt_conv_fwd_i8       Conv2d_q.forward  y = conv(Xq, Wq)          (dynamic_fixed_point.py:287-291)
+//  lbt_conv_dgrad_i8     Conv2d_q.backward dX = conv^T(gradq, Wq)    (dynamic_fixed_point.py:305)
+//  lbt_conv_wgrad_i8     Conv2d_q.backward dW = sum_p Xq (x) gradq   (dynamic_fixed_point.py:302)
+//  lbt_conv_wgrad_reduce     + 2*wd*W, dequant, split reduction
+//
+// Operand maps (probed on MI355X with exact integer data): for 16x16x64_i8 lane l supplies
+// A[row l&15][k = 16*(l>>4) .. +15] and B[k = 16*(l>>4) .. +15][col l&15] as 16 int8 each;
+// C/D: col = l&15, row = 4*(l>>4) + reg.
+//
+// fwd / dgrad: GEMM rows = output pixels (fwd) or input pixels (dgrad), cols = output channels,
+// k = (tap, 16-channel slice).  Every A fragment is one 16-byte NHWC channel slice of one
+// pixel, gathered straight from global memory by its lane (the 9x tap re-reads of a 3x3 conv
+// hit L1/L2; the whole activation is a few MB).  B (packed weights, <= 37 KB) is L2-resident.
+// Out-of-bounds taps read the encoding of 0: -128 for the unsigned-9-bit offset encoding
+// (q - 128), 0 otherwise; the offset is undone in the epilogue with 128 * sum_k W[k][co].
+//
+// wgrad: GEMM rows = (tap, ci), cols = co, k = pixels.  Each wave stages 64 pixels of G and of
+// the tap-shifted X into LDS transposed ([channel][pixel]) and issues 16x16x64 MFMAs; each
+// workgroup owns a pixel range and one tap and writes an int32 partial (exact, no atomics).
+#include "dfxp_device.h"
+
+using namespace lbt;
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kThreads = 256;
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+
+struct GemmArgs {
+  const int8_t* a;      // gathered operand (xq for fwd, gq for dgrad), NHWC
+  const int8_t* b;      // packed weights [ncol][ks*16]
+  int ks;               // 16-byte k-slices per column (multiple of 4)
+  int nslices;          // real k-slices = taps * CS
+  int a_fill;           // fill word for out-of-bounds taps
+  const int32_t* colsum;
+  lbt_conv_desc d;
+  lbt_qdesc qa, qb;     // scale sources
+  float* y;             // fp32 output
+  const float* add_src; // fp32 addend (dgrad)
+  int8_t* yq;           // quantised output (fwd epilogue quantiser)
+  lbt_qdesc qout;
+  int64_t* ychsum;
+  int64_t M;            // GEMM rows
+  int ncol;             // GEMM cols
+};
+
+template <int MODE, int CS>
+__global__ __launch_bounds__(kThreads) void conv_gemm_kernel(GemmArgs p) {
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  __shared__ long long sh_sum[2 * 128];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nt_total = p.ncol >> 4;
+  const int wpm = nt_total < 4 ? nt_total : 4;  // waves per M-tile
+  const int ntw = nt_total / wpm;               // n-tiles per wave (1 or 2)
+  const int mtb = 4 / wpm;                      // M-tiles per block
+  const int mt_local = wave / wpm;
+  const int nt0 = (wave % wpm) * ntw;
+  const int64_t mtile = (int64_t)blockIdx.x * mtb + mt_local;
+  const bool wave_live = mt_local < mtb;
+  const int r = lane & 15, kg = lane >> 4;
+  const lbt_conv_desc& d = p.d;
+
+  const bool want_q = p.yq != nullptr;
+  const bool want_sum = want_q && p.ychsum != nullptr;
+  if (want_sum) {
+    for (int i = threadIdx.x; i < 2 * p.ncol; i += kThreads) sh_sum[i] = 0;
+    __syncthreads();
+  }
+
+  // this lane's GEMM row -> pixel (n, y, x) of the "row" space
+  const int OH = MODE == MODE_FWD ? d.Ho : d.H, OW = MODE == MODE_FWD ? d.Wo : d.W;
+  const int64_t m = mtile * 16 + r;
+  const bool row_ok = wave_live && m < p.M;
+  int n = 0, py = 0, px = 0;
+  if (row_ok) {
+    px = (int)(m % OW);
+    const int64_t t = m / OW;
+    py = (int)(t % OH);
+    n = (int)(t / OH);
+  }
+  const int cred = CS * 16;  // channels of the gathered operand
+  const int SH = MODE == MODE_FWD ? d.H : d.Ho, SW = MODE == MODE_FWD ? d.W : d.Wo;
+
+  v4i acc[2];
+  acc[0] = v4i{0, 0, 0, 0};
+  acc[1] = v4i{0, 0, 0, 0};
+
+  if (wave_live) {
+    for (int ks = 0; ks < p.ks; ks += 4) {
+      const int s = ks + kg;
+      v4i a = v4i{p.a_fill, p.a_fill, p.a_fill, p.a_fill};
+      if (s < p.nslices && row_ok) {
+        const int tap = s / CS, cs = s - tap * CS;
+        const int kh = tap / d.KW, kw = tap - kh * d.KW;
+        int sy, sx;
+        bool ok;
+        if (MODE == MODE_FWD) {
+          sy = py * d.SH + kh - d.PT;
+          sx = px * d.SW + kw - d.PL;
+          ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+        } else {
+          const int ny = py + d.PT - kh, nx = px + d.PL - kw;
+          sy = ny / d.SH;
+          sx = nx / d.SW;
+          ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
+        }
+        if (ok)
+          a = *reinterpret_cast<const v4i*>(p.a + (((int64_t)n * SH + sy) * SW + sx) * cred + cs * 16);
+        else if (MODE == MODE_DGRAD)
+          a = v4i{0, 0, 0, 0};
+      } else if (s >= p.nslices) {
+        a = v4i{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (j < ntw) {
+          const int col = (nt0 + j) * 16 + r;
+          const v4i b = *reinterpret_cast<const v4i*>(p.b + ((int64_t)col * p.ks + s) * 16);
+          acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, acc[j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---------------- epilogue
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
+  QState qs;
+  if (want_q) qs = qstate(p.qout);
+  int ov1 = 0, ov2 = 0;
+  const int64_t HWo = (int64_t)OH * OW;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (!(wave_live && j < ntw)) continue;
+    const int col = (nt0 + j) * 16 + r;
+    const int corr = p.colsum ? 128 * p.colsum[col] : 0;
+    int s1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = mtile * 16 + kg * 4 + i;
+      if (row >= p.M) continue;
+      const float v = (float)(acc[j][i] + corr) * scale;
+      const int64_t e = row * p.ncol + col;
+      if (p.y) p.y[e] = p.add_src ? v + p.add_src[e] : v;
+      if (want_q) {
+        const int64_t nidx = (row % HWo) * p.ncol + col;
+        const float u = p.qout.stochastic ? noise1(nidx, p.qout.qid, qs.step, p.qout.seed) : 0.f;
+        const int c = quant1(qs, p.qout.stochastic, v, u, ov1, ov2);
+        p.yq[e] = (int8_t)c;
+        s1 += c;
+        s2 += c * c;
+      }
+    }
+    if (want_sum) {
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (kg == 0) {
+        atomicAdd((unsigned long long*)&sh_sum[col], (unsigned long long)(long long)s1);
+        atomicAdd((unsigned long long*)&sh_sum[p.ncol + col], (unsigned long long)(long long)s2);
+      }
+    }
+  }
+  if (want_q) block_flush_counts(p.qout, ov1, ov2, sh_cnt);
+  if (want_sum) {
+    __syncthreads();
+    block_flush_sums(sh_sum, 2 * p.ncol, p.ychsum, 2 * p.ncol);
+  }
+}
+
+// ----------------------------------------------------------------------------- wgrad
+// grid (nsplit, taps); block 256 = 4 waves, each wave walks 64-pixel chunks of the block's
+// pixel range.  LDS per wave: Xt [CSI*16][64+16] and Gt [CSO*16][64+16] bytes.
+constexpr int kWP = 64;        // pixels per wave chunk
+constexpr int kLdsRow = 80;    // 64 + 16 pad (keeps 16-B alignment)
+
+template <int CSI, int CSO>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __restrict__ xq,
+                                                              const int8_t* __restrict__ gq,
+                                                              lbt_conv_desc d, int x_fill,
+                                                              int32_t* __restrict__ slab, int64_t P,
+                                                              int nsplit) {
+  constexpr int CI = CSI * 16, CO = CSO * 16;
+  __shared__ __attribute__((aligned(16))) int8_t lds[4][(CI + CO) * kLdsRow];
+  __shared__ int red[CI * CO];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int tap = blockIdx.y;
+  const int kh = tap / d.KW, kw = tap - kh * d.KW;
+  int8_t* Xt = lds[wave];
+  int8_t* Gt = lds[wave] + CI * kLdsRow;
+
+  for (int i = threadIdx.x; i < CI * CO; i += kThreads) red[i] = 0;
+
+  const int64_t per = (P + nsplit - 1) / nsplit;
+  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p1 = p0 + per < P ? p0 + per : P;
+
+  v4i acc[CSI][CSO];
+#pragma unroll
+  for (int a = 0; a < CSI; ++a)
+#pragma unroll
+    for (int b = 0; b < CSO; ++b) acc[a][b] = v4i{0, 0, 0, 0};
+
+  const int64_t HWo = (int64_t)d.Ho * d.Wo;
+  // chunks are interleaved across the 4 waves of the block
+  for (int64_t c0 = p0 + (int64_t)wave * kWP; c0 < p1; c0 += 4 * kWP) {
+    const int64_t p = c0 + lane;
+    const bool pv = p < p1;
+    // ---- gather this lane's pixel: G row and tap-shifted X row
+    int n = 0, oh = 0, ow = 0;
+    if (pv) {
+      n = (int)(p / HWo);
+      const int64_t rem = p - (int64_t)n * HWo;
+      oh = (int)(rem / d.Wo);
+      ow = (int)(rem - (int64_t)oh * d.Wo);
+    }
+    const int ih = oh * d.SH + kh - d.PT, iw = ow * d.SW + kw - d.PL;
+    const bool xv = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+#pragma unroll
+    for (int cs = 0; cs < CSO; ++cs) {
+      v4i g = v4i{0, 0, 0, 0};
+      if (pv) g = *reinterpret_cast<const v4i*>(gq + p * CO + cs * 16);
+      const int8_t* gb = reinterpret_cast<const int8_t*>(&g);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) Gt[(cs * 16 + j) * kLdsRow + lane] = gb[j];
+    }
+#pragma unroll
+    for (int cs = 0; cs < CSI; ++cs) {
+      v4i x = v4i{x_fill, x_fill, x_fill, x_fill};
+      if (!pv) x = v4i{0, 0, 0, 0};
+      else if (xv) x = *reinterpret_cast<const v4i*>(xq + (((int64_t)n * d.H + ih) * d.W + iw) * CI + cs * 16);
+      const int8_t* xb = reinterpret_cast<const int8_t*>(&x);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) Xt[(cs * 16 + j) * kLdsRow + lane] = xb[j];
+    }
+    // this wave's transposed tiles are read by other lanes of the same wave only
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    v4i bf[CSO];
+#pragma unroll
+    for (int b = 0; b < CSO; ++b) bf[b] = *reinterpret_cast<const v4i*>(Gt + (b * 16 + r) * kLdsRow + kg * 16);
+#pragma unroll
+    for (int a = 0; a < CSI; ++a) {
+      const v4i af = *reinterpret_cast<const v4i*>(Xt + (a * 16 + r) * kLdsRow + kg * 16);
+#pragma unroll
+      for (int b = 0; b < CSO; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[b], acc[a][b], 0, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  __syncthreads();
+  // acc[a][b] element i: row = a*16 + 4*kg + i (ci), col = b*16 + r (co)
+#pragma unroll
+  for (int a = 0; a < CSI; ++a)
+#pragma unroll
+    for (int b = 0; b < CSO; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) atomicAdd(&red[(a * 16 + kg * 4 + i) * CO + b * 16 + r], acc[a][b][i]);
+  __syncthreads();
+  int32_t* dst = slab + ((int64_t)blockIdx.x * (d.KH * d.KW) + tap) * CI * CO;
+  for (int i = threadIdx.x; i < CI * CO; i += kThreads) dst[i] = red[i];
+}
+
+__global__ void wgrad_reduce_kernel(const int32_t* __restrict__ slab, int nsplit, int K, int Cout, int x_u8off,
+                                    const int64_t* __restrict__ gcolsum, lbt_qdesc qx, lbt_qdesc qg,
+                                    const float* __restrict__ w, float wd2, float* __restrict__ dw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)K * Cout;
+  if (i >= total) return;
+  long long s = 0;
+  for (int b = 0; b < nsplit; ++b) s += slab[(int64_t)b * total + i];
+  if (x_u8off && gcolsum) {
+    const int co = (int)(i % Cout);
+    long long cs = 0;
+    for (int k = 0; k < LBT_NSHARD; ++k) cs += gcolsum[(int64_t)k * 2 * Cout + co];
+    s += 128ll * cs;
+  }
+  const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qg)));
+  const float a = (float)s * scale;
+  const float b = wd2 * w[i];
+  dw[i] = a + b;
+}
+
+template <int MODE>
+int launch_gemm(const GemmArgs& p, int cs, hipStream_t st) {
+  const int nt = p.ncol / 16;
+  const int wpm = nt < 4 ? nt : 4;
+  if (nt != 1 && nt != 2 && nt != 4 && nt != 8) return LBT_EINVAL;
+  const int mtb = 4 / wpm;
+  const int64_t mtiles = (p.M + 15) / 16;
+  const int64_t blocks = (mtiles + mtb - 1) / mtb;
+  if (blocks > 0x7fffffff) return LBT_EINVAL;
+  switch (cs) {
+    case 1: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 8>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    default: return LBT_EINVAL;
+  }
+  return (int)hipGetLastError();
+}
+
+bool desc_ok(const lbt_conv_desc& d) {
+  return d.N > 0 && d.H > 0 && d.W > 0 && d.KH > 0 && d.KW > 0 && d.SH > 0 && d.SW > 0 && d.Ho > 0 &&
+         d.Wo > 0 && d.Cin > 0 && d.Cout > 0;
+}
+
+}  // namespace
+
+extern "C" int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf,
+                               const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,
+                               int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream) {
+  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cout > 128) return LBT_EINVAL;
+  const int cs = d.Cin / 16;
+  GemmArgs p;
+  p.a = xq; p.b = wf; p.ks = ksf; p.nslices = d.KH * d.KW * cs;
+  if (ksf % 4 || ksf < p.nslices) return LBT_EINVAL;
+  p.a_fill = x_u8off ? (int)0x80808080u : 0;
+  p.colsum = x_u8off ? wcolsum : nullptr;
+  if (x_u8off && !wcolsum) return LBT_EINVAL;
+  p.d = d; p.qa = qx; p.qb = qw; p.y = y; p.add_src = nullptr; p.yq = yq; p.qout = qout; p.ychsum = ychsum;
+  p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
+  return launch_gemm<MODE_FWD>(p, cs, (hipStream_t)stream);
+}
+
+extern "C" int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                                 lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
+  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cin > 128) return LBT_EINVAL;
+  const int cs = d.Cout / 16;
+  GemmArgs p;
+  p.a = gq; p.b = wd; p.ks = ksd; p.nslices = d.KH * d.KW * cs;
+  if (ksd % 4 || ksd < p.nslices) return LBT_EINVAL;
+  p.a_fill = 0; p.colsum = nullptr;
+  p.d = d; p.qa = qg; p.qb = qw; p.y = dx; p.add_src = add_src; p.yq = nullptr; p.qout = lbt_qdesc{};
+  p.ychsum = nullptr;
+  p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
+  return launch_gemm<MODE_DGRAD>(p, cs, (hipStream_t)stream);
+}
+
+extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t* gq, lbt_conv_desc d,
+                                    int32_t* slab, int32_t nsplit, void* stream) {
+  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || nsplit <= 0) return LBT_EINVAL;
+  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
+  if ((P + nsplit - 1) / nsplit > 65536) return LBT_EINVAL;  // int32 partial bound
+  const int csi = d.Cin / 16, cso = d.Cout / 16;
+  const int fill = x_u8off ? (int)0x80808080u : 0;
+  dim3 grid(nsplit, d.KH * d.KW);
+  hipStream_t st = (hipStream_t)stream;
+#define LBT_WG(A, B)                                                                                          \
+  if (csi == A && cso == B) {                                                                                 \
+    hipLaunchKernelGGL((conv_wgrad_kernel<A, B>), grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); \
+    return (int)hipGetLastError();                                                                            \
+  }
+  LBT_WG(1, 1) LBT_WG(1, 2) LBT_WG(1, 4) LBT_WG(2, 1) LBT_WG(2, 2) LBT_WG(2, 4) LBT_WG(4, 1) LBT_WG(4, 2)
+  LBT_WG(4, 4)
+#undef LBT_WG
+  return LBT_EINVAL;
+}
+
+extern "C" int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int32_t x_u8off,
+                                     const int64_t* gcolsum, lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2,
+                                     float* dw, void* stream) {
+  const int64_t total = (int64_t)K * Cout;
+  const int64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, slab, nsplit, K,
+                     Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,149 @@
+// dfxp_device.h -- device-side building blocks of the gfx950 DFXP path:
+//   * Philox4x32-10 noise (the build's counter RNG; oracle/philox.py is its CPU twin)
+//   * the DFXP quantiser of dynamic_fixed_point.py:26-38 on one element
+//   * the overflow predicates of dynamic_fixed_point.py:60-66
+//   * wave64 reductions
+// Compiled with -ffp-contract=off: every fp32 op below rounds exactly like the numpy oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lbt_dfxp.h"
+
+#define LBT_DEV __device__ __forceinline__
+
+namespace lbt {
+
+constexpr int kEMax = 30;  // reference computes 2**e in int32: defined for 0 <= e <= 30
+
+// ------------------------------------------------------------------ Philox4x32-10
+struct U4 { uint32_t x, y, z, w; };
+
+LBT_DEV U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+LBT_DEV float u24(uint32_t r) { return (float)(r >> 8) * 5.9604644775390625e-8f; }  // * 2^-24
+
+// Noise for the 4 consecutive noise indices 4*blk .. 4*blk+3 of one quantiser at one step.
+struct Noise4 { float u[4]; };
+LBT_DEV Noise4 noise4(uint64_t blk, uint32_t qid, uint64_t step, uint64_t seed) {
+  U4 r = philox((uint32_t)blk, qid, (uint32_t)step, (uint32_t)(step >> 32), (uint32_t)seed,
+                (uint32_t)(seed >> 32));
+  Noise4 n;
+  n.u[0] = u24(r.x); n.u[1] = u24(r.y); n.u[2] = u24(r.z); n.u[3] = u24(r.w);
+  return n;
+}
+LBT_DEV float noise1(uint64_t idx, uint32_t qid, uint64_t step, uint64_t seed) {
+  U4 r = philox((uint32_t)(idx >> 2), qid, (uint32_t)step, (uint32_t)(step >> 32), (uint32_t)seed,
+                (uint32_t)(seed >> 32));
+  const uint32_t k = (uint32_t)(idx & 3);
+  return u24(k == 0 ? r.x : k == 1 ? r.y : k == 2 ? r.z : r.w);
+}
+
+// ------------------------------------------------------------------ quantiser state
+// The per-call view of one quantiser: multiplier m = 2^e, limit L = 2^(bits-1).
+struct QState {
+  float m, inv_m, L, Lm1, Lh;
+  int e;
+  uint64_t step;
+  int active;
+};
+
+LBT_DEV int frac_exp(const lbt_qdesc& q) {
+  int e = q.bits - q.exps[q.slot] - 1;
+  return e < 0 ? 0 : (e > kEMax ? kEMax : e);
+}
+
+LBT_DEV QState qstate(const lbt_qdesc& q) {
+  QState s;
+  s.active = q.bits > 0;
+  if (!s.active) { s.m = s.inv_m = s.L = s.Lm1 = s.Lh = 0.f; s.e = 0; s.step = 0; return s; }
+  s.e = frac_exp(q);
+  s.m = ldexpf(1.0f, s.e);
+  s.inv_m = ldexpf(1.0f, -s.e);
+  s.L = ldexpf(1.0f, q.bits - 1);
+  s.Lm1 = s.L - 1.0f;
+  s.Lh = ldexpf(1.0f, q.bits - 2);
+  s.step = q.step ? *q.step : 0ull;
+  return s;
+}
+
+// dequant scale 2^-e of a quantiser (the exponent the codes were produced with)
+LBT_DEV float qscale(const lbt_qdesc& q) { return ldexpf(1.0f, -frac_exp(q)); }
+
+// One element: integer code + overflow predicates (on the UNquantised x, against I_t).
+// stochastic: floor(clip(x*m + u, -L, L-1)); nearest: rint(clip(x*m, -L, L-1)) (half-even).
+LBT_DEV int quant1(const QState& s, int stochastic, float x, float u, int& ov1, int& ov2) {
+  const float xm = x * s.m;  // exact: m is a power of two
+  ov1 += (xm >= s.L) | (xm < -s.L);
+  ov2 += (xm >= s.Lh) | (xm < -s.Lh);
+  float v = stochastic ? (xm + u) : xm;
+  v = fminf(fmaxf(v, -s.L), s.Lm1);
+  v = stochastic ? floorf(v) : rintf(v);
+  return (int)v;
+}
+
+// ------------------------------------------------------------------ reductions
+LBT_DEV int wave_sum_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+LBT_DEV long long wave_sum_i64(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+LBT_DEV int shard_id() {
+  return (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 13u) % LBT_NSHARD);
+}
+
+// Flush per-thread overflow counts: wave reduce -> LDS -> one atomic per workgroup into this
+// workgroup's shard.  EVERY thread of the block must call it (contains barriers).
+// sh must hold 2 ints per wave.
+LBT_DEV void block_flush_counts(const lbt_qdesc& q, int ov1, int ov2, int* sh) {
+  if (!q.counts) return;  // uniform
+  ov1 = wave_sum_i32(ov1);
+  ov2 = wave_sum_i32(ov2);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[2 * w] = ov1; sh[2 * w + 1] = ov2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t1 = 0, t2 = 0;
+    for (int i = 0; i < nw; ++i) { t1 += sh[2 * i]; t2 += sh[2 * i + 1]; }
+    int32_t* c = q.counts + ((int64_t)q.slot * LBT_NSHARD + shard_id()) * 2;
+    if (t1) atomicAdd(&c[0], t1);
+    if (t2) atomicAdd(&c[1], t2);
+  }
+  __syncthreads();
+}
+
+// Add a block-local per-channel partial (LDS, long long[n]) into shard shard_id() of a
+// sharded int64 buffer laid out [LBT_NSHARD][stride].
+LBT_DEV void block_flush_sums(const long long* sh, int n, int64_t* dst, int stride) {
+  int64_t* d = dst + (int64_t)shard_id() * stride;
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    if (sh[i]) atomicAdd((unsigned long long*)&d[i], (unsigned long long)sh[i]);
+}
+
+// Store one code in the requested encoding.
+LBT_DEV void store_code(void* out, int kind, int64_t i, int qv, float inv_m) {
+  switch (kind) {
+    case LBT_OUT_I8: ((int8_t*)out)[i] = (int8_t)qv; break;
+    case LBT_OUT_U8OFF: ((int8_t*)out)[i] = (int8_t)((qv < 0 ? 0 : qv) - 128); break;
+    case LBT_OUT_I16: ((int16_t*)out)[i] = (int16_t)qv; break;
+    default: ((float*)out)[i] = (float)qv * inv_m; break;
+  }
+}
+
+}  // namespace lbt

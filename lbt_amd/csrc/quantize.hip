@@ -1,0 +1,214 @@
+// quantize.hip -- DFXP quantiser, range controller and weight packing for gfx950.
+//
+//  lbt_dfxp_quantize        weight_quantization + overflow statistics (dynamic_fixed_point.py:4-67)
+//  lbt_dfxp_range_update    update_range for every quantiser slot (dynamic_fixed_point.py:70-94)
+//  lbt_dfxp_quantize_weight weight quantiser fused with the GEMM operand packing
+//
+// HBM-bound: the activation/gradient quantiser reads 4 B and writes 1 B per element. Each
+// thread owns 4 consecutive noise indices (one Philox call, one float4 load per row) and
+// walks `rpt` rows of the batch, so the noise -- shared across dim 0 by the reference's
+// tf.random_uniform(X.shape[1:]) -- is generated once per thread, not once per element.
+#include "dfxp_device.h"
+
+using namespace lbt;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+// rows x inner, inner % 4 == 0: vectorised path.
+__global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
+    const float* __restrict__ x, void* __restrict__ out, int out_kind, int64_t rows, int64_t inner,
+    int rpt, lbt_qdesc q, int64_t* __restrict__ chsum, int C) {
+  extern __shared__ long long sh_sum[];  // [2*C] when chsum
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const QState s = qstate(q);
+  const int64_t groups = inner >> 2;
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * rpt;
+  if (chsum) {
+    for (int i = threadIdx.x; i < 2 * C; i += kThreads) sh_sum[i] = 0;
+    __syncthreads();
+  }
+  int ov1 = 0, ov2 = 0;
+  if (g < groups) {
+    Noise4 n = {{0.f, 0.f, 0.f, 0.f}};
+    if (q.stochastic) n = noise4(g, q.qid, s.step, q.seed);
+    int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+    const int64_t rend = r0 + rpt < rows ? r0 + rpt : rows;
+    for (int64_t r = r0; r < rend; ++r) {
+      const int64_t base = r * inner + (g << 2);
+      const float4 v = *reinterpret_cast<const float4*>(x + base);
+      int c[4];
+      c[0] = quant1(s, q.stochastic, v.x, n.u[0], ov1, ov2);
+      c[1] = quant1(s, q.stochastic, v.y, n.u[1], ov1, ov2);
+      c[2] = quant1(s, q.stochastic, v.z, n.u[2], ov1, ov2);
+      c[3] = quant1(s, q.stochastic, v.w, n.u[3], ov1, ov2);
+      if (out_kind == LBT_OUT_I8 || out_kind == LBT_OUT_U8OFF) {
+        const int off = out_kind == LBT_OUT_U8OFF ? 128 : 0;
+        char4 o;
+        o.x = (int8_t)((out_kind == LBT_OUT_U8OFF && c[0] < 0 ? 0 : c[0]) - off);
+        o.y = (int8_t)((out_kind == LBT_OUT_U8OFF && c[1] < 0 ? 0 : c[1]) - off);
+        o.z = (int8_t)((out_kind == LBT_OUT_U8OFF && c[2] < 0 ? 0 : c[2]) - off);
+        o.w = (int8_t)((out_kind == LBT_OUT_U8OFF && c[3] < 0 ? 0 : c[3]) - off);
+        *reinterpret_cast<char4*>((int8_t*)out + base) = o;
+      } else if (out_kind == LBT_OUT_I16) {
+        short4 o;
+        o.x = (short)c[0]; o.y = (short)c[1]; o.z = (short)c[2]; o.w = (short)c[3];
+        *reinterpret_cast<short4*>((int16_t*)out + base) = o;
+      } else {
+        float4 o;
+        o.x = (float)c[0] * s.inv_m; o.y = (float)c[1] * s.inv_m;
+        o.z = (float)c[2] * s.inv_m; o.w = (float)c[3] * s.inv_m;
+        *reinterpret_cast<float4*>((float*)out + base) = o;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s1[k] += c[k]; s2[k] += c[k] * c[k]; }
+    }
+    if (chsum) {
+      const int ch = (int)((g << 2) % C);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        atomicAdd((unsigned long long*)&sh_sum[(ch + k) % C], (unsigned long long)(long long)s1[k]);
+        atomicAdd((unsigned long long*)&sh_sum[C + (ch + k) % C], (unsigned long long)(long long)s2[k]);
+      }
+    }
+  }
+  block_flush_counts(q, ov1, ov2, sh_cnt);
+  if (chsum) {
+    __syncthreads();
+    block_flush_sums(sh_sum, 2 * C, chsum, 2 * C);
+  }
+}
+
+// Any shape: one element per thread, per-element Philox (weights, gamma/beta, odd shapes).
+__global__ __launch_bounds__(kThreads) void quantize_generic_kernel(
+    const float* __restrict__ x, void* __restrict__ out, int out_kind, int64_t n, int64_t inner,
+    lbt_qdesc q, int64_t* __restrict__ chsum, int C) {
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const QState s = qstate(q);
+  int64_t* cs = chsum ? chsum + (int64_t)shard_id() * 2 * C : nullptr;
+  int ov1 = 0, ov2 = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const float u = q.stochastic ? noise1(i % inner, q.qid, s.step, q.seed) : 0.f;
+    const int c = quant1(s, q.stochastic, x[i], u, ov1, ov2);
+    store_code(out, out_kind, i, c, s.inv_m);
+    if (cs) {
+      const int ch = (int)(i % C);
+      atomicAdd((unsigned long long*)&cs[ch], (unsigned long long)(long long)c);
+      atomicAdd((unsigned long long*)&cs[C + ch], (unsigned long long)(long long)(c * c));
+    }
+  }
+  block_flush_counts(q, ov1, ov2, sh_cnt);
+}
+
+__global__ void range_update_kernel(int32_t* exps, int32_t* counts, const int32_t* bits,
+                                    const float* target, const float* nelem, int nslots,
+                                    uint64_t* step) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nslots && nelem[i] > 0.f) {  // slots not fed this step keep their exponent
+    int c1 = 0, c2 = 0;
+    int32_t* c = counts + (int64_t)i * LBT_NSHARD * 2;
+    for (int k = 0; k < LBT_NSHARD; ++k) { c1 += c[2 * k]; c2 += c[2 * k + 1]; c[2 * k] = 0; c[2 * k + 1] = 0; }
+    const float r1 = (float)c1 / nelem[i];
+    const float r2 = (float)c2 / nelem[i];
+    const float t = target[i];
+    const int delta = r1 > t ? 1 : (r2 <= t ? -1 : 0);
+    int I = exps[i] + delta;
+    const int hi = bits[i] - 1, lo = bits[i] - 1 - kEMax;
+    I = I > hi ? hi : (I < lo ? lo : I);
+    exps[i] = I;
+  }
+  if (i == 0) step[0] += 1ull;
+}
+
+// One block per output channel co: quantise W[:, :, :, co], write every packed layout and the
+// column sum (no atomics -> no zeroing needed between steps).
+__global__ __launch_bounds__(kThreads) void quantize_weight_kernel(
+    const float* __restrict__ w, int KH, int KW, int Cin, int Cout, lbt_qdesc q,
+    int8_t* __restrict__ w_hwio, int8_t* __restrict__ wf, int ksf, int8_t* __restrict__ wd, int ksd,
+    int32_t* __restrict__ colsum) {
+  __shared__ int red[kThreads / 64];
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const QState s = qstate(q);
+  const int co = blockIdx.x;
+  const int K = KH * KW * Cin;
+  const int64_t inner = (int64_t)KW * Cin * Cout;
+  const int cslices_in = (Cin + 15) / 16, cslices_out = (Cout + 15) / 16;
+  int ov1 = 0, ov2 = 0, csum = 0;
+  for (int k = threadIdx.x; k < K; k += kThreads) {
+    const int tap = k / Cin, ci = k % Cin;
+    const int64_t idx = (int64_t)k * Cout + co;  // HWIO flat index
+    const float u = q.stochastic ? noise1(idx % inner, q.qid, s.step, q.seed) : 0.f;
+    const int c = quant1(s, q.stochastic, w[idx], u, ov1, ov2);
+    csum += c;
+    if (w_hwio) w_hwio[idx] = (int8_t)c;
+    if (wf) wf[((int64_t)co * ksf + tap * cslices_in + ci / 16) * 16 + (ci & 15)] = (int8_t)c;
+    if (wd) wd[((int64_t)ci * ksd + tap * cslices_out + co / 16) * 16 + (co & 15)] = (int8_t)c;
+  }
+  block_flush_counts(q, ov1, ov2, sh_cnt);
+  if (colsum) {
+    csum = wave_sum_i32(csum);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = csum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      colsum[co] = t;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int lbt_dfxp_quantize(const float* x, void* out, int out_kind, int64_t rows, int64_t inner,
+                                 lbt_qdesc q, int64_t* chsum, int32_t C, void* stream) {
+  if (rows <= 0 || inner <= 0) return LBT_OK;
+  if (q.bits < 2 || q.bits > 16) return LBT_EINVAL;
+  if ((out_kind == LBT_OUT_I8 && q.bits > 8) || (out_kind == LBT_OUT_U8OFF && q.bits > 9)) return LBT_EINVAL;
+  if (chsum && (C <= 0 || inner % C)) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n = rows * inner;
+  const bool vec = (inner % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
+                   (!chsum || C % 4 == 0) && (inner >= 64);
+  if (vec) {
+    const int64_t groups = inner / 4;
+    const int64_t gblocks = (groups + kThreads - 1) / kThreads;
+    // aim for >= ~2048 blocks in flight; at least 1 row per thread
+    int64_t rpt = (gblocks * rows) / 2048;
+    if (rpt < 1) rpt = 1;
+    if (rpt > 64) rpt = 64;
+    const int64_t yblocks = (rows + rpt - 1) / rpt;
+    if (yblocks > 65535) return LBT_EINVAL;
+    const size_t shm = chsum ? sizeof(long long) * 2 * C : 0;
+    hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)gblocks, (unsigned)yblocks), dim3(kThreads), shm, st,
+                       x, out, out_kind, rows, inner, (int)rpt, q, chsum, C);
+  } else {
+    int64_t blocks = (n + kThreads - 1) / kThreads;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(quantize_generic_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st, x, out, out_kind, n,
+                       inner, q, chsum, C);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_dfxp_range_update(int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
+                                     const float* nelem, int32_t nslots, uint64_t* step, void* stream) {
+  const int blocks = nslots > 0 ? (nslots + 255) / 256 : 1;
+  hipLaunchKernelGGL(range_update_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, exps, counts, bits,
+                     target, nelem, nslots, step);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, int32_t Cin, int32_t Cout,
+                                        lbt_qdesc q, int8_t* w_hwio, int8_t* wf, int32_t ksf, int8_t* wd,
+                                        int32_t ksd, int32_t* colsum, void* stream) {
+  if (q.bits < 2 || q.bits > 8) return LBT_EINVAL;
+  if (wf && ksf * 16 < KH * KW * ((Cin + 15) / 16) * 16) return LBT_EINVAL;
+  if (wd && ksd * 16 < KH * KW * ((Cout + 15) / 16) * 16) return LBT_EINVAL;
+  hipLaunchKernelGGL(quantize_weight_kernel, dim3(Cout), dim3(kThreads), 0, (hipStream_t)stream, w, KH, KW, Cin,
+                     Cout, q, w_hwio, wf, ksf, wd, ksd, colsum);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_abi_version(void) { return 1; }

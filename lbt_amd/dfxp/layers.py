@@ -1,0 +1,572 @@
+"""The reference's quantised-layer API (``dynamic_fixed_point.py:97-1053``) on the gfx950 kernels.
+
+Same class names, constructor signatures and ``Layer_q`` protocol as the reference:
+``forward(X) -> y``, ``backward(grad, stochastic) -> dX``, ``grads_and_vars() -> [(dW, W)]``,
+``info() -> str``. Tensors are CUDA (HIP) torch tensors in the reference's layouts: NHWC
+activations, HWIO conv weights, ``[in, out]`` dense weights.
+
+Differences from TF (documented in DESIGN.md):
+* Range variables are slots of a device-resident :class:`~lbt_amd.runtime.DfxpContext`
+  (``layer.X_range`` etc. are :class:`~lbt_amd.runtime.Quantizer` objects); their updates are
+  applied by ``ctx.update_range_op()`` -- the reference's ``'update_range'`` collection.
+* Quantised operands are kept as integer codes (int8 / offset-uint8 / int16) plus the shared
+  exponent; the convolutions and matmuls run as exact integer GEMMs.
+* Outputs live in per-layer buffers that are reused every step (static-graph semantics).
+* ``Conv2d_q(..., input_nonnegative=True)`` declares a post-ReLU input: its (bits+1)-bit codes
+  are unsigned and take the int8 MFMA path; otherwise the signed codes take the VALU path.
+"""
+import numpy as np
+import torch
+
+from .. import _lib
+from .._lib import NO_Q, OUT_F32, OUT_I8, OUT_I16, OUT_U8OFF, BnNorm, BwdBranch, ChainBranch, ChainBwdA, \
+    ChainBwdB, ChainFwd, ptr
+from ..runtime import default_context, qid_of
+from . import ops
+
+
+def _rng(ctx, name):
+    return np.random.default_rng([ctx.seed & 0xFFFFFFFF, qid_of(name)])
+
+
+class _Cache:
+    """Per-layer device buffers, allocated on first use for a given shape and then reused."""
+
+    def __init__(self):
+        self.d = {}
+
+    def get(self, key, shape, dtype, device, zero=False):
+        t = self.d.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = (torch.zeros if zero else torch.empty)(tuple(shape), dtype=dtype, device=device)
+            self.d[key] = t
+        return t
+
+
+def _as_param(t, ctx):
+    return torch.as_tensor(t, dtype=torch.float32).to(ctx.device).contiguous()
+
+
+class Layer_q:
+    """Base class: identity forward, gradient pass-through backward (``:97-126``)."""
+
+    def forward(self, X):
+        self.X = X
+        self.y = X
+        return self.y
+
+    def backward(self, grad, stochastic=True):
+        return grad
+
+    def grads_and_vars(self):
+        return []
+
+    def param_slots(self):
+        """[(owner, var_attr, grad_attr)] -- used to bind parameters into flat buffers."""
+        return []
+
+    def info(self):
+        return "quantized layer (default identity)"
+
+
+class Conv2d_q(Layer_q):
+    """Quantised 2-D convolution (``:224-316``): Xq at bits+1, Wq / bq / gradq at bits."""
+
+    def __init__(self, name, bits, ksize, strides, padding, use_bias=True, weight_decay=0,
+                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2,
+                 input_nonnegative=False, ctx=None):
+        self.ctx = ctx = ctx or default_context()
+        h, w, Cin, Cout = self.ksize = list(ksize)
+        self.strides = list(strides)
+        self.padding = padding
+        self.name, self.use_bias, self.bits = name, use_bias, bits
+        self.target_overflow_rate, self.weight_decay = target_overflow_rate, weight_decay
+        self.input_nonnegative = input_nonnegative
+        limit = (3 / (h * w * Cin)) ** 0.5
+        self.W = _as_param(_rng(ctx, name + "/W").uniform(-limit, limit, size=ksize).astype(np.float32), ctx)
+        self.dW = torch.zeros_like(self.W)
+        t = target_overflow_rate
+        self.W_range = ctx.quantizer(name + "/W_range", bits, weight_range, t)
+        self.X_range = ctx.quantizer(name + "/X_range", bits + 1, input_range, t)
+        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, t)
+        if use_bias:
+            self.b = torch.zeros(Cout, dtype=torch.float32, device=ctx.device)
+            self.db = torch.zeros_like(self.b)
+            self.b_range = ctx.quantizer(name + "/b_range", bits, bias_range, t)
+        self.mfma = ops.mfma_ok(Cin, Cout) and bits <= 8
+        # x codes: unsigned 9-bit (offset int8, MFMA) / signed <= 8 bit (int8, MFMA) / int16 (VALU)
+        if bits + 1 <= 8:
+            self.x_kind = OUT_I8
+        elif bits + 1 == 9 and input_nonnegative:
+            self.x_kind = OUT_U8OFF
+        else:
+            self.x_kind = OUT_I16
+        self.x_mfma = self.mfma and self.x_kind != OUT_I16
+        self.ksf = ops.packed_slices(h, w, Cin)
+        self.ksd = ops.packed_slices(h, w, Cout)
+        dev = ctx.device
+        self.w_hwio = torch.zeros(ksize, dtype=torch.int8, device=dev)
+        self.wf = torch.zeros((Cout, self.ksf * 16), dtype=torch.int8, device=dev)
+        self.wd = torch.zeros((Cin, self.ksd * 16), dtype=torch.int8, device=dev)
+        self.wcolsum = torch.zeros(Cout, dtype=torch.int32, device=dev)
+        self._c = _Cache()
+
+    def param_slots(self):
+        s = [(self, "W", "dW")]
+        if self.use_bias:
+            s.append((self, "b", "db"))
+        return s
+
+    def quantize_weights(self):
+        ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio,
+                            wf=self.wf if self.mfma else None, ksf=self.ksf,
+                            wd=self.wd if self.mfma else None, ksd=self.ksd,
+                            colsum=self.wcolsum if self.mfma else None)
+
+    def forward(self, X):
+        self.X = X
+        N, H, W, Cin = X.shape
+        kh, kw, _, Cout = self.ksize
+        self.d = d = ops.conv_desc(N, H, W, Cin, Cout, kh, kw, self.strides[1], self.strides[2], self.padding)
+        self.xq = ops.quantize(X, self.X_range, self.x_kind, out=self._c.get("xq", X.shape, ops.out_dtype(self.x_kind),
+                                                                                X.device))
+        self.quantize_weights()
+        y = self._c.get("y", (N, d.Ho, d.Wo, Cout), torch.float32, X.device)
+        if self.x_mfma:
+            ops.conv_fwd_i8(self.xq, self.x_kind == OUT_U8OFF, self.wf, self.ksf, self.wcolsum, d,
+                            self.X_range.desc, self.W_range.desc, y=y)
+        else:
+            ops.conv_fwd_generic(self.xq, self.x_kind == OUT_I16, self.w_hwio, d, self.X_range.desc,
+                                 self.W_range.desc, y)
+        if self.use_bias:
+            self.bq = ops.quantize(self.b, self.b_range, OUT_F32, out=self._c.get("bq", (Cout,), torch.float32,
+                                                                                   X.device))
+            ops.bias_add(y, self.bq, Cout)
+        self.y = y
+        return y
+
+    def backward(self, grad, stochastic=True):
+        d = self.d
+        Cout, Cin = d.Cout, d.Cin
+        dev = grad.device
+        gsum = self._c.get("gsum", (ops.NSHARD * 2 * Cout,), torch.int64, dev)
+        gsum.zero_()
+        self.gradq = ops.quantize(grad, self.grad_range, OUT_I8, out=self._c.get("gq", grad.shape, torch.int8, dev),
+                                  chsum=gsum, C=Cout)
+        wd2 = ops.f32(2 * self.weight_decay)
+        K = d.KH * d.KW * Cin
+        if self.x_mfma:
+            ns = ops.wgrad_nsplit(d)
+            slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
+            ops.conv_wgrad_i8(self.xq, self.x_kind == OUT_U8OFF, self.gradq, d, slab, ns)
+        else:
+            ns = ops.wgrad_nsplit(d, generic=True)
+            slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
+            ops.conv_wgrad_generic(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
+        ops.conv_wgrad_reduce(slab, ns, K, Cout, self.x_kind == OUT_U8OFF, gsum, self.X_range.desc,
+                              self.grad_range.desc, self.W, wd2, self.dW)
+        if self.use_bias:
+            ops.bias_grad(gsum, Cout, self.grad_range.desc, self.db)
+        dx = self._c.get("dx", (d.N, d.H, d.W, Cin), torch.float32, dev)
+        if self.mfma:
+            ops.conv_dgrad_i8(self.gradq, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
+        else:
+            ops.conv_dgrad_generic(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
+        return dx
+
+    def grads_and_vars(self):
+        if self.use_bias:
+            return [(self.dW, self.W), (self.db, self.b)]
+        return [(self.dW, self.W)]
+
+    def info(self):
+        return "%d bits conv2d: %dx%dx%d stride %dx%d pad %s weight_decay %f" % (
+            self.bits, self.ksize[0], self.ksize[1], self.ksize[3],
+            self.strides[1], self.strides[2], self.padding, self.weight_decay)
+
+
+Conv2d_pq = Conv2d_q  # byte-identical copy in the reference (``:129-221``)
+
+
+class Dense_q(Layer_q):
+    """Quantised fully-connected layer (``:319-470``): X, W, b and grad all at bits."""
+
+    def __init__(self, name, bits, in_units, units, use_bias=True, weight_decay=0,
+                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, ctx=None):
+        self.ctx = ctx = ctx or default_context()
+        self.name, self.bits, self.in_units, self.units = name, bits, in_units, units
+        self.use_bias, self.weight_decay, self.target_overflow_rate = use_bias, weight_decay, target_overflow_rate
+        limit = (6 / (in_units + units)) ** 0.5
+        self.W = _as_param(_rng(ctx, name + "/W").uniform(-limit, limit, size=(in_units, units)).astype(np.float32),
+                           ctx)
+        self.dW = torch.zeros_like(self.W)
+        t = target_overflow_rate
+        self.W_range = ctx.quantizer(name + "/W_range", bits, weight_range, t)
+        self.X_range = ctx.quantizer(name + "/X_range", bits, input_range, t)
+        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, t)
+        if use_bias:
+            self.b = torch.zeros(units, dtype=torch.float32, device=ctx.device)
+            self.db = torch.zeros_like(self.b)
+            self.b_range = ctx.quantizer(name + "/b_range", bits, bias_range, t)
+        self.x_kind = OUT_I8 if bits <= 8 else OUT_I16
+        self.w_hwio = torch.zeros((in_units, units), dtype=torch.int8, device=ctx.device)
+        self._c = _Cache()
+
+    def param_slots(self):
+        s = [(self, "W", "dW")]
+        if self.use_bias:
+            s.append((self, "b", "db"))
+        return s
+
+    def forward(self, X):
+        self.X = X
+        N = X.shape[0]
+        dev = X.device
+        self.d = d = _lib.ConvDesc(N, 1, 1, self.in_units, self.units, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
+        self.xq = ops.quantize(X, self.X_range, self.x_kind, out=self._c.get("xq", X.shape,
+                                                                              ops.out_dtype(self.x_kind), dev))
+        ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio)
+        y = self._c.get("y", (N, self.units), torch.float32, dev)
+        ops.conv_fwd_generic(self.xq, self.x_kind == OUT_I16, self.w_hwio, d, self.X_range.desc,
+                             self.W_range.desc, y)
+        if self.use_bias:
+            self.bq = ops.quantize(self.b, self.b_range, OUT_F32, out=self._c.get("bq", (self.units,), torch.float32,
+                                                                                   dev))
+            ops.bias_add(y, self.bq, self.units)
+        self.y = y
+        return y
+
+    def backward(self, grad, stochastic=True):
+        d = self.d
+        dev = grad.device
+        gsum = self._c.get("gsum", (ops.NSHARD * 2 * self.units,), torch.int64, dev)
+        gsum.zero_()
+        self.gradq = ops.quantize(grad, self.grad_range, OUT_I8, out=self._c.get("gq", grad.shape, torch.int8, dev),
+                                  chsum=gsum, C=self.units)
+        ns = ops.wgrad_nsplit(d, generic=True)
+        slab = self._c.get("slab", (ns, self.in_units, self.units), torch.int32, dev)
+        ops.conv_wgrad_generic(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
+        ops.conv_wgrad_reduce(slab, ns, self.in_units, self.units, 0, None, self.X_range.desc,
+                              self.grad_range.desc, self.W, ops.f32(2 * self.weight_decay), self.dW)
+        if self.use_bias:
+            ops.bias_grad(gsum, self.units, self.grad_range.desc, self.db)
+        dx = self._c.get("dx", (d.N, self.in_units), torch.float32, dev)
+        ops.conv_dgrad_generic(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
+        return dx
+
+    def grads_and_vars(self):
+        if self.use_bias:
+            return [(self.dW, self.W), (self.db, self.b)]
+        return [(self.dW, self.W)]
+
+    def info(self):
+        return "%d bits dense: %dx%d weight_decay %f" % (self.bits, self.in_units, self.units, self.weight_decay)
+
+
+class Sequential_q(Layer_q):
+    def __init__(self, *args):
+        self.layers = args
+
+    def forward(self, X):
+        self.X = X
+        for layer in self.layers:
+            X = layer.forward(X)
+        self.y = X
+        return self.y
+
+    def backward(self, grad, stochastic=True):
+        for layer in reversed(self.layers):
+            grad = layer.backward(grad, stochastic)
+        return grad
+
+    def grads_and_vars(self):
+        res = []
+        for layer in self.layers:
+            res += layer.grads_and_vars()
+        return res
+
+    def param_slots(self):
+        return [s for layer in self.layers for s in layer.param_slots()]
+
+    def info(self):
+        return "\n\t".join(["Sequential layer:"] + [layer.info() for layer in self.layers])
+
+
+class Normalization_q(Layer_q):
+    """BN normalisation half (``:539-623``): quantise X, biased batch moments, normalise."""
+
+    def __init__(self, name, bits, num_features, training=True, momentum=0.999, eps=1e-5, target_overflow_rate=0,
+                 input_range=2, grad_range=2, ctx=None):
+        self.ctx = ctx = ctx or default_context()
+        self.name, self.bits, self.C, self.train = name, bits, num_features, training
+        self.momentum, self.eps, self.target_overflow_rate = momentum, eps, target_overflow_rate
+        self.X_range = ctx.quantizer(name + "/X_range", bits, input_range, target_overflow_rate)
+        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, target_overflow_rate)
+        self.X_mean_running = torch.zeros(num_features, dtype=torch.float32, device=ctx.device)
+        self.X_var_running = torch.ones(num_features, dtype=torch.float32, device=ctx.device)
+        self.ms = torch.zeros(2 * num_features, dtype=torch.float32, device=ctx.device)
+        self._c = _Cache()
+
+    def norm_desc(self, q, chsum, n):
+        return BnNorm(ptr(q).value, self.X_range.desc, ptr(chsum).value, n, ops.f32(self.eps),
+                      ops.f32(self.momentum), ops.f32(1 - self.momentum), self.ms.data_ptr(),
+                      self.X_mean_running.data_ptr(), self.X_var_running.data_ptr())
+
+    def forward(self, X):
+        if self.train is False:
+            raise NotImplementedError("Normalization_q eval mode (running statistics) is not on the hot path")
+        self.X = X
+        dev = X.device
+        C = X.shape[-1]
+        rows, inner = ops.rows_inner(tuple(X.shape))
+        chsum = self._c.get("chsum", (ops.NSHARD * 2 * C,), torch.int64, dev)
+        chsum.zero_()
+        self.q = ops.quantize(X, self.X_range, OUT_I8, out=self._c.get("q", X.shape, torch.int8, dev), chsum=chsum,
+                              C=C)
+        self.n = X.numel() // C
+        y = self._c.get("y", X.shape, torch.float32, dev)
+        a = ChainFwd()
+        a.b1.nrm = self.norm_desc(self.q, chsum, self.n)
+        a.relu = 0
+        a.y = y.data_ptr()
+        a.rows, a.inner, a.C = rows, inner, C
+        ops.chain_fwd(a)
+        self.y = y
+        return y
+
+    def backward(self, grad, stochastic=True):
+        dev = grad.device
+        C = self.C
+        rows, inner = ops.rows_inner(tuple(grad.shape))
+        sums = self._c.get("sums", (ops.NSHARD * 4 * C,), torch.int64, dev)
+        sums.zero_()
+        G = self._c.get("G", grad.shape, torch.int8, dev)
+        self.grad_range.observe(grad.numel())
+        a = ChainBwdA()
+        a.g = grad.data_ptr()
+        a.b1 = BwdBranch(NO_Q, None, NO_Q, None, self.grad_range.desc, self.q.data_ptr(), G.data_ptr(), None,
+                         sums.data_ptr())
+        a.rows, a.inner, a.C = rows, inner, C
+        ops.chain_bwd_a(a)
+        dx = self._c.get("dx", grad.shape, torch.float32, dev)
+        b = ChainBwdB(G.data_ptr(), self.grad_range.desc, self.q.data_ptr(), self.X_range.desc, self.ms.data_ptr(),
+                      sums.data_ptr(), self.n, dx.data_ptr(), None, NO_Q, None, rows, inner, C)
+        ops.chain_bwd_b(b)
+        return dx
+
+    def info(self):
+        return "BatchNorm normalization"
+
+
+class Rescale_q(Layer_q):
+    """BN rescale half (``:626-694``): y = Q(X) * Q(gamma) + Q(beta)."""
+
+    def __init__(self, name, bits, num_features, weight_decay=0, target_overflow_rate=0, input_range=2,
+                 gamma_range=2, beta_range=2, grad_range=2, ctx=None):
+        self.ctx = ctx = ctx or default_context()
+        self.name, self.bits, self.C, self.weight_decay = name, bits, num_features, weight_decay
+        self.target_overflow_rate = target_overflow_rate
+        dev = ctx.device
+        self.gamma = torch.ones(num_features, dtype=torch.float32, device=dev)
+        self.beta = torch.zeros(num_features, dtype=torch.float32, device=dev)
+        self.dgamma = torch.zeros_like(self.gamma)
+        self.dbeta = torch.zeros_like(self.beta)
+        t = target_overflow_rate
+        self.g_range = ctx.quantizer(name + "/g_range", bits, gamma_range, t)
+        self.b_range = ctx.quantizer(name + "/b_range", bits, beta_range, t)
+        self.X_range = ctx.quantizer(name + "/X_range", bits, input_range, t)
+        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, t)
+        self.gb = torch.zeros(2 * num_features, dtype=torch.float32, device=dev)
+        self._c = _Cache()
+
+    def param_slots(self):
+        return [(self, "gamma", "dgamma"), (self, "beta", "dbeta")]
+
+    def quantize_params(self):
+        C = self.C
+        ops.quantize(self.gamma, self.g_range, OUT_F32, out=self.gb[:C])
+        ops.quantize(self.beta, self.b_range, OUT_F32, out=self.gb[C:])
+
+    def forward(self, X):
+        self.X = X
+        dev = X.device
+        C = self.C
+        rows, inner = ops.rows_inner(tuple(X.shape))
+        self.quantize_params()
+        self.R = self._c.get("R", X.shape, torch.int8, dev)
+        y = self._c.get("y", X.shape, torch.float32, dev)
+        self.X_range.observe(X.numel())
+        a = ChainFwd()
+        a.b1.xin = X.data_ptr()
+        a.b1.qr = self.X_range.desc
+        a.b1.rout = self.R.data_ptr()
+        a.b1.gb = self.gb.data_ptr()
+        a.y = y.data_ptr()
+        a.rows, a.inner, a.C = rows, inner, C
+        ops.chain_fwd(a)
+        self.y = y
+        return y
+
+    def backward(self, grad, stochastic=True):
+        dev = grad.device
+        C = self.C
+        rows, inner = ops.rows_inner(tuple(grad.shape))
+        sums = self._c.get("sums", (ops.NSHARD * 4 * C,), torch.int64, dev)
+        sums.zero_()
+        dx = self._c.get("dx", grad.shape, torch.float32, dev)
+        self.grad_range.observe(grad.numel())
+        a = ChainBwdA()
+        a.g = grad.data_ptr()
+        a.b1 = BwdBranch(self.grad_range.desc, self.R.data_ptr(), self.X_range.desc, self.gb.data_ptr(), NO_Q,
+                         None, None, dx.data_ptr(), sums.data_ptr())
+        a.rows, a.inner, a.C = rows, inner, C
+        ops.chain_bwd_a(a)
+        ops.bn_param_grads(sums, C, self.grad_range.desc, self.X_range.desc, self.gamma,
+                           ops.f32(2 * self.weight_decay), self.dgamma, self.dbeta)
+        return dx
+
+    def grads_and_vars(self):
+        return [(self.dgamma, self.gamma), (self.dbeta, self.beta)]
+
+    def info(self):
+        return "BatchNorm rescale"
+
+
+class BatchNorm_q(Sequential_q):
+    """``Sequential_q(Normalization_q(name-norm), Rescale_q(name-rescale))`` (``:697-743``)."""
+
+    def __init__(self, name, bits, num_features, training=True, momentum=0.999, eps=1e-5, weight_decay=0,
+                 target_overflow_rate=0, input_range=2, gamma_range=2, beta_range=2, grad_range=2, ctx=None):
+        super().__init__(
+            Normalization_q(name=name + "-norm", bits=bits, num_features=num_features, training=training,
+                            momentum=momentum, eps=eps, target_overflow_rate=target_overflow_rate,
+                            input_range=input_range, grad_range=grad_range, ctx=ctx),
+            Rescale_q(name=name + "-rescale", bits=bits, num_features=num_features, weight_decay=weight_decay,
+                      target_overflow_rate=target_overflow_rate, input_range=2, gamma_range=gamma_range,
+                      beta_range=beta_range, grad_range=grad_range, ctx=ctx))
+
+    def info(self):
+        return "BatchNorm"
+
+
+class ReLU_q(Layer_q):
+    def __init__(self):
+        self._c = _Cache()
+
+    def forward(self, X):
+        self.X = X
+        self.y = self._c.get("y", X.shape, torch.float32, X.device)
+        ops.relu_fwd(X, self.y)
+        return self.y
+
+    def backward(self, grad, stochastic=True):
+        dx = self._c.get("dx", grad.shape, torch.float32, grad.device)
+        ops.relu_bwd(grad, self.X, dx)
+        return dx
+
+    def info(self):
+        return "ReLU"
+
+
+class ResidualBlock_q(Layer_q):
+    """Basic residual block (``:746-875``): conv-BN-ReLU-conv-BN + (identity | 1x1 conv-BN), ReLU."""
+    expansion = 1
+
+    def __init__(self, name, bits, in_channels, channels, stride, training=True, batch_norm=True, weight_decay=0,
+                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, ctx=None):
+        self.train = training
+        self.name = name
+        common = dict(bits=bits, use_bias=not batch_norm, weight_decay=weight_decay, input_range=input_range,
+                      weight_range=weight_range, bias_range=bias_range, grad_range=grad_range,
+                      input_nonnegative=True, ctx=ctx)
+        bn = dict(bits=bits, num_features=channels, training=training, weight_decay=weight_decay,
+                  target_overflow_rate=target_overflow_rate, input_range=input_range, grad_range=grad_range, ctx=ctx)
+        self.residual = Sequential_q(
+            Conv2d_q(name=name + "-1", ksize=[3, 3, in_channels, channels], strides=[1, stride, stride, 1],
+                     padding="SAME", **common),
+            BatchNorm_q(name=name + "-bn1", **bn) if batch_norm else Layer_q(),
+            ReLU_q(),
+            Conv2d_q(name=name + "-2", ksize=[3, 3, channels, channels], strides=[1, 1, 1, 1], padding="SAME",
+                     **common),
+            BatchNorm_q(name=name + "-bn2", **bn) if batch_norm else Layer_q(),
+        )
+        if stride == 1 and in_channels == self.expansion * channels:
+            self.shortcut = Sequential_q()
+        else:
+            self.shortcut = Sequential_q(
+                Conv2d_q(name=name + "-shortcut", ksize=[1, 1, in_channels, self.expansion * channels],
+                         strides=[1, stride, stride, 1], padding="SAME", target_overflow_rate=target_overflow_rate,
+                         **common),
+                BatchNorm_q(name=name + "-shortcut-bn", **bn) if batch_norm else Layer_q(),
+            )
+        self.relu = ReLU_q()
+        self._c = _Cache()
+
+    def forward(self, X):
+        self.X = X
+        self.y1 = self.residual.forward(X)
+        self.y2 = self.shortcut.forward(X)
+        s = self._c.get("sum", self.y1.shape, torch.float32, X.device)
+        ops.add(self.y1, self.y2, s)
+        self.y = self.relu.forward(s)
+        return self.y
+
+    def backward(self, grad, stochastic=True):
+        grad = self.relu.backward(grad, stochastic)
+        g1 = self.residual.backward(grad, stochastic)
+        g2 = self.shortcut.backward(grad, stochastic)
+        out = self._c.get("dx", g1.shape, torch.float32, grad.device)
+        ops.add(g1, g2, out)
+        return out
+
+    def grads_and_vars(self):
+        return self.residual.grads_and_vars() + self.shortcut.grads_and_vars()
+
+    def param_slots(self):
+        return self.residual.param_slots() + self.shortcut.param_slots()
+
+    def info(self):
+        return "Residual block with " + self.residual.info()
+
+
+class AvgPool_q(Layer_q):
+    """Average pool over the whole feature map (``:1009-1022`` as used by ResNet: 8x8 VALID)."""
+
+    def __init__(self, ksize, strides, padding):
+        self.ksize, self.strides, self.padding = ksize, strides, padding
+        self._c = _Cache()
+
+    def forward(self, X):
+        N, H, W, C = X.shape
+        if self.padding != "VALID" or self.ksize[1] != H or self.ksize[2] != W:
+            raise NotImplementedError("AvgPool_q: only global (ksize == map) VALID pooling is on the hot path")
+        self.X = X
+        y = self._c.get("y", (N, 1, 1, C), torch.float32, X.device)
+        ops.avgpool_fwd(X, y, N, H * W, C)
+        self.y = y
+        return y
+
+    def backward(self, grad, stochastic=True):
+        N, H, W, C = self.X.shape
+        dx = self._c.get("dx", self.X.shape, torch.float32, grad.device)
+        ops.avgpool_bwd(grad.contiguous(), dx, N, H * W, C)
+        return dx
+
+    def info(self):
+        return "avg pool: %dx%d stride %dx%d" % (self.ksize[1], self.ksize[2], self.strides[1], self.strides[2])
+
+
+class Flatten_q(Layer_q):
+    def __init__(self, dim):
+        self.dim = dim
+
+    def forward(self, X):
+        self.X = X
+        self.y = X.reshape(-1, self.dim)
+        return self.y
+
+    def backward(self, grad, stochastic=True):
+        return grad.reshape(self.X.shape)
+
+    def info(self):
+        return "flatten"

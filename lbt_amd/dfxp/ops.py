@@ -1,0 +1,199 @@
+"""Typed wrappers over the C-ABI (include/lbt_dfxp.h). Tensors in, kernels launched on the
+current torch stream, nothing synchronised. All shape logic of the HIP path lives here."""
+import math
+
+import torch
+
+from .. import _lib
+from .._lib import NSHARD, OUT_F32, OUT_I8, OUT_I16, OUT_U8OFF, ConvDesc, QDesc, call, ptr, stream
+
+NO_Q = _lib.NO_Q
+
+
+def _check(t, dtype, name):
+    if not t.is_cuda:
+        raise ValueError("%s must be a CUDA (HIP) tensor" % name)
+    if t.dtype != dtype:
+        raise ValueError("%s must be %s, got %s" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+
+
+def rows_inner(shape):
+    """(rows, inner) of the reference's noise broadcast: noise over shape[1:], rows = shape[0]."""
+    if len(shape) <= 1:
+        return (int(shape[0]) if len(shape) else 1), 1
+    return int(shape[0]), int(math.prod(shape[1:]))
+
+
+def out_dtype(kind):
+    return {OUT_I8: torch.int8, OUT_U8OFF: torch.int8, OUT_I16: torch.int16, OUT_F32: torch.float32}[kind]
+
+
+def new_sums(C, per_shard, device):
+    return torch.zeros(NSHARD * per_shard * C, dtype=torch.int64, device=device)
+
+
+# ----------------------------------------------------------------------------- quantiser
+def quantize(x, q, kind, out=None, chsum=None, C=0, stats=True):
+    """weight_quantization of x with quantiser q (dynamic_fixed_point.py:4-45) -> codes in `kind`."""
+    _check(x, torch.float32, "x")
+    rows, inner = rows_inner(tuple(x.shape))
+    if out is None:
+        out = torch.empty(x.shape, dtype=out_dtype(kind), device=x.device)
+    if stats:
+        q.observe(x.numel())
+    desc = q.desc if stats else q.desc_nostats()
+    call("lbt_dfxp_quantize", ptr(x), ptr(out), kind, rows, inner, desc, ptr(chsum), int(C), stream())
+    return out
+
+
+def quantize_weight(w, q, w_hwio=None, wf=None, ksf=0, wd=None, ksd=0, colsum=None):
+    """Weight quantiser + GEMM operand packing. w: fp32 HWIO [KH,KW,Cin,Cout] (or [in,out])."""
+    _check(w, torch.float32, "w")
+    if w.dim() == 2:
+        KH = KW = 1
+        Cin, Cout = w.shape
+    else:
+        KH, KW, Cin, Cout = w.shape
+    q.observe(w.numel())
+    call("lbt_dfxp_quantize_weight", ptr(w), KH, KW, Cin, Cout, q.desc, ptr(w_hwio), ptr(wf), int(ksf), ptr(wd),
+         int(ksd), ptr(colsum), stream())
+
+
+def packed_slices(KH, KW, C):
+    """16-byte k-slices per GEMM column for a tap-major (tap, 16-channel slice) k order, padded to 4."""
+    s = KH * KW * ((C + 15) // 16)
+    return (s + 3) // 4 * 4
+
+
+# ----------------------------------------------------------------------------- conv geometry
+def tf_same(in_size, k, s):
+    out = -(-in_size // s)
+    total = max((out - 1) * s + k - in_size, 0)
+    return out, total // 2, total - total // 2
+
+
+def conv_desc(N, H, W, Cin, Cout, KH, KW, SH, SW, padding):
+    """TF 'SAME' / 'VALID' (dynamic_fixed_point.py:291 tf.nn.conv2d) or explicit symmetric int
+    padding (the torch face), resolved to (top, bottom, left, right)."""
+    if padding == "SAME":
+        Ho, pt, pb = tf_same(H, KH, SH)
+        Wo, pl, pr = tf_same(W, KW, SW)
+    elif padding == "VALID":
+        Ho = -(-(H - KH + 1) // SH)
+        Wo = -(-(W - KW + 1) // SW)
+        pt = pb = pl = pr = 0
+    else:
+        ph, pw = (padding, padding) if isinstance(padding, int) else padding
+        pt = pb = ph
+        pl = pr = pw
+        Ho = (H + 2 * ph - KH) // SH + 1
+        Wo = (W + 2 * pw - KW) // SW + 1
+    if Ho <= 0 or Wo <= 0:
+        raise ValueError("empty conv output for input %dx%d kernel %dx%d" % (H, W, KH, KW))
+    return ConvDesc(N, H, W, Cin, Cout, KH, KW, SH, SW, pt, pb, pl, pr, Ho, Wo)
+
+
+def mfma_ok(Cin, Cout):
+    return Cin % 16 == 0 and Cout % 16 == 0 and Cin <= 128 and Cout <= 128
+
+
+def conv_fwd_i8(xq, x_u8off, wf, ksf, wcolsum, d, qx, qw, y=None, yq=None, qout=None, ychsum=None):
+    call("lbt_conv_fwd_i8", ptr(xq), int(x_u8off), ptr(wf), int(ksf), ptr(wcolsum), d, qx, qw, ptr(y), ptr(yq),
+         qout if qout is not None else NO_Q, ptr(ychsum), stream())
+
+
+def conv_dgrad_i8(gq, wd, ksd, d, qg, qw, dx, add_src=None):
+    call("lbt_conv_dgrad_i8", ptr(gq), ptr(wd), int(ksd), d, qg, qw, ptr(dx), ptr(add_src), stream())
+
+
+def wgrad_nsplit(d, generic=False):
+    P = d.N * d.Ho * d.Wo
+    taps = d.KH * d.KW
+    if generic:
+        lo = -(-P // 8192)
+        return max(lo, min(256, -(-P // 32)))
+    lo = -(-P // 65536)
+    want = max(1, -(-512 // taps))
+    return max(lo, min(want, max(1, P // 256)))
+
+
+def conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit):
+    call("lbt_conv_wgrad_i8", ptr(xq), int(x_u8off), ptr(gq), d, ptr(slab), int(nsplit), stream())
+
+
+def conv_wgrad_reduce(slab, nsplit, K, Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw):
+    call("lbt_conv_wgrad_reduce", ptr(slab), int(nsplit), int(K), int(Cout), int(x_u8off), ptr(gcolsum), qx, qg,
+         ptr(w), float(wd2), ptr(dw), stream())
+
+
+def conv_fwd_generic(xq, x_i16, w_hwio, d, qx, qw, y):
+    call("lbt_conv_fwd_generic", ptr(xq), int(x_i16), ptr(w_hwio), d, qx, qw, ptr(y), stream())
+
+
+def conv_dgrad_generic(gq, w_hwio, d, qg, qw, dx, add_src=None):
+    call("lbt_conv_dgrad_generic", ptr(gq), ptr(w_hwio), d, qg, qw, ptr(dx), ptr(add_src), stream())
+
+
+def conv_wgrad_generic(xq, x_i16, gq, d, slab, nsplit):
+    call("lbt_conv_wgrad_generic", ptr(xq), int(x_i16), ptr(gq), d, ptr(slab), int(nsplit), stream())
+
+
+# ----------------------------------------------------------------------------- BN chains
+def chain_fwd(desc):
+    call("lbt_bn_chain_fwd", _lib.ctypes.byref(desc), stream())
+
+
+def chain_bwd_a(desc):
+    call("lbt_bn_chain_bwd_a", _lib.ctypes.byref(desc), stream())
+
+
+def chain_bwd_b(desc):
+    call("lbt_bn_chain_bwd_b", _lib.ctypes.byref(desc), stream())
+
+
+def bn_param_grads(sums, C, qrg, qr, gamma, wd2, dgamma, dbeta):
+    call("lbt_bn_param_grads", ptr(sums), int(C), qrg, qr, ptr(gamma), float(wd2), ptr(dgamma), ptr(dbeta), stream())
+
+
+# ----------------------------------------------------------------------------- glue
+def relu_fwd(x, y):
+    call("lbt_relu_fwd", ptr(x), ptr(y), x.numel(), stream())
+
+
+def relu_bwd(g, x, dx):
+    call("lbt_relu_bwd", ptr(g), ptr(x), ptr(dx), g.numel(), stream())
+
+
+def add(a, b, y):
+    call("lbt_add", ptr(a), ptr(b), ptr(y), a.numel(), stream())
+
+
+def avgpool_fwd(x, y, N, HW, C):
+    call("lbt_avgpool_fwd", ptr(x), ptr(y), int(N), int(HW), int(C), stream())
+
+
+def avgpool_bwd(g, dx, N, HW, C):
+    call("lbt_avgpool_bwd", ptr(g), ptr(dx), int(N), int(HW), int(C), stream())
+
+
+def softmax_xent(z, labels, loss, dz):
+    N, K = z.shape
+    call("lbt_softmax_xent", ptr(z), ptr(labels), int(N), int(K), ptr(loss), ptr(dz), stream())
+
+
+def sgd_momentum(w, a, g, lr, mu, gscale=1.0):
+    call("lbt_sgd_momentum", ptr(w), ptr(a), ptr(g), w.numel(), float(lr), float(mu), float(gscale), stream())
+
+
+def bias_add(y, bq, C):
+    call("lbt_bias_add", ptr(y), ptr(bq), y.numel(), int(C), stream())
+
+
+def bias_grad(chsum, C, qg, db):
+    call("lbt_bias_grad", ptr(chsum), int(C), qg, ptr(db), stream())
+
+
+def f32(x):
+    return torch.tensor(x, dtype=torch.float32).item()

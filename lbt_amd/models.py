@@ -1,0 +1,116 @@
+"""Models of the reference (``models.py``) on the gfx950 DFXP layers.
+
+``Model`` mirrors ``models.py:7-54``: it owns the layer list, runs the forward pass, the mean
+sparse softmax cross-entropy (``:30-32``) and the manual backward from d loss / d logits through
+``reversed(layers)`` (``:47-51``). ``CIFAR10_Resnet`` / ``CIFAR10_Resnet20/32/44/56`` mirror
+``:371-470``. Inputs are NHWC fp32 CUDA tensors, labels int32.
+"""
+import torch
+
+from . import dynamic_fixed_point as L
+from .dfxp import ops
+from .dfxp.layers import _Cache
+from .runtime import default_context
+
+
+class Model:
+    def __init__(self, bits, input_shape, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
+        self.bits = bits
+        self.input_shape = input_shape
+        self.dropout = dropout
+        self.weight_decay = weight_decay
+        self.stochastic = stochastic
+        self.ctx = ctx or default_context()
+        self.training = True
+        self.layers = self.get_layers()
+        self._c = _Cache()
+        self.logits = None
+        self.loss = None
+
+    def get_layers(self):
+        return []
+
+    def forward(self, X):
+        for layer in self.layers:
+            X = layer.forward(X)
+        self.logits = X
+        return X
+
+    def compute_loss(self, labels):
+        """loss = mean(sparse_softmax_cross_entropy(labels, logits)); keeps d loss / d logits."""
+        z = self.logits
+        self.loss = self._c.get("loss", (1,), torch.float32, z.device)
+        self.dlogits = self._c.get("dz", z.shape, torch.float32, z.device)
+        ops.softmax_xent(z, labels, self.loss, self.dlogits)
+        return self.loss
+
+    def accuracy(self, labels):
+        return (self.logits.argmax(dim=1).to(torch.int32) == labels).float().mean()
+
+    def backward(self):
+        grad = self.dlogits
+        for layer in reversed(self.layers):
+            grad = layer.backward(grad, self.stochastic)
+        return grad
+
+    def grads_and_vars(self):
+        res = []
+        for layer in self.layers:
+            res += layer.grads_and_vars()
+        return res
+
+    def param_slots(self):
+        return [s for layer in self.layers for s in layer.param_slots()]
+
+    def info(self):
+        return "\n".join([layer.info() for layer in self.layers])
+
+
+class CIFAR10_Resnet(Model):
+    def __init__(self, bits, num_blocks, block, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
+        self.num_blocks = num_blocks
+        self.block = block
+        super().__init__(bits, [None, 32, 32, 3], dropout, weight_decay, stochastic, ctx)
+
+    def _build_blocks(self, channels, num_blocks, stride):
+        blocks = []
+        for i in range(1, 1 + num_blocks):
+            blocks.append(self.block(name="block%d-%d" % (channels, i), bits=self.bits, in_channels=self.channels,
+                                     channels=channels, stride=1 if i > 1 else stride, training=self.training,
+                                     weight_decay=self.weight_decay, ctx=self.ctx))
+            self.channels = channels * self.block.expansion
+        return blocks
+
+    def get_layers(self):
+        self.channels = 16
+        return [
+            L.Conv2d_pq(name="conv1", bits=self.bits, ksize=[3, 3, 3, 16], strides=[1, 1, 1, 1], padding="SAME",
+                        use_bias=False, weight_decay=self.weight_decay, ctx=self.ctx),
+            L.BatchNorm_q(name="conv1-bn", bits=self.bits, num_features=16, training=self.training,
+                          weight_decay=self.weight_decay, ctx=self.ctx),
+            L.ReLU_q(),
+        ] + self._build_blocks(16, self.num_blocks[0], 1) \
+          + self._build_blocks(32, self.num_blocks[1], 2) \
+          + self._build_blocks(64, self.num_blocks[2], 2) \
+          + [
+            L.AvgPool_q(ksize=[1, 8, 8, 1], strides=[1, 1, 1, 1], padding="VALID"),
+            L.Flatten_q(64),
+            L.Dense_q(name="softmax", bits=self.bits, in_units=64, units=10, use_bias=False,
+                      weight_decay=self.weight_decay, ctx=self.ctx),
+        ]
+
+
+def CIFAR10_Resnet20(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
+    return CIFAR10_Resnet(bits, [3, 3, 3], L.ResidualBlock_q, dropout, weight_decay, stochastic, ctx)
+
+
+def CIFAR10_Resnet32(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
+    return CIFAR10_Resnet(bits, [5, 5, 5], L.ResidualBlock_q, dropout, weight_decay, stochastic, ctx)
+
+
+def CIFAR10_Resnet44(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
+    return CIFAR10_Resnet(bits, [7, 7, 7], L.ResidualBlock_q, dropout, weight_decay, stochastic, ctx)
+
+
+def CIFAR10_Resnet56(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
+    return CIFAR10_Resnet(bits, [9, 9, 9], L.ResidualBlock_q, dropout, weight_decay, stochastic, ctx)

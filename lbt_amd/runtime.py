@@ -1,0 +1,149 @@
+"""Device-resident DFXP state: the build's counterpart of the reference's range variables.
+
+In the reference every quantised tensor has an int32 TF variable ``<layer>/<X|W|grad|...>_range``
+(the integer bits I, ``dynamic_fixed_point.py:161-171,256-266,...``) and
+``weight_quantization`` adds an ``update_range`` op to the graph collection
+``'update_range'`` (``:40-41``) that the trainer fetches with every step
+(``trainer.py:63,157``).
+
+Here one ``DfxpContext`` owns, in device memory,
+  exps   int32 [capacity]                 I per quantiser slot
+  counts int32 [capacity, NSHARD, 2]      overflow counters accumulated by the kernels
+  step   int64 [1]                        noise counter (incremented by every range update)
+  bits / target / nelem                   per-slot controller constants
+and ``update_range_op()`` is the collection: ONE kernel that applies update_range to every
+slot. Nothing is read back to the host during a step, so a whole step can be captured in a
+HIP graph.
+"""
+import zlib
+
+import torch
+
+from . import _lib
+from ._lib import NSHARD, QDesc
+
+
+def qid_of(name):
+    """Stable 31-bit noise-stream id of a quantiser, from its range variable's name."""
+    return zlib.crc32(name.encode("utf-8")) & 0x7FFFFFFF
+
+
+class Quantizer:
+    """One DFXP quantiser slot: name, bits, rounding mode; its I lives in ``ctx.exps[slot]``."""
+
+    def __init__(self, ctx, name, slot, bits, stochastic, target):
+        self.ctx, self.name, self.slot, self.bits = ctx, name, slot, int(bits)
+        self.stochastic, self.target = bool(stochastic), float(target)
+        self.qid = qid_of(name)
+        self._nelem = None
+        self._desc = None
+
+    @property
+    def desc(self):
+        if self._desc is None:
+            c = self.ctx
+            self._desc = QDesc(c.exps.data_ptr(), c.counts.data_ptr(), c.step.data_ptr(), c.seed, self.qid,
+                               self.slot, self.bits, 1 if self.stochastic else 0)
+        return self._desc
+
+    def desc_nostats(self):
+        d = QDesc.from_buffer_copy(self.desc)
+        d.counts = None
+        return d
+
+    def observe(self, nelem):
+        """Declare how many elements this quantiser sees per step (update_range's mean)."""
+        n = int(nelem) * self.ctx.world_size
+        if n != self._nelem:
+            self._nelem = n
+            self.ctx.nelem[self.slot] = float(n)
+
+    @property
+    def integer_bits(self):
+        return int(self.ctx.exps[self.slot].item())
+
+    def __repr__(self):
+        return "Quantizer(%s, bits=%d, slot=%d)" % (self.name, self.bits, self.slot)
+
+
+class DfxpContext:
+    def __init__(self, device="cuda", capacity=1024, seed=0, world_size=1):
+        self.device = torch.device(device)
+        self.capacity = capacity
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.world_size = int(world_size)
+        dev = self.device
+        self.exps = torch.zeros(capacity, dtype=torch.int32, device=dev)
+        self.counts = torch.zeros(capacity * NSHARD * 2, dtype=torch.int32, device=dev)
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.bits = torch.zeros(capacity, dtype=torch.int32, device=dev)
+        self.target = torch.zeros(capacity, dtype=torch.float32, device=dev)
+        self.nelem = torch.zeros(capacity, dtype=torch.float32, device=dev)
+        self.quantizers = []
+        self.by_name = {}
+
+    def quantizer(self, name, bits, initial=2, target=0.0, stochastic=True):
+        """Register a quantiser (a ``*_range`` variable initialised to ``initial``)."""
+        if name in self.by_name:
+            raise ValueError("duplicate DFXP range variable %r" % name)
+        if not 2 <= bits <= 16:
+            raise ValueError("DFXP bits must be in [2, 16] on this path, got %d" % bits)
+        if not 0 <= bits - initial - 1 <= 30:
+            raise ValueError("initial range %d invalid for %d bits (reference: 2**(bits-I-1) in int32)"
+                             % (initial, bits))
+        slot = len(self.quantizers)
+        if slot >= self.capacity:
+            raise RuntimeError("DfxpContext capacity exhausted")
+        q = Quantizer(self, name, slot, bits, stochastic, target)
+        self.exps[slot] = int(initial)
+        self.bits[slot] = int(bits)
+        self.target[slot] = float(target)
+        self.quantizers.append(q)
+        self.by_name[name] = q
+        return q
+
+    # the 'update_range' collection (trainer.py:63,157)
+    def update_range_op(self):
+        n = len(self.quantizers)
+        _lib.call("lbt_dfxp_range_update", _lib.ptr(self.exps), _lib.ptr(self.counts), _lib.ptr(self.bits),
+                  _lib.ptr(self.target), _lib.ptr(self.nelem), n, _lib.ptr(self.step), _lib.stream())
+
+    def counts_view(self):
+        return self.counts.view(self.capacity, NSHARD, 2)[: len(self.quantizers)]
+
+    def ranges(self):
+        """{range variable name: I} (host read -- not for the timed loop)."""
+        e = self.exps[: len(self.quantizers)].cpu().tolist()
+        return {q.name: int(v) for q, v in zip(self.quantizers, e)}
+
+    def set_ranges(self, ranges):
+        for name, v in ranges.items():
+            self.exps[self.by_name[name].slot] = int(v)
+
+    def state_dict(self):
+        return {"exps": self.exps.clone(), "step": self.step.clone(),
+                "names": [q.name for q in self.quantizers]}
+
+    def load_state_dict(self, sd):
+        names = [q.name for q in self.quantizers]
+        if list(sd["names"]) != names:
+            raise ValueError("quantiser layout mismatch")
+        self.exps.copy_(sd["exps"])
+        self.step.copy_(sd["step"])
+
+
+_default = None
+
+
+def default_context():
+    """The process-wide context (the counterpart of TF's default graph)."""
+    global _default
+    if _default is None:
+        _default = DfxpContext()
+    return _default
+
+
+def set_default_context(ctx):
+    global _default
+    _default = ctx
+    return ctx

@@ -1,0 +1,172 @@
+"""The timed training step of the reference (``trainer.py:109-162``) on the HIP path.
+
+One ``Trainer.step(X, y)`` = ``sess.run([train_op, update_range_op])`` of ``trainer.py:157``:
+forward, loss, manual backward, ``MomentumOptimizer.apply_gradients`` (``acc = mu*acc + g;
+w -= lr*acc``, ``trainer.py:79-84``) and the ``'update_range'`` collection.
+
+MI355X-native execution:
+* all trainable variables live in ONE flat fp32 buffer (and their gradients / momentum in two
+  more), so the optimiser is a single kernel and the data-parallel exchange is one all-reduce;
+* after a warm-up step the whole step is captured into a HIP graph (``torch.cuda.CUDAGraph``)
+  and replayed: ~300 kernel launches become one graph launch;
+* data parallelism (``torch.distributed``, backend ``nccl`` = RCCL over xGMI): each rank runs
+  the step on its own batch shard; between the backward graph and the update graph ONE
+  all-reduce sums the flat gradient buffer and, in the same call, the quantisers' overflow
+  counters (packed as fp32), so every rank applies identical updates and identical DFXP
+  exponents. Noise keys (seed, step, quantiser) do not depend on the rank.
+"""
+import torch
+import torch.distributed as dist
+
+from .dfxp import ops
+from ._lib import NSHARD
+
+
+class FlatParams:
+    """Bind every (var, grad) of a model into contiguous flat buffers (grads_and_vars order)."""
+
+    def __init__(self, model):
+        slots = model.param_slots()
+        dev = model.ctx.device
+        sizes = [getattr(o, v).numel() for o, v, _ in slots]
+        n = sum(sizes)
+        self.n = n
+        self.w = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.g = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.a = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        self.offsets = []
+        for (o, v, gname), sz in zip(slots, sizes):
+            t = getattr(o, v)
+            wv = self.w[off:off + sz].view(t.shape)
+            wv.copy_(t)
+            setattr(o, v, wv)
+            setattr(o, gname, self.g[off:off + sz].view(t.shape))
+            self.offsets.append((o, v, off, sz))
+            off += sz
+
+
+class Trainer:
+    def __init__(self, model, dataset=None, logger=None, logdir=None, lr=1e-2, lr_decay_factor=0.5,
+                 lr_decay_epoch=50, momentum=0.95, n_epoch=5, batch_size=128, use_graph=True,
+                 process_group=None):
+        self.model = model
+        self.dataset = dataset
+        self.logger = logger
+        self.lr, self.momentum = lr, momentum
+        self.lr_decay_factor, self.lr_decay_epoch = lr_decay_factor, lr_decay_epoch
+        self.n_epoch, self.batch_size = n_epoch, batch_size
+        self.use_graph = use_graph
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.ctx = model.ctx
+        if self.world != self.ctx.world_size:
+            raise ValueError("DfxpContext.world_size (%d) must equal the process-group size (%d)"
+                             % (self.ctx.world_size, self.world))
+        self.flat = FlatParams(model)
+        self.global_step = 0
+        self._graphs = None
+        self._static = None
+        # fp32 comm buffer: [grads | overflow counters] -> ONE all-reduce per step
+        nq = len(self.ctx.quantizers)
+        self._ncnt = nq * NSHARD * 2
+        if self.world > 1:
+            self.comm = torch.zeros(self.flat.n + self._ncnt, dtype=torch.float32, device=self.ctx.device)
+        if logger is not None:
+            logger.info("Model info:\n" + model.info())
+
+    # -- the reference's API ---------------------------------------------------------------
+    def init_model(self):
+        self.flat.a.zero_()
+
+    def get_train_op(self):
+        """Rebuilding MomentumOptimizer resets its accumulators (trainer.py:79-84)."""
+        self.flat.a.zero_()
+        self._graphs = None  # lr is baked into the captured optimiser kernel
+        return self.step
+
+    # -- the step ----------------------------------------------------------------------------
+    def _fwd_bwd(self, X, y):
+        m = self.model
+        m.forward(X)
+        m.compute_loss(y)
+        m.backward()
+
+    def _exchange(self):
+        """Sum grads + overflow counters across ranks (RCCL); counts travel as exact fp32."""
+        n = self.flat.n
+        cnt = self.ctx.counts[: self._ncnt]
+        self.comm[:n].copy_(self.flat.g)
+        self.comm[n:].copy_(cnt)
+        dist.all_reduce(self.comm, group=self.pg)
+        self.flat.g.copy_(self.comm[:n])
+        cnt.copy_(self.comm[n:])
+
+    def _update(self):
+        ops.sgd_momentum(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0 / self.world)
+        self.ctx.update_range_op()
+
+    def _eager(self, X, y):
+        self._fwd_bwd(X, y)
+        if self.world > 1:
+            self._exchange()
+        self._update()
+
+    def _capture(self, X, y):
+        self._static = (torch.empty_like(X), torch.empty_like(y))
+        sX, sy = self._static
+        sX.copy_(X)
+        sy.copy_(y)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            # warm-up: allocates every per-layer buffer outside the capture
+            self._fwd_bwd(sX, sy)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        # undo the warm-up's side effects on the DFXP counters (no update was applied)
+        self.ctx.counts.zero_()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            self._fwd_bwd(sX, sy)
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2):
+            self._update()
+        self._graphs = (g1, g2)
+
+    def step(self, X, y):
+        """One training step on batch (X [B,32,32,3] fp32 NHWC, y [B] int32), device tensors."""
+        if not self.use_graph:
+            self._eager(X, y)
+        else:
+            if self._graphs is None or self._static[0].shape != X.shape:
+                self._capture(X, y)
+            else:
+                self._static[0].copy_(X)
+                self._static[1].copy_(y)
+            g1, g2 = self._graphs
+            g1.replay()
+            if self.world > 1:
+                self._exchange()
+            g2.replay()
+        self.global_step += 1
+        return self.model.loss
+
+    def train(self):
+        """Epoch loop of trainer.py:117-162 over an in-memory dataset ((Xtr, ytr), (Xte, yte))."""
+        (Xtr, ytr), _ = self.dataset
+        dev = self.ctx.device
+        for epoch in range(self.n_epoch):
+            if epoch == 0:
+                self.get_train_op()
+            elif epoch in (80, 120, 140):
+                self.lr *= self.lr_decay_factor
+                self.get_train_op()
+            perm = torch.randperm(len(Xtr))
+            for b in range(0, len(Xtr) - self.batch_size + 1, self.batch_size):
+                idx = perm[b:b + self.batch_size]
+                X = torch.as_tensor(Xtr[idx.numpy()], dtype=torch.float32).to(dev).contiguous()
+                y = torch.as_tensor(ytr[idx.numpy()], dtype=torch.int32).to(dev)
+                loss = self.step(X, y)
+                if self.logger is not None and (b // self.batch_size + 1) % 100 == 0:
+                    self.logger.info("Batch %d loss %f" % (b // self.batch_size + 1, loss.item()))

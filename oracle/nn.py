@@ -1,0 +1,417 @@
+"""Quantised layers of the DFXP path in numpy (oracle; test infrastructure only).
+
+Each class restates one reference layer (``dynamic_fixed_point.py``) with the
+Layer_q protocol ``forward(X) / backward(grad) / grads_and_vars()``:
+
+* Conv2dQ    -- ``Conv2d_q`` / ``Conv2d_pq`` ``:129-316`` (X at bits+1, W at bits,
+                grad at bits; dW = wgrad(Xq, gq) + 2*wd*W; dX = dgrad(gq, Wq)).
+* DenseQ     -- ``Dense_q`` ``:319-470`` (X, W, grad all at bits).
+* NormQ      -- ``Normalization_q`` ``:539-623`` (biased batch moments of Xq,
+                eps 1e-5, running averages momentum 0.999; full BN backward).
+* RescaleQ   -- ``Rescale_q`` ``:626-694`` (y = Xq*gq + bq; dgamma = sum gq*Xq + 2wd*gamma).
+* BatchNormQ -- ``BatchNorm_q`` ``:697-743`` (Sequential(Norm, Rescale)).
+* ReluQ / AvgPoolQ / FlattenQ / SequentialQ / ResidualBlockQ -- ``:983-1053``,
+                ``:512-536``, ``:746-875``.
+
+Integer arithmetic: integer GEMMs (conv fwd/dgrad/wgrad, dense) are computed
+exactly (float64 BLAS on integer-valued operands, all partial sums < 2**53) and
+dequantised once: ``float32(acc) * 2**-(e_a+e_b)``. TF sums the same integer
+products in fp32; the two agree whenever the partial sums stay below 2**24 LSB.
+BN moments and BN/Rescale backward reductions are taken from exact integer sums
+of the quantised codes (see DESIGN.md "Numerics"): they are the same quantities
+the reference computes with ``tf.nn.moments`` / ``tf.gradients``, without
+order-dependent fp32 summation.
+"""
+import numpy as np
+
+from . import dfxp
+
+F32 = np.float32
+
+
+def tf_same_pads(in_size, k, s):
+    """TF 'SAME' padding (before, after) and output size."""
+    out = -(-in_size // s)
+    total = max((out - 1) * s + k - in_size, 0)
+    return out, total // 2, total - total // 2
+
+
+def conv_geometry(H, W, kh, kw, sh, sw, padding):
+    if padding == "SAME":
+        Ho, pt, pb = tf_same_pads(H, kh, sh)
+        Wo, pl, pr = tf_same_pads(W, kw, sw)
+    elif padding == "VALID":
+        Ho = -(-(H - kh + 1) // sh)
+        Wo = -(-(W - kw + 1) // sw)
+        pt = pb = pl = pr = 0
+    else:
+        raise ValueError(padding)
+    return Ho, Wo, pt, pb, pl, pr
+
+
+def _windows(x, kh, kw, sh, sw, Ho, Wo, pt, pl):
+    """x: [N,H,W,C] -> padded input and a function giving the [N,Ho,Wo,C] slice for tap (i,j)."""
+    N, H, W, C = x.shape
+    Hp = max(H + pt, (Ho - 1) * sh + kh)
+    Wp = max(W + pl, (Wo - 1) * sw + kw)
+    xp = np.zeros((N, Hp, Wp, C), dtype=np.float64)
+    xp[:, pt:pt + H, pl:pl + W, :] = x
+    return xp
+
+
+def conv_fwd_int(xq, wq, strides, padding):
+    """Exact integer conv (NHWC x HWIO). Returns int64 [N,Ho,Wo,Cout]."""
+    N, H, W, Cin = xq.shape
+    kh, kw, _, Cout = wq.shape
+    sh, sw = strides
+    Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    xp = _windows(xq.astype(np.float64), kh, kw, sh, sw, Ho, Wo, pt, pl)
+    acc = np.zeros((N * Ho * Wo, Cout), dtype=np.float64)
+    wf = wq.astype(np.float64)
+    for i in range(kh):
+        for j in range(kw):
+            xs = xp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :]
+            acc += xs.reshape(-1, Cin) @ wf[i, j]
+    return np.rint(acc).astype(np.int64).reshape(N, Ho, Wo, Cout)
+
+
+def conv_dgrad_int(gq, wq, strides, padding, in_shape):
+    """Exact integer input-gradient of conv_fwd_int. Returns int64 [N,H,W,Cin]."""
+    N, H, W, Cin = in_shape
+    kh, kw, _, Cout = wq.shape
+    sh, sw = strides
+    Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    Hp = max(H + pt, (Ho - 1) * sh + kh)
+    Wp = max(W + pl, (Wo - 1) * sw + kw)
+    dxp = np.zeros((N, Hp, Wp, Cin), dtype=np.float64)
+    g = gq.astype(np.float64).reshape(-1, Cout)
+    wf = wq.astype(np.float64)
+    for i in range(kh):
+        for j in range(kw):
+            contrib = (g @ wf[i, j].T).reshape(N, Ho, Wo, Cin)
+            dxp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :] += contrib
+    return np.rint(dxp[:, pt:pt + H, pl:pl + W, :]).astype(np.int64)
+
+
+def conv_wgrad_int(xq, gq, strides, padding, kshape):
+    """Exact integer weight-gradient. Returns int64 [kh,kw,Cin,Cout]."""
+    N, H, W, Cin = xq.shape
+    kh, kw = kshape
+    Cout = gq.shape[-1]
+    sh, sw = strides
+    Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    xp = _windows(xq.astype(np.float64), kh, kw, sh, sw, Ho, Wo, pt, pl)
+    g = gq.astype(np.float64).reshape(-1, Cout)
+    dw = np.zeros((kh, kw, Cin, Cout), dtype=np.float64)
+    for i in range(kh):
+        for j in range(kw):
+            xs = xp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :]
+            dw[i, j] = xs.reshape(-1, Cin).T @ g
+    return np.rint(dw).astype(np.int64)
+
+
+def scale_int(acc, e):
+    """float32(acc) * 2**-e, the dequant epilogue of every integer GEMM."""
+    return (np.asarray(acc).astype(np.float32) * F32(2.0 ** -e)).astype(np.float32)
+
+
+class Ctx:
+    """Per-step quantiser context: exponents I_t, overflow counts, noise key."""
+
+    def __init__(self, ranges, step, seed, target=0.0):
+        self.I = ranges            # name -> int exponent (I_t), shared with the model
+        self.step = int(step)
+        self.seed = int(seed)
+        self.target = target
+        self.counts = {}           # name -> (c1, c2, n, bits)
+        self.record = {}           # name -> int codes (for parity tests)
+
+    def q(self, name, x, bits, stochastic=True):
+        """Quantise with I_t; record overflow counts of x against I_t."""
+        x = np.asarray(x, dtype=np.float32)
+        I = self.I[name]
+        noise = dfxp.noise_for(x.shape, dfxp.qid_of(name), self.step, self.seed) if stochastic else None
+        q = dfxp.quantize_int(x, bits, I, stochastic, noise)
+        c1, c2 = dfxp.overflow_counts(x, bits, I)
+        self.counts[name] = (c1, c2, x.size, bits)
+        self.record[name] = q
+        return q, dfxp.frac_bits(bits, I)
+
+    def new_ranges(self):
+        out = dict(self.I)
+        for name, (c1, c2, n, bits) in self.counts.items():
+            out[name] = dfxp.update_range_from_counts(c1, c2, n, self.target, bits, self.I[name])
+        return out
+
+
+class LayerQ:
+    def forward(self, X, ctx):
+        return X
+
+    def backward(self, g, ctx):
+        return g
+
+    def params(self):
+        return []
+
+    def range_names(self):
+        return []
+
+
+class Conv2dQ(LayerQ):
+    def __init__(self, name, bits, ksize, strides, padding, weight_decay=0.0):
+        self.name, self.bits, self.ksize = name, bits, tuple(ksize)
+        self.strides = (strides[1], strides[2]) if len(strides) == 4 else tuple(strides)
+        self.padding, self.wd = padding, weight_decay
+        self.W = None
+
+    def range_names(self):
+        return [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
+
+    def params(self):
+        return [(self.name + "/W", self)]
+
+    def forward(self, X, ctx):
+        self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits + 1)
+        self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.bits)
+        self.in_shape = X.shape
+        acc = conv_fwd_int(self.xq, self.wq, self.strides, self.padding)
+        return scale_int(acc, self.ex + self.ew)
+
+    def backward(self, g, ctx):
+        gq, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        self.gq = gq
+        acc_w = conv_wgrad_int(self.xq, gq, self.strides, self.padding, self.ksize[:2])
+        c = F32(2 * self.wd)
+        self.dW = (scale_int(acc_w, self.ex + eg) + (c * self.W).astype(F32)).astype(F32)
+        acc_x = conv_dgrad_int(gq, self.wq, self.strides, self.padding, self.in_shape)
+        return scale_int(acc_x, eg + self.ew)
+
+
+class DenseQ(LayerQ):
+    def __init__(self, name, bits, in_units, units, weight_decay=0.0):
+        self.name, self.bits, self.in_units, self.units, self.wd = name, bits, in_units, units, weight_decay
+        self.W = None
+
+    def range_names(self):
+        return [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
+
+    def params(self):
+        return [(self.name + "/W", self)]
+
+    def forward(self, X, ctx):
+        self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits)
+        self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.bits)
+        acc = np.rint(self.xq.astype(np.float64) @ self.wq.astype(np.float64)).astype(np.int64)
+        return scale_int(acc, self.ex + self.ew)
+
+    def backward(self, g, ctx):
+        gq, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        self.gq = gq
+        acc_w = np.rint(self.xq.astype(np.float64).T @ gq.astype(np.float64)).astype(np.int64)
+        c = F32(2 * self.wd)
+        self.dW = (scale_int(acc_w, self.ex + eg) + (c * self.W).astype(F32)).astype(F32)
+        acc_x = np.rint(gq.astype(np.float64) @ self.wq.astype(np.float64).T).astype(np.int64)
+        return scale_int(acc_x, eg + self.ew)
+
+
+class NormQ(LayerQ):
+    def __init__(self, name, bits, num_features, momentum=0.999, eps=1e-5):
+        self.name, self.bits, self.C = name, bits, num_features
+        self.momentum, self.eps = momentum, eps
+        self.mean_running = np.zeros(num_features, F32)
+        self.var_running = np.ones(num_features, F32)
+
+    def range_names(self):
+        return [self.name + "/X_range", self.name + "/grad_range"]
+
+    def forward(self, X, ctx):
+        q, e = ctx.q(self.name + "/X_range", X, self.bits)
+        s = 2.0 ** -e
+        C = X.shape[-1]
+        qf = q.reshape(-1, C).astype(np.int64)
+        n = qf.shape[0]
+        S1 = qf.sum(0)
+        S2 = (qf * qf).sum(0)
+        mean_d = S1.astype(np.float64) * s / n
+        var_d = S2.astype(np.float64) * (s * s) / n - mean_d * mean_d
+        mu = mean_d.astype(F32)
+        var = var_d.astype(F32)
+        sigma = np.sqrt((var + F32(self.eps)).astype(F32)).astype(F32)
+        xhat = (((q.astype(F32) * F32(s)).astype(F32) - mu).astype(F32) / sigma).astype(F32)
+        m = F32(self.momentum)
+        self.mean_running = ((m * self.mean_running).astype(F32) + (F32(1 - self.momentum) * mu).astype(F32)).astype(F32)
+        self.var_running = ((m * self.var_running).astype(F32) + (F32(1 - self.momentum) * var).astype(F32)).astype(F32)
+        self.q, self.e, self.mu, self.sigma, self.xhat, self.n = q, e, mu, sigma, xhat, n
+        return xhat
+
+    def backward(self, g, ctx):
+        G, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        sg = 2.0 ** -eg
+        s = 2.0 ** -self.e
+        C = g.shape[-1]
+        Gf = G.reshape(-1, C).astype(np.int64)
+        qf = self.q.reshape(-1, C).astype(np.int64)
+        SG = Gf.sum(0)
+        SGQ = (Gf * qf).sum(0)
+        n = self.n
+        mu_d = self.mu.astype(np.float64)
+        sig_d = self.sigma.astype(np.float64)
+        mg = (sg * SG.astype(np.float64) / n).astype(F32)
+        mgx = (sg * (s * SGQ.astype(np.float64) - mu_d * SG.astype(np.float64)) / (n * sig_d)).astype(F32)
+        ghat = (G.astype(F32) * F32(sg)).astype(F32)
+        a = (ghat - mg).astype(F32)
+        b = (self.xhat * mgx).astype(F32)
+        return ((a - b).astype(F32) / self.sigma).astype(F32)
+
+
+class RescaleQ(LayerQ):
+    def __init__(self, name, bits, num_features, weight_decay=0.0):
+        self.name, self.bits, self.C, self.wd = name, bits, num_features, weight_decay
+        self.gamma = np.ones(num_features, F32)
+        self.beta = np.zeros(num_features, F32)
+
+    def range_names(self):
+        return [self.name + "/g_range", self.name + "/b_range", self.name + "/X_range", self.name + "/grad_range"]
+
+    def params(self):
+        return [(self.name + "/g", self), (self.name + "/b", self)]
+
+    def forward(self, X, ctx):
+        R, er = ctx.q(self.name + "/X_range", X, self.bits)
+        gq, eg = ctx.q(self.name + "/g_range", self.gamma, self.bits)
+        bq, eb = ctx.q(self.name + "/b_range", self.beta, self.bits)
+        self.R, self.er = R, er
+        self.gq_f = (gq.astype(F32) * F32(2.0 ** -eg)).astype(F32)
+        bq_f = (bq.astype(F32) * F32(2.0 ** -eb)).astype(F32)
+        xr = (R.astype(F32) * F32(2.0 ** -er)).astype(F32)
+        return ((xr * self.gq_f).astype(F32) + bq_f).astype(F32)
+
+    def backward(self, g, ctx):
+        G, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        C = g.shape[-1]
+        Gf = G.reshape(-1, C).astype(np.int64)
+        Rf = self.R.reshape(-1, C).astype(np.int64)
+        sg = 2.0 ** -eg
+        sr = 2.0 ** -self.er
+        c = F32(2 * self.wd)
+        self.dgamma = ((Gf * Rf).sum(0).astype(np.float64) * (sg * sr)).astype(F32)
+        self.dgamma = (self.dgamma + (c * self.gamma).astype(F32)).astype(F32)
+        self.dbeta = (Gf.sum(0).astype(np.float64) * sg).astype(F32)
+        ghat = (G.astype(F32) * F32(sg)).astype(F32)
+        return (ghat * self.gq_f).astype(F32)
+
+
+class SequentialQ(LayerQ):
+    def __init__(self, *layers):
+        self.layers = list(layers)
+
+    def forward(self, X, ctx):
+        for l in self.layers:
+            X = l.forward(X, ctx)
+        return X
+
+    def backward(self, g, ctx):
+        for l in reversed(self.layers):
+            g = l.backward(g, ctx)
+        return g
+
+    def params(self):
+        return [p for l in self.layers for p in l.params()]
+
+    def range_names(self):
+        return [r for l in self.layers for r in l.range_names()]
+
+
+def BatchNormQ(name, bits, num_features, weight_decay=0.0):
+    return SequentialQ(NormQ(name + "-norm", bits, num_features),
+                       RescaleQ(name + "-rescale", bits, num_features, weight_decay))
+
+
+class ReluQ(LayerQ):
+    def forward(self, X, ctx):
+        self.X = X
+        return np.maximum(F32(0), X).astype(F32)
+
+    def backward(self, g, ctx):
+        return np.where(self.X > 0, g, F32(0)).astype(F32)
+
+
+class ResidualBlockQ(LayerQ):
+    def __init__(self, name, bits, in_channels, channels, stride, weight_decay=0.0):
+        self.residual = SequentialQ(
+            Conv2dQ(name + "-1", bits, [3, 3, in_channels, channels], [1, stride, stride, 1], "SAME", weight_decay),
+            BatchNormQ(name + "-bn1", bits, channels, weight_decay),
+            ReluQ(),
+            Conv2dQ(name + "-2", bits, [3, 3, channels, channels], [1, 1, 1, 1], "SAME", weight_decay),
+            BatchNormQ(name + "-bn2", bits, channels, weight_decay))
+        if stride == 1 and in_channels == channels:
+            self.shortcut = SequentialQ()
+        else:
+            self.shortcut = SequentialQ(
+                Conv2dQ(name + "-shortcut", bits, [1, 1, in_channels, channels], [1, stride, stride, 1], "SAME",
+                        weight_decay),
+                BatchNormQ(name + "-shortcut-bn", bits, channels, weight_decay))
+        self.relu = ReluQ()
+
+    def forward(self, X, ctx):
+        y1 = self.residual.forward(X, ctx)
+        y2 = self.shortcut.forward(X, ctx)
+        return self.relu.forward((y1 + y2).astype(F32), ctx)
+
+    def backward(self, g, ctx):
+        g = self.relu.backward(g, ctx)
+        g1 = self.residual.backward(g, ctx)
+        g2 = self.shortcut.backward(g, ctx)
+        return (g1 + g2).astype(F32)
+
+    def params(self):
+        return self.residual.params() + self.shortcut.params()
+
+    def range_names(self):
+        return self.residual.range_names() + self.shortcut.range_names()
+
+
+class AvgPoolQ(LayerQ):
+    """8x8 VALID average pool over the whole map: sequential fp32 sum then * 2**-6."""
+
+    def forward(self, X, ctx):
+        N, H, W, C = X.shape
+        self.shape = X.shape
+        xs = X.reshape(N, H * W, C)
+        acc = np.zeros((N, C), F32)
+        for i in range(H * W):
+            acc = (acc + xs[:, i, :]).astype(F32)
+        return (acc * F32(1.0 / (H * W))).astype(F32).reshape(N, 1, 1, C)
+
+    def backward(self, g, ctx):
+        N, H, W, C = self.shape
+        return np.broadcast_to((g.reshape(N, 1, 1, C) * F32(1.0 / (H * W))).astype(F32), self.shape).copy()
+
+
+class FlattenQ(LayerQ):
+    def __init__(self, dim):
+        self.dim = dim
+
+    def forward(self, X, ctx):
+        self.shape = X.shape
+        return X.reshape(-1, self.dim)
+
+    def backward(self, g, ctx):
+        return g.reshape(self.shape)
+
+
+def softmax_xent(logits, labels):
+    """mean sparse softmax cross-entropy (``models.py:30-32``) and d loss / d logits, fp32."""
+    z = logits.astype(F32)
+    N = z.shape[0]
+    m = z.max(axis=1, keepdims=True)
+    ez = np.exp((z - m).astype(F32)).astype(F32)
+    s = ez.sum(axis=1, keepdims=True, dtype=F32)
+    p = (ez / s).astype(F32)
+    lse = (np.log(s).astype(F32) + m).astype(F32)
+    loss = float(np.mean((lse[:, 0] - z[np.arange(N), labels]).astype(np.float64)))
+    onehot = np.zeros_like(p)
+    onehot[np.arange(N), labels] = 1
+    dz = ((p - onehot).astype(F32) / F32(N)).astype(F32)
+    return loss, dz
