@@ -75,30 +75,36 @@ __global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const int8_t* _
   dx[i] = add_src ? v + add_src[i] : v;
 }
 
-// grid = nsplit blocks; block b reduces pixels [b*per, (b+1)*per) in chunks of kChunk staged in
-// LDS (im2col patch of X and the G rows), every thread owning (k, co) outputs.
+// grid = (nsplit, output tiles of kMaxOut*256); block (b, t) reduces pixels [b*per, (b+1)*per)
+// for outputs [t*kTile, (t+1)*kTile) in chunks of kChunk pixels staged in LDS (the im2col
+// patch columns k in [klo, khi) that tile needs, and the G rows), each thread owning <= 16 outputs.
 constexpr int kChunk = 32;
+constexpr int kMaxOut = 16;
+constexpr int kTile = kMaxOut * 256;
 template <typename TX>
 __global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __restrict__ x, const int8_t* __restrict__ g,
                                                                 lbt_conv_desc d, int32_t* __restrict__ slab,
                                                                 int64_t P, int nsplit) {
-  extern __shared__ int16_t sh[];  // Xs[kChunk][K] then Gs[kChunk][Cout]
+  extern __shared__ int16_t sh[];
   const int K = d.KH * d.KW * d.Cin;
-  int16_t* Xs = sh;
-  int16_t* Gs = sh + kChunk * K;
+  const int nout = K * d.Cout;
+  const int o0 = blockIdx.y * kTile;
+  const int o1 = o0 + kTile < nout ? o0 + kTile : nout;
+  const int klo = o0 / d.Cout, khi = (o1 - 1) / d.Cout + 1;
+  const int KS = khi - klo;
+  int16_t* Xs = sh;                 // [kChunk][KS]
+  int16_t* Gs = sh + kChunk * KS;   // [kChunk][Cout]
   const int64_t per = (P + nsplit - 1) / nsplit;
   const int64_t p0 = (int64_t)blockIdx.x * per;
   const int64_t p1 = p0 + per < P ? p0 + per : P;
-  const int nout = K * d.Cout;
-  constexpr int kMaxOut = 16;  // outputs per thread (K*Cout <= 4096)
   int acc[kMaxOut];
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) acc[j] = 0;
   const int64_t HWo = (int64_t)d.Ho * d.Wo;
   for (int64_t c0 = p0; c0 < p1; c0 += kChunk) {
     const int cn = (int)(p1 - c0 < kChunk ? p1 - c0 : kChunk);
-    for (int t = threadIdx.x; t < kChunk * K; t += blockDim.x) {
-      const int pl = t / K, k = t - pl * K;
+    for (int t = threadIdx.x; t < kChunk * KS; t += blockDim.x) {
+      const int pl = t / KS, k = klo + (t - pl * KS);
       int v = 0;
       if (pl < cn) {
         const int64_t p = c0 + pl;
@@ -120,11 +126,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __res
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kMaxOut; ++j) {
-      const int o = threadIdx.x + j * blockDim.x;
-      if (o < nout) {
+      const int o = o0 + threadIdx.x + j * blockDim.x;
+      if (o < o1) {
         const int k = o / d.Cout, co = o - k * d.Cout;
         int a = acc[j];
-        for (int pl = 0; pl < kChunk; ++pl) a += (int)Xs[pl * K + k] * (int)Gs[pl * d.Cout + co];
+        for (int pl = 0; pl < kChunk; ++pl) a += (int)Xs[pl * KS + (k - klo)] * (int)Gs[pl * d.Cout + co];
         acc[j] = a;
       }
     }
@@ -133,8 +139,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __res
   int32_t* dst = slab + (int64_t)blockIdx.x * nout;
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) {
-    const int o = threadIdx.x + j * blockDim.x;
-    if (o < nout) dst[o] = acc[j];
+    const int o = o0 + threadIdx.x + j * blockDim.x;
+    if (o < o1) dst[o] = acc[j];
   }
 }
 
@@ -173,18 +179,22 @@ extern "C" int lbt_conv_dgrad_generic(const int8_t* gq, const int8_t* w_hwio, lb
 extern "C" int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
                                       int32_t* slab, int32_t nsplit, void* stream) {
   if (!desc_ok(d) || nsplit <= 0) return LBT_EINVAL;
-  const int K = d.KH * d.KW * d.Cin;
-  if ((int64_t)K * d.Cout > 16 * 256) return LBT_EINVAL;
+  const int64_t K = (int64_t)d.KH * d.KW * d.Cin;
+  const int64_t nout = K * d.Cout;
+  const int64_t tiles = (nout + kTile - 1) / kTile;
+  if (tiles > 65535) return LBT_EINVAL;
   const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
   if ((P + nsplit - 1) / nsplit > 8192) return LBT_EINVAL;  // int32 partial bound for 9-bit x 8-bit
-  const size_t shm = sizeof(int16_t) * kChunk * (K + d.Cout);
+  const int64_t ks_max = (kTile + d.Cout - 1) / d.Cout + 1 < K ? (kTile + d.Cout - 1) / d.Cout + 1 : K;
+  const size_t shm = sizeof(int16_t) * kChunk * (ks_max + d.Cout);
   if (shm > 64 * 1024) return LBT_EINVAL;
+  dim3 grid(nsplit, (unsigned)tiles);
   hipStream_t st = (hipStream_t)stream;
   if (x_i16)
-    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int16_t>, dim3(nsplit), dim3(256), shm, st, (const int16_t*)xq, gq, d,
+    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int16_t>, grid, dim3(256), shm, st, (const int16_t*)xq, gq, d,
                        slab, P, nsplit);
   else
-    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int8_t>, dim3(nsplit), dim3(256), shm, st, (const int8_t*)xq, gq, d,
+    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int8_t>, grid, dim3(256), shm, st, (const int8_t*)xq, gq, d,
                        slab, P, nsplit);
   return (int)hipGetLastError();
 }

@@ -52,8 +52,12 @@ def quantize_weight(w, q, w_hwio=None, wf=None, ksf=0, wd=None, ksd=0, colsum=No
     """Weight quantiser + GEMM operand packing. w: fp32 HWIO [KH,KW,Cin,Cout] (or [in,out])."""
     _check(w, torch.float32, "w")
     if w.dim() == 2:
-        KH = KW = 1
-        Cin, Cout = w.shape
+        # Dense_q W [in, out]: noise over shape[1:] = [out]. Presented as KH=in, KW=Cin=1 the
+        # HWIO flat index and the noise period (KW*Cin*Cout = out) are exactly [in, out]'s.
+        if wf is not None or wd is not None:
+            raise ValueError("2-D weights are packed for the generic kernels only")
+        KH, Cout = w.shape
+        KW = Cin = 1
     else:
         KH, KW, Cin, Cout = w.shape
     q.observe(w.numel())

@@ -1,0 +1,319 @@
+"""GPU parity: the HIP path (through the C-ABI) against the numpy oracle on the same seeded inputs.
+
+Integer work (quantiser codes, overflow counters, exponent updates, every integer GEMM and the
+dequantised fp32 results built from them, BN moments and backward sums) is required to be
+BIT-EXACT. The only op that is not bit-exact is the softmax (expf/logf): loss and d loss / d
+logits are compared with rtol 1e-5; the model backward is then checked bit-exact by feeding
+the GPU's d loss / d logits into the oracle backward.
+"""
+import numpy as np
+import pytest
+import torch
+
+from lbt_amd import dynamic_fixed_point as D
+from lbt_amd._lib import NSHARD, OUT_F32, OUT_I8, OUT_I16, OUT_U8OFF
+from lbt_amd.dfxp import ops
+from lbt_amd.runtime import DfxpContext, qid_of
+from oracle import dfxp as odfxp
+from oracle import nn as onn
+from oracle import resnet as oresnet
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def decode(t, kind):
+    a = t.cpu().numpy()
+    if kind == OUT_U8OFF:
+        return a.astype(np.int32) + 128
+    return a.astype(np.int32) if kind != OUT_F32 else a
+
+
+@pytest.mark.parametrize("shape,bits,I,stoch,kind,lo,hi", [
+    ((128, 32, 32, 16), 9, 2, True, OUT_U8OFF, 0.0, 4.5),
+    ((128, 32, 32, 16), 8, 2, True, OUT_I8, -5.0, 5.0),
+    ((16, 16, 16, 32), 8, -3, True, OUT_I8, -0.2, 0.2),
+    ((16, 8, 8, 64), 8, 2, False, OUT_I8, -5.0, 5.0),
+    ((8, 32, 32, 3), 9, 0, True, OUT_I16, -1.0, 1.0),
+    ((3, 7, 5), 8, 1, True, OUT_I8, -3.0, 3.0),
+    ((64,), 8, 2, True, OUT_I8, -3.0, 3.0),
+    ((128, 10), 8, -5, True, OUT_I8, -0.01, 0.01),
+    ((4, 6, 6, 8), 4, 1, True, OUT_I8, -2.0, 2.0),
+    ((4, 6, 6, 8), 12, 2, True, OUT_I16, -5.0, 5.0),
+])
+def test_quantize_codes_and_counts(shape, bits, I, stoch, kind, lo, hi):
+    rng = np.random.default_rng(abs(hash((shape, bits, I))) % 2**32)
+    x = rng.uniform(lo, hi, size=shape).astype(np.float32)
+    ctx = DfxpContext(seed=1234)
+    q = ctx.quantizer("t/X_range", bits, I, stochastic=stoch)
+    out = ops.quantize(torch.from_numpy(x).to(DEV), q, kind)
+    noise = odfxp.noise_for(shape, qid_of("t/X_range"), 0, 1234) if stoch else None
+    ref = odfxp.quantize_int(x, bits, I, stoch, noise)
+    got = decode(out, kind)
+    if kind == OUT_F32:
+        assert np.array_equal(got, odfxp.dequant(ref, odfxp.frac_bits(bits, I)))
+    else:
+        assert np.array_equal(got, ref)
+    c = ctx.counts_view()[0].sum(0).cpu().tolist()
+    assert tuple(c) == odfxp.overflow_counts(x, bits, I)
+
+
+def test_quantize_channel_sums_and_range_update():
+    rng = np.random.default_rng(3)
+    x = rng.normal(0, 1.5, size=(32, 8, 8, 16)).astype(np.float32)
+    ctx = DfxpContext(seed=9)
+    q = ctx.quantizer("a/X_range", 8, 2)
+    q2 = ctx.quantizer("b/X_range", 8, 2)   # fed nothing: must keep its exponent
+    chsum = ops.new_sums(16, 2, DEV)
+    codes = ops.quantize(torch.from_numpy(x).to(DEV), q, OUT_I8, chsum=chsum, C=16)
+    ref = odfxp.quantize_int(x, 8, 2, True, odfxp.noise_for(x.shape, qid_of("a/X_range"), 0, 9))
+    assert np.array_equal(codes.cpu().numpy(), ref)
+    s = chsum.view(NSHARD, 32).sum(0).cpu().numpy()
+    r = ref.reshape(-1, 16).astype(np.int64)
+    assert np.array_equal(s[:16], r.sum(0)) and np.array_equal(s[16:], (r * r).sum(0))
+    ctx.update_range_op()
+    assert ctx.ranges() == {"a/X_range": odfxp.update_range(x, 0.0, 8, 2), "b/X_range": 2}
+    assert int(ctx.step.item()) == 1
+    assert int(ctx.counts.abs().sum().item()) == 0
+
+
+def test_tf_face_functions():
+    rng = np.random.default_rng(4)
+    x = rng.normal(0, 2, size=(16, 5, 5, 4)).astype(np.float32)
+    ctx = DfxpContext(seed=2)
+    q = ctx.quantizer("f/X_range", 8, 2)
+    xt = torch.from_numpy(x).to(DEV)
+    fq = D.weight_quantization(xt, 0, 8, q, stochastic=False).cpu().numpy()
+    assert np.array_equal(fq, odfxp.dequant(odfxp.quantize_int(x, 8, 2, False), 5))
+    r1, r2 = D.overflow_rate(xt, 8, q)
+    e1, e2 = odfxp.overflow_rate(x, 8, 2)
+    assert (r1, r2) == (float(e1), float(e2))
+    D.update_range(xt, 0, 8, q)
+    assert q.integer_bits == odfxp.update_range(x, 0.0, 8, 2)
+
+
+def test_weight_packing():
+    rng = np.random.default_rng(5)
+    KH, KW, Cin, Cout = 3, 3, 32, 64
+    w = rng.uniform(-0.1, 0.1, size=(KH, KW, Cin, Cout)).astype(np.float32)
+    ctx = DfxpContext(seed=3)
+    q = ctx.quantizer("c/W_range", 8, 2)
+    ksf, ksd = ops.packed_slices(KH, KW, Cin), ops.packed_slices(KH, KW, Cout)
+    hwio = torch.zeros((KH, KW, Cin, Cout), dtype=torch.int8, device=DEV)
+    wf = torch.zeros((Cout, ksf * 16), dtype=torch.int8, device=DEV)
+    wd = torch.zeros((Cin, ksd * 16), dtype=torch.int8, device=DEV)
+    cs = torch.zeros(Cout, dtype=torch.int32, device=DEV)
+    ops.quantize_weight(torch.from_numpy(w).to(DEV), q, hwio, wf, ksf, wd, ksd, cs)
+    ref = odfxp.quantize_int(w, 8, 2, True, odfxp.noise_for(w.shape, qid_of("c/W_range"), 0, 3))
+    assert np.array_equal(hwio.cpu().numpy(), ref)
+    K = KH * KW * Cin
+    assert np.array_equal(wf.cpu().numpy()[:, :K], ref.reshape(K, Cout).T)
+    assert np.array_equal(wd.cpu().numpy()[:, :KH * KW * Cout],
+                          ref.transpose(2, 0, 1, 3).reshape(Cin, KH * KW * Cout))
+    assert np.array_equal(cs.cpu().numpy(), ref.reshape(K, Cout).sum(0))
+
+
+def _copy_conv(gl, ol):
+    ol.W = gl.W.cpu().numpy().copy()
+
+
+# (N, H, Cin, Cout, k, s, nonneg)
+CONV_CASES = [
+    (8, 32, 16, 16, 3, 1, True),     # stage-1 block conv (MFMA, offset uint8)
+    (8, 32, 16, 32, 3, 2, True),     # downsample conv, TF SAME (0,1) padding
+    (8, 32, 16, 32, 1, 2, True),     # 1x1 stride-2 shortcut
+    (8, 16, 32, 32, 3, 1, True),
+    (8, 16, 32, 64, 3, 2, True),
+    (8, 8, 64, 64, 3, 1, True),      # stage-3 block conv
+    (8, 32, 3, 16, 3, 1, False),     # conv1: signed 9-bit image, VALU path
+    (4, 12, 16, 16, 3, 1, False),    # signed 9-bit input on a 16-channel conv -> VALU path
+    (4, 9, 32, 16, 3, 2, True),      # odd spatial size
+    (128, 32, 16, 16, 3, 1, True),   # full ResNet-20 stage-1 size (B=128)
+]
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,nonneg", CONV_CASES)
+def test_conv_layer_bitexact(N, H, Cin, Cout, k, s, nonneg):
+    rng = np.random.default_rng(N * 1000 + H * 10 + Cin + Cout + k + s)
+    ctx = DfxpContext(seed=77)
+    name = "blk"
+    gl = D.Conv2d_q(name, 8, [k, k, Cin, Cout], [1, s, s, 1], "SAME", use_bias=False, weight_decay=2e-4,
+                    input_nonnegative=nonneg, ctx=ctx)
+    ol = onn.Conv2dQ(name, 8, [k, k, Cin, Cout], [1, s, s, 1], "SAME", 2e-4)
+    _copy_conv(gl, ol)
+    x = (rng.uniform(0, 3.5, size=(N, H, H, Cin)) if nonneg else rng.uniform(-1, 1, size=(N, H, H, Cin)))
+    x = x.astype(np.float32)
+    octx = onn.Ctx({r: 2 for r in ol.range_names()}, 0, 77)
+    y = gl.forward(torch.from_numpy(x).to(DEV))
+    yr = ol.forward(x, octx)
+    assert np.array_equal(y.cpu().numpy(), yr)
+    g = rng.normal(0, 0.05, size=yr.shape).astype(np.float32)
+    dx = gl.backward(torch.from_numpy(g).to(DEV))
+    dxr = ol.backward(g, octx)
+    assert np.array_equal(gl.gradq.cpu().numpy(), octx.record[name + "/grad_range"])
+    assert np.array_equal(gl.dW.cpu().numpy(), ol.dW)
+    assert np.array_equal(dx.cpu().numpy(), dxr)
+    ctx.update_range_op()
+    assert ctx.ranges() == octx.new_ranges()
+
+
+def test_dense_layer_bitexact():
+    rng = np.random.default_rng(11)
+    ctx = DfxpContext(seed=5)
+    gl = D.Dense_q("softmax", 8, 64, 10, use_bias=False, weight_decay=2e-4, ctx=ctx)
+    ol = onn.DenseQ("softmax", 8, 64, 10, 2e-4)
+    ol.W = gl.W.cpu().numpy().copy()
+    x = rng.uniform(0, 2, size=(128, 64)).astype(np.float32)
+    octx = onn.Ctx({r: 2 for r in ol.range_names()}, 0, 5)
+    y = gl.forward(torch.from_numpy(x).to(DEV))
+    assert np.array_equal(y.cpu().numpy(), ol.forward(x, octx))
+    g = rng.normal(0, 0.004, size=(128, 10)).astype(np.float32)
+    dx = gl.backward(torch.from_numpy(g).to(DEV))
+    dxr = ol.backward(g, octx)
+    assert np.array_equal(gl.dW.cpu().numpy(), ol.dW)
+    assert np.array_equal(dx.cpu().numpy(), dxr)
+
+
+@pytest.mark.parametrize("shape", [(16, 32, 32, 16), (16, 8, 8, 64), (128, 16, 16, 32)])
+def test_batchnorm_bitexact(shape):
+    rng = np.random.default_rng(shape[0] + shape[-1])
+    C = shape[-1]
+    ctx = DfxpContext(seed=21)
+    gbn = D.BatchNorm_q("bn", 8, C, weight_decay=2e-4, ctx=ctx)
+    obn = onn.BatchNormQ("bn", 8, C, 2e-4)
+    gam = (1 + 0.2 * rng.standard_normal(C)).astype(np.float32)
+    bet = (0.2 * rng.standard_normal(C)).astype(np.float32)
+    gbn.layers[1].gamma.copy_(torch.from_numpy(gam))
+    gbn.layers[1].beta.copy_(torch.from_numpy(bet))
+    obn.layers[1].gamma, obn.layers[1].beta = gam.copy(), bet.copy()
+    x = (rng.standard_normal(shape) * 1.3 + 0.4).astype(np.float32)
+    octx = onn.Ctx({r: 2 for r in obn.range_names()}, 0, 21)
+    y = gbn.forward(torch.from_numpy(x).to(DEV))
+    yr = obn.forward(x, octx)
+    assert np.array_equal(y.cpu().numpy(), yr)
+    g = (rng.standard_normal(shape) * 0.03).astype(np.float32)
+    dx = gbn.backward(torch.from_numpy(g).to(DEV))
+    dxr = obn.backward(g, octx)
+    assert np.array_equal(gbn.layers[1].dgamma.cpu().numpy(), obn.layers[1].dgamma)
+    assert np.array_equal(gbn.layers[1].dbeta.cpu().numpy(), obn.layers[1].dbeta)
+    assert np.array_equal(dx.cpu().numpy(), dxr)
+    ctx.update_range_op()
+    assert ctx.ranges() == octx.new_ranges()
+
+
+def _build_pair(batch_seed=0, wd=2e-4, seed=0):
+    from lbt_amd.models import CIFAR10_Resnet20
+    ctx = DfxpContext(seed=seed)
+    gm = CIFAR10_Resnet20(8, weight_decay=wd, ctx=ctx)
+    om = oresnet.build_resnet((3, 3, 3), 8, wd)
+    return ctx, gm, om
+
+
+def gpu_params(gm):
+    out = {}
+    for owner, var, _ in gm.param_slots():
+        suffix = {"W": "/W", "gamma": "/g", "beta": "/b"}[var]
+        out[owner.name + suffix] = getattr(owner, var).detach().cpu().numpy().copy()
+    return out
+
+
+def gpu_grads(gm):
+    out = {}
+    for owner, var, gname in gm.param_slots():
+        suffix = {"W": "/W", "gamma": "/g", "beta": "/b"}[var]
+        out[owner.name + suffix] = getattr(owner, gname).detach().cpu().numpy().copy()
+    return out
+
+
+def synthetic_batch(B, seed=0):
+    rng = np.random.default_rng(seed)
+    x = ((rng.integers(0, 256, size=(B, 32, 32, 3)) - 127.5) / 128).astype(np.float32)
+    y = rng.integers(0, 10, size=B).astype(np.int32)
+    return x, y
+
+
+def test_resnet20_step_parity():
+    ctx, gm, om = _build_pair()
+    params = gpu_params(gm)
+    oresnet.set_params(om, params)
+    x, y = synthetic_batch(16, seed=1)
+    xt, yt = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    octx = onn.Ctx(oresnet.init_ranges(om), 0, 0)
+    logits = gm.forward(xt)
+    lr = om.forward(x, octx)
+    assert np.array_equal(logits.cpu().numpy(), lr), "forward must be bit-exact"
+    loss = gm.compute_loss(yt)
+    lref, dzr = onn.softmax_xent(lr, y)
+    assert abs(loss.item() - lref) <= 1e-5 * abs(lref)
+    dz = gm.dlogits.cpu().numpy()
+    np.testing.assert_allclose(dz, dzr, rtol=1e-5, atol=1e-9)
+    gm.backward()
+    om.backward(dz, octx)   # same d loss / d logits -> the whole backward must be bit-exact
+    gg, og = gpu_grads(gm), oresnet.get_grads(om)
+    assert gg.keys() == og.keys()
+    for k in gg:
+        assert np.array_equal(gg[k], og[k]), k
+    ctx.update_range_op()
+    assert ctx.ranges() == octx.new_ranges()
+
+
+def test_trainer_graph_replay_equals_eager():
+    from lbt_amd.trainer import Trainer
+    x, y = synthetic_batch(32, seed=2)
+    xt, yt = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    res = []
+    for use_graph in (False, True):
+        ctx, gm, _ = _build_pair(seed=3)
+        tr = Trainer(gm, lr=1e-2, momentum=0.9, batch_size=32, use_graph=use_graph)
+        tr.init_model()
+        losses = [tr.step(xt, yt).item() for _ in range(4)]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.w.cpu().numpy(), ctx.ranges(), int(ctx.step.item())))
+    (l0, w0, r0, s0), (l1, w1, r1, s1) = res
+    assert l0 == l1 and r0 == r1 and s0 == s1 == 4
+    assert np.array_equal(w0, w1)
+
+
+def test_resnet20_trains_against_oracle_two_steps():
+    """Two full optimiser steps: weights after step 2 agree with the oracle to fp32 tolerance
+    (the softmax is the only non-bit-exact op) and the exponents agree exactly."""
+    from lbt_amd.trainer import Trainer
+    ctx, gm, om = _build_pair(seed=4)
+    state = dict(params=gpu_params(gm), accum=None, ranges=oresnet.init_ranges(om), step=0)
+    state["accum"] = {k: np.zeros_like(v) for k, v in state["params"].items()}
+    tr = Trainer(gm, lr=1e-2, momentum=0.9, batch_size=16, use_graph=False)
+    for i in range(2):
+        x, y = synthetic_batch(16, seed=10 + i)
+        tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+        _, state, _ = oresnet.train_step(om, state, x, y, lr=1e-2, momentum=0.9, seed=4)
+    gp = gpu_params(gm)
+    worst = max(float(np.max(np.abs(gp[k] - state["params"][k]))) for k in gp)
+    assert worst < 1e-3, worst
+    assert ctx.ranges() == state["ranges"]
+
+
+def test_torch_face_conv_matches_layer():
+    from lbt_amd.dfxp import Conv2d_q, Linear_q, BatchNorm2d_q
+    ctx = DfxpContext(seed=8)
+    m = Conv2d_q(8, 16, 16, kernel_size=3, stride=1, padding=1, bias=False, ctx=ctx, name="tc",
+                 input_nonnegative=True)
+    ref = onn.Conv2dQ("tc", 8, [3, 3, 16, 16], [1, 1, 1, 1], "SAME", 0.0)
+    ref.W = m.weight.detach().permute(2, 3, 1, 0).cpu().numpy().copy()
+    rng = np.random.default_rng(8)
+    x = rng.uniform(0, 2, size=(4, 16, 10, 10)).astype(np.float32)  # NCHW
+    xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    y = m(xt)
+    octx = onn.Ctx({r: 2 for r in ref.range_names()}, 0, 8)
+    yr = ref.forward(x.transpose(0, 2, 3, 1).copy(), octx)
+    assert np.array_equal(y.detach().permute(0, 2, 3, 1).cpu().numpy(), yr)
+    g = rng.normal(0, 0.05, size=y.shape).astype(np.float32)
+    y.backward(torch.from_numpy(g).to(DEV))
+    dxr = ref.backward(g.transpose(0, 2, 3, 1).copy(), octx)
+    assert np.array_equal(xt.grad.permute(0, 2, 3, 1).cpu().numpy(), dxr)
+    assert np.array_equal(m.weight.grad.permute(2, 3, 1, 0).cpu().numpy(), ref.dW)
+    # custom.py-style composition runs end to end
+    lin = Linear_q(8, 16 * 10 * 10, 10, ctx=ctx)
+    bn = BatchNorm2d_q(8, 16, ctx=ctx)
+    out = lin(torch.relu(bn(y.detach())).reshape(4, -1))
+    out.sum().backward()
+    assert torch.isfinite(lin.weight.grad).all() and torch.isfinite(bn.weight.grad).all()
