@@ -1,0 +1,155 @@
+#!/usr/bin/env python
+"""bench.py -- train-step samples/s of ResNet-20 / CIFAR-10, 8-bit DFXP, on 1..8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one ``Trainer.step`` (reference trainer.py:157): forward, mean softmax-CE, manual
+backward through all 192 DFXP quantisers, MomentumOptimizer update and the update_range
+collection, on a synthetic CIFAR-shaped batch already resident in HBM. Data parallel runs use
+128 images per GPU (weak scaling) and one RCCL all-reduce of gradients + overflow counters per
+step. Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+METRIC = "train-step samples/sec, ResNet-20 CIFAR-10 8-bit DFP, 1/2/4/8 MI355X"
+
+
+def synthetic_batches(n, B, seed, device):
+    """x = (randint(0,256,[B,32,32,3]) - 127.5)/128 fp32 NHWC, labels randint(0,10)."""
+    g = torch.Generator().manual_seed(seed)
+    xs, ys = [], []
+    for _ in range(n):
+        x = ((torch.randint(0, 256, (B, 32, 32, 3), generator=g).float() - 127.5) / 128).to(device)
+        y = torch.randint(0, 10, (B,), generator=g).to(torch.int32).to(device)
+        xs.append(x.contiguous())
+        ys.append(y)
+    return xs, ys
+
+
+def cpu_baseline(seconds=15.0, batch=128):
+    """The oracle's ResNet-20 step (reference-semantics CPU restatement, numpy) on the host."""
+    from oracle import resnet as oresnet
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    m = oresnet.build_resnet((3, 3, 3), 8, 2e-4)
+    rng = np.random.default_rng(0)
+    params = {}
+    for name, owner in m.params():
+        if name.endswith("/W"):
+            shp = owner.ksize if hasattr(owner, "ksize") else (owner.in_units, owner.units)
+            fan = float(np.prod(shp[:-1]))
+            params[name] = rng.uniform(-np.sqrt(3 / fan), np.sqrt(3 / fan), size=shp).astype(np.float32)
+        elif name.endswith("/g"):
+            params[name] = np.ones(owner.C, np.float32)
+        else:
+            params[name] = np.zeros(owner.C, np.float32)
+    state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()},
+                 ranges=oresnet.init_ranges(m), step=0)
+    x = ((rng.integers(0, 256, size=(batch, 32, 32, 3)) - 127.5) / 128).astype(np.float32)
+    y = rng.integers(0, 10, size=batch)
+    oresnet.train_step(m, state, x, y)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        _, state, _ = oresnet.train_step(m, state, x, y)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(n * batch / el, 2), "unit": "samples/s", "cores": int(cores), "kind": "port",
+            "sample": "%d oracle train steps (numpy restatement of dynamic_fixed_point/models/trainer), "
+                      "ResNet-20 B=%d, %.1f s" % (n, batch, el)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=128, help="images per GPU")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph (diagnostics)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.runtime import DfxpContext
+    from lbt_amd.trainer import Trainer
+
+    ctx = DfxpContext(device=device, seed=0, world_size=world)
+    model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+    trainer = Trainer(model, lr=1e-2, momentum=0.9, batch_size=args.batch, use_graph=not args.eager)
+    trainer.init_model()
+    xs, ys = synthetic_batches(4, args.batch, seed=1000 + rank, device=device)
+
+    for i in range(args.warmup):
+        trainer.step(xs[i % 4], ys[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(xs[i % 4], ys[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss = float(model.loss.item())
+
+    out = {
+        "metric": METRIC,
+        "value": round(args.batch * world * args.steps / el, 2),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * el / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic CIFAR-10-shaped batches (uniform uint8 pixels, (p-127.5)/128), random-init weights",
+        "config": {"workload": "ResNet-20 CIFAR-10 8-bit DFXP W/A/G train step (fwd+bwd+SGD-momentum+range update)",
+                   "global_batch": args.batch * world, "per_gpu_batch": args.batch, "image": [32, 32, 3],
+                   "parallelism": "dp%d" % world, "hip_graph": not args.eager, "final_loss": round(loss, 4)},
+    }
+    if rank == 0 and world == 1 and not args.no_roofline:
+        from lbt_amd.roofline import measure_dominant
+        out["roofline"] = measure_dominant(trainer, xs[0], ys[0])
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.batch)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

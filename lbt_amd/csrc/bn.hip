@@ -91,78 +91,74 @@ LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long 
 }
 
 // ============================================================================ forward chain
-struct BranchState {
-  QState qn, qr;
-  float sn, sr;
-};
+template <int B>
+LBT_DEV const lbt_chain_branch& fbranch(const lbt_chain_fwd& a) { return B == 0 ? a.b1 : a.b2; }
 
+template <int NB>
 __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, int rpt) {
   extern __shared__ float shf[];  // per branch: mu, sigma, gq, bq [C each]; then long long tmp[2C]
   __shared__ int sh_cnt[2 * kThreads / 64];
   const int C = a.C;
-  float* P1 = shf;
-  float* P2 = shf + 4 * C;
   long long* tmp = reinterpret_cast<long long*>(shf + 8 * C);
-  const lbt_chain_branch* br[2] = {&a.b1, &a.b2};
-  const int nb = a.has_b2 ? 2 : 1;
-  BranchState bs[2];
-  for (int b = 0; b < nb; ++b) {
-    const lbt_chain_branch& B = *br[b];
-    float* P = b ? P2 : P1;
-    bs[b].qr = qstate(B.qr);
-    bs[b].sr = bs[b].qr.active ? bs[b].qr.inv_m : 0.f;
+  QState qr[2];
+  float sn[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_chain_branch& B = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+    float* P = shf + 4 * C * b;
+    qr[b] = qstate(B.qr);
+    sn[b] = 0.f;
     if (B.nrm.q) {
-      bs[b].qn = qstate(B.nrm.qn);
-      bs[b].sn = bs[b].qn.inv_m;
+      sn[b] = qscale(B.nrm.qn);
       bn_moments(B.nrm, C, P, P + C, tmp);
       __syncthreads();
-    } else {
-      bs[b].qn.active = 0;
-      bs[b].sn = 0.f;
     }
-    if (bs[b].qr.active)
+    if (qr[b].active)
       for (int c = threadIdx.x; c < C; c += kThreads) { P[2 * C + c] = B.gb[c]; P[3 * C + c] = B.gb[C + c]; }
   }
   __syncthreads();
   const QState so1 = qstate(a.qo1), so2 = qstate(a.qo2);
   const bool o1 = a.o1 && so1.active, o2 = a.o2 && so2.active;
-  int ov[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};  // qr1, qr2, qo1, qo2
+  int ovr[2][2] = {{0, 0}, {0, 0}};
+  int ovo[2][2] = {{0, 0}, {0, 0}};
 
   const int64_t groups = a.inner >> 2;
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (g < groups) {
     const int c0 = (int)((g << 2) % C);
-    Noise4 nr[2], no1, no2;
-    for (int b = 0; b < nb; ++b) nr[b] = noise_for(br[b]->qr, bs[b].qr, g);
-    no1 = noise_for(a.qo1, so1, g);
-    no2 = noise_for(a.qo2, so2, g);
+    Noise4 nr[2];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) nr[b] = noise_for(b == 0 ? a.b1.qr : a.b2.qr, qr[b], g);
+    const Noise4 no1 = noise_for(a.qo1, so1, g);
+    const Noise4 no2 = noise_for(a.qo2, so2, g);
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
     for (int64_t r = r0; r < rend; ++r) {
       const int64_t e = r * a.inner + (g << 2);
       float v[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int b = 0; b < nb; ++b) {
-        const lbt_chain_branch& B = *br[b];
-        const float* P = b ? P2 : P1;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const lbt_chain_branch& B = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+        const float* P = shf + 4 * C * b;
         float t[4];
         if (B.nrm.q) {
           int q[4];
           load4_i8(B.nrm.q, e, q);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const float x1 = (float)q[k] * bs[b].sn;
+            const float x1 = (float)q[k] * sn[b];
             const float x2 = x1 - P[c0 + k];
             t[k] = x2 / P[C + c0 + k];
           }
         } else {
           load4_f32(B.xin, e, t);
         }
-        if (bs[b].qr.active) {
+        if (qr[b].active) {
           int R[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            R[k] = quant1(bs[b].qr, B.qr.stochastic, t[k], nr[b].u[k], ov[b][0], ov[b][1]);
-            const float xr = (float)R[k] * bs[b].sr;
+            R[k] = quant1(qr[b], B.qr.stochastic, t[k], nr[b].u[k], ovr[b][0], ovr[b][1]);
+            const float xr = (float)R[k] * qr[b].inv_m;
             const float m1 = xr * P[2 * C + c0 + k];
             t[k] = m1 + P[3 * C + c0 + k];
           }
@@ -185,34 +181,34 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
       if (o1) {
         int c[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = quant1(so1, a.qo1.stochastic, v[k], no1.u[k], ov[2][0], ov[2][1]);
+        for (int k = 0; k < 4; ++k) c[k] = quant1(so1, a.qo1.stochastic, v[k], no1.u[k], ovo[0][0], ovo[0][1]);
         store4_code(a.o1, a.o1_kind, e, c, so1.inv_m);
       }
       if (o2) {
         int c[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = quant1(so2, a.qo2.stochastic, v[k], no2.u[k], ov[3][0], ov[3][1]);
+        for (int k = 0; k < 4; ++k) c[k] = quant1(so2, a.qo2.stochastic, v[k], no2.u[k], ovo[1][0], ovo[1][1]);
         store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
       }
     }
   }
-  if (bs[0].qr.active) block_flush_counts(a.b1.qr, ov[0][0], ov[0][1], sh_cnt);
-  if (nb > 1 && bs[1].qr.active) block_flush_counts(a.b2.qr, ov[1][0], ov[1][1], sh_cnt);
-  if (o1) block_flush_counts(a.qo1, ov[2][0], ov[2][1], sh_cnt);
-  if (o2) block_flush_counts(a.qo2, ov[3][0], ov[3][1], sh_cnt);
+  if (qr[0].active) block_flush_counts(a.b1.qr, ovr[0][0], ovr[0][1], sh_cnt);
+  if (NB > 1 && qr[NB - 1].active) block_flush_counts(a.b2.qr, ovr[NB - 1][0], ovr[NB - 1][1], sh_cnt);
+  if (o1) block_flush_counts(a.qo1, ovo[0][0], ovo[0][1], sh_cnt);
+  if (o2) block_flush_counts(a.qo2, ovo[1][0], ovo[1][1], sh_cnt);
 }
 
 // ============================================================================ backward pass A
+template <int NB>
 __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a, int rpt) {
   extern __shared__ float shf[];  // per branch: gq, bq [C]; then long long sums[2][4C]
   __shared__ int sh_cnt[2 * kThreads / 64];
   const int C = a.C;
   long long* S = reinterpret_cast<long long*>(shf + 4 * C);  // [2][4C]
-  const lbt_bwd_branch* br[2] = {&a.b1, &a.b2};
-  const int nb = a.has_b2 ? 2 : 1;
   QState qrg[2], qng[2], qr[2];
-  for (int b = 0; b < nb; ++b) {
-    const lbt_bwd_branch& B = *br[b];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
     qrg[b] = qstate(B.qrg);
     qng[b] = qstate(B.qng);
     qr[b] = qstate(B.qr);
@@ -221,23 +217,25 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
   }
   for (int i = threadIdx.x; i < 8 * C; i += kThreads) S[i] = 0;
   __syncthreads();
-  int ov[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};  // qrg1, qng1, qrg2, qng2
+  int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};  // [branch][rescale|norm][c1|c2]
   const int64_t groups = a.inner >> 2;
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int c0 = (int)((g << 2) % C);
+  int acc[2][4][4];  // [branch][sum][k]
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[b][s][k] = 0;
   if (g < groups) {
-    const int c0 = (int)((g << 2) % C);
     Noise4 nrg[2], nng[2];
-    for (int b = 0; b < nb; ++b) {
-      nrg[b] = noise_for(br[b]->qrg, qrg[b], g);
-      nng[b] = noise_for(br[b]->qng, qng[b], g);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
+      nrg[b] = noise_for(B.qrg, qrg[b], g);
+      nng[b] = noise_for(B.qng, qng[b], g);
     }
-    int acc[2][4][4];  // [branch][sum][k]
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc[b][s][k] = 0;
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
     for (int64_t r = r0; r < rend; ++r) {
@@ -262,17 +260,15 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
       }
       if (a.gmask_out) store4_f32(a.gmask_out, e, gv);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if (b >= nb) break;
-        const lbt_bwd_branch& B = *br[b];
+      for (int b = 0; b < NB; ++b) {
+        const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
         float d[4] = {gv[0], gv[1], gv[2], gv[3]};
         if (qrg[b].active) {
-          int R[4];
-          if (b == 0) { R[0] = R1[0]; R[1] = R1[1]; R[2] = R1[2]; R[3] = R1[3]; }
-          else load4_i8(B.R, e, R);
+          int R[4] = {R1[0], R1[1], R1[2], R1[3]};
+          if (b) load4_i8(B.R, e, R);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const int G2 = quant1(qrg[b], B.qrg.stochastic, d[k], nrg[b].u[k], ov[2 * b][0], ov[2 * b][1]);
+            const int G2 = quant1(qrg[b], B.qrg.stochastic, d[k], nrg[b].u[k], ov[b][0][0], ov[b][0][1]);
             acc[b][0][k] += G2 * R[k];
             acc[b][1][k] += G2;
             const float gh = (float)G2 * qrg[b].inv_m;
@@ -284,7 +280,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
           load4_i8(B.qn_codes, e, qn);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            G[k] = quant1(qng[b], B.qng.stochastic, d[k], nng[b].u[k], ov[2 * b + 1][0], ov[2 * b + 1][1]);
+            G[k] = quant1(qng[b], B.qng.stochastic, d[k], nng[b].u[k], ov[b][1][0], ov[b][1][1]);
             acc[b][2][k] += G[k];
             acc[b][3][k] += G[k] * qn[k];
           }
@@ -294,21 +290,32 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
         }
       }
     }
-    for (int b = 0; b < nb; ++b)
+  }
+  {
+    const int per = chan_period(C);
+    const bool own = chan_owner(per);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (acc[b][s][k])
-            atomicAdd((unsigned long long*)&S[b * 4 * C + s * C + c0 + k], (unsigned long long)(long long)acc[b][s][k]);
+        for (int k = 0; k < 4; ++k) {
+          const int v = wave_chan_reduce(acc[b][s][k], per);
+          if (own && v) atomicAdd((unsigned long long*)&S[b * 4 * C + s * C + c0 + k], (unsigned long long)(long long)v);
+        }
   }
-  for (int b = 0; b < nb; ++b) {
-    if (qrg[b].active) block_flush_counts(br[b]->qrg, ov[2 * b][0], ov[2 * b][1], sh_cnt);
-    if (qng[b].active) block_flush_counts(br[b]->qng, ov[2 * b + 1][0], ov[2 * b + 1][1], sh_cnt);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
+    if (qrg[b].active) block_flush_counts(B.qrg, ov[b][0][0], ov[b][0][1], sh_cnt);
+    if (qng[b].active) block_flush_counts(B.qng, ov[b][1][0], ov[b][1][1], sh_cnt);
   }
   __syncthreads();
-  for (int b = 0; b < nb; ++b)
-    if (br[b]->sums) block_flush_sums(S + b * 4 * C, 4 * C, br[b]->sums, 4 * C);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
+    if (B.sums) block_flush_sums(S + b * 4 * C, 4 * C, B.sums, 4 * C);
+  }
 }
 
 // ============================================================================ backward pass B
@@ -347,10 +354,10 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
   int ov1 = 0, ov2 = 0;
   const int64_t groups = a.inner >> 2;
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int c0 = (int)((g << 2) % C);
+  int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   if (g < groups) {
-    const int c0 = (int)((g << 2) % C);
     const Noise4 no = noise_for(a.qo, so, g);
-    int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
     for (int64_t r = r0; r < rend; ++r) {
@@ -382,12 +389,15 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
         store4_i8(a.gq, e, c, 0);
       }
     }
-    if (want_q && a.gcolsum) {
+  }
+  if (want_q && a.gcolsum) {
+    const int per = chan_period(C);
+    const bool own = chan_owner(per);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (s1[k]) atomicAdd((unsigned long long*)&tmp[c0 + k], (unsigned long long)(long long)s1[k]);
-        if (s2[k]) atomicAdd((unsigned long long*)&tmp[C + c0 + k], (unsigned long long)(long long)s2[k]);
-      }
+    for (int k = 0; k < 4; ++k) {
+      const int v1 = wave_chan_reduce(s1[k], per), v2 = wave_chan_reduce(s2[k], per);
+      if (own && v1) atomicAdd((unsigned long long*)&tmp[c0 + k], (unsigned long long)(long long)v1);
+      if (own && v2) atomicAdd((unsigned long long*)&tmp[C + c0 + k], (unsigned long long)(long long)v2);
     }
   }
   if (want_q) block_flush_counts(a.qo, ov1, ov2, sh_cnt);
@@ -417,7 +427,7 @@ __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lb
 bool grid_for(int64_t rows, int64_t inner, dim3& grid, int& rpt) {
   const int64_t groups = inner / 4;
   const int64_t gblocks = (groups + kThreads - 1) / kThreads;
-  int64_t r = (gblocks * rows) / 2048;
+  int64_t r = (gblocks * rows) / 512;
   if (r < 1) r = 1;
   if (r > 64) r = 64;
   const int64_t yb = (rows + r - 1) / r;
@@ -439,7 +449,10 @@ extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
   const size_t shm = sizeof(float) * 8 * a->C + sizeof(long long) * 2 * a->C;
-  hipLaunchKernelGGL(chain_fwd_kernel, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  if (a->has_b2)
+    hipLaunchKernelGGL(chain_fwd_kernel<2>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  else
+    hipLaunchKernelGGL(chain_fwd_kernel<1>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
   return (int)hipGetLastError();
 }
 
@@ -449,7 +462,10 @@ extern "C" int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream) {
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
   const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 8 * a->C;
-  hipLaunchKernelGGL(chain_bwd_a_kernel, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  if (a->has_b2)
+    hipLaunchKernelGGL(chain_bwd_a_kernel<2>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  else
+    hipLaunchKernelGGL(chain_bwd_a_kernel<1>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
   return (int)hipGetLastError();
 }
 

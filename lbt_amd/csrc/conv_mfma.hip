@@ -269,14 +269,24 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
   for (int i = threadIdx.x; i < CI * CO; i += kThreads) dst[i] = red[i];
 }
 
-__global__ void wgrad_reduce_kernel(const int32_t* __restrict__ slab, int nsplit, int K, int Cout, int x_u8off,
-                                    const int64_t* __restrict__ gcolsum, lbt_qdesc qx, lbt_qdesc qg,
-                                    const float* __restrict__ w, float wd2, float* __restrict__ dw) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// 256 threads = 32 outputs x 8 split groups; coalesced 128-B slab rows; exact int64 sums.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const int32_t* __restrict__ slab, int nsplit, int K,
+                                                           int Cout, int x_u8off, const int64_t* __restrict__ gcolsum,
+                                                           lbt_qdesc qx, lbt_qdesc qg, const float* __restrict__ w,
+                                                           float wd2, float* __restrict__ dw) {
+  __shared__ long long red[8][32];
+  const int lo = threadIdx.x & 31, sg = threadIdx.x >> 5;
   const int64_t total = (int64_t)K * Cout;
-  if (i >= total) return;
+  const int64_t i = (int64_t)blockIdx.x * 32 + lo;
   long long s = 0;
-  for (int b = 0; b < nsplit; ++b) s += slab[(int64_t)b * total + i];
+  if (i < total) {
+#pragma unroll 4
+    for (int b = sg; b < nsplit; b += 8) s += slab[(int64_t)b * total + i];
+  }
+  red[sg][lo] = s;
+  __syncthreads();
+  if (sg != 0 || i >= total) return;
+  for (int k = 1; k < 8; ++k) s += red[k][lo];
   if (x_u8off && gcolsum) {
     const int co = (int)(i % Cout);
     long long cs = 0;
@@ -369,7 +379,7 @@ extern "C" int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_
                                      const int64_t* gcolsum, lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2,
                                      float* dw, void* stream) {
   const int64_t total = (int64_t)K * Cout;
-  const int64_t blocks = (total + 255) / 256;
+  const int64_t blocks = (total + 31) / 32;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, slab, nsplit, K,
                      Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw);
   return (int)hipGetLastError();

@@ -136,6 +136,23 @@ LBT_DEV void block_flush_sums(const long long* sh, int n, int64_t* dst, int stri
     if (sh[i]) atomicAdd((unsigned long long*)&d[i], (unsigned long long)sh[i]);
 }
 
+// Per-channel partial sums of "channel-quad" threads: thread g owns elements 4g..4g+3 of a row,
+// i.e. channels c0..c0+3 with c0 = 4g mod C, so lanes whose g differ by a multiple of C/4 hold the
+// same channels. chan_period(C) = C/4 when that is a power of two <= 32 (then a xor-butterfly
+// over offsets C/4 .. 32 leaves the wave total in lanes 0 .. C/4-1), else 0 (no pre-reduction).
+LBT_DEV int chan_period(int C) {
+  const int p = C >> 2;
+  return (C % 4 == 0 && p > 0 && p <= 32 && (p & (p - 1)) == 0) ? p : 0;
+}
+// All 64 lanes must call it.
+LBT_DEV int wave_chan_reduce(int v, int period) {
+  if (period)
+    for (int o = period; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// true if this lane should publish its (reduced) per-channel partials
+LBT_DEV bool chan_owner(int period) { return period == 0 || (int)(threadIdx.x & 63) < period; }
+
 // Store one code in the requested encoding.
 LBT_DEV void store_code(void* out, int kind, int64_t i, int qv, float inv_m) {
   switch (kind) {

@@ -31,11 +31,12 @@ __global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
     __syncthreads();
   }
   int ov1 = 0, ov2 = 0;
+  int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   if (g < groups) {
     Noise4 n = {{0.f, 0.f, 0.f, 0.f}};
     if (q.stochastic) n = noise4(g, q.qid, s.step, q.seed);
-    int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
     const int64_t rend = r0 + rpt < rows ? r0 + rpt : rows;
+#pragma unroll 4
     for (int64_t r = r0; r < rend; ++r) {
       const int64_t base = r * inner + (g << 2);
       const float4 v = *reinterpret_cast<const float4*>(x + base);
@@ -65,12 +66,17 @@ __global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) { s1[k] += c[k]; s2[k] += c[k] * c[k]; }
     }
-    if (chsum) {
-      const int ch = (int)((g << 2) % C);
+  }
+  if (chsum) {
+    const int per = chan_period(C);
+    const int ch = (int)((g << 2) % C);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { s1[k] = wave_chan_reduce(s1[k], per); s2[k] = wave_chan_reduce(s2[k], per); }
+    if (chan_owner(per)) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        atomicAdd((unsigned long long*)&sh_sum[(ch + k) % C], (unsigned long long)(long long)s1[k]);
-        atomicAdd((unsigned long long*)&sh_sum[C + (ch + k) % C], (unsigned long long)(long long)s2[k]);
+        if (s1[k]) atomicAdd((unsigned long long*)&sh_sum[ch + k], (unsigned long long)(long long)s1[k]);
+        if (s2[k]) atomicAdd((unsigned long long*)&sh_sum[C + ch + k], (unsigned long long)(long long)s2[k]);
       }
     }
   }
@@ -174,8 +180,8 @@ extern "C" int lbt_dfxp_quantize(const float* x, void* out, int out_kind, int64_
   if (vec) {
     const int64_t groups = inner / 4;
     const int64_t gblocks = (groups + kThreads - 1) / kThreads;
-    // aim for >= ~2048 blocks in flight; at least 1 row per thread
-    int64_t rpt = (gblocks * rows) / 2048;
+    // aim for ~512 fat workgroups: Philox and the per-channel reductions amortise over rpt rows
+    int64_t rpt = (gblocks * rows) / 512;
     if (rpt < 1) rpt = 1;
     if (rpt > 64) rpt = 64;
     const int64_t yblocks = (rows + rpt - 1) / rpt;

@@ -35,6 +35,18 @@ class _Cache:
     def __init__(self):
         self.d = {}
 
+    def sums(self, key, n, ctx):
+        """An int64 reduction buffer from the context's sums arena, zeroed before use (unless a
+        Trainer zeroes the whole arena once per step)."""
+        t = self.d.get(key)
+        if t is None or t.numel() < n:
+            t = ctx.alloc_sums(n)
+            self.d[key] = t
+        t = t[:n]
+        if not ctx.sums_managed:
+            t.zero_()
+        return t
+
     def get(self, key, shape, dtype, device, zero=False):
         t = self.d.get(key)
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
@@ -82,6 +94,7 @@ class Conv2d_q(Layer_q):
         self.name, self.use_bias, self.bits = name, use_bias, bits
         self.target_overflow_rate, self.weight_decay = target_overflow_rate, weight_decay
         self.input_nonnegative = input_nonnegative
+        self.need_input_grad = True  # the model clears it for its first layer (TF prunes that dX)
         limit = (3 / (h * w * Cin)) ** 0.5
         self.W = _as_param(_rng(ctx, name + "/W").uniform(-limit, limit, size=ksize).astype(np.float32), ctx)
         self.dW = torch.zeros_like(self.W)
@@ -149,8 +162,7 @@ class Conv2d_q(Layer_q):
         d = self.d
         Cout, Cin = d.Cout, d.Cin
         dev = grad.device
-        gsum = self._c.get("gsum", (ops.NSHARD * 2 * Cout,), torch.int64, dev)
-        gsum.zero_()
+        gsum = self._c.sums("gsum", ops.NSHARD * 2 * Cout, self.ctx)
         self.gradq = ops.quantize(grad, self.grad_range, OUT_I8, out=self._c.get("gq", grad.shape, torch.int8, dev),
                                   chsum=gsum, C=Cout)
         wd2 = ops.f32(2 * self.weight_decay)
@@ -167,6 +179,8 @@ class Conv2d_q(Layer_q):
                               self.grad_range.desc, self.W, wd2, self.dW)
         if self.use_bias:
             ops.bias_grad(gsum, Cout, self.grad_range.desc, self.db)
+        if not self.need_input_grad:
+            return None
         dx = self._c.get("dx", (d.N, d.H, d.W, Cin), torch.float32, dev)
         if self.mfma:
             ops.conv_dgrad_i8(self.gradq, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
@@ -239,8 +253,7 @@ class Dense_q(Layer_q):
     def backward(self, grad, stochastic=True):
         d = self.d
         dev = grad.device
-        gsum = self._c.get("gsum", (ops.NSHARD * 2 * self.units,), torch.int64, dev)
-        gsum.zero_()
+        gsum = self._c.sums("gsum", ops.NSHARD * 2 * self.units, self.ctx)
         self.gradq = ops.quantize(grad, self.grad_range, OUT_I8, out=self._c.get("gq", grad.shape, torch.int8, dev),
                                   chsum=gsum, C=self.units)
         ns = ops.wgrad_nsplit(d, generic=True)
@@ -319,8 +332,7 @@ class Normalization_q(Layer_q):
         dev = X.device
         C = X.shape[-1]
         rows, inner = ops.rows_inner(tuple(X.shape))
-        chsum = self._c.get("chsum", (ops.NSHARD * 2 * C,), torch.int64, dev)
-        chsum.zero_()
+        chsum = self._c.sums("chsum", ops.NSHARD * 2 * C, self.ctx)
         self.q = ops.quantize(X, self.X_range, OUT_I8, out=self._c.get("q", X.shape, torch.int8, dev), chsum=chsum,
                               C=C)
         self.n = X.numel() // C
@@ -338,8 +350,7 @@ class Normalization_q(Layer_q):
         dev = grad.device
         C = self.C
         rows, inner = ops.rows_inner(tuple(grad.shape))
-        sums = self._c.get("sums", (ops.NSHARD * 4 * C,), torch.int64, dev)
-        sums.zero_()
+        sums = self._c.sums("sums", ops.NSHARD * 4 * C, self.ctx)
         G = self._c.get("G", grad.shape, torch.int8, dev)
         self.grad_range.observe(grad.numel())
         a = ChainBwdA()
@@ -411,8 +422,7 @@ class Rescale_q(Layer_q):
         dev = grad.device
         C = self.C
         rows, inner = ops.rows_inner(tuple(grad.shape))
-        sums = self._c.get("sums", (ops.NSHARD * 4 * C,), torch.int64, dev)
-        sums.zero_()
+        sums = self._c.sums("sums", ops.NSHARD * 4 * C, self.ctx)
         dx = self._c.get("dx", grad.shape, torch.float32, dev)
         self.grad_range.observe(grad.numel())
         a = ChainBwdA()

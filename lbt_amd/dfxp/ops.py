@@ -9,6 +9,34 @@ from .._lib import NSHARD, OUT_F32, OUT_I8, OUT_I16, OUT_U8OFF, ConvDesc, QDesc,
 
 NO_Q = _lib.NO_Q
 
+# --------------------------------------------------------------------------- launch timing hook
+# When PROFILE is a dict, every wrapped launch is bracketed by HIP events on the current stream
+# and its algorithmic bytes (each operand read once, each output written once) are recorded as
+# PROFILE[kernel] -> [(start_event, end_event, bytes), ...]  (see lbt_amd/roofline.py).
+PROFILE = None
+
+
+class _Timed:
+    def __init__(self, kernel, nbytes):
+        self.kernel, self.nbytes = kernel, nbytes
+
+    def __enter__(self):
+        if PROFILE is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if PROFILE is not None and exc[0] is None:
+            self.e1.record()
+            PROFILE.setdefault(self.kernel, []).append((self.e0, self.e1, int(self.nbytes)))
+        return False
+
+
+def _code_bytes(kind):
+    return {OUT_I8: 1, OUT_U8OFF: 1, OUT_I16: 2, OUT_F32: 4}[kind]
+
 
 def _check(t, dtype, name):
     if not t.is_cuda:
@@ -44,7 +72,9 @@ def quantize(x, q, kind, out=None, chsum=None, C=0, stats=True):
     if stats:
         q.observe(x.numel())
     desc = q.desc if stats else q.desc_nostats()
-    call("lbt_dfxp_quantize", ptr(x), ptr(out), kind, rows, inner, desc, ptr(chsum), int(C), stream())
+    vec = inner % 4 == 0 and inner >= 64 and x.data_ptr() % 16 == 0 and (chsum is None or C % 4 == 0)
+    with _Timed("quantize_rows_kernel" if vec else "quantize_generic_kernel", x.numel() * (4 + _code_bytes(kind))):
+        call("lbt_dfxp_quantize", ptr(x), ptr(out), kind, rows, inner, desc, ptr(chsum), int(C), stream())
     return out
 
 
@@ -104,11 +134,24 @@ def mfma_ok(Cin, Cout):
 
 
 def conv_fwd_i8(xq, x_u8off, wf, ksf, wcolsum, d, qx, qw, y=None, yq=None, qout=None, ychsum=None):
+    M = d.N * d.Ho * d.Wo
+    nb = xq.numel() + wf.numel() + (M * d.Cout * 4 if y is not None else 0) + (M * d.Cout if yq is not None else 0)
+    with _Timed("conv_fwd_i8", nb):
+        _conv_fwd_i8(xq, x_u8off, wf, ksf, wcolsum, d, qx, qw, y, yq, qout, ychsum)
+
+
+def _conv_fwd_i8(xq, x_u8off, wf, ksf, wcolsum, d, qx, qw, y, yq, qout, ychsum):
     call("lbt_conv_fwd_i8", ptr(xq), int(x_u8off), ptr(wf), int(ksf), ptr(wcolsum), d, qx, qw, ptr(y), ptr(yq),
          qout if qout is not None else NO_Q, ptr(ychsum), stream())
 
 
 def conv_dgrad_i8(gq, wd, ksd, d, qg, qw, dx, add_src=None):
+    nb = gq.numel() + wd.numel() + dx.numel() * (8 if add_src is not None else 4)
+    with _Timed("conv_dgrad_i8", nb):
+        _conv_dgrad_i8(gq, wd, ksd, d, qg, qw, dx, add_src)
+
+
+def _conv_dgrad_i8(gq, wd, ksd, d, qg, qw, dx, add_src):
     call("lbt_conv_dgrad_i8", ptr(gq), ptr(wd), int(ksd), d, qg, qw, ptr(dx), ptr(add_src), stream())
 
 
@@ -124,6 +167,11 @@ def wgrad_nsplit(d, generic=False):
 
 
 def conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit):
+    with _Timed("conv_wgrad_i8", xq.numel() + gq.numel() + nsplit * d.KH * d.KW * d.Cin * d.Cout * 4):
+        _conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit)
+
+
+def _conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit):
     call("lbt_conv_wgrad_i8", ptr(xq), int(x_u8off), ptr(gq), d, ptr(slab), int(nsplit), stream())
 
 
@@ -145,16 +193,41 @@ def conv_wgrad_generic(xq, x_i16, gq, d, slab, nsplit):
 
 
 # ----------------------------------------------------------------------------- BN chains
+def _chain_fwd_bytes(a):
+    per = 0
+    for b in ([a.b1, a.b2] if a.has_b2 else [a.b1]):
+        per += 1 if b.nrm.q else 4
+        per += 1 if b.rout else 0
+    per += 4 if a.res else 0
+    per += 4 if a.y else 0
+    per += _code_bytes(a.o1_kind) if a.o1 else 0
+    per += _code_bytes(a.o2_kind) if a.o2 else 0
+    return per * a.rows * a.inner
+
+
+def _chain_bwd_a_bytes(a):
+    per = 4 + (4 if a.y_mask else 0) + (4 if a.gmask_out else 0)
+    for b in ([a.b1, a.b2] if a.has_b2 else [a.b1]):
+        per += 1 if (b.R and (b.qrg.bits or a.mask_from_r)) else 0
+        per += 1 if b.qng.bits else 0
+        per += 1 if b.gout else (4 if b.dout else 0)
+    return per * a.rows * a.inner
+
+
 def chain_fwd(desc):
-    call("lbt_bn_chain_fwd", _lib.ctypes.byref(desc), stream())
+    with _Timed("chain_fwd_kernel", _chain_fwd_bytes(desc)):
+        call("lbt_bn_chain_fwd", _lib.ctypes.byref(desc), stream())
 
 
 def chain_bwd_a(desc):
-    call("lbt_bn_chain_bwd_a", _lib.ctypes.byref(desc), stream())
+    with _Timed("chain_bwd_a_kernel", _chain_bwd_a_bytes(desc)):
+        call("lbt_bn_chain_bwd_a", _lib.ctypes.byref(desc), stream())
 
 
 def chain_bwd_b(desc):
-    call("lbt_bn_chain_bwd_b", _lib.ctypes.byref(desc), stream())
+    per = 2 + (4 if desc.dx else 0) + (1 if desc.gq else 0)
+    with _Timed("chain_bwd_b_kernel", per * desc.rows * desc.inner):
+        call("lbt_bn_chain_bwd_b", _lib.ctypes.byref(desc), stream())
 
 
 def bn_param_grads(sums, C, qrg, qr, gamma, wd2, dgamma, dbeta):

@@ -23,6 +23,8 @@ class Model:
         self.ctx = ctx or default_context()
         self.training = True
         self.layers = self.get_layers()
+        if self.layers and hasattr(self.layers[0], "need_input_grad"):
+            self.layers[0].need_input_grad = False  # d loss / d input is never consumed
         self._c = _Cache()
         self.logits = None
         self.loss = None

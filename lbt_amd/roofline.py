@@ -1,0 +1,74 @@
+"""Live roofline of the dominant kernel of the training step (used by bench.py).
+
+One eager training step is run with every wrapped launch bracketed by HIP events recorded on
+the stream the kernel is launched on (``lbt_amd.dfxp.ops.PROFILE``). The kernel with the largest
+total event time is the dominant one; for it
+
+    achieved = (algorithmic bytes per launch, each operand read once and each output written
+                once -- see ops._Timed call sites) / (average event-timed launch duration)
+
+is reported against the MI355X HBM3E peak (8 TB/s, MI355X_MICROARCH.md "Chip-level parameters").
+Every kernel of this path is an HBM-bound element pass or a low-intensity int8 GEMM
+(<= 227 int-op/B vs a ~625 op/B ridge), so the bound is "hbm".
+"""
+import json
+import os
+
+import torch
+
+from .dfxp import ops
+
+HBM_PEAK_GBS = 8000.0
+
+
+def measure_step_kernels(trainer, x, y, steps=3):
+    """{kernel: (launches per step, avg us, avg algorithmic bytes)} over `steps` eager steps.
+    Parameters / exponents are restored afterwards so the measurement does not perturb training."""
+    flat = trainer.flat
+    saved = (flat.w.clone(), flat.a.clone(), trainer.ctx.exps.clone(), trainer.ctx.step.clone())
+    ops.PROFILE = {}
+    try:
+        for _ in range(steps):
+            # hold the stream with a ~150 ms spin so the host enqueues the whole step (event
+            # records + launches) before the GPU reaches it: the events then bracket device
+            # execution of each kernel, not host submission gaps
+            torch.cuda.synchronize()
+            torch.cuda._sleep(300_000_000)
+            trainer._eager(x, y)
+        torch.cuda.synchronize()
+        prof = ops.PROFILE
+    finally:
+        ops.PROFILE = None
+    flat.w.copy_(saved[0])
+    flat.a.copy_(saved[1])
+    trainer.ctx.exps.copy_(saved[2])
+    trainer.ctx.step.copy_(saved[3])
+    trainer.ctx.counts.zero_()
+    out = {}
+    for k, recs in prof.items():
+        ms = [e0.elapsed_time(e1) for e0, e1, _ in recs]
+        out[k] = (len(recs) / steps, 1000.0 * sum(ms) / len(ms), sum(b for _, _, b in recs) / len(recs),
+                  1000.0 * sum(ms) / steps)
+    return out
+
+
+def measure_dominant(trainer, x, y, traffic_file=None):
+    stats = measure_step_kernels(trainer, x, y)
+    name = max(stats, key=lambda k: stats[k][3])
+    calls, avg_us, avg_bytes, _ = stats[name]
+    achieved = avg_bytes / (avg_us * 1e-6) / 1e9
+    traffic = None
+    tf = traffic_file or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                                      "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            t = json.load(open(tf))
+            if name in t.get("kernels", {}):
+                traffic = t["kernels"][name]["hbm_bytes_per_launch"]
+        except Exception:  # pragma: no cover
+            traffic = None
+    return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "avg_launch_us": round(avg_us, 3), "algorithmic_bytes_per_launch": int(avg_bytes),
+            "launches_per_step": calls,
+            "per_kernel_us_per_step": {k: round(v[3], 1) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][3])}}

@@ -67,7 +67,7 @@ class Quantizer:
 
 
 class DfxpContext:
-    def __init__(self, device="cuda", capacity=1024, seed=0, world_size=1):
+    def __init__(self, device="cuda", capacity=1024, seed=0, world_size=1, sums_capacity=1 << 20):
         self.device = torch.device(device)
         self.capacity = capacity
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -81,6 +81,11 @@ class DfxpContext:
         self.nelem = torch.zeros(capacity, dtype=torch.float32, device=dev)
         self.quantizers = []
         self.by_name = {}
+        # per-step integer reduction buffers (BN channel sums, grad column sums), bump-allocated
+        # from one arena so a whole step zeroes them with ONE fill (see zero_sums).
+        self.sums_arena = torch.zeros(sums_capacity, dtype=torch.int64, device=dev)
+        self._sums_used = 0
+        self.sums_managed = False  # True while a Trainer zeroes the arena once per step
 
     def quantizer(self, name, bits, initial=2, target=0.0, stochastic=True):
         """Register a quantiser (a ``*_range`` variable initialised to ``initial``)."""
@@ -101,6 +106,18 @@ class DfxpContext:
         self.quantizers.append(q)
         self.by_name[name] = q
         return q
+
+    def alloc_sums(self, n):
+        n = (int(n) + 31) // 32 * 32
+        if self._sums_used + n > self.sums_arena.numel():
+            raise RuntimeError("DfxpContext sums arena exhausted (raise sums_capacity)")
+        t = self.sums_arena[self._sums_used:self._sums_used + n]
+        self._sums_used += n
+        return t
+
+    def zero_sums(self):
+        if self._sums_used:
+            self.sums_arena[: self._sums_used].zero_()
 
     # the 'update_range' collection (trainer.py:63,157)
     def update_range_op(self):

@@ -64,6 +64,7 @@ class Trainer:
             raise ValueError("DfxpContext.world_size (%d) must equal the process-group size (%d)"
                              % (self.ctx.world_size, self.world))
         self.flat = FlatParams(model)
+        self.ctx.sums_managed = True
         self.global_step = 0
         self._graphs = None
         self._static = None
@@ -88,6 +89,7 @@ class Trainer:
     # -- the step ----------------------------------------------------------------------------
     def _fwd_bwd(self, X, y):
         m = self.model
+        self.ctx.zero_sums()
         m.forward(X)
         m.compute_loss(y)
         m.backward()

@@ -317,3 +317,22 @@ def test_torch_face_conv_matches_layer():
     out = lin(torch.relu(bn(y.detach())).reshape(4, -1))
     out.sum().backward()
     assert torch.isfinite(lin.weight.grad).all() and torch.isfinite(bn.weight.grad).all()
+
+
+def test_bench_workload_loss_trajectory_matches_oracle():
+    """The exact bench workload (B=128, bench.py batches, graph-captured Trainer): the first 3 steps'
+    losses and exponents match the oracle's step-for-step (the reference semantics on this random-
+    label synthetic data diverge after a few steps in BOTH implementations identically)."""
+    import bench
+    from lbt_amd.trainer import Trainer
+    ctx, gm, om = _build_pair(seed=0)
+    state = dict(params=gpu_params(gm), accum=None, ranges=oresnet.init_ranges(om), step=0)
+    state["accum"] = {k: np.zeros_like(v) for k, v in state["params"].items()}
+    tr = Trainer(gm, lr=1e-2, momentum=0.9, batch_size=128, use_graph=True)
+    xs, ys = bench.synthetic_batches(4, 128, 1000, DEV)
+    for i in range(3):
+        loss = tr.step(xs[i], ys[i]).item()
+        lref, state, _ = oresnet.train_step(om, state, xs[i].cpu().numpy(), ys[i].cpu().numpy(), lr=1e-2,
+                                            momentum=0.9, seed=0)
+        assert abs(loss - lref) <= 1e-5 * abs(lref), (i, loss, lref)
+        assert ctx.ranges() == state["ranges"], i
