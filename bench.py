@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (diagnostics)")
+    ap.add_argument("--layerwise", action="store_true", help="run the Layer_q path instead of the fused plan")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
@@ -99,6 +100,9 @@ def main():
 
     ctx = DfxpContext(device=device, seed=0, world_size=world)
     model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+    if not args.layerwise:
+        from lbt_amd.fused import FusedResNet
+        model = FusedResNet(model)
     trainer = Trainer(model, lr=1e-2, momentum=0.9, batch_size=args.batch, use_graph=not args.eager)
     trainer.init_model()
     xs, ys = synthetic_batches(4, args.batch, seed=1000 + rank, device=device)
@@ -138,7 +142,8 @@ def main():
         "data": "synthetic CIFAR-10-shaped batches (uniform uint8 pixels, (p-127.5)/128), random-init weights",
         "config": {"workload": "ResNet-20 CIFAR-10 8-bit DFXP W/A/G train step (fwd+bwd+SGD-momentum+range update)",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch, "image": [32, 32, 3],
-                   "parallelism": "dp%d" % world, "hip_graph": not args.eager, "final_loss": round(loss, 4)},
+                   "parallelism": "dp%d" % world, "hip_graph": not args.eager,
+                   "executor": "layerwise" if args.layerwise else "fused", "final_loss": round(loss, 4)},
     }
     if rank == 0 and world == 1 and not args.no_roofline:
         from lbt_amd.roofline import measure_dominant

@@ -243,6 +243,35 @@ int lbt_sgd_momentum(float* w, float* a, const float* g, int64_t n, float lr, fl
 int lbt_bias_add(float* y, const float* bq, int64_t n, int32_t C, void* stream);
 int lbt_bias_grad(const int64_t* chsum, int32_t C, lbt_qdesc qg, float* db, void* stream);
 
+/* ---------------------------------------------------------------- batched (one launch per step)
+ * Job arrays live in DEVICE memory (uploaded once by the caller); grid.y = job index.          */
+
+/* lbt_dfxp_quantize_weight for many weights. */
+typedef struct lbt_wjob {
+  const float* w; int32_t KH, KW, Cin, Cout; lbt_qdesc q;
+  int8_t* w_hwio; int8_t* wf; int32_t ksf; int8_t* wd; int32_t ksd; int32_t* colsum;
+} lbt_wjob;
+int lbt_dfxp_quantize_weights(const lbt_wjob* jobs, int32_t njobs, int32_t max_cout, void* stream);
+
+/* lbt_dfxp_quantize (generic path) for many small tensors (Rescale_q gamma / beta, :679-682). */
+typedef struct lbt_qjob {
+  const float* x; void* out; int32_t out_kind; int64_t n, inner; lbt_qdesc q;
+} lbt_qjob;
+int lbt_dfxp_quantize_many(const lbt_qjob* jobs, int32_t njobs, void* stream);
+
+/* lbt_conv_wgrad_reduce for many layers. */
+typedef struct lbt_rjob {
+  const int32_t* slab; int32_t nsplit, K, Cout, x_u8off; const int64_t* gcolsum;
+  lbt_qdesc qx, qg; const float* w; float wd2; float* dw;
+} lbt_rjob;
+int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, int32_t max_blocks, void* stream);
+
+/* lbt_bn_param_grads for many Rescale_q layers. */
+typedef struct lbt_pjob {
+  const int64_t* sums; int32_t C; lbt_qdesc qrg, qr; const float* gamma; float wd2; float* dgamma; float* dbeta;
+} lbt_pjob;
+int lbt_bn_param_grads_many(const lbt_pjob* jobs, int32_t njobs, int32_t max_c, void* stream);
+
 /* ABI version for the Python loader. */
 int lbt_abi_version(void);
 

@@ -71,6 +71,28 @@ class ChainBwdB(ctypes.Structure):
                 ("rows", c_int64), ("inner", c_int64), ("C", c_int32)]
 
 
+class WJob(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("KH", c_int32), ("KW", c_int32), ("Cin", c_int32), ("Cout", c_int32),
+                ("q", QDesc), ("w_hwio", c_void_p), ("wf", c_void_p), ("ksf", c_int32), ("wd", c_void_p),
+                ("ksd", c_int32), ("colsum", c_void_p)]
+
+
+class QJob(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("out", c_void_p), ("out_kind", c_int32), ("n", c_int64), ("inner", c_int64),
+                ("q", QDesc)]
+
+
+class RJob(ctypes.Structure):
+    _fields_ = [("slab", c_void_p), ("nsplit", c_int32), ("K", c_int32), ("Cout", c_int32), ("x_u8off", c_int32),
+                ("gcolsum", c_void_p), ("qx", QDesc), ("qg", QDesc), ("w", c_void_p), ("wd2", c_float),
+                ("dw", c_void_p)]
+
+
+class PJob(ctypes.Structure):
+    _fields_ = [("sums", c_void_p), ("C", c_int32), ("qrg", QDesc), ("qr", QDesc), ("gamma", c_void_p),
+                ("wd2", c_float), ("dgamma", c_void_p), ("dbeta", c_void_p)]
+
+
 _P = c_void_p
 _SIGS = {
     "lbt_abi_version": [],
@@ -98,6 +120,10 @@ _SIGS = {
     "lbt_sgd_momentum": [_P, _P, _P, c_int64, c_float, c_float, c_float, _P],
     "lbt_bias_add": [_P, _P, c_int64, c_int32, _P],
     "lbt_bias_grad": [_P, c_int32, QDesc, _P, _P],
+    "lbt_dfxp_quantize_weights": [_P, c_int32, c_int32, _P],
+    "lbt_dfxp_quantize_many": [_P, c_int32, _P],
+    "lbt_conv_wgrad_reduce_many": [_P, c_int32, c_int32, _P],
+    "lbt_bn_param_grads_many": [_P, c_int32, c_int32, _P],
 }
 EXPORTED = sorted(_SIGS)
 

@@ -1,0 +1,135 @@
+// batched.hip -- one launch for the per-layer "small" work of a training step:
+//   weight quantisation + GEMM operand packing of every conv / dense (dynamic_fixed_point.py:289-290,386-387),
+//   gamma / beta quantisation of every Rescale_q (:679-682), the split reduction + dequant + 2*wd*W of every
+//   weight gradient (:302, :457) and every Rescale_q's dgamma / dbeta (:689-690).
+// Each of these is a few KB of work whose cost as its own kernel is the ~2-4 us launch/latency floor; ~90
+// such launches per ResNet-20 step become 4. Job descriptors are read from device memory (grid.y = job).
+#include "dfxp_device.h"
+
+using namespace lbt;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__global__ __launch_bounds__(kThreads) void quantize_weights_kernel(const lbt_wjob* __restrict__ jobs) {
+  __shared__ int red[kThreads / 64];
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const lbt_wjob j = jobs[blockIdx.y];
+  const int co = blockIdx.x;
+  if (co >= j.Cout) return;  // uniform per block
+  const QState s = qstate(j.q);
+  const int K = j.KH * j.KW * j.Cin;
+  const int64_t inner = (int64_t)j.KW * j.Cin * j.Cout;
+  const int csi = (j.Cin + 15) / 16, cso = (j.Cout + 15) / 16;
+  int ov1 = 0, ov2 = 0, csum = 0;
+  for (int k = threadIdx.x; k < K; k += kThreads) {
+    const int tap = k / j.Cin, ci = k % j.Cin;
+    const int64_t idx = (int64_t)k * j.Cout + co;
+    const float u = j.q.stochastic ? noise1(idx % inner, j.q.qid, s.step, j.q.seed) : 0.f;
+    const int c = quant1(s, j.q.stochastic, j.w[idx], u, ov1, ov2);
+    csum += c;
+    if (j.w_hwio) j.w_hwio[idx] = (int8_t)c;
+    if (j.wf) j.wf[((int64_t)co * j.ksf + tap * csi + ci / 16) * 16 + (ci & 15)] = (int8_t)c;
+    if (j.wd) j.wd[((int64_t)ci * j.ksd + tap * cso + co / 16) * 16 + (co & 15)] = (int8_t)c;
+  }
+  block_flush_counts(j.q, ov1, ov2, sh_cnt);
+  if (j.colsum) {
+    csum = wave_sum_i32(csum);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = csum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      j.colsum[co] = t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob* __restrict__ jobs) {
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const lbt_qjob j = jobs[blockIdx.y];
+  const QState s = qstate(j.q);
+  int ov1 = 0, ov2 = 0;
+  for (int64_t i = threadIdx.x; i < j.n; i += kThreads) {
+    const float u = j.q.stochastic ? noise1(i % j.inner, j.q.qid, s.step, j.q.seed) : 0.f;
+    const int c = quant1(s, j.q.stochastic, j.x[i], u, ov1, ov2);
+    store_code(j.out, j.out_kind, i, c, s.inv_m);
+  }
+  block_flush_counts(j.q, ov1, ov2, sh_cnt);
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs) {
+  __shared__ long long red[8][32];
+  const lbt_rjob j = jobs[blockIdx.y];
+  const int64_t total = (int64_t)j.K * j.Cout;
+  if ((int64_t)blockIdx.x * 32 >= total) return;  // uniform per block
+  const int lo = threadIdx.x & 31, sg = threadIdx.x >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 32 + lo;
+  long long s = 0;
+  if (i < total) {
+#pragma unroll 4
+    for (int b = sg; b < j.nsplit; b += 8) s += j.slab[(int64_t)b * total + i];
+  }
+  red[sg][lo] = s;
+  __syncthreads();
+  if (sg != 0 || i >= total) return;
+  for (int k = 1; k < 8; ++k) s += red[k][lo];
+  if (j.x_u8off && j.gcolsum) {
+    const int co = (int)(i % j.Cout);
+    long long cs = 0;
+    for (int k = 0; k < LBT_NSHARD; ++k) cs += j.gcolsum[(int64_t)k * 2 * j.Cout + co];
+    s += 128ll * cs;
+  }
+  const float scale = ldexpf(1.0f, -(frac_exp(j.qx) + frac_exp(j.qg)));
+  const float a = (float)s * scale;
+  const float b = j.wd2 * j.w[i];
+  j.dw[i] = a + b;
+}
+
+__global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
+  const lbt_pjob j = jobs[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= j.C) return;
+  long long sgr = 0, sg = 0;
+  for (int k = 0; k < LBT_NSHARD; ++k) {
+    sgr += j.sums[(int64_t)k * 4 * j.C + c];
+    sg += j.sums[(int64_t)k * 4 * j.C + j.C + c];
+  }
+  const double g2 = ldexp(1.0, -frac_exp(j.qrg)), r = ldexp(1.0, -frac_exp(j.qr));
+  const float a = (float)((double)sgr * (g2 * r));
+  const float b = j.wd2 * j.gamma[c];
+  j.dgamma[c] = a + b;
+  j.dbeta[c] = (float)((double)sg * g2);
+}
+
+}  // namespace
+
+extern "C" int lbt_dfxp_quantize_weights(const lbt_wjob* jobs, int32_t njobs, int32_t max_cout, void* stream) {
+  if (njobs <= 0) return LBT_OK;
+  if (njobs > 65535 || max_cout <= 0) return LBT_EINVAL;
+  hipLaunchKernelGGL(quantize_weights_kernel, dim3(max_cout, njobs), dim3(kThreads), 0, (hipStream_t)stream, jobs);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_dfxp_quantize_many(const lbt_qjob* jobs, int32_t njobs, void* stream) {
+  if (njobs <= 0) return LBT_OK;
+  if (njobs > 65535) return LBT_EINVAL;
+  hipLaunchKernelGGL(quantize_many_kernel, dim3(1, njobs), dim3(kThreads), 0, (hipStream_t)stream, jobs);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, int32_t max_blocks, void* stream) {
+  if (njobs <= 0) return LBT_OK;
+  if (njobs > 65535 || max_blocks <= 0) return LBT_EINVAL;
+  hipLaunchKernelGGL(wgrad_reduce_many_kernel, dim3(max_blocks, njobs), dim3(256), 0, (hipStream_t)stream, jobs);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_bn_param_grads_many(const lbt_pjob* jobs, int32_t njobs, int32_t max_c, void* stream) {
+  if (njobs <= 0) return LBT_OK;
+  if (njobs > 65535 || max_c <= 0) return LBT_EINVAL;
+  hipLaunchKernelGGL(param_grads_many_kernel, dim3((max_c + 255) / 256, njobs), dim3(256), 0, (hipStream_t)stream,
+                     jobs);
+  return (int)hipGetLastError();
+}

@@ -129,44 +129,88 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(GemmArgs p) {
 
   // ---------------- epilogue
   const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
-  QState qs;
-  if (want_q) qs = qstate(p.qout);
-  int ov1 = 0, ov2 = 0;
-  const int64_t HWo = (int64_t)OH * OW;
+  if (!want_q) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    if (!(wave_live && j < ntw)) continue;
-    const int col = (nt0 + j) * 16 + r;
-    const int corr = p.colsum ? 128 * p.colsum[col] : 0;
-    int s1 = 0, s2 = 0;
+    for (int j = 0; j < 2; ++j) {
+      if (!(wave_live && j < ntw)) continue;
+      const int col = (nt0 + j) * 16 + r;
+      const int corr = p.colsum ? 128 * p.colsum[col] : 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t row = mtile * 16 + kg * 4 + i;
-      if (row >= p.M) continue;
-      const float v = (float)(acc[j][i] + corr) * scale;
-      const int64_t e = row * p.ncol + col;
-      if (p.y) p.y[e] = p.add_src ? v + p.add_src[e] : v;
-      if (want_q) {
-        const int64_t nidx = (row % HWo) * p.ncol + col;
-        const float u = p.qout.stochastic ? noise1(nidx, p.qout.qid, qs.step, p.qout.seed) : 0.f;
-        const int c = quant1(qs, p.qout.stochastic, v, u, ov1, ov2);
-        p.yq[e] = (int8_t)c;
-        s1 += c;
-        s2 += c * c;
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = mtile * 16 + kg * 4 + i;
+        if (row >= p.M) continue;
+        const float v = (float)(acc[j][i] + corr) * scale;
+        const int64_t e = row * p.ncol + col;
+        p.y[e] = p.add_src ? v + p.add_src[e] : v;
       }
     }
-    if (want_sum) {
-      s1 += __shfl_xor(s1, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (kg == 0) {
-        atomicAdd((unsigned long long*)&sh_sum[col], (unsigned long long)(long long)s1);
-        atomicAdd((unsigned long long*)&sh_sum[p.ncol + col], (unsigned long long)(long long)s2);
+    return;
+  }
+  // Quantising epilogue (Normalization_q input quantiser fused into the conv): the wave's
+  // 16 x (16*ntw) tile goes through LDS so each lane owns 4 CONSECUTIVE channels of one row:
+  // one Philox call per 4 outputs (its 4 noise indices share a Philox block), char4 stores,
+  // and per-channel sums reduced across the lanes that share a channel quad.
+  __shared__ float tile[4][16][33];
+  const QState qs = qstate(p.qout);
+  int ov1 = 0, ov2 = 0;
+  if (wave_live) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j >= ntw) continue;
+      const int col = (nt0 + j) * 16 + r;
+      const int corr = p.colsum ? 128 * p.colsum[col] : 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tile[wave][kg * 4 + i][j * 16 + r] = (float)(acc[j][i] + corr) * scale;
+    }
+  }
+  __syncthreads();
+  const int64_t HWo = (int64_t)OH * OW;
+  const int quads = 4 * ntw;  // channel quads per row of this wave's tile
+  int s1[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass >= ntw) continue;
+    const int id = pass * 64 + lane;
+    const int rr = id / quads, cq = id - rr * quads;
+    const int64_t row = mtile * 16 + rr;
+    if (!wave_live || row >= p.M) continue;
+    const int col0 = nt0 * 16 + cq * 4;
+    const Noise4 n = p.qout.stochastic ? noise4((uint64_t)(((row % HWo) * p.ncol + col0) >> 2), p.qout.qid, qs.step,
+                                                p.qout.seed)
+                                       : Noise4{{0.f, 0.f, 0.f, 0.f}};
+    char4 o;
+    int c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c[k] = quant1(qs, p.qout.stochastic, tile[wave][rr][cq * 4 + k], n.u[k], ov1, ov2);
+      s1[pass][k] = c[k];
+      s2[pass][k] = c[k] * c[k];
+    }
+    o.x = (int8_t)c[0]; o.y = (int8_t)c[1]; o.z = (int8_t)c[2]; o.w = (int8_t)c[3];
+    *reinterpret_cast<char4*>(p.yq + row * p.ncol + col0) = o;
+  }
+  if (want_sum) {
+    // lanes with equal (lane % quads) hold the same channel quad: xor-reduce over quads..32
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass >= ntw) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int a1 = s1[pass][k], a2 = s2[pass][k];
+        for (int o = quads; o < 64; o <<= 1) {
+          a1 += __shfl_xor(a1, o, 64);
+          a2 += __shfl_xor(a2, o, 64);
+        }
+        const int cq = (pass * 64 + lane) % quads;
+        if (wave_live && lane < quads) {
+          const int ch = nt0 * 16 + cq * 4 + k;
+          if (a1) atomicAdd((unsigned long long*)&sh_sum[ch], (unsigned long long)(long long)a1);
+          if (a2) atomicAdd((unsigned long long*)&sh_sum[p.ncol + ch], (unsigned long long)(long long)a2);
+        }
       }
     }
   }
-  if (want_q) block_flush_counts(p.qout, ov1, ov2, sh_cnt);
+  block_flush_counts(p.qout, ov1, ov2, sh_cnt);
   if (want_sum) {
     __syncthreads();
     block_flush_sums(sh_sum, 2 * p.ncol, p.ychsum, 2 * p.ncol);

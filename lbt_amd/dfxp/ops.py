@@ -214,6 +214,10 @@ def _chain_bwd_a_bytes(a):
     return per * a.rows * a.inner
 
 
+def _chain_bwd_b_bytes(a):
+    return (2 + (4 if a.dx else 0) + (1 if a.gq else 0)) * a.rows * a.inner
+
+
 def chain_fwd(desc):
     with _Timed("chain_fwd_kernel", _chain_fwd_bytes(desc)):
         call("lbt_bn_chain_fwd", _lib.ctypes.byref(desc), stream())
@@ -225,8 +229,7 @@ def chain_bwd_a(desc):
 
 
 def chain_bwd_b(desc):
-    per = 2 + (4 if desc.dx else 0) + (1 if desc.gq else 0)
-    with _Timed("chain_bwd_b_kernel", per * desc.rows * desc.inner):
+    with _Timed("chain_bwd_b_kernel", _chain_bwd_b_bytes(desc)):
         call("lbt_bn_chain_bwd_b", _lib.ctypes.byref(desc), stream())
 
 

@@ -1,0 +1,516 @@
+"""Fused execution plan of a ``CIFAR10_Resnet`` -- the MI355X-native hot path.
+
+Same parameters, quantisers (names, noise streams, exponents) and arithmetic as executing the
+model layer by layer through the Layer_q API, so the results are BIT-IDENTICAL (tested); only
+the kernel schedule changes. Per residual block the reference's 13 layer calls
+(conv, BN-norm, BN-rescale, ReLU, conv, BN-norm, BN-rescale, [conv, BN-norm, BN-rescale], add,
+ReLU) become 4-5 kernels forward and 8-11 backward:
+
+forward   conv-1 (int8 MFMA, epilogue = bn1-norm quantiser + exact channel sums)
+          chain  (bn1 moments -> normalise -> rescale quantiser -> affine -> ReLU -> conv-2 input quantiser)
+          conv-2 (epilogue = bn2-norm quantiser + sums)            [+ 1x1 shortcut conv, same epilogue]
+          chain  (bn2 [+ shortcut BN] + residual -> ReLU -> block output + next block's input quantisers)
+backward  chain A (ReLU mask, bn2-rescale grad quantiser, dgamma/dbeta sums, bn2-norm grad quantiser)
+          chain B (bn2-norm backward -> conv-2 grad quantiser + column sums)     [+ shortcut BN]
+          conv-2 dgrad, conv-2 wgrad, chain A/B for bn1, [shortcut dgrad], conv-1 dgrad (+ residual
+          gradient), conv-1 wgrad [+ shortcut wgrad]
+and all weight / gamma / beta quantisers, all split wgrad reductions and all dgamma / dbeta are one
+batched launch each. Every launch is prebuilt (ctypes arguments fixed) on the first call, so a
+step is a flat list of C calls -- and one HIP graph once captured by the Trainer.
+"""
+import ctypes
+import math
+import os
+
+import torch
+
+from . import _lib
+from ._lib import NO_Q, OUT_I8, OUT_I16, OUT_U8OFF, BnNorm, BwdBranch, ChainBwdA, ChainBwdB, ChainFwd, PJob, QJob, \
+    RJob, WJob, call, ptr
+from .dfxp import ops
+from .dfxp.layers import _Cache
+
+
+def _desc(q):
+    return q.desc
+
+
+def _dev_array(jobs, device):
+    """Upload an array of ctypes job structs to device memory (kept alive by the returned tensor)."""
+    n = len(jobs)
+    T = type(jobs[0])
+    buf = (T * n)(*jobs)
+    host = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8)
+    return host.to(device)
+
+
+class _Block:
+    def __init__(self, blk):
+        r = blk.residual.layers
+        self.c1, self.n1, self.r1 = r[0], r[1].layers[0], r[1].layers[1]
+        self.c2, self.n2, self.r2 = r[3], r[4].layers[0], r[4].layers[1]
+        sc = blk.shortcut.layers
+        if sc:
+            self.cs, self.ns, self.rs = sc[0], sc[1].layers[0], sc[1].layers[1]
+        else:
+            self.cs = self.ns = self.rs = None
+        self.blk = blk
+
+
+class FusedResNet:
+    """Drop-in for the Trainer (forward / compute_loss / backward / param_slots / ctx / loss)."""
+
+    def __init__(self, model):
+        self.model = model
+        self.ctx = model.ctx
+        L = model.layers
+        self.conv1, bn0 = L[0], L[1]
+        self.n0, self.r0 = bn0.layers[0], bn0.layers[1]
+        self.blocks = [_Block(b) for b in L[3:-3]]
+        self.dense = L[-1]
+        self.convs = [self.conv1] + [c for b in self.blocks for c in (b.c1, b.c2, b.cs) if c is not None]
+        self.rescales = [self.r0] + [r for b in self.blocks for r in (b.r1, b.r2, b.rs) if r is not None]
+        self._c = _Cache()
+        self._shape = None
+        self.loss = None
+        self.dlogits = None
+        self.overlap_wgrad = os.environ.get("LBT_OVERLAP_WGRAD", "0") == "1"  # measured: a loss here (60K vs 67K samples/s)
+        self._side = None
+
+    # ------------------------------------------------------------------ Trainer interface
+    def param_slots(self):
+        return self.model.param_slots()
+
+    def grads_and_vars(self):
+        return self.model.grads_and_vars()
+
+    def info(self):
+        return "fused " + self.model.info()
+
+    def input_buffer(self, shape):
+        """The plan's own input buffer (a caller may write batches straight into it)."""
+        return self._c.get("X", tuple(shape), torch.float32, self.ctx.device)
+
+    def forward(self, X):
+        self._ensure(X)
+        if X.data_ptr() != self._X.data_ptr():
+            self._X.copy_(X)
+        if not self.ctx.sums_managed:
+            self.ctx.zero_sums()
+        for f in self._fwd:
+            f()
+        return self.logits
+
+    def compute_loss(self, labels):
+        if labels.data_ptr() != self._labels.data_ptr():
+            self._labels.copy_(labels)
+        ops.softmax_xent(self.logits, self._labels, self.loss, self.dlogits)
+        return self.loss
+
+    def backward(self):
+        for f in self._bwd:
+            f()
+
+    # ------------------------------------------------------------------ streams
+    def _on_side(self, run):
+        """Run a launch on the side stream after everything already queued on the main stream
+        (the weight-gradient GEMMs only feed the final reduction, so they overlap the serial
+        dgrad -> BN-backward chain; under graph capture this becomes a parallel branch)."""
+        if not self.overlap_wgrad:
+            return run
+
+        def f():
+            main = torch.cuda.current_stream()
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self._side.wait_event(ev)
+            with torch.cuda.stream(self._side):
+                run()
+        return f
+
+    def _join_side(self):
+        def f():
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+            torch.cuda.current_stream().wait_event(ev)
+        return f
+
+    # ------------------------------------------------------------------ plan
+    def _buf(self, key, shape, dtype):
+        return self._c.get(key, shape, dtype, self.ctx.device)
+
+    def _sums(self, key, n):
+        return self._c.sums(key, n, self.ctx)
+
+    def _ensure(self, X):
+        if self._shape == tuple(X.shape):
+            return
+        if self._shape is not None:
+            raise RuntimeError("FusedResNet plan is built for one batch shape; got %s after %s"
+                               % (tuple(X.shape), self._shape))
+        self._shape = tuple(X.shape)
+        self._build(X)
+
+    def _build(self, X):
+        ctx = self.ctx
+        st = _lib.stream
+        N, H, W, Cin0 = X.shape
+        self._X = self.input_buffer(X.shape)
+        self._labels = torch.zeros(N, dtype=torch.int32, device=ctx.device)
+        fwd, bwd = [], []
+        lib = _lib.load()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=ctx.device)
+
+        def L(name, *args, k=None, nb=0):
+            """A prebuilt launch; `k` / `nb` = kernel name and algorithmic bytes for the roofline hook."""
+            fn = getattr(lib, name)
+            kname = k or name
+
+            def run(fn=fn, args=args, name=name):
+                with ops._Timed(kname, nb):
+                    rc = fn(*args, st())
+                if rc:
+                    raise _lib.LbtError("%s failed with status %d" % (name, rc))
+            return run
+
+        def obs(q, n):
+            q.observe(n)
+
+        # ---- batched weight + gamma/beta quantisation (all layers, one launch each)
+        wjobs = []
+        for c in self.convs:
+            kh, kw, ci, co = c.ksize
+            obs(c.W_range, c.W.numel())
+            wjobs.append(WJob(c.W.data_ptr(), kh, kw, ci, co, c.W_range.desc, c.w_hwio.data_ptr(),
+                              c.wf.data_ptr() if c.mfma else None, c.ksf, c.wd.data_ptr() if c.mfma else None,
+                              c.ksd, c.wcolsum.data_ptr() if c.mfma else None))
+        d = self.dense
+        obs(d.W_range, d.W.numel())
+        wjobs.append(WJob(d.W.data_ptr(), d.in_units, 1, 1, d.units, d.W_range.desc, d.w_hwio.data_ptr(),
+                          None, 0, None, 0, None))
+        self._wjobs = _dev_array(wjobs, ctx.device)
+        max_cout = max(j.Cout for j in wjobs)
+        fwd.append(L("lbt_dfxp_quantize_weights", ptr(self._wjobs), len(wjobs), max_cout))
+        qjobs = []
+        for r in self.rescales:
+            C = r.C
+            obs(r.g_range, C)
+            obs(r.b_range, C)
+            qjobs.append(QJob(r.gamma.data_ptr(), r.gb.data_ptr(), _lib.OUT_F32, C, 1, r.g_range.desc))
+            qjobs.append(QJob(r.beta.data_ptr(), r.gb.data_ptr() + 4 * C, _lib.OUT_F32, C, 1, r.b_range.desc))
+        self._qjobs = _dev_array(qjobs, ctx.device)
+        fwd.append(L("lbt_dfxp_quantize_many", ptr(self._qjobs), len(qjobs)))
+
+        # ---- stem: conv1 on the signed 9-bit image (VALU), BN, ReLU
+        c = self.conv1
+        kh, kw, _, C0 = c.ksize
+        dc = ops.conv_desc(N, H, W, Cin0, C0, kh, kw, c.strides[1], c.strides[2], c.padding)
+        c.d = dc
+        ximg = self._buf("ximg", (N, H, W, Cin0), torch.int16)
+        obs(c.X_range, X.numel())
+        fwd.append(L("lbt_dfxp_quantize", ptr(self._X), ptr(ximg), OUT_I16, N, H * W * Cin0, c.X_range.desc, None,
+                     0, k="quantize_rows_kernel", nb=X.numel() * 6))
+        y0 = self._buf("y0", (N, dc.Ho, dc.Wo, C0), torch.float32)
+        fwd.append(L("lbt_conv_fwd_generic", ptr(ximg), 1, ptr(c.w_hwio), dc, c.X_range.desc, c.W_range.desc,
+                     ptr(y0), k="conv_fwd_generic_kernel", nb=ximg.numel() * 2 + y0.numel() * 4))
+        n0, r0 = self.n0, self.r0
+        qn0 = self._buf("qn0", y0.shape, torch.int8)
+        chs0 = self._sums("chs0", ops.NSHARD * 2 * C0)
+        obs(n0.X_range, y0.numel())
+        fwd.append(L("lbt_dfxp_quantize", ptr(y0), ptr(qn0), OUT_I8, N, y0.numel() // N, n0.X_range.desc, ptr(chs0),
+                     C0, k="quantize_rows_kernel", nb=y0.numel() * 5))
+        R0 = self._buf("R0", y0.shape, torch.int8)
+        X0 = self._buf("X0", y0.shape, torch.float32)
+        b0 = self.blocks[0]
+        xa = self._buf("xa0", y0.shape, torch.int8)
+        xs = self._buf("xs0", y0.shape, torch.int8) if b0.cs is not None else None
+        obs(r0.X_range, y0.numel())
+        obs(b0.c1.X_range, y0.numel())
+        if xs is not None:
+            obs(b0.cs.X_range, y0.numel())
+        a = self._chain_fwd(n0, qn0, chs0, r0, R0, None, None, None, None, None, relu=True, y=X0,
+                            o1=xa, q1=b0.c1.X_range, o2=xs, q2=b0.cs.X_range if xs is not None else None)
+        fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a)))
+        self._keep = [a]
+
+        # ---- residual blocks
+        Xin = X0
+        saved = []
+        for i, b in enumerate(self.blocks):
+            nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            Xin, xa, xs, info = self._block_fwd(i, b, nxt, Xin, xa, xs, fwd, L, obs)
+            saved.append(info)
+        Ylast = Xin
+
+        # ---- head: avg pool, dense, loss
+        Nb, Hh, Wh, Ch = Ylast.shape
+        pooled = self._buf("pool", (Nb, Ch), torch.float32)
+        fwd.append(L("lbt_avgpool_fwd", ptr(Ylast), ptr(pooled), Nb, Hh * Wh, Ch))
+        dd = _lib.ConvDesc(Nb, 1, 1, d.in_units, d.units, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
+        d.d = dd
+        pq = self._buf("pq", (Nb, Ch), torch.int8)
+        obs(d.X_range, pooled.numel())
+        fwd.append(L("lbt_dfxp_quantize", ptr(pooled), ptr(pq), OUT_I8, Nb, Ch, d.X_range.desc, None, 0))
+        self.logits = self._buf("logits", (Nb, d.units), torch.float32)
+        fwd.append(L("lbt_conv_fwd_generic", ptr(pq), 0, ptr(d.w_hwio), dd, d.X_range.desc, d.W_range.desc,
+                     ptr(self.logits)))
+        self.loss = self._buf("loss", (1,), torch.float32)
+        self.dlogits = self._buf("dz", (Nb, d.units), torch.float32)
+
+        # ================================================================ backward
+        rjobs, pjobs = [], []
+        gqd = self._buf("gqd", (Nb, d.units), torch.int8)
+        obs(d.grad_range, self.dlogits.numel())
+        bwd.append(L("lbt_dfxp_quantize", ptr(self.dlogits), ptr(gqd), OUT_I8, Nb, d.units, d.grad_range.desc, None,
+                     0))
+        nsd = ops.wgrad_nsplit(dd, generic=True)
+        slabd = self._buf("slabd", (nsd, d.in_units, d.units), torch.int32)
+        bwd.append(self._on_side(L("lbt_conv_wgrad_generic", ptr(pq), 0, ptr(gqd), dd, ptr(slabd), nsd,
+                                   k="conv_wgrad_generic_kernel", nb=pq.numel() + gqd.numel() + 4 * slabd.numel())))
+        rjobs.append(RJob(slabd.data_ptr(), nsd, d.in_units, d.units, 0, None, d.X_range.desc, d.grad_range.desc,
+                          d.W.data_ptr(), ops.f32(2 * d.weight_decay), d.dW.data_ptr()))
+        dpool = self._buf("dpool", (Nb, Ch), torch.float32)
+        bwd.append(L("lbt_conv_dgrad_generic", ptr(gqd), ptr(d.w_hwio), dd, d.grad_range.desc, d.W_range.desc,
+                     ptr(dpool), None))
+        gY = self._buf("gYlast", Ylast.shape, torch.float32)
+        bwd.append(L("lbt_avgpool_bwd", ptr(dpool), ptr(gY), Nb, Hh * Wh, Ch))
+        for i in reversed(range(len(self.blocks))):
+            gY = self._block_bwd(i, self.blocks[i], saved[i], gY, bwd, L, obs, rjobs, pjobs)
+
+        # ---- stem backward (d loss / d image is never needed)
+        gq0 = self._buf("gq0", y0.shape, torch.int8)
+        Gn0 = self._buf("Gn0", y0.shape, torch.int8)
+        sums0 = self._sums("sums0", ops.NSHARD * 4 * C0)
+        obs(r0.grad_range, y0.numel())
+        obs(n0.grad_range, y0.numel())
+        obs(c.grad_range, y0.numel())
+        aA = self._chain_bwd_a(gY, X0, False, None, (r0, R0, n0, qn0, Gn0, sums0), None, y0.shape, C0)
+        bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
+        aB = self._chain_bwd_b(n0, Gn0, qn0, sums0, y0.shape, C0, gq0, c.grad_range, None)
+        bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB)))
+        self._keep += [aA, aB]
+        ns0 = ops.wgrad_nsplit(dc, generic=True)
+        slab0 = self._buf("slab0", (ns0, kh * kw * Cin0, C0), torch.int32)
+        bwd.append(L("lbt_conv_wgrad_generic", ptr(ximg), 1, ptr(gq0), dc, ptr(slab0), ns0,
+                     k="conv_wgrad_generic_kernel", nb=2 * ximg.numel() + gq0.numel() + 4 * slab0.numel()))
+        rjobs.append(RJob(slab0.data_ptr(), ns0, kh * kw * Cin0, C0, 0, None, c.X_range.desc, c.grad_range.desc,
+                          c.W.data_ptr(), ops.f32(2 * c.weight_decay), c.dW.data_ptr()))
+        pjobs.append(PJob(sums0.data_ptr(), C0, r0.grad_range.desc, r0.X_range.desc, r0.gamma.data_ptr(),
+                          ops.f32(2 * r0.weight_decay), r0.dgamma.data_ptr(), r0.dbeta.data_ptr()))
+
+        # ---- batched reductions (after the side-stream weight gradients have landed)
+        if self.overlap_wgrad:
+            bwd.append(self._join_side())
+        self._rjobs = _dev_array(rjobs, ctx.device)
+        maxb = max((j.K * j.Cout + 31) // 32 for j in rjobs)
+        bwd.append(L("lbt_conv_wgrad_reduce_many", ptr(self._rjobs), len(rjobs), maxb))
+        self._pjobs = _dev_array(pjobs, ctx.device)
+        bwd.append(L("lbt_bn_param_grads_many", ptr(self._pjobs), len(pjobs), max(j.C for j in pjobs)))
+        self._fwd, self._bwd = fwd, bwd
+
+    # ------------------------------------------------------------------ descriptor builders
+    def _bn_norm(self, n, q, chsum, numel, C):
+        return BnNorm(q.data_ptr(), n.X_range.desc, chsum.data_ptr(), numel // C, ops.f32(n.eps),
+                      ops.f32(n.momentum), ops.f32(1 - n.momentum), n.ms.data_ptr(), n.X_mean_running.data_ptr(),
+                      n.X_var_running.data_ptr())
+
+    def _chain_fwd(self, n, qn, chs, r, R, n2, qn2, chs2, r2, R2, relu, y, o1=None, q1=None, o2=None, q2=None,
+                   res=None):
+        C = qn.shape[-1]
+        a = ChainFwd()
+        a.b1.nrm = self._bn_norm(n, qn, chs, qn.numel(), C)
+        a.b1.qr = r.X_range.desc
+        a.b1.rout = R.data_ptr()
+        a.b1.gb = r.gb.data_ptr()
+        if n2 is not None:
+            a.has_b2 = 1
+            a.b2.nrm = self._bn_norm(n2, qn2, chs2, qn2.numel(), C)
+            a.b2.qr = r2.X_range.desc
+            a.b2.rout = R2.data_ptr()
+            a.b2.gb = r2.gb.data_ptr()
+        a.res = res.data_ptr() if res is not None else None
+        a.relu = 1 if relu else 0
+        a.y = y.data_ptr() if y is not None else None
+        if o1 is not None:
+            a.o1, a.o1_kind, a.qo1 = o1.data_ptr(), OUT_U8OFF, q1.desc
+        if o2 is not None:
+            a.o2, a.o2_kind, a.qo2 = o2.data_ptr(), OUT_U8OFF, q2.desc
+        a.rows, a.inner, a.C = qn.shape[0], qn.numel() // qn.shape[0], C
+        return a
+
+    def _chain_bwd_a(self, g, y_mask, mask_from_r, gmask, br1, br2, shape, C):
+        a = ChainBwdA()
+        a.g = g.data_ptr()
+        a.y_mask = y_mask.data_ptr() if y_mask is not None else None
+        a.mask_from_r = 1 if mask_from_r else 0
+        a.gmask_out = gmask.data_ptr() if gmask is not None else None
+        for slot, br in ((0, br1), (1, br2)):
+            if br is None:
+                continue
+            r, R, n, qn, G, sums = br
+            bb = BwdBranch(r.grad_range.desc, R.data_ptr(), r.X_range.desc, r.gb.data_ptr(), n.grad_range.desc,
+                           qn.data_ptr(), G.data_ptr(), None, sums.data_ptr())
+            if slot == 0:
+                a.b1 = bb
+            else:
+                a.b2 = bb
+                a.has_b2 = 1
+        a.rows, a.inner, a.C = shape[0], math.prod(shape[1:]), C
+        return a
+
+    def _chain_bwd_b(self, n, G, qn, sums, shape, C, gq, qo, gcol):
+        rows = shape[0]
+        inner = math.prod(shape[1:])
+        return ChainBwdB(G.data_ptr(), n.grad_range.desc, qn.data_ptr(), n.X_range.desc, n.ms.data_ptr(),
+                         sums.data_ptr(), rows * inner // C, None, gq.data_ptr(), qo.desc,
+                         gcol.data_ptr() if gcol is not None else None, rows, inner, C)
+
+    # ------------------------------------------------------------------ one residual block
+    def _block_fwd(self, i, b, nxt, Xin, xa, xs, fwd, L, obs):
+        N, H, W, Cin = Xin.shape
+        c1, c2, cs = b.c1, b.c2, b.cs
+        C = c1.ksize[3]
+        s = c1.strides[1]
+        d1 = ops.conv_desc(N, H, W, Cin, C, 3, 3, s, s, c1.padding)
+        d2 = ops.conv_desc(N, d1.Ho, d1.Wo, C, C, 3, 3, 1, 1, c2.padding)
+        c1.d, c2.d = d1, d2
+        shp = (N, d1.Ho, d1.Wo, C)
+        numel = N * d1.Ho * d1.Wo * C
+        k = "b%d_" % i
+        qn1 = self._buf(k + "qn1", shp, torch.int8)
+        chs1 = self._sums(k + "chs1", ops.NSHARD * 2 * C)
+        obs(b.n1.X_range, numel)
+        fwd.append(L("lbt_conv_fwd_i8", ptr(xa), 1, ptr(c1.wf), c1.ksf, ptr(c1.wcolsum), d1, c1.X_range.desc,
+                     c1.W_range.desc, None, ptr(qn1), b.n1.X_range.desc, ptr(chs1), k="conv_gemm_kernel<0> (fwd)",
+                     nb=xa.numel() + c1.wf.numel() + qn1.numel()))
+        R1 = self._buf(k + "R1", shp, torch.int8)
+        xb = self._buf(k + "xb", shp, torch.int8)
+        obs(b.r1.X_range, numel)
+        obs(c2.X_range, numel)
+        a1 = self._chain_fwd(b.n1, qn1, chs1, b.r1, R1, None, None, None, None, None, relu=True, y=None, o1=xb,
+                             q1=c2.X_range)
+        fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a1), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a1)))
+        qn2 = self._buf(k + "qn2", shp, torch.int8)
+        chs2 = self._sums(k + "chs2", ops.NSHARD * 2 * C)
+        obs(b.n2.X_range, numel)
+        fwd.append(L("lbt_conv_fwd_i8", ptr(xb), 1, ptr(c2.wf), c2.ksf, ptr(c2.wcolsum), d2, c2.X_range.desc,
+                     c2.W_range.desc, None, ptr(qn2), b.n2.X_range.desc, ptr(chs2), k="conv_gemm_kernel<0> (fwd)",
+                     nb=xb.numel() + c2.wf.numel() + qn2.numel()))
+        ds = qns = chss = Rs = None
+        if cs is not None:
+            ds = ops.conv_desc(N, H, W, Cin, C, 1, 1, s, s, cs.padding)
+            cs.d = ds
+            qns = self._buf(k + "qns", shp, torch.int8)
+            chss = self._sums(k + "chss", ops.NSHARD * 2 * C)
+            obs(b.ns.X_range, numel)
+            fwd.append(L("lbt_conv_fwd_i8", ptr(xs), 1, ptr(cs.wf), cs.ksf, ptr(cs.wcolsum), ds, cs.X_range.desc,
+                         cs.W_range.desc, None, ptr(qns), b.ns.X_range.desc, ptr(chss), k="conv_gemm_kernel<0> (fwd)",
+                         nb=xs.numel() + cs.wf.numel() + qns.numel()))
+            Rs = self._buf(k + "Rs", shp, torch.int8)
+            obs(b.rs.X_range, numel)
+        R2 = self._buf(k + "R2", shp, torch.int8)
+        obs(b.r2.X_range, numel)
+        Y = self._buf(k + "Y", shp, torch.float32)
+        xa_n = xs_n = None
+        if nxt is not None:
+            xa_n = self._buf("xa%d" % (i + 1), shp, torch.int8)
+            obs(nxt.c1.X_range, numel)
+            if nxt.cs is not None:
+                xs_n = self._buf("xs%d" % (i + 1), shp, torch.int8)
+                obs(nxt.cs.X_range, numel)
+        a2 = self._chain_fwd(b.n2, qn2, chs2, b.r2, R2, b.ns, qns, chss, b.rs, Rs, relu=True, y=Y,
+                             o1=xa_n, q1=nxt.c1.X_range if nxt is not None else None,
+                             o2=xs_n, q2=nxt.cs.X_range if xs_n is not None else None,
+                             res=None if cs is not None else Xin)
+        fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a2), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a2)))
+        self._keep += [a1, a2]
+        info = dict(Xin=Xin, xa=xa, xs=xs, d1=d1, d2=d2, ds=ds, qn1=qn1, R1=R1, xb=xb, qn2=qn2, R2=R2, qns=qns,
+                    Rs=Rs, Y=Y, shp=shp, C=C, Cin=Cin)
+        return Y, xa_n, xs_n, info
+
+    def _block_bwd(self, i, b, f, gY, bwd, L, obs, rjobs, pjobs):
+        k = "b%d_" % i
+        shp, C, Cin = f["shp"], f["C"], f["Cin"]
+        numel = 1
+        for v in shp:
+            numel *= v
+        c1, c2, cs = b.c1, b.c2, b.cs
+        d1, d2, ds = f["d1"], f["d2"], f["ds"]
+        Gn2 = self._buf(k + "Gn2", shp, torch.int8)
+        sums2 = self._sums(k + "sums2", ops.NSHARD * 4 * C)
+        for q in (b.r2.grad_range, b.n2.grad_range, c2.grad_range, b.r1.grad_range, b.n1.grad_range,
+                  c1.grad_range):
+            obs(q, numel)
+        gm = None
+        br2 = None
+        Gns = sumss = None
+        if cs is not None:
+            Gns = self._buf(k + "Gns", shp, torch.int8)
+            sumss = self._sums(k + "sumss", ops.NSHARD * 4 * C)
+            br2 = (b.rs, f["Rs"], b.ns, f["qns"], Gns, sumss)
+            for q in (b.rs.grad_range, b.ns.grad_range, cs.grad_range):
+                obs(q, numel)
+        else:
+            gm = self._buf(k + "gm", shp, torch.float32)
+        aA2 = self._chain_bwd_a(gY, f["Y"], False, gm, (b.r2, f["R2"], b.n2, f["qn2"], Gn2, sums2), br2, shp, C)
+        bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA2), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA2)))
+        gq2 = self._buf(k + "gq2", shp, torch.int8)
+        gcol2 = self._sums(k + "gcol2", ops.NSHARD * 2 * C)
+        aB2 = self._chain_bwd_b(b.n2, Gn2, f["qn2"], sums2, shp, C, gq2, c2.grad_range, gcol2)
+        bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB2), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB2)))
+        keep = [aA2, aB2]
+        gqs = gcols = None
+        if cs is not None:
+            gqs = self._buf(k + "gqs", shp, torch.int8)
+            gcols = self._sums(k + "gcols", ops.NSHARD * 2 * C)
+            aBs = self._chain_bwd_b(b.ns, Gns, f["qns"], sumss, shp, C, gqs, cs.grad_range, gcols)
+            bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aBs), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aBs)))
+            keep.append(aBs)
+        d1g = self._buf(k + "d1", shp, torch.float32)
+        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, c2.grad_range.desc, c2.W_range.desc,
+                     ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=gq2.numel() + c2.wd.numel() + 4 * d1g.numel()))
+        ns2 = ops.wgrad_nsplit(d2)
+        slab2 = self._buf(k + "slab2", (ns2, 9 * C, C), torch.int32)
+        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), ns2,
+                                   k="conv_wgrad_kernel", nb=f["xb"].numel() + gq2.numel() + 4 * slab2.numel())))
+        rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), c2.X_range.desc, c2.grad_range.desc,
+                          c2.W.data_ptr(), ops.f32(2 * c2.weight_decay), c2.dW.data_ptr()))
+        Gn1 = self._buf(k + "Gn1", shp, torch.int8)
+        sums1 = self._sums(k + "sums1", ops.NSHARD * 4 * C)
+        aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
+        bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA1), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA1)))
+        gq1 = self._buf(k + "gq1", shp, torch.int8)
+        gcol1 = self._sums(k + "gcol1", ops.NSHARD * 2 * C)
+        aB1 = self._chain_bwd_b(b.n1, Gn1, f["qn1"], sums1, shp, C, gq1, c1.grad_range, gcol1)
+        bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB1), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB1)))
+        keep += [aA1, aB1]
+        gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
+        add = gm
+        if cs is not None:
+            dsg = self._buf(k + "dsc", f["Xin"].shape, torch.float32)
+            bwd.append(L("lbt_conv_dgrad_i8", ptr(gqs), ptr(cs.wd), cs.ksd, ds, cs.grad_range.desc,
+                         cs.W_range.desc, ptr(dsg), None, k="conv_gemm_kernel<1> (dgrad)",
+                         nb=gqs.numel() + cs.wd.numel() + 4 * dsg.numel()))
+            add = dsg
+        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, c1.grad_range.desc, c1.W_range.desc,
+                     ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=gq1.numel() + c1.wd.numel() + 8 * gin.numel()))
+        ns1 = ops.wgrad_nsplit(d1)
+        slab1 = self._buf(k + "slab1", (ns1, 9 * Cin, C), torch.int32)
+        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), ns1,
+                                   k="conv_wgrad_kernel", nb=f["xa"].numel() + gq1.numel() + 4 * slab1.numel())))
+        rjobs.append(RJob(slab1.data_ptr(), ns1, 9 * Cin, C, 1, gcol1.data_ptr(), c1.X_range.desc,
+                          c1.grad_range.desc, c1.W.data_ptr(), ops.f32(2 * c1.weight_decay), c1.dW.data_ptr()))
+        if cs is not None:
+            nss = ops.wgrad_nsplit(ds)
+            slabs = self._buf(k + "slabs", (nss, Cin, C), torch.int32)
+            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xs"]), 1, ptr(gqs), ds, ptr(slabs), nss,
+                                       k="conv_wgrad_kernel", nb=f["xs"].numel() + gqs.numel() + 4 * slabs.numel())))
+            rjobs.append(RJob(slabs.data_ptr(), nss, Cin, C, 1, gcols.data_ptr(), cs.X_range.desc,
+                              cs.grad_range.desc, cs.W.data_ptr(), ops.f32(2 * cs.weight_decay), cs.dW.data_ptr()))
+        for r in (b.r1, b.r2) + ((b.rs,) if cs is not None else ()):
+            sm = {id(b.r1): sums1, id(b.r2): sums2}.get(id(r), sumss)
+            pjobs.append(PJob(sm.data_ptr(), C, r.grad_range.desc, r.X_range.desc, r.gamma.data_ptr(),
+                              ops.f32(2 * r.weight_decay), r.dgamma.data_ptr(), r.dbeta.data_ptr()))
+        self._keep += keep
+        return gin

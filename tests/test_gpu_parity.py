@@ -336,3 +336,40 @@ def test_bench_workload_loss_trajectory_matches_oracle():
                                             momentum=0.9, seed=0)
         assert abs(loss - lref) <= 1e-5 * abs(lref), (i, loss, lref)
         assert ctx.ranges() == state["ranges"], i
+
+
+def test_fused_executor_bitidentical_to_layerwise():
+    """FusedResNet (the bench path) == the Layer_q model executed layer by layer, bit for bit:
+    logits, loss, every gradient and every exponent update, then 3 graph-captured optimiser steps."""
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.trainer import Trainer
+    x, y = synthetic_batch(32, seed=5)
+    xt, yt = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    ctxA, ctxB = DfxpContext(seed=6), DfxpContext(seed=6)
+    A = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctxA)
+    B = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctxB))
+    la = A.forward(xt).cpu().numpy()
+    lb = B.forward(xt).cpu().numpy()
+    assert np.array_equal(la, lb)
+    assert A.compute_loss(yt).item() == B.compute_loss(yt).item()
+    A.backward()
+    B.backward()
+    ga, gb = gpu_grads(A), gpu_grads(B.model)
+    for k in ga:
+        assert np.array_equal(ga[k], gb[k]), k
+    ctxA.update_range_op()
+    ctxB.update_range_op()
+    assert ctxA.ranges() == ctxB.ranges()
+    # training: eager layer-wise vs graph-captured fused
+    ctxA, ctxB = DfxpContext(seed=7), DfxpContext(seed=7)
+    tA = Trainer(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctxA), lr=1e-2, momentum=0.9, use_graph=False)
+    tB = Trainer(FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctxB)), lr=1e-2, momentum=0.9,
+                 use_graph=True)
+    for i in range(3):
+        x, y = synthetic_batch(32, seed=20 + i)
+        xt, yt = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+        assert tA.step(xt, yt).item() == tB.step(xt, yt).item()
+    torch.cuda.synchronize()
+    assert np.array_equal(tA.flat.w.cpu().numpy(), tB.flat.w.cpu().numpy())
+    assert ctxA.ranges() == ctxB.ranges()
