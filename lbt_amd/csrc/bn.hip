@@ -8,6 +8,8 @@
 // integer sums (moments of the quantised input; G*R, G, G*q for the backward), reduced
 // wave -> LDS -> one atomic per workgroup into a shard, so they are deterministic and
 // independent of the launch geometry.
+#include <cstdlib>
+
 #include "dfxp_device.h"
 
 using namespace lbt;
@@ -133,6 +135,7 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
     const Noise4 no2 = noise_for(a.qo2, so2, g);
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+#pragma unroll 2
     for (int64_t r = r0; r < rend; ++r) {
       const int64_t e = r * a.inner + (g << 2);
       float v[4] = {0.f, 0.f, 0.f, 0.f};
@@ -238,6 +241,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
     }
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+#pragma unroll 2
     for (int64_t r = r0; r < rend; ++r) {
       const int64_t e = r * a.inner + (g << 2);
       float gv[4];
@@ -360,6 +364,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
     const Noise4 no = noise_for(a.qo, so, g);
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+#pragma unroll 2
     for (int64_t r = r0; r < rend; ++r) {
       const int64_t e = r * a.inner + (g << 2);
       int G[4], q[4];
@@ -427,7 +432,11 @@ __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lb
 bool grid_for(int64_t rows, int64_t inner, dim3& grid, int& rpt) {
   const int64_t groups = inner / 4;
   const int64_t gblocks = (groups + kThreads - 1) / kThreads;
-  int64_t r = (gblocks * rows) / 512;
+  static const int64_t target = [] {
+    const char* e = getenv("LBT_CHAIN_BLOCKS");
+    return (int64_t)(e ? atoi(e) : 512);
+  }();
+  int64_t r = (gblocks * rows) / target;
   if (r < 1) r = 1;
   if (r > 64) r = 64;
   const int64_t yb = (rows + r - 1) / r;

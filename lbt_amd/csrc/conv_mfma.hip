@@ -90,39 +90,61 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(GemmArgs p) {
   acc[0] = v4i{0, 0, 0, 0};
   acc[1] = v4i{0, 0, 0, 0};
 
+  // A fragment of k-step kk (slice s = 4*kk + kg) for this lane's row
+  auto load_a = [&](int kk) -> v4i {
+    const int s = kk * 4 + kg;
+    v4i a = v4i{p.a_fill, p.a_fill, p.a_fill, p.a_fill};
+    if (s >= p.nslices) return v4i{0, 0, 0, 0};
+    if (!row_ok) return a;
+    const int tap = s / CS, cs = s - tap * CS;
+    const int kh = tap / d.KW, kw = tap - kh * d.KW;
+    int sy, sx;
+    bool ok;
+    if (MODE == MODE_FWD) {
+      sy = py * d.SH + kh - d.PT;
+      sx = px * d.SW + kw - d.PL;
+      ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+    } else {
+      const int ny = py + d.PT - kh, nx = px + d.PL - kw;
+      sy = ny / d.SH;
+      sx = nx / d.SW;
+      ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
+    }
+    if (ok) return *reinterpret_cast<const v4i*>(p.a + (((int64_t)n * SH + sy) * SW + sx) * cred + cs * 16);
+    return MODE == MODE_DGRAD ? v4i{0, 0, 0, 0} : a;
+  };
+  auto load_b = [&](int kk, int j) -> v4i {
+    const int col = (nt0 + j) * 16 + r;
+    return *reinterpret_cast<const v4i*>(p.b + ((int64_t)col * p.ks + kk * 4 + kg) * 16);
+  };
+
   if (wave_live) {
-    for (int ks = 0; ks < p.ks; ks += 4) {
-      const int s = ks + kg;
-      v4i a = v4i{p.a_fill, p.a_fill, p.a_fill, p.a_fill};
-      if (s < p.nslices && row_ok) {
-        const int tap = s / CS, cs = s - tap * CS;
-        const int kh = tap / d.KW, kw = tap - kh * d.KW;
-        int sy, sx;
-        bool ok;
-        if (MODE == MODE_FWD) {
-          sy = py * d.SH + kh - d.PT;
-          sx = px * d.SW + kw - d.PL;
-          ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
-        } else {
-          const int ny = py + d.PT - kh, nx = px + d.PL - kw;
-          sy = ny / d.SH;
-          sx = nx / d.SW;
-          ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
+    const int nks = p.ks >> 2;
+    // every operand of a 3x3 conv's k loop fits in registers: issue ALL loads, then the MFMAs
+    // (one memory round trip per wave instead of one per k-step)
+    constexpr int kMaxKS = (9 * CS + 3) / 4;
+    if (nks <= kMaxKS) {
+      v4i af[kMaxKS], bf[kMaxKS][2];
+#pragma unroll
+      for (int kk = 0; kk < kMaxKS; ++kk) {
+        if (kk < nks) {
+          af[kk] = load_a(kk);
+          bf[kk][0] = load_b(kk, 0);
+          if (ntw > 1) bf[kk][1] = load_b(kk, 1);
         }
-        if (ok)
-          a = *reinterpret_cast<const v4i*>(p.a + (((int64_t)n * SH + sy) * SW + sx) * cred + cs * 16);
-        else if (MODE == MODE_DGRAD)
-          a = v4i{0, 0, 0, 0};
-      } else if (s >= p.nslices) {
-        a = v4i{0, 0, 0, 0};
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (j < ntw) {
-          const int col = (nt0 + j) * 16 + r;
-          const v4i b = *reinterpret_cast<const v4i*>(p.b + ((int64_t)col * p.ks + s) * 16);
-          acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, acc[j], 0, 0, 0);
+      for (int kk = 0; kk < kMaxKS; ++kk) {
+        if (kk < nks) {
+          acc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk], bf[kk][0], acc[0], 0, 0, 0);
+          if (ntw > 1) acc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk], bf[kk][1], acc[1], 0, 0, 0);
         }
+      }
+    } else {
+      for (int kk = 0; kk < nks; ++kk) {
+        const v4i a = load_a(kk);
+        acc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, load_b(kk, 0), acc[0], 0, 0, 0);
+        if (ntw > 1) acc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, load_b(kk, 1), acc[1], 0, 0, 0);
       }
     }
   }
