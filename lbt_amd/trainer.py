@@ -18,8 +18,9 @@ MI355X-native execution:
 import torch
 import torch.distributed as dist
 
-from .dfxp import ops
+from . import distributed as D
 from ._lib import NSHARD
+from .dfxp import ops
 
 
 class FlatParams:
@@ -72,7 +73,7 @@ class Trainer:
         nq = len(self.ctx.quantizers)
         self._ncnt = nq * NSHARD * 2
         if self.world > 1:
-            self.comm = torch.zeros(self.flat.n + self._ncnt, dtype=torch.float32, device=self.ctx.device)
+            self.comm = D.make_comm_buffer(self.flat.n, self._ncnt, self.ctx.device)
         if logger is not None:
             logger.info("Model info:\n" + model.info())
 
@@ -95,14 +96,8 @@ class Trainer:
         m.backward()
 
     def _exchange(self):
-        """Sum grads + overflow counters across ranks (RCCL); counts travel as exact fp32."""
-        n = self.flat.n
-        cnt = self.ctx.counts[: self._ncnt]
-        self.comm[:n].copy_(self.flat.g)
-        self.comm[n:].copy_(cnt)
-        dist.all_reduce(self.comm, group=self.pg)
-        self.flat.g.copy_(self.comm[:n])
-        cnt.copy_(self.comm[n:])
+        """Sum grads + overflow counters across ranks (one RCCL all-reduce; lbt_amd/distributed.py)."""
+        D.allreduce_grads_and_counts(self.flat.g, self.ctx.counts[: self._ncnt], self.comm, self.pg)
 
     def _update(self):
         ops.sgd_momentum(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0 / self.world)

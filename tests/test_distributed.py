@@ -1,0 +1,81 @@
+"""Data-parallel path on CPU: world_size-2 gloo processes run the REAL exchange function of the
+trainer (lbt_amd.distributed) on oracle gradients / overflow counters of their batch shards."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lbt_amd import distributed as D
+        from oracle import dfxp, nn
+        from oracle import resnet as R
+        rng = np.random.default_rng(0)          # identical weights on every rank
+        model = R.build_resnet((1, 1, 1), 8, 2e-4)
+        params = {}
+        for name, owner in model.params():
+            if name.endswith("/W"):
+                shp = owner.ksize if hasattr(owner, "ksize") else (owner.in_units, owner.units)
+                lim = np.sqrt(3 / np.prod(shp[:-1]))
+                params[name] = rng.uniform(-lim, lim, size=shp).astype(np.float32)
+            elif name.endswith("/g"):
+                params[name] = np.ones(owner.C, np.float32)
+            else:
+                params[name] = np.zeros(owner.C, np.float32)
+        R.set_params(model, params)
+        xr = np.random.default_rng(100 + rank)  # each rank its own batch shard
+        x = ((xr.integers(0, 256, size=(4, 32, 32, 3)) - 127.5) / 128).astype(np.float32)
+        y = xr.integers(0, 10, size=4)
+        ranges = R.init_ranges(model)
+        _, _, grads, ctx = R.forward_backward(model, ranges, x, y, step=0, seed=0)
+        names = sorted(grads)
+        flat = torch.from_numpy(np.concatenate([grads[k].ravel() for k in names]).astype(np.float32))
+        qn = sorted(ctx.counts)
+        counts = torch.tensor([c for k in qn for c in ctx.counts[k][:2]], dtype=torch.int32)
+        local = (flat.clone(), counts.clone())
+        comm = D.make_comm_buffer(flat.numel(), counts.numel(), "cpu")
+        D.allreduce_grads_and_counts(flat, counts, comm)
+        c = counts.view(-1, 2).tolist()
+        new_I = {k: dfxp.update_range_from_counts(c[i][0], c[i][1], ctx.counts[k][2] * world, 0.0,
+                                                  ctx.counts[k][3], ranges[k]) for i, k in enumerate(qn)}
+        out_q.put((rank, local[0].numpy(), local[1].numpy(), flat.numpy(), counts.numpy(), new_I))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_exchange_two_ranks_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, g0, c0, G0, C0, I0), (_, g1, c1, G1, C1, I1) = res
+    # every rank holds the exact sums
+    assert np.array_equal(G0, G1) and np.array_equal(C0, C1)
+    assert np.array_equal(C0, c0 + c1)                        # integer counters: exact
+    np.testing.assert_allclose(G0, g0 + g1, rtol=1e-6, atol=1e-12)
+    assert not np.array_equal(g0, g1)                          # shards really differ
+    # identical DFXP exponents on both ranks, from the global counts
+    assert I0 == I1
