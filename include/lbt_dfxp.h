@@ -17,7 +17,7 @@
  *     e = bits - I - 1, I = "integer_bits" held per quantiser slot in device memory.
  *   - Quantiser slots live in three device arrays owned by the caller:
  *       exps[slot]      int32  integer bits I (dynamic_fixed_point.py:27,34 "integer_bits")
- *       counts[(slot*LBT_NSHARD + shard)*2 + {0,1}]  int32
+ *       counts[(slot*LBT_NSHARD + shard)*LBT_CSTRIDE + {0,1}]  int32
  *                              #(x*m >= L or x*m < -L), #(x*m >= L/2 or x*m < -L/2)
  *                              (the numerators of overflow_rate, dynamic_fixed_point.py:48-67)
  *       step[0]         uint64 training-step counter (noise counter)
@@ -42,6 +42,9 @@ extern "C" {
  * its per-workgroup partial into shard (workgroup id % LBT_NSHARD) so that thousands of
  * workgroups never serialise on one address; consumers sum the shards.                  */
 #define LBT_NSHARD 32
+/* int32 stride between the overflow-counter shards of one slot: one 128-byte line per shard,
+ * so concurrent workgroups' counter atomics never share a cache line.                    */
+#define LBT_CSTRIDE 32
 
 /* Output encodings of a quantiser. */
 enum {
@@ -54,13 +57,16 @@ enum {
 /* One quantiser: where its exponent / counters live and how it rounds. */
 typedef struct lbt_qdesc {
   const int32_t* exps;   /* device [slots]                                   */
-  int32_t* counts;       /* device [slots][LBT_NSHARD][2]; NULL = no stats   */
+  int32_t* counts;       /* device [slots][LBT_NSHARD][LBT_CSTRIDE]; NULL = no stats */
   const uint64_t* step;  /* device [1]                                       */
   uint64_t seed;         /* noise key                                        */
   uint32_t qid;          /* noise stream id (crc32 of the range variable)    */
   int32_t slot;
   int32_t bits;          /* total bits incl. sign, 2..16                     */
   int32_t stochastic;    /* 1: floor(x*m + u)  0: round-half-even(x*m)       */
+  const float* noise;    /* NULL: Philox inline. Else this step's noise table u[i] for
+                            i < ceil(inner/4)*4, filled by lbt_dfxp_noise_fill (the noise
+                            depends only on (seed, qid, step, i mod inner)).  */
 } lbt_qdesc;
 
 /* Convolution geometry, TF padding already resolved into (top,bottom,left,right). */
@@ -85,6 +91,30 @@ int lbt_dfxp_quantize(const float* x, void* out, int out_kind, int64_t rows, int
  * Slots with nelem <= 0 (not fed this step) are left untouched.                          */
 int lbt_dfxp_range_update(int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
                           const float* nelem, int32_t nslots, uint64_t* step, void* stream);
+
+/* Data-parallel form of the range update (the counters must be summed over ranks first).
+ * counts_fold sums each slot's shards, zeroes them and writes the totals EXACTLY as fp32
+ * (so they can ride in the gradient all-reduce buffer):
+ *   folded[4s+0] = c1 >> 12, folded[4s+1] = c1 & 4095, folded[4s+2] = c2 >> 12, [4s+3] = c2 & 4095
+ * (any rank count < 2^12 keeps every partial sum of the all-reduce below 2^24).
+ * range_update_folded applies the rule above to c = 4096*hi + lo of the (reduced) buffer.  */
+int lbt_dfxp_counts_fold(int32_t* counts, int32_t nslots, float* folded, void* stream);
+int lbt_dfxp_range_update_folded(int32_t* exps, const float* folded, const int32_t* bits, const float* target,
+                                 const float* nelem, int32_t nslots, uint64_t* step, void* stream);
+
+/* Per-step noise tables. Job j writes u[i] = Philox(i>>2, qid, step, seed)[i&3] >> 8 * 2^-24 for
+ * i < ceil(n/4)*4 into out (16-byte aligned), reading *step on the device; one launch fills every
+ * table (grid.y = job). A qdesc whose .noise points at its table then loads 16 B per 4 codes
+ * instead of running Philox per element (dynamic_fixed_point.py:36).                      */
+typedef struct lbt_njob {
+  const uint64_t* step;
+  uint64_t seed;
+  uint32_t qid;
+  int32_t pad;
+  int64_t n;
+  float* out;
+} lbt_njob;
+int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t max_n, void* stream);
 
 /* Quantise a conv / dense weight (HWIO fp32, noise over shape[1:] = [KW,Cin,Cout]) into the
  * layouts the GEMM kernels consume (any output may be NULL):
@@ -136,6 +166,21 @@ int lbt_conv_dgrad_generic(const int8_t* gq, const int8_t* w_hwio, lbt_conv_desc
                            lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
 int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
                            int32_t* slab, int32_t nsplit, void* stream);
+
+/* Stem convolution (conv1 of the CIFAR ResNets, models.py:387-391): input = the image's SIGNED
+ * (bits+1)-bit codes as int16 (|x| <= 2048), patch K = KH*KW*Cin <= 32, Cout % 16 == 0.
+ * Runs on fp16 MFMA, which is exact here (every code and product is an fp16/fp32-exact
+ * integer and every partial sum < 2^24), i.e. bit-identical to lbt_conv_fwd_generic /
+ * lbt_conv_wgrad_generic (dynamic_fixed_point.py:287-305).
+ * fwd: exactly one of y (fp32, Cout <= 128) / yq (int8 codes of qout, + counters, + optional
+ *      sharded channel sums ychsum, as lbt_conv_fwd_i8) is non-NULL.
+ * wgrad: int32 partials slab[nsplit][K][Cout] with nsplit = ceil(N*Ho*Wo / LBT_STEM_WG_PIXELS),
+ *      Cout <= 64; finish with lbt_conv_wgrad_reduce(_many) (x_u8off = 0, gcolsum = NULL).   */
+#define LBT_STEM_WG_PIXELS 256
+int lbt_conv_stem_fwd(const int16_t* x, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw,
+                      float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream);
+int lbt_conv_stem_wgrad(const int16_t* x, const int8_t* gq, lbt_conv_desc d, int32_t* slab, int32_t nsplit,
+                        void* stream);
 
 /* ---------------------------------------------------------------- batch norm -------- */
 
@@ -271,6 +316,11 @@ typedef struct lbt_pjob {
   const int64_t* sums; int32_t C; lbt_qdesc qrg, qr; const float* gamma; float wd2; float* dgamma; float* dbeta;
 } lbt_pjob;
 int lbt_bn_param_grads_many(const lbt_pjob* jobs, int32_t njobs, int32_t max_c, void* stream);
+
+/* Diagnostics: counts (atomically into *bad) the i < n where the BN kernels' division by a
+ * reused divisor (div_by(x, recip(y)), dfxp_device.h) differs in any bit from x / y; if qa
+ * is not NULL also writes x / y to qa and div_by to qb.                                      */
+int lbt_selftest_div(const float* x, const float* y, int64_t n, int32_t* bad, float* qa, float* qb, void* stream);
 
 /* ABI version for the Python loader. */
 int lbt_abi_version(void);

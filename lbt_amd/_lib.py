@@ -14,8 +14,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblbt_dfxp.so")
 
 NSHARD = 32
+STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
+CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 1
+ABI_VERSION = 3
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -23,7 +25,8 @@ c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
 
 class QDesc(ctypes.Structure):
     _fields_ = [("exps", c_void_p), ("counts", c_void_p), ("step", c_void_p), ("seed", c_uint64),
-                ("qid", c_uint32), ("slot", c_int32), ("bits", c_int32), ("stochastic", c_int32)]
+                ("qid", c_uint32), ("slot", c_int32), ("bits", c_int32), ("stochastic", c_int32),
+                ("noise", c_void_p)]
 
 
 NO_Q = QDesc()  # bits == 0: inactive quantiser
@@ -82,6 +85,11 @@ class QJob(ctypes.Structure):
                 ("q", QDesc)]
 
 
+class NJob(ctypes.Structure):
+    _fields_ = [("step", c_void_p), ("seed", c_uint64), ("qid", c_uint32), ("pad", c_int32), ("n", c_int64),
+                ("out", c_void_p)]
+
+
 class RJob(ctypes.Structure):
     _fields_ = [("slab", c_void_p), ("nsplit", c_int32), ("K", c_int32), ("Cout", c_int32), ("x_u8off", c_int32),
                 ("gcolsum", c_void_p), ("qx", QDesc), ("qg", QDesc), ("w", c_void_p), ("wd2", c_float),
@@ -98,6 +106,8 @@ _SIGS = {
     "lbt_abi_version": [],
     "lbt_dfxp_quantize": [_P, _P, c_int32, c_int64, c_int64, QDesc, _P, c_int32, _P],
     "lbt_dfxp_range_update": [_P, _P, _P, _P, _P, c_int32, _P, _P],
+    "lbt_dfxp_counts_fold": [_P, c_int32, _P, _P],
+    "lbt_dfxp_range_update_folded": [_P, _P, _P, _P, _P, c_int32, _P, _P],
     "lbt_dfxp_quantize_weight": [_P, c_int32, c_int32, c_int32, c_int32, QDesc, _P, _P, c_int32, _P, c_int32,
                                  _P, _P],
     "lbt_conv_fwd_i8": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
@@ -107,6 +117,8 @@ _SIGS = {
     "lbt_conv_fwd_generic": [_P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_conv_dgrad_generic": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_generic": [_P, c_int32, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_stem_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
+    "lbt_conv_stem_wgrad": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_bn_chain_fwd": [_P, _P],
     "lbt_bn_chain_bwd_a": [_P, _P],
     "lbt_bn_chain_bwd_b": [_P, _P],
@@ -122,6 +134,8 @@ _SIGS = {
     "lbt_bias_grad": [_P, c_int32, QDesc, _P, _P],
     "lbt_dfxp_quantize_weights": [_P, c_int32, c_int32, _P],
     "lbt_dfxp_quantize_many": [_P, c_int32, _P],
+    "lbt_dfxp_noise_fill": [_P, c_int32, c_int64, _P],
+    "lbt_selftest_div": [_P, _P, c_int64, _P, _P, _P, _P],
     "lbt_conv_wgrad_reduce_many": [_P, c_int32, c_int32, _P],
     "lbt_bn_param_grads_many": [_P, c_int32, c_int32, _P],
 }

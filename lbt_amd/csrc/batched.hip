@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kThreads) void quantize_weights_kernel(const lbt_wj
   for (int k = threadIdx.x; k < K; k += kThreads) {
     const int tap = k / j.Cin, ci = k % j.Cin;
     const int64_t idx = (int64_t)k * j.Cout + co;
-    const float u = j.q.stochastic ? noise1(idx % inner, j.q.qid, s.step, j.q.seed) : 0.f;
+    const float u = j.q.stochastic ? qnoise1(j.q, s.step, idx % inner) : 0.f;
     const int c = quant1(s, j.q.stochastic, j.w[idx], u, ov1, ov2);
     csum += c;
     if (j.w_hwio) j.w_hwio[idx] = (int8_t)c;
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob*
   const QState s = qstate(j.q);
   int ov1 = 0, ov2 = 0;
   for (int64_t i = threadIdx.x; i < j.n; i += kThreads) {
-    const float u = j.q.stochastic ? noise1(i % j.inner, j.q.qid, s.step, j.q.seed) : 0.f;
+    const float u = j.q.stochastic ? qnoise1(j.q, s.step, i % j.inner) : 0.f;
     const int c = quant1(s, j.q.stochastic, j.x[i], u, ov1, ov2);
     store_code(j.out, j.out_kind, i, c, s.inv_m);
   }
@@ -103,7 +103,25 @@ __global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
   j.dbeta[c] = (float)((double)sg * g2);
 }
 
+// grid (blocks, njobs): thread -> noise block b (4 values, one Philox call)
+__global__ __launch_bounds__(kThreads) void noise_fill_kernel(const lbt_njob* __restrict__ jobs) {
+  const lbt_njob j = jobs[blockIdx.y];
+  const int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (4 * b >= j.n) return;
+  const uint64_t step = *j.step;
+  const Noise4 n = noise4((uint64_t)b, j.qid, step, j.seed);
+  *reinterpret_cast<float4*>(j.out + 4 * b) = make_float4(n.u[0], n.u[1], n.u[2], n.u[3]);
+}
+
 }  // namespace
+
+extern "C" int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t max_n, void* stream) {
+  if (njobs <= 0 || max_n <= 0) return LBT_OK;
+  const int64_t blocks = (max_n + 4 * kThreads - 1) / (4 * kThreads);
+  if (njobs > 65535 || blocks > 0x7fffffff) return LBT_EINVAL;
+  hipLaunchKernelGGL(noise_fill_kernel, dim3((unsigned)blocks, njobs), dim3(kThreads), 0, (hipStream_t)stream, jobs);
+  return (int)hipGetLastError();
+}
 
 extern "C" int lbt_dfxp_quantize_weights(const lbt_wjob* jobs, int32_t njobs, int32_t max_cout, void* stream) {
   if (njobs <= 0) return LBT_OK;

@@ -22,6 +22,19 @@ LBT_DEV void load4_i8(const int8_t* p, int64_t i, int v[4]) {
   const char4 c = *reinterpret_cast<const char4*>(p + i);
   v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
 }
+LBT_DEV void unpack4_i8(int w, int v[4]) {
+  v[0] = (int8_t)(w & 0xff); v[1] = (int8_t)((w >> 8) & 0xff);
+  v[2] = (int8_t)((w >> 16) & 0xff); v[3] = (int8_t)(w >> 24);
+}
+LBT_DEV int ld_i8x4(const int8_t* p, int64_t i) { return *reinterpret_cast<const int*>(p + i); }
+LBT_DEV float4 ld_f32x4(const float* p, int64_t i) { return *reinterpret_cast<const float4*>(p + i); }
+LBT_DEV void f4(const float4& c, float v[4]) { v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w; }
+
+// Rows are processed in batches of kRB: every load of a batch is issued before any of its
+// arithmetic (stores may alias the inputs as far as the compiler knows, so it would not hoist
+// them itself) -- one HBM round trip per batch instead of one per row.
+constexpr int kRB = 4;
+
 LBT_DEV void load4_f32(const float* p, int64_t i, float v[4]) {
   const float4 c = *reinterpret_cast<const float4*>(p + i);
   v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
@@ -55,7 +68,7 @@ LBT_DEV void store4_code(void* out, int kind, int64_t i, const int c[4], float i
 
 LBT_DEV Noise4 noise_for(const lbt_qdesc& q, const QState& s, int64_t g) {
   Noise4 n = {{0.f, 0.f, 0.f, 0.f}};
-  if (s.active && q.stochastic) n = noise4((uint64_t)g, q.qid, s.step, q.seed);
+  if (s.active && q.stochastic) n = qnoise4(q, s.step, (uint64_t)g);
   return n;
 }
 
@@ -99,7 +112,8 @@ LBT_DEV const lbt_chain_branch& fbranch(const lbt_chain_fwd& a) { return B == 0 
 template <int NB>
 __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, int rpt) {
   extern __shared__ float shf[];  // per branch: mu, sigma, gq, bq [C each]; then long long tmp[2C]
-  __shared__ int sh_cnt[2 * kThreads / 64];
+  __shared__ int sh_cnt[8 * kThreads / 64];
+  LBT_TS(0);
   const int C = a.C;
   long long* tmp = reinterpret_cast<long long*>(shf + 8 * C);
   QState qr[2];
@@ -119,15 +133,30 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
       for (int c = threadIdx.x; c < C; c += kThreads) { P[2 * C + c] = B.gb[c]; P[3 * C + c] = B.gb[C + c]; }
   }
   __syncthreads();
+  LBT_TS(1);
+  // this thread's channel quad is fixed: its per-channel constants live in registers
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int c0 = (int)(((uint32_t)g << 2) % (uint32_t)C);
+  float pm[NB][4], pg[NB][4], pb[NB][4];
+  Recip ps[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const float* P = shf + 4 * C * b;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pm[b][k] = P[c0 + k];
+      ps[b][k] = recip(P[C + c0 + k]);
+      pg[b][k] = P[2 * C + c0 + k];
+      pb[b][k] = P[3 * C + c0 + k];
+    }
+  }
   const QState so1 = qstate(a.qo1), so2 = qstate(a.qo2);
   const bool o1 = a.o1 && so1.active, o2 = a.o2 && so2.active;
   int ovr[2][2] = {{0, 0}, {0, 0}};
   int ovo[2][2] = {{0, 0}, {0, 0}};
 
   const int64_t groups = a.inner >> 2;
-  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (g < groups) {
-    const int c0 = (int)((g << 2) % C);
     Noise4 nr[2];
 #pragma unroll
     for (int b = 0; b < NB; ++b) nr[b] = noise_for(b == 0 ? a.b1.qr : a.b2.qr, qr[b], g);
@@ -135,26 +164,42 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
     const Noise4 no2 = noise_for(a.qo2, so2, g);
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
-#pragma unroll 2
-    for (int64_t r = r0; r < rend; ++r) {
-      const int64_t e = r * a.inner + (g << 2);
+    for (int64_t rb = r0; rb < rend; rb += kRB) {
+      int qv[NB][kRB];
+      float4 xv[NB][kRB], rv[kRB];
+#pragma unroll
+      for (int j = 0; j < kRB; ++j) {
+        const int64_t e = (rb + j) * a.inner + (g << 2);
+        if (rb + j < rend) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const lbt_chain_branch& B = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+            if (B.nrm.q) qv[b][j] = ld_i8x4(B.nrm.q, e);
+            else xv[b][j] = ld_f32x4(B.xin, e);
+          }
+          if (a.res) rv[j] = ld_f32x4(a.res, e);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kRB; ++j) {
+      if (rb + j >= rend) break;
+      const int64_t e = (rb + j) * a.inner + (g << 2);
       float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         const lbt_chain_branch& B = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
-        const float* P = shf + 4 * C * b;
         float t[4];
         if (B.nrm.q) {
           int q[4];
-          load4_i8(B.nrm.q, e, q);
+          unpack4_i8(qv[b][j], q);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float x1 = (float)q[k] * sn[b];
-            const float x2 = x1 - P[c0 + k];
-            t[k] = x2 / P[C + c0 + k];
+            const float x2 = x1 - pm[b][k];
+            t[k] = div_by(x2, ps[b][k]);  // == x2 / sigma
           }
         } else {
-          load4_f32(B.xin, e, t);
+          f4(xv[b][j], t);
         }
         if (qr[b].active) {
           int R[4];
@@ -162,8 +207,8 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
           for (int k = 0; k < 4; ++k) {
             R[k] = quant1(qr[b], B.qr.stochastic, t[k], nr[b].u[k], ovr[b][0], ovr[b][1]);
             const float xr = (float)R[k] * qr[b].inv_m;
-            const float m1 = xr * P[2 * C + c0 + k];
-            t[k] = m1 + P[3 * C + c0 + k];
+            const float m1 = xr * pg[b][k];
+            t[k] = m1 + pb[b][k];
           }
           if (B.rout) store4_i8(B.rout, e, R, 0);
         }
@@ -172,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
       }
       if (a.res) {
         float rr[4];
-        load4_f32(a.res, e, rr);
+        f4(rv[j], rr);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = v[k] + rr[k];
       }
@@ -193,19 +238,31 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
         for (int k = 0; k < 4; ++k) c[k] = quant1(so2, a.qo2.stochastic, v[k], no2.u[k], ovo[1][0], ovo[1][1]);
         store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
       }
+      }
     }
   }
-  if (qr[0].active) block_flush_counts(a.b1.qr, ovr[0][0], ovr[0][1], sh_cnt);
-  if (NB > 1 && qr[NB - 1].active) block_flush_counts(a.b2.qr, ovr[NB - 1][0], ovr[NB - 1][1], sh_cnt);
-  if (o1) block_flush_counts(a.qo1, ovo[0][0], ovo[0][1], sh_cnt);
-  if (o2) block_flush_counts(a.qo2, ovo[1][0], ovo[1][1], sh_cnt);
+  LBT_TS(2);
+  // every quantiser's counters behind one barrier
+  const bool st[4] = {qr[0].active && a.b1.qr.counts, NB > 1 && qr[NB - 1].active && a.b2.qr.counts,
+                      o1 && a.qo1.counts, o2 && a.qo2.counts};
+  if (st[0]) counts_stage(0, 4, ovr[0][0], ovr[0][1], sh_cnt);
+  if (st[1]) counts_stage(1, 4, ovr[NB - 1][0], ovr[NB - 1][1], sh_cnt);
+  if (st[2]) counts_stage(2, 4, ovo[0][0], ovo[0][1], sh_cnt);
+  if (st[3]) counts_stage(3, 4, ovo[1][0], ovo[1][1], sh_cnt);
+  if (!(st[0] || st[1] || st[2] || st[3])) return;
+  __syncthreads();
+  if (st[0]) counts_publish(0, 4, a.b1.qr, sh_cnt);
+  if (st[1]) counts_publish(1, 4, a.b2.qr, sh_cnt);
+  if (st[2]) counts_publish(2, 4, a.qo1, sh_cnt);
+  if (st[3]) counts_publish(3, 4, a.qo2, sh_cnt);
+  LBT_TS(3);
 }
 
 // ============================================================================ backward pass A
 template <int NB>
 __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a, int rpt) {
   extern __shared__ float shf[];  // per branch: gq, bq [C]; then long long sums[2][4C]
-  __shared__ int sh_cnt[2 * kThreads / 64];
+  __shared__ int sh_cnt[8 * kThreads / 64];
   const int C = a.C;
   long long* S = reinterpret_cast<long long*>(shf + 4 * C);  // [2][4C]
   QState qrg[2], qng[2], qr[2];
@@ -223,7 +280,14 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
   int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};  // [branch][rescale|norm][c1|c2]
   const int64_t groups = a.inner >> 2;
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int c0 = (int)((g << 2) % C);
+  const int c0 = (int)(((uint32_t)g << 2) % (uint32_t)C);
+  float gam[2][4], bet[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) gam[b][k] = shf[b * 2 * C + c0 + k];
+    bet[k] = shf[C + c0 + k];
+  }
   int acc[2][4][4];  // [branch][sum][k]
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -241,24 +305,42 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
     }
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
-#pragma unroll 2
-    for (int64_t r = r0; r < rend; ++r) {
-      const int64_t e = r * a.inner + (g << 2);
+    for (int64_t rb = r0; rb < rend; rb += kRB) {
+      float4 gv4[kRB], ym4[kRB];
+      int R1v[kRB], R2v[kRB], qnv[2][kRB];
+#pragma unroll
+      for (int j = 0; j < kRB; ++j) {
+        const int64_t e = (rb + j) * a.inner + (g << 2);
+        R1v[j] = 0;
+        if (rb + j < rend) {
+          gv4[j] = ld_f32x4(a.g, e);
+          if (a.b1.R) R1v[j] = ld_i8x4(a.b1.R, e);
+          if (a.y_mask) ym4[j] = ld_f32x4(a.y_mask, e);
+          if (NB > 1 && qrg[NB - 1].active) R2v[j] = ld_i8x4(a.b2.R, e);
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            if (qng[b].active) qnv[b][j] = ld_i8x4(b == 0 ? a.b1.qn_codes : a.b2.qn_codes, e);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kRB; ++j) {
+      if (rb + j >= rend) break;
+      const int64_t e = (rb + j) * a.inner + (g << 2);
       float gv[4];
-      load4_f32(a.g, e, gv);
-      int R1[4] = {0, 0, 0, 0};
-      if (a.b1.R) load4_i8(a.b1.R, e, R1);
+      f4(gv4[j], gv);
+      int R1[4];
+      unpack4_i8(R1v[j], R1);
       if (a.y_mask) {
         float ym[4];
-        load4_f32(a.y_mask, e, ym);
+        f4(ym4[j], ym);
 #pragma unroll
         for (int k = 0; k < 4; ++k) gv[k] = ym[k] > 0.f ? gv[k] : 0.f;
       } else if (a.mask_from_r) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float xr = (float)R1[k] * qr[0].inv_m;
-          const float m1 = xr * shf[c0 + k];
-          const float yv = m1 + shf[C + c0 + k];
+          const float m1 = xr * gam[0][k];
+          const float yv = m1 + bet[k];
           gv[k] = yv > 0.f ? gv[k] : 0.f;
         }
       }
@@ -269,19 +351,19 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
         float d[4] = {gv[0], gv[1], gv[2], gv[3]};
         if (qrg[b].active) {
           int R[4] = {R1[0], R1[1], R1[2], R1[3]};
-          if (b) load4_i8(B.R, e, R);
+          if (b) unpack4_i8(R2v[j], R);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const int G2 = quant1(qrg[b], B.qrg.stochastic, d[k], nrg[b].u[k], ov[b][0][0], ov[b][0][1]);
             acc[b][0][k] += G2 * R[k];
             acc[b][1][k] += G2;
             const float gh = (float)G2 * qrg[b].inv_m;
-            d[k] = gh * shf[b * 2 * C + c0 + k];
+            d[k] = gh * gam[b][k];
           }
         }
         if (qng[b].active) {
           int G[4], qn[4];
-          load4_i8(B.qn_codes, e, qn);
+          unpack4_i8(qnv[b][j], qn);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             G[k] = quant1(qng[b], B.qng.stochastic, d[k], nng[b].u[k], ov[b][1][0], ov[b][1][1]);
@@ -292,6 +374,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
         } else if (B.dout) {
           store4_f32(B.dout, e, d);
         }
+      }
       }
     }
   }
@@ -311,13 +394,15 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
-    if (qrg[b].active) block_flush_counts(B.qrg, ov[b][0][0], ov[b][0][1], sh_cnt);
-    if (qng[b].active) block_flush_counts(B.qng, ov[b][1][0], ov[b][1][1], sh_cnt);
+    if (qrg[b].active && B.qrg.counts) counts_stage(2 * b, 4, ov[b][0][0], ov[b][0][1], sh_cnt);
+    if (qng[b].active && B.qng.counts) counts_stage(2 * b + 1, 4, ov[b][1][0], ov[b][1][1], sh_cnt);
   }
-  __syncthreads();
+  __syncthreads();  // the only barrier after the main loop: LDS sums and counters complete
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
+    if (qrg[b].active) counts_publish(2 * b, 4, B.qrg, sh_cnt);
+    if (qng[b].active) counts_publish(2 * b + 1, 4, B.qng, sh_cnt);
     if (B.sums) block_flush_sums(S + b * 4 * C, 4 * C, B.sums, 4 * C);
   }
 }
@@ -325,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
 // ============================================================================ backward pass B
 __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a, int rpt) {
   extern __shared__ float shf[];  // mu, sigma, mg, mgx [C]; then long long tmp[2C] / colsum[2C]
-  __shared__ int sh_cnt[2 * kThreads / 64];
+  __shared__ int sh_cnt[8 * kThreads / 64];
   const int C = a.C;
   float* mu = shf;
   float* sg = shf + C;
@@ -358,29 +443,48 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
   int ov1 = 0, ov2 = 0;
   const int64_t groups = a.inner >> 2;
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int c0 = (int)((g << 2) % C);
+  const int c0 = (int)(((uint32_t)g << 2) % (uint32_t)C);
+  float rmu[4], rmg[4], rmgx[4];
+  Recip rsg[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rmu[k] = mu[c0 + k];
+    rsg[k] = recip(sg[c0 + k]);
+    rmg[k] = mg[c0 + k];
+    rmgx[k] = mgx[c0 + k];
+  }
   int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   if (g < groups) {
     const Noise4 no = noise_for(a.qo, so, g);
     const int64_t r0 = (int64_t)blockIdx.y * rpt;
     const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
-#pragma unroll 2
-    for (int64_t r = r0; r < rend; ++r) {
-      const int64_t e = r * a.inner + (g << 2);
+    for (int64_t rb = r0; rb < rend; rb += kRB) {
+      int Gv[kRB], qv[kRB];
+#pragma unroll
+      for (int j = 0; j < kRB; ++j) {
+        const int64_t e = (rb + j) * a.inner + (g << 2);
+        if (rb + j < rend) {
+          Gv[j] = ld_i8x4(a.G, e);
+          qv[j] = ld_i8x4(a.qn_codes, e);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kRB; ++j) {
+      if (rb + j >= rend) break;
+      const int64_t e = (rb + j) * a.inner + (g << 2);
       int G[4], q[4];
-      load4_i8(a.G, e, G);
-      load4_i8(a.qn_codes, e, q);
+      unpack4_i8(Gv[j], G);
+      unpack4_i8(qv[j], q);
       float dx[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int c = c0 + k;
         const float x1 = (float)q[k] * sn.inv_m;
-        const float x2 = x1 - mu[c];
-        const float xh = x2 / sg[c];
+        const float x2 = x1 - rmu[k];
+        const float xh = div_by(x2, rsg[k]);  // == x2 / sigma
         const float gh = (float)G[k] * sgq.inv_m;
-        const float t1 = gh - mg[c];
-        const float t2 = xh * mgx[c];
-        dx[k] = (t1 - t2) / sg[c];
+        const float t1 = gh - rmg[k];
+        const float t2 = xh * rmgx[k];
+        dx[k] = div_by(t1 - t2, rsg[k]);      // == (t1 - t2) / sigma
       }
       if (a.dx) store4_f32(a.dx, e, dx);
       if (want_q) {
@@ -392,6 +496,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
           s2[k] += c[k] * c[k];
         }
         store4_i8(a.gq, e, c, 0);
+      }
       }
     }
   }
@@ -405,11 +510,11 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
       if (own && v2) atomicAdd((unsigned long long*)&tmp[C + c0 + k], (unsigned long long)(long long)v2);
     }
   }
-  if (want_q) block_flush_counts(a.qo, ov1, ov2, sh_cnt);
-  if (want_q && a.gcolsum) {
-    __syncthreads();
-    block_flush_sums(tmp, 2 * C, a.gcolsum, 2 * C);
-  }
+  if (!want_q) return;
+  if (a.qo.counts) counts_stage(0, 1, ov1, ov2, sh_cnt);
+  __syncthreads();
+  counts_publish(0, 1, a.qo, sh_cnt);
+  if (a.gcolsum) block_flush_sums(tmp, 2 * C, a.gcolsum, 2 * C);
 }
 
 __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
@@ -451,6 +556,8 @@ bool shape_ok(int64_t rows, int64_t inner, int C) {
 }
 
 }  // namespace
+
+LBT_TRACE_SETTER(bn)
 
 extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   if (!shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;

@@ -19,7 +19,7 @@
 // wgrad: GEMM rows = (tap, ci), cols = co, k = pixels.  Each wave stages 64 pixels of G and of
 // the tap-shifted X into LDS transposed ([channel][pixel]) and issues 16x16x64 MFMAs; each
 // workgroup owns a pixel range and one tap and writes an int32 partial (exact, no atomics).
-#include "dfxp_device.h"
+#include "conv_epilogue.h"
 
 using namespace lbt;
 
@@ -50,9 +50,10 @@ struct GemmArgs {
 };
 
 template <int MODE, int CS>
-__global__ __launch_bounds__(kThreads) void conv_gemm_kernel(GemmArgs p) {
+__global__ __launch_bounds__(kThreads, CS == 1 ? 8 : 1) void conv_gemm_kernel(GemmArgs p) {
   __shared__ int sh_cnt[2 * kThreads / 64];
   __shared__ long long sh_sum[2 * 128];
+  LBT_TS(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nt_total = p.ncol >> 4;
   const int wpm = nt_total < 4 ? nt_total : 4;  // waves per M-tile
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(GemmArgs p) {
     }
   }
 
+  LBT_TS(1);
   // ---------------- epilogue
   const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
   if (!want_q) {
@@ -168,13 +170,8 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(GemmArgs p) {
     }
     return;
   }
-  // Quantising epilogue (Normalization_q input quantiser fused into the conv): the wave's
-  // 16 x (16*ntw) tile goes through LDS so each lane owns 4 CONSECUTIVE channels of one row:
-  // one Philox call per 4 outputs (its 4 noise indices share a Philox block), char4 stores,
-  // and per-channel sums reduced across the lanes that share a channel quad.
+  // Quantising epilogue (conv_epilogue.h): tile -> LDS -> 4 consecutive channels per lane.
   __shared__ float tile[4][16][33];
-  const QState qs = qstate(p.qout);
-  int ov1 = 0, ov2 = 0;
   if (wave_live) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -185,58 +182,11 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(GemmArgs p) {
       for (int i = 0; i < 4; ++i) tile[wave][kg * 4 + i][j * 16 + r] = (float)(acc[j][i] + corr) * scale;
     }
   }
-  __syncthreads();
-  const int64_t HWo = (int64_t)OH * OW;
-  const int quads = 4 * ntw;  // channel quads per row of this wave's tile
-  int s1[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (pass >= ntw) continue;
-    const int id = pass * 64 + lane;
-    const int rr = id / quads, cq = id - rr * quads;
-    const int64_t row = mtile * 16 + rr;
-    if (!wave_live || row >= p.M) continue;
-    const int col0 = nt0 * 16 + cq * 4;
-    const Noise4 n = p.qout.stochastic ? noise4((uint64_t)(((row % HWo) * p.ncol + col0) >> 2), p.qout.qid, qs.step,
-                                                p.qout.seed)
-                                       : Noise4{{0.f, 0.f, 0.f, 0.f}};
-    char4 o;
-    int c[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      c[k] = quant1(qs, p.qout.stochastic, tile[wave][rr][cq * 4 + k], n.u[k], ov1, ov2);
-      s1[pass][k] = c[k];
-      s2[pass][k] = c[k] * c[k];
-    }
-    o.x = (int8_t)c[0]; o.y = (int8_t)c[1]; o.z = (int8_t)c[2]; o.w = (int8_t)c[3];
-    *reinterpret_cast<char4*>(p.yq + row * p.ncol + col0) = o;
-  }
-  if (want_sum) {
-    // lanes with equal (lane % quads) hold the same channel quad: xor-reduce over quads..32
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      if (pass >= ntw) continue;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int a1 = s1[pass][k], a2 = s2[pass][k];
-        for (int o = quads; o < 64; o <<= 1) {
-          a1 += __shfl_xor(a1, o, 64);
-          a2 += __shfl_xor(a2, o, 64);
-        }
-        const int cq = (pass * 64 + lane) % quads;
-        if (wave_live && lane < quads) {
-          const int ch = nt0 * 16 + cq * 4 + k;
-          if (a1) atomicAdd((unsigned long long*)&sh_sum[ch], (unsigned long long)(long long)a1);
-          if (a2) atomicAdd((unsigned long long*)&sh_sum[p.ncol + ch], (unsigned long long)(long long)a2);
-        }
-      }
-    }
-  }
-  block_flush_counts(p.qout, ov1, ov2, sh_cnt);
-  if (want_sum) {
-    __syncthreads();
-    block_flush_sums(sh_sum, 2 * p.ncol, p.ychsum, 2 * p.ncol);
-  }
+  wave_lds_sync();
+  LBT_TS(2);
+  const QOut qo{p.yq, p.qout, want_sum ? p.ychsum : nullptr, p.M, p.ncol, (int64_t)OH * OW};
+  quant_epilogue(qo, tile[wave], wave_live, mtile, nt0, ntw, sh_sum, sh_cnt);
+  LBT_TS(3);
 }
 
 // ----------------------------------------------------------------------------- wgrad
@@ -390,6 +340,8 @@ bool desc_ok(const lbt_conv_desc& d) {
 }
 
 }  // namespace
+
+LBT_TRACE_SETTER(conv)
 
 extern "C" int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf,
                                const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,

@@ -12,6 +12,33 @@
 
 #define LBT_DEV __device__ __forceinline__
 
+// Phase timestamps for kernel studies (scratch builds with -DLBT_TRACE only): LBT_TS(i) stores
+// s_memrealtime (100 MHz) of workgroup thread 0 into trace[wg*8 + i]; slot 7 = XCC id.
+#ifdef LBT_TRACE
+static __device__ unsigned long long* lbt_trace_buf;
+#define LBT_TS(i)                                                                                       \
+  do {                                                                                                  \
+    if (threadIdx.x == 0 && lbt_trace_buf) {                                                            \
+      const size_t wg_ = (size_t)blockIdx.x + (size_t)blockIdx.y * gridDim.x;                           \
+      lbt_trace_buf[wg_ * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                                  \
+      if ((i) == 0) {                                                                                   \
+        unsigned x_;                                                                                    \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x_));                               \
+        lbt_trace_buf[wg_ * 8 + 7] = x_;                                                                \
+      }                                                                                                 \
+    }                                                                                                   \
+  } while (0)
+#define LBT_TRACE_SETTER(tu)                                                                            \
+  extern "C" int lbt_trace_set_##tu(void* p) {                                                          \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(lbt_trace_buf), &p, sizeof(p));                            \
+  }
+#else
+#define LBT_TS(i) \
+  do {            \
+  } while (0)
+#define LBT_TRACE_SETTER(tu)
+#endif
+
 namespace lbt {
 
 constexpr int kEMax = 30;  // reference computes 2**e in int32: defined for 0 <= e <= 30
@@ -42,11 +69,23 @@ LBT_DEV Noise4 noise4(uint64_t blk, uint32_t qid, uint64_t step, uint64_t seed) 
   n.u[0] = u24(r.x); n.u[1] = u24(r.y); n.u[2] = u24(r.z); n.u[3] = u24(r.w);
   return n;
 }
+// Noise of noise-block blk (indices 4blk..4blk+3) of quantiser q: from its per-step table if it
+// has one (lbt_dfxp_noise_fill wrote the same Philox values), else Philox inline.
+LBT_DEV Noise4 qnoise4(const lbt_qdesc& q, uint64_t step, uint64_t blk) {
+  if (q.noise) {
+    const float4 v = *reinterpret_cast<const float4*>(q.noise + 4 * blk);
+    return Noise4{{v.x, v.y, v.z, v.w}};
+  }
+  return noise4(blk, q.qid, step, q.seed);
+}
 LBT_DEV float noise1(uint64_t idx, uint32_t qid, uint64_t step, uint64_t seed) {
   U4 r = philox((uint32_t)(idx >> 2), qid, (uint32_t)step, (uint32_t)(step >> 32), (uint32_t)seed,
                 (uint32_t)(seed >> 32));
   const uint32_t k = (uint32_t)(idx & 3);
   return u24(k == 0 ? r.x : k == 1 ? r.y : k == 2 ? r.z : r.w);
+}
+LBT_DEV float qnoise1(const lbt_qdesc& q, uint64_t step, uint64_t idx) {
+  return q.noise ? q.noise[idx] : noise1(idx, q.qid, step, q.seed);
 }
 
 // ------------------------------------------------------------------ quantiser state
@@ -92,6 +131,31 @@ LBT_DEV int quant1(const QState& s, int stochastic, float x, float u, int& ov1, 
   return (int)v;
 }
 
+// ------------------------------------------------------------------ division by a reused divisor
+// The compiler's correctly rounded fp32 x / y is
+//   ys = div_scale(y); r0 = rcp(ys); e = fma(-ys, r0, 1); rc = fma(e, r0, r0);
+//   xs = div_scale(x); q = xs * rc; r = fma(-ys, q, xs); q1 = fma(r, rc, q); r1 = fma(-ys, q1, xs);
+//   div_fixup(div_fmas(r1, rc, q1))
+// where div_scale / div_fmas / div_fixup are identities unless an operand or the quotient is
+// near the ends of the exponent range (|x|,|y| in [2^-60, 2^60] here: BN moments of DFXP codes).
+// Recip holds the divisor-only part (once per channel); div_by runs the rest: the SAME operations,
+// so the same bits as '/' (tests/test_gpu_parity.py hammers it against '/').
+struct Recip { float y, rc; };
+LBT_DEV Recip recip(float y) {
+  const float r0 = __builtin_amdgcn_rcpf(y);
+  const float e = fmaf(-y, r0, 1.0f);
+  return Recip{y, fmaf(e, r0, r0)};
+}
+// y > 0. copysign restores what div_fixup does for x = -0 (the fma chain yields +0); for x != 0
+// the quotient already carries x's sign.
+LBT_DEV float div_by(float x, const Recip& d) {
+  const float q = x * d.rc;
+  const float r = fmaf(-d.y, q, x);
+  const float q1 = fmaf(r, d.rc, q);
+  const float r1 = fmaf(-d.y, q1, x);
+  return copysignf(fmaf(r1, d.rc, q1), x);
+}
+
 // ------------------------------------------------------------------ reductions
 LBT_DEV int wave_sum_i32(int v) {
 #pragma unroll
@@ -108,23 +172,37 @@ LBT_DEV int shard_id() {
   return (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 13u) % LBT_NSHARD);
 }
 
-// Flush per-thread overflow counts: wave reduce -> LDS -> one atomic per workgroup into this
-// workgroup's shard.  EVERY thread of the block must call it (contains barriers).
-// sh must hold 2 ints per wave.
-LBT_DEV void block_flush_counts(const lbt_qdesc& q, int ov1, int ov2, int* sh) {
-  if (!q.counts) return;  // uniform
+// Overflow counts of nq quantisers flushed behind ONE barrier:
+//   counts_stage(i, nq, ov1, ov2, sh)  every thread, before the barrier: wave totals -> LDS
+//                                      (sh holds 2*nq ints per wave)
+//   __syncthreads()
+//   counts_publish(i, nq, q, sh)       every thread, after it: lanes 2i, 2i+1 add the workgroup
+//                                      totals of quantiser i into this workgroup's shard
+LBT_DEV void counts_stage(int i, int nq, int ov1, int ov2, int* sh) {
   ov1 = wave_sum_i32(ov1);
   ov2 = wave_sum_i32(ov2);
-  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  if ((threadIdx.x & 63) == 0) { sh[2 * w] = ov1; sh[2 * w + 1] = ov2; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t1 = 0, t2 = 0;
-    for (int i = 0; i < nw; ++i) { t1 += sh[2 * i]; t2 += sh[2 * i + 1]; }
-    int32_t* c = q.counts + ((int64_t)q.slot * LBT_NSHARD + shard_id()) * 2;
-    if (t1) atomicAdd(&c[0], t1);
-    if (t2) atomicAdd(&c[1], t2);
+  if ((threadIdx.x & 63) == 0) {
+    int* p = sh + (threadIdx.x >> 6) * 2 * nq + 2 * i;
+    p[0] = ov1;
+    p[1] = ov2;
   }
+}
+LBT_DEV void counts_publish(int i, int nq, const lbt_qdesc& q, const int* sh) {
+  const int j = (int)threadIdx.x - 2 * i;
+  if (!q.counts || j < 0 || j > 1) return;
+  const int nw = (blockDim.x + 63) >> 6;
+  int t = 0;
+  for (int w = 0; w < nw; ++w) t += sh[w * 2 * nq + 2 * i + j];
+  if (t) atomicAdd(q.counts + ((int64_t)q.slot * LBT_NSHARD + shard_id()) * LBT_CSTRIDE + j, t);
+}
+
+// Single-quantiser flush for kernels with nothing else to publish. EVERY thread of the block
+// must call it (contains barriers). sh must hold 2 ints per wave.
+LBT_DEV void block_flush_counts(const lbt_qdesc& q, int ov1, int ov2, int* sh) {
+  if (!q.counts) return;  // uniform
+  counts_stage(0, 1, ov1, ov2, sh);
+  __syncthreads();
+  counts_publish(0, 1, q, sh);
   __syncthreads();
 }
 

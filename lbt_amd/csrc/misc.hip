@@ -121,6 +121,17 @@ __global__ void bias_grad_kernel(const int64_t* __restrict__ chsum, int C, lbt_q
 
 unsigned blocks4(int64_t n) { return (unsigned)(((n + 3) / 4 + 255) / 256); }
 
+// bitwise comparison of div_by(x, recip(y)) with the compiler's correctly rounded x / y
+__global__ void selftest_div_kernel(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
+                                    int32_t* __restrict__ bad, float* __restrict__ qa, float* __restrict__ qb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float a = x[i] / y[i];
+  const float b = div_by(x[i], recip(y[i]));
+  if (__float_as_uint(a) != __float_as_uint(b)) atomicAdd(bad, 1);
+  if (qa) { qa[i] = a; qb[i] = b; }
+}
+
 }  // namespace
 
 extern "C" int lbt_relu_fwd(const float* x, float* y, int64_t n, void* stream) {
@@ -167,5 +178,13 @@ extern "C" int lbt_bias_add(float* y, const float* b, int64_t n, int32_t C, void
 }
 extern "C" int lbt_bias_grad(const int64_t* chsum, int32_t C, lbt_qdesc qg, float* db, void* stream) {
   hipLaunchKernelGGL(bias_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, chsum, C, qg, db);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_selftest_div(const float* x, const float* y, int64_t n, int32_t* bad, float* qa, float* qb,
+                                void* stream) {
+  if (n <= 0) return LBT_OK;
+  hipLaunchKernelGGL(selftest_div_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, y,
+                     n, bad, qa, qb);
   return (int)hipGetLastError();
 }

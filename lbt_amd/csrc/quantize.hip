@@ -34,7 +34,7 @@ __global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
   int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   if (g < groups) {
     Noise4 n = {{0.f, 0.f, 0.f, 0.f}};
-    if (q.stochastic) n = noise4(g, q.qid, s.step, q.seed);
+    if (q.stochastic) n = qnoise4(q, s.step, g);
     const int64_t rend = r0 + rpt < rows ? r0 + rpt : rows;
 #pragma unroll 4
     for (int64_t r = r0; r < rend; ++r) {
@@ -80,11 +80,11 @@ __global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
       }
     }
   }
-  block_flush_counts(q, ov1, ov2, sh_cnt);
-  if (chsum) {
-    __syncthreads();
-    block_flush_sums(sh_sum, 2 * C, chsum, 2 * C);
-  }
+  if (q.counts) counts_stage(0, 1, ov1, ov2, sh_cnt);
+  if (!(chsum || q.counts)) return;
+  __syncthreads();  // one barrier publishes counters and channel sums
+  counts_publish(0, 1, q, sh_cnt);
+  if (chsum) block_flush_sums(sh_sum, 2 * C, chsum, 2 * C);
 }
 
 // Any shape: one element per thread, per-element Philox (weights, gamma/beta, odd shapes).
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(kThreads) void quantize_generic_kernel(
   int64_t* cs = chsum ? chsum + (int64_t)shard_id() * 2 * C : nullptr;
   int ov1 = 0, ov2 = 0;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
-    const float u = q.stochastic ? noise1(i % inner, q.qid, s.step, q.seed) : 0.f;
+    const float u = q.stochastic ? qnoise1(q, s.step, i % inner) : 0.f;
     const int c = quant1(s, q.stochastic, x[i], u, ov1, ov2);
     store_code(out, out_kind, i, c, s.inv_m);
     if (cs) {
@@ -108,22 +108,62 @@ __global__ __launch_bounds__(kThreads) void quantize_generic_kernel(
   block_flush_counts(q, ov1, ov2, sh_cnt);
 }
 
+// update_range on one slot from its total counters (dynamic_fixed_point.py:70-94).
+LBT_DEV void range_apply(int i, int c1, int c2, int32_t* exps, const int32_t* bits, const float* target,
+                         const float* nelem) {
+  const float r1 = (float)c1 / nelem[i];
+  const float r2 = (float)c2 / nelem[i];
+  const float t = target[i];
+  const int delta = r1 > t ? 1 : (r2 <= t ? -1 : 0);
+  int I = exps[i] + delta;
+  const int hi = bits[i] - 1, lo = bits[i] - 1 - kEMax;
+  I = I > hi ? hi : (I < lo ? lo : I);
+  exps[i] = I;
+}
+
+// Sum (and zero) the shards of slot i.
+LBT_DEV void shard_totals(int32_t* counts, int i, int& c1, int& c2) {
+  c1 = 0; c2 = 0;
+  int32_t* c = counts + (int64_t)i * LBT_NSHARD * LBT_CSTRIDE;
+  for (int k = 0; k < LBT_NSHARD; ++k) {
+    c1 += c[k * LBT_CSTRIDE];
+    c2 += c[k * LBT_CSTRIDE + 1];
+    c[k * LBT_CSTRIDE] = 0;
+    c[k * LBT_CSTRIDE + 1] = 0;
+  }
+}
+
 __global__ void range_update_kernel(int32_t* exps, int32_t* counts, const int32_t* bits,
                                     const float* target, const float* nelem, int nslots,
                                     uint64_t* step) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nslots && nelem[i] > 0.f) {  // slots not fed this step keep their exponent
-    int c1 = 0, c2 = 0;
-    int32_t* c = counts + (int64_t)i * LBT_NSHARD * 2;
-    for (int k = 0; k < LBT_NSHARD; ++k) { c1 += c[2 * k]; c2 += c[2 * k + 1]; c[2 * k] = 0; c[2 * k + 1] = 0; }
-    const float r1 = (float)c1 / nelem[i];
-    const float r2 = (float)c2 / nelem[i];
-    const float t = target[i];
-    const int delta = r1 > t ? 1 : (r2 <= t ? -1 : 0);
-    int I = exps[i] + delta;
-    const int hi = bits[i] - 1, lo = bits[i] - 1 - kEMax;
-    I = I > hi ? hi : (I < lo ? lo : I);
-    exps[i] = I;
+    int c1, c2;
+    shard_totals(counts, i, c1, c2);
+    range_apply(i, c1, c2, exps, bits, target, nelem);
+  }
+  if (i == 0) step[0] += 1ull;
+}
+
+__global__ void counts_fold_kernel(int32_t* counts, int nslots, float* folded) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  int c1, c2;
+  shard_totals(counts, i, c1, c2);
+  folded[4 * i + 0] = (float)(c1 >> 12);
+  folded[4 * i + 1] = (float)(c1 & 4095);
+  folded[4 * i + 2] = (float)(c2 >> 12);
+  folded[4 * i + 3] = (float)(c2 & 4095);
+}
+
+__global__ void range_update_folded_kernel(int32_t* exps, const float* folded, const int32_t* bits,
+                                           const float* target, const float* nelem, int nslots,
+                                           uint64_t* step) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nslots && nelem[i] > 0.f) {
+    const int c1 = (int)folded[4 * i + 0] * 4096 + (int)folded[4 * i + 1];
+    const int c2 = (int)folded[4 * i + 2] * 4096 + (int)folded[4 * i + 3];
+    range_apply(i, c1, c2, exps, bits, target, nelem);
   }
   if (i == 0) step[0] += 1ull;
 }
@@ -145,7 +185,7 @@ __global__ __launch_bounds__(kThreads) void quantize_weight_kernel(
   for (int k = threadIdx.x; k < K; k += kThreads) {
     const int tap = k / Cin, ci = k % Cin;
     const int64_t idx = (int64_t)k * Cout + co;  // HWIO flat index
-    const float u = q.stochastic ? noise1(idx % inner, q.qid, s.step, q.seed) : 0.f;
+    const float u = q.stochastic ? qnoise1(q, s.step, idx % inner) : 0.f;
     const int c = quant1(s, q.stochastic, w[idx], u, ov1, ov2);
     csum += c;
     if (w_hwio) w_hwio[idx] = (int8_t)c;
@@ -206,6 +246,22 @@ extern "C" int lbt_dfxp_range_update(int32_t* exps, int32_t* counts, const int32
   return (int)hipGetLastError();
 }
 
+extern "C" int lbt_dfxp_counts_fold(int32_t* counts, int32_t nslots, float* folded, void* stream) {
+  if (nslots <= 0) return LBT_OK;
+  hipLaunchKernelGGL(counts_fold_kernel, dim3((nslots + 255) / 256), dim3(256), 0, (hipStream_t)stream, counts,
+                     nslots, folded);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_dfxp_range_update_folded(int32_t* exps, const float* folded, const int32_t* bits,
+                                            const float* target, const float* nelem, int32_t nslots,
+                                            uint64_t* step, void* stream) {
+  const int blocks = nslots > 0 ? (nslots + 255) / 256 : 1;
+  hipLaunchKernelGGL(range_update_folded_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, exps, folded,
+                     bits, target, nelem, nslots, step);
+  return (int)hipGetLastError();
+}
+
 extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, int32_t Cin, int32_t Cout,
                                         lbt_qdesc q, int8_t* w_hwio, int8_t* wf, int32_t ksf, int8_t* wd,
                                         int32_t ksd, int32_t* colsum, void* stream) {
@@ -217,4 +273,4 @@ extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, 
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_abi_version(void) { return 1; }
+extern "C" int lbt_abi_version(void) { return 3; }

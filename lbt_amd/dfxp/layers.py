@@ -130,6 +130,10 @@ class Conv2d_q(Layer_q):
             s.append((self, "b", "db"))
         return s
 
+    def stem(self, d):
+        """int16 (9..12-bit) input codes and a small patch: the fp16-MFMA stem kernels."""
+        return self.x_kind == OUT_I16 and self.X_range.bits <= 12 and self.bits <= 8 and ops.stem_ok(d)
+
     def quantize_weights(self):
         ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio,
                             wf=self.wf if self.mfma else None, ksf=self.ksf,
@@ -148,6 +152,8 @@ class Conv2d_q(Layer_q):
         if self.x_mfma:
             ops.conv_fwd_i8(self.xq, self.x_kind == OUT_U8OFF, self.wf, self.ksf, self.wcolsum, d,
                             self.X_range.desc, self.W_range.desc, y=y)
+        elif self.stem(d):
+            ops.conv_stem_fwd(self.xq, self.w_hwio, d, self.X_range.desc, self.W_range.desc, y=y)
         else:
             ops.conv_fwd_generic(self.xq, self.x_kind == OUT_I16, self.w_hwio, d, self.X_range.desc,
                                  self.W_range.desc, y)
@@ -171,6 +177,10 @@ class Conv2d_q(Layer_q):
             ns = ops.wgrad_nsplit(d)
             slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
             ops.conv_wgrad_i8(self.xq, self.x_kind == OUT_U8OFF, self.gradq, d, slab, ns)
+        elif self.stem(d):
+            ns = ops.stem_nsplit(d)
+            slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
+            ops.conv_stem_wgrad(self.xq, self.gradq, d, slab, ns)
         else:
             ns = ops.wgrad_nsplit(d, generic=True)
             slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)

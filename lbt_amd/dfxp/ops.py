@@ -192,6 +192,29 @@ def conv_wgrad_generic(xq, x_i16, gq, d, slab, nsplit):
     call("lbt_conv_wgrad_generic", ptr(xq), int(x_i16), ptr(gq), d, ptr(slab), int(nsplit), stream())
 
 
+def stem_ok(d):
+    """The fp16-MFMA stem kernels take this conv (small patch, 16-multiple Cout)."""
+    K = d.KH * d.KW * d.Cin
+    return 0 < K <= 32 and d.Cout % 16 == 0 and 0 < d.Cout <= 64
+
+
+def stem_nsplit(d):
+    return -(-(d.N * d.Ho * d.Wo) // _lib.STEM_WG_PIXELS)
+
+
+def conv_stem_fwd(x16, w_hwio, d, qx, qw, y=None, yq=None, qout=None, ychsum=None):
+    M = d.N * d.Ho * d.Wo
+    nb = x16.numel() * 2 + (M * d.Cout * 4 if y is not None else 0) + (M * d.Cout if yq is not None else 0)
+    with _Timed("stem_fwd_kernel", nb):
+        call("lbt_conv_stem_fwd", ptr(x16), ptr(w_hwio), d, qx, qw, ptr(y), ptr(yq),
+             qout if qout is not None else NO_Q, ptr(ychsum), stream())
+
+
+def conv_stem_wgrad(x16, gq, d, slab, nsplit):
+    with _Timed("stem_wgrad_kernel", x16.numel() * 2 + gq.numel() + slab.numel() * 4):
+        call("lbt_conv_stem_wgrad", ptr(x16), ptr(gq), d, ptr(slab), int(nsplit), stream())
+
+
 # ----------------------------------------------------------------------------- BN chains
 def _chain_fwd_bytes(a):
     per = 0

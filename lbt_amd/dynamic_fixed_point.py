@@ -10,7 +10,7 @@ A range variable (the reference's int32 ``integer_bits`` tf.Variable) is a
 import torch
 
 from . import _lib
-from ._lib import NSHARD, OUT_F32, QDesc
+from ._lib import CSTRIDE, NSHARD, OUT_F32, QDesc
 from .dfxp import ops
 from .dfxp.layers import (AvgPool_q, BatchNorm_q, Conv2d_pq, Conv2d_q, Dense_q, Flatten_q, Layer_q,  # noqa: F401
                           Normalization_q, ReLU_q, Rescale_q, ResidualBlock_q, Sequential_q)
@@ -46,12 +46,12 @@ def _scratch_counts(X, bits, integer_bits):
     ctx = integer_bits.ctx
     X = X.contiguous()
     exps = ctx.exps[integer_bits.slot:integer_bits.slot + 1].clone()
-    counts = torch.zeros(NSHARD * 2, dtype=torch.int32, device=X.device)
+    counts = torch.zeros(NSHARD * CSTRIDE, dtype=torch.int32, device=X.device)
     d = QDesc(exps.data_ptr(), counts.data_ptr(), ctx.step.data_ptr(), ctx.seed, integer_bits.qid, 0, bits, 0)
     rows, inner = ops.rows_inner(tuple(X.shape))
     out = torch.empty_like(X)
     _lib.call("lbt_dfxp_quantize", _lib.ptr(X), _lib.ptr(out), OUT_F32, rows, inner, d, None, 0, _lib.stream())
-    c = counts.view(NSHARD, 2).sum(0).tolist()
+    c = counts.view(NSHARD, CSTRIDE)[:, :2].sum(0).tolist()
     return c[0], c[1], exps
 
 
@@ -68,7 +68,7 @@ def update_range(X, target_overflow_rate, bits, integer_bits):
     ctx = integer_bits.ctx
     X = X.contiguous()
     exps = ctx.exps[integer_bits.slot:integer_bits.slot + 1]
-    counts = torch.zeros(NSHARD * 2, dtype=torch.int32, device=X.device)
+    counts = torch.zeros(NSHARD * CSTRIDE, dtype=torch.int32, device=X.device)
     d = QDesc(exps.data_ptr(), counts.data_ptr(), ctx.step.data_ptr(), ctx.seed, integer_bits.qid, 0, bits, 0)
     rows, inner = ops.rows_inner(tuple(X.shape))
     out = torch.empty_like(X)

@@ -25,8 +25,8 @@ import os
 import torch
 
 from . import _lib
-from ._lib import NO_Q, OUT_I8, OUT_I16, OUT_U8OFF, BnNorm, BwdBranch, ChainBwdA, ChainBwdB, ChainFwd, PJob, QJob, \
-    RJob, WJob, call, ptr
+from ._lib import NO_Q, OUT_I8, OUT_I16, OUT_U8OFF, BnNorm, BwdBranch, ChainBwdA, ChainBwdB, ChainFwd, NJob, PJob, \
+    QJob, RJob, WJob, call, ptr
 from .dfxp import ops
 from .dfxp.layers import _Cache
 
@@ -174,19 +174,30 @@ class FusedResNet:
                     raise _lib.LbtError("%s failed with status %d" % (name, rc))
             return run
 
+        self._nd, njobs = {}, []
+
         def obs(q, n):
+            """Declare an activation / gradient quantiser's per-step element count and give it a
+            noise table (its inner = n / N noise values, refreshed by the step's first launch)."""
             q.observe(n)
+            if q.stochastic and q not in self._nd:
+                inner = n // N
+                tab = self._buf("noise:" + q.name, ((inner + 3) // 4 * 4,), torch.float32)
+                d = _lib.QDesc.from_buffer_copy(q.desc)
+                d.noise = tab.data_ptr()
+                self._nd[q] = d
+                njobs.append(NJob(ctx.step.data_ptr(), ctx.seed, q.qid, 0, inner, tab.data_ptr()))
 
         # ---- batched weight + gamma/beta quantisation (all layers, one launch each)
         wjobs = []
         for c in self.convs:
             kh, kw, ci, co = c.ksize
-            obs(c.W_range, c.W.numel())
+            c.W_range.observe(c.W.numel())
             wjobs.append(WJob(c.W.data_ptr(), kh, kw, ci, co, c.W_range.desc, c.w_hwio.data_ptr(),
                               c.wf.data_ptr() if c.mfma else None, c.ksf, c.wd.data_ptr() if c.mfma else None,
                               c.ksd, c.wcolsum.data_ptr() if c.mfma else None))
         d = self.dense
-        obs(d.W_range, d.W.numel())
+        d.W_range.observe(d.W.numel())
         wjobs.append(WJob(d.W.data_ptr(), d.in_units, 1, 1, d.units, d.W_range.desc, d.w_hwio.data_ptr(),
                           None, 0, None, 0, None))
         self._wjobs = _dev_array(wjobs, ctx.device)
@@ -195,8 +206,8 @@ class FusedResNet:
         qjobs = []
         for r in self.rescales:
             C = r.C
-            obs(r.g_range, C)
-            obs(r.b_range, C)
+            r.g_range.observe(C)
+            r.b_range.observe(C)
             qjobs.append(QJob(r.gamma.data_ptr(), r.gb.data_ptr(), _lib.OUT_F32, C, 1, r.g_range.desc))
             qjobs.append(QJob(r.beta.data_ptr(), r.gb.data_ptr() + 4 * C, _lib.OUT_F32, C, 1, r.b_range.desc))
         self._qjobs = _dev_array(qjobs, ctx.device)
@@ -209,26 +220,35 @@ class FusedResNet:
         c.d = dc
         ximg = self._buf("ximg", (N, H, W, Cin0), torch.int16)
         obs(c.X_range, X.numel())
-        fwd.append(L("lbt_dfxp_quantize", ptr(self._X), ptr(ximg), OUT_I16, N, H * W * Cin0, c.X_range.desc, None,
+        fwd.append(L("lbt_dfxp_quantize", ptr(self._X), ptr(ximg), OUT_I16, N, H * W * Cin0, self._qd(c.X_range), None,
                      0, k="quantize_rows_kernel", nb=X.numel() * 6))
-        y0 = self._buf("y0", (N, dc.Ho, dc.Wo, C0), torch.float32)
-        fwd.append(L("lbt_conv_fwd_generic", ptr(ximg), 1, ptr(c.w_hwio), dc, c.X_range.desc, c.W_range.desc,
-                     ptr(y0), k="conv_fwd_generic_kernel", nb=ximg.numel() * 2 + y0.numel() * 4))
         n0, r0 = self.n0, self.r0
-        qn0 = self._buf("qn0", y0.shape, torch.int8)
+        shp0 = (N, dc.Ho, dc.Wo, C0)
+        numel0 = math.prod(shp0)
+        qn0 = self._buf("qn0", shp0, torch.int8)
         chs0 = self._sums("chs0", ops.NSHARD * 2 * C0)
-        obs(n0.X_range, y0.numel())
-        fwd.append(L("lbt_dfxp_quantize", ptr(y0), ptr(qn0), OUT_I8, N, y0.numel() // N, n0.X_range.desc, ptr(chs0),
-                     C0, k="quantize_rows_kernel", nb=y0.numel() * 5))
-        R0 = self._buf("R0", y0.shape, torch.int8)
-        X0 = self._buf("X0", y0.shape, torch.float32)
+        obs(n0.X_range, numel0)
+        self._stem = c.stem(dc)
+        if self._stem:
+            # fp16-MFMA stem with the bn0-norm quantiser + channel sums in its epilogue
+            fwd.append(L("lbt_conv_stem_fwd", ptr(ximg), ptr(c.w_hwio), dc, self._qd(c.X_range), c.W_range.desc, None,
+                         ptr(qn0), self._qd(n0.X_range), ptr(chs0), k="stem_fwd_kernel",
+                         nb=ximg.numel() * 2 + c.w_hwio.numel() + numel0))
+        else:
+            y0 = self._buf("y0", shp0, torch.float32)
+            fwd.append(L("lbt_conv_fwd_generic", ptr(ximg), 1, ptr(c.w_hwio), dc, self._qd(c.X_range), c.W_range.desc,
+                         ptr(y0), k="conv_fwd_generic_kernel", nb=ximg.numel() * 2 + numel0 * 4))
+            fwd.append(L("lbt_dfxp_quantize", ptr(y0), ptr(qn0), OUT_I8, N, numel0 // N, self._qd(n0.X_range), ptr(chs0),
+                         C0, k="quantize_rows_kernel", nb=numel0 * 5))
+        R0 = self._buf("R0", shp0, torch.int8)
+        X0 = self._buf("X0", shp0, torch.float32)
         b0 = self.blocks[0]
-        xa = self._buf("xa0", y0.shape, torch.int8)
-        xs = self._buf("xs0", y0.shape, torch.int8) if b0.cs is not None else None
-        obs(r0.X_range, y0.numel())
-        obs(b0.c1.X_range, y0.numel())
+        xa = self._buf("xa0", shp0, torch.int8)
+        xs = self._buf("xs0", shp0, torch.int8) if b0.cs is not None else None
+        obs(r0.X_range, numel0)
+        obs(b0.c1.X_range, numel0)
         if xs is not None:
-            obs(b0.cs.X_range, y0.numel())
+            obs(b0.cs.X_range, numel0)
         a = self._chain_fwd(n0, qn0, chs0, r0, R0, None, None, None, None, None, relu=True, y=X0,
                             o1=xa, q1=b0.c1.X_range, o2=xs, q2=b0.cs.X_range if xs is not None else None)
         fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a)))
@@ -251,9 +271,9 @@ class FusedResNet:
         d.d = dd
         pq = self._buf("pq", (Nb, Ch), torch.int8)
         obs(d.X_range, pooled.numel())
-        fwd.append(L("lbt_dfxp_quantize", ptr(pooled), ptr(pq), OUT_I8, Nb, Ch, d.X_range.desc, None, 0))
+        fwd.append(L("lbt_dfxp_quantize", ptr(pooled), ptr(pq), OUT_I8, Nb, Ch, self._qd(d.X_range), None, 0))
         self.logits = self._buf("logits", (Nb, d.units), torch.float32)
-        fwd.append(L("lbt_conv_fwd_generic", ptr(pq), 0, ptr(d.w_hwio), dd, d.X_range.desc, d.W_range.desc,
+        fwd.append(L("lbt_conv_fwd_generic", ptr(pq), 0, ptr(d.w_hwio), dd, self._qd(d.X_range), d.W_range.desc,
                      ptr(self.logits)))
         self.loss = self._buf("loss", (1,), torch.float32)
         self.dlogits = self._buf("dz", (Nb, d.units), torch.float32)
@@ -262,16 +282,16 @@ class FusedResNet:
         rjobs, pjobs = [], []
         gqd = self._buf("gqd", (Nb, d.units), torch.int8)
         obs(d.grad_range, self.dlogits.numel())
-        bwd.append(L("lbt_dfxp_quantize", ptr(self.dlogits), ptr(gqd), OUT_I8, Nb, d.units, d.grad_range.desc, None,
+        bwd.append(L("lbt_dfxp_quantize", ptr(self.dlogits), ptr(gqd), OUT_I8, Nb, d.units, self._qd(d.grad_range), None,
                      0))
         nsd = ops.wgrad_nsplit(dd, generic=True)
         slabd = self._buf("slabd", (nsd, d.in_units, d.units), torch.int32)
         bwd.append(self._on_side(L("lbt_conv_wgrad_generic", ptr(pq), 0, ptr(gqd), dd, ptr(slabd), nsd,
                                    k="conv_wgrad_generic_kernel", nb=pq.numel() + gqd.numel() + 4 * slabd.numel())))
-        rjobs.append(RJob(slabd.data_ptr(), nsd, d.in_units, d.units, 0, None, d.X_range.desc, d.grad_range.desc,
+        rjobs.append(RJob(slabd.data_ptr(), nsd, d.in_units, d.units, 0, None, self._qd(d.X_range), self._qd(d.grad_range),
                           d.W.data_ptr(), ops.f32(2 * d.weight_decay), d.dW.data_ptr()))
         dpool = self._buf("dpool", (Nb, Ch), torch.float32)
-        bwd.append(L("lbt_conv_dgrad_generic", ptr(gqd), ptr(d.w_hwio), dd, d.grad_range.desc, d.W_range.desc,
+        bwd.append(L("lbt_conv_dgrad_generic", ptr(gqd), ptr(d.w_hwio), dd, self._qd(d.grad_range), d.W_range.desc,
                      ptr(dpool), None))
         gY = self._buf("gYlast", Ylast.shape, torch.float32)
         bwd.append(L("lbt_avgpool_bwd", ptr(dpool), ptr(gY), Nb, Hh * Wh, Ch))
@@ -279,24 +299,30 @@ class FusedResNet:
             gY = self._block_bwd(i, self.blocks[i], saved[i], gY, bwd, L, obs, rjobs, pjobs)
 
         # ---- stem backward (d loss / d image is never needed)
-        gq0 = self._buf("gq0", y0.shape, torch.int8)
-        Gn0 = self._buf("Gn0", y0.shape, torch.int8)
+        gq0 = self._buf("gq0", shp0, torch.int8)
+        Gn0 = self._buf("Gn0", shp0, torch.int8)
         sums0 = self._sums("sums0", ops.NSHARD * 4 * C0)
-        obs(r0.grad_range, y0.numel())
-        obs(n0.grad_range, y0.numel())
-        obs(c.grad_range, y0.numel())
-        aA = self._chain_bwd_a(gY, X0, False, None, (r0, R0, n0, qn0, Gn0, sums0), None, y0.shape, C0)
+        obs(r0.grad_range, numel0)
+        obs(n0.grad_range, numel0)
+        obs(c.grad_range, numel0)
+        aA = self._chain_bwd_a(gY, X0, False, None, (r0, R0, n0, qn0, Gn0, sums0), None, shp0, C0)
         bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
-        aB = self._chain_bwd_b(n0, Gn0, qn0, sums0, y0.shape, C0, gq0, c.grad_range, None)
+        aB = self._chain_bwd_b(n0, Gn0, qn0, sums0, shp0, C0, gq0, c.grad_range, None)
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB)))
         self._keep += [aA, aB]
-        ns0 = ops.wgrad_nsplit(dc, generic=True)
-        slab0 = self._buf("slab0", (ns0, kh * kw * Cin0, C0), torch.int32)
-        bwd.append(L("lbt_conv_wgrad_generic", ptr(ximg), 1, ptr(gq0), dc, ptr(slab0), ns0,
-                     k="conv_wgrad_generic_kernel", nb=2 * ximg.numel() + gq0.numel() + 4 * slab0.numel()))
-        rjobs.append(RJob(slab0.data_ptr(), ns0, kh * kw * Cin0, C0, 0, None, c.X_range.desc, c.grad_range.desc,
+        if self._stem:
+            ns0 = ops.stem_nsplit(dc)
+            slab0 = self._buf("slab0", (ns0, kh * kw * Cin0, C0), torch.int32)
+            bwd.append(L("lbt_conv_stem_wgrad", ptr(ximg), ptr(gq0), dc, ptr(slab0), ns0, k="stem_wgrad_kernel",
+                         nb=2 * ximg.numel() + gq0.numel() + 4 * slab0.numel()))
+        else:
+            ns0 = ops.wgrad_nsplit(dc, generic=True)
+            slab0 = self._buf("slab0", (ns0, kh * kw * Cin0, C0), torch.int32)
+            bwd.append(L("lbt_conv_wgrad_generic", ptr(ximg), 1, ptr(gq0), dc, ptr(slab0), ns0,
+                         k="conv_wgrad_generic_kernel", nb=2 * ximg.numel() + gq0.numel() + 4 * slab0.numel()))
+        rjobs.append(RJob(slab0.data_ptr(), ns0, kh * kw * Cin0, C0, 0, None, self._qd(c.X_range), self._qd(c.grad_range),
                           c.W.data_ptr(), ops.f32(2 * c.weight_decay), c.dW.data_ptr()))
-        pjobs.append(PJob(sums0.data_ptr(), C0, r0.grad_range.desc, r0.X_range.desc, r0.gamma.data_ptr(),
+        pjobs.append(PJob(sums0.data_ptr(), C0, self._qd(r0.grad_range), self._qd(r0.X_range), r0.gamma.data_ptr(),
                           ops.f32(2 * r0.weight_decay), r0.dgamma.data_ptr(), r0.dbeta.data_ptr()))
 
         # ---- batched reductions (after the side-stream weight gradients have landed)
@@ -307,11 +333,20 @@ class FusedResNet:
         bwd.append(L("lbt_conv_wgrad_reduce_many", ptr(self._rjobs), len(rjobs), maxb))
         self._pjobs = _dev_array(pjobs, ctx.device)
         bwd.append(L("lbt_bn_param_grads_many", ptr(self._pjobs), len(pjobs), max(j.C for j in pjobs)))
+        # ---- this step's noise tables: one launch ahead of everything else
+        self._njobs = _dev_array(njobs, ctx.device)
+        max_n = max(j.n for j in njobs)
+        fwd.insert(0, L("lbt_dfxp_noise_fill", ptr(self._njobs), len(njobs), max_n, k="noise_fill_kernel",
+                        nb=4 * sum(j.n for j in njobs)))
         self._fwd, self._bwd = fwd, bwd
+
+    def _qd(self, q):
+        """The plan's descriptor of quantiser q: with its noise table when it has one."""
+        return self._nd.get(q, q.desc)
 
     # ------------------------------------------------------------------ descriptor builders
     def _bn_norm(self, n, q, chsum, numel, C):
-        return BnNorm(q.data_ptr(), n.X_range.desc, chsum.data_ptr(), numel // C, ops.f32(n.eps),
+        return BnNorm(q.data_ptr(), self._qd(n.X_range), chsum.data_ptr(), numel // C, ops.f32(n.eps),
                       ops.f32(n.momentum), ops.f32(1 - n.momentum), n.ms.data_ptr(), n.X_mean_running.data_ptr(),
                       n.X_var_running.data_ptr())
 
@@ -320,22 +355,22 @@ class FusedResNet:
         C = qn.shape[-1]
         a = ChainFwd()
         a.b1.nrm = self._bn_norm(n, qn, chs, qn.numel(), C)
-        a.b1.qr = r.X_range.desc
+        a.b1.qr = self._qd(r.X_range)
         a.b1.rout = R.data_ptr()
         a.b1.gb = r.gb.data_ptr()
         if n2 is not None:
             a.has_b2 = 1
             a.b2.nrm = self._bn_norm(n2, qn2, chs2, qn2.numel(), C)
-            a.b2.qr = r2.X_range.desc
+            a.b2.qr = self._qd(r2.X_range)
             a.b2.rout = R2.data_ptr()
             a.b2.gb = r2.gb.data_ptr()
         a.res = res.data_ptr() if res is not None else None
         a.relu = 1 if relu else 0
         a.y = y.data_ptr() if y is not None else None
         if o1 is not None:
-            a.o1, a.o1_kind, a.qo1 = o1.data_ptr(), OUT_U8OFF, q1.desc
+            a.o1, a.o1_kind, a.qo1 = o1.data_ptr(), OUT_U8OFF, self._qd(q1)
         if o2 is not None:
-            a.o2, a.o2_kind, a.qo2 = o2.data_ptr(), OUT_U8OFF, q2.desc
+            a.o2, a.o2_kind, a.qo2 = o2.data_ptr(), OUT_U8OFF, self._qd(q2)
         a.rows, a.inner, a.C = qn.shape[0], qn.numel() // qn.shape[0], C
         return a
 
@@ -349,7 +384,7 @@ class FusedResNet:
             if br is None:
                 continue
             r, R, n, qn, G, sums = br
-            bb = BwdBranch(r.grad_range.desc, R.data_ptr(), r.X_range.desc, r.gb.data_ptr(), n.grad_range.desc,
+            bb = BwdBranch(self._qd(r.grad_range), R.data_ptr(), self._qd(r.X_range), r.gb.data_ptr(), self._qd(n.grad_range),
                            qn.data_ptr(), G.data_ptr(), None, sums.data_ptr())
             if slot == 0:
                 a.b1 = bb
@@ -362,8 +397,8 @@ class FusedResNet:
     def _chain_bwd_b(self, n, G, qn, sums, shape, C, gq, qo, gcol):
         rows = shape[0]
         inner = math.prod(shape[1:])
-        return ChainBwdB(G.data_ptr(), n.grad_range.desc, qn.data_ptr(), n.X_range.desc, n.ms.data_ptr(),
-                         sums.data_ptr(), rows * inner // C, None, gq.data_ptr(), qo.desc,
+        return ChainBwdB(G.data_ptr(), self._qd(n.grad_range), qn.data_ptr(), self._qd(n.X_range), n.ms.data_ptr(),
+                         sums.data_ptr(), rows * inner // C, None, gq.data_ptr(), self._qd(qo),
                          gcol.data_ptr() if gcol is not None else None, rows, inner, C)
 
     # ------------------------------------------------------------------ one residual block
@@ -381,8 +416,8 @@ class FusedResNet:
         qn1 = self._buf(k + "qn1", shp, torch.int8)
         chs1 = self._sums(k + "chs1", ops.NSHARD * 2 * C)
         obs(b.n1.X_range, numel)
-        fwd.append(L("lbt_conv_fwd_i8", ptr(xa), 1, ptr(c1.wf), c1.ksf, ptr(c1.wcolsum), d1, c1.X_range.desc,
-                     c1.W_range.desc, None, ptr(qn1), b.n1.X_range.desc, ptr(chs1), k="conv_gemm_kernel<0> (fwd)",
+        fwd.append(L("lbt_conv_fwd_i8", ptr(xa), 1, ptr(c1.wf), c1.ksf, ptr(c1.wcolsum), d1, self._qd(c1.X_range),
+                     c1.W_range.desc, None, ptr(qn1), self._qd(b.n1.X_range), ptr(chs1), k="conv_gemm_kernel<0> (fwd)",
                      nb=xa.numel() + c1.wf.numel() + qn1.numel()))
         R1 = self._buf(k + "R1", shp, torch.int8)
         xb = self._buf(k + "xb", shp, torch.int8)
@@ -394,8 +429,8 @@ class FusedResNet:
         qn2 = self._buf(k + "qn2", shp, torch.int8)
         chs2 = self._sums(k + "chs2", ops.NSHARD * 2 * C)
         obs(b.n2.X_range, numel)
-        fwd.append(L("lbt_conv_fwd_i8", ptr(xb), 1, ptr(c2.wf), c2.ksf, ptr(c2.wcolsum), d2, c2.X_range.desc,
-                     c2.W_range.desc, None, ptr(qn2), b.n2.X_range.desc, ptr(chs2), k="conv_gemm_kernel<0> (fwd)",
+        fwd.append(L("lbt_conv_fwd_i8", ptr(xb), 1, ptr(c2.wf), c2.ksf, ptr(c2.wcolsum), d2, self._qd(c2.X_range),
+                     c2.W_range.desc, None, ptr(qn2), self._qd(b.n2.X_range), ptr(chs2), k="conv_gemm_kernel<0> (fwd)",
                      nb=xb.numel() + c2.wf.numel() + qn2.numel()))
         ds = qns = chss = Rs = None
         if cs is not None:
@@ -404,8 +439,8 @@ class FusedResNet:
             qns = self._buf(k + "qns", shp, torch.int8)
             chss = self._sums(k + "chss", ops.NSHARD * 2 * C)
             obs(b.ns.X_range, numel)
-            fwd.append(L("lbt_conv_fwd_i8", ptr(xs), 1, ptr(cs.wf), cs.ksf, ptr(cs.wcolsum), ds, cs.X_range.desc,
-                         cs.W_range.desc, None, ptr(qns), b.ns.X_range.desc, ptr(chss), k="conv_gemm_kernel<0> (fwd)",
+            fwd.append(L("lbt_conv_fwd_i8", ptr(xs), 1, ptr(cs.wf), cs.ksf, ptr(cs.wcolsum), ds, self._qd(cs.X_range),
+                         cs.W_range.desc, None, ptr(qns), self._qd(b.ns.X_range), ptr(chss), k="conv_gemm_kernel<0> (fwd)",
                          nb=xs.numel() + cs.wf.numel() + qns.numel()))
             Rs = self._buf(k + "Rs", shp, torch.int8)
             obs(b.rs.X_range, numel)
@@ -468,13 +503,13 @@ class FusedResNet:
             bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aBs), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aBs)))
             keep.append(aBs)
         d1g = self._buf(k + "d1", shp, torch.float32)
-        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, c2.grad_range.desc, c2.W_range.desc,
+        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range), c2.W_range.desc,
                      ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=gq2.numel() + c2.wd.numel() + 4 * d1g.numel()))
         ns2 = ops.wgrad_nsplit(d2)
         slab2 = self._buf(k + "slab2", (ns2, 9 * C, C), torch.int32)
         bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), ns2,
                                    k="conv_wgrad_kernel", nb=f["xb"].numel() + gq2.numel() + 4 * slab2.numel())))
-        rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), c2.X_range.desc, c2.grad_range.desc,
+        rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), self._qd(c2.X_range), self._qd(c2.grad_range),
                           c2.W.data_ptr(), ops.f32(2 * c2.weight_decay), c2.dW.data_ptr()))
         Gn1 = self._buf(k + "Gn1", shp, torch.int8)
         sums1 = self._sums(k + "sums1", ops.NSHARD * 4 * C)
@@ -489,28 +524,28 @@ class FusedResNet:
         add = gm
         if cs is not None:
             dsg = self._buf(k + "dsc", f["Xin"].shape, torch.float32)
-            bwd.append(L("lbt_conv_dgrad_i8", ptr(gqs), ptr(cs.wd), cs.ksd, ds, cs.grad_range.desc,
+            bwd.append(L("lbt_conv_dgrad_i8", ptr(gqs), ptr(cs.wd), cs.ksd, ds, self._qd(cs.grad_range),
                          cs.W_range.desc, ptr(dsg), None, k="conv_gemm_kernel<1> (dgrad)",
                          nb=gqs.numel() + cs.wd.numel() + 4 * dsg.numel()))
             add = dsg
-        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, c1.grad_range.desc, c1.W_range.desc,
+        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range), c1.W_range.desc,
                      ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=gq1.numel() + c1.wd.numel() + 8 * gin.numel()))
         ns1 = ops.wgrad_nsplit(d1)
         slab1 = self._buf(k + "slab1", (ns1, 9 * Cin, C), torch.int32)
         bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), ns1,
                                    k="conv_wgrad_kernel", nb=f["xa"].numel() + gq1.numel() + 4 * slab1.numel())))
-        rjobs.append(RJob(slab1.data_ptr(), ns1, 9 * Cin, C, 1, gcol1.data_ptr(), c1.X_range.desc,
-                          c1.grad_range.desc, c1.W.data_ptr(), ops.f32(2 * c1.weight_decay), c1.dW.data_ptr()))
+        rjobs.append(RJob(slab1.data_ptr(), ns1, 9 * Cin, C, 1, gcol1.data_ptr(), self._qd(c1.X_range),
+                          self._qd(c1.grad_range), c1.W.data_ptr(), ops.f32(2 * c1.weight_decay), c1.dW.data_ptr()))
         if cs is not None:
             nss = ops.wgrad_nsplit(ds)
             slabs = self._buf(k + "slabs", (nss, Cin, C), torch.int32)
             bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xs"]), 1, ptr(gqs), ds, ptr(slabs), nss,
                                        k="conv_wgrad_kernel", nb=f["xs"].numel() + gqs.numel() + 4 * slabs.numel())))
-            rjobs.append(RJob(slabs.data_ptr(), nss, Cin, C, 1, gcols.data_ptr(), cs.X_range.desc,
-                              cs.grad_range.desc, cs.W.data_ptr(), ops.f32(2 * cs.weight_decay), cs.dW.data_ptr()))
+            rjobs.append(RJob(slabs.data_ptr(), nss, Cin, C, 1, gcols.data_ptr(), self._qd(cs.X_range),
+                              self._qd(cs.grad_range), cs.W.data_ptr(), ops.f32(2 * cs.weight_decay), cs.dW.data_ptr()))
         for r in (b.r1, b.r2) + ((b.rs,) if cs is not None else ()):
             sm = {id(b.r1): sums1, id(b.r2): sums2}.get(id(r), sumss)
-            pjobs.append(PJob(sm.data_ptr(), C, r.grad_range.desc, r.X_range.desc, r.gamma.data_ptr(),
+            pjobs.append(PJob(sm.data_ptr(), C, self._qd(r.grad_range), self._qd(r.X_range), r.gamma.data_ptr(),
                               ops.f32(2 * r.weight_decay), r.dgamma.data_ptr(), r.dbeta.data_ptr()))
         self._keep += keep
         return gin

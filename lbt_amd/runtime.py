@@ -8,7 +8,8 @@ In the reference every quantised tensor has an int32 TF variable ``<layer>/<X|W|
 
 Here one ``DfxpContext`` owns, in device memory,
   exps   int32 [capacity]                 I per quantiser slot
-  counts int32 [capacity, NSHARD, 2]      overflow counters accumulated by the kernels
+  counts int32 [capacity, NSHARD, CSTRIDE] overflow counters accumulated by the kernels
+                                         (2 used per shard; one cache line per shard)
   step   int64 [1]                        noise counter (incremented by every range update)
   bits / target / nelem                   per-slot controller constants
 and ``update_range_op()`` is the collection: ONE kernel that applies update_range to every
@@ -20,7 +21,7 @@ import zlib
 import torch
 
 from . import _lib
-from ._lib import NSHARD, QDesc
+from ._lib import CSTRIDE, NSHARD, QDesc
 
 
 def qid_of(name):
@@ -74,7 +75,7 @@ class DfxpContext:
         self.world_size = int(world_size)
         dev = self.device
         self.exps = torch.zeros(capacity, dtype=torch.int32, device=dev)
-        self.counts = torch.zeros(capacity * NSHARD * 2, dtype=torch.int32, device=dev)
+        self.counts = torch.zeros(capacity * NSHARD * CSTRIDE, dtype=torch.int32, device=dev)
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
         self.bits = torch.zeros(capacity, dtype=torch.int32, device=dev)
         self.target = torch.zeros(capacity, dtype=torch.float32, device=dev)
@@ -125,8 +126,20 @@ class DfxpContext:
         _lib.call("lbt_dfxp_range_update", _lib.ptr(self.exps), _lib.ptr(self.counts), _lib.ptr(self.bits),
                   _lib.ptr(self.target), _lib.ptr(self.nelem), n, _lib.ptr(self.step), _lib.stream())
 
+    def update_range_folded_op(self, folded):
+        """Data-parallel variant: the range update from all-reduced folded totals (see fold_counts)."""
+        n = len(self.quantizers)
+        _lib.call("lbt_dfxp_range_update_folded", _lib.ptr(self.exps), _lib.ptr(folded), _lib.ptr(self.bits),
+                  _lib.ptr(self.target), _lib.ptr(self.nelem), n, _lib.ptr(self.step), _lib.stream())
+
+    def fold_counts(self, folded):
+        """Sum + zero every slot's counter shards into folded[4*slot ..] (exact fp32 hi/lo pairs)."""
+        _lib.call("lbt_dfxp_counts_fold", _lib.ptr(self.counts), len(self.quantizers), _lib.ptr(folded),
+                  _lib.stream())
+
     def counts_view(self):
-        return self.counts.view(self.capacity, NSHARD, 2)[: len(self.quantizers)]
+        """[slots, NSHARD, 2] view of the live counters."""
+        return self.counts.view(self.capacity, NSHARD, CSTRIDE)[: len(self.quantizers), :, :2]
 
     def ranges(self):
         """{range variable name: I} (host read -- not for the timed loop)."""

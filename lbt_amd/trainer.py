@@ -11,29 +11,29 @@ MI355X-native execution:
   and replayed: ~300 kernel launches become one graph launch;
 * data parallelism (``torch.distributed``, backend ``nccl`` = RCCL over xGMI): each rank runs
   the step on its own batch shard; between the backward graph and the update graph ONE
-  all-reduce sums the flat gradient buffer and, in the same call, the quantisers' overflow
-  counters (packed as fp32), so every rank applies identical updates and identical DFXP
+  all-reduce sums the flat gradient buffer (which is the head of the comm buffer) and, in the
+  same call, the quantisers' overflow counters (folded into the tail as exact fp32 pairs by the
+  last kernel of the backward graph), so every rank applies identical updates and identical DFXP
   exponents. Noise keys (seed, step, quantiser) do not depend on the rank.
 """
 import torch
 import torch.distributed as dist
 
 from . import distributed as D
-from ._lib import NSHARD
 from .dfxp import ops
 
 
 class FlatParams:
     """Bind every (var, grad) of a model into contiguous flat buffers (grads_and_vars order)."""
 
-    def __init__(self, model):
+    def __init__(self, model, grad_buffer=None):
         slots = model.param_slots()
         dev = model.ctx.device
         sizes = [getattr(o, v).numel() for o, v, _ in slots]
         n = sum(sizes)
         self.n = n
         self.w = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.g = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.g = grad_buffer[:n] if grad_buffer is not None else torch.zeros(n, dtype=torch.float32, device=dev)
         self.a = torch.zeros(n, dtype=torch.float32, device=dev)
         off = 0
         self.offsets = []
@@ -64,16 +64,16 @@ class Trainer:
         if self.world != self.ctx.world_size:
             raise ValueError("DfxpContext.world_size (%d) must equal the process-group size (%d)"
                              % (self.ctx.world_size, self.world))
-        self.flat = FlatParams(model)
+        # fp32 comm buffer [grads | folded overflow counters] -> ONE in-place all-reduce per step
+        self.comm = None
+        if self.world > 1:
+            n = sum(getattr(o, v).numel() for o, v, _ in model.param_slots())
+            self.comm = D.make_comm_buffer(n, len(self.ctx.quantizers), self.ctx.device)
+        self.flat = FlatParams(model, self.comm)
         self.ctx.sums_managed = True
         self.global_step = 0
         self._graphs = None
         self._static = None
-        # fp32 comm buffer: [grads | overflow counters] -> ONE all-reduce per step
-        nq = len(self.ctx.quantizers)
-        self._ncnt = nq * NSHARD * 2
-        if self.world > 1:
-            self.comm = D.make_comm_buffer(self.flat.n, self._ncnt, self.ctx.device)
         if logger is not None:
             logger.info("Model info:\n" + model.info())
 
@@ -94,14 +94,19 @@ class Trainer:
         m.forward(X)
         m.compute_loss(y)
         m.backward()
+        if self.comm is not None:
+            self.ctx.fold_counts(self.comm[self.flat.n:])
 
     def _exchange(self):
         """Sum grads + overflow counters across ranks (one RCCL all-reduce; lbt_amd/distributed.py)."""
-        D.allreduce_grads_and_counts(self.flat.g, self.ctx.counts[: self._ncnt], self.comm, self.pg)
+        D.allreduce_comm(self.comm, self.pg)
 
     def _update(self):
         ops.sgd_momentum(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0 / self.world)
-        self.ctx.update_range_op()
+        if self.comm is not None:
+            self.ctx.update_range_folded_op(self.comm[self.flat.n:])
+        else:
+            self.ctx.update_range_op()
 
     def _eager(self, X, y):
         self._fwd_bwd(X, y)

@@ -1,5 +1,5 @@
-"""Data-parallel path on CPU: world_size-2 gloo processes run the REAL exchange function of the
-trainer (lbt_amd.distributed) on oracle gradients / overflow counters of their batch shards."""
+"""Data-parallel path on CPU: world_size-2 gloo processes run the REAL exchange of the trainer
+(lbt_amd.distributed: one all-reduce of [grads | folded counters]) on oracle gradients / overflow counters of their batch shards."""
 import os
 import socket
 
@@ -49,8 +49,19 @@ def _worker(rank, world, port, out_q):
         qn = sorted(ctx.counts)
         counts = torch.tensor([c for k in qn for c in ctx.counts[k][:2]], dtype=torch.int32)
         local = (flat.clone(), counts.clone())
-        comm = D.make_comm_buffer(flat.numel(), counts.numel(), "cpu")
-        D.allreduce_grads_and_counts(flat, counts, comm)
+        # the trainer's layout: grads are the comm head, folded counters the tail
+        comm = D.make_comm_buffer(flat.numel(), len(qn), "cpu")
+        n = flat.numel()
+        comm[:n].copy_(flat)
+        comm[n:].copy_(D.fold_host(counts))
+        # large counters (2**30-element tensors overflowing) must also survive exactly
+        big = torch.tensor([[2 ** 29 + 12345 + rank, 2 ** 28 + 4095]], dtype=torch.int64)
+        bigc = D.fold_host(big)
+        D.allreduce_comm(comm)
+        D.allreduce_comm(bigc)
+        flat = comm[:n]
+        counts = D.unfold_host(comm[n:]).view(-1).to(torch.int32)
+        assert D.unfold_host(bigc).tolist() == [[2 ** 30 + 24690 + 1, 2 ** 29 + 8190]]
         c = counts.view(-1, 2).tolist()
         new_I = {k: dfxp.update_range_from_counts(c[i][0], c[i][1], ctx.counts[k][2] * world, 0.0,
                                                   ctx.counts[k][3], ranges[k]) for i, k in enumerate(qn)}

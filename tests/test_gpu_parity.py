@@ -77,6 +77,58 @@ def test_quantize_channel_sums_and_range_update():
     assert int(ctx.counts.abs().sum().item()) == 0
 
 
+def test_counts_fold_and_folded_range_update():
+    """The data-parallel controller path (fold -> [all-reduce] -> folded update) equals the
+    sharded one; large counters survive the fp32 fold exactly."""
+    from lbt_amd import distributed as Dd
+    rng = np.random.default_rng(31)
+    xs = [rng.normal(0, s, size=(64, 16, 16, 16)).astype(np.float32) for s in (0.5, 3.0, 40.0)]
+    ref_ranges, folded_all = [], []
+    for mode in ("sharded", "folded"):
+        ctx = DfxpContext(seed=5)
+        qs = [ctx.quantizer("s%d/X_range" % i, 8, 2) for i in range(3)]
+        for x, q in zip(xs, qs):
+            ops.quantize(torch.from_numpy(x).to(DEV), q, OUT_I8)
+        if mode == "sharded":
+            ctx.update_range_op()
+            ref_ranges = ctx.ranges()
+        else:
+            folded = torch.full((4 * 3,), -1.0, device=DEV)
+            ctx.fold_counts(folded)
+            assert int(ctx.counts.abs().sum().item()) == 0
+            got = Dd.unfold_host(folded.cpu()).tolist()
+            assert got == [list(odfxp.overflow_counts(x, 8, 2)) for x in xs]
+            ctx.update_range_folded_op(folded)
+            assert ctx.ranges() == ref_ranges
+            assert int(ctx.step.item()) == 1
+    big = torch.tensor([[2 ** 30 + 777, 5]], dtype=torch.int64)
+    f = Dd.fold_host(big).to(DEV)
+    ctx = DfxpContext(seed=5)
+    ctx.quantizer("big/X_range", 8, 2)
+    ctx.nelem[0] = 2.0 ** 31
+    ctx.update_range_folded_op(f)
+    # r1 = (2^30+777)/2^31 > 0 -> I + 1
+    assert ctx.ranges() == {"big/X_range": 3}
+
+
+def test_division_by_reused_divisor_is_bitexact():
+    """The BN kernels divide by sigma with the divisor-only part of the division hoisted
+    (div_by / recip); it must equal '/' in every bit over the ranges the BN moments take."""
+    from lbt_amd import _lib
+    g = torch.Generator(device=DEV).manual_seed(0)
+    n = 1 << 24
+    y = torch.exp2(torch.empty(n, device=DEV).uniform_(-8, 12, generator=g))     # sigma = sqrt(var + eps)
+    y = torch.where(torch.arange(n, device=DEV) % 7 == 0, y.view(torch.int32).bitwise_or(0x7FFFFF).view(torch.float32), y)
+    x = torch.empty(n, device=DEV).uniform_(-1, 1, generator=g) * torch.exp2(torch.empty(n, device=DEV).uniform_(-40, 12,
+                                                                                                          generator=g))
+    x[::11] = 0.0
+    x[3::17] = -0.0
+    x[5::13] = torch.round(x[5::13] * 256) / 256                               # code-valued numerators (and -0)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    _lib.call("lbt_selftest_div", _lib.ptr(x), _lib.ptr(y), n, _lib.ptr(bad), None, None, _lib.stream())
+    assert int(bad.item()) == 0
+
+
 def test_tf_face_functions():
     rng = np.random.default_rng(4)
     x = rng.normal(0, 2, size=(16, 5, 5, 4)).astype(np.float32)
@@ -125,7 +177,10 @@ CONV_CASES = [
     (8, 16, 32, 32, 3, 1, True),
     (8, 16, 32, 64, 3, 2, True),
     (8, 8, 64, 64, 3, 1, True),      # stage-3 block conv
-    (8, 32, 3, 16, 3, 1, False),     # conv1: signed 9-bit image, VALU path
+    (8, 32, 3, 16, 3, 1, False),     # conv1: signed 9-bit image, fp16-MFMA stem path
+    (128, 32, 3, 16, 3, 1, False),   # conv1 at the bench size
+    (5, 7, 3, 32, 3, 2, False),      # stem: odd size, stride 2, two column tiles
+    (3, 6, 2, 64, 3, 1, False),      # stem: K = 18, Cout = 64
     (4, 12, 16, 16, 3, 1, False),    # signed 9-bit input on a 16-channel conv -> VALU path
     (4, 9, 32, 16, 3, 2, True),      # odd spatial size
     (128, 32, 16, 16, 3, 1, True),   # full ResNet-20 stage-1 size (B=128)
@@ -155,6 +210,38 @@ def test_conv_layer_bitexact(N, H, Cin, Cout, k, s, nonneg):
     assert np.array_equal(dx.cpu().numpy(), dxr)
     ctx.update_range_op()
     assert ctx.ranges() == octx.new_ranges()
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,s", [(8, 32, 3, 16, 1), (5, 9, 3, 32, 2), (2, 5, 1, 16, 1),
+                                             (4, 8, 3, 64, 1), (4, 8, 3, 128, 1)])
+def test_stem_kernels_equal_integer_gemm(N, H, Cin, Cout, s):
+    """fp16-MFMA stem fwd / wgrad at the extreme codes of its contract (|x| <= 2048, int8 w / g)
+    equal the exact integer convolution (int64 numpy) and the generic VALU kernels."""
+    rng = np.random.default_rng(N + H + Cin + Cout)
+    x = rng.integers(-2048, 2048, size=(N, H, H, Cin)).astype(np.int16)
+    x.flat[:7] = -2048
+    w = rng.integers(-128, 128, size=(3, 3, Cin, Cout)).astype(np.int8)
+    w.flat[:5] = -128
+    d = ops.conv_desc(N, H, H, Cin, Cout, 3, 3, s, s, "SAME")
+    ctx = DfxpContext(seed=1)
+    qx = ctx.quantizer("x/X_range", 12, 2)
+    qw = ctx.quantizer("x/W_range", 8, 1)
+    xt, wt = torch.from_numpy(x).to(DEV), torch.from_numpy(w).to(DEV)
+    y_ref = onn.scale_int(onn.conv_fwd_int(x, w, (s, s), "SAME"), (12 - 2 - 1) + (8 - 1 - 1))
+    y = torch.empty((N, d.Ho, d.Wo, Cout), dtype=torch.float32, device=DEV)
+    ops.conv_stem_fwd(xt, wt, d, qx.desc, qw.desc, y=y)
+    assert np.array_equal(y.cpu().numpy(), y_ref)
+    if Cout <= 64:
+        y2 = torch.empty_like(y)
+        ops.conv_fwd_generic(xt, 1, wt, d, qx.desc, qw.desc, y2)
+        assert torch.equal(y, y2)
+        g = rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout)).astype(np.int8)
+        g.flat[:3] = -128
+        ns = ops.stem_nsplit(d)
+        slab = torch.full((ns, 9 * Cin, Cout), 7, dtype=torch.int32, device=DEV)
+        ops.conv_stem_wgrad(xt, torch.from_numpy(g).to(DEV), d, slab, ns)
+        dw_ref = onn.conv_wgrad_int(x, g, (s, s), "SAME", (3, 3))
+        assert np.array_equal(slab.cpu().numpy().astype(np.int64).sum(0), dw_ref.reshape(9 * Cin, Cout))
 
 
 def test_dense_layer_bitexact():
