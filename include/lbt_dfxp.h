@@ -114,7 +114,8 @@ typedef struct lbt_njob {
   int64_t n;
   float* out;
 } lbt_njob;
-int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t max_n, void* stream);
+int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t max_n, int64_t* zero, int64_t nzero,
+                        void* stream);  /* also zeroes zero[0, nzero) (the step's sums arena) */
 
 /* Quantise a conv / dense weight (HWIO fp32, noise over shape[1:] = [KW,Cin,Cout]) into the
  * layouts the GEMM kernels consume (any output may be NULL):
@@ -132,7 +133,8 @@ int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, int32_t Cin
  * int8 implicit GEMM on v_mfma_i32_16x16x64_i8.  xq: NHWC int8 codes (x_u8off: unsigned
  * 9-bit offset encoding, else signed 8-bit); wf/wcolsum from lbt_dfxp_quantize_weight.
  * Epilogue: acc -> fp32 * 2^-(ex+ew); written to y (fp32 NHWC) if y != NULL and/or
- * quantised with qout into yq (int8 NHWC) with per-channel sums into ychsum.
+ * quantised with qout into yq (int8 NHWC) with per-channel sums into ychsum; a stochastic
+ * qout must carry its noise table (qout.noise, lbt_dfxp_noise_fill), else LBT_EINVAL.
  * Requires Cin % 16 == 0 and Cout % 16 == 0.                                               */
 int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf,
                     const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw,
@@ -173,13 +175,16 @@ int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_
  * integer and every partial sum < 2^24), i.e. bit-identical to lbt_conv_fwd_generic /
  * lbt_conv_wgrad_generic (dynamic_fixed_point.py:287-305).
  * fwd: exactly one of y (fp32, Cout <= 128) / yq (int8 codes of qout, + counters, + optional
- *      sharded channel sums ychsum, as lbt_conv_fwd_i8) is non-NULL.
- * wgrad: int32 partials slab[nsplit][K][Cout] with nsplit = ceil(N*Ho*Wo / LBT_STEM_WG_PIXELS),
- *      Cout <= 64; finish with lbt_conv_wgrad_reduce(_many) (x_u8off = 0, gcolsum = NULL).   */
+ *      sharded channel sums ychsum; a stochastic qout needs its noise table, as
+ *      lbt_conv_fwd_i8) is non-NULL.
+ * wgrad: ADDS exact int32 partials into slab[nshard][K][Cout] (zeroed by the caller; workgroup w of
+ *      LBT_STEM_WG_PIXELS pixels adds into shard w % nshard), Cout <= 64; requires
+ *      ceil(ceil(N*Ho*Wo / LBT_STEM_WG_PIXELS) / nshard) <= 31 (int32 exactness). Finish with
+ *      lbt_conv_wgrad_reduce(_many) over nsplit = nshard (x_u8off = 0, gcolsum = NULL).    */
 #define LBT_STEM_WG_PIXELS 256
 int lbt_conv_stem_fwd(const int16_t* x, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw,
                       float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream);
-int lbt_conv_stem_wgrad(const int16_t* x, const int8_t* gq, lbt_conv_desc d, int32_t* slab, int32_t nsplit,
+int lbt_conv_stem_wgrad(const int16_t* x, const int8_t* gq, lbt_conv_desc d, int32_t* slab, int32_t nshard,
                         void* stream);
 
 /* ---------------------------------------------------------------- batch norm -------- */

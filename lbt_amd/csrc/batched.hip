@@ -68,19 +68,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* 
   const int64_t i = (int64_t)blockIdx.x * 32 + lo;
   long long s = 0;
   if (i < total) {
-#pragma unroll 4
+#pragma unroll 8
     for (int b = sg; b < j.nsplit; b += 8) s += j.slab[(int64_t)b * total + i];
+    if (j.x_u8off && j.gcolsum) {  // offset correction 128 * sum_p g: shards split over the groups
+      const int co = (int)(i % j.Cout);
+      long long cs = 0;
+#pragma unroll
+      for (int k = sg; k < LBT_NSHARD; k += 8) cs += j.gcolsum[(int64_t)k * 2 * j.Cout + co];
+      s += 128ll * cs;
+    }
   }
   red[sg][lo] = s;
   __syncthreads();
   if (sg != 0 || i >= total) return;
   for (int k = 1; k < 8; ++k) s += red[k][lo];
-  if (j.x_u8off && j.gcolsum) {
-    const int co = (int)(i % j.Cout);
-    long long cs = 0;
-    for (int k = 0; k < LBT_NSHARD; ++k) cs += j.gcolsum[(int64_t)k * 2 * j.Cout + co];
-    s += 128ll * cs;
-  }
   const float scale = ldexpf(1.0f, -(frac_exp(j.qx) + frac_exp(j.qg)));
   const float a = (float)s * scale;
   const float b = j.wd2 * j.w[i];
@@ -104,9 +105,20 @@ __global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
 }
 
 // grid (blocks, njobs): thread -> noise block b (4 values, one Philox call)
-__global__ __launch_bounds__(kThreads) void noise_fill_kernel(const lbt_njob* __restrict__ jobs) {
-  const lbt_njob j = jobs[blockIdx.y];
+__global__ __launch_bounds__(kThreads) void noise_fill_kernel(const lbt_njob* __restrict__ jobs, int64_t* zero,
+                                                             int64_t nzero) {
   const int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (blockIdx.y == 0) {  // the first job row also clears the sums arena (4 x int64 per thread)
+    for (int64_t z = 4 * b; z < nzero; z += 4 * (int64_t)gridDim.x * kThreads) {
+      if (z + 4 <= nzero) {
+        *reinterpret_cast<longlong2*>(zero + z) = make_longlong2(0, 0);
+        *reinterpret_cast<longlong2*>(zero + z + 2) = make_longlong2(0, 0);
+      } else {
+        for (int64_t t = z; t < nzero; ++t) zero[t] = 0;
+      }
+    }
+  }
+  const lbt_njob j = jobs[blockIdx.y];
   if (4 * b >= j.n) return;
   const uint64_t step = *j.step;
   const Noise4 n = noise4((uint64_t)b, j.qid, step, j.seed);
@@ -115,11 +127,14 @@ __global__ __launch_bounds__(kThreads) void noise_fill_kernel(const lbt_njob* __
 
 }  // namespace
 
-extern "C" int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t max_n, void* stream) {
+extern "C" int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t max_n, int64_t* zero, int64_t nzero,
+                                   void* stream) {
   if (njobs <= 0 || max_n <= 0) return LBT_OK;
+  if (nzero > 0 && (reinterpret_cast<uintptr_t>(zero) % 16)) return LBT_EINVAL;
   const int64_t blocks = (max_n + 4 * kThreads - 1) / (4 * kThreads);
   if (njobs > 65535 || blocks > 0x7fffffff) return LBT_EINVAL;
-  hipLaunchKernelGGL(noise_fill_kernel, dim3((unsigned)blocks, njobs), dim3(kThreads), 0, (hipStream_t)stream, jobs);
+  hipLaunchKernelGGL(noise_fill_kernel, dim3((unsigned)blocks, njobs), dim3(kThreads), 0, (hipStream_t)stream, jobs,
+                     zero, nzero > 0 ? nzero : 0);
   return (int)hipGetLastError();
 }
 

@@ -1,13 +1,16 @@
 // conv_epilogue.h -- the quantising epilogue shared by the int8 MFMA convolutions and the
 // fp16-MFMA stem convolution: the Normalization_q input quantiser (dynamic_fixed_point.py:
-// 575-590 -> :26-38) fused into the producing GEMM.
+// 575-590 -> :26-38) fused into the producing GEMM, working directly on the accumulator layout.
 //
-// Each wave has written its 16 x (16*ntw) fp32 output tile into its own LDS tile; the tile is
-// re-read so that each lane owns 4 CONSECUTIVE channels of one row: one Philox call per 4
-// outputs (its 4 noise indices share a Philox block), char4 stores, and exact per-channel sums
-// (S1 = sum q, S2 = sum q^2) reduced across the lanes sharing a channel quad, then LDS, then
-// one shard of the global sums; overflow counters likewise.  Noise index of output (row, col)
-// = (row mod Ho*Wo) * ncol + col: the reference's noise over X.shape[1:].
+// Block = 4 waves; the GEMM's NT 16-column tiles are spread over WPM = min(NT, 4) waves (NTW
+// tiles each) and a block covers MTB = 4 / WPM 16-row tiles.  In a 16x16 MFMA accumulator lane l
+// holds column l&15 of rows 4*(l>>4) + i, i < 4, so each lane quantises 4 * NTW outputs of ONE
+// column per tile: noise u[(row mod Ho*Wo) * ncol + col] (the reference's noise over
+// X.shape[1:]) comes from the quantiser's per-step table and is PREFETCHED with the GEMM
+// operands; the exact per-channel sums (S1 = sum q, S2 = sum q^2) reduce in registers (rows of
+// the lane, then xor-16 / xor-32 across the lanes of the column), each wave parks its column
+// totals in LDS with plain stores, and ONE barrier later every counter and channel sum of the
+// block is published with one atomic per (channel, sum) into the block's shard.
 #pragma once
 #include "dfxp_device.h"
 
@@ -17,76 +20,101 @@ struct QOut {
   int8_t* yq;       // [M][ncol] int8 codes
   lbt_qdesc q;
   int64_t* chsum;   // sharded [LBT_NSHARD][2*ncol] or NULL
-  int64_t M;
+  int64_t M;        // < 2^31
   int ncol;
   int64_t HWo;
 };
 
-// Make this wave's LDS tile writes visible to the wave (the tile is wave-private).
-LBT_DEV void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+template <int NT>
+struct EpiGeom {
+  static constexpr int WPM = NT < 4 ? NT : 4;  // waves per 16-row tile
+  static constexpr int NTW = NT / WPM;         // 16-column tiles per wave
+  static constexpr int MTB = 4 / WPM;          // 16-row tiles per block
+};
+
+// LDS a block needs for the epilogue
+template <int NT>
+struct EpiShared {
+  int cnt[2 * 4];                          // counters staged per wave
+  int part[4][2][16 * EpiGeom<NT>::NTW];   // per wave: S1 / S2 of its columns
+};
+
+// Noise of this lane's outputs (rows mtile*16 + 4*kg + i, columns (nt0 + j)*16 + r), from the
+// quantiser's per-step table (a stochastic quantising epilogue requires one: see the header).
+template <int NTW>
+LBT_DEV void epi_noise(const QOut& o, int64_t mtile, int nt0, int lane, float (&u)[NTW][4]) {
+  const int r = lane & 15, kg = lane >> 4;
+  const bool tab = o.q.stochastic && o.q.noise;   // else quant1 ignores u: read zeros
+  const float* src = tab ? o.q.noise : zf();
+  const uint32_t mask = tab ? 0xffffffffu : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = mtile * 16 + 4 * kg + i;
+    const uint32_t pix = (uint32_t)(row < o.M ? row : 0) % (uint32_t)o.HWo;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) u[j][i] = src[(pix * (uint32_t)o.ncol + (nt0 + j) * 16 + r) & mask];
+  }
 }
 
-// Every thread of the block calls it. sh_sum (2*ncol long long) must have been zeroed and the
-// zeroing made visible (barrier) before any wave got here; sh_cnt holds 2 ints per wave.
-LBT_DEV void quant_epilogue(const QOut& o, float (*tile)[33], bool wave_live, int64_t mtile, int nt0, int ntw,
-                            long long* sh_sum, int* sh_cnt) {
-  const int lane = threadIdx.x & 63;
-  const QState qs = qstate(o.q);
-  const bool want_sum = o.chsum != nullptr;
+// Quantise + store + publish. v holds the fp32 outputs (acc * scale) of this lane. Every thread
+// of the block calls it (one barrier).
+template <int NT>
+LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, int wave, int lane,
+                       const float (&v)[EpiGeom<NT>::NTW][4], const float (&u)[EpiGeom<NT>::NTW][4],
+                       EpiShared<NT>& sh) {
+  constexpr int NTW = EpiGeom<NT>::NTW, WPM = EpiGeom<NT>::WPM, MTB = EpiGeom<NT>::MTB;
+  const int r = lane & 15, kg = lane >> 4;
   int ov1 = 0, ov2 = 0;
-  const int quads = 4 * ntw;  // channel quads per row of this wave's tile
-  int s1[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  int s1[NTW], s2[NTW];
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (pass >= ntw) continue;
-    const int id = pass * 64 + lane;
-    const int rr = id / quads, cq = id - rr * quads;
-    const int64_t row = mtile * 16 + rr;
-    if (!wave_live || row >= o.M) continue;
-    const int col0 = nt0 * 16 + cq * 4;
-    const uint32_t pix = (uint32_t)row % (uint32_t)o.HWo;  // M < 2^31 (checked by the launchers)
-    const Noise4 n = o.q.stochastic ? qnoise4(o.q, qs.step, ((uint64_t)pix * o.ncol + col0) >> 2)
-                                    : Noise4{{0.f, 0.f, 0.f, 0.f}};
-    char4 w;
-    int c[4];
+  for (int j = 0; j < NTW; ++j) {
+    s1[j] = 0;
+    s2[j] = 0;
+    const int col = (nt0 + j) * 16 + r;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      c[k] = quant1(qs, o.q.stochastic, tile[rr][cq * 4 + k], n.u[k], ov1, ov2);
-      s1[pass][k] = c[k];
-      s2[pass][k] = c[k] * c[k];
-    }
-    w.x = (int8_t)c[0]; w.y = (int8_t)c[1]; w.z = (int8_t)c[2]; w.w = (int8_t)c[3];
-    *reinterpret_cast<char4*>(o.yq + row * o.ncol + col0) = w;
-  }
-  if (want_sum) {
-    // lanes with equal (lane % quads) hold the same channel quad: xor-reduce over quads..32
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      if (pass >= ntw) continue;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int a1 = s1[pass][k], a2 = s2[pass][k];
-        for (int off = quads; off < 64; off <<= 1) {
-          a1 += __shfl_xor(a1, off, 64);
-          a2 += __shfl_xor(a2, off, 64);
-        }
-        const int cq = (pass * 64 + lane) % quads;
-        if (wave_live && lane < quads) {
-          const int ch = nt0 * 16 + cq * 4 + k;
-          if (a1) atomicAdd((unsigned long long*)&sh_sum[ch], (unsigned long long)(long long)a1);
-          if (a2) atomicAdd((unsigned long long*)&sh_sum[o.ncol + ch], (unsigned long long)(long long)a2);
-        }
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = mtile * 16 + 4 * kg + i;
+      if (row < o.M) {
+        const int c = quant1(qs, o.q.stochastic, v[j][i], u[j][i], ov1, ov2);
+        o.yq[row * o.ncol + col] = (int8_t)c;
+        s1[j] += c;
+        s2[j] += c * c;
       }
     }
   }
-  if (o.q.counts) counts_stage(0, 1, ov1, ov2, sh_cnt);
+  const bool want_sum = o.chsum != nullptr;
+  if (want_sum) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16, 64);
+      s2[j] += __shfl_xor(s2[j], 16, 64);
+      s1[j] += __shfl_xor(s1[j], 32, 64);
+      s2[j] += __shfl_xor(s2[j], 32, 64);
+      if (kg == 0) {
+        sh.part[wave][0][j * 16 + r] = s1[j];
+        sh.part[wave][1][j * 16 + r] = s2[j];
+      }
+    }
+  }
+  if (o.q.counts) counts_stage(0, 1, ov1, ov2, sh.cnt);
   if (!(want_sum || o.q.counts)) return;
-  __syncthreads();  // one barrier publishes counters and channel sums
-  counts_publish(0, 1, o.q, sh_cnt);
-  if (want_sum) block_flush_sums(sh_sum, 2 * o.ncol, o.chsum, 2 * o.ncol);
+  __syncthreads();  // the only barrier: counters and channel sums of the whole block
+  counts_publish(0, 1, o.q, sh.cnt);
+  if (want_sum) {
+    const int t = threadIdx.x;
+    if (t < 2 * o.ncol) {
+      const int which = t >= o.ncol, col = t - which * o.ncol;
+      const int wcol = (col >> 4) / NTW;           // which wave column-group covers col
+      const int lc = col - wcol * NTW * 16;        // its column within that wave
+      long long tot = 0;
+#pragma unroll
+      for (int mt = 0; mt < MTB; ++mt) {
+        const int64_t row0 = ((int64_t)blockIdx.x * MTB + mt) * 16;
+        if (row0 < o.M) tot += sh.part[mt * WPM + wcol][which][lc];
+      }
+      if (tot) atomicAdd((unsigned long long*)&o.chsum[(int64_t)shard_id() * 2 * o.ncol + t], (unsigned long long)tot);
+    }
+  }
 }
 
 }  // namespace lbt

@@ -20,12 +20,13 @@ __global__ __launch_bounds__(256) void conv_fwd_generic_kernel(const TX* __restr
   const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cout;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int co = (int)(i % d.Cout);
-  int64_t m = i / d.Cout;
-  const int ow = (int)(m % d.Wo);
-  m /= d.Wo;
-  const int oh = (int)(m % d.Ho);
-  const int n = (int)(m / d.Ho);
+  const uint32_t iu = (uint32_t)i;  // total < 2^31 (launcher)
+  const int co = (int)(iu % (uint32_t)d.Cout);
+  uint32_t m = iu / (uint32_t)d.Cout;
+  const int ow = (int)(m % (uint32_t)d.Wo);
+  m /= (uint32_t)d.Wo;
+  const int oh = (int)(m % (uint32_t)d.Ho);
+  const int n = (int)(m / (uint32_t)d.Ho);
   int acc = 0;
   for (int kh = 0; kh < d.KH; ++kh) {
     const int ih = oh * d.SH + kh - d.PT;
@@ -49,12 +50,13 @@ __global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const int8_t* _
   const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int ci = (int)(i % d.Cin);
-  int64_t m = i / d.Cin;
-  const int iw = (int)(m % d.W);
-  m /= d.W;
-  const int ih = (int)(m % d.H);
-  const int n = (int)(m / d.H);
+  const uint32_t iu = (uint32_t)i;  // total < 2^31 (launcher)
+  const int ci = (int)(iu % (uint32_t)d.Cin);
+  uint32_t m = iu / (uint32_t)d.Cin;
+  const int iw = (int)(m % (uint32_t)d.W);
+  m /= (uint32_t)d.W;
+  const int ih = (int)(m % (uint32_t)d.H);
+  const int n = (int)(m / (uint32_t)d.H);
   int acc = 0;
   for (int kh = 0; kh < d.KH; ++kh) {
     const int ny = ih + d.PT - kh;
@@ -107,10 +109,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __res
       const int pl = t / KS, k = klo + (t - pl * KS);
       int v = 0;
       if (pl < cn) {
-        const int64_t p = c0 + pl;
-        const int n = (int)(p / HWo);
-        const int64_t rem = p - (int64_t)n * HWo;
-        const int oh = (int)(rem / d.Wo), ow = (int)(rem - (int64_t)oh * d.Wo);
+        const uint32_t p = (uint32_t)(c0 + pl);  // P < 2^31 (launcher)
+        const uint32_t n = p / (uint32_t)HWo;
+        const uint32_t rem = p - n * (uint32_t)HWo;
+        const int oh = (int)(rem / (uint32_t)d.Wo), ow = (int)(rem - (uint32_t)oh * (uint32_t)d.Wo);
         const int tap = k / d.Cin, ci = k - tap * d.Cin;
         const int kh = tap / d.KW, kw = tap - kh * d.KW;
         const int ih = oh * d.SH + kh - d.PT, iw = ow * d.SW + kw - d.PL;
@@ -155,6 +157,7 @@ extern "C" int lbt_conv_fwd_generic(const void* xq, int32_t x_i16, const int8_t*
                                     lbt_qdesc qx, lbt_qdesc qw, float* y, void* stream) {
   if (!desc_ok(d)) return LBT_EINVAL;
   const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cout;
+  if (total >= ((int64_t)1 << 31)) return LBT_EINVAL;
   const unsigned blocks = (unsigned)((total + 255) / 256);
   hipStream_t st = (hipStream_t)stream;
   if (x_i16)
@@ -170,6 +173,7 @@ extern "C" int lbt_conv_dgrad_generic(const int8_t* gq, const int8_t* w_hwio, lb
                                       lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
   if (!desc_ok(d)) return LBT_EINVAL;
   const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
+  if (total >= ((int64_t)1 << 31)) return LBT_EINVAL;
   const unsigned blocks = (unsigned)((total + 255) / 256);
   hipLaunchKernelGGL(conv_dgrad_generic_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, gq, w_hwio, d, qg,
                      qw, dx, add_src);
@@ -184,7 +188,7 @@ extern "C" int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_
   const int64_t tiles = (nout + kTile - 1) / kTile;
   if (tiles > 65535) return LBT_EINVAL;
   const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
-  if ((P + nsplit - 1) / nsplit > 8192) return LBT_EINVAL;  // int32 partial bound for 9-bit x 8-bit
+  if (P >= ((int64_t)1 << 31) || (P + nsplit - 1) / nsplit > 8192) return LBT_EINVAL;  // int32 partial bound for 9-bit x 8-bit
   const int64_t ks_max = (kTile + d.Cout - 1) / d.Cout + 1 < K ? (kTile + d.Cout - 1) / d.Cout + 1 : K;
   const size_t shm = sizeof(int16_t) * kChunk * (ks_max + d.Cout);
   if (shm > 64 * 1024) return LBT_EINVAL;

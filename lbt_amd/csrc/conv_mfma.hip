@@ -49,54 +49,43 @@ struct GemmArgs {
   int ncol;             // GEMM cols
 };
 
-template <int MODE, int CS>
-__global__ __launch_bounds__(kThreads, CS == 1 ? 8 : 1) void conv_gemm_kernel(GemmArgs p) {
-  __shared__ int sh_cnt[2 * kThreads / 64];
-  __shared__ long long sh_sum[2 * 128];
+template <int MODE, int CS, int NT>
+__global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD) ? 8 : 1) void conv_gemm_kernel(GemmArgs p) {
+  using G = EpiGeom<NT>;
+  constexpr int NTW = G::NTW, WPM = G::WPM, MTB = G::MTB;
+  __shared__ EpiShared<NT> sh;
   LBT_TS(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nt_total = p.ncol >> 4;
-  const int wpm = nt_total < 4 ? nt_total : 4;  // waves per M-tile
-  const int ntw = nt_total / wpm;               // n-tiles per wave (1 or 2)
-  const int mtb = 4 / wpm;                      // M-tiles per block
-  const int mt_local = wave / wpm;
-  const int nt0 = (wave % wpm) * ntw;
-  const int64_t mtile = (int64_t)blockIdx.x * mtb + mt_local;
-  const bool wave_live = mt_local < mtb;
+  const int mt_local = wave / WPM;
+  const int nt0 = (wave % WPM) * NTW;
+  const int64_t mtile = (int64_t)blockIdx.x * MTB + mt_local;
   const int r = lane & 15, kg = lane >> 4;
   const lbt_conv_desc& d = p.d;
-
   const bool want_q = p.yq != nullptr;
-  const bool want_sum = want_q && p.ychsum != nullptr;
-  if (want_sum) {
-    for (int i = threadIdx.x; i < 2 * p.ncol; i += kThreads) sh_sum[i] = 0;
-    __syncthreads();
-  }
 
-  // this lane's GEMM row -> pixel (n, y, x) of the "row" space
+  // this lane's GEMM row -> pixel (n, y, x) of the "row" space (M < 2^31: 32-bit math)
   const int OH = MODE == MODE_FWD ? d.Ho : d.H, OW = MODE == MODE_FWD ? d.Wo : d.W;
   const int64_t m = mtile * 16 + r;
-  const bool row_ok = wave_live && m < p.M;
+  const bool row_ok = m < p.M;
   int n = 0, py = 0, px = 0;
   if (row_ok) {
-    px = (int)(m % OW);
-    const int64_t t = m / OW;
-    py = (int)(t % OH);
-    n = (int)(t / OH);
+    const uint32_t mu = (uint32_t)m;
+    px = (int)(mu % (uint32_t)OW);
+    const uint32_t t = mu / (uint32_t)OW;
+    py = (int)(t % (uint32_t)OH);
+    n = (int)(t / (uint32_t)OH);
   }
   const int cred = CS * 16;  // channels of the gathered operand
   const int SH = MODE == MODE_FWD ? d.H : d.Ho, SW = MODE == MODE_FWD ? d.W : d.Wo;
 
-  v4i acc[2];
-  acc[0] = v4i{0, 0, 0, 0};
-  acc[1] = v4i{0, 0, 0, 0};
-
-  // A fragment of k-step kk (slice s = 4*kk + kg) for this lane's row
-  auto load_a = [&](int kk) -> v4i {
+  // A fragment of k-step kk (slice s = 4*kk + kg) for this lane's row: its address, and the
+  // value it takes instead when the slice is padding (0) or the tap is outside the image (fill)
+  auto addr_a = [&](int kk, bool& use, int& alt) -> const v4i* {
     const int s = kk * 4 + kg;
-    v4i a = v4i{p.a_fill, p.a_fill, p.a_fill, p.a_fill};
-    if (s >= p.nslices) return v4i{0, 0, 0, 0};
-    if (!row_ok) return a;
+    use = false;
+    alt = 0;
+    if (s >= p.nslices) return reinterpret_cast<const v4i*>(p.a);
+    alt = MODE == MODE_DGRAD ? 0 : p.a_fill;
     const int tap = s / CS, cs = s - tap * CS;
     const int kh = tap / d.KW, kw = tap - kh * d.KW;
     int sy, sx;
@@ -111,82 +100,118 @@ __global__ __launch_bounds__(kThreads, CS == 1 ? 8 : 1) void conv_gemm_kernel(Ge
       sx = nx / d.SW;
       ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
     }
-    if (ok) return *reinterpret_cast<const v4i*>(p.a + (((int64_t)n * SH + sy) * SW + sx) * cred + cs * 16);
-    return MODE == MODE_DGRAD ? v4i{0, 0, 0, 0} : a;
+    use = ok && row_ok;
+    if (!use) return reinterpret_cast<const v4i*>(p.a);
+    return reinterpret_cast<const v4i*>(p.a + (((int64_t)n * SH + sy) * SW + sx) * cred + cs * 16);
   };
   auto load_b = [&](int kk, int j) -> v4i {
     const int col = (nt0 + j) * 16 + r;
     return *reinterpret_cast<const v4i*>(p.b + ((int64_t)col * p.ks + kk * 4 + kg) * 16);
   };
 
-  if (wave_live) {
-    const int nks = p.ks >> 2;
-    // every operand of a 3x3 conv's k loop fits in registers: issue ALL loads, then the MFMAs
-    // (one memory round trip per wave instead of one per k-step)
-    constexpr int kMaxKS = (9 * CS + 3) / 4;
-    if (nks <= kMaxKS) {
-      v4i af[kMaxKS], bf[kMaxKS][2];
+  v4i acc[NTW];
 #pragma unroll
-      for (int kk = 0; kk < kMaxKS; ++kk) {
-        if (kk < nks) {
-          af[kk] = load_a(kk);
-          bf[kk][0] = load_b(kk, 0);
-          if (ntw > 1) bf[kk][1] = load_b(kk, 1);
-        }
-      }
+  for (int j = 0; j < NTW; ++j) acc[j] = v4i{0, 0, 0, 0};
+  // epilogue operands, fetched together with the GEMM operands: noise (fwd) / addend (dgrad)
+  float ea[NTW][4];
+  int corr[NTW];
+  const QOut qo{p.yq, p.qout, p.ychsum, p.M, p.ncol, (int64_t)OH * OW};
+  const QState qs = qstate(p.qout);
+
+  const int nks = p.ks >> 2;
+  // every operand of a 3x3 conv's k loop fits in registers: issue ALL loads (no branches around
+  // them), then the MFMAs -- one memory round trip per wave instead of one per k-step
+  constexpr int kMaxKS = (9 * CS + 3) / 4;
+  const bool preload = nks <= kMaxKS;
+  v4i af[kMaxKS], bf[kMaxKS][NTW];
+  if (preload) {
+    bool use[kMaxKS];
+    int alt[kMaxKS];
+    const v4i* pa[kMaxKS];
 #pragma unroll
-      for (int kk = 0; kk < kMaxKS; ++kk) {
-        if (kk < nks) {
-          acc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk], bf[kk][0], acc[0], 0, 0, 0);
-          if (ntw > 1) acc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk], bf[kk][1], acc[1], 0, 0, 0);
-        }
-      }
+    for (int kk = 0; kk < kMaxKS; ++kk) {
+      pa[kk] = addr_a(kk < nks ? kk : 0, use[kk], alt[kk]);
+      if (kk >= nks) { use[kk] = false; alt[kk] = 0; }  // zero A: its MFMA adds nothing
+    }
+#pragma unroll
+    for (int kk = 0; kk < kMaxKS; ++kk) {
+      af[kk] = *pa[kk];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) bf[kk][j] = load_b(kk < nks ? kk : 0, j);
+    }
+    const int* cs_src = (MODE == MODE_FWD && p.colsum) ? p.colsum : zi();
+    const uint32_t cmask = (MODE == MODE_FWD && p.colsum) ? 0xffffffffu : 0u;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) corr[j] = 128 * cs_src[((nt0 + j) * 16 + r) & cmask];
+    if constexpr (MODE == MODE_FWD) {
+      epi_noise<NTW>(qo, mtile, nt0, lane, ea);
     } else {
-      for (int kk = 0; kk < nks; ++kk) {
-        const v4i a = load_a(kk);
-        acc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, load_b(kk, 0), acc[0], 0, 0, 0);
-        if (ntw > 1) acc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, load_b(kk, 1), acc[1], 0, 0, 0);
-      }
+      const float* as = p.add_src ? p.add_src : zf();
+      const uint32_t amask = p.add_src ? 0xffffffffu : 0u;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t row = mtile * 16 + kg * 4 + i;
+          ea[j][i] = as[(uint32_t)((row < p.M ? row : 0) * p.ncol + (nt0 + j) * 16 + r) & amask];
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < kMaxKS; ++kk)
+      if (!use[kk]) af[kk] = v4i{alt[kk], alt[kk], alt[kk], alt[kk]};
+#pragma unroll
+    for (int kk = 0; kk < kMaxKS; ++kk)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk], bf[kk][j], acc[j], 0, 0, 0);
+  } else {
+    for (int kk = 0; kk < nks; ++kk) {
+      bool use;
+      int alt;
+      const v4i* pa = addr_a(kk, use, alt);
+      v4i a = *pa;
+      if (!use) a = v4i{alt, alt, alt, alt};
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, load_b(kk, j), acc[j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) corr[j] = (MODE == MODE_FWD && p.colsum) ? 128 * p.colsum[(nt0 + j) * 16 + r] : 0;
+    if constexpr (MODE == MODE_FWD) {
+      epi_noise<NTW>(qo, mtile, nt0, lane, ea);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t row = mtile * 16 + kg * 4 + i;
+          ea[j][i] = (p.add_src && row < p.M) ? p.add_src[row * p.ncol + (nt0 + j) * 16 + r] : 0.f;
+        }
     }
   }
-
   LBT_TS(1);
-  // ---------------- epilogue
+
+  // ---------------- epilogue: lane owns column (nt0+j)*16 + r of rows mtile*16 + 4*kg + i
   const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
-  if (!want_q) {
+  float v[NTW][4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (!(wave_live && j < ntw)) continue;
-      const int col = (nt0 + j) * 16 + r;
-      const int corr = p.colsum ? 128 * p.colsum[col] : 0;
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[j][i] = (float)(acc[j][i] + corr[j]) * scale;
+  if (!want_q) {
+    const bool addv = MODE == MODE_DGRAD && p.add_src;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t row = mtile * 16 + kg * 4 + i;
-        if (row >= p.M) continue;
-        const float v = (float)(acc[j][i] + corr) * scale;
-        const int64_t e = row * p.ncol + col;
-        p.y[e] = p.add_src ? v + p.add_src[e] : v;
+        if (row < p.M) p.y[row * p.ncol + (nt0 + j) * 16 + r] = addv ? v[j][i] + ea[j][i] : v[j][i];
       }
-    }
     return;
   }
-  // Quantising epilogue (conv_epilogue.h): tile -> LDS -> 4 consecutive channels per lane.
-  __shared__ float tile[4][16][33];
-  if (wave_live) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j >= ntw) continue;
-      const int col = (nt0 + j) * 16 + r;
-      const int corr = p.colsum ? 128 * p.colsum[col] : 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) tile[wave][kg * 4 + i][j * 16 + r] = (float)(acc[j][i] + corr) * scale;
-    }
+  if constexpr (MODE == MODE_FWD) {
+    LBT_TS(2);
+    epi_quant<NT>(qo, qs, mtile, nt0, wave, lane, v, ea, sh);
+    LBT_TS(3);
   }
-  wave_lds_sync();
-  LBT_TS(2);
-  const QOut qo{p.yq, p.qout, want_sum ? p.ychsum : nullptr, p.M, p.ncol, (int64_t)OH * OW};
-  quant_epilogue(qo, tile[wave], wave_live, mtile, nt0, ntw, sh_sum, sh_cnt);
-  LBT_TS(3);
 }
 
 // ----------------------------------------------------------------------------- wgrad
@@ -315,23 +340,32 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const int32_t* __rest
   dw[i] = a + b;
 }
 
-template <int MODE>
-int launch_gemm(const GemmArgs& p, int cs, hipStream_t st) {
-  const int nt = p.ncol / 16;
-  const int wpm = nt < 4 ? nt : 4;
-  if (nt != 1 && nt != 2 && nt != 4 && nt != 8) return LBT_EINVAL;
-  const int mtb = 4 / wpm;
+template <int MODE, int NT>
+int launch_gemm_nt(const GemmArgs& p, int cs, hipStream_t st) {
+  constexpr int MTB = EpiGeom<NT>::MTB;
   const int64_t mtiles = (p.M + 15) / 16;
-  const int64_t blocks = (mtiles + mtb - 1) / mtb;
+  const int64_t blocks = (mtiles + MTB - 1) / MTB;
   if (blocks > 0x7fffffff) return LBT_EINVAL;
   switch (cs) {
-    case 1: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
-    case 4: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
-    case 8: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 8>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 4, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 8, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
     default: return LBT_EINVAL;
   }
   return (int)hipGetLastError();
+}
+
+template <int MODE>
+int launch_gemm(const GemmArgs& p, int cs, hipStream_t st) {
+  if (p.M >= (int64_t)1 << 31) return LBT_EINVAL;  // 32-bit row arithmetic
+  switch (p.ncol / 16) {
+    case 1: return launch_gemm_nt<MODE, 1>(p, cs, st);
+    case 2: return launch_gemm_nt<MODE, 2>(p, cs, st);
+    case 4: return launch_gemm_nt<MODE, 4>(p, cs, st);
+    case 8: return launch_gemm_nt<MODE, 8>(p, cs, st);
+    default: return LBT_EINVAL;
+  }
 }
 
 bool desc_ok(const lbt_conv_desc& d) {
@@ -354,6 +388,7 @@ extern "C" int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* 
   p.a_fill = x_u8off ? (int)0x80808080u : 0;
   p.colsum = x_u8off ? wcolsum : nullptr;
   if (x_u8off && !wcolsum) return LBT_EINVAL;
+  if (yq && qout.stochastic && !qout.noise) return LBT_EINVAL;  // quantising epilogue reads the noise table
   p.d = d; p.qa = qx; p.qb = qw; p.y = y; p.add_src = nullptr; p.yq = yq; p.qout = qout; p.ychsum = ychsum;
   p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
   return launch_gemm<MODE_FWD>(p, cs, (hipStream_t)stream);

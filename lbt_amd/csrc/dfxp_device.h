@@ -156,6 +156,14 @@ LBT_DEV float div_by(float x, const Recip& d) {
   return copysignf(fmaf(r1, d.rc, q1), x);
 }
 
+// ------------------------------------------------------------------ branch-free operand loads
+// A load whose value leaves a branch becomes a register copy that must wait for the load, which
+// serialises a kernel's gathers. Optional operands therefore load from this zero block instead
+// (index masked to 0) and out-of-range gathers from a clamped address, selected afterwards.
+static __device__ int32_t kZeroBlock[64];  // zero-initialised, never written (global space)
+LBT_DEV const float* zf() { return reinterpret_cast<const float*>(kZeroBlock); }
+LBT_DEV const int32_t* zi() { return kZeroBlock; }
+
 // ------------------------------------------------------------------ reductions
 LBT_DEV int wave_sum_i32(int v) {
 #pragma unroll

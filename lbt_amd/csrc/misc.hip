@@ -52,7 +52,15 @@ __global__ void avgpool_fwd_kernel(const float* __restrict__ x, float* __restric
   const int n = i / C, c = i - n * C;
   const float* p = x + (int64_t)n * HW * C + c;
   float acc = 0.f;
-  for (int k = 0; k < HW; ++k) acc = acc + p[(int64_t)k * C];
+  // same sequential order as before (bit-exact), but 16 loads in flight per round trip
+  for (int k0 = 0; k0 < HW; k0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = p[(int64_t)(k0 + k < HW ? k0 + k : k0) * C];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k0 + k < HW) acc = acc + v[k];
+  }
   y[i] = acc * (1.0f / (float)HW);
 }
 
@@ -150,7 +158,7 @@ extern "C" int lbt_add(const float* a, const float* b, float* y, int64_t n, void
   return (int)hipGetLastError();
 }
 extern "C" int lbt_avgpool_fwd(const float* x, float* y, int32_t N, int32_t HW, int32_t C, void* stream) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((N * C + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, y, N, HW, C);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((N * C + 63) / 64), dim3(64), 0, (hipStream_t)stream, x, y, N, HW, C);
   return (int)hipGetLastError();
 }
 extern "C" int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW, int32_t C, void* stream) {

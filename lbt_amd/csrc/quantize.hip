@@ -121,39 +121,44 @@ LBT_DEV void range_apply(int i, int c1, int c2, int32_t* exps, const int32_t* bi
   exps[i] = I;
 }
 
-// Sum (and zero) the shards of slot i.
-LBT_DEV void shard_totals(int32_t* counts, int i, int& c1, int& c2) {
-  c1 = 0; c2 = 0;
-  int32_t* c = counts + (int64_t)i * LBT_NSHARD * LBT_CSTRIDE;
-  for (int k = 0; k < LBT_NSHARD; ++k) {
-    c1 += c[k * LBT_CSTRIDE];
-    c2 += c[k * LBT_CSTRIDE + 1];
-    c[k * LBT_CSTRIDE] = 0;
-    c[k * LBT_CSTRIDE + 1] = 0;
+// One wave per slot: lane k < LBT_NSHARD reads (and zeroes) shard k, a wave sum gives the totals.
+LBT_DEV bool wave_shard_totals(int32_t* counts, int i, int& c1, int& c2) {
+  const int lane = threadIdx.x & 63;
+  int a = 0, b = 0;
+  if (lane < LBT_NSHARD) {
+    int32_t* c = counts + ((int64_t)i * LBT_NSHARD + lane) * LBT_CSTRIDE;
+    a = c[0];
+    b = c[1];
+    c[0] = 0;
+    c[1] = 0;
   }
+  c1 = wave_sum_i32(a);
+  c2 = wave_sum_i32(b);
+  return lane == 0;
 }
 
+// grid: one wave per slot (4 slots per 256-thread block)
 __global__ void range_update_kernel(int32_t* exps, int32_t* counts, const int32_t* bits,
                                     const float* target, const float* nelem, int nslots,
                                     uint64_t* step) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i < nslots && nelem[i] > 0.f) {  // slots not fed this step keep their exponent
     int c1, c2;
-    shard_totals(counts, i, c1, c2);
-    range_apply(i, c1, c2, exps, bits, target, nelem);
+    if (wave_shard_totals(counts, i, c1, c2)) range_apply(i, c1, c2, exps, bits, target, nelem);
   }
-  if (i == 0) step[0] += 1ull;
+  if (blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1ull;
 }
 
 __global__ void counts_fold_kernel(int32_t* counts, int nslots, float* folded) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nslots) return;
   int c1, c2;
-  shard_totals(counts, i, c1, c2);
-  folded[4 * i + 0] = (float)(c1 >> 12);
-  folded[4 * i + 1] = (float)(c1 & 4095);
-  folded[4 * i + 2] = (float)(c2 >> 12);
-  folded[4 * i + 3] = (float)(c2 & 4095);
+  if (wave_shard_totals(counts, i, c1, c2)) {
+    folded[4 * i + 0] = (float)(c1 >> 12);
+    folded[4 * i + 1] = (float)(c1 & 4095);
+    folded[4 * i + 2] = (float)(c2 >> 12);
+    folded[4 * i + 3] = (float)(c2 & 4095);
+  }
 }
 
 __global__ void range_update_folded_kernel(int32_t* exps, const float* folded, const int32_t* bits,
@@ -240,7 +245,7 @@ extern "C" int lbt_dfxp_quantize(const float* x, void* out, int out_kind, int64_
 
 extern "C" int lbt_dfxp_range_update(int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
                                      const float* nelem, int32_t nslots, uint64_t* step, void* stream) {
-  const int blocks = nslots > 0 ? (nslots + 255) / 256 : 1;
+  const int blocks = nslots > 0 ? (nslots + 3) / 4 : 1;
   hipLaunchKernelGGL(range_update_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, exps, counts, bits,
                      target, nelem, nslots, step);
   return (int)hipGetLastError();
@@ -248,8 +253,8 @@ extern "C" int lbt_dfxp_range_update(int32_t* exps, int32_t* counts, const int32
 
 extern "C" int lbt_dfxp_counts_fold(int32_t* counts, int32_t nslots, float* folded, void* stream) {
   if (nslots <= 0) return LBT_OK;
-  hipLaunchKernelGGL(counts_fold_kernel, dim3((nslots + 255) / 256), dim3(256), 0, (hipStream_t)stream, counts,
-                     nslots, folded);
+  hipLaunchKernelGGL(counts_fold_kernel, dim3((nslots + 3) / 4), dim3(256), 0, (hipStream_t)stream, counts, nslots,
+                     folded);
   return (int)hipGetLastError();
 }
 
@@ -273,4 +278,4 @@ extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, 
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_abi_version(void) { return 3; }
+extern "C" int lbt_abi_version(void) { return 4; }

@@ -16,7 +16,8 @@
 //        epilogue (Normalization_q input quantiser + exact channel sums, conv_epilogue.h).
 // wgrad: rows = patch index k, cols = Cout, k-dim = pixels: each wave sums 64 pixels (2 MFMAs
 //        per 16x16 tile), the 4 waves of a workgroup are combined in LDS and each workgroup
-//        writes one int32 partial slab[wg][K][Cout] for lbt_conv_wgrad_reduce(_many).
+//        adds its exact int32 partial into shard (wg % nshard) of a zeroed slab[nshard][K][Cout]
+//        (integer atomics) for lbt_conv_wgrad_reduce(_many).
 #include "conv_epilogue.h"
 
 using namespace lbt;
@@ -39,101 +40,105 @@ struct StemFwdArgs {
   QOut o;
 };
 
-// patch element k of output pixel (n, oy, ox) -> input code (0 outside the image)
-LBT_DEV int patch_code(const int16_t* x, const lbt_conv_desc& d, int n, int oy, int ox, int k) {
+// Offset of patch element k of output pixel (n, oy, ox) in the NHWC code image, or -1 outside
+// it. Callers compute every offset of a fragment first and then issue all the loads, so the
+// gathers of a lane are in flight together.
+LBT_DEV int64_t patch_off(const lbt_conv_desc& d, int n, int oy, int ox, int k) {
   const int tap = k / d.Cin, ci = k - tap * d.Cin;
   const int kh = tap / d.KW, kw = tap - kh * d.KW;
   const int iy = oy * d.SH + kh - d.PT, ix = ox * d.SW + kw - d.PL;
-  if ((unsigned)iy >= (unsigned)d.H || (unsigned)ix >= (unsigned)d.W) return 0;
-  return x[(((int64_t)n * d.H + iy) * d.W + ix) * d.Cin + ci];
+  if ((unsigned)iy >= (unsigned)d.H || (unsigned)ix >= (unsigned)d.W) return -1;
+  return (((int64_t)n * d.H + iy) * d.W + ix) * d.Cin + ci;
 }
 
+// 8 patch codes -> fp16 fragment (offsets < 0 read as 0)
+LBT_DEV h8 gather8(const int16_t* __restrict__ x, const int64_t (&off)[8]) {
+  int16_t v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = x[off[j] < 0 ? 0 : off[j]];
+  h8 a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = (_Float16)(float)(off[j] < 0 ? 0 : (int)v[j]);
+  return a;
+}
+
+template <int NT>
 __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(StemFwdArgs p) {
-  __shared__ int sh_cnt[2 * kThreads / 64];
-  __shared__ long long sh_sum[2 * 128];
-  __shared__ float tile[4][16][33];
+  using G = EpiGeom<NT>;
+  constexpr int NTW = G::NTW, WPM = G::WPM, MTB = G::MTB;
+  __shared__ EpiShared<NT> sh;
   LBT_TS(0);
   const lbt_conv_desc& d = p.d;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nt_total = d.Cout >> 4;
-  const int wpm = nt_total < 4 ? nt_total : 4;  // waves per M-tile
-  const int ntw = nt_total / wpm;               // n-tiles per wave (1 or 2)
-  const int mtb = 4 / wpm;                      // M-tiles per block
-  const int mt_local = wave / wpm;
-  const int nt0 = (wave % wpm) * ntw;
-  const int64_t mtile = (int64_t)blockIdx.x * mtb + mt_local;
-  const bool wave_live = mt_local < mtb;
+  const int mt_local = wave / WPM;
+  const int nt0 = (wave % WPM) * NTW;
+  const int64_t mtile = (int64_t)blockIdx.x * MTB + mt_local;
   const int r = lane & 15, kg = lane >> 4;
   const int64_t M = p.o.M;
   const bool want_q = p.o.yq != nullptr;
-  const bool want_sum = want_q && p.o.chsum != nullptr;
-  if (want_sum) {
-    for (int i = threadIdx.x; i < 2 * d.Cout; i += kThreads) sh_sum[i] = 0;
-    __syncthreads();
-  }
-  f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
-  if (wave_live) {
-    const int64_t m = mtile * 16 + r;
-    h8 a;
+  const QState qs = qstate(p.o.q);
+  f4v acc[NTW];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = (_Float16)0.f;
-    if (m < M) {
-      const int ox = (int)(m % d.Wo);
-      const int64_t t = m / d.Wo;
-      const int oy = (int)(t % d.Ho), n = (int)(t / d.Ho);
+  for (int j = 0; j < NTW; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int64_t m = mtile * 16 + r;
+  int64_t off[8];
+  {
+    const uint32_t mu = (uint32_t)(m < M ? m : 0);
+    const int ox = (int)(mu % (uint32_t)d.Wo);
+    const uint32_t t = mu / (uint32_t)d.Wo;
+    const int oy = (int)(t % (uint32_t)d.Ho), n = (int)(t / (uint32_t)d.Ho);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * kg + j;
+      off[j] = (m < M && k < p.K) ? patch_off(d, n, oy, ox, k) : -1;
+    }
+  }
+  const h8 a = gather8(p.x, off);
+  h8 b[NTW];
+  {
+    int8_t wv[NTW][8];
+#pragma unroll
+    for (int jt = 0; jt < NTW; ++jt)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 8 * kg + j;
-        if (k < p.K) a[j] = (_Float16)(float)patch_code(p.x, d, n, oy, ox, k);
+        wv[jt][j] = p.w[(int64_t)(k < p.K ? k : 0) * d.Cout + (nt0 + jt) * 16 + r];
       }
-    }
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      if (jt >= ntw) continue;
-      const int col = (nt0 + jt) * 16 + r;
-      h8 b;
+    for (int jt = 0; jt < NTW; ++jt)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * kg + j;
-        b[j] = (_Float16)(float)(k < p.K ? (int)p.w[(int64_t)k * d.Cout + col] : 0);
-      }
-      acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[jt], 0, 0, 0);
-    }
+      for (int j = 0; j < 8; ++j) b[jt][j] = (_Float16)(float)(8 * kg + j < p.K ? (int)wv[jt][j] : 0);
   }
+  float u[NTW][4];
+  if (want_q) epi_noise<NTW>(p.o, mtile, nt0, lane, u);
+#pragma unroll
+  for (int jt = 0; jt < NTW; ++jt) acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[jt], acc[jt], 0, 0, 0);
   LBT_TS(1);
   const float scale = ldexpf(1.0f, -(frac_exp(p.qx) + frac_exp(p.qw)));
-  if (!want_q) {
-    if (!wave_live) return;
+  float v[NTW][4];
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      if (jt >= ntw) continue;
-      const int col = (nt0 + jt) * 16 + r;
+  for (int jt = 0; jt < NTW; ++jt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[jt][i] = acc[jt][i] * scale;
+  if (!want_q) {
+#pragma unroll
+    for (int jt = 0; jt < NTW; ++jt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t row = mtile * 16 + kg * 4 + i;
-        if (row < M) p.y[row * d.Cout + col] = acc[jt][i] * scale;
+        if (row < M) p.y[row * d.Cout + (nt0 + jt) * 16 + r] = v[jt][i];
       }
-    }
     return;
   }
-  if (wave_live) {
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      if (jt >= ntw) continue;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) tile[wave][kg * 4 + i][jt * 16 + r] = acc[jt][i] * scale;
-    }
-  }
-  wave_lds_sync();
   LBT_TS(2);
-  quant_epilogue(p.o, tile[wave], wave_live, mtile, nt0, ntw, sh_sum, sh_cnt);
+  epi_quant<NT>(p.o, qs, mtile, nt0, wave, lane, v, u, sh);
   LBT_TS(3);
 }
 
 // grid = nsplit workgroups of kWgPixels pixels; Cout <= 64 (ct tiles), K <= 32 (2 kt tiles)
 __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const int16_t* __restrict__ x,
                                                               const int8_t* __restrict__ gq, lbt_conv_desc d, int K,
-                                                              int64_t M, int32_t* __restrict__ slab) {
+                                                              int64_t M, int32_t* __restrict__ slab, int nshard) {
   __shared__ int red[4][32][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kg = lane >> 4;
@@ -155,27 +160,36 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const int16_t* __r
     for (int j = 0; j < 8; ++j) {
       const int64_t m = p0 + 32 * s + 8 * kg + j;
       pv[j] = m < M;
-      const int64_t mm = pv[j] ? m : 0;
-      pox[j] = (int)(mm % d.Wo);
-      const int64_t t = mm / d.Wo;
-      poy[j] = (int)(t % d.Ho);
-      pn[j] = (int)(t / d.Ho);
+      const uint32_t mu = (uint32_t)(pv[j] ? m : 0);
+      pox[j] = (int)(mu % (uint32_t)d.Wo);
+      const uint32_t t = mu / (uint32_t)d.Wo;
+      poy[j] = (int)(t % (uint32_t)d.Ho);
+      pn[j] = (int)(t / (uint32_t)d.Ho);
     }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const int k = kt * 16 + r;
+      int64_t off[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        a[s][kt][j] = (_Float16)(float)((kt < nkt && k < K && pv[j]) ? patch_code(x, d, pn[j], poy[j], pox[j], k) : 0);
+      for (int j = 0; j < 8; ++j) off[j] = (kt < nkt && k < K && pv[j]) ? patch_off(d, pn[j], poy[j], pox[j], k) : -1;
+      a[s][kt] = gather8(x, off);
     }
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
+      if (ct >= nct) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[s][ct][j] = (_Float16)0.f;
+        continue;
+      }
       const int c = ct * 16 + r;
+      int8_t gv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int64_t m = p0 + 32 * s + 8 * kg + j;
-        b[s][ct][j] = (_Float16)(float)((ct < nct && pv[j]) ? (int)gq[m * d.Cout + c] : 0);
+        gv[j] = gq[(pv[j] ? m : 0) * d.Cout + c];
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[s][ct][j] = (_Float16)(float)(pv[j] ? (int)gv[j] : 0);
     }
   }
 #pragma unroll
@@ -194,10 +208,11 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const int16_t* __r
       for (int i = 0; i < 4; ++i)
         if (kt < nkt && ct < nct) red[wave][kt * 16 + 4 * kg + i][ct * 16 + r] = (int)acc[kt][ct][i];
   __syncthreads();
-  int32_t* out = slab + (int64_t)blockIdx.x * K * d.Cout;
+  int32_t* out = slab + (int64_t)(blockIdx.x % nshard) * K * d.Cout;
   for (int i = threadIdx.x; i < K * d.Cout; i += kThreads) {
     const int k = i / d.Cout, c = i - k * d.Cout;
-    out[i] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    const int v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    if (v) atomicAdd(&out[i], v);  // integer atomics: exact, order-independent
   }
 }
 
@@ -210,27 +225,35 @@ extern "C" int lbt_conv_stem_fwd(const int16_t* x, const int8_t* w_hwio, lbt_con
   const int K = d.KH * d.KW * d.Cin;
   if (K <= 0 || K > 32 || d.Cout <= 0 || d.Cout % 16 || d.Cout > 128) return LBT_EINVAL;
   if ((y == nullptr) == (yq == nullptr)) return LBT_EINVAL;
-  if (yq && qout.bits > 8) return LBT_EINVAL;
+  if (yq && (qout.bits > 8 || (qout.stochastic && !qout.noise))) return LBT_EINVAL;
   const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
   if (M <= 0) return LBT_OK;
   StemFwdArgs p;
   p.x = x; p.w = w_hwio; p.d = d; p.K = K; p.qx = qx; p.qw = qw; p.y = y;
   p.o = QOut{yq, qout, yq ? ychsum : nullptr, M, d.Cout, (int64_t)d.Ho * d.Wo};
-  const int nt = d.Cout / 16, wpm = nt < 4 ? nt : 4, mtb = 4 / wpm;
-  const int64_t blocks = ((M + 15) / 16 + mtb - 1) / mtb;
-  if (blocks > 0x7fffffff) return LBT_EINVAL;
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, p);
+  if (M >= (int64_t)1 << 31) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t mtiles = (M + 15) / 16;
+  switch (d.Cout / 16) {
+    case 1: hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3((unsigned)((mtiles + 3) / 4)), dim3(kThreads), 0, st, p); break;
+    case 2: hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3((unsigned)((mtiles + 1) / 2)), dim3(kThreads), 0, st, p); break;
+    case 4: hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3((unsigned)mtiles), dim3(kThreads), 0, st, p); break;
+    case 8: hipLaunchKernelGGL(stem_fwd_kernel<8>, dim3((unsigned)mtiles), dim3(kThreads), 0, st, p); break;
+    default: return LBT_EINVAL;
+  }
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_conv_stem_wgrad(const int16_t* x, const int8_t* gq, lbt_conv_desc d, int32_t* slab, int32_t nsplit,
+extern "C" int lbt_conv_stem_wgrad(const int16_t* x, const int8_t* gq, lbt_conv_desc d, int32_t* slab, int32_t nshard,
                                    void* stream) {
   const int K = d.KH * d.KW * d.Cin;
-  if (K <= 0 || K > 32 || d.Cout <= 0 || d.Cout % 16 || d.Cout > 64) return LBT_EINVAL;
+  if (K <= 0 || K > 32 || d.Cout <= 0 || d.Cout % 16 || d.Cout > 64 || nshard <= 0) return LBT_EINVAL;
   const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
-  if (nsplit != (int32_t)((M + kWgPixels - 1) / kWgPixels)) return LBT_EINVAL;
   if (M <= 0) return LBT_OK;
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3((unsigned)nsplit), dim3(kThreads), 0, (hipStream_t)stream, x, gq, d, K, M,
-                     slab);
+  const int64_t blocks = (M + kWgPixels - 1) / kWgPixels;
+  // int32 shard totals stay exact: <= ceil(blocks/nshard) * 256 pixels * 2048 * 128 < 2^31
+  if ((blocks + nshard - 1) / nshard > 31 || M >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, x, gq, d, K, M,
+                     slab, (int)nshard);
   return (int)hipGetLastError();
 }

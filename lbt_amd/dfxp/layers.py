@@ -178,8 +178,7 @@ class Conv2d_q(Layer_q):
             slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
             ops.conv_wgrad_i8(self.xq, self.x_kind == OUT_U8OFF, self.gradq, d, slab, ns)
         elif self.stem(d):
-            ns = ops.stem_nsplit(d)
-            slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
+            ns, slab = ops.stem_slab(self._c, "stem_slab", d, self.ctx)
             ops.conv_stem_wgrad(self.xq, self.gradq, d, slab, ns)
         else:
             ns = ops.wgrad_nsplit(d, generic=True)

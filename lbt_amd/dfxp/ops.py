@@ -130,7 +130,8 @@ def conv_desc(N, H, W, Cin, Cout, KH, KW, SH, SW, padding):
 
 
 def mfma_ok(Cin, Cout):
-    return Cin % 16 == 0 and Cout % 16 == 0 and Cin <= 128 and Cout <= 128
+    """Shapes the int8 MFMA kernels take (16-channel slices, 1/2/4/8 of them on each side)."""
+    return Cin in (16, 32, 64, 128) and Cout in (16, 32, 64, 128)
 
 
 def conv_fwd_i8(xq, x_u8off, wf, ksf, wcolsum, d, qx, qw, y=None, yq=None, qout=None, ychsum=None):
@@ -160,7 +161,7 @@ def wgrad_nsplit(d, generic=False):
     taps = d.KH * d.KW
     if generic:
         lo = -(-P // 8192)
-        return max(lo, min(256, -(-P // 32)))
+        return max(lo, min(256, -(-P // (8 if P <= 4096 else 32))))
     lo = -(-P // 65536)
     want = max(1, -(-512 // taps))
     return max(lo, min(want, max(1, P // 256)))
@@ -195,11 +196,20 @@ def conv_wgrad_generic(xq, x_i16, gq, d, slab, nsplit):
 def stem_ok(d):
     """The fp16-MFMA stem kernels take this conv (small patch, 16-multiple Cout)."""
     K = d.KH * d.KW * d.Cin
-    return 0 < K <= 32 and d.Cout % 16 == 0 and 0 < d.Cout <= 64
+    return 0 < K <= 32 and d.Cout in (16, 32, 64)
 
 
 def stem_nsplit(d):
-    return -(-(d.N * d.Ho * d.Wo) // _lib.STEM_WG_PIXELS)
+    """Shards of the stem wgrad slab (>= 32; each <= 31 workgroups for int32 exactness)."""
+    blocks = -(-(d.N * d.Ho * d.Wo) // _lib.STEM_WG_PIXELS)
+    return max(32, -(-blocks // 31))
+
+
+def stem_slab(cache, key, d, ctx):
+    """Zeroed int32 [nshard, K, Cout] stem-wgrad slab carved from the context's sums arena."""
+    ns = stem_nsplit(d)
+    n = ns * d.KH * d.KW * d.Cin * d.Cout
+    return ns, cache.sums(key, (n + 1) // 2, ctx).view(torch.int32)[:n].view(ns, d.KH * d.KW * d.Cin, d.Cout)
 
 
 def conv_stem_fwd(x16, w_hwio, d, qx, qw, y=None, yq=None, qout=None, ychsum=None):

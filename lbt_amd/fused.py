@@ -87,17 +87,20 @@ class FusedResNet:
     def info(self):
         return "fused " + self.model.info()
 
+    zeroes_own_sums = True  # the plan's first launch clears the sums arena
+
     def input_buffer(self, shape):
         """The plan's own input buffer (a caller may write batches straight into it)."""
         return self._c.get("X", tuple(shape), torch.float32, self.ctx.device)
+
+    def label_buffer(self, n):
+        return self._c.get("labels", (int(n),), torch.int32, self.ctx.device)
 
     def forward(self, X):
         self._ensure(X)
         if X.data_ptr() != self._X.data_ptr():
             self._X.copy_(X)
-        if not self.ctx.sums_managed:
-            self.ctx.zero_sums()
-        for f in self._fwd:
+        for f in self._fwd:  # the first launch also zeroes the step's sums
             f()
         return self.logits
 
@@ -156,7 +159,7 @@ class FusedResNet:
         st = _lib.stream
         N, H, W, Cin0 = X.shape
         self._X = self.input_buffer(X.shape)
-        self._labels = torch.zeros(N, dtype=torch.int32, device=ctx.device)
+        self._labels = self.label_buffer(N)
         fwd, bwd = [], []
         lib = _lib.load()
         if self._side is None:
@@ -311,8 +314,7 @@ class FusedResNet:
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB)))
         self._keep += [aA, aB]
         if self._stem:
-            ns0 = ops.stem_nsplit(dc)
-            slab0 = self._buf("slab0", (ns0, kh * kw * Cin0, C0), torch.int32)
+            ns0, slab0 = ops.stem_slab(self._c, "slab0", dc, ctx)
             bwd.append(L("lbt_conv_stem_wgrad", ptr(ximg), ptr(gq0), dc, ptr(slab0), ns0, k="stem_wgrad_kernel",
                          nb=2 * ximg.numel() + gq0.numel() + 4 * slab0.numel()))
         else:
@@ -336,8 +338,10 @@ class FusedResNet:
         # ---- this step's noise tables: one launch ahead of everything else
         self._njobs = _dev_array(njobs, ctx.device)
         max_n = max(j.n for j in njobs)
-        fwd.insert(0, L("lbt_dfxp_noise_fill", ptr(self._njobs), len(njobs), max_n, k="noise_fill_kernel",
-                        nb=4 * sum(j.n for j in njobs)))
+        # ... which also clears the step's integer sums (everything this plan carved from the arena)
+        nz = ctx._sums_used
+        fwd.insert(0, L("lbt_dfxp_noise_fill", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
+                        k="noise_fill_kernel", nb=4 * sum(j.n for j in njobs) + 8 * nz))
         self._fwd, self._bwd = fwd, bwd
 
     def _qd(self, q):

@@ -90,7 +90,8 @@ class Trainer:
     # -- the step ----------------------------------------------------------------------------
     def _fwd_bwd(self, X, y):
         m = self.model
-        self.ctx.zero_sums()
+        if not getattr(m, "zeroes_own_sums", False):
+            self.ctx.zero_sums()
         m.forward(X)
         m.compute_loss(y)
         m.backward()
@@ -115,7 +116,12 @@ class Trainer:
         self._update()
 
     def _capture(self, X, y):
-        self._static = (torch.empty_like(X), torch.empty_like(y))
+        m = self.model
+        if hasattr(m, "input_buffer") and hasattr(m, "label_buffer"):
+            # capture on the model's own buffers: no copies inside the graph
+            self._static = (m.input_buffer(X.shape), m.label_buffer(y.shape[0]))
+        else:
+            self._static = (torch.empty_like(X), torch.empty_like(y))
         sX, sy = self._static
         sX.copy_(X)
         sy.copy_(y)

@@ -238,7 +238,7 @@ def test_stem_kernels_equal_integer_gemm(N, H, Cin, Cout, s):
         g = rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout)).astype(np.int8)
         g.flat[:3] = -128
         ns = ops.stem_nsplit(d)
-        slab = torch.full((ns, 9 * Cin, Cout), 7, dtype=torch.int32, device=DEV)
+        slab = torch.zeros((ns, 9 * Cin, Cout), dtype=torch.int32, device=DEV)
         ops.conv_stem_wgrad(xt, torch.from_numpy(g).to(DEV), d, slab, ns)
         dw_ref = onn.conv_wgrad_int(x, g, (s, s), "SAME", (3, 3))
         assert np.array_equal(slab.cpu().numpy().astype(np.int64).sum(0), dw_ref.reshape(9 * Cin, Cout))
