@@ -106,37 +106,92 @@ LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long 
 }
 
 // ============================================================================ forward chain
+// Kernel variants: F holds the chain's configuration as compile-time flags for the combinations
+// the fused ResNet plan launches (no per-element branches, constant rounding mode and output
+// encoding); kRt selects the variant that reads everything from the descriptor at run time.
+enum : int {
+  kRt = 1 << 20,
+  // forward
+  kFQ = 1,       // branch inputs are int8 Normalization_q codes (else fp32 xin)
+  kFRout = 2,    // store the Rescale_q codes R
+  kFRes = 4,     // residual add
+  kFRelu = 8,
+  kFY = 16,      // store fp32 y
+  kFO1 = 32,     // first output quantiser
+  kFO2 = 64,     // second output quantiser
+  kFStoch = 128, // every quantiser stochastic
+  kFU8 = 256,    // outputs in the unsigned 9-bit offset encoding
+};
+#define LBT_FL(bit, rt) ((F & kRt) ? (rt) : ((F & (bit)) != 0))
+
 template <int B>
 LBT_DEV const lbt_chain_branch& fbranch(const lbt_chain_fwd& a) { return B == 0 ? a.b1 : a.b2; }
 
-template <int NB>
+template <int NB, int F>
 __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, int rpt) {
   extern __shared__ float shf[];  // per branch: mu, sigma, gq, bq [C each]; then long long tmp[2C]
   __shared__ int sh_cnt[8 * kThreads / 64];
+  constexpr int ST = (F & kRt) ? -1 : ((F & kFStoch) ? 1 : 0);
   LBT_TS(0);
   const int C = a.C;
   long long* tmp = reinterpret_cast<long long*>(shf + 8 * C);
+  const int64_t groups = a.inner >> 2;
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool live = g < groups;
+  const int64_t gl = live ? g : 0;
+  const int c0 = (int)(((uint32_t)gl << 2) % (uint32_t)C);
+  const int64_t r0 = (int64_t)blockIdx.y * rpt;
+  const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+  const bool q_in[2] = {LBT_FL(kFQ, a.b1.nrm.q != nullptr), LBT_FL(kFQ, a.b2.nrm.q != nullptr)};
+  const bool res = LBT_FL(kFRes, a.res != nullptr);
+
+  // ---- the first rows and the noise go out before the moment prologue (their latency overlaps it)
+  int qv[NB][kRB];
+  float4 xv[NB][kRB], rv[kRB];
+  auto load_batch = [&](int64_t rb) {
+#pragma unroll
+    for (int j = 0; j < kRB; ++j) {
+      const int64_t e = (rb + j < rend ? rb + j : r0) * a.inner + (gl << 2);  // clamped: never branch
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+        if (q_in[b]) qv[b][j] = ld_i8x4(Bb.nrm.q, e);
+        else xv[b][j] = ld_f32x4(Bb.xin, e);
+      }
+      if (res) rv[j] = ld_f32x4(a.res, e);
+    }
+  };
+  load_batch(r0);
   QState qr[2];
+  Noise4 nr[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+    qr[b] = qstate(Bb.qr);
+    nr[b] = noise_for(Bb.qr, qr[b], gl);
+  }
+  const QState so1 = qstate(a.qo1), so2 = qstate(a.qo2);
+  const bool o1 = LBT_FL(kFO1, a.o1 && so1.active), o2 = LBT_FL(kFO2, a.o2 && so2.active);
+  const Noise4 no1 = noise_for(a.qo1, so1, gl);
+  const Noise4 no2 = noise_for(a.qo2, so2, gl);
+
   float sn[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const lbt_chain_branch& B = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+    const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
     float* P = shf + 4 * C * b;
-    qr[b] = qstate(B.qr);
     sn[b] = 0.f;
-    if (B.nrm.q) {
-      sn[b] = qscale(B.nrm.qn);
-      bn_moments(B.nrm, C, P, P + C, tmp);
+    if (q_in[b]) {
+      sn[b] = qscale(Bb.nrm.qn);
+      bn_moments(Bb.nrm, C, P, P + C, tmp);
       __syncthreads();
     }
     if (qr[b].active)
-      for (int c = threadIdx.x; c < C; c += kThreads) { P[2 * C + c] = B.gb[c]; P[3 * C + c] = B.gb[C + c]; }
+      for (int c = threadIdx.x; c < C; c += kThreads) { P[2 * C + c] = Bb.gb[c]; P[3 * C + c] = Bb.gb[C + c]; }
   }
   __syncthreads();
   LBT_TS(1);
   // this thread's channel quad is fixed: its per-channel constants live in registers
-  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int c0 = (int)(((uint32_t)g << 2) % (uint32_t)C);
   float pm[NB][4], pg[NB][4], pb[NB][4];
   Recip ps[NB][4];
 #pragma unroll
@@ -150,94 +205,74 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
       pb[b][k] = P[3 * C + c0 + k];
     }
   }
-  const QState so1 = qstate(a.qo1), so2 = qstate(a.qo2);
-  const bool o1 = a.o1 && so1.active, o2 = a.o2 && so2.active;
-  int ovr[2][2] = {{0, 0}, {0, 0}};
+  int ovr[2][2] = {{0, 0}, {0, 0}};  // wave totals (quant_w)
   int ovo[2][2] = {{0, 0}, {0, 0}};
+  const bool relu = LBT_FL(kFRelu, a.relu != 0), ystore = LBT_FL(kFY, a.y != nullptr);
+  const bool u8 = LBT_FL(kFU8, a.o1_kind == LBT_OUT_U8OFF && (!o2 || a.o2_kind == LBT_OUT_U8OFF));
 
-  const int64_t groups = a.inner >> 2;
-  if (g < groups) {
-    Noise4 nr[2];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) nr[b] = noise_for(b == 0 ? a.b1.qr : a.b2.qr, qr[b], g);
-    const Noise4 no1 = noise_for(a.qo1, so1, g);
-    const Noise4 no2 = noise_for(a.qo2, so2, g);
-    const int64_t r0 = (int64_t)blockIdx.y * rpt;
-    const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
-    for (int64_t rb = r0; rb < rend; rb += kRB) {
-      int qv[NB][kRB];
-      float4 xv[NB][kRB], rv[kRB];
+  for (int64_t rb = r0; rb < rend; rb += kRB) {
+    if (rb != r0) load_batch(rb);
+    if (live) {
 #pragma unroll
       for (int j = 0; j < kRB; ++j) {
+        if (rb + j >= rend) break;
         const int64_t e = (rb + j) * a.inner + (g << 2);
-        if (rb + j < rend) {
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int b = 0; b < NB; ++b) {
-            const lbt_chain_branch& B = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
-            if (B.nrm.q) qv[b][j] = ld_i8x4(B.nrm.q, e);
-            else xv[b][j] = ld_f32x4(B.xin, e);
+        for (int b = 0; b < NB; ++b) {
+          const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+          float t[4];
+          if (q_in[b]) {
+            int q[4];
+            unpack4_i8(qv[b][j], q);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float x1 = (float)q[k] * sn[b];
+              const float x2 = x1 - pm[b][k];
+              t[k] = div_by(x2, ps[b][k]);  // == x2 / sigma
+            }
+          } else {
+            f4(xv[b][j], t);
           }
-          if (a.res) rv[j] = ld_f32x4(a.res, e);
-        }
-      }
+          if ((F & kRt) ? qr[b].active : true) {
+            int R[4];
 #pragma unroll
-      for (int j = 0; j < kRB; ++j) {
-      if (rb + j >= rend) break;
-      const int64_t e = (rb + j) * a.inner + (g << 2);
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        const lbt_chain_branch& B = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
-        float t[4];
-        if (B.nrm.q) {
-          int q[4];
-          unpack4_i8(qv[b][j], q);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float x1 = (float)q[k] * sn[b];
-            const float x2 = x1 - pm[b][k];
-            t[k] = div_by(x2, ps[b][k]);  // == x2 / sigma
+            for (int k = 0; k < 4; ++k) {
+              R[k] = quant_w<ST>(qr[b], Bb.qr.stochastic, t[k], nr[b].u[k], ovr[b][0], ovr[b][1]);
+              const float xr = (float)R[k] * qr[b].inv_m;
+              const float m1 = xr * pg[b][k];
+              t[k] = m1 + pb[b][k];
+            }
+            if (LBT_FL(kFRout, Bb.rout != nullptr)) store4_i8(Bb.rout, e, R, 0);
           }
-        } else {
-          f4(xv[b][j], t);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = b ? v[k] + t[k] : t[k];
         }
-        if (qr[b].active) {
-          int R[4];
+        if (res) {
+          float rr[4];
+          f4(rv[j], rr);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            R[k] = quant1(qr[b], B.qr.stochastic, t[k], nr[b].u[k], ovr[b][0], ovr[b][1]);
-            const float xr = (float)R[k] * qr[b].inv_m;
-            const float m1 = xr * pg[b][k];
-            t[k] = m1 + pb[b][k];
-          }
-          if (B.rout) store4_i8(B.rout, e, R, 0);
+          for (int k = 0; k < 4; ++k) v[k] = v[k] + rr[k];
         }
+        if (relu) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = b ? v[k] + t[k] : t[k];
-      }
-      if (a.res) {
-        float rr[4];
-        f4(rv[j], rr);
+          for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+        }
+        if (ystore) store4_f32(a.y, e, v);
+        if (o1) {
+          int c[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = v[k] + rr[k];
-      }
-      if (a.relu) {
+          for (int k = 0; k < 4; ++k) c[k] = quant_w<ST>(so1, a.qo1.stochastic, v[k], no1.u[k], ovo[0][0], ovo[0][1]);
+          if (u8) store4_code(a.o1, LBT_OUT_U8OFF, e, c, 0.f);
+          else store4_code(a.o1, a.o1_kind, e, c, so1.inv_m);
+        }
+        if (o2) {
+          int c[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
-      }
-      if (a.y) store4_f32(a.y, e, v);
-      if (o1) {
-        int c[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = quant1(so1, a.qo1.stochastic, v[k], no1.u[k], ovo[0][0], ovo[0][1]);
-        store4_code(a.o1, a.o1_kind, e, c, so1.inv_m);
-      }
-      if (o2) {
-        int c[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = quant1(so2, a.qo2.stochastic, v[k], no2.u[k], ovo[1][0], ovo[1][1]);
-        store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
-      }
+          for (int k = 0; k < 4; ++k) c[k] = quant_w<ST>(so2, a.qo2.stochastic, v[k], no2.u[k], ovo[1][0], ovo[1][1]);
+          if (u8) store4_code(a.o2, LBT_OUT_U8OFF, e, c, 0.f);
+          else store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
+        }
       }
     }
   }
@@ -245,10 +280,10 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
   // every quantiser's counters behind one barrier
   const bool st[4] = {qr[0].active && a.b1.qr.counts, NB > 1 && qr[NB - 1].active && a.b2.qr.counts,
                       o1 && a.qo1.counts, o2 && a.qo2.counts};
-  if (st[0]) counts_stage(0, 4, ovr[0][0], ovr[0][1], sh_cnt);
-  if (st[1]) counts_stage(1, 4, ovr[NB - 1][0], ovr[NB - 1][1], sh_cnt);
-  if (st[2]) counts_stage(2, 4, ovo[0][0], ovo[0][1], sh_cnt);
-  if (st[3]) counts_stage(3, 4, ovo[1][0], ovo[1][1], sh_cnt);
+  if (st[0]) counts_stage_w(0, 4, ovr[0][0], ovr[0][1], sh_cnt);
+  if (st[1]) counts_stage_w(1, 4, ovr[NB - 1][0], ovr[NB - 1][1], sh_cnt);
+  if (st[2]) counts_stage_w(2, 4, ovo[0][0], ovo[0][1], sh_cnt);
+  if (st[3]) counts_stage_w(3, 4, ovo[1][0], ovo[1][1], sh_cnt);
   if (!(st[0] || st[1] || st[2] || st[3])) return;
   __syncthreads();
   if (st[0]) counts_publish(0, 4, a.b1.qr, sh_cnt);
@@ -259,28 +294,75 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
 }
 
 // ============================================================================ backward pass A
-template <int NB>
+enum : int {
+  kAYMask = 1,   // ReLU mask from the fp32 forward output y_mask
+  kAMaskR = 2,   // ReLU mask recomputed from the Rescale_q codes of branch 1
+  kAGmask = 4,   // store the masked fp32 gradient
+  kAStoch = 8,   // every quantiser stochastic
+  kAFB = 16,     // every branch: both quantisers active, int8 G codes and sums out
+};
+
+template <int NB, int F>
 __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a, int rpt) {
   extern __shared__ float shf[];  // per branch: gq, bq [C]; then long long sums[2][4C]
   __shared__ int sh_cnt[8 * kThreads / 64];
+  constexpr int ST = (F & kRt) ? -1 : ((F & kAStoch) ? 1 : 0);
   const int C = a.C;
   long long* S = reinterpret_cast<long long*>(shf + 4 * C);  // [2][4C]
+  const int64_t groups = a.inner >> 2;
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool live = g < groups;
+  const int64_t gl = live ? g : 0;
+  const int c0 = (int)(((uint32_t)gl << 2) % (uint32_t)C);
+  const int64_t r0 = (int64_t)blockIdx.y * rpt;
+  const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+  const bool ymask = LBT_FL(kAYMask, a.y_mask != nullptr);
+  const bool maskr = LBT_FL(kAMaskR, a.y_mask == nullptr && a.mask_from_r);
   QState qrg[2], qng[2], qr[2];
+  bool arg[2], ang[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
-    qrg[b] = qstate(B.qrg);
-    qng[b] = qstate(B.qng);
-    qr[b] = qstate(B.qr);
-    if (B.gb)
-      for (int c = threadIdx.x; c < C; c += kThreads) { shf[b * 2 * C + c] = B.gb[c]; shf[b * 2 * C + C + c] = B.gb[C + c]; }
+    const lbt_bwd_branch& Bb = b == 0 ? a.b1 : a.b2;
+    qrg[b] = qstate(Bb.qrg);
+    qng[b] = qstate(Bb.qng);
+    qr[b] = qstate(Bb.qr);
+    arg[b] = LBT_FL(kAFB, qrg[b].active);
+    ang[b] = LBT_FL(kAFB, qng[b].active);
+  }
+  const bool r1 = LBT_FL(kAFB, a.b1.R != nullptr);
+
+  // ---- first rows + noise before the (short) prologue
+  float4 gv4[kRB], ym4[kRB];
+  int R1v[kRB], R2v[kRB], qnv[2][kRB];
+  auto load_batch = [&](int64_t rb) {
+#pragma unroll
+    for (int j = 0; j < kRB; ++j) {
+      const int64_t e = (rb + j < rend ? rb + j : r0) * a.inner + (gl << 2);
+      gv4[j] = ld_f32x4(a.g, e);
+      R1v[j] = r1 ? ld_i8x4(a.b1.R, e) : 0;
+      if (ymask) ym4[j] = ld_f32x4(a.y_mask, e);
+      if (NB > 1 && arg[NB - 1]) R2v[j] = ld_i8x4(a.b2.R, e);
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (ang[b]) qnv[b][j] = ld_i8x4(b == 0 ? a.b1.qn_codes : a.b2.qn_codes, e);
+    }
+  };
+  load_batch(r0);
+  Noise4 nrg[2], nng[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& Bb = b == 0 ? a.b1 : a.b2;
+    nrg[b] = noise_for(Bb.qrg, qrg[b], gl);
+    nng[b] = noise_for(Bb.qng, qng[b], gl);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& Bb = b == 0 ? a.b1 : a.b2;
+    if (Bb.gb)
+      for (int c = threadIdx.x; c < C; c += kThreads) { shf[b * 2 * C + c] = Bb.gb[c]; shf[b * 2 * C + C + c] = Bb.gb[C + c]; }
   }
   for (int i = threadIdx.x; i < 8 * C; i += kThreads) S[i] = 0;
   __syncthreads();
-  int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};  // [branch][rescale|norm][c1|c2]
-  const int64_t groups = a.inner >> 2;
-  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int c0 = (int)(((uint32_t)g << 2) % (uint32_t)C);
   float gam[2][4], bet[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -288,6 +370,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
     for (int b = 0; b < NB; ++b) gam[b][k] = shf[b * 2 * C + c0 + k];
     bet[k] = shf[C + c0 + k];
   }
+  int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};  // [branch][rescale|norm][c1|c2], wave totals
   int acc[2][4][4];  // [branch][sum][k]
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -295,86 +378,64 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc[b][s][k] = 0;
-  if (g < groups) {
-    Noise4 nrg[2], nng[2];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
-      nrg[b] = noise_for(B.qrg, qrg[b], g);
-      nng[b] = noise_for(B.qng, qng[b], g);
-    }
-    const int64_t r0 = (int64_t)blockIdx.y * rpt;
-    const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
-    for (int64_t rb = r0; rb < rend; rb += kRB) {
-      float4 gv4[kRB], ym4[kRB];
-      int R1v[kRB], R2v[kRB], qnv[2][kRB];
+  const bool gmask = LBT_FL(kAGmask, a.gmask_out != nullptr);
+
+  for (int64_t rb = r0; rb < rend; rb += kRB) {
+    if (rb != r0) load_batch(rb);
+    if (live) {
 #pragma unroll
       for (int j = 0; j < kRB; ++j) {
+        if (rb + j >= rend) break;
         const int64_t e = (rb + j) * a.inner + (g << 2);
-        R1v[j] = 0;
-        if (rb + j < rend) {
-          gv4[j] = ld_f32x4(a.g, e);
-          if (a.b1.R) R1v[j] = ld_i8x4(a.b1.R, e);
-          if (a.y_mask) ym4[j] = ld_f32x4(a.y_mask, e);
-          if (NB > 1 && qrg[NB - 1].active) R2v[j] = ld_i8x4(a.b2.R, e);
+        float gv[4];
+        f4(gv4[j], gv);
+        int R1[4];
+        unpack4_i8(R1v[j], R1);
+        if (ymask) {
+          float ym[4];
+          f4(ym4[j], ym);
 #pragma unroll
-          for (int b = 0; b < NB; ++b)
-            if (qng[b].active) qnv[b][j] = ld_i8x4(b == 0 ? a.b1.qn_codes : a.b2.qn_codes, e);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kRB; ++j) {
-      if (rb + j >= rend) break;
-      const int64_t e = (rb + j) * a.inner + (g << 2);
-      float gv[4];
-      f4(gv4[j], gv);
-      int R1[4];
-      unpack4_i8(R1v[j], R1);
-      if (a.y_mask) {
-        float ym[4];
-        f4(ym4[j], ym);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) gv[k] = ym[k] > 0.f ? gv[k] : 0.f;
-      } else if (a.mask_from_r) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float xr = (float)R1[k] * qr[0].inv_m;
-          const float m1 = xr * gam[0][k];
-          const float yv = m1 + bet[k];
-          gv[k] = yv > 0.f ? gv[k] : 0.f;
-        }
-      }
-      if (a.gmask_out) store4_f32(a.gmask_out, e, gv);
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
-        float d[4] = {gv[0], gv[1], gv[2], gv[3]};
-        if (qrg[b].active) {
-          int R[4] = {R1[0], R1[1], R1[2], R1[3]};
-          if (b) unpack4_i8(R2v[j], R);
+          for (int k = 0; k < 4; ++k) gv[k] = ym[k] > 0.f ? gv[k] : 0.f;
+        } else if (maskr) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const int G2 = quant1(qrg[b], B.qrg.stochastic, d[k], nrg[b].u[k], ov[b][0][0], ov[b][0][1]);
-            acc[b][0][k] += G2 * R[k];
-            acc[b][1][k] += G2;
-            const float gh = (float)G2 * qrg[b].inv_m;
-            d[k] = gh * gam[b][k];
+            const float xr = (float)R1[k] * qr[0].inv_m;
+            const float m1 = xr * gam[0][k];
+            const float yv = m1 + bet[k];
+            gv[k] = yv > 0.f ? gv[k] : 0.f;
           }
         }
-        if (qng[b].active) {
-          int G[4], qn[4];
-          unpack4_i8(qnv[b][j], qn);
+        if (gmask) store4_f32(a.gmask_out, e, gv);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            G[k] = quant1(qng[b], B.qng.stochastic, d[k], nng[b].u[k], ov[b][1][0], ov[b][1][1]);
-            acc[b][2][k] += G[k];
-            acc[b][3][k] += G[k] * qn[k];
+        for (int b = 0; b < NB; ++b) {
+          const lbt_bwd_branch& Bb = b == 0 ? a.b1 : a.b2;
+          float d[4] = {gv[0], gv[1], gv[2], gv[3]};
+          if (arg[b]) {
+            int R[4] = {R1[0], R1[1], R1[2], R1[3]};
+            if (b) unpack4_i8(R2v[j], R);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int G2 = quant_w<ST>(qrg[b], Bb.qrg.stochastic, d[k], nrg[b].u[k], ov[b][0][0], ov[b][0][1]);
+              acc[b][0][k] += G2 * R[k];
+              acc[b][1][k] += G2;
+              const float gh = (float)G2 * qrg[b].inv_m;
+              d[k] = gh * gam[b][k];
+            }
           }
-          store4_i8(B.gout, e, G, 0);
-        } else if (B.dout) {
-          store4_f32(B.dout, e, d);
+          if (ang[b]) {
+            int G[4], qn[4];
+            unpack4_i8(qnv[b][j], qn);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              G[k] = quant_w<ST>(qng[b], Bb.qng.stochastic, d[k], nng[b].u[k], ov[b][1][0], ov[b][1][1]);
+              acc[b][2][k] += G[k];
+              acc[b][3][k] += G[k] * qn[k];
+            }
+            store4_i8(Bb.gout, e, G, 0);
+          } else if (Bb.dout) {
+            store4_f32(Bb.dout, e, d);
+          }
         }
-      }
       }
     }
   }
@@ -393,57 +454,82 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
-    if (qrg[b].active && B.qrg.counts) counts_stage(2 * b, 4, ov[b][0][0], ov[b][0][1], sh_cnt);
-    if (qng[b].active && B.qng.counts) counts_stage(2 * b + 1, 4, ov[b][1][0], ov[b][1][1], sh_cnt);
+    const lbt_bwd_branch& Bb = b == 0 ? a.b1 : a.b2;
+    if (qrg[b].active && Bb.qrg.counts) counts_stage_w(2 * b, 4, ov[b][0][0], ov[b][0][1], sh_cnt);
+    if (qng[b].active && Bb.qng.counts) counts_stage_w(2 * b + 1, 4, ov[b][1][0], ov[b][1][1], sh_cnt);
   }
   __syncthreads();  // the only barrier after the main loop: LDS sums and counters complete
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const lbt_bwd_branch& B = b == 0 ? a.b1 : a.b2;
-    if (qrg[b].active) counts_publish(2 * b, 4, B.qrg, sh_cnt);
-    if (qng[b].active) counts_publish(2 * b + 1, 4, B.qng, sh_cnt);
-    if (B.sums) block_flush_sums(S + b * 4 * C, 4 * C, B.sums, 4 * C);
+    const lbt_bwd_branch& Bb = b == 0 ? a.b1 : a.b2;
+    if (qrg[b].active) counts_publish(2 * b, 4, Bb.qrg, sh_cnt);
+    if (qng[b].active) counts_publish(2 * b + 1, 4, Bb.qng, sh_cnt);
+    if (Bb.sums) block_flush_sums(S + b * 4 * C, 4 * C, Bb.sums, 4 * C);
   }
 }
 
 // ============================================================================ backward pass B
+enum : int {
+  kBQ = 1,      // quantised gq output (else fp32 dx)
+  kBGcol = 2,   // per-channel sums of gq
+  kBStoch = 4,  // stochastic output quantiser
+  kBDx = 8,     // fp32 dx output
+};
+
+template <int F>
 __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a, int rpt) {
   extern __shared__ float shf[];  // mu, sigma, mg, mgx [C]; then long long tmp[2C] / colsum[2C]
   __shared__ int sh_cnt[8 * kThreads / 64];
+  constexpr int ST = (F & kRt) ? -1 : ((F & kBStoch) ? 1 : 0);
   const int C = a.C;
   float* mu = shf;
   float* sg = shf + C;
   float* mg = shf + 2 * C;
   float* mgx = shf + 3 * C;
   long long* tmp = reinterpret_cast<long long*>(shf + 4 * C);
+  const int64_t groups = a.inner >> 2;
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool live = g < groups;
+  const int64_t gl = live ? g : 0;
+  const int c0 = (int)(((uint32_t)gl << 2) % (uint32_t)C);
+  const int64_t r0 = (int64_t)blockIdx.y * rpt;
+  const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
+  // ---- first rows + noise before the moment prologue
+  int Gv[kRB], qv[kRB];
+  auto load_batch = [&](int64_t rb) {
+#pragma unroll
+    for (int j = 0; j < kRB; ++j) {
+      const int64_t e = (rb + j < rend ? rb + j : r0) * a.inner + (gl << 2);
+      Gv[j] = ld_i8x4(a.G, e);
+      qv[j] = ld_i8x4(a.qn_codes, e);
+    }
+  };
+  load_batch(r0);
+  const QState sgq = qstate(a.qng), sn = qstate(a.qn), so = qstate(a.qo);
+  const bool want_q = LBT_FL(kBQ, a.gq && so.active);
+  const Noise4 no = noise_for(a.qo, so, gl);
   // SG at sums[2C:3C), SGQ at sums[3C:4C) of each shard
   for (int i = threadIdx.x; i < 2 * C; i += kThreads) {
     long long s = 0;
+#pragma unroll 8
     for (int k = 0; k < LBT_NSHARD; ++k) s += a.sums[(int64_t)k * 4 * C + 2 * C + i];
     tmp[i] = s;
   }
   __syncthreads();
-  const QState sgq = qstate(a.qng), sn = qstate(a.qn), so = qstate(a.qo);
   {
-    const double s = (double)sn.inv_m, g = (double)sgq.inv_m, n = (double)a.n;
+    const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, n = (double)a.n;
     for (int c = threadIdx.x; c < C; c += kThreads) {
       const float m = a.ms[c], sig = a.ms[C + c];
       mu[c] = m;
       sg[c] = sig;
       const double SG = (double)tmp[c], SGQ = (double)tmp[C + c];
-      mg[c] = (float)(g * SG / n);
-      mgx[c] = (float)(g * (s * SGQ - (double)m * SG) / (n * (double)sig));
+      mg[c] = (float)(gsc * SG / n);
+      mgx[c] = (float)(gsc * (s * SGQ - (double)m * SG) / (n * (double)sig));
     }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 2 * C; i += kThreads) tmp[i] = 0;
   __syncthreads();
-  const bool want_q = a.gq && so.active;
-  int ov1 = 0, ov2 = 0;
-  const int64_t groups = a.inner >> 2;
-  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int c0 = (int)(((uint32_t)g << 2) % (uint32_t)C);
   float rmu[4], rmg[4], rmgx[4];
   Recip rsg[4];
 #pragma unroll
@@ -453,54 +539,46 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
     rmg[k] = mg[c0 + k];
     rmgx[k] = mgx[c0 + k];
   }
+  int ov1 = 0, ov2 = 0;  // wave totals
   int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-  if (g < groups) {
-    const Noise4 no = noise_for(a.qo, so, g);
-    const int64_t r0 = (int64_t)blockIdx.y * rpt;
-    const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
-    for (int64_t rb = r0; rb < rend; rb += kRB) {
-      int Gv[kRB], qv[kRB];
+  const bool dxo = LBT_FL(kBDx, a.dx != nullptr);
+  for (int64_t rb = r0; rb < rend; rb += kRB) {
+    if (rb != r0) load_batch(rb);
+    if (live) {
 #pragma unroll
       for (int j = 0; j < kRB; ++j) {
+        if (rb + j >= rend) break;
         const int64_t e = (rb + j) * a.inner + (g << 2);
-        if (rb + j < rend) {
-          Gv[j] = ld_i8x4(a.G, e);
-          qv[j] = ld_i8x4(a.qn_codes, e);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kRB; ++j) {
-      if (rb + j >= rend) break;
-      const int64_t e = (rb + j) * a.inner + (g << 2);
-      int G[4], q[4];
-      unpack4_i8(Gv[j], G);
-      unpack4_i8(qv[j], q);
-      float dx[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float x1 = (float)q[k] * sn.inv_m;
-        const float x2 = x1 - rmu[k];
-        const float xh = div_by(x2, rsg[k]);  // == x2 / sigma
-        const float gh = (float)G[k] * sgq.inv_m;
-        const float t1 = gh - rmg[k];
-        const float t2 = xh * rmgx[k];
-        dx[k] = div_by(t1 - t2, rsg[k]);      // == (t1 - t2) / sigma
-      }
-      if (a.dx) store4_f32(a.dx, e, dx);
-      if (want_q) {
-        int c[4];
+        int G[4], q[4];
+        unpack4_i8(Gv[j], G);
+        unpack4_i8(qv[j], q);
+        float dx[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          c[k] = quant1(so, a.qo.stochastic, dx[k], no.u[k], ov1, ov2);
-          s1[k] += c[k];
-          s2[k] += c[k] * c[k];
+          const float x1 = (float)q[k] * sn.inv_m;
+          const float x2 = x1 - rmu[k];
+          const float xh = div_by(x2, rsg[k]);  // == x2 / sigma
+          const float gh = (float)G[k] * sgq.inv_m;
+          const float t1 = gh - rmg[k];
+          const float t2 = xh * rmgx[k];
+          dx[k] = div_by(t1 - t2, rsg[k]);      // == (t1 - t2) / sigma
         }
-        store4_i8(a.gq, e, c, 0);
-      }
+        if (dxo) store4_f32(a.dx, e, dx);
+        if (want_q) {
+          int c[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            c[k] = quant_w<ST>(so, a.qo.stochastic, dx[k], no.u[k], ov1, ov2);
+            s1[k] += c[k];
+            s2[k] += c[k] * c[k];
+          }
+          store4_i8(a.gq, e, c, 0);
+        }
       }
     }
   }
-  if (want_q && a.gcolsum) {
+  const bool gcol = LBT_FL(kBGcol, a.gcolsum != nullptr);
+  if (want_q && gcol) {
     const int per = chan_period(C);
     const bool own = chan_owner(per);
 #pragma unroll
@@ -511,10 +589,10 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
     }
   }
   if (!want_q) return;
-  if (a.qo.counts) counts_stage(0, 1, ov1, ov2, sh_cnt);
+  if (a.qo.counts) counts_stage_w(0, 1, ov1, ov2, sh_cnt);
   __syncthreads();
   counts_publish(0, 1, a.qo, sh_cnt);
-  if (a.gcolsum) block_flush_sums(tmp, 2 * C, a.gcolsum, 2 * C);
+  if (gcol) block_flush_sums(tmp, 2 * C, a.gcolsum, 2 * C);
 }
 
 __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
@@ -559,16 +637,98 @@ bool shape_ok(int64_t rows, int64_t inner, int C) {
 
 LBT_TRACE_SETTER(bn)
 
+// ---- host-side variant selection: the descriptor's configuration as a flag word, or kRt when
+// it is not uniform across branches / quantisers.
+namespace {
+
+int tri(bool all, bool none) { return all ? 1 : (none ? 0 : -1); }
+
+int fwd_flags(const lbt_chain_fwd& a) {
+  const int nb = a.has_b2 ? 2 : 1;
+  const lbt_chain_branch* br[2] = {&a.b1, &a.b2};
+  bool q_all = true, q_none = true, r_all = true, r_none = true, act = true;
+  bool st_all = true, st_none = true;
+  for (int b = 0; b < nb; ++b) {
+    q_all &= br[b]->nrm.q != nullptr; q_none &= br[b]->nrm.q == nullptr;
+    r_all &= br[b]->rout != nullptr; r_none &= br[b]->rout == nullptr;
+    act &= br[b]->qr.bits > 0;
+    st_all &= br[b]->qr.stochastic != 0; st_none &= br[b]->qr.stochastic == 0;
+  }
+  const bool o1 = a.o1 && a.qo1.bits > 0, o2 = a.o2 && a.qo2.bits > 0;
+  if (o1) { st_all &= a.qo1.stochastic != 0; st_none &= a.qo1.stochastic == 0; }
+  if (o2) { st_all &= a.qo2.stochastic != 0; st_none &= a.qo2.stochastic == 0; }
+  const int q = tri(q_all, q_none), r = tri(r_all, r_none), st = tri(st_all, st_none);
+  if (q < 0 || r < 0 || st < 0 || !act) return kRt;
+  int f = 0;
+  if (q) f |= kFQ;
+  if (r) f |= kFRout;
+  if (a.res) f |= kFRes;
+  if (a.relu) f |= kFRelu;
+  if (a.y) f |= kFY;
+  if (o1) f |= kFO1;
+  if (o2) f |= kFO2;
+  if (st) f |= kFStoch;
+  if ((o1 || o2) && (!o1 || a.o1_kind == LBT_OUT_U8OFF) && (!o2 || a.o2_kind == LBT_OUT_U8OFF)) f |= kFU8;
+  return f;
+}
+
+int bwd_a_flags(const lbt_chain_bwd_a& a) {
+  const int nb = a.has_b2 ? 2 : 1;
+  const lbt_bwd_branch* br[2] = {&a.b1, &a.b2};
+  bool fb = a.b1.R != nullptr, st_all = true, st_none = true;
+  for (int b = 0; b < nb; ++b) {
+    const lbt_bwd_branch& B = *br[b];
+    fb &= B.qrg.bits > 0 && B.qng.bits > 0 && B.gout && B.sums && B.R && !B.dout && B.qn_codes;
+    st_all &= B.qrg.stochastic != 0 && B.qng.stochastic != 0;
+    st_none &= B.qrg.stochastic == 0 && B.qng.stochastic == 0;
+  }
+  if (!fb) return kRt;
+  int f = kAFB;
+  if (a.y_mask) f |= kAYMask;
+  else if (a.mask_from_r) f |= kAMaskR;
+  if (a.gmask_out) f |= kAGmask;
+  if (st_all) f |= kAStoch;
+  else if (!st_none) return kRt;
+  return f;
+}
+
+int bwd_b_flags(const lbt_chain_bwd_b& a) {
+  int f = 0;
+  if (a.gq && a.qo.bits > 0) f |= kBQ | (a.qo.stochastic ? kBStoch : 0);
+  if (a.gcolsum) f |= kBGcol;
+  if (a.dx) f |= kBDx;
+  return f;
+}
+
+constexpr int kFwdBlk = kFQ | kFRout | kFRelu | kFStoch;  // every fused-plan forward chain
+
+}  // namespace
+
 extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   if (!shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;
   dim3 grid;
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
   const size_t shm = sizeof(float) * 8 * a->C + sizeof(long long) * 2 * a->C;
+  hipStream_t st = (hipStream_t)stream;
+  const int f = fwd_flags(*a);
+#define LBT_CF(NB, FL)                                                                            \
+  if (a->has_b2 == (NB == 2) && f == (FL)) {                                                      \
+    hipLaunchKernelGGL((chain_fwd_kernel<NB, FL>), grid, dim3(kThreads), shm, st, *a, rpt);       \
+    return (int)hipGetLastError();                                                                \
+  }
+  LBT_CF(1, kFwdBlk | kFY | kFO1 | kFU8)                  // stem: bn0 -> relu -> X0 + block-0 input
+  LBT_CF(1, kFwdBlk | kFO1 | kFU8)                        // block, first BN: -> conv-2 input
+  LBT_CF(1, kFwdBlk | kFRes | kFY | kFO1 | kFU8)          // block end, identity shortcut
+  LBT_CF(1, kFwdBlk | kFRes | kFY | kFO1 | kFO2 | kFU8)   // ... next block downsamples
+  LBT_CF(1, kFwdBlk | kFRes | kFY)                        // last block
+  LBT_CF(2, kFwdBlk | kFY | kFO1 | kFU8)                  // block end, projection shortcut
+  LBT_CF(2, kFwdBlk | kFY | kFO1 | kFO2 | kFU8)
+#undef LBT_CF
   if (a->has_b2)
-    hipLaunchKernelGGL(chain_fwd_kernel<2>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+    hipLaunchKernelGGL((chain_fwd_kernel<2, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
   else
-    hipLaunchKernelGGL(chain_fwd_kernel<1>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+    hipLaunchKernelGGL((chain_fwd_kernel<1, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
   return (int)hipGetLastError();
 }
 
@@ -578,10 +738,22 @@ extern "C" int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream) {
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
   const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 8 * a->C;
+  hipStream_t st = (hipStream_t)stream;
+  const int f = bwd_a_flags(*a);
+#define LBT_CA(NB, FL)                                                                            \
+  if (a->has_b2 == (NB == 2) && f == (FL)) {                                                      \
+    hipLaunchKernelGGL((chain_bwd_a_kernel<NB, FL>), grid, dim3(kThreads), shm, st, *a, rpt);     \
+    return (int)hipGetLastError();                                                                \
+  }
+  LBT_CA(1, kAFB | kAStoch | kAYMask | kAGmask)  // block end, identity shortcut
+  LBT_CA(1, kAFB | kAStoch | kAYMask)            // stem
+  LBT_CA(1, kAFB | kAStoch | kAMaskR)            // block, first BN (mask recomputed from R)
+  LBT_CA(2, kAFB | kAStoch | kAYMask)            // block end, projection shortcut
+#undef LBT_CA
   if (a->has_b2)
-    hipLaunchKernelGGL(chain_bwd_a_kernel<2>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+    hipLaunchKernelGGL((chain_bwd_a_kernel<2, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
   else
-    hipLaunchKernelGGL(chain_bwd_a_kernel<1>, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+    hipLaunchKernelGGL((chain_bwd_a_kernel<1, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
   return (int)hipGetLastError();
 }
 
@@ -591,7 +763,14 @@ extern "C" int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream) {
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
   const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 2 * a->C;
-  hipLaunchKernelGGL(chain_bwd_b_kernel, grid, dim3(kThreads), shm, (hipStream_t)stream, *a, rpt);
+  hipStream_t st = (hipStream_t)stream;
+  const int f = bwd_b_flags(*a);
+  if (f == (kBQ | kBStoch | kBGcol))
+    hipLaunchKernelGGL((chain_bwd_b_kernel<kBQ | kBStoch | kBGcol>), grid, dim3(kThreads), shm, st, *a, rpt);
+  else if (f == (kBQ | kBStoch))
+    hipLaunchKernelGGL((chain_bwd_b_kernel<kBQ | kBStoch>), grid, dim3(kThreads), shm, st, *a, rpt);
+  else
+    hipLaunchKernelGGL((chain_bwd_b_kernel<kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
   return (int)hipGetLastError();
 }
 

@@ -164,6 +164,37 @@ static __device__ int32_t kZeroBlock[64];  // zero-initialised, never written (g
 LBT_DEV const float* zf() { return reinterpret_cast<const float*>(kZeroBlock); }
 LBT_DEV const int32_t* zi() { return kZeroBlock; }
 
+// Same quantiser, overflow predicates counted per WAVE: the compares become lane masks and
+// s_bcnt1 / s_add on the scalar unit accumulate them, so ov1w / ov2w are wave totals (identical in
+// every lane) and cost no VALU beyond the compares. STOCH is the rounding mode when known.
+template <int STOCH>  // 1 stochastic, 0 nearest, -1 from `stochastic`
+LBT_DEV int quant_w(const QState& s, int stochastic, float x, float u, int& ov1w, int& ov2w) {
+  const float xm = x * s.m;
+  ov1w += __popcll(__ballot((xm >= s.L) | (xm < -s.L)));
+  ov2w += __popcll(__ballot((xm >= s.Lh) | (xm < -s.Lh)));
+  const bool st = STOCH < 0 ? stochastic != 0 : STOCH == 1;
+  float v = st ? (xm + u) : xm;
+  v = fminf(fmaxf(v, -s.L), s.Lm1);
+  v = st ? floorf(v) : rintf(v);
+  return (int)v;
+}
+
+// Wave-total counters (from quant_w) of quantiser i of nq into the block's LDS staging area.
+// A lane inactive during some quant_w calls holds a partial total: the wave max is the total
+// (callers keep at least one lane active through every call). All 64 lanes must call it.
+LBT_DEV void counts_stage_w(int i, int nq, int ov1w, int ov2w, int* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ov1w = max(ov1w, __shfl_xor(ov1w, o, 64));
+    ov2w = max(ov2w, __shfl_xor(ov2w, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    int* p = sh + (threadIdx.x >> 6) * 2 * nq + 2 * i;
+    p[0] = ov1w;
+    p[1] = ov2w;
+  }
+}
+
 // ------------------------------------------------------------------ reductions
 LBT_DEV int wave_sum_i32(int v) {
 #pragma unroll
