@@ -252,6 +252,16 @@ typedef struct lbt_chain_bwd_a {
 } lbt_chain_bwd_a;
 int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream);
 
+/* Conv2d_q backward dX (as lbt_conv_dgrad_i8) fused with the pass A that consumes it: the
+ * dgrad output is never written; each output element e of [N,H,W,Cin] enters chain a as
+ * g[e] = dx[e] (+ add_src[e], the residual gradient, if add_src != NULL), with a->g ignored
+ * and a->rows = N, a->inner = H*W*Cin, a->C = Cin. Bit-identical to lbt_conv_dgrad_i8 followed
+ * by lbt_bn_chain_bwd_a. Supported chains (else LBT_EINVAL -- run the pair): 1 or 2 branches,
+ * each with both (stochastic, noise-table) quantisers, int8 G codes and sums; ReLU mask from
+ * y_mask or from branch-1 R; optional gmask_out.                                          */
+int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                            lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream);
+
 /* Pass B (the rest of Normalization_q.backward): with SG = sum G, SGQ = sum G*q from pass A,
  *   mg = sg*SG/n, mgx = sg*(s*SGQ - mu*SG)/(n*sigma)   (double -> fp32)
  *   dx = (((float)G*sg - mg) - xhat*mgx) / sigma,  xhat = ((float)q*s - mu)/sigma

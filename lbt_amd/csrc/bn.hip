@@ -10,7 +10,7 @@
 // independent of the launch geometry.
 #include <cstdlib>
 
-#include "dfxp_device.h"
+#include "chain_flags.h"
 
 using namespace lbt;
 
@@ -109,20 +109,6 @@ LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long 
 // Kernel variants: F holds the chain's configuration as compile-time flags for the combinations
 // the fused ResNet plan launches (no per-element branches, constant rounding mode and output
 // encoding); kRt selects the variant that reads everything from the descriptor at run time.
-enum : int {
-  kRt = 1 << 20,
-  // forward
-  kFQ = 1,       // branch inputs are int8 Normalization_q codes (else fp32 xin)
-  kFRout = 2,    // store the Rescale_q codes R
-  kFRes = 4,     // residual add
-  kFRelu = 8,
-  kFY = 16,      // store fp32 y
-  kFO1 = 32,     // first output quantiser
-  kFO2 = 64,     // second output quantiser
-  kFStoch = 128, // every quantiser stochastic
-  kFU8 = 256,    // outputs in the unsigned 9-bit offset encoding
-};
-#define LBT_FL(bit, rt) ((F & kRt) ? (rt) : ((F & (bit)) != 0))
 
 template <int B>
 LBT_DEV const lbt_chain_branch& fbranch(const lbt_chain_fwd& a) { return B == 0 ? a.b1 : a.b2; }
@@ -294,19 +280,13 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
 }
 
 // ============================================================================ backward pass A
-enum : int {
-  kAYMask = 1,   // ReLU mask from the fp32 forward output y_mask
-  kAMaskR = 2,   // ReLU mask recomputed from the Rescale_q codes of branch 1
-  kAGmask = 4,   // store the masked fp32 gradient
-  kAStoch = 8,   // every quantiser stochastic
-  kAFB = 16,     // every branch: both quantisers active, int8 G codes and sums out
-};
 
 template <int NB, int F>
 __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a, int rpt) {
   extern __shared__ float shf[];  // per branch: gq, bq [C]; then long long sums[2][4C]
   __shared__ int sh_cnt[8 * kThreads / 64];
   constexpr int ST = (F & kRt) ? -1 : ((F & kAStoch) ? 1 : 0);
+  LBT_TS(0);
   const int C = a.C;
   long long* S = reinterpret_cast<long long*>(shf + 4 * C);  // [2][4C]
   const int64_t groups = a.inner >> 2;
@@ -363,6 +343,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
   }
   for (int i = threadIdx.x; i < 8 * C; i += kThreads) S[i] = 0;
   __syncthreads();
+  LBT_TS(1);
   float gam[2][4], bet[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -439,6 +420,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
       }
     }
   }
+  LBT_TS(2);
   {
     const int per = chan_period(C);
     const bool own = chan_owner(per);
@@ -466,21 +448,17 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
     if (qng[b].active) counts_publish(2 * b + 1, 4, Bb.qng, sh_cnt);
     if (Bb.sums) block_flush_sums(S + b * 4 * C, 4 * C, Bb.sums, 4 * C);
   }
+  LBT_TS(3);
 }
 
 // ============================================================================ backward pass B
-enum : int {
-  kBQ = 1,      // quantised gq output (else fp32 dx)
-  kBGcol = 2,   // per-channel sums of gq
-  kBStoch = 4,  // stochastic output quantiser
-  kBDx = 8,     // fp32 dx output
-};
 
 template <int F>
 __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a, int rpt) {
   extern __shared__ float shf[];  // mu, sigma, mg, mgx [C]; then long long tmp[2C] / colsum[2C]
   __shared__ int sh_cnt[8 * kThreads / 64];
   constexpr int ST = (F & kRt) ? -1 : ((F & kBStoch) ? 1 : 0);
+  LBT_TS(0);
   const int C = a.C;
   float* mu = shf;
   float* sg = shf + C;
@@ -530,6 +508,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
   __syncthreads();
   for (int i = threadIdx.x; i < 2 * C; i += kThreads) tmp[i] = 0;
   __syncthreads();
+  LBT_TS(1);
   float rmu[4], rmg[4], rmgx[4];
   Recip rsg[4];
 #pragma unroll
@@ -577,6 +556,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
       }
     }
   }
+  LBT_TS(2);
   const bool gcol = LBT_FL(kBGcol, a.gcolsum != nullptr);
   if (want_q && gcol) {
     const int per = chan_period(C);
@@ -593,6 +573,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
   __syncthreads();
   counts_publish(0, 1, a.qo, sh_cnt);
   if (gcol) block_flush_sums(tmp, 2 * C, a.gcolsum, 2 * C);
+  LBT_TS(3);
 }
 
 __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
@@ -619,7 +600,15 @@ bool grid_for(int64_t rows, int64_t inner, dim3& grid, int& rpt) {
     const char* e = getenv("LBT_CHAIN_BLOCKS");
     return (int64_t)(e ? atoi(e) : 512);
   }();
+  // a workgroup's fixed costs (moment prologue, counter / channel-sum flush) must amortise over
+  // enough rows: at least min_rpt per thread even if that leaves fewer than `target` workgroups
+  static const int64_t min_rpt = [] {
+    const char* e = getenv("LBT_CHAIN_MINRPT");
+    return (int64_t)(e ? atoi(e) : 1);
+  }();
   int64_t r = (gblocks * rows) / target;
+  if (r < min_rpt) r = min_rpt;
+  if (r > rows) r = rows;
   if (r < 1) r = 1;
   if (r > 64) r = 64;
   const int64_t yb = (rows + r - 1) / r;
@@ -637,68 +626,8 @@ bool shape_ok(int64_t rows, int64_t inner, int C) {
 
 LBT_TRACE_SETTER(bn)
 
-// ---- host-side variant selection: the descriptor's configuration as a flag word, or kRt when
-// it is not uniform across branches / quantisers.
+// ---- host-side variant selection (flag words: chain_flags.h)
 namespace {
-
-int tri(bool all, bool none) { return all ? 1 : (none ? 0 : -1); }
-
-int fwd_flags(const lbt_chain_fwd& a) {
-  const int nb = a.has_b2 ? 2 : 1;
-  const lbt_chain_branch* br[2] = {&a.b1, &a.b2};
-  bool q_all = true, q_none = true, r_all = true, r_none = true, act = true;
-  bool st_all = true, st_none = true;
-  for (int b = 0; b < nb; ++b) {
-    q_all &= br[b]->nrm.q != nullptr; q_none &= br[b]->nrm.q == nullptr;
-    r_all &= br[b]->rout != nullptr; r_none &= br[b]->rout == nullptr;
-    act &= br[b]->qr.bits > 0;
-    st_all &= br[b]->qr.stochastic != 0; st_none &= br[b]->qr.stochastic == 0;
-  }
-  const bool o1 = a.o1 && a.qo1.bits > 0, o2 = a.o2 && a.qo2.bits > 0;
-  if (o1) { st_all &= a.qo1.stochastic != 0; st_none &= a.qo1.stochastic == 0; }
-  if (o2) { st_all &= a.qo2.stochastic != 0; st_none &= a.qo2.stochastic == 0; }
-  const int q = tri(q_all, q_none), r = tri(r_all, r_none), st = tri(st_all, st_none);
-  if (q < 0 || r < 0 || st < 0 || !act) return kRt;
-  int f = 0;
-  if (q) f |= kFQ;
-  if (r) f |= kFRout;
-  if (a.res) f |= kFRes;
-  if (a.relu) f |= kFRelu;
-  if (a.y) f |= kFY;
-  if (o1) f |= kFO1;
-  if (o2) f |= kFO2;
-  if (st) f |= kFStoch;
-  if ((o1 || o2) && (!o1 || a.o1_kind == LBT_OUT_U8OFF) && (!o2 || a.o2_kind == LBT_OUT_U8OFF)) f |= kFU8;
-  return f;
-}
-
-int bwd_a_flags(const lbt_chain_bwd_a& a) {
-  const int nb = a.has_b2 ? 2 : 1;
-  const lbt_bwd_branch* br[2] = {&a.b1, &a.b2};
-  bool fb = a.b1.R != nullptr, st_all = true, st_none = true;
-  for (int b = 0; b < nb; ++b) {
-    const lbt_bwd_branch& B = *br[b];
-    fb &= B.qrg.bits > 0 && B.qng.bits > 0 && B.gout && B.sums && B.R && !B.dout && B.qn_codes;
-    st_all &= B.qrg.stochastic != 0 && B.qng.stochastic != 0;
-    st_none &= B.qrg.stochastic == 0 && B.qng.stochastic == 0;
-  }
-  if (!fb) return kRt;
-  int f = kAFB;
-  if (a.y_mask) f |= kAYMask;
-  else if (a.mask_from_r) f |= kAMaskR;
-  if (a.gmask_out) f |= kAGmask;
-  if (st_all) f |= kAStoch;
-  else if (!st_none) return kRt;
-  return f;
-}
-
-int bwd_b_flags(const lbt_chain_bwd_b& a) {
-  int f = 0;
-  if (a.gq && a.qo.bits > 0) f |= kBQ | (a.qo.stochastic ? kBStoch : 0);
-  if (a.gcolsum) f |= kBGcol;
-  if (a.dx) f |= kBDx;
-  return f;
-}
 
 constexpr int kFwdBlk = kFQ | kFRout | kFRelu | kFStoch;  // every fused-plan forward chain
 

@@ -118,3 +118,164 @@ LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, 
 }
 
 }  // namespace lbt
+
+// ============================================================================ pass-A epilogue
+// Pass A of the BatchNorm backward (bn.hip chain_bwd_a_kernel: ReLU mask, Rescale_q grad
+// quantiser + dgamma/dbeta sums, Normalization_q grad quantiser + its sums) applied to a dgrad
+// GEMM's outputs, so the fp32 gradient never goes to memory. Same arithmetic, element for
+// element, as the chain kernel; the lane owns one column (channel) of 4 * NTW outputs.
+#include "chain_flags.h"
+
+namespace lbt {
+
+template <int NT, int NB>
+struct ChainShared {
+  int cnt[2 * 4 * 4];                              // counters: 4 quantisers x 4 waves
+  int part[4][NB][4][16 * EpiGeom<NT>::NTW];       // per wave: the 4 channel sums per branch
+};
+
+// Operands of this lane's outputs, fetched with the GEMM operands (every load unconditional).
+template <int NT, int NB, int CF>
+struct ChainPre {
+  static constexpr int NTW = EpiGeom<NT>::NTW;
+  float add[NTW][4], ym[NTW][4];
+  int R[NB][NTW][4], qn[NB][NTW][4];
+  float urg[NB][NTW][4], ung[NB][NTW][4];
+  float gam[NB][NTW], bet[NTW];
+};
+
+template <int NT, int NB, int CF>
+LBT_DEV void chain_prefetch(const lbt_chain_bwd_a& c, const float* add_src, int64_t M, int ncol, uint32_t HW,
+                            int64_t mtile, int nt0, int lane, ChainPre<NT, NB, CF>& p) {
+  constexpr int NTW = EpiGeom<NT>::NTW;
+  const int r = lane & 15, kg = lane >> 4;
+  const float* as = add_src ? add_src : zf();
+  const uint32_t amask = add_src ? 0xffffffffu : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = mtile * 16 + 4 * kg + i;
+    const int64_t rr = row < M ? row : 0;
+    const uint32_t pix = (uint32_t)rr % HW;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int col = (nt0 + j) * 16 + r;
+      const int64_t e = rr * ncol + col;
+      const uint32_t ni = pix * (uint32_t)ncol + col;
+      p.add[j][i] = as[(uint32_t)e & amask];
+      if (CF & kAYMask) p.ym[j][i] = c.y_mask[e];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const lbt_bwd_branch& B = b == 0 ? c.b1 : c.b2;
+        p.R[b][j][i] = B.R[e];
+        p.qn[b][j][i] = B.qn_codes[e];
+        p.urg[b][j][i] = B.qrg.noise[ni];
+        p.ung[b][j][i] = B.qng.noise[ni];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int col = (nt0 + j) * 16 + r;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) p.gam[b][j] = (b == 0 ? c.b1 : c.b2).gb[col];
+    p.bet[j] = c.b1.gb[ncol + col];
+  }
+}
+
+// v: this lane's dgrad outputs (fp32, exactly the unfused kernel's dx values). Every thread of
+// the block calls it (one barrier).
+template <int NT, int NB, int CF>
+LBT_DEV void chain_epi(const lbt_chain_bwd_a& c, bool has_add, int64_t M, int ncol, int64_t mtile, int nt0, int wave,
+                       int lane, const float (&v)[EpiGeom<NT>::NTW][4], const ChainPre<NT, NB, CF>& p,
+                       ChainShared<NT, NB>& sh) {
+  constexpr int NTW = EpiGeom<NT>::NTW, WPM = EpiGeom<NT>::WPM, MTB = EpiGeom<NT>::MTB;
+  constexpr int ST = (CF & kAStoch) ? 1 : 0;
+  const int r = lane & 15, kg = lane >> 4;
+  QState qrg[2], qng[2];
+  float r_inv = 0.f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& B = b == 0 ? c.b1 : c.b2;
+    qrg[b] = qstate(B.qrg);
+    qng[b] = qstate(B.qng);
+  }
+  if (CF & kAMaskR) r_inv = qstate(c.b1.qr).inv_m;
+  int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};  // wave totals
+  int acc[NB][NTW][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[b][j][s] = 0;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int col = (nt0 + j) * 16 + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = mtile * 16 + 4 * kg + i;
+      if (row >= M) continue;
+      const int64_t e = row * ncol + col;
+      float g = has_add ? v[j][i] + p.add[j][i] : v[j][i];
+      if (CF & kAYMask) {
+        g = p.ym[j][i] > 0.f ? g : 0.f;
+      } else if (CF & kAMaskR) {
+        const float xr = (float)p.R[0][j][i] * r_inv;
+        const float m1 = xr * p.gam[0][j];
+        const float yv = m1 + p.bet[j];
+        g = yv > 0.f ? g : 0.f;
+      }
+      if (CF & kAGmask) c.gmask_out[e] = g;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const lbt_bwd_branch& B = b == 0 ? c.b1 : c.b2;
+        const int G2 = quant_w<ST>(qrg[b], B.qrg.stochastic, g, p.urg[b][j][i], ov[b][0][0], ov[b][0][1]);
+        acc[b][j][0] += G2 * p.R[b][j][i];
+        acc[b][j][1] += G2;
+        const float gh = (float)G2 * qrg[b].inv_m;
+        const float d = gh * p.gam[b][j];
+        const int G = quant_w<ST>(qng[b], B.qng.stochastic, d, p.ung[b][j][i], ov[b][1][0], ov[b][1][1]);
+        acc[b][j][2] += G;
+        acc[b][j][3] += G * p.qn[b][j][i];
+        B.gout[e] = (int8_t)G;
+      }
+    }
+  }
+  // column totals: lanes r, r+16, r+32, r+48 share a column
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        int t = acc[b][j][s];
+        t += __shfl_xor(t, 16, 64);
+        t += __shfl_xor(t, 32, 64);
+        if (kg == 0) sh.part[wave][b][s][j * 16 + r] = t;
+      }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& B = b == 0 ? c.b1 : c.b2;
+    if (B.qrg.counts) counts_stage_w(2 * b, 4, ov[b][0][0], ov[b][0][1], sh.cnt);
+    if (B.qng.counts) counts_stage_w(2 * b + 1, 4, ov[b][1][0], ov[b][1][1], sh.cnt);
+  }
+  __syncthreads();  // the only barrier
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& B = b == 0 ? c.b1 : c.b2;
+    counts_publish(2 * b, 4, B.qrg, sh.cnt);
+    counts_publish(2 * b + 1, 4, B.qng, sh.cnt);
+  }
+  // sums layout per shard: [4][C] (G2*R, G2, G, G*q) -- as chain_bwd_a's S
+  for (int t = threadIdx.x; t < NB * 4 * ncol; t += 256) {
+    const int b = t / (4 * ncol), rem = t - b * 4 * ncol, s = rem / ncol, col = rem - s * ncol;
+    const int wcol = (col >> 4) / NTW, lc = col - wcol * NTW * 16;
+    long long tot = 0;
+#pragma unroll
+    for (int mt = 0; mt < MTB; ++mt) tot += sh.part[mt * WPM + wcol][b][s][lc];
+    int64_t* dst = (b == 0 ? c.b1 : c.b2).sums;
+    if (tot) atomicAdd((unsigned long long*)&dst[(int64_t)shard_id() * 4 * ncol + rem], (unsigned long long)tot);
+  }
+}
+
+}  // namespace lbt

@@ -20,6 +20,7 @@
 // the tap-shifted X into LDS transposed ([channel][pixel]) and issues 16x16x64 MFMAs; each
 // workgroup owns a pixel range and one tap and writes an int32 partial (exact, no atomics).
 #include "conv_epilogue.h"
+#include "chain_flags.h"
 
 using namespace lbt;
 
@@ -47,13 +48,17 @@ struct GemmArgs {
   int64_t* ychsum;
   int64_t M;            // GEMM rows
   int ncol;             // GEMM cols
+  lbt_chain_bwd_a chain;  // dgrad epilogue = pass A of this chain (CF != 0)
 };
 
-template <int MODE, int CS, int NT>
-__global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD) ? 8 : 1) void conv_gemm_kernel(GemmArgs p) {
+template <int MODE, int CS, int NT, int CF = 0, int NB = 1>
+__global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0) ? 8 : 1) void conv_gemm_kernel(
+    GemmArgs p) {
   using G = EpiGeom<NT>;
   constexpr int NTW = G::NTW, WPM = G::WPM, MTB = G::MTB;
   __shared__ EpiShared<NT> sh;
+  __shared__ ChainShared<NT, (CF ? NB : 1)> csh;
+  ChainPre<NT, NB, CF> cp;
   LBT_TS(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int mt_local = wave / WPM;
@@ -143,7 +148,9 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD) ? 8 : 1) 
     const uint32_t cmask = (MODE == MODE_FWD && p.colsum) ? 0xffffffffu : 0u;
 #pragma unroll
     for (int j = 0; j < NTW; ++j) corr[j] = 128 * cs_src[((nt0 + j) * 16 + r) & cmask];
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (CF != 0) {
+      chain_prefetch<NT, NB, CF>(p.chain, p.add_src, p.M, p.ncol, (uint32_t)(OH * OW), mtile, nt0, lane, cp);
+    } else if constexpr (MODE == MODE_FWD) {
       epi_noise<NTW>(qo, mtile, nt0, lane, ea);
     } else {
       const float* as = p.add_src ? p.add_src : zf();
@@ -175,7 +182,9 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD) ? 8 : 1) 
     }
 #pragma unroll
     for (int j = 0; j < NTW; ++j) corr[j] = (MODE == MODE_FWD && p.colsum) ? 128 * p.colsum[(nt0 + j) * 16 + r] : 0;
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (CF != 0) {
+      chain_prefetch<NT, NB, CF>(p.chain, p.add_src, p.M, p.ncol, (uint32_t)(OH * OW), mtile, nt0, lane, cp);
+    } else if constexpr (MODE == MODE_FWD) {
       epi_noise<NTW>(qo, mtile, nt0, lane, ea);
     } else {
 #pragma unroll
@@ -196,6 +205,10 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD) ? 8 : 1) 
   for (int j = 0; j < NTW; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[j][i] = (float)(acc[j][i] + corr[j]) * scale;
+  if constexpr (CF != 0) {
+    chain_epi<NT, NB, CF>(p.chain, p.add_src != nullptr, p.M, p.ncol, mtile, nt0, wave, lane, v, cp, csh);
+    return;
+  }
   if (!want_q) {
     const bool addv = MODE == MODE_DGRAD && p.add_src;
 #pragma unroll
@@ -229,6 +242,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
   constexpr int CI = CSI * 16, CO = CSO * 16;
   __shared__ __attribute__((aligned(16))) int8_t lds[4][(CI + CO) * kLdsRow];
   __shared__ int red[CI * CO];
+  LBT_TS(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kg = lane >> 4;
   const int tap = blockIdx.y;
@@ -297,7 +311,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
+  LBT_TS(1);
   __syncthreads();
+  LBT_TS(2);
   // acc[a][b] element i: row = a*16 + 4*kg + i (ci), col = b*16 + r (co)
 #pragma unroll
   for (int a = 0; a < CSI; ++a)
@@ -308,6 +324,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
   __syncthreads();
   int32_t* dst = slab + ((int64_t)blockIdx.x * (d.KH * d.KW) + tap) * CI * CO;
   for (int i = threadIdx.x; i < CI * CO; i += kThreads) dst[i] = red[i];
+  LBT_TS(3);
 }
 
 // 256 threads = 32 outputs x 8 split groups; coalesced 128-B slab rows; exact int64 sums.
@@ -406,6 +423,55 @@ extern "C" int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd
   p.ychsum = nullptr;
   p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
   return launch_gemm<MODE_DGRAD>(p, cs, (hipStream_t)stream);
+}
+
+namespace {
+
+template <int CS, int NT, int CF, int NB>
+int launch_dgrad_chain(const GemmArgs& p, hipStream_t st) {
+  constexpr int MTB = EpiGeom<NT>::MTB;
+  const int64_t blocks = ((p.M + 15) / 16 + MTB - 1) / MTB;
+  hipLaunchKernelGGL((conv_gemm_kernel<MODE_DGRAD, CS, NT, CF, NB>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+constexpr int kAFused = kAFB | kAStoch;
+
+}  // namespace
+
+extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                                       lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream) {
+  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cin > 128 || !a) return LBT_EINVAL;
+  if (a->C != d.Cin || a->rows != d.N || a->inner != (int64_t)d.H * d.W * d.Cin) return LBT_EINVAL;
+  const int f = bwd_a_flags(*a);
+  if ((f & kAFused) != kAFused) return LBT_EINVAL;
+  const lbt_bwd_branch* br[2] = {&a->b1, &a->b2};
+  for (int b = 0; b < (a->has_b2 ? 2 : 1); ++b)
+    if (!br[b]->qrg.noise || !br[b]->qng.noise || !br[b]->gb) return LBT_EINVAL;
+  const int cs = d.Cout / 16;
+  GemmArgs p;
+  p.a = gq; p.b = wd; p.ks = ksd; p.nslices = d.KH * d.KW * cs;
+  if (ksd % 4 || ksd < p.nslices) return LBT_EINVAL;
+  p.a_fill = 0; p.colsum = nullptr;
+  p.d = d; p.qa = qg; p.qb = qw; p.y = nullptr; p.add_src = add_src; p.yq = nullptr; p.qout = lbt_qdesc{};
+  p.ychsum = nullptr;
+  p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
+  p.chain = *a;
+  if (p.M >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int nt = d.Cin / 16;
+  const int key = (cs << 8) | (nt << 4) | (a->has_b2 ? 1 : 0);
+#define LBT_DC(CS_, NT_, CF_, NB_)                                                                  \
+  if (key == ((CS_ << 8) | (NT_ << 4) | (NB_ == 2)) && f == (CF_)) return launch_dgrad_chain<CS_, NT_, CF_, NB_>(p, st);
+#define LBT_DC_SHAPES(CF_, NB_) \
+  LBT_DC(1, 1, CF_, NB_) LBT_DC(2, 2, CF_, NB_) LBT_DC(4, 4, CF_, NB_) LBT_DC(2, 1, CF_, NB_) LBT_DC(4, 2, CF_, NB_)
+  LBT_DC_SHAPES(kAFused | kAMaskR, 1)             // block, first BN (mask from R1)
+  LBT_DC_SHAPES(kAFused | kAYMask | kAGmask, 1)   // block end, identity shortcut
+  LBT_DC_SHAPES(kAFused | kAYMask, 2)             // block end, projection shortcut
+  LBT_DC_SHAPES(kAFused | kAYMask, 1)             // stem
+#undef LBT_DC_SHAPES
+#undef LBT_DC
+  return LBT_EINVAL;
 }
 
 extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t* gq, lbt_conv_desc d,

@@ -75,6 +75,8 @@ class FusedResNet:
         self.loss = None
         self.dlogits = None
         self.overlap_wgrad = os.environ.get("LBT_OVERLAP_WGRAD", "0") == "1"  # measured: a loss here (60K vs 67K samples/s)
+        # run each BN backward pass A inside the dgrad that produces its input (1 = default)
+        self.fuse_dgrad_chain = os.environ.get("LBT_FUSE_DGRAD_CHAIN", "1") == "1"
         self._side = None
 
     # ------------------------------------------------------------------ Trainer interface
@@ -298,18 +300,26 @@ class FusedResNet:
                      ptr(dpool), None))
         gY = self._buf("gYlast", Ylast.shape, torch.float32)
         bwd.append(L("lbt_avgpool_bwd", ptr(dpool), ptr(gY), Nb, Hh * Wh, Ch))
-        for i in reversed(range(len(self.blocks))):
-            gY = self._block_bwd(i, self.blocks[i], saved[i], gY, bwd, L, obs, rjobs, pjobs)
-
-        # ---- stem backward (d loss / d image is never needed)
+        # Pass-A descriptors of every block-end BN chain and of the stem's, built first: each runs
+        # as the epilogue of the dgrad that produces its input gradient (lbt_conv_dgrad_chain_i8),
+        # except the last block's, which follows the avgpool backward.
+        ends = [self._block_end_chain(i, b, saved[i], obs) for i, b in enumerate(self.blocks)]
         gq0 = self._buf("gq0", shp0, torch.int8)
         Gn0 = self._buf("Gn0", shp0, torch.int8)
         sums0 = self._sums("sums0", ops.NSHARD * 4 * C0)
         obs(r0.grad_range, numel0)
         obs(n0.grad_range, numel0)
         obs(c.grad_range, numel0)
-        aA = self._chain_bwd_a(gY, X0, False, None, (r0, R0, n0, qn0, Gn0, sums0), None, shp0, C0)
-        bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
+        aA = self._chain_bwd_a(None, X0, False, None, (r0, R0, n0, qn0, Gn0, sums0), None, shp0, C0)
+        stem_end = dict(a=aA)
+        for i in reversed(range(len(self.blocks))):
+            consumer = ends[i - 1] if i > 0 else stem_end
+            gY = self._block_bwd(i, self.blocks[i], saved[i], gY, ends[i], consumer, bwd, L, obs, rjobs, pjobs)
+
+        # ---- stem backward (d loss / d image is never needed)
+        if gY is not None:  # pass A not fused into block 0's dgrad
+            aA.g = gY.data_ptr()
+            bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
         aB = self._chain_bwd_b(n0, Gn0, qn0, sums0, shp0, C0, gq0, c.grad_range, None)
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB)))
         self._keep += [aA, aB]
@@ -380,7 +390,7 @@ class FusedResNet:
 
     def _chain_bwd_a(self, g, y_mask, mask_from_r, gmask, br1, br2, shape, C):
         a = ChainBwdA()
-        a.g = g.data_ptr()
+        a.g = g.data_ptr() if g is not None else None
         a.y_mask = y_mask.data_ptr() if y_mask is not None else None
         a.mask_from_r = 1 if mask_from_r else 0
         a.gmask_out = gmask.data_ptr() if gmask is not None else None
@@ -468,37 +478,55 @@ class FusedResNet:
                     Rs=Rs, Y=Y, shp=shp, C=C, Cin=Cin)
         return Y, xa_n, xs_n, info
 
-    def _block_bwd(self, i, b, f, gY, bwd, L, obs, rjobs, pjobs):
+    def _block_end_chain(self, i, b, f, obs):
+        """Pass A of block i's output BN(s): ReLU mask from Y, bn2 (and shortcut-BN) gradient
+        quantisers and sums. Its input gradient is set later (fused dgrad or explicit g)."""
         k = "b%d_" % i
-        shp, C, Cin = f["shp"], f["C"], f["Cin"]
-        numel = 1
-        for v in shp:
-            numel *= v
-        c1, c2, cs = b.c1, b.c2, b.cs
-        d1, d2, ds = f["d1"], f["d2"], f["ds"]
+        shp, C = f["shp"], f["C"]
+        numel = math.prod(shp)
+        c2, cs = b.c2, b.cs
         Gn2 = self._buf(k + "Gn2", shp, torch.int8)
         sums2 = self._sums(k + "sums2", ops.NSHARD * 4 * C)
-        for q in (b.r2.grad_range, b.n2.grad_range, c2.grad_range, b.r1.grad_range, b.n1.grad_range,
-                  c1.grad_range):
+        for q in (b.r2.grad_range, b.n2.grad_range):
             obs(q, numel)
-        gm = None
-        br2 = None
-        Gns = sumss = None
+        gm = br2 = Gns = sumss = None
         if cs is not None:
             Gns = self._buf(k + "Gns", shp, torch.int8)
             sumss = self._sums(k + "sumss", ops.NSHARD * 4 * C)
             br2 = (b.rs, f["Rs"], b.ns, f["qns"], Gns, sumss)
-            for q in (b.rs.grad_range, b.ns.grad_range, cs.grad_range):
+            for q in (b.rs.grad_range, b.ns.grad_range):
                 obs(q, numel)
         else:
             gm = self._buf(k + "gm", shp, torch.float32)
-        aA2 = self._chain_bwd_a(gY, f["Y"], False, gm, (b.r2, f["R2"], b.n2, f["qn2"], Gn2, sums2), br2, shp, C)
-        bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA2), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA2)))
+        a = self._chain_bwd_a(None, f["Y"], False, gm, (b.r2, f["R2"], b.n2, f["qn2"], Gn2, sums2), br2, shp, C)
+        self._keep.append(a)
+        return dict(a=a, Gn2=Gn2, sums2=sums2, gm=gm, Gns=Gns, sumss=sumss)
+
+    def _block_bwd(self, i, b, f, gY, end, consumer, bwd, L, obs, rjobs, pjobs):
+        """Block i's backward. gY: materialised d loss / d Y (or None: pass A already ran inside
+        the next block's dgrad). consumer: the pass A fed by this block's input gradient.
+        Returns the materialised input gradient, or None when it was fused into `consumer`."""
+        k = "b%d_" % i
+        shp, C, Cin = f["shp"], f["C"], f["Cin"]
+        numel = math.prod(shp)
+        c1, c2, cs = b.c1, b.c2, b.cs
+        d1, d2, ds = f["d1"], f["d2"], f["ds"]
+        fuse = self.fuse_dgrad_chain
+        for q in (c2.grad_range, b.r1.grad_range, b.n1.grad_range, c1.grad_range):
+            obs(q, numel)
+        if cs is not None:
+            obs(cs.grad_range, numel)
+        Gn2, sums2, gm, Gns, sumss = end["Gn2"], end["sums2"], end["gm"], end["Gns"], end["sumss"]
+        if gY is not None:
+            aA2 = end["a"]
+            aA2.g = gY.data_ptr()
+            bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA2), k="chain_bwd_a_kernel",
+                         nb=ops._chain_bwd_a_bytes(aA2)))
         gq2 = self._buf(k + "gq2", shp, torch.int8)
         gcol2 = self._sums(k + "gcol2", ops.NSHARD * 2 * C)
         aB2 = self._chain_bwd_b(b.n2, Gn2, f["qn2"], sums2, shp, C, gq2, c2.grad_range, gcol2)
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB2), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB2)))
-        keep = [aA2, aB2]
+        keep = [aB2]
         gqs = gcols = None
         if cs is not None:
             gqs = self._buf(k + "gqs", shp, torch.int8)
@@ -506,25 +534,34 @@ class FusedResNet:
             aBs = self._chain_bwd_b(b.ns, Gns, f["qns"], sumss, shp, C, gqs, cs.grad_range, gcols)
             bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aBs), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aBs)))
             keep.append(aBs)
-        d1g = self._buf(k + "d1", shp, torch.float32)
-        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range), c2.W_range.desc,
-                     ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=gq2.numel() + c2.wd.numel() + 4 * d1g.numel()))
+        # conv-2 dgrad, fused with pass A of bn1 (ReLU mask recomputed from R1)
+        Gn1 = self._buf(k + "Gn1", shp, torch.int8)
+        sums1 = self._sums(k + "sums1", ops.NSHARD * 4 * C)
+        nb_dg2 = gq2.numel() + c2.wd.numel()
+        if fuse:
+            aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
+            bwd.append(L("lbt_conv_dgrad_chain_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range),
+                         c2.W_range.desc, None, ctypes.byref(aA1), k="conv_gemm_kernel<1> (dgrad+A)",
+                         nb=nb_dg2 + 4 * numel))
+        else:
+            d1g = self._buf(k + "d1", shp, torch.float32)
+            bwd.append(L("lbt_conv_dgrad_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range),
+                         c2.W_range.desc, ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg2 + 4 * numel))
+            aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
+        keep.append(aA1)
         ns2 = ops.wgrad_nsplit(d2)
         slab2 = self._buf(k + "slab2", (ns2, 9 * C, C), torch.int32)
         bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), ns2,
                                    k="conv_wgrad_kernel", nb=f["xb"].numel() + gq2.numel() + 4 * slab2.numel())))
-        rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), self._qd(c2.X_range), self._qd(c2.grad_range),
-                          c2.W.data_ptr(), ops.f32(2 * c2.weight_decay), c2.dW.data_ptr()))
-        Gn1 = self._buf(k + "Gn1", shp, torch.int8)
-        sums1 = self._sums(k + "sums1", ops.NSHARD * 4 * C)
-        aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
-        bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA1), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA1)))
+        rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), self._qd(c2.X_range),
+                          self._qd(c2.grad_range), c2.W.data_ptr(), ops.f32(2 * c2.weight_decay), c2.dW.data_ptr()))
+        if not fuse:
+            bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA1), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA1)))
         gq1 = self._buf(k + "gq1", shp, torch.int8)
         gcol1 = self._sums(k + "gcol1", ops.NSHARD * 2 * C)
         aB1 = self._chain_bwd_b(b.n1, Gn1, f["qn1"], sums1, shp, C, gq1, c1.grad_range, gcol1)
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB1), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB1)))
-        keep += [aA1, aB1]
-        gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
+        keep.append(aB1)
         add = gm
         if cs is not None:
             dsg = self._buf(k + "dsc", f["Xin"].shape, torch.float32)
@@ -532,8 +569,18 @@ class FusedResNet:
                          cs.W_range.desc, ptr(dsg), None, k="conv_gemm_kernel<1> (dgrad)",
                          nb=gqs.numel() + cs.wd.numel() + 4 * dsg.numel()))
             add = dsg
-        bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range), c1.W_range.desc,
-                     ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=gq1.numel() + c1.wd.numel() + 8 * gin.numel()))
+        # conv-1 dgrad (+ shortcut gradient), fused with the consumer's pass A
+        nin = math.prod(f["Xin"].shape)
+        nb_dg1 = gq1.numel() + c1.wd.numel() + 8 * nin
+        gin = None
+        if fuse:
+            bwd.append(L("lbt_conv_dgrad_chain_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range),
+                         c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]), k="conv_gemm_kernel<1> (dgrad+A)",
+                         nb=nb_dg1))
+        else:
+            gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
+            bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range),
+                         c1.W_range.desc, ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg1))
         ns1 = ops.wgrad_nsplit(d1)
         slab1 = self._buf(k + "slab1", (ns1, 9 * Cin, C), torch.int32)
         bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), ns1,
