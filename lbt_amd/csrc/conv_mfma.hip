@@ -228,102 +228,104 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0
 }
 
 // ----------------------------------------------------------------------------- wgrad
-// grid (nsplit, taps); block 256 = 4 waves, each wave walks 64-pixel chunks of the block's
-// pixel range.  LDS per wave: Xt [CSI*16][64+16] and Gt [CSO*16][64+16] bytes.
-constexpr int kWP = 64;        // pixels per wave chunk
-constexpr int kLdsRow = 80;    // 64 + 16 pad (keeps 16-B alignment)
+// dW[tap][ci][co] = sum_p X[p shifted by tap][ci] * G[p][co]: GEMM rows = ci, cols = co, k = pixels.
+// grid (nsplit, taps, Cout/16): workgroup = one tap, one 16-channel co slice, a pixel range; each
+// wave walks 64-pixel chunks. A lane loads one pixel's 16-byte channel slices (X: CSI of them,
+// G: one) and stores them as rows of [pixel][16 B] LDS images (one ds_write_b128 each); the MFMA
+// fragments -- 16 consecutive pixels of one channel -- come back with the gfx950 transposing read
+// ds_read_b64_tr_b8 (probed: in a 16-lane group, lane i receives byte i of the 8 rows formed by
+// lane pairs 2r, 2r+1). Each workgroup writes one exact int32 partial [CI][16] into
+// slab[split][tap][ci][co] for the batched reduce.
+constexpr int kWP = 64;  // pixels per wave chunk
 
-template <int CSI, int CSO>
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+// 16 pixels (rows base..base+15 of a [pixel][16 B] image) of channel (lane & 15): 16 bytes
+LBT_DEV v4i tr_frag(const int8_t* img, int base, int lane) {
+  const int j = lane & 15;
+  const int8_t* p0 = img + (base + (j >> 1)) * 16 + 8 * (j & 1);
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p0));
+  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p0 + 8 * 16));
+  return v4i{lo.x, lo.y, hi.x, hi.y};
+}
+
+template <int CSI>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __restrict__ xq,
                                                               const int8_t* __restrict__ gq,
                                                               lbt_conv_desc d, int x_fill,
                                                               int32_t* __restrict__ slab, int64_t P,
                                                               int nsplit) {
-  constexpr int CI = CSI * 16, CO = CSO * 16;
-  __shared__ __attribute__((aligned(16))) int8_t lds[4][(CI + CO) * kLdsRow];
-  __shared__ int red[CI * CO];
+  constexpr int CI = CSI * 16;
+  // per wave: X image [CSI][64 px][16 B] and G image [64 px][16 B]
+  __shared__ __attribute__((aligned(16))) int8_t lds[4][(CSI + 1) * kWP * 16];
+  __shared__ int red[4][CI * 16];
   LBT_TS(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kg = lane >> 4;
-  const int tap = blockIdx.y;
+  const int tap = blockIdx.y, cso = blockIdx.z;
   const int kh = tap / d.KW, kw = tap - kh * d.KW;
-  int8_t* Xt = lds[wave];
-  int8_t* Gt = lds[wave] + CI * kLdsRow;
-
-  for (int i = threadIdx.x; i < CI * CO; i += kThreads) red[i] = 0;
-
+  int8_t* Xi = lds[wave];
+  int8_t* Gi = lds[wave] + CSI * kWP * 16;
   const int64_t per = (P + nsplit - 1) / nsplit;
   const int64_t p0 = (int64_t)blockIdx.x * per;
   const int64_t p1 = p0 + per < P ? p0 + per : P;
+  const uint32_t HWo = (uint32_t)d.Ho * d.Wo;
 
-  v4i acc[CSI][CSO];
+  v4i acc[CSI];
 #pragma unroll
-  for (int a = 0; a < CSI; ++a)
-#pragma unroll
-    for (int b = 0; b < CSO; ++b) acc[a][b] = v4i{0, 0, 0, 0};
+  for (int a = 0; a < CSI; ++a) acc[a] = v4i{0, 0, 0, 0};
 
-  const int64_t HWo = (int64_t)d.Ho * d.Wo;
   // chunks are interleaved across the 4 waves of the block
   for (int64_t c0 = p0 + (int64_t)wave * kWP; c0 < p1; c0 += 4 * kWP) {
     const int64_t p = c0 + lane;
     const bool pv = p < p1;
-    // ---- gather this lane's pixel: G row and tap-shifted X row
-    int n = 0, oh = 0, ow = 0;
-    if (pv) {
-      n = (int)(p / HWo);
-      const int64_t rem = p - (int64_t)n * HWo;
-      oh = (int)(rem / d.Wo);
-      ow = (int)(rem - (int64_t)oh * d.Wo);
-    }
+    const uint32_t pu = (uint32_t)(pv ? p : p0);  // P < 2^31 (launcher)
+    const uint32_t n = pu / HWo, rem = pu - n * HWo;
+    const int oh = (int)(rem / (uint32_t)d.Wo), ow = (int)(rem - (uint32_t)oh * (uint32_t)d.Wo);
     const int ih = oh * d.SH + kh - d.PT, iw = ow * d.SW + kw - d.PL;
     const bool xv = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+    // all loads first (clamped addresses, no branches), fills selected afterwards
+    const int8_t* xp = xq + (xv ? ((((int64_t)n * d.H + ih) * d.W + iw) * CI) : 0);
+    v4i xs[CSI];
 #pragma unroll
-    for (int cs = 0; cs < CSO; ++cs) {
-      v4i g = v4i{0, 0, 0, 0};
-      if (pv) g = *reinterpret_cast<const v4i*>(gq + p * CO + cs * 16);
-      const int8_t* gb = reinterpret_cast<const int8_t*>(&g);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) Gt[(cs * 16 + j) * kLdsRow + lane] = gb[j];
-    }
+    for (int cs = 0; cs < CSI; ++cs) xs[cs] = *reinterpret_cast<const v4i*>(xp + cs * 16);
+    v4i g = *reinterpret_cast<const v4i*>(gq + (int64_t)pu * d.Cout + cso * 16);
+    const int xf = pv ? x_fill : 0;
 #pragma unroll
     for (int cs = 0; cs < CSI; ++cs) {
-      v4i x = v4i{x_fill, x_fill, x_fill, x_fill};
-      if (!pv) x = v4i{0, 0, 0, 0};
-      else if (xv) x = *reinterpret_cast<const v4i*>(xq + (((int64_t)n * d.H + ih) * d.W + iw) * CI + cs * 16);
-      const int8_t* xb = reinterpret_cast<const int8_t*>(&x);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) Xt[(cs * 16 + j) * kLdsRow + lane] = xb[j];
+      if (!xv) xs[cs] = v4i{xf, xf, xf, xf};
+      *reinterpret_cast<v4i*>(Xi + (cs * kWP + lane) * 16) = xs[cs];
     }
-    // this wave's transposed tiles are read by other lanes of the same wave only
+    if (!pv) g = v4i{0, 0, 0, 0};
+    *reinterpret_cast<v4i*>(Gi + lane * 16) = g;
+    // the images are read by other lanes of the same wave only
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    v4i bf[CSO];
-#pragma unroll
-    for (int b = 0; b < CSO; ++b) bf[b] = *reinterpret_cast<const v4i*>(Gt + (b * 16 + r) * kLdsRow + kg * 16);
+    const v4i bfrag = tr_frag(Gi, 16 * kg, lane);
 #pragma unroll
     for (int a = 0; a < CSI; ++a) {
-      const v4i af = *reinterpret_cast<const v4i*>(Xt + (a * 16 + r) * kLdsRow + kg * 16);
-#pragma unroll
-      for (int b = 0; b < CSO; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[b], acc[a][b], 0, 0, 0);
+      const v4i afrag = tr_frag(Xi + a * kWP * 16, 16 * kg, lane);
+      acc[a] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag, bfrag, acc[a], 0, 0, 0);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   LBT_TS(1);
-  __syncthreads();
-  LBT_TS(2);
-  // acc[a][b] element i: row = a*16 + 4*kg + i (ci), col = b*16 + r (co)
+  // acc[a] element i: row = a*16 + 4*kg + i (ci), col = r (co within the slice)
 #pragma unroll
   for (int a = 0; a < CSI; ++a)
 #pragma unroll
-    for (int b = 0; b < CSO; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(&red[(a * 16 + kg * 4 + i) * CO + b * 16 + r], acc[a][b][i]);
+    for (int i = 0; i < 4; ++i) red[wave][(a * 16 + kg * 4 + i) * 16 + r] = acc[a][i];
   __syncthreads();
-  int32_t* dst = slab + ((int64_t)blockIdx.x * (d.KH * d.KW) + tap) * CI * CO;
-  for (int i = threadIdx.x; i < CI * CO; i += kThreads) dst[i] = red[i];
+  LBT_TS(2);
+  int32_t* dst = slab + ((int64_t)blockIdx.x * (d.KH * d.KW) + tap) * CI * d.Cout + cso * 16;
+  for (int i = threadIdx.x; i < CI * 16; i += kThreads) {
+    const int ci = i >> 4, co = i & 15;
+    dst[(int64_t)ci * d.Cout + co] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
   LBT_TS(3);
 }
 
@@ -478,20 +480,20 @@ extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t
                                     int32_t* slab, int32_t nsplit, void* stream) {
   if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || nsplit <= 0) return LBT_EINVAL;
   const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
+  if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
   if ((P + nsplit - 1) / nsplit > 65536) return LBT_EINVAL;  // int32 partial bound
-  const int csi = d.Cin / 16, cso = d.Cout / 16;
+  const int csi = d.Cin / 16;
   const int fill = x_u8off ? (int)0x80808080u : 0;
-  dim3 grid(nsplit, d.KH * d.KW);
+  dim3 grid(nsplit, d.KH * d.KW, d.Cout / 16);
   hipStream_t st = (hipStream_t)stream;
-#define LBT_WG(A, B)                                                                                          \
-  if (csi == A && cso == B) {                                                                                 \
-    hipLaunchKernelGGL((conv_wgrad_kernel<A, B>), grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); \
-    return (int)hipGetLastError();                                                                            \
+  switch (csi) {
+    case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
+    case 2: hipLaunchKernelGGL(conv_wgrad_kernel<2>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
+    case 4: hipLaunchKernelGGL(conv_wgrad_kernel<4>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
+    case 8: hipLaunchKernelGGL(conv_wgrad_kernel<8>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
+    default: return LBT_EINVAL;
   }
-  LBT_WG(1, 1) LBT_WG(1, 2) LBT_WG(1, 4) LBT_WG(2, 1) LBT_WG(2, 2) LBT_WG(2, 4) LBT_WG(4, 1) LBT_WG(4, 2)
-  LBT_WG(4, 4)
-#undef LBT_WG
-  return LBT_EINVAL;
+  return (int)hipGetLastError();
 }
 
 extern "C" int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int32_t x_u8off,

@@ -162,9 +162,10 @@ def wgrad_nsplit(d, generic=False):
     if generic:
         lo = -(-P // 8192)
         return max(lo, min(256, -(-P // (8 if P <= 4096 else 32))))
+    # MFMA wgrad grid = (nsplit, taps, Cout/16): ~512 workgroups of >= 512 pixels each
     lo = -(-P // 65536)
-    want = max(1, -(-512 // taps))
-    return max(lo, min(want, max(1, P // 256)))
+    want = max(1, -(-512 // (taps * (d.Cout // 16))))
+    return max(lo, min(want, max(1, P // 512)))
 
 
 def conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit):
@@ -245,6 +246,15 @@ def _chain_bwd_a_bytes(a):
         per += 1 if b.qng.bits else 0
         per += 1 if b.gout else (4 if b.dout else 0)
     return per * a.rows * a.inner
+
+
+def _dgrad_chain_bytes(gq_numel, wd_numel, a, add):
+    """lbt_conv_dgrad_chain_i8: the dgrad operands + pass A's element traffic without its fp32 g
+    input (it never leaves the GEMM), + the residual addend, + each quantiser's noise table."""
+    per = (4 if add else 0) + (4 if a.y_mask else 0) + (4 if a.gmask_out else 0)
+    nb = 2 if a.has_b2 else 1
+    per += 3 * nb  # R, qn codes in; G codes out
+    return gq_numel + wd_numel + per * a.rows * a.inner + nb * 2 * 4 * a.inner
 
 
 def _chain_bwd_b_bytes(a):

@@ -542,7 +542,7 @@ class FusedResNet:
             aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
             bwd.append(L("lbt_conv_dgrad_chain_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range),
                          c2.W_range.desc, None, ctypes.byref(aA1), k="conv_gemm_kernel<1> (dgrad+A)",
-                         nb=nb_dg2 + 4 * numel))
+                         nb=ops._dgrad_chain_bytes(gq2.numel(), c2.wd.numel(), aA1, False)))
         else:
             d1g = self._buf(k + "d1", shp, torch.float32)
             bwd.append(L("lbt_conv_dgrad_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range),
@@ -576,7 +576,7 @@ class FusedResNet:
         if fuse:
             bwd.append(L("lbt_conv_dgrad_chain_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range),
                          c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]), k="conv_gemm_kernel<1> (dgrad+A)",
-                         nb=nb_dg1))
+                         nb=ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], add is not None)))
         else:
             gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
             bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range),

@@ -21,6 +21,23 @@ from .dfxp import ops
 HBM_PEAK_GBS = 8000.0
 
 
+def family(kernel_name):
+    """Kernel family of a device symbol / bench label: the unit the roofline and the PMC traffic
+    summary (tools/pmc_summary.py) agree on. conv_gemm_kernel<MODE, CS, NT, CF, NB> splits into
+    forward, plain dgrad and dgrad fused with a BN pass A (CF != 0); other kernels drop their
+    template arguments."""
+    n = kernel_name.replace("(anonymous namespace)::", "").replace("void ", "").strip()
+    if n.startswith("conv_gemm_kernel<"):
+        args = [a.strip() for a in n[len("conv_gemm_kernel<"):].split(">")[0].split(",")]
+        if len(args) < 3:  # already a family label, e.g. "conv_gemm_kernel<1> (dgrad+A)"
+            return n
+        if args[0] == "0":
+            return "conv_gemm_kernel<0> (fwd)"
+        cf = int(args[3]) if len(args) >= 4 else 0
+        return "conv_gemm_kernel<1> (dgrad+A)" if cf else "conv_gemm_kernel<1> (dgrad)"
+    return n.split("(")[0].split("<")[0].strip()
+
+
 def measure_step_kernels(trainer, x, y, steps=3):
     """{kernel: (launches per step, avg us, avg algorithmic bytes)} over `steps` eager steps.
     Parameters / exponents are restored afterwards so the measurement does not perturb training."""
@@ -63,8 +80,9 @@ def measure_dominant(trainer, x, y, traffic_file=None):
     if os.path.exists(tf):
         try:
             t = json.load(open(tf))
-            if name in t.get("kernels", {}):
-                traffic = t["kernels"][name]["hbm_bytes_per_launch"]
+            fam = t.get("families", {})
+            if family(name) in fam:
+                traffic = fam[family(name)]["hbm_bytes_per_launch"]
         except Exception:  # pragma: no cover
             traffic = None
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
