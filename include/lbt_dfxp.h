@@ -147,10 +147,13 @@ int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_
                       lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
 
 /* Conv2d_q backward dW = tf.gradients(y, W, gradq) (dynamic_fixed_point.py:302), pass 1:
- * int32 partial sums over `nsplit` pixel ranges into slab [nsplit][KH*KW][Cin][Cout]
- * (x_u8off: xq in the unsigned-9-bit offset encoding; the offset is undone in pass 2).       */
+ * the pixels are split into `nsplit` ranges (x Cout/16 column slices x taps = the grid); the
+ * exact int32 partial of range s is ADDED into shard s % nshard of slab[nshard][KH*KW][Cin][Cout],
+ * which the caller zeroes (integer atomics: order-independent). Requires every shard to cover
+ * <= 65536 pixels (int32 exactness). x_u8off: xq in the unsigned-9-bit offset encoding; the
+ * offset is undone in pass 2 (lbt_conv_wgrad_reduce, nsplit = nshard).                       */
 int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t* gq, lbt_conv_desc d,
-                      int32_t* slab, int32_t nsplit, void* stream);
+                      int32_t* slab, int32_t nsplit, int32_t nshard, void* stream);
 
 /* pass 2: dW = float(sum_split slab + 128*x_u8off*gcolsum[co]) * 2^-(ex+eg) + wd2 * W,
  * written HWIO into dw (wd2 = 2*weight_decay as fp32, the "+ 2*wd*W" of :302).
@@ -319,12 +322,13 @@ typedef struct lbt_qjob {
 } lbt_qjob;
 int lbt_dfxp_quantize_many(const lbt_qjob* jobs, int32_t njobs, void* stream);
 
-/* lbt_conv_wgrad_reduce for many layers. */
+/* lbt_conv_wgrad_reduce for many layers: one 1-D launch of total_blocks = sum over the jobs of
+ * ceil(K*Cout / 256) workgroups (jobs[] in device memory, Cout <= 256).                    */
 typedef struct lbt_rjob {
   const int32_t* slab; int32_t nsplit, K, Cout, x_u8off; const int64_t* gcolsum;
   lbt_qdesc qx, qg; const float* w; float wd2; float* dw;
 } lbt_rjob;
-int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, int32_t max_blocks, void* stream);
+int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, int32_t total_blocks, void* stream);
 
 /* lbt_bn_param_grads for many Rescale_q layers. */
 typedef struct lbt_pjob {

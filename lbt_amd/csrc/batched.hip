@@ -59,29 +59,50 @@ __global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob*
   block_flush_counts(j.q, ov1, ov2, sh_cnt);
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs) {
-  __shared__ long long red[8][32];
-  const lbt_rjob j = jobs[blockIdx.y];
-  const int64_t total = (int64_t)j.K * j.Cout;
-  if ((int64_t)blockIdx.x * 32 >= total) return;  // uniform per block
-  const int lo = threadIdx.x & 31, sg = threadIdx.x >> 5;
-  const int64_t i = (int64_t)blockIdx.x * 32 + lo;
-  long long s = 0;
-  if (i < total) {
-#pragma unroll 8
-    for (int b = sg; b < j.nsplit; b += 8) s += j.slab[(int64_t)b * total + i];
-    if (j.x_u8off && j.gcolsum) {  // offset correction 128 * sum_p g: shards split over the groups
-      const int co = (int)(i % j.Cout);
-      long long cs = 0;
-#pragma unroll
-      for (int k = sg; k < LBT_NSHARD; k += 8) cs += j.gcolsum[(int64_t)k * 2 * j.Cout + co];
-      s += 128ll * cs;
-    }
-  }
-  red[sg][lo] = s;
+// Blocks are allotted to the jobs in order, ceil(K*Cout/256) each (1-D grid); a block reduces 256
+// consecutive outputs over the slab's shards, with the offset correction 128 * sum_p g[co]
+// (x_u8off) summed once per column into LDS.
+__global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs, int njobs) {
+  __shared__ int s_job;
+  __shared__ int64_t s_base;
+  __shared__ int64_t nbs[256];
+  __shared__ long long colsum[256];
+  // every job's block count loaded in parallel (a serial scan of device memory would cost one
+  // memory round trip per job), then scanned in LDS
+  for (int j = threadIdx.x; j < njobs; j += 256) nbs[j] = ((int64_t)jobs[j].K * jobs[j].Cout + 255) / 256;
   __syncthreads();
-  if (sg != 0 || i >= total) return;
-  for (int k = 1; k < 8; ++k) s += red[k][lo];
+  if (threadIdx.x == 0) {
+    int64_t b = blockIdx.x;
+    int jj = njobs;  // past the end: nothing to do
+    for (int j = 0; j < njobs; ++j) {
+      if (b < nbs[j]) { jj = j; break; }
+      b -= nbs[j];
+    }
+    s_job = jj;
+    s_base = b * 256;
+  }
+  __syncthreads();
+  if (s_job >= njobs) return;
+  const lbt_rjob j = jobs[s_job];
+  const int64_t total = (int64_t)j.K * j.Cout;
+  const int64_t i = s_base + threadIdx.x;
+  const bool corr = j.x_u8off && j.gcolsum;
+  if (corr) {
+    for (int c = threadIdx.x; c < j.Cout; c += 256) {
+      long long v[LBT_NSHARD];
+#pragma unroll
+      for (int k = 0; k < LBT_NSHARD; ++k) v[k] = j.gcolsum[(int64_t)k * 2 * j.Cout + c];
+      long long t = 0;
+#pragma unroll
+      for (int k = 0; k < LBT_NSHARD; ++k) t += v[k];
+      colsum[c] = t;
+    }
+    __syncthreads();
+  }
+  if (i >= total) return;
+  long long s = 0;
+  for (int b = 0; b < j.nsplit; ++b) s += j.slab[(int64_t)b * total + i];
+  if (corr) s += 128ll * colsum[i % j.Cout];
   const float scale = ldexpf(1.0f, -(frac_exp(j.qx) + frac_exp(j.qg)));
   const float a = (float)s * scale;
   const float b = j.wd2 * j.w[i];
@@ -92,10 +113,17 @@ __global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
   const lbt_pjob j = jobs[blockIdx.y];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= j.C) return;
-  long long sgr = 0, sg = 0;
+  long long vr[LBT_NSHARD], vg[LBT_NSHARD];  // all shard loads in flight at once
+#pragma unroll
   for (int k = 0; k < LBT_NSHARD; ++k) {
-    sgr += j.sums[(int64_t)k * 4 * j.C + c];
-    sg += j.sums[(int64_t)k * 4 * j.C + j.C + c];
+    vr[k] = j.sums[(int64_t)k * 4 * j.C + c];
+    vg[k] = j.sums[(int64_t)k * 4 * j.C + j.C + c];
+  }
+  long long sgr = 0, sg = 0;
+#pragma unroll
+  for (int k = 0; k < LBT_NSHARD; ++k) {
+    sgr += vr[k];
+    sg += vg[k];
   }
   const double g2 = ldexp(1.0, -frac_exp(j.qrg)), r = ldexp(1.0, -frac_exp(j.qr));
   const float a = (float)((double)sgr * (g2 * r));
@@ -152,10 +180,10 @@ extern "C" int lbt_dfxp_quantize_many(const lbt_qjob* jobs, int32_t njobs, void*
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, int32_t max_blocks, void* stream) {
+extern "C" int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, int32_t total_blocks, void* stream) {
   if (njobs <= 0) return LBT_OK;
-  if (njobs > 65535 || max_blocks <= 0) return LBT_EINVAL;
-  hipLaunchKernelGGL(wgrad_reduce_many_kernel, dim3(max_blocks, njobs), dim3(256), 0, (hipStream_t)stream, jobs);
+  if (total_blocks <= 0 || njobs > 256) return LBT_EINVAL;
+  hipLaunchKernelGGL(wgrad_reduce_many_kernel, dim3(total_blocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs);
   return (int)hipGetLastError();
 }
 

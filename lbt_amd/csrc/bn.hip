@@ -75,8 +75,12 @@ LBT_DEV Noise4 noise_for(const lbt_qdesc& q, const QState& s, int64_t g) {
 // Sum a sharded [LBT_NSHARD][stride] int64 buffer's first n entries into LDS tmp[n].
 LBT_DEV void sum_shards(const int64_t* src, int n, int stride, long long* tmp) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    long long v[LBT_NSHARD];  // every shard's load in flight at once
+#pragma unroll
+    for (int k = 0; k < LBT_NSHARD; ++k) v[k] = src[(int64_t)k * stride + i];
     long long s = 0;
-    for (int k = 0; k < LBT_NSHARD; ++k) s += src[(int64_t)k * stride + i];
+#pragma unroll
+    for (int k = 0; k < LBT_NSHARD; ++k) s += v[k];
     tmp[i] = s;
   }
 }
@@ -455,7 +459,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
 
 template <int F>
 __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a, int rpt) {
-  extern __shared__ float shf[];  // mu, sigma, mg, mgx [C]; then long long tmp[2C] / colsum[2C]
+  extern __shared__ float shf[];  // mu, sigma, mg, mgx [C]; then long long tmp[2C], csum[2C]
   __shared__ int sh_cnt[8 * kThreads / 64];
   constexpr int ST = (F & kRt) ? -1 : ((F & kBStoch) ? 1 : 0);
   LBT_TS(0);
@@ -487,12 +491,9 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
   const bool want_q = LBT_FL(kBQ, a.gq && so.active);
   const Noise4 no = noise_for(a.qo, so, gl);
   // SG at sums[2C:3C), SGQ at sums[3C:4C) of each shard
-  for (int i = threadIdx.x; i < 2 * C; i += kThreads) {
-    long long s = 0;
-#pragma unroll 8
-    for (int k = 0; k < LBT_NSHARD; ++k) s += a.sums[(int64_t)k * 4 * C + 2 * C + i];
-    tmp[i] = s;
-  }
+  sum_shards(a.sums + 2 * C, 2 * C, 4 * C, tmp);
+  long long* csum = tmp + 2 * C;  // this block's gq channel sums [2C]
+  for (int i = threadIdx.x; i < 2 * C; i += kThreads) csum[i] = 0;
   __syncthreads();
   {
     const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, n = (double)a.n;
@@ -505,8 +506,6 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
       mgx[c] = (float)(gsc * (s * SGQ - (double)m * SG) / (n * (double)sig));
     }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C; i += kThreads) tmp[i] = 0;
   __syncthreads();
   LBT_TS(1);
   float rmu[4], rmg[4], rmgx[4];
@@ -564,15 +563,15 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int v1 = wave_chan_reduce(s1[k], per), v2 = wave_chan_reduce(s2[k], per);
-      if (own && v1) atomicAdd((unsigned long long*)&tmp[c0 + k], (unsigned long long)(long long)v1);
-      if (own && v2) atomicAdd((unsigned long long*)&tmp[C + c0 + k], (unsigned long long)(long long)v2);
+      if (own && v1) atomicAdd((unsigned long long*)&csum[c0 + k], (unsigned long long)(long long)v1);
+      if (own && v2) atomicAdd((unsigned long long*)&csum[C + c0 + k], (unsigned long long)(long long)v2);
     }
   }
   if (!want_q) return;
   if (a.qo.counts) counts_stage_w(0, 1, ov1, ov2, sh_cnt);
   __syncthreads();
   counts_publish(0, 1, a.qo, sh_cnt);
-  if (gcol) block_flush_sums(tmp, 2 * C, a.gcolsum, 2 * C);
+  if (gcol) block_flush_sums(csum, 2 * C, a.gcolsum, 2 * C);
   LBT_TS(3);
 }
 
@@ -691,7 +690,7 @@ extern "C" int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream) {
   dim3 grid;
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
-  const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 2 * a->C;
+  const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 4 * a->C;
   hipStream_t st = (hipStream_t)stream;
   const int f = bwd_b_flags(*a);
   if (f == (kBQ | kBStoch | kBGcol))

@@ -234,8 +234,8 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0
 // G: one) and stores them as rows of [pixel][16 B] LDS images (one ds_write_b128 each); the MFMA
 // fragments -- 16 consecutive pixels of one channel -- come back with the gfx950 transposing read
 // ds_read_b64_tr_b8 (probed: in a 16-lane group, lane i receives byte i of the 8 rows formed by
-// lane pairs 2r, 2r+1). Each workgroup writes one exact int32 partial [CI][16] into
-// slab[split][tap][ci][co] for the batched reduce.
+// lane pairs 2r, 2r+1). Each workgroup adds its exact int32 partial [CI][16] into shard
+// (split % nshard) of a zeroed slab[nshard][tap][ci][co] for the batched reduce.
 constexpr int kWP = 64;  // pixels per wave chunk
 
 typedef int v2i __attribute__((ext_vector_type(2)));
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
                                                               const int8_t* __restrict__ gq,
                                                               lbt_conv_desc d, int x_fill,
                                                               int32_t* __restrict__ slab, int64_t P,
-                                                              int nsplit) {
+                                                              int nsplit, int nshard) {
   constexpr int CI = CSI * 16;
   // per wave: X image [CSI][64 px][16 B] and G image [64 px][16 B]
   __shared__ __attribute__((aligned(16))) int8_t lds[4][(CSI + 1) * kWP * 16];
@@ -321,10 +321,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
     for (int i = 0; i < 4; ++i) red[wave][(a * 16 + kg * 4 + i) * 16 + r] = acc[a][i];
   __syncthreads();
   LBT_TS(2);
-  int32_t* dst = slab + ((int64_t)blockIdx.x * (d.KH * d.KW) + tap) * CI * d.Cout + cso * 16;
+  int32_t* dst = slab + ((int64_t)(blockIdx.x % nshard) * (d.KH * d.KW) + tap) * CI * d.Cout + cso * 16;
   for (int i = threadIdx.x; i < CI * 16; i += kThreads) {
     const int ci = i >> 4, co = i & 15;
-    dst[(int64_t)ci * d.Cout + co] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    const int v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    if (v) atomicAdd(&dst[(int64_t)ci * d.Cout + co], v);  // integer atomics: exact, order-independent
   }
   LBT_TS(3);
 }
@@ -477,20 +478,21 @@ extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32
 }
 
 extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t* gq, lbt_conv_desc d,
-                                    int32_t* slab, int32_t nsplit, void* stream) {
-  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || nsplit <= 0) return LBT_EINVAL;
+                                    int32_t* slab, int32_t nsplit, int32_t nshard, void* stream) {
+  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || nsplit <= 0 || nshard <= 0 || nshard > nsplit) return LBT_EINVAL;
   const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
   if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
-  if ((P + nsplit - 1) / nsplit > 65536) return LBT_EINVAL;  // int32 partial bound
+  // int32 shard totals: the pixels of one shard times |x*g| <= 255*128 stay below 2^31
+  if ((P + nsplit - 1) / nsplit * ((nsplit + nshard - 1) / nshard) > 65536) return LBT_EINVAL;
   const int csi = d.Cin / 16;
   const int fill = x_u8off ? (int)0x80808080u : 0;
   dim3 grid(nsplit, d.KH * d.KW, d.Cout / 16);
   hipStream_t st = (hipStream_t)stream;
   switch (csi) {
-    case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
-    case 2: hipLaunchKernelGGL(conv_wgrad_kernel<2>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
-    case 4: hipLaunchKernelGGL(conv_wgrad_kernel<4>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
-    case 8: hipLaunchKernelGGL(conv_wgrad_kernel<8>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit); break;
+    case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
+    case 2: hipLaunchKernelGGL(conv_wgrad_kernel<2>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
+    case 4: hipLaunchKernelGGL(conv_wgrad_kernel<4>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
+    case 8: hipLaunchKernelGGL(conv_wgrad_kernel<8>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
     default: return LBT_EINVAL;
   }
   return (int)hipGetLastError();

@@ -174,9 +174,8 @@ class Conv2d_q(Layer_q):
         wd2 = ops.f32(2 * self.weight_decay)
         K = d.KH * d.KW * Cin
         if self.x_mfma:
-            ns = ops.wgrad_nsplit(d)
-            slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
-            ops.conv_wgrad_i8(self.xq, self.x_kind == OUT_U8OFF, self.gradq, d, slab, ns)
+            nsplit, ns, slab = ops.wgrad_slab(self._c, "wslab", d, self.ctx)
+            ops.conv_wgrad_i8(self.xq, self.x_kind == OUT_U8OFF, self.gradq, d, slab, nsplit, ns)
         elif self.stem(d):
             ns, slab = ops.stem_slab(self._c, "stem_slab", d, self.ctx)
             ops.conv_stem_wgrad(self.xq, self.gradq, d, slab, ns)

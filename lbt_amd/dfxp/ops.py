@@ -168,13 +168,29 @@ def wgrad_nsplit(d, generic=False):
     return max(lo, min(want, max(1, P // 512)))
 
 
-def conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit):
-    with _Timed("conv_wgrad_i8", xq.numel() + gq.numel() + nsplit * d.KH * d.KW * d.Cin * d.Cout * 4):
-        _conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit)
+def wgrad_nshard(d, nsplit):
+    """Shards of the MFMA wgrad slab: each covers <= 65536 pixels (int32-exact partial sums)."""
+    P = d.N * d.Ho * d.Wo
+    per = -(-P // nsplit)
+    return -(-nsplit // max(1, 65536 // per))
 
 
-def _conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit):
-    call("lbt_conv_wgrad_i8", ptr(xq), int(x_u8off), ptr(gq), d, ptr(slab), int(nsplit), stream())
+def wgrad_slab(cache, key, d, ctx):
+    """(nsplit, nshard, zeroed int32 slab [nshard, K, Cout]) carved from the context's sums arena."""
+    ns = wgrad_nsplit(d)
+    nh = wgrad_nshard(d, ns)
+    n = nh * d.KH * d.KW * d.Cin * d.Cout
+    slab = cache.sums(key, (n + 1) // 2, ctx).view(torch.int32)[:n].view(nh, d.KH * d.KW * d.Cin, d.Cout)
+    return ns, nh, slab
+
+
+def conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit, nshard):
+    with _Timed("conv_wgrad_i8", xq.numel() + gq.numel() + nshard * d.KH * d.KW * d.Cin * d.Cout * 4):
+        _conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit, nshard)
+
+
+def _conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit, nshard):
+    call("lbt_conv_wgrad_i8", ptr(xq), int(x_u8off), ptr(gq), d, ptr(slab), int(nsplit), int(nshard), stream())
 
 
 def conv_wgrad_reduce(slab, nsplit, K, Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw):

@@ -341,8 +341,9 @@ class FusedResNet:
         if self.overlap_wgrad:
             bwd.append(self._join_side())
         self._rjobs = _dev_array(rjobs, ctx.device)
-        maxb = max((j.K * j.Cout + 31) // 32 for j in rjobs)
-        bwd.append(L("lbt_conv_wgrad_reduce_many", ptr(self._rjobs), len(rjobs), maxb))
+        total_blocks = sum((j.K * j.Cout + 255) // 256 for j in rjobs)
+        bwd.append(L("lbt_conv_wgrad_reduce_many", ptr(self._rjobs), len(rjobs), total_blocks, k="wgrad_reduce_many_kernel",
+                     nb=sum(4 * j.nsplit * j.K * j.Cout + 8 * j.K * j.Cout for j in rjobs)))
         self._pjobs = _dev_array(pjobs, ctx.device)
         bwd.append(L("lbt_bn_param_grads_many", ptr(self._pjobs), len(pjobs), max(j.C for j in pjobs)))
         # ---- this step's noise tables: one launch ahead of everything else
@@ -549,9 +550,8 @@ class FusedResNet:
                          c2.W_range.desc, ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg2 + 4 * numel))
             aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
         keep.append(aA1)
-        ns2 = ops.wgrad_nsplit(d2)
-        slab2 = self._buf(k + "slab2", (ns2, 9 * C, C), torch.int32)
-        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), ns2,
+        sp2, ns2, slab2 = ops.wgrad_slab(self._c, k + "slab2", d2, self.ctx)
+        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), sp2, ns2,
                                    k="conv_wgrad_kernel", nb=f["xb"].numel() + gq2.numel() + 4 * slab2.numel())))
         rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), self._qd(c2.X_range),
                           self._qd(c2.grad_range), c2.W.data_ptr(), ops.f32(2 * c2.weight_decay), c2.dW.data_ptr()))
@@ -581,16 +581,14 @@ class FusedResNet:
             gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
             bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range),
                          c1.W_range.desc, ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg1))
-        ns1 = ops.wgrad_nsplit(d1)
-        slab1 = self._buf(k + "slab1", (ns1, 9 * Cin, C), torch.int32)
-        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), ns1,
+        sp1, ns1, slab1 = ops.wgrad_slab(self._c, k + "slab1", d1, self.ctx)
+        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), sp1, ns1,
                                    k="conv_wgrad_kernel", nb=f["xa"].numel() + gq1.numel() + 4 * slab1.numel())))
         rjobs.append(RJob(slab1.data_ptr(), ns1, 9 * Cin, C, 1, gcol1.data_ptr(), self._qd(c1.X_range),
                           self._qd(c1.grad_range), c1.W.data_ptr(), ops.f32(2 * c1.weight_decay), c1.dW.data_ptr()))
         if cs is not None:
-            nss = ops.wgrad_nsplit(ds)
-            slabs = self._buf(k + "slabs", (nss, Cin, C), torch.int32)
-            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xs"]), 1, ptr(gqs), ds, ptr(slabs), nss,
+            sps, nss, slabs = ops.wgrad_slab(self._c, k + "slabs", ds, self.ctx)
+            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xs"]), 1, ptr(gqs), ds, ptr(slabs), sps, nss,
                                        k="conv_wgrad_kernel", nb=f["xs"].numel() + gqs.numel() + 4 * slabs.numel())))
             rjobs.append(RJob(slabs.data_ptr(), nss, Cin, C, 1, gcols.data_ptr(), self._qd(cs.X_range),
                               self._qd(cs.grad_range), cs.W.data_ptr(), ops.f32(2 * cs.weight_decay), cs.dW.data_ptr()))
