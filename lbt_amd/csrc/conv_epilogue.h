@@ -75,8 +75,8 @@ LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, 
     for (int i = 0; i < 4; ++i) {
       const int64_t row = mtile * 16 + 4 * kg + i;
       if (row < o.M) {
-        const int c = quant1(qs, o.q.stochastic, v[j][i], u[j][i], ov1, ov2);
-        o.yq[row * o.ncol + col] = (int8_t)c;
+        const int c = quant_w<-1>(qs, o.q.stochastic, v[j][i], u[j][i], ov1, ov2);
+        o.yq[(uint32_t)row * (uint32_t)o.ncol + col] = (int8_t)c;  // M * ncol < 2^31 (launchers)
         s1[j] += c;
         s2[j] += c * c;
       }
@@ -96,7 +96,7 @@ LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, 
       }
     }
   }
-  if (o.q.counts) counts_stage(0, 1, ov1, ov2, sh.cnt);
+  if (o.q.counts) counts_stage_w(0, 1, ov1, ov2, sh.cnt);  // wave totals (quant_w)
   if (!(want_sum || o.q.counts)) return;
   __syncthreads();  // the only barrier: counters and channel sums of the whole block
   counts_publish(0, 1, o.q, sh.cnt);
@@ -159,9 +159,9 @@ LBT_DEV void chain_prefetch(const lbt_chain_bwd_a& c, const float* add_src, int6
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int col = (nt0 + j) * 16 + r;
-      const int64_t e = rr * ncol + col;
+      const uint32_t e = (uint32_t)rr * (uint32_t)ncol + col;  // M * ncol < 2^31 (launcher)
       const uint32_t ni = pix * (uint32_t)ncol + col;
-      p.add[j][i] = as[(uint32_t)e & amask];
+      p.add[j][i] = as[e & amask];
       if (CF & kAYMask) p.ym[j][i] = c.y_mask[e];
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
@@ -215,7 +215,7 @@ LBT_DEV void chain_epi(const lbt_chain_bwd_a& c, bool has_add, int64_t M, int nc
     for (int i = 0; i < 4; ++i) {
       const int64_t row = mtile * 16 + 4 * kg + i;
       if (row >= M) continue;
-      const int64_t e = row * ncol + col;
+      const uint32_t e = (uint32_t)row * (uint32_t)ncol + col;
       float g = has_add ? v[j][i] + p.add[j][i] : v[j][i];
       if (CF & kAYMask) {
         g = p.ym[j][i] > 0.f ? g : 0.f;

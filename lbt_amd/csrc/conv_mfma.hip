@@ -206,7 +206,9 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[j][i] = (float)(acc[j][i] + corr[j]) * scale;
   if constexpr (CF != 0) {
+    LBT_TS(2);
     chain_epi<NT, NB, CF>(p.chain, p.add_src != nullptr, p.M, p.ncol, mtile, nt0, wave, lane, v, cp, csh);
+    LBT_TS(3);
     return;
   }
   if (!want_q) {
@@ -378,7 +380,7 @@ int launch_gemm_nt(const GemmArgs& p, int cs, hipStream_t st) {
 
 template <int MODE>
 int launch_gemm(const GemmArgs& p, int cs, hipStream_t st) {
-  if (p.M >= (int64_t)1 << 31) return LBT_EINVAL;  // 32-bit row arithmetic
+  if (p.M * p.ncol >= (int64_t)1 << 31) return LBT_EINVAL;  // 32-bit row / element arithmetic
   switch (p.ncol / 16) {
     case 1: return launch_gemm_nt<MODE, 1>(p, cs, st);
     case 2: return launch_gemm_nt<MODE, 2>(p, cs, st);
@@ -460,7 +462,7 @@ extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32
   p.ychsum = nullptr;
   p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
   p.chain = *a;
-  if (p.M >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  if (p.M * p.ncol >= ((int64_t)1 << 31)) return LBT_EINVAL;  // 32-bit element offsets
   hipStream_t st = (hipStream_t)stream;
   const int nt = d.Cin / 16;
   const int key = (cs << 8) | (nt << 4) | (a->has_b2 ? 1 : 0);

@@ -180,14 +180,10 @@ LBT_DEV int quant_w(const QState& s, int stochastic, float x, float u, int& ov1w
 }
 
 // Wave-total counters (from quant_w) of quantiser i of nq into the block's LDS staging area.
-// A lane inactive during some quant_w calls holds a partial total: the wave max is the total
-// (callers keep at least one lane active through every call). All 64 lanes must call it.
+// Lane 0 publishes: callers guarantee lane 0 was active in every quant_w call of the wave (their
+// inactive lanes are trailing ones -- elements past the end -- so the lowest lane always has work
+// when any lane does), hence its running totals are the wave's.
 LBT_DEV void counts_stage_w(int i, int nq, int ov1w, int ov2w, int* sh) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    ov1w = max(ov1w, __shfl_xor(ov1w, o, 64));
-    ov2w = max(ov2w, __shfl_xor(ov2w, o, 64));
-  }
   if ((threadIdx.x & 63) == 0) {
     int* p = sh + (threadIdx.x >> 6) * 2 * nq + 2 * i;
     p[0] = ov1w;

@@ -231,7 +231,7 @@ extern "C" int lbt_conv_stem_fwd(const int16_t* x, const int8_t* w_hwio, lbt_con
   StemFwdArgs p;
   p.x = x; p.w = w_hwio; p.d = d; p.K = K; p.qx = qx; p.qw = qw; p.y = y;
   p.o = QOut{yq, qout, yq ? ychsum : nullptr, M, d.Cout, (int64_t)d.Ho * d.Wo};
-  if (M >= (int64_t)1 << 31) return LBT_EINVAL;
+  if (M * d.Cout >= (int64_t)1 << 31) return LBT_EINVAL;  // 32-bit element offsets
   hipStream_t st = (hipStream_t)stream;
   const int64_t mtiles = (M + 15) / 16;
   switch (d.Cout / 16) {

@@ -177,6 +177,7 @@ class FusedResNet:
                     rc = fn(*args, st())
                 if rc:
                     raise _lib.LbtError("%s failed with status %d" % (name, rc))
+            run.kname = kname
             return run
 
         self._nd, njobs = {}, []
