@@ -11,7 +11,9 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime before the kernels library)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblbt_dfxp.so")
+# LBT_LIBRARY: an alternative build of the same C-ABI (e.g. instrumented scratch builds for kernel
+# studies); the default is the in-tree build.
+LIB_PATH = os.environ.get("LBT_LIBRARY") or os.path.join(HERE, "liblbt_dfxp.so")
 
 NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS

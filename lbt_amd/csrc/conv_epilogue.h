@@ -112,7 +112,7 @@ LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, 
         const int64_t row0 = ((int64_t)blockIdx.x * MTB + mt) * 16;
         if (row0 < o.M) tot += sh.part[mt * WPM + wcol][which][lc];
       }
-      if (tot) atomicAdd((unsigned long long*)&o.chsum[(int64_t)shard_id() * 2 * o.ncol + t], (unsigned long long)tot);
+      if (tot) LBT_GADD((unsigned long long*)&o.chsum[(int64_t)shard_id() * 2 * o.ncol + t], (unsigned long long)tot);
     }
   }
 }
@@ -274,7 +274,7 @@ LBT_DEV void chain_epi(const lbt_chain_bwd_a& c, bool has_add, int64_t M, int nc
 #pragma unroll
     for (int mt = 0; mt < MTB; ++mt) tot += sh.part[mt * WPM + wcol][b][s][lc];
     int64_t* dst = (b == 0 ? c.b1 : c.b2).sums;
-    if (tot) atomicAdd((unsigned long long*)&dst[(int64_t)shard_id() * 4 * ncol + rem], (unsigned long long)tot);
+    if (tot) LBT_GADD((unsigned long long*)&dst[(int64_t)shard_id() * 4 * ncol + rem], (unsigned long long)tot);
   }
 }
 

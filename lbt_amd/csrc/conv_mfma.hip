@@ -21,10 +21,10 @@
 // workgroup owns a pixel range and one tap and writes an int32 partial (exact, no atomics).
 #include "conv_epilogue.h"
 #include "chain_flags.h"
+#include "lds_tr.h"
 
 using namespace lbt;
 
-typedef int v4i __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -240,17 +240,6 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0
 // (split % nshard) of a zeroed slab[nshard][tap][ci][co] for the batched reduce.
 constexpr int kWP = 64;  // pixels per wave chunk
 
-typedef int v2i __attribute__((ext_vector_type(2)));
-
-// 16 pixels (rows base..base+15 of a [pixel][16 B] image) of channel (lane & 15): 16 bytes
-LBT_DEV v4i tr_frag(const int8_t* img, int base, int lane) {
-  const int j = lane & 15;
-  const int8_t* p0 = img + (base + (j >> 1)) * 16 + 8 * (j & 1);
-  typedef __attribute__((address_space(3))) v2i lds_v2i;
-  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p0));
-  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p0 + 8 * 16));
-  return v4i{lo.x, lo.y, hi.x, hi.y};
-}
 
 template <int CSI>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __restrict__ xq,
@@ -327,7 +316,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
   for (int i = threadIdx.x; i < CI * 16; i += kThreads) {
     const int ci = i >> 4, co = i & 15;
     const int v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-    if (v) atomicAdd(&dst[(int64_t)ci * d.Cout + co], v);  // integer atomics: exact, order-independent
+    if (v) LBT_GADD(&dst[(int64_t)ci * d.Cout + co], v);  // integer atomics: exact, order-independent
   }
   LBT_TS(3);
 }

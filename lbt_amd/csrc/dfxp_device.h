@@ -12,6 +12,14 @@
 
 #define LBT_DEV __device__ __forceinline__
 
+// Global reduction flushes (counters, channel sums, weight-gradient shards). LBT_EXP_PLAINSTORE
+// is a timing experiment only (scratch builds): plain stores instead of atomics, wrong results.
+#ifdef LBT_EXP_PLAINSTORE
+#define LBT_GADD(p, v) (*(p) = (v))
+#else
+#define LBT_GADD(p, v) atomicAdd((p), (v))
+#endif
+
 // Phase timestamps for kernel studies (scratch builds with -DLBT_TRACE only): LBT_TS(i) stores
 // s_memrealtime (100 MHz) of workgroup thread 0 into trace[wg*8 + i]; slot 7 = XCC id.
 #ifdef LBT_TRACE
@@ -228,7 +236,7 @@ LBT_DEV void counts_publish(int i, int nq, const lbt_qdesc& q, const int* sh) {
   const int nw = (blockDim.x + 63) >> 6;
   int t = 0;
   for (int w = 0; w < nw; ++w) t += sh[w * 2 * nq + 2 * i + j];
-  if (t) atomicAdd(q.counts + ((int64_t)q.slot * LBT_NSHARD + shard_id()) * LBT_CSTRIDE + j, t);
+  if (t) LBT_GADD(q.counts + ((int64_t)q.slot * LBT_NSHARD + shard_id()) * LBT_CSTRIDE + j, t);
 }
 
 // Single-quantiser flush for kernels with nothing else to publish. EVERY thread of the block
@@ -246,7 +254,7 @@ LBT_DEV void block_flush_counts(const lbt_qdesc& q, int ov1, int ov2, int* sh) {
 LBT_DEV void block_flush_sums(const long long* sh, int n, int64_t* dst, int stride) {
   int64_t* d = dst + (int64_t)shard_id() * stride;
   for (int i = threadIdx.x; i < n; i += blockDim.x)
-    if (sh[i]) atomicAdd((unsigned long long*)&d[i], (unsigned long long)sh[i]);
+    if (sh[i]) LBT_GADD((unsigned long long*)&d[i], (unsigned long long)sh[i]);
 }
 
 // Per-channel partial sums of "channel-quad" threads: thread g owns elements 4g..4g+3 of a row,

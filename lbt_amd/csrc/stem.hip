@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const int16_t* __r
   for (int i = threadIdx.x; i < K * d.Cout; i += kThreads) {
     const int k = i / d.Cout, c = i - k * d.Cout;
     const int v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
-    if (v) atomicAdd(&out[i], v);  // integer atomics: exact, order-independent
+    if (v) LBT_GADD(&out[i], v);  // integer atomics: exact, order-independent
   }
 }
 
