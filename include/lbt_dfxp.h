@@ -296,6 +296,32 @@ int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW, int32_t C,
 /* mean sparse softmax cross-entropy (models.py:30-32) -> loss[0] (fp32, device), dz = d loss / d z. */
 int lbt_softmax_xent(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss,
                      float* dz, void* stream);
+/* The whole classifier head of CIFAR10_Resnet20 in ONE launch (one workgroup per sample plus a
+ * last-arriving workgroup), fwd AND bwd -- replaces lbt_avgpool_fwd, lbt_dfxp_quantize (pooled,
+ * Dense_q X), lbt_conv_fwd_generic (Dense_q y = Xq Wq), lbt_softmax_xent, lbt_dfxp_quantize
+ * (Dense_q grad), lbt_conv_wgrad_generic + its reduce, lbt_conv_dgrad_generic and
+ * lbt_avgpool_bwd with the same arithmetic bit for bit:
+ *   AvgPool_q   dynamic_fixed_point.py:1009-1022, Dense_q :319-395 (fwd) / :441-466 (bwd),
+ *   loss        models.py:30-32 (mean sparse softmax cross-entropy).
+ * x [N][HW][C] fp32 (last block output) -> logits, loss[0], dz; dw = dequant(sum_n pq^T gq) + wd2*w
+ * (exactly lbt_conv_wgrad_reduce's formula); gx [N][HW][C] = d loss / d x. wq is the Dense_q
+ * weight codes [C][K] (lbt_dfxp_quantize_weights' w_hwio of a C x 1 x 1 x K job). qx / qg are
+ * the stochastic X / grad quantisers (noise tables of C / K values, or Philox inline).
+ * pooled, pq, gq are optional outputs (NULL = not stored). scratch: lbt_head_scratch_bytes(N, C, K)
+ * bytes, any content. *ticket must be 0 on entry; the kernel leaves it 0.
+ * Limits: C <= 256, C % 4 == 0, 1 <= K <= 64, HW >= 1.                                        */
+typedef struct lbt_head {
+  const float* x; int32_t N, HW, C, K;
+  float* pooled; int8_t* pq; lbt_qdesc qx;
+  const int8_t* wq; lbt_qdesc qw;
+  const int32_t* labels; float* logits; float* loss; float* dz;
+  int8_t* gq; lbt_qdesc qg;
+  const float* w; float wd2; float* dw;
+  float* gx;
+  void* scratch; uint32_t* ticket;
+} lbt_head;
+int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K);  /* = N * (C + 72) */
+int lbt_head_fwd_bwd(const lbt_head* h, void* stream);
 /* MomentumOptimizer.apply_gradients (trainer.py:81-82): a = mu*a + g*gscale; w -= lr*a. */
 int lbt_sgd_momentum(float* w, float* a, const float* g, int64_t n, float lr, float mu,
                      float gscale, void* stream);

@@ -103,6 +103,17 @@ class PJob(ctypes.Structure):
                 ("wd2", c_float), ("dgamma", c_void_p), ("dbeta", c_void_p)]
 
 
+class Head(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("N", c_int32), ("HW", c_int32), ("C", c_int32), ("K", c_int32),
+                ("pooled", c_void_p), ("pq", c_void_p), ("qx", QDesc),
+                ("wq", c_void_p), ("qw", QDesc),
+                ("labels", c_void_p), ("logits", c_void_p), ("loss", c_void_p), ("dz", c_void_p),
+                ("gq", c_void_p), ("qg", QDesc),
+                ("w", c_void_p), ("wd2", c_float), ("dw", c_void_p),
+                ("gx", c_void_p),
+                ("scratch", c_void_p), ("ticket", c_void_p)]
+
+
 _P = c_void_p
 _SIGS = {
     "lbt_abi_version": [],
@@ -141,6 +152,8 @@ _SIGS = {
     "lbt_selftest_div": [_P, _P, c_int64, _P, _P, _P, _P],
     "lbt_conv_wgrad_reduce_many": [_P, c_int32, c_int32, _P],
     "lbt_bn_param_grads_many": [_P, c_int32, c_int32, _P],
+    "lbt_head_scratch_bytes": [c_int32, c_int32, c_int32],
+    "lbt_head_fwd_bwd": [_P, _P],
 }
 EXPORTED = sorted(_SIGS)
 

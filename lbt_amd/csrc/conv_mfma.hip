@@ -254,12 +254,21 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
   LBT_TS(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kg = lane >> 4;
-  const int tap = blockIdx.y, cso = blockIdx.z;
+  // XCD-aware unit order: workgroups are dealt round-robin over the 8 XCDs, so unit u of the
+  // split-major order (split, tap, co-slice) goes to linear block (u % chunk) * 8 + u / chunk:
+  // all taps / co-slices of one pixel split -- which re-read the same G and X bytes -- share one
+  // XCD's L2 (speed only; any order gives the same integer sums).
+  const int ntap = d.KH * d.KW, ncos = d.Cout >> 4, total = nsplit * ntap * ncos;
+  const int chunk = (total + 7) >> 3;
+  const int u = (int)(blockIdx.x & 7) * chunk + (int)(blockIdx.x >> 3);
+  if (u >= total) return;
+  const int split = u / (ntap * ncos), urem = u - split * (ntap * ncos);
+  const int tap = urem / ncos, cso = urem - tap * ncos;
   const int kh = tap / d.KW, kw = tap - kh * d.KW;
   int8_t* Xi = lds[wave];
   int8_t* Gi = lds[wave] + CSI * kWP * 16;
   const int64_t per = (P + nsplit - 1) / nsplit;
-  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p0 = (int64_t)split * per;
   const int64_t p1 = p0 + per < P ? p0 + per : P;
   const uint32_t HWo = (uint32_t)d.Ho * d.Wo;
 
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
     for (int i = 0; i < 4; ++i) red[wave][(a * 16 + kg * 4 + i) * 16 + r] = acc[a][i];
   __syncthreads();
   LBT_TS(2);
-  int32_t* dst = slab + ((int64_t)(blockIdx.x % nshard) * (d.KH * d.KW) + tap) * CI * d.Cout + cso * 16;
+  int32_t* dst = slab + ((int64_t)(split % nshard) * (d.KH * d.KW) + tap) * CI * d.Cout + cso * 16;
   for (int i = threadIdx.x; i < CI * 16; i += kThreads) {
     const int ci = i >> 4, co = i & 15;
     const int v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
@@ -477,7 +486,9 @@ extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t
   if ((P + nsplit - 1) / nsplit * ((nsplit + nshard - 1) / nshard) > 65536) return LBT_EINVAL;
   const int csi = d.Cin / 16;
   const int fill = x_u8off ? (int)0x80808080u : 0;
-  dim3 grid(nsplit, d.KH * d.KW, d.Cout / 16);
+  const int64_t units = (int64_t)nsplit * d.KH * d.KW * (d.Cout / 16);
+  if (units >= ((int64_t)1 << 30)) return LBT_EINVAL;
+  dim3 grid((unsigned)((units + 7) / 8 * 8));
   hipStream_t st = (hipStream_t)stream;
   switch (csi) {
     case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;

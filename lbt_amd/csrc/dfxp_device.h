@@ -96,6 +96,14 @@ LBT_DEV float qnoise1(const lbt_qdesc& q, uint64_t step, uint64_t idx) {
   return q.noise ? q.noise[idx] : noise1(idx, q.qid, step, q.seed);
 }
 
+// ------------------------------------------------------------------ branch-free operand loads
+// A load whose value leaves a branch becomes a register copy that must wait for the load, which
+// serialises a kernel's gathers. Optional operands therefore load from this zero block instead
+// (index masked to 0) and out-of-range gathers from a clamped address, selected afterwards.
+static __device__ __attribute__((aligned(16))) int32_t kZeroBlock[64];  // zero-initialised, never written
+LBT_DEV const float* zf() { return reinterpret_cast<const float*>(kZeroBlock); }
+LBT_DEV const int32_t* zi() { return kZeroBlock; }
+
 // ------------------------------------------------------------------ quantiser state
 // The per-call view of one quantiser: multiplier m = 2^e, limit L = 2^(bits-1).
 struct QState {
@@ -110,17 +118,26 @@ LBT_DEV int frac_exp(const lbt_qdesc& q) {
   return e < 0 ? 0 : (e > kEMax ? kEMax : e);
 }
 
+// Branch-free: the exponent and step loads of every quantiser a kernel uses issue together (an
+// inactive quantiser, or one without a step counter, reads the zero block), so a kernel's
+// prologue pays one dependent scalar-memory round trip for all of them instead of one (or two)
+// per quantiser.
 LBT_DEV QState qstate(const lbt_qdesc& q) {
   QState s;
   s.active = q.bits > 0;
-  if (!s.active) { s.m = s.inv_m = s.L = s.Lm1 = s.Lh = 0.f; s.e = 0; s.step = 0; return s; }
-  s.e = frac_exp(q);
-  s.m = ldexpf(1.0f, s.e);
-  s.inv_m = ldexpf(1.0f, -s.e);
-  s.L = ldexpf(1.0f, q.bits - 1);
-  s.Lm1 = s.L - 1.0f;
-  s.Lh = ldexpf(1.0f, q.bits - 2);
-  s.step = q.step ? *q.step : 0ull;
+  const int32_t* ep = s.active ? q.exps + q.slot : zi();
+  const uint64_t* sp = (s.active && q.step) ? q.step : reinterpret_cast<const uint64_t*>(zi());
+  const int I = *ep;
+  const uint64_t st = *sp;
+  int e = q.bits - I - 1;
+  e = e < 0 ? 0 : (e > kEMax ? kEMax : e);
+  s.e = s.active ? e : 0;
+  s.m = s.active ? ldexpf(1.0f, e) : 0.f;
+  s.inv_m = s.active ? ldexpf(1.0f, -e) : 0.f;
+  s.L = s.active ? ldexpf(1.0f, q.bits - 1) : 0.f;
+  s.Lm1 = s.active ? s.L - 1.0f : 0.f;
+  s.Lh = s.active ? ldexpf(1.0f, q.bits - 2) : 0.f;
+  s.step = st;
   return s;
 }
 
@@ -164,13 +181,6 @@ LBT_DEV float div_by(float x, const Recip& d) {
   return copysignf(fmaf(r1, d.rc, q1), x);
 }
 
-// ------------------------------------------------------------------ branch-free operand loads
-// A load whose value leaves a branch becomes a register copy that must wait for the load, which
-// serialises a kernel's gathers. Optional operands therefore load from this zero block instead
-// (index masked to 0) and out-of-range gathers from a clamped address, selected afterwards.
-static __device__ int32_t kZeroBlock[64];  // zero-initialised, never written (global space)
-LBT_DEV const float* zf() { return reinterpret_cast<const float*>(kZeroBlock); }
-LBT_DEV const int32_t* zi() { return kZeroBlock; }
 
 // Same quantiser, overflow predicates counted per WAVE: the compares become lane masks and
 // s_bcnt1 / s_add on the scalar unit accumulate them, so ov1w / ov2w are wave totals (identical in

@@ -102,19 +102,32 @@ class FusedResNet:
         self._ensure(X)
         if X.data_ptr() != self._X.data_ptr():
             self._X.copy_(X)
-        for f in self._fwd:  # the first launch also zeroes the step's sums
+        for f in self._fwd + self._hfwd:  # the first launch also zeroes the step's sums
             f()
         return self.logits
 
     def compute_loss(self, labels):
         if labels.data_ptr() != self._labels.data_ptr():
             self._labels.copy_(labels)
-        ops.softmax_xent(self.logits, self._labels, self.loss, self.dlogits)
+        for f in self._hloss:
+            f()
         return self.loss
 
     def backward(self):
-        for f in self._bwd:
+        for f in self._hbwd + self._bwd:
             f()
+
+    def train_fwd_bwd(self, X, labels):
+        """forward + compute_loss + backward of one training step, the head as one launch
+        (lbt_head_fwd_bwd): same results bit for bit as the three calls."""
+        self._ensure(X)
+        if X.data_ptr() != self._X.data_ptr():
+            self._X.copy_(X)
+        if labels.data_ptr() != self._labels.data_ptr():
+            self._labels.copy_(labels)
+        for f in self._fwd + self._hfused + self._bwd:
+            f()
+        return self.loss
 
     # ------------------------------------------------------------------ streams
     def _on_side(self, run):
@@ -269,38 +282,53 @@ class FusedResNet:
             saved.append(info)
         Ylast = Xin
 
-        # ---- head: avg pool, dense, loss
+        # ---- head: avg pool, dense, loss -- as separate launches (forward / compute_loss /
+        # backward called one by one) and as ONE fused launch (train_fwd_bwd, the training step)
         Nb, Hh, Wh, Ch = Ylast.shape
         pooled = self._buf("pool", (Nb, Ch), torch.float32)
-        fwd.append(L("lbt_avgpool_fwd", ptr(Ylast), ptr(pooled), Nb, Hh * Wh, Ch))
+        hfwd, hloss, hbwd = [], [], []
+        hfwd.append(L("lbt_avgpool_fwd", ptr(Ylast), ptr(pooled), Nb, Hh * Wh, Ch))
         dd = _lib.ConvDesc(Nb, 1, 1, d.in_units, d.units, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
         d.d = dd
         pq = self._buf("pq", (Nb, Ch), torch.int8)
         obs(d.X_range, pooled.numel())
-        fwd.append(L("lbt_dfxp_quantize", ptr(pooled), ptr(pq), OUT_I8, Nb, Ch, self._qd(d.X_range), None, 0))
+        hfwd.append(L("lbt_dfxp_quantize", ptr(pooled), ptr(pq), OUT_I8, Nb, Ch, self._qd(d.X_range), None, 0))
         self.logits = self._buf("logits", (Nb, d.units), torch.float32)
-        fwd.append(L("lbt_conv_fwd_generic", ptr(pq), 0, ptr(d.w_hwio), dd, self._qd(d.X_range), d.W_range.desc,
-                     ptr(self.logits)))
+        hfwd.append(L("lbt_conv_fwd_generic", ptr(pq), 0, ptr(d.w_hwio), dd, self._qd(d.X_range), d.W_range.desc,
+                      ptr(self.logits)))
         self.loss = self._buf("loss", (1,), torch.float32)
         self.dlogits = self._buf("dz", (Nb, d.units), torch.float32)
+        hloss.append(L("lbt_softmax_xent", ptr(self.logits), ptr(self._labels), Nb, d.units, ptr(self.loss),
+                       ptr(self.dlogits)))
 
         # ================================================================ backward
         rjobs, pjobs = [], []
         gqd = self._buf("gqd", (Nb, d.units), torch.int8)
         obs(d.grad_range, self.dlogits.numel())
-        bwd.append(L("lbt_dfxp_quantize", ptr(self.dlogits), ptr(gqd), OUT_I8, Nb, d.units, self._qd(d.grad_range), None,
-                     0))
+        hbwd.append(L("lbt_dfxp_quantize", ptr(self.dlogits), ptr(gqd), OUT_I8, Nb, d.units, self._qd(d.grad_range), None,
+                      0))
         nsd = ops.wgrad_nsplit(dd, generic=True)
         slabd = self._buf("slabd", (nsd, d.in_units, d.units), torch.int32)
-        bwd.append(self._on_side(L("lbt_conv_wgrad_generic", ptr(pq), 0, ptr(gqd), dd, ptr(slabd), nsd,
-                                   k="conv_wgrad_generic_kernel", nb=pq.numel() + gqd.numel() + 4 * slabd.numel())))
-        rjobs.append(RJob(slabd.data_ptr(), nsd, d.in_units, d.units, 0, None, self._qd(d.X_range), self._qd(d.grad_range),
-                          d.W.data_ptr(), ops.f32(2 * d.weight_decay), d.dW.data_ptr()))
+        hbwd.append(L("lbt_conv_wgrad_generic", ptr(pq), 0, ptr(gqd), dd, ptr(slabd), nsd,
+                      k="conv_wgrad_generic_kernel", nb=pq.numel() + gqd.numel() + 4 * slabd.numel()))
+        hbwd.append(L("lbt_conv_wgrad_reduce", ptr(slabd), nsd, d.in_units, d.units, 0, None, self._qd(d.X_range),
+                      self._qd(d.grad_range), ptr(d.W), ops.f32(2 * d.weight_decay), ptr(d.dW)))
         dpool = self._buf("dpool", (Nb, Ch), torch.float32)
-        bwd.append(L("lbt_conv_dgrad_generic", ptr(gqd), ptr(d.w_hwio), dd, self._qd(d.grad_range), d.W_range.desc,
-                     ptr(dpool), None))
+        hbwd.append(L("lbt_conv_dgrad_generic", ptr(gqd), ptr(d.w_hwio), dd, self._qd(d.grad_range), d.W_range.desc,
+                      ptr(dpool), None))
         gY = self._buf("gYlast", Ylast.shape, torch.float32)
-        bwd.append(L("lbt_avgpool_bwd", ptr(dpool), ptr(gY), Nb, Hh * Wh, Ch))
+        hbwd.append(L("lbt_avgpool_bwd", ptr(dpool), ptr(gY), Nb, Hh * Wh, Ch))
+        scratch = self._buf("head_scratch", (lib.lbt_head_scratch_bytes(Nb, Ch, d.units),), torch.uint8)
+        ticket = self._sums("head_ticket", 1)  # zeroed with the step's sums (and left zero by the kernel)
+        hd = _lib.Head(Ylast.data_ptr(), Nb, Hh * Wh, Ch, d.units, pooled.data_ptr(), pq.data_ptr(), self._qd(d.X_range),
+                       d.w_hwio.data_ptr(), d.W_range.desc, self._labels.data_ptr(), self.logits.data_ptr(),
+                       self.loss.data_ptr(), self.dlogits.data_ptr(), gqd.data_ptr(), self._qd(d.grad_range),
+                       d.W.data_ptr(), ops.f32(2 * d.weight_decay), d.dW.data_ptr(), gY.data_ptr(),
+                       scratch.data_ptr(), ticket.data_ptr())
+        self._head = hd
+        hfused = [L("lbt_head_fwd_bwd", ctypes.byref(hd), k="head_kernel",
+                    nb=4 * Ylast.numel() * 2 + 4 * d.W.numel() * 3)]
+        self._hfwd, self._hloss, self._hbwd, self._hfused = hfwd, hloss, hbwd, hfused
         # Pass-A descriptors of every block-end BN chain and of the stem's, built first: each runs
         # as the epilogue of the dgrad that produces its input gradient (lbt_conv_dgrad_chain_i8),
         # except the last block's, which follows the avgpool backward.

@@ -92,9 +92,12 @@ class Trainer:
         m = self.model
         if not getattr(m, "zeroes_own_sums", False):
             self.ctx.zero_sums()
-        m.forward(X)
-        m.compute_loss(y)
-        m.backward()
+        if hasattr(m, "train_fwd_bwd"):
+            m.train_fwd_bwd(X, y)
+        else:
+            m.forward(X)
+            m.compute_loss(y)
+            m.backward()
         if self.comm is not None:
             self.ctx.fold_counts(self.comm[self.flat.n:])
 
@@ -137,9 +140,13 @@ class Trainer:
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             self._fwd_bwd(sX, sy)
-        g2 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g2):
-            self._update()
+            if self.world == 1:  # nothing to exchange: the whole step is one graph
+                self._update()
+        g2 = None
+        if self.world > 1:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._update()
         self._graphs = (g1, g2)
 
     def step(self, X, y):
@@ -154,9 +161,9 @@ class Trainer:
                 self._static[1].copy_(y)
             g1, g2 = self._graphs
             g1.replay()
-            if self.world > 1:
+            if g2 is not None:
                 self._exchange()
-            g2.replay()
+                g2.replay()
         self.global_step += 1
         return self.model.loss
 

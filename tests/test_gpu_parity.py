@@ -460,3 +460,74 @@ def test_fused_executor_bitidentical_to_layerwise():
     torch.cuda.synchronize()
     assert np.array_equal(tA.flat.w.cpu().numpy(), tB.flat.w.cpu().numpy())
     assert ctxA.ranges() == ctxB.ranges()
+
+
+@pytest.mark.parametrize("N,HW,C,K,table", [(128, 64, 64, 10, True), (300, 16, 32, 7, False), (5, 3, 256, 64, True)])
+def test_head_kernel_equals_launch_sequence(N, HW, C, K, table):
+    """lbt_head_fwd_bwd == avgpool_fwd, quantize, dense fwd, softmax_xent, quantize, dense wgrad +
+    reduce, dense dgrad, avgpool_bwd as separate launches: every output and counter bit for bit
+    (with noise tables and with inline Philox; N > 256 exercises the loss-term striding)."""
+    import ctypes
+    from lbt_amd import _lib
+    rng = np.random.default_rng(N + C)
+    x = torch.from_numpy(rng.uniform(0, 3, size=(N, HW, C)).astype(np.float32)).to(DEV)
+    W = torch.from_numpy(rng.uniform(-0.5, 0.5, size=(C, K)).astype(np.float32)).to(DEV)
+    labels = torch.from_numpy(rng.integers(0, K, size=N).astype(np.int32)).to(DEV)
+    out = {}
+    for mode in ("seq", "head"):
+        ctx = DfxpContext(seed=77)
+        qx = ctx.quantizer("d/X_range", 8, 2)
+        qw = ctx.quantizer("d/W_range", 8, 1)
+        qg = ctx.quantizer("d/grad_range", 8, -4)
+        dx, dg = _lib.QDesc.from_buffer_copy(qx.desc), _lib.QDesc.from_buffer_copy(qg.desc)
+        keep = []
+        if table:
+            for d_, q, n in ((dx, qx, C), (dg, qg, K)):
+                t = torch.from_numpy(odfxp.noise_for((1, n), q.qid, 0, 77).reshape(-1).astype(np.float32)).to(DEV)
+                keep.append(t)
+                d_.noise = t.data_ptr()
+        wq = torch.empty((C, K), dtype=torch.int8, device=DEV)
+        _lib.call("lbt_dfxp_quantize", _lib.ptr(W), _lib.ptr(wq), OUT_I8, 1, C * K, qw.desc_nostats(), None, 0,
+                  _lib.stream())
+        pooled = torch.empty((N, C), device=DEV)
+        pq = torch.empty((N, C), dtype=torch.int8, device=DEV)
+        logits = torch.empty((N, K), device=DEV)
+        loss = torch.empty(1, device=DEV)
+        dz = torch.empty((N, K), device=DEV)
+        gq = torch.empty((N, K), dtype=torch.int8, device=DEV)
+        dW = torch.empty((C, K), device=DEV)
+        gx = torch.empty((N, HW, C), device=DEV)
+        wd2 = ops.f32(4e-4)
+        st = _lib.stream()
+        if mode == "seq":
+            dd = _lib.ConvDesc(N, 1, 1, C, K, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
+            _lib.call("lbt_avgpool_fwd", _lib.ptr(x), _lib.ptr(pooled), N, HW, C, st)
+            _lib.call("lbt_dfxp_quantize", _lib.ptr(pooled), _lib.ptr(pq), OUT_I8, N, C, dx, None, 0, st)
+            _lib.call("lbt_conv_fwd_generic", _lib.ptr(pq), 0, _lib.ptr(wq), dd, dx, qw.desc, _lib.ptr(logits), st)
+            _lib.call("lbt_softmax_xent", _lib.ptr(logits), _lib.ptr(labels), N, K, _lib.ptr(loss), _lib.ptr(dz), st)
+            _lib.call("lbt_dfxp_quantize", _lib.ptr(dz), _lib.ptr(gq), OUT_I8, N, K, dg, None, 0, st)
+            ns = ops.wgrad_nsplit(dd, generic=True)
+            slab = torch.empty((ns, C, K), dtype=torch.int32, device=DEV)
+            _lib.call("lbt_conv_wgrad_generic", _lib.ptr(pq), 0, _lib.ptr(gq), dd, _lib.ptr(slab), ns, st)
+            _lib.call("lbt_conv_wgrad_reduce", _lib.ptr(slab), ns, C, K, 0, None, dx, dg, _lib.ptr(W), wd2,
+                      _lib.ptr(dW), st)
+            dp = torch.empty((N, C), device=DEV)
+            _lib.call("lbt_conv_dgrad_generic", _lib.ptr(gq), _lib.ptr(wq), dd, dg, qw.desc, _lib.ptr(dp), None, st)
+            _lib.call("lbt_avgpool_bwd", _lib.ptr(dp), _lib.ptr(gx), N, HW, C, st)
+        else:
+            lib = _lib.load()
+            scratch = torch.empty(lib.lbt_head_scratch_bytes(N, C, K), dtype=torch.uint8, device=DEV)
+            ticket = torch.zeros(2, dtype=torch.int32, device=DEV)
+            h = _lib.Head(x.data_ptr(), N, HW, C, K, pooled.data_ptr(), pq.data_ptr(), dx, wq.data_ptr(), qw.desc,
+                          labels.data_ptr(), logits.data_ptr(), loss.data_ptr(), dz.data_ptr(), gq.data_ptr(), dg,
+                          W.data_ptr(), wd2, dW.data_ptr(), gx.data_ptr(), scratch.data_ptr(), ticket.data_ptr())
+            for _ in range(2):  # twice: the ticket must come back to zero
+                ctx.counts.zero_()
+                _lib.call("lbt_head_fwd_bwd", ctypes.byref(h), st)
+            torch.cuda.synchronize()
+            assert int(ticket[0].item()) == 0
+        torch.cuda.synchronize()
+        out[mode] = dict(pooled=pooled, pq=pq, logits=logits, loss=loss, dz=dz, gq=gq, dW=dW, gx=gx,
+                         counts=ctx.counts_view()[:3].sum(1))
+    for k, v in out["seq"].items():
+        assert torch.equal(v, out["head"][k]), k
