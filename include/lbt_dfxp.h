@@ -296,20 +296,20 @@ int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW, int32_t C,
 /* mean sparse softmax cross-entropy (models.py:30-32) -> loss[0] (fp32, device), dz = d loss / d z. */
 int lbt_softmax_xent(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss,
                      float* dz, void* stream);
-/* The whole classifier head of CIFAR10_Resnet20 in ONE launch (one workgroup per sample plus a
- * last-arriving workgroup), fwd AND bwd -- replaces lbt_avgpool_fwd, lbt_dfxp_quantize (pooled,
- * Dense_q X), lbt_conv_fwd_generic (Dense_q y = Xq Wq), lbt_softmax_xent, lbt_dfxp_quantize
- * (Dense_q grad), lbt_conv_wgrad_generic + its reduce, lbt_conv_dgrad_generic and
- * lbt_avgpool_bwd with the same arithmetic bit for bit:
+/* The classifier head of CIFAR10_Resnet20, fwd AND bwd, per sample in ONE launch (a workgroup
+ * per sample) -- replaces lbt_avgpool_fwd, lbt_dfxp_quantize (pooled, Dense_q X),
+ * lbt_conv_fwd_generic (Dense_q y = Xq Wq), lbt_softmax_xent, lbt_dfxp_quantize (Dense_q grad),
+ * lbt_conv_dgrad_generic and lbt_avgpool_bwd with the same arithmetic bit for bit:
  *   AvgPool_q   dynamic_fixed_point.py:1009-1022, Dense_q :319-395 (fwd) / :441-466 (bwd),
  *   loss        models.py:30-32 (mean sparse softmax cross-entropy).
- * x [N][HW][C] fp32 (last block output) -> logits, loss[0], dz; dw = dequant(sum_n pq^T gq) + wd2*w
- * (exactly lbt_conv_wgrad_reduce's formula); gx [N][HW][C] = d loss / d x. wq is the Dense_q
- * weight codes [C][K] (lbt_dfxp_quantize_weights' w_hwio of a C x 1 x 1 x K job). qx / qg are
- * the stochastic X / grad quantisers (noise tables of C / K values, or Philox inline).
- * pooled, pq, gq are optional outputs (NULL = not stored). scratch: lbt_head_scratch_bytes(N, C, K)
- * bytes, any content. *ticket must be 0 on entry; the kernel leaves it 0.
- * Limits: C <= 256, C % 4 == 0, 1 <= K <= 64, HW >= 1.                                        */
+ * x [N][HW][C] fp32 (last block output) -> logits, dz, gx [N][HW][C] = d loss / d x, and per
+ * sample a record (pq, gq, loss term) in scratch (lbt_head_scratch_bytes(N, C, K) bytes) from
+ * which lbt_step_reduce later forms the two batch reductions: the Dense_q weight gradient
+ * dw = dequant(sum_n pq^T gq) + wd2*w (lbt_conv_wgrad_reduce's formula) and loss[0].
+ * wq is the Dense_q weight codes [C][K] (lbt_dfxp_quantize_weights' w_hwio of a C x 1 x 1 x K job,
+ * 4-byte aligned). qx / qg are the stochastic X / grad quantisers (noise tables of C / K values,
+ * or Philox inline). pooled, pq, gq are optional outputs (NULL = not stored).
+ * Limits: C <= 256, C % 8 == 0, 1 <= K <= 64, HW >= 1, x 16-byte aligned.                   */
 typedef struct lbt_head {
   const float* x; int32_t N, HW, C, K;
   float* pooled; int8_t* pq; lbt_qdesc qx;
@@ -318,10 +318,11 @@ typedef struct lbt_head {
   int8_t* gq; lbt_qdesc qg;
   const float* w; float wd2; float* dw;
   float* gx;
-  void* scratch; uint32_t* ticket;
+  void* scratch;
 } lbt_head;
 int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K);  /* = N * (C + 72) */
 int lbt_head_fwd_bwd(const lbt_head* h, void* stream);
+
 /* MomentumOptimizer.apply_gradients (trainer.py:81-82): a = mu*a + g*gscale; w -= lr*a. */
 int lbt_sgd_momentum(float* w, float* a, const float* g, int64_t n, float lr, float mu,
                      float gscale, void* stream);
@@ -361,6 +362,19 @@ typedef struct lbt_pjob {
   const int64_t* sums; int32_t C; lbt_qdesc qrg, qr; const float* gamma; float wd2; float* dgamma; float* dbeta;
 } lbt_pjob;
 int lbt_bn_param_grads_many(const lbt_pjob* jobs, int32_t njobs, int32_t max_c, void* stream);
+
+/* The end of a step's backward in ONE launch: lbt_conv_wgrad_reduce_many's jobs (r_blocks =
+ * sum of ceil(K*Cout/256)), lbt_bn_param_grads_many's jobs (Cout <= max_c) and, if head is not
+ * NULL, the head's batch reductions (Dense_q dw and loss[0], from lbt_head_fwd_bwd's records:
+ * the loss summed in softmax_xent's order). Job arrays in device memory, *head in host memory.  */
+int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
+                    int32_t max_c, const lbt_head* head, void* stream);
+
+/* lbt_sgd_momentum and lbt_dfxp_range_update in ONE launch (independent: the optimiser reads no
+ * exponent; the range update reads only the step's counters).                              */
+int lbt_step_update(float* w, float* a, const float* g, int64_t n, float lr, float mu, float gscale,
+                    int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
+                    const float* nelem, int32_t nslots, uint64_t* step, void* stream);
 
 /* Diagnostics: counts (atomically into *bad) the i < n where the BN kernels' division by a
  * reused divisor (div_by(x, recip(y)), dfxp_device.h) differs in any bit from x / y; if qa

@@ -5,6 +5,7 @@
 // Each of these is a few KB of work whose cost as its own kernel is the ~2-4 us launch/latency floor; ~90
 // such launches per ResNet-20 step become 4. Job descriptors are read from device memory (grid.y = job).
 #include "dfxp_device.h"
+#include "head.h"
 
 using namespace lbt;
 
@@ -61,31 +62,31 @@ __global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob*
 
 // Blocks are allotted to the jobs in order, ceil(K*Cout/256) each (1-D grid); a block reduces 256
 // consecutive outputs over the slab's shards, with the offset correction 128 * sum_p g[co]
-// (x_u8off) summed once per column into LDS.
-__global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs, int njobs) {
-  __shared__ int s_job;
-  __shared__ int64_t s_base;
-  __shared__ int64_t nbs[256];
-  __shared__ long long colsum[256];
+// (x_u8off) summed once per column into LDS. lds: >= 4 KB.
+LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, uint8_t* lds) {
+  int64_t* nbs = reinterpret_cast<int64_t*>(lds);                   // [256]
+  long long* colsum = reinterpret_cast<long long*>(lds + 2048);      // [256]
+  int* s_job = reinterpret_cast<int*>(lds + 4096);
+  int64_t* s_base = reinterpret_cast<int64_t*>(lds + 4104);
   // every job's block count loaded in parallel (a serial scan of device memory would cost one
   // memory round trip per job), then scanned in LDS
   for (int j = threadIdx.x; j < njobs; j += 256) nbs[j] = ((int64_t)jobs[j].K * jobs[j].Cout + 255) / 256;
   __syncthreads();
   if (threadIdx.x == 0) {
-    int64_t b = blockIdx.x;
+    int64_t b = blk;
     int jj = njobs;  // past the end: nothing to do
     for (int j = 0; j < njobs; ++j) {
       if (b < nbs[j]) { jj = j; break; }
       b -= nbs[j];
     }
-    s_job = jj;
-    s_base = b * 256;
+    *s_job = jj;
+    *s_base = b * 256;
   }
   __syncthreads();
-  if (s_job >= njobs) return;
-  const lbt_rjob j = jobs[s_job];
+  if (*s_job >= njobs) return;
+  const lbt_rjob j = jobs[*s_job];
   const int64_t total = (int64_t)j.K * j.Cout;
-  const int64_t i = s_base + threadIdx.x;
+  const int64_t i = *s_base + threadIdx.x;
   const bool corr = j.x_u8off && j.gcolsum;
   if (corr) {
     for (int c = threadIdx.x; c < j.Cout; c += 256) {
@@ -109,9 +110,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* 
   j.dw[i] = a + b;
 }
 
-__global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
-  const lbt_pjob j = jobs[blockIdx.y];
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs, int njobs) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4112];
+  rjob_block(jobs, njobs, blockIdx.x, lds);
+}
+
+LBT_DEV void pjob_channel(const lbt_pjob& j, int c) {
   if (c >= j.C) return;
   long long vr[LBT_NSHARD], vg[LBT_NSHARD];  // all shard loads in flight at once
 #pragma unroll
@@ -130,6 +134,28 @@ __global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
   const float b = j.wd2 * j.gamma[c];
   j.dgamma[c] = a + b;
   j.dbeta[c] = (float)((double)sg * g2);
+}
+
+__global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
+  pjob_channel(jobs[blockIdx.y], blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// lbt_step_reduce: [r_blocks wgrad-reduce blocks][np * pblk param-grad blocks][1 head block]
+__global__ __launch_bounds__(256) void step_reduce_kernel(const lbt_rjob* __restrict__ rjobs, int nr, int r_blocks,
+                                                          const lbt_pjob* __restrict__ pjobs, int np, int pblk,
+                                                          lbt_head head) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLds];
+  const int b = blockIdx.x;
+  if (b < r_blocks) {
+    rjob_block(rjobs, nr, b, lds);
+    return;
+  }
+  const int b2 = b - r_blocks;
+  if (b2 < np * pblk) {
+    pjob_channel(pjobs[b2 / pblk], (b2 % pblk) * 256 + threadIdx.x);
+    return;
+  }
+  head_reduce(head, lds);
 }
 
 // grid (blocks, njobs): thread -> noise block b (4 values, one Philox call)
@@ -184,6 +210,24 @@ extern "C" int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, i
   if (njobs <= 0) return LBT_OK;
   if (total_blocks <= 0 || njobs > 256) return LBT_EINVAL;
   hipLaunchKernelGGL(wgrad_reduce_many_kernel, dim3(total_blocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
+                               int32_t max_c, const lbt_head* head, void* stream) {
+  if (nr < 0 || np < 0 || nr > 256 || r_blocks < 0 || (nr > 0 && r_blocks == 0) || (np > 0 && max_c <= 0))
+    return LBT_EINVAL;
+  lbt_head h = {};
+  if (head) {
+    h = *head;
+    if (h.N <= 0 || h.C <= 0 || h.C > 256 || h.C % 8 || h.K <= 0 || h.K > 64 || !h.scratch || !h.w || !h.dw || !h.loss)
+      return LBT_EINVAL;
+  }
+  const int pblk = np > 0 ? (max_c + 255) / 256 : 0;
+  const int64_t blocks = (int64_t)r_blocks + (int64_t)np * pblk + (head ? 1 : 0);
+  if (blocks <= 0) return LBT_OK;
+  hipLaunchKernelGGL(step_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rjobs, nr, r_blocks,
+                     pjobs, np, pblk, h);
   return (int)hipGetLastError();
 }
 

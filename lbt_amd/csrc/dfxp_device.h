@@ -284,6 +284,16 @@ LBT_DEV int wave_chan_reduce(int v, int period) {
 // true if this lane should publish its (reduced) per-channel partials
 LBT_DEV bool chan_owner(int period) { return period == 0 || (int)(threadIdx.x & 63) < period; }
 
+// MomentumOptimizer.apply_gradients (trainer.py:81-82) on element i: a = mu*a + g*gscale; w -= lr*a.
+LBT_DEV void sgd_momentum_elem(float* w, float* a, const float* g, int64_t i, float lr, float mu, float gscale) {
+  const float t = mu * a[i];
+  const float gg = g[i] * gscale;
+  const float an = t + gg;
+  a[i] = an;
+  const float step = lr * an;
+  w[i] = w[i] - step;
+}
+
 // Store one code in the requested encoding.
 LBT_DEV void store_code(void* out, int kind, int64_t i, int qv, float inv_m) {
   switch (kind) {

@@ -104,12 +104,7 @@ __global__ void sgd_momentum_kernel(float* __restrict__ w, float* __restrict__ a
                                     int64_t n, float lr, float mu, float gscale) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float t = mu * a[i];
-  const float gg = g[i] * gscale;
-  const float an = t + gg;
-  a[i] = an;
-  const float step = lr * an;
-  w[i] = w[i] - step;
+  sgd_momentum_elem(w, a, g, i, lr, mu, gscale);
 }
 
 __global__ void bias_add_kernel(float* __restrict__ y, const float* __restrict__ b, int64_t n, int C) {

@@ -149,6 +149,26 @@ __global__ void range_update_kernel(int32_t* exps, int32_t* counts, const int32_
   if (blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1ull;
 }
 
+// lbt_step_update: [sgd_blocks optimiser blocks][range-update blocks (4 slots each)]
+__global__ __launch_bounds__(256) void step_update_kernel(float* __restrict__ w, float* __restrict__ a,
+                                                          const float* __restrict__ g, int64_t n, float lr, float mu,
+                                                          float gscale, int sgd_blocks, int32_t* exps, int32_t* counts,
+                                                          const int32_t* bits, const float* target, const float* nelem,
+                                                          int nslots, uint64_t* step) {
+  if ((int)blockIdx.x < sgd_blocks) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) sgd_momentum_elem(w, a, g, i, lr, mu, gscale);
+    return;
+  }
+  const int rb = (int)blockIdx.x - sgd_blocks;
+  const int i = rb * 4 + (threadIdx.x >> 6);
+  if (i < nslots && nelem[i] > 0.f) {
+    int c1, c2;
+    if (wave_shard_totals(counts, i, c1, c2)) range_apply(i, c1, c2, exps, bits, target, nelem);
+  }
+  if (rb == 0 && threadIdx.x == 0) step[0] += 1ull;
+}
+
 __global__ void counts_fold_kernel(int32_t* counts, int nslots, float* folded) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= nslots) return;
@@ -251,6 +271,18 @@ extern "C" int lbt_dfxp_range_update(int32_t* exps, int32_t* counts, const int32
   return (int)hipGetLastError();
 }
 
+extern "C" int lbt_step_update(float* w, float* a, const float* g, int64_t n, float lr, float mu, float gscale,
+                               int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
+                               const float* nelem, int32_t nslots, uint64_t* step, void* stream) {
+  if (n < 0 || nslots < 0) return LBT_EINVAL;
+  const int64_t sgd_blocks = (n + 255) / 256;
+  const int rblocks = nslots > 0 ? (nslots + 3) / 4 : 1;
+  if (sgd_blocks + rblocks >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  hipLaunchKernelGGL(step_update_kernel, dim3((unsigned)(sgd_blocks + rblocks)), dim3(256), 0, (hipStream_t)stream, w, a,
+                     g, n, lr, mu, gscale, (int)sgd_blocks, exps, counts, bits, target, nelem, nslots, step);
+  return (int)hipGetLastError();
+}
+
 extern "C" int lbt_dfxp_counts_fold(int32_t* counts, int32_t nslots, float* folded, void* stream) {
   if (nslots <= 0) return LBT_OK;
   hipLaunchKernelGGL(counts_fold_kernel, dim3((nslots + 3) / 4), dim3(256), 0, (hipStream_t)stream, counts, nslots,
@@ -278,4 +310,4 @@ extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, 
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_abi_version(void) { return 5; }
+extern "C" int lbt_abi_version(void) { return 6; }

@@ -114,7 +114,7 @@ class FusedResNet:
         return self.loss
 
     def backward(self):
-        for f in self._hbwd + self._bwd:
+        for f in self._hbwd + self._bwd + self._tail_sep:
             f()
 
     def train_fwd_bwd(self, X, labels):
@@ -125,7 +125,7 @@ class FusedResNet:
             self._X.copy_(X)
         if labels.data_ptr() != self._labels.data_ptr():
             self._labels.copy_(labels)
-        for f in self._fwd + self._hfused + self._bwd:
+        for f in self._fwd + self._hfused + self._bwd + self._tail_fused:
             f()
         return self.loss
 
@@ -319,15 +319,14 @@ class FusedResNet:
         gY = self._buf("gYlast", Ylast.shape, torch.float32)
         hbwd.append(L("lbt_avgpool_bwd", ptr(dpool), ptr(gY), Nb, Hh * Wh, Ch))
         scratch = self._buf("head_scratch", (lib.lbt_head_scratch_bytes(Nb, Ch, d.units),), torch.uint8)
-        ticket = self._sums("head_ticket", 1)  # zeroed with the step's sums (and left zero by the kernel)
         hd = _lib.Head(Ylast.data_ptr(), Nb, Hh * Wh, Ch, d.units, pooled.data_ptr(), pq.data_ptr(), self._qd(d.X_range),
                        d.w_hwio.data_ptr(), d.W_range.desc, self._labels.data_ptr(), self.logits.data_ptr(),
                        self.loss.data_ptr(), self.dlogits.data_ptr(), gqd.data_ptr(), self._qd(d.grad_range),
                        d.W.data_ptr(), ops.f32(2 * d.weight_decay), d.dW.data_ptr(), gY.data_ptr(),
-                       scratch.data_ptr(), ticket.data_ptr())
+                       scratch.data_ptr())
         self._head = hd
         hfused = [L("lbt_head_fwd_bwd", ctypes.byref(hd), k="head_kernel",
-                    nb=4 * Ylast.numel() * 2 + 4 * d.W.numel() * 3)]
+                    nb=4 * Ylast.numel() * 2 + d.w_hwio.numel())]
         self._hfwd, self._hloss, self._hbwd, self._hfused = hfwd, hloss, hbwd, hfused
         # Pass-A descriptors of every block-end BN chain and of the stem's, built first: each runs
         # as the epilogue of the dgrad that produces its input gradient (lbt_conv_dgrad_chain_i8),
@@ -366,15 +365,21 @@ class FusedResNet:
         pjobs.append(PJob(sums0.data_ptr(), C0, self._qd(r0.grad_range), self._qd(r0.X_range), r0.gamma.data_ptr(),
                           ops.f32(2 * r0.weight_decay), r0.dgamma.data_ptr(), r0.dbeta.data_ptr()))
 
-        # ---- batched reductions (after the side-stream weight gradients have landed)
+        # ---- batched reductions (after the side-stream weight gradients have landed): every
+        # split wgrad, every dgamma / dbeta and -- in the training step -- the head's Dense_q dW
+        # and loss, one launch (lbt_step_reduce)
         if self.overlap_wgrad:
             bwd.append(self._join_side())
         self._rjobs = _dev_array(rjobs, ctx.device)
         total_blocks = sum((j.K * j.Cout + 255) // 256 for j in rjobs)
-        bwd.append(L("lbt_conv_wgrad_reduce_many", ptr(self._rjobs), len(rjobs), total_blocks, k="wgrad_reduce_many_kernel",
-                     nb=sum(4 * j.nsplit * j.K * j.Cout + 8 * j.K * j.Cout for j in rjobs)))
         self._pjobs = _dev_array(pjobs, ctx.device)
-        bwd.append(L("lbt_bn_param_grads_many", ptr(self._pjobs), len(pjobs), max(j.C for j in pjobs)))
+        max_c = max(j.C for j in pjobs)
+        nb_red = sum(4 * j.nsplit * j.K * j.Cout + 8 * j.K * j.Cout for j in rjobs)
+        self._tail_sep = [L("lbt_step_reduce", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs), len(pjobs),
+                            max_c, None, k="step_reduce_kernel", nb=nb_red)]
+        self._tail_fused = [L("lbt_step_reduce", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs), len(pjobs),
+                              max_c, ctypes.byref(hd), k="step_reduce_kernel",
+                              nb=nb_red + scratch.numel() + 8 * d.W.numel())]
         # ---- this step's noise tables: one launch ahead of everything else
         self._njobs = _dev_array(njobs, ctx.device)
         max_n = max(j.n for j in njobs)

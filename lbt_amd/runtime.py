@@ -121,10 +121,18 @@ class DfxpContext:
             self.sums_arena[: self._sums_used].zero_()
 
     # the 'update_range' collection (trainer.py:63,157)
-    def update_range_op(self):
+    def update_range_op(self, sgd=None):
+        """The 'update_range' collection: one launch. sgd = (w, a, g, lr, mu, gscale) also runs the
+        momentum optimiser in the same launch (lbt_step_update)."""
         n = len(self.quantizers)
-        _lib.call("lbt_dfxp_range_update", _lib.ptr(self.exps), _lib.ptr(self.counts), _lib.ptr(self.bits),
-                  _lib.ptr(self.target), _lib.ptr(self.nelem), n, _lib.ptr(self.step), _lib.stream())
+        if sgd is None:
+            _lib.call("lbt_dfxp_range_update", _lib.ptr(self.exps), _lib.ptr(self.counts), _lib.ptr(self.bits),
+                      _lib.ptr(self.target), _lib.ptr(self.nelem), n, _lib.ptr(self.step), _lib.stream())
+        else:
+            w, a, g, lr, mu, gscale = sgd
+            _lib.call("lbt_step_update", _lib.ptr(w), _lib.ptr(a), _lib.ptr(g), w.numel(), float(lr), float(mu),
+                      float(gscale), _lib.ptr(self.exps), _lib.ptr(self.counts), _lib.ptr(self.bits),
+                      _lib.ptr(self.target), _lib.ptr(self.nelem), n, _lib.ptr(self.step), _lib.stream())
 
     def update_range_folded_op(self, folded):
         """Data-parallel variant: the range update from all-reduced folded totals (see fold_counts)."""

@@ -106,11 +106,11 @@ class Trainer:
         D.allreduce_comm(self.comm, self.pg)
 
     def _update(self):
-        ops.sgd_momentum(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0 / self.world)
         if self.comm is not None:
+            ops.sgd_momentum(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0 / self.world)
             self.ctx.update_range_folded_op(self.comm[self.flat.n:])
-        else:
-            self.ctx.update_range_op()
+        else:  # optimiser + range update in one launch
+            self.ctx.update_range_op(sgd=(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0))
 
     def _eager(self, X, y):
         self._fwd_bwd(X, y)

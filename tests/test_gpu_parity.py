@@ -462,11 +462,12 @@ def test_fused_executor_bitidentical_to_layerwise():
     assert ctxA.ranges() == ctxB.ranges()
 
 
-@pytest.mark.parametrize("N,HW,C,K,table", [(128, 64, 64, 10, True), (300, 16, 32, 7, False), (5, 3, 256, 64, True)])
+@pytest.mark.parametrize("N,HW,C,K,table", [(128, 64, 64, 10, True), (300, 16, 32, 7, False), (5, 3, 256, 64, True), (700, 4, 8, 3, True)])
 def test_head_kernel_equals_launch_sequence(N, HW, C, K, table):
-    """lbt_head_fwd_bwd == avgpool_fwd, quantize, dense fwd, softmax_xent, quantize, dense wgrad +
-    reduce, dense dgrad, avgpool_bwd as separate launches: every output and counter bit for bit
-    (with noise tables and with inline Philox; N > 256 exercises the loss-term striding)."""
+    """lbt_head_fwd_bwd + lbt_step_reduce's head block == avgpool_fwd, quantize, dense fwd,
+    softmax_xent, quantize, dense wgrad + reduce, dense dgrad, avgpool_bwd as separate launches:
+    every output and counter bit for bit (with noise tables and with inline Philox; N > 256
+    exercises the loss-term striding)."""
     import ctypes
     from lbt_amd import _lib
     rng = np.random.default_rng(N + C)
@@ -517,15 +518,12 @@ def test_head_kernel_equals_launch_sequence(N, HW, C, K, table):
         else:
             lib = _lib.load()
             scratch = torch.empty(lib.lbt_head_scratch_bytes(N, C, K), dtype=torch.uint8, device=DEV)
-            ticket = torch.zeros(2, dtype=torch.int32, device=DEV)
             h = _lib.Head(x.data_ptr(), N, HW, C, K, pooled.data_ptr(), pq.data_ptr(), dx, wq.data_ptr(), qw.desc,
                           labels.data_ptr(), logits.data_ptr(), loss.data_ptr(), dz.data_ptr(), gq.data_ptr(), dg,
-                          W.data_ptr(), wd2, dW.data_ptr(), gx.data_ptr(), scratch.data_ptr(), ticket.data_ptr())
-            for _ in range(2):  # twice: the ticket must come back to zero
-                ctx.counts.zero_()
-                _lib.call("lbt_head_fwd_bwd", ctypes.byref(h), st)
-            torch.cuda.synchronize()
-            assert int(ticket[0].item()) == 0
+                          W.data_ptr(), wd2, dW.data_ptr(), gx.data_ptr(), scratch.data_ptr())
+            _lib.call("lbt_head_fwd_bwd", ctypes.byref(h), st)
+            # the batch reductions (Dense_q dW, loss) run in the step's final reduce launch
+            _lib.call("lbt_step_reduce", None, 0, 0, None, 0, 0, ctypes.byref(h), st)
         torch.cuda.synchronize()
         out[mode] = dict(pooled=pooled, pq=pq, logits=logits, loss=loss, dz=dz, gq=gq, dW=dW, gx=gx,
                          counts=ctx.counts_view()[:3].sum(1))
