@@ -376,6 +376,23 @@ int lbt_step_update(float* w, float* a, const float* g, int64_t n, float lr, flo
                     int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
                     const float* nelem, int32_t nslots, uint64_t* step, void* stream);
 
+/* ---------------------------------------------------------------- either side of the path ---
+ * GradientBuffer_q.backward (dynamic_fixed_point.py:473-509): total = pad(g, n_buf) + buffer;
+ * gq = Q(total) (dequantised fp32; noise index i % inner, inner = prod(buffer.shape[1:]));
+ * buffer = total - gq; gq[0 : n_g] out. q.bits == 32: the reference's bypass (gq = total).    */
+int lbt_grad_buffer_bwd(const float* g, int64_t n_g, float* buffer, int64_t n_buf, int64_t inner, lbt_qdesc q,
+                        float* gq, void* stream);
+/* Dense_q._pre_dense_func (:397-439, dormant in the reference): grad [rows][cols] updated in place
+ * against the per-element state accu / init_flag / rem_flag [state_rows][state_cols] (initially
+ * 0.001 / 1 / 0, :364-366,449), eps = 2^-(bits - I_grad) (:444). rows <= state_rows.          */
+int lbt_pre_dense(float* grad, int32_t rows, int32_t cols, int32_t state_rows, int32_t state_cols, lbt_qdesc qg,
+                  float* accu, int32_t* init_flag, int32_t* rem_flag, void* stream);
+/* preprocess_image (trainer.py:24-28): per sample a random left-right flip and a random crop of
+ * the zero-padded (pad on each side) image back to H x W; the draws are Philox4x32-10 of
+ * (sample, "AUG!", counter; seed): flip = r0 & 1, oy = r1 % (2pad+1), ox = r2 % (2pad+1).    */
+int lbt_augment_flip_crop(const float* x, float* y, int32_t N, int32_t H, int32_t W, int32_t C, int32_t pad,
+                          uint64_t seed, uint64_t counter, void* stream);
+
 /* Diagnostics: counts (atomically into *bad) the i < n where the BN kernels' division by a
  * reused divisor (div_by(x, recip(y)), dfxp_device.h) differs in any bit from x / y; if qa
  * is not NULL also writes x / y to qa and div_by to qb.                                      */

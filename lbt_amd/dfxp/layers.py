@@ -259,6 +259,7 @@ class Dense_q(Layer_q):
         return y
 
     def backward(self, grad, stochastic=True):
+        self.grad = grad  # kept for pre_dense_func (the reference's self.grad, :442)
         d = self.d
         dev = grad.device
         gsum = self._c.sums("gsum", ops.NSHARD * 2 * self.units, self.ctx)
@@ -275,6 +276,19 @@ class Dense_q(Layer_q):
         ops.conv_dgrad_generic(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
         return dx
 
+    def pre_dense_func(self, grad=None):
+        """``Dense_q.pre_dense_func`` (:397-439; dormant in the reference's trainer, which never
+        fetches ``pre_dense_op``): the per-element small-gradient accumulator applied in place to
+        ``grad`` (default: the last backward's incoming gradient), eps = 2^-(bits - grad_range).
+        State (:364-366, :449): accu = 0.001, init_flag = 1, rem_flag = 0, [in_units, units]."""
+        grad = self.grad if grad is None else grad
+        if not hasattr(self, "_pd_accu"):
+            dev = self.ctx.device
+            self._pd_accu = torch.full((self.in_units, self.units), 0.001, dtype=torch.float32, device=dev)
+            self._pd_init = torch.ones((self.in_units, self.units), dtype=torch.int32, device=dev)
+            self._pd_rem = torch.zeros((self.in_units, self.units), dtype=torch.int32, device=dev)
+        return ops.pre_dense(grad, self.grad_range.desc, self._pd_accu, self._pd_init, self._pd_rem)
+
     def grads_and_vars(self):
         if self.use_bias:
             return [(self.dW, self.W), (self.db, self.b)]
@@ -282,6 +296,36 @@ class Dense_q(Layer_q):
 
     def info(self):
         return "%d bits dense: %dx%d weight_decay %f" % (self.bits, self.in_units, self.units, self.weight_decay)
+
+
+class GradientBuffer_q(Layer_q):
+    """Gradient buffer (``:472-509``): identity forward; backward quantises the incoming gradient
+    plus the buffered residue (zero-padded to ``shape``) and keeps the new residue
+    (error feedback): ``total = pad(grad) + buffer; gq = Q(total); buffer = total - gq``."""
+
+    def __init__(self, name, bits, shape, target_overflow_rate=0, grad_range=2, ctx=None):
+        self.ctx = ctx = ctx or default_context()
+        self.name, self.bits, self.shape = name, bits, tuple(int(s) for s in shape)
+        self.target_overflow_rate = target_overflow_rate
+        self.buffer = torch.zeros(self.shape, dtype=torch.float32, device=ctx.device)
+        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, target_overflow_rate) \
+            if bits != 32 else None
+
+    def backward(self, grad, stochastic=True):
+        if tuple(grad.shape[1:]) != self.shape[1:] or grad.shape[0] > self.shape[0]:
+            raise ValueError("gradient %s does not fit the buffer %s" % (tuple(grad.shape), self.shape))
+        inner = int(np.prod(self.shape[1:])) if len(self.shape) > 1 else 1
+        if self.grad_range is not None:
+            self.grad_range.observe(self.buffer.numel())
+            desc = self.grad_range.desc
+        else:
+            desc = _lib.QDesc()
+            desc.bits = 32
+        self.gradq = ops.grad_buffer_bwd(grad.contiguous(), self.buffer, desc, inner)
+        return self.gradq
+
+    def info(self):
+        return "Gradient buffer"
 
 
 class Sequential_q(Layer_q):

@@ -336,3 +336,33 @@ def bias_grad(chsum, C, qg, db):
 
 def f32(x):
     return torch.tensor(x, dtype=torch.float32).item()
+
+
+# ---------------------------------------------------------------- either side of the hot path
+def grad_buffer_bwd(g, buffer, q_desc, inner):
+    """GradientBuffer_q.backward (lbt_grad_buffer_bwd): returns gq [g.shape]; buffer updated."""
+    _check(g, torch.float32, "g")
+    _check(buffer, torch.float32, "buffer")
+    gq = torch.empty_like(g)
+    call("lbt_grad_buffer_bwd", ptr(g), g.numel(), ptr(buffer), buffer.numel(), int(inner), q_desc, ptr(gq), stream())
+    return gq
+
+
+def pre_dense(grad, qg_desc, accu, init_flag, rem_flag):
+    """Dense_q._pre_dense_func (lbt_pre_dense), in place on grad [rows, cols]."""
+    _check(grad, torch.float32, "grad")
+    rows, cols = grad.shape
+    call("lbt_pre_dense", ptr(grad), rows, cols, accu.shape[0], accu.shape[1], qg_desc, ptr(accu), ptr(init_flag),
+         ptr(rem_flag), stream())
+    return grad
+
+
+def augment_flip_crop(x, pad, seed, counter, out=None):
+    """preprocess_image (trainer.py:24-28) on device: random flip + zero pad + random crop."""
+    _check(x, torch.float32, "x")
+    N, H, W, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    call("lbt_augment_flip_crop", ptr(x), ptr(out), N, H, W, C, int(pad), int(seed) & 0xFFFFFFFFFFFFFFFF,
+         int(counter) & 0xFFFFFFFFFFFFFFFF, stream())
+    return out

@@ -74,6 +74,8 @@ class Trainer:
         self.global_step = 0
         self._graphs = None
         self._static = None
+        self._eval = {}
+        self._aug = None
         if logger is not None:
             logger.info("Model info:\n" + model.info())
 
@@ -167,10 +169,14 @@ class Trainer:
         self.global_step += 1
         return self.model.loss
 
-    def train(self):
-        """Epoch loop of trainer.py:117-162 over an in-memory dataset ((Xtr, ytr), (Xte, yte))."""
-        (Xtr, ytr), _ = self.dataset
+    def train(self, augment=True):
+        """Epoch loop of trainer.py:117-192 over an in-memory dataset ((Xtr, ytr), (Xte, yte)):
+        shuffled batches, preprocess_image on device (random flip + pad-4 random crop,
+        lbt_augment_flip_crop), the lr schedule of :122-140, and the test loop after every epoch.
+        Returns the per-epoch test accuracies."""
+        (Xtr, ytr), (Xte, yte) = self.dataset
         dev = self.ctx.device
+        history = []
         for epoch in range(self.n_epoch):
             if epoch == 0:
                 self.get_train_op()
@@ -182,6 +188,112 @@ class Trainer:
                 idx = perm[b:b + self.batch_size]
                 X = torch.as_tensor(Xtr[idx.numpy()], dtype=torch.float32).to(dev).contiguous()
                 y = torch.as_tensor(ytr[idx.numpy()], dtype=torch.int32).to(dev)
+                if augment:
+                    if self._aug is None or self._aug.shape != X.shape:
+                        self._aug = torch.empty_like(X)
+                    X = ops.augment_flip_crop(X, 4, self.ctx.seed, self.global_step, out=self._aug)
                 loss = self.step(X, y)
                 if self.logger is not None and (b // self.batch_size + 1) % 100 == 0:
                     self.logger.info("Batch %d loss %f" % (b // self.batch_size + 1, loss.item()))
+            if Xte is not None and len(Xte):
+                acc, _ = self.evaluate(Xte, yte)
+                history.append(acc)
+                if self.logger is not None:
+                    self.logger.info("Epoch %d test accuracy %f" % (epoch + 1, acc))
+        return history
+
+    # -- test loop and checkpoint (trainer.py:164-197) ----------------------------------------
+    def _eval_model(self, n):
+        """The model the test loop runs for a batch of n: a FusedResNet gets a plan of its own per
+        test-batch size (its own buffers, so the captured training graph stays valid); a
+        layer-wise model is shared (its per-layer buffers are re-sized by the test batch, so the
+        training graph is re-captured afterwards)."""
+        from .fused import FusedResNet
+        m = self.model
+        if isinstance(m, FusedResNet):
+            if n not in self._eval:
+                self._eval[n] = FusedResNet(m.model)
+            return self._eval[n], False
+        return m, True
+
+    def evaluate(self, X, y, batch_size=1000):
+        """The reference's test loop (trainer.py:166-190): per batch of 1000 the forward pass in
+        training mode (batch-statistic BN, stochastic quantisers -- the reference never runs
+        set_testing, :164-165), loss and accuracy; returns (mean accuracy, mean loss) over the
+        batches. The overflow counters these forwards accumulate are discarded (the loop does not
+        fetch update_range_op); BN running statistics are updated, as the reference's are."""
+        dev = self.ctx.device
+        saved = self.ctx.counts.clone()
+        acc_sum, loss_sum, nb, shared = 0.0, 0.0, 0, False
+        for b in range(0, len(X), batch_size):
+            Xb = torch.as_tensor(X[b:b + batch_size], dtype=torch.float32).to(dev).contiguous()
+            yb = torch.as_tensor(y[b:b + batch_size], dtype=torch.int32).to(dev)
+            m, shared = self._eval_model(len(Xb))
+            logits = m.forward(Xb)
+            loss = m.compute_loss(yb)
+            acc = (logits.argmax(dim=1).to(torch.int32) == yb).float().mean()
+            acc_sum += float(acc.item())
+            loss_sum += float(loss.item())
+            nb += 1
+        self.ctx.counts.copy_(saved)
+        if shared:
+            self._graphs = None
+        return acc_sum / max(nb, 1), loss_sum / max(nb, 1)
+
+    def _bn_layers(self):
+        out = []
+
+        def walk(layers):
+            for layer in layers:
+                if hasattr(layer, "X_mean_running"):
+                    out.append(layer)
+                for attr in ("layers", "residual", "shortcut"):
+                    sub = getattr(layer, attr, None)
+                    if sub is None:
+                        continue
+                    walk(sub.layers if hasattr(sub, "layers") and not isinstance(sub, (list, tuple)) else sub)
+        root = getattr(self.model, "model", self.model)
+        walk(root.layers)
+        return out
+
+    def save_model(self, exp_path):
+        """Checkpoint (trainer.py:194-197, tf.train.Saver): parameters, momentum accumulators, DFXP
+        exponents + noise step, BN running statistics and the trainer's step / lr, as one
+        safetensors file exp_path/model.safetensors (no pickled objects)."""
+        import json
+        import os
+
+        from safetensors.torch import save_file
+        os.makedirs(exp_path, exist_ok=True)
+        t = {"w": self.flat.w, "a": self.flat.a, "exps": self.ctx.exps, "step": self.ctx.step}
+        for i, bn in enumerate(self._bn_layers()):
+            t["bn%d/mean" % i] = bn.X_mean_running
+            t["bn%d/var" % i] = bn.X_var_running
+        meta = {"global_step": str(self.global_step), "lr": repr(self.lr), "momentum": repr(self.momentum),
+                "quantizers": json.dumps([q.name for q in self.ctx.quantizers]),
+                "params": json.dumps([[o.name if hasattr(o, "name") else "", v, off, sz]
+                                      for o, v, off, sz in self.flat.offsets])}
+        path = os.path.join(exp_path, "model.safetensors")
+        save_file({k: v.detach().contiguous().cpu() for k, v in t.items()}, path, metadata=meta)
+        return path
+
+    def load_model(self, path):
+        """Restore a save_model checkpoint into this trainer (same model layout)."""
+        import json
+
+        from safetensors import safe_open
+        with safe_open(path, framework="pt") as f:
+            meta = f.metadata()
+            if json.loads(meta["quantizers"]) != [q.name for q in self.ctx.quantizers]:
+                raise ValueError("checkpoint quantiser layout differs from this model's")
+            self.flat.w.copy_(f.get_tensor("w"))
+            self.flat.a.copy_(f.get_tensor("a"))
+            self.ctx.exps.copy_(f.get_tensor("exps"))
+            self.ctx.step.copy_(f.get_tensor("step"))
+            for i, bn in enumerate(self._bn_layers()):
+                bn.X_mean_running.copy_(f.get_tensor("bn%d/mean" % i))
+                bn.X_var_running.copy_(f.get_tensor("bn%d/var" % i))
+        self.global_step = int(meta["global_step"])
+        self.lr = float(meta["lr"])
+        self.momentum = float(meta["momentum"])
+        self._graphs = None  # lr is baked into the captured optimiser
