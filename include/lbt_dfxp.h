@@ -171,6 +171,16 @@ int lbt_conv_dgrad_generic(const int8_t* gq, const int8_t* w_hwio, lbt_conv_desc
                            lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
 int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
                            int32_t* slab, int32_t nsplit, void* stream);
+/* 9..16-bit gradient codes ("16-bit grad DFP"): the same
+ * generic dgrad / wgrad with int16 codes and int64 accumulation (int16 x int8 sums overflow
+ * int32), an int64 wgrad slab [nsplit][K][Cout], and its reduce (same dequant + 2*wd*W formula
+ * as lbt_conv_wgrad_reduce, x_u8off = 0).                                                    */
+int lbt_conv_dgrad_generic16(const int16_t* gq, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
+                             float* dx, const float* add_src, void* stream);
+int lbt_conv_wgrad_generic16(const void* xq, int32_t x_i16, const int16_t* gq, lbt_conv_desc d, int64_t* slab,
+                             int32_t nsplit, void* stream);
+int lbt_conv_wgrad_reduce64(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, lbt_qdesc qx, lbt_qdesc qg,
+                            const float* w, float wd2, float* dw, void* stream);
 
 /* Stem convolution (conv1 of the CIFAR ResNets, models.py:387-391): input = the image's SIGNED
  * (bits+1)-bit codes as int16 (|x| <= 2048), patch K = KH*KW*Cin <= 32, Cout % 16 == 0.
@@ -278,6 +288,18 @@ typedef struct lbt_chain_bwd_b {
 } lbt_chain_bwd_b;
 int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream);
 
+/* BN backward passes A and B for 9..16-bit gradient quantisers (config 4): the arithmetic of
+ * lbt_bn_chain_bwd_a / _b (one branch, no mask) with int16 grad codes and int64 channel sums.
+ * Rows here are pixels: g / R / qn / gout / dout / dx are [rows][C]; inner = the per-sample
+ * element count (noise period). A: qrg.bits == 0 skips the rescale part, qng.bits == 0 writes
+ * dout instead of norm codes; sums [NSHARD][4C] as lbt_chain_bwd_a's. B: dx from gout, qn, the
+ * forward's ms and pass A's sums (n = elements per channel).                                */
+int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R, const float* gamma_q, lbt_qdesc qng,
+                      const int8_t* qn, int16_t* gout, float* dout, int64_t* sums, int64_t rows, int64_t inner,
+                      int32_t C, void* stream);
+int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qdesc qn_q, const float* ms,
+                      const int64_t* sums, int64_t n, float* dx, int64_t rows, int32_t C, void* stream);
+
 /* Rescale_q parameter gradients (:689-690) from pass-A sums:
  * dgamma = (float)((double)sum(G2*R) * sg2*sr) + wd2*gamma,  dbeta = (float)((double)sum G2 * sg2). */
 int lbt_bn_param_grads(const int64_t* sums, int32_t C, lbt_qdesc qrg, lbt_qdesc qr,
@@ -293,6 +315,12 @@ int lbt_add(const float* a, const float* b, float* y, int64_t n, void* stream);
 /* AvgPool_q over the whole HxW map (:1017): y[n,c] = (sequential fp32 sum) * (1/(H*W)). */
 int lbt_avgpool_fwd(const float* x, float* y, int32_t N, int32_t HW, int32_t C, void* stream);
 int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW, int32_t C, void* stream);
+/* MaxPool_q (:993-1006, tf.nn.max_pool; TF SAME pads with -inf): y = window max (first maximum in
+ * (kh, kw) order wins), amax = its window position (one byte per output); backward (TF MaxPoolGrad)
+ * routes each output gradient to its argmax input, summed per input in ascending output order.
+ * d: N, H, W, Cin (= channels), KH, KW, SH, SW, PT, PL, Ho, Wo; Cout, PB, PR unused.           */
+int lbt_maxpool_fwd(const float* x, float* y, uint8_t* amax, lbt_conv_desc d, void* stream);
+int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, lbt_conv_desc d, void* stream);
 /* mean sparse softmax cross-entropy (models.py:30-32) -> loss[0] (fp32, device), dz = d loss / d z. */
 int lbt_softmax_xent(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss,
                      float* dz, void* stream);

@@ -131,15 +131,22 @@ _SIGS = {
     "lbt_conv_fwd_generic": [_P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_conv_dgrad_generic": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_generic": [_P, c_int32, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_dgrad_generic16": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, _P],
+    "lbt_conv_wgrad_generic16": [_P, c_int32, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_wgrad_reduce64": [_P, c_int32, c_int32, c_int32, QDesc, QDesc, _P, c_float, _P, _P],
     "lbt_conv_stem_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
     "lbt_conv_stem_wgrad": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_bn_chain_fwd": [_P, _P],
     "lbt_bn_chain_bwd_a": [_P, _P],
     "lbt_bn_chain_bwd_b": [_P, _P],
+    "lbt_bn_bwd_a_wide": [_P, QDesc, _P, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64, c_int32, _P],
+    "lbt_bn_bwd_b_wide": [_P, QDesc, _P, QDesc, _P, _P, c_int64, _P, c_int64, c_int32, _P],
     "lbt_bn_param_grads": [_P, c_int32, QDesc, QDesc, _P, c_float, _P, _P, _P],
     "lbt_relu_fwd": [_P, _P, c_int64, _P],
     "lbt_relu_bwd": [_P, _P, _P, c_int64, _P],
     "lbt_add": [_P, _P, _P, c_int64, _P],
+    "lbt_maxpool_fwd": [_P, _P, _P, ConvDesc, _P],
+    "lbt_maxpool_bwd": [_P, _P, _P, ConvDesc, _P],
     "lbt_avgpool_fwd": [_P, _P, c_int32, c_int32, c_int32, _P],
     "lbt_avgpool_bwd": [_P, _P, c_int32, c_int32, c_int32, _P],
     "lbt_softmax_xent": [_P, _P, c_int32, c_int32, _P, _P, _P],

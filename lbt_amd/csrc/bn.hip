@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
   constexpr int ST = (F & kRt) ? -1 : ((F & kAStoch) ? 1 : 0);
   LBT_TS(0);
   const int C = a.C;
-  long long* S = reinterpret_cast<long long*>(shf + 4 * C);  // [2][4C]
+  long long* S = reinterpret_cast<long long*>(shf + 4 * C);  // [NB][4C]
   const int64_t groups = a.inner >> 2;
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const bool live = g < groups;
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
     if (Bb.gb)
       for (int c = threadIdx.x; c < C; c += kThreads) { shf[b * 2 * C + c] = Bb.gb[c]; shf[b * 2 * C + C + c] = Bb.gb[C + c]; }
   }
-  for (int i = threadIdx.x; i < 8 * C; i += kThreads) S[i] = 0;
+  for (int i = threadIdx.x; i < NB * 4 * C; i += kThreads) S[i] = 0;
   __syncthreads();
   LBT_TS(1);
   float gam[2][4], bet[4];
@@ -621,6 +621,19 @@ bool shape_ok(int64_t rows, int64_t inner, int C) {
   return rows > 0 && inner > 0 && C > 0 && C % 4 == 0 && inner % C == 0 && inner % 4 == 0;
 }
 
+// Dynamic LDS above the default 64 KiB (BN layers with C > ~680; gfx950 gives one workgroup up to
+// 160 KiB): raise the kernel's limit before launching it.
+template <typename K>
+void allow_shm(K kernel, size_t shm) {
+  if (shm > 65536) hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)shm);
+}
+#define LBT_LAUNCH(KERNEL, GRID, SHM, ST, ...)                                  \
+  do {                                                                          \
+    allow_shm(KERNEL, SHM);                                                     \
+    hipLaunchKernelGGL(KERNEL, GRID, dim3(kThreads), SHM, ST, __VA_ARGS__);     \
+  } while (0)
+
 }  // namespace
 
 LBT_TRACE_SETTER(bn)
@@ -642,7 +655,7 @@ extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   const int f = fwd_flags(*a);
 #define LBT_CF(NB, FL)                                                                            \
   if (a->has_b2 == (NB == 2) && f == (FL)) {                                                      \
-    hipLaunchKernelGGL((chain_fwd_kernel<NB, FL>), grid, dim3(kThreads), shm, st, *a, rpt);       \
+    LBT_LAUNCH((chain_fwd_kernel<NB, FL>), grid, shm, st, *a, rpt);       \
     return (int)hipGetLastError();                                                                \
   }
   LBT_CF(1, kFwdBlk | kFY | kFO1 | kFU8)                  // stem: bn0 -> relu -> X0 + block-0 input
@@ -654,9 +667,9 @@ extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   LBT_CF(2, kFwdBlk | kFY | kFO1 | kFO2 | kFU8)
 #undef LBT_CF
   if (a->has_b2)
-    hipLaunchKernelGGL((chain_fwd_kernel<2, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
+    LBT_LAUNCH((chain_fwd_kernel<2, kRt>), grid, shm, st, *a, rpt);
   else
-    hipLaunchKernelGGL((chain_fwd_kernel<1, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
+    LBT_LAUNCH((chain_fwd_kernel<1, kRt>), grid, shm, st, *a, rpt);
   return (int)hipGetLastError();
 }
 
@@ -665,12 +678,12 @@ extern "C" int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream) {
   dim3 grid;
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
-  const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 8 * a->C;
+  const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * (a->has_b2 ? 8 : 4) * a->C;
   hipStream_t st = (hipStream_t)stream;
   const int f = bwd_a_flags(*a);
 #define LBT_CA(NB, FL)                                                                            \
   if (a->has_b2 == (NB == 2) && f == (FL)) {                                                      \
-    hipLaunchKernelGGL((chain_bwd_a_kernel<NB, FL>), grid, dim3(kThreads), shm, st, *a, rpt);     \
+    LBT_LAUNCH((chain_bwd_a_kernel<NB, FL>), grid, shm, st, *a, rpt);     \
     return (int)hipGetLastError();                                                                \
   }
   LBT_CA(1, kAFB | kAStoch | kAYMask | kAGmask)  // block end, identity shortcut
@@ -679,9 +692,9 @@ extern "C" int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream) {
   LBT_CA(2, kAFB | kAStoch | kAYMask)            // block end, projection shortcut
 #undef LBT_CA
   if (a->has_b2)
-    hipLaunchKernelGGL((chain_bwd_a_kernel<2, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
+    LBT_LAUNCH((chain_bwd_a_kernel<2, kRt>), grid, shm, st, *a, rpt);
   else
-    hipLaunchKernelGGL((chain_bwd_a_kernel<1, kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
+    LBT_LAUNCH((chain_bwd_a_kernel<1, kRt>), grid, shm, st, *a, rpt);
   return (int)hipGetLastError();
 }
 
@@ -694,11 +707,11 @@ extern "C" int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int f = bwd_b_flags(*a);
   if (f == (kBQ | kBStoch | kBGcol))
-    hipLaunchKernelGGL((chain_bwd_b_kernel<kBQ | kBStoch | kBGcol>), grid, dim3(kThreads), shm, st, *a, rpt);
+    LBT_LAUNCH((chain_bwd_b_kernel<kBQ | kBStoch | kBGcol>), grid, shm, st, *a, rpt);
   else if (f == (kBQ | kBStoch))
-    hipLaunchKernelGGL((chain_bwd_b_kernel<kBQ | kBStoch>), grid, dim3(kThreads), shm, st, *a, rpt);
+    LBT_LAUNCH((chain_bwd_b_kernel<kBQ | kBStoch>), grid, shm, st, *a, rpt);
   else
-    hipLaunchKernelGGL((chain_bwd_b_kernel<kRt>), grid, dim3(kThreads), shm, st, *a, rpt);
+    LBT_LAUNCH((chain_bwd_b_kernel<kRt>), grid, shm, st, *a, rpt);
   return (int)hipGetLastError();
 }
 

@@ -42,7 +42,10 @@ __global__ __launch_bounds__(256) void conv_fwd_generic_kernel(const TX* __restr
   y[i] = (float)acc * scale;
 }
 
-__global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const int8_t* __restrict__ g,
+// TG = int16_t with TACC = int64: 9..16-bit gradient codes (config 4), whose products with 8-bit
+// weights overflow an int32 sum.
+template <typename TG, typename TACC>
+__global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const TG* __restrict__ g,
                                                                 const int8_t* __restrict__ w, lbt_conv_desc d,
                                                                 lbt_qdesc qg, lbt_qdesc qw, float* __restrict__ dx,
                                                                 const float* __restrict__ add_src) {
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const int8_t* _
   m /= (uint32_t)d.W;
   const int ih = (int)(m % (uint32_t)d.H);
   const int n = (int)(m / (uint32_t)d.H);
-  int acc = 0;
+  TACC acc = 0;
   for (int kh = 0; kh < d.KH; ++kh) {
     const int ny = ih + d.PT - kh;
     if (ny < 0 || ny % d.SH) continue;
@@ -68,9 +71,9 @@ __global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const int8_t* _
       if (nx < 0 || nx % d.SW) continue;
       const int ow = nx / d.SW;
       if (ow >= d.Wo) continue;
-      const int8_t* gp = g + (((int64_t)n * d.Ho + oh) * d.Wo + ow) * d.Cout;
+      const TG* gp = g + (((int64_t)n * d.Ho + oh) * d.Wo + ow) * d.Cout;
       const int8_t* wp = w + ((int64_t)(kh * d.KW + kw) * d.Cin + ci) * d.Cout;
-      for (int co = 0; co < d.Cout; ++co) acc += (int)gp[co] * (int)wp[co];
+      for (int co = 0; co < d.Cout; ++co) acc += (TACC)((int)gp[co] * (int)wp[co]);
     }
   }
   const float v = (float)acc * scale;
@@ -80,13 +83,13 @@ __global__ __launch_bounds__(256) void conv_dgrad_generic_kernel(const int8_t* _
 // grid = (nsplit, output tiles of kMaxOut*256); block (b, t) reduces pixels [b*per, (b+1)*per)
 // for outputs [t*kTile, (t+1)*kTile) in chunks of kChunk pixels staged in LDS (the im2col
 // patch columns k in [klo, khi) that tile needs, and the G rows), each thread owning <= 16 outputs.
-constexpr int kChunk = 32;
+constexpr int kMaxChunk = 32;  // pixels per LDS pass (fewer when Cout is large: the G rows must fit)
 constexpr int kMaxOut = 16;
 constexpr int kTile = kMaxOut * 256;
-template <typename TX>
-__global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __restrict__ x, const int8_t* __restrict__ g,
-                                                                lbt_conv_desc d, int32_t* __restrict__ slab,
-                                                                int64_t P, int nsplit) {
+template <typename TX, typename TG, typename TACC>
+__global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __restrict__ x, const TG* __restrict__ g,
+                                                                lbt_conv_desc d, TACC* __restrict__ slab,
+                                                                int64_t P, int nsplit, int kChunk) {
   extern __shared__ int16_t sh[];
   const int K = d.KH * d.KW * d.Cin;
   const int nout = K * d.Cout;
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __res
   const int64_t per = (P + nsplit - 1) / nsplit;
   const int64_t p0 = (int64_t)blockIdx.x * per;
   const int64_t p1 = p0 + per < P ? p0 + per : P;
-  int acc[kMaxOut];
+  TACC acc[kMaxOut];
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) acc[j] = 0;
   const int64_t HWo = (int64_t)d.Ho * d.Wo;
@@ -131,14 +134,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_generic_kernel(const TX* __res
       const int o = o0 + threadIdx.x + j * blockDim.x;
       if (o < o1) {
         const int k = o / d.Cout, co = o - k * d.Cout;
-        int a = acc[j];
-        for (int pl = 0; pl < kChunk; ++pl) a += (int)Xs[pl * KS + (k - klo)] * (int)Gs[pl * d.Cout + co];
+        TACC a = acc[j];
+        for (int pl = 0; pl < kChunk; ++pl) a += (TACC)((int)Xs[pl * KS + (k - klo)] * (int)Gs[pl * d.Cout + co]);
         acc[j] = a;
       }
     }
     __syncthreads();
   }
-  int32_t* dst = slab + (int64_t)blockIdx.x * nout;
+  TACC* dst = slab + (int64_t)blockIdx.x * nout;
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) {
     const int o = o0 + threadIdx.x + j * blockDim.x;
@@ -175,30 +178,98 @@ extern "C" int lbt_conv_dgrad_generic(const int8_t* gq, const int8_t* w_hwio, lb
   const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
   if (total >= ((int64_t)1 << 31)) return LBT_EINVAL;
   const unsigned blocks = (unsigned)((total + 255) / 256);
-  hipLaunchKernelGGL(conv_dgrad_generic_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, gq, w_hwio, d, qg,
-                     qw, dx, add_src);
+  hipLaunchKernelGGL((conv_dgrad_generic_kernel<int8_t, int>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, gq,
+                     w_hwio, d, qg, qw, dx, add_src);
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
-                                      int32_t* slab, int32_t nsplit, void* stream) {
-  if (!desc_ok(d) || nsplit <= 0) return LBT_EINVAL;
+extern "C" int lbt_conv_dgrad_generic16(const int16_t* gq, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qg,
+                                        lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
+  if (!desc_ok(d)) return LBT_EINVAL;
+  const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
+  if (total >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL((conv_dgrad_generic_kernel<int16_t, long long>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     gq, w_hwio, d, qg, qw, dx, add_src);
+  return (int)hipGetLastError();
+}
+
+namespace {
+
+// shared geometry of the generic wgrad launches; false = shape not supported
+bool wgrad_geom(const lbt_conv_desc& d, int nsplit, dim3& grid, int& chunk, size_t& shm, int64_t& P) {
+  if (!desc_ok(d) || nsplit <= 0) return false;
   const int64_t K = (int64_t)d.KH * d.KW * d.Cin;
   const int64_t nout = K * d.Cout;
   const int64_t tiles = (nout + kTile - 1) / kTile;
-  if (tiles > 65535) return LBT_EINVAL;
-  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
-  if (P >= ((int64_t)1 << 31) || (P + nsplit - 1) / nsplit > 8192) return LBT_EINVAL;  // int32 partial bound for 9-bit x 8-bit
+  if (tiles > 65535) return false;
+  P = (int64_t)d.N * d.Ho * d.Wo;
+  if (P >= ((int64_t)1 << 31)) return false;
   const int64_t ks_max = (kTile + d.Cout - 1) / d.Cout + 1 < K ? (kTile + d.Cout - 1) / d.Cout + 1 : K;
-  const size_t shm = sizeof(int16_t) * kChunk * (ks_max + d.Cout);
-  if (shm > 64 * 1024) return LBT_EINVAL;
-  dim3 grid(nsplit, (unsigned)tiles);
+  chunk = (int)((64 * 1024) / (sizeof(int16_t) * (ks_max + d.Cout)));
+  if (chunk > kMaxChunk) chunk = kMaxChunk;
+  if (chunk < 1) return false;
+  shm = sizeof(int16_t) * chunk * (ks_max + d.Cout);
+  grid = dim3(nsplit, (unsigned)tiles);
+  return true;
+}
+
+template <typename TACC>
+__global__ __launch_bounds__(256) void wgrad_reduce_generic_kernel(const TACC* __restrict__ slab, int nsplit, int64_t total,
+                                                                  lbt_qdesc qx, lbt_qdesc qg, const float* __restrict__ w,
+                                                                  float wd2, float* __restrict__ dw) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  long long s = 0;
+  for (int b = 0; b < nsplit; ++b) s += (long long)slab[(int64_t)b * total + i];
+  const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qg)));
+  const float a = (float)s * scale;
+  const float b = wd2 * w[i];
+  dw[i] = a + b;
+}
+
+}  // namespace
+
+extern "C" int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
+                                      int32_t* slab, int32_t nsplit, void* stream) {
+  dim3 grid;
+  int chunk;
+  size_t shm;
+  int64_t P;
+  if (!wgrad_geom(d, nsplit, grid, chunk, shm, P)) return LBT_EINVAL;
+  if ((P + nsplit - 1) / nsplit > 8192) return LBT_EINVAL;  // int32 partial bound for 9-bit x 8-bit
   hipStream_t st = (hipStream_t)stream;
   if (x_i16)
-    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int16_t>, grid, dim3(256), shm, st, (const int16_t*)xq, gq, d,
-                       slab, P, nsplit);
+    hipLaunchKernelGGL((conv_wgrad_generic_kernel<int16_t, int8_t, int32_t>), grid, dim3(256), shm, st,
+                       (const int16_t*)xq, gq, d, slab, P, nsplit, chunk);
   else
-    hipLaunchKernelGGL(conv_wgrad_generic_kernel<int8_t>, grid, dim3(256), shm, st, (const int8_t*)xq, gq, d,
-                       slab, P, nsplit);
+    hipLaunchKernelGGL((conv_wgrad_generic_kernel<int8_t, int8_t, int32_t>), grid, dim3(256), shm, st,
+                       (const int8_t*)xq, gq, d, slab, P, nsplit, chunk);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_conv_wgrad_generic16(const void* xq, int32_t x_i16, const int16_t* gq, lbt_conv_desc d,
+                                        int64_t* slab, int32_t nsplit, void* stream) {
+  dim3 grid;
+  int chunk;
+  size_t shm;
+  int64_t P;
+  if (!wgrad_geom(d, nsplit, grid, chunk, shm, P)) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (x_i16)
+    hipLaunchKernelGGL((conv_wgrad_generic_kernel<int16_t, int16_t, long long>), grid, dim3(256), shm, st,
+                       (const int16_t*)xq, gq, d, (long long*)slab, P, nsplit, chunk);
+  else
+    hipLaunchKernelGGL((conv_wgrad_generic_kernel<int8_t, int16_t, long long>), grid, dim3(256), shm, st,
+                       (const int8_t*)xq, gq, d, (long long*)slab, P, nsplit, chunk);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_conv_wgrad_reduce64(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, lbt_qdesc qx,
+                                       lbt_qdesc qg, const float* w, float wd2, float* dw, void* stream) {
+  if (nsplit <= 0 || K <= 0 || Cout <= 0) return LBT_EINVAL;
+  const int64_t total = (int64_t)K * Cout;
+  hipLaunchKernelGGL((wgrad_reduce_generic_kernel<long long>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw);
   return (int)hipGetLastError();
 }

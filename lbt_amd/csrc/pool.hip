@@ -1,0 +1,94 @@
+// pool.hip -- MaxPool_q (dynamic_fixed_point.py:993-1006, tf.nn.max_pool) forward and backward.
+//
+// Forward: thread per output, the window scanned in (kh, kw) order with a strict '>' so the FIRST
+// maximum wins; padding positions (TF SAME pads with -inf) are skipped. The winning window
+// position is kept as one byte per output for the backward.
+// Backward (TF MaxPoolGrad): each output's gradient goes to its argmax input; thread per INPUT
+// element sums the gradients of the windows that chose it in ascending output order (oh, ow) --
+// the order TF's CPU kernel accumulates them in -- starting from 0.
+#include "dfxp_device.h"
+
+namespace {
+
+constexpr int kT = 256;
+
+__global__ __launch_bounds__(kT) void maxpool_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                         uint8_t* __restrict__ amax, lbt_conv_desc d) {
+  const int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x;
+  const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
+  if (e >= total) return;
+  const int c = (int)(e % d.Cin);
+  int64_t m = e / d.Cin;
+  const int ow = (int)(m % d.Wo);
+  m /= d.Wo;
+  const int oh = (int)(m % d.Ho);
+  const int n = (int)(m / d.Ho);
+  float best = -INFINITY;
+  int bi = 0;
+  for (int kh = 0; kh < d.KH; ++kh) {
+    const int ih = oh * d.SH + kh - d.PT;
+    if ((unsigned)ih >= (unsigned)d.H) continue;
+    for (int kw = 0; kw < d.KW; ++kw) {
+      const int iw = ow * d.SW + kw - d.PL;
+      if ((unsigned)iw >= (unsigned)d.W) continue;
+      const float v = x[(((int64_t)n * d.H + ih) * d.W + iw) * d.Cin + c];
+      if (v > best) {
+        best = v;
+        bi = kh * d.KW + kw;
+      }
+    }
+  }
+  y[e] = best;
+  amax[e] = (uint8_t)bi;
+}
+
+__global__ __launch_bounds__(kT) void maxpool_bwd_kernel(const float* __restrict__ g, const uint8_t* __restrict__ amax,
+                                                         float* __restrict__ dx, lbt_conv_desc d) {
+  const int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x;
+  const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
+  if (e >= total) return;
+  const int c = (int)(e % d.Cin);
+  int64_t m = e / d.Cin;
+  const int iw = (int)(m % d.W);
+  m /= d.W;
+  const int ih = (int)(m % d.H);
+  const int n = (int)(m / d.H);
+  // outputs whose window covers ih: oh*SH - PT <= ih <= oh*SH - PT + KH - 1
+  const int ylo = ih + d.PT - d.KH + 1, yhi = ih + d.PT;
+  const int xlo = iw + d.PL - d.KW + 1, xhi = iw + d.PL;
+  int oh0 = ylo <= 0 ? 0 : (ylo + d.SH - 1) / d.SH, oh1 = yhi < 0 ? -1 : yhi / d.SH;
+  int ow0 = xlo <= 0 ? 0 : (xlo + d.SW - 1) / d.SW, ow1 = xhi < 0 ? -1 : xhi / d.SW;
+  if (oh1 >= d.Ho) oh1 = d.Ho - 1;
+  if (ow1 >= d.Wo) ow1 = d.Wo - 1;
+  float s = 0.f;
+  for (int oh = oh0; oh <= oh1; ++oh)
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int64_t o = (((int64_t)n * d.Ho + oh) * d.Wo + ow) * d.Cin + c;
+      const int pos = (ih - (oh * d.SH - d.PT)) * d.KW + (iw - (ow * d.SW - d.PL));
+      if ((int)amax[o] == pos) s = s + g[o];
+    }
+  dx[e] = s;
+}
+
+}  // namespace
+
+// d: N, H, W, Cin (= C), KH, KW, SH, SW, PT, PL, Ho, Wo (Cout, PB, PR unused)
+extern "C" int lbt_maxpool_fwd(const float* x, float* y, uint8_t* amax, lbt_conv_desc d, void* stream) {
+  if (d.N <= 0 || d.H <= 0 || d.W <= 0 || d.Cin <= 0 || d.KH <= 0 || d.KW <= 0 || d.KH * d.KW > 256 || d.SH <= 0 ||
+      d.SW <= 0 || d.Ho <= 0 || d.Wo <= 0)
+    return LBT_EINVAL;
+  const int64_t n = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, x, y,
+                     amax, d);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, lbt_conv_desc d, void* stream) {
+  if (d.N <= 0 || d.H <= 0 || d.W <= 0 || d.Cin <= 0 || d.KH <= 0 || d.KW <= 0 || d.SH <= 0 || d.SW <= 0 ||
+      d.Ho <= 0 || d.Wo <= 0)
+    return LBT_EINVAL;
+  const int64_t n = (int64_t)d.N * d.H * d.W * d.Cin;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, g,
+                     amax, dx, d);
+  return (int)hipGetLastError();
+}

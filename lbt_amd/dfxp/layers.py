@@ -86,9 +86,10 @@ class Conv2d_q(Layer_q):
 
     def __init__(self, name, bits, ksize, strides, padding, use_bias=True, weight_decay=0,
                  target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2,
-                 input_nonnegative=False, ctx=None):
+                 input_nonnegative=False, grad_bits=None, ctx=None):
         self.ctx = ctx = ctx or default_context()
         h, w, Cin, Cout = self.ksize = list(ksize)
+        self.grad_bits = grad_bits = grad_bits or bits  # config 4: 16-bit gradients (the reference: one `bits`)
         self.strides = list(strides)
         self.padding = padding
         self.name, self.use_bias, self.bits = name, use_bias, bits
@@ -101,17 +102,20 @@ class Conv2d_q(Layer_q):
         t = target_overflow_rate
         self.W_range = ctx.quantizer(name + "/W_range", bits, weight_range, t)
         self.X_range = ctx.quantizer(name + "/X_range", bits + 1, input_range, t)
-        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, t)
+        self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, t)
         if use_bias:
             self.b = torch.zeros(Cout, dtype=torch.float32, device=ctx.device)
             self.db = torch.zeros_like(self.b)
             self.b_range = ctx.quantizer(name + "/b_range", bits, bias_range, t)
-        self.mfma = ops.mfma_ok(Cin, Cout) and bits <= 8
+        # int8 MFMA kernels: 8-bit codes on both GEMM sides (16-bit gradients: generic int64 kernels)
+        self.mfma = ops.mfma_ok(Cin, Cout) and bits <= 8 and grad_bits <= 8
+        if grad_bits > 8 and use_bias:
+            raise NotImplementedError("bias with > 8-bit gradient codes")
         # x codes: unsigned 9-bit (offset int8, MFMA) / signed <= 8 bit (int8, MFMA) / int16 (VALU)
         if bits + 1 <= 8:
             self.x_kind = OUT_I8
-        elif bits + 1 == 9 and input_nonnegative:
-            self.x_kind = OUT_U8OFF
+        elif bits + 1 == 9 and input_nonnegative and self.mfma:
+            self.x_kind = OUT_U8OFF  # offset codes are undone by the MFMA kernels only
         else:
             self.x_kind = OUT_I16
         self.x_mfma = self.mfma and self.x_kind != OUT_I16
@@ -164,7 +168,26 @@ class Conv2d_q(Layer_q):
         self.y = y
         return y
 
+    def _backward_wide(self, grad):
+        """9..16-bit gradient codes (config 4): int16 codes, int64 generic GEMMs."""
+        d = self.d
+        dev = grad.device
+        K = d.KH * d.KW * d.Cin
+        self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16, dev))
+        ns = ops.wgrad_nsplit(d, generic=True)
+        slab = self._c.get("slab64", (ns, K, d.Cout), torch.int64, dev)
+        ops.conv_wgrad_generic16(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
+        ops.conv_wgrad_reduce64(slab, ns, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
+                                ops.f32(2 * self.weight_decay), self.dW)
+        if not self.need_input_grad:
+            return None
+        dx = self._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, dev)
+        ops.conv_dgrad_generic16(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
+        return dx
+
     def backward(self, grad, stochastic=True):
+        if self.grad_bits > 8:
+            return self._backward_wide(grad)
         d = self.d
         Cout, Cin = d.Cout, d.Cin
         dev = grad.device
@@ -214,9 +237,11 @@ class Dense_q(Layer_q):
     """Quantised fully-connected layer (``:319-470``): X, W, b and grad all at bits."""
 
     def __init__(self, name, bits, in_units, units, use_bias=True, weight_decay=0,
-                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, ctx=None):
+                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, grad_bits=None,
+                 ctx=None):
         self.ctx = ctx = ctx or default_context()
         self.name, self.bits, self.in_units, self.units = name, bits, in_units, units
+        self.grad_bits = grad_bits = grad_bits or bits
         self.use_bias, self.weight_decay, self.target_overflow_rate = use_bias, weight_decay, target_overflow_rate
         limit = (6 / (in_units + units)) ** 0.5
         self.W = _as_param(_rng(ctx, name + "/W").uniform(-limit, limit, size=(in_units, units)).astype(np.float32),
@@ -225,7 +250,7 @@ class Dense_q(Layer_q):
         t = target_overflow_rate
         self.W_range = ctx.quantizer(name + "/W_range", bits, weight_range, t)
         self.X_range = ctx.quantizer(name + "/X_range", bits, input_range, t)
-        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, t)
+        self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, t)
         if use_bias:
             self.b = torch.zeros(units, dtype=torch.float32, device=ctx.device)
             self.db = torch.zeros_like(self.b)
@@ -262,6 +287,19 @@ class Dense_q(Layer_q):
         self.grad = grad  # kept for pre_dense_func (the reference's self.grad, :442)
         d = self.d
         dev = grad.device
+        if self.grad_bits > 8:
+            if self.use_bias:
+                raise NotImplementedError("bias with > 8-bit gradient codes")
+            self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16,
+                                                                                       dev))
+            ns = ops.wgrad_nsplit(d, generic=True)
+            slab = self._c.get("slab64", (ns, self.in_units, self.units), torch.int64, dev)
+            ops.conv_wgrad_generic16(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
+            ops.conv_wgrad_reduce64(slab, ns, self.in_units, self.units, self.X_range.desc, self.grad_range.desc,
+                                    self.W, ops.f32(2 * self.weight_decay), self.dW)
+            dx = self._c.get("dx", (d.N, self.in_units), torch.float32, dev)
+            ops.conv_dgrad_generic16(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
+            return dx
         gsum = self._c.sums("gsum", ops.NSHARD * 2 * self.units, self.ctx)
         self.gradq = ops.quantize(grad, self.grad_range, OUT_I8, out=self._c.get("gq", grad.shape, torch.int8, dev),
                                   chsum=gsum, C=self.units)
@@ -361,12 +399,13 @@ class Normalization_q(Layer_q):
     """BN normalisation half (``:539-623``): quantise X, biased batch moments, normalise."""
 
     def __init__(self, name, bits, num_features, training=True, momentum=0.999, eps=1e-5, target_overflow_rate=0,
-                 input_range=2, grad_range=2, ctx=None):
+                 input_range=2, grad_range=2, grad_bits=None, ctx=None):
         self.ctx = ctx = ctx or default_context()
         self.name, self.bits, self.C, self.train = name, bits, num_features, training
+        self.grad_bits = grad_bits = grad_bits or bits
         self.momentum, self.eps, self.target_overflow_rate = momentum, eps, target_overflow_rate
         self.X_range = ctx.quantizer(name + "/X_range", bits, input_range, target_overflow_rate)
-        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, target_overflow_rate)
+        self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, target_overflow_rate)
         self.X_mean_running = torch.zeros(num_features, dtype=torch.float32, device=ctx.device)
         self.X_var_running = torch.ones(num_features, dtype=torch.float32, device=ctx.device)
         self.ms = torch.zeros(2 * num_features, dtype=torch.float32, device=ctx.device)
@@ -403,6 +442,14 @@ class Normalization_q(Layer_q):
         C = self.C
         rows, inner = ops.rows_inner(tuple(grad.shape))
         sums = self._c.sums("sums", ops.NSHARD * 4 * C, self.ctx)
+        if self.grad_bits > 8:  # 16-bit gradient codes (config 4)
+            self.grad_range.observe(grad.numel())
+            G16 = self._c.get("G16", grad.shape, torch.int16, dev)
+            dx = self._c.get("dx", grad.shape, torch.float32, dev)
+            pix = grad.numel() // C
+            ops.bn_bwd_a_wide(grad, NO_Q, None, None, self.grad_range.desc, self.q, G16, None, sums, pix, inner, C)
+            ops.bn_bwd_b_wide(G16, self.grad_range.desc, self.q, self.X_range.desc, self.ms, sums, self.n, dx, pix, C)
+            return dx
         G = self._c.get("G", grad.shape, torch.int8, dev)
         self.grad_range.observe(grad.numel())
         a = ChainBwdA()
@@ -425,7 +472,7 @@ class Rescale_q(Layer_q):
     """BN rescale half (``:626-694``): y = Q(X) * Q(gamma) + Q(beta)."""
 
     def __init__(self, name, bits, num_features, weight_decay=0, target_overflow_rate=0, input_range=2,
-                 gamma_range=2, beta_range=2, grad_range=2, ctx=None):
+                 gamma_range=2, beta_range=2, grad_range=2, grad_bits=None, ctx=None):
         self.ctx = ctx = ctx or default_context()
         self.name, self.bits, self.C, self.weight_decay = name, bits, num_features, weight_decay
         self.target_overflow_rate = target_overflow_rate
@@ -438,7 +485,8 @@ class Rescale_q(Layer_q):
         self.g_range = ctx.quantizer(name + "/g_range", bits, gamma_range, t)
         self.b_range = ctx.quantizer(name + "/b_range", bits, beta_range, t)
         self.X_range = ctx.quantizer(name + "/X_range", bits, input_range, t)
-        self.grad_range = ctx.quantizer(name + "/grad_range", bits, grad_range, t)
+        self.grad_bits = grad_bits = grad_bits or bits
+        self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, t)
         self.gb = torch.zeros(2 * num_features, dtype=torch.float32, device=dev)
         self._c = _Cache()
 
@@ -477,6 +525,12 @@ class Rescale_q(Layer_q):
         sums = self._c.sums("sums", ops.NSHARD * 4 * C, self.ctx)
         dx = self._c.get("dx", grad.shape, torch.float32, dev)
         self.grad_range.observe(grad.numel())
+        if self.grad_bits > 8:  # 16-bit gradient codes (config 4)
+            ops.bn_bwd_a_wide(grad, self.grad_range.desc, self.R, self.gb[:C], NO_Q, None, None, dx, sums,
+                              grad.numel() // C, inner, C)
+            ops.bn_param_grads(sums, C, self.grad_range.desc, self.X_range.desc, self.gamma,
+                               ops.f32(2 * self.weight_decay), self.dgamma, self.dbeta)
+            return dx
         a = ChainBwdA()
         a.g = grad.data_ptr()
         a.b1 = BwdBranch(self.grad_range.desc, self.R.data_ptr(), self.X_range.desc, self.gb.data_ptr(), NO_Q,
@@ -498,14 +552,15 @@ class BatchNorm_q(Sequential_q):
     """``Sequential_q(Normalization_q(name-norm), Rescale_q(name-rescale))`` (``:697-743``)."""
 
     def __init__(self, name, bits, num_features, training=True, momentum=0.999, eps=1e-5, weight_decay=0,
-                 target_overflow_rate=0, input_range=2, gamma_range=2, beta_range=2, grad_range=2, ctx=None):
+                 target_overflow_rate=0, input_range=2, gamma_range=2, beta_range=2, grad_range=2, grad_bits=None,
+                 ctx=None):
         super().__init__(
             Normalization_q(name=name + "-norm", bits=bits, num_features=num_features, training=training,
                             momentum=momentum, eps=eps, target_overflow_rate=target_overflow_rate,
-                            input_range=input_range, grad_range=grad_range, ctx=ctx),
+                            input_range=input_range, grad_range=grad_range, grad_bits=grad_bits, ctx=ctx),
             Rescale_q(name=name + "-rescale", bits=bits, num_features=num_features, weight_decay=weight_decay,
                       target_overflow_rate=target_overflow_rate, input_range=2, gamma_range=gamma_range,
-                      beta_range=beta_range, grad_range=grad_range, ctx=ctx))
+                      beta_range=beta_range, grad_range=grad_range, grad_bits=grad_bits, ctx=ctx))
 
     def info(self):
         return "BatchNorm"
@@ -589,6 +644,73 @@ class ResidualBlock_q(Layer_q):
 
     def info(self):
         return "Residual block with " + self.residual.info()
+
+
+class ResidualBottleneck_q(ResidualBlock_q):
+    """Bottleneck residual block (``:878-980``): 1x1 -> BN -> ReLU -> 3x3 (stride) -> BN -> ReLU ->
+    1x1 (4x channels) -> BN, plus the shortcut of ``_build_shortcut`` (``:825-856``), ReLU."""
+    expansion = 4
+
+    def __init__(self, name, bits, in_channels, channels, stride, training=True, batch_norm=True, weight_decay=0,
+                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, grad_bits=None,
+                 ctx=None):
+        self.train = training
+        self.name = name
+        out = self.expansion * channels
+        common = dict(bits=bits, use_bias=not batch_norm, weight_decay=weight_decay, input_range=input_range,
+                      weight_range=weight_range, bias_range=bias_range, grad_range=grad_range,
+                      input_nonnegative=True, grad_bits=grad_bits, ctx=ctx)
+        bn = dict(bits=bits, training=training, weight_decay=weight_decay, target_overflow_rate=target_overflow_rate,
+                  input_range=input_range, grad_range=grad_range, grad_bits=grad_bits, ctx=ctx)
+        self.residual = Sequential_q(
+            Conv2d_q(name=name + "-1", ksize=[1, 1, in_channels, channels], strides=[1, 1, 1, 1], padding="SAME",
+                     **common),
+            BatchNorm_q(name=name + "-bn1", num_features=channels, **bn) if batch_norm else Layer_q(),
+            ReLU_q(),
+            Conv2d_q(name=name + "-2", ksize=[3, 3, channels, channels], strides=[1, stride, stride, 1],
+                     padding="SAME", **common),
+            BatchNorm_q(name=name + "-bn2", num_features=channels, **bn) if batch_norm else Layer_q(),
+            ReLU_q(),
+            Conv2d_q(name=name + "-3", ksize=[1, 1, channels, out], strides=[1, 1, 1, 1], padding="SAME", **common),
+            BatchNorm_q(name=name + "-bn3", num_features=out, **bn) if batch_norm else Layer_q(),
+        )
+        if stride == 1 and in_channels == out:
+            self.shortcut = Sequential_q()
+        else:
+            self.shortcut = Sequential_q(
+                Conv2d_q(name=name + "-shortcut", ksize=[1, 1, in_channels, out], strides=[1, stride, stride, 1],
+                         padding="SAME", target_overflow_rate=target_overflow_rate, **common),
+                BatchNorm_q(name=name + "-shortcut-bn", num_features=out, **bn) if batch_norm else Layer_q(),
+            )
+        self.relu = ReLU_q()
+        self._c = _Cache()
+
+
+class MaxPool_q(Layer_q):
+    """``MaxPool_q`` (``:993-1006``, ``tf.nn.max_pool``) and its TF gradient (lbt_maxpool_fwd/_bwd)."""
+
+    def __init__(self, ksize, strides, padding):
+        self.ksize, self.strides, self.padding = ksize, strides, padding
+        self._c = _Cache()
+
+    def forward(self, X):
+        N, H, W, C = X.shape
+        self.X = X
+        self.d = d = ops.conv_desc(N, H, W, C, C, self.ksize[1], self.ksize[2], self.strides[1], self.strides[2],
+                                   self.padding)
+        y = self._c.get("y", (N, d.Ho, d.Wo, C), torch.float32, X.device)
+        self.amax = self._c.get("amax", (N, d.Ho, d.Wo, C), torch.uint8, X.device)
+        ops.maxpool_fwd(X, y, self.amax, d)
+        self.y = y
+        return y
+
+    def backward(self, grad, stochastic=True):
+        dx = self._c.get("dx", self.X.shape, torch.float32, grad.device)
+        ops.maxpool_bwd(grad.contiguous(), self.amax, dx, self.d)
+        return dx
+
+    def info(self):
+        return "max pool: %dx%d stride %dx%d" % (self.ksize[1], self.ksize[2], self.strides[1], self.strides[2])
 
 
 class AvgPool_q(Layer_q):

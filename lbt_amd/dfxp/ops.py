@@ -366,3 +366,40 @@ def augment_flip_crop(x, pad, seed, counter, out=None):
     call("lbt_augment_flip_crop", ptr(x), ptr(out), N, H, W, C, int(pad), int(seed) & 0xFFFFFFFFFFFFFFFF,
          int(counter) & 0xFFFFFFFFFFFFFFFF, stream())
     return out
+
+
+def maxpool_fwd(x, y, amax, d):
+    _check(x, torch.float32, "x")
+    with _Timed("maxpool_fwd_kernel", 4 * x.numel() + 5 * y.numel()):
+        call("lbt_maxpool_fwd", ptr(x), ptr(y), ptr(amax), d, stream())
+
+
+def maxpool_bwd(g, amax, dx, d):
+    _check(g, torch.float32, "g")
+    with _Timed("maxpool_bwd_kernel", 5 * g.numel() + 4 * dx.numel()):
+        call("lbt_maxpool_bwd", ptr(g), ptr(amax), ptr(dx), d, stream())
+
+
+# ---------------------------------------------------------------- 9..16-bit gradient codes
+def conv_dgrad_generic16(gq, w_hwio, d, qg, qw, dx, add_src=None):
+    with _Timed("conv_dgrad_generic_kernel16", 2 * gq.numel() + w_hwio.numel() + 4 * dx.numel()):
+        call("lbt_conv_dgrad_generic16", ptr(gq), ptr(w_hwio), d, qg, qw, ptr(dx), ptr(add_src), stream())
+
+
+def conv_wgrad_generic16(xq, x_i16, gq, d, slab, nsplit):
+    with _Timed("conv_wgrad_generic_kernel16", xq.numel() * xq.element_size() + 2 * gq.numel() + 8 * slab.numel()):
+        call("lbt_conv_wgrad_generic16", ptr(xq), int(x_i16), ptr(gq), d, ptr(slab), int(nsplit), stream())
+
+
+def conv_wgrad_reduce64(slab, nsplit, K, Cout, qx, qg, w, wd2, dw):
+    call("lbt_conv_wgrad_reduce64", ptr(slab), int(nsplit), int(K), int(Cout), qx, qg, ptr(w), wd2, ptr(dw), stream())
+
+
+def bn_bwd_a_wide(g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C):
+    call("lbt_bn_bwd_a_wide", ptr(g), qrg, ptr(R), ptr(gamma_q), qng, ptr(qn), ptr(gout), ptr(dout), ptr(sums),
+         int(rows), int(inner), int(C), stream())
+
+
+def bn_bwd_b_wide(G, qng, qn, qn_q, ms, sums, n, dx, rows, C):
+    call("lbt_bn_bwd_b_wide", ptr(G), qng, ptr(qn), qn_q, ptr(ms), ptr(sums), int(n), ptr(dx), int(rows), int(C),
+         stream())

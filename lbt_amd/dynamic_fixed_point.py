@@ -12,9 +12,9 @@ import torch
 from . import _lib
 from ._lib import CSTRIDE, NSHARD, OUT_F32, QDesc
 from .dfxp import ops
-from .dfxp.layers import (AvgPool_q, BatchNorm_q, Conv2d_pq, Conv2d_q, Dense_q, Flatten_q, GradientBuffer_q,  # noqa: F401
-                          Layer_q,
-                          Normalization_q, ReLU_q, Rescale_q, ResidualBlock_q, Sequential_q)
+from .dfxp.layers import (AvgPool_q, BatchNorm_q, Conv2d_pq, Conv2d_q, Dense_q, Flatten_q,  # noqa: F401
+                          GradientBuffer_q, Layer_q, MaxPool_q, Normalization_q, ReLU_q, Rescale_q,
+                          ResidualBlock_q, ResidualBottleneck_q, Sequential_q)
 from .runtime import DfxpContext, Quantizer, default_context  # noqa: F401
 
 

@@ -116,3 +116,50 @@ def CIFAR10_Resnet44(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=No
 
 def CIFAR10_Resnet56(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
     return CIFAR10_Resnet(bits, [9, 9, 9], L.ResidualBlock_q, dropout, weight_decay, stochastic, ctx)
+
+
+class ImageNet_Resnet(Model):
+    """ResNet on ImageNet-shape inputs composed from ``ResidualBottleneck_q`` (``:878-980``) and
+    ``MaxPool_q`` (``:993-1006``) -- the reference has both but no builder:
+    conv 7x7/2 -> BN -> ReLU -> max pool 3x3/2 SAME -> stages of bottlenecks at width, 2w, 4w, 8w
+    (strides 1, 2, 2, 2, the stride on the 3x3 as the reference block has it) -> global average
+    pool -> flatten -> Dense_q. ``grad_bits`` sets every gradient quantiser's width (config 4: 16)."""
+
+    def __init__(self, bits, num_blocks, grad_bits=None, width=64, classes=1000, image=224, weight_decay=0,
+                 stochastic=False, ctx=None):
+        self.num_blocks, self.grad_bits, self.width, self.classes = tuple(num_blocks), grad_bits, width, classes
+        super().__init__(bits, [None, image, image, 3], 0.5, weight_decay, stochastic, ctx)
+
+    def get_layers(self):
+        c, gb, wd, ctx, bits = self.width, self.grad_bits, self.weight_decay, self.ctx, self.bits
+        image = self.input_shape[1]
+        layers = [
+            L.Conv2d_pq(name="conv1", bits=bits, ksize=[7, 7, 3, c], strides=[1, 2, 2, 1], padding="SAME",
+                        use_bias=False, weight_decay=wd, grad_bits=gb, ctx=ctx),
+            L.BatchNorm_q(name="conv1-bn", bits=bits, num_features=c, training=self.training, weight_decay=wd,
+                          grad_bits=gb, ctx=ctx),
+            L.ReLU_q(),
+            L.MaxPool_q(ksize=[1, 3, 3, 1], strides=[1, 2, 2, 1], padding="SAME"),
+        ]
+        in_ch = c
+        for si, (nb, stride) in enumerate(zip(self.num_blocks, (1, 2, 2, 2))):
+            ch = c << si
+            for i in range(1, nb + 1):
+                layers.append(L.ResidualBottleneck_q(name="block%d-%d" % (ch, i), bits=bits, in_channels=in_ch,
+                                                     channels=ch, stride=stride if i == 1 else 1,
+                                                     training=self.training, weight_decay=wd, grad_bits=gb, ctx=ctx))
+                in_ch = 4 * ch
+        hw = image
+        for s in (2, 2, 1, 2, 2, 2):  # conv1, max pool, stage strides
+            hw = -(-hw // s)
+        layers += [
+            L.AvgPool_q(ksize=[1, hw, hw, 1], strides=[1, 1, 1, 1], padding="VALID"),
+            L.Flatten_q(in_ch),
+            L.Dense_q(name="fc", bits=bits, in_units=in_ch, units=self.classes, use_bias=False, weight_decay=wd,
+                      grad_bits=gb, ctx=ctx),
+        ]
+        return layers
+
+
+def ImageNet_Resnet50(bits, grad_bits=None, weight_decay=0, classes=1000, image=224, width=64, ctx=None):
+    return ImageNet_Resnet(bits, (3, 4, 6, 3), grad_bits, width, classes, image, weight_decay, ctx=ctx)

@@ -68,7 +68,7 @@ class Quantizer:
 
 
 class DfxpContext:
-    def __init__(self, device="cuda", capacity=1024, seed=0, world_size=1, sums_capacity=1 << 20):
+    def __init__(self, device="cuda", capacity=1024, seed=0, world_size=1, sums_capacity=1 << 24):
         self.device = torch.device(device)
         self.capacity = capacity
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF

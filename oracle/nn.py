@@ -159,8 +159,9 @@ class LayerQ:
 
 
 class Conv2dQ(LayerQ):
-    def __init__(self, name, bits, ksize, strides, padding, weight_decay=0.0):
+    def __init__(self, name, bits, ksize, strides, padding, weight_decay=0.0, grad_bits=None):
         self.name, self.bits, self.ksize = name, bits, tuple(ksize)
+        self.grad_bits = grad_bits or bits
         self.strides = (strides[1], strides[2]) if len(strides) == 4 else tuple(strides)
         self.padding, self.wd = padding, weight_decay
         self.W = None
@@ -179,7 +180,7 @@ class Conv2dQ(LayerQ):
         return scale_int(acc, self.ex + self.ew)
 
     def backward(self, g, ctx):
-        gq, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        gq, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         self.gq = gq
         acc_w = conv_wgrad_int(self.xq, gq, self.strides, self.padding, self.ksize[:2])
         c = F32(2 * self.wd)
@@ -189,8 +190,9 @@ class Conv2dQ(LayerQ):
 
 
 class DenseQ(LayerQ):
-    def __init__(self, name, bits, in_units, units, weight_decay=0.0):
+    def __init__(self, name, bits, in_units, units, weight_decay=0.0, grad_bits=None):
         self.name, self.bits, self.in_units, self.units, self.wd = name, bits, in_units, units, weight_decay
+        self.grad_bits = grad_bits or bits
         self.W = None
 
     def range_names(self):
@@ -206,7 +208,7 @@ class DenseQ(LayerQ):
         return scale_int(acc, self.ex + self.ew)
 
     def backward(self, g, ctx):
-        gq, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        gq, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         self.gq = gq
         acc_w = np.rint(self.xq.astype(np.float64).T @ gq.astype(np.float64)).astype(np.int64)
         c = F32(2 * self.wd)
@@ -216,8 +218,9 @@ class DenseQ(LayerQ):
 
 
 class NormQ(LayerQ):
-    def __init__(self, name, bits, num_features, momentum=0.999, eps=1e-5):
+    def __init__(self, name, bits, num_features, momentum=0.999, eps=1e-5, grad_bits=None):
         self.name, self.bits, self.C = name, bits, num_features
+        self.grad_bits = grad_bits or bits
         self.momentum, self.eps = momentum, eps
         self.mean_running = np.zeros(num_features, F32)
         self.var_running = np.ones(num_features, F32)
@@ -246,7 +249,7 @@ class NormQ(LayerQ):
         return xhat
 
     def backward(self, g, ctx):
-        G, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        G, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         sg = 2.0 ** -eg
         s = 2.0 ** -self.e
         C = g.shape[-1]
@@ -266,8 +269,9 @@ class NormQ(LayerQ):
 
 
 class RescaleQ(LayerQ):
-    def __init__(self, name, bits, num_features, weight_decay=0.0):
+    def __init__(self, name, bits, num_features, weight_decay=0.0, grad_bits=None):
         self.name, self.bits, self.C, self.wd = name, bits, num_features, weight_decay
+        self.grad_bits = grad_bits or bits
         self.gamma = np.ones(num_features, F32)
         self.beta = np.zeros(num_features, F32)
 
@@ -288,7 +292,7 @@ class RescaleQ(LayerQ):
         return ((xr * self.gq_f).astype(F32) + bq_f).astype(F32)
 
     def backward(self, g, ctx):
-        G, eg = ctx.q(self.name + "/grad_range", g, self.bits)
+        G, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         C = g.shape[-1]
         Gf = G.reshape(-1, C).astype(np.int64)
         Rf = self.R.reshape(-1, C).astype(np.int64)
@@ -323,9 +327,9 @@ class SequentialQ(LayerQ):
         return [r for l in self.layers for r in l.range_names()]
 
 
-def BatchNormQ(name, bits, num_features, weight_decay=0.0):
-    return SequentialQ(NormQ(name + "-norm", bits, num_features),
-                       RescaleQ(name + "-rescale", bits, num_features, weight_decay))
+def BatchNormQ(name, bits, num_features, weight_decay=0.0, grad_bits=None):
+    return SequentialQ(NormQ(name + "-norm", bits, num_features, grad_bits=grad_bits),
+                       RescaleQ(name + "-rescale", bits, num_features, weight_decay, grad_bits=grad_bits))
 
 
 class ReluQ(LayerQ):
@@ -370,6 +374,79 @@ class ResidualBlockQ(LayerQ):
 
     def range_names(self):
         return self.residual.range_names() + self.shortcut.range_names()
+
+
+class MaxPoolQ(LayerQ):
+    """``MaxPool_q`` (``dynamic_fixed_point.py:993-1006``, ``tf.nn.max_pool``; SAME pads with -inf).
+    Backward = TF MaxPoolGrad: each output's gradient goes to the first maximum of its window in
+    (kh, kw) order, accumulated per input in ascending output order (fp32, from 0)."""
+
+    def __init__(self, ksize, strides, padding):
+        self.kh, self.kw = ksize[1], ksize[2]
+        self.sh, self.sw = strides[1], strides[2]
+        self.padding = padding
+
+    def forward(self, X, ctx):
+        N, H, W, C = X.shape
+        Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, self.kh, self.kw, self.sh, self.sw, self.padding)
+        self.shape, self.geom = X.shape, (Ho, Wo, pt, pl)
+        y = np.full((N, Ho, Wo, C), -np.inf, F32)
+        amax = np.zeros((N, Ho, Wo, C), np.int64)
+        for i in range(self.kh):
+            for j in range(self.kw):
+                for oh in range(Ho):
+                    ih = oh * self.sh + i - pt
+                    if not 0 <= ih < H:
+                        continue
+                    for ow in range(Wo):
+                        iw = ow * self.sw + j - pl
+                        if not 0 <= iw < W:
+                            continue
+                        v = X[:, ih, iw, :]
+                        better = v > y[:, oh, ow, :]
+                        y[:, oh, ow, :] = np.where(better, v, y[:, oh, ow, :])
+                        amax[:, oh, ow, :] = np.where(better, i * self.kw + j, amax[:, oh, ow, :])
+        self.amax = amax
+        return y
+
+    def backward(self, g, ctx):
+        N, H, W, C = self.shape
+        Ho, Wo, pt, pl = self.geom
+        dx = np.zeros(self.shape, F32)
+        for oh in range(Ho):
+            for ow in range(Wo):
+                a = self.amax[:, oh, ow, :]
+                ih = oh * self.sh - pt + a // self.kw
+                iw = ow * self.sw - pl + a % self.kw
+                n_idx, c_idx = np.meshgrid(np.arange(N), np.arange(C), indexing="ij")
+                dx[n_idx, ih, iw, c_idx] = (dx[n_idx, ih, iw, c_idx] + g[:, oh, ow, :]).astype(F32)
+        return dx
+
+
+class BottleneckQ(ResidualBlockQ):
+    """``ResidualBottleneck_q`` (``:878-980``): 1x1 -> BN -> ReLU -> 3x3 (stride) -> BN -> ReLU ->
+    1x1 (4x channels) -> BN, shortcut as ``_build_shortcut`` (``:825-856``) with expansion 4."""
+
+    def __init__(self, name, bits, in_channels, channels, stride, weight_decay=0.0, grad_bits=None):
+        out = 4 * channels
+        gb = dict(grad_bits=grad_bits)
+        self.residual = SequentialQ(
+            Conv2dQ(name + "-1", bits, [1, 1, in_channels, channels], [1, 1, 1, 1], "SAME", weight_decay, **gb),
+            BatchNormQ(name + "-bn1", bits, channels, weight_decay, **gb),
+            ReluQ(),
+            Conv2dQ(name + "-2", bits, [3, 3, channels, channels], [1, stride, stride, 1], "SAME", weight_decay, **gb),
+            BatchNormQ(name + "-bn2", bits, channels, weight_decay, **gb),
+            ReluQ(),
+            Conv2dQ(name + "-3", bits, [1, 1, channels, out], [1, 1, 1, 1], "SAME", weight_decay, **gb),
+            BatchNormQ(name + "-bn3", bits, out, weight_decay, **gb))
+        if stride == 1 and in_channels == out:
+            self.shortcut = SequentialQ()
+        else:
+            self.shortcut = SequentialQ(
+                Conv2dQ(name + "-shortcut", bits, [1, 1, in_channels, out], [1, stride, stride, 1], "SAME",
+                        weight_decay, **gb),
+                BatchNormQ(name + "-shortcut-bn", bits, out, weight_decay, **gb))
+        self.relu = ReluQ()
 
 
 class AvgPoolQ(LayerQ):

@@ -28,6 +28,28 @@ def build_resnet(num_blocks=(3, 3, 3), bits=8, weight_decay=0.0):
     return nn.SequentialQ(*layers)
 
 
+def build_resnet50(blocks=(3, 4, 6, 3), width=64, classes=1000, bits=8, grad_bits=None, weight_decay=0.0):
+    """ResNet-50 composed from ``ResidualBottleneck_q`` (the reference has the block, ``:878-980``,
+    and ``MaxPool_q``, ``:993-1006``, but no builder): conv 7x7/2 -> BN -> ReLU -> max pool 3x3/2
+    SAME -> 4 stages of bottlenecks at width, 2w, 4w, 8w (strides 1, 2, 2, 2; the stride on the 3x3,
+    as the reference block has it) -> global average pool -> flatten -> Dense_q. grad_bits: the
+    gradient quantisers' width (config 4: 16)."""
+    gb = dict(grad_bits=grad_bits)
+    layers = [nn.Conv2dQ("conv1", bits, [7, 7, 3, width], [1, 2, 2, 1], "SAME", weight_decay, **gb),
+              nn.BatchNormQ("conv1-bn", bits, width, weight_decay, **gb),
+              nn.ReluQ(),
+              nn.MaxPoolQ([1, 3, 3, 1], [1, 2, 2, 1], "SAME")]
+    in_ch = width
+    for si, (nb, stride) in enumerate(zip(blocks, (1, 2, 2, 2))):
+        ch = width << si
+        for i in range(1, nb + 1):
+            layers.append(nn.BottleneckQ("block%d-%d" % (ch, i), bits, in_ch, ch, stride if i == 1 else 1,
+                                         weight_decay, **gb))
+            in_ch = 4 * ch
+    layers += [nn.AvgPoolQ(), nn.FlattenQ(in_ch), nn.DenseQ("fc", bits, in_ch, classes, weight_decay, **gb)]
+    return nn.SequentialQ(*layers)
+
+
 def param_list(model):
     """[(name, owner)] in grads_and_vars order."""
     return model.params()

@@ -1,0 +1,128 @@
+"""ResNet-50 (ResidualBottleneck_q, MaxPool_q) on ImageNet-shape inputs, with
+8-bit and 16-bit gradient quantisers.
+
+CPU: the oracle's MaxPoolQ against a direct loop restatement of tf.nn.max_pool and its gradient.
+GPU: the HIP layer path against the oracle, bit-exact (forward logits, every gradient given the
+same d loss / d logits, every exponent update), on reduced widths / depths so the numpy oracle
+finishes in seconds; the full-size model through a training step (shape and finiteness checks).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nn as onn
+from oracle import resnet as oresnet
+
+DEV = "cuda"
+F32 = np.float32
+
+
+def _maxpool_loops(x, k, s, padding):
+    N, H, W, C = x.shape
+    Ho, Wo, pt, _, pl, _ = onn.conv_geometry(H, W, k, k, s, s, padding)
+    y = np.zeros((N, Ho, Wo, C), F32)
+    arg = np.zeros((N, Ho, Wo, C, 2), np.int64)
+    for n in range(N):
+        for oh in range(Ho):
+            for ow in range(Wo):
+                for c in range(C):
+                    best, bi = -np.inf, None
+                    for i in range(k):
+                        for j in range(k):
+                            ih, iw = oh * s + i - pt, ow * s + j - pl
+                            if 0 <= ih < H and 0 <= iw < W and x[n, ih, iw, c] > best:
+                                best, bi = x[n, ih, iw, c], (ih, iw)
+                    y[n, oh, ow, c] = best
+                    arg[n, oh, ow, c] = bi
+    return y, arg
+
+
+def test_oracle_maxpool_matches_loops():
+    rng = np.random.default_rng(0)
+    # ReLU-like input: many exact ties at 0 exercise the first-maximum rule
+    x = np.maximum(rng.normal(size=(2, 7, 6, 3)), 0).astype(F32)
+    g = rng.normal(size=(2, 4, 3, 3)).astype(F32)
+    mp = onn.MaxPoolQ([1, 3, 3, 1], [1, 2, 2, 1], "SAME")
+    y = mp.forward(x, None)
+    yl, arg = _maxpool_loops(x, 3, 2, "SAME")
+    assert np.array_equal(y, yl)
+    dx = mp.backward(g, None)
+    want = np.zeros_like(x)
+    for n in range(2):
+        for oh in range(4):
+            for ow in range(3):
+                for c in range(3):
+                    ih, iw = arg[n, oh, ow, c]
+                    want[n, ih, iw, c] = F32(want[n, ih, iw, c] + g[n, oh, ow, c])
+    assert np.array_equal(dx, want)
+
+
+def _pair(blocks, width, classes, image, grad_bits, seed=0):
+    from lbt_amd.models import ImageNet_Resnet
+    from lbt_amd.runtime import DfxpContext
+    ctx = DfxpContext(seed=seed)
+    gm = ImageNet_Resnet(8, blocks, grad_bits=grad_bits, width=width, classes=classes, image=image, ctx=ctx)
+    om = oresnet.build_resnet50(blocks, width, classes, 8, grad_bits)
+    return ctx, gm, om
+
+
+def _params(gm):
+    out = {}
+    for owner, var, _ in gm.param_slots():
+        out[owner.name + {"W": "/W", "gamma": "/g", "beta": "/b"}[var]] = getattr(owner, var).detach().cpu().numpy()
+    return out
+
+
+def _grads(gm):
+    out = {}
+    for owner, var, gname in gm.param_slots():
+        out[owner.name + {"W": "/W", "gamma": "/g", "beta": "/b"}[var]] = getattr(owner, gname).detach().cpu().numpy()
+    return out
+
+
+def _batch(B, image, classes, seed):
+    rng = np.random.default_rng(seed)
+    x = ((rng.integers(0, 256, size=(B, image, image, 3)) - 127.5) / 128).astype(F32)
+    return x, rng.integers(0, classes, size=B).astype(np.int32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grad_bits", [8, 16])
+@pytest.mark.parametrize("blocks,width,image", [((1, 1, 1, 1), 8, 32), ((2, 1, 1, 1), 16, 40)])
+def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, grad_bits):
+    ctx, gm, om = _pair(blocks, width, 10, image, grad_bits, seed=1)
+    oresnet.set_params(om, _params(gm))
+    x, y = _batch(4, image, 10, seed=2)
+    octx = onn.Ctx(oresnet.init_ranges(om), 0, ctx.seed)
+    logits = gm.forward(torch.from_numpy(x).to(DEV))
+    lr = om.forward(x, octx)
+    assert np.array_equal(logits.cpu().numpy(), lr), "forward must be bit-exact"
+    gm.compute_loss(torch.from_numpy(y).to(DEV))
+    dz = gm.dlogits.cpu().numpy()
+    gm.backward()
+    om.backward(dz, octx)
+    gg, og = _grads(gm), oresnet.get_grads(om)
+    assert gg.keys() == og.keys()
+    for k in gg:
+        assert np.array_equal(gg[k], og[k]), k
+    ctx.update_range_op()
+    assert ctx.ranges() == octx.new_ranges()
+
+
+@pytest.mark.gpu
+def test_resnet50_full_size_step():
+    """The real ResNet-50 (224x224, 1000 classes, [3,4,6,3]) through one graph-captured training
+    step with 16-bit gradients: finite loss, every gradient finite, exponents updated."""
+    from lbt_amd.models import ImageNet_Resnet50
+    from lbt_amd.runtime import DfxpContext
+    from lbt_amd.trainer import Trainer
+    ctx = DfxpContext(seed=0)
+    m = ImageNet_Resnet50(8, grad_bits=16, weight_decay=1e-4, ctx=ctx)
+    t = Trainer(m, lr=0.01, momentum=0.9, use_graph=True)
+    x, y = _batch(2, 224, 1000, seed=3)
+    for _ in range(2):
+        loss = t.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+    torch.cuda.synchronize()
+    assert np.isfinite(loss.item())
+    assert torch.isfinite(t.flat.g).all() and torch.isfinite(t.flat.w).all()
+    assert int(ctx.step.item()) == 2
