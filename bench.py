@@ -21,6 +21,8 @@ import torch
 import torch.distributed as dist
 
 METRIC = "train-step samples/sec, ResNet-20 CIFAR-10 8-bit DFP, 1/2/4/8 MI355X"
+# BASELINE.json configs[3]: not the headline metric, a workload of its own
+METRIC_R50 = "train-step samples/sec, ResNet-50 ImageNet-shape 8-bit W/A 16-bit grad DFP"
 
 
 def synthetic_batches(n, B, seed, device):
@@ -33,6 +35,51 @@ def synthetic_batches(n, B, seed, device):
         xs.append(x.contiguous())
         ys.append(y)
     return xs, ys
+
+
+def synthetic_imagenet(n, B, seed, device, image=224, classes=1000):
+    g = torch.Generator().manual_seed(seed)
+    xs, ys = [], []
+    for _ in range(n):
+        x = ((torch.randint(0, 256, (B, image, image, 3), generator=g).float() - 127.5) / 128).to(device)
+        xs.append(x.contiguous())
+        ys.append(torch.randint(0, classes, (B,), generator=g).to(torch.int32).to(device))
+    return xs, ys
+
+
+def cpu_baseline_r50(seconds=15.0, batch=1):
+    """The oracle's ResNet-50 step (16-bit gradients) on the host, B=1 per step."""
+    from oracle import resnet as oresnet
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    m = oresnet.build_resnet50(bits=8, grad_bits=16, weight_decay=1e-4)
+    rng = np.random.default_rng(0)
+    params = {}
+    for name, owner in m.params():
+        if name.endswith("/W"):
+            shp = owner.ksize if hasattr(owner, "ksize") else (owner.in_units, owner.units)
+            fan = float(np.prod(shp[:-1]))
+            params[name] = rng.uniform(-np.sqrt(3 / fan), np.sqrt(3 / fan), size=shp).astype(np.float32)
+        elif name.endswith("/g"):
+            params[name] = np.ones(owner.C, np.float32)
+        else:
+            params[name] = np.zeros(owner.C, np.float32)
+    state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()},
+                 ranges=oresnet.init_ranges(m), step=0)
+    x = ((rng.integers(0, 256, size=(batch, 224, 224, 3)) - 127.5) / 128).astype(np.float32)
+    y = rng.integers(0, 1000, size=batch)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        _, state, _ = oresnet.train_step(m, state, x, y)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(n * batch / el, 3), "unit": "samples/s", "cores": int(cores), "kind": "port",
+            "sample": "%d oracle ResNet-50 train steps (numpy restatement), B=%d, 224x224, %.1f s" % (n, batch, el)}
 
 
 def cpu_baseline(seconds=15.0, batch=128):
@@ -83,7 +130,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--workload", choices=("resnet20", "resnet50"), default="resnet20",
+                    help="resnet50: BASELINE configs[3], ImageNet-shape, 16-bit gradients (layer path)")
     args = ap.parse_args()
+    r50 = args.workload == "resnet50"
+    if r50 and args.batch == 128:
+        args.batch = 32
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -99,13 +151,18 @@ def main():
     from lbt_amd.trainer import Trainer
 
     ctx = DfxpContext(device=device, seed=0, world_size=world)
-    model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
-    if not args.layerwise:
-        from lbt_amd.fused import FusedResNet
-        model = FusedResNet(model)
+    if r50:
+        from lbt_amd.models import ImageNet_Resnet50
+        model = ImageNet_Resnet50(8, grad_bits=16, weight_decay=1e-4, ctx=ctx)
+        xs, ys = synthetic_imagenet(4, args.batch, 1000 + rank, device)
+    else:
+        model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+        if not args.layerwise:
+            from lbt_amd.fused import FusedResNet
+            model = FusedResNet(model)
+        xs, ys = synthetic_batches(4, args.batch, seed=1000 + rank, device=device)
     trainer = Trainer(model, lr=1e-2, momentum=0.9, batch_size=args.batch, use_graph=not args.eager)
     trainer.init_model()
-    xs, ys = synthetic_batches(4, args.batch, seed=1000 + rank, device=device)
 
     for i in range(args.warmup):
         trainer.step(xs[i % 4], ys[i % 4])
@@ -128,7 +185,7 @@ def main():
     loss = float(model.loss.item())
 
     out = {
-        "metric": METRIC,
+        "metric": METRIC_R50 if r50 else METRIC,
         "value": round(args.batch * world * args.steps / el, 2),
         "unit": "samples/s",
         "n_gpus": world,
@@ -145,11 +202,17 @@ def main():
                    "parallelism": "dp%d" % world, "hip_graph": not args.eager,
                    "executor": "layerwise" if args.layerwise else "fused", "final_loss": round(loss, 4)},
     }
+    if r50:
+        out["data"] = "synthetic ImageNet-shaped batches (224x224x3 uniform uint8 pixels, (p-127.5)/128), random-init"
+        out["config"] = {"workload": "ResNet-50 ImageNet-shape, 8-bit DFXP W/A, 16-bit DFXP gradients, train step",
+                         "global_batch": args.batch * world, "per_gpu_batch": args.batch, "image": [224, 224, 3],
+                         "classes": 1000, "parallelism": "dp%d" % world, "hip_graph": not args.eager,
+                         "executor": "layerwise", "final_loss": round(loss, 4)}
     if rank == 0 and world == 1 and not args.no_roofline:
         from lbt_amd.roofline import measure_dominant
         out["roofline"] = measure_dominant(trainer, xs[0], ys[0])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.batch)
+        out["cpu_baseline"] = cpu_baseline_r50(args.cpu_seconds) if r50 else cpu_baseline(args.cpu_seconds, args.batch)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
