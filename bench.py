@@ -23,6 +23,7 @@ import torch.distributed as dist
 METRIC = "train-step samples/sec, ResNet-20 CIFAR-10 8-bit DFP, 1/2/4/8 MI355X"
 # BASELINE.json configs[3]: not the headline metric, a workload of its own
 METRIC_R50 = "train-step samples/sec, ResNet-50 ImageNet-shape 8-bit W/A 16-bit grad DFP"
+METRIC_W4 = "train-step samples/sec, ResNet-20 CIFAR-10 4-bit W / 8-bit A,G DFP"  # configs[4]
 
 
 def synthetic_batches(n, B, seed, device):
@@ -130,10 +131,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--workload", choices=("resnet20", "resnet50"), default="resnet20",
-                    help="resnet50: BASELINE configs[3], ImageNet-shape, 16-bit gradients (layer path)")
+    ap.add_argument("--workload", choices=("resnet20", "resnet50", "resnet20w4"), default="resnet20",
+                    help="resnet50: BASELINE configs[3], ImageNet-shape, 16-bit gradients (layer path); "
+                         "resnet20w4: configs[4], 4-bit packed weights")
     args = ap.parse_args()
     r50 = args.workload == "resnet50"
+    w4 = args.workload == "resnet20w4"
     if r50 and args.batch == 128:
         args.batch = 32
 
@@ -156,7 +159,7 @@ def main():
         model = ImageNet_Resnet50(8, grad_bits=16, weight_decay=1e-4, ctx=ctx)
         xs, ys = synthetic_imagenet(4, args.batch, 1000 + rank, device)
     else:
-        model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+        model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, weight_bits=4 if w4 else None)
         if not args.layerwise:
             from lbt_amd.fused import FusedResNet
             model = FusedResNet(model)
@@ -185,7 +188,7 @@ def main():
     loss = float(model.loss.item())
 
     out = {
-        "metric": METRIC_R50 if r50 else METRIC,
+        "metric": METRIC_R50 if r50 else (METRIC_W4 if w4 else METRIC),
         "value": round(args.batch * world * args.steps / el, 2),
         "unit": "samples/s",
         "n_gpus": world,
@@ -202,6 +205,8 @@ def main():
                    "parallelism": "dp%d" % world, "hip_graph": not args.eager,
                    "executor": "layerwise" if args.layerwise else "fused", "final_loss": round(loss, 4)},
     }
+    if w4:
+        out["config"]["workload"] = "ResNet-20 CIFAR-10, 4-bit DFXP weights (packed, 2 per byte), 8-bit A/G, train step"
     if r50:
         out["data"] = "synthetic ImageNet-shaped batches (224x224x3 uniform uint8 pixels, (p-127.5)/128), random-init"
         out["config"] = {"workload": "ResNet-50 ImageNet-shape, 8-bit DFXP W/A, 16-bit DFXP gradients, train step",

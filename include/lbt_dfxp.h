@@ -145,6 +145,17 @@ int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t
  * acc * 2^-(eg+ew) (+ add_src[e] if add_src != NULL).  Requires Cin%16 == 0, Cout%16 == 0. */
 int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
                       lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
+/* 4-bit weights (W 4-bit / A 8-bit): the same GEMMs with the weight
+ * image packed two signed 4-bit codes per byte (lbt_pack_int4 of lbt_dfxp_quantize_weight's wf /
+ * wd at qw.bits <= 4; ksf / ksd still count 16-element k-slices, 8 bytes each). gfx950 has no
+ * int4 MFMA: the kernels unpack to int8 in registers -- half the weight bytes from HBM.        */
+int lbt_conv_fwd_i8w4(const int8_t* xq, int32_t x_u8off, const uint8_t* wf4, int32_t ksf, const int32_t* wcolsum,
+                      lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, int8_t* yq, lbt_qdesc qout,
+                      int64_t* ychsum, void* stream);
+int lbt_conv_dgrad_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
+                        float* dx, const float* add_src, void* stream);
+/* dst[i] = (src[2i] & 15) | (src[2i+1] << 4), n even: pack signed 4-bit codes held in int8.   */
+int lbt_pack_int4(const int8_t* src, uint8_t* dst, int64_t n, void* stream);
 
 /* Conv2d_q backward dW = tf.gradients(y, W, gradq) (dynamic_fixed_point.py:302), pass 1:
  * the pixels are split into `nsplit` ranges (x Cout/16 column slices x taps = the grid); the
@@ -274,6 +285,9 @@ int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream);
  * y_mask or from branch-1 R; optional gmask_out.                                          */
 int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                             lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream);
+/* ... with the 4-bit packed weight image (see lbt_conv_fwd_i8w4). */
+int lbt_conv_dgrad_chain_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                              lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream);
 
 /* Pass B (the rest of Normalization_q.backward): with SG = sum G, SGQ = sum G*q from pass A,
  *   mg = sg*SG/n, mgx = sg*(s*SGQ - mu*SG)/(n*sigma)   (double -> fp32)

@@ -112,7 +112,24 @@ __global__ __launch_bounds__(kT) void augment_kernel(const float* __restrict__ x
   y[e] = v;
 }
 
+// ---------------------------------------------------------------- 4-bit weight images
+// dst[i] = (src[2i] & 15) | (src[2i+1] << 4): two signed 4-bit codes per byte, element order kept.
+__global__ __launch_bounds__(kT) void pack_int4_kernel(const int8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                       int64_t nbytes) {
+  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= nbytes) return;
+  dst[i] = (uint8_t)((src[2 * i] & 15) | ((src[2 * i + 1] & 15) << 4));
+}
+
 }  // namespace
+
+extern "C" int lbt_pack_int4(const int8_t* src, uint8_t* dst, int64_t n, void* stream) {
+  if (n <= 0 || n % 2) return LBT_EINVAL;
+  const int64_t nb = n / 2;
+  hipLaunchKernelGGL(pack_int4_kernel, dim3((unsigned)((nb + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, src, dst,
+                     nb);
+  return (int)hipGetLastError();
+}
 
 extern "C" int lbt_grad_buffer_bwd(const float* g, int64_t n_g, float* buffer, int64_t n_buf, int64_t inner,
                                    lbt_qdesc q, float* gq, void* stream) {

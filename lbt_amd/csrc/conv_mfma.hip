@@ -51,7 +51,26 @@ struct GemmArgs {
   lbt_chain_bwd_a chain;  // dgrad epilogue = pass A of this chain (CF != 0)
 };
 
-template <int MODE, int CS, int NT, int CF = 0, int NB = 1>
+// 16 signed 4-bit codes (element e = nibble e: low nibble of byte e/2 first) -> 16 int8 lanes of an
+// MFMA operand: lo / hi nibbles interleaved with v_perm_b32, then sign-extended bytewise without
+// carries: (b & 7) | ((b & 8) * 0x1F) sets bits 3-7 exactly when bit 3 (the sign) is set.
+LBT_DEV v4i unpack_i4x16(v2i pk) {
+  v4i o;
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const uint32_t x = (uint32_t)(w == 0 ? pk.x : pk.y);
+    const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+    const uint32_t a = __builtin_amdgcn_perm(hi, lo, 0x05010400u);  // e0 e1 e2 e3
+    const uint32_t b = __builtin_amdgcn_perm(hi, lo, 0x07030602u);  // e4 e5 e6 e7
+    o[2 * w] = (int)((a & 0x07070707u) | ((a & 0x08080808u) * 0x1Fu));
+    o[2 * w + 1] = (int)((b & 0x07070707u) | ((b & 0x08080808u) * 0x1Fu));
+  }
+  return o;
+}
+
+// W4: the B operand (weights) is stored as packed signed 4-bit codes, 8 bytes per 16-element
+// k-slice (no int4 MFMA on gfx950 -- unpacked to int8 in registers).
+template <int MODE, int CS, int NT, int CF = 0, int NB = 1, bool W4 = false>
 __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0) ? 8 : 1) void conv_gemm_kernel(
     GemmArgs p) {
   using G = EpiGeom<NT>;
@@ -111,7 +130,10 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0
   };
   auto load_b = [&](int kk, int j) -> v4i {
     const int col = (nt0 + j) * 16 + r;
-    return *reinterpret_cast<const v4i*>(p.b + ((int64_t)col * p.ks + kk * 4 + kg) * 16);
+    if constexpr (W4)
+      return unpack_i4x16(*reinterpret_cast<const v2i*>(p.b + ((int64_t)col * p.ks + kk * 4 + kg) * 8));
+    else
+      return *reinterpret_cast<const v4i*>(p.b + ((int64_t)col * p.ks + kk * 4 + kg) * 16);
   };
 
   v4i acc[NTW];
@@ -360,30 +382,30 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const int32_t* __rest
   dw[i] = a + b;
 }
 
-template <int MODE, int NT>
+template <int MODE, int NT, bool W4>
 int launch_gemm_nt(const GemmArgs& p, int cs, hipStream_t st) {
   constexpr int MTB = EpiGeom<NT>::MTB;
   const int64_t mtiles = (p.M + 15) / 16;
   const int64_t blocks = (mtiles + MTB - 1) / MTB;
   if (blocks > 0x7fffffff) return LBT_EINVAL;
   switch (cs) {
-    case 1: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
-    case 4: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 4, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
-    case 8: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 8, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, NT, 0, 1, W4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, NT, 0, 1, W4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 4, NT, 0, 1, W4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((conv_gemm_kernel<MODE, 8, NT, 0, 1, W4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p); break;
     default: return LBT_EINVAL;
   }
   return (int)hipGetLastError();
 }
 
-template <int MODE>
+template <int MODE, bool W4 = false>
 int launch_gemm(const GemmArgs& p, int cs, hipStream_t st) {
   if (p.M * p.ncol >= (int64_t)1 << 31) return LBT_EINVAL;  // 32-bit row / element arithmetic
   switch (p.ncol / 16) {
-    case 1: return launch_gemm_nt<MODE, 1>(p, cs, st);
-    case 2: return launch_gemm_nt<MODE, 2>(p, cs, st);
-    case 4: return launch_gemm_nt<MODE, 4>(p, cs, st);
-    case 8: return launch_gemm_nt<MODE, 8>(p, cs, st);
+    case 1: return launch_gemm_nt<MODE, 1, W4>(p, cs, st);
+    case 2: return launch_gemm_nt<MODE, 2, W4>(p, cs, st);
+    case 4: return launch_gemm_nt<MODE, 4, W4>(p, cs, st);
+    case 8: return launch_gemm_nt<MODE, 8, W4>(p, cs, st);
     default: return LBT_EINVAL;
   }
 }
@@ -397,9 +419,11 @@ bool desc_ok(const lbt_conv_desc& d) {
 
 LBT_TRACE_SETTER(conv)
 
-extern "C" int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf,
-                               const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,
-                               int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream) {
+namespace {
+template <bool W4>
+int conv_fwd(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf, const int32_t* wcolsum,
+             lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum,
+             void* stream) {
   if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cout > 128) return LBT_EINVAL;
   const int cs = d.Cin / 16;
   GemmArgs p;
@@ -411,11 +435,12 @@ extern "C" int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* 
   if (yq && qout.stochastic && !qout.noise) return LBT_EINVAL;  // quantising epilogue reads the noise table
   p.d = d; p.qa = qx; p.qb = qw; p.y = y; p.add_src = nullptr; p.yq = yq; p.qout = qout; p.ychsum = ychsum;
   p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
-  return launch_gemm<MODE_FWD>(p, cs, (hipStream_t)stream);
+  return launch_gemm<MODE_FWD, W4>(p, cs, (hipStream_t)stream);
 }
 
-extern "C" int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
-                                 lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
+template <bool W4>
+int conv_dgrad(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
+               float* dx, const float* add_src, void* stream) {
   if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cin > 128) return LBT_EINVAL;
   const int cs = d.Cout / 16;
   GemmArgs p;
@@ -425,25 +450,48 @@ extern "C" int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd
   p.d = d; p.qa = qg; p.qb = qw; p.y = dx; p.add_src = add_src; p.yq = nullptr; p.qout = lbt_qdesc{};
   p.ychsum = nullptr;
   p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
-  return launch_gemm<MODE_DGRAD>(p, cs, (hipStream_t)stream);
+  return launch_gemm<MODE_DGRAD, W4>(p, cs, (hipStream_t)stream);
+}
+}  // namespace
+
+extern "C" int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf,
+                               const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,
+                               int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream) {
+  return conv_fwd<false>(xq, x_u8off, wf, ksf, wcolsum, d, qx, qw, y, yq, qout, ychsum, stream);
+}
+extern "C" int lbt_conv_fwd_i8w4(const int8_t* xq, int32_t x_u8off, const uint8_t* wf4, int32_t ksf,
+                                 const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,
+                                 int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream) {
+  if (qw.bits > 4) return LBT_EINVAL;
+  return conv_fwd<true>(xq, x_u8off, (const int8_t*)wf4, ksf, wcolsum, d, qx, qw, y, yq, qout, ychsum, stream);
+}
+extern "C" int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                                 lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
+  return conv_dgrad<false>(gq, wd, ksd, d, qg, qw, dx, add_src, stream);
+}
+extern "C" int lbt_conv_dgrad_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                                   lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
+  if (qw.bits > 4) return LBT_EINVAL;
+  return conv_dgrad<true>(gq, (const int8_t*)wd4, ksd, d, qg, qw, dx, add_src, stream);
 }
 
 namespace {
 
-template <int CS, int NT, int CF, int NB>
+template <int CS, int NT, int CF, int NB, bool W4>
 int launch_dgrad_chain(const GemmArgs& p, hipStream_t st) {
   constexpr int MTB = EpiGeom<NT>::MTB;
   const int64_t blocks = ((p.M + 15) / 16 + MTB - 1) / MTB;
-  hipLaunchKernelGGL((conv_gemm_kernel<MODE_DGRAD, CS, NT, CF, NB>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p);
+  hipLaunchKernelGGL((conv_gemm_kernel<MODE_DGRAD, CS, NT, CF, NB, W4>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
+                     p);
   return (int)hipGetLastError();
 }
 
 constexpr int kAFused = kAFB | kAStoch;
 
-}  // namespace
 
-extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
-                                       lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream) {
+template <bool W4>
+int dgrad_chain(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
+                const float* add_src, const lbt_chain_bwd_a* a, void* stream) {
   if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cin > 128 || !a) return LBT_EINVAL;
   if (a->C != d.Cin || a->rows != d.N || a->inner != (int64_t)d.H * d.W * d.Cin) return LBT_EINVAL;
   const int f = bwd_a_flags(*a);
@@ -465,7 +513,7 @@ extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32
   const int nt = d.Cin / 16;
   const int key = (cs << 8) | (nt << 4) | (a->has_b2 ? 1 : 0);
 #define LBT_DC(CS_, NT_, CF_, NB_)                                                                  \
-  if (key == ((CS_ << 8) | (NT_ << 4) | (NB_ == 2)) && f == (CF_)) return launch_dgrad_chain<CS_, NT_, CF_, NB_>(p, st);
+  if (key == ((CS_ << 8) | (NT_ << 4) | (NB_ == 2)) && f == (CF_)) return launch_dgrad_chain<CS_, NT_, CF_, NB_, W4>(p, st);
 #define LBT_DC_SHAPES(CF_, NB_) \
   LBT_DC(1, 1, CF_, NB_) LBT_DC(2, 2, CF_, NB_) LBT_DC(4, 4, CF_, NB_) LBT_DC(2, 1, CF_, NB_) LBT_DC(4, 2, CF_, NB_)
   LBT_DC_SHAPES(kAFused | kAMaskR, 1)             // block, first BN (mask from R1)
@@ -475,6 +523,19 @@ extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32
 #undef LBT_DC_SHAPES
 #undef LBT_DC
   return LBT_EINVAL;
+}
+
+}  // namespace
+
+extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                                       lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream) {
+  return dgrad_chain<false>(gq, wd, ksd, d, qg, qw, add_src, a, stream);
+}
+extern "C" int lbt_conv_dgrad_chain_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d,
+                                         lbt_qdesc qg, lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a,
+                                         void* stream) {
+  if (qw.bits > 4) return LBT_EINVAL;
+  return dgrad_chain<true>(gq, (const int8_t*)wd4, ksd, d, qg, qw, add_src, a, stream);
 }
 
 extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t* gq, lbt_conv_desc d,

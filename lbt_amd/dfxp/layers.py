@@ -86,10 +86,11 @@ class Conv2d_q(Layer_q):
 
     def __init__(self, name, bits, ksize, strides, padding, use_bias=True, weight_decay=0,
                  target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2,
-                 input_nonnegative=False, grad_bits=None, ctx=None):
+                 input_nonnegative=False, grad_bits=None, weight_bits=None, ctx=None):
         self.ctx = ctx = ctx or default_context()
         h, w, Cin, Cout = self.ksize = list(ksize)
         self.grad_bits = grad_bits = grad_bits or bits  # config 4: 16-bit gradients (the reference: one `bits`)
+        self.weight_bits = weight_bits = weight_bits or bits  # config 5: 4-bit weights
         self.strides = list(strides)
         self.padding = padding
         self.name, self.use_bias, self.bits = name, use_bias, bits
@@ -100,7 +101,7 @@ class Conv2d_q(Layer_q):
         self.W = _as_param(_rng(ctx, name + "/W").uniform(-limit, limit, size=ksize).astype(np.float32), ctx)
         self.dW = torch.zeros_like(self.W)
         t = target_overflow_rate
-        self.W_range = ctx.quantizer(name + "/W_range", bits, weight_range, t)
+        self.W_range = ctx.quantizer(name + "/W_range", weight_bits, weight_range, t)
         self.X_range = ctx.quantizer(name + "/X_range", bits + 1, input_range, t)
         self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, t)
         if use_bias:
@@ -126,6 +127,11 @@ class Conv2d_q(Layer_q):
         self.wf = torch.zeros((Cout, self.ksf * 16), dtype=torch.int8, device=dev)
         self.wd = torch.zeros((Cin, self.ksd * 16), dtype=torch.int8, device=dev)
         self.wcolsum = torch.zeros(Cout, dtype=torch.int32, device=dev)
+        # W4 (weight_bits <= 4): the MFMA kernels read the packed images, two codes per byte
+        self.w4 = self.mfma and weight_bits <= 4
+        if self.w4:
+            self.wf4 = torch.zeros((Cout, self.ksf * 8), dtype=torch.uint8, device=dev)
+            self.wd4 = torch.zeros((Cin, self.ksd * 8), dtype=torch.uint8, device=dev)
         self._c = _Cache()
 
     def param_slots(self):
@@ -143,6 +149,9 @@ class Conv2d_q(Layer_q):
                             wf=self.wf if self.mfma else None, ksf=self.ksf,
                             wd=self.wd if self.mfma else None, ksd=self.ksd,
                             colsum=self.wcolsum if self.mfma else None)
+        if self.w4:
+            ops.pack_int4(self.wf, self.wf4)
+            ops.pack_int4(self.wd, self.wd4)
 
     def forward(self, X):
         self.X = X
@@ -153,7 +162,10 @@ class Conv2d_q(Layer_q):
                                                                                 X.device))
         self.quantize_weights()
         y = self._c.get("y", (N, d.Ho, d.Wo, Cout), torch.float32, X.device)
-        if self.x_mfma:
+        if self.x_mfma and self.w4:
+            ops.conv_fwd_i8w4(self.xq, self.x_kind == OUT_U8OFF, self.wf4, self.ksf, self.wcolsum, d,
+                              self.X_range.desc, self.W_range.desc, y)
+        elif self.x_mfma:
             ops.conv_fwd_i8(self.xq, self.x_kind == OUT_U8OFF, self.wf, self.ksf, self.wcolsum, d,
                             self.X_range.desc, self.W_range.desc, y=y)
         elif self.stem(d):
@@ -213,7 +225,9 @@ class Conv2d_q(Layer_q):
         if not self.need_input_grad:
             return None
         dx = self._c.get("dx", (d.N, d.H, d.W, Cin), torch.float32, dev)
-        if self.mfma:
+        if self.w4:
+            ops.conv_dgrad_i8w4(self.gradq, self.wd4, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
+        elif self.mfma:
             ops.conv_dgrad_i8(self.gradq, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
         else:
             ops.conv_dgrad_generic(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
@@ -238,17 +252,18 @@ class Dense_q(Layer_q):
 
     def __init__(self, name, bits, in_units, units, use_bias=True, weight_decay=0,
                  target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, grad_bits=None,
-                 ctx=None):
+                 weight_bits=None, ctx=None):
         self.ctx = ctx = ctx or default_context()
         self.name, self.bits, self.in_units, self.units = name, bits, in_units, units
         self.grad_bits = grad_bits = grad_bits or bits
+        self.weight_bits = weight_bits = weight_bits or bits
         self.use_bias, self.weight_decay, self.target_overflow_rate = use_bias, weight_decay, target_overflow_rate
         limit = (6 / (in_units + units)) ** 0.5
         self.W = _as_param(_rng(ctx, name + "/W").uniform(-limit, limit, size=(in_units, units)).astype(np.float32),
                            ctx)
         self.dW = torch.zeros_like(self.W)
         t = target_overflow_rate
-        self.W_range = ctx.quantizer(name + "/W_range", bits, weight_range, t)
+        self.W_range = ctx.quantizer(name + "/W_range", weight_bits, weight_range, t)
         self.X_range = ctx.quantizer(name + "/X_range", bits, input_range, t)
         self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, t)
         if use_bias:
@@ -590,12 +605,13 @@ class ResidualBlock_q(Layer_q):
     expansion = 1
 
     def __init__(self, name, bits, in_channels, channels, stride, training=True, batch_norm=True, weight_decay=0,
-                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, ctx=None):
+                 target_overflow_rate=0, input_range=2, weight_range=2, bias_range=2, grad_range=2, weight_bits=None,
+                 ctx=None):
         self.train = training
         self.name = name
         common = dict(bits=bits, use_bias=not batch_norm, weight_decay=weight_decay, input_range=input_range,
                       weight_range=weight_range, bias_range=bias_range, grad_range=grad_range,
-                      input_nonnegative=True, ctx=ctx)
+                      input_nonnegative=True, weight_bits=weight_bits, ctx=ctx)
         bn = dict(bits=bits, num_features=channels, training=training, weight_decay=weight_decay,
                   target_overflow_rate=target_overflow_rate, input_range=input_range, grad_range=grad_range, ctx=ctx)
         self.residual = Sequential_q(

@@ -156,6 +156,23 @@ def _conv_dgrad_i8(gq, wd, ksd, d, qg, qw, dx, add_src):
     call("lbt_conv_dgrad_i8", ptr(gq), ptr(wd), int(ksd), d, qg, qw, ptr(dx), ptr(add_src), stream())
 
 
+def pack_int4(src, dst):
+    """Two signed 4-bit codes per byte (the W4 weight images)."""
+    call("lbt_pack_int4", ptr(src), ptr(dst), src.numel(), stream())
+
+
+def conv_fwd_i8w4(xq, x_u8off, wf4, ksf, wcolsum, d, qx, qw, y):
+    M = d.N * d.Ho * d.Wo
+    with _Timed("conv_fwd_i8w4", xq.numel() + wf4.numel() + M * d.Cout * 4):
+        call("lbt_conv_fwd_i8w4", ptr(xq), int(x_u8off), ptr(wf4), int(ksf), ptr(wcolsum), d, qx, qw, ptr(y), None,
+             NO_Q, None, stream())
+
+
+def conv_dgrad_i8w4(gq, wd4, ksd, d, qg, qw, dx):
+    with _Timed("conv_dgrad_i8w4", gq.numel() + wd4.numel() + dx.numel() * 4):
+        call("lbt_conv_dgrad_i8w4", ptr(gq), ptr(wd4), int(ksd), d, qg, qw, ptr(dx), None, stream())
+
+
 def wgrad_nsplit(d, generic=False):
     P = d.N * d.Ho * d.Wo
     taps = d.KH * d.KW

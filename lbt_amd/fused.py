@@ -207,6 +207,23 @@ class FusedResNet:
                 self._nd[q] = d
                 njobs.append(NJob(ctx.step.data_ptr(), ctx.seed, q.qid, 0, inner, tab.data_ptr()))
 
+        # ---- 4-bit weights (config 5): every MFMA conv's int8 operand images live in ONE arena so a
+        # single lbt_pack_int4 launch packs them all (two codes per byte) after quantisation
+        w4 = [c for c in self.convs if c.mfma and c.w4]
+        if w4:
+            sizes = [(c.wf.numel(), c.wd.numel()) for c in w4]
+            total = sum(a + b for a, b in sizes)
+            self._w8 = torch.zeros(total, dtype=torch.int8, device=ctx.device)
+            self._w4 = torch.zeros(total // 2, dtype=torch.uint8, device=ctx.device)
+            off = 0
+            for c, (a, b) in zip(w4, sizes):
+                c.wf = self._w8[off:off + a].view(c.wf.shape)
+                c.wf4 = self._w4[off // 2:(off + a) // 2].view(c.wf4.shape)
+                off += a
+                c.wd = self._w8[off:off + b].view(c.wd.shape)
+                c.wd4 = self._w4[off // 2:(off + b) // 2].view(c.wd4.shape)
+                off += b
+
         # ---- batched weight + gamma/beta quantisation (all layers, one launch each)
         wjobs = []
         for c in self.convs:
@@ -222,6 +239,9 @@ class FusedResNet:
         self._wjobs = _dev_array(wjobs, ctx.device)
         max_cout = max(j.Cout for j in wjobs)
         fwd.append(L("lbt_dfxp_quantize_weights", ptr(self._wjobs), len(wjobs), max_cout))
+        if w4:
+            fwd.append(L("lbt_pack_int4", ptr(self._w8), ptr(self._w4), self._w8.numel(), k="pack_int4_kernel",
+                         nb=self._w8.numel() + self._w4.numel()))
         qjobs = []
         for r in self.rescales:
             C = r.C
@@ -389,6 +409,19 @@ class FusedResNet:
                         k="noise_fill_kernel", nb=4 * sum(j.n for j in njobs) + 8 * nz))
         self._fwd, self._bwd = fwd, bwd
 
+    # W4: the packed weight image and the *_w4 entry point of a conv's GEMM
+    @staticmethod
+    def _fn(c, name):
+        return name + "w4" if getattr(c, "w4", False) else name
+
+    @staticmethod
+    def _wf(c):
+        return ptr(c.wf4 if getattr(c, "w4", False) else c.wf)
+
+    @staticmethod
+    def _wd(c):
+        return ptr(c.wd4 if getattr(c, "w4", False) else c.wd)
+
     def _qd(self, q):
         """The plan's descriptor of quantiser q: with its noise table when it has one."""
         return self._nd.get(q, q.desc)
@@ -465,7 +498,7 @@ class FusedResNet:
         qn1 = self._buf(k + "qn1", shp, torch.int8)
         chs1 = self._sums(k + "chs1", ops.NSHARD * 2 * C)
         obs(b.n1.X_range, numel)
-        fwd.append(L("lbt_conv_fwd_i8", ptr(xa), 1, ptr(c1.wf), c1.ksf, ptr(c1.wcolsum), d1, self._qd(c1.X_range),
+        fwd.append(L(self._fn(c1, "lbt_conv_fwd_i8"), ptr(xa), 1, self._wf(c1), c1.ksf, ptr(c1.wcolsum), d1, self._qd(c1.X_range),
                      c1.W_range.desc, None, ptr(qn1), self._qd(b.n1.X_range), ptr(chs1), k="conv_gemm_kernel<0> (fwd)",
                      nb=xa.numel() + c1.wf.numel() + qn1.numel()))
         R1 = self._buf(k + "R1", shp, torch.int8)
@@ -478,7 +511,7 @@ class FusedResNet:
         qn2 = self._buf(k + "qn2", shp, torch.int8)
         chs2 = self._sums(k + "chs2", ops.NSHARD * 2 * C)
         obs(b.n2.X_range, numel)
-        fwd.append(L("lbt_conv_fwd_i8", ptr(xb), 1, ptr(c2.wf), c2.ksf, ptr(c2.wcolsum), d2, self._qd(c2.X_range),
+        fwd.append(L(self._fn(c2, "lbt_conv_fwd_i8"), ptr(xb), 1, self._wf(c2), c2.ksf, ptr(c2.wcolsum), d2, self._qd(c2.X_range),
                      c2.W_range.desc, None, ptr(qn2), self._qd(b.n2.X_range), ptr(chs2), k="conv_gemm_kernel<0> (fwd)",
                      nb=xb.numel() + c2.wf.numel() + qn2.numel()))
         ds = qns = chss = Rs = None
@@ -488,7 +521,7 @@ class FusedResNet:
             qns = self._buf(k + "qns", shp, torch.int8)
             chss = self._sums(k + "chss", ops.NSHARD * 2 * C)
             obs(b.ns.X_range, numel)
-            fwd.append(L("lbt_conv_fwd_i8", ptr(xs), 1, ptr(cs.wf), cs.ksf, ptr(cs.wcolsum), ds, self._qd(cs.X_range),
+            fwd.append(L(self._fn(cs, "lbt_conv_fwd_i8"), ptr(xs), 1, self._wf(cs), cs.ksf, ptr(cs.wcolsum), ds, self._qd(cs.X_range),
                          cs.W_range.desc, None, ptr(qns), self._qd(b.ns.X_range), ptr(chss), k="conv_gemm_kernel<0> (fwd)",
                          nb=xs.numel() + cs.wf.numel() + qns.numel()))
             Rs = self._buf(k + "Rs", shp, torch.int8)
@@ -575,12 +608,12 @@ class FusedResNet:
         nb_dg2 = gq2.numel() + c2.wd.numel()
         if fuse:
             aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
-            bwd.append(L("lbt_conv_dgrad_chain_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range),
+            bwd.append(L(self._fn(c2, "lbt_conv_dgrad_chain_i8"), ptr(gq2), self._wd(c2), c2.ksd, d2, self._qd(c2.grad_range),
                          c2.W_range.desc, None, ctypes.byref(aA1), k="conv_gemm_kernel<1> (dgrad+A)",
                          nb=ops._dgrad_chain_bytes(gq2.numel(), c2.wd.numel(), aA1, False)))
         else:
             d1g = self._buf(k + "d1", shp, torch.float32)
-            bwd.append(L("lbt_conv_dgrad_i8", ptr(gq2), ptr(c2.wd), c2.ksd, d2, self._qd(c2.grad_range),
+            bwd.append(L(self._fn(c2, "lbt_conv_dgrad_i8"), ptr(gq2), self._wd(c2), c2.ksd, d2, self._qd(c2.grad_range),
                          c2.W_range.desc, ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg2 + 4 * numel))
             aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
         keep.append(aA1)
@@ -599,7 +632,7 @@ class FusedResNet:
         add = gm
         if cs is not None:
             dsg = self._buf(k + "dsc", f["Xin"].shape, torch.float32)
-            bwd.append(L("lbt_conv_dgrad_i8", ptr(gqs), ptr(cs.wd), cs.ksd, ds, self._qd(cs.grad_range),
+            bwd.append(L(self._fn(cs, "lbt_conv_dgrad_i8"), ptr(gqs), self._wd(cs), cs.ksd, ds, self._qd(cs.grad_range),
                          cs.W_range.desc, ptr(dsg), None, k="conv_gemm_kernel<1> (dgrad)",
                          nb=gqs.numel() + cs.wd.numel() + 4 * dsg.numel()))
             add = dsg
@@ -608,12 +641,12 @@ class FusedResNet:
         nb_dg1 = gq1.numel() + c1.wd.numel() + 8 * nin
         gin = None
         if fuse:
-            bwd.append(L("lbt_conv_dgrad_chain_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range),
+            bwd.append(L(self._fn(c1, "lbt_conv_dgrad_chain_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1, self._qd(c1.grad_range),
                          c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]), k="conv_gemm_kernel<1> (dgrad+A)",
                          nb=ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], add is not None)))
         else:
             gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
-            bwd.append(L("lbt_conv_dgrad_i8", ptr(gq1), ptr(c1.wd), c1.ksd, d1, self._qd(c1.grad_range),
+            bwd.append(L(self._fn(c1, "lbt_conv_dgrad_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1, self._qd(c1.grad_range),
                          c1.W_range.desc, ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg1))
         sp1, ns1, slab1 = ops.wgrad_slab(self._c, k + "slab1", d1, self.ctx)
         bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), sp1, ns1,

@@ -159,9 +159,10 @@ class LayerQ:
 
 
 class Conv2dQ(LayerQ):
-    def __init__(self, name, bits, ksize, strides, padding, weight_decay=0.0, grad_bits=None):
+    def __init__(self, name, bits, ksize, strides, padding, weight_decay=0.0, grad_bits=None, weight_bits=None):
         self.name, self.bits, self.ksize = name, bits, tuple(ksize)
         self.grad_bits = grad_bits or bits
+        self.weight_bits = weight_bits or bits  # config 5: 4-bit weights
         self.strides = (strides[1], strides[2]) if len(strides) == 4 else tuple(strides)
         self.padding, self.wd = padding, weight_decay
         self.W = None
@@ -174,7 +175,7 @@ class Conv2dQ(LayerQ):
 
     def forward(self, X, ctx):
         self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits + 1)
-        self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.bits)
+        self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.weight_bits)
         self.in_shape = X.shape
         acc = conv_fwd_int(self.xq, self.wq, self.strides, self.padding)
         return scale_int(acc, self.ex + self.ew)
@@ -190,9 +191,10 @@ class Conv2dQ(LayerQ):
 
 
 class DenseQ(LayerQ):
-    def __init__(self, name, bits, in_units, units, weight_decay=0.0, grad_bits=None):
+    def __init__(self, name, bits, in_units, units, weight_decay=0.0, grad_bits=None, weight_bits=None):
         self.name, self.bits, self.in_units, self.units, self.wd = name, bits, in_units, units, weight_decay
         self.grad_bits = grad_bits or bits
+        self.weight_bits = weight_bits or bits
         self.W = None
 
     def range_names(self):
@@ -203,7 +205,7 @@ class DenseQ(LayerQ):
 
     def forward(self, X, ctx):
         self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits)
-        self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.bits)
+        self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.weight_bits)
         acc = np.rint(self.xq.astype(np.float64) @ self.wq.astype(np.float64)).astype(np.int64)
         return scale_int(acc, self.ex + self.ew)
 
@@ -342,19 +344,21 @@ class ReluQ(LayerQ):
 
 
 class ResidualBlockQ(LayerQ):
-    def __init__(self, name, bits, in_channels, channels, stride, weight_decay=0.0):
+    def __init__(self, name, bits, in_channels, channels, stride, weight_decay=0.0, weight_bits=None):
+        wb = dict(weight_bits=weight_bits)
         self.residual = SequentialQ(
-            Conv2dQ(name + "-1", bits, [3, 3, in_channels, channels], [1, stride, stride, 1], "SAME", weight_decay),
+            Conv2dQ(name + "-1", bits, [3, 3, in_channels, channels], [1, stride, stride, 1], "SAME", weight_decay,
+                    **wb),
             BatchNormQ(name + "-bn1", bits, channels, weight_decay),
             ReluQ(),
-            Conv2dQ(name + "-2", bits, [3, 3, channels, channels], [1, 1, 1, 1], "SAME", weight_decay),
+            Conv2dQ(name + "-2", bits, [3, 3, channels, channels], [1, 1, 1, 1], "SAME", weight_decay, **wb),
             BatchNormQ(name + "-bn2", bits, channels, weight_decay))
         if stride == 1 and in_channels == channels:
             self.shortcut = SequentialQ()
         else:
             self.shortcut = SequentialQ(
                 Conv2dQ(name + "-shortcut", bits, [1, 1, in_channels, channels], [1, stride, stride, 1], "SAME",
-                        weight_decay),
+                        weight_decay, **wb),
                 BatchNormQ(name + "-shortcut-bn", bits, channels, weight_decay))
         self.relu = ReluQ()
 

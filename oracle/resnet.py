@@ -14,17 +14,19 @@ from . import nn
 from .nn import F32
 
 
-def build_resnet(num_blocks=(3, 3, 3), bits=8, weight_decay=0.0):
-    layers = [nn.Conv2dQ("conv1", bits, [3, 3, 3, 16], [1, 1, 1, 1], "SAME", weight_decay),
+def build_resnet(num_blocks=(3, 3, 3), bits=8, weight_decay=0.0, weight_bits=None):
+    """weight_bits: the weight quantisers' width (config 5: 4)."""
+    wb = dict(weight_bits=weight_bits)
+    layers = [nn.Conv2dQ("conv1", bits, [3, 3, 3, 16], [1, 1, 1, 1], "SAME", weight_decay, **wb),
               nn.BatchNormQ("conv1-bn", bits, 16, weight_decay),
               nn.ReluQ()]
     in_ch = 16
     for channels, nb, stride in zip((16, 32, 64), num_blocks, (1, 2, 2)):
         for i in range(1, nb + 1):
             layers.append(nn.ResidualBlockQ("block%d-%d" % (channels, i), bits, in_ch, channels,
-                                            stride if i == 1 else 1, weight_decay))
+                                            stride if i == 1 else 1, weight_decay, **wb))
             in_ch = channels
-    layers += [nn.AvgPoolQ(), nn.FlattenQ(64), nn.DenseQ("softmax", bits, 64, 10, weight_decay)]
+    layers += [nn.AvgPoolQ(), nn.FlattenQ(64), nn.DenseQ("softmax", bits, 64, 10, weight_decay, **wb)]
     return nn.SequentialQ(*layers)
 
 
