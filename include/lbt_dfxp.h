@@ -145,6 +145,17 @@ int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t
  * acc * 2^-(eg+ew) (+ add_src[e] if add_src != NULL).  Requires Cin%16 == 0, Cout%16 == 0. */
 int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
                       lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
+/* Wide layers (ResNet-50 shapes): LDS-tiled int8-MFMA implicit GEMM, 128 x 128 workgroup tiles,
+ * k-blocks of one tap x 64 channels (gathered channels % 64 == 0, output channels % 16 == 0),
+ * same weight images and the same results bit for bit as the generic kernels.
+ * fwd a_kind: 0 int8 codes, 1 offset int8 (q - 128), 2 int16 codes (9..16-bit; split into two
+ * int8 MFMA passes, a = 256 hi + lo' + 128). dgrad g_i16: int16 gradient codes (config 4).
+ * colsum is unused (the kernel forms sum_k W itself) and may be NULL.                        */
+int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* wf, int32_t ksf, const int32_t* colsum,
+                       lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, void* stream);
+int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                         lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
+
 /* 4-bit weights (W 4-bit / A 8-bit): the same GEMMs with the weight
  * image packed two signed 4-bit codes per byte (lbt_pack_int4 of lbt_dfxp_quantize_weight's wf /
  * wd at qw.bits <= 4; ksf / ksd still count 16-element k-slices, 8 bytes each). gfx950 has no

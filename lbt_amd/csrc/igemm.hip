@@ -1,0 +1,247 @@
+// igemm.hip -- LDS-tiled int8 MFMA implicit GEMM for the wide layers (ResNet-50 shapes, SURVEY 8(f)
+// rank 1): channel counts that are multiples of 64 on the gathered side and of 16 on the output
+// side, any count (conv_mfma.hip's register-resident kernels take <= 128 channels).
+//
+//   fwd   : y[m = (n,oh,ow)][co] = sum_{tap,ci} x[n, oh*S+kh-P, ow*S+kw-P, ci] * W[tap][ci][co]
+//   dgrad : dx[m = (n,ih,iw)][ci] = sum_{tap,co} g[n, (ih+P-kh)/S, (iw+P-kw)/S, co] * W[tap][ci][co]
+//                                   (taps whose position is not an output pixel contribute 0)
+// B = the packed weight image of lbt_dfxp_quantize_weight ([col][k], k = (tap, 16-channel slice)).
+//
+// Workgroup tile 128 rows x 128 columns, 4 waves of 64 x 64 (4 x 4 v_mfma_i32_16x16x64_i8 tiles),
+// k-blocks of 64 = one tap x 64 channels; operands staged through double-buffered LDS: the next
+// k-block's global loads are in flight while the current one is multiplied.
+//
+// A16: the gathered operand is int16 codes (9..16-bit: the signed 9-bit image of a Conv2d_q input
+// or 16-bit gradient codes, config 4). Each code is split a = 256*hi + lo' + 128 with hi, lo' int8,
+// so sum a*w = 256 sum hi*w + sum lo'*w + 128 sum w: two int8 MFMA passes, plus one against an
+// all-ones A fragment for sum_k w per column; combined exactly in int64 in the epilogue. Positions
+// outside the image (a = 0) are (hi, lo') = (0, -128), which the identity keeps exact.
+// A8: int8 codes, either signed (fill 0) or offset-by-128 ("u8off", fill -128, + 128 sum_k w).
+#include "dfxp_device.h"
+
+namespace {
+
+using namespace lbt;
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int kT = 256, kBM = 128, kBN = 128, kBK = 64;
+constexpr int kRow = kBK + 16;  // LDS row stride in bytes (16-byte pad staggers the banks)
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+
+struct IgArgs {
+  const void* a;        // x codes (fwd) or g codes (dgrad), NHWC
+  const int8_t* b;      // packed weight image [ncol][ks * 16]
+  int ks;               // 16-byte slices per column
+  int cred;             // channels of the gathered operand (multiple of 64)
+  int a_u8off;          // A8 only: codes are q - 128
+  lbt_conv_desc d;
+  lbt_qdesc qa, qb;
+  const int32_t* colsum;  // A8 u8off: sum_k W per column (the wcolsum of the fwd image)
+  float* y;
+  const float* add_src;
+  int64_t M;
+  int ncol;
+};
+
+template <int MODE, bool A16>
+__global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
+  constexpr int NA = A16 ? 2 : 1;  // A tiles per k-block: (hi, lo') or one
+  __shared__ __attribute__((aligned(16))) int8_t sA[2][NA][kBM * kRow];
+  __shared__ __attribute__((aligned(16))) int8_t sB[2][kBN * kRow];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * kBM;
+  const int n0 = blockIdx.y * kBN;
+  const lbt_conv_desc& d = p.d;
+  const int OH = MODE == MODE_FWD ? d.Ho : d.H, OW = MODE == MODE_FWD ? d.Wo : d.W;
+  const int SH = MODE == MODE_FWD ? d.H : d.Ho, SW = MODE == MODE_FWD ? d.W : d.Wo;
+  const int cblocks = p.cred / kBK, nk = d.KH * d.KW * cblocks;
+
+  // ---- loader roles: A rows (t >> 2) and (t >> 2) + 64, 16-byte segment (t & 3) of the 64 channels
+  // (A16: 32-byte segments = 16 codes); B columns likewise
+  const int lr = t >> 2, seg = t & 3;
+  int an[2], ay[2], ax[2];
+  bool arow[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t m = m0 + lr + 64 * h;
+    arow[h] = m < p.M;
+    const uint32_t mu = (uint32_t)(arow[h] ? m : 0);
+    ax[h] = (int)(mu % (uint32_t)OW);
+    const uint32_t tt = mu / (uint32_t)OW;
+    ay[h] = (int)(tt % (uint32_t)OH);
+    an[h] = (int)(tt / (uint32_t)OH);
+  }
+  // global -> register stage of one k-block
+  v4i ra[2][A16 ? 2 : 1], rb[2];
+  bool rv[2];
+  auto load_k = [&](int kb) {
+    const int tap = kb / cblocks, cb = kb - tap * cblocks;
+    const int kh = tap / d.KW, kw = tap - kh * d.KW;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int sy, sx;
+      bool ok;
+      if (MODE == MODE_FWD) {
+        sy = ay[h] * d.SH + kh - d.PT;
+        sx = ax[h] * d.SW + kw - d.PL;
+        ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+      } else {
+        const int ny = ay[h] + d.PT - kh, nx = ax[h] + d.PL - kw;
+        sy = ny / d.SH;
+        sx = nx / d.SW;
+        ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
+      }
+      ok = ok && arow[h];
+      rv[h] = ok;
+      const int64_t pix = ok ? (((int64_t)an[h] * SH + sy) * SW + sx) : 0;
+      if constexpr (A16) {
+        const int16_t* src = reinterpret_cast<const int16_t*>(p.a) + pix * p.cred + cb * kBK + seg * 16;
+        ra[h][0] = *reinterpret_cast<const v4i*>(src);
+        ra[h][1] = *reinterpret_cast<const v4i*>(src + 8);
+      } else {
+        const int8_t* src = reinterpret_cast<const int8_t*>(p.a) + pix * p.cred + cb * kBK + seg * 16;
+        ra[h][0] = *reinterpret_cast<const v4i*>(src);
+      }
+      const int col = n0 + lr + 64 * h;
+      const int colc = col < p.ncol ? col : 0;
+      rb[h] = *reinterpret_cast<const v4i*>(p.b + ((int64_t)colc * p.ks + kb * 4 + seg) * 16);
+      if (col >= p.ncol) rb[h] = v4i{0, 0, 0, 0};
+    }
+  };
+  auto store_k = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = lr + 64 * h;
+      if constexpr (A16) {
+        // 16 codes -> 16 hi bytes and 16 lo' bytes (a = 256 hi + lo' + 128); outside: (0, -128)
+        int hi[4], lo[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const uint32_t c01 = (uint32_t)ra[h][w >> 1][(w & 1) * 2], c23 = (uint32_t)ra[h][w >> 1][(w & 1) * 2 + 1];
+          // codes (int16) e0 e1 | e2 e3; hi = arithmetic >> 8 (the high byte), lo' = low byte ^ 0x80
+          hi[w] = (int)__builtin_amdgcn_perm(c23, c01, 0x07050301u);
+          lo[w] = (int)(__builtin_amdgcn_perm(c23, c01, 0x06040200u) ^ 0x80808080u);
+          if (!rv[h]) { hi[w] = 0; lo[w] = (int)0x80808080u; }
+        }
+        *reinterpret_cast<v4i*>(&sA[buf][0][row * kRow + seg * 16]) = v4i{hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<v4i*>(&sA[buf][1][row * kRow + seg * 16]) = v4i{lo[0], lo[1], lo[2], lo[3]};
+      } else {
+        const int fill = p.a_u8off ? (int)0x80808080u : 0;
+        v4i v = ra[h][0];
+        if (!rv[h]) v = v4i{fill, fill, fill, fill};
+        *reinterpret_cast<v4i*>(&sA[buf][0][row * kRow + seg * 16]) = v;
+      }
+      *reinterpret_cast<v4i*>(&sB[buf][row * kRow + seg * 16]) = rb[h];
+    }
+  };
+
+  v4i acc[NA][4][4], accw[4];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[a][i][j] = v4i{0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) accw[j] = v4i{0, 0, 0, 0};
+  const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
+  const bool want_w = A16 || p.a_u8off;  // sum_k W per column (the +128 term)
+
+  load_k(0);
+  store_k(0);
+  __syncthreads();
+  const int r = lane & 15, q = lane >> 4;
+  for (int kb = 0; kb < nk; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nk) load_k(kb + 1);  // in flight during the MFMAs below
+    v4i bf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bf[j] = *reinterpret_cast<const v4i*>(&sB[cur][(wn * 64 + j * 16 + r) * kRow + q * 16]);
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const v4i af = *reinterpret_cast<const v4i*>(&sA[cur][a][(wm * 64 + i * 16 + r) * kRow + q * 16]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[a][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[a][i][j], 0, 0, 0);
+      }
+    if (want_w) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accw[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[j], accw[j], 0, 0, 0);
+    }
+    if (kb + 1 < nk) {
+      store_k(cur ^ 1);  // the other buffer: its readers finished before the last barrier
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns column (tile col + r), rows (tile row + 4q + e)
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + r;
+    if (col >= p.ncol) continue;
+    const long long wsum = want_w ? (long long)accw[j][0] : 0;  // every row of accw holds sum_k W[col][k]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = m0 + wm * 64 + i * 16 + q * 4 + e;
+        if (row >= p.M) continue;
+        long long s;
+        if constexpr (A16)
+          s = 256ll * (long long)acc[0][i][j][e] + (long long)acc[1][i][j][e] + 128ll * wsum;
+        else
+          s = (long long)acc[0][i][j][e] + (p.a_u8off ? 128ll * wsum : 0ll);
+        const float v = (float)s * scale;
+        const int64_t o = row * p.ncol + col;
+        p.y[o] = (MODE == MODE_DGRAD && p.add_src) ? v + p.add_src[o] : v;
+      }
+  }
+}
+
+template <int MODE, bool A16>
+int launch(const IgArgs& p, hipStream_t st) {
+  const int64_t mb = (p.M + kBM - 1) / kBM;
+  const int nb = (p.ncol + kBN - 1) / kBN;
+  if (mb > 0x7fffffff || nb > 65535) return LBT_EINVAL;
+  hipLaunchKernelGGL((igemm_kernel<MODE, A16>), dim3((unsigned)mb, (unsigned)nb), dim3(kT), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+bool desc_ok(const lbt_conv_desc& d) {
+  return d.N > 0 && d.H > 0 && d.W > 0 && d.KH > 0 && d.KW > 0 && d.SH > 0 && d.SW > 0 && d.Ho > 0 && d.Wo > 0 &&
+         d.Cin > 0 && d.Cout > 0;
+}
+
+}  // namespace
+
+// a_kind: 0 int8 signed, 1 int8 offset (q - 128; needs colsum = sum_k W per output channel), 2 int16
+extern "C" int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* wf, int32_t ksf,
+                                  const int32_t* colsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,
+                                  void* stream) {
+  if (!desc_ok(d) || d.Cin % kBK || d.Cout % 16 || !y || !wf) return LBT_EINVAL;
+  if (ksf * 16 < d.KH * d.KW * d.Cin) return LBT_EINVAL;
+  IgArgs p{};
+  p.a = xq; p.b = wf; p.ks = ksf; p.cred = d.Cin; p.a_u8off = a_kind == 1; p.d = d; p.qa = qx; p.qb = qw;
+  p.colsum = colsum; p.y = y; p.add_src = nullptr; p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
+  if (p.M * p.ncol >= ((int64_t)1 << 40)) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  return a_kind == 2 ? launch<MODE_FWD, true>(p, st) : launch<MODE_FWD, false>(p, st);
+}
+
+// g_i16: gradient codes are int16 (9..16-bit) instead of int8
+extern "C" int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                                    lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
+  if (!desc_ok(d) || d.Cout % kBK || d.Cin % 16 || !dx || !wd) return LBT_EINVAL;
+  if (ksd * 16 < d.KH * d.KW * d.Cout) return LBT_EINVAL;
+  IgArgs p{};
+  p.a = gq; p.b = wd; p.ks = ksd; p.cred = d.Cout; p.a_u8off = 0; p.d = d; p.qa = qg; p.qb = qw;
+  p.colsum = nullptr; p.y = dx; p.add_src = add_src; p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
+  hipStream_t st = (hipStream_t)stream;
+  return g_i16 ? launch<MODE_DGRAD, true>(p, st) : launch<MODE_DGRAD, false>(p, st);
+}

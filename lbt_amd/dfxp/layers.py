@@ -120,6 +120,10 @@ class Conv2d_q(Layer_q):
         else:
             self.x_kind = OUT_I16
         self.x_mfma = self.mfma and self.x_kind != OUT_I16
+        # wide layers (channels beyond the register-resident MFMA kernels, or 16-bit gradients):
+        # the LDS-tiled MFMA implicit GEMM for the forward and the input gradient
+        self.igemm_f = not self.x_mfma and ops.igemm_ok(Cin, Cout)
+        self.igemm_d = not self.mfma and ops.igemm_ok(Cout, Cin)
         self.ksf = ops.packed_slices(h, w, Cin)
         self.ksd = ops.packed_slices(h, w, Cout)
         dev = ctx.device
@@ -146,8 +150,8 @@ class Conv2d_q(Layer_q):
 
     def quantize_weights(self):
         ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio,
-                            wf=self.wf if self.mfma else None, ksf=self.ksf,
-                            wd=self.wd if self.mfma else None, ksd=self.ksd,
+                            wf=self.wf if (self.mfma or self.igemm_f) else None, ksf=self.ksf,
+                            wd=self.wd if (self.mfma or self.igemm_d) else None, ksd=self.ksd,
                             colsum=self.wcolsum if self.mfma else None)
         if self.w4:
             ops.pack_int4(self.wf, self.wf4)
@@ -170,6 +174,9 @@ class Conv2d_q(Layer_q):
                             self.X_range.desc, self.W_range.desc, y=y)
         elif self.stem(d):
             ops.conv_stem_fwd(self.xq, self.w_hwio, d, self.X_range.desc, self.W_range.desc, y=y)
+        elif self.igemm_f:
+            a_kind = 2 if self.x_kind == OUT_I16 else (1 if self.x_kind == OUT_U8OFF else 0)
+            ops.conv_fwd_igemm(self.xq, a_kind, self.wf, self.ksf, d, self.X_range.desc, self.W_range.desc, y)
         else:
             ops.conv_fwd_generic(self.xq, self.x_kind == OUT_I16, self.w_hwio, d, self.X_range.desc,
                                  self.W_range.desc, y)
@@ -194,7 +201,10 @@ class Conv2d_q(Layer_q):
         if not self.need_input_grad:
             return None
         dx = self._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, dev)
-        ops.conv_dgrad_generic16(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
+        if self.igemm_d:
+            ops.conv_dgrad_igemm(self.gradq, 1, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
+        else:
+            ops.conv_dgrad_generic16(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
         return dx
 
     def backward(self, grad, stochastic=True):
@@ -229,6 +239,8 @@ class Conv2d_q(Layer_q):
             ops.conv_dgrad_i8w4(self.gradq, self.wd4, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
         elif self.mfma:
             ops.conv_dgrad_i8(self.gradq, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
+        elif self.igemm_d:
+            ops.conv_dgrad_igemm(self.gradq, 0, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx)
         else:
             ops.conv_dgrad_generic(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
         return dx

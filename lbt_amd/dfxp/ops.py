@@ -420,3 +420,21 @@ def bn_bwd_a_wide(g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C)
 def bn_bwd_b_wide(G, qng, qn, qn_q, ms, sums, n, dx, rows, C):
     call("lbt_bn_bwd_b_wide", ptr(G), qng, ptr(qn), qn_q, ptr(ms), ptr(sums), int(n), ptr(dx), int(rows), int(C),
          stream())
+
+
+# ---------------------------------------------------------------- wide layers (igemm.hip)
+def igemm_ok(c_gather, c_out):
+    """Shapes the LDS-tiled MFMA implicit GEMM takes: gathered channels % 64, outputs % 16."""
+    return c_gather % 64 == 0 and c_out % 16 == 0
+
+
+def conv_fwd_igemm(xq, a_kind, wf, ksf, d, qx, qw, y):
+    M = d.N * d.Ho * d.Wo
+    with _Timed("igemm_kernel<fwd>", xq.numel() * xq.element_size() + wf.numel() + 4 * M * d.Cout):
+        call("lbt_conv_fwd_igemm", ptr(xq), int(a_kind), ptr(wf), int(ksf), None, d, qx, qw, ptr(y), stream())
+
+
+def conv_dgrad_igemm(gq, g_i16, wd, ksd, d, qg, qw, dx, add_src=None):
+    with _Timed("igemm_kernel<dgrad>", gq.numel() * gq.element_size() + wd.numel() + 4 * dx.numel()):
+        call("lbt_conv_dgrad_igemm", ptr(gq), int(g_i16), ptr(wd), int(ksd), d, qg, qw, ptr(dx), ptr(add_src),
+             stream())

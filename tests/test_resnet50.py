@@ -126,3 +126,52 @@ def test_resnet50_full_size_step():
     assert np.isfinite(loss.item())
     assert torch.isfinite(t.flat.g).all() and torch.isfinite(t.flat.w).all()
     assert int(ctx.step.item()) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,akind", [
+    (2, 14, 64, 128, 3, 1, 2), (2, 15, 128, 64, 3, 2, 2), (3, 7, 256, 160, 1, 1, 0), (2, 8, 64, 2048, 1, 2, 1),
+    (1, 9, 192, 48, 3, 2, 0)])
+def test_igemm_matches_generic(N, H, Cin, Cout, k, s, akind):
+    """The LDS-tiled MFMA implicit GEMM (fwd: int8 / offset int8 / int16 codes; dgrad: int8 and
+    int16 gradient codes) == the generic VALU kernels, bit for bit, incl. ragged tiles and stride 2."""
+    from lbt_amd import _lib
+    from lbt_amd.dfxp import ops
+    from lbt_amd.runtime import DfxpContext
+    rng = np.random.default_rng(N * H + Cin)
+    ctx = DfxpContext(seed=0)
+    qx, qw, qg = ctx.quantizer("t/X", 9, 2), ctx.quantizer("t/W", 8, 0), ctx.quantizer("t/g", 16, -3)
+    d = ops.conv_desc(N, H, H, Cin, Cout, k, k, s, s, "SAME")
+    W = torch.from_numpy(rng.uniform(-1, 1, size=(k, k, Cin, Cout)).astype(np.float32)).to(DEV)
+    w_hwio = torch.empty((k, k, Cin, Cout), dtype=torch.int8, device=DEV)
+    ksf, ksd = ops.packed_slices(k, k, Cin), ops.packed_slices(k, k, Cout)
+    wf = torch.zeros((Cout, ksf * 16), dtype=torch.int8, device=DEV)
+    wd = torch.zeros((Cin, ksd * 16), dtype=torch.int8, device=DEV)
+    ops.quantize_weight(W, qw, w_hwio=w_hwio, wf=wf, ksf=ksf, wd=wd, ksd=ksd)
+    # forward
+    if akind == 2:
+        x = torch.from_numpy(rng.integers(-256, 256, size=(N, H, H, Cin)).astype(np.int16)).to(DEV)
+    else:
+        x = torch.from_numpy(rng.integers(-128, 128, size=(N, H, H, Cin)).astype(np.int8)).to(DEV)
+    y1 = torch.empty((N, d.Ho, d.Wo, Cout), device=DEV)
+    y2 = torch.empty_like(y1)
+    ops.conv_fwd_igemm(x, akind, wf, ksf, d, qx.desc, qw.desc, y1)
+    if akind == 1:  # offset codes q - 128: the generic kernel takes the codes themselves (int16)
+        ops.conv_fwd_generic(x.to(torch.int16) + 128, True, w_hwio, d, qx.desc, qw.desc, y2)
+    else:
+        ops.conv_fwd_generic(x, akind == 2, w_hwio, d, qx.desc, qw.desc, y2)
+    assert torch.equal(y1, y2)
+    # input gradient, 8- and 16-bit codes (gathered side = Cout: multiples of 64 only)
+    for g_i16 in ((0, 1) if Cout % 64 == 0 else ()):
+        if g_i16:
+            g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, d.Ho, d.Wo, Cout)).astype(np.int16)).to(DEV)
+        else:
+            g = torch.from_numpy(rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout)).astype(np.int8)).to(DEV)
+        dx1 = torch.empty((N, H, H, Cin), device=DEV)
+        dx2 = torch.empty_like(dx1)
+        ops.conv_dgrad_igemm(g, g_i16, wd, ksd, d, qg.desc, qw.desc, dx1)
+        if g_i16:
+            ops.conv_dgrad_generic16(g, w_hwio, d, qg.desc, qw.desc, dx2)
+        else:
+            ops.conv_dgrad_generic(g, w_hwio, d, qg.desc, qw.desc, dx2)
+        assert torch.equal(dx1, dx2), g_i16
