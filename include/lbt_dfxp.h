@@ -155,6 +155,11 @@ int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* wf, int32_t
                        lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, void* stream);
 int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
                          lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream);
+/* Wide-layer weight gradient: x offset int8 codes (post-ReLU 9-bit, q - 128), g int8 or int16
+ * (g_i16) codes; Cin, Cout % 64 == 0; adds exact int64 partials into a ZEROED slab
+ * [nshard][KH*KW*Cin][Cout] (pixel split b -> shard b % nshard; reduce: lbt_conv_wgrad_reduce64). */
+int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
+                         int32_t nsplit, int32_t nshard, void* stream);
 
 /* 4-bit weights (W 4-bit / A 8-bit): the same GEMMs with the weight
  * image packed two signed 4-bit codes per byte (lbt_pack_int4 of lbt_dfxp_quantize_weight's wf /

@@ -130,6 +130,7 @@ _SIGS = {
     "lbt_pack_int4": [_P, _P, c_int64, _P],
     "lbt_conv_fwd_igemm": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_conv_dgrad_igemm": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
+    "lbt_conv_wgrad_igemm": [_P, _P, c_int32, ConvDesc, _P, c_int32, c_int32, _P],
     "lbt_conv_dgrad_chain_i8w4": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_dgrad_chain_i8": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_i8": [_P, c_int32, _P, ConvDesc, _P, c_int32, c_int32, _P],

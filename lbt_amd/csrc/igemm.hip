@@ -18,12 +18,11 @@
 // outside the image (a = 0) are (hi, lo') = (0, -128), which the identity keeps exact.
 // A8: int8 codes, either signed (fill 0) or offset-by-128 ("u8off", fill -128, + 128 sum_k w).
 #include "dfxp_device.h"
+#include "lds_tr.h"
 
 namespace {
 
 using namespace lbt;
-
-typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kT = 256, kBM = 128, kBN = 128, kBK = 64;
 constexpr int kRow = kBK + 16;  // LDS row stride in bytes (16-byte pad staggers the banks)
@@ -244,4 +243,176 @@ extern "C" int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t*
   p.colsum = nullptr; p.y = dx; p.add_src = add_src; p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
   hipStream_t st = (hipStream_t)stream;
   return g_i16 ? launch<MODE_DGRAD, true>(p, st) : launch<MODE_DGRAD, false>(p, st);
+}
+
+namespace {
+
+// ----------------------------------------------------------------------------- wide wgrad
+// dW[tap][ci][co] = sum_p x[p shifted by tap][ci] * g[p][co] for the wide layers. x is offset int8
+// (x' = x - 128, post-ReLU 9-bit codes 0..255); g is int8 or int16 (G16: g = 256 gh + gl' + 128).
+// Per workgroup: one tap, 64 ci x 64 co, a pixel range; each wave walks 64-pixel chunks, stores
+// [pixel][16 B] LDS images and multiplies ds_read_b64_tr_b8 fragments (as conv_mfma.hip's wgrad).
+// Exact identity (over every processed lane, invalid ones carrying x' = -128, g = 0):
+//   sum x g = 256 sum x' gh + sum x' gl' + 128 sum x' + 128 (256 sum gh + sum gl' + 128 npix)
+// (G8: sum x g = sum x' g + 128 sum g); the row / column sums come from MFMAs against ones.
+// The 4 waves meet in LDS (int64), then one int64 atomic per output into shard (split % nshard).
+
+constexpr int kWP = 64;
+
+template <bool G16>
+__global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
+                                                        lbt_conv_desc d, long long* __restrict__ slab, int64_t P,
+                                                        int nsplit, int nshard) {
+  constexpr int NG = G16 ? 2 : 1;  // G images: (gh, gl') or g
+  // per wave: X [4 slices][64 px][16 B], G [NG][4 slices][64 px][16 B]; reused as the int64 tile
+  __shared__ __attribute__((aligned(16))) int8_t lds[4][(4 + 4 * NG) * kWP * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int cib = d.Cin / 64;
+  const int tap = blockIdx.y / cib, cb = blockIdx.y - tap * cib, ob = blockIdx.z;
+  const int kh = tap / d.KW, kw = tap - kh * d.KW;
+  int8_t* Xi = lds[wave];
+  int8_t* Gi = lds[wave] + 4 * kWP * 16;
+  const int64_t per = (P + nsplit - 1) / nsplit;
+  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p1 = p0 + per < P ? p0 + per : P;
+  const uint32_t HWo = (uint32_t)d.Ho * d.Wo;
+  v4i acc[NG][4][4], ax[4], ag[NG][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    ax[a] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int h = 0; h < NG; ++h) acc[h][a][b] = v4i{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int h = 0; h < NG; ++h)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) ag[h][b] = v4i{0, 0, 0, 0};
+  const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
+  long long nchunks = 0;
+  for (int64_t c0 = p0 + (int64_t)wave * kWP; c0 < p1; c0 += 4 * kWP) {
+    ++nchunks;
+    const int64_t p = c0 + lane;
+    const bool pv = p < p1;
+    const uint32_t pu = (uint32_t)(pv ? p : p0);
+    const uint32_t n = pu / HWo, rem = pu - n * HWo;
+    const int oh = (int)(rem / (uint32_t)d.Wo), ow = (int)(rem - (uint32_t)oh * (uint32_t)d.Wo);
+    const int ih = oh * d.SH + kh - d.PT, iw = ow * d.SW + kw - d.PL;
+    const bool xv = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+    const int8_t* xp = xq + (xv ? ((((int64_t)n * d.H + ih) * d.W + iw) * d.Cin + cb * 64) : 0);
+    v4i xs[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xs[s] = *reinterpret_cast<const v4i*>(xp + s * 16);
+    v4i gs[G16 ? 8 : 4];
+    if constexpr (G16) {
+      const int16_t* gp = reinterpret_cast<const int16_t*>(gq) + (int64_t)pu * d.Cout + ob * 64;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) gs[s] = *reinterpret_cast<const v4i*>(gp + s * 8);
+    } else {
+      const int8_t* gp = reinterpret_cast<const int8_t*>(gq) + (int64_t)pu * d.Cout + ob * 64;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) gs[s] = *reinterpret_cast<const v4i*>(gp + s * 16);
+    }
+    const int fx = (int)0x80808080u;  // x' = -128: x = 0 (padding, pixels past the range)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (!xv) xs[s] = v4i{fx, fx, fx, fx};
+      *reinterpret_cast<v4i*>(Xi + (s * kWP + lane) * 16) = xs[s];
+    }
+    if constexpr (G16) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {  // 16 codes -> 16 gh bytes, 16 gl' bytes; past the range g = 0
+        int hi[4], lo[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const uint32_t c01 = (uint32_t)gs[2 * s + (w >> 1)][(w & 1) * 2];
+          const uint32_t c23 = (uint32_t)gs[2 * s + (w >> 1)][(w & 1) * 2 + 1];
+          hi[w] = pv ? (int)__builtin_amdgcn_perm(c23, c01, 0x07050301u) : 0;
+          lo[w] = pv ? (int)(__builtin_amdgcn_perm(c23, c01, 0x06040200u) ^ 0x80808080u) : (int)0x80808080u;
+        }
+        *reinterpret_cast<v4i*>(Gi + (s * kWP + lane) * 16) = v4i{hi[0], hi[1], hi[2], hi[3]};
+        *reinterpret_cast<v4i*>(Gi + ((4 + s) * kWP + lane) * 16) = v4i{lo[0], lo[1], lo[2], lo[3]};
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (!pv) gs[s] = v4i{0, 0, 0, 0};
+        *reinterpret_cast<v4i*>(Gi + (s * kWP + lane) * 16) = gs[s];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    v4i gf[NG][4];
+#pragma unroll
+    for (int h = 0; h < NG; ++h)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        gf[h][b] = tr_frag(Gi + (h * 4 + b) * kWP * 16, 16 * q, lane);
+        ag[h][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, gf[h][b], ag[h][b], 0, 0, 0);
+      }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const v4i xf = tr_frag(Xi + a * kWP * 16, 16 * q, lane);
+      ax[a] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf, ones, ax[a], 0, 0, 0);
+#pragma unroll
+      for (int h = 0; h < NG; ++h)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[h][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf, gf[h][b], acc[h][a][b], 0, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  // ---- combine exactly, meet the other waves in LDS (int64 [64 ci][64 co]), one atomic per output
+  __syncthreads();
+  unsigned long long* tile = reinterpret_cast<unsigned long long*>(&lds[0][0]);
+  for (int i = threadIdx.x; i < 64 * 64; i += kT) tile[i] = 0ull;
+  __syncthreads();
+  const long long npix = nchunks * kWP;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        long long v;
+        if constexpr (G16) {
+          const long long sg = 256ll * ag[0][b][i] + (long long)ag[1][b][i] + 128ll * npix;  // sum_p g[co]
+          v = 256ll * acc[0][a][b][i] + (long long)acc[1][a][b][i] + 128ll * ax[a][i] + 128ll * sg;
+        } else {
+          v = (long long)acc[0][a][b][i] + 128ll * ag[0][b][i];
+        }
+        if (v) atomicAdd(&tile[(a * 16 + q * 4 + i) * 64 + b * 16 + r], (unsigned long long)v);
+      }
+  __syncthreads();
+  long long* dst = slab + ((int64_t)(blockIdx.x % nshard) * (d.KH * d.KW) + tap) * d.Cin * d.Cout;
+  for (int i = threadIdx.x; i < 64 * 64; i += kT) {
+    const long long v = (long long)tile[i];
+    const int ci = cb * 64 + (i >> 6), co = ob * 64 + (i & 63);
+    if (v) atomicAdd((unsigned long long*)&dst[(int64_t)ci * d.Cout + co], (unsigned long long)v);
+  }
+}
+
+}  // namespace
+
+// wide wgrad: x offset int8 codes (q - 128), g int8 (g_i16 = 0) or int16 codes; adds into a
+// ZEROED int64 slab [nshard][KH*KW*Cin][Cout] (reduce with lbt_conv_wgrad_reduce64 over nshard).
+extern "C" int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
+                                    int32_t nsplit, int32_t nshard, void* stream) {
+  if (!desc_ok(d) || d.Cin % 64 || d.Cout % 64 || nsplit <= 0 || nshard <= 0 || nshard > nsplit) return LBT_EINVAL;
+  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
+  if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
+  if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
+  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
+  hipStream_t st = (hipStream_t)stream;
+  if (g_i16)
+    hipLaunchKernelGGL(wgrad_wide_kernel<true>, grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit, nshard);
+  else
+    hipLaunchKernelGGL(wgrad_wide_kernel<false>, grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
+                       nshard);
+  return (int)hipGetLastError();
 }

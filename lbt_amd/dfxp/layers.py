@@ -113,15 +113,18 @@ class Conv2d_q(Layer_q):
         if grad_bits > 8 and use_bias:
             raise NotImplementedError("bias with > 8-bit gradient codes")
         # x codes: unsigned 9-bit (offset int8, MFMA) / signed <= 8 bit (int8, MFMA) / int16 (VALU)
+        # wide layers (channels beyond the register-resident MFMA kernels, or 16-bit gradients):
+        # LDS-tiled MFMA implicit GEMMs (igemm.hip) -- the weight gradient too when the input is a
+        # post-ReLU 9-bit code (offset int8) and both channel counts are multiples of 64
+        self.igemm_w = (not self.mfma and input_nonnegative and bits + 1 == 9 and Cin % 64 == 0
+                        and Cout % 64 == 0)
         if bits + 1 <= 8:
             self.x_kind = OUT_I8
-        elif bits + 1 == 9 and input_nonnegative and self.mfma:
+        elif bits + 1 == 9 and input_nonnegative and (self.mfma or self.igemm_w):
             self.x_kind = OUT_U8OFF  # offset codes are undone by the MFMA kernels only
         else:
             self.x_kind = OUT_I16
         self.x_mfma = self.mfma and self.x_kind != OUT_I16
-        # wide layers (channels beyond the register-resident MFMA kernels, or 16-bit gradients):
-        # the LDS-tiled MFMA implicit GEMM for the forward and the input gradient
         self.igemm_f = not self.x_mfma and ops.igemm_ok(Cin, Cout)
         self.igemm_d = not self.mfma and ops.igemm_ok(Cout, Cin)
         self.ksf = ops.packed_slices(h, w, Cin)
@@ -193,11 +196,14 @@ class Conv2d_q(Layer_q):
         dev = grad.device
         K = d.KH * d.KW * d.Cin
         self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16, dev))
-        ns = ops.wgrad_nsplit(d, generic=True)
-        slab = self._c.get("slab64", (ns, K, d.Cout), torch.int64, dev)
-        ops.conv_wgrad_generic16(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
-        ops.conv_wgrad_reduce64(slab, ns, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
-                                ops.f32(2 * self.weight_decay), self.dW)
+        if self.igemm_w:
+            self._wgrad_igemm(1)
+        else:
+            ns = ops.wgrad_nsplit(d, generic=True)
+            slab = self._c.get("slab64", (ns, K, d.Cout), torch.int64, dev)
+            ops.conv_wgrad_generic16(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
+            ops.conv_wgrad_reduce64(slab, ns, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
+                                    ops.f32(2 * self.weight_decay), self.dW)
         if not self.need_input_grad:
             return None
         dx = self._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, dev)
@@ -206,6 +212,16 @@ class Conv2d_q(Layer_q):
         else:
             ops.conv_dgrad_generic16(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
         return dx
+
+    def _wgrad_igemm(self, g_i16):
+        """Weight gradient on the wide-layer MFMA kernel (int64 slab, one shard) + its reduce."""
+        d = self.d
+        K = d.KH * d.KW * d.Cin
+        slab = self._c.get("wslab64", (1, K, d.Cout), torch.int64, self.ctx.device)
+        slab.zero_()
+        ops.conv_wgrad_igemm(self.xq, self.gradq, g_i16, d, slab, ops.wgrad_igemm_nsplit(d), 1)
+        ops.conv_wgrad_reduce64(slab, 1, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
+                                ops.f32(2 * self.weight_decay), self.dW)
 
     def backward(self, grad, stochastic=True):
         if self.grad_bits > 8:
@@ -218,7 +234,10 @@ class Conv2d_q(Layer_q):
                                   chsum=gsum, C=Cout)
         wd2 = ops.f32(2 * self.weight_decay)
         K = d.KH * d.KW * Cin
-        if self.x_mfma:
+        if self.igemm_w:
+            self._wgrad_igemm(0)
+            slab = None
+        elif self.x_mfma:
             nsplit, ns, slab = ops.wgrad_slab(self._c, "wslab", d, self.ctx)
             ops.conv_wgrad_i8(self.xq, self.x_kind == OUT_U8OFF, self.gradq, d, slab, nsplit, ns)
         elif self.stem(d):
@@ -228,8 +247,9 @@ class Conv2d_q(Layer_q):
             ns = ops.wgrad_nsplit(d, generic=True)
             slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
             ops.conv_wgrad_generic(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
-        ops.conv_wgrad_reduce(slab, ns, K, Cout, self.x_kind == OUT_U8OFF, gsum, self.X_range.desc,
-                              self.grad_range.desc, self.W, wd2, self.dW)
+        if slab is not None:
+            ops.conv_wgrad_reduce(slab, ns, K, Cout, self.x_kind == OUT_U8OFF, gsum, self.X_range.desc,
+                                  self.grad_range.desc, self.W, wd2, self.dW)
         if self.use_bias:
             ops.bias_grad(gsum, Cout, self.grad_range.desc, self.db)
         if not self.need_input_grad:

@@ -438,3 +438,16 @@ def conv_dgrad_igemm(gq, g_i16, wd, ksd, d, qg, qw, dx, add_src=None):
     with _Timed("igemm_kernel<dgrad>", gq.numel() * gq.element_size() + wd.numel() + 4 * dx.numel()):
         call("lbt_conv_dgrad_igemm", ptr(gq), int(g_i16), ptr(wd), int(ksd), d, qg, qw, ptr(dx), ptr(add_src),
              stream())
+
+
+def wgrad_igemm_nsplit(d):
+    """Pixel splits of the wide wgrad: ~1024 workgroups, int32 MFMA sums exact (<= 2^17 pixels a wave)."""
+    P = d.N * d.Ho * d.Wo
+    tiles = d.KH * d.KW * (d.Cin // 64) * (d.Cout // 64)
+    lo = -(-P // (4 * 131072))
+    return max(lo, min(max(1, P // 256), -(-1024 // tiles)))
+
+
+def conv_wgrad_igemm(xq, gq, g_i16, d, slab, nsplit, nshard):
+    with _Timed("wgrad_wide_kernel", xq.numel() + gq.numel() * gq.element_size() + 8 * slab.numel()):
+        call("lbt_conv_wgrad_igemm", ptr(xq), ptr(gq), int(g_i16), d, ptr(slab), int(nsplit), int(nshard), stream())

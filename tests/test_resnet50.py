@@ -175,3 +175,35 @@ def test_igemm_matches_generic(N, H, Cin, Cout, k, s, akind):
         else:
             ops.conv_dgrad_generic(g, w_hwio, d, qg.desc, qw.desc, dx2)
         assert torch.equal(dx1, dx2), g_i16
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s", [(2, 14, 64, 64, 3, 1), (2, 15, 128, 64, 3, 2), (3, 7, 64, 192, 1, 1),
+                                              (1, 16, 64, 128, 1, 2)])
+def test_wgrad_igemm_matches_generic(N, H, Cin, Cout, k, s):
+    """Wide-layer MFMA weight gradient (offset int8 x; int8 and int16 g) == the generic kernels'
+    exact integer sums."""
+    from lbt_amd.dfxp import ops
+    rng = np.random.default_rng(N + H + Cin + Cout)
+    d = ops.conv_desc(N, H, H, Cin, Cout, k, k, s, s, "SAME")
+    K = k * k * Cin
+    x = rng.integers(0, 256, size=(N, H, H, Cin))
+    x_off = torch.from_numpy((x - 128).astype(np.int8)).to(DEV)
+    x16 = torch.from_numpy(x.astype(np.int16)).to(DEV)
+    for g_i16 in (0, 1):
+        if g_i16:
+            g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, d.Ho, d.Wo, Cout)).astype(np.int16)).to(DEV)
+        else:
+            g = torch.from_numpy(rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout)).astype(np.int8)).to(DEV)
+        nsplit = ops.wgrad_igemm_nsplit(d)
+        slab = torch.zeros((2, K, Cout), dtype=torch.int64, device=DEV)
+        ops.conv_wgrad_igemm(x_off, g, g_i16, d, slab, nsplit, min(2, nsplit))
+        got = slab.sum(0)
+        ns = ops.wgrad_nsplit(d, generic=True)
+        if g_i16:
+            ref = torch.zeros((ns, K, Cout), dtype=torch.int64, device=DEV)
+            ops.conv_wgrad_generic16(x16, True, g, d, ref, ns)
+        else:
+            ref = torch.zeros((ns, K, Cout), dtype=torch.int32, device=DEV)
+            ops.conv_wgrad_generic(x16, True, g, d, ref, ns)
+        assert torch.equal(got, ref.to(torch.int64).sum(0)), g_i16
