@@ -29,58 +29,83 @@ struct WideA {
   int C, rpb;            // rows per workgroup
 };
 
+// Thread = 4 consecutive channels (one Philox4x32 call covers their 4 noise values) x one row lane.
+constexpr int kCQ = 16;        // channel quads per workgroup (64 channels)
+constexpr int kRL4 = kT / kCQ; // 16 row lanes
+
 __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
-  __shared__ long long red[kRL][4][kCB];
+  __shared__ long long red[kRL4][4][kCB];
   __shared__ int sh_cnt[2 * 2 * (kT / 64)];
-  const int cl = threadIdx.x & (kCB - 1), rl = threadIdx.x / kCB;
-  const int c = blockIdx.x * kCB + cl;
-  const bool cv = c < a.C;
+  const int cq = threadIdx.x % kCQ, rl = threadIdx.x / kCQ;
+  const int c0 = blockIdx.x * kCB + 4 * cq;
+  const bool cv = c0 < a.C;  // C % 4 == 0: the quad is whole
   const QState srg = qstate(a.qrg), sng = qstate(a.qng);
   const int64_t r0 = (int64_t)blockIdx.y * a.rpb;
   const int64_t r1 = r0 + a.rpb < a.rows ? r0 + a.rpb : a.rows;
-  const float gam = (cv && a.gamma_q) ? a.gamma_q[c] : 0.f;
-  long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  float gam[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) gam[k] = (cv && a.gamma_q) ? a.gamma_q[c0 + k] : 0.f;
+  long long s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0};
   int o1 = 0, o2 = 0, p1 = 0, p2 = 0;
   if (cv) {
-    for (int64_t r = r0 + rl; r < r1; r += kRL) {
-      const int64_t e = r * a.C + c;
-      const uint64_t ni = (uint64_t)(e % a.inner);
-      float d = a.g[e];
+    for (int64_t r = r0 + rl; r < r1; r += kRL4) {
+      const int64_t e = r * a.C + c0;
+      const uint64_t blk = (uint64_t)(e % a.inner) >> 2;  // inner % 4 == 0
+      const float4 gv = *reinterpret_cast<const float4*>(a.g + e);
+      float d[4] = {gv.x, gv.y, gv.z, gv.w};
       if (srg.active) {
-        const float u = a.qrg.stochastic ? qnoise1(a.qrg, srg.step, ni) : 0.f;
-        const int G2 = quant1(srg, a.qrg.stochastic, d, u, o1, o2);
-        s0 += (long long)G2 * a.R[e];
-        s1 += G2;
-        const float gh = (float)G2 * srg.inv_m;
-        d = gh * gam;
+        const Noise4 nz = a.qrg.stochastic ? qnoise4(a.qrg, srg.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+        const char4 rv = *reinterpret_cast<const char4*>(a.R + e);
+        const int R[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int G2 = quant1(srg, a.qrg.stochastic, d[k], nz.u[k], o1, o2);
+          s0[k] += (long long)G2 * R[k];
+          s1[k] += G2;
+          const float gh = (float)G2 * srg.inv_m;
+          d[k] = gh * gam[k];
+        }
       }
       if (sng.active) {
-        const float u = a.qng.stochastic ? qnoise1(a.qng, sng.step, ni) : 0.f;
-        const int G = quant1(sng, a.qng.stochastic, d, u, p1, p2);
-        s2 += G;
-        s3 += (long long)G * a.qn[e];
-        a.gout[e] = (int16_t)G;
+        const Noise4 nz = a.qng.stochastic ? qnoise4(a.qng, sng.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+        const char4 qv = *reinterpret_cast<const char4*>(a.qn + e);
+        const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
+        int G[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          G[k] = quant1(sng, a.qng.stochastic, d[k], nz.u[k], p1, p2);
+          s2[k] += G[k];
+          s3[k] += (long long)G[k] * qn[k];
+        }
+        short4 o;
+        o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
+        *reinterpret_cast<short4*>(a.gout + e) = o;
       } else if (a.dout) {
-        a.dout[e] = d;
+        *reinterpret_cast<float4*>(a.dout + e) = make_float4(d[0], d[1], d[2], d[3]);
       }
     }
   }
-  red[rl][0][cl] = s0;
-  red[rl][1][cl] = s1;
-  red[rl][2][cl] = s2;
-  red[rl][3][cl] = s3;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[rl][0][4 * cq + k] = s0[k];
+    red[rl][1][4 * cq + k] = s1[k];
+    red[rl][2][4 * cq + k] = s2[k];
+    red[rl][3][4 * cq + k] = s3[k];
+  }
   // per-thread counters -> wave totals -> LDS (one barrier publishes counters and sums)
   counts_stage(0, 2, o1, o2, sh_cnt);
   counts_stage(1, 2, p1, p2, sh_cnt);
   __syncthreads();
   if (srg.active) counts_publish(0, 2, a.qrg, sh_cnt);
   if (sng.active) counts_publish(1, 2, a.qng, sh_cnt);
-  if (a.sums && threadIdx.x < kCB && cv) {
+  if (a.sums) {
     int64_t* dst = a.sums + (int64_t)(blockIdx.y % LBT_NSHARD) * 4 * a.C;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const long long v = red[0][s][cl] + red[1][s][cl] + red[2][s][cl] + red[3][s][cl];
-      if (v) atomicAdd((unsigned long long*)&dst[s * a.C + c], (unsigned long long)v);
+    for (int i = threadIdx.x; i < 4 * kCB; i += kT) {
+      const int sidx = i / kCB, cl = i - sidx * kCB, c = blockIdx.x * kCB + cl;
+      if (c >= a.C) continue;
+      long long v = 0;
+      for (int l = 0; l < kRL4; ++l) v += red[l][sidx][cl];
+      if (v) atomicAdd((unsigned long long*)&dst[sidx * a.C + c], (unsigned long long)v);
     }
   }
 }
@@ -100,11 +125,12 @@ struct WideB {
 
 __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
   __shared__ float s_mg[kCB], s_mgx[kCB];
-  const int cl = threadIdx.x & (kCB - 1), rl = threadIdx.x / kCB;
-  const int c = blockIdx.x * kCB + cl;
-  const bool cv = c < b.C;
+  const int cq = threadIdx.x % kCQ, rl = threadIdx.x / kCQ;
+  const int c0 = blockIdx.x * kCB + 4 * cq;
   const QState sgq = qstate(b.qng), sn = qstate(b.qn_q);
-  if (rl == 0 && cv) {  // bn.hip chain_bwd_b's moment prologue, for this workgroup's channels
+  if (threadIdx.x < kCB && blockIdx.x * kCB + (int)threadIdx.x < b.C) {
+    // bn.hip chain_bwd_b's moment prologue, for this workgroup's channels
+    const int c = blockIdx.x * kCB + threadIdx.x;
     long long SG = 0, SGQ = 0;
     for (int k = 0; k < LBT_NSHARD; ++k) {
       SG += b.sums[(int64_t)k * 4 * b.C + 2 * b.C + c];
@@ -112,23 +138,38 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
     }
     const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, n = (double)b.n;
     const float m = b.ms[c], sig = b.ms[b.C + c];
-    s_mg[cl] = (float)(gsc * (double)SG / n);
-    s_mgx[cl] = (float)(gsc * (s * (double)SGQ - (double)m * (double)SG) / (n * (double)sig));
+    s_mg[threadIdx.x] = (float)(gsc * (double)SG / n);
+    s_mgx[threadIdx.x] = (float)(gsc * (s * (double)SGQ - (double)m * (double)SG) / (n * (double)sig));
   }
   __syncthreads();
-  if (!cv) return;
-  const float mu = b.ms[c], sig = b.ms[b.C + c], mg = s_mg[cl], mgx = s_mgx[cl];
+  if (c0 >= b.C) return;
+  float mu[4], sig[4], mg[4], mgx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    mu[k] = b.ms[c0 + k];
+    sig[k] = b.ms[b.C + c0 + k];
+    mg[k] = s_mg[4 * cq + k];
+    mgx[k] = s_mgx[4 * cq + k];
+  }
   const int64_t r0 = (int64_t)blockIdx.y * b.rpb;
   const int64_t r1 = r0 + b.rpb < b.rows ? r0 + b.rpb : b.rows;
-  for (int64_t r = r0 + rl; r < r1; r += kRL) {
-    const int64_t e = r * b.C + c;
-    const float x1 = (float)b.qn[e] * sn.inv_m;
-    const float x2 = x1 - mu;
-    const float xh = x2 / sig;
-    const float gh = (float)b.G[e] * sgq.inv_m;
-    const float t1 = gh - mg;
-    const float t2 = xh * mgx;
-    b.dx[e] = (t1 - t2) / sig;
+  for (int64_t r = r0 + rl; r < r1; r += kRL4) {
+    const int64_t e = r * b.C + c0;
+    const char4 qv = *reinterpret_cast<const char4*>(b.qn + e);
+    const short4 gv = *reinterpret_cast<const short4*>(b.G + e);
+    const int q[4] = {qv.x, qv.y, qv.z, qv.w}, G[4] = {gv.x, gv.y, gv.z, gv.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x1 = (float)q[k] * sn.inv_m;
+      const float x2 = x1 - mu[k];
+      const float xh = x2 / sig[k];
+      const float gh = (float)G[k] * sgq.inv_m;
+      const float t1 = gh - mg[k];
+      const float t2 = xh * mgx[k];
+      o[k] = (t1 - t2) / sig[k];
+    }
+    *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -137,7 +178,7 @@ int rows_per_block(int64_t rows, int cblocks) {
   int64_t splits = 512 / (cblocks > 0 ? cblocks : 1);
   if (splits < 1) splits = 1;
   int64_t rpb = (rows + splits - 1) / splits;
-  if (rpb < kRL) rpb = kRL;
+  if (rpb < kRL4) rpb = kRL4;
   return (int)rpb;
 }
 
@@ -146,7 +187,7 @@ int rows_per_block(int64_t rows, int cblocks) {
 extern "C" int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R, const float* gamma_q, lbt_qdesc qng,
                                  const int8_t* qn, int16_t* gout, float* dout, int64_t* sums, int64_t rows,
                                  int64_t inner, int32_t C, void* stream) {
-  if (rows <= 0 || C <= 0 || inner <= 0 || inner % C) return LBT_EINVAL;
+  if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gamma_q)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
   WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0};
   const int cb = (C + kCB - 1) / kCB;
@@ -159,7 +200,7 @@ extern "C" int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R,
 
 extern "C" int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qdesc qn_q, const float* ms,
                                  const int64_t* sums, int64_t n, float* dx, int64_t rows, int32_t C, void* stream) {
-  if (rows <= 0 || C <= 0 || !G || !qn || !ms || !sums || !dx) return LBT_EINVAL;
+  if (rows <= 0 || C <= 0 || C % 4 || !G || !qn || !ms || !sums || !dx) return LBT_EINVAL;
   WideB b{G, qng, qn, qn_q, ms, sums, n, dx, rows, C, 0};
   const int cb = (C + kCB - 1) / kCB;
   b.rpb = rows_per_block(rows, cb);
