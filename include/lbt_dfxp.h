@@ -421,6 +421,15 @@ typedef struct lbt_pjob {
 } lbt_pjob;
 int lbt_bn_param_grads_many(const lbt_pjob* jobs, int32_t njobs, int32_t max_c, void* stream);
 
+/* The start of a step in ONE launch: lbt_dfxp_noise_fill's jobs (+ the arena clear),
+ * lbt_dfxp_quantize_weights' jobs, lbt_dfxp_quantize_many's jobs and, if input is not NULL, the
+ * step's input images quantised to int16 codes (input->out_kind == LBT_OUT_I16, n and inner
+ * multiples of 4, Philox noise inline -- the input quantiser needs no table). Independent parts:
+ * nothing here reads another part's output. Job arrays in device memory, *input in host memory. */
+int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_n, int64_t* zero, int64_t nzero,
+                      const lbt_wjob* wjobs, int32_t nw, int32_t max_cout, const lbt_qjob* qjobs, int32_t nq,
+                      const lbt_qjob* input, void* stream);
+
 /* The end of a step's backward in ONE launch: lbt_conv_wgrad_reduce_many's jobs (r_blocks =
  * sum of ceil(K*Cout/256)), lbt_bn_param_grads_many's jobs (Cout <= max_c) and, if head is not
  * NULL, the head's batch reductions (Dense_q dw and loss[0], from lbt_head_fwd_bwd's records:

@@ -168,6 +168,7 @@ _SIGS = {
     "lbt_bn_param_grads_many": [_P, c_int32, c_int32, _P],
     "lbt_head_scratch_bytes": [c_int32, c_int32, c_int32],
     "lbt_head_fwd_bwd": [_P, _P],
+    "lbt_step_prologue": [_P, c_int32, c_int64, _P, c_int64, _P, c_int32, c_int32, _P, c_int32, _P, _P],
     "lbt_step_reduce": [_P, c_int32, c_int32, _P, c_int32, c_int32, _P, _P],
     "lbt_grad_buffer_bwd": [_P, c_int64, _P, c_int64, c_int64, QDesc, _P, _P],
     "lbt_pre_dense": [_P, c_int32, c_int32, c_int32, c_int32, QDesc, _P, _P, _P, _P],

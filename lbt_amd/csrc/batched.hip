@@ -13,11 +13,11 @@ namespace {
 
 constexpr int kThreads = 256;
 
-__global__ __launch_bounds__(kThreads) void quantize_weights_kernel(const lbt_wjob* __restrict__ jobs) {
+LBT_DEV void quantize_weights_block(const lbt_wjob* __restrict__ jobs, int bx, int by) {
   __shared__ int red[kThreads / 64];
   __shared__ int sh_cnt[2 * kThreads / 64];
-  const lbt_wjob j = jobs[blockIdx.y];
-  const int co = blockIdx.x;
+  const lbt_wjob j = jobs[by];
+  const int co = bx;
   if (co >= j.Cout) return;  // uniform per block
   const QState s = qstate(j.q);
   const int K = j.KH * j.KW * j.Cin;
@@ -47,9 +47,13 @@ __global__ __launch_bounds__(kThreads) void quantize_weights_kernel(const lbt_wj
   }
 }
 
-__global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob* __restrict__ jobs) {
+__global__ __launch_bounds__(kThreads) void quantize_weights_kernel(const lbt_wjob* __restrict__ jobs) {
+  quantize_weights_block(jobs, blockIdx.x, blockIdx.y);
+}
+
+LBT_DEV void quantize_many_block(const lbt_qjob* __restrict__ jobs, int by) {
   __shared__ int sh_cnt[2 * kThreads / 64];
-  const lbt_qjob j = jobs[blockIdx.y];
+  const lbt_qjob j = jobs[by];
   const QState s = qstate(j.q);
   int ov1 = 0, ov2 = 0;
   for (int64_t i = threadIdx.x; i < j.n; i += kThreads) {
@@ -58,6 +62,10 @@ __global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob*
     store_code(j.out, j.out_kind, i, c, s.inv_m);
   }
   block_flush_counts(j.q, ov1, ov2, sh_cnt);
+}
+
+__global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob* __restrict__ jobs) {
+  quantize_many_block(jobs, blockIdx.y);
 }
 
 // Blocks are allotted to the jobs in order, ceil(K*Cout/256) each (1-D grid); a block reduces 256
@@ -159,11 +167,10 @@ __global__ __launch_bounds__(256) void step_reduce_kernel(const lbt_rjob* __rest
 }
 
 // grid (blocks, njobs): thread -> noise block b (4 values, one Philox call)
-__global__ __launch_bounds__(kThreads) void noise_fill_kernel(const lbt_njob* __restrict__ jobs, int64_t* zero,
-                                                             int64_t nzero) {
-  const int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (blockIdx.y == 0) {  // the first job row also clears the sums arena (4 x int64 per thread)
-    for (int64_t z = 4 * b; z < nzero; z += 4 * (int64_t)gridDim.x * kThreads) {
+LBT_DEV void noise_fill_block(const lbt_njob* __restrict__ jobs, int64_t* zero, int64_t nzero, int bx, int by, int gx) {
+  const int64_t b = (int64_t)bx * kThreads + threadIdx.x;
+  if (by == 0) {  // the first job row also clears the sums arena (4 x int64 per thread)
+    for (int64_t z = 4 * b; z < nzero; z += 4 * (int64_t)gx * kThreads) {
       if (z + 4 <= nzero) {
         *reinterpret_cast<longlong2*>(zero + z) = make_longlong2(0, 0);
         *reinterpret_cast<longlong2*>(zero + z + 2) = make_longlong2(0, 0);
@@ -172,11 +179,68 @@ __global__ __launch_bounds__(kThreads) void noise_fill_kernel(const lbt_njob* __
       }
     }
   }
-  const lbt_njob j = jobs[blockIdx.y];
+  const lbt_njob j = jobs[by];
   if (4 * b >= j.n) return;
   const uint64_t step = *j.step;
   const Noise4 n = noise4((uint64_t)b, j.qid, step, j.seed);
   *reinterpret_cast<float4*>(j.out + 4 * b) = make_float4(n.u[0], n.u[1], n.u[2], n.u[3]);
+}
+
+__global__ __launch_bounds__(kThreads) void noise_fill_kernel(const lbt_njob* __restrict__ jobs, int64_t* zero,
+                                                             int64_t nzero) {
+  noise_fill_block(jobs, zero, nzero, blockIdx.x, blockIdx.y, gridDim.x);
+}
+
+// The step's input images -> int16 codes: 4 consecutive elements per thread (one Philox call),
+// quant1 per element exactly as lbt_dfxp_quantize (noise index = element mod inner).
+LBT_DEV void quantize_input_block(const lbt_qjob& j, int bx) {
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const QState s = qstate(j.q);
+  const int64_t e0 = 4 * ((int64_t)bx * kThreads + threadIdx.x);
+  int ov1 = 0, ov2 = 0;
+  if (e0 < j.n) {  // n % 4 == 0, inner % 4 == 0 (launcher)
+    const float4 v = *reinterpret_cast<const float4*>(j.x + e0);
+    Noise4 nz = {{0.f, 0.f, 0.f, 0.f}};
+    if (j.q.stochastic) nz = qnoise4(j.q, s.step, (uint64_t)((e0 % j.inner) >> 2));
+    const int c0 = quant1(s, j.q.stochastic, v.x, nz.u[0], ov1, ov2);
+    const int c1 = quant1(s, j.q.stochastic, v.y, nz.u[1], ov1, ov2);
+    const int c2 = quant1(s, j.q.stochastic, v.z, nz.u[2], ov1, ov2);
+    const int c3 = quant1(s, j.q.stochastic, v.w, nz.u[3], ov1, ov2);
+    short4 o;
+    o.x = (short)c0; o.y = (short)c1; o.z = (short)c2; o.w = (short)c3;
+    *reinterpret_cast<short4*>((int16_t*)j.out + e0) = o;
+  }
+  block_flush_counts(j.q, ov1, ov2, sh_cnt);
+}
+
+// lbt_step_prologue: [noise rows x njobs][max_cout x nw weight blocks][nq parameter blocks][input blocks]
+struct Prologue {
+  const lbt_njob* njobs; int nn, nbx; int64_t* zero; int64_t nzero;
+  const lbt_wjob* wjobs; int nw, max_cout;
+  const lbt_qjob* qjobs; int nq;
+  lbt_qjob input; int nin;
+};
+
+__global__ __launch_bounds__(kThreads) void step_prologue_kernel(Prologue a) {
+  int b = blockIdx.x;
+  const int n1 = a.nbx * a.nn;
+  if (b < n1) {
+    noise_fill_block(a.njobs, a.zero, a.nzero, b % a.nbx, b / a.nbx, a.nbx);
+    return;
+  }
+  b -= n1;
+  const int n2 = a.max_cout * a.nw;
+  if (b < n2) {
+    quantize_weights_block(a.wjobs, b % a.max_cout, b / a.max_cout);
+    return;
+  }
+  b -= n2;
+  if (b < a.nq) {
+    quantize_many_block(a.qjobs, b);
+    return;
+  }
+  b -= a.nq;
+  quantize_input_block(a.input, b);
 }
 
 }  // namespace
@@ -189,6 +253,30 @@ extern "C" int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t 
   if (njobs > 65535 || blocks > 0x7fffffff) return LBT_EINVAL;
   hipLaunchKernelGGL(noise_fill_kernel, dim3((unsigned)blocks, njobs), dim3(kThreads), 0, (hipStream_t)stream, jobs,
                      zero, nzero > 0 ? nzero : 0);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_n, int64_t* zero, int64_t nzero,
+                                 const lbt_wjob* wjobs, int32_t nw, int32_t max_cout, const lbt_qjob* qjobs, int32_t nq,
+                                 const lbt_qjob* input, void* stream) {
+  if (nn < 0 || nw < 0 || nq < 0 || (nn > 0 && max_n <= 0) || (nw > 0 && max_cout <= 0)) return LBT_EINVAL;
+  if (nzero > 0 && (reinterpret_cast<uintptr_t>(zero) % 16)) return LBT_EINVAL;
+  Prologue a{};
+  a.njobs = njobs; a.nn = nn; a.zero = zero; a.nzero = nzero > 0 ? nzero : 0;
+  a.nbx = nn > 0 ? (int)((max_n + 4 * kThreads - 1) / (4 * kThreads)) : 0;
+  a.wjobs = wjobs; a.nw = nw; a.max_cout = nw > 0 ? max_cout : 0;
+  a.qjobs = qjobs; a.nq = nq;
+  if (input) {
+    a.input = *input;
+    if (a.input.n % 4 || a.input.inner % 4 || a.input.out_kind != LBT_OUT_I16 ||
+        (reinterpret_cast<uintptr_t>(a.input.x) % 16))
+      return LBT_EINVAL;
+    a.nin = (int)((a.input.n / 4 + kThreads - 1) / kThreads);
+  }
+  const int64_t blocks = (int64_t)a.nbx * nn + (int64_t)a.max_cout * nw + nq + a.nin;
+  if (blocks <= 0) return LBT_OK;
+  if (blocks > 0x7fffffff) return LBT_EINVAL;
+  hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

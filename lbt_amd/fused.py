@@ -195,11 +195,11 @@ class FusedResNet:
 
         self._nd, njobs = {}, []
 
-        def obs(q, n):
+        def obs(q, n, table=True):
             """Declare an activation / gradient quantiser's per-step element count and give it a
             noise table (its inner = n / N noise values, refreshed by the step's first launch)."""
             q.observe(n)
-            if q.stochastic and q not in self._nd:
+            if table and q.stochastic and q not in self._nd:
                 inner = n // N
                 tab = self._buf("noise:" + q.name, ((inner + 3) // 4 * 4,), torch.float32)
                 d = _lib.QDesc.from_buffer_copy(q.desc)
@@ -238,10 +238,9 @@ class FusedResNet:
                           None, 0, None, 0, None))
         self._wjobs = _dev_array(wjobs, ctx.device)
         max_cout = max(j.Cout for j in wjobs)
-        fwd.append(L("lbt_dfxp_quantize_weights", ptr(self._wjobs), len(wjobs), max_cout))
         if w4:
-            fwd.append(L("lbt_pack_int4", ptr(self._w8), ptr(self._w4), self._w8.numel(), k="pack_int4_kernel",
-                         nb=self._w8.numel() + self._w4.numel()))
+            self._w4_pack = L("lbt_pack_int4", ptr(self._w8), ptr(self._w4), self._w8.numel(), k="pack_int4_kernel",
+                              nb=self._w8.numel() + self._w4.numel())
         qjobs = []
         for r in self.rescales:
             C = r.C
@@ -250,7 +249,6 @@ class FusedResNet:
             qjobs.append(QJob(r.gamma.data_ptr(), r.gb.data_ptr(), _lib.OUT_F32, C, 1, r.g_range.desc))
             qjobs.append(QJob(r.beta.data_ptr(), r.gb.data_ptr() + 4 * C, _lib.OUT_F32, C, 1, r.b_range.desc))
         self._qjobs = _dev_array(qjobs, ctx.device)
-        fwd.append(L("lbt_dfxp_quantize_many", ptr(self._qjobs), len(qjobs)))
 
         # ---- stem: conv1 on the signed 9-bit image (VALU), BN, ReLU
         c = self.conv1
@@ -258,9 +256,8 @@ class FusedResNet:
         dc = ops.conv_desc(N, H, W, Cin0, C0, kh, kw, c.strides[1], c.strides[2], c.padding)
         c.d = dc
         ximg = self._buf("ximg", (N, H, W, Cin0), torch.int16)
-        obs(c.X_range, X.numel())
-        fwd.append(L("lbt_dfxp_quantize", ptr(self._X), ptr(ximg), OUT_I16, N, H * W * Cin0, self._qd(c.X_range), None,
-                     0, k="quantize_rows_kernel", nb=X.numel() * 6))
+        obs(c.X_range, X.numel(), table=False)  # quantised inside the step prologue (Philox inline)
+        self._input_job = QJob(self._X.data_ptr(), ximg.data_ptr(), OUT_I16, X.numel(), H * W * Cin0, c.X_range.desc)
         n0, r0 = self.n0, self.r0
         shp0 = (N, dc.Ho, dc.Wo, C0)
         numel0 = math.prod(shp0)
@@ -405,8 +402,13 @@ class FusedResNet:
         max_n = max(j.n for j in njobs)
         # ... which also clears the step's integer sums (everything this plan carved from the arena)
         nz = ctx._sums_used
-        fwd.insert(0, L("lbt_dfxp_noise_fill", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
-                        k="noise_fill_kernel", nb=4 * sum(j.n for j in njobs) + 8 * nz))
+        # (together with every weight / gamma / beta quantiser and the input image: one launch)
+        fwd.insert(0, L("lbt_step_prologue", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
+                        ptr(self._wjobs), len(wjobs), max_cout, ptr(self._qjobs), len(qjobs),
+                        ctypes.byref(self._input_job), k="step_prologue_kernel",
+                        nb=4 * sum(j.n for j in njobs) + 8 * nz + 6 * X.numel()))
+        if w4:  # the packed weight images need the quantised ones
+            fwd.insert(1, self._w4_pack)
         self._fwd, self._bwd = fwd, bwd
 
     # W4: the packed weight image and the *_w4 entry point of a conv's GEMM
