@@ -625,7 +625,7 @@ bool shape_ok(int64_t rows, int64_t inner, int C) {
 // 160 KiB): raise the kernel's limit before launching it.
 template <typename K>
 void allow_shm(K kernel, size_t shm) {
-  if (shm > 65536) hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+  if (shm > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)shm);
 }
 #define LBT_LAUNCH(KERNEL, GRID, SHM, ST, ...)                                  \

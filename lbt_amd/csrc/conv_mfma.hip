@@ -71,7 +71,7 @@ LBT_DEV v4i unpack_i4x16(v2i pk) {
 // W4: the B operand (weights) is stored as packed signed 4-bit codes, 8 bytes per 16-element
 // k-slice (no int4 MFMA on gfx950 -- unpacked to int8 in registers).
 template <int MODE, int CS, int NT, int CF = 0, int NB = 1, bool W4 = false>
-__global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && CF == 0) ? 8 : 1) void conv_gemm_kernel(
+__global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1) ? 8 : 1) void conv_gemm_kernel(
     GemmArgs p) {
   using G = EpiGeom<NT>;
   constexpr int NTW = G::NTW, WPM = G::WPM, MTB = G::MTB;
@@ -569,4 +569,20 @@ extern "C" int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, slab, nsplit, K,
                      Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw);
   return (int)hipGetLastError();
+}
+
+// Diagnostics: resident workgroups per CU of a few conv GEMM variants (hipOccupancy API), written
+// to out[0..n): fwd<CS1,NT1>, dgrad+A<CS1,NT1,26>, dgrad<CS4,NT2>, dgrad+A<CS2,NT2,26>, wgrad<1>.
+extern "C" int lbt_diag_occupancy(int32_t* out, int32_t n) {
+  const void* k[5] = {reinterpret_cast<const void*>(&conv_gemm_kernel<MODE_FWD, 1, 1, 0, 1, false>),
+                      reinterpret_cast<const void*>(&conv_gemm_kernel<MODE_DGRAD, 1, 1, 26, 1, false>),
+                      reinterpret_cast<const void*>(&conv_gemm_kernel<MODE_DGRAD, 4, 2, 0, 1, false>),
+                      reinterpret_cast<const void*>(&conv_gemm_kernel<MODE_DGRAD, 2, 2, 26, 1, false>),
+                      reinterpret_cast<const void*>(&conv_wgrad_kernel<1>)};
+  for (int i = 0; i < n && i < 5; ++i) {
+    int b = -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k[i], kThreads, 0) != hipSuccess) b = -1;
+    out[i] = b;
+  }
+  return 0;
 }
