@@ -304,6 +304,17 @@ int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt
 /* ... with the 4-bit packed weight image (see lbt_conv_fwd_i8w4). */
 int lbt_conv_dgrad_chain_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                               lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream);
+/* lbt_conv_dgrad_chain_i8 and lbt_conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit, nshard) of the
+ * SAME conv in ONE launch (the two read the same gradient codes and are independent): the
+ * workgroups of the wgrad grid come first, then the dgrad tiles. Results identical to the two
+ * separate calls. (Conv2d_q.backward dynamic_fixed_point.py:302-305 -- dW and dX of one layer.) */
+int lbt_conv_dgrad_chain_wgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                                  lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, const int8_t* xq,
+                                  int32_t x_u8off, int32_t* slab, int32_t nsplit, int32_t nshard, void* stream);
+int lbt_conv_dgrad_chain_wgrad_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d,
+                                    lbt_qdesc qg, lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a,
+                                    const int8_t* xq, int32_t x_u8off, int32_t* slab, int32_t nsplit,
+                                    int32_t nshard, void* stream);
 
 /* Pass B (the rest of Normalization_q.backward): with SG = sum G, SGQ = sum G*q from pass A,
  *   mg = sg*SG/n, mgx = sg*(s*SGQ - mu*SG)/(n*sigma)   (double -> fp32)

@@ -70,9 +70,10 @@ LBT_DEV v4i unpack_i4x16(v2i pk) {
 
 // W4: the B operand (weights) is stored as packed signed 4-bit codes, 8 bytes per 16-element
 // k-slice (no int4 MFMA on gfx950 -- unpacked to int8 in registers).
-template <int MODE, int CS, int NT, int CF = 0, int NB = 1, bool W4 = false>
-__global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1) ? 8 : 1) void conv_gemm_kernel(
-    GemmArgs p) {
+// One workgroup's tile (bid = its index in the GEMM's grid); the body of conv_gemm_kernel and of
+// the dgrad half of dgrad_wgrad_kernel.
+template <int MODE, int CS, int NT, int CF, int NB, bool W4>
+__device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid) {
   using G = EpiGeom<NT>;
   constexpr int NTW = G::NTW, WPM = G::WPM, MTB = G::MTB;
   __shared__ EpiShared<NT> sh;
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int mt_local = wave / WPM;
   const int nt0 = (wave % WPM) * NTW;
-  const int64_t mtile = (int64_t)blockIdx.x * MTB + mt_local;
+  const int64_t mtile = (int64_t)bid * MTB + mt_local;
   const int r = lane & 15, kg = lane >> 4;
   const lbt_conv_desc& d = p.d;
   const bool want_q = p.yq != nullptr;
@@ -251,6 +252,12 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1
   }
 }
 
+template <int MODE, int CS, int NT, int CF = 0, int NB = 1, bool W4 = false>
+__global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1) ? 8 : 1) void conv_gemm_kernel(
+    GemmArgs p) {
+  conv_gemm_body<MODE, CS, NT, CF, NB, W4>(p, blockIdx.x);
+}
+
 // ----------------------------------------------------------------------------- wgrad
 // dW[tap][ci][co] = sum_p X[p shifted by tap][ci] * G[p][co]: GEMM rows = ci, cols = co, k = pixels.
 // grid (nsplit, taps, Cout/16): workgroup = one tap, one 16-channel co slice, a pixel range; each
@@ -263,12 +270,24 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1
 constexpr int kWP = 64;  // pixels per wave chunk
 
 
+struct WgradArgs {
+  const int8_t* xq;
+  const int8_t* gq;
+  lbt_conv_desc d;
+  int x_fill;
+  int32_t* slab;
+  int64_t P;
+  int nsplit, nshard;
+};
+
 template <int CSI>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __restrict__ xq,
-                                                              const int8_t* __restrict__ gq,
-                                                              lbt_conv_desc d, int x_fill,
-                                                              int32_t* __restrict__ slab, int64_t P,
-                                                              int nsplit, int nshard) {
+__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bid) {
+  const int8_t* __restrict__ xq = wa.xq;
+  const int8_t* __restrict__ gq = wa.gq;
+  const lbt_conv_desc& d = wa.d;
+  const int x_fill = wa.x_fill, nsplit = wa.nsplit, nshard = wa.nshard;
+  int32_t* __restrict__ slab = wa.slab;
+  const int64_t P = wa.P;
   constexpr int CI = CSI * 16;
   // per wave: X image [CSI][64 px][16 B] and G image [64 px][16 B]
   __shared__ __attribute__((aligned(16))) int8_t lds[4][(CSI + 1) * kWP * 16];
@@ -282,7 +301,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
   // XCD's L2 (speed only; any order gives the same integer sums).
   const int ntap = d.KH * d.KW, ncos = d.Cout >> 4, total = nsplit * ntap * ncos;
   const int chunk = (total + 7) >> 3;
-  const int u = (int)(blockIdx.x & 7) * chunk + (int)(blockIdx.x >> 3);
+  const int u = (int)(bid & 7) * chunk + (int)(bid >> 3);
   if (u >= total) return;
   const int split = u / (ntap * ncos), urem = u - split * (ntap * ncos);
   const int tap = urem / ncos, cso = urem - tap * ncos;
@@ -350,6 +369,24 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const int8_t* __re
     if (v) LBT_GADD(&dst[(int64_t)ci * d.Cout + co], v);  // integer atomics: exact, order-independent
   }
   LBT_TS(3);
+}
+
+template <int CSI>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs wa) {
+  conv_wgrad_body<CSI>(wa, blockIdx.x);
+}
+
+// Horizontal fusion of one conv's two backward GEMMs, which read the same gradient codes and
+// are independent of each other: workgroups [0, nwg) are the wgrad's (the longer ones, dispatched
+// first), the rest the dgrad (+ chain pass A) tiles. One launch instead of two; nwg is a multiple
+// of 8, so both halves keep their XCD-aware block order.
+template <int CS, int NT, int CF, int NB, bool W4>
+__global__ __launch_bounds__(kThreads, (CS == 1 && NB == 1) ? 8 : 1) void dgrad_wgrad_kernel(GemmArgs p, WgradArgs wa,
+                                                                                          uint32_t nwg) {
+  if (blockIdx.x < nwg)
+    conv_wgrad_body<NT>(wa, blockIdx.x);
+  else
+    conv_gemm_body<MODE_DGRAD, CS, NT, CF, NB, W4>(p, blockIdx.x - nwg);
 }
 
 // 256 threads = 32 outputs x 8 split groups; coalesced 128-B slab rows; exact int64 sums.
@@ -477,12 +514,35 @@ extern "C" int lbt_conv_dgrad_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t
 
 namespace {
 
+// The wgrad launch of one conv: its argument block and grid (a multiple of 8 workgroups).
+int wgrad_setup(const int8_t* xq, int32_t x_u8off, const int8_t* gq, const lbt_conv_desc& d, int32_t* slab,
+                int32_t nsplit, int32_t nshard, WgradArgs& wa, uint32_t& blocks) {
+  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || nsplit <= 0 || nshard <= 0 || nshard > nsplit) return LBT_EINVAL;
+  if (d.Cin / 16 != 1 && d.Cin / 16 != 2 && d.Cin / 16 != 4 && d.Cin / 16 != 8) return LBT_EINVAL;
+  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
+  if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  // int32 shard totals: the pixels of one shard times |x*g| <= 255*128 stay below 2^31
+  if ((P + nsplit - 1) / nsplit * ((nsplit + nshard - 1) / nshard) > 65536) return LBT_EINVAL;
+  const int64_t units = (int64_t)nsplit * d.KH * d.KW * (d.Cout / 16);
+  if (units >= ((int64_t)1 << 30)) return LBT_EINVAL;
+  wa = WgradArgs{xq, gq, d, x_u8off ? (int)0x80808080u : 0, slab, P, nsplit, nshard};
+  blocks = (uint32_t)((units + 7) / 8 * 8);
+  return 0;
+}
+
+// dgrad + pass A, optionally with the same conv's wgrad in the same launch (wa != nullptr)
 template <int CS, int NT, int CF, int NB, bool W4>
-int launch_dgrad_chain(const GemmArgs& p, hipStream_t st) {
+int launch_dgrad_chain(const GemmArgs& p, const WgradArgs* wa, uint32_t wblocks, hipStream_t st) {
   constexpr int MTB = EpiGeom<NT>::MTB;
   const int64_t blocks = ((p.M + 15) / 16 + MTB - 1) / MTB;
-  hipLaunchKernelGGL((conv_gemm_kernel<MODE_DGRAD, CS, NT, CF, NB, W4>), dim3((unsigned)blocks), dim3(kThreads), 0, st,
-                     p);
+  if (wa) {
+    if (wa->d.Cin != NT * 16 || blocks + wblocks > 0x7fffffff) return LBT_EINVAL;
+    hipLaunchKernelGGL((dgrad_wgrad_kernel<CS, NT, CF, NB, W4>), dim3((unsigned)(blocks + wblocks)), dim3(kThreads), 0,
+                       st, p, *wa, wblocks);
+  } else {
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE_DGRAD, CS, NT, CF, NB, W4>), dim3((unsigned)blocks), dim3(kThreads), 0,
+                       st, p);
+  }
   return (int)hipGetLastError();
 }
 
@@ -491,7 +551,7 @@ constexpr int kAFused = kAFB | kAStoch;
 
 template <bool W4>
 int dgrad_chain(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
-                const float* add_src, const lbt_chain_bwd_a* a, void* stream) {
+                const float* add_src, const lbt_chain_bwd_a* a, const WgradArgs* wa, uint32_t wblocks, void* stream) {
   if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cin > 128 || !a) return LBT_EINVAL;
   if (a->C != d.Cin || a->rows != d.N || a->inner != (int64_t)d.H * d.W * d.Cin) return LBT_EINVAL;
   const int f = bwd_a_flags(*a);
@@ -513,7 +573,8 @@ int dgrad_chain(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d
   const int nt = d.Cin / 16;
   const int key = (cs << 8) | (nt << 4) | (a->has_b2 ? 1 : 0);
 #define LBT_DC(CS_, NT_, CF_, NB_)                                                                  \
-  if (key == ((CS_ << 8) | (NT_ << 4) | (NB_ == 2)) && f == (CF_)) return launch_dgrad_chain<CS_, NT_, CF_, NB_, W4>(p, st);
+  if (key == ((CS_ << 8) | (NT_ << 4) | (NB_ == 2)) && f == (CF_))                                  \
+    return launch_dgrad_chain<CS_, NT_, CF_, NB_, W4>(p, wa, wblocks, st);
 #define LBT_DC_SHAPES(CF_, NB_) \
   LBT_DC(1, 1, CF_, NB_) LBT_DC(2, 2, CF_, NB_) LBT_DC(4, 4, CF_, NB_) LBT_DC(2, 1, CF_, NB_) LBT_DC(4, 2, CF_, NB_)
   LBT_DC_SHAPES(kAFused | kAMaskR, 1)             // block, first BN (mask from R1)
@@ -525,37 +586,56 @@ int dgrad_chain(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d
   return LBT_EINVAL;
 }
 
+template <bool W4>
+int dgrad_chain_wgrad(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
+                      const float* add_src, const lbt_chain_bwd_a* a, const int8_t* xq, int32_t x_u8off,
+                      int32_t* slab, int32_t nsplit, int32_t nshard, void* stream) {
+  WgradArgs wa;
+  uint32_t wblocks = 0;
+  const int e = wgrad_setup(xq, x_u8off, gq, d, slab, nsplit, nshard, wa, wblocks);
+  if (e) return e;
+  return dgrad_chain<W4>(gq, wd, ksd, d, qg, qw, add_src, a, &wa, wblocks, stream);
+}
+
 }  // namespace
 
 extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                                        lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream) {
-  return dgrad_chain<false>(gq, wd, ksd, d, qg, qw, add_src, a, stream);
+  return dgrad_chain<false>(gq, wd, ksd, d, qg, qw, add_src, a, nullptr, 0, stream);
 }
 extern "C" int lbt_conv_dgrad_chain_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d,
                                          lbt_qdesc qg, lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a,
                                          void* stream) {
   if (qw.bits > 4) return LBT_EINVAL;
-  return dgrad_chain<true>(gq, (const int8_t*)wd4, ksd, d, qg, qw, add_src, a, stream);
+  return dgrad_chain<true>(gq, (const int8_t*)wd4, ksd, d, qg, qw, add_src, a, nullptr, 0, stream);
+}
+extern "C" int lbt_conv_dgrad_chain_wgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                                             lbt_qdesc qg, lbt_qdesc qw, const float* add_src,
+                                             const lbt_chain_bwd_a* a, const int8_t* xq, int32_t x_u8off,
+                                             int32_t* slab, int32_t nsplit, int32_t nshard, void* stream) {
+  return dgrad_chain_wgrad<false>(gq, wd, ksd, d, qg, qw, add_src, a, xq, x_u8off, slab, nsplit, nshard, stream);
+}
+extern "C" int lbt_conv_dgrad_chain_wgrad_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d,
+                                               lbt_qdesc qg, lbt_qdesc qw, const float* add_src,
+                                               const lbt_chain_bwd_a* a, const int8_t* xq, int32_t x_u8off,
+                                               int32_t* slab, int32_t nsplit, int32_t nshard, void* stream) {
+  if (qw.bits > 4) return LBT_EINVAL;
+  return dgrad_chain_wgrad<true>(gq, (const int8_t*)wd4, ksd, d, qg, qw, add_src, a, xq, x_u8off, slab, nsplit,
+                                 nshard, stream);
 }
 
 extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t* gq, lbt_conv_desc d,
                                     int32_t* slab, int32_t nsplit, int32_t nshard, void* stream) {
-  if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || nsplit <= 0 || nshard <= 0 || nshard > nsplit) return LBT_EINVAL;
-  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
-  if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
-  // int32 shard totals: the pixels of one shard times |x*g| <= 255*128 stay below 2^31
-  if ((P + nsplit - 1) / nsplit * ((nsplit + nshard - 1) / nshard) > 65536) return LBT_EINVAL;
-  const int csi = d.Cin / 16;
-  const int fill = x_u8off ? (int)0x80808080u : 0;
-  const int64_t units = (int64_t)nsplit * d.KH * d.KW * (d.Cout / 16);
-  if (units >= ((int64_t)1 << 30)) return LBT_EINVAL;
-  dim3 grid((unsigned)((units + 7) / 8 * 8));
+  WgradArgs wa;
+  uint32_t blocks = 0;
+  const int e = wgrad_setup(xq, x_u8off, gq, d, slab, nsplit, nshard, wa, blocks);
+  if (e) return e;
   hipStream_t st = (hipStream_t)stream;
-  switch (csi) {
-    case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
-    case 2: hipLaunchKernelGGL(conv_wgrad_kernel<2>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
-    case 4: hipLaunchKernelGGL(conv_wgrad_kernel<4>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
-    case 8: hipLaunchKernelGGL(conv_wgrad_kernel<8>, grid, dim3(kThreads), 0, st, xq, gq, d, fill, slab, P, nsplit, (int)nshard); break;
+  switch (d.Cin / 16) {
+    case 1: hipLaunchKernelGGL(conv_wgrad_kernel<1>, dim3(blocks), dim3(kThreads), 0, st, wa); break;
+    case 2: hipLaunchKernelGGL(conv_wgrad_kernel<2>, dim3(blocks), dim3(kThreads), 0, st, wa); break;
+    case 4: hipLaunchKernelGGL(conv_wgrad_kernel<4>, dim3(blocks), dim3(kThreads), 0, st, wa); break;
+    case 8: hipLaunchKernelGGL(conv_wgrad_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, wa); break;
     default: return LBT_EINVAL;
   }
   return (int)hipGetLastError();

@@ -77,6 +77,8 @@ class FusedResNet:
         self.overlap_wgrad = os.environ.get("LBT_OVERLAP_WGRAD", "0") == "1"  # measured: a loss here (60K vs 67K samples/s)
         # run each BN backward pass A inside the dgrad that produces its input (1 = default)
         self.fuse_dgrad_chain = os.environ.get("LBT_FUSE_DGRAD_CHAIN", "1") == "1"
+        # a conv's wgrad launched together with its dgrad (+ pass A): one launch per conv, not two
+        self.fuse_wgrad = os.environ.get("LBT_FUSE_WGRAD", "1") == "1" and not self.overlap_wgrad
         self._side = None
 
     # ------------------------------------------------------------------ Trainer interface
@@ -608,20 +610,28 @@ class FusedResNet:
         Gn1 = self._buf(k + "Gn1", shp, torch.int8)
         sums1 = self._sums(k + "sums1", ops.NSHARD * 4 * C)
         nb_dg2 = gq2.numel() + c2.wd.numel()
+        sp2, ns2, slab2 = ops.wgrad_slab(self._c, k + "slab2", d2, self.ctx)
+        nb_wg2 = f["xb"].numel() + gq2.numel() + 4 * slab2.numel()
         if fuse:
             aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
-            bwd.append(L(self._fn(c2, "lbt_conv_dgrad_chain_i8"), ptr(gq2), self._wd(c2), c2.ksd, d2, self._qd(c2.grad_range),
-                         c2.W_range.desc, None, ctypes.byref(aA1), k="conv_gemm_kernel<1> (dgrad+A)",
-                         nb=ops._dgrad_chain_bytes(gq2.numel(), c2.wd.numel(), aA1, False)))
+            nb = ops._dgrad_chain_bytes(gq2.numel(), c2.wd.numel(), aA1, False)
+            if self.fuse_wgrad:  # conv-2 wgrad in the same launch
+                bwd.append(L(self._fn(c2, "lbt_conv_dgrad_chain_wgrad_i8"), ptr(gq2), self._wd(c2), c2.ksd, d2,
+                             self._qd(c2.grad_range), c2.W_range.desc, None, ctypes.byref(aA1), ptr(f["xb"]), 1,
+                             ptr(slab2), sp2, ns2, k="dgrad_wgrad_kernel", nb=nb + nb_wg2 - gq2.numel()))
+            else:
+                bwd.append(L(self._fn(c2, "lbt_conv_dgrad_chain_i8"), ptr(gq2), self._wd(c2), c2.ksd, d2,
+                             self._qd(c2.grad_range), c2.W_range.desc, None, ctypes.byref(aA1),
+                             k="conv_gemm_kernel<1> (dgrad+A)", nb=nb))
         else:
             d1g = self._buf(k + "d1", shp, torch.float32)
             bwd.append(L(self._fn(c2, "lbt_conv_dgrad_i8"), ptr(gq2), self._wd(c2), c2.ksd, d2, self._qd(c2.grad_range),
                          c2.W_range.desc, ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg2 + 4 * numel))
             aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
         keep.append(aA1)
-        sp2, ns2, slab2 = ops.wgrad_slab(self._c, k + "slab2", d2, self.ctx)
-        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), sp2, ns2,
-                                   k="conv_wgrad_kernel", nb=f["xb"].numel() + gq2.numel() + 4 * slab2.numel())))
+        if not (fuse and self.fuse_wgrad):
+            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), sp2, ns2,
+                                       k="conv_wgrad_kernel", nb=nb_wg2)))
         rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), self._qd(c2.X_range),
                           self._qd(c2.grad_range), c2.W.data_ptr(), ops.f32(2 * c2.weight_decay), c2.dW.data_ptr()))
         if not fuse:
@@ -642,17 +652,26 @@ class FusedResNet:
         nin = math.prod(f["Xin"].shape)
         nb_dg1 = gq1.numel() + c1.wd.numel() + 8 * nin
         gin = None
+        sp1, ns1, slab1 = ops.wgrad_slab(self._c, k + "slab1", d1, self.ctx)
+        nb_wg1 = f["xa"].numel() + gq1.numel() + 4 * slab1.numel()
         if fuse:
-            bwd.append(L(self._fn(c1, "lbt_conv_dgrad_chain_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1, self._qd(c1.grad_range),
-                         c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]), k="conv_gemm_kernel<1> (dgrad+A)",
-                         nb=ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], add is not None)))
+            nb = ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], add is not None)
+            if self.fuse_wgrad:  # conv-1 wgrad in the same launch
+                bwd.append(L(self._fn(c1, "lbt_conv_dgrad_chain_wgrad_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1,
+                             self._qd(c1.grad_range), c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]),
+                             ptr(f["xa"]), 1, ptr(slab1), sp1, ns1, k="dgrad_wgrad_kernel",
+                             nb=nb + nb_wg1 - gq1.numel()))
+            else:
+                bwd.append(L(self._fn(c1, "lbt_conv_dgrad_chain_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1,
+                             self._qd(c1.grad_range), c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]),
+                             k="conv_gemm_kernel<1> (dgrad+A)", nb=nb))
         else:
             gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
             bwd.append(L(self._fn(c1, "lbt_conv_dgrad_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1, self._qd(c1.grad_range),
                          c1.W_range.desc, ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg1))
-        sp1, ns1, slab1 = ops.wgrad_slab(self._c, k + "slab1", d1, self.ctx)
-        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), sp1, ns1,
-                                   k="conv_wgrad_kernel", nb=f["xa"].numel() + gq1.numel() + 4 * slab1.numel())))
+        if not (fuse and self.fuse_wgrad):
+            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), sp1, ns1,
+                                       k="conv_wgrad_kernel", nb=nb_wg1)))
         rjobs.append(RJob(slab1.data_ptr(), ns1, 9 * Cin, C, 1, gcol1.data_ptr(), self._qd(c1.X_range),
                           self._qd(c1.grad_range), c1.W.data_ptr(), ops.f32(2 * c1.weight_decay), c1.dW.data_ptr()))
         if cs is not None:
