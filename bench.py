@@ -125,7 +125,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=128, help="images per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 128; resnet50: 32)")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (diagnostics)")
     ap.add_argument("--layerwise", action="store_true", help="run the Layer_q path instead of the fused plan")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -137,8 +137,8 @@ def main():
     args = ap.parse_args()
     r50 = args.workload == "resnet50"
     w4 = args.workload == "resnet20w4"
-    if r50 and args.batch == 128:
-        args.batch = 32
+    if args.batch is None:
+        args.batch = 32 if r50 else 128
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

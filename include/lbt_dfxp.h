@@ -227,6 +227,20 @@ int lbt_conv_stem_fwd(const int16_t* x, const int8_t* w_hwio, lbt_conv_desc d, l
 int lbt_conv_stem_wgrad(const int16_t* x, const int8_t* gq, lbt_conv_desc d, int32_t* slab, int32_t nshard,
                         void* stream);
 
+/* The ImageNet ResNet's conv1 (7x7/2, 3 -> 64; dynamic_fixed_point.py:287-305)
+ * on v_mfma_f32_16x16x32_f16 (stem_wide.hip): signed <= 9-bit int16 image codes, K = KH*KW*Cin
+ * <= 480 patch elements, Cout % 16 == 0; exact (integer partial sums < 2^24), bit-identical to
+ * lbt_conv_fwd_generic / lbt_conv_wgrad_generic16.
+ * fwd: y fp32 [N*Ho*Wo][Cout]; rejects K * 2^(qx.bits-1) * 2^(qw.bits-1) > 2^24.
+ * wgrad: g = int8 (g16 = 0) or int16 (g16 = 1, 9..16-bit gradient codes) [N*Ho*Wo][Cout]; WRITES
+ *      every element of the int64 slab[nsplit][K][Cout] (nsplit = lbt_stem_wide_nsplit(d)); finish
+ *      with lbt_conv_wgrad_reduce64. x_bits <= 9.                                              */
+int lbt_conv_stem_wide_fwd(const int16_t* x, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw,
+                           float* y, void* stream);
+int lbt_stem_wide_nsplit(lbt_conv_desc d);  /* returns nsplit (> 0) */
+int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const void* g, int32_t g16, lbt_conv_desc d,
+                             int64_t* slab, int32_t nsplit, void* stream);
+
 /* ---------------------------------------------------------------- batch norm -------- */
 
 /* The statistics of one Normalization_q (dynamic_fixed_point.py:584-616): its input codes q
@@ -475,6 +489,25 @@ int lbt_augment_flip_crop(const float* x, float* y, int32_t N, int32_t H, int32_
  * reused divisor (div_by(x, recip(y)), dfxp_device.h) differs in any bit from x / y; if qa
  * is not NULL also writes x / y to qa and div_by to qb.                                      */
 int lbt_selftest_div(const float* x, const float* y, int64_t n, int32_t* bad, float* qa, float* qb, void* stream);
+
+/* Dense_q for wide classifier heads (dynamic_fixed_point.py:319-395, 441-466; ResNet-50's
+ * 2048 -> 1000 fc) on int8 MFMA (dense.hip); exact, bit-identical to the generic kernels.
+ * lbt_dense_pack: HWIO codes W[in][out] -> wf [out][kf] and wd [in][up] (zero-padded; kf, up
+ *      multiples of 64 >= in, out).
+ * lbt_dense_gemm: out[rows][cols] = a[rows][:kvalid] . b[cols][:kb]^T * 2^-(e_a + e_b); a int8
+ *      codes (a16 = 0) or int16 9..16-bit codes (a16 = 1); kvalid, lda multiples of 8. fwd: a = xq,
+ *      b = wf; dgrad: a = gq, b = wd.
+ * lbt_dense_wgrad: dw[in][out] = (float)(sum_n x[n][k] g[n][u]) * 2^-(e_x + e_g) + wd2 * w (the
+ *      reduce of lbt_conv_wgrad_reduce64 fused in); g int8 / int16; out % 4 == 0.
+ * lbt_softmax_xent_wide: lbt_softmax_xent for wide K (one wave per row).                      */
+int lbt_dense_pack(const int8_t* w_hwio, int32_t in_units, int32_t units, int8_t* wf, int32_t kf, int8_t* wd,
+                   int32_t up, void* stream);
+int lbt_dense_gemm(const void* a, int32_t a16, int32_t lda, int32_t kvalid, const int8_t* b, int32_t kb, int32_t rows,
+                   int32_t cols, lbt_qdesc qa, lbt_qdesc qb, float* out, void* stream);
+int lbt_dense_wgrad(const int8_t* xq, const void* g, int32_t g16, int32_t N, int32_t in_units, int32_t units,
+                    lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2, float* dw, void* stream);
+int lbt_softmax_xent_wide(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss, float* dz,
+                          void* stream);
 
 /* ABI version for the Python loader. */
 int lbt_abi_version(void);

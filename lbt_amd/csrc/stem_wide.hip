@@ -1,0 +1,314 @@
+// stem_wide.hip -- the ImageNet ResNet's conv1 (7x7 / 2, 3 -> 64 channels; SURVEY 8(f) rank 1,
+// dynamic_fixed_point.py:287-305) on v_mfma_f32_16x16x32_f16, forward and weight gradient.
+//
+// Like stem.hip, the operand is the image quantised to SIGNED 9-bit codes, which int8 MFMA cannot
+// take; fp16 holds them (|x| <= 256) and every 8-bit weight / gradient code exactly, and the fp32
+// accumulator stays exact while every partial sum is an integer of magnitude <= 2^24:
+//   fwd   : K (= 147 here) products of |x*w| <= 2^8 * 2^7 per output -- the launcher checks
+//           K * 2^(xbits-1) * 2^(wbits-1) <= 2^24, so the whole K loop accumulates in fp32;
+//   wgrad : k-dim = pixels. A 16-bit gradient code is split g = 256*hi + lo with hi = g >> 8 in
+//           [-128, 127] and lo = g & 255 in [0, 255], both exact in fp16; one MFMA step sums 32
+//           pixels, and every kFlush = 4 steps (128 pixels, |sum| <= 128 * 256 * 255 < 2^24) the
+//           fp32 tiles are moved into int32 accumulators. A workgroup covers <= kMaxWgPixels
+//           pixels, so those stay below 2^31; it stores 256*hi + lo as int64 into its own slice of
+//           slab[split][k][co] (plain stores: every slab element has exactly one writer), and
+//           lbt_conv_wgrad_reduce64 finishes dW exactly as for the generic kernels.
+// The results are the integer GEMM's, bit for bit (same as conv_generic.hip and the oracle).
+//
+// fp16 16x16x32 operand map (gfx950): lane l holds A[row l&15][k = 8*(l>>4) + j] and
+// B[k = 8*(l>>4) + j][col l&15], j = 0..7; C/D: col = l&15, row = 4*(l>>4) + reg.
+#include "dfxp_device.h"
+
+using namespace lbt;
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxK = 480;           // patch elements (LDS budget; exactness is checked separately)
+constexpr int kFwdRows = 128;        // output pixels per forward workgroup (4 waves x 2 m-tiles)
+constexpr int kWgChunk = 64;         // wgrad pixels staged per LDS pass (2 MFMA k-steps)
+constexpr int kFlush = 4;            // wgrad MFMA k-steps between fp32 -> int32 flushes
+constexpr int kMaxWgPixels = 16384;  // wgrad pixels per workgroup (int32 accumulator bound)
+
+// patch element k = (kh, kw, ci) in HWIO order -> (dy, dx, ci) relative to (oy*SH - PT, ox*SW - PL)
+LBT_DEV int patch_code(const lbt_conv_desc& d, int k) {
+  const int tap = k / d.Cin, ci = k - tap * d.Cin;
+  const int kh = tap / d.KW, kw = tap - kh * d.KW;
+  return (kh << 20) | (kw << 10) | ci;
+}
+
+// ------------------------------------------------------------------ forward
+// grid (ceil(M / 128), ceil(Cout / 64)); wave = 2 m-tiles x NCT column tiles of its 64-column
+// group. The W slice lives in LDS as fp16, transposed ([col][k]), so a B fragment is one 16-byte
+// read; the patch-element decode table too. A fragments are gathered from the int16 image.
+template <int NCT>
+__global__ __launch_bounds__(kThreads) void stem_wide_fwd_kernel(const int16_t* __restrict__ x,
+                                                                 const int8_t* __restrict__ w, lbt_conv_desc d, int K,
+                                                                 int KP, lbt_qdesc qx, lbt_qdesc qw,
+                                                                 float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  _Float16* sW = reinterpret_cast<_Float16*>(smem);        // [NCT*16][KP]
+  int* sK = reinterpret_cast<int*>(smem + (size_t)NCT * 16 * KP * 2);  // [KP]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int c0 = blockIdx.y * 64;
+  const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
+  for (int i = threadIdx.x; i < NCT * 16 * KP; i += kThreads) {
+    const int col = i / KP, k = i - col * KP;
+    const int c = c0 + col;
+    const int v = (k < K && c < d.Cout) ? (int)w[(int64_t)k * d.Cout + c] : 0;
+    sW[i] = (_Float16)(float)v;
+  }
+  for (int k = threadIdx.x; k < KP; k += kThreads) sK[k] = k < K ? patch_code(d, k) : -1;
+  __syncthreads();
+
+  // this lane's two A rows (output pixels)
+  int base[2], iy0[2], ix0[2];
+  bool rv[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int64_t m = (int64_t)blockIdx.x * kFwdRows + wave * 32 + mt * 16 + r;
+    rv[mt] = m < M;
+    const uint32_t mu = (uint32_t)(rv[mt] ? m : 0);
+    const int ox = (int)(mu % (uint32_t)d.Wo);
+    const uint32_t t = mu / (uint32_t)d.Wo;
+    const int oy = (int)(t % (uint32_t)d.Ho), n = (int)(t / (uint32_t)d.Ho);
+    iy0[mt] = oy * d.SH - d.PT;
+    ix0[mt] = ox * d.SW - d.PL;
+    base[mt] = n * d.H;
+  }
+  f4v acc[2][NCT];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[mt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < KP; k0 += 32) {
+    int code[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) code[j] = sK[k0 + 8 * kg + j];
+    h8 a[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      int off[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = code[j];
+        const int iy = iy0[mt] + (c >> 20), ix = ix0[mt] + ((c >> 10) & 1023);
+        const bool ok = c >= 0 && rv[mt] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        off[j] = ok ? ((base[mt] + iy) * d.W + ix) * d.Cin + (c & 1023) : -1;
+      }
+      int16_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = x[off[j] < 0 ? 0 : off[j]];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[mt][j] = (_Float16)(float)(off[j] < 0 ? 0 : (int)v[j]);
+    }
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const h8 b = *reinterpret_cast<const h8*>(sW + (ct * 16 + r) * KP + k0 + 8 * kg);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) acc[mt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt], b, acc[mt][ct], 0, 0, 0);
+    }
+  }
+  const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qw)));
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const int c = c0 + ct * 16 + r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = (int64_t)blockIdx.x * kFwdRows + wave * 32 + mt * 16 + kg * 4 + i;
+        if (row < M && c < d.Cout) y[row * d.Cout + c] = acc[mt][ct][i] * scale;  // exact integer * 2^-e
+      }
+    }
+}
+
+// ------------------------------------------------------------------ weight gradient
+// grid (nsplit, ceil(K / 64), ceil(Cout / 64)): workgroup = one pixel range, 4 k-tiles (one per
+// wave: 16 patch elements), 64 output channels. Per 64-pixel pass the gradient rows are staged
+// in LDS transposed and split ([hi|lo][col][pixel] fp16), with the pass's pixel decode; each wave
+// gathers its patch rows (A) from the int16 image.
+template <bool G16, int NCT>
+__global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t* __restrict__ x,
+                                                                   const void* __restrict__ g_, lbt_conv_desc d,
+                                                                   int K, int64_t per, int64_t* __restrict__ slab) {
+  constexpr int NH = G16 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) _Float16 sG[NH][NCT * 16][kWgChunk + 8];
+  __shared__ int sBase[kWgChunk], sYX[kWgChunk];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int c0 = blockIdx.z * 64;
+  const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
+  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p1 = p0 + per < M ? p0 + per : M;
+  // this lane's A row: patch element k of this wave's k-tile
+  const int k = (blockIdx.y * 4 + wave) * 16 + r;
+  const int code = k < K ? patch_code(d, k) : -1;
+  const int dy = code >> 20, dx = (code >> 10) & 1023, ci = code & 1023;
+
+  f4v facc[NH][NCT];
+  int iacc[NH][NCT][4];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      facc[h][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) iacc[h][ct][i] = 0;
+    }
+  int steps = 0;
+  for (int64_t q0 = p0; q0 < p1; q0 += kWgChunk) {
+    __syncthreads();  // the previous pass's LDS reads are done
+    // stage: pixel decode (64 threads) and the gradient rows, transposed + split
+    if (threadIdx.x < kWgChunk) {
+      const int64_t p = q0 + threadIdx.x;
+      const bool pv = p < p1;
+      const uint32_t pu = (uint32_t)(pv ? p : p0);
+      const int ox = (int)(pu % (uint32_t)d.Wo);
+      const uint32_t t = pu / (uint32_t)d.Wo;
+      const int oy = (int)(t % (uint32_t)d.Ho), n = (int)(t / (uint32_t)d.Ho);
+      sBase[threadIdx.x] = pv ? n * d.H : -1;
+      sYX[threadIdx.x] = ((oy * d.SH - d.PT) << 16) | ((ox * d.SW - d.PL) & 0xFFFF);
+    }
+    for (int i = threadIdx.x; i < kWgChunk * NCT * 16; i += kThreads) {
+      const int px = i / (NCT * 16), col = i - px * (NCT * 16);
+      const int64_t p = q0 + px;
+      const int c = c0 + col;
+      int v = 0;
+      if (p < p1 && c < d.Cout)
+        v = G16 ? (int)reinterpret_cast<const int16_t*>(g_)[p * d.Cout + c]
+                : (int)reinterpret_cast<const int8_t*>(g_)[p * d.Cout + c];
+      if constexpr (G16) {
+        sG[0][col][px] = (_Float16)(float)(v >> 8);   // hi, arithmetic shift: [-128, 127]
+        sG[NH - 1][col][px] = (_Float16)(float)(v & 255);  // lo: [0, 255]
+      } else {
+        sG[0][col][px] = (_Float16)(float)v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kWgChunk / 32; ++s) {
+      h8 a;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int px = s * 32 + 8 * kg + j;
+        const int b = sBase[px], yx = sYX[px];
+        const int iy = (yx >> 16) + dy, ix = (int)(int16_t)(yx & 0xFFFF) + dx;
+        const bool ok = code >= 0 && b >= 0 && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const int off = ok ? ((b + iy) * d.W + ix) * d.Cin + ci : 0;
+        const int v = x[off];
+        a[j] = (_Float16)(float)(ok ? v : 0);
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const h8 b = *reinterpret_cast<const h8*>(&sG[h][ct * 16 + r][s * 32 + 8 * kg]);
+          facc[h][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, facc[h][ct], 0, 0, 0);
+        }
+      if (++steps == kFlush) {
+        steps = 0;
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) iacc[h][ct][i] += (int)facc[h][ct][i];
+            facc[h][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+    }
+  }
+  // D[row = k][col]: row = k-tile*16 + 4*kg + i, col = ct*16 + r
+  int64_t* out = slab + (int64_t)blockIdx.x * K * d.Cout;
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int c = c0 + ct * 16 + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = (blockIdx.y * 4 + wave) * 16 + 4 * kg + i;
+      int64_t v = (int64_t)(iacc[0][ct][i] + (int)facc[0][ct][i]);
+      if constexpr (G16) v = 256 * v + (int64_t)(iacc[1][ct][i] + (int)facc[1][ct][i]);
+      if (kk < K && c < d.Cout) out[(int64_t)kk * d.Cout + c] = v;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int lbt_conv_stem_wide_fwd(const int16_t* x, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qx,
+                                      lbt_qdesc qw, float* y, void* stream) {
+  const int K = d.KH * d.KW * d.Cin;
+  if (K <= 0 || K > kMaxK || d.Cout <= 0 || d.Cout % 16 || qx.bits > 16 || qw.bits > 8) return LBT_EINVAL;
+  // exact fp32 accumulation: K * max|x| * max|w| <= 2^24
+  if ((double)K * ldexp(1.0, qx.bits - 1) * ldexp(1.0, qw.bits - 1) > 16777216.0) return LBT_EINVAL;
+  if (d.KH >= 1024 || d.KW >= 1024 || d.Cin >= 1024 || d.PT >= 1024 || d.PL >= 1024) return LBT_EINVAL;
+  const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
+  if (M <= 0) return LBT_OK;
+  if ((int64_t)d.N * d.H * d.W * d.Cin >= ((int64_t)1 << 31) || M * d.Cout >= ((int64_t)1 << 40)) return LBT_EINVAL;
+  const int KP = (K + 31) / 32 * 32;
+  const int nct = d.Cout >= 64 ? 4 : d.Cout / 16;
+  const size_t shm = (size_t)nct * 16 * KP * 2 + (size_t)KP * 4;
+  dim3 grid((unsigned)((M + kFwdRows - 1) / kFwdRows), (unsigned)((d.Cout + 63) / 64));
+  hipStream_t st = (hipStream_t)stream;
+  switch (nct) {
+    case 1: hipLaunchKernelGGL(stem_wide_fwd_kernel<1>, grid, dim3(kThreads), shm, st, x, w_hwio, d, K, KP, qx, qw, y); break;
+    case 2: hipLaunchKernelGGL(stem_wide_fwd_kernel<2>, grid, dim3(kThreads), shm, st, x, w_hwio, d, K, KP, qx, qw, y); break;
+    case 3: hipLaunchKernelGGL(stem_wide_fwd_kernel<3>, grid, dim3(kThreads), shm, st, x, w_hwio, d, K, KP, qx, qw, y); break;
+    default: hipLaunchKernelGGL(stem_wide_fwd_kernel<4>, grid, dim3(kThreads), shm, st, x, w_hwio, d, K, KP, qx, qw, y); break;
+  }
+  return (int)hipGetLastError();
+}
+
+// slab: int64 [nsplit][K][Cout], fully written (no zeroing needed); nsplit from lbt_stem_wide_nsplit.
+extern "C" int lbt_stem_wide_nsplit(lbt_conv_desc d) {
+  const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
+  // ~2048 pixels per workgroup (>= 2 waves of workgroups on 256 CUs for conv1 at B=32), within
+  // the int32 accumulator bound
+  int64_t ns = (M + 2047) / 2048;
+  if (ns < 1) ns = 1;
+  while ((M + ns - 1) / ns > kMaxWgPixels) ++ns;
+  return (int)ns;
+}
+
+extern "C" int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const void* g, int32_t g16, lbt_conv_desc d,
+                                        int64_t* slab, int32_t nsplit, void* stream) {
+  const int K = d.KH * d.KW * d.Cin;
+  if (K <= 0 || K > kMaxK || d.Cout <= 0 || d.Cout % 16 || nsplit <= 0) return LBT_EINVAL;
+  // fp32 flush bound (128 pixels x max|x| x 255 <= 2^24) and the int32 accumulator bound
+  if (x_bits < 1 || x_bits > 9) return LBT_EINVAL;
+  if (d.KH >= 1024 || d.KW >= 1024 || d.Cin >= 1024 || d.PT >= 1024 || d.PL >= 1024) return LBT_EINVAL;
+  if (d.H >= 32768 || d.W >= 32768 || (int64_t)d.Ho * d.SH >= 32768 || (int64_t)d.Wo * d.SW >= 32768) return LBT_EINVAL;
+  const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
+  if (M <= 0) return LBT_OK;
+  if ((int64_t)d.N * d.H * d.W * d.Cin >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  const int64_t per = (M + nsplit - 1) / nsplit;
+  if (per > kMaxWgPixels) return LBT_EINVAL;
+  const int nct = d.Cout >= 64 ? 4 : d.Cout / 16;
+  dim3 grid((unsigned)nsplit, (unsigned)((K + 63) / 64), (unsigned)((d.Cout + 63) / 64));
+  hipStream_t st = (hipStream_t)stream;
+#define LBT_STEM_W(G, N) \
+  hipLaunchKernelGGL((stem_wide_wgrad_kernel<G, N>), grid, dim3(kThreads), 0, st, x, g, d, K, per, slab)
+  if (g16) {
+    switch (nct) {
+      case 1: LBT_STEM_W(true, 1); break;
+      case 2: LBT_STEM_W(true, 2); break;
+      case 3: LBT_STEM_W(true, 3); break;
+      default: LBT_STEM_W(true, 4); break;
+    }
+  } else {
+    switch (nct) {
+      case 1: LBT_STEM_W(false, 1); break;
+      case 2: LBT_STEM_W(false, 2); break;
+      case 3: LBT_STEM_W(false, 3); break;
+      default: LBT_STEM_W(false, 4); break;
+    }
+  }
+#undef LBT_STEM_W
+  return (int)hipGetLastError();
+}

@@ -151,6 +151,20 @@ class Conv2d_q(Layer_q):
         """int16 (9..12-bit) input codes and a small patch: the fp16-MFMA stem kernels."""
         return self.x_kind == OUT_I16 and self.X_range.bits <= 12 and self.bits <= 8 and ops.stem_ok(d)
 
+    def stem_wide(self, d):
+        """Signed <= 9-bit image codes and a large patch (the ImageNet conv1, 7x7x3): stem_wide.hip."""
+        return (self.x_kind == OUT_I16 and not self.stem(d)
+                and ops.stem_wide_ok(d, self.X_range.bits, self.weight_bits))
+
+    def _wgrad_stem_wide(self):
+        d = self.d
+        K = d.KH * d.KW * d.Cin
+        ns = ops.stem_wide_nsplit(d)
+        slab = self._c.get("stemw_slab", (ns, K, d.Cout), torch.int64, self.ctx.device)
+        ops.conv_stem_wide_wgrad(self.xq, self.X_range.bits, self.gradq, d, slab, ns)
+        ops.conv_wgrad_reduce64(slab, ns, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
+                                ops.f32(2 * self.weight_decay), self.dW)
+
     def quantize_weights(self):
         ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio,
                             wf=self.wf if (self.mfma or self.igemm_f) else None, ksf=self.ksf,
@@ -177,6 +191,8 @@ class Conv2d_q(Layer_q):
                             self.X_range.desc, self.W_range.desc, y=y)
         elif self.stem(d):
             ops.conv_stem_fwd(self.xq, self.w_hwio, d, self.X_range.desc, self.W_range.desc, y=y)
+        elif self.stem_wide(d):
+            ops.conv_stem_wide_fwd(self.xq, self.w_hwio, d, self.X_range.desc, self.W_range.desc, y)
         elif self.igemm_f:
             a_kind = 2 if self.x_kind == OUT_I16 else (1 if self.x_kind == OUT_U8OFF else 0)
             ops.conv_fwd_igemm(self.xq, a_kind, self.wf, self.ksf, d, self.X_range.desc, self.W_range.desc, y)
@@ -198,6 +214,8 @@ class Conv2d_q(Layer_q):
         self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16, dev))
         if self.igemm_w:
             self._wgrad_igemm(1)
+        elif self.stem_wide(d):
+            self._wgrad_stem_wide()
         else:
             ns = ops.wgrad_nsplit(d, generic=True)
             slab = self._c.get("slab64", (ns, K, d.Cout), torch.int64, dev)
@@ -243,6 +261,9 @@ class Conv2d_q(Layer_q):
         elif self.stem(d):
             ns, slab = ops.stem_slab(self._c, "stem_slab", d, self.ctx)
             ops.conv_stem_wgrad(self.xq, self.gradq, d, slab, ns)
+        elif self.stem_wide(d):
+            self._wgrad_stem_wide()
+            slab = None
         else:
             ns = ops.wgrad_nsplit(d, generic=True)
             slab = self._c.get("slab", (ns, K, Cout), torch.int32, dev)
@@ -304,6 +325,11 @@ class Dense_q(Layer_q):
             self.b_range = ctx.quantizer(name + "/b_range", bits, bias_range, t)
         self.x_kind = OUT_I8 if bits <= 8 else OUT_I16
         self.w_hwio = torch.zeros((in_units, units), dtype=torch.int8, device=ctx.device)
+        # wide heads (ResNet-50's fc): int8-MFMA GEMMs on packed images of the quantised W
+        self.mfma = ops.dense_mfma_ok(in_units, units, bits, weight_bits)
+        if self.mfma:
+            self.wf = torch.zeros((units, -(-in_units // 64) * 64), dtype=torch.int8, device=ctx.device)
+            self.wd = torch.zeros((in_units, -(-units // 64) * 64), dtype=torch.int8, device=ctx.device)
         self._c = _Cache()
 
     def param_slots(self):
@@ -321,8 +347,13 @@ class Dense_q(Layer_q):
                                                                               ops.out_dtype(self.x_kind), dev))
         ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio)
         y = self._c.get("y", (N, self.units), torch.float32, dev)
-        ops.conv_fwd_generic(self.xq, self.x_kind == OUT_I16, self.w_hwio, d, self.X_range.desc,
-                             self.W_range.desc, y)
+        if self.mfma:
+            ops.dense_pack(self.w_hwio, self.wf, self.wd)
+            ops.dense_gemm(self.xq, self.wf, self.in_units, self.X_range.desc, self.W_range.desc, y,
+                           kernel="dense_fwd_kernel")
+        else:
+            ops.conv_fwd_generic(self.xq, self.x_kind == OUT_I16, self.w_hwio, d, self.X_range.desc,
+                                 self.W_range.desc, y)
         if self.use_bias:
             self.bq = ops.quantize(self.b, self.b_range, OUT_F32, out=self._c.get("bq", (self.units,), torch.float32,
                                                                                    dev))
@@ -339,6 +370,8 @@ class Dense_q(Layer_q):
                 raise NotImplementedError("bias with > 8-bit gradient codes")
             self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16,
                                                                                        dev))
+            if self.mfma:
+                return self._backward_mfma(dev)
             ns = ops.wgrad_nsplit(d, generic=True)
             slab = self._c.get("slab64", (ns, self.in_units, self.units), torch.int64, dev)
             ops.conv_wgrad_generic16(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
@@ -350,6 +383,10 @@ class Dense_q(Layer_q):
         gsum = self._c.sums("gsum", ops.NSHARD * 2 * self.units, self.ctx)
         self.gradq = ops.quantize(grad, self.grad_range, OUT_I8, out=self._c.get("gq", grad.shape, torch.int8, dev),
                                   chsum=gsum, C=self.units)
+        if self.mfma:
+            if self.use_bias:
+                ops.bias_grad(gsum, self.units, self.grad_range.desc, self.db)
+            return self._backward_mfma(dev)
         ns = ops.wgrad_nsplit(d, generic=True)
         slab = self._c.get("slab", (ns, self.in_units, self.units), torch.int32, dev)
         ops.conv_wgrad_generic(self.xq, self.x_kind == OUT_I16, self.gradq, d, slab, ns)
@@ -359,6 +396,15 @@ class Dense_q(Layer_q):
             ops.bias_grad(gsum, self.units, self.grad_range.desc, self.db)
         dx = self._c.get("dx", (d.N, self.in_units), torch.float32, dev)
         ops.conv_dgrad_generic(self.gradq, self.w_hwio, d, self.grad_range.desc, self.W_range.desc, dx)
+        return dx
+
+    def _backward_mfma(self, dev):
+        """dW (VALU, exact int64, reduce fused) and dX (int8 MFMA; int16 codes split hi/lo)."""
+        ops.dense_wgrad(self.xq, self.gradq, self.X_range.desc, self.grad_range.desc, self.W,
+                        ops.f32(2 * self.weight_decay), self.dW)
+        dx = self._c.get("dx", (self.d.N, self.in_units), torch.float32, dev)
+        ops.dense_gemm(self.gradq, self.wd, self.units, self.grad_range.desc, self.W_range.desc, dx,
+                       kernel="dense_dgrad_kernel")
         return dx
 
     def pre_dense_func(self, grad=None):

@@ -259,6 +259,31 @@ def conv_stem_wgrad(x16, gq, d, slab, nsplit):
         call("lbt_conv_stem_wgrad", ptr(x16), ptr(gq), d, ptr(slab), int(nsplit), stream())
 
 
+def stem_wide_ok(d, x_bits, w_bits):
+    """The wide fp16-MFMA stem (stem_wide.hip) takes this conv: the ImageNet conv1 shape class --
+    signed <= 9-bit image codes, K <= 480 patch elements, exact fp32 sums (K*2^(xb-1)*2^(wb-1) <= 2^24)."""
+    K = d.KH * d.KW * d.Cin
+    return (0 < K <= 480 and d.Cout % 16 == 0 and x_bits <= 9 and w_bits <= 8
+            and K * 2 ** (x_bits - 1) * 2 ** (w_bits - 1) <= 2 ** 24)
+
+
+def conv_stem_wide_fwd(x16, w_hwio, d, qx, qw, y):
+    M = d.N * d.Ho * d.Wo
+    with _Timed("stem_wide_fwd_kernel", x16.numel() * 2 + w_hwio.numel() + M * d.Cout * 4):
+        call("lbt_conv_stem_wide_fwd", ptr(x16), ptr(w_hwio), d, qx, qw, ptr(y), stream())
+
+
+def stem_wide_nsplit(d):
+    return int(_lib.load().lbt_stem_wide_nsplit(d))
+
+
+def conv_stem_wide_wgrad(x16, x_bits, g, d, slab, nsplit):
+    """int64 slab [nsplit][K][Cout], every element written; g int8 or int16 codes."""
+    with _Timed("stem_wide_wgrad_kernel", x16.numel() * 2 + g.numel() * g.element_size() + slab.numel() * 8):
+        call("lbt_conv_stem_wide_wgrad", ptr(x16), int(x_bits), ptr(g), int(g.dtype == torch.int16), d, ptr(slab),
+             int(nsplit), stream())
+
+
 # ----------------------------------------------------------------------------- BN chains
 def _chain_fwd_bytes(a):
     per = 0
@@ -336,7 +361,36 @@ def avgpool_bwd(g, dx, N, HW, C):
 
 def softmax_xent(z, labels, loss, dz):
     N, K = z.shape
+    if K > 64:  # wide heads: one wave per row (the narrow kernel keeps the fused head's order)
+        with _Timed("softmax_xent_wide_kernel", 8 * z.numel()):
+            call("lbt_softmax_xent_wide", ptr(z), ptr(labels), int(N), int(K), ptr(loss), ptr(dz), stream())
+        return
     call("lbt_softmax_xent", ptr(z), ptr(labels), int(N), int(K), ptr(loss), ptr(dz), stream())
+
+
+def dense_mfma_ok(in_units, units, x_bits, w_bits):
+    """Dense_q shapes the int8-MFMA dense kernels take (dense.hip)."""
+    return x_bits <= 8 and w_bits <= 8 and in_units % 8 == 0 and units % 8 == 0
+
+
+def dense_pack(w_hwio, wf, wd):
+    IN, OUT = w_hwio.shape
+    call("lbt_dense_pack", ptr(w_hwio), int(IN), int(OUT), ptr(wf), int(wf.shape[1]), ptr(wd), int(wd.shape[1]),
+         stream())
+
+
+def dense_gemm(a, b, kvalid, qa, qb, out, kernel="dense_gemm_kernel"):
+    rows, cols = out.shape
+    with _Timed(kernel, a.numel() * a.element_size() + b.numel() + 4 * out.numel()):
+        call("lbt_dense_gemm", ptr(a), int(a.dtype == torch.int16), int(a.shape[1]), int(kvalid), ptr(b),
+             int(b.shape[1]), int(rows), int(cols), qa, qb, ptr(out), stream())
+
+
+def dense_wgrad(xq, g, qx, qg, w, wd2, dw):
+    N, IN = xq.shape
+    with _Timed("dense_wgrad_kernel", xq.numel() + g.numel() * g.element_size() + 8 * w.numel()):
+        call("lbt_dense_wgrad", ptr(xq), ptr(g), int(g.dtype == torch.int16), int(N), int(IN), int(g.shape[1]), qx,
+             qg, ptr(w), wd2, ptr(dw), stream())
 
 
 def sgd_momentum(w, a, g, lr, mu, gscale=1.0):

@@ -88,11 +88,14 @@ def _batch(B, image, classes, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("grad_bits", [8, 16])
-@pytest.mark.parametrize("blocks,width,image", [((1, 1, 1, 1), 8, 32), ((2, 1, 1, 1), 16, 40)])
-def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, grad_bits):
-    ctx, gm, om = _pair(blocks, width, 10, image, grad_bits, seed=1)
+@pytest.mark.parametrize("blocks,width,image,classes", [((1, 1, 1, 1), 8, 32, 10), ((2, 1, 1, 1), 16, 40, 10),
+                                                        ((1, 1, 1, 1), 8, 32, 16)])
+def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, classes, grad_bits):
+    """classes=16: the fc runs on the int8-MFMA dense kernels (dense.hip), 10: the generic ones."""
+    ctx, gm, om = _pair(blocks, width, classes, image, grad_bits, seed=1)
+    assert gm.layers[-1].mfma == (classes % 8 == 0)
     oresnet.set_params(om, _params(gm))
-    x, y = _batch(4, image, 10, seed=2)
+    x, y = _batch(4, image, classes, seed=2)
     octx = onn.Ctx(oresnet.init_ranges(om), 0, ctx.seed)
     logits = gm.forward(torch.from_numpy(x).to(DEV))
     lr = om.forward(x, octx)
@@ -207,3 +210,111 @@ def test_wgrad_igemm_matches_generic(N, H, Cin, Cout, k, s):
             ref = torch.zeros((ns, K, Cout), dtype=torch.int32, device=DEV)
             ops.conv_wgrad_generic(x16, True, g, d, ref, ns)
         assert torch.equal(got, ref.to(torch.int64).sum(0)), g_i16
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,Cout,k,s", [(2, 32, 64, 7, 2), (1, 40, 16, 7, 2), (2, 23, 48, 5, 1), (1, 224, 64, 7, 2),
+                                          (3, 17, 32, 3, 2)])
+def test_stem_wide_matches_generic(N, H, Cout, k, s):
+    """The ImageNet conv1 on fp16 MFMA (stem_wide.hip: signed 9-bit image codes, K = k*k*3 patch
+    elements; 8- and 16-bit gradient codes split hi/lo) == the generic VALU kernels' exact integer
+    results, bit for bit, incl. ragged pixel tiles and SAME padding at both strides."""
+    from lbt_amd.dfxp import ops
+    from lbt_amd.runtime import DfxpContext
+    rng = np.random.default_rng(N * H + Cout + k)
+    ctx = DfxpContext(seed=0)
+    qx, qw, qg = ctx.quantizer("t/X", 9, 2), ctx.quantizer("t/W", 8, 0), ctx.quantizer("t/g", 16, -3)
+    d = ops.conv_desc(N, H, H, 3, Cout, k, k, s, s, "SAME")
+    assert ops.stem_wide_ok(d, 9, 8)
+    K = k * k * 3
+    W = torch.from_numpy(rng.uniform(-1, 1, size=(k, k, 3, Cout)).astype(np.float32)).to(DEV)
+    w_hwio = torch.empty((k, k, 3, Cout), dtype=torch.int8, device=DEV)
+    ops.quantize_weight(W, qw, w_hwio=w_hwio)
+    x = torch.from_numpy(rng.integers(-256, 256, size=(N, H, H, 3)).astype(np.int16)).to(DEV)
+    y1 = torch.empty((N, d.Ho, d.Wo, Cout), device=DEV)
+    y2 = torch.empty_like(y1)
+    ops.conv_stem_wide_fwd(x, w_hwio, d, qx.desc, qw.desc, y1)
+    ops.conv_fwd_generic(x, True, w_hwio, d, qx.desc, qw.desc, y2)
+    assert torch.equal(y1, y2)
+    for g_i16 in (0, 1):
+        if g_i16:
+            g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, d.Ho, d.Wo, Cout)).astype(np.int16)).to(DEV)
+        else:
+            g = torch.from_numpy(rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout)).astype(np.int8)).to(DEV)
+        ns = ops.stem_wide_nsplit(d)
+        slab = torch.full((ns, K, Cout), 7, dtype=torch.int64, device=DEV)  # fully overwritten
+        ops.conv_stem_wide_wgrad(x, 9, g, d, slab, ns)
+        nr = ops.wgrad_nsplit(d, generic=True)
+        if g_i16:
+            ref = torch.zeros((nr, K, Cout), dtype=torch.int64, device=DEV)
+            ops.conv_wgrad_generic16(x, True, g, d, ref, nr)
+        else:
+            ref = torch.zeros((nr, K, Cout), dtype=torch.int32, device=DEV)
+            ops.conv_wgrad_generic(x, True, g, d, ref, nr)
+        assert torch.equal(slab.sum(0), ref.to(torch.int64).sum(0)), g_i16
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,IN,OUT", [(32, 2048, 1000), (3, 128, 40), (17, 64, 8)])
+def test_dense_mfma_matches_generic(N, IN, OUT):
+    """Dense_q on int8 MFMA (fwd; dgrad with int8 and hi/lo-split int16 gradient codes) and the
+    fused-reduce VALU wgrad == the generic kernels + reduce, bit for bit."""
+    from lbt_amd import _lib
+    from lbt_amd.dfxp import ops
+    from lbt_amd.runtime import DfxpContext
+    rng = np.random.default_rng(N + IN + OUT)
+    ctx = DfxpContext(seed=0)
+    qx, qw, qg = ctx.quantizer("t/X", 8, 2), ctx.quantizer("t/W", 8, 0), ctx.quantizer("t/g", 16, -3)
+    d = _lib.ConvDesc(N, 1, 1, IN, OUT, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
+    W = torch.from_numpy(rng.uniform(-1, 1, size=(IN, OUT)).astype(np.float32)).to(DEV)
+    w_hwio = torch.empty((IN, OUT), dtype=torch.int8, device=DEV)
+    ops.quantize_weight(W, qw, w_hwio=w_hwio)
+    wf = torch.full((OUT, -(-IN // 64) * 64), 5, dtype=torch.int8, device=DEV)
+    wd = torch.full((IN, -(-OUT // 64) * 64), 5, dtype=torch.int8, device=DEV)
+    ops.dense_pack(w_hwio, wf, wd)
+    x = torch.from_numpy(rng.integers(-128, 128, size=(N, IN)).astype(np.int8)).to(DEV)
+    y1, y2 = torch.empty((N, OUT), device=DEV), torch.empty((N, OUT), device=DEV)
+    ops.dense_gemm(x, wf, IN, qx.desc, qw.desc, y1)
+    ops.conv_fwd_generic(x, False, w_hwio, d, qx.desc, qw.desc, y2)
+    assert torch.equal(y1, y2)
+    wd2 = ops.f32(2 * 1e-4)
+    for g16 in (0, 1):
+        if g16:
+            g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, OUT)).astype(np.int16)).to(DEV)
+        else:
+            g = torch.from_numpy(rng.integers(-128, 128, size=(N, OUT)).astype(np.int8)).to(DEV)
+        dx1, dx2 = torch.empty((N, IN), device=DEV), torch.empty((N, IN), device=DEV)
+        ops.dense_gemm(g, wd, OUT, qg.desc, qw.desc, dx1)
+        (ops.conv_dgrad_generic16 if g16 else ops.conv_dgrad_generic)(g, w_hwio, d, qg.desc, qw.desc, dx2)
+        assert torch.equal(dx1, dx2), g16
+        dw1, dw2 = torch.empty_like(W), torch.empty_like(W)
+        ops.dense_wgrad(x, g, qx.desc, qg.desc, W, wd2, dw1)
+        ns = ops.wgrad_nsplit(d, generic=True)
+        slab = torch.zeros((ns, IN, OUT), dtype=torch.int64 if g16 else torch.int32, device=DEV)
+        if g16:
+            ops.conv_wgrad_generic16(x, False, g, d, slab, ns)
+            ops.conv_wgrad_reduce64(slab, ns, IN, OUT, qx.desc, qg.desc, W, wd2, dw2)
+        else:
+            ops.conv_wgrad_generic(x, False, g, d, slab, ns)
+            ops.conv_wgrad_reduce(slab, ns, IN, OUT, 0, None, qx.desc, qg.desc, W, wd2, dw2)
+        assert torch.equal(dw1, dw2), g16
+
+
+@pytest.mark.gpu
+def test_softmax_xent_wide():
+    """The wide-K softmax-CE (one wave per row) against float64 numpy: loss and d loss / d z."""
+    from lbt_amd.dfxp import ops
+    rng = np.random.default_rng(5)
+    z = (rng.normal(size=(32, 1000)) * 4).astype(np.float32)
+    y = rng.integers(0, 1000, size=32).astype(np.int32)
+    loss = torch.empty(1, device=DEV)
+    dz = torch.empty((32, 1000), device=DEV)
+    ops.softmax_xent(torch.from_numpy(z).to(DEV), torch.from_numpy(y).to(DEV), loss, dz)
+    zd = z.astype(np.float64)
+    m = zd.max(1, keepdims=True)
+    p = np.exp(zd - m) / np.exp(zd - m).sum(1, keepdims=True)
+    want_loss = np.mean(-np.log(p[np.arange(32), y]))
+    onehot = np.zeros_like(p)
+    onehot[np.arange(32), y] = 1
+    assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss)
+    assert np.allclose(dz.cpu().numpy(), (p - onehot) / 32, rtol=1e-5, atol=1e-9)
