@@ -355,6 +355,21 @@ int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R, const floa
 int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qdesc qn_q, const float* ms,
                       const int64_t* sums, int64_t n, float* dx, int64_t rows, int32_t C, void* stream);
 
+/* The same passes as one bottleneck block's fused backward runs them (ResidualBottleneck_q,
+ * SURVEY 8(f) rank 1): pass A with the ReLU_q mask folded in -- y_mask > 0, or mask_r: the
+ * forward chain's pre-ReLU value ((float)R * s_qr) * gb[c] + gb[C+c] > 0 recomputed from the R
+ * codes (gb = [gamma_q | beta_q], also the gamma_q of the rescale part) -- and the masked fp32
+ * gradient optionally stored (gmask_out: the identity shortcut's gradient); pass B with dx fed
+ * straight into the consuming conv's 9..16-bit gradient quantiser qo (int16 codes gq, overflow
+ * counters, noise period inner) instead of storing dx. Bit-identical to the unfused sequence. */
+int lbt_bn_bwd_a_wide_masked(const float* g, const float* y_mask, int32_t mask_r, lbt_qdesc qr, const float* gb,
+                             float* gmask_out, lbt_qdesc qrg, const int8_t* R, lbt_qdesc qng, const int8_t* qn,
+                             int16_t* gout, float* dout, int64_t* sums, int64_t rows, int64_t inner, int32_t C,
+                             void* stream);
+int lbt_bn_bwd_b_wide_q(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qdesc qn_q, const float* ms,
+                        const int64_t* sums, int64_t n, int16_t* gq, lbt_qdesc qo, int64_t rows, int64_t inner,
+                        int32_t C, void* stream);
+
 /* Rescale_q parameter gradients (:689-690) from pass-A sums:
  * dgamma = (float)((double)sum(G2*R) * sg2*sr) + wd2*gamma,  dbeta = (float)((double)sum G2 * sg2). */
 int lbt_bn_param_grads(const int64_t* sums, int32_t C, lbt_qdesc qrg, lbt_qdesc qr,

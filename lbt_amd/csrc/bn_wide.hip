@@ -27,6 +27,14 @@ struct WideA {
   int64_t* sums;         // [NSHARD][4C]: S(G2 R), S(G2), S(G), S(G qn)
   int64_t rows, inner;
   int C, rpb;            // rows per workgroup
+  // ReLU mask on the incoming gradient (ReLU_q backward): from the forward output y_mask > 0, or
+  // (mask_r) recomputed from the R codes as the forward chain's pre-ReLU value
+  // ((float)R * s_r) * gb[c] + gb[C + c] > 0; the masked gradient optionally out (gmask_out).
+  const float* y_mask;
+  int mask_r;
+  lbt_qdesc qr;          // the R codes' quantiser (mask_r)
+  const float* gb;       // [gamma_q | beta_q] (mask_r)
+  float* gmask_out;
 };
 
 // Thread = 4 consecutive channels (one Philox4x32 call covers their 4 noise values) x one row lane.
@@ -42,9 +50,13 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
   const QState srg = qstate(a.qrg), sng = qstate(a.qng);
   const int64_t r0 = (int64_t)blockIdx.y * a.rpb;
   const int64_t r1 = r0 + a.rpb < a.rows ? r0 + a.rpb : a.rows;
-  float gam[4];
+  float gam[4], bet[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) gam[k] = (cv && a.gamma_q) ? a.gamma_q[c0 + k] : 0.f;
+  for (int k = 0; k < 4; ++k) {
+    gam[k] = (cv && a.gamma_q) ? a.gamma_q[c0 + k] : 0.f;
+    bet[k] = (cv && a.mask_r) ? a.gb[a.C + c0 + k] : 0.f;
+  }
+  const float sr = a.mask_r ? qstate(a.qr).inv_m : 0.f;
   long long s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0};
   int o1 = 0, o2 = 0, p1 = 0, p2 = 0;
   if (cv) {
@@ -53,6 +65,23 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
       const uint64_t blk = (uint64_t)(e % a.inner) >> 2;  // inner % 4 == 0
       const float4 gv = *reinterpret_cast<const float4*>(a.g + e);
       float d[4] = {gv.x, gv.y, gv.z, gv.w};
+      if (a.y_mask) {
+        const float4 ym = *reinterpret_cast<const float4*>(a.y_mask + e);
+        const float m[4] = {ym.x, ym.y, ym.z, ym.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = m[k] > 0.f ? d[k] : 0.f;
+      } else if (a.mask_r) {
+        const char4 rv = *reinterpret_cast<const char4*>(a.R + e);
+        const int R[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // bn.hip chain_bwd_a's recomputation, op for op
+          const float xr = (float)R[k] * sr;
+          const float m1 = xr * gam[k];
+          const float yv = m1 + bet[k];
+          d[k] = yv > 0.f ? d[k] : 0.f;
+        }
+      }
+      if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(d[0], d[1], d[2], d[3]);
       if (srg.active) {
         const Noise4 nz = a.qrg.stochastic ? qnoise4(a.qrg, srg.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
         const char4 rv = *reinterpret_cast<const char4*>(a.R + e);
@@ -121,13 +150,20 @@ struct WideB {
   float* dx;
   int64_t rows;
   int C, rpb;
+  // optional: the consuming conv's gradient quantiser applied to dx (int16 codes, Conv2d_q
+  // :299-300 at 9..16 bits) instead of storing dx; inner = per-sample elements (noise period)
+  int16_t* gq;
+  lbt_qdesc qo;
+  int64_t inner;
 };
 
 __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
   __shared__ float s_mg[kCB], s_mgx[kCB];
+  __shared__ int sh_cnt[2 * (kT / 64)];
   const int cq = threadIdx.x % kCQ, rl = threadIdx.x / kCQ;
   const int c0 = blockIdx.x * kCB + 4 * cq;
-  const QState sgq = qstate(b.qng), sn = qstate(b.qn_q);
+  const QState sgq = qstate(b.qng), sn = qstate(b.qn_q), so = qstate(b.qo);
+  const bool quant = b.gq != nullptr;
   if (threadIdx.x < kCB && blockIdx.x * kCB + (int)threadIdx.x < b.C) {
     // bn.hip chain_bwd_b's moment prologue, for this workgroup's channels
     const int c = blockIdx.x * kCB + threadIdx.x;
@@ -142,7 +178,11 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
     s_mgx[threadIdx.x] = (float)(gsc * (s * (double)SGQ - (double)m * (double)SG) / (n * (double)sig));
   }
   __syncthreads();
-  if (c0 >= b.C) return;
+  int o1 = 0, o2 = 0;
+  if (c0 >= b.C) {
+    if (quant) block_flush_counts(b.qo, o1, o2, sh_cnt);  // every thread takes part in the flush
+    return;
+  }
   float mu[4], sig[4], mg[4], mgx[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -169,8 +209,20 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
       const float t2 = xh * mgx[k];
       o[k] = (t1 - t2) / sig[k];
     }
-    *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0], o[1], o[2], o[3]);
+    if (quant) {
+      const uint64_t blk = (uint64_t)(e % b.inner) >> 2;  // inner % 4 == 0
+      const Noise4 nz = b.qo.stochastic ? qnoise4(b.qo, so.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+      short4 v;
+      v.x = (short)quant1(so, b.qo.stochastic, o[0], nz.u[0], o1, o2);
+      v.y = (short)quant1(so, b.qo.stochastic, o[1], nz.u[1], o1, o2);
+      v.z = (short)quant1(so, b.qo.stochastic, o[2], nz.u[2], o1, o2);
+      v.w = (short)quant1(so, b.qo.stochastic, o[3], nz.u[3], o1, o2);
+      *reinterpret_cast<short4*>(b.gq + e) = v;
+    } else {
+      *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0], o[1], o[2], o[3]);
+    }
   }
+  if (quant) block_flush_counts(b.qo, o1, o2, sh_cnt);
 }
 
 // ~512 workgroups in all
@@ -189,7 +241,7 @@ extern "C" int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R,
                                  int64_t inner, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gamma_q)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
-  WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0};
+  WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0, nullptr, 0, lbt_qdesc{}, nullptr, nullptr};
   const int cb = (C + kCB - 1) / kCB;
   a.rpb = rows_per_block(rows, cb);
   const int64_t yb = (rows + a.rpb - 1) / a.rpb;
@@ -201,7 +253,41 @@ extern "C" int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R,
 extern "C" int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qdesc qn_q, const float* ms,
                                  const int64_t* sums, int64_t n, float* dx, int64_t rows, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || !G || !qn || !ms || !sums || !dx) return LBT_EINVAL;
-  WideB b{G, qng, qn, qn_q, ms, sums, n, dx, rows, C, 0};
+  WideB b{G, qng, qn, qn_q, ms, sums, n, dx, rows, C, 0, nullptr, lbt_qdesc{}, 1};
+  const int cb = (C + kCB - 1) / kCB;
+  b.rpb = rows_per_block(rows, cb);
+  const int64_t yb = (rows + b.rpb - 1) / b.rpb;
+  if (yb > 65535) return LBT_EINVAL;
+  hipLaunchKernelGGL(bn_bwd_b_wide_kernel, dim3((unsigned)cb, (unsigned)yb), dim3(kT), 0, (hipStream_t)stream, b);
+  return (int)hipGetLastError();
+}
+
+// Pass A with the ReLU mask folded in (y_mask, or mask_r: recomputed from R with qr and
+// gb = [gamma_q | beta_q]) and the masked gradient optionally stored (gmask_out).
+extern "C" int lbt_bn_bwd_a_wide_masked(const float* g, const float* y_mask, int32_t mask_r, lbt_qdesc qr,
+                                        const float* gb, float* gmask_out, lbt_qdesc qrg, const int8_t* R,
+                                        lbt_qdesc qng, const int8_t* qn, int16_t* gout, float* dout, int64_t* sums,
+                                        int64_t rows, int64_t inner, int32_t C, void* stream) {
+  if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
+  if ((qrg.bits > 0 && (!R || !gb)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
+  if (mask_r && (y_mask || !R || !gb || qr.bits <= 0)) return LBT_EINVAL;
+  WideA a{g, qrg, R, gb, qng, qn, gout, dout, sums, rows, inner, C, 0, y_mask, mask_r, qr, gb, gmask_out};
+  const int cb = (C + kCB - 1) / kCB;
+  a.rpb = rows_per_block(rows, cb);
+  const int64_t yb = (rows + a.rpb - 1) / a.rpb;
+  if (yb > 65535) return LBT_EINVAL;
+  hipLaunchKernelGGL(bn_bwd_a_wide_kernel, dim3((unsigned)cb, (unsigned)yb), dim3(kT), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// Pass B whose dx goes straight into the consuming conv's 9..16-bit gradient quantiser: gq int16
+// codes [rows][C] + that quantiser's overflow counters (noise period inner), no fp32 dx.
+extern "C" int lbt_bn_bwd_b_wide_q(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qdesc qn_q, const float* ms,
+                                   const int64_t* sums, int64_t n, int16_t* gq, lbt_qdesc qo, int64_t rows,
+                                   int64_t inner, int32_t C, void* stream) {
+  if (rows <= 0 || C <= 0 || C % 4 || !G || !qn || !ms || !sums || !gq || inner <= 0 || inner % C) return LBT_EINVAL;
+  if (qo.bits <= 0 || qo.bits > 16 || (qo.stochastic && !qo.step && !qo.noise)) return LBT_EINVAL;
+  WideB b{G, qng, qn, qn_q, ms, sums, n, nullptr, rows, C, 0, gq, qo, inner};
   const int cb = (C + kCB - 1) / kCB;
   b.rpb = rows_per_block(rows, cb);
   const int64_t yb = (rows + b.rpb - 1) / b.rpb;

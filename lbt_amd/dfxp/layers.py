@@ -15,6 +15,8 @@ Differences from TF (documented in DESIGN.md):
 * ``Conv2d_q(..., input_nonnegative=True)`` declares a post-ReLU input: its (bits+1)-bit codes
   are unsigned and take the int8 MFMA path; otherwise the signed codes take the VALU path.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -164,6 +166,31 @@ class Conv2d_q(Layer_q):
         ops.conv_stem_wide_wgrad(self.xq, self.X_range.bits, self.gradq, d, slab, ns)
         ops.conv_wgrad_reduce64(slab, ns, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
                                 ops.f32(2 * self.weight_decay), self.dW)
+
+    def fwd_codes(self, xq, N, H, W):
+        """Forward from X codes the caller already quantised with self.X_range (offset int8,
+        x_kind U8OFF): the LDS-tiled int8-MFMA implicit GEMM -> fp32 y (a fused block's conv)."""
+        kh, kw, Cin, Cout = self.ksize
+        self.d = d = ops.conv_desc(N, H, W, Cin, Cout, kh, kw, self.strides[1], self.strides[2], self.padding)
+        self.xq = xq
+        self.quantize_weights()
+        y = self._c.get("y", (N, d.Ho, d.Wo, Cout), torch.float32, xq.device)
+        ops.conv_fwd_igemm(xq, 1, self.wf, self.ksf, d, self.X_range.desc, self.W_range.desc, y)
+        self.y = y
+        return y
+
+    def bwd_codes16(self, gq16, add_src=None):
+        """Backward from int16 gradient codes the caller already quantised with self.grad_range:
+        wide MFMA wgrad (+ reduce) and dgrad (dx + add_src, the other branch's gradient)."""
+        self.gradq = gq16
+        self._wgrad_igemm(1)
+        if not self.need_input_grad:
+            return None
+        d = self.d
+        dx = self._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, gq16.device)
+        ops.conv_dgrad_igemm(gq16, 1, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx,
+                             add_src=add_src)
+        return dx
 
     def quantize_weights(self):
         ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio,
@@ -778,6 +805,148 @@ class ResidualBottleneck_q(ResidualBlock_q):
             )
         self.relu = ReLU_q()
         self._c = _Cache()
+
+
+    # ---- fused execution of the block (bit-identical to the Sequential_q composition above)
+    def _fusable(self):
+        """16-bit gradients (config 4) and every conv on the wide MFMA kernels with offset int8 X
+        codes: then forward / backward run the block as one fused kernel schedule."""
+        if getattr(self, "_fuse", None) is None:
+            r = self.residual.layers
+            if len(r) != 8 or not isinstance(r[1], BatchNorm_q):
+                self._fuse = False
+            else:
+                convs = [r[0], r[3], r[6]] + ([self.shortcut.layers[0]] if self.shortcut.layers else [])
+                self._fuse = (os.environ.get("LBT_FUSE_BOTTLENECK", "1") == "1"
+                              and all(c.grad_bits > 8 and c.x_kind == OUT_U8OFF and c.igemm_f and c.igemm_d
+                                      and c.igemm_w and not c.use_bias for c in convs))
+        return self._fuse
+
+    def forward(self, X):
+        if not self._fusable():
+            return super().forward(X)
+        return self._forward_fused(X)
+
+    def backward(self, grad, stochastic=True):
+        if not self._fusable():
+            return super().backward(grad, stochastic)
+        return self._backward_fused(grad)
+
+    @staticmethod
+    def _chain(c, bn, y, relu, res=None, bn2=None, out=None, o1=None, o1_conv=None, o2=None, o2_conv=None):
+        """One forward element chain: bn (norm of its input codes -> rescale quantiser ->
+        affine) [+ bn2 | + res] [-> ReLU] -> fp32 out and / or the next convs' X codes."""
+        a = ChainFwd()
+        for br, b in ((a.b1, bn), (a.b2, bn2)):
+            if b is None:
+                continue
+            n, r = b.layers
+            r.quantize_params()
+            r.X_range.observe(y.numel())
+            br.nrm = n.norm_desc(n.q, n._chsum, n.n)
+            br.qr = r.X_range.desc
+            br.rout = r.R.data_ptr()
+            br.gb = r.gb.data_ptr()
+        a.has_b2 = int(bn2 is not None)
+        a.res = res.data_ptr() if res is not None else None
+        a.relu = int(relu)
+        a.y = out.data_ptr() if out is not None else None
+        if o1 is not None:
+            o1_conv.X_range.observe(y.numel())
+            a.o1, a.o1_kind, a.qo1 = o1.data_ptr(), OUT_U8OFF, o1_conv.X_range.desc
+        if o2 is not None:
+            o2_conv.X_range.observe(y.numel())
+            a.o2, a.o2_kind, a.qo2 = o2.data_ptr(), OUT_U8OFF, o2_conv.X_range.desc
+        a.rows, a.inner = ops.rows_inner(tuple(y.shape))
+        a.C = y.shape[-1]
+        ops.chain_fwd(a)
+
+    @staticmethod
+    def _norm_in(bn, y, ctx):
+        """Normalization_q's input quantiser on a conv output (codes + exact channel sums) and
+        the Rescale_q code buffer the chain will fill."""
+        n, r = bn.layers
+        C = y.shape[-1]
+        n._chsum = n._c.sums("chsum", ops.NSHARD * 2 * C, ctx)
+        n.q = ops.quantize(y, n.X_range, OUT_I8, out=n._c.get("q", y.shape, torch.int8, y.device), chsum=n._chsum, C=C)
+        n.n = y.numel() // C
+        r.R = r._c.get("R", y.shape, torch.int8, y.device)
+
+    def _forward_fused(self, X):
+        """conv-1 -> [bn1 + ReLU + conv-2's X quantiser] -> conv-2 -> [bn2 + ReLU + conv-3's X
+        quantiser] -> conv-3 (+ shortcut conv) -> [bn3 (+ shortcut bn | + X) + ReLU]: 3 element
+        chains instead of 9 element layers (dynamic_fixed_point.py:858-862, :878-980)."""
+        r = self.residual.layers
+        c1, bn1, c2, bn2, c3, bn3 = r[0], r[1], r[3], r[4], r[6], r[7]
+        sc = self.shortcut.layers
+        ctx = c1.ctx
+        self.X = X
+        N, H, W, _ = X.shape
+        dev = X.device
+        x1 = ops.quantize(X, c1.X_range, OUT_U8OFF, out=self._c.get("x1", X.shape, torch.int8, dev))
+        xs = (ops.quantize(X, sc[0].X_range, OUT_U8OFF, out=self._c.get("xs", X.shape, torch.int8, dev))
+              if sc else None)
+        y1 = c1.fwd_codes(x1, N, H, W)
+        self._norm_in(bn1, y1, ctx)
+        x2 = self._c.get("x2", y1.shape, torch.int8, dev)
+        self._chain(c1, bn1, y1, True, o1=x2, o1_conv=c2)
+        y2 = c2.fwd_codes(x2, N, y1.shape[1], y1.shape[2])
+        self._norm_in(bn2, y2, ctx)
+        x3 = self._c.get("x3", y2.shape, torch.int8, dev)
+        self._chain(c2, bn2, y2, True, o1=x3, o1_conv=c3)
+        y3 = c3.fwd_codes(x3, N, y2.shape[1], y2.shape[2])
+        self._norm_in(bn3, y3, ctx)
+        out = self._c.get("y", y3.shape, torch.float32, dev)
+        if sc:
+            ys = sc[0].fwd_codes(xs, N, H, W)
+            self._norm_in(sc[1], ys, ctx)
+            self._chain(c3, bn3, y3, True, bn2=sc[1], out=out)
+        else:
+            self._chain(c3, bn3, y3, True, res=X, out=out)
+        self.y = out
+        return out
+
+    @staticmethod
+    def _bn_bwd(bn, conv_out, g, ctx, y_mask=None, mask_r=False, gmask_out=None, into=None):
+        """One BN's backward with the ReLU mask in front (pass A: rescale + norm gradient
+        quantisers, dgamma / dbeta), then pass B straight into the producing conv's 16-bit
+        gradient quantiser: returns that conv's int16 gradient codes."""
+        n, r = bn.layers
+        C = g.shape[-1]
+        rows, inner = g.numel() // C, g.numel() // g.shape[0]
+        dev = g.device
+        sums = r._c.sums("fsums", ops.NSHARD * 4 * C, ctx)
+        r.grad_range.observe(g.numel())
+        n.grad_range.observe(g.numel())
+        G16 = n._c.get("G16", g.shape, torch.int16, dev)
+        ops.bn_bwd_a_wide_masked(g, y_mask, mask_r, r.X_range.desc, r.gb, gmask_out, r.grad_range.desc, r.R,
+                                 n.grad_range.desc, n.q, G16, sums, rows, inner, C)
+        ops.bn_param_grads(sums, C, r.grad_range.desc, r.X_range.desc, r.gamma, ops.f32(2 * r.weight_decay),
+                           r.dgamma, r.dbeta)
+        conv_out.grad_range.observe(g.numel())
+        gq = conv_out._c.get("gq16", g.shape, torch.int16, dev)
+        ops.bn_bwd_b_wide_q(G16, n.grad_range.desc, n.q, n.X_range.desc, n.ms, sums, n.n, gq,
+                            conv_out.grad_range.desc, rows, inner, C)
+        return gq
+
+    def _backward_fused(self, grad):
+        r = self.residual.layers
+        c1, bn1, c2, bn2, c3, bn3 = r[0], r[1], r[3], r[4], r[6], r[7]
+        sc = self.shortcut.layers
+        ctx = c1.ctx
+        dev = grad.device
+        # block ReLU mask from the block output; bn3 (and the shortcut bn) see the same masked g
+        gmask = None if sc else self._c.get("gmask", grad.shape, torch.float32, dev)
+        g3 = self._bn_bwd(bn3, c3, grad, ctx, y_mask=self.y, gmask_out=gmask)
+        gs = self._bn_bwd(sc[1], sc[0], grad, ctx, y_mask=self.y) if sc else None
+        d3 = c3.bwd_codes16(g3)
+        g2 = self._bn_bwd(bn2, c2, d3, ctx, mask_r=True)
+        d2 = c2.bwd_codes16(g2)
+        g1 = self._bn_bwd(bn1, c1, d2, ctx, mask_r=True)
+        if sc:
+            ds = sc[0].bwd_codes16(gs)
+            return c1.bwd_codes16(g1, add_src=ds)
+        return c1.bwd_codes16(g1, add_src=gmask)
 
 
 class MaxPool_q(Layer_q):

@@ -477,6 +477,19 @@ def bn_bwd_b_wide(G, qng, qn, qn_q, ms, sums, n, dx, rows, C):
 
 
 # ---------------------------------------------------------------- wide layers (igemm.hip)
+def bn_bwd_a_wide_masked(g, y_mask, mask_r, qr, gb, gmask_out, qrg, R, qng, qn, gout, sums, rows, inner, C):
+    with _Timed("bn_bwd_a_wide_kernel", g.numel() * (4 + 1 + 1 + 2) + (4 * g.numel() if y_mask is not None else 0)
+                + (4 * g.numel() if gmask_out is not None else 0)):
+        call("lbt_bn_bwd_a_wide_masked", ptr(g), ptr(y_mask), int(mask_r), qr, ptr(gb), ptr(gmask_out), qrg, ptr(R),
+             qng, ptr(qn), ptr(gout), None, ptr(sums), int(rows), int(inner), int(C), stream())
+
+
+def bn_bwd_b_wide_q(G, qng, qn, qn_q, ms, sums, n, gq, qo, rows, inner, C):
+    with _Timed("bn_bwd_b_wide_kernel", G.numel() * (2 + 1 + 2)):
+        call("lbt_bn_bwd_b_wide_q", ptr(G), qng, ptr(qn), qn_q, ptr(ms), ptr(sums), int(n), ptr(gq), qo, int(rows),
+             int(inner), int(C), stream())
+
+
 def igemm_ok(c_gather, c_out):
     """Shapes the LDS-tiled MFMA implicit GEMM takes: gathered channels % 64, outputs % 16."""
     return c_gather % 64 == 0 and c_out % 16 == 0

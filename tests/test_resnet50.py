@@ -89,11 +89,16 @@ def _batch(B, image, classes, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("grad_bits", [8, 16])
 @pytest.mark.parametrize("blocks,width,image,classes", [((1, 1, 1, 1), 8, 32, 10), ((2, 1, 1, 1), 16, 40, 10),
-                                                        ((1, 1, 1, 1), 8, 32, 16)])
+                                                        ((1, 1, 1, 1), 8, 32, 16), ((2, 1, 1, 1), 64, 32, 16)])
 def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, classes, grad_bits):
-    """classes=16: the fc runs on the int8-MFMA dense kernels (dense.hip), 10: the generic ones."""
+    """classes=16: the fc runs on the int8-MFMA dense kernels (dense.hip), 10: the generic ones.
+    width 64 with 16-bit gradients: every bottleneck runs fused (ResidualBottleneck_q._fusable)."""
+    from lbt_amd.dfxp.layers import ResidualBottleneck_q
     ctx, gm, om = _pair(blocks, width, classes, image, grad_bits, seed=1)
     assert gm.layers[-1].mfma == (classes % 8 == 0)
+    blocks_ = [l for l in gm.layers if isinstance(l, ResidualBottleneck_q)]
+    if width % 64 == 0:
+        assert all(b._fusable() == (grad_bits > 8) for b in blocks_)
     oresnet.set_params(om, _params(gm))
     x, y = _batch(4, image, classes, seed=2)
     octx = onn.Ctx(oresnet.init_ranges(om), 0, ctx.seed)
