@@ -441,6 +441,14 @@ typedef struct lbt_wjob {
 } lbt_wjob;
 int lbt_dfxp_quantize_weights(const lbt_wjob* jobs, int32_t njobs, int32_t max_cout, void* stream);
 
+/* The same for wide layers, element-parallel (coalesced float4 loads, one Philox call per 4
+ * noise indices): every job's Cout % 4 == 0, w 16-byte aligned, colsum unused (NULL). Block
+ * ranges: job j owns blocks [starts[j], starts[j+1]) of the 1-D grid (starts in device memory,
+ * starts[0] = 0, starts[njobs] = total_blocks), lbt_flat_weight_blocks(KH*KW*Cin*Cout) each. */
+int lbt_flat_weight_blocks(int64_t n);
+int lbt_dfxp_quantize_weights_flat(const lbt_wjob* jobs, const int32_t* starts, int32_t njobs, int32_t total_blocks,
+                                   void* stream);
+
 /* lbt_dfxp_quantize (generic path) for many small tensors (Rescale_q gamma / beta, :679-682). */
 typedef struct lbt_qjob {
   const float* x; void* out; int32_t out_kind; int64_t n, inner; lbt_qdesc q;

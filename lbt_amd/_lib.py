@@ -151,6 +151,8 @@ _SIGS = {
     "lbt_stem_wide_nsplit": [ConvDesc],
     "lbt_conv_stem_wide_wgrad": [_P, c_int32, _P, c_int32, ConvDesc, _P, c_int32, _P],
     "lbt_dense_pack": [_P, c_int32, c_int32, _P, c_int32, _P, c_int32, _P],
+    "lbt_flat_weight_blocks": [c_int64],
+    "lbt_dfxp_quantize_weights_flat": [_P, _P, c_int32, c_int32, _P],
     "lbt_bn_bwd_a_wide_masked": [_P, _P, c_int32, QDesc, _P, _P, QDesc, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64,
                                  c_int32, _P],
     "lbt_bn_bwd_b_wide_q": [_P, QDesc, _P, QDesc, _P, _P, c_int64, _P, QDesc, c_int64, c_int64, c_int32, _P],

@@ -280,6 +280,69 @@ extern "C" int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_
   return (int)hipGetLastError();
 }
 
+namespace {
+
+// Element-parallel form of quantize_weights_block for wide layers (ResNet-50: 23.5 M weights in
+// 54 tensors): block b of the 1-D grid takes 1024 consecutive HWIO elements of the job whose range
+// [starts[j], starts[j+1]) holds b; a thread quantises 4 consecutive elements (one float4 load,
+// one Philox call for their 4 noise indices: Cout % 4 == 0 keeps them in one noise block) and
+// writes them to every image. Same codes and counters as quantize_weights_block; no column sums.
+constexpr int kFlatPerBlock = 4 * kThreads;
+
+__global__ __launch_bounds__(kThreads) void quantize_weights_flat_kernel(const lbt_wjob* __restrict__ jobs,
+                                                                         const int32_t* __restrict__ starts,
+                                                                         int njobs) {
+  __shared__ int sh_cnt[2 * kThreads / 64];
+  const int b = (int)blockIdx.x;
+  int jlo = 0, jhi = njobs;  // starts[jlo] <= b < starts[jhi]
+  while (jhi - jlo > 1) {
+    const int mid = (jlo + jhi) >> 1;
+    if (starts[mid] <= b) jlo = mid; else jhi = mid;
+  }
+  const lbt_wjob j = jobs[jlo];
+  const QState s = qstate(j.q);
+  const int64_t n = (int64_t)j.KH * j.KW * j.Cin * j.Cout;
+  const int64_t inner = (int64_t)j.KW * j.Cin * j.Cout;
+  const int csi = (j.Cin + 15) / 16, cso = (j.Cout + 15) / 16;
+  const int64_t idx = ((int64_t)(b - starts[jlo]) * kFlatPerBlock) + 4 * threadIdx.x;
+  int ov1 = 0, ov2 = 0;
+  if (idx < n) {
+    const float4 wv = *reinterpret_cast<const float4*>(j.w + idx);
+    const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+    const Noise4 nz = j.q.stochastic ? qnoise4(j.q, s.step, (uint64_t)((idx % inner) >> 2)) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+    int c[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c[e] = quant1(s, j.q.stochastic, w4[e], nz.u[e], ov1, ov2);
+    if (j.w_hwio) {
+      char4 v;
+      v.x = (char)c[0]; v.y = (char)c[1]; v.z = (char)c[2]; v.w = (char)c[3];
+      *reinterpret_cast<char4*>(j.w_hwio + idx) = v;
+    }
+    const int64_t k = idx / j.Cout;
+    const int co0 = (int)(idx - k * j.Cout);
+    const int tap = (int)(k / j.Cin), ci = (int)(k - (int64_t)tap * j.Cin);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int co = co0 + e;
+      if (j.wf) j.wf[((int64_t)co * j.ksf + tap * csi + ci / 16) * 16 + (ci & 15)] = (int8_t)c[e];
+      if (j.wd) j.wd[((int64_t)ci * j.ksd + tap * cso + co / 16) * 16 + (co & 15)] = (int8_t)c[e];
+    }
+  }
+  block_flush_counts(j.q, ov1, ov2, sh_cnt);
+}
+
+}  // namespace
+
+extern "C" int lbt_flat_weight_blocks(int64_t n) { return (int)((n + kFlatPerBlock - 1) / kFlatPerBlock); }
+
+extern "C" int lbt_dfxp_quantize_weights_flat(const lbt_wjob* jobs, const int32_t* starts, int32_t njobs,
+                                              int32_t total_blocks, void* stream) {
+  if (njobs <= 0 || total_blocks <= 0) return LBT_OK;
+  hipLaunchKernelGGL(quantize_weights_flat_kernel, dim3((unsigned)total_blocks), dim3(kThreads), 0,
+                     (hipStream_t)stream, jobs, starts, njobs);
+  return (int)hipGetLastError();
+}
+
 extern "C" int lbt_dfxp_quantize_weights(const lbt_wjob* jobs, int32_t njobs, int32_t max_cout, void* stream) {
   if (njobs <= 0) return LBT_OK;
   if (njobs > 65535 || max_cout <= 0) return LBT_EINVAL;

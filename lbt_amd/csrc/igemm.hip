@@ -185,6 +185,17 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
     const int col = n0 + wn * 64 + j * 16 + r;
     if (col >= p.ncol) continue;
     const long long wsum = want_w ? (long long)accw[j][0] : 0;  // every row of accw holds sum_k W[col][k]
+    // dgrad addend: all 16 loads of this column issued before any store (p.y may alias it as far
+    // as the compiler knows, so interleaved load / store pairs would serialise)
+    float av[4][4];
+    const bool addv = MODE == MODE_DGRAD && p.add_src != nullptr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = m0 + wm * 64 + i * 16 + q * 4 + e;
+        av[i][e] = (addv && row < p.M) ? p.add_src[row * p.ncol + col] : 0.f;
+      }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -198,7 +209,7 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
           s = (long long)acc[0][i][j][e] + (p.a_u8off ? 128ll * wsum : 0ll);
         const float v = (float)s * scale;
         const int64_t o = row * p.ncol + col;
-        p.y[o] = (MODE == MODE_DGRAD && p.add_src) ? v + p.add_src[o] : v;
+        p.y[o] = addv ? v + av[i][e] : v;
       }
   }
 }

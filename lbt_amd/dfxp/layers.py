@@ -63,6 +63,7 @@ def _as_param(t, ctx):
 
 class Layer_q:
     """Base class: identity forward, gradient pass-through backward (``:97-126``)."""
+    _batched_q = False  # parameters quantised by the model's batched prologue (Model.forward)
 
     def forward(self, X):
         self.X = X
@@ -193,6 +194,8 @@ class Conv2d_q(Layer_q):
         return dx
 
     def quantize_weights(self):
+        if self._batched_q and self.ctx.params_ready:
+            return  # done by the model's batched prologue this step
         ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio,
                             wf=self.wf if (self.mfma or self.igemm_f) else None, ksf=self.ksf,
                             wd=self.wd if (self.mfma or self.igemm_d) else None, ksd=self.ksd,
@@ -262,8 +265,7 @@ class Conv2d_q(Layer_q):
         """Weight gradient on the wide-layer MFMA kernel (int64 slab, one shard) + its reduce."""
         d = self.d
         K = d.KH * d.KW * d.Cin
-        slab = self._c.get("wslab64", (1, K, d.Cout), torch.int64, self.ctx.device)
-        slab.zero_()
+        slab = self._c.sums("wslab64", K * d.Cout, self.ctx).view(1, K, d.Cout)  # zeroed per step
         ops.conv_wgrad_igemm(self.xq, self.gradq, g_i16, d, slab, ops.wgrad_igemm_nsplit(d), 1)
         ops.conv_wgrad_reduce64(slab, 1, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
                                 ops.f32(2 * self.weight_decay), self.dW)
@@ -372,7 +374,8 @@ class Dense_q(Layer_q):
         self.d = d = _lib.ConvDesc(N, 1, 1, self.in_units, self.units, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
         self.xq = ops.quantize(X, self.X_range, self.x_kind, out=self._c.get("xq", X.shape,
                                                                               ops.out_dtype(self.x_kind), dev))
-        ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio)
+        if not (self._batched_q and self.ctx.params_ready):
+            ops.quantize_weight(self.W, self.W_range, w_hwio=self.w_hwio)
         y = self._c.get("y", (N, self.units), torch.float32, dev)
         if self.mfma:
             ops.dense_pack(self.w_hwio, self.wf, self.wd)
@@ -614,6 +617,8 @@ class Rescale_q(Layer_q):
         return [(self, "gamma", "dgamma"), (self, "beta", "dbeta")]
 
     def quantize_params(self):
+        if self._batched_q and self.ctx.params_ready:
+            return
         C = self.C
         ops.quantize(self.gamma, self.g_range, OUT_F32, out=self.gb[:C])
         ops.quantize(self.beta, self.b_range, OUT_F32, out=self.gb[C:])
@@ -808,6 +813,9 @@ class ResidualBottleneck_q(ResidualBlock_q):
 
 
     # ---- fused execution of the block (bit-identical to the Sequential_q composition above)
+    next_block = None  # set by the model builder: the block that consumes this block's output
+    _x_pre = None      # the input tensor whose conv codes the previous block already wrote
+
     def _fusable(self):
         """16-bit gradients (config 4) and every conv on the wide MFMA kernels with offset int8 X
         codes: then forward / backward run the block as one fused kernel schedule."""
@@ -883,9 +891,13 @@ class ResidualBottleneck_q(ResidualBlock_q):
         self.X = X
         N, H, W, _ = X.shape
         dev = X.device
-        x1 = ops.quantize(X, c1.X_range, OUT_U8OFF, out=self._c.get("x1", X.shape, torch.int8, dev))
-        xs = (ops.quantize(X, sc[0].X_range, OUT_U8OFF, out=self._c.get("xs", X.shape, torch.int8, dev))
-              if sc else None)
+        x1 = self._c.get("x1", X.shape, torch.int8, dev)
+        xs = self._c.get("xs", X.shape, torch.int8, dev) if sc else None
+        if self._x_pre is not X:  # not already written by the previous block's last chain
+            ops.quantize(X, c1.X_range, OUT_U8OFF, out=x1)
+            if sc:
+                ops.quantize(X, sc[0].X_range, OUT_U8OFF, out=xs)
+        self._x_pre = None
         y1 = c1.fwd_codes(x1, N, H, W)
         self._norm_in(bn1, y1, ctx)
         x2 = self._c.get("x2", y1.shape, torch.int8, dev)
@@ -897,12 +909,22 @@ class ResidualBottleneck_q(ResidualBlock_q):
         y3 = c3.fwd_codes(x3, N, y2.shape[1], y2.shape[2])
         self._norm_in(bn3, y3, ctx)
         out = self._c.get("y", y3.shape, torch.float32, dev)
+        # the next block's input quantisers (conv-1, shortcut conv) ride in this chain as well
+        nb = self.next_block if (self.next_block is not None and self.next_block._fusable()) else None
+        o = {}
+        if nb is not None:
+            nsc = nb.shortcut.layers
+            o = dict(o1=nb._c.get("x1", y3.shape, torch.int8, dev), o1_conv=nb.residual.layers[0])
+            if nsc:
+                o.update(o2=nb._c.get("xs", y3.shape, torch.int8, dev), o2_conv=nsc[0])
         if sc:
             ys = sc[0].fwd_codes(xs, N, H, W)
             self._norm_in(sc[1], ys, ctx)
-            self._chain(c3, bn3, y3, True, bn2=sc[1], out=out)
+            self._chain(c3, bn3, y3, True, bn2=sc[1], out=out, **o)
         else:
-            self._chain(c3, bn3, y3, True, res=X, out=out)
+            self._chain(c3, bn3, y3, True, res=X, out=out, **o)
+        if nb is not None:
+            nb._x_pre = out
         self.y = out
         return out
 

@@ -95,6 +95,16 @@ def quantize_weight(w, q, w_hwio=None, wf=None, ksf=0, wd=None, ksd=0, colsum=No
          int(ksd), ptr(colsum), stream())
 
 
+def quantize_weights_flat(jobs, starts, njobs, nblocks):
+    """Every job of a device array of lbt_wjob in one element-parallel launch (batched.hip)."""
+    with _Timed("quantize_weights_flat_kernel", 0):
+        call("lbt_dfxp_quantize_weights_flat", ptr(jobs), ptr(starts), int(njobs), int(nblocks), stream())
+
+
+def quantize_many(jobs, njobs):
+    call("lbt_dfxp_quantize_many", ptr(jobs), int(njobs), stream())
+
+
 def packed_slices(KH, KW, C):
     """16-byte k-slices per GEMM column for a tap-major (tap, 16-channel slice) k order, padded to 4."""
     s = KH * KW * ((C + 15) // 16)

@@ -404,6 +404,8 @@ class FusedResNet:
         max_n = max(j.n for j in njobs)
         # ... which also clears the step's integer sums (everything this plan carved from the arena)
         nz = ctx._sums_used
+        if ctx._extra_arenas:  # the prologue clears the first arena only
+            raise RuntimeError("FusedResNet: the sums arena overflowed (raise DfxpContext sums_capacity)")
         # (together with every weight / gamma / beta quantiser and the input image: one launch)
         fwd.insert(0, L("lbt_step_prologue", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
                         ptr(self._wjobs), len(wjobs), max_cout, ptr(self._qjobs), len(qjobs),

@@ -13,6 +13,11 @@ from .dfxp.layers import _Cache
 from .runtime import default_context
 
 
+def _lib_load():
+    from . import _lib
+    return _lib.load()
+
+
 class Model:
     def __init__(self, bits, input_shape, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
         self.bits = bits
@@ -32,9 +37,77 @@ class Model:
     def get_layers(self):
         return []
 
-    def forward(self, X):
+    batched_params = True  # one launch for every weight quantiser, one for every gamma / beta
+
+    def _walk(self):
+        out = []
+
+        def rec(layer):
+            out.append(layer)
+            for sub in getattr(layer, "layers", []):
+                rec(sub)
+            for attr in ("residual", "shortcut"):
+                if hasattr(layer, attr):
+                    rec(getattr(layer, attr))
         for layer in self.layers:
-            X = layer.forward(X)
+            rec(layer)
+        return out
+
+    def _build_param_prologue(self):
+        """Job lists of the batched parameter quantisers (batched.hip): every conv / dense weight
+        whose packed images need no column sums (the wide, LDS-tiled kernels' layers) and every
+        Rescale_q gamma / beta -- bit-identical to each layer quantising its own."""
+        from ._lib import OUT_F32, QJob, WJob
+        from .fused import _dev_array
+        wjobs, starts, qjobs = [], [0], []
+        for layer in self._walk():
+            if isinstance(layer, L.Conv2d_q) and not layer.mfma and not getattr(layer, "w4", False) \
+                    and layer.ksize[3] % 4 == 0:
+                kh, kw, ci, co = layer.ksize
+                layer.W_range.observe(layer.W.numel())
+                wjobs.append(WJob(layer.W.data_ptr(), kh, kw, ci, co, layer.W_range.desc, layer.w_hwio.data_ptr(),
+                                  layer.wf.data_ptr() if layer.igemm_f else None, layer.ksf,
+                                  layer.wd.data_ptr() if layer.igemm_d else None, layer.ksd, None))
+            elif isinstance(layer, L.Dense_q) and layer.units % 4 == 0:
+                layer.W_range.observe(layer.W.numel())
+                wjobs.append(WJob(layer.W.data_ptr(), layer.in_units, 1, 1, layer.units, layer.W_range.desc,
+                                  layer.w_hwio.data_ptr(), None, 0, None, 0, None))
+            elif isinstance(layer, L.Rescale_q):
+                C = layer.C
+                layer.g_range.observe(C)
+                layer.b_range.observe(C)
+                qjobs.append(QJob(layer.gamma.data_ptr(), layer.gb.data_ptr(), OUT_F32, C, 1, layer.g_range.desc))
+                qjobs.append(QJob(layer.beta.data_ptr(), layer.gb.data_ptr() + 4 * C, OUT_F32, C, 1,
+                                  layer.b_range.desc))
+            else:
+                continue
+            layer._batched_q = True
+        lib = _lib_load()
+        for j in wjobs:
+            starts.append(starts[-1] + lib.lbt_flat_weight_blocks(j.KH * j.KW * j.Cin * j.Cout))
+        dev = self.ctx.device
+        self._pro = (_dev_array(wjobs, dev) if wjobs else None, len(wjobs),
+                     torch.tensor(starts, dtype=torch.int32, device=dev), starts[-1],
+                     _dev_array(qjobs, dev) if qjobs else None, len(qjobs))
+
+    def _param_prologue(self):
+        if getattr(self, "_pro", None) is None:
+            self._build_param_prologue()
+        wj, nw, starts, nb, qj, nq = self._pro
+        if nw:
+            ops.quantize_weights_flat(wj, starts, nw, nb)
+        if nq:
+            ops.quantize_many(qj, nq)
+        self.ctx.params_ready = True
+
+    def forward(self, X):
+        if self.batched_params:
+            self._param_prologue()
+        try:
+            for layer in self.layers:
+                X = layer.forward(X)
+        finally:
+            self.ctx.params_ready = False
         self.logits = X
         return X
 
@@ -154,6 +227,9 @@ class ImageNet_Resnet(Model):
         hw = image
         for s in (2, 2, 1, 2, 2, 2):  # conv1, max pool, stage strides
             hw = -(-hw // s)
+        blocks = [l for l in layers if isinstance(l, L.ResidualBottleneck_q)]
+        for a, b in zip(blocks, blocks[1:]):
+            a.next_block = b  # fused blocks hand their output's conv codes to the next block
         layers += [
             L.AvgPool_q(ksize=[1, hw, hw, 1], strides=[1, 1, 1, 1], padding="VALID"),
             L.Flatten_q(in_ch),

@@ -86,7 +86,9 @@ class DfxpContext:
         # from one arena so a whole step zeroes them with ONE fill (see zero_sums).
         self.sums_arena = torch.zeros(sums_capacity, dtype=torch.int64, device=dev)
         self._sums_used = 0
-        self.sums_managed = False  # True while a Trainer zeroes the arena once per step
+        self._extra_arenas = []
+        self.sums_managed = False
+        self.params_ready = False  # a model's batched prologue quantised every participating parameter  # True while a Trainer zeroes the arena once per step
 
     def quantizer(self, name, bits, initial=2, target=0.0, stochastic=True):
         """Register a quantiser (a ``*_range`` variable initialised to ``initial``)."""
@@ -109,16 +111,27 @@ class DfxpContext:
         return q
 
     def alloc_sums(self, n):
+        """n int64 from the arena. When the first arena is full (wide models: ResNet-50's weight-
+        gradient slabs), further buffers come from overflow arenas of at least the same size --
+        one more fill each per step."""
         n = (int(n) + 31) // 32 * 32
-        if self._sums_used + n > self.sums_arena.numel():
-            raise RuntimeError("DfxpContext sums arena exhausted (raise sums_capacity)")
-        t = self.sums_arena[self._sums_used:self._sums_used + n]
-        self._sums_used += n
-        return t
+        if self._sums_used + n <= self.sums_arena.numel():
+            t = self.sums_arena[self._sums_used:self._sums_used + n]
+            self._sums_used += n
+            return t
+        for i, (arena, used) in enumerate(self._extra_arenas):
+            if used + n <= arena.numel():
+                self._extra_arenas[i] = (arena, used + n)
+                return arena[used:used + n]
+        arena = torch.zeros(max(n, self.sums_arena.numel()), dtype=torch.int64, device=self.device)
+        self._extra_arenas.append((arena, n))
+        return arena[:n]
 
     def zero_sums(self):
         if self._sums_used:
             self.sums_arena[: self._sums_used].zero_()
+        for arena, used in self._extra_arenas:
+            arena[:used].zero_()
 
     # the 'update_range' collection (trainer.py:63,157)
     def update_range_op(self, sgd=None):
