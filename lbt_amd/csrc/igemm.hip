@@ -20,9 +20,17 @@
 #include "dfxp_device.h"
 #include "lds_tr.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace lbt;
+
+// tuning knobs read once per process (experiments; the defaults are the measured choice)
+int getenv_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
 
 constexpr int kT = 256, kBM = 128, kBN = 128, kBK = 64;
 constexpr int kRow = kBK + 16;  // LDS row stride in bytes (16-byte pad staggers the banks)
@@ -44,15 +52,18 @@ struct IgArgs {
   int ncol;
 };
 
-template <int MODE, bool A16>
+// BM x BN workgroup tile (64 or 128 each), 2 x 2 waves of (BM/2) x (BN/2): MI x NJ MFMA tiles
+template <int MODE, bool A16, bool ADD, int BM, int BN>
 __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   constexpr int NA = A16 ? 2 : 1;  // A tiles per k-block: (hi, lo') or one
-  __shared__ __attribute__((aligned(16))) int8_t sA[2][NA][kBM * kRow];
-  __shared__ __attribute__((aligned(16))) int8_t sB[2][kBN * kRow];
+  constexpr int HA = BM / 64, HB = BN / 64;  // 64-row loader passes of A / B
+  constexpr int MI = BM / 32, NJ = BN / 32;  // 16x16 tiles per wave
+  __shared__ __attribute__((aligned(16))) int8_t sA[2][NA][BM * kRow];
+  __shared__ __attribute__((aligned(16))) int8_t sB[2][BN * kRow];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * kBM;
-  const int n0 = blockIdx.y * kBN;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
   const lbt_conv_desc& d = p.d;
   const int OH = MODE == MODE_FWD ? d.Ho : d.H, OW = MODE == MODE_FWD ? d.Wo : d.W;
   const int SH = MODE == MODE_FWD ? d.H : d.Ho, SW = MODE == MODE_FWD ? d.W : d.Wo;
@@ -61,10 +72,10 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   // ---- loader roles: A rows (t >> 2) and (t >> 2) + 64, 16-byte segment (t & 3) of the 64 channels
   // (A16: 32-byte segments = 16 codes); B columns likewise
   const int lr = t >> 2, seg = t & 3;
-  int an[2], ay[2], ax[2];
-  bool arow[2];
+  int an[HA], ay[HA], ax[HA];
+  bool arow[HA];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < HA; ++h) {
     const int64_t m = m0 + lr + 64 * h;
     arow[h] = m < p.M;
     const uint32_t mu = (uint32_t)(arow[h] ? m : 0);
@@ -74,13 +85,13 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
     an[h] = (int)(tt / (uint32_t)OH);
   }
   // global -> register stage of one k-block
-  v4i ra[2][A16 ? 2 : 1], rb[2];
-  bool rv[2];
+  v4i ra[HA][A16 ? 2 : 1], rb[HB];
+  bool rv[HA];
   auto load_k = [&](int kb) {
     const int tap = kb / cblocks, cb = kb - tap * cblocks;
     const int kh = tap / d.KW, kw = tap - kh * d.KW;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < HA; ++h) {
       int sy, sx;
       bool ok;
       if (MODE == MODE_FWD) {
@@ -104,6 +115,9 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
         const int8_t* src = reinterpret_cast<const int8_t*>(p.a) + pix * p.cred + cb * kBK + seg * 16;
         ra[h][0] = *reinterpret_cast<const v4i*>(src);
       }
+    }
+#pragma unroll
+    for (int h = 0; h < HB; ++h) {
       const int col = n0 + lr + 64 * h;
       const int colc = col < p.ncol ? col : 0;
       rb[h] = *reinterpret_cast<const v4i*>(p.b + ((int64_t)colc * p.ks + kb * 4 + seg) * 16);
@@ -112,7 +126,7 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   };
   auto store_k = [&](int buf) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < HA; ++h) {
       const int row = lr + 64 * h;
       if constexpr (A16) {
         // 16 codes -> 16 hi bytes and 16 lo' bytes (a = 256 hi + lo' + 128); outside: (0, -128)
@@ -133,19 +147,20 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
         if (!rv[h]) v = v4i{fill, fill, fill, fill};
         *reinterpret_cast<v4i*>(&sA[buf][0][row * kRow + seg * 16]) = v;
       }
-      *reinterpret_cast<v4i*>(&sB[buf][row * kRow + seg * 16]) = rb[h];
     }
+#pragma unroll
+    for (int h = 0; h < HB; ++h) *reinterpret_cast<v4i*>(&sB[buf][(lr + 64 * h) * kRow + seg * 16]) = rb[h];
   };
 
-  v4i acc[NA][4][4], accw[4];
+  v4i acc[NA][MI][NJ], accw[NJ];
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[a][i][j] = v4i{0, 0, 0, 0};
+      for (int j = 0; j < NJ; ++j) acc[a][i][j] = v4i{0, 0, 0, 0};
 #pragma unroll
-  for (int j = 0; j < 4; ++j) accw[j] = v4i{0, 0, 0, 0};
+  for (int j = 0; j < NJ; ++j) accw[j] = v4i{0, 0, 0, 0};
   const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
   const bool want_w = A16 || p.a_u8off;  // sum_k W per column (the +128 term)
 
@@ -156,21 +171,21 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   for (int kb = 0; kb < nk; ++kb) {
     const int cur = kb & 1;
     if (kb + 1 < nk) load_k(kb + 1);  // in flight during the MFMAs below
-    v4i bf[4];
+    v4i bf[NJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bf[j] = *reinterpret_cast<const v4i*>(&sB[cur][(wn * 64 + j * 16 + r) * kRow + q * 16]);
+    for (int j = 0; j < NJ; ++j)
+      bf[j] = *reinterpret_cast<const v4i*>(&sB[cur][(wn * (BN / 2) + j * 16 + r) * kRow + q * 16]);
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const v4i af = *reinterpret_cast<const v4i*>(&sA[cur][a][(wm * 64 + i * 16 + r) * kRow + q * 16]);
+      for (int i = 0; i < MI; ++i) {
+        const v4i af = *reinterpret_cast<const v4i*>(&sA[cur][a][(wm * (BM / 2) + i * 16 + r) * kRow + q * 16]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[a][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[a][i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j) acc[a][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[a][i][j], 0, 0, 0);
       }
     if (want_w) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) accw[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[j], accw[j], 0, 0, 0);
+      for (int j = 0; j < NJ; ++j) accw[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[j], accw[j], 0, 0, 0);
     }
     if (kb + 1 < nk) {
       store_k(cur ^ 1);  // the other buffer: its readers finished before the last barrier
@@ -181,26 +196,26 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   // ---- epilogue: lane owns column (tile col + r), rows (tile row + 4q + e)
   const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + r;
+  for (int j = 0; j < NJ; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 16 + r;
     if (col >= p.ncol) continue;
     const long long wsum = want_w ? (long long)accw[j][0] : 0;  // every row of accw holds sum_k W[col][k]
     // dgrad addend: all 16 loads of this column issued before any store (p.y may alias it as far
     // as the compiler knows, so interleaved load / store pairs would serialise)
-    float av[4][4];
-    const bool addv = MODE == MODE_DGRAD && p.add_src != nullptr;
+    float av[MI][4];
+    constexpr bool addv = MODE == MODE_DGRAD && ADD;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t row = m0 + wm * 64 + i * 16 + q * 4 + e;
-        av[i][e] = (addv && row < p.M) ? p.add_src[row * p.ncol + col] : 0.f;
+        const int64_t row = m0 + wm * (BM / 2) + i * 16 + q * 4 + e;
+        if constexpr (addv) av[i][e] = row < p.M ? p.add_src[row * p.ncol + col] : 0.f;
       }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t row = m0 + wm * 64 + i * 16 + q * 4 + e;
+        const int64_t row = m0 + wm * (BM / 2) + i * 16 + q * 4 + e;
         if (row >= p.M) continue;
         long long s;
         if constexpr (A16)
@@ -214,12 +229,29 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   }
 }
 
+template <int MODE, bool A16, int BM, int BN>
+void launch_tile(const IgArgs& p, hipStream_t st) {
+  const dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.ncol + BN - 1) / BN));
+  if (MODE == MODE_DGRAD && p.add_src)
+    hipLaunchKernelGGL((igemm_kernel<MODE, A16, true, BM, BN>), grid, dim3(kT), 0, st, p);
+  else
+    hipLaunchKernelGGL((igemm_kernel<MODE, A16, false, BM, BN>), grid, dim3(kT), 0, st, p);
+}
+
+// Tile choice: 64 columns when the GEMM has <= 64 (no MFMAs on padding columns), and 64 rows
+// when 128-row tiles would leave the 256 CUs without two workgroups each.
 template <int MODE, bool A16>
 int launch(const IgArgs& p, hipStream_t st) {
   const int64_t mb = (p.M + kBM - 1) / kBM;
-  const int nb = (p.ncol + kBN - 1) / kBN;
-  if (mb > 0x7fffffff || nb > 65535) return LBT_EINVAL;
-  hipLaunchKernelGGL((igemm_kernel<MODE, A16>), dim3((unsigned)mb, (unsigned)nb), dim3(kT), 0, st, p);
+  if (mb > 0x7fffffff / 2 || (p.ncol + 63) / 64 > 65535) return LBT_EINVAL;
+  const bool bn64 = p.ncol <= 64 || getenv_int("LBT_IGEMM_BN", 128) == 64;
+  const int64_t nb = (p.ncol + (bn64 ? 63 : 127)) / (bn64 ? 64 : 128);
+  const bool bm64 = mb * nb < getenv_int("LBT_IGEMM_MIN_WG", 512);
+  if (bm64) {
+    if (bn64) launch_tile<MODE, A16, 64, 64>(p, st); else launch_tile<MODE, A16, 64, 128>(p, st);
+  } else {
+    if (bn64) launch_tile<MODE, A16, 128, 64>(p, st); else launch_tile<MODE, A16, 128, 128>(p, st);
+  }
   return (int)hipGetLastError();
 }
 
