@@ -160,6 +160,10 @@ int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t* wd, int32_
  * [nshard][KH*KW*Cin][Cout] (pixel split b -> shard b % nshard; reduce: lbt_conv_wgrad_reduce64). */
 int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
                          int32_t nsplit, int32_t nshard, void* stream);
+/* ... storing one partial per pixel split: slab [nsplit][KH*KW*Cin][Cout] is fully WRITTEN (no
+ * zeroing, no atomics); (N*Ho*Wo)/nsplit <= 2^19 pixels. Reduce with lbt_conv_wgrad_reduce64. */
+int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
+                               int32_t nsplit, void* stream);
 
 /* 4-bit weights (W 4-bit / A 8-bit): the same GEMMs with the weight
  * image packed two signed 4-bit codes per byte (lbt_pack_int4 of lbt_dfxp_quantize_weight's wf /
@@ -361,8 +365,11 @@ int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qde
  * codes (gb = [gamma_q | beta_q], also the gamma_q of the rescale part) -- and the masked fp32
  * gradient optionally stored (gmask_out: the identity shortcut's gradient); pass B with dx fed
  * straight into the consuming conv's 9..16-bit gradient quantiser qo (int16 codes gq, overflow
- * counters, noise period inner) instead of storing dx. Bit-identical to the unfused sequence. */
-int lbt_bn_bwd_a_wide_masked(const float* g, const float* y_mask, int32_t mask_r, lbt_qdesc qr, const float* gb,
+ * counters, noise period inner) instead of storing dx. g2 (optional): the incoming gradient is
+ * g + g2 (the block's two branch gradients, ResidualBlock_q.backward :865-869, summed here
+ * instead of in their own pass). Bit-identical to the unfused sequence.                      */
+int lbt_bn_bwd_a_wide_masked(const float* g, const float* g2, const float* y_mask, int32_t mask_r, lbt_qdesc qr,
+                             const float* gb,
                              float* gmask_out, lbt_qdesc qrg, const int8_t* R, lbt_qdesc qng, const int8_t* qn,
                              int16_t* gout, float* dout, int64_t* sums, int64_t rows, int64_t inner, int32_t C,
                              void* stream);

@@ -131,6 +131,7 @@ _SIGS = {
     "lbt_conv_fwd_igemm": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_conv_dgrad_igemm": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_igemm": [_P, _P, c_int32, ConvDesc, _P, c_int32, c_int32, _P],
+    "lbt_conv_wgrad_igemm_store": [_P, _P, c_int32, ConvDesc, _P, c_int32, _P],
     "lbt_conv_dgrad_chain_i8w4": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_dgrad_chain_i8": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_dgrad_chain_wgrad_i8": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int32, _P, c_int32,
@@ -153,7 +154,7 @@ _SIGS = {
     "lbt_dense_pack": [_P, c_int32, c_int32, _P, c_int32, _P, c_int32, _P],
     "lbt_flat_weight_blocks": [c_int64],
     "lbt_dfxp_quantize_weights_flat": [_P, _P, c_int32, c_int32, _P],
-    "lbt_bn_bwd_a_wide_masked": [_P, _P, c_int32, QDesc, _P, _P, QDesc, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64,
+    "lbt_bn_bwd_a_wide_masked": [_P, _P, _P, c_int32, QDesc, _P, _P, QDesc, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64,
                                  c_int32, _P],
     "lbt_bn_bwd_b_wide_q": [_P, QDesc, _P, QDesc, _P, _P, c_int64, _P, QDesc, c_int64, c_int64, c_int32, _P],
     "lbt_dense_gemm": [_P, c_int32, c_int32, c_int32, _P, c_int32, c_int32, c_int32, QDesc, QDesc, _P, _P],

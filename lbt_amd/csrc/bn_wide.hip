@@ -35,6 +35,8 @@ struct WideA {
   lbt_qdesc qr;          // the R codes' quantiser (mask_r)
   const float* gb;       // [gamma_q | beta_q] (mask_r)
   float* gmask_out;
+  const float* g2;       // optional second summand of the incoming gradient: g + g2 (ResidualBlock_q
+                         // .backward's add of the two branch gradients, :865-869, done here)
 };
 
 // Thread = 4 consecutive channels (one Philox4x32 call covers their 4 noise values) x one row lane.
@@ -65,6 +67,10 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
       const uint64_t blk = (uint64_t)(e % a.inner) >> 2;  // inner % 4 == 0
       const float4 gv = *reinterpret_cast<const float4*>(a.g + e);
       float d[4] = {gv.x, gv.y, gv.z, gv.w};
+      if (a.g2) {
+        const float4 g2v = *reinterpret_cast<const float4*>(a.g2 + e);
+        d[0] = d[0] + g2v.x; d[1] = d[1] + g2v.y; d[2] = d[2] + g2v.z; d[3] = d[3] + g2v.w;
+      }
       if (a.y_mask) {
         const float4 ym = *reinterpret_cast<const float4*>(a.y_mask + e);
         const float m[4] = {ym.x, ym.y, ym.z, ym.w};
@@ -241,7 +247,8 @@ extern "C" int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R,
                                  int64_t inner, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gamma_q)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
-  WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0, nullptr, 0, lbt_qdesc{}, nullptr, nullptr};
+  WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0, nullptr, 0, lbt_qdesc{}, nullptr, nullptr,
+          nullptr};
   const int cb = (C + kCB - 1) / kCB;
   a.rpb = rows_per_block(rows, cb);
   const int64_t yb = (rows + a.rpb - 1) / a.rpb;
@@ -264,14 +271,14 @@ extern "C" int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* 
 
 // Pass A with the ReLU mask folded in (y_mask, or mask_r: recomputed from R with qr and
 // gb = [gamma_q | beta_q]) and the masked gradient optionally stored (gmask_out).
-extern "C" int lbt_bn_bwd_a_wide_masked(const float* g, const float* y_mask, int32_t mask_r, lbt_qdesc qr,
+extern "C" int lbt_bn_bwd_a_wide_masked(const float* g, const float* g2, const float* y_mask, int32_t mask_r, lbt_qdesc qr,
                                         const float* gb, float* gmask_out, lbt_qdesc qrg, const int8_t* R,
                                         lbt_qdesc qng, const int8_t* qn, int16_t* gout, float* dout, int64_t* sums,
                                         int64_t rows, int64_t inner, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gb)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
   if (mask_r && (y_mask || !R || !gb || qr.bits <= 0)) return LBT_EINVAL;
-  WideA a{g, qrg, R, gb, qng, qn, gout, dout, sums, rows, inner, C, 0, y_mask, mask_r, qr, gb, gmask_out};
+  WideA a{g, qrg, R, gb, qng, qn, gout, dout, sums, rows, inner, C, 0, y_mask, mask_r, qr, gb, gmask_out, g2};
   const int cb = (C + kCB - 1) / kCB;
   a.rpb = rows_per_block(rows, cb);
   const int64_t yb = (rows + a.rpb - 1) / a.rpb;

@@ -302,7 +302,9 @@ namespace {
 
 constexpr int kWP = 64;
 
-template <bool G16>
+// STORE: the workgroup's partial is STORED into slab[split] (every element of slab[nsplit][K][Cout]
+// has exactly one writer -- no zeroing, no atomics); else atomically added into shard split % nshard.
+template <bool G16, bool STORE>
 __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
                                                         lbt_conv_desc d, long long* __restrict__ slab, int64_t P,
                                                         int nsplit, int nshard) {
@@ -409,33 +411,48 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
-  // ---- combine exactly, meet the other waves in LDS (int64 [64 ci][64 co]), one atomic per output
+  // ---- combine exactly; the 4 waves meet in LDS (int64 [64 ci][64 co]) one after another
+  // (plain read-modify-write, each wave owning the tile between two barriers)
   __syncthreads();
-  unsigned long long* tile = reinterpret_cast<unsigned long long*>(&lds[0][0]);
-  for (int i = threadIdx.x; i < 64 * 64; i += kT) tile[i] = 0ull;
-  __syncthreads();
+  long long* tile = reinterpret_cast<long long*>(&lds[0][0]);
   const long long npix = nchunks * kWP;
+  long long vv[4][4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        long long v;
         if constexpr (G16) {
           const long long sg = 256ll * ag[0][b][i] + (long long)ag[1][b][i] + 128ll * npix;  // sum_p g[co]
-          v = 256ll * acc[0][a][b][i] + (long long)acc[1][a][b][i] + 128ll * ax[a][i] + 128ll * sg;
+          vv[a][b][i] = 256ll * acc[0][a][b][i] + (long long)acc[1][a][b][i] + 128ll * ax[a][i] + 128ll * sg;
         } else {
-          v = (long long)acc[0][a][b][i] + 128ll * ag[0][b][i];
+          vv[a][b][i] = (long long)acc[0][a][b][i] + 128ll * ag[0][b][i];
         }
-        if (v) atomicAdd(&tile[(a * 16 + q * 4 + i) * 64 + b * 16 + r], (unsigned long long)v);
       }
-  __syncthreads();
-  long long* dst = slab + ((int64_t)(blockIdx.x % nshard) * (d.KH * d.KW) + tap) * d.Cin * d.Cout;
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            long long* t = &tile[(a * 16 + q * 4 + i) * 64 + b * 16 + r];
+            *t = w == 0 ? vv[a][b][i] : *t + vv[a][b][i];
+          }
+    }
+    __syncthreads();
+  }
+  const int64_t shard = STORE ? (int64_t)blockIdx.x : (int64_t)(blockIdx.x % nshard);
+  long long* dst = slab + (shard * (d.KH * d.KW) + tap) * d.Cin * d.Cout;
   for (int i = threadIdx.x; i < 64 * 64; i += kT) {
-    const long long v = (long long)tile[i];
+    const long long v = tile[i];
     const int ci = cb * 64 + (i >> 6), co = ob * 64 + (i & 63);
-    if (v) atomicAdd((unsigned long long*)&dst[(int64_t)ci * d.Cout + co], (unsigned long long)v);
+    if constexpr (STORE)
+      dst[(int64_t)ci * d.Cout + co] = v;
+    else if (v)
+      atomicAdd((unsigned long long*)&dst[(int64_t)ci * d.Cout + co], (unsigned long long)v);
   }
 }
 
@@ -453,9 +470,31 @@ extern "C" int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_
   dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
   hipStream_t st = (hipStream_t)stream;
   if (g_i16)
-    hipLaunchKernelGGL(wgrad_wide_kernel<true>, grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit, nshard);
-  else
-    hipLaunchKernelGGL(wgrad_wide_kernel<false>, grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
+    hipLaunchKernelGGL((wgrad_wide_kernel<true, false>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
                        nshard);
+  else
+    hipLaunchKernelGGL((wgrad_wide_kernel<false, false>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
+                       nshard);
+  return (int)hipGetLastError();
+}
+
+// ... storing: slab [nsplit][KH*KW*Cin][Cout] is fully WRITTEN (one partial per pixel split; no
+// zeroing, no atomics); reduce with lbt_conv_wgrad_reduce64 over nsplit.
+extern "C" int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d,
+                                          int64_t* slab, int32_t nsplit, void* stream) {
+  if (!desc_ok(d) || d.Cin % 64 || d.Cout % 64 || nsplit <= 0) return LBT_EINVAL;
+  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
+  if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  if ((P + nsplit - 1) / nsplit > 4 * 131072) return LBT_EINVAL;  // int32 MFMA sums of a wave stay exact
+  const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
+  if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
+  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
+  hipStream_t st = (hipStream_t)stream;
+  if (g_i16)
+    hipLaunchKernelGGL((wgrad_wide_kernel<true, true>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
+                       nsplit);
+  else
+    hipLaunchKernelGGL((wgrad_wide_kernel<false, true>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
+                       nsplit);
   return (int)hipGetLastError();
 }

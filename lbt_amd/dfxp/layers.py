@@ -265,9 +265,10 @@ class Conv2d_q(Layer_q):
         """Weight gradient on the wide-layer MFMA kernel (int64 slab, one shard) + its reduce."""
         d = self.d
         K = d.KH * d.KW * d.Cin
-        slab = self._c.sums("wslab64", K * d.Cout, self.ctx).view(1, K, d.Cout)  # zeroed per step
-        ops.conv_wgrad_igemm(self.xq, self.gradq, g_i16, d, slab, ops.wgrad_igemm_nsplit(d), 1)
-        ops.conv_wgrad_reduce64(slab, 1, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
+        ns = ops.wgrad_store_nsplit(d)
+        slab = self._c.get("wslab64", (ns, K, d.Cout), torch.int64, self.ctx.device)  # fully written
+        ops.conv_wgrad_igemm_store(self.xq, self.gradq, g_i16, d, slab, ns)
+        ops.conv_wgrad_reduce64(slab, ns, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
                                 ops.f32(2 * self.weight_decay), self.dW)
 
     def backward(self, grad, stochastic=True):
@@ -814,6 +815,7 @@ class ResidualBottleneck_q(ResidualBlock_q):
 
     # ---- fused execution of the block (bit-identical to the Sequential_q composition above)
     next_block = None  # set by the model builder: the block that consumes this block's output
+    prev_block = None  # ... and the block whose output this block consumes
     _x_pre = None      # the input tensor whose conv codes the previous block already wrote
 
     def _fusable(self):
@@ -929,7 +931,7 @@ class ResidualBottleneck_q(ResidualBlock_q):
         return out
 
     @staticmethod
-    def _bn_bwd(bn, conv_out, g, ctx, y_mask=None, mask_r=False, gmask_out=None, into=None):
+    def _bn_bwd(bn, conv_out, g, ctx, y_mask=None, mask_r=False, gmask_out=None, g2=None):
         """One BN's backward with the ReLU mask in front (pass A: rescale + norm gradient
         quantisers, dgamma / dbeta), then pass B straight into the producing conv's 16-bit
         gradient quantiser: returns that conv's int16 gradient codes."""
@@ -942,7 +944,7 @@ class ResidualBottleneck_q(ResidualBlock_q):
         n.grad_range.observe(g.numel())
         G16 = n._c.get("G16", g.shape, torch.int16, dev)
         ops.bn_bwd_a_wide_masked(g, y_mask, mask_r, r.X_range.desc, r.gb, gmask_out, r.grad_range.desc, r.R,
-                                 n.grad_range.desc, n.q, G16, sums, rows, inner, C)
+                                 n.grad_range.desc, n.q, G16, sums, rows, inner, C, g2=g2)
         ops.bn_param_grads(sums, C, r.grad_range.desc, r.X_range.desc, r.gamma, ops.f32(2 * r.weight_decay),
                            r.dgamma, r.dbeta)
         conv_out.grad_range.observe(g.numel())
@@ -952,23 +954,29 @@ class ResidualBottleneck_q(ResidualBlock_q):
         return gq
 
     def _backward_fused(self, grad):
+        """grad: the block output's gradient, or the pair (g1, g2) of the next fused block's two
+        branch gradients, whose sum g1 + g2 is formed inside this block's first pass A. Returns
+        the pair (residual-branch dX, shortcut dX) when the previous block is fused too, else
+        their sum (dgrad epilogue add)."""
         r = self.residual.layers
         c1, bn1, c2, bn2, c3, bn3 = r[0], r[1], r[3], r[4], r[6], r[7]
         sc = self.shortcut.layers
         ctx = c1.ctx
-        dev = grad.device
+        gin, gin2 = grad if isinstance(grad, tuple) else (grad, None)
+        dev = gin.device
         # block ReLU mask from the block output; bn3 (and the shortcut bn) see the same masked g
-        gmask = None if sc else self._c.get("gmask", grad.shape, torch.float32, dev)
-        g3 = self._bn_bwd(bn3, c3, grad, ctx, y_mask=self.y, gmask_out=gmask)
-        gs = self._bn_bwd(sc[1], sc[0], grad, ctx, y_mask=self.y) if sc else None
+        gmask = None if sc else self._c.get("gmask", gin.shape, torch.float32, dev)
+        g3 = self._bn_bwd(bn3, c3, gin, ctx, y_mask=self.y, gmask_out=gmask, g2=gin2)
+        gs = self._bn_bwd(sc[1], sc[0], gin, ctx, y_mask=self.y, g2=gin2) if sc else None
         d3 = c3.bwd_codes16(g3)
         g2 = self._bn_bwd(bn2, c2, d3, ctx, mask_r=True)
         d2 = c2.bwd_codes16(g2)
         g1 = self._bn_bwd(bn1, c1, d2, ctx, mask_r=True)
-        if sc:
-            ds = sc[0].bwd_codes16(gs)
-            return c1.bwd_codes16(g1, add_src=ds)
-        return c1.bwd_codes16(g1, add_src=gmask)
+        other = sc[0].bwd_codes16(gs) if sc else gmask
+        pb = self.prev_block
+        if pb is not None and pb._fusable():
+            return (c1.bwd_codes16(g1), other)
+        return c1.bwd_codes16(g1, add_src=other)
 
 
 class MaxPool_q(Layer_q):

@@ -487,10 +487,10 @@ def bn_bwd_b_wide(G, qng, qn, qn_q, ms, sums, n, dx, rows, C):
 
 
 # ---------------------------------------------------------------- wide layers (igemm.hip)
-def bn_bwd_a_wide_masked(g, y_mask, mask_r, qr, gb, gmask_out, qrg, R, qng, qn, gout, sums, rows, inner, C):
+def bn_bwd_a_wide_masked(g, y_mask, mask_r, qr, gb, gmask_out, qrg, R, qng, qn, gout, sums, rows, inner, C, g2=None):
     with _Timed("bn_bwd_a_wide_kernel", g.numel() * (4 + 1 + 1 + 2) + (4 * g.numel() if y_mask is not None else 0)
-                + (4 * g.numel() if gmask_out is not None else 0)):
-        call("lbt_bn_bwd_a_wide_masked", ptr(g), ptr(y_mask), int(mask_r), qr, ptr(gb), ptr(gmask_out), qrg, ptr(R),
+                + (4 * g.numel() if gmask_out is not None else 0) + (4 * g.numel() if g2 is not None else 0)):
+        call("lbt_bn_bwd_a_wide_masked", ptr(g), ptr(g2), ptr(y_mask), int(mask_r), qr, ptr(gb), ptr(gmask_out), qrg, ptr(R),
              qng, ptr(qn), ptr(gout), None, ptr(sums), int(rows), int(inner), int(C), stream())
 
 
@@ -523,6 +523,19 @@ def wgrad_igemm_nsplit(d):
     tiles = d.KH * d.KW * (d.Cin // 64) * (d.Cout // 64)
     lo = -(-P // (4 * 131072))
     return max(lo, min(max(1, P // 256), -(-1024 // tiles)))
+
+
+def wgrad_store_nsplit(d):
+    """Pixel splits of the storing wide wgrad: >= ~512 workgroups, each split's slab written once."""
+    P = d.N * d.Ho * d.Wo
+    tiles = d.KH * d.KW * (d.Cin // 64) * (d.Cout // 64)
+    lo = -(-P // (4 * 131072))
+    return max(lo, min(max(1, P // 1024), -(-512 // tiles)))
+
+
+def conv_wgrad_igemm_store(xq, gq, g_i16, d, slab, nsplit):
+    with _Timed("wgrad_wide_kernel", xq.numel() + gq.numel() * gq.element_size() + 8 * slab.numel()):
+        call("lbt_conv_wgrad_igemm_store", ptr(xq), ptr(gq), int(g_i16), d, ptr(slab), int(nsplit), stream())
 
 
 def conv_wgrad_igemm(xq, gq, g_i16, d, slab, nsplit, nshard):

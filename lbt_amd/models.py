@@ -230,6 +230,7 @@ class ImageNet_Resnet(Model):
         blocks = [l for l in layers if isinstance(l, L.ResidualBottleneck_q)]
         for a, b in zip(blocks, blocks[1:]):
             a.next_block = b  # fused blocks hand their output's conv codes to the next block
+            b.prev_block = a  # ... and their input gradient back as an unsummed pair
         layers += [
             L.AvgPool_q(ksize=[1, hw, hw, 1], strides=[1, 1, 1, 1], padding="VALID"),
             L.Flatten_q(in_ch),

@@ -215,6 +215,10 @@ def test_wgrad_igemm_matches_generic(N, H, Cin, Cout, k, s):
             ref = torch.zeros((ns, K, Cout), dtype=torch.int32, device=DEV)
             ops.conv_wgrad_generic(x16, True, g, d, ref, ns)
         assert torch.equal(got, ref.to(torch.int64).sum(0)), g_i16
+        ns2 = ops.wgrad_store_nsplit(d)
+        slab2 = torch.full((ns2, K, Cout), 3, dtype=torch.int64, device=DEV)  # every element overwritten
+        ops.conv_wgrad_igemm_store(x_off, g, g_i16, d, slab2, ns2)
+        assert torch.equal(slab2.sum(0), ref.to(torch.int64).sum(0)), ("store", g_i16)
 
 
 @pytest.mark.gpu
