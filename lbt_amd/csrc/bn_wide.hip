@@ -44,7 +44,7 @@ constexpr int kCQ = 16;        // channel quads per workgroup (64 channels)
 constexpr int kRL4 = kT / kCQ; // 16 row lanes
 
 __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
-  __shared__ long long red[kRL4][4][kCB];
+  __shared__ long long red[kT / 64][4][kCB];
   __shared__ int sh_cnt[2 * 2 * (kT / 64)];
   const int cq = threadIdx.x % kCQ, rl = threadIdx.x / kCQ;
   const int c0 = blockIdx.x * kCB + 4 * cq;
@@ -59,73 +59,106 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
     bet[k] = (cv && a.mask_r) ? a.gb[a.C + c0 + k] : 0.f;
   }
   const float sr = a.mask_r ? qstate(a.qr).inv_m : 0.f;
+  const float* __restrict__ gp = a.g;
+  const float* __restrict__ g2p = a.g2;
+  const float* __restrict__ ymp = a.y_mask;
+  const int8_t* __restrict__ Rp = a.R;
+  const int8_t* __restrict__ qnp = a.qn;
+  const bool needR = a.mask_r || srg.active;
   long long s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0};
   int o1 = 0, o2 = 0, p1 = 0, p2 = 0;
+  constexpr int U = 2;  // rows in flight per thread: every load of both issued before any use
   if (cv) {
-    for (int64_t r = r0 + rl; r < r1; r += kRL4) {
-      const int64_t e = r * a.C + c0;
-      const uint64_t blk = (uint64_t)(e % a.inner) >> 2;  // inner % 4 == 0
-      const float4 gv = *reinterpret_cast<const float4*>(a.g + e);
-      float d[4] = {gv.x, gv.y, gv.z, gv.w};
-      if (a.g2) {
-        const float4 g2v = *reinterpret_cast<const float4*>(a.g2 + e);
-        d[0] = d[0] + g2v.x; d[1] = d[1] + g2v.y; d[2] = d[2] + g2v.z; d[3] = d[3] + g2v.w;
+    for (int64_t rb = r0 + rl; rb < r1; rb += U * kRL4) {
+      float4 gv[U], g2v[U], ym[U];
+      char4 rv[U], qv[U];
+      bool live[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = rb + u * kRL4;
+        live[u] = r < r1;
+        const int64_t e = (live[u] ? r : rb) * a.C + c0;
+        gv[u] = *reinterpret_cast<const float4*>(gp + e);
+        if (g2p) g2v[u] = *reinterpret_cast<const float4*>(g2p + e);
+        if (ymp) ym[u] = *reinterpret_cast<const float4*>(ymp + e);
+        if (needR) rv[u] = *reinterpret_cast<const char4*>(Rp + e);
+        if (sng.active) qv[u] = *reinterpret_cast<const char4*>(qnp + e);
       }
-      if (a.y_mask) {
-        const float4 ym = *reinterpret_cast<const float4*>(a.y_mask + e);
-        const float m[4] = {ym.x, ym.y, ym.z, ym.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = m[k] > 0.f ? d[k] : 0.f;
-      } else if (a.mask_r) {
-        const char4 rv = *reinterpret_cast<const char4*>(a.R + e);
-        const int R[4] = {rv.x, rv.y, rv.z, rv.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {  // bn.hip chain_bwd_a's recomputation, op for op
-          const float xr = (float)R[k] * sr;
-          const float m1 = xr * gam[k];
-          const float yv = m1 + bet[k];
-          d[k] = yv > 0.f ? d[k] : 0.f;
+      for (int u = 0; u < U; ++u) {
+        if (!live[u]) break;
+        const int64_t e = (rb + u * kRL4) * a.C + c0;
+        const uint64_t blk = (uint64_t)(e % a.inner) >> 2;  // inner % 4 == 0
+        float d[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+        if (g2p) {
+          d[0] = d[0] + g2v[u].x; d[1] = d[1] + g2v[u].y; d[2] = d[2] + g2v[u].z; d[3] = d[3] + g2v[u].w;
         }
-      }
-      if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(d[0], d[1], d[2], d[3]);
-      if (srg.active) {
-        const Noise4 nz = a.qrg.stochastic ? qnoise4(a.qrg, srg.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
-        const char4 rv = *reinterpret_cast<const char4*>(a.R + e);
-        const int R[4] = {rv.x, rv.y, rv.z, rv.w};
+        const int R[4] = {needR ? rv[u].x : 0, needR ? rv[u].y : 0, needR ? rv[u].z : 0, needR ? rv[u].w : 0};
+        if (ymp) {
+          const float m[4] = {ym[u].x, ym[u].y, ym[u].z, ym[u].w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int G2 = quant1(srg, a.qrg.stochastic, d[k], nz.u[k], o1, o2);
-          s0[k] += (long long)G2 * R[k];
-          s1[k] += G2;
-          const float gh = (float)G2 * srg.inv_m;
-          d[k] = gh * gam[k];
-        }
-      }
-      if (sng.active) {
-        const Noise4 nz = a.qng.stochastic ? qnoise4(a.qng, sng.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
-        const char4 qv = *reinterpret_cast<const char4*>(a.qn + e);
-        const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
-        int G[4];
+          for (int k = 0; k < 4; ++k) d[k] = m[k] > 0.f ? d[k] : 0.f;
+        } else if (a.mask_r) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          G[k] = quant1(sng, a.qng.stochastic, d[k], nz.u[k], p1, p2);
-          s2[k] += G[k];
-          s3[k] += (long long)G[k] * qn[k];
+          for (int k = 0; k < 4; ++k) {  // bn.hip chain_bwd_a's recomputation, op for op
+            const float xr = (float)R[k] * sr;
+            const float m1 = xr * gam[k];
+            const float yv = m1 + bet[k];
+            d[k] = yv > 0.f ? d[k] : 0.f;
+          }
         }
-        short4 o;
-        o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
-        *reinterpret_cast<short4*>(a.gout + e) = o;
-      } else if (a.dout) {
-        *reinterpret_cast<float4*>(a.dout + e) = make_float4(d[0], d[1], d[2], d[3]);
+        if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(d[0], d[1], d[2], d[3]);
+        if (srg.active) {
+          const Noise4 nz = a.qrg.stochastic ? qnoise4(a.qrg, srg.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int G2 = quant1(srg, a.qrg.stochastic, d[k], nz.u[k], o1, o2);
+            s0[k] += (long long)G2 * R[k];
+            s1[k] += G2;
+            const float gh = (float)G2 * srg.inv_m;
+            d[k] = gh * gam[k];
+          }
+        }
+        if (sng.active) {
+          const Noise4 nz = a.qng.stochastic ? qnoise4(a.qng, sng.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+          const int qn[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
+          int G[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            G[k] = quant1(sng, a.qng.stochastic, d[k], nz.u[k], p1, p2);
+            s2[k] += G[k];
+            s3[k] += (long long)G[k] * qn[k];
+          }
+          short4 o;
+          o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
+          *reinterpret_cast<short4*>(a.gout + e) = o;
+        } else if (a.dout) {
+          *reinterpret_cast<float4*>(a.dout + e) = make_float4(d[0], d[1], d[2], d[3]);
+        }
       }
     }
   }
+  // the 4 row lanes of a wave hold the same channels (lanes cq, cq + 16, cq + 32, cq + 48): fold
+  // them with shuffles, then one LDS row per wave
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    red[rl][0][4 * cq + k] = s0[k];
-    red[rl][1][4 * cq + k] = s1[k];
-    red[rl][2][4 * cq + k] = s2[k];
-    red[rl][3][4 * cq + k] = s3[k];
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      s0[k] += __shfl_xor(s0[k], o, 64);
+      s1[k] += __shfl_xor(s1[k], o, 64);
+      s2[k] += __shfl_xor(s2[k], o, 64);
+      s3[k] += __shfl_xor(s3[k], o, 64);
+    }
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < kCQ) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[wv][0][4 * cq + k] = s0[k];
+      red[wv][1][4 * cq + k] = s1[k];
+      red[wv][2][4 * cq + k] = s2[k];
+      red[wv][3][4 * cq + k] = s3[k];
+    }
   }
   // per-thread counters -> wave totals -> LDS (one barrier publishes counters and sums)
   counts_stage(0, 2, o1, o2, sh_cnt);
@@ -139,7 +172,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
       const int sidx = i / kCB, cl = i - sidx * kCB, c = blockIdx.x * kCB + cl;
       if (c >= a.C) continue;
       long long v = 0;
-      for (int l = 0; l < kRL4; ++l) v += red[l][sidx][cl];
+      for (int l = 0; l < kT / 64; ++l) v += red[l][sidx][cl];
       if (v) atomicAdd((unsigned long long*)&dst[sidx * a.C + c], (unsigned long long)v);
     }
   }
@@ -199,10 +232,24 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
   }
   const int64_t r0 = (int64_t)blockIdx.y * b.rpb;
   const int64_t r1 = r0 + b.rpb < b.rows ? r0 + b.rpb : b.rows;
-  for (int64_t r = r0 + rl; r < r1; r += kRL4) {
-    const int64_t e = r * b.C + c0;
-    const char4 qv = *reinterpret_cast<const char4*>(b.qn + e);
-    const short4 gv = *reinterpret_cast<const short4*>(b.G + e);
+  const int8_t* __restrict__ qnp = b.qn;
+  const int16_t* __restrict__ Gp = b.G;
+  constexpr int U = 2;  // rows in flight per thread
+  for (int64_t rb = r0 + rl; rb < r1; rb += U * kRL4) {
+    char4 qva[U];
+    short4 gva[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + u * kRL4 < r1 ? rb + u * kRL4 : rb;
+      qva[u] = *reinterpret_cast<const char4*>(qnp + r * b.C + c0);
+      gva[u] = *reinterpret_cast<const short4*>(Gp + r * b.C + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    if (rb + u * kRL4 >= r1) break;
+    const int64_t e = (rb + u * kRL4) * b.C + c0;
+    const char4 qv = qva[u];
+    const short4 gv = gva[u];
     const int q[4] = {qv.x, qv.y, qv.z, qv.w}, G[4] = {gv.x, gv.y, gv.z, gv.w};
     float o[4];
 #pragma unroll
@@ -227,13 +274,14 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
     } else {
       *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0], o[1], o[2], o[3]);
     }
+    }
   }
   if (quant) block_flush_counts(b.qo, o1, o2, sh_cnt);
 }
 
-// ~512 workgroups in all
+// ~2048 workgroups in all
 int rows_per_block(int64_t rows, int cblocks) {
-  int64_t splits = 512 / (cblocks > 0 ? cblocks : 1);
+  int64_t splits = 2048 / (cblocks > 0 ? cblocks : 1);  // ~2048 workgroups: up to 8 per CU in flight
   if (splits < 1) splits = 1;
   int64_t rpb = (rows + splits - 1) / splits;
   if (rpb < kRL4) rpb = kRL4;

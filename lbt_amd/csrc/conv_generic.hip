@@ -228,6 +228,30 @@ __global__ __launch_bounds__(256) void wgrad_reduce_generic_kernel(const TACC* _
   dw[i] = a + b;
 }
 
+// Many splits (the wide wgrad kernels' stored partials): 64 outputs x 4 split groups per block,
+// each group summing every 4th split; groups meet in LDS. Same exact int64 total, same epilogue.
+__global__ __launch_bounds__(256) void wgrad_reduce64_split_kernel(const long long* __restrict__ slab, int nsplit,
+                                                                   int64_t total, lbt_qdesc qx, lbt_qdesc qg,
+                                                                   const float* __restrict__ w, float wd2,
+                                                                   float* __restrict__ dw) {
+  __shared__ long long red[4][64];
+  const int lo = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lo;
+  long long s = 0;
+  if (i < total) {
+#pragma unroll 4
+    for (int b = sg; b < nsplit; b += 4) s += slab[(int64_t)b * total + i];
+  }
+  red[sg][lo] = s;
+  __syncthreads();
+  if (sg != 0 || i >= total) return;
+  s = red[0][lo] + red[1][lo] + red[2][lo] + red[3][lo];
+  const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qg)));
+  const float a = (float)s * scale;
+  const float b = wd2 * w[i];
+  dw[i] = a + b;
+}
+
 }  // namespace
 
 extern "C" int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
@@ -269,7 +293,11 @@ extern "C" int lbt_conv_wgrad_reduce64(const int64_t* slab, int32_t nsplit, int3
                                        lbt_qdesc qg, const float* w, float wd2, float* dw, void* stream) {
   if (nsplit <= 0 || K <= 0 || Cout <= 0) return LBT_EINVAL;
   const int64_t total = (int64_t)K * Cout;
-  hipLaunchKernelGGL((wgrad_reduce_generic_kernel<long long>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw);
+  if (nsplit > 8)
+    hipLaunchKernelGGL(wgrad_reduce64_split_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0,
+                       (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw);
+  else
+    hipLaunchKernelGGL((wgrad_reduce_generic_kernel<long long>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw);
   return (int)hipGetLastError();
 }
