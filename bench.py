@@ -215,7 +215,9 @@ def main():
                          "executor": "layerwise", "final_loss": round(loss, 4)}
     if rank == 0 and world == 1 and not args.no_roofline:
         from lbt_amd.roofline import measure_dominant
-        out["roofline"] = measure_dominant(trainer, xs[0], ys[0])
+        tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                          "pmc_traffic_resnet50.json" if r50 else "pmc_traffic.json")
+        out["roofline"] = measure_dominant(trainer, xs[0], ys[0], traffic_file=tf)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_r50(args.cpu_seconds) if r50 else cpu_baseline(args.cpu_seconds, args.batch)
     if rank == 0:

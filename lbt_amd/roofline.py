@@ -27,6 +27,11 @@ def family(kernel_name):
     forward, plain dgrad and dgrad fused with a BN pass A (CF != 0); other kernels drop their
     template arguments."""
     n = kernel_name.replace("(anonymous namespace)::", "").replace("void ", "").strip()
+    if n.startswith("igemm_kernel<"):
+        args = n[len("igemm_kernel<"):].split(">")[0]
+        if args in ("fwd", "dgrad"):  # already a family label
+            return n
+        return "igemm_kernel<fwd>" if args.split(",")[0].strip() == "0" else "igemm_kernel<dgrad>"
     if n.startswith("conv_gemm_kernel<"):
         args = [a.strip() for a in n[len("conv_gemm_kernel<"):].split(">")[0].split(",")]
         if len(args) < 3:  # already a family label, e.g. "conv_gemm_kernel<1> (dgrad+A)"
