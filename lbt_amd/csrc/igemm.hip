@@ -53,7 +53,7 @@ struct IgArgs {
 };
 
 // BM x BN workgroup tile (64 or 128 each), 2 x 2 waves of (BM/2) x (BN/2): MI x NJ MFMA tiles
-template <int MODE, bool A16, bool ADD, int BM, int BN>
+template <int MODE, bool A16, bool ADD, int BM, int BN, int D>
 __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   constexpr int NA = A16 ? 2 : 1;  // A tiles per k-block: (hi, lo') or one
   constexpr int HA = BM / 64, HB = BN / 64;  // 64-row loader passes of A / B
@@ -85,9 +85,10 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
     an[h] = (int)(tt / (uint32_t)OH);
   }
   // global -> register stage of one k-block
-  v4i ra[HA][A16 ? 2 : 1], rb[HB];
-  bool rv[HA];
-  auto load_k = [&](int kb) {
+  // D register stages: the global loads of k-block b land in stage b % D, D k-blocks ahead of use
+  v4i ra[D][HA][A16 ? 2 : 1], rb[D][HB];
+  bool rv[D][HA];
+  auto load_k = [&](int kb, int st) {
     const int tap = kb / cblocks, cb = kb - tap * cblocks;
     const int kh = tap / d.KW, kw = tap - kh * d.KW;
 #pragma unroll
@@ -105,26 +106,26 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
         ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
       }
       ok = ok && arow[h];
-      rv[h] = ok;
+      rv[st][h] = ok;
       const int64_t pix = ok ? (((int64_t)an[h] * SH + sy) * SW + sx) : 0;
       if constexpr (A16) {
         const int16_t* src = reinterpret_cast<const int16_t*>(p.a) + pix * p.cred + cb * kBK + seg * 16;
-        ra[h][0] = *reinterpret_cast<const v4i*>(src);
-        ra[h][1] = *reinterpret_cast<const v4i*>(src + 8);
+        ra[st][h][0] = *reinterpret_cast<const v4i*>(src);
+        ra[st][h][1] = *reinterpret_cast<const v4i*>(src + 8);
       } else {
         const int8_t* src = reinterpret_cast<const int8_t*>(p.a) + pix * p.cred + cb * kBK + seg * 16;
-        ra[h][0] = *reinterpret_cast<const v4i*>(src);
+        ra[st][h][0] = *reinterpret_cast<const v4i*>(src);
       }
     }
 #pragma unroll
     for (int h = 0; h < HB; ++h) {
       const int col = n0 + lr + 64 * h;
       const int colc = col < p.ncol ? col : 0;
-      rb[h] = *reinterpret_cast<const v4i*>(p.b + ((int64_t)colc * p.ks + kb * 4 + seg) * 16);
-      if (col >= p.ncol) rb[h] = v4i{0, 0, 0, 0};
+      rb[st][h] = *reinterpret_cast<const v4i*>(p.b + ((int64_t)colc * p.ks + kb * 4 + seg) * 16);
+      if (col >= p.ncol) rb[st][h] = v4i{0, 0, 0, 0};
     }
   };
-  auto store_k = [&](int buf) {
+  auto store_k = [&](int buf, int st) {
 #pragma unroll
     for (int h = 0; h < HA; ++h) {
       const int row = lr + 64 * h;
@@ -133,23 +134,23 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
         int hi[4], lo[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          const uint32_t c01 = (uint32_t)ra[h][w >> 1][(w & 1) * 2], c23 = (uint32_t)ra[h][w >> 1][(w & 1) * 2 + 1];
+          const uint32_t c01 = (uint32_t)ra[st][h][w >> 1][(w & 1) * 2], c23 = (uint32_t)ra[st][h][w >> 1][(w & 1) * 2 + 1];
           // codes (int16) e0 e1 | e2 e3; hi = arithmetic >> 8 (the high byte), lo' = low byte ^ 0x80
           hi[w] = (int)__builtin_amdgcn_perm(c23, c01, 0x07050301u);
           lo[w] = (int)(__builtin_amdgcn_perm(c23, c01, 0x06040200u) ^ 0x80808080u);
-          if (!rv[h]) { hi[w] = 0; lo[w] = (int)0x80808080u; }
+          if (!rv[st][h]) { hi[w] = 0; lo[w] = (int)0x80808080u; }
         }
         *reinterpret_cast<v4i*>(&sA[buf][0][row * kRow + seg * 16]) = v4i{hi[0], hi[1], hi[2], hi[3]};
         *reinterpret_cast<v4i*>(&sA[buf][1][row * kRow + seg * 16]) = v4i{lo[0], lo[1], lo[2], lo[3]};
       } else {
         const int fill = p.a_u8off ? (int)0x80808080u : 0;
-        v4i v = ra[h][0];
-        if (!rv[h]) v = v4i{fill, fill, fill, fill};
+        v4i v = ra[st][h][0];
+        if (!rv[st][h]) v = v4i{fill, fill, fill, fill};
         *reinterpret_cast<v4i*>(&sA[buf][0][row * kRow + seg * 16]) = v;
       }
     }
 #pragma unroll
-    for (int h = 0; h < HB; ++h) *reinterpret_cast<v4i*>(&sB[buf][(lr + 64 * h) * kRow + seg * 16]) = rb[h];
+    for (int h = 0; h < HB; ++h) *reinterpret_cast<v4i*>(&sB[buf][(lr + 64 * h) * kRow + seg * 16]) = rb[st][h];
   };
 
   v4i acc[NA][MI][NJ], accw[NJ];
@@ -164,44 +165,55 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
   const bool want_w = A16 || p.a_u8off;  // sum_k W per column (the +128 term)
 
-  load_k(0);
-  store_k(0);
+  // prologue: block 0 into LDS[0], blocks 1 .. D in flight (stage b % D). nk % D == 0 (launcher) and
+  // every load / store below is unconditional (block indices clamped, a stale store into the buffer
+  // nobody reads any more is harmless): straight-line code, so the compiler's wait counts let the
+  // younger stages stay in flight instead of draining them (vmcnt(0)) at every branch
+  load_k(0, 0);
+  store_k(0, 0);
+#pragma unroll
+  for (int b = 1; b <= D; ++b) load_k(b < nk ? b : nk - 1, b % D);
   __syncthreads();
   const int r = lane & 15, q = lane >> 4;
-  for (int kb = 0; kb < nk; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nk) load_k(kb + 1);  // in flight during the MFMAs below
-    v4i bf[NJ];
+  for (int kb0 = 0; kb0 < nk; kb0 += D) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      bf[j] = *reinterpret_cast<const v4i*>(&sB[cur][(wn * (BN / 2) + j * 16 + r) * kRow + q * 16]);
+    for (int u = 0; u < D; ++u) {  // kb0 % D == 0: stage indices below are compile-time
+      const int kb = kb0 + u;
+      const int cur = kb & 1;
+      v4i bf[NJ];
 #pragma unroll
-    for (int a = 0; a < NA; ++a)
+      for (int j = 0; j < NJ; ++j)
+        bf[j] = *reinterpret_cast<const v4i*>(&sB[cur][(wn * (BN / 2) + j * 16 + r) * kRow + q * 16]);
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const v4i af = *reinterpret_cast<const v4i*>(&sA[cur][a][(wm * (BM / 2) + i * 16 + r) * kRow + q * 16]);
+      for (int a = 0; a < NA; ++a)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[a][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[a][i][j], 0, 0, 0);
+        for (int i = 0; i < MI; ++i) {
+          const v4i af = *reinterpret_cast<const v4i*>(&sA[cur][a][(wm * (BM / 2) + i * 16 + r) * kRow + q * 16]);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[a][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[j], acc[a][i][j], 0, 0, 0);
+        }
+      if (want_w) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) accw[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[j], accw[j], 0, 0, 0);
       }
-    if (want_w) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) accw[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[j], accw[j], 0, 0, 0);
+      const int st = (u + 1) % D;  // block kb + 1's stage
+      store_k(cur ^ 1, st);  // the other buffer: its readers finished before the last barrier
+      load_k(kb + 1 + D < nk ? kb + 1 + D : nk - 1, st);
+      __syncthreads();
     }
-    if (kb + 1 < nk) {
-      store_k(cur ^ 1);  // the other buffer: its readers finished before the last barrier
-    }
-    __syncthreads();
   }
 
   // ---- epilogue: lane owns column (tile col + r), rows (tile row + 4q + e)
+  // (an LDS-staged variant writing whole float4 rows measured slower: these stores are not the limit)
   const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = n0 + wn * (BN / 2) + j * 16 + r;
     if (col >= p.ncol) continue;
     const long long wsum = want_w ? (long long)accw[j][0] : 0;  // every row of accw holds sum_k W[col][k]
-    // dgrad addend: all 16 loads of this column issued before any store (p.y may alias it as far
-    // as the compiler knows, so interleaved load / store pairs would serialise)
+    // dgrad addend: all loads of this column issued before any store (p.y may alias it as far as
+    // the compiler knows, so interleaved load / store pairs would serialise)
     float av[MI][4];
     constexpr bool addv = MODE == MODE_DGRAD && ADD;
 #pragma unroll
@@ -232,10 +244,19 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
 template <int MODE, bool A16, int BM, int BN>
 void launch_tile(const IgArgs& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.ncol + BN - 1) / BN));
-  if (MODE == MODE_DGRAD && p.add_src)
-    hipLaunchKernelGGL((igemm_kernel<MODE, A16, true, BM, BN>), grid, dim3(kT), 0, st, p);
-  else
-    hipLaunchKernelGGL((igemm_kernel<MODE, A16, false, BM, BN>), grid, dim3(kT), 0, st, p);
+  // register stages in flight: a divisor of the k-block count (3x3 convs: 9 * Cin/64 -> 3; 1x1: 2),
+  // 1 for the VGPR-heavy 128x128 tiles
+  const int nk = p.d.KH * p.d.KW * (p.cred / kBK);
+  const int D = (BM == 128 && BN == 128) ? 1 : (nk % 3 == 0 ? 3 : (nk % 2 == 0 ? 2 : 1));
+#define LBT_IG(DD)                                                                      \
+  do {                                                                                  \
+    if (MODE == MODE_DGRAD && p.add_src)                                                \
+      hipLaunchKernelGGL((igemm_kernel<MODE, A16, true, BM, BN, DD>), grid, dim3(kT), 0, st, p);  \
+    else                                                                                \
+      hipLaunchKernelGGL((igemm_kernel<MODE, A16, false, BM, BN, DD>), grid, dim3(kT), 0, st, p); \
+  } while (0)
+  if (D == 3) LBT_IG(3); else if (D == 2) LBT_IG(2); else LBT_IG(1);
+#undef LBT_IG
 }
 
 // Tile choice: 64 columns when the GEMM has <= 64 (no MFMAs on padding columns), and 64 rows
@@ -246,7 +267,9 @@ int launch(const IgArgs& p, hipStream_t st) {
   if (mb > 0x7fffffff / 2 || (p.ncol + 63) / 64 > 65535) return LBT_EINVAL;
   const bool bn64 = p.ncol <= 64 || getenv_int("LBT_IGEMM_BN", 128) == 64;
   const int64_t nb = (p.ncol + (bn64 ? 63 : 127)) / (bn64 ? 64 : 128);
-  const bool bm64 = mb * nb < getenv_int("LBT_IGEMM_MIN_WG", 512);
+  // ... and always for 16-bit codes when the tile would be 128 x 128: that variant needs 256 VGPRs
+  // (one wave per SIMD), which leaves its fp32 epilogue stores unhidden
+  const bool bm64 = mb * nb < getenv_int("LBT_IGEMM_MIN_WG", 512) || (A16 && !bn64);
   if (bm64) {
     if (bn64) launch_tile<MODE, A16, 64, 64>(p, st); else launch_tile<MODE, A16, 64, 128>(p, st);
   } else {
