@@ -88,6 +88,7 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   // D register stages: the global loads of k-block b land in stage b % D, D k-blocks ahead of use
   v4i ra[D][HA][A16 ? 2 : 1], rb[D][HB];
   bool rv[D][HA];
+  const bool unit_stride = d.SH == 1 && d.SW == 1;
   auto load_k = [&](int kb, int st) {
     const int tap = kb / cblocks, cb = kb - tap * cblocks;
     const int kh = tap / d.KW, kw = tap - kh * d.KW;
@@ -99,6 +100,10 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
         sy = ay[h] * d.SH + kh - d.PT;
         sx = ax[h] * d.SW + kw - d.PL;
         ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+      } else if (unit_stride) {  // uniform: no divisions
+        sy = ay[h] + d.PT - kh;
+        sx = ax[h] + d.PL - kw;
+        ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
       } else {
         const int ny = ay[h] + d.PT - kh, nx = ax[h] + d.PL - kw;
         sy = ny / d.SH;
@@ -107,13 +112,14 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
       }
       ok = ok && arow[h];
       rv[st][h] = ok;
-      const int64_t pix = ok ? (((int64_t)an[h] * SH + sy) * SW + sx) : 0;
+      // 32-bit element offsets (launcher: every operand < 2^31 elements)
+      const uint32_t pix = ok ? (uint32_t)((an[h] * SH + sy) * SW + sx) : 0u;
       if constexpr (A16) {
-        const int16_t* src = reinterpret_cast<const int16_t*>(p.a) + pix * p.cred + cb * kBK + seg * 16;
+        const int16_t* src = reinterpret_cast<const int16_t*>(p.a) + (pix * (uint32_t)p.cred + (uint32_t)(cb * kBK + seg * 16));
         ra[st][h][0] = *reinterpret_cast<const v4i*>(src);
         ra[st][h][1] = *reinterpret_cast<const v4i*>(src + 8);
       } else {
-        const int8_t* src = reinterpret_cast<const int8_t*>(p.a) + pix * p.cred + cb * kBK + seg * 16;
+        const int8_t* src = reinterpret_cast<const int8_t*>(p.a) + (pix * (uint32_t)p.cred + (uint32_t)(cb * kBK + seg * 16));
         ra[st][h][0] = *reinterpret_cast<const v4i*>(src);
       }
     }
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
     for (int h = 0; h < HB; ++h) {
       const int col = n0 + lr + 64 * h;
       const int colc = col < p.ncol ? col : 0;
-      rb[st][h] = *reinterpret_cast<const v4i*>(p.b + ((int64_t)colc * p.ks + kb * 4 + seg) * 16);
+      rb[st][h] = *reinterpret_cast<const v4i*>(p.b + ((uint32_t)(colc * p.ks + kb * 4 + seg) << 4));
       if (col >= p.ncol) rb[st][h] = v4i{0, 0, 0, 0};
     }
   };
@@ -204,39 +210,46 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
     }
   }
 
-  // ---- epilogue: lane owns column (tile col + r), rows (tile row + 4q + e)
-  // (an LDS-staged variant writing whole float4 rows measured slower: these stores are not the limit)
+  // ---- epilogue: lane owns column (tile col + r), rows (tile row + 4q + e). Index math kept
+  // off the per-element path: one 64-bit base per column tile, 32-bit row offsets, row checks only
+  // on the last (ragged) tile; A8 sums fit int32 (launcher: K * 255 * 128 < 2^31), A16 sums are
+  // formed exactly in double (|s| < 2^53) and rounded once to fp32 -- the same value as
+  // (float)(int64) s.
   const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
+  constexpr bool addv = MODE == MODE_DGRAD && ADD;
+  const int ncol = p.ncol;
+  const int64_t rtile = m0 + wm * (BM / 2) + q * 4;  // + i * 16 + e
+  const bool full = m0 + BM <= p.M;
+  const int rlim = full ? (BM / 2) : (int)(p.M - rtile);  // rows (i * 16 + e) < rlim are real
+  const int u8 = p.a_u8off ? 128 : 0;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int col = n0 + wn * (BN / 2) + j * 16 + r;
-    if (col >= p.ncol) continue;
-    const long long wsum = want_w ? (long long)accw[j][0] : 0;  // every row of accw holds sum_k W[col][k]
-    // dgrad addend: all loads of this column issued before any store (p.y may alias it as far as
-    // the compiler knows, so interleaved load / store pairs would serialise)
+    const int ctile = n0 + wn * (BN / 2) + j * 16;
+    if (ctile >= ncol) continue;  // uniform: ncol % 16 == 0
+    const int col = ctile + r;
+    float* yp = p.y + rtile * ncol + col;
+    const float* ap = addv ? p.add_src + rtile * ncol + col : nullptr;
     float av[MI][4];
-    constexpr bool addv = MODE == MODE_DGRAD && ADD;
+    if constexpr (addv) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) av[i][e] = (i * 16 + e < rlim) ? ap[(i * 16 + e) * ncol] : 0.f;
+    }
+    const int wsum = want_w ? accw[j][0] : 0;  // every row of accw holds sum_k W[col][k]
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t row = m0 + wm * (BM / 2) + i * 16 + q * 4 + e;
-        if constexpr (addv) av[i][e] = row < p.M ? p.add_src[row * p.ncol + col] : 0.f;
-      }
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t row = m0 + wm * (BM / 2) + i * 16 + q * 4 + e;
-        if (row >= p.M) continue;
-        long long s;
-        if constexpr (A16)
-          s = 256ll * (long long)acc[0][i][j][e] + (long long)acc[1][i][j][e] + 128ll * wsum;
-        else
-          s = (long long)acc[0][i][j][e] + (p.a_u8off ? 128ll * wsum : 0ll);
-        const float v = (float)s * scale;
-        const int64_t o = row * p.ncol + col;
-        p.y[o] = addv ? v + av[i][e] : v;
+        float v;
+        if constexpr (A16) {
+          const double hs = (double)acc[0][i][j][e] * 256.0;  // exact
+          const double ls = (double)(acc[1][i][j][e] + 128 * wsum);  // |.| < 2^31: K * 255 * 128 bound
+          v = (float)(hs + ls) * scale;  // hs + ls exact (< 2^53): one rounding, as (float)(int64)
+        } else {
+          v = (float)(acc[0][i][j][e] + u8 * wsum) * scale;
+        }
+        if (full || i * 16 + e < rlim) yp[(i * 16 + e) * ncol] = addv ? v + av[i][e] : v;
       }
   }
 }
@@ -290,6 +303,9 @@ extern "C" int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* 
                                   const int32_t* colsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,
                                   void* stream) {
   if (!desc_ok(d) || d.Cin % kBK || d.Cout % 16 || !y || !wf) return LBT_EINVAL;
+  if ((int64_t)d.KH * d.KW * d.Cin * 255 * 128 >= ((int64_t)1 << 31)) return LBT_EINVAL;  // int32 epilogue sums
+  if ((int64_t)d.N * d.H * d.W * d.Cin >= ((int64_t)1 << 31) || (int64_t)ksf * 16 * d.Cout >= ((int64_t)1 << 31))
+    return LBT_EINVAL;  // 32-bit operand offsets
   if (ksf * 16 < d.KH * d.KW * d.Cin) return LBT_EINVAL;
   IgArgs p{};
   p.a = xq; p.b = wf; p.ks = ksf; p.cred = d.Cin; p.a_u8off = a_kind == 1; p.d = d; p.qa = qx; p.qb = qw;
@@ -303,6 +319,9 @@ extern "C" int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* 
 extern "C" int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
                                     lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* stream) {
   if (!desc_ok(d) || d.Cout % kBK || d.Cin % 16 || !dx || !wd) return LBT_EINVAL;
+  if ((int64_t)d.KH * d.KW * d.Cout * 255 * 128 >= ((int64_t)1 << 31)) return LBT_EINVAL;  // int32 epilogue sums
+  if ((int64_t)d.N * d.Ho * d.Wo * d.Cout >= ((int64_t)1 << 31) || (int64_t)ksd * 16 * d.Cin >= ((int64_t)1 << 31))
+    return LBT_EINVAL;  // 32-bit operand offsets
   if (ksd * 16 < d.KH * d.KW * d.Cout) return LBT_EINVAL;
   IgArgs p{};
   p.a = gq; p.b = wd; p.ks = ksd; p.cred = d.Cout; p.a_u8off = 0; p.d = d; p.qa = qg; p.qb = qw;

@@ -1,0 +1,46 @@
+"""Time single igemm launches on ResNet-50 shapes (diagnostics): python tools/igemm_probe.py"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from lbt_amd.dfxp import ops  # noqa: E402
+from lbt_amd.runtime import DfxpContext  # noqa: E402
+
+dev = "cuda"
+ctx = DfxpContext(seed=0)
+qx, qw, qg = ctx.quantizer("t/X", 9, 2), ctx.quantizer("t/W", 8, 0), ctx.quantizer("t/g", 16, -3)
+# (name, N, H, Cin, Cout, k, s, mode)
+shapes = [("l1_c3_fwd", 32, 56, 64, 256, 1, 1, "fwd"), ("l1_c1_dgrad16", 32, 56, 256, 64, 1, 1, "dgrad"),
+          ("l1_c2_fwd", 32, 56, 64, 64, 3, 1, "fwd"), ("l4_c2_fwd", 32, 7, 512, 512, 3, 1, "fwd"),
+          ("l4_c2_dgrad16", 32, 7, 512, 512, 3, 1, "dgrad"), ("l3_c2_fwd", 32, 14, 256, 256, 3, 1, "fwd")]
+for name, N, H, Cin, Cout, k, s, mode in shapes:
+    d = ops.conv_desc(N, H, H, Cin, Cout, k, k, s, s, "SAME")
+    W = torch.rand((k, k, Cin, Cout), device=dev) * 2 - 1
+    ksf, ksd = ops.packed_slices(k, k, Cin), ops.packed_slices(k, k, Cout)
+    wf = torch.zeros((Cout, ksf * 16), dtype=torch.int8, device=dev)
+    wd = torch.zeros((Cin, ksd * 16), dtype=torch.int8, device=dev)
+    ops.quantize_weight(W, qw, w_hwio=torch.empty((k, k, Cin, Cout), dtype=torch.int8, device=dev),
+                        wf=wf, ksf=ksf, wd=wd, ksd=ksd)
+    if mode == "fwd":
+        x = torch.randint(-128, 128, (N, H, H, Cin), dtype=torch.int8, device=dev)
+        y = torch.empty((N, d.Ho, d.Wo, Cout), device=dev)
+        fn = lambda: ops.conv_fwd_igemm(x, 1, wf, ksf, d, qx.desc, qw.desc, y)  # noqa: E731
+        macs = N * d.Ho * d.Wo * Cout * k * k * Cin
+    else:
+        g = torch.randint(-32768, 32768, (N, d.Ho, d.Wo, Cout), dtype=torch.int16, device=dev)
+        dx = torch.empty((N, H, H, Cin), device=dev)
+        fn = lambda: ops.conv_dgrad_igemm(g, 1, wd, ksd, d, qg.desc, qw.desc, dx)  # noqa: E731
+        macs = N * H * H * Cin * k * k * Cout
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 20 * 1000
+    print("%-16s %8.1f us  %7.1f TOPS (algorithmic)" % (name, us, 2 * macs / us / 1e6), flush=True)
