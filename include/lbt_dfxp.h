@@ -158,6 +158,16 @@ int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t* wd, int32_
 /* Wide-layer weight gradient: x offset int8 codes (post-ReLU 9-bit, q - 128), g int8 or int16
  * (g_i16) codes; Cin, Cout % 64 == 0; adds exact int64 partials into a ZEROED slab
  * [nshard][KH*KW*Cin][Cout] (pixel split b -> shard b % nshard; reduce: lbt_conv_wgrad_reduce64). */
+/* The same fwd / dgrad with a caller-owned workspace: GEMMs whose row tiles leave the 256 CUs
+ * short of work split K over workgroups (exact int32 partials + one reduce launch, bit-identical);
+ * lbt_igemm_workspace_bytes(d, mode 0 fwd | 1 dgrad, a16) = the bytes needed (0: no split).   */
+int64_t lbt_igemm_workspace_bytes(lbt_conv_desc d, int32_t mode, int32_t a16);
+int lbt_conv_fwd_igemm_ws(const void* xq, int32_t a_kind, const int8_t* wf, int32_t ksf, const int32_t* colsum,
+                          lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, void* ws, int64_t ws_bytes,
+                          void* stream);
+int lbt_conv_dgrad_igemm_ws(const void* gq, int32_t g_i16, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                            lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* ws, int64_t ws_bytes,
+                            void* stream);
 int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
                          int32_t nsplit, int32_t nshard, void* stream);
 /* ... storing one partial per pixel split: slab [nsplit][KH*KW*Cin][Cout] is fully WRITTEN (no

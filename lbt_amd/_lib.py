@@ -131,6 +131,9 @@ _SIGS = {
     "lbt_conv_fwd_igemm": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_conv_dgrad_igemm": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_igemm": [_P, _P, c_int32, ConvDesc, _P, c_int32, c_int32, _P],
+    "lbt_igemm_workspace_bytes": [ConvDesc, c_int32, c_int32],
+    "lbt_conv_fwd_igemm_ws": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P, c_int64, _P],
+    "lbt_conv_dgrad_igemm_ws": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int64, _P],
     "lbt_conv_wgrad_igemm_store": [_P, _P, c_int32, ConvDesc, _P, c_int32, _P],
     "lbt_conv_dgrad_chain_i8w4": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_dgrad_chain_i8": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
@@ -213,6 +216,7 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = c_int32
+    lib.lbt_igemm_workspace_bytes.restype = c_int64  # the one int64-valued query
     if lib.lbt_abi_version() != ABI_VERSION:
         raise ImportError("lbt_amd ABI mismatch: library %d, bindings %d" % (lib.lbt_abi_version(), ABI_VERSION))
     _lib = lib

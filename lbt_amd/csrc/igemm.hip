@@ -50,6 +50,11 @@ struct IgArgs {
   const float* add_src;
   int64_t M;
   int ncol;
+  // split-K: blockIdx.z = split, each taking nk / ksplit consecutive k-blocks and STORING its exact
+  // int32 partial sums (A8: one component; A16: hi and lo' + 128 sum W) into part[split][comp][M][ncol];
+  // igemm_splitk_reduce_kernel adds the splits and runs the epilogue (ksplit == 1: none of this)
+  int ksplit;
+  int32_t* part;
 };
 
 // BM x BN workgroup tile (64 or 128 each), 2 x 2 waves of (BM/2) x (BN/2): MI x NJ MFMA tiles
@@ -67,7 +72,8 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   const lbt_conv_desc& d = p.d;
   const int OH = MODE == MODE_FWD ? d.Ho : d.H, OW = MODE == MODE_FWD ? d.Wo : d.W;
   const int SH = MODE == MODE_FWD ? d.H : d.Ho, SW = MODE == MODE_FWD ? d.W : d.Wo;
-  const int cblocks = p.cred / kBK, nk = d.KH * d.KW * cblocks;
+  const int cblocks = p.cred / kBK, nk_all = d.KH * d.KW * cblocks;
+  const int nk = nk_all / p.ksplit, kbase = (int)blockIdx.z * nk;  // this split's k-blocks
 
   // ---- loader roles: A rows (t >> 2) and (t >> 2) + 64, 16-byte segment (t & 3) of the 64 channels
   // (A16: 32-byte segments = 16 codes); B columns likewise
@@ -89,7 +95,8 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   v4i ra[D][HA][A16 ? 2 : 1], rb[D][HB];
   bool rv[D][HA];
   const bool unit_stride = d.SH == 1 && d.SW == 1;
-  auto load_k = [&](int kb, int st) {
+  auto load_k = [&](int kbl, int st) {
+    const int kb = kbase + kbl;
     const int tap = kb / cblocks, cb = kb - tap * cblocks;
     const int kh = tap / d.KW, kw = tap - kh * d.KW;
 #pragma unroll
@@ -222,6 +229,29 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   const bool full = m0 + BM <= p.M;
   const int rlim = full ? (BM / 2) : (int)(p.M - rtile);  // rows (i * 16 + e) < rlim are real
   const int u8 = p.a_u8off ? 128 : 0;
+  if (p.ksplit > 1) {  // uniform: store this split's exact partials
+    const int64_t plane = p.M * ncol;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int ctile = n0 + wn * (BN / 2) + j * 16;
+      if (ctile >= ncol) continue;
+      const int wsum = want_w ? accw[j][0] : 0;
+      int32_t* pp = p.part + (int64_t)blockIdx.z * (A16 ? 2 : 1) * plane + rtile * ncol + ctile + r;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (!(full || i * 16 + e < rlim)) continue;
+          if constexpr (A16) {
+            pp[(i * 16 + e) * ncol] = acc[0][i][j][e];
+            pp[plane + (i * 16 + e) * ncol] = acc[1][i][j][e] + 128 * wsum;
+          } else {
+            pp[(i * 16 + e) * ncol] = acc[0][i][j][e] + u8 * wsum;
+          }
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int ctile = n0 + wn * (BN / 2) + j * 16;
@@ -254,12 +284,44 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   }
 }
 
+// Sum of the split partials + the epilogue of igemm_kernel, element-wise (4 per thread).
+template <bool A16, bool ADD>
+__global__ __launch_bounds__(256) void igemm_splitk_reduce_kernel(IgArgs p) {
+  const int64_t plane = p.M * p.ncol;
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= plane) return;
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
+  int4 s0 = make_int4(0, 0, 0, 0), s1 = make_int4(0, 0, 0, 0);
+  for (int z = 0; z < p.ksplit; ++z) {
+    const int4 a = *reinterpret_cast<const int4*>(p.part + (int64_t)z * (A16 ? 2 : 1) * plane + i4);
+    s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+    if constexpr (A16) {
+      const int4 b = *reinterpret_cast<const int4*>(p.part + ((int64_t)z * 2 + 1) * plane + i4);
+      s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+    }
+  }
+  const int h[4] = {s0.x, s0.y, s0.z, s0.w}, l[4] = {s1.x, s1.y, s1.z, s1.w};
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if constexpr (A16)
+      v[k] = (float)((double)h[k] * 256.0 + (double)l[k]) * scale;  // exact sum, one rounding
+    else
+      v[k] = (float)h[k] * scale;
+  }
+  if constexpr (ADD) {
+    const float4 a = *reinterpret_cast<const float4*>(p.add_src + i4);
+    v[0] = v[0] + a.x; v[1] = v[1] + a.y; v[2] = v[2] + a.z; v[3] = v[3] + a.w;
+  }
+  *reinterpret_cast<float4*>(p.y + i4) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 template <int MODE, bool A16, int BM, int BN>
 void launch_tile(const IgArgs& p, hipStream_t st) {
-  const dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.ncol + BN - 1) / BN));
-  // register stages in flight: a divisor of the k-block count (3x3 convs: 9 * Cin/64 -> 3; 1x1: 2),
-  // 1 for the VGPR-heavy 128x128 tiles
-  const int nk = p.d.KH * p.d.KW * (p.cred / kBK);
+  const dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.ncol + BN - 1) / BN), (unsigned)p.ksplit);
+  // register stages in flight: a divisor of the split's k-block count (3x3 convs: 9 * Cin/64 -> 3;
+  // 1x1: 2), 1 for the VGPR-heavy 128x128 tiles
+  const int nk = p.d.KH * p.d.KW * (p.cred / kBK) / p.ksplit;
   const int D = (BM == 128 && BN == 128) ? 1 : (nk % 3 == 0 ? 3 : (nk % 2 == 0 ? 2 : 1));
 #define LBT_IG(DD)                                                                      \
   do {                                                                                  \
@@ -270,6 +332,35 @@ void launch_tile(const IgArgs& p, hipStream_t st) {
   } while (0)
   if (D == 3) LBT_IG(3); else if (D == 2) LBT_IG(2); else LBT_IG(1);
 #undef LBT_IG
+  if (p.ksplit > 1) {
+    const dim3 g2((unsigned)((p.M * p.ncol / 4 + 255) / 256));
+    if (MODE == MODE_DGRAD && p.add_src)
+      hipLaunchKernelGGL((igemm_splitk_reduce_kernel<A16, true>), g2, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((igemm_splitk_reduce_kernel<A16, false>), g2, dim3(256), 0, st, p);
+  }
+}
+
+// Split-K factor: when even 64 x 64-row tiles leave the chip with fewer than ~2 workgroups per CU
+// and the k loop is long, the smallest divisor of the k-block count that reaches ~512 workgroups
+// (each split keeping >= 4 k-blocks). 1 = no split.
+int choose_ksplit(int64_t M, int ncol, int nk) {
+  const int64_t tiles = ((M + 63) / 64) * ((ncol + 127) / 128);
+  if (tiles >= 256 || nk < 8 || getenv_int("LBT_IGEMM_SPLITK", 1) == 0) return 1;
+  static const int cand[] = {2, 3, 4, 6, 8, 9, 12, 16};
+  int best = 1;
+  for (int c : cand) {
+    if (nk % c || nk / c < 4) continue;
+    best = c;
+    if (tiles * c >= 512) break;
+  }
+  return best;
+}
+
+// workspace bytes a split launch needs (0: none)
+int64_t splitk_bytes(int64_t M, int ncol, int nk, bool a16) {
+  const int ks = choose_ksplit(M, ncol, nk);
+  return ks > 1 ? (int64_t)ks * (a16 ? 2 : 1) * M * ncol * 4 : 0;
 }
 
 // Tile choice: 64 columns when the GEMM has <= 64 (no MFMAs on padding columns), and 64 rows
@@ -282,7 +373,7 @@ int launch(const IgArgs& p, hipStream_t st) {
   const int64_t nb = (p.ncol + (bn64 ? 63 : 127)) / (bn64 ? 64 : 128);
   // ... and always for 16-bit codes when the tile would be 128 x 128: that variant needs 256 VGPRs
   // (one wave per SIMD), which leaves its fp32 epilogue stores unhidden
-  const bool bm64 = mb * nb < getenv_int("LBT_IGEMM_MIN_WG", 512) || (A16 && !bn64);
+  const bool bm64 = mb * nb < getenv_int("LBT_IGEMM_MIN_WG", 512) || (A16 && !bn64) || p.ksplit > 1;
   if (bm64) {
     if (bn64) launch_tile<MODE, A16, 64, 64>(p, st); else launch_tile<MODE, A16, 64, 128>(p, st);
   } else {
@@ -311,6 +402,36 @@ extern "C" int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* 
   p.a = xq; p.b = wf; p.ks = ksf; p.cred = d.Cin; p.a_u8off = a_kind == 1; p.d = d; p.qa = qx; p.qb = qw;
   p.colsum = colsum; p.y = y; p.add_src = nullptr; p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
   if (p.M * p.ncol >= ((int64_t)1 << 40)) return LBT_EINVAL;
+  p.ksplit = 1;
+  hipStream_t st = (hipStream_t)stream;
+  return a_kind == 2 ? launch<MODE_FWD, true>(p, st) : launch<MODE_FWD, false>(p, st);
+}
+
+// Workspace of the split-K variants below (0: that GEMM does not split). mode 0 fwd, 1 dgrad.
+extern "C" int64_t lbt_igemm_workspace_bytes(lbt_conv_desc d, int32_t mode, int32_t a16) {
+  if (!desc_ok(d)) return 0;
+  if (mode == 0)
+    return splitk_bytes((int64_t)d.N * d.Ho * d.Wo, d.Cout, d.KH * d.KW * (d.Cin / kBK), a16 != 0);
+  return splitk_bytes((int64_t)d.N * d.H * d.W, d.Cin, d.KH * d.KW * (d.Cout / kBK), a16 != 0);
+}
+
+// lbt_conv_fwd_igemm with a caller-owned workspace (ws_bytes >= lbt_igemm_workspace_bytes): the
+// short-M / long-K GEMMs split K over workgroups, exact int32 partials, one reduce launch after.
+extern "C" int lbt_conv_fwd_igemm_ws(const void* xq, int32_t a_kind, const int8_t* wf, int32_t ksf,
+                                     const int32_t* colsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y,
+                                     void* ws, int64_t ws_bytes, void* stream) {
+  if (!desc_ok(d) || d.Cin % kBK || d.Cout % 16 || !y || !wf) return LBT_EINVAL;
+  if ((int64_t)d.KH * d.KW * d.Cin * 255 * 128 >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  if ((int64_t)d.N * d.H * d.W * d.Cin >= ((int64_t)1 << 31) || (int64_t)ksf * 16 * d.Cout >= ((int64_t)1 << 31))
+    return LBT_EINVAL;
+  if (ksf * 16 < d.KH * d.KW * d.Cin) return LBT_EINVAL;
+  IgArgs p{};
+  p.a = xq; p.b = wf; p.ks = ksf; p.cred = d.Cin; p.a_u8off = a_kind == 1; p.d = d; p.qa = qx; p.qb = qw;
+  p.colsum = colsum; p.y = y; p.add_src = nullptr; p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
+  if (p.M * p.ncol >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  const int64_t need = lbt_igemm_workspace_bytes(d, 0, a_kind == 2);
+  p.ksplit = (need > 0 && ws && ws_bytes >= need) ? choose_ksplit(p.M, p.ncol, d.KH * d.KW * (d.Cin / kBK)) : 1;
+  p.part = reinterpret_cast<int32_t*>(ws);
   hipStream_t st = (hipStream_t)stream;
   return a_kind == 2 ? launch<MODE_FWD, true>(p, st) : launch<MODE_FWD, false>(p, st);
 }
@@ -326,6 +447,26 @@ extern "C" int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t*
   IgArgs p{};
   p.a = gq; p.b = wd; p.ks = ksd; p.cred = d.Cout; p.a_u8off = 0; p.d = d; p.qa = qg; p.qb = qw;
   p.colsum = nullptr; p.y = dx; p.add_src = add_src; p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
+  p.ksplit = 1;
+  hipStream_t st = (hipStream_t)stream;
+  return g_i16 ? launch<MODE_DGRAD, true>(p, st) : launch<MODE_DGRAD, false>(p, st);
+}
+
+extern "C" int lbt_conv_dgrad_igemm_ws(const void* gq, int32_t g_i16, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                                       lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* ws,
+                                       int64_t ws_bytes, void* stream) {
+  if (!desc_ok(d) || d.Cout % kBK || d.Cin % 16 || !dx || !wd) return LBT_EINVAL;
+  if ((int64_t)d.KH * d.KW * d.Cout * 255 * 128 >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  if ((int64_t)d.N * d.Ho * d.Wo * d.Cout >= ((int64_t)1 << 31) || (int64_t)ksd * 16 * d.Cin >= ((int64_t)1 << 31))
+    return LBT_EINVAL;
+  if (ksd * 16 < d.KH * d.KW * d.Cout) return LBT_EINVAL;
+  IgArgs p{};
+  p.a = gq; p.b = wd; p.ks = ksd; p.cred = d.Cout; p.a_u8off = 0; p.d = d; p.qa = qg; p.qb = qw;
+  p.colsum = nullptr; p.y = dx; p.add_src = add_src; p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
+  if (p.M * p.ncol >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  const int64_t need = lbt_igemm_workspace_bytes(d, 1, g_i16);
+  p.ksplit = (need > 0 && ws && ws_bytes >= need) ? choose_ksplit(p.M, p.ncol, d.KH * d.KW * (d.Cout / kBK)) : 1;
+  p.part = reinterpret_cast<int32_t*>(ws);
   hipStream_t st = (hipStream_t)stream;
   return g_i16 ? launch<MODE_DGRAD, true>(p, st) : launch<MODE_DGRAD, false>(p, st);
 }

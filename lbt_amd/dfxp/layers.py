@@ -176,9 +176,17 @@ class Conv2d_q(Layer_q):
         self.xq = xq
         self.quantize_weights()
         y = self._c.get("y", (N, d.Ho, d.Wo, Cout), torch.float32, xq.device)
-        ops.conv_fwd_igemm(xq, 1, self.wf, self.ksf, d, self.X_range.desc, self.W_range.desc, y)
+        ops.conv_fwd_igemm_ws(xq, 1, self.wf, self.ksf, d, self.X_range.desc, self.W_range.desc, y,
+                              self._ws(d, 0, False))
         self.y = y
         return y
+
+    def _ws(self, d, mode, a16):
+        """Split-K workspace of this conv's wide GEMM (None when it does not split)."""
+        n = ops.igemm_workspace_bytes(d, mode, a16)
+        if n == 0:
+            return None
+        return self._c.get("ws%d" % mode, ((n + 3) // 4,), torch.int32, self.ctx.device)
 
     def bwd_codes16(self, gq16, add_src=None):
         """Backward from int16 gradient codes the caller already quantised with self.grad_range:
@@ -189,8 +197,8 @@ class Conv2d_q(Layer_q):
             return None
         d = self.d
         dx = self._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, gq16.device)
-        ops.conv_dgrad_igemm(gq16, 1, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx,
-                             add_src=add_src)
+        ops.conv_dgrad_igemm_ws(gq16, 1, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx,
+                                self._ws(d, 1, True), add_src=add_src)
         return dx
 
     def quantize_weights(self):

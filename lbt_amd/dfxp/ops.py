@@ -505,6 +505,23 @@ def igemm_ok(c_gather, c_out):
     return c_gather % 64 == 0 and c_out % 16 == 0
 
 
+def igemm_workspace_bytes(d, mode, a16):
+    return int(_lib.load().lbt_igemm_workspace_bytes(d, int(mode), int(a16)))
+
+
+def conv_fwd_igemm_ws(xq, a_kind, wf, ksf, d, qx, qw, y, ws):
+    M = d.N * d.Ho * d.Wo
+    with _Timed("igemm_kernel<fwd>", xq.numel() * xq.element_size() + wf.numel() + 4 * M * d.Cout):
+        call("lbt_conv_fwd_igemm_ws", ptr(xq), int(a_kind), ptr(wf), int(ksf), None, d, qx, qw, ptr(y), ptr(ws),
+             0 if ws is None else ws.numel() * ws.element_size(), stream())
+
+
+def conv_dgrad_igemm_ws(gq, g_i16, wd, ksd, d, qg, qw, dx, ws, add_src=None):
+    with _Timed("igemm_kernel<dgrad>", gq.numel() * gq.element_size() + wd.numel() + 4 * dx.numel()):
+        call("lbt_conv_dgrad_igemm_ws", ptr(gq), int(g_i16), ptr(wd), int(ksd), d, qg, qw, ptr(dx), ptr(add_src),
+             ptr(ws), 0 if ws is None else ws.numel() * ws.element_size(), stream())
+
+
 def conv_fwd_igemm(xq, a_kind, wf, ksf, d, qx, qw, y):
     M = d.N * d.Ho * d.Wo
     with _Timed("igemm_kernel<fwd>", xq.numel() * xq.element_size() + wf.numel() + 4 * M * d.Cout):

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "lbt_dfxp.h")
 
 def header_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^int\s+(lbt_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t)\s+(lbt_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_and_bindings_agree():

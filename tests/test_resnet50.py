@@ -327,3 +327,37 @@ def test_softmax_xent_wide():
     onehot[np.arange(32), y] = 1
     assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss)
     assert np.allclose(dz.cpu().numpy(), (p - onehot) / 32, rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,Cin,Cout,k", [(2, 7, 512, 512, 3), (4, 7, 1024, 1024, 1), (1, 14, 256, 256, 3)])
+def test_igemm_splitk_matches_generic(N, H, Cin, Cout, k):
+    """Short-M / long-K wide GEMMs split K over workgroups (exact int32 partials + reduce): fwd with
+    offset int8 codes, dgrad with int16 codes and the addend, bit-identical to the generic kernels."""
+    from lbt_amd.dfxp import ops
+    from lbt_amd.runtime import DfxpContext
+    rng = np.random.default_rng(N * H + Cin + Cout)
+    ctx = DfxpContext(seed=0)
+    qx, qw, qg = ctx.quantizer("t/X", 9, 2), ctx.quantizer("t/W", 8, 0), ctx.quantizer("t/g", 16, -3)
+    d = ops.conv_desc(N, H, H, Cin, Cout, k, k, 1, 1, "SAME")
+    assert ops.igemm_workspace_bytes(d, 0, False) > 0 and ops.igemm_workspace_bytes(d, 1, True) > 0
+    W = torch.from_numpy(rng.uniform(-1, 1, size=(k, k, Cin, Cout)).astype(np.float32)).to(DEV)
+    w_hwio = torch.empty((k, k, Cin, Cout), dtype=torch.int8, device=DEV)
+    ksf, ksd = ops.packed_slices(k, k, Cin), ops.packed_slices(k, k, Cout)
+    wf = torch.zeros((Cout, ksf * 16), dtype=torch.int8, device=DEV)
+    wd = torch.zeros((Cin, ksd * 16), dtype=torch.int8, device=DEV)
+    ops.quantize_weight(W, qw, w_hwio=w_hwio, wf=wf, ksf=ksf, wd=wd, ksd=ksd)
+    x = rng.integers(0, 256, size=(N, H, H, Cin))
+    x_off = torch.from_numpy((x - 128).astype(np.int8)).to(DEV)
+    ws = torch.empty(ops.igemm_workspace_bytes(d, 0, False) // 4, dtype=torch.int32, device=DEV)
+    y1, y2 = torch.empty((N, H, H, Cout), device=DEV), torch.empty((N, H, H, Cout), device=DEV)
+    ops.conv_fwd_igemm_ws(x_off, 1, wf, ksf, d, qx.desc, qw.desc, y1, ws)
+    ops.conv_fwd_generic(torch.from_numpy(x.astype(np.int16)).to(DEV), True, w_hwio, d, qx.desc, qw.desc, y2)
+    assert torch.equal(y1, y2)
+    g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, H, H, Cout)).astype(np.int16)).to(DEV)
+    add = torch.from_numpy(rng.normal(size=(N, H, H, Cin)).astype(np.float32)).to(DEV)
+    ws2 = torch.empty(ops.igemm_workspace_bytes(d, 1, True) // 4, dtype=torch.int32, device=DEV)
+    dx1, dx2 = torch.empty((N, H, H, Cin), device=DEV), torch.empty((N, H, H, Cin), device=DEV)
+    ops.conv_dgrad_igemm_ws(g, 1, wd, ksd, d, qg.desc, qw.desc, dx1, ws2, add_src=add)
+    ops.conv_dgrad_generic16(g, w_hwio, d, qg.desc, qw.desc, dx2)
+    assert torch.equal(dx1, dx2 + add)
