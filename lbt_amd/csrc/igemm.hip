@@ -488,12 +488,13 @@ constexpr int kWP = 64;
 // STORE: the workgroup's partial is STORED into slab[split] (every element of slab[nsplit][K][Cout]
 // has exactly one writer -- no zeroing, no atomics); else atomically added into shard split % nshard.
 template <bool G16, bool STORE>
-__global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
+__global__ __launch_bounds__(kT, 2) void wgrad_wide_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
                                                         lbt_conv_desc d, long long* __restrict__ slab, int64_t P,
                                                         int nsplit, int nshard) {
   constexpr int NG = G16 ? 2 : 1;  // G images: (gh, gl') or g
+  constexpr int NBS = G16 ? 2 : 4, COW = 16 * NBS;  // output-channel slices per workgroup (VGPR budget)
   // per wave: X [4 slices][64 px][16 B], G [NG][4 slices][64 px][16 B]; reused as the int64 tile
-  __shared__ __attribute__((aligned(16))) int8_t lds[4][(4 + 4 * NG) * kWP * 16];
+  __shared__ __attribute__((aligned(16))) int8_t lds[4][(4 + NBS * NG) * kWP * 16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int cib = d.Cin / 64;
@@ -505,44 +506,50 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
   const int64_t p0 = (int64_t)blockIdx.x * per;
   const int64_t p1 = p0 + per < P ? p0 + per : P;
   const uint32_t HWo = (uint32_t)d.Ho * d.Wo;
-  v4i acc[NG][4][4], ax[4], ag[NG][4];
+  v4i acc[NG][4][NBS], ax[4], ag[NG][NBS];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     ax[a] = v4i{0, 0, 0, 0};
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < NBS; ++b)
 #pragma unroll
       for (int h = 0; h < NG; ++h) acc[h][a][b] = v4i{0, 0, 0, 0};
   }
 #pragma unroll
   for (int h = 0; h < NG; ++h)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) ag[h][b] = v4i{0, 0, 0, 0};
+    for (int b = 0; b < NBS; ++b) ag[h][b] = v4i{0, 0, 0, 0};
   const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
   long long nchunks = 0;
-  for (int64_t c0 = p0 + (int64_t)wave * kWP; c0 < p1; c0 += 4 * kWP) {
-    ++nchunks;
+  // operand registers of one 64-pixel chunk; the next chunk's loads are issued right after this
+  // chunk's registers are in LDS, so they fly during its MFMAs (no extra registers)
+  v4i xs[4], gs[G16 ? 2 * NBS : NBS];
+  bool xv = false, pv = false;
+  auto issue = [&](int64_t c0) {
     const int64_t p = c0 + lane;
-    const bool pv = p < p1;
+    pv = p < p1;
     const uint32_t pu = (uint32_t)(pv ? p : p0);
     const uint32_t n = pu / HWo, rem = pu - n * HWo;
     const int oh = (int)(rem / (uint32_t)d.Wo), ow = (int)(rem - (uint32_t)oh * (uint32_t)d.Wo);
     const int ih = oh * d.SH + kh - d.PT, iw = ow * d.SW + kw - d.PL;
-    const bool xv = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+    xv = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
     const int8_t* xp = xq + (xv ? ((((int64_t)n * d.H + ih) * d.W + iw) * d.Cin + cb * 64) : 0);
-    v4i xs[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) xs[s] = *reinterpret_cast<const v4i*>(xp + s * 16);
-    v4i gs[G16 ? 8 : 4];
     if constexpr (G16) {
-      const int16_t* gp = reinterpret_cast<const int16_t*>(gq) + (int64_t)pu * d.Cout + ob * 64;
+      const int16_t* gp = reinterpret_cast<const int16_t*>(gq) + (int64_t)pu * d.Cout + ob * COW;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) gs[s] = *reinterpret_cast<const v4i*>(gp + s * 8);
+      for (int s = 0; s < 2 * NBS; ++s) gs[s] = *reinterpret_cast<const v4i*>(gp + s * 8);
     } else {
-      const int8_t* gp = reinterpret_cast<const int8_t*>(gq) + (int64_t)pu * d.Cout + ob * 64;
+      const int8_t* gp = reinterpret_cast<const int8_t*>(gq) + (int64_t)pu * d.Cout + ob * COW;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) gs[s] = *reinterpret_cast<const v4i*>(gp + s * 16);
+      for (int s = 0; s < NBS; ++s) gs[s] = *reinterpret_cast<const v4i*>(gp + s * 16);
     }
+  };
+  const int64_t cfirst = p0 + (int64_t)wave * kWP;
+  issue(cfirst < p1 ? cfirst : p0);
+  for (int64_t c0 = cfirst; c0 < p1; c0 += 4 * kWP) {
+    ++nchunks;
     const int fx = (int)0x80808080u;  // x' = -128: x = 0 (padding, pixels past the range)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -551,7 +558,7 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
     }
     if constexpr (G16) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {  // 16 codes -> 16 gh bytes, 16 gl' bytes; past the range g = 0
+      for (int s = 0; s < NBS; ++s) {  // 16 codes -> 16 gh bytes, 16 gl' bytes; past the range g = 0
         int hi[4], lo[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -561,24 +568,26 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
           lo[w] = pv ? (int)(__builtin_amdgcn_perm(c23, c01, 0x06040200u) ^ 0x80808080u) : (int)0x80808080u;
         }
         *reinterpret_cast<v4i*>(Gi + (s * kWP + lane) * 16) = v4i{hi[0], hi[1], hi[2], hi[3]};
-        *reinterpret_cast<v4i*>(Gi + ((4 + s) * kWP + lane) * 16) = v4i{lo[0], lo[1], lo[2], lo[3]};
+        *reinterpret_cast<v4i*>(Gi + ((NBS + s) * kWP + lane) * 16) = v4i{lo[0], lo[1], lo[2], lo[3]};
       }
     } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < NBS; ++s) {
         if (!pv) gs[s] = v4i{0, 0, 0, 0};
         *reinterpret_cast<v4i*>(Gi + (s * kWP + lane) * 16) = gs[s];
       }
     }
+    const int64_t cn = c0 + 4 * kWP;
+    issue(cn < p1 ? cn : c0);  // the next chunk (clamped: straight-line, a redundant last load)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    v4i gf[NG][4];
+    v4i gf[NG][NBS];
 #pragma unroll
     for (int h = 0; h < NG; ++h)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        gf[h][b] = tr_frag(Gi + (h * 4 + b) * kWP * 16, 16 * q, lane);
+      for (int b = 0; b < NBS; ++b) {
+        gf[h][b] = tr_frag(Gi + (h * NBS + b) * kWP * 16, 16 * q, lane);
         ag[h][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, gf[h][b], ag[h][b], 0, 0, 0);
       }
 #pragma unroll
@@ -588,7 +597,7 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
 #pragma unroll
       for (int h = 0; h < NG; ++h)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[h][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf, gf[h][b], acc[h][a][b], 0, 0, 0);
+        for (int b = 0; b < NBS; ++b) acc[h][a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf, gf[h][b], acc[h][a][b], 0, 0, 0);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -599,11 +608,11 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
   __syncthreads();
   long long* tile = reinterpret_cast<long long*>(&lds[0][0]);
   const long long npix = nchunks * kWP;
-  long long vv[4][4][4];
+  long long vv[4][NBS][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < NBS; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if constexpr (G16) {
@@ -618,10 +627,10 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < NBS; ++b)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            long long* t = &tile[(a * 16 + q * 4 + i) * 64 + b * 16 + r];
+            long long* t = &tile[(a * 16 + q * 4 + i) * COW + b * 16 + r];
             *t = w == 0 ? vv[a][b][i] : *t + vv[a][b][i];
           }
     }
@@ -629,9 +638,9 @@ __global__ __launch_bounds__(kT) void wgrad_wide_kernel(const int8_t* __restrict
   }
   const int64_t shard = STORE ? (int64_t)blockIdx.x : (int64_t)(blockIdx.x % nshard);
   long long* dst = slab + (shard * (d.KH * d.KW) + tap) * d.Cin * d.Cout;
-  for (int i = threadIdx.x; i < 64 * 64; i += kT) {
+  for (int i = threadIdx.x; i < 64 * COW; i += kT) {
     const long long v = tile[i];
-    const int ci = cb * 64 + (i >> 6), co = ob * 64 + (i & 63);
+    const int ci = cb * 64 + i / COW, co = ob * COW + i % COW;
     if constexpr (STORE)
       dst[(int64_t)ci * d.Cout + co] = v;
     else if (v)
@@ -650,7 +659,7 @@ extern "C" int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_
   if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
   const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
   if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
-  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
+  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / (g_i16 ? 32 : 64)));
   hipStream_t st = (hipStream_t)stream;
   if (g_i16)
     hipLaunchKernelGGL((wgrad_wide_kernel<true, false>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
@@ -671,7 +680,7 @@ extern "C" int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int3
   if ((P + nsplit - 1) / nsplit > 4 * 131072) return LBT_EINVAL;  // int32 MFMA sums of a wave stay exact
   const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
   if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
-  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
+  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / (g_i16 ? 32 : 64)));
   hipStream_t st = (hipStream_t)stream;
   if (g_i16)
     hipLaunchKernelGGL((wgrad_wide_kernel<true, true>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
