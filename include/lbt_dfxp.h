@@ -158,6 +158,13 @@ int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t* wd, int32_
 /* Wide-layer weight gradient: x offset int8 codes (post-ReLU 9-bit, q - 128), g int8 or int16
  * (g_i16) codes; Cin, Cout % 64 == 0; adds exact int64 partials into a ZEROED slab
  * [nshard][KH*KW*Cin][Cout] (pixel split b -> shard b % nshard; reduce: lbt_conv_wgrad_reduce64). */
+/* Wide forward whose epilogue is the consuming Normalization_q's input quantiser (Conv2d_q.forward
+ * :291 then Normalization_q :584-588): int8 codes yq [N*Ho*Wo][Cout] of qout (<= 8 bits), its
+ * overflow counters and exact per-channel sums chsum[NSHARD][2*Cout] (sum q, sum q^2) -- the
+ * same as lbt_conv_fwd_igemm followed by lbt_dfxp_quantize(y, qout, chsum), without y.
+ * a_kind 0 / 1 (int8 / offset int8 codes).                                                   */
+int lbt_conv_fwd_igemm_q(const void* xq, int32_t a_kind, const int8_t* wf, int32_t ksf, lbt_conv_desc d, lbt_qdesc qx,
+                         lbt_qdesc qw, int8_t* yq, lbt_qdesc qout, int64_t* chsum, void* stream);
 /* The same fwd / dgrad with a caller-owned workspace: GEMMs whose row tiles leave the 256 CUs
  * short of work split K over workgroups (exact int32 partials + one reduce launch, bit-identical);
  * lbt_igemm_workspace_bytes(d, mode 0 fwd | 1 dgrad, a16) = the bytes needed (0: no split).   */

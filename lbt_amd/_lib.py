@@ -132,6 +132,7 @@ _SIGS = {
     "lbt_conv_dgrad_igemm": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_igemm": [_P, _P, c_int32, ConvDesc, _P, c_int32, c_int32, _P],
     "lbt_igemm_workspace_bytes": [ConvDesc, c_int32, c_int32],
+    "lbt_conv_fwd_igemm_q": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, QDesc, _P, _P],
     "lbt_conv_fwd_igemm_ws": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P, c_int64, _P],
     "lbt_conv_dgrad_igemm_ws": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int64, _P],
     "lbt_conv_wgrad_igemm_store": [_P, _P, c_int32, ConvDesc, _P, c_int32, _P],

@@ -55,7 +55,91 @@ struct IgArgs {
   // igemm_splitk_reduce_kernel adds the splits and runs the epilogue (ksplit == 1: none of this)
   int ksplit;
   int32_t* part;
+  // fwd only, ksplit == 1: the epilogue is the consuming Normalization_q's input quantiser --
+  // int8 codes yq, overflow counters of qout, exact per-channel sums chsum[NSHARD][2 * ncol]
+  // (sum q, sum q^2); noise index = (row % hw) * ncol + col (noise over shape[1:]); y unused
+  int8_t* yq;
+  lbt_qdesc qout;
+  int64_t* chsum;
+  int hw;
 };
+
+// The conv-output quantiser in the GEMM epilogue (fwd, A8). Lane (r, q) holds column cw + 16 j + r
+// of rows rtile + 16 i + e. Noise: one Philox4x32 call yields the 4 values of 4 consecutive channels
+// of one pixel, so the 4 lanes r = 4g .. 4g+3 each draw the block of one of their 4 rows (e = r & 3)
+// and pass values round in 4 shuffle steps -- one Philox call per 4 outputs, the same values as
+// quantize_rows_kernel's qnoise4 of that block. Rows past M quantise 0 (no overflow, code 0).
+template <int MI, int NJ>
+LBT_DEV void quant_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i (&accw)[NJ], int u8, float scale,
+                            int64_t rtile, int rlim, bool full, int cw, int r, int q) {
+  const QState qs = qstate(p.qout);
+  const int ncol = p.ncol;
+  const int jj = r & 3, gbase = (int)(threadIdx.x & 63) & ~3;  // this lane's slot and its group's first lane
+  int ov1w = 0, ov2w = 0;
+  int cs1[NJ], cs2[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) { cs1[j] = 0; cs2[j] = 0; }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    // the pixel (within its image) of row e = jj of this i: this lane draws its noise block
+    const int64_t myrow = rtile + i * 16 + jj;
+    const uint32_t pix = (uint32_t)((myrow < p.M ? myrow : 0) % (uint32_t)p.hw);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = cw + j * 16 + r;
+      if (cw + j * 16 >= ncol) continue;  // uniform
+      const uint64_t blk = ((uint64_t)pix * (uint32_t)ncol + (uint32_t)(col & ~3)) >> 2;
+      Noise4 mine = {{0.f, 0.f, 0.f, 0.f}};
+      if (p.qout.stochastic) mine = qnoise4(p.qout, qs.step, blk);
+      float u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        // step k: lane jj sends its block's value for column (jj - k) & 3 of the group and
+        // receives, from lane (jj + k) & 3, the value of this lane's column for row (jj + k) & 3
+        const int sc = (jj - k) & 3;
+        const float send = sc == 0 ? mine.u[0] : sc == 1 ? mine.u[1] : sc == 2 ? mine.u[2] : mine.u[3];
+        const float got = __shfl(send, gbase + ((jj + k) & 3), 64);
+        const int re = (jj + k) & 3;
+        if (k == 0) u[0] = u[1] = u[2] = u[3] = 0.f;
+        u[0] = re == 0 ? got : u[0];
+        u[1] = re == 1 ? got : u[1];
+        u[2] = re == 2 ? got : u[2];
+        u[3] = re == 3 ? got : u[3];
+      }
+      const int wsum = accw[j][0];
+      int8_t* yp = p.yq + (rtile + i * 16) * ncol + col;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = full || i * 16 + e < rlim;
+        const float v = ok ? (float)(acc[i][j][e] + u8 * wsum) * scale : 0.f;
+        const int c = quant_w<-1>(qs, p.qout.stochastic, v, u[e], ov1w, ov2w);
+        if (ok) yp[e * ncol] = (int8_t)c;
+        cs1[j] += c;
+        cs2[j] += c * c;
+      }
+    }
+  }
+  // per-column sums: the 4 q-lanes of a column meet by shuffles, then one int64 atomic per column
+  // and sum into this workgroup's shard; overflow counters: wave totals, one atomic each
+  const int shard = (int)((blockIdx.x + blockIdx.y * 7u) % LBT_NSHARD);
+  int64_t* cs = p.chsum + (int64_t)shard * 2 * ncol;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    int a = cs1[j], b = cs2[j];
+    a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
+    b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
+    const int col = cw + j * 16 + r;
+    if (q == 0 && cw + j * 16 < ncol) {
+      if (a) atomicAdd((unsigned long long*)&cs[col], (unsigned long long)(long long)a);
+      if (b) atomicAdd((unsigned long long*)&cs[ncol + col], (unsigned long long)(long long)b);
+    }
+  }
+  if ((threadIdx.x & 63) == 0 && p.qout.counts) {
+    int32_t* ct = p.qout.counts + ((int64_t)p.qout.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+    if (ov1w) atomicAdd(ct, ov1w);
+    if (ov2w) atomicAdd(ct + 1, ov2w);
+  }
+}
 
 // BM x BN workgroup tile (64 or 128 each), 2 x 2 waves of (BM/2) x (BN/2): MI x NJ MFMA tiles
 template <int MODE, bool A16, bool ADD, int BM, int BN, int D>
@@ -252,6 +336,12 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
     }
     return;
   }
+  if constexpr (MODE == MODE_FWD && !A16) {
+    if (p.yq) {  // uniform: quantising epilogue
+      quant_epilogue<MI, NJ>(p, acc[0], accw, want_w ? u8 : 0, scale, rtile, rlim, full, n0 + wn * (BN / 2), r, q);
+      return;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int ctile = n0 + wn * (BN / 2) + j * 16;
@@ -405,6 +495,27 @@ extern "C" int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* 
   p.ksplit = 1;
   hipStream_t st = (hipStream_t)stream;
   return a_kind == 2 ? launch<MODE_FWD, true>(p, st) : launch<MODE_FWD, false>(p, st);
+}
+
+// Forward whose epilogue is the consuming Normalization_q's input quantiser (no fp32 y): int8 codes
+// yq + qout's overflow counters + exact channel sums chsum[NSHARD][2 * Cout]. A8 codes only (a_kind
+// 0 / 1); never split (short-M GEMMs use lbt_conv_fwd_igemm_ws + lbt_dfxp_quantize).
+extern "C" int lbt_conv_fwd_igemm_q(const void* xq, int32_t a_kind, const int8_t* wf, int32_t ksf, lbt_conv_desc d,
+                                    lbt_qdesc qx, lbt_qdesc qw, int8_t* yq, lbt_qdesc qout, int64_t* chsum,
+                                    void* stream) {
+  if (!desc_ok(d) || d.Cin % kBK || d.Cout % 16 || !yq || !wf || !chsum || a_kind == 2) return LBT_EINVAL;
+  if (qout.bits < 2 || qout.bits > 8) return LBT_EINVAL;
+  if ((int64_t)d.KH * d.KW * d.Cin * 255 * 128 >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  if ((int64_t)d.N * d.H * d.W * d.Cin >= ((int64_t)1 << 31) || (int64_t)ksf * 16 * d.Cout >= ((int64_t)1 << 31))
+    return LBT_EINVAL;
+  if (ksf * 16 < d.KH * d.KW * d.Cin) return LBT_EINVAL;
+  IgArgs p{};
+  p.a = xq; p.b = wf; p.ks = ksf; p.cred = d.Cin; p.a_u8off = a_kind == 1; p.d = d; p.qa = qx; p.qb = qw;
+  p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
+  if (p.M * p.ncol >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  p.ksplit = 1;
+  p.yq = yq; p.qout = qout; p.chsum = chsum; p.hw = d.Ho * d.Wo;
+  return launch<MODE_FWD, false>(p, (hipStream_t)stream);
 }
 
 // Workspace of the split-K variants below (0: that GEMM does not split). mode 0 fwd, 1 dgrad.

@@ -880,6 +880,30 @@ class ResidualBottleneck_q(ResidualBlock_q):
         ops.chain_fwd(a)
 
     @staticmethod
+    def _conv_norm(conv, bn, xq, N, H, W, ctx):
+        """conv forward + bn's input quantiser: in the GEMM epilogue when the GEMM does not split K
+        (int8 codes straight from the MFMA accumulators), else fp32 y + the quantise pass."""
+        kh, kw, Cin, Cout = conv.ksize
+        d = ops.conv_desc(N, H, W, Cin, Cout, kh, kw, conv.strides[1], conv.strides[2], conv.padding)
+        # the quantising epilogue is exact but measured slower than fp32 y + the quantise pass on
+        # MI355X (its Philox / ballot / byte-store work lands on the GEMM's critical path): opt-in
+        if ops.igemm_workspace_bytes(d, 0, False) or os.environ.get("LBT_FUSE_CONV_QUANT", "0") != "1":
+            y = conv.fwd_codes(xq, N, H, W)
+            ResidualBottleneck_q._norm_in(bn, y, ctx)
+            return y
+        conv.d, conv.xq = d, xq
+        conv.quantize_weights()
+        n, r = bn.layers
+        shape = (N, d.Ho, d.Wo, Cout)
+        n._chsum = n._c.sums("chsum", ops.NSHARD * 2 * Cout, ctx)
+        n.q = n._c.get("q", shape, torch.int8, xq.device)
+        ops.conv_fwd_igemm_q(xq, 1, conv.wf, conv.ksf, d, conv.X_range.desc, conv.W_range.desc, n.q, n.X_range,
+                             n._chsum)
+        n.n = N * d.Ho * d.Wo
+        r.R = r._c.get("R", shape, torch.int8, xq.device)
+        return n.q  # the chain needs only its shape
+
+    @staticmethod
     def _norm_in(bn, y, ctx):
         """Normalization_q's input quantiser on a conv output (codes + exact channel sums) and
         the Rescale_q code buffer the chain will fill."""
@@ -908,16 +932,13 @@ class ResidualBottleneck_q(ResidualBlock_q):
             if sc:
                 ops.quantize(X, sc[0].X_range, OUT_U8OFF, out=xs)
         self._x_pre = None
-        y1 = c1.fwd_codes(x1, N, H, W)
-        self._norm_in(bn1, y1, ctx)
+        y1 = self._conv_norm(c1, bn1, x1, N, H, W, ctx)
         x2 = self._c.get("x2", y1.shape, torch.int8, dev)
         self._chain(c1, bn1, y1, True, o1=x2, o1_conv=c2)
-        y2 = c2.fwd_codes(x2, N, y1.shape[1], y1.shape[2])
-        self._norm_in(bn2, y2, ctx)
+        y2 = self._conv_norm(c2, bn2, x2, N, y1.shape[1], y1.shape[2], ctx)
         x3 = self._c.get("x3", y2.shape, torch.int8, dev)
         self._chain(c2, bn2, y2, True, o1=x3, o1_conv=c3)
-        y3 = c3.fwd_codes(x3, N, y2.shape[1], y2.shape[2])
-        self._norm_in(bn3, y3, ctx)
+        y3 = self._conv_norm(c3, bn3, x3, N, y2.shape[1], y2.shape[2], ctx)
         out = self._c.get("y", y3.shape, torch.float32, dev)
         # the next block's input quantisers (conv-1, shortcut conv) ride in this chain as well
         nb = self.next_block if (self.next_block is not None and self.next_block._fusable()) else None
@@ -928,8 +949,7 @@ class ResidualBottleneck_q(ResidualBlock_q):
             if nsc:
                 o.update(o2=nb._c.get("xs", y3.shape, torch.int8, dev), o2_conv=nsc[0])
         if sc:
-            ys = sc[0].fwd_codes(xs, N, H, W)
-            self._norm_in(sc[1], ys, ctx)
+            self._conv_norm(sc[0], sc[1], xs, N, H, W, ctx)
             self._chain(c3, bn3, y3, True, bn2=sc[1], out=out, **o)
         else:
             self._chain(c3, bn3, y3, True, res=X, out=out, **o)

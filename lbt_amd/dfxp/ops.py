@@ -522,6 +522,15 @@ def conv_dgrad_igemm_ws(gq, g_i16, wd, ksd, d, qg, qw, dx, ws, add_src=None):
              ptr(ws), 0 if ws is None else ws.numel() * ws.element_size(), stream())
 
 
+def conv_fwd_igemm_q(xq, a_kind, wf, ksf, d, qx, qw, yq, qout, chsum):
+    """Wide fwd + the Normalization_q input quantiser in its epilogue (int8 codes, sums, counters)."""
+    M = d.N * d.Ho * d.Wo
+    qout.observe(M * d.Cout)
+    with _Timed("igemm_kernel<fwd>", xq.numel() * xq.element_size() + wf.numel() + M * d.Cout):
+        call("lbt_conv_fwd_igemm_q", ptr(xq), int(a_kind), ptr(wf), int(ksf), d, qx, qw, ptr(yq), qout.desc,
+             ptr(chsum), stream())
+
+
 def conv_fwd_igemm(xq, a_kind, wf, ksf, d, qx, qw, y):
     M = d.N * d.Ho * d.Wo
     with _Timed("igemm_kernel<fwd>", xq.numel() * xq.element_size() + wf.numel() + 4 * M * d.Cout):

@@ -361,3 +361,12 @@ def test_igemm_splitk_matches_generic(N, H, Cin, Cout, k):
     ops.conv_dgrad_igemm_ws(g, 1, wd, ksd, d, qg.desc, qw.desc, dx1, ws2, add_src=add)
     ops.conv_dgrad_generic16(g, w_hwio, d, qg.desc, qw.desc, dx2)
     assert torch.equal(dx1, dx2 + add)
+
+
+@pytest.mark.gpu
+def test_resnet50_fused_conv_quant_epilogue_bitexact(monkeypatch):
+    """The opt-in quantising igemm epilogue (LBT_FUSE_CONV_QUANT=1: Normalization_q's input
+    quantiser on the MFMA accumulators, in-register Philox exchange, exact channel sums) keeps
+    the fused bottleneck bit-exact against the oracle."""
+    monkeypatch.setenv("LBT_FUSE_CONV_QUANT", "1")
+    test_resnet50_layers_bitexact_vs_oracle((1, 1, 1, 1), 64, 32, 16, 16)
