@@ -100,16 +100,32 @@ class FusedResNet:
     def label_buffer(self, n):
         return self._c.get("labels", (int(n),), torch.int32, self.ctx.device)
 
+    binds_inputs = True  # the step reads the caller's batch buffers in place (Trainer caches a graph per pair)
+
+    def _bind(self, X, labels=None):
+        """Point the step's input launches at the caller's batch (no copy into the plan's own
+        buffers): the prologue's image quantiser job and the fused head's labels. Buffers of
+        another dtype / layout are copied into the plan's own first."""
+        if X.dtype != torch.float32 or not X.is_contiguous() or X.device != self._X_own.device:
+            self._X_own.copy_(X)
+            X = self._X_own
+        self._X = X
+        self._input_job.x = X.data_ptr()
+        if labels is not None:
+            if labels.dtype != torch.int32 or not labels.is_contiguous():
+                self._labels_own.copy_(labels)
+                labels = self._labels_own
+            self._head.labels = labels.data_ptr()
+
     def forward(self, X):
         self._ensure(X)
-        if X.data_ptr() != self._X.data_ptr():
-            self._X.copy_(X)
+        self._bind(X)
         for f in self._fwd + self._hfwd:  # the first launch also zeroes the step's sums
             f()
         return self.logits
 
     def compute_loss(self, labels):
-        if labels.data_ptr() != self._labels.data_ptr():
+        if labels.data_ptr() != self._labels.data_ptr():  # the separate softmax-CE reads the own buffer
             self._labels.copy_(labels)
         for f in self._hloss:
             f()
@@ -123,10 +139,7 @@ class FusedResNet:
         """forward + compute_loss + backward of one training step, the head as one launch
         (lbt_head_fwd_bwd): same results bit for bit as the three calls."""
         self._ensure(X)
-        if X.data_ptr() != self._X.data_ptr():
-            self._X.copy_(X)
-        if labels.data_ptr() != self._labels.data_ptr():
-            self._labels.copy_(labels)
+        self._bind(X, labels)
         for f in self._fwd + self._hfused + self._bwd + self._tail_fused:
             f()
         return self.loss
@@ -175,8 +188,8 @@ class FusedResNet:
         ctx = self.ctx
         st = _lib.stream
         N, H, W, Cin0 = X.shape
-        self._X = self.input_buffer(X.shape)
-        self._labels = self.label_buffer(N)
+        self._X = self._X_own = self.input_buffer(X.shape)
+        self._labels = self._labels_own = self.label_buffer(N)
         fwd, bwd = [], []
         lib = _lib.load()
         if self._side is None:
