@@ -125,7 +125,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 128; resnet50: 32)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="images per GPU (default 128 = BASELINE configs[1]; resnet50: 256, the usual per-GPU "
+                         "ImageNet batch -- configs[3] names none; measured 2.65K / 3.38K / 3.85K / 4.15K "
+                         "samples/s at 32 / 64 / 128 / 256)")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (diagnostics)")
     ap.add_argument("--layerwise", action="store_true", help="run the Layer_q path instead of the fused plan")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -138,7 +141,7 @@ def main():
     r50 = args.workload == "resnet50"
     w4 = args.workload == "resnet20w4"
     if args.batch is None:
-        args.batch = 32 if r50 else 128
+        args.batch = 256 if r50 else 128
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
