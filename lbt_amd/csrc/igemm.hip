@@ -107,16 +107,28 @@ LBT_DEV void quant_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i
         u[3] = re == 3 ? got : u[3];
       }
       const int wsum = accw[j][0];
-      int8_t* yp = p.yq + (rtile + i * 16) * ncol + col;
+      int cc[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const bool ok = full || i * 16 + e < rlim;
         const float v = ok ? (float)(acc[i][j][e] + u8 * wsum) * scale : 0.f;
         const int c = quant_w<-1>(qs, p.qout.stochastic, v, u[e], ov1w, ov2w);
-        if (ok) yp[e * ncol] = (int8_t)c;
+        cc[e] = c;
         cs1[j] += c;
         cs2[j] += c * c;
       }
+      // the same 4-lane transpose on the codes: lane jj collects row jj's codes of the group's 4
+      // columns and stores them as one dword
+      uint32_t packed = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int sc = (jj - k) & 3;
+        const int send = sc == 0 ? cc[0] : sc == 1 ? cc[1] : sc == 2 ? cc[2] : cc[3];
+        const int got = __shfl(send, gbase + ((jj + k) & 3), 64);
+        packed |= ((uint32_t)got & 0xFFu) << (8 * ((jj + k) & 3));
+      }
+      if (full || i * 16 + jj < rlim)
+        *reinterpret_cast<uint32_t*>(p.yq + (rtile + i * 16 + jj) * ncol + (col & ~3)) = packed;
     }
   }
   // per-column sums: the 4 q-lanes of a column meet by shuffles, then one int64 atomic per column
