@@ -146,9 +146,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LBT_DIST_BACKEND=gloo + LBT_SHARE_GPU=1: a rehearsal of the N-rank path with every rank on the
+    # box's GPUs round-robin (one-GPU boxes); the measured configuration is RCCL, one GPU per rank
+    backend = os.environ.get("LBT_DIST_BACKEND", "nccl")
+    if os.environ.get("LBT_SHARE_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
