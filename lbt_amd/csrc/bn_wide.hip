@@ -3,10 +3,15 @@
 // chain_bwd_b element for element, with int16 gradient codes and int64 channel sums (int16 x
 // int8 products summed over a channel overflow int32).
 //
-// Layout: workgroup = 64 channels x 4 row lanes; grid = (ceil(C/64), row splits). A thread walks
-// rows r = lane_r, lane_r + 4, ... of its split for one channel (a wave reads 64 consecutive
-// channels of a row: coalesced), keeps its channel sums in registers, and the 4 row lanes meet in
-// LDS before one atomic per (channel, sum) into shard (blockIdx.y mod LBT_NSHARD).
+// Layout: workgroup = 64 channels (16 channel quads) x 16 pixel positions, over a run of spb
+// samples; grid = (ceil(C/64), ceil(HW/16), ceil(N/spb)). A thread owns ONE position of the sample
+// (pixel hw, channels c0..c0+3) and walks it through its samples: the stochastic-rounding noise
+// (dynamic_fixed_point.py:32-38: over x.shape[1:], broadcast over the batch) depends on the
+// position only, so its Philox call is made once per thread, not once per element (that call
+// was what bounded these passes: ~4 quarter-rate 32-bit multiplies per round). A wave reads
+// 4 pixels x 64 consecutive channels of one sample (coalesced), keeps its channel sums in
+// registers, and the 16 pixel lanes meet (shuffles, then LDS) before one atomic per
+// (channel, sum) into a shard.
 #include "dfxp_device.h"
 
 namespace {
@@ -26,7 +31,8 @@ struct WideA {
   float* dout;           // fp32 output when there is no norm part
   int64_t* sums;         // [NSHARD][4C]: S(G2 R), S(G2), S(G), S(G qn)
   int64_t rows, inner;
-  int C, rpb;            // rows per workgroup
+  int C, spb;            // samples per workgroup
+  int64_t hw, samples;   // positions per sample (inner / C), samples (rows / hw)
   // ReLU mask on the incoming gradient (ReLU_q backward): from the forward output y_mask > 0, or
   // (mask_r) recomputed from the R codes as the forward chain's pre-ReLU value
   // ((float)R * s_r) * gb[c] + gb[C + c] > 0; the masked gradient optionally out (gmask_out).
@@ -39,19 +45,30 @@ struct WideA {
                          // .backward's add of the two branch gradients, :865-869, done here)
 };
 
-// Thread = 4 consecutive channels (one Philox4x32 call covers their 4 noise values) x one row lane.
+// Thread = 4 consecutive channels (one Philox4x32 call covers their 4 noise values) x one pixel.
 constexpr int kCQ = 16;        // channel quads per workgroup (64 channels)
-constexpr int kRL4 = kT / kCQ; // 16 row lanes
+constexpr int kRL4 = kT / kCQ; // 16 pixel lanes
 
-__global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
+// Per-thread channel sums run in int32: a thread sees at most kRowsA samples (|G| <= 2^15 codes
+// times |R|, |qn| <= 2^7 gives |product| <= 2^22, so 2^8 of them stay below 2^31) and the workgroup
+// widens to int64 when it folds its lanes. YM: the y_mask / g2 operands exist (ResidualBottleneck_q's last BN
+// and its shortcut BN); the mask_r and plain forms carry no registers for them.
+constexpr int kRowsA = 256;
+
+template <bool YM>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn_bwd_a_wide_kernel(WideA a) {
   __shared__ long long red[kT / 64][4][kCB];
   __shared__ int sh_cnt[2 * 2 * (kT / 64)];
-  const int cq = threadIdx.x % kCQ, rl = threadIdx.x / kCQ;
+  const int cq = threadIdx.x % kCQ, pl = threadIdx.x / kCQ;
   const int c0 = blockIdx.x * kCB + 4 * cq;
-  const bool cv = c0 < a.C;  // C % 4 == 0: the quad is whole
+  const int64_t hw = (int64_t)blockIdx.y * kRL4 + pl;
+  // C % 4 == 0: the quad is whole. A wave's lane 0 has the smallest pixel and channel of the wave,
+  // so an invalid lane 0 means an idle wave (the wave-total counters below read lane 0)
+  const bool cv = c0 < a.C && hw < a.hw;
   const QState srg = qstate(a.qrg), sng = qstate(a.qng);
-  const int64_t r0 = (int64_t)blockIdx.y * a.rpb;
-  const int64_t r1 = r0 + a.rpb < a.rows ? r0 + a.rpb : a.rows;
+  const int64_t n0 = (int64_t)blockIdx.z * a.spb;
+  const int64_t n1 = n0 + a.spb < a.samples ? n0 + a.spb : a.samples;
+  const int64_t pos = hw * a.C + c0;  // offset inside a sample: the noise position
   float gam[4], bet[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -60,41 +77,42 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
   }
   const float sr = a.mask_r ? qstate(a.qr).inv_m : 0.f;
   const float* __restrict__ gp = a.g;
-  const float* __restrict__ g2p = a.g2;
-  const float* __restrict__ ymp = a.y_mask;
+  const float* __restrict__ g2p = YM ? a.g2 : nullptr;
+  const float* __restrict__ ymp = YM ? a.y_mask : nullptr;
   const int8_t* __restrict__ Rp = a.R;
   const int8_t* __restrict__ qnp = a.qn;
   const bool needR = a.mask_r || srg.active;
-  long long s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0};
-  int o1 = 0, o2 = 0, p1 = 0, p2 = 0;
-  constexpr int U = 2;  // rows in flight per thread: every load of both issued before any use
+  int s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0}, s3[4] = {0, 0, 0, 0};
+  int o1 = 0, o2 = 0, p1 = 0, p2 = 0;  // wave totals (quant_w)
+  constexpr int U = 2;  // samples in flight per thread: every load of both issued before any use
   if (cv) {
-    for (int64_t rb = r0 + rl; rb < r1; rb += U * kRL4) {
-      float4 gv[U], g2v[U], ym[U];
+    const uint64_t blk = (uint64_t)pos >> 2;
+    const Noise4 z{{0.f, 0.f, 0.f, 0.f}};
+    const Noise4 nz1 = (srg.active && a.qrg.stochastic) ? qnoise4(a.qrg, srg.step, blk) : z;
+    const Noise4 nz2 = (sng.active && a.qng.stochastic) ? qnoise4(a.qng, sng.step, blk) : z;
+    for (int64_t nb = n0; nb < n1; nb += U) {
+      float4 gv[U], g2v[YM ? U : 1], ym[YM ? U : 1];
       char4 rv[U], qv[U];
-      bool live[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t r = rb + u * kRL4;
-        live[u] = r < r1;
-        const int64_t e = (live[u] ? r : rb) * a.C + c0;
+        const int64_t n = nb + u < n1 ? nb + u : nb;
+        const int64_t e = n * a.inner + pos;
         gv[u] = *reinterpret_cast<const float4*>(gp + e);
-        if (g2p) g2v[u] = *reinterpret_cast<const float4*>(g2p + e);
-        if (ymp) ym[u] = *reinterpret_cast<const float4*>(ymp + e);
+        if (YM && g2p) g2v[u] = *reinterpret_cast<const float4*>(g2p + e);
+        if (YM && ymp) ym[u] = *reinterpret_cast<const float4*>(ymp + e);
         if (needR) rv[u] = *reinterpret_cast<const char4*>(Rp + e);
         if (sng.active) qv[u] = *reinterpret_cast<const char4*>(qnp + e);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (!live[u]) break;
-        const int64_t e = (rb + u * kRL4) * a.C + c0;
-        const uint64_t blk = (uint64_t)(e % a.inner) >> 2;  // inner % 4 == 0
+        if (nb + u >= n1) break;
+        const int64_t e = (nb + u) * a.inner + pos;
         float d[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
-        if (g2p) {
+        if (YM && g2p) {
           d[0] = d[0] + g2v[u].x; d[1] = d[1] + g2v[u].y; d[2] = d[2] + g2v[u].z; d[3] = d[3] + g2v[u].w;
         }
         const int R[4] = {needR ? rv[u].x : 0, needR ? rv[u].y : 0, needR ? rv[u].z : 0, needR ? rv[u].w : 0};
-        if (ymp) {
+        if (YM && ymp) {
           const float m[4] = {ym[u].x, ym[u].y, ym[u].z, ym[u].w};
 #pragma unroll
           for (int k = 0; k < 4; ++k) d[k] = m[k] > 0.f ? d[k] : 0.f;
@@ -109,25 +127,23 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
         }
         if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(d[0], d[1], d[2], d[3]);
         if (srg.active) {
-          const Noise4 nz = a.qrg.stochastic ? qnoise4(a.qrg, srg.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const int G2 = quant1(srg, a.qrg.stochastic, d[k], nz.u[k], o1, o2);
-            s0[k] += (long long)G2 * R[k];
+            const int G2 = quant_w<-1>(srg, a.qrg.stochastic, d[k], nz1.u[k], o1, o2);
+            s0[k] += G2 * R[k];
             s1[k] += G2;
             const float gh = (float)G2 * srg.inv_m;
             d[k] = gh * gam[k];
           }
         }
         if (sng.active) {
-          const Noise4 nz = a.qng.stochastic ? qnoise4(a.qng, sng.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
           const int qn[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
           int G[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            G[k] = quant1(sng, a.qng.stochastic, d[k], nz.u[k], p1, p2);
+            G[k] = quant_w<-1>(sng, a.qng.stochastic, d[k], nz2.u[k], p1, p2);
             s2[k] += G[k];
-            s3[k] += (long long)G[k] * qn[k];
+            s3[k] += G[k] * qn[k];
           }
           short4 o;
           o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
@@ -138,36 +154,38 @@ __global__ __launch_bounds__(kT) void bn_bwd_a_wide_kernel(WideA a) {
       }
     }
   }
-  // the 4 row lanes of a wave hold the same channels (lanes cq, cq + 16, cq + 32, cq + 48): fold
-  // them with shuffles, then one LDS row per wave
+  // the 4 pixel lanes of a wave hold the same channels (lanes cq, cq + 16, cq + 32, cq + 48): fold
+  // them with shuffles (in int64 from here), then one LDS row per wave
+  long long t0[4], t1[4], t2[4], t3[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
+    t0[k] = s0[k]; t1[k] = s1[k]; t2[k] = s2[k]; t3[k] = s3[k];
 #pragma unroll
     for (int o = 16; o < 64; o <<= 1) {
-      s0[k] += __shfl_xor(s0[k], o, 64);
-      s1[k] += __shfl_xor(s1[k], o, 64);
-      s2[k] += __shfl_xor(s2[k], o, 64);
-      s3[k] += __shfl_xor(s3[k], o, 64);
+      t0[k] += __shfl_xor(t0[k], o, 64);
+      t1[k] += __shfl_xor(t1[k], o, 64);
+      t2[k] += __shfl_xor(t2[k], o, 64);
+      t3[k] += __shfl_xor(t3[k], o, 64);
     }
   }
   const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) < kCQ) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      red[wv][0][4 * cq + k] = s0[k];
-      red[wv][1][4 * cq + k] = s1[k];
-      red[wv][2][4 * cq + k] = s2[k];
-      red[wv][3][4 * cq + k] = s3[k];
+      red[wv][0][4 * cq + k] = t0[k];
+      red[wv][1][4 * cq + k] = t1[k];
+      red[wv][2][4 * cq + k] = t2[k];
+      red[wv][3][4 * cq + k] = t3[k];
     }
   }
   // per-thread counters -> wave totals -> LDS (one barrier publishes counters and sums)
-  counts_stage(0, 2, o1, o2, sh_cnt);
-  counts_stage(1, 2, p1, p2, sh_cnt);
+  counts_stage_w(0, 2, o1, o2, sh_cnt);
+  counts_stage_w(1, 2, p1, p2, sh_cnt);
   __syncthreads();
   if (srg.active) counts_publish(0, 2, a.qrg, sh_cnt);
   if (sng.active) counts_publish(1, 2, a.qng, sh_cnt);
   if (a.sums) {
-    int64_t* dst = a.sums + (int64_t)(blockIdx.y % LBT_NSHARD) * 4 * a.C;
+    int64_t* dst = a.sums + (int64_t)shard_id() * 4 * a.C;
     for (int i = threadIdx.x; i < 4 * kCB; i += kT) {
       const int sidx = i / kCB, cl = i - sidx * kCB, c = blockIdx.x * kCB + cl;
       if (c >= a.C) continue;
@@ -188,7 +206,8 @@ struct WideB {
   int64_t n;             // elements per channel
   float* dx;
   int64_t rows;
-  int C, rpb;
+  int C, spb;            // samples per workgroup (pass A's layout)
+  int64_t hw, samples;
   // optional: the consuming conv's gradient quantiser applied to dx (int16 codes, Conv2d_q
   // :299-300 at 9..16 bits) instead of storing dx; inner = per-sample elements (noise period)
   int16_t* gq;
@@ -199,7 +218,7 @@ struct WideB {
 __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
   __shared__ float s_mg[kCB], s_mgx[kCB];
   __shared__ int sh_cnt[2 * (kT / 64)];
-  const int cq = threadIdx.x % kCQ, rl = threadIdx.x / kCQ;
+  const int cq = threadIdx.x % kCQ;
   const int c0 = blockIdx.x * kCB + 4 * cq;
   const QState sgq = qstate(b.qng), sn = qstate(b.qn_q), so = qstate(b.qo);
   const bool quant = b.gq != nullptr;
@@ -217,75 +236,108 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
     s_mgx[threadIdx.x] = (float)(gsc * (s * (double)SGQ - (double)m * (double)SG) / (n * (double)sig));
   }
   __syncthreads();
-  int o1 = 0, o2 = 0;
-  if (c0 >= b.C) {
-    if (quant) block_flush_counts(b.qo, o1, o2, sh_cnt);  // every thread takes part in the flush
-    return;
-  }
-  float mu[4], sig[4], mg[4], mgx[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    mu[k] = b.ms[c0 + k];
-    sig[k] = b.ms[b.C + c0 + k];
-    mg[k] = s_mg[4 * cq + k];
-    mgx[k] = s_mgx[4 * cq + k];
-  }
-  const int64_t r0 = (int64_t)blockIdx.y * b.rpb;
-  const int64_t r1 = r0 + b.rpb < b.rows ? r0 + b.rpb : b.rows;
-  const int8_t* __restrict__ qnp = b.qn;
-  const int16_t* __restrict__ Gp = b.G;
-  constexpr int U = 2;  // rows in flight per thread
-  for (int64_t rb = r0 + rl; rb < r1; rb += U * kRL4) {
-    char4 qva[U];
-    short4 gva[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t r = rb + u * kRL4 < r1 ? rb + u * kRL4 : rb;
-      qva[u] = *reinterpret_cast<const char4*>(qnp + r * b.C + c0);
-      gva[u] = *reinterpret_cast<const short4*>(Gp + r * b.C + c0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-    if (rb + u * kRL4 >= r1) break;
-    const int64_t e = (rb + u * kRL4) * b.C + c0;
-    const char4 qv = qva[u];
-    const short4 gv = gva[u];
-    const int q[4] = {qv.x, qv.y, qv.z, qv.w}, G[4] = {gv.x, gv.y, gv.z, gv.w};
-    float o[4];
+  int o1 = 0, o2 = 0;  // wave totals (quant_w)
+  const int64_t hw = (int64_t)blockIdx.y * kRL4 + threadIdx.x / kCQ;
+  // as in pass A: an invalid lane 0 means an idle wave. No early exit: every thread reaches the
+  // barriers of the counter flush the same number of times
+  if (c0 < b.C && hw < b.hw) {
+    float mu[4], mg[4], mgx[4];
+    Recip rs[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float x1 = (float)q[k] * sn.inv_m;
-      const float x2 = x1 - mu[k];
-      const float xh = x2 / sig[k];
-      const float gh = (float)G[k] * sgq.inv_m;
-      const float t1 = gh - mg[k];
-      const float t2 = xh * mgx[k];
-      o[k] = (t1 - t2) / sig[k];
+      mu[k] = b.ms[c0 + k];
+      rs[k] = recip(b.ms[b.C + c0 + k]);
+      mg[k] = s_mg[4 * cq + k];
+      mgx[k] = s_mgx[4 * cq + k];
     }
-    if (quant) {
-      const uint64_t blk = (uint64_t)(e % b.inner) >> 2;  // inner % 4 == 0
-      const Noise4 nz = b.qo.stochastic ? qnoise4(b.qo, so.step, blk) : Noise4{{0.f, 0.f, 0.f, 0.f}};
-      short4 v;
-      v.x = (short)quant1(so, b.qo.stochastic, o[0], nz.u[0], o1, o2);
-      v.y = (short)quant1(so, b.qo.stochastic, o[1], nz.u[1], o1, o2);
-      v.z = (short)quant1(so, b.qo.stochastic, o[2], nz.u[2], o1, o2);
-      v.w = (short)quant1(so, b.qo.stochastic, o[3], nz.u[3], o1, o2);
-      *reinterpret_cast<short4*>(b.gq + e) = v;
-    } else {
-      *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0], o[1], o[2], o[3]);
-    }
+    const int64_t n0 = (int64_t)blockIdx.z * b.spb;
+    const int64_t n1 = n0 + b.spb < b.samples ? n0 + b.spb : b.samples;
+    const int64_t pos = hw * b.C + c0, inner = b.hw * b.C;
+    const Noise4 nz = (quant && b.qo.stochastic) ? qnoise4(b.qo, so.step, (uint64_t)pos >> 2)
+                                                 : Noise4{{0.f, 0.f, 0.f, 0.f}};
+    const int8_t* __restrict__ qnp = b.qn;
+    const int16_t* __restrict__ Gp = b.G;
+    constexpr int U = 2;  // samples in flight per thread
+    for (int64_t nb = n0; nb < n1; nb += U) {
+      char4 qva[U];
+      short4 gva[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = (nb + u < n1 ? nb + u : nb) * inner + pos;
+        qva[u] = *reinterpret_cast<const char4*>(qnp + e);
+        gva[u] = *reinterpret_cast<const short4*>(Gp + e);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+      if (nb + u >= n1) break;
+      const int64_t e = (nb + u) * inner + pos;
+      const char4 qv = qva[u];
+      const short4 gv = gva[u];
+      const int q[4] = {qv.x, qv.y, qv.z, qv.w}, G[4] = {gv.x, gv.y, gv.z, gv.w};
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x1 = (float)q[k] * sn.inv_m;
+        const float x2 = x1 - mu[k];
+        const float xh = div_by(x2, rs[k]);  // == x2 / sigma
+        const float gh = (float)G[k] * sgq.inv_m;
+        const float t1 = gh - mg[k];
+        const float t2 = xh * mgx[k];
+        o[k] = div_by(t1 - t2, rs[k]);       // == (t1 - t2) / sigma
+      }
+      if (quant) {
+        short4 v;
+        v.x = (short)quant_w<-1>(so, b.qo.stochastic, o[0], nz.u[0], o1, o2);
+        v.y = (short)quant_w<-1>(so, b.qo.stochastic, o[1], nz.u[1], o1, o2);
+        v.z = (short)quant_w<-1>(so, b.qo.stochastic, o[2], nz.u[2], o1, o2);
+        v.w = (short)quant_w<-1>(so, b.qo.stochastic, o[3], nz.u[3], o1, o2);
+        *reinterpret_cast<short4*>(b.gq + e) = v;
+      } else {
+        *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+      }
     }
   }
-  if (quant) block_flush_counts(b.qo, o1, o2, sh_cnt);
+  if (quant) block_flush_counts_w(b.qo, o1, o2, sh_cnt);
 }
 
-// ~2048 workgroups in all
-int rows_per_block(int64_t rows, int cblocks) {
-  int64_t splits = 2048 / (cblocks > 0 ? cblocks : 1);  // ~2048 workgroups: up to 8 per CU in flight
-  if (splits < 1) splits = 1;
-  int64_t rpb = (rows + splits - 1) / splits;
-  if (rpb < kRL4) rpb = kRL4;
-  return (int)rpb;
+// Samples per workgroup: up to 16 (one noise call per 16 elements of a thread's position) while
+// the grid keeps ~1024+ workgroups.
+int samples_per_block(int64_t xy, int64_t samples) {
+  int64_t s = samples * xy / 1024;
+  if (s > 16) s = 16;
+  if (s < 1) s = 1;
+  if ((samples + s - 1) / s > 65535) s = (samples + 65534) / 65535;  // grid.z limit
+  return (int)s;
+}
+
+int launch_b(WideB b, int cb, hipStream_t st) {
+  b.hw = b.inner / b.C;
+  if (b.rows % b.hw) return LBT_EINVAL;
+  b.samples = b.rows / b.hw;
+  const int64_t yb = (b.hw + kRL4 - 1) / kRL4;
+  b.spb = samples_per_block((int64_t)cb * yb, b.samples);
+  const int64_t zb = (b.samples + b.spb - 1) / b.spb;
+  if (yb > 65535 || zb > 65535) return LBT_EINVAL;
+  hipLaunchKernelGGL(bn_bwd_b_wide_kernel, dim3((unsigned)cb, (unsigned)yb, (unsigned)zb), dim3(kT), 0, st, b);
+  return (int)hipGetLastError();
+}
+
+int launch_a(WideA a, int cb, hipStream_t st) {
+  if (a.qrg.bits > 16 || a.qng.bits > 16) return LBT_EINVAL;  // the int32 lane sums assume <= 16-bit codes
+  a.hw = a.inner / a.C;
+  if (a.rows % a.hw) return LBT_EINVAL;
+  a.samples = a.rows / a.hw;
+  const int64_t yb = (a.hw + kRL4 - 1) / kRL4;
+  a.spb = samples_per_block((int64_t)cb * yb, a.samples);
+  const int64_t zb = (a.samples + a.spb - 1) / a.spb;
+  if (yb > 65535 || zb > 65535 || a.spb > kRowsA) return LBT_EINVAL;
+  const dim3 grid((unsigned)cb, (unsigned)yb, (unsigned)zb);
+  if (a.y_mask || a.g2)
+    hipLaunchKernelGGL(bn_bwd_a_wide_kernel<true>, grid, dim3(kT), 0, st, a);
+  else
+    hipLaunchKernelGGL(bn_bwd_a_wide_kernel<false>, grid, dim3(kT), 0, st, a);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -295,26 +347,18 @@ extern "C" int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R,
                                  int64_t inner, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gamma_q)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
-  WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0, nullptr, 0, lbt_qdesc{}, nullptr, nullptr,
-          nullptr};
-  const int cb = (C + kCB - 1) / kCB;
-  a.rpb = rows_per_block(rows, cb);
-  const int64_t yb = (rows + a.rpb - 1) / a.rpb;
-  if (yb > 65535) return LBT_EINVAL;
-  hipLaunchKernelGGL(bn_bwd_a_wide_kernel, dim3((unsigned)cb, (unsigned)yb), dim3(kT), 0, (hipStream_t)stream, a);
-  return (int)hipGetLastError();
+  WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0, 0, 0, nullptr, 0, lbt_qdesc{}, nullptr,
+          nullptr, nullptr};
+  return launch_a(a, (C + kCB - 1) / kCB, (hipStream_t)stream);
 }
 
 extern "C" int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qdesc qn_q, const float* ms,
                                  const int64_t* sums, int64_t n, float* dx, int64_t rows, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || !G || !qn || !ms || !sums || !dx) return LBT_EINVAL;
-  WideB b{G, qng, qn, qn_q, ms, sums, n, dx, rows, C, 0, nullptr, lbt_qdesc{}, 1};
-  const int cb = (C + kCB - 1) / kCB;
-  b.rpb = rows_per_block(rows, cb);
-  const int64_t yb = (rows + b.rpb - 1) / b.rpb;
-  if (yb > 65535) return LBT_EINVAL;
-  hipLaunchKernelGGL(bn_bwd_b_wide_kernel, dim3((unsigned)cb, (unsigned)yb), dim3(kT), 0, (hipStream_t)stream, b);
-  return (int)hipGetLastError();
+  int64_t hw = 1024;  // no quantiser, so no noise period: any split of the rows into "samples" of hw pixels
+  while (rows % hw) hw >>= 1;
+  WideB b{G, qng, qn, qn_q, ms, sums, n, dx, rows, C, 0, 0, 0, nullptr, lbt_qdesc{}, hw * C};
+  return launch_b(b, (C + kCB - 1) / kCB, (hipStream_t)stream);
 }
 
 // Pass A with the ReLU mask folded in (y_mask, or mask_r: recomputed from R with qr and
@@ -326,13 +370,8 @@ extern "C" int lbt_bn_bwd_a_wide_masked(const float* g, const float* g2, const f
   if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gb)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
   if (mask_r && (y_mask || !R || !gb || qr.bits <= 0)) return LBT_EINVAL;
-  WideA a{g, qrg, R, gb, qng, qn, gout, dout, sums, rows, inner, C, 0, y_mask, mask_r, qr, gb, gmask_out, g2};
-  const int cb = (C + kCB - 1) / kCB;
-  a.rpb = rows_per_block(rows, cb);
-  const int64_t yb = (rows + a.rpb - 1) / a.rpb;
-  if (yb > 65535) return LBT_EINVAL;
-  hipLaunchKernelGGL(bn_bwd_a_wide_kernel, dim3((unsigned)cb, (unsigned)yb), dim3(kT), 0, (hipStream_t)stream, a);
-  return (int)hipGetLastError();
+  WideA a{g, qrg, R, gb, qng, qn, gout, dout, sums, rows, inner, C, 0, 0, 0, y_mask, mask_r, qr, gb, gmask_out, g2};
+  return launch_a(a, (C + kCB - 1) / kCB, (hipStream_t)stream);
 }
 
 // Pass B whose dx goes straight into the consuming conv's 9..16-bit gradient quantiser: gq int16
@@ -342,11 +381,6 @@ extern "C" int lbt_bn_bwd_b_wide_q(const int16_t* G, lbt_qdesc qng, const int8_t
                                    int64_t inner, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || !G || !qn || !ms || !sums || !gq || inner <= 0 || inner % C) return LBT_EINVAL;
   if (qo.bits <= 0 || qo.bits > 16 || (qo.stochastic && !qo.step && !qo.noise)) return LBT_EINVAL;
-  WideB b{G, qng, qn, qn_q, ms, sums, n, nullptr, rows, C, 0, gq, qo, inner};
-  const int cb = (C + kCB - 1) / kCB;
-  b.rpb = rows_per_block(rows, cb);
-  const int64_t yb = (rows + b.rpb - 1) / b.rpb;
-  if (yb > 65535) return LBT_EINVAL;
-  hipLaunchKernelGGL(bn_bwd_b_wide_kernel, dim3((unsigned)cb, (unsigned)yb), dim3(kT), 0, (hipStream_t)stream, b);
-  return (int)hipGetLastError();
+  WideB b{G, qng, qn, qn_q, ms, sums, n, nullptr, rows, C, 0, 0, 0, gq, qo, inner};
+  return launch_b(b, (C + kCB - 1) / kCB, (hipStream_t)stream);
 }

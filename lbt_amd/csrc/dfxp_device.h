@@ -259,6 +259,15 @@ LBT_DEV void block_flush_counts(const lbt_qdesc& q, int ov1, int ov2, int* sh) {
   __syncthreads();
 }
 
+// block_flush_counts with wave totals (quant_w): lane 0 of each wave holds its wave's counts.
+LBT_DEV void block_flush_counts_w(const lbt_qdesc& q, int ov1w, int ov2w, int* sh) {
+  if (!q.counts) return;  // uniform
+  counts_stage_w(0, 1, ov1w, ov2w, sh);
+  __syncthreads();
+  counts_publish(0, 1, q, sh);
+  __syncthreads();
+}
+
 // Add a block-local per-channel partial (LDS, long long[n]) into shard shard_id() of a
 // sharded int64 buffer laid out [LBT_NSHARD][stride].
 LBT_DEV void block_flush_sums(const long long* sh, int n, int64_t* dst, int stride) {
