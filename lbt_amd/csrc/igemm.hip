@@ -611,11 +611,11 @@ constexpr int kWP = 64;
 // STORE: the workgroup's partial is STORED into slab[split] (every element of slab[nsplit][K][Cout]
 // has exactly one writer -- no zeroing, no atomics); else atomically added into shard split % nshard.
 template <bool G16, bool STORE>
-__global__ __launch_bounds__(kT, 2) void wgrad_wide_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
+__global__ __launch_bounds__(kT, 1) void wgrad_wide_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
                                                         lbt_conv_desc d, long long* __restrict__ slab, int64_t P,
                                                         int nsplit, int nshard) {
   constexpr int NG = G16 ? 2 : 1;  // G images: (gh, gl') or g
-  constexpr int NBS = G16 ? 2 : 4, COW = 16 * NBS;  // output-channel slices per workgroup (VGPR budget)
+  constexpr int NBS = 4, COW = 16 * NBS;  // output-channel slices per workgroup
   // per wave: X [4 slices][64 px][16 B], G [NG][4 slices][64 px][16 B]; reused as the int64 tile
   __shared__ __attribute__((aligned(16))) int8_t lds[4][(4 + NBS * NG) * kWP * 16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -782,7 +782,7 @@ extern "C" int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_
   if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
   const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
   if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
-  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / (g_i16 ? 32 : 64)));
+  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
   hipStream_t st = (hipStream_t)stream;
   if (g_i16)
     hipLaunchKernelGGL((wgrad_wide_kernel<true, false>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
@@ -803,7 +803,7 @@ extern "C" int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int3
   if ((P + nsplit - 1) / nsplit > 4 * 131072) return LBT_EINVAL;  // int32 MFMA sums of a wave stay exact
   const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
   if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
-  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / (g_i16 ? 32 : 64)));
+  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
   hipStream_t st = (hipStream_t)stream;
   if (g_i16)
     hipLaunchKernelGGL((wgrad_wide_kernel<true, true>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
