@@ -62,7 +62,23 @@ struct IgArgs {
   lbt_qdesc qout;
   int64_t* chsum;
   int hw;
+  // taps of the k loop: dgrad kh = kh0 + SH * th (th < nkh), kw likewise (fwd and unit-stride dgrad:
+  // every tap, kh = th). Strided dgrad runs one launch per parity class (cpy, cpx) of the dx pixels, whose rows are
+  // (n, yc, xc) -> (n, yc * SH + cpy, xc * SW + cpx) over a ch x cw grid: only the taps with
+  // (ih + PT - kh) % SH == 0 reach such a pixel, and for them the source row is yc + oy - th (no
+  // zero rows, no division in the loop).
+  int nkh, nkw, kh0, kw0, oy, ox, ch, cw, cpy, cpx;
 };
+
+// every tap, rows = every output pixel (fwd, unit-stride dgrad)
+void all_taps(IgArgs& p, int mode) {
+  const lbt_conv_desc& d = p.d;
+  p.nkh = d.KH; p.nkw = d.KW; p.kh0 = 0; p.kw0 = 0;
+  p.oy = d.PT; p.ox = d.PL;
+  p.ch = mode == MODE_FWD ? d.Ho : d.H;
+  p.cw = mode == MODE_FWD ? d.Wo : d.W;
+  p.cpy = 0; p.cpx = 0;
+}
 
 // The conv-output quantiser in the GEMM epilogue (fwd, A8). Lane (r, q) holds column cw + 16 j + r
 // of rows rtile + 16 i + e. Noise: one Philox4x32 call yields the 4 values of 4 consecutive channels
@@ -154,7 +170,7 @@ LBT_DEV void quant_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i
 }
 
 // BM x BN workgroup tile (64 or 128 each), 2 x 2 waves of (BM/2) x (BN/2): MI x NJ MFMA tiles
-template <int MODE, bool A16, bool ADD, int BM, int BN, int D>
+template <int MODE, bool A16, bool ADD, int BM, int BN, int D, bool CLS>
 __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   constexpr int NA = A16 ? 2 : 1;  // A tiles per k-block: (hi, lo') or one
   constexpr int HA = BM / 64, HB = BN / 64;  // 64-row loader passes of A / B
@@ -166,9 +182,9 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   const int64_t m0 = (int64_t)blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const lbt_conv_desc& d = p.d;
-  const int OH = MODE == MODE_FWD ? d.Ho : d.H, OW = MODE == MODE_FWD ? d.Wo : d.W;
+  const int OH = p.ch, OW = p.cw;  // the row grid (dgrad parity class: its ch x cw pixels)
   const int SH = MODE == MODE_FWD ? d.H : d.Ho, SW = MODE == MODE_FWD ? d.W : d.Wo;
-  const int cblocks = p.cred / kBK, nk_all = d.KH * d.KW * cblocks;
+  const int cblocks = p.cred / kBK, nk_all = p.nkh * p.nkw * cblocks;
   const int nk = nk_all / p.ksplit, kbase = (int)blockIdx.z * nk;  // this split's k-blocks
 
   // ---- loader roles: A rows (t >> 2) and (t >> 2) + 64, 16-byte segment (t & 3) of the 64 channels
@@ -190,30 +206,23 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
   // D register stages: the global loads of k-block b land in stage b % D, D k-blocks ahead of use
   v4i ra[D][HA][A16 ? 2 : 1], rb[D][HB];
   bool rv[D][HA];
-  const bool unit_stride = d.SH == 1 && d.SW == 1;
   auto load_k = [&](int kbl, int st) {
     const int kb = kbase + kbl;
     const int tap = kb / cblocks, cb = kb - tap * cblocks;
-    const int kh = tap / d.KW, kw = tap - kh * d.KW;
+    const int th = tap / p.nkw, tw = tap - th * p.nkw;
+    const int kh = MODE == MODE_FWD ? th : p.kh0 + d.SH * th, kw = MODE == MODE_FWD ? tw : p.kw0 + d.SW * tw;
+    const int kbw = (kh * d.KW + kw) * cblocks + cb;  // the weight image's k-block
 #pragma unroll
     for (int h = 0; h < HA; ++h) {
       int sy, sx;
-      bool ok;
       if (MODE == MODE_FWD) {
         sy = ay[h] * d.SH + kh - d.PT;
         sx = ax[h] * d.SW + kw - d.PL;
-        ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
-      } else if (unit_stride) {  // uniform: no divisions
-        sy = ay[h] + d.PT - kh;
-        sx = ax[h] + d.PL - kw;
-        ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
-      } else {
-        const int ny = ay[h] + d.PT - kh, nx = ax[h] + d.PL - kw;
-        sy = ny / d.SH;
-        sx = nx / d.SW;
-        ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
+      } else {  // ih = yc * SH + cpy: (ih + PT - kh) / SH = yc + oy - th exactly
+        sy = ay[h] + p.oy - th;
+        sx = ax[h] + p.ox - tw;
       }
-      ok = ok && arow[h];
+      const bool ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW && arow[h];
       rv[st][h] = ok;
       // 32-bit element offsets (launcher: every operand < 2^31 elements)
       const uint32_t pix = ok ? (uint32_t)((an[h] * SH + sy) * SW + sx) : 0u;
@@ -230,7 +239,7 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
     for (int h = 0; h < HB; ++h) {
       const int col = n0 + lr + 64 * h;
       const int colc = col < p.ncol ? col : 0;
-      rb[st][h] = *reinterpret_cast<const v4i*>(p.b + ((uint32_t)(colc * p.ks + kb * 4 + seg) << 4));
+      rb[st][h] = *reinterpret_cast<const v4i*>(p.b + ((uint32_t)(colc * p.ks + kbw * 4 + seg) << 4));
       if (col >= p.ncol) rb[st][h] = v4i{0, 0, 0, 0};
     }
   };
@@ -354,6 +363,44 @@ __global__ __launch_bounds__(kT) void igemm_kernel(IgArgs p) {
       return;
     }
   }
+  if constexpr (CLS) {  // parity-class rows: each row's dx pixel, 32-bit (launcher: dx < 2^31 elements)
+    uint32_t roff[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t m = rtile + i * 16 + e;
+        const uint32_t mu = (uint32_t)(m < p.M ? m : 0);
+        const uint32_t xc = mu % (uint32_t)p.cw, t2 = mu / (uint32_t)p.cw;
+        const uint32_t yc = t2 % (uint32_t)p.ch, n = t2 / (uint32_t)p.ch;
+        roff[i][e] = ((n * (uint32_t)d.H + yc * (uint32_t)d.SH + (uint32_t)p.cpy) * (uint32_t)d.W +
+                      xc * (uint32_t)d.SW + (uint32_t)p.cpx) * (uint32_t)ncol;
+      }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int ctile = n0 + wn * (BN / 2) + j * 16;
+      if (ctile >= ncol) continue;
+      const uint32_t col = (uint32_t)(ctile + r);
+      const int wsum = want_w ? accw[j][0] : 0;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (!(full || i * 16 + e < rlim)) continue;
+          float v;
+          if constexpr (A16) {
+            const double hs = (double)acc[0][i][j][e] * 256.0;
+            const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
+            v = (float)(hs + ls) * scale;
+          } else {
+            v = (float)(acc[0][i][j][e] + u8 * wsum) * scale;
+          }
+          if constexpr (addv) v = v + p.add_src[roff[i][e] + col];
+          p.y[roff[i][e] + col] = v;
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int ctile = n0 + wn * (BN / 2) + j * 16;
@@ -418,21 +465,25 @@ __global__ __launch_bounds__(256) void igemm_splitk_reduce_kernel(IgArgs p) {
   *reinterpret_cast<float4*>(p.y + i4) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-template <int MODE, bool A16, int BM, int BN>
+template <int MODE, bool A16, int BM, int BN, bool CLS = false>
 void launch_tile(const IgArgs& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.ncol + BN - 1) / BN), (unsigned)p.ksplit);
   // register stages in flight: a divisor of the split's k-block count (3x3 convs: 9 * Cin/64 -> 3;
   // 1x1: 2), 1 for the VGPR-heavy 128x128 tiles
-  const int nk = p.d.KH * p.d.KW * (p.cred / kBK) / p.ksplit;
-  const int D = (BM == 128 && BN == 128) ? 1 : (nk % 3 == 0 ? 3 : (nk % 2 == 0 ? 2 : 1));
+  const int nk = p.nkh * p.nkw * (p.cred / kBK) / p.ksplit;
+  const int D = (BM == 128 && BN == 128) ? 1 : (nk % 3 == 0 && !CLS ? 3 : (nk % 2 == 0 ? 2 : 1));
 #define LBT_IG(DD)                                                                      \
   do {                                                                                  \
     if (MODE == MODE_DGRAD && p.add_src)                                                \
-      hipLaunchKernelGGL((igemm_kernel<MODE, A16, true, BM, BN, DD>), grid, dim3(kT), 0, st, p);  \
+      hipLaunchKernelGGL((igemm_kernel<MODE, A16, true, BM, BN, DD, CLS>), grid, dim3(kT), 0, st, p);  \
     else                                                                                \
-      hipLaunchKernelGGL((igemm_kernel<MODE, A16, false, BM, BN, DD>), grid, dim3(kT), 0, st, p); \
+      hipLaunchKernelGGL((igemm_kernel<MODE, A16, false, BM, BN, DD, CLS>), grid, dim3(kT), 0, st, p); \
   } while (0)
-  if (D == 3) LBT_IG(3); else if (D == 2) LBT_IG(2); else LBT_IG(1);
+  if constexpr (CLS) {
+    if (D == 2) LBT_IG(2); else LBT_IG(1);
+  } else {
+    if (D == 3) LBT_IG(3); else if (D == 2) LBT_IG(2); else LBT_IG(1);
+  }
 #undef LBT_IG
   if (p.ksplit > 1) {
     const dim3 g2((unsigned)((p.M * p.ncol / 4 + 255) / 256));
@@ -467,11 +518,15 @@ int64_t splitk_bytes(int64_t M, int ncol, int nk, bool a16) {
 
 // Tile choice: 64 columns when the GEMM has <= 64 (no MFMAs on padding columns), and 64 rows
 // when 128-row tiles would leave the 256 CUs without two workgroups each.
-template <int MODE, bool A16>
+template <int MODE, bool A16, bool CLS = false>
 int launch(const IgArgs& p, hipStream_t st) {
   const int64_t mb = (p.M + kBM - 1) / kBM;
   if (mb > 0x7fffffff / 2 || (p.ncol + 63) / 64 > 65535) return LBT_EINVAL;
   const bool bn64 = p.ncol <= 64 || getenv_int("LBT_IGEMM_BN", 128) == 64;
+  if constexpr (CLS) {  // parity classes of a strided dgrad: 64-row tiles only (fewer variants)
+    if (bn64) launch_tile<MODE, A16, 64, 64, true>(p, st); else launch_tile<MODE, A16, 64, 128, true>(p, st);
+    return (int)hipGetLastError();
+  }
   const int64_t nb = (p.ncol + (bn64 ? 63 : 127)) / (bn64 ? 64 : 128);
   // ... and always for 16-bit codes when the tile would be 128 x 128: that variant needs 256 VGPRs
   // (one wave per SIMD), which leaves its fp32 epilogue stores unhidden
@@ -487,6 +542,51 @@ int launch(const IgArgs& p, hipStream_t st) {
 bool desc_ok(const lbt_conv_desc& d) {
   return d.N > 0 && d.H > 0 && d.W > 0 && d.KH > 0 && d.KW > 0 && d.SH > 0 && d.SW > 0 && d.Ho > 0 && d.Wo > 0 &&
          d.Cin > 0 && d.Cout > 0;
+}
+
+// dx of a parity class no tap reaches (a 1x1 stride-2 conv's odd pixels): add_src, or 0
+__global__ __launch_bounds__(256) void dgrad_fill_class_kernel(IgArgs p) {
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= p.M * p.ncol) return;
+  const int64_t m = i4 / p.ncol;
+  const int c = (int)(i4 - m * p.ncol);
+  const lbt_conv_desc& d = p.d;
+  const int64_t xc = m % p.cw, t2 = m / p.cw, yc = t2 % p.ch, n = t2 / p.ch;
+  const int64_t off = ((n * d.H + yc * d.SH + p.cpy) * d.W + xc * d.SW + p.cpx) * p.ncol + c;
+  *reinterpret_cast<float4*>(p.y + off) =
+      p.add_src ? *reinterpret_cast<const float4*>(p.add_src + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Strided dgrad as SH x SW parity-class GEMMs (IgArgs: nkh ...): each class runs only the taps that
+// reach it, so no MFMA multiplies the zero rows of the stride's implicit upsampling. Never split.
+template <bool A16>
+int dgrad_classes(IgArgs p, hipStream_t st) {
+  const lbt_conv_desc& d = p.d;
+  if ((int64_t)d.N * d.H * d.W * d.Cin >= ((int64_t)1 << 31)) return LBT_EINVAL;  // 32-bit row offsets
+  p.ksplit = 1;
+  for (int py = 0; py < d.SH; ++py)
+    for (int px = 0; px < d.SW; ++px) {
+      const int ch = py < d.H ? (d.H - py + d.SH - 1) / d.SH : 0;
+      const int cw = px < d.W ? (d.W - px + d.SW - 1) / d.SW : 0;
+      if (!ch || !cw) continue;
+      const int kh0 = (py + d.PT) % d.SH, kw0 = (px + d.PL) % d.SW;
+      p.nkh = kh0 < d.KH ? (d.KH - kh0 + d.SH - 1) / d.SH : 0;
+      p.nkw = kw0 < d.KW ? (d.KW - kw0 + d.SW - 1) / d.SW : 0;
+      p.kh0 = kh0; p.kw0 = kw0;
+      p.oy = (py + d.PT - kh0) / d.SH; p.ox = (px + d.PL - kw0) / d.SW;
+      p.cpy = py; p.cpx = px; p.ch = ch; p.cw = cw;
+      p.M = (int64_t)d.N * ch * cw;
+      int rc;
+      if (!p.nkh || !p.nkw) {
+        hipLaunchKernelGGL(dgrad_fill_class_kernel, dim3((unsigned)((p.M * p.ncol / 4 + 255) / 256)), dim3(256), 0, st,
+                           p);
+        rc = (int)hipGetLastError();
+      } else {
+        rc = launch<MODE_DGRAD, A16, true>(p, st);
+      }
+      if (rc) return rc;
+    }
+  return 0;
 }
 
 }  // namespace
@@ -505,6 +605,7 @@ extern "C" int lbt_conv_fwd_igemm(const void* xq, int32_t a_kind, const int8_t* 
   p.colsum = colsum; p.y = y; p.add_src = nullptr; p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
   if (p.M * p.ncol >= ((int64_t)1 << 40)) return LBT_EINVAL;
   p.ksplit = 1;
+  all_taps(p, MODE_FWD);
   hipStream_t st = (hipStream_t)stream;
   return a_kind == 2 ? launch<MODE_FWD, true>(p, st) : launch<MODE_FWD, false>(p, st);
 }
@@ -526,6 +627,7 @@ extern "C" int lbt_conv_fwd_igemm_q(const void* xq, int32_t a_kind, const int8_t
   p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
   if (p.M * p.ncol >= ((int64_t)1 << 31)) return LBT_EINVAL;
   p.ksplit = 1;
+  all_taps(p, MODE_FWD);
   p.yq = yq; p.qout = qout; p.chsum = chsum; p.hw = d.Ho * d.Wo;
   return launch<MODE_FWD, false>(p, (hipStream_t)stream);
 }
@@ -535,6 +637,7 @@ extern "C" int64_t lbt_igemm_workspace_bytes(lbt_conv_desc d, int32_t mode, int3
   if (!desc_ok(d)) return 0;
   if (mode == 0)
     return splitk_bytes((int64_t)d.N * d.Ho * d.Wo, d.Cout, d.KH * d.KW * (d.Cin / kBK), a16 != 0);
+  if (d.SH > 1 || d.SW > 1) return 0;  // strided dgrad: parity classes, never split
   return splitk_bytes((int64_t)d.N * d.H * d.W, d.Cin, d.KH * d.KW * (d.Cout / kBK), a16 != 0);
 }
 
@@ -555,6 +658,7 @@ extern "C" int lbt_conv_fwd_igemm_ws(const void* xq, int32_t a_kind, const int8_
   const int64_t need = lbt_igemm_workspace_bytes(d, 0, a_kind == 2);
   p.ksplit = (need > 0 && ws && ws_bytes >= need) ? choose_ksplit(p.M, p.ncol, d.KH * d.KW * (d.Cin / kBK)) : 1;
   p.part = reinterpret_cast<int32_t*>(ws);
+  all_taps(p, MODE_FWD);
   hipStream_t st = (hipStream_t)stream;
   return a_kind == 2 ? launch<MODE_FWD, true>(p, st) : launch<MODE_FWD, false>(p, st);
 }
@@ -571,7 +675,9 @@ extern "C" int lbt_conv_dgrad_igemm(const void* gq, int32_t g_i16, const int8_t*
   p.a = gq; p.b = wd; p.ks = ksd; p.cred = d.Cout; p.a_u8off = 0; p.d = d; p.qa = qg; p.qb = qw;
   p.colsum = nullptr; p.y = dx; p.add_src = add_src; p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
   p.ksplit = 1;
+  all_taps(p, MODE_DGRAD);
   hipStream_t st = (hipStream_t)stream;
+  if (d.SH > 1 || d.SW > 1) return g_i16 ? dgrad_classes<true>(p, st) : dgrad_classes<false>(p, st);
   return g_i16 ? launch<MODE_DGRAD, true>(p, st) : launch<MODE_DGRAD, false>(p, st);
 }
 
@@ -590,7 +696,9 @@ extern "C" int lbt_conv_dgrad_igemm_ws(const void* gq, int32_t g_i16, const int8
   const int64_t need = lbt_igemm_workspace_bytes(d, 1, g_i16);
   p.ksplit = (need > 0 && ws && ws_bytes >= need) ? choose_ksplit(p.M, p.ncol, d.KH * d.KW * (d.Cout / kBK)) : 1;
   p.part = reinterpret_cast<int32_t*>(ws);
+  all_taps(p, MODE_DGRAD);
   hipStream_t st = (hipStream_t)stream;
+  if (d.SH > 1 || d.SW > 1) return g_i16 ? dgrad_classes<true>(p, st) : dgrad_classes<false>(p, st);
   return g_i16 ? launch<MODE_DGRAD, true>(p, st) : launch<MODE_DGRAD, false>(p, st);
 }
 
