@@ -415,6 +415,11 @@ int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW, int32_t C,
  * d: N, H, W, Cin (= channels), KH, KW, SH, SW, PT, PL, Ho, Wo; Cout, PB, PR unused.           */
 int lbt_maxpool_fwd(const float* x, float* y, uint8_t* amax, lbt_conv_desc d, void* stream);
 int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, lbt_conv_desc d, void* stream);
+/* The preceding ReLU_q's backward (:983-990, mask x > 0) folded in: y = this pool's forward output
+ * (the pool input is the ReLU output, so an input that receives gradient has x > 0 <=> y[o] > 0);
+ * dx = relu_bwd(maxpool_bwd(g)) bit for bit, in one pass. C % 4 == 0.                           */
+int lbt_maxpool_relu_bwd(const float* g, const uint8_t* amax, const float* y, float* dx, lbt_conv_desc d,
+                         void* stream);
 /* mean sparse softmax cross-entropy (models.py:30-32) -> loss[0] (fp32, device), dz = d loss / d z. */
 int lbt_softmax_xent(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss,
                      float* dz, void* stream);

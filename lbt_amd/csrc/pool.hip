@@ -70,6 +70,52 @@ __global__ __launch_bounds__(kT) void maxpool_bwd_kernel(const float* __restrict
   dx[e] = s;
 }
 
+// The same gradient routing for 4 channels per thread (C % 4 == 0: 16-byte g / y and 4-byte amax
+// loads), optionally with the preceding ReLU_q's backward folded in (ymask = this pool's forward
+// output): the mask x > 0 of an input element is needed only where some window routes gradient to
+// it, i.e. where it is that window's maximum, and then relu(x) = y[o] (the pool input is the ReLU
+// output), so x > 0 <=> y[o] > 0 -- the mask costs one 16-byte load per window instead of a pass
+// over the ReLU input, and dx is the exact value relu_bwd(maxpool_bwd(g)) stores (sum or +0).
+__global__ __launch_bounds__(kT) void maxpool_bwd4_kernel(const float* __restrict__ g, const uint8_t* __restrict__ amax,
+                                                          const float* __restrict__ ymask, float* __restrict__ dx,
+                                                          lbt_conv_desc d) {
+  const int64_t e4 = ((int64_t)blockIdx.x * kT + threadIdx.x) * 4;
+  const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
+  if (e4 >= total) return;
+  const int c = (int)(e4 % d.Cin);
+  int64_t m = e4 / d.Cin;
+  const int iw = (int)(m % d.W);
+  m /= d.W;
+  const int ih = (int)(m % d.H);
+  const int n = (int)(m / d.H);
+  const int ylo = ih + d.PT - d.KH + 1, yhi = ih + d.PT;
+  const int xlo = iw + d.PL - d.KW + 1, xhi = iw + d.PL;
+  int oh0 = ylo <= 0 ? 0 : (ylo + d.SH - 1) / d.SH, oh1 = yhi < 0 ? -1 : yhi / d.SH;
+  int ow0 = xlo <= 0 ? 0 : (xlo + d.SW - 1) / d.SW, ow1 = xhi < 0 ? -1 : xhi / d.SW;
+  if (oh1 >= d.Ho) oh1 = d.Ho - 1;
+  if (ow1 >= d.Wo) ow1 = d.Wo - 1;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int oh = oh0; oh <= oh1; ++oh)
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int64_t o = (((int64_t)n * d.Ho + oh) * d.Wo + ow) * d.Cin + c;
+      const int pos = (ih - (oh * d.SH - d.PT)) * d.KW + (iw - (ow * d.SW - d.PL));
+      const uchar4 a = *reinterpret_cast<const uchar4*>(amax + o);
+      const float4 gv = *reinterpret_cast<const float4*>(g + o);
+      float4 yv = make_float4(1.f, 1.f, 1.f, 1.f);
+      if (ymask) yv = *reinterpret_cast<const float4*>(ymask + o);
+      if ((int)a.x == pos && yv.x > 0.f) s[0] = s[0] + gv.x;
+      if ((int)a.y == pos && yv.y > 0.f) s[1] = s[1] + gv.y;
+      if ((int)a.z == pos && yv.z > 0.f) s[2] = s[2] + gv.z;
+      if ((int)a.w == pos && yv.w > 0.f) s[3] = s[3] + gv.w;
+    }
+  *reinterpret_cast<float4*>(dx + e4) = make_float4(s[0], s[1], s[2], s[3]);
+}
+
+bool pool_desc_ok(const lbt_conv_desc& d) {
+  return d.N > 0 && d.H > 0 && d.W > 0 && d.Cin > 0 && d.KH > 0 && d.KW > 0 && d.SH > 0 && d.SW > 0 && d.Ho > 0 &&
+         d.Wo > 0;
+}
+
 }  // namespace
 
 // d: N, H, W, Cin (= C), KH, KW, SH, SW, PT, PL, Ho, Wo (Cout, PB, PR unused)
@@ -88,7 +134,22 @@ extern "C" int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, l
       d.Ho <= 0 || d.Wo <= 0)
     return LBT_EINVAL;
   const int64_t n = (int64_t)d.N * d.H * d.W * d.Cin;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, g,
-                     amax, dx, d);
+  if (d.Cin % 4 == 0)
+    hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
+                       g, amax, nullptr, dx, d);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, g,
+                       amax, dx, d);
+  return (int)hipGetLastError();
+}
+
+// ReLU_q backward of the pool's input folded into the pool backward (y = this pool's forward
+// output): dx = relu_bwd(maxpool_bwd(g)) in one pass. C % 4 == 0.
+extern "C" int lbt_maxpool_relu_bwd(const float* g, const uint8_t* amax, const float* y, float* dx, lbt_conv_desc d,
+                                    void* stream) {
+  if (!pool_desc_ok(d) || d.Cin % 4 || !y) return LBT_EINVAL;
+  const int64_t n = (int64_t)d.N * d.H * d.W * d.Cin;
+  hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
+                     g, amax, y, dx, d);
   return (int)hipGetLastError();
 }

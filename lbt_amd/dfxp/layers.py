@@ -710,7 +710,12 @@ class ReLU_q(Layer_q):
         ops.relu_fwd(X, self.y)
         return self.y
 
+    # set by a following MaxPool_q that applies this mask in its own backward (pool_relu)
+    mask_in_pool = False
+
     def backward(self, grad, stochastic=True):
+        if self.mask_in_pool:
+            return grad
         dx = self._c.get("dx", grad.shape, torch.float32, grad.device)
         ops.relu_bwd(grad, self.X, dx)
         return dx
@@ -1025,9 +1030,19 @@ class MaxPool_q(Layer_q):
         self.y = y
         return y
 
+    # the ReLU_q in front of this pool whose backward this one performs (its input > 0 mask): set
+    # by the model builder, see ops.maxpool_relu_bwd
+    pool_relu = None
+
     def backward(self, grad, stochastic=True):
         dx = self._c.get("dx", self.X.shape, torch.float32, grad.device)
-        ops.maxpool_bwd(grad.contiguous(), self.amax, dx, self.d)
+        fuse = self.pool_relu is not None and self.d.Cin % 4 == 0
+        if self.pool_relu is not None:
+            self.pool_relu.mask_in_pool = fuse
+        if fuse:
+            ops.maxpool_relu_bwd(grad.contiguous(), self.amax, self.y, dx, self.d)
+        else:
+            ops.maxpool_bwd(grad.contiguous(), self.amax, dx, self.d)
         return dx
 
     def info(self):

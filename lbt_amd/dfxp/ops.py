@@ -461,6 +461,12 @@ def maxpool_bwd(g, amax, dx, d):
         call("lbt_maxpool_bwd", ptr(g), ptr(amax), ptr(dx), d, stream())
 
 
+def maxpool_relu_bwd(g, amax, y, dx, d):
+    """MaxPool_q backward with the preceding ReLU_q's backward folded in (y: the pool's output)."""
+    with _Timed("maxpool_bwd_kernel", 9 * g.numel() + 4 * dx.numel()):
+        call("lbt_maxpool_relu_bwd", ptr(g), ptr(amax), ptr(y), ptr(dx), d, stream())
+
+
 # ---------------------------------------------------------------- 9..16-bit gradient codes
 def conv_dgrad_generic16(gq, w_hwio, d, qg, qw, dx, add_src=None):
     with _Timed("conv_dgrad_generic_kernel16", 2 * gq.numel() + w_hwio.numel() + 4 * dx.numel()):
