@@ -70,6 +70,41 @@ __global__ __launch_bounds__(kT) void maxpool_bwd_kernel(const float* __restrict
   dx[e] = s;
 }
 
+// maxpool_fwd_kernel for 4 channels per thread (C % 4 == 0): the same scan and strict '>' per
+// channel, 16-byte loads, one 4-byte argmax store.
+__global__ __launch_bounds__(kT) void maxpool_fwd4_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                          uint8_t* __restrict__ amax, lbt_conv_desc d) {
+  const int64_t e4 = ((int64_t)blockIdx.x * kT + threadIdx.x) * 4;
+  const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
+  if (e4 >= total) return;
+  const int c = (int)(e4 % d.Cin);
+  int64_t m = e4 / d.Cin;
+  const int ow = (int)(m % d.Wo);
+  m /= d.Wo;
+  const int oh = (int)(m % d.Ho);
+  const int n = (int)(m / d.Ho);
+  float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int bi[4] = {0, 0, 0, 0};
+  for (int kh = 0; kh < d.KH; ++kh) {
+    const int ih = oh * d.SH + kh - d.PT;
+    if ((unsigned)ih >= (unsigned)d.H) continue;
+    for (int kw = 0; kw < d.KW; ++kw) {
+      const int iw = ow * d.SW + kw - d.PL;
+      if ((unsigned)iw >= (unsigned)d.W) continue;
+      const float4 v4 = *reinterpret_cast<const float4*>(x + (((int64_t)n * d.H + ih) * d.W + iw) * d.Cin + c);
+      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (v[j] > best[j]) {
+          best[j] = v[j];
+          bi[j] = kh * d.KW + kw;
+        }
+    }
+  }
+  *reinterpret_cast<float4*>(y + e4) = make_float4(best[0], best[1], best[2], best[3]);
+  *reinterpret_cast<uchar4*>(amax + e4) = make_uchar4((uint8_t)bi[0], (uint8_t)bi[1], (uint8_t)bi[2], (uint8_t)bi[3]);
+}
+
 // The same gradient routing for 4 channels per thread (C % 4 == 0: 16-byte g / y and 4-byte amax
 // loads), optionally with the preceding ReLU_q's backward folded in (ymask = this pool's forward
 // output): the mask x > 0 of an input element is needed only where some window routes gradient to
@@ -124,8 +159,12 @@ extern "C" int lbt_maxpool_fwd(const float* x, float* y, uint8_t* amax, lbt_conv
       d.SW <= 0 || d.Ho <= 0 || d.Wo <= 0)
     return LBT_EINVAL;
   const int64_t n = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, x, y,
-                     amax, d);
+  if (d.Cin % 4 == 0)
+    hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
+                       x, y, amax, d);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, x,
+                       y, amax, d);
   return (int)hipGetLastError();
 }
 
