@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t
                                                                    int K, int64_t per, int64_t* __restrict__ slab) {
   constexpr int NH = G16 ? 2 : 1;
   __shared__ __attribute__((aligned(16))) _Float16 sG[NH][NCT * 16][kWgChunk + 8];
-  __shared__ int sBase[kWgChunk], sYX[kWgChunk];
+  __shared__ int sOff[kWgChunk], sYX[kWgChunk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kg = lane >> 4;
   const int c0 = blockIdx.z * 64;
@@ -150,6 +150,7 @@ __global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t
   const int k = (blockIdx.y * 4 + wave) * 16 + r;
   const int code = k < K ? patch_code(d, k) : -1;
   const int dy = code >> 20, dx = (code >> 10) & 1023, ci = code & 1023;
+  const int koff = code >= 0 ? (dy * d.W + dx) * d.Cin + ci : 0;  // the patch element's offset from its pixel's
 
   f4v facc[NH][NCT];
   int iacc[NH][NCT][4];
@@ -172,22 +173,38 @@ __global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t
       const int ox = (int)(pu % (uint32_t)d.Wo);
       const uint32_t t = pu / (uint32_t)d.Wo;
       const int oy = (int)(t % (uint32_t)d.Ho), n = (int)(t / (uint32_t)d.Ho);
-      sBase[threadIdx.x] = pv ? n * d.H : -1;
-      sYX[threadIdx.x] = ((oy * d.SH - d.PT) << 16) | ((ox * d.SW - d.PL) & 0xFFFF);
+      const int y0 = oy * d.SH - d.PT, x0 = ox * d.SW - d.PL;
+      // window origin offset (may be negative: only in-range taps are ever added to it); a pixel
+      // past the range gets a row far out of [0, H) so every tap of it fails the bounds test
+      sOff[threadIdx.x] = ((n * d.H + y0) * d.W + x0) * d.Cin;
+      sYX[threadIdx.x] = pv ? ((y0 << 16) | (x0 & 0xFFFF)) : (int)(0x8000u << 16);
     }
-    for (int i = threadIdx.x; i < kWgChunk * NCT * 16; i += kThreads) {
-      const int px = i / (NCT * 16), col = i - px * (NCT * 16);
+    // gradient rows: 8 consecutive channels of one pixel per 16- (8-) byte load, written transposed
+    for (int i = threadIdx.x; i < kWgChunk * NCT * 2; i += kThreads) {
+      const int px = i / (NCT * 2), col = (i - px * (NCT * 2)) * 8;
       const int64_t p = q0 + px;
       const int c = c0 + col;
-      int v = 0;
-      if (p < p1 && c < d.Cout)
-        v = G16 ? (int)reinterpret_cast<const int16_t*>(g_)[p * d.Cout + c]
-                : (int)reinterpret_cast<const int8_t*>(g_)[p * d.Cout + c];
-      if constexpr (G16) {
-        sG[0][col][px] = (_Float16)(float)(v >> 8);   // hi, arithmetic shift: [-128, 127]
-        sG[NH - 1][col][px] = (_Float16)(float)(v & 255);  // lo: [0, 255]
-      } else {
-        sG[0][col][px] = (_Float16)(float)v;
+      int v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (p < p1 && c < d.Cout) {  // Cout % 16 == 0: the 8 channels are all in range
+        if constexpr (G16) {
+          const int4 w4 = *reinterpret_cast<const int4*>(reinterpret_cast<const int16_t*>(g_) + p * d.Cout + c);
+          const int w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[2 * j] = (int)(int16_t)(w[j] & 0xFFFF); v[2 * j + 1] = w[j] >> 16; }
+        } else {
+          const int2 w = *reinterpret_cast<const int2*>(reinterpret_cast<const int8_t*>(g_) + p * d.Cout + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[j] = (int)(int8_t)(w.x >> (8 * j)); v[4 + j] = (int)(int8_t)(w.y >> (8 * j)); }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (G16) {
+          sG[0][col + j][px] = (_Float16)(float)(v[j] >> 8);        // hi, arithmetic shift: [-128, 127]
+          sG[NH - 1][col + j][px] = (_Float16)(float)(v[j] & 255);  // lo: [0, 255]
+        } else {
+          sG[0][col + j][px] = (_Float16)(float)v[j];
+        }
       }
     }
     __syncthreads();
@@ -197,10 +214,10 @@ __global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int px = s * 32 + 8 * kg + j;
-        const int b = sBase[px], yx = sYX[px];
+        const int yx = sYX[px];
         const int iy = (yx >> 16) + dy, ix = (int)(int16_t)(yx & 0xFFFF) + dx;
-        const bool ok = code >= 0 && b >= 0 && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-        const int off = ok ? ((b + iy) * d.W + ix) * d.Cin + ci : 0;
+        const bool ok = code >= 0 && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const int off = ok ? sOff[px] + koff : 0;
         const int v = x[off];
         a[j] = (_Float16)(float)(ok ? v : 0);
       }
