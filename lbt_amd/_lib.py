@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -176,6 +176,7 @@ _SIGS = {
     "lbt_maxpool_fwd": [_P, _P, _P, ConvDesc, _P],
     "lbt_maxpool_bwd": [_P, _P, _P, ConvDesc, _P],
     "lbt_maxpool_relu_bwd": [_P, _P, _P, _P, ConvDesc, _P],
+    "lbt_maxpool_relu_fwd": [_P, _P, _P, ConvDesc, _P],
     "lbt_avgpool_fwd": [_P, _P, c_int32, c_int32, c_int32, _P],
     "lbt_avgpool_bwd": [_P, _P, c_int32, c_int32, c_int32, _P],
     "lbt_softmax_xent": [_P, _P, c_int32, c_int32, _P, _P, _P],

@@ -72,8 +72,12 @@ __global__ __launch_bounds__(kT) void maxpool_bwd_kernel(const float* __restrict
 
 // maxpool_fwd_kernel for 4 channels per thread (C % 4 == 0): the same scan and strict '>' per
 // channel, 16-byte loads, one 4-byte argmax store.
+// relu != 0: the pool of the preceding ReLU_q's output computed from its INPUT: max(relu(a), ...) =
+// relu(max(a, ...)), so y is bit-identical. The argmax differs only where the window's max is <= 0
+// (the reference's first zero vs the first raw maximum), and there y = 0 makes the fused backward
+// (maxpool_relu_bwd) route nothing either way.
 __global__ __launch_bounds__(kT) void maxpool_fwd4_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                          uint8_t* __restrict__ amax, lbt_conv_desc d) {
+                                                          uint8_t* __restrict__ amax, lbt_conv_desc d, int relu) {
   const int64_t e4 = ((int64_t)blockIdx.x * kT + threadIdx.x) * 4;
   const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
   if (e4 >= total) return;
@@ -100,6 +104,10 @@ __global__ __launch_bounds__(kT) void maxpool_fwd4_kernel(const float* __restric
           bi[j] = kh * d.KW + kw;
         }
     }
+  }
+  if (relu) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) best[j] = best[j] > 0.f ? best[j] : 0.f;
   }
   *reinterpret_cast<float4*>(y + e4) = make_float4(best[0], best[1], best[2], best[3]);
   *reinterpret_cast<uchar4*>(amax + e4) = make_uchar4((uint8_t)bi[0], (uint8_t)bi[1], (uint8_t)bi[2], (uint8_t)bi[3]);
@@ -161,7 +169,7 @@ extern "C" int lbt_maxpool_fwd(const float* x, float* y, uint8_t* amax, lbt_conv
   const int64_t n = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
   if (d.Cin % 4 == 0)
     hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
-                       x, y, amax, d);
+                       x, y, amax, d, 0);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, x,
                        y, amax, d);
@@ -179,6 +187,16 @@ extern "C" int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, l
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, g,
                        amax, dx, d);
+  return (int)hipGetLastError();
+}
+
+// ReLU_q (forward) of the pool's input folded into the pool: x = the ReLU's input, y = pool(relu(x)).
+// Only for use with lbt_maxpool_relu_bwd (see maxpool_fwd4_kernel). C % 4 == 0.
+extern "C" int lbt_maxpool_relu_fwd(const float* x, float* y, uint8_t* amax, lbt_conv_desc d, void* stream) {
+  if (!pool_desc_ok(d) || d.Cin % 4 || d.KH * d.KW > 256) return LBT_EINVAL;
+  const int64_t n = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
+  hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
+                     x, y, amax, d, 1);
   return (int)hipGetLastError();
 }
 

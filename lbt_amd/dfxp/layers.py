@@ -706,12 +706,17 @@ class ReLU_q(Layer_q):
 
     def forward(self, X):
         self.X = X
+        if self.act_in_pool and X.shape[-1] % 4 == 0:
+            self.y = X
+            return X  # the pool computes pool(relu(X)) (ops.maxpool_relu_fwd)
         self.y = self._c.get("y", X.shape, torch.float32, X.device)
         ops.relu_fwd(X, self.y)
         return self.y
 
     # set by a following MaxPool_q that applies this mask in its own backward (pool_relu)
     mask_in_pool = False
+    # set by the model builder when that pool also applies the activation (forward returns X)
+    act_in_pool = False
 
     def backward(self, grad, stochastic=True):
         if self.mask_in_pool:
@@ -1026,7 +1031,10 @@ class MaxPool_q(Layer_q):
                                    self.padding)
         y = self._c.get("y", (N, d.Ho, d.Wo, C), torch.float32, X.device)
         self.amax = self._c.get("amax", (N, d.Ho, d.Wo, C), torch.uint8, X.device)
-        ops.maxpool_fwd(X, y, self.amax, d)
+        if self.pool_relu is not None and self.pool_relu.act_in_pool and C % 4 == 0:
+            ops.maxpool_relu_fwd(X, y, self.amax, d)  # X is the ReLU's input
+        else:
+            ops.maxpool_fwd(X, y, self.amax, d)
         self.y = y
         return y
 

@@ -455,6 +455,13 @@ def maxpool_fwd(x, y, amax, d):
         call("lbt_maxpool_fwd", ptr(x), ptr(y), ptr(amax), d, stream())
 
 
+def maxpool_relu_fwd(x, y, amax, d):
+    """MaxPool_q of the preceding ReLU_q's output, from the ReLU's input x (one pass)."""
+    _check(x, torch.float32, "x")
+    with _Timed("maxpool_fwd_kernel", 4 * x.numel() + 5 * y.numel()):
+        call("lbt_maxpool_relu_fwd", ptr(x), ptr(y), ptr(amax), d, stream())
+
+
 def maxpool_bwd(g, amax, dx, d):
     _check(g, torch.float32, "g")
     with _Timed("maxpool_bwd_kernel", 5 * g.numel() + 4 * dx.numel()):

@@ -227,7 +227,8 @@ class ImageNet_Resnet(Model):
         hw = image
         for s in (2, 2, 1, 2, 2, 2):  # conv1, max pool, stage strides
             hw = -(-hw // s)
-        layers[3].pool_relu = layers[2]  # the stem ReLU's backward runs inside the pool's
+        layers[3].pool_relu = layers[2]  # the stem ReLU (forward and backward) runs inside the pool
+        layers[2].act_in_pool = True
         blocks = [l for l in layers if isinstance(l, L.ResidualBottleneck_q)]
         for a, b in zip(blocks, blocks[1:]):
             a.next_block = b  # fused blocks hand their output's conv codes to the next block
