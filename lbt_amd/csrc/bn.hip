@@ -8,6 +8,7 @@
 // integer sums (moments of the quantised input; G*R, G, G*q for the backward), reduced
 // wave -> LDS -> one atomic per workgroup into a shard, so they are deterministic and
 // independent of the launch geometry.
+#include <cstdio>
 #include <cstdlib>
 
 #include "chain_flags.h"
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
           } else {
             f4(xv[b][j], t);
           }
-          if ((F & kRt) ? qr[b].active : true) {
+          if ((F & kRt) ? qr[b].active : !(F & kFNoR)) {
             int R[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -665,7 +666,14 @@ extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   LBT_CF(1, kFwdBlk | kFRes | kFY)                        // last block
   LBT_CF(2, kFwdBlk | kFY | kFO1 | kFU8)                  // block end, projection shortcut
   LBT_CF(2, kFwdBlk | kFY | kFO1 | kFO2 | kFU8)
+  LBT_CF(1, kFQ | kFNoR | kFY)                            // layer-path Normalization_q (ResNet-50 stem)
+  LBT_CF(1, kFRout | kFStoch | kFY)                       // ... and its Rescale_q
 #undef LBT_CF
+  if (getenv("LBT_CHAIN_DEBUG"))
+    fprintf(stderr, "chain_fwd kRt: f=%d nb=%d q=%d,%d rout=%d,%d qr=%d/%d,%d/%d o1=%d/%d/%d o2=%d/%d/%d relu=%d res=%d y=%d\n", f,
+            a->has_b2 ? 2 : 1, a->b1.nrm.q != nullptr, a->b2.nrm.q != nullptr, a->b1.rout != nullptr, a->b2.rout != nullptr,
+            a->b1.qr.bits, a->b1.qr.stochastic, a->b2.qr.bits, a->b2.qr.stochastic, a->o1 != nullptr, a->qo1.bits,
+            a->qo1.stochastic, a->o2 != nullptr, a->qo2.bits, a->qo2.stochastic, a->relu, a->res != nullptr, a->y != nullptr);
   if (a->has_b2)
     LBT_LAUNCH((chain_fwd_kernel<2, kRt>), grid, shm, st, *a, rpt);
   else

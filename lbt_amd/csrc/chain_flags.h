@@ -19,6 +19,7 @@ enum : int {
   kFO2 = 64,     // second output quantiser
   kFStoch = 128, // every quantiser stochastic
   kFU8 = 256,    // outputs in the unsigned 9-bit offset encoding
+  kFNoR = 512,   // no Rescale_q part (a layer-path Normalization_q alone)
 };
 
 enum : int {
@@ -45,20 +46,21 @@ inline int tri(bool all, bool none) { return all ? 1 : (none ? 0 : -1); }
 inline int fwd_flags(const lbt_chain_fwd& a) {
   const int nb = a.has_b2 ? 2 : 1;
   const lbt_chain_branch* br[2] = {&a.b1, &a.b2};
-  bool q_all = true, q_none = true, r_all = true, r_none = true, act = true;
+  bool q_all = true, q_none = true, r_all = true, r_none = true, act = true, act_none = true;
   bool st_all = true, st_none = true;
   for (int b = 0; b < nb; ++b) {
     q_all &= br[b]->nrm.q != nullptr; q_none &= br[b]->nrm.q == nullptr;
     r_all &= br[b]->rout != nullptr; r_none &= br[b]->rout == nullptr;
     act &= br[b]->qr.bits > 0;
+    act_none &= br[b]->qr.bits <= 0;
     st_all &= br[b]->qr.stochastic != 0; st_none &= br[b]->qr.stochastic == 0;
   }
   const bool o1 = a.o1 && a.qo1.bits > 0, o2 = a.o2 && a.qo2.bits > 0;
   if (o1) { st_all &= a.qo1.stochastic != 0; st_none &= a.qo1.stochastic == 0; }
   if (o2) { st_all &= a.qo2.stochastic != 0; st_none &= a.qo2.stochastic == 0; }
   const int q = tri(q_all, q_none), r = tri(r_all, r_none), st = tri(st_all, st_none);
-  if (q < 0 || r < 0 || st < 0 || !act) return kRt;
-  int f = 0;
+  if (q < 0 || r < 0 || st < 0 || !(act || (act_none && r == 0))) return kRt;
+  int f = act ? 0 : kFNoR;
   if (q) f |= kFQ;
   if (r) f |= kFRout;
   if (a.res) f |= kFRes;
