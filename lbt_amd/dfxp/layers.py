@@ -15,6 +15,7 @@ Differences from TF (documented in DESIGN.md):
 * ``Conv2d_q(..., input_nonnegative=True)`` declares a post-ReLU input: its (bits+1)-bit codes
   are unsigned and take the int8 MFMA path; otherwise the signed codes take the VALU path.
 """
+import contextlib
 import os
 
 import numpy as np
@@ -55,6 +56,37 @@ class _Cache:
             t = (torch.zeros if zero else torch.empty)(tuple(shape), dtype=dtype, device=device)
             self.d[key] = t
         return t
+
+
+# ---- side stream for work nothing later in the backward reads (weight gradients, BN dgamma /
+# dbeta): it runs concurrently with the dgrad / BN chain that is the backward's critical path and
+# is joined before the backward returns (join_side_work). LBT_SIDE_STREAM=0 keeps one stream.
+_SIDE = {}
+_PENDING = set()
+
+
+@contextlib.contextmanager
+def side_work():
+    main = torch.cuda.current_stream()
+    if os.environ.get("LBT_SIDE_STREAM", "1") == "0":
+        yield
+        return
+    side = _SIDE.get(main.device)
+    if side is None:
+        side = _SIDE[main.device] = torch.cuda.Stream(device=main.device)
+    side.wait_stream(main)  # its inputs were produced on the main stream
+    with torch.cuda.stream(side):
+        yield
+    _PENDING.add(side)
+
+
+def join_side_work():
+    """Make the current stream wait for every side_work launch so far (end of a backward)."""
+    if _PENDING:
+        main = torch.cuda.current_stream()
+        for s in _PENDING:
+            main.wait_stream(s)
+        _PENDING.clear()
 
 
 def _as_param(t, ctx):
@@ -192,7 +224,8 @@ class Conv2d_q(Layer_q):
         """Backward from int16 gradient codes the caller already quantised with self.grad_range:
         wide MFMA wgrad (+ reduce) and dgrad (dx + add_src, the other branch's gradient)."""
         self.gradq = gq16
-        self._wgrad_igemm(1)
+        with side_work():  # dW is read only by the optimizer: off the dgrad chain's critical path
+            self._wgrad_igemm(1)
         if not self.need_input_grad:
             return None
         d = self.d
@@ -983,8 +1016,9 @@ class ResidualBottleneck_q(ResidualBlock_q):
         G16 = n._c.get("G16", g.shape, torch.int16, dev)
         ops.bn_bwd_a_wide_masked(g, y_mask, mask_r, r.X_range.desc, r.gb, gmask_out, r.grad_range.desc, r.R,
                                  n.grad_range.desc, n.q, G16, sums, rows, inner, C, g2=g2)
-        ops.bn_param_grads(sums, C, r.grad_range.desc, r.X_range.desc, r.gamma, ops.f32(2 * r.weight_decay),
-                           r.dgamma, r.dbeta)
+        with side_work():
+            ops.bn_param_grads(sums, C, r.grad_range.desc, r.X_range.desc, r.gamma, ops.f32(2 * r.weight_decay),
+                               r.dgamma, r.dbeta)
         conv_out.grad_range.observe(g.numel())
         gq = conv_out._c.get("gq16", g.shape, torch.int16, dev)
         ops.bn_bwd_b_wide_q(G16, n.grad_range.desc, n.q, n.X_range.desc, n.ms, sums, n.n, gq,

@@ -9,7 +9,7 @@ import torch
 
 from . import dynamic_fixed_point as L
 from .dfxp import ops
-from .dfxp.layers import _Cache
+from .dfxp.layers import _Cache, join_side_work
 from .runtime import default_context
 
 
@@ -126,6 +126,7 @@ class Model:
         grad = self.dlogits
         for layer in reversed(self.layers):
             grad = layer.backward(grad, self.stochastic)
+        join_side_work()  # weight / BN-parameter gradients launched on the side stream
         return grad
 
     def grads_and_vars(self):
