@@ -49,6 +49,8 @@ def measure_step_kernels(trainer, x, y, steps=3):
     flat = trainer.flat
     saved = (flat.w.clone(), flat.a.clone(), trainer.ctx.exps.clone(), trainer.ctx.step.clone())
     ops.PROFILE = {}
+    side = os.environ.get("LBT_SIDE_STREAM")
+    os.environ["LBT_SIDE_STREAM"] = "0"  # one stream: each launch's events bracket it alone
     try:
         for _ in range(steps):
             # hold the stream with a ~150 ms spin so the host enqueues the whole step (event
@@ -61,6 +63,10 @@ def measure_step_kernels(trainer, x, y, steps=3):
         prof = ops.PROFILE
     finally:
         ops.PROFILE = None
+        if side is None:
+            os.environ.pop("LBT_SIDE_STREAM", None)
+        else:
+            os.environ["LBT_SIDE_STREAM"] = side
     flat.w.copy_(saved[0])
     flat.a.copy_(saved[1])
     trainer.ctx.exps.copy_(saved[2])
