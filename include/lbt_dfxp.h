@@ -440,7 +440,9 @@ int lbt_softmax_xent(const float* z, const int32_t* labels, int32_t N, int32_t K
  * wq is the Dense_q weight codes [C][K] (lbt_dfxp_quantize_weights' w_hwio of a C x 1 x 1 x K job,
  * 4-byte aligned). qx / qg are the stochastic X / grad quantisers (noise tables of C / K values,
  * or Philox inline). pooled, pq, gq are optional outputs (NULL = not stored).
- * Limits: C <= 256, C % 8 == 0, 1 <= K <= 64, HW >= 1, x 16-byte aligned.                   */
+ * Limits: C <= 256, C % 8 == 0, 1 <= K <= 64, HW >= 1, x 16-byte aligned.
+ * loss_n: the batch the mean is over (0 = N). A data-parallel rank passes the GLOBAL batch, so its
+ * dz rows and its loss share are exactly those of one process running the whole batch.       */
 typedef struct lbt_head {
   const float* x; int32_t N, HW, C, K;
   float* pooled; int8_t* pq; lbt_qdesc qx;
@@ -450,6 +452,7 @@ typedef struct lbt_head {
   const float* w; float wd2; float* dw;
   float* gx;
   void* scratch;
+  int32_t loss_n;
 } lbt_head;
 int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K);  /* = N * (C + 72) */
 int lbt_head_fwd_bwd(const lbt_head* h, void* stream);
@@ -523,6 +526,41 @@ int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const l
 int lbt_step_update(float* w, float* a, const float* g, int64_t n, float lr, float mu, float gscale,
                     int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
                     const float* nelem, int32_t nslots, uint64_t* step, void* stream);
+
+/* ---------------------------------------------------------------- data-parallel exchange ----
+ * SURVEY 8(e) / DESIGN 7. The step's gradients cross ranks as their EXACT integer numerators
+ * (the quantised-gradient exchange): lbt_step_reduce_x runs lbt_step_reduce's jobs but, instead of
+ * dequantising, writes each gradient element's int64 numerator into xbuf at its flat index
+ * (dw - gbase): a weight gradient's slab sum + 128 * its grad-code column sum (:302), a Rescale_q's
+ * sum G2*R and sum G2 (:689-690), the head's sum pq^T gq (:457); every quantiser's overflow counts
+ * (shards summed and ZEROED) at buf[cnt_off + 2*slot + {0,1}]; and the head's loss-term sum in
+ * 2^-32 fixed point at buf[loss_off]. One int64 SUM all-reduce over the ranks is exact and
+ * order-independent; lbt_step_finish then dequantises the totals with the single-process formulas
+ * (so a data-parallel step equals the one-process step whenever the per-sample work does), runs
+ * SGD-momentum, and lbt_dfxp_range_update_x applies update_range to the summed counts (a separate
+ * launch: the dequantisation reads the exponents the range update rewrites).
+ * pjob_scale multiplies the gamma / beta numerators: 1, or under SyncBN -- whose pass-A sums were
+ * already all-reduced -- 1 on one rank and 0 on the others.                                     */
+typedef struct lbt_xchg {
+  int64_t* buf; const float* gbase; int32_t pjob_scale; int32_t nslots;
+  int32_t* counts; int64_t cnt_off; int64_t loss_off;
+} lbt_xchg;
+int lbt_step_reduce_x(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
+                      int32_t max_c, const lbt_head* head, const lbt_xchg* x, void* stream);
+/* One parameter tensor of the flat buffers, [off, off + n): kind 0 = conv / dense weight
+ * (g = (float)S * 2^-(ex+eg) + wd2*w), 1 = Rescale_q gamma (g = (float)((double)S * 2^-eg * 2^-ex)
+ * + wd2*w; qx = its X quantiser, qg = its grad quantiser), 2 = Rescale_q beta (g = (float)((double)S
+ * * 2^-eg)). Blocks: ceil(n / 256) per segment in order (total_blocks = their sum).             */
+typedef struct lbt_fseg {
+  int64_t off, n; int32_t kind; lbt_qdesc qx, qg; float wd2;
+} lbt_fseg;
+/* g[i] (if g != NULL) = the dequantised gradient of xbuf[i]; a = mu*a + g; w -= lr*a (gscale 1);
+ * loss[0] = (float)(xbuf[loss_off] * 2^-32 / loss_n) if loss != NULL.                          */
+int lbt_step_finish(const lbt_fseg* segs, int32_t nseg, int32_t total_blocks, const int64_t* xbuf, float* w,
+                    float* a, float* g, float lr, float mu, float* loss, int64_t loss_off, int32_t loss_n,
+                    void* stream);
+int lbt_dfxp_range_update_x(int32_t* exps, const int64_t* xbuf, int64_t cnt_off, const int32_t* bits,
+                            const float* target, const float* nelem, int32_t nslots, uint64_t* step, void* stream);
 
 /* ---------------------------------------------------------------- either side of the path ---
  * GradientBuffer_q.backward (dynamic_fixed_point.py:473-509): total = pad(g, n_buf) + buffer;

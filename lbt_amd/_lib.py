@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -111,7 +111,16 @@ class Head(ctypes.Structure):
                 ("gq", c_void_p), ("qg", QDesc),
                 ("w", c_void_p), ("wd2", c_float), ("dw", c_void_p),
                 ("gx", c_void_p),
-                ("scratch", c_void_p)]
+                ("scratch", c_void_p), ("loss_n", c_int32)]
+
+
+class Xchg(ctypes.Structure):
+    _fields_ = [("buf", c_void_p), ("gbase", c_void_p), ("pjob_scale", c_int32), ("nslots", c_int32),
+                ("counts", c_void_p), ("cnt_off", c_int64), ("loss_off", c_int64)]
+
+
+class FSeg(ctypes.Structure):
+    _fields_ = [("off", c_int64), ("n", c_int64), ("kind", c_int32), ("qx", QDesc), ("qg", QDesc), ("wd2", c_float)]
 
 
 _P = c_void_p
@@ -193,6 +202,9 @@ _SIGS = {
     "lbt_head_fwd_bwd": [_P, _P],
     "lbt_step_prologue": [_P, c_int32, c_int64, _P, c_int64, _P, c_int32, c_int32, _P, c_int32, _P, _P],
     "lbt_step_reduce": [_P, c_int32, c_int32, _P, c_int32, c_int32, _P, _P],
+    "lbt_step_reduce_x": [_P, c_int32, c_int32, _P, c_int32, c_int32, _P, _P, _P],
+    "lbt_step_finish": [_P, c_int32, c_int32, _P, _P, _P, _P, c_float, c_float, _P, c_int64, c_int32, _P],
+    "lbt_dfxp_range_update_x": [_P, _P, c_int64, _P, _P, _P, c_int32, _P, _P],
     "lbt_grad_buffer_bwd": [_P, c_int64, _P, c_int64, c_int64, QDesc, _P, _P],
     "lbt_pre_dense": [_P, c_int32, c_int32, c_int32, c_int32, QDesc, _P, _P, _P, _P],
     "lbt_augment_flip_crop": [_P, _P, c_int32, c_int32, c_int32, c_int32, c_int32, c_uint64, c_uint64, _P],

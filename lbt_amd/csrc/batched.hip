@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob*
 // Blocks are allotted to the jobs in order, ceil(K*Cout/256) each (1-D grid); a block reduces 256
 // consecutive outputs over the slab's shards, with the offset correction 128 * sum_p g[co]
 // (x_u8off) summed once per column into LDS. lds: >= 4 KB.
-LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, uint8_t* lds) {
+LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, uint8_t* lds, const lbt_xchg& x) {
   int64_t* nbs = reinterpret_cast<int64_t*>(lds);                   // [256]
   long long* colsum = reinterpret_cast<long long*>(lds + 2048);      // [256]
   int* s_job = reinterpret_cast<int*>(lds + 4096);
@@ -112,6 +112,10 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
   long long s = 0;
   for (int b = 0; b < j.nsplit; ++b) s += j.slab[(int64_t)b * total + i];
   if (corr) s += 128ll * colsum[i % j.Cout];
+  if (x.buf) {  // data-parallel exchange: the exact numerator, dequantised after the all-reduce
+    x.buf[(j.dw - x.gbase) + i] = s;
+    return;
+  }
   const float scale = ldexpf(1.0f, -(frac_exp(j.qx) + frac_exp(j.qg)));
   const float a = (float)s * scale;
   const float b = j.wd2 * j.w[i];
@@ -120,10 +124,10 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
 
 __global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs, int njobs) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4112];
-  rjob_block(jobs, njobs, blockIdx.x, lds);
+  rjob_block(jobs, njobs, blockIdx.x, lds, lbt_xchg{});
 }
 
-LBT_DEV void pjob_channel(const lbt_pjob& j, int c) {
+LBT_DEV void pjob_channel(const lbt_pjob& j, int c, const lbt_xchg& x) {
   if (c >= j.C) return;
   long long vr[LBT_NSHARD], vg[LBT_NSHARD];  // all shard loads in flight at once
 #pragma unroll
@@ -137,6 +141,11 @@ LBT_DEV void pjob_channel(const lbt_pjob& j, int c) {
     sgr += vr[k];
     sg += vg[k];
   }
+  if (x.buf) {
+    x.buf[(j.dgamma - x.gbase) + c] = sgr * x.pjob_scale;
+    x.buf[(j.dbeta - x.gbase) + c] = sg * x.pjob_scale;
+    return;
+  }
   const double g2 = ldexp(1.0, -frac_exp(j.qrg)), r = ldexp(1.0, -frac_exp(j.qr));
   const float a = (float)((double)sgr * (g2 * r));
   const float b = j.wd2 * j.gamma[c];
@@ -145,25 +154,51 @@ LBT_DEV void pjob_channel(const lbt_pjob& j, int c) {
 }
 
 __global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
-  pjob_channel(jobs[blockIdx.y], blockIdx.x * blockDim.x + threadIdx.x);
+  pjob_channel(jobs[blockIdx.y], blockIdx.x * blockDim.x + threadIdx.x, lbt_xchg{});
 }
 
-// lbt_step_reduce: [r_blocks wgrad-reduce blocks][np * pblk param-grad blocks][1 head block]
+// One wave per slot: lane k < LBT_NSHARD reads (and zeroes) shard k of the overflow counters.
+LBT_DEV void fold_slot_x(const lbt_xchg& x, int i) {
+  const int lane = threadIdx.x & 63;
+  int a = 0, b = 0;
+  if (lane < LBT_NSHARD) {
+    int32_t* c = x.counts + ((int64_t)i * LBT_NSHARD + lane) * LBT_CSTRIDE;
+    a = c[0];
+    b = c[1];
+    c[0] = 0;
+    c[1] = 0;
+  }
+  a = wave_sum_i32(a);
+  b = wave_sum_i32(b);
+  if (lane == 0) {
+    x.buf[x.cnt_off + 2 * i] = a;
+    x.buf[x.cnt_off + 2 * i + 1] = b;
+  }
+}
+
+// lbt_step_reduce(_x): [r_blocks wgrad-reduce blocks][np * pblk param-grad blocks][1 head block]
+// [exchange only: ceil(nslots / 4) counter-fold blocks]
 __global__ __launch_bounds__(256) void step_reduce_kernel(const lbt_rjob* __restrict__ rjobs, int nr, int r_blocks,
                                                           const lbt_pjob* __restrict__ pjobs, int np, int pblk,
-                                                          lbt_head head) {
+                                                          lbt_head head, int has_head, lbt_xchg x) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLds];
   const int b = blockIdx.x;
   if (b < r_blocks) {
-    rjob_block(rjobs, nr, b, lds);
+    rjob_block(rjobs, nr, b, lds, x);
     return;
   }
   const int b2 = b - r_blocks;
   if (b2 < np * pblk) {
-    pjob_channel(pjobs[b2 / pblk], (b2 % pblk) * 256 + threadIdx.x);
+    pjob_channel(pjobs[b2 / pblk], (b2 % pblk) * 256 + threadIdx.x, x);
     return;
   }
-  head_reduce(head, lds);
+  const int b3 = b2 - np * pblk;
+  if (has_head && b3 == 0) {
+    head_reduce(head, x, lds);
+    return;
+  }
+  const int i = (b3 - has_head) * 4 + (int)(threadIdx.x >> 6);
+  if (x.buf && i < x.nslots) fold_slot_x(x, i);
 }
 
 // grid (blocks, njobs): thread -> noise block b (4 values, one Philox call)
@@ -364,8 +399,9 @@ extern "C" int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, i
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
-                               int32_t max_c, const lbt_head* head, void* stream) {
+namespace {
+int step_reduce_launch(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
+                       int32_t max_c, const lbt_head* head, const lbt_xchg& x, void* stream) {
   if (nr < 0 || np < 0 || nr > 256 || r_blocks < 0 || (nr > 0 && r_blocks == 0) || (np > 0 && max_c <= 0))
     return LBT_EINVAL;
   lbt_head h = {};
@@ -374,11 +410,119 @@ extern "C" int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_bloc
     if (h.N <= 0 || h.C <= 0 || h.C > 256 || h.C % 8 || h.K <= 0 || h.K > 64 || !h.scratch || !h.w || !h.dw || !h.loss)
       return LBT_EINVAL;
   }
+  if (x.buf && (!x.gbase || x.nslots < 0 || (x.nslots > 0 && !x.counts) || x.cnt_off < 0 || x.loss_off < 0 ||
+                (x.pjob_scale != 0 && x.pjob_scale != 1)))
+    return LBT_EINVAL;
   const int pblk = np > 0 ? (max_c + 255) / 256 : 0;
-  const int64_t blocks = (int64_t)r_blocks + (int64_t)np * pblk + (head ? 1 : 0);
+  const int fold = x.buf ? (x.nslots + 3) / 4 : 0;
+  const int64_t blocks = (int64_t)r_blocks + (int64_t)np * pblk + (head ? 1 : 0) + fold;
   if (blocks <= 0) return LBT_OK;
   hipLaunchKernelGGL(step_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rjobs, nr, r_blocks,
-                     pjobs, np, pblk, h);
+                     pjobs, np, pblk, h, head ? 1 : 0, x);
+  return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
+                               int32_t max_c, const lbt_head* head, void* stream) {
+  return step_reduce_launch(rjobs, nr, r_blocks, pjobs, np, max_c, head, lbt_xchg{}, stream);
+}
+
+extern "C" int lbt_step_reduce_x(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
+                                 int32_t max_c, const lbt_head* head, const lbt_xchg* x, void* stream) {
+  if (!x || !x->buf) return LBT_EINVAL;
+  return step_reduce_launch(rjobs, nr, r_blocks, pjobs, np, max_c, head, *x, stream);
+}
+
+namespace {
+
+// lbt_step_finish: blocks are dealt to the segments in order, ceil(n / 256) each (like rjob_block);
+// the last block also writes the loss.
+__global__ __launch_bounds__(256) void step_finish_kernel(const lbt_fseg* __restrict__ segs, int nseg,
+                                                          const int64_t* __restrict__ xbuf, float* __restrict__ w,
+                                                          float* __restrict__ a, float* __restrict__ g, float lr,
+                                                          float mu, float* loss, int64_t loss_off, int loss_n) {
+  __shared__ int64_t nbs[256];
+  __shared__ int s_seg;
+  __shared__ int64_t s_base;
+  for (int j = threadIdx.x; j < nseg; j += 256) nbs[j] = (segs[j].n + 255) / 256;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t b = blockIdx.x;
+    int jj = nseg;
+    for (int j = 0; j < nseg; ++j) {
+      if (b < nbs[j]) { jj = j; break; }
+      b -= nbs[j];
+    }
+    s_seg = jj;
+    s_base = b * 256;
+  }
+  __syncthreads();
+  if (loss && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    loss[0] = (float)((double)xbuf[loss_off] * 2.3283064365386963e-10 / (double)loss_n);  // * 2^-32
+  if (s_seg >= nseg) return;
+  const lbt_fseg sg = segs[s_seg];
+  const int64_t k = s_base + threadIdx.x;
+  if (k >= sg.n) return;
+  const int64_t i = sg.off + k;
+  const long long S = xbuf[i];
+  float gv;
+  if (sg.kind == 0) {  // wgrad_reduce / rjob_block / head_reduce: (float)S * 2^-(ex+eg) + wd2 * w
+    const float scale = ldexpf(1.0f, -(frac_exp(sg.qx) + frac_exp(sg.qg)));
+    const float p = (float)S * scale;
+    const float q = sg.wd2 * w[i];
+    gv = p + q;
+  } else if (sg.kind == 1) {  // pjob_channel dgamma
+    const double g2 = ldexp(1.0, -frac_exp(sg.qg)), r = ldexp(1.0, -frac_exp(sg.qx));
+    const float p = (float)((double)S * (g2 * r));
+    const float q = sg.wd2 * w[i];
+    gv = p + q;
+  } else {  // pjob_channel dbeta
+    gv = (float)((double)S * ldexp(1.0, -frac_exp(sg.qg)));
+  }
+  if (g) g[i] = gv;
+  const float t = mu * a[i];
+  const float an = t + gv;
+  a[i] = an;
+  const float step = lr * an;
+  w[i] = w[i] - step;
+}
+
+__global__ void range_update_x_kernel(int32_t* exps, const int64_t* xbuf, int64_t cnt_off, const int32_t* bits,
+                                      const float* target, const float* nelem, int nslots, uint64_t* step) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nslots && nelem[i] > 0.f) {  // update_range (dynamic_fixed_point.py:70-94) on the summed counts
+    const long long c1 = xbuf[cnt_off + 2 * i], c2 = xbuf[cnt_off + 2 * i + 1];
+    const float r1 = (float)c1 / nelem[i];
+    const float r2 = (float)c2 / nelem[i];
+    const float t = target[i];
+    const int delta = r1 > t ? 1 : (r2 <= t ? -1 : 0);
+    int I = exps[i] + delta;
+    const int hi = bits[i] - 1, lo = bits[i] - 1 - kEMax;
+    I = I > hi ? hi : (I < lo ? lo : I);
+    exps[i] = I;
+  }
+  if (i == 0) step[0] += 1ull;
+}
+
+}  // namespace
+
+extern "C" int lbt_step_finish(const lbt_fseg* segs, int32_t nseg, int32_t total_blocks, const int64_t* xbuf, float* w,
+                               float* a, float* g, float lr, float mu, float* loss, int64_t loss_off, int32_t loss_n,
+                               void* stream) {
+  if (nseg <= 0 || nseg > 256 || total_blocks <= 0 || !xbuf || !w || !a || (loss && loss_n <= 0)) return LBT_EINVAL;
+  hipLaunchKernelGGL(step_finish_kernel, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream, segs, nseg,
+                     xbuf, w, a, g, lr, mu, loss, loss_off, loss_n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_dfxp_range_update_x(int32_t* exps, const int64_t* xbuf, int64_t cnt_off, const int32_t* bits,
+                                       const float* target, const float* nelem, int32_t nslots, uint64_t* step,
+                                       void* stream) {
+  if (nslots < 0 || !xbuf || cnt_off < 0) return LBT_EINVAL;
+  const int blocks = nslots > 0 ? (nslots + 255) / 256 : 1;
+  hipLaunchKernelGGL(range_update_x_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, exps, xbuf, cnt_off, bits,
+                     target, nelem, nslots, step);
   return (int)hipGetLastError();
 }
 

@@ -14,8 +14,10 @@ constexpr int kHeadRecBytes = 24576;                        // records staged pe
 constexpr int kHeadLds = kHeadRecBytes + kHeadT * 16 * 4;   // + per-thread partials
 
 // One 256-thread workgroup: dw = dequant(sum_n pq[n]^T gq[n]) + wd2 * w (wgrad_reduce's formula)
-// and loss[0] = (float)(sum of the terms in softmax_xent_kernel's order / N). lds: kHeadLds bytes.
-LBT_DEV void head_reduce(const lbt_head& h, uint8_t* lds) {
+// and loss[0] = (float)(sum of the terms in softmax_xent_kernel's order / loss_n). lds: kHeadLds
+// bytes. With an exchange buffer (x.buf, lbt_step_reduce_x) the integer sums go to
+// x.buf[(dw - gbase) + ...] instead, and the loss-term sum, in 2^-32 fixed point, to x.buf[loss_off].
+LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds) {
   uint32_t* s_rec = reinterpret_cast<uint32_t*>(lds);
   int(*s_acc)[16] = reinterpret_cast<int(*)[16]>(lds + kHeadRecBytes);
   __shared__ double s_red[kHeadT];
@@ -84,6 +86,10 @@ LBT_DEV void head_reduce(const lbt_head& h, uint8_t* lds) {
       if (oc < C && ok < K) {
         int sum = 0;
         for (int gg = 0; gg < G; ++gg) sum += s_acc[gg * C + oc][o & 15];
+        if (x.buf) {
+          x.buf[(h.dw - x.gbase) + oc * K + ok] = (long long)sum;
+          continue;
+        }
         const float a = (float)(long long)sum * wscale;
         const float b = h.wd2 * wf[j];
         h.dw[oc * K + ok] = a + b;
@@ -96,7 +102,10 @@ LBT_DEV void head_reduce(const lbt_head& h, uint8_t* lds) {
     if (t < o) s_red[t] += s_red[t + o];
     __syncthreads();
   }
-  if (t == 0) h.loss[0] = (float)(s_red[0] / (double)N);
+  if (t == 0) {
+    h.loss[0] = (float)(s_red[0] / (double)(h.loss_n > 0 ? h.loss_n : N));
+    if (x.buf) x.buf[x.loss_off] = (long long)llrint(s_red[0] * 4294967296.0);
+  }
 }
 
 }  // namespace lbt

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h) {
     for (int k = 0; k < K; ++k) s = s + __shfl(e, k, 64);
     if (lane < K) {
       const float p = e / s;
-      const float dz = (p - (lane == y ? 1.f : 0.f)) / (float)N;
+      const float dz = (p - (lane == y ? 1.f : 0.f)) / (float)(h.loss_n > 0 ? h.loss_n : N);
       h.dz[(int64_t)n * K + lane] = dz;
       // Dense_q grad quantiser (:454), noise index = class
       const int q = sg.active ? quant_w<-1>(sg, h.qg.stochastic, dz, ug, ovg1, ovg2) : 0;

@@ -59,34 +59,60 @@ class _Cache:
 
 
 # ---- side stream for work nothing later in the backward reads (weight gradients, BN dgamma /
-# dbeta): it runs concurrently with the dgrad / BN chain that is the backward's critical path and
-# is joined before the backward returns (join_side_work). LBT_SIDE_STREAM=0 keeps one stream.
+# dbeta): it runs concurrently with the dgrad / BN chain that is the backward's critical path.
+# Contract: the OUTERMOST backward joins it before returning (backward_scope), so the caller of any
+# layer's backward -- Model.backward, a user Sequential_q, or block.backward called directly --
+# finds finished gradients on its stream. Side streams and pending joins are keyed by the main
+# stream that forked them: one model's join never waits on, or clears, another stream's work.
+# SIDE_STREAM is read once from LBT_SIDE_STREAM (0 = one stream); assign the attribute to change
+# it (a HIP graph captured earlier keeps the schedule it was captured with).
+SIDE_STREAM = os.environ.get("LBT_SIDE_STREAM", "1") != "0"
 _SIDE = {}
-_PENDING = set()
+_PENDING = {}
+_DEPTH = [0]
+
+
+def _stream_key(s):
+    return (s.device, s.cuda_stream)
 
 
 @contextlib.contextmanager
 def side_work():
     main = torch.cuda.current_stream()
-    if os.environ.get("LBT_SIDE_STREAM", "1") == "0":
+    if not SIDE_STREAM:
         yield
         return
-    side = _SIDE.get(main.device)
+    key = _stream_key(main)
+    side = _SIDE.get(key)
     if side is None:
-        side = _SIDE[main.device] = torch.cuda.Stream(device=main.device)
+        side = _SIDE[key] = torch.cuda.Stream(device=main.device)
     side.wait_stream(main)  # its inputs were produced on the main stream
+    # registered before anything is queued on it: a launch wrapper that raises part-way still
+    # leaves the main stream joined to whatever it did queue
+    _PENDING.setdefault(key, set()).add(side)
     with torch.cuda.stream(side):
         yield
-    _PENDING.add(side)
 
 
 def join_side_work():
-    """Make the current stream wait for every side_work launch so far (end of a backward)."""
-    if _PENDING:
-        main = torch.cuda.current_stream()
-        for s in _PENDING:
-            main.wait_stream(s)
-        _PENDING.clear()
+    """Make the current stream wait for every side_work launch it forked so far."""
+    main = torch.cuda.current_stream()
+    pend = _PENDING.pop(_stream_key(main), None)
+    for s in pend or ():
+        main.wait_stream(s)
+
+
+@contextlib.contextmanager
+def backward_scope():
+    """Wrap a backward: nested scopes (a block inside Model.backward) keep overlapping; the
+    outermost one joins the side stream before returning, also when the backward raises."""
+    _DEPTH[0] += 1
+    try:
+        yield
+    finally:
+        _DEPTH[0] -= 1
+        if _DEPTH[0] == 0:
+            join_side_work()
 
 
 def _as_param(t, ctx):
@@ -224,15 +250,16 @@ class Conv2d_q(Layer_q):
         """Backward from int16 gradient codes the caller already quantised with self.grad_range:
         wide MFMA wgrad (+ reduce) and dgrad (dx + add_src, the other branch's gradient)."""
         self.gradq = gq16
-        with side_work():  # dW is read only by the optimizer: off the dgrad chain's critical path
-            self._wgrad_igemm(1)
-        if not self.need_input_grad:
-            return None
-        d = self.d
-        dx = self._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, gq16.device)
-        ops.conv_dgrad_igemm_ws(gq16, 1, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx,
-                                self._ws(d, 1, True), add_src=add_src)
-        return dx
+        with backward_scope():
+            with side_work():  # dW is read only by the optimizer: off the dgrad chain's critical path
+                self._wgrad_igemm(1)
+            if not self.need_input_grad:
+                return None
+            d = self.d
+            dx = self._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, gq16.device)
+            ops.conv_dgrad_igemm_ws(gq16, 1, self.wd, self.ksd, d, self.grad_range.desc, self.W_range.desc, dx,
+                                    self._ws(d, 1, True), add_src=add_src)
+            return dx
 
     def quantize_weights(self):
         if self._batched_q and self.ctx.params_ready:
@@ -891,7 +918,8 @@ class ResidualBottleneck_q(ResidualBlock_q):
     def backward(self, grad, stochastic=True):
         if not self._fusable():
             return super().backward(grad, stochastic)
-        return self._backward_fused(grad)
+        with backward_scope():  # dW / dgamma / dbeta of the side stream are joined by the outermost backward
+            return self._backward_fused(grad)
 
     @staticmethod
     def _chain(c, bn, y, relu, res=None, bn2=None, out=None, o1=None, o1_conv=None, o2=None, o2_conv=None):

@@ -60,9 +60,17 @@ class _Block:
 class FusedResNet:
     """Drop-in for the Trainer (forward / compute_loss / backward / param_slots / ctx / loss)."""
 
-    def __init__(self, model):
+    def __init__(self, model, sync_bn=False, process_group=None):
+        """sync_bn: data-parallel parity mode -- every BatchNorm takes its moments (forward) and its
+        pass-A sums (backward) over the GLOBAL batch: the per-rank integer sums are all-reduced
+        (exact) before the kernel that consumes them, so N ranks of b samples compute what one
+        process computes on the N*b batch (tf.nn.moments over the whole batch,
+        dynamic_fixed_point.py:588). The step then holds blocking collectives: run it eagerly."""
         self.model = model
         self.ctx = model.ctx
+        self.sync_bn = bool(sync_bn) and self.ctx.world_size > 1
+        self.pg = process_group
+        self.xchg = None  # data-parallel exchange descriptor (Trainer.set_exchange)
         L = model.layers
         self.conv1, bn0 = L[0], L[1]
         self.n0, self.r0 = bn0.layers[0], bn0.layers[1]
@@ -132,8 +140,27 @@ class FusedResNet:
         return self.loss
 
     def backward(self):
+        if self.xchg is not None:
+            raise NotImplementedError("the data-parallel exchange runs with the fused head (train_fwd_bwd)")
         for f in self._hbwd + self._bwd + self._tail_sep:
             f()
+
+    def set_exchange(self, xchg):
+        """Write the step's gradient numerators / counters / loss into the exchange buffer instead of
+        dequantising them (lbt_step_reduce_x); set before the first step."""
+        if self._shape is not None:
+            raise RuntimeError("set_exchange after the plan was built")
+        self.xchg = xchg
+
+    def _allreduce(self, t):
+        """A SyncBN collective inside the launch list: the exact int64 sum of t over the ranks."""
+        import torch.distributed as dist
+        pg = self.pg
+
+        def run():
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg)
+        run.kname = "allreduce"
+        return run
 
     def train_fwd_bwd(self, X, labels):
         """forward + compute_loss + backward of one training step, the head as one launch
@@ -302,6 +329,8 @@ class FusedResNet:
             obs(b0.cs.X_range, numel0)
         a = self._chain_fwd(n0, qn0, chs0, r0, R0, None, None, None, None, None, relu=True, y=X0,
                             o1=xa, q1=b0.c1.X_range, o2=xs, q2=b0.cs.X_range if xs is not None else None)
+        if self.sync_bn:
+            fwd.append(self._allreduce(chs0))
         fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a)))
         self._keep = [a]
 
@@ -355,7 +384,7 @@ class FusedResNet:
                        d.w_hwio.data_ptr(), d.W_range.desc, self._labels.data_ptr(), self.logits.data_ptr(),
                        self.loss.data_ptr(), self.dlogits.data_ptr(), gqd.data_ptr(), self._qd(d.grad_range),
                        d.W.data_ptr(), ops.f32(2 * d.weight_decay), d.dW.data_ptr(), gY.data_ptr(),
-                       scratch.data_ptr())
+                       scratch.data_ptr(), Nb * ctx.world_size)  # mean over the global batch
         self._head = hd
         hfused = [L("lbt_head_fwd_bwd", ctypes.byref(hd), k="head_kernel",
                     nb=4 * Ylast.numel() * 2 + d.w_hwio.numel())]
@@ -381,6 +410,8 @@ class FusedResNet:
             aA.g = gY.data_ptr()
             bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
         aB = self._chain_bwd_b(n0, Gn0, qn0, sums0, shp0, C0, gq0, c.grad_range, None)
+        if self.sync_bn:
+            bwd.append(self._allreduce(sums0))
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB)))
         self._keep += [aA, aB]
         if self._stem:
@@ -409,9 +440,14 @@ class FusedResNet:
         nb_red = sum(4 * j.nsplit * j.K * j.Cout + 8 * j.K * j.Cout for j in rjobs)
         self._tail_sep = [L("lbt_step_reduce", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs), len(pjobs),
                             max_c, None, k="step_reduce_kernel", nb=nb_red)]
-        self._tail_fused = [L("lbt_step_reduce", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs), len(pjobs),
-                              max_c, ctypes.byref(hd), k="step_reduce_kernel",
-                              nb=nb_red + scratch.numel() + 8 * d.W.numel())]
+        if self.xchg is not None:  # data parallel: the numerators go to the exchange buffer
+            self._tail_fused = [L("lbt_step_reduce_x", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs),
+                                  len(pjobs), max_c, ctypes.byref(hd), ctypes.byref(self.xchg), k="step_reduce_kernel",
+                                  nb=nb_red + scratch.numel() + 8 * d.W.numel())]
+        else:
+            self._tail_fused = [L("lbt_step_reduce", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs),
+                                  len(pjobs), max_c, ctypes.byref(hd), k="step_reduce_kernel",
+                                  nb=nb_red + scratch.numel() + 8 * d.W.numel())]
         # ---- this step's noise tables: one launch ahead of everything else
         self._njobs = _dev_array(njobs, ctx.device)
         max_n = max(j.n for j in njobs)
@@ -446,8 +482,12 @@ class FusedResNet:
         return self._nd.get(q, q.desc)
 
     # ------------------------------------------------------------------ descriptor builders
+    def _gn(self, n):
+        """Elements per channel a BatchNorm's statistics are over: global under SyncBN."""
+        return n * self.ctx.world_size if self.sync_bn else n
+
     def _bn_norm(self, n, q, chsum, numel, C):
-        return BnNorm(q.data_ptr(), self._qd(n.X_range), chsum.data_ptr(), numel // C, ops.f32(n.eps),
+        return BnNorm(q.data_ptr(), self._qd(n.X_range), chsum.data_ptr(), self._gn(numel // C), ops.f32(n.eps),
                       ops.f32(n.momentum), ops.f32(1 - n.momentum), n.ms.data_ptr(), n.X_mean_running.data_ptr(),
                       n.X_var_running.data_ptr())
 
@@ -499,7 +539,7 @@ class FusedResNet:
         rows = shape[0]
         inner = math.prod(shape[1:])
         return ChainBwdB(G.data_ptr(), self._qd(n.grad_range), qn.data_ptr(), self._qd(n.X_range), n.ms.data_ptr(),
-                         sums.data_ptr(), rows * inner // C, None, gq.data_ptr(), self._qd(qo),
+                         sums.data_ptr(), self._gn(rows * inner // C), None, gq.data_ptr(), self._qd(qo),
                          gcol.data_ptr() if gcol is not None else None, rows, inner, C)
 
     # ------------------------------------------------------------------ one residual block
@@ -526,6 +566,8 @@ class FusedResNet:
         obs(c2.X_range, numel)
         a1 = self._chain_fwd(b.n1, qn1, chs1, b.r1, R1, None, None, None, None, None, relu=True, y=None, o1=xb,
                              q1=c2.X_range)
+        if self.sync_bn:
+            fwd.append(self._allreduce(chs1))
         fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a1), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a1)))
         qn2 = self._buf(k + "qn2", shp, torch.int8)
         chs2 = self._sums(k + "chs2", ops.NSHARD * 2 * C)
@@ -559,6 +601,10 @@ class FusedResNet:
                              o1=xa_n, q1=nxt.c1.X_range if nxt is not None else None,
                              o2=xs_n, q2=nxt.cs.X_range if xs_n is not None else None,
                              res=None if cs is not None else Xin)
+        if self.sync_bn:
+            fwd.append(self._allreduce(chs2))
+            if chss is not None:
+                fwd.append(self._allreduce(chss))
         fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a2), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a2)))
         self._keep += [a1, a2]
         info = dict(Xin=Xin, xa=xa, xs=xs, d1=d1, d2=d2, ds=ds, qn1=qn1, R1=R1, xb=xb, qn2=qn2, R2=R2, qns=qns,
@@ -612,6 +658,10 @@ class FusedResNet:
         gq2 = self._buf(k + "gq2", shp, torch.int8)
         gcol2 = self._sums(k + "gcol2", ops.NSHARD * 2 * C)
         aB2 = self._chain_bwd_b(b.n2, Gn2, f["qn2"], sums2, shp, C, gq2, c2.grad_range, gcol2)
+        if self.sync_bn:
+            bwd.append(self._allreduce(sums2))
+            if sumss is not None:
+                bwd.append(self._allreduce(sumss))
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB2), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB2)))
         keep = [aB2]
         gqs = gcols = None
@@ -654,6 +704,8 @@ class FusedResNet:
         gq1 = self._buf(k + "gq1", shp, torch.int8)
         gcol1 = self._sums(k + "gcol1", ops.NSHARD * 2 * C)
         aB1 = self._chain_bwd_b(b.n1, Gn1, f["qn1"], sums1, shp, C, gq1, c1.grad_range, gcol1)
+        if self.sync_bn:
+            bwd.append(self._allreduce(sums1))
         bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB1), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB1)))
         keep.append(aB1)
         add = gm

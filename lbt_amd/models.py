@@ -9,7 +9,7 @@ import torch
 
 from . import dynamic_fixed_point as L
 from .dfxp import ops
-from .dfxp.layers import _Cache, join_side_work
+from .dfxp.layers import _Cache, backward_scope
 from .runtime import default_context
 
 
@@ -124,9 +124,9 @@ class Model:
 
     def backward(self):
         grad = self.dlogits
-        for layer in reversed(self.layers):
-            grad = layer.backward(grad, self.stochastic)
-        join_side_work()  # weight / BN-parameter gradients launched on the side stream
+        with backward_scope():  # joins the weight / BN-parameter gradients launched on the side stream
+            for layer in reversed(self.layers):
+                grad = layer.backward(grad, self.stochastic)
         return grad
 
     def grads_and_vars(self):

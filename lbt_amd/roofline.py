@@ -16,7 +16,7 @@ import os
 
 import torch
 
-from .dfxp import ops
+from .dfxp import layers, ops
 
 HBM_PEAK_GBS = 8000.0
 
@@ -49,8 +49,8 @@ def measure_step_kernels(trainer, x, y, steps=3):
     flat = trainer.flat
     saved = (flat.w.clone(), flat.a.clone(), trainer.ctx.exps.clone(), trainer.ctx.step.clone())
     ops.PROFILE = {}
-    side = os.environ.get("LBT_SIDE_STREAM")
-    os.environ["LBT_SIDE_STREAM"] = "0"  # one stream: each launch's events bracket it alone
+    side = layers.SIDE_STREAM
+    layers.SIDE_STREAM = False  # one stream: each launch's events bracket it alone
     try:
         for _ in range(steps):
             # hold the stream with a ~150 ms spin so the host enqueues the whole step (event
@@ -63,10 +63,7 @@ def measure_step_kernels(trainer, x, y, steps=3):
         prof = ops.PROFILE
     finally:
         ops.PROFILE = None
-        if side is None:
-            os.environ.pop("LBT_SIDE_STREAM", None)
-        else:
-            os.environ["LBT_SIDE_STREAM"] = side
+        layers.SIDE_STREAM = side
     flat.w.copy_(saved[0])
     flat.a.copy_(saved[1])
     trainer.ctx.exps.copy_(saved[2])

@@ -10,15 +10,22 @@ MI355X-native execution:
 * after a warm-up step the whole step is captured into a HIP graph (``torch.cuda.CUDAGraph``)
   and replayed: ~300 kernel launches become one graph launch;
 * data parallelism (``torch.distributed``, backend ``nccl`` = RCCL over xGMI): each rank runs
-  the step on its own batch shard; between the backward graph and the update graph ONE
-  all-reduce sums the flat gradient buffer (which is the head of the comm buffer) and, in the
-  same call, the quantisers' overflow counters (folded into the tail as exact fp32 pairs by the
-  last kernel of the backward graph), so every rank applies identical updates and identical DFXP
+  the step on its own batch shard, with the loss a mean over the GLOBAL batch; between the
+  backward graph and the update graph ONE all-reduce sums the step's gradients and the
+  quantisers' overflow counters, so every rank applies identical updates and identical DFXP
   exponents. Noise keys (seed, step, quantiser) do not depend on the rank.
+  - fused plans (FusedResNet): the gradients travel as their exact int64 numerators (the
+    quantised-gradient exchange, lbt_step_reduce_x -> all-reduce -> lbt_step_finish): exact and
+    order-independent, so the update is the single-process formula applied to the global sums;
+    with ``FusedResNet(sync_bn=True)`` (global BatchNorm statistics) a step on N ranks of b
+    samples is bit-identical to one process on the N*b batch.
+  - layer-wise models: dequantised fp32 gradients + counters folded into exact fp32 pairs, one
+    fp32 all-reduce (gscale = 1/world).
 """
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from . import distributed as D
 from .dfxp import ops
 
@@ -64,12 +71,16 @@ class Trainer:
         if self.world != self.ctx.world_size:
             raise ValueError("DfxpContext.world_size (%d) must equal the process-group size (%d)"
                              % (self.ctx.world_size, self.world))
-        # fp32 comm buffer [grads | folded overflow counters] -> ONE in-place all-reduce per step
-        self.comm = None
-        if self.world > 1:
+        # data-parallel exchange: int64 [numerators | counters | loss] (fused plans) or fp32
+        # [grads | folded overflow counters] (layer-wise models) -> ONE in-place all-reduce per step
+        self.comm = self.xbuf = None
+        exact = self.world > 1 and hasattr(model, "set_exchange")
+        if self.world > 1 and not exact:
             n = sum(getattr(o, v).numel() for o, v, _ in model.param_slots())
             self.comm = D.make_comm_buffer(n, len(self.ctx.quantizers), self.ctx.device)
         self.flat = FlatParams(model, self.comm)
+        if exact:
+            self._setup_exchange()
         self.ctx.sums_managed = True
         self.global_step = 0
         self._graphs = None
@@ -79,6 +90,20 @@ class Trainer:
         self._aug = None
         if logger is not None:
             logger.info("Model info:\n" + model.info())
+
+    def _setup_exchange(self):
+        """The exact exchange of a fused plan: buffer, descriptor, and the finish kernel's segments."""
+        m, ctx, flat = self.model, self.ctx, self.flat
+        Q = len(ctx.quantizers)
+        self.xbuf, x = D.make_exchange(flat.n, Q, ctx.device)
+        x.gbase = flat.g.data_ptr()
+        rank = dist.get_rank(self.pg)
+        # SyncBN: the gamma / beta numerators come from pass-A sums that are already global
+        x.pjob_scale = 1 if (not getattr(m, "sync_bn", False) or rank == 0) else 0
+        x.counts = ctx.counts.data_ptr()
+        self._xchg = x
+        m.set_exchange(x)
+        self._segs, self._seg_blocks = D.finish_segments(flat, ctx.device)
 
     # -- the reference's API ---------------------------------------------------------------
     def init_model(self):
@@ -106,11 +131,22 @@ class Trainer:
             self.ctx.fold_counts(self.comm[self.flat.n:])
 
     def _exchange(self):
-        """Sum grads + overflow counters across ranks (one RCCL all-reduce; lbt_amd/distributed.py)."""
-        D.allreduce_comm(self.comm, self.pg)
+        """Sum the step's gradients + overflow counters across ranks (one RCCL all-reduce;
+        lbt_amd/distributed.py)."""
+        D.allreduce_comm(self.xbuf if self.xbuf is not None else self.comm, self.pg)
 
     def _update(self):
-        if self.comm is not None:
+        if self.xbuf is not None:  # exact exchange: dequantise the global sums, SGD, range update
+            ctx, f = self.ctx, self.flat
+            x = self._xchg
+            _lib.call("lbt_step_finish", _lib.ptr(self._segs), len(self._segs) // _lib.ctypes.sizeof(_lib.FSeg),
+                      self._seg_blocks, _lib.ptr(self.xbuf), _lib.ptr(f.w), _lib.ptr(f.a), _lib.ptr(f.g),
+                      float(self.lr), float(self.momentum), _lib.ptr(self.model.loss), x.loss_off,
+                      int(self.model._head.loss_n), _lib.stream())
+            _lib.call("lbt_dfxp_range_update_x", _lib.ptr(ctx.exps), _lib.ptr(self.xbuf), x.cnt_off,
+                      _lib.ptr(ctx.bits), _lib.ptr(ctx.target), _lib.ptr(ctx.nelem), len(ctx.quantizers),
+                      _lib.ptr(ctx.step), _lib.stream())
+        elif self.comm is not None:
             ops.sgd_momentum(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0 / self.world)
             self.ctx.update_range_folded_op(self.comm[self.flat.n:])
         else:  # optimiser + range update in one launch
@@ -122,6 +158,22 @@ class Trainer:
             self._exchange()
         self._update()
 
+    def _warmup(self, X, y):
+        """One un-captured forward + backward that allocates every per-layer buffer before a capture.
+        Its side effects are undone: the overflow counters (no update is applied) and the BN running
+        statistics (the reference moves them once per step, dynamic_fixed_point.py:601-612)."""
+        saved = [(bn.X_mean_running.clone(), bn.X_var_running.clone()) for bn in self._bn_layers()]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._fwd_bwd(X, y)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.ctx.counts.zero_()
+        for bn, (m, v) in zip(self._bn_layers(), saved):
+            bn.X_mean_running.copy_(m)
+            bn.X_var_running.copy_(v)
+
     def _capture(self, X, y):
         m = self.model
         if hasattr(m, "input_buffer") and hasattr(m, "label_buffer"):
@@ -132,15 +184,7 @@ class Trainer:
         sX, sy = self._static
         sX.copy_(X)
         sy.copy_(y)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            # warm-up: allocates every per-layer buffer outside the capture
-            self._fwd_bwd(sX, sy)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        # undo the warm-up's side effects on the DFXP counters (no update was applied)
-        self.ctx.counts.zero_()
+        self._warmup(sX, sy)
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             self._fwd_bwd(sX, sy)
@@ -157,13 +201,7 @@ class Trainer:
         """Capture the step reading (X, y) in place (models with binds_inputs): one graph per batch
         buffer pair, the first capture after a warm-up that allocates every per-layer buffer."""
         if not self._gcache:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                self._fwd_bwd(X, y)
-            torch.cuda.current_stream().wait_stream(s)
-            torch.cuda.synchronize()
-            self.ctx.counts.zero_()  # undo the warm-up's counters (no update was applied)
+            self._warmup(X, y)
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             self._fwd_bwd(X, y)
@@ -177,8 +215,9 @@ class Trainer:
         return g1, g2
 
     def step(self, X, y):
-        """One training step on batch (X [B,32,32,3] fp32 NHWC, y [B] int32), device tensors."""
-        if not self.use_graph:
+        """One training step on batch (X [B,32,32,3] fp32 NHWC, y [B] int32), device tensors.
+        A SyncBN plan holds collectives inside the step and runs eagerly."""
+        if not self.use_graph or getattr(self.model, "sync_bn", False):
             self._eager(X, y)
         else:
             key = (X.data_ptr(), y.data_ptr(), tuple(X.shape))

@@ -37,6 +37,11 @@ def tf_same_pads(in_size, k, s):
 
 
 def conv_geometry(H, W, kh, kw, sh, sw, padding):
+    """(Ho, Wo, pt, pb, pl, pr) for TF 'SAME' / 'VALID' or an explicit symmetric int padding (the torch
+    face, ``custom.py:11-12`` ``padding=1``)."""
+    if not isinstance(padding, str):
+        ph, pw = (padding, padding) if isinstance(padding, int) else padding
+        return (H + 2 * ph - kh) // sh + 1, (W + 2 * pw - kw) // sw + 1, ph, ph, pw, pw
     if padding == "SAME":
         Ho, pt, pb = tf_same_pads(H, kh, sh)
         Wo, pl, pr = tf_same_pads(W, kw, sw)
@@ -158,61 +163,98 @@ class LayerQ:
         return []
 
 
+def _bias_fwd(layer, y, ctx):
+    """y + Q(b) (``:198-201``, ``:390-393``): b quantised at bits, noise over b.shape[1:] = () (one
+    scalar); fp32 add."""
+    bq, eb = ctx.q(layer.name + "/b_range", layer.b, layer.bits)
+    return (y + dequant_f32(bq, eb)).astype(F32)
+
+
+def _bias_bwd(layer, gq, eg):
+    """db = sum of the dequantised grad codes over every axis but the last (``:209``, ``:459``),
+    from the exact integer sum: float32(float64(S) * 2**-eg)."""
+    layer.db_int = gq.reshape(-1, gq.shape[-1]).astype(np.int64).sum(0)
+    layer.db = (layer.db_int.astype(np.float64) * 2.0 ** -eg).astype(F32)
+
+
+def dequant_f32(q, e):
+    return (np.asarray(q).astype(F32) * F32(2.0 ** -e)).astype(F32)
+
+
 class Conv2dQ(LayerQ):
-    def __init__(self, name, bits, ksize, strides, padding, weight_decay=0.0, grad_bits=None, weight_bits=None):
+    """The integer weight-gradient numerator of the last backward is kept as ``acc_w`` (int64), and
+    its exponent as ``ew_grad`` (e_x + e_g), for the data-parallel oracle (``dp_train_step``)."""
+
+    def __init__(self, name, bits, ksize, strides, padding, weight_decay=0.0, grad_bits=None, weight_bits=None,
+                 use_bias=False):
         self.name, self.bits, self.ksize = name, bits, tuple(ksize)
         self.grad_bits = grad_bits or bits
         self.weight_bits = weight_bits or bits  # config 5: 4-bit weights
         self.strides = (strides[1], strides[2]) if len(strides) == 4 else tuple(strides)
         self.padding, self.wd = padding, weight_decay
+        self.use_bias = use_bias
         self.W = None
+        self.b = np.zeros(self.ksize[3], F32) if use_bias else None
 
     def range_names(self):
-        return [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
+        r = [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
+        return r + ([self.name + "/b_range"] if self.use_bias else [])
 
     def params(self):
-        return [(self.name + "/W", self)]
+        return [(self.name + "/W", self)] + ([(self.name + "/bias", self)] if self.use_bias else [])
 
     def forward(self, X, ctx):
         self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits + 1)
         self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.weight_bits)
         self.in_shape = X.shape
         acc = conv_fwd_int(self.xq, self.wq, self.strides, self.padding)
-        return scale_int(acc, self.ex + self.ew)
+        y = scale_int(acc, self.ex + self.ew)
+        return _bias_fwd(self, y, ctx) if self.use_bias else y
 
     def backward(self, g, ctx):
         gq, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         self.gq = gq
         acc_w = conv_wgrad_int(self.xq, gq, self.strides, self.padding, self.ksize[:2])
+        self.acc_w, self.ew_grad = acc_w, self.ex + eg
         c = F32(2 * self.wd)
         self.dW = (scale_int(acc_w, self.ex + eg) + (c * self.W).astype(F32)).astype(F32)
+        if self.use_bias:
+            _bias_bwd(self, gq, eg)
         acc_x = conv_dgrad_int(gq, self.wq, self.strides, self.padding, self.in_shape)
         return scale_int(acc_x, eg + self.ew)
 
 
 class DenseQ(LayerQ):
-    def __init__(self, name, bits, in_units, units, weight_decay=0.0, grad_bits=None, weight_bits=None):
+    def __init__(self, name, bits, in_units, units, weight_decay=0.0, grad_bits=None, weight_bits=None,
+                 use_bias=False):
         self.name, self.bits, self.in_units, self.units, self.wd = name, bits, in_units, units, weight_decay
         self.grad_bits = grad_bits or bits
         self.weight_bits = weight_bits or bits
+        self.use_bias = use_bias
         self.W = None
+        self.b = np.zeros(units, F32) if use_bias else None
 
     def range_names(self):
-        return [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
+        r = [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
+        return r + ([self.name + "/b_range"] if self.use_bias else [])
 
     def params(self):
-        return [(self.name + "/W", self)]
+        return [(self.name + "/W", self)] + ([(self.name + "/bias", self)] if self.use_bias else [])
 
     def forward(self, X, ctx):
         self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits)
         self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.weight_bits)
         acc = np.rint(self.xq.astype(np.float64) @ self.wq.astype(np.float64)).astype(np.int64)
-        return scale_int(acc, self.ex + self.ew)
+        y = scale_int(acc, self.ex + self.ew)
+        return _bias_fwd(self, y, ctx) if self.use_bias else y
 
     def backward(self, g, ctx):
         gq, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         self.gq = gq
         acc_w = np.rint(self.xq.astype(np.float64).T @ gq.astype(np.float64)).astype(np.int64)
+        self.acc_w, self.ew_grad = acc_w, self.ex + eg
+        if self.use_bias:
+            _bias_bwd(self, gq, eg)
         c = F32(2 * self.wd)
         self.dW = (scale_int(acc_w, self.ex + eg) + (c * self.W).astype(F32)).astype(F32)
         acc_x = np.rint(gq.astype(np.float64) @ self.wq.astype(np.float64).T).astype(np.int64)
@@ -301,6 +343,8 @@ class RescaleQ(LayerQ):
         sg = 2.0 ** -eg
         sr = 2.0 ** -self.er
         c = F32(2 * self.wd)
+        # integer numerators of dgamma / dbeta and their scales, for the data-parallel oracle
+        self.sgr, self.sg, self.eg, self.sgsr = (Gf * Rf).sum(0), Gf.sum(0), sg, sg * sr
         self.dgamma = ((Gf * Rf).sum(0).astype(np.float64) * (sg * sr)).astype(F32)
         self.dgamma = (self.dgamma + (c * self.gamma).astype(F32)).astype(F32)
         self.dbeta = (Gf.sum(0).astype(np.float64) * sg).astype(F32)
@@ -482,17 +526,20 @@ class FlattenQ(LayerQ):
         return g.reshape(self.shape)
 
 
-def softmax_xent(logits, labels):
-    """mean sparse softmax cross-entropy (``models.py:30-32``) and d loss / d logits, fp32."""
+def softmax_xent(logits, labels, norm=None):
+    """mean sparse softmax cross-entropy (``models.py:30-32``) and d loss / d logits, fp32.
+    norm: the batch the mean is over (default: these rows). A data-parallel shard passes the GLOBAL
+    batch, so its loss is its share of the global mean and dz its rows of the global gradient."""
     z = logits.astype(F32)
-    N = z.shape[0]
+    N = z.shape[0] if norm is None else int(norm)
     m = z.max(axis=1, keepdims=True)
     ez = np.exp((z - m).astype(F32)).astype(F32)
     s = ez.sum(axis=1, keepdims=True, dtype=F32)
     p = (ez / s).astype(F32)
     lse = (np.log(s).astype(F32) + m).astype(F32)
-    loss = float(np.mean((lse[:, 0] - z[np.arange(N), labels]).astype(np.float64)))
+    rows = np.arange(z.shape[0])
+    loss = float(np.sum((lse[:, 0] - z[rows, labels]).astype(np.float64)) / N)
     onehot = np.zeros_like(p)
-    onehot[np.arange(N), labels] = 1
+    onehot[rows, labels] = 1
     dz = ((p - onehot).astype(F32) / F32(N)).astype(F32)
     return loss, dz

@@ -10,7 +10,7 @@ d loss / d logits through ``reversed(layers)``) and the timed step of
 """
 import numpy as np
 
-from . import nn
+from . import dfxp, nn
 from .nn import F32
 
 
@@ -99,12 +99,16 @@ def init_ranges(model, initial=2):
     return {r: initial for r in model.range_names()}
 
 
-def forward_backward(model, ranges, x, labels, step, seed, target=0.0):
-    """Forward + loss + manual backward. Returns (loss, logits, grads, ctx)."""
+def forward_backward(model, ranges, x, labels, step, seed, target=0.0, dz=None, norm=None):
+    """Forward + loss + manual backward. Returns (loss, logits, grads, ctx).
+    dz: d loss / d logits to back-propagate instead of the oracle's own (a test injects the GPU's:
+    the softmax is the one op of the step that is not bit-exact, so with the same dz the whole
+    backward and update are). norm: the batch the loss mean is over (data-parallel shards: global)."""
     ctx = nn.Ctx(ranges, step, seed, target)
     logits = model.forward(np.asarray(x, F32), ctx)
-    loss, dz = nn.softmax_xent(logits, np.asarray(labels))
-    model.backward(dz, ctx)
+    loss, dz_own = nn.softmax_xent(logits, np.asarray(labels), norm)
+    model.backward(dz_own if dz is None else np.asarray(dz, F32), ctx)
+    ctx.logits, ctx.dz = logits, dz_own
     return loss, logits, get_grads(model), ctx
 
 
@@ -120,13 +124,77 @@ def sgd_momentum(params, grads, accum, lr, momentum):
     return new_p, new_a
 
 
-def train_step(model, state, x, labels, lr=1e-2, momentum=0.9, seed=0, target=0.0):
+def train_step(model, state, x, labels, lr=1e-2, momentum=0.9, seed=0, target=0.0, dz=None):
     """One ``Trainer.train`` batch (``trainer.py:157``) on the numpy model.
 
     ``state`` = dict(params, accum, ranges, step). Returns (loss, new_state, ctx).
+    dz: injected d loss / d logits (see forward_backward).
     """
     set_params(model, state["params"])
-    loss, logits, grads, ctx = forward_backward(model, state["ranges"], x, labels, state["step"], seed, target)
+    loss, logits, grads, ctx = forward_backward(model, state["ranges"], x, labels, state["step"], seed, target, dz)
     params, accum = sgd_momentum(state["params"], grads, state["accum"], lr, momentum)
     new_state = dict(params=params, accum=accum, ranges=ctx.new_ranges(), step=state["step"] + 1)
     return loss, new_state, ctx
+
+
+def _walk(layer):
+    yield layer
+    for attr in ("layers", "residual", "shortcut"):
+        sub = getattr(layer, attr, None)
+        if sub is None:
+            continue
+        for s in (sub if isinstance(sub, list) else [sub]):
+            yield from _walk(s)
+
+
+def _numerators(model):
+    """{param name: (kind, int64 numerator, scale, owner)} of the last backward: the integers each
+    gradient is dequantised from (the data-parallel exchange sums exactly these)."""
+    out = {}
+    for layer in _walk(model):
+        if isinstance(layer, (nn.Conv2dQ, nn.DenseQ)):
+            out[layer.name + "/W"] = ("w", layer.acc_w, layer.ew_grad, layer)
+        elif isinstance(layer, nn.RescaleQ):
+            out[layer.name + "/g"] = ("g", layer.sgr, layer.sgsr, layer)
+            out[layer.name + "/b"] = ("b", layer.sg, layer.eg, layer)
+    return out
+
+
+def dp_train_step(model, state, shards, lr=1e-2, momentum=0.9, seed=0, target=0.0, dzs=None):
+    """One data-parallel step over batch shards [(x_r, labels_r)], each
+    rank with its own batch statistics (standard DDP BatchNorm): every shard runs forward +
+    backward with the loss normalised by the GLOBAL batch; the exact integer numerators of every
+    weight / gamma / beta gradient and every quantiser's overflow counts are summed over the
+    shards (the build's one int64 all-reduce) and dequantised once, with the formulas of the
+    single-process step; then one SGD-momentum update and one range update from the summed
+    counts. dzs: per-shard injected d loss / d logits. Returns (global loss, new_state, ctxs)."""
+    B = sum(len(y) for _, y in shards)
+    num, counts, loss, ctxs = None, {}, 0.0, []
+    for r, (x, y) in enumerate(shards):
+        set_params(model, state["params"])
+        l, _, _, ctx = forward_backward(model, state["ranges"], x, y, state["step"], seed, target,
+                                        None if dzs is None else dzs[r], norm=B)
+        loss += l
+        ctxs.append(ctx)
+        nr = _numerators(model)
+        if num is None:
+            num = {k: [kind, v.astype(np.int64).copy(), sc, owner] for k, (kind, v, sc, owner) in nr.items()}
+        else:
+            for k, (_, v, _, _) in nr.items():
+                num[k][1] = num[k][1] + v
+        for name, (c1, c2, n, bits) in ctx.counts.items():
+            a = counts.get(name, (0, 0, 0, bits))
+            counts[name] = (a[0] + c1, a[1] + c2, a[2] + n, bits)
+    grads = {}
+    for k, (kind, S, sc, owner) in num.items():
+        if kind == "w":
+            grads[k] = (nn.scale_int(S, sc) + (F32(2 * owner.wd) * owner.W).astype(F32)).astype(F32)
+        elif kind == "g":
+            grads[k] = ((S.astype(np.float64) * sc).astype(F32) + (F32(2 * owner.wd) * owner.gamma).astype(F32)).astype(F32)
+        else:
+            grads[k] = (S.astype(np.float64) * sc).astype(F32)
+    params, accum = sgd_momentum(state["params"], grads, state["accum"], lr, momentum)
+    ranges = dict(state["ranges"])
+    for name, (c1, c2, n, bits) in counts.items():
+        ranges[name] = dfxp.update_range_from_counts(c1, c2, n, target, bits, state["ranges"][name])
+    return loss, dict(params=params, accum=accum, ranges=ranges, step=state["step"] + 1), ctxs

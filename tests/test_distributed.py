@@ -90,3 +90,86 @@ def test_dp_exchange_two_ranks_gloo():
     assert not np.array_equal(g0, g1)                          # shards really differ
     # identical DFXP exponents on both ranks, from the global counts
     assert I0 == I1
+
+
+def _xworker(rank, world, port, out_q):
+    """The exact exchange's layout on CPU: each rank packs its shard's integer gradient numerators,
+    overflow counts and loss share into the int64 buffer of lbt_amd.distributed.make_exchange, one
+    gloo all-reduce sums them, and the dequantised result must equal the oracle's global step."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lbt_amd import distributed as D
+        from oracle import resnet as R
+        model = R.build_resnet((1, 1, 1), 8, 2e-4)
+        rng = np.random.default_rng(0)
+        params = {}
+        for name, owner in model.params():
+            if name.endswith("/W"):
+                shp = owner.ksize if hasattr(owner, "ksize") else (owner.in_units, owner.units)
+                params[name] = rng.uniform(-0.3, 0.3, size=shp).astype(np.float32)
+            elif name.endswith("/g"):
+                params[name] = np.ones(owner.C, np.float32)
+            else:
+                params[name] = np.zeros(owner.C, np.float32)
+        state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()},
+                     ranges=R.init_ranges(model), step=0)
+        xr = np.random.default_rng(7)
+        X = ((xr.integers(0, 256, size=(2 * world, 32, 32, 3)) - 127.5) / 128).astype(np.float32)
+        Y = xr.integers(0, 10, size=2 * world)
+        shards = [(X[2 * r:2 * r + 2], Y[2 * r:2 * r + 2]) for r in range(world)]
+        R.set_params(model, params)
+        loss, _, _, ctx = R.forward_backward(model, state["ranges"], *shards[rank], step=0, seed=0, norm=2 * world)
+        num = R._numerators(model)
+        keys = sorted(num)
+        names = sorted(ctx.counts)
+        n = sum(num[k][1].size for k in keys)
+        buf, x = D.make_exchange(n, len(names), "cpu")
+        off = 0
+        for k in keys:
+            v = num[k][1].ravel()
+            buf[off:off + v.size] = torch.from_numpy(v.astype(np.int64))
+            off += v.size
+        for i, k in enumerate(names):
+            buf[x.cnt_off + 2 * i] = ctx.counts[k][0]
+            buf[x.cnt_off + 2 * i + 1] = ctx.counts[k][1]
+        buf[x.loss_off] = int(round(loss * 2 ** 32))
+        D.allreduce_comm(buf)
+        want_loss, want, _ = R.dp_train_step(model, state, shards)
+        got = {}
+        off = 0
+        for k in keys:
+            kind, S, sc, owner = num[k]
+            tot = buf[off:off + S.size].numpy().reshape(S.shape)
+            off += S.size
+            if kind == "w":
+                got[k] = (R.nn.scale_int(tot, sc) + (np.float32(2 * owner.wd) * params[k]).astype(np.float32)).astype(np.float32)
+            elif kind == "g":
+                got[k] = ((tot.astype(np.float64) * sc).astype(np.float32) + (np.float32(2 * owner.wd) * params[k]).astype(np.float32)).astype(np.float32)
+            else:
+                got[k] = (tot.astype(np.float64) * sc).astype(np.float32)
+        new_p, _ = R.sgd_momentum(params, got, state["accum"], 1e-2, 0.9)
+        ok = all(np.array_equal(new_p[k], want["params"][k]) for k in keys)
+        counts = {k: (int(buf[x.cnt_off + 2 * i]), int(buf[x.cnt_off + 2 * i + 1])) for i, k in enumerate(names)}
+        out_q.put((rank, ok, counts, float(buf[x.loss_off]) / 2 ** 32, want_loss))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_exact_int64_exchange_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xworker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, ok, counts, loss, want_loss in res:
+        assert ok                                   # exact: bit-identical to the oracle's global step
+        assert counts == res[0][2]                  # every rank sees the same global counts
+        assert abs(loss - want_loss) < 1e-6
