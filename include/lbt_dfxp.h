@@ -270,11 +270,14 @@ int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const void* g, in
  * Moments (biased, as tf.nn.moments): mu = S1*s/n, var = S2*s^2/n - mu^2 in double,
  * sigma = sqrtf((float)var + eps).  The first workgroup writes ms = [mu[C], sigma[C]] and,
  * if run_mean != NULL, the running averages avg = momentum*avg + one_minus_momentum*x
- * (:601-612).                                                                              */
+ * (:601-612).
+ * frozen != 0: the testing branch of the tf.cond (:590-600, set_testing, models.py:15): mu and
+ * var are the running averages (chsum unused), sigma = sqrtf(run_var + eps), nothing updated.  */
 typedef struct lbt_bn_norm {
   const int8_t* q; lbt_qdesc qn; const int64_t* chsum; int64_t n;
   float eps, momentum, one_minus_momentum;
   float* ms; float* run_mean; float* run_var;
+  int32_t frozen;
 } lbt_bn_norm;
 
 /* One branch of the forward element chain:
@@ -409,6 +412,12 @@ int lbt_add(const float* a, const float* b, float* y, int64_t n, void* stream);
 /* AvgPool_q over the whole HxW map (:1017): y[n,c] = (sequential fp32 sum) * (1/(H*W)). */
 int lbt_avgpool_fwd(const float* x, float* y, int32_t N, int32_t HW, int32_t C, void* stream);
 int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW, int32_t C, void* stream);
+/* AvgPool_q with any window (:1009-1022, tf.nn.avg_pool, SAME or VALID): y = (fp32 sum of the window's
+ * valid inputs in (kh, kw) order) / count, count = valid positions (TF SAME excludes padding);
+ * backward: each input sums g[o] / count[o] over the windows holding it, ascending output order.
+ * d as for lbt_maxpool_fwd.                                                                      */
+int lbt_avgpool_gen_fwd(const float* x, float* y, lbt_conv_desc d, void* stream);
+int lbt_avgpool_gen_bwd(const float* g, float* dx, lbt_conv_desc d, void* stream);
 /* MaxPool_q (:993-1006, tf.nn.max_pool; TF SAME pads with -inf): y = window max (first maximum in
  * (kh, kw) order wins), amax = its window position (one byte per output); backward (TF MaxPoolGrad)
  * routes each output gradient to its argmax input, summed per input in ascending output order.
@@ -602,6 +611,36 @@ int lbt_dense_wgrad(const int8_t* xq, const void* g, int32_t g16, int32_t N, int
                     lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2, float* dw, void* stream);
 int lbt_softmax_xent_wide(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss, float* dz,
                           void* stream);
+
+/* ---------------------------------------------------------------- 17..32-bit quantisers --------
+ * The top of weight_quantization's domain (1 <= bits <= 32, dynamic_fixed_point.py:21-23): a 17..31-
+ * bit quantiser's codes no longer fit the int8 / int16 GEMM operands, so it writes fake-quantised fp32
+ * values (lbt_dfxp_quantize, LBT_OUT_F32 -- the reference's own STE output), and bits == 32 is the
+ * full-precision bypass. The layers then contract fp32 operands as TF does (fp32.hip), accumulating
+ * in double in a fixed order (deterministic):
+ *   conv fwd / dgrad (dx += add_src if not NULL) / wgrad (pixels split nsplit ways into a double slab
+ *   [nsplit][KH*KW*Cin][Cout], then reduce: dw = (float)sum + wd2 * w); Dense_q = a 1x1 conv on a 1x1 map;
+ *   chan_sums: part[split][c] = sum a, part[split][C + c] = sum a*b (b NULL: a*a) over [rows][C];
+ *   bn_f32_fwd: biased moments from those sums, sigma = sqrtf(var + eps), y = (x - mu) / sigma, running
+ *   averages and ms = [mu | sigma] as lbt_bn_norm (frozen: testing mode, the running averages);
+ *   bn_f32_bwd: part = chan sums of (g, x); dx = ((g - mg) - xhat*mgx) / sigma (frozen: g / sigma);
+ *   affine: y = x*gb[c] + gb[C + c] (bwd != 0: y = x*gb[c]); affine_grads: dgamma = (float)sum g*x + wd2*gamma,
+ *   dbeta = (float)sum g, from chan sums of (g, x).                                                   */
+int lbt_conv_fwd_f32(const float* x, const float* w, lbt_conv_desc d, float* y, void* stream);
+int lbt_conv_dgrad_f32(const float* g, const float* w, lbt_conv_desc d, float* dx, const float* add_src, void* stream);
+int lbt_conv_wgrad_f32(const float* x, const float* g, lbt_conv_desc d, double* slab, int32_t nsplit, void* stream);
+int lbt_conv_wgrad_reduce_f32(const double* slab, int32_t nsplit, int64_t total, const float* w, float wd2, float* dw,
+                              void* stream);
+int lbt_chan_sums_f32(const float* a, const float* b, int64_t rows, int32_t C, int32_t nsplit, double* part,
+                      void* stream);
+int lbt_bn_f32_fwd(const float* x, const double* part, int32_t nsplit, int64_t rows, int32_t C, float eps,
+                   float momentum, float one_minus_momentum, float* ms, float* run_mean, float* run_var, int32_t frozen,
+                   float* y, void* stream);
+int lbt_bn_f32_bwd(const float* g, const float* x, const float* ms, const double* part, int32_t nsplit, int64_t rows,
+                   int32_t C, int32_t frozen, float* dx, void* stream);
+int lbt_affine_f32(const float* x, const float* gb, int64_t n, int32_t C, int32_t bwd, float* y, void* stream);
+int lbt_affine_grads_f32(const double* part, int32_t nsplit, int32_t C, const float* gamma, float wd2, float* dgamma,
+                         float* dbeta, void* stream);
 
 /* ABI version for the Python loader. */
 int lbt_abi_version(void);

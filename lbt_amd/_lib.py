@@ -42,7 +42,7 @@ class ConvDesc(ctypes.Structure):
 class BnNorm(ctypes.Structure):
     _fields_ = [("q", c_void_p), ("qn", QDesc), ("chsum", c_void_p), ("n", c_int64),
                 ("eps", c_float), ("momentum", c_float), ("one_minus_momentum", c_float),
-                ("ms", c_void_p), ("run_mean", c_void_p), ("run_var", c_void_p)]
+                ("ms", c_void_p), ("run_mean", c_void_p), ("run_var", c_void_p), ("frozen", c_int32)]
 
 
 class ChainBranch(ctypes.Structure):
@@ -188,6 +188,17 @@ _SIGS = {
     "lbt_maxpool_relu_fwd": [_P, _P, _P, ConvDesc, _P],
     "lbt_avgpool_fwd": [_P, _P, c_int32, c_int32, c_int32, _P],
     "lbt_avgpool_bwd": [_P, _P, c_int32, c_int32, c_int32, _P],
+    "lbt_avgpool_gen_fwd": [_P, _P, ConvDesc, _P],
+    "lbt_conv_fwd_f32": [_P, _P, ConvDesc, _P, _P],
+    "lbt_conv_dgrad_f32": [_P, _P, ConvDesc, _P, _P, _P],
+    "lbt_conv_wgrad_f32": [_P, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_wgrad_reduce_f32": [_P, c_int32, c_int64, _P, c_float, _P, _P],
+    "lbt_chan_sums_f32": [_P, _P, c_int64, c_int32, c_int32, _P, _P],
+    "lbt_bn_f32_fwd": [_P, _P, c_int32, c_int64, c_int32, c_float, c_float, c_float, _P, _P, _P, c_int32, _P, _P],
+    "lbt_bn_f32_bwd": [_P, _P, _P, _P, c_int32, c_int64, c_int32, c_int32, _P, _P],
+    "lbt_affine_f32": [_P, _P, c_int64, c_int32, c_int32, _P, _P],
+    "lbt_affine_grads_f32": [_P, c_int32, c_int32, _P, c_float, _P, _P, _P],
+    "lbt_avgpool_gen_bwd": [_P, _P, ConvDesc, _P],
     "lbt_softmax_xent": [_P, _P, c_int32, c_int32, _P, _P, _P],
     "lbt_sgd_momentum": [_P, _P, _P, c_int64, c_float, c_float, c_float, _P],
     "lbt_bias_add": [_P, _P, c_int64, c_int32, _P],

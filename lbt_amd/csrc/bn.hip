@@ -89,10 +89,19 @@ LBT_DEV void sum_shards(const int64_t* src, int n, int stride, long long* tmp) {
 // Normalization_q moments from the exact integer sums -> mu / sigma in LDS (and ms / running
 // stats from the first workgroup).
 LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long long* tmp) {
+  const bool writer = blockIdx.x == 0 && blockIdx.y == 0;
+  if (b.frozen) {  // testing mode: the running averages, no update
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float m = b.run_mean[c], sigma = sqrtf(b.run_var[c] + b.eps);
+      mu[c] = m;
+      sg[c] = sigma;
+      if (writer && b.ms) { b.ms[c] = m; b.ms[C + c] = sigma; }
+    }
+    return;
+  }
   sum_shards(b.chsum, 2 * C, 2 * C, tmp);
   __syncthreads();
   const double s = ldexp(1.0, -frac_exp(b.qn));
-  const bool writer = blockIdx.x == 0 && blockIdx.y == 0;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const double mean_d = (double)tmp[c] * s / (double)b.n;
     const double var_d = (double)tmp[C + c] * (s * s) / (double)b.n - mean_d * mean_d;

@@ -210,3 +210,87 @@ extern "C" int lbt_maxpool_relu_bwd(const float* g, const uint8_t* amax, const f
                      g, amax, y, dx, d);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- AvgPool_q, any window
+// dynamic_fixed_point.py:1009-1022 (tf.nn.avg_pool): y = (sum of the window's valid inputs in (kh, kw)
+// order, fp32) / count, count = the number of valid (non-padding) positions -- TF SAME excludes the
+// padding from the mean. Backward (TF AvgPoolGrad): each output spreads g / count over its window;
+// a thread per INPUT adds the shares of the windows holding it in ascending output order.
+namespace {
+
+LBT_DEV int avg_count(const lbt_conv_desc& d, int oh, int ow) {
+  int ch = 0, cw = 0;
+  for (int kh = 0; kh < d.KH; ++kh) ch += (unsigned)(oh * d.SH + kh - d.PT) < (unsigned)d.H;
+  for (int kw = 0; kw < d.KW; ++kw) cw += (unsigned)(ow * d.SW + kw - d.PL) < (unsigned)d.W;
+  return ch * cw;
+}
+
+__global__ __launch_bounds__(kT) void avgpool_gen_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                             lbt_conv_desc d) {
+  const int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x;
+  const int64_t total = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
+  if (e >= total) return;
+  const int c = (int)(e % d.Cin);
+  int64_t m = e / d.Cin;
+  const int ow = (int)(m % d.Wo);
+  m /= d.Wo;
+  const int oh = (int)(m % d.Ho);
+  const int n = (int)(m / d.Ho);
+  float acc = 0.f;
+  for (int kh = 0; kh < d.KH; ++kh) {
+    const int ih = oh * d.SH + kh - d.PT;
+    if ((unsigned)ih >= (unsigned)d.H) continue;
+    for (int kw = 0; kw < d.KW; ++kw) {
+      const int iw = ow * d.SW + kw - d.PL;
+      if ((unsigned)iw >= (unsigned)d.W) continue;
+      acc = acc + x[(((int64_t)n * d.H + ih) * d.W + iw) * d.Cin + c];
+    }
+  }
+  y[e] = acc / (float)avg_count(d, oh, ow);
+}
+
+__global__ __launch_bounds__(kT) void avgpool_gen_bwd_kernel(const float* __restrict__ g, float* __restrict__ dx,
+                                                             lbt_conv_desc d) {
+  const int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x;
+  const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
+  if (e >= total) return;
+  const int c = (int)(e % d.Cin);
+  int64_t m = e / d.Cin;
+  const int iw = (int)(m % d.W);
+  m /= d.W;
+  const int ih = (int)(m % d.H);
+  const int n = (int)(m / d.H);
+  // outputs whose window holds (ih, iw): oh*SH - PT <= ih < oh*SH - PT + KH
+  const int oh_lo = max(0, (ih + d.PT - d.KH + d.SH) / d.SH), oh_hi = min(d.Ho - 1, (ih + d.PT) / d.SH);
+  const int ow_lo = max(0, (iw + d.PL - d.KW + d.SW) / d.SW), ow_hi = min(d.Wo - 1, (iw + d.PL) / d.SW);
+  float acc = 0.f;
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    const int r = ih + d.PT - oh * d.SH;
+    if (r < 0 || r >= d.KH) continue;
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const int q = iw + d.PL - ow * d.SW;
+      if (q < 0 || q >= d.KW) continue;
+      const float share = g[(((int64_t)n * d.Ho + oh) * d.Wo + ow) * d.Cin + c] / (float)avg_count(d, oh, ow);
+      acc = acc + share;
+    }
+  }
+  dx[e] = acc;
+}
+
+}  // namespace
+
+extern "C" int lbt_avgpool_gen_fwd(const float* x, float* y, lbt_conv_desc d, void* stream) {
+  if (!pool_desc_ok(d)) return LBT_EINVAL;
+  const int64_t n = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
+  hipLaunchKernelGGL(avgpool_gen_fwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, x,
+                     y, d);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_avgpool_gen_bwd(const float* g, float* dx, lbt_conv_desc d, void* stream) {
+  if (!pool_desc_ok(d)) return LBT_EINVAL;
+  const int64_t n = (int64_t)d.N * d.H * d.W * d.Cin;
+  hipLaunchKernelGGL(avgpool_gen_bwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, g,
+                     dx, d);
+  return (int)hipGetLastError();
+}

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(kThreads) void quantize_generic_kernel(
 // update_range on one slot from its total counters (dynamic_fixed_point.py:70-94).
 LBT_DEV void range_apply(int i, int c1, int c2, int32_t* exps, const int32_t* bits, const float* target,
                          const float* nelem) {
+  if (bits[i] >= 32) return;  // the 32-bit bypass adds no update_range op (:22-23)
   const float r1 = (float)c1 / nelem[i];
   const float r2 = (float)c2 / nelem[i];
   const float t = target[i];
@@ -235,7 +236,8 @@ __global__ __launch_bounds__(kThreads) void quantize_weight_kernel(
 extern "C" int lbt_dfxp_quantize(const float* x, void* out, int out_kind, int64_t rows, int64_t inner,
                                  lbt_qdesc q, int64_t* chsum, int32_t C, void* stream) {
   if (rows <= 0 || inner <= 0) return LBT_OK;
-  if (q.bits < 2 || q.bits > 16) return LBT_EINVAL;
+  // 1..16 bits: integer codes; 17..31 bits: fake-quantised fp32 values only (the codes exceed int16)
+  if (q.bits < 1 || q.bits > 31 || (q.bits > 16 && out_kind != LBT_OUT_F32)) return LBT_EINVAL;
   if ((out_kind == LBT_OUT_I8 && q.bits > 8) || (out_kind == LBT_OUT_U8OFF && q.bits > 9)) return LBT_EINVAL;
   if (chsum && (C <= 0 || inner % C)) return LBT_EINVAL;
   hipStream_t st = (hipStream_t)stream;
@@ -302,7 +304,7 @@ extern "C" int lbt_dfxp_range_update_folded(int32_t* exps, const float* folded, 
 extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, int32_t Cin, int32_t Cout,
                                         lbt_qdesc q, int8_t* w_hwio, int8_t* wf, int32_t ksf, int8_t* wd,
                                         int32_t ksd, int32_t* colsum, void* stream) {
-  if (q.bits < 2 || q.bits > 8) return LBT_EINVAL;
+  if (q.bits < 1 || q.bits > 8) return LBT_EINVAL;
   if (wf && ksf * 16 < KH * KW * ((Cin + 15) / 16) * 16) return LBT_EINVAL;
   if (wd && ksd * 16 < KH * KW * ((Cout + 15) / 16) * 16) return LBT_EINVAL;
   hipLaunchKernelGGL(quantize_weight_kernel, dim3(Cout), dim3(kThreads), 0, (hipStream_t)stream, w, KH, KW, Cin,

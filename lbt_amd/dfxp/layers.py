@@ -119,6 +119,60 @@ def _as_param(t, ctx):
     return torch.as_tensor(t, dtype=torch.float32).to(ctx.device).contiguous()
 
 
+# ---- 17..32-bit quantisers (fp32.hip): weight_quantization's domain is 1 <= bits <= 32
+# (dynamic_fixed_point.py:21-23). Above 16 bits the integer codes no longer fit the int8 / int16 GEMM
+# operands; the quantiser then writes the fake-quantised fp32 values (the reference's own STE
+# output) and the layer contracts fp32 operands (fp32.hip), as TF does. bits == 32 is the bypass:
+# the tensor itself, no range update (:22-23).
+FLOAT_BITS = 16  # a layer whose quantisers exceed this many bits runs in float mode
+
+
+def _check_bits(bits):
+    assert 1 <= bits <= 32, "invalid value for bits: %d" % bits  # the reference's own assertion (:21)
+
+
+def _fq(x, q, cache, key):
+    """weight_quantization(x) as fp32 values: the quantiser's fake-quant output, or x itself at 32 bits."""
+    _check_bits(q.bits)
+    if q.bits == 32:
+        return x.contiguous()
+    x = x.contiguous()
+    return ops.quantize(x, q, OUT_F32, out=cache.get(key, x.shape, torch.float32, x.device))
+
+
+_FSPLIT = 64  # pixel / row splits of the fp32 reductions (fixed: deterministic double sums)
+
+
+def _chan_sums(a, b, C, cache, key):
+    rows = a.numel() // C
+    part = cache.get(key, (_FSPLIT, 2 * C), torch.float64, a.device)
+    _lib.call("lbt_chan_sums_f32", ptr(a), ptr(b), rows, C, _FSPLIT, ptr(part), _lib.stream())
+    return part
+
+
+def _conv_f32(xq, wq, d, y):
+    _lib.call("lbt_conv_fwd_f32", ptr(xq), ptr(wq), d, ptr(y), _lib.stream())
+
+
+def _conv_bwd_f32(layer, gq, d, dev):
+    """dW (+ 2*wd*W), db, dX of a float-mode conv / dense (layer.xq, layer.wq: its fp32 operands)."""
+    K = d.KH * d.KW * d.Cin
+    slab = layer._c.get("fslab", (_FSPLIT, K, d.Cout), torch.float64, dev)
+    _lib.call("lbt_conv_wgrad_f32", ptr(layer.xq), ptr(gq), d, ptr(slab), _FSPLIT, _lib.stream())
+    _lib.call("lbt_conv_wgrad_reduce_f32", ptr(slab), _FSPLIT, K * d.Cout, ptr(layer.W), ops.f32(2 * layer.weight_decay),
+              ptr(layer.dW), _lib.stream())
+    if layer.use_bias:
+        part = _chan_sums(gq, None, d.Cout, layer._c, "bpart")
+        scratch = layer._c.get("bscr", (d.Cout,), torch.float32, dev)
+        _lib.call("lbt_affine_grads_f32", ptr(part), _FSPLIT, d.Cout, ptr(layer.b), 0.0, ptr(scratch), ptr(layer.db),
+                  _lib.stream())
+    if not getattr(layer, "need_input_grad", True):
+        return None
+    dx = layer._c.get("dx", (d.N, d.H, d.W, d.Cin), torch.float32, dev)
+    _lib.call("lbt_conv_dgrad_f32", ptr(gq), ptr(layer.wq), d, ptr(dx), None, _lib.stream())
+    return dx
+
+
 class Layer_q:
     """Base class: identity forward, gradient pass-through backward (``:97-126``)."""
     _batched_q = False  # parameters quantised by the model's batched prologue (Model.forward)
@@ -158,17 +212,25 @@ class Conv2d_q(Layer_q):
         self.target_overflow_rate, self.weight_decay = target_overflow_rate, weight_decay
         self.input_nonnegative = input_nonnegative
         self.need_input_grad = True  # the model clears it for its first layer (TF prunes that dX)
+        # float mode: a quantiser beyond 16 bits (X at bits + 1: bits >= 16; at bits == 32 the X
+        # quantiser is 33 bits and the reference's assertion fires in forward, :21,287-288)
+        self.fmode = max(bits + 1, grad_bits or bits, weight_bits or bits) > FLOAT_BITS
         limit = (3 / (h * w * Cin)) ** 0.5
         self.W = _as_param(_rng(ctx, name + "/W").uniform(-limit, limit, size=ksize).astype(np.float32), ctx)
         self.dW = torch.zeros_like(self.W)
         t = target_overflow_rate
         self.W_range = ctx.quantizer(name + "/W_range", weight_bits, weight_range, t)
-        self.X_range = ctx.quantizer(name + "/X_range", bits + 1, input_range, t)
+        self.X_range = ctx.quantizer(name + "/X_range", min(bits + 1, 32), input_range, t)
         self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, t)
         if use_bias:
             self.b = torch.zeros(Cout, dtype=torch.float32, device=ctx.device)
             self.db = torch.zeros_like(self.b)
             self.b_range = ctx.quantizer(name + "/b_range", bits, bias_range, t)
+        if self.fmode:
+            self.mfma = self.igemm_w = self.igemm_f = self.igemm_d = self.x_mfma = self.w4 = False
+            self.x_kind = OUT_F32
+            self._c = _Cache()
+            return
         # int8 MFMA kernels: 8-bit codes on both GEMM sides (16-bit gradients: generic int64 kernels)
         self.mfma = ops.mfma_ok(Cin, Cout) and bits <= 8 and grad_bits <= 8
         if grad_bits > 8 and use_bias:
@@ -272,8 +334,24 @@ class Conv2d_q(Layer_q):
             ops.pack_int4(self.wf, self.wf4)
             ops.pack_int4(self.wd, self.wd4)
 
+    def _forward_f32(self, X):
+        _check_bits(self.bits + 1)  # bits == 32: the reference quantises X at 33 bits and asserts (:287-288)
+        N, H, W, Cin = X.shape
+        kh, kw, _, Cout = self.ksize
+        self.d = d = ops.conv_desc(N, H, W, Cin, Cout, kh, kw, self.strides[1], self.strides[2], self.padding)
+        self.xq = _fq(X, self.X_range, self._c, "xq")
+        self.wq = _fq(self.W, self.W_range, self._c, "wq")
+        y = self._c.get("y", (N, d.Ho, d.Wo, Cout), torch.float32, X.device)
+        _conv_f32(self.xq, self.wq, d, y)
+        if self.use_bias:
+            ops.bias_add(y, _fq(self.b, self.b_range, self._c, "bq"), Cout)
+        self.y = y
+        return y
+
     def forward(self, X):
         self.X = X
+        if self.fmode:
+            return self._forward_f32(X)
         N, H, W, Cin = X.shape
         kh, kw, _, Cout = self.ksize
         self.d = d = ops.conv_desc(N, H, W, Cin, Cout, kh, kw, self.strides[1], self.strides[2], self.padding)
@@ -340,6 +418,9 @@ class Conv2d_q(Layer_q):
                                 ops.f32(2 * self.weight_decay), self.dW)
 
     def backward(self, grad, stochastic=True):
+        if self.fmode:
+            self.gradq = _fq(grad, self.grad_range, self._c, "gq")
+            return _conv_bwd_f32(self, self.gradq, self.d, grad.device)
         if self.grad_bits > 8:
             return self._backward_wide(grad)
         d = self.d
@@ -421,10 +502,11 @@ class Dense_q(Layer_q):
             self.b = torch.zeros(units, dtype=torch.float32, device=ctx.device)
             self.db = torch.zeros_like(self.b)
             self.b_range = ctx.quantizer(name + "/b_range", bits, bias_range, t)
-        self.x_kind = OUT_I8 if bits <= 8 else OUT_I16
+        self.fmode = max(bits, grad_bits, weight_bits) > FLOAT_BITS
+        self.x_kind = OUT_F32 if self.fmode else (OUT_I8 if bits <= 8 else OUT_I16)
         self.w_hwio = torch.zeros((in_units, units), dtype=torch.int8, device=ctx.device)
         # wide heads (ResNet-50's fc): int8-MFMA GEMMs on packed images of the quantised W
-        self.mfma = ops.dense_mfma_ok(in_units, units, bits, weight_bits)
+        self.mfma = ops.dense_mfma_ok(in_units, units, bits, weight_bits) and not self.fmode
         if self.mfma:
             self.wf = torch.zeros((units, -(-in_units // 64) * 64), dtype=torch.int8, device=ctx.device)
             self.wd = torch.zeros((in_units, -(-units // 64) * 64), dtype=torch.int8, device=ctx.device)
@@ -441,6 +523,15 @@ class Dense_q(Layer_q):
         N = X.shape[0]
         dev = X.device
         self.d = d = _lib.ConvDesc(N, 1, 1, self.in_units, self.units, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
+        if self.fmode:  # Xq @ Wq on fp32 operands (a 1x1 conv on a 1x1 map)
+            self.xq = _fq(X, self.X_range, self._c, "xq")
+            self.wq = _fq(self.W, self.W_range, self._c, "wq")
+            y = self._c.get("y", (N, self.units), torch.float32, dev)
+            _conv_f32(self.xq, self.wq, d, y)
+            if self.use_bias:
+                ops.bias_add(y, _fq(self.b, self.b_range, self._c, "bq"), self.units)
+            self.y = y
+            return y
         self.xq = ops.quantize(X, self.X_range, self.x_kind, out=self._c.get("xq", X.shape,
                                                                               ops.out_dtype(self.x_kind), dev))
         if not (self._batched_q and self.ctx.params_ready):
@@ -464,6 +555,10 @@ class Dense_q(Layer_q):
         self.grad = grad  # kept for pre_dense_func (the reference's self.grad, :442)
         d = self.d
         dev = grad.device
+        if self.fmode:
+            self.gradq = _fq(grad, self.grad_range, self._c, "gq")
+            dx = _conv_bwd_f32(self, self.gradq, d, dev)
+            return dx.view(d.N, self.in_units)
         if self.grad_bits > 8:
             if self.use_bias:
                 raise NotImplementedError("bias with > 8-bit gradient codes")
@@ -601,17 +696,28 @@ class Normalization_q(Layer_q):
         self.X_mean_running = torch.zeros(num_features, dtype=torch.float32, device=ctx.device)
         self.X_var_running = torch.ones(num_features, dtype=torch.float32, device=ctx.device)
         self.ms = torch.zeros(2 * num_features, dtype=torch.float32, device=ctx.device)
+        self.fmode = max(bits, grad_bits) > FLOAT_BITS
         self._c = _Cache()
 
     def norm_desc(self, q, chsum, n):
         return BnNorm(ptr(q).value, self.X_range.desc, ptr(chsum).value, n, ops.f32(self.eps),
                       ops.f32(self.momentum), ops.f32(1 - self.momentum), self.ms.data_ptr(),
-                      self.X_mean_running.data_ptr(), self.X_var_running.data_ptr())
+                      self.X_mean_running.data_ptr(), self.X_var_running.data_ptr(), 0 if self.train else 1)
 
     def forward(self, X):
-        if self.train is False:
-            raise NotImplementedError("Normalization_q eval mode (running statistics) is not on the hot path")
+        """Training: batch moments of Xq (and the running averages move); testing (train False,
+        Model.set_testing): the running averages normalise and nothing moves (:590-612)."""
         self.X = X
+        if self.fmode:  # fp32 statistics of the fake-quantised (or, at 32 bits, raw) input
+            C = X.shape[-1]
+            self.q = _fq(X, self.X_range, self._c, "xq")
+            part = _chan_sums(self.q, None, C, self._c, "part") if self.train else None
+            y = self._c.get("y", X.shape, torch.float32, X.device)
+            _lib.call("lbt_bn_f32_fwd", ptr(self.q), ptr(part), _FSPLIT, X.numel() // C, C, ops.f32(self.eps),
+                      ops.f32(self.momentum), ops.f32(1 - self.momentum), ptr(self.ms), ptr(self.X_mean_running),
+                      ptr(self.X_var_running), 0 if self.train else 1, ptr(y), _lib.stream())
+            self.y = y
+            return y
         dev = X.device
         C = X.shape[-1]
         rows, inner = ops.rows_inner(tuple(X.shape))
@@ -632,9 +738,18 @@ class Normalization_q(Layer_q):
     def backward(self, grad, stochastic=True):
         dev = grad.device
         C = self.C
+        if self.fmode:
+            gq = _fq(grad, self.grad_range, self._c, "gq")
+            part = _chan_sums(gq, self.q, C, self._c, "gpart") if self.train else None
+            dx = self._c.get("dx", grad.shape, torch.float32, dev)
+            _lib.call("lbt_bn_f32_bwd", ptr(gq), ptr(self.q), ptr(self.ms), ptr(part), _FSPLIT, grad.numel() // C, C,
+                      0 if self.train else 1, ptr(dx), _lib.stream())
+            return dx
         rows, inner = ops.rows_inner(tuple(grad.shape))
         sums = self._c.sums("sums", ops.NSHARD * 4 * C, self.ctx)
         if self.grad_bits > 8:  # 16-bit gradient codes (config 4)
+            if not self.train:
+                raise NotImplementedError("Normalization_q testing-mode backward with > 8-bit gradient codes")
             self.grad_range.observe(grad.numel())
             G16 = self._c.get("G16", grad.shape, torch.int16, dev)
             dx = self._c.get("dx", grad.shape, torch.float32, dev)
@@ -651,8 +766,11 @@ class Normalization_q(Layer_q):
         a.rows, a.inner, a.C = rows, inner, C
         ops.chain_bwd_a(a)
         dx = self._c.get("dx", grad.shape, torch.float32, dev)
+        # testing mode: mean / variance are constants, dX = Gq / sigma -- pass B with zero sums
+        # (mg = mgx = 0 makes its ((g - mg) - xhat*mgx) / sigma exactly g / sigma)
+        bsums = sums if self.train else self._c.get("zsums", sums.shape, torch.int64, dev, zero=True)
         b = ChainBwdB(G.data_ptr(), self.grad_range.desc, self.q.data_ptr(), self.X_range.desc, self.ms.data_ptr(),
-                      sums.data_ptr(), self.n, dx.data_ptr(), None, NO_Q, None, rows, inner, C)
+                      bsums.data_ptr(), self.n, dx.data_ptr(), None, NO_Q, None, rows, inner, C)
         ops.chain_bwd_b(b)
         return dx
 
@@ -680,6 +798,7 @@ class Rescale_q(Layer_q):
         self.grad_bits = grad_bits = grad_bits or bits
         self.grad_range = ctx.quantizer(name + "/grad_range", grad_bits, grad_range, t)
         self.gb = torch.zeros(2 * num_features, dtype=torch.float32, device=dev)
+        self.fmode = max(bits, grad_bits) > FLOAT_BITS
         self._c = _Cache()
 
     def param_slots(self):
@@ -689,6 +808,10 @@ class Rescale_q(Layer_q):
         if self._batched_q and self.ctx.params_ready:
             return
         C = self.C
+        if self.fmode:
+            self.gb[:C].copy_(_fq(self.gamma, self.g_range, self._c, "gq_"))
+            self.gb[C:].copy_(_fq(self.beta, self.b_range, self._c, "bq_"))
+            return
         ops.quantize(self.gamma, self.g_range, OUT_F32, out=self.gb[:C])
         ops.quantize(self.beta, self.b_range, OUT_F32, out=self.gb[C:])
 
@@ -698,6 +821,12 @@ class Rescale_q(Layer_q):
         C = self.C
         rows, inner = ops.rows_inner(tuple(X.shape))
         self.quantize_params()
+        if self.fmode:
+            self.xr = _fq(X, self.X_range, self._c, "xr")
+            y = self._c.get("y", X.shape, torch.float32, dev)
+            _lib.call("lbt_affine_f32", ptr(self.xr), ptr(self.gb), X.numel(), C, 0, ptr(y), _lib.stream())
+            self.y = y
+            return y
         self.R = self._c.get("R", X.shape, torch.int8, dev)
         y = self._c.get("y", X.shape, torch.float32, dev)
         self.X_range.observe(X.numel())
@@ -716,8 +845,15 @@ class Rescale_q(Layer_q):
         dev = grad.device
         C = self.C
         rows, inner = ops.rows_inner(tuple(grad.shape))
-        sums = self._c.sums("sums", ops.NSHARD * 4 * C, self.ctx)
         dx = self._c.get("dx", grad.shape, torch.float32, dev)
+        if self.fmode:
+            g2 = _fq(grad, self.grad_range, self._c, "g2")
+            _lib.call("lbt_affine_f32", ptr(g2), ptr(self.gb), grad.numel(), C, 1, ptr(dx), _lib.stream())
+            part = _chan_sums(g2, self.xr, C, self._c, "part")
+            _lib.call("lbt_affine_grads_f32", ptr(part), _FSPLIT, C, ptr(self.gamma), ops.f32(2 * self.weight_decay),
+                      ptr(self.dgamma), ptr(self.dbeta), _lib.stream())
+            return dx
+        sums = self._c.sums("sums", ops.NSHARD * 4 * C, self.ctx)
         self.grad_range.observe(grad.numel())
         if self.grad_bits > 8:  # 16-bit gradient codes (config 4)
             ops.bn_bwd_a_wide(grad, self.grad_range.desc, self.R, self.gb[:C], NO_Q, None, None, dx, sums,
@@ -1120,26 +1256,38 @@ class MaxPool_q(Layer_q):
 
 
 class AvgPool_q(Layer_q):
-    """Average pool over the whole feature map (``:1009-1022`` as used by ResNet: 8x8 VALID)."""
+    """``AvgPool_q`` (``:1009-1022``, tf.nn.avg_pool). The window that covers the whole map (VALID) --
+    the ResNets' global pool -- sums in order and scales by 1/(H*W) (lbt_avgpool_fwd); any other
+    window / stride / SAME padding takes lbt_avgpool_gen_fwd (sum / count of valid positions)."""
 
     def __init__(self, ksize, strides, padding):
         self.ksize, self.strides, self.padding = ksize, strides, padding
         self._c = _Cache()
 
+    def _global(self, H, W):
+        return self.padding == "VALID" and self.ksize[1] == H and self.ksize[2] == W
+
     def forward(self, X):
         N, H, W, C = X.shape
-        if self.padding != "VALID" or self.ksize[1] != H or self.ksize[2] != W:
-            raise NotImplementedError("AvgPool_q: only global (ksize == map) VALID pooling is on the hot path")
         self.X = X
-        y = self._c.get("y", (N, 1, 1, C), torch.float32, X.device)
-        ops.avgpool_fwd(X, y, N, H * W, C)
+        if self._global(H, W):
+            y = self._c.get("y", (N, 1, 1, C), torch.float32, X.device)
+            ops.avgpool_fwd(X, y, N, H * W, C)
+        else:
+            self.d = d = ops.conv_desc(N, H, W, C, C, self.ksize[1], self.ksize[2], self.strides[1], self.strides[2],
+                                       self.padding)
+            y = self._c.get("y", (N, d.Ho, d.Wo, C), torch.float32, X.device)
+            ops.avgpool_gen_fwd(X.contiguous(), y, d)
         self.y = y
         return y
 
     def backward(self, grad, stochastic=True):
         N, H, W, C = self.X.shape
         dx = self._c.get("dx", self.X.shape, torch.float32, grad.device)
-        ops.avgpool_bwd(grad.contiguous(), dx, N, H * W, C)
+        if self._global(H, W):
+            ops.avgpool_bwd(grad.contiguous(), dx, N, H * W, C)
+        else:
+            ops.avgpool_gen_bwd(grad.contiguous(), dx, self.d)
         return dx
 
     def info(self):

@@ -369,6 +369,16 @@ def avgpool_bwd(g, dx, N, HW, C):
     call("lbt_avgpool_bwd", ptr(g), ptr(dx), int(N), int(HW), int(C), stream())
 
 
+def avgpool_gen_fwd(x, y, d):
+    _check(x, torch.float32, "x")
+    call("lbt_avgpool_gen_fwd", ptr(x), ptr(y), d, stream())
+
+
+def avgpool_gen_bwd(g, dx, d):
+    _check(g, torch.float32, "g")
+    call("lbt_avgpool_gen_bwd", ptr(g), ptr(dx), d, stream())
+
+
 def softmax_xent(z, labels, loss, dz):
     N, K = z.shape
     if K > 64:  # wide heads: one wave per row (the narrow kernel keeps the fused head's order)

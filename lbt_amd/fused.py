@@ -212,6 +212,9 @@ class FusedResNet:
         self._build(X)
 
     def _build(self, X):
+        if not getattr(self.model, "training", True):
+            raise NotImplementedError("FusedResNet runs training-mode BatchNorm; use the layer-wise model after "
+                                      "set_testing()")
         ctx = self.ctx
         st = _lib.stream
         N, H, W, Cin0 = X.shape

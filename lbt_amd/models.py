@@ -61,6 +61,8 @@ class Model:
         from .fused import _dev_array
         wjobs, starts, qjobs = [], [0], []
         for layer in self._walk():
+            if getattr(layer, "fmode", False):
+                continue  # 17..32-bit layers quantise their own parameters as fp32 values
             if isinstance(layer, L.Conv2d_q) and not layer.mfma and not getattr(layer, "w4", False) \
                     and layer.ksize[3] % 4 == 0:
                 kh, kw, ci, co = layer.ksize
@@ -110,6 +112,23 @@ class Model:
             self.ctx.params_ready = False
         self.logits = X
         return X
+
+    def _norm_layers(self):
+        return [l for l in self._walk() if isinstance(l, L.Normalization_q)]
+
+    def set_testing(self):
+        """models.py:15 ``set_testing``: every Normalization_q normalises with its running averages
+        (dynamic_fixed_point.py:590-600). The layer-wise model only (a FusedResNet plan is built for
+        training-mode BatchNorm, which is also what the reference's test loop runs, trainer.py:164)."""
+        self.training = False
+        for n in self._norm_layers():
+            n.train = False
+
+    def set_training(self):
+        """models.py:14 ``set_training``."""
+        self.training = True
+        for n in self._norm_layers():
+            n.train = True
 
     def compute_loss(self, labels):
         """loss = mean(sparse_softmax_cross_entropy(labels, logits)); keeps d loss / d logits."""

@@ -94,9 +94,9 @@ class DfxpContext:
         """Register a quantiser (a ``*_range`` variable initialised to ``initial``)."""
         if name in self.by_name:
             raise ValueError("duplicate DFXP range variable %r" % name)
-        if not 2 <= bits <= 16:
-            raise ValueError("DFXP bits must be in [2, 16] on this path, got %d" % bits)
-        if not 0 <= bits - initial - 1 <= 30:
+        if not 1 <= bits <= 32:  # weight_quantization's assertion (dynamic_fixed_point.py:21)
+            raise ValueError("invalid value for bits: %d" % bits)
+        if bits < 32 and not 0 <= bits - initial - 1 <= 30:
             raise ValueError("initial range %d invalid for %d bits (reference: 2**(bits-I-1) in int32)"
                              % (initial, bits))
         slot = len(self.quantizers)

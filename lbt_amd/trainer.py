@@ -87,6 +87,8 @@ class Trainer:
         self._static = None
         self._gcache = {}  # (X ptr, y ptr, shape) -> captured graphs (models that bind inputs)
         self._eval = {}
+        self._plans = {}
+        self._active = model
         self._aug = None
         if logger is not None:
             logger.info("Model info:\n" + model.info())
@@ -117,8 +119,27 @@ class Trainer:
         return self.step
 
     # -- the step ----------------------------------------------------------------------------
-    def _fwd_bwd(self, X, y):
+    def _plan(self, N):
+        """The execution plan for a batch of N: a fused plan is built for one batch shape, so another
+        N (the epoch's final partial batch, trainer.py:98) gets a plan of its own over the same
+        layers, parameters and quantisers."""
         m = self.model
+        if not hasattr(m, "set_exchange") or m._shape is None or m._shape[0] == N:
+            return m
+        p = self._plans.get(N)
+        if p is None:
+            from .fused import FusedResNet
+            p = FusedResNet(m.model, sync_bn=m.sync_bn, process_group=m.pg)
+            if self.xbuf is not None:
+                p.set_exchange(self._xchg)
+            self._plans[N] = p
+        return p
+
+    def _fwd_bwd(self, X, y):
+        m = self._active = self._plan(X.shape[0])
+        nel = getattr(m, "_nelem", None)
+        if nel is not None and self._plans:  # several plans: this one's per-step element counts
+            self.ctx.nelem.copy_(nel)
         if not getattr(m, "zeroes_own_sums", False):
             self.ctx.zero_sums()
         if hasattr(m, "train_fwd_bwd"):
@@ -127,6 +148,8 @@ class Trainer:
             m.forward(X)
             m.compute_loss(y)
             m.backward()
+        if nel is None and hasattr(m, "set_exchange"):
+            m._nelem = self.ctx.nelem.clone()  # what its build declared (Quantizer.observe)
         if self.comm is not None:
             self.ctx.fold_counts(self.comm[self.flat.n:])
 
@@ -141,8 +164,8 @@ class Trainer:
             x = self._xchg
             _lib.call("lbt_step_finish", _lib.ptr(self._segs), len(self._segs) // _lib.ctypes.sizeof(_lib.FSeg),
                       self._seg_blocks, _lib.ptr(self.xbuf), _lib.ptr(f.w), _lib.ptr(f.a), _lib.ptr(f.g),
-                      float(self.lr), float(self.momentum), _lib.ptr(self.model.loss), x.loss_off,
-                      int(self.model._head.loss_n), _lib.stream())
+                      float(self.lr), float(self.momentum), _lib.ptr(self._active.loss), x.loss_off,
+                      int(self._active._head.loss_n), _lib.stream())
             _lib.call("lbt_dfxp_range_update_x", _lib.ptr(ctx.exps), _lib.ptr(self.xbuf), x.cnt_off,
                       _lib.ptr(ctx.bits), _lib.ptr(ctx.target), _lib.ptr(ctx.nelem), len(ctx.quantizers),
                       _lib.ptr(ctx.step), _lib.stream())
@@ -200,8 +223,8 @@ class Trainer:
     def _capture_bound(self, X, y):
         """Capture the step reading (X, y) in place (models with binds_inputs): one graph per batch
         buffer pair, the first capture after a warm-up that allocates every per-layer buffer."""
-        if not self._gcache:
-            self._warmup(X, y)
+        if getattr(self._plan(X.shape[0]), "_shape", 0) is None or not self._gcache:
+            self._warmup(X, y)  # every plan's first run allocates its buffers outside a capture
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             self._fwd_bwd(X, y)
@@ -217,6 +240,7 @@ class Trainer:
     def step(self, X, y):
         """One training step on batch (X [B,32,32,3] fp32 NHWC, y [B] int32), device tensors.
         A SyncBN plan holds collectives inside the step and runs eagerly."""
+        self._active = self._plan(X.shape[0])
         if not self.use_graph or getattr(self.model, "sync_bn", False):
             self._eager(X, y)
         else:
@@ -238,7 +262,7 @@ class Trainer:
                 self._exchange()
                 g2.replay()
         self.global_step += 1
-        return self.model.loss
+        return self._active.loss
 
     def train(self, augment=True):
         """Epoch loop of trainer.py:117-192 over an in-memory dataset ((Xtr, ytr), (Xte, yte)):
@@ -255,7 +279,8 @@ class Trainer:
                 self.lr *= self.lr_decay_factor
                 self.get_train_op()
             perm = torch.randperm(len(Xtr))
-            for b in range(0, len(Xtr) - self.batch_size + 1, self.batch_size):
+            self.batch_sizes = []
+            for b in range(0, len(Xtr), self.batch_size):  # the final partial batch too (trainer.py:98)
                 idx = perm[b:b + self.batch_size]
                 X = torch.as_tensor(Xtr[idx.numpy()], dtype=torch.float32).to(dev).contiguous()
                 y = torch.as_tensor(ytr[idx.numpy()], dtype=torch.int32).to(dev)
@@ -264,6 +289,7 @@ class Trainer:
                         self._aug = torch.empty_like(X)
                     X = ops.augment_flip_crop(X, 4, self.ctx.seed, self.global_step, out=self._aug)
                 loss = self.step(X, y)
+                self.batch_sizes.append(len(idx))
                 if self.logger is not None and (b // self.batch_size + 1) % 100 == 0:
                     self.logger.info("Batch %d loss %f" % (b // self.batch_size + 1, loss.item()))
             if Xte is not None and len(Xte):
@@ -295,6 +321,7 @@ class Trainer:
         fetch update_range_op); BN running statistics are updated, as the reference's are."""
         dev = self.ctx.device
         saved = self.ctx.counts.clone()
+        saved_nelem = self.ctx.nelem.clone()  # an eval plan's build declares its own element counts
         acc_sum, loss_sum, nb, shared = 0.0, 0.0, 0, False
         for b in range(0, len(X), batch_size):
             Xb = torch.as_tensor(X[b:b + batch_size], dtype=torch.float32).to(dev).contiguous()
@@ -307,6 +334,7 @@ class Trainer:
             loss_sum += float(loss.item())
             nb += 1
         self.ctx.counts.copy_(saved)
+        self.ctx.nelem.copy_(saved_nelem)
         if shared:
             self._graphs = None
         return acc_sum / max(nb, 1), loss_sum / max(nb, 1)

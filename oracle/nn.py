@@ -115,6 +115,56 @@ def conv_wgrad_int(xq, gq, strides, padding, kshape):
     return np.rint(dw).astype(np.int64)
 
 
+FLOAT_BITS = 16  # layers whose quantisers exceed this run on fp32 values (lbt_amd fp32.hip)
+
+
+def conv_f32(x, w, strides, padding):
+    """fp32 conv of float operands, accumulated exactly enough (float64) and rounded once."""
+    N, H, W, Cin = x.shape
+    kh, kw, _, Cout = w.shape
+    sh, sw = strides
+    Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    xp = _windows(x.astype(np.float64), kh, kw, sh, sw, Ho, Wo, pt, pl)
+    acc = np.zeros((N * Ho * Wo, Cout), dtype=np.float64)
+    for i in range(kh):
+        for j in range(kw):
+            xs = xp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :]
+            acc += xs.reshape(-1, Cin) @ w[i, j].astype(np.float64)
+    return acc.reshape(N, Ho, Wo, Cout).astype(F32)
+
+
+def conv_dgrad_f32(g, w, strides, padding, in_shape):
+    N, H, W, Cin = in_shape
+    kh, kw, _, Cout = w.shape
+    sh, sw = strides
+    Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    Hp = max(H + pt, (Ho - 1) * sh + kh)
+    Wp = max(W + pl, (Wo - 1) * sw + kw)
+    dxp = np.zeros((N, Hp, Wp, Cin), dtype=np.float64)
+    gg = g.astype(np.float64).reshape(-1, Cout)
+    for i in range(kh):
+        for j in range(kw):
+            dxp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :] += \
+                (gg @ w[i, j].astype(np.float64).T).reshape(N, Ho, Wo, Cin)
+    return dxp[:, pt:pt + H, pl:pl + W, :].astype(F32)
+
+
+def conv_wgrad_f64(x, g, strides, padding, kshape):
+    N, H, W, Cin = x.shape
+    kh, kw = kshape
+    Cout = g.shape[-1]
+    sh, sw = strides
+    Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    xp = _windows(x.astype(np.float64), kh, kw, sh, sw, Ho, Wo, pt, pl)
+    gg = g.astype(np.float64).reshape(-1, Cout)
+    dw = np.zeros((kh, kw, Cin, Cout), dtype=np.float64)
+    for i in range(kh):
+        for j in range(kw):
+            xs = xp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :]
+            dw[i, j] = xs.reshape(-1, Cin).T @ gg
+    return dw
+
+
 def scale_int(acc, e):
     """float32(acc) * 2**-e, the dequant epilogue of every integer GEMM."""
     return (np.asarray(acc).astype(np.float32) * F32(2.0 ** -e)).astype(np.float32)
@@ -130,6 +180,14 @@ class Ctx:
         self.target = target
         self.counts = {}           # name -> (c1, c2, n, bits)
         self.record = {}           # name -> int codes (for parity tests)
+
+    def fq(self, name, x, bits, stochastic=True):
+        """weight_quantization's fp32 output: the dequantised codes, or x itself at 32 bits (:22-23)."""
+        assert 1 <= bits <= 32, "invalid value for bits: %d" % bits
+        if bits == 32:
+            return np.asarray(x, dtype=np.float32)
+        q, e = self.q(name, x, bits, stochastic)
+        return dequant_f32(q, e)
 
     def q(self, name, x, bits, stochastic=True):
         """Quantise with I_t; record overflow counts of x against I_t."""
@@ -195,6 +253,7 @@ class Conv2dQ(LayerQ):
         self.use_bias = use_bias
         self.W = None
         self.b = np.zeros(self.ksize[3], F32) if use_bias else None
+        self.fmode = max(bits + 1, self.grad_bits, self.weight_bits) > FLOAT_BITS
 
     def range_names(self):
         r = [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
@@ -204,14 +263,29 @@ class Conv2dQ(LayerQ):
         return [(self.name + "/W", self)] + ([(self.name + "/bias", self)] if self.use_bias else [])
 
     def forward(self, X, ctx):
+        self.in_shape = X.shape
+        if self.fmode:  # 17..32-bit quantisers: fp32 operands (X at bits + 1 <= 32, :287-288)
+            self.xf = ctx.fq(self.name + "/X_range", X, self.bits + 1)
+            self.wf = ctx.fq(self.name + "/W_range", self.W, self.weight_bits)
+            y = conv_f32(self.xf, self.wf, self.strides, self.padding)
+            if self.use_bias:
+                y = (y + ctx.fq(self.name + "/b_range", self.b, self.bits)).astype(F32)
+            return y
         self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits + 1)
         self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.weight_bits)
-        self.in_shape = X.shape
         acc = conv_fwd_int(self.xq, self.wq, self.strides, self.padding)
         y = scale_int(acc, self.ex + self.ew)
         return _bias_fwd(self, y, ctx) if self.use_bias else y
 
     def backward(self, g, ctx):
+        if self.fmode:
+            gf = ctx.fq(self.name + "/grad_range", g, self.grad_bits)
+            c = F32(2 * self.wd)
+            dw = conv_wgrad_f64(self.xf, gf, self.strides, self.padding, self.ksize[:2]).astype(F32)
+            self.dW = (dw + (c * self.W).astype(F32)).astype(F32)
+            if self.use_bias:
+                self.db = gf.reshape(-1, gf.shape[-1]).astype(np.float64).sum(0).astype(F32)
+            return conv_dgrad_f32(gf, self.wf, self.strides, self.padding, self.in_shape)
         gq, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         self.gq = gq
         acc_w = conv_wgrad_int(self.xq, gq, self.strides, self.padding, self.ksize[:2])
@@ -233,6 +307,7 @@ class DenseQ(LayerQ):
         self.use_bias = use_bias
         self.W = None
         self.b = np.zeros(units, F32) if use_bias else None
+        self.fmode = max(bits, self.grad_bits, self.weight_bits) > FLOAT_BITS
 
     def range_names(self):
         r = [self.name + "/W_range", self.name + "/X_range", self.name + "/grad_range"]
@@ -242,6 +317,13 @@ class DenseQ(LayerQ):
         return [(self.name + "/W", self)] + ([(self.name + "/bias", self)] if self.use_bias else [])
 
     def forward(self, X, ctx):
+        if self.fmode:
+            self.xf = ctx.fq(self.name + "/X_range", X, self.bits)
+            self.wf = ctx.fq(self.name + "/W_range", self.W, self.weight_bits)
+            y = (self.xf.astype(np.float64) @ self.wf.astype(np.float64)).astype(F32)
+            if self.use_bias:
+                y = (y + ctx.fq(self.name + "/b_range", self.b, self.bits)).astype(F32)
+            return y
         self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits)
         self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.weight_bits)
         acc = np.rint(self.xq.astype(np.float64) @ self.wq.astype(np.float64)).astype(np.int64)
@@ -249,6 +331,13 @@ class DenseQ(LayerQ):
         return _bias_fwd(self, y, ctx) if self.use_bias else y
 
     def backward(self, g, ctx):
+        if self.fmode:
+            gf = ctx.fq(self.name + "/grad_range", g, self.grad_bits).astype(np.float64)
+            c = F32(2 * self.wd)
+            self.dW = ((self.xf.astype(np.float64).T @ gf).astype(F32) + (c * self.W).astype(F32)).astype(F32)
+            if self.use_bias:
+                self.db = gf.sum(0).astype(F32)
+            return (gf @ self.wf.astype(np.float64).T).astype(F32)
         gq, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         self.gq = gq
         acc_w = np.rint(self.xq.astype(np.float64).T @ gq.astype(np.float64)).astype(np.int64)
@@ -262,20 +351,53 @@ class DenseQ(LayerQ):
 
 
 class NormQ(LayerQ):
+    """train False: the testing branch of ``:590-600`` (mean / var = the running averages, which do
+    not move; backward dX = Gq / sigma since mean and var are constants of the graph)."""
+
     def __init__(self, name, bits, num_features, momentum=0.999, eps=1e-5, grad_bits=None):
         self.name, self.bits, self.C = name, bits, num_features
         self.grad_bits = grad_bits or bits
         self.momentum, self.eps = momentum, eps
         self.mean_running = np.zeros(num_features, F32)
         self.var_running = np.ones(num_features, F32)
+        self.train = True
+        self.fmode = max(bits, self.grad_bits) > FLOAT_BITS
 
     def range_names(self):
         return [self.name + "/X_range", self.name + "/grad_range"]
 
+    def _forward_f32(self, X, ctx):
+        """fp32 input (fake-quantised, or raw at 32 bits): moments from float64 sums (the build's
+        fixed-order double sums), the same fp32 normalisation as the integer path."""
+        x = ctx.fq(self.name + "/X_range", X, self.bits)
+        C = X.shape[-1]
+        xf = x.reshape(-1, C).astype(np.float64)
+        n = xf.shape[0]
+        if self.train:
+            mean_d = xf.sum(0) / n
+            var_d = (xf * xf).sum(0) / n - mean_d * mean_d
+            mu, var = mean_d.astype(F32), var_d.astype(F32)
+            m = F32(self.momentum)
+            self.mean_running = ((m * self.mean_running).astype(F32) + (F32(1 - self.momentum) * mu).astype(F32)).astype(F32)
+            self.var_running = ((m * self.var_running).astype(F32) + (F32(1 - self.momentum) * var).astype(F32)).astype(F32)
+        else:
+            mu, var = self.mean_running, self.var_running
+        sigma = np.sqrt((var + F32(self.eps)).astype(F32)).astype(F32)
+        self.xf, self.mu, self.sigma, self.n = x, mu, sigma, n
+        return ((x - mu).astype(F32) / sigma).astype(F32)
+
     def forward(self, X, ctx):
+        if self.fmode:
+            return self._forward_f32(X, ctx)
         q, e = ctx.q(self.name + "/X_range", X, self.bits)
         s = 2.0 ** -e
         C = X.shape[-1]
+        if not self.train:
+            mu, var = self.mean_running, self.var_running
+            sigma = np.sqrt((var + F32(self.eps)).astype(F32)).astype(F32)
+            xhat = (((q.astype(F32) * F32(s)).astype(F32) - mu).astype(F32) / sigma).astype(F32)
+            self.q, self.e, self.mu, self.sigma, self.xhat, self.n = q, e, mu, sigma, xhat, q.size // C
+            return xhat
         qf = q.reshape(-1, C).astype(np.int64)
         n = qf.shape[0]
         S1 = qf.sum(0)
@@ -293,10 +415,26 @@ class NormQ(LayerQ):
         return xhat
 
     def backward(self, g, ctx):
+        if self.fmode:
+            gf = ctx.fq(self.name + "/grad_range", g, self.grad_bits)
+            if not self.train:
+                return (gf / self.sigma).astype(F32)
+            C = g.shape[-1]
+            g2 = gf.reshape(-1, C).astype(np.float64)
+            x2 = self.xf.reshape(-1, C).astype(np.float64)
+            Sg, Sgx = g2.sum(0), (g2 * x2).sum(0)
+            mg = (Sg / self.n).astype(F32)
+            mgx = ((Sgx - self.mu.astype(np.float64) * Sg) / (self.n * self.sigma.astype(np.float64))).astype(F32)
+            xhat = ((self.xf - self.mu).astype(F32) / self.sigma).astype(F32)
+            a = (gf - mg).astype(F32)
+            b = (xhat * mgx).astype(F32)
+            return ((a - b).astype(F32) / self.sigma).astype(F32)
         G, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         sg = 2.0 ** -eg
         s = 2.0 ** -self.e
         C = g.shape[-1]
+        if not self.train:
+            return ((G.astype(F32) * F32(sg)).astype(F32) / self.sigma).astype(F32)
         Gf = G.reshape(-1, C).astype(np.int64)
         qf = self.q.reshape(-1, C).astype(np.int64)
         SG = Gf.sum(0)
@@ -318,6 +456,7 @@ class RescaleQ(LayerQ):
         self.grad_bits = grad_bits or bits
         self.gamma = np.ones(num_features, F32)
         self.beta = np.zeros(num_features, F32)
+        self.fmode = max(bits, self.grad_bits) > FLOAT_BITS
 
     def range_names(self):
         return [self.name + "/g_range", self.name + "/b_range", self.name + "/X_range", self.name + "/grad_range"]
@@ -326,6 +465,11 @@ class RescaleQ(LayerQ):
         return [(self.name + "/g", self), (self.name + "/b", self)]
 
     def forward(self, X, ctx):
+        if self.fmode:
+            self.xr = ctx.fq(self.name + "/X_range", X, self.bits)
+            self.gq_f = ctx.fq(self.name + "/g_range", self.gamma, self.bits)
+            bq_f = ctx.fq(self.name + "/b_range", self.beta, self.bits)
+            return ((self.xr * self.gq_f).astype(F32) + bq_f).astype(F32)
         R, er = ctx.q(self.name + "/X_range", X, self.bits)
         gq, eg = ctx.q(self.name + "/g_range", self.gamma, self.bits)
         bq, eb = ctx.q(self.name + "/b_range", self.beta, self.bits)
@@ -336,6 +480,15 @@ class RescaleQ(LayerQ):
         return ((xr * self.gq_f).astype(F32) + bq_f).astype(F32)
 
     def backward(self, g, ctx):
+        if self.fmode:
+            gf = ctx.fq(self.name + "/grad_range", g, self.grad_bits)
+            C = g.shape[-1]
+            g2 = gf.reshape(-1, C).astype(np.float64)
+            c = F32(2 * self.wd)
+            self.dgamma = ((g2 * self.xr.reshape(-1, C).astype(np.float64)).sum(0).astype(F32)
+                           + (c * self.gamma).astype(F32)).astype(F32)
+            self.dbeta = g2.sum(0).astype(F32)
+            return (gf * self.gq_f).astype(F32)
         G, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         C = g.shape[-1]
         Gf = G.reshape(-1, C).astype(np.int64)
@@ -498,19 +651,73 @@ class BottleneckQ(ResidualBlockQ):
 
 
 class AvgPoolQ(LayerQ):
-    """8x8 VALID average pool over the whole map: sequential fp32 sum then * 2**-6."""
+    """``AvgPool_q`` (``:1009-1022``, tf.nn.avg_pool). Global (no ksize, or a VALID window equal to
+    the map -- the ResNets' 8x8 pool): sequential fp32 sum then * 1/(H*W). Any other window:
+    fp32 sum of the window's valid inputs in (kh, kw) order / count of valid positions (TF SAME
+    leaves the padding out of the mean); backward: each input adds g[o] / count[o] over the windows
+    holding it in ascending output order (TF AvgPoolGrad)."""
+
+    def __init__(self, ksize=None, strides=None, padding="VALID"):
+        self.ksize, self.strides, self.padding = ksize, strides, padding
+
+    def _global(self, H, W):
+        return self.ksize is None or (self.padding == "VALID" and self.ksize[1] == H and self.ksize[2] == W)
 
     def forward(self, X, ctx):
         N, H, W, C = X.shape
         self.shape = X.shape
+        if not self._global(H, W):
+            return self._forward_window(X)
         xs = X.reshape(N, H * W, C)
         acc = np.zeros((N, C), F32)
         for i in range(H * W):
             acc = (acc + xs[:, i, :]).astype(F32)
         return (acc * F32(1.0 / (H * W))).astype(F32).reshape(N, 1, 1, C)
 
+    def _geom(self, H, W):
+        kh, kw, sh, sw = self.ksize[1], self.ksize[2], self.strides[1], self.strides[2]
+        Ho, Wo, pt, _, pl, _ = conv_geometry(H, W, kh, kw, sh, sw, self.padding)
+        cnt = np.zeros((Ho, Wo), F32)
+        for oh in range(Ho):
+            for ow in range(Wo):
+                rh = sum(0 <= oh * sh + i - pt < H for i in range(kh))
+                rw = sum(0 <= ow * sw + j - pl < W for j in range(kw))
+                cnt[oh, ow] = rh * rw
+        return kh, kw, sh, sw, Ho, Wo, pt, pl, cnt
+
+    def _forward_window(self, X):
+        N, H, W, C = X.shape
+        kh, kw, sh, sw, Ho, Wo, pt, pl, cnt = self._geom(H, W)
+        acc = np.zeros((N, Ho, Wo, C), F32)
+        for i in range(kh):
+            for j in range(kw):
+                for oh in range(Ho):
+                    ih = oh * sh + i - pt
+                    if not 0 <= ih < H:
+                        continue
+                    for ow in range(Wo):
+                        iw = ow * sw + j - pl
+                        if 0 <= iw < W:
+                            acc[:, oh, ow, :] = (acc[:, oh, ow, :] + X[:, ih, iw, :]).astype(F32)
+        return (acc / cnt[None, :, :, None]).astype(F32)
+
     def backward(self, g, ctx):
         N, H, W, C = self.shape
+        if not self._global(H, W):
+            kh, kw, sh, sw, Ho, Wo, pt, pl, cnt = self._geom(H, W)
+            share = (g / cnt[None, :, :, None]).astype(F32)
+            dx = np.zeros(self.shape, F32)
+            for oh in range(Ho):
+                for ow in range(Wo):
+                    for i in range(kh):
+                        ih = oh * sh + i - pt
+                        if not 0 <= ih < H:
+                            continue
+                        for j in range(kw):
+                            iw = ow * sw + j - pl
+                            if 0 <= iw < W:
+                                dx[:, ih, iw, :] = (dx[:, ih, iw, :] + share[:, oh, ow, :]).astype(F32)
+            return dx
         return np.broadcast_to((g.reshape(N, 1, 1, C) * F32(1.0 / (H * W))).astype(F32), self.shape).copy()
 
 

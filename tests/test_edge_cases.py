@@ -1,0 +1,242 @@
+"""Reference edge cases beyond the timed ResNet-20 step (VERDICT r1 "missing" 3-7):
+
+* ``AvgPool_q`` with any window / stride / padding (``dynamic_fixed_point.py:1009-1022``);
+* ``Normalization_q`` in testing mode -- ``set_testing`` (``models.py:15``) switches every BatchNorm to
+  its running averages through ``tf.cond(self.train, ...)`` (``:590-612``);
+* the final partial batch of an epoch (``trainer.py:98`` ``.batch(batch_size)`` keeps it) and the test
+  loop (``trainer.py:166-190``) against the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nn as onn
+from oracle import resnet as oresnet
+
+DEV = "cuda"
+F32 = np.float32
+
+
+# ------------------------------------------------------------------------------ CPU (oracle pins)
+def test_oracle_avgpool_window_known_answer():
+    """3x3 / stride 2 / SAME on a 4x4 map of ones with one marked element: TF averages over the
+    valid positions only (corner windows hold 4, edge 6, inner 9 positions)."""
+    x = np.ones((1, 4, 4, 1), F32)
+    x[0, 1, 1, 0] = 10.0
+    p = onn.AvgPoolQ([1, 3, 3, 1], [1, 2, 2, 1], "SAME")
+    y = p.forward(x, None)
+    # TF SAME for 4 -> 2 with k3 s2: pad (0, 1); window of output (0, 0) = rows 0..2, cols 0..2 (9 valid)
+    assert y.shape == (1, 2, 2, 1)
+    assert y[0, 0, 0, 0] == F32((8 + 10) / F32(9))
+    assert y[0, 1, 1, 0] == 1.0  # rows 2..3, cols 2..3 valid: 4 ones / 4
+    assert y[0, 0, 1, 0] == 1.0  # rows 0..2, cols 2..3: 6 ones / 6
+    g = np.ones((1, 2, 2, 1), F32)
+    dx = p.backward(g, None)
+    # input (2, 2) sits in all four windows: 1/9 + 1/6 + 1/6 + 1/4, summed in output order
+    want = F32(F32(F32(F32(1 / F32(9)) + F32(1 / F32(6))) + F32(1 / F32(6))) + F32(1 / F32(4)))
+    assert dx[0, 2, 2, 0] == want
+    # global pool (no window) keeps the ResNet formula: sum * 1/(H*W)
+    gp = onn.AvgPoolQ()
+    assert gp.forward(x, None)[0, 0, 0, 0] == F32(F32(25.0) * F32(1 / 16))
+
+
+def test_oracle_testing_mode_bn_formula():
+    """Normalization_q testing mode: y = (Xq - running_mean) / sqrt(running_var + eps), dX = Gq / sigma."""
+    n = onn.NormQ("bn-norm", 8, 3)
+    n.mean_running = np.array([0.5, -0.25, 0.0], F32)
+    n.var_running = np.array([4.0, 0.25, 1.0], F32)
+    n.train = False
+    x = np.array([[[[1.0, 0.5, -1.0]]]], F32)
+    ctx = onn.Ctx({"bn-norm/X_range": 2, "bn-norm/grad_range": 2}, 0, 0)
+    y = n.forward(x, ctx)
+    sig = np.sqrt((n.var_running + F32(1e-5)).astype(F32)).astype(F32)
+    q = ctx.record["bn-norm/X_range"].astype(F32) * F32(2 ** -5)
+    assert np.array_equal(y[0, 0, 0], ((q[0, 0, 0] - n.mean_running).astype(F32) / sig).astype(F32))
+    assert np.array_equal(n.mean_running, [0.5, -0.25, 0.0])  # nothing moves
+    g = np.array([[[[0.5, -1.0, 0.25]]]], F32)
+    dx = n.backward(g, ctx)
+    G = ctx.record["bn-norm/grad_range"].astype(F32) * F32(2 ** -5)
+    assert np.array_equal(dx[0, 0, 0], (G[0, 0, 0] / sig).astype(F32))
+
+
+# ------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,k,s,pad", [((4, 9, 9, 8), 3, 2, "SAME"), ((3, 8, 8, 5), 2, 2, "VALID"),
+                                           ((2, 7, 6, 16), 3, 1, "SAME"), ((2, 11, 11, 3), 5, 3, "VALID"),
+                                           ((5, 8, 8, 64), 8, 1, "VALID")])
+def test_avgpool_any_window_matches_oracle(shape, k, s, pad):
+    from lbt_amd.dfxp.layers import AvgPool_q
+    rng = np.random.default_rng(sum(shape) + k)
+    x = rng.normal(size=shape).astype(F32)
+    layer = AvgPool_q([1, k, k, 1], [1, s, s, 1], pad)
+    ref = onn.AvgPoolQ([1, k, k, 1], [1, s, s, 1], pad)
+    y = layer.forward(torch.from_numpy(x).to(DEV))
+    yr = ref.forward(x, None)
+    assert np.array_equal(y.cpu().numpy(), yr)
+    g = rng.normal(size=yr.shape).astype(F32)
+    dx = layer.backward(torch.from_numpy(g).to(DEV))
+    assert np.array_equal(dx.cpu().numpy(), ref.backward(g, None))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8, 16, 16, 32), (16, 8, 8, 64)])
+def test_batchnorm_testing_mode_matches_oracle(shape):
+    """Two training-mode steps move the running averages; then in testing mode the forward uses them,
+    the backward is dX = Gq / sigma, and nothing moves -- all bit-identical to the oracle."""
+    from lbt_amd import dynamic_fixed_point as D
+    from lbt_amd.runtime import DfxpContext
+    rng = np.random.default_rng(shape[0])
+    C = shape[-1]
+    ctx = DfxpContext(seed=8)
+    gbn = D.BatchNorm_q("bn", 8, C, weight_decay=2e-4, ctx=ctx)
+    obn = onn.BatchNormQ("bn", 8, C, 2e-4)
+    ranges = {r: 2 for r in obn.range_names()}
+    for step in range(3):
+        testing = step == 2
+        gbn.layers[0].train = not testing
+        obn.layers[0].train = not testing
+        x = (rng.standard_normal(shape) * 1.3 + 0.4).astype(F32)
+        g = (rng.standard_normal(shape) * 0.03).astype(F32)
+        octx = onn.Ctx(dict(ranges), step, 8)
+        assert ctx.ranges() == ranges
+        y = gbn.forward(torch.from_numpy(x).to(DEV))
+        assert np.array_equal(y.cpu().numpy(), obn.forward(x, octx)), step
+        dx = gbn.backward(torch.from_numpy(g).to(DEV))
+        assert np.array_equal(dx.cpu().numpy(), obn.backward(g, octx)), step
+        n = gbn.layers[0]
+        assert np.array_equal(n.X_mean_running.cpu().numpy(), obn.layers[0].mean_running), step
+        assert np.array_equal(n.X_var_running.cpu().numpy(), obn.layers[0].var_running), step
+        ctx.update_range_op()
+        ranges = octx.new_ranges()
+        assert ctx.ranges() == ranges
+
+
+@pytest.mark.gpu
+def test_model_set_testing_forward_matches_oracle():
+    """Model.set_testing on the layer-wise ResNet-20 after two training steps: logits bit-exact
+    against the oracle with every NormQ in testing mode and the same running averages."""
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.runtime import DfxpContext
+    from lbt_amd.trainer import Trainer
+    ctx = DfxpContext(seed=9)
+    gm = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+    tr = Trainer(gm, lr=1e-2, momentum=0.9, batch_size=16, use_graph=False)
+    rng = np.random.default_rng(9)
+    for _ in range(2):
+        x = ((rng.integers(0, 256, size=(16, 32, 32, 3)) - 127.5) / 128).astype(F32)
+        tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(rng.integers(0, 10, 16).astype(np.int32)).to(DEV))
+    gm.set_testing()
+    om = oresnet.build_resnet((3, 3, 3), 8, 2e-4)
+    params = {}
+    for owner, var, _ in gm.param_slots():
+        params[owner.name + {"W": "/W", "gamma": "/g", "beta": "/b"}[var]] = getattr(owner, var).cpu().numpy()
+    oresnet.set_params(om, params)
+    gn = gm._norm_layers()
+    on = [l for l in oresnet._walk(om) if isinstance(l, onn.NormQ)]
+    for g_, o in zip(gn, on):
+        o.mean_running = g_.X_mean_running.cpu().numpy().copy()
+        o.var_running = g_.X_var_running.cpu().numpy().copy()
+        o.train = False
+    x = ((rng.integers(0, 256, size=(8, 32, 32, 3)) - 127.5) / 128).astype(F32)
+    logits = gm.forward(torch.from_numpy(x).to(DEV))
+    octx = onn.Ctx(ctx.ranges(), int(ctx.step.item()), 9)
+    assert np.array_equal(logits.cpu().numpy(), om.forward(x, octx))
+    for g_, o in zip(gn, on):  # testing mode moves nothing
+        assert np.array_equal(g_.X_mean_running.cpu().numpy(), o.mean_running)
+    gm.set_training()
+    assert all(n.train for n in gm._norm_layers())
+
+
+def _fused_trainer(seed, B):
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.runtime import DfxpContext
+    from lbt_amd.trainer import Trainer
+    ctx = DfxpContext(seed=seed)
+    gm = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+    return ctx, gm, Trainer(FusedResNet(gm), lr=1e-2, momentum=0.9, batch_size=B, use_graph=True)
+
+
+def _params_of(gm):
+    return {o.name + {"W": "/W", "gamma": "/g", "beta": "/b"}[v]: getattr(o, v).cpu().numpy().copy()
+            for o, v, _ in gm.param_slots()}
+
+
+@pytest.mark.gpu
+def test_partial_final_batch_steps_match_oracle():
+    """An epoch of 40 images at batch 16 ends with a batch of 8 (trainer.py:98 keeps it): the fused
+    trainer runs it on a second plan over the same parameters and quantisers (graph-captured), and
+    all three steps -- 16, 16, 8 -- are bit-identical to the oracle's (dz injected; loss 1e-5),
+    including the overflow-rate denominators of the short batch."""
+    ctx, gm, tr = _fused_trainer(21, 16)
+    om = oresnet.build_resnet((3, 3, 3), 8, 2e-4)
+    p = _params_of(gm)
+    state = dict(params=p, accum={k: np.zeros_like(v) for k, v in p.items()}, ranges=oresnet.init_ranges(om), step=0)
+    rng = np.random.default_rng(21)
+    X = ((rng.integers(0, 256, size=(40, 32, 32, 3)) - 127.5) / 128).astype(F32)
+    Y = rng.integers(0, 10, size=40).astype(np.int32)
+    xs = [torch.from_numpy(X[b:b + 16]).to(DEV) for b in range(0, 40, 16)]
+    ys = [torch.from_numpy(Y[b:b + 16]).to(DEV) for b in range(0, 40, 16)]
+    for epoch in range(2):  # the second epoch replays both plans' graphs
+        for i, (x, y) in enumerate(zip(xs, ys)):
+            loss = tr.step(x, y).item()
+            torch.cuda.synchronize()
+            dz = tr._active.dlogits.cpu().numpy()
+            lref, state, _ = oresnet.train_step(om, state, x.cpu().numpy(), y.cpu().numpy(), seed=21, dz=dz)
+            assert abs(loss - lref) <= 1e-5 * abs(lref), (epoch, i)
+            gp = _params_of(gm)
+            for k in gp:
+                assert np.array_equal(gp[k], state["params"][k]), (epoch, i, k)
+            assert ctx.ranges() == state["ranges"], (epoch, i)
+
+
+@pytest.mark.gpu
+def test_train_epoch_keeps_partial_batch():
+    ctx, gm, tr = _fused_trainer(22, 16)
+    rng = np.random.default_rng(22)
+    X = ((rng.integers(0, 256, size=(40, 32, 32, 3)) - 127.5) / 128).astype(F32)
+    Y = rng.integers(0, 10, size=40).astype(np.int32)
+    tr.dataset = ((X, Y), (X[:0], Y[:0]))
+    tr.n_epoch = 1
+    tr.train(augment=True)
+    assert tr.batch_sizes == [16, 16, 8] and tr.global_step == 3 and int(ctx.step.item()) == 3
+
+
+@pytest.mark.gpu
+def test_evaluate_matches_oracle_test_loop():
+    """Trainer.evaluate == the reference test loop (trainer.py:166-190) on the oracle: per batch the
+    training-mode forward (batch-statistic BN and stochastic quantisers at the current exponents and
+    noise step, as the reference runs it, :164-165), accuracy exact, loss at 1e-5; the BN running
+    averages move as the reference's control dependencies move them (:601-614); the overflow
+    counters and the training state are left as they were."""
+    ctx, gm, tr = _fused_trainer(23, 16)
+    rng = np.random.default_rng(23)
+    for _ in range(2):
+        x = ((rng.integers(0, 256, size=(16, 32, 32, 3)) - 127.5) / 128).astype(F32)
+        tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(rng.integers(0, 10, 16).astype(np.int32)).to(DEV))
+    torch.cuda.synchronize()
+    om = oresnet.build_resnet((3, 3, 3), 8, 2e-4)
+    oresnet.set_params(om, _params_of(gm))
+    on = [l for l in oresnet._walk(om) if isinstance(l, onn.NormQ)]
+    gn = gm._norm_layers()
+    for g_, o in zip(gn, on):
+        o.mean_running = g_.X_mean_running.cpu().numpy().copy()
+        o.var_running = g_.X_var_running.cpu().numpy().copy()
+    Xte = ((rng.integers(0, 256, size=(50, 32, 32, 3)) - 127.5) / 128).astype(F32)
+    Yte = rng.integers(0, 10, size=50).astype(np.int32)
+    ranges, step = ctx.ranges(), int(ctx.step.item())
+    counts = ctx.counts.clone()
+    acc, loss = tr.evaluate(Xte, Yte, batch_size=20)  # 20, 20, 10
+    accs, losses = [], []
+    for b in range(0, 50, 20):
+        octx = onn.Ctx(dict(ranges), step, 23)
+        z = om.forward(Xte[b:b + 20], octx)
+        l, _ = onn.softmax_xent(z, Yte[b:b + 20])
+        accs.append(float(np.mean((np.argmax(z, 1) == Yte[b:b + 20]).astype(np.float32))))
+        losses.append(l)
+    assert acc == pytest.approx(sum(accs) / 3, abs=1e-7)
+    assert abs(loss - sum(losses) / 3) <= 1e-5 * abs(sum(losses) / 3)
+    for g_, o in zip(gn, on):
+        assert np.array_equal(g_.X_mean_running.cpu().numpy(), o.mean_running)
+        assert np.array_equal(g_.X_var_running.cpu().numpy(), o.var_running)
+    assert torch.equal(counts, ctx.counts) and ctx.ranges() == ranges

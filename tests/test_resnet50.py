@@ -370,3 +370,61 @@ def test_resnet50_fused_conv_quant_epilogue_bitexact(monkeypatch):
     the fused bottleneck bit-exact against the oracle."""
     monkeypatch.setenv("LBT_FUSE_CONV_QUANT", "1")
     test_resnet50_layers_bitexact_vs_oracle((1, 1, 1, 1), 64, 32, 16, 16)
+
+
+@pytest.mark.gpu
+def test_side_stream_schedule_bitidentical_under_graph_capture():
+    """The backward's weight / BN-parameter gradients on a side stream (layers.SIDE_STREAM) at a size
+    where the two streams really overlap (width 64, 16-bit gradients: every bottleneck fused; batch 16
+    at 96x96), three graph-captured Trainer steps: gradients, weights and exponents are bit-identical
+    to the one-stream schedule (a missing cross-stream dependency would show up here)."""
+    from lbt_amd.dfxp import layers
+    from lbt_amd.models import ImageNet_Resnet
+    from lbt_amd.runtime import DfxpContext
+    from lbt_amd.trainer import Trainer
+    xs = [_batch(16, 96, 16, seed=10 + i) for i in range(3)]
+    out = []
+    saved = layers.SIDE_STREAM
+    try:
+        for side in (True, False):
+            layers.SIDE_STREAM = side
+            ctx = DfxpContext(seed=4)
+            m = ImageNet_Resnet(8, (2, 1, 1, 1), grad_bits=16, width=64, classes=16, image=96, ctx=ctx)
+            t = Trainer(m, lr=0.01, momentum=0.9, use_graph=True)
+            for x, y in xs:
+                t.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+            torch.cuda.synchronize()
+            out.append((t.flat.g.cpu().clone(), t.flat.w.cpu().clone(), ctx.exps.cpu().clone()))
+    finally:
+        layers.SIDE_STREAM = saved
+    (ga, wa, ea), (gb, wb, eb) = out
+    assert torch.equal(ga, gb) and torch.equal(wa, wb) and torch.equal(ea, eb)
+
+
+@pytest.mark.gpu
+def test_bottleneck_backward_called_directly_joins_side_stream():
+    """The Layer_q contract: a fused bottleneck's backward called on its own (not inside
+    Model.backward) returns with its dW / dgamma / dbeta finished on the caller's stream."""
+    from lbt_amd.dfxp import layers
+    from lbt_amd.runtime import DfxpContext
+    ctx = DfxpContext(seed=6)
+    blk = layers.ResidualBottleneck_q("blk", 8, 256, 64, 1, grad_bits=16, weight_decay=1e-4, ctx=ctx)
+    assert blk._fusable()
+    rng = np.random.default_rng(6)
+    x = torch.from_numpy(np.maximum(rng.normal(size=(8, 28, 28, 256)), 0).astype(F32)).to(DEV)
+    g = torch.from_numpy((rng.normal(size=(8, 28, 28, 256)) * 1e-3).astype(F32)).to(DEV)
+    saved = layers.SIDE_STREAM
+    res = []
+    try:
+        for side in (True, False):
+            layers.SIDE_STREAM = side
+            blk.forward(x)
+            blk.backward(g)
+            # read on the caller's stream with no synchronisation of our own
+            c1 = blk.residual.layers[0]
+            res.append((c1.dW.clone(), blk.residual.layers[1].layers[1].dgamma.clone()))
+            torch.cuda.synchronize()
+            ctx.counts.zero_()
+    finally:
+        layers.SIDE_STREAM = saved
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
