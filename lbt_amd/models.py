@@ -163,10 +163,13 @@ class Model:
 
 class CIFAR10_Resnet(Model):
     def __init__(self, bits, num_blocks, block, dropout=0.5, weight_decay=0, stochastic=False, ctx=None,
-                 weight_bits=None):
+                 weight_bits=None, grad_range=2):
         self.num_blocks = num_blocks
         self.block = block
         self.weight_bits = weight_bits  # config 5: 4-bit weights, 8-bit activations / gradients
+        # the initial value of every layer's grad_range variable (the layers' own constructor argument,
+        # dynamic_fixed_point.py:225,321,541,628; the reference builder leaves it at its default 2)
+        self.grad_range = grad_range
         super().__init__(bits, [None, 32, 32, 3], dropout, weight_decay, stochastic, ctx)
 
     def _build_blocks(self, channels, num_blocks, stride):
@@ -174,7 +177,8 @@ class CIFAR10_Resnet(Model):
         for i in range(1, 1 + num_blocks):
             blocks.append(self.block(name="block%d-%d" % (channels, i), bits=self.bits, in_channels=self.channels,
                                      channels=channels, stride=1 if i > 1 else stride, training=self.training,
-                                     weight_decay=self.weight_decay, weight_bits=self.weight_bits, ctx=self.ctx))
+                                     weight_decay=self.weight_decay, weight_bits=self.weight_bits,
+                                     grad_range=self.grad_range, ctx=self.ctx))
             self.channels = channels * self.block.expansion
         return blocks
 
@@ -182,9 +186,10 @@ class CIFAR10_Resnet(Model):
         self.channels = 16
         return [
             L.Conv2d_pq(name="conv1", bits=self.bits, ksize=[3, 3, 3, 16], strides=[1, 1, 1, 1], padding="SAME",
-                        use_bias=False, weight_decay=self.weight_decay, weight_bits=self.weight_bits, ctx=self.ctx),
+                        use_bias=False, weight_decay=self.weight_decay, weight_bits=self.weight_bits,
+                        grad_range=self.grad_range, ctx=self.ctx),
             L.BatchNorm_q(name="conv1-bn", bits=self.bits, num_features=16, training=self.training,
-                          weight_decay=self.weight_decay, ctx=self.ctx),
+                          weight_decay=self.weight_decay, grad_range=self.grad_range, ctx=self.ctx),
             L.ReLU_q(),
         ] + self._build_blocks(16, self.num_blocks[0], 1) \
           + self._build_blocks(32, self.num_blocks[1], 2) \
@@ -193,12 +198,14 @@ class CIFAR10_Resnet(Model):
             L.AvgPool_q(ksize=[1, 8, 8, 1], strides=[1, 1, 1, 1], padding="VALID"),
             L.Flatten_q(64),
             L.Dense_q(name="softmax", bits=self.bits, in_units=64, units=10, use_bias=False,
-                      weight_decay=self.weight_decay, weight_bits=self.weight_bits, ctx=self.ctx),
+                      weight_decay=self.weight_decay, weight_bits=self.weight_bits, grad_range=self.grad_range,
+                      ctx=self.ctx),
         ]
 
 
-def CIFAR10_Resnet20(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None, weight_bits=None):
-    return CIFAR10_Resnet(bits, [3, 3, 3], L.ResidualBlock_q, dropout, weight_decay, stochastic, ctx, weight_bits)
+def CIFAR10_Resnet20(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None, weight_bits=None, grad_range=2):
+    return CIFAR10_Resnet(bits, [3, 3, 3], L.ResidualBlock_q, dropout, weight_decay, stochastic, ctx, weight_bits,
+                          grad_range)
 
 
 def CIFAR10_Resnet32(bits, dropout=0.5, weight_decay=0, stochastic=False, ctx=None):
