@@ -367,6 +367,38 @@ typedef struct lbt_chain_bwd_b {
 } lbt_chain_bwd_b;
 int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream);
 
+/* The weight gradient of one conv (the arguments of lbt_conv_wgrad_i8), as a job another launch
+ * carries out; slab == NULL: no job.                                                        */
+typedef struct lbt_wgrad_job {
+  const int8_t* xq; int32_t x_u8off; const int8_t* gq; lbt_conv_desc d;
+  int32_t* slab; int32_t nsplit, nshard;
+} lbt_wgrad_job;
+
+/* One stride-1 3x3 Conv2d_q's backward in ONE launch, with the BN backward passes on either side
+ * (Conv2d_q.backward dynamic_fixed_point.py:299-305 between Normalization_q.backward :620-623 of
+ * the BN it feeds and the BN it consumes):
+ *   gq = pass B of the BN AFTER the conv (b, exactly lbt_bn_chain_bwd_b; b.gq is required and
+ *        stored -- it is this conv's weight-gradient operand -- b.dx must be NULL)
+ *   dx = dgrad(gq, wd)  (as lbt_conv_dgrad_i8 with qg = b.qo, qw; never stored)
+ *   pass A of the BN BEFORE the conv on g = dx (+ add_src)  (a, as lbt_conv_dgrad_chain_i8)
+ * plus, in the same grid, the weight-gradient workgroups of job w (typically the deferred wgrad of
+ * the previous such launch, whose gq is complete when this launch starts).
+ * Each dgrad workgroup owns 4 image rows and recomputes pass B over its rows plus a one-pixel
+ * halo into LDS (no inter-workgroup exchange); gq, its channel sums and its overflow counters are
+ * produced by the owning workgroup only. Every output is bit-identical to lbt_bn_chain_bwd_b,
+ * lbt_conv_dgrad_chain_i8 (and lbt_conv_wgrad_i8 for w) run one after another.
+ * Shapes: KH = KW = 3, strides 1, pads 1, Cin = Cout = C in {16, 32, 64}, H % 4 == 0,
+ * (W + 2) * C <= 704 and W * C <= 512 (CIFAR ResNet stages); chains as lbt_conv_dgrad_chain_i8;
+ * w4 != 0: wd is the packed 4-bit image (lbt_conv_dgrad_i8w4). Else LBT_EINVAL.              */
+typedef struct lbt_conv_bwd {
+  lbt_chain_bwd_b b;
+  const int8_t* wd; int32_t ksd; int32_t w4; lbt_conv_desc d; lbt_qdesc qw;
+  const float* add_src;
+  lbt_chain_bwd_a a;
+  lbt_wgrad_job w;
+} lbt_conv_bwd;
+int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* p, void* stream);
+
 /* BN backward passes A and B for 9..16-bit gradient quantisers (config 4): the arithmetic of
  * lbt_bn_chain_bwd_a / _b (one branch, no mask) with int16 grad codes and int64 channel sums.
  * Rows here are pixels: g / R / qn / gout / dout / dx are [rows][C]; inner = the per-sample

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -74,6 +74,16 @@ class ChainBwdB(ctypes.Structure):
                 ("sums", c_void_p), ("n", c_int64),
                 ("dx", c_void_p), ("gq", c_void_p), ("qo", QDesc), ("gcolsum", c_void_p),
                 ("rows", c_int64), ("inner", c_int64), ("C", c_int32)]
+
+
+class WgradJob(ctypes.Structure):
+    _fields_ = [("xq", c_void_p), ("x_u8off", c_int32), ("gq", c_void_p), ("d", ConvDesc), ("slab", c_void_p),
+                ("nsplit", c_int32), ("nshard", c_int32)]
+
+
+class ConvBwd(ctypes.Structure):
+    _fields_ = [("b", ChainBwdB), ("wd", c_void_p), ("ksd", c_int32), ("w4", c_int32), ("d", ConvDesc),
+                ("qw", QDesc), ("add_src", c_void_p), ("a", ChainBwdA), ("w", WgradJob)]
 
 
 class WJob(ctypes.Structure):
@@ -176,6 +186,7 @@ _SIGS = {
     "lbt_bn_chain_fwd": [_P, _P],
     "lbt_bn_chain_bwd_a": [_P, _P],
     "lbt_bn_chain_bwd_b": [_P, _P],
+    "lbt_conv_bwd_fused_i8": [_P, _P],
     "lbt_bn_bwd_a_wide": [_P, QDesc, _P, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64, c_int32, _P],
     "lbt_bn_bwd_b_wide": [_P, QDesc, _P, QDesc, _P, _P, c_int64, _P, c_int64, c_int32, _P],
     "lbt_bn_param_grads": [_P, c_int32, QDesc, QDesc, _P, c_float, _P, _P, _P],

@@ -280,8 +280,17 @@ struct WgradArgs {
   int nsplit, nshard;
 };
 
-template <int CSI>
-__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bid) {
+// LDS of one wgrad workgroup: per wave an X image [CSI][64 px][16 B] and a G image [64 px][16 B],
+// then the per-wave partials [4][CI][16]
+template <int CSI, int NW = 4>
+struct WgradShared {
+  int8_t lds[NW][(CSI + 1) * kWP * 16];
+  int red[NW][CSI * 16 * 16];
+};
+
+// NW waves per workgroup (4 in the wgrad / dgrad_wgrad kernels, 8 in conv_bwd_kernel)
+template <int CSI, int NW = 4>
+__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bid, WgradShared<CSI, NW>& sm) {
   const int8_t* __restrict__ xq = wa.xq;
   const int8_t* __restrict__ gq = wa.gq;
   const lbt_conv_desc& d = wa.d;
@@ -289,9 +298,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bi
   int32_t* __restrict__ slab = wa.slab;
   const int64_t P = wa.P;
   constexpr int CI = CSI * 16;
-  // per wave: X image [CSI][64 px][16 B] and G image [64 px][16 B]
-  __shared__ __attribute__((aligned(16))) int8_t lds[4][(CSI + 1) * kWP * 16];
-  __shared__ int red[4][CI * 16];
+  auto& lds = sm.lds;
+  auto& red = sm.red;
   LBT_TS(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kg = lane >> 4;
@@ -317,8 +325,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bi
 #pragma unroll
   for (int a = 0; a < CSI; ++a) acc[a] = v4i{0, 0, 0, 0};
 
-  // chunks are interleaved across the 4 waves of the block
-  for (int64_t c0 = p0 + (int64_t)wave * kWP; c0 < p1; c0 += 4 * kWP) {
+  // chunks are interleaved across the NW waves of the block
+  for (int64_t c0 = p0 + (int64_t)wave * kWP; c0 < p1; c0 += NW * kWP) {
     const int64_t p = c0 + lane;
     const bool pv = p < p1;
     const uint32_t pu = (uint32_t)(pv ? p : p0);  // P < 2^31 (launcher)
@@ -363,9 +371,11 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bi
   __syncthreads();
   LBT_TS(2);
   int32_t* dst = slab + ((int64_t)(split % nshard) * (d.KH * d.KW) + tap) * CI * d.Cout + cso * 16;
-  for (int i = threadIdx.x; i < CI * 16; i += kThreads) {
+  for (int i = threadIdx.x; i < CI * 16; i += NW * 64) {
     const int ci = i >> 4, co = i & 15;
-    const int v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    int v = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][i];
     if (v) LBT_GADD(&dst[(int64_t)ci * d.Cout + co], v);  // integer atomics: exact, order-independent
   }
   LBT_TS(3);
@@ -373,7 +383,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bi
 
 template <int CSI>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs wa) {
-  conv_wgrad_body<CSI>(wa, blockIdx.x);
+  __shared__ __attribute__((aligned(16))) WgradShared<CSI> sm;
+  conv_wgrad_body<CSI>(wa, blockIdx.x, sm);
 }
 
 // Horizontal fusion of one conv's two backward GEMMs, which read the same gradient codes and
@@ -383,9 +394,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs wa) {
 template <int CS, int NT, int CF, int NB, bool W4>
 __global__ __launch_bounds__(kThreads, (CS == 1 && NB == 1) ? 8 : 1) void dgrad_wgrad_kernel(GemmArgs p, WgradArgs wa,
                                                                                           uint32_t nwg) {
-  if (blockIdx.x < nwg)
-    conv_wgrad_body<NT>(wa, blockIdx.x);
-  else
+  if (blockIdx.x < nwg) {
+    __shared__ __attribute__((aligned(16))) WgradShared<NT> sm;
+    conv_wgrad_body<NT>(wa, blockIdx.x, sm);
+  } else
     conv_gemm_body<MODE_DGRAD, CS, NT, CF, NB, W4>(p, blockIdx.x - nwg);
 }
 
@@ -665,4 +677,459 @@ extern "C" int lbt_diag_occupancy(int32_t* out, int32_t n) {
     out[i] = b;
   }
   return 0;
+}
+
+// ============================================================================ fused conv backward
+// lbt_conv_bwd_fused_i8: one stride-1 3x3 conv's backward with both neighbouring BN passes in ONE
+// launch. A dgrad workgroup owns kBTH image rows of one sample:
+//   phase 1  pass B of the BN after the conv (bn.hip chain_bwd_b_kernel's arithmetic) over the rows
+//            plus a one-pixel halo -> int8 gq codes in LDS; owned pixels also store gq (the weight
+//            gradient's operand), count overflows and add the gq channel sums
+//   phase 2  dgrad on v_mfma_i32_16x16x64_i8 with every A fragment a 16-byte ds_read of the LDS
+//            gq image (the 9 taps never go back to memory) -> fp32 tile in LDS
+//   phase 3  pass A of the BN before the conv (chain_bwd_a_kernel's arithmetic) over the tile, one
+//            channel quad per thread with vector loads / stores
+// Workgroups [0, nwg) run a weight-gradient job instead (conv_wgrad_body): the deferred wgrad of the
+// conv of the previous launch.
+namespace {
+
+constexpr int kBTH = 4;    // image rows per dgrad workgroup
+constexpr int kBNW = 8;    // waves per workgroup
+constexpr int kBThreads = kBNW * 64;
+constexpr int kBIt = 2;    // phase-1 groups per thread (host: (kBTH+2)(W+2)C/4 <= 1024)
+
+struct ConvBwdArgs {
+  lbt_chain_bwd_b b;
+  const int8_t* wd;
+  int ks, nslices, w4;
+  lbt_qdesc qw;
+  int H, W;
+  const float* add_src;
+  lbt_chain_bwd_a a;
+};
+
+template <int C>
+struct BwdShared {
+  int8_t gq[(kBTH + 2) * (512 / C + 2) * C];   // halo image [(kBTH+2)][(W+2)][C], W*C == 512
+  float tile[kBTH * (512 / C) * (C + 4)];       // dgrad outputs [kBTH*W][C+4] (padded rows)
+  float pb[2 * C];                               // pass-B constants mg, mgx per channel
+  int part[kBNW][(2 * 4 + 2) * C];               // per wave: pass-A sums per branch, gq sums
+  int cnt[kBNW * 2 * 5];                         // counters: 5 quantisers x waves
+};
+
+LBT_DEV int ld4i8(const int8_t* p, int64_t i) { return *reinterpret_cast<const int*>(p + i); }
+LBT_DEV void unpack4(int w, int v[4]) {
+  v[0] = (int8_t)(w & 0xff); v[1] = (int8_t)((w >> 8) & 0xff);
+  v[2] = (int8_t)((w >> 16) & 0xff); v[3] = (int8_t)(w >> 24);
+}
+LBT_DEV int pack4(const int c[4]) {
+  return (int)((uint32_t)(c[0] & 0xff) | ((uint32_t)(c[1] & 0xff) << 8) | ((uint32_t)(c[2] & 0xff) << 16) |
+               ((uint32_t)c[3] << 24));
+}
+LBT_DEV float4 ld4f(const float* p, int64_t i) { return *reinterpret_cast<const float4*>(p + i); }
+
+// Wave total of the lanes holding the same channel quad (lanes l, l + C4, l + 2*C4, ...): DPP
+// rotations inside each 16-lane row, then the rows paired by a lane shuffle (xor 16) and the halves
+// by v_permlane32_swap (its two results are the lane's own half and the other half, both ways:
+// their sum is the pair total in every lane). The total lands in every lane.
+template <int C4>
+LBT_DEV int chan_reduce(int v) {
+  if constexpr (C4 <= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  if constexpr (C4 <= 4) v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += __shfl_xor(v, 16, 64);
+  const auto h = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (int)h[0] + (int)h[1];
+}
+
+// quant_w<1> (stochastic) whose overflow predicates count only where `cnt` (halo lanes compute
+// the same codes as the owning workgroup but must not count them twice)
+LBT_DEV int quant_sc(const QState& s, float x, float u, bool cnt, int& ov1w, int& ov2w) {
+  const float xm = x * s.m;
+  ov1w += __popcll(__ballot(cnt && ((xm >= s.L) | (xm < -s.L))));
+  ov2w += __popcll(__ballot(cnt && ((xm >= s.Lh) | (xm < -s.Lh))));
+  float v = xm + u;
+  v = fminf(fmaxf(v, -s.L), s.Lm1);
+  return (int)floorf(v);
+}
+
+template <int CS, int CF, int NB, bool W4, int WCS>
+__global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(ConvBwdArgs p, WgradArgs wa, uint32_t nwg) {
+  constexpr int C = CS * 16, C4 = C / 4, NT = CS;
+  constexpr int kMaxKS = (9 * CS + 3) / 4;
+  constexpr int WC = WCS ? WCS : 1;
+  union Smem {
+    BwdShared<C> b;
+    WgradShared<WC, kBNW> w;
+  };
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  if (WCS != 0 && blockIdx.x < nwg) {
+    conv_wgrad_body<WC, kBNW>(wa, blockIdx.x, sm.w);
+    return;
+  }
+  BwdShared<C>& sh = sm.b;
+  LBT_TS(0);
+  const lbt_chain_bwd_b& B = p.b;
+  const lbt_chain_bwd_a& A = p.a;
+  const uint32_t bid = blockIdx.x - nwg;
+  constexpr int W = 512 / C, Wp = W + 2;  // W * C == 512 (host check)
+  const int H = p.H;
+  const int tpi = H / kBTH;
+  const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * kBTH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int cq = (tid % C4) * 4;  // this thread's channel quad (512 % C4 == 0: fixed over its groups)
+  const int64_t img = (int64_t)n * H * W * C;
+
+  // ---------------- every load that does not depend on the sums goes out first
+  // phase-1 operands: G / q codes and the output quantiser's noise over the halo rows
+  const int ngrp = (kBTH + 2) * Wp * C4;
+  int Gv[kBIt], Qv[kBIt];
+  float4 Uv[kBIt];
+#pragma unroll
+  for (int it = 0; it < kBIt; ++it) {
+    const int g = tid + it * kBThreads;
+    const int pix = g / C4, hy = pix / Wp, hx = pix - hy * Wp;
+    const int y = row0 - 1 + hy, x = hx - 1;
+    const bool in = g < ngrp && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const uint32_t off = in ? (uint32_t)((y * W + x) * C + cq) : 0u;
+    Gv[it] = ld4i8(B.G, img + off);
+    Qv[it] = ld4i8(B.qn_codes, img + off);
+    Uv[it] = ld4f(B.qo.noise, off);
+  }
+  // phase-2 B operands (dgrad weights) of this wave's (m-tile, n-tile) pair (pair = wave, the 8
+  // pairs of a 4-row tile: W*C == 512); ks == 4 * kMaxKS (host check)
+  v4i bf[kMaxKS];
+  {
+    const int col = (wave % NT) * 16 + r;
+#pragma unroll
+    for (int kk = 0; kk < kMaxKS; ++kk) {
+      if constexpr (W4)
+        bf[kk] = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wd + ((int64_t)col * (4 * kMaxKS) + kk * 4 + kg) * 8));
+      else
+        bf[kk] = *reinterpret_cast<const v4i*>(p.wd + ((int64_t)col * (4 * kMaxKS) + kk * 4 + kg) * 16);
+    }
+  }
+  constexpr int J = 1;  // phase-3 groups per thread (kBTH*W*C/4 == 512 == kBThreads)
+  float mu[4], sg[4], gam[2][4], bet[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    mu[k] = B.ms[cq + k];
+    sg[k] = B.ms[C + cq + k];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) gam[b][k] = (b == 0 ? A.b1 : A.b2).gb[cq + k];
+    bet[k] = A.b1.gb[C + cq + k];
+  }
+  const QState sgq = qstate(B.qng), sn = qstate(B.qn), so = qstate(B.qo);
+  QState qrg[2], qng[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    qrg[b] = qstate((b == 0 ? A.b1 : A.b2).qrg);
+    qng[b] = qstate((b == 0 ? A.b1 : A.b2).qng);
+  }
+  const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
+  const float scale = ldexpf(1.0f, -(frac_exp(B.qo) + frac_exp(p.qw)));
+
+  // ---------------- pass-B statistics (SG, SGQ of every shard), LDS sums cleared
+  // pass-B constants of channel c (threads c < C): SG, SGQ summed over the shards, then in double
+  // exactly as chain_bwd_b_kernel
+  if (tid < C) {
+    long long v[2][LBT_NSHARD];
+#pragma unroll
+    for (int k = 0; k < LBT_NSHARD; ++k) {
+      v[0][k] = B.sums[(int64_t)k * 4 * C + 2 * C + tid];
+      v[1][k] = B.sums[(int64_t)k * 4 * C + 3 * C + tid];
+    }
+    long long SGi = 0, SGQi = 0;
+#pragma unroll
+    for (int k = 0; k < LBT_NSHARD; ++k) {
+      SGi += v[0][k];
+      SGQi += v[1][k];
+    }
+    const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, nn = (double)B.n;
+    const double SG = (double)SGi, SGQ = (double)SGQi;
+    const float m = B.ms[tid], sig = B.ms[C + tid];
+    sh.pb[tid] = (float)(gsc * SG / nn);
+    sh.pb[C + tid] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
+  }
+  __syncthreads();
+  LBT_TS(1);
+  float rmg[4], rmgx[4];
+  Recip rsg[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rmg[k] = sh.pb[cq + k];
+    rmgx[k] = sh.pb[C + cq + k];
+    rsg[k] = recip(sg[k]);
+  }
+
+  // ---------------- phase 1: pass B over the rows + halo -> LDS gq image
+  int ovq1 = 0, ovq2 = 0;
+  int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int it = 0; it < kBIt; ++it) {
+    if (it * kBThreads >= ngrp) break;  // uniform
+    const int g = tid + it * kBThreads;
+    const int pix = g / C4, hy = pix / Wp, hx = pix - hy * Wp;
+    const int y = row0 - 1 + hy, x = hx - 1;
+    const bool valid = g < ngrp;
+    const bool in = valid && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const bool own = in && hy >= 1 && hy <= kBTH;
+    int G[4], q[4], c[4];
+    unpack4(Gv[it], G);
+    unpack4(Qv[it], q);
+    const float u[4] = {Uv[it].x, Uv[it].y, Uv[it].z, Uv[it].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x1 = (float)q[k] * sn.inv_m;
+      const float x2 = x1 - mu[k];
+      const float xh = div_by(x2, rsg[k]);
+      const float gh = (float)G[k] * sgq.inv_m;
+      const float t1 = gh - rmg[k];
+      const float t2 = xh * rmgx[k];
+      const float dx = div_by(t1 - t2, rsg[k]);
+      c[k] = quant_sc(so, dx, u[k], own, ovq1, ovq2);
+      if (!in) c[k] = 0;  // the conv's zero padding
+    }
+    if (valid) *reinterpret_cast<int*>(sh.gq + pix * C + cq) = pack4(c);
+    if (own) {
+      *reinterpret_cast<int*>(B.gq + img + (uint32_t)((y * W + x) * C + cq)) = pack4(c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s1[k] += c[k];
+        s2[k] += c[k] * c[k];
+      }
+    }
+  }
+  __syncthreads();
+  LBT_TS(2);
+
+  // phase-3 operands (addend, mask source, R / qn codes and both quantisers' noise per branch),
+  // issued now: they land while the MFMAs run, and phase 1's registers are free
+  float4 av[J], ymv[J], urg[NB][J], ung[NB][J];
+  int Rv[NB][J], qnv[NB][J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pix = (tid + j * kBThreads) / C4;
+    const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);  // tile rows are consecutive pixels
+    av[j] = p.add_src ? ld4f(p.add_src, img + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (CF & kAYMask) ymv[j] = ld4f(A.y_mask, img + off);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+      Rv[b][j] = ld4i8(Bb.R, img + off);
+      qnv[b][j] = ld4i8(Bb.qn_codes, img + off);
+      urg[b][j] = ld4f(Bb.qrg.noise, off);
+      ung[b][j] = ld4f(Bb.qng.noise, off);
+    }
+  }
+
+  // ---------------- phase 2: dgrad from the LDS image, two (m-tile, n-tile) pairs per wave
+  {
+    const int pr = wave;
+    const int mt = pr / NT, nt = pr - mt * NT;
+    const int m = mt * 16 + r;
+    const int ly = m / W, px = m - ly * W;
+    const int8_t* base = sh.gq + ((ly + 2) * Wp + px + 2) * C;
+    v4i acc = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < kMaxKS; ++kk) {
+      const int s = kk * 4 + kg;  // the k-slice this lane group supplies: (tap, 16-channel slice)
+      const int tap = s / CS, cs = s - tap * CS;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      v4i a = *reinterpret_cast<const v4i*>(base - (kh * Wp + kw) * C + cs * 16);
+      if (s >= 9 * CS) a = v4i{0, 0, 0, 0};  // zero padding of the k dimension
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bf[kk], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sh.tile[(mt * 16 + 4 * kg + i) * (C + 4) + nt * 16 + r] = (float)acc[i] * scale;
+  }
+  __syncthreads();
+  LBT_TS(3);
+
+  // ---------------- phase 3: pass A over the tile
+  int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};
+  int acc3[NB][4][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc3[b][s][k] = 0;
+  const bool has_add = p.add_src != nullptr;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pix = (tid + j * kBThreads) / C4;
+    const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);
+    const float4 t = *reinterpret_cast<const float4*>(sh.tile + pix * (C + 4) + cq);
+    float g[4] = {t.x, t.y, t.z, t.w};
+    if (has_add) {
+      g[0] = g[0] + av[j].x; g[1] = g[1] + av[j].y; g[2] = g[2] + av[j].z; g[3] = g[3] + av[j].w;
+    }
+    int R1[4];
+    unpack4(Rv[0][j], R1);
+    if (CF & kAYMask) {
+      const float ym[4] = {ymv[j].x, ymv[j].y, ymv[j].z, ymv[j].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] = ym[k] > 0.f ? g[k] : 0.f;
+    } else if (CF & kAMaskR) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float xr = (float)R1[k] * r_inv;
+        const float m1 = xr * gam[0][k];
+        const float yv = m1 + bet[k];
+        g[k] = yv > 0.f ? g[k] : 0.f;
+      }
+    }
+    if (CF & kAGmask) *reinterpret_cast<float4*>(A.gmask_out + img + off) = make_float4(g[0], g[1], g[2], g[3]);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+      int R[4], qn[4], Gc[4];
+      unpack4(Rv[b][j], R);
+      unpack4(qnv[b][j], qn);
+      const float ur[4] = {urg[b][j].x, urg[b][j].y, urg[b][j].z, urg[b][j].w};
+      const float un[4] = {ung[b][j].x, ung[b][j].y, ung[b][j].z, ung[b][j].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int G2 = quant_w<1>(qrg[b], 1, g[k], ur[k], ov[b][0][0], ov[b][0][1]);
+        acc3[b][0][k] += G2 * R[k];
+        acc3[b][1][k] += G2;
+        const float gh = (float)G2 * qrg[b].inv_m;
+        const float d = gh * gam[b][k];
+        Gc[k] = quant_w<1>(qng[b], 1, d, un[k], ov[b][1][0], ov[b][1][1]);
+        acc3[b][2][k] += Gc[k];
+        acc3[b][3][k] += Gc[k] * qn[k];
+      }
+      *reinterpret_cast<int*>(Bb.gout + img + off) = pack4(Gc);
+    }
+  }
+
+  // ---------------- channel sums: wave butterfly -> this wave's LDS slots (plain stores, no LDS
+  // atomics); counters; one barrier; the waves' slots summed and flushed
+  {
+    const bool own = lane < C4;  // lanes l, l + C4, ... hold the same channels (C4 <= 16 divides 64)
+    int* part = sh.part[wave];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        int v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = chan_reduce<C4>(acc3[b][s][k]);
+        if (own) *reinterpret_cast<int4*>(part + (b * 4 + s) * C + cq) = make_int4(v[0], v[1], v[2], v[3]);
+      }
+    int v1[4], v2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v1[k] = chan_reduce<C4>(s1[k]);
+      v2[k] = chan_reduce<C4>(s2[k]);
+    }
+    if (own) {
+      *reinterpret_cast<int4*>(part + 8 * C + cq) = make_int4(v1[0], v1[1], v1[2], v1[3]);
+      *reinterpret_cast<int4*>(part + 9 * C + cq) = make_int4(v2[0], v2[1], v2[2], v2[3]);
+    }
+  }
+  counts_stage_w(0, 5, ovq1, ovq2, sh.cnt);  // (counts_publish sums blockDim.x / 64 waves)
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    counts_stage_w(1 + 2 * b, 5, ov[b][0][0], ov[b][0][1], sh.cnt);
+    counts_stage_w(2 + 2 * b, 5, ov[b][1][0], ov[b][1][1], sh.cnt);
+  }
+  __syncthreads();
+  LBT_TS(4);
+  counts_publish(0, 5, B.qo, sh.cnt);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+    counts_publish(1 + 2 * b, 5, Bb.qrg, sh.cnt);
+    counts_publish(2 + 2 * b, 5, Bb.qng, sh.cnt);
+  }
+  // slot i of [NB*4C pass-A sums | 2C gq sums]: one thread each, the waves' partials in int64
+  const int shard = shard_id();
+  for (int i = tid; i < (NB * 4 + 2) * C; i += kBThreads) {
+    const int slot = i < NB * 4 * C ? i : 8 * C + (i - NB * 4 * C);
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kBNW; ++w) t += sh.part[w][slot];
+    if (!t) continue;
+    int64_t* dst;
+    if (i < NB * 4 * C) {
+      const int b = i / (4 * C);
+      dst = (b == 0 ? A.b1 : A.b2).sums + (int64_t)shard * 4 * C + (i - b * 4 * C);
+    } else {
+      if (!B.gcolsum) continue;
+      dst = B.gcolsum + (int64_t)shard * 2 * C + (i - NB * 4 * C);
+    }
+    LBT_GADD((unsigned long long*)dst, (unsigned long long)t);
+  }
+  LBT_TS(5);
+}
+
+bool noise_ok(const lbt_qdesc& q) { return q.bits > 0 && q.stochastic && q.noise; }
+
+}  // namespace
+
+extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
+  if (!q) return LBT_EINVAL;
+  const lbt_conv_desc& d = q->d;
+  const int C = d.Cin;
+  if (!desc_ok(d) || d.KH != 3 || d.KW != 3 || d.SH != 1 || d.SW != 1 || d.PT != 1 || d.PB != 1 || d.PL != 1 ||
+      d.PR != 1 || d.Ho != d.H || d.Wo != d.W || d.Cout != C || (C != 16 && C != 32 && C != 64) ||
+      d.H % kBTH || d.W * C != 512)
+    return LBT_EINVAL;
+  const int CS = C / 16;
+  const int64_t inner = (int64_t)d.H * d.W * C;
+  const lbt_chain_bwd_b& b = q->b;
+  if (!b.G || !b.qn_codes || !b.ms || !b.sums || !b.gq || b.dx || !noise_ok(b.qo) || b.C != C || b.rows != d.N ||
+      b.inner != inner)
+    return LBT_EINVAL;
+  const lbt_chain_bwd_a& a = q->a;
+  if (a.C != C || a.rows != d.N || a.inner != inner) return LBT_EINVAL;
+  const int f = bwd_a_flags(a);
+  if ((f & kAFused) != kAFused) return LBT_EINVAL;
+  for (int br = 0; br < (a.has_b2 ? 2 : 1); ++br) {
+    const lbt_bwd_branch& Bb = br ? a.b2 : a.b1;
+    if (!noise_ok(Bb.qrg) || !noise_ok(Bb.qng) || !Bb.gb) return LBT_EINVAL;
+  }
+  if (q->ksd != 4 * ((9 * CS + 3) / 4) || !q->wd) return LBT_EINVAL;
+  if (q->w4 && q->qw.bits > 4) return LBT_EINVAL;
+  if ((int64_t)(kBTH + 2) * (d.W + 2) * C / 4 > kBIt * kBThreads) return LBT_EINVAL;
+  WgradArgs wa{};
+  uint32_t wblocks = 0;
+  int wcs = 0;
+  if (q->w.slab) {
+    const int e = wgrad_setup(q->w.xq, q->w.x_u8off, q->w.gq, q->w.d, q->w.slab, q->w.nsplit, q->w.nshard, wa, wblocks);
+    if (e) return e;
+    wcs = q->w.d.Cin / 16;
+  }
+  ConvBwdArgs p;
+  p.b = b; p.wd = q->wd; p.ks = q->ksd; p.nslices = 9 * CS; p.w4 = q->w4; p.qw = q->qw;
+  p.H = d.H; p.W = d.W; p.add_src = q->add_src; p.a = a;
+  const int64_t tiles = (int64_t)d.N * (d.H / kBTH);
+  if (tiles + wblocks > 0x7fffffff) return LBT_EINVAL;
+  const dim3 grid((unsigned)(tiles + wblocks));
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = a.has_b2 ? 2 : 1;
+  // the combinations the fused ResNet plan runs (c2: mask from R1, deferred wgrad of the next
+  // block's c1 or none; c1: its consumer's chain, deferred wgrad of the same block's c2)
+#define LBT_BW(CS_, CF_, NB_, WCS_)                                                                  \
+  if (CS == CS_ && f == (CF_) && nb == NB_ && wcs == WCS_) {                                       \
+    if (q->w4)                                                                                     \
+      hipLaunchKernelGGL((conv_bwd_kernel<CS_, CF_, NB_, true, WCS_>), grid, dim3(kBThreads), 0, st, p, wa, wblocks); \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv_bwd_kernel<CS_, CF_, NB_, false, WCS_>), grid, dim3(kBThreads), 0, st, p, wa, wblocks); \
+    return (int)hipGetLastError();                                                                 \
+  }
+#define LBT_BW_CS(CS_)                                          \
+  LBT_BW(CS_, kAFused | kAMaskR, 1, 0)                          \
+  LBT_BW(CS_, kAFused | kAMaskR, 1, CS_)                        \
+  LBT_BW(CS_, kAFused | kAYMask | kAGmask, 1, CS_)              \
+  LBT_BW(CS_, kAFused | kAYMask, 2, CS_)                        \
+  LBT_BW(CS_, kAFused | kAYMask, 1, CS_)
+  LBT_BW_CS(1)
+  LBT_BW_CS(2)
+  LBT_BW_CS(4)
+#undef LBT_BW_CS
+#undef LBT_BW
+  return LBT_EINVAL;
 }

@@ -25,8 +25,8 @@ import os
 import torch
 
 from . import _lib
-from ._lib import NO_Q, OUT_I8, OUT_I16, OUT_U8OFF, BnNorm, BwdBranch, ChainBwdA, ChainBwdB, ChainFwd, NJob, PJob, \
-    QJob, RJob, WJob, call, ptr
+from ._lib import NO_Q, OUT_I8, OUT_I16, OUT_U8OFF, BnNorm, BwdBranch, ChainBwdA, ChainBwdB, ChainFwd, ConvBwd, \
+    NJob, PJob, QJob, RJob, WgradJob, WJob, call, ptr
 from .dfxp import ops
 from .dfxp.layers import _Cache
 
@@ -87,6 +87,10 @@ class FusedResNet:
         self.fuse_dgrad_chain = os.environ.get("LBT_FUSE_DGRAD_CHAIN", "1") == "1"
         # a conv's wgrad launched together with its dgrad (+ pass A): one launch per conv, not two
         self.fuse_wgrad = os.environ.get("LBT_FUSE_WGRAD", "1") == "1" and not self.overlap_wgrad
+        # stride-1 3x3 convs: pass B + dgrad + pass A in one launch (lbt_conv_bwd_fused_i8), each
+        # conv's wgrad deferred into the next such launch (1 = default)
+        self.fuse_bwd = (os.environ.get("LBT_FUSE_BWD", "1") == "1" and self.fuse_dgrad_chain and self.fuse_wgrad)
+        self._pending = None  # the deferred wgrad job (lbt_wgrad_job) of the last fused backward launch
         self._side = None
 
     # ------------------------------------------------------------------ Trainer interface
@@ -236,6 +240,7 @@ class FusedResNet:
                 if rc:
                     raise _lib.LbtError("%s failed with status %d" % (name, rc))
             run.kname = kname
+            run.nbytes = nb
             return run
 
         self._nd, njobs = {}, []
@@ -409,6 +414,7 @@ class FusedResNet:
             gY = self._block_bwd(i, self.blocks[i], saved[i], gY, ends[i], consumer, bwd, L, obs, rjobs, pjobs)
 
         # ---- stem backward (d loss / d image is never needed)
+        self._flush_pending(bwd, L)
         if gY is not None:  # pass A not fused into block 0's dgrad
             aA.g = gY.data_ptr()
             bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
@@ -638,6 +644,50 @@ class FusedResNet:
         self._keep.append(a)
         return dict(a=a, Gn2=Gn2, sums2=sums2, gm=gm, Gns=Gns, sumss=sumss)
 
+    def _fusable_bwd(self, c, d):
+        """lbt_conv_bwd_fused_i8 takes this conv: stride-1 3x3 SAME, Cin = Cout, W*C = 512."""
+        return (self.fuse_bwd and c.mfma and d.KH == 3 and d.KW == 3 and d.SH == 1 and d.SW == 1 and d.PT == 1
+                and d.PB == 1 and d.PL == 1 and d.PR == 1 and d.Cin == d.Cout and d.Cin in (16, 32, 64)
+                and d.H % 4 == 0 and d.W * d.Cin == 512)
+
+    def _flush_pending(self, bwd, L):
+        """Run the deferred wgrad job on its own (the next launch is not a fused conv backward)."""
+        w = self._pending
+        if w is None:
+            return
+        self._pending = None
+        bwd.append(L("lbt_conv_wgrad_i8", w.xq, w.x_u8off, w.gq, w.d, w.slab, w.nsplit, w.nshard,
+                     k="conv_wgrad_kernel", nb=w._nb))
+
+    def _conv_bwd(self, aB, c, d, add, aA, bwd, L, wjob):
+        """Append one lbt_conv_bwd_fused_i8 launch (pass B aB -> dgrad of conv c -> pass A aA), carrying
+        the pending wgrad job; wjob (this conv's own wgrad) becomes the pending one."""
+        cb = ConvBwd()
+        cb.b = aB
+        cb.wd = self._wd(c).value
+        cb.ksd = c.ksd
+        cb.w4 = 1 if getattr(c, "w4", False) else 0
+        cb.d = d
+        cb.qw = c.W_range.desc
+        cb.add_src = add.data_ptr() if add is not None else None
+        cb.a = aA
+        nbw = 0
+        if self._pending is not None:
+            cb.w = self._pending
+            nbw = self._pending._nb
+        inner = aB.inner
+        nb = (ops._chain_bwd_b_bytes(aB) + 4 * inner
+              + ops._dgrad_chain_bytes(0, c.wd.numel(), aA, add is not None) + nbw)
+        bwd.append(L("lbt_conv_bwd_fused_i8", ctypes.byref(cb), k="conv_bwd_kernel", nb=nb))
+        self._keep.append(cb)
+        self._pending = wjob
+
+    @staticmethod
+    def _wjob(xq, gq, d, slab, nsplit, nshard):
+        w = WgradJob(xq.data_ptr(), 1, gq.data_ptr(), d, slab.data_ptr(), nsplit, nshard)
+        w._nb = xq.numel() + gq.numel() + 4 * slab.numel()
+        return w
+
     def _block_bwd(self, i, b, f, gY, end, consumer, bwd, L, obs, rjobs, pjobs):
         """Block i's backward. gY: materialised d loss / d Y (or None: pass A already ran inside
         the next block's dgrad). consumer: the pass A fed by this block's input gradient.
@@ -665,14 +715,21 @@ class FusedResNet:
             bwd.append(self._allreduce(sums2))
             if sumss is not None:
                 bwd.append(self._allreduce(sumss))
-        bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB2), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB2)))
+        fb2 = self._fusable_bwd(c2, d2)
+        fb1 = self._fusable_bwd(c1, d1)
+        if not fb2:
+            self._flush_pending(bwd, L)
+            bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB2), k="chain_bwd_b_kernel",
+                         nb=ops._chain_bwd_b_bytes(aB2)))
         keep = [aB2]
-        gqs = gcols = None
+        gqs = gcols = aBs = None
         if cs is not None:
             gqs = self._buf(k + "gqs", shp, torch.int8)
             gcols = self._sums(k + "gcols", ops.NSHARD * 2 * C)
             aBs = self._chain_bwd_b(b.ns, Gns, f["qns"], sumss, shp, C, gqs, cs.grad_range, gcols)
-            bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aBs), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aBs)))
+            if not fb2:
+                bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aBs), k="chain_bwd_b_kernel",
+                             nb=ops._chain_bwd_b_bytes(aBs)))
             keep.append(aBs)
         # conv-2 dgrad, fused with pass A of bn1 (ReLU mask recomputed from R1)
         Gn1 = self._buf(k + "Gn1", shp, torch.int8)
@@ -680,7 +737,13 @@ class FusedResNet:
         nb_dg2 = gq2.numel() + c2.wd.numel()
         sp2, ns2, slab2 = ops.wgrad_slab(self._c, k + "slab2", d2, self.ctx)
         nb_wg2 = f["xb"].numel() + gq2.numel() + 4 * slab2.numel()
-        if fuse:
+        if fb2:  # pass B (bn2) + dgrad + pass A (bn1) in one launch, conv-2 wgrad deferred
+            if cs is not None:  # the shortcut BN's pass B (its conv is not fused) goes first
+                bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aBs), k="chain_bwd_b_kernel",
+                             nb=ops._chain_bwd_b_bytes(aBs)))
+            aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
+            self._conv_bwd(aB2, c2, d2, None, aA1, bwd, L, self._wjob(f["xb"], gq2, d2, slab2, sp2, ns2))
+        elif fuse:
             aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
             nb = ops._dgrad_chain_bytes(gq2.numel(), c2.wd.numel(), aA1, False)
             if self.fuse_wgrad:  # conv-2 wgrad in the same launch
@@ -697,7 +760,7 @@ class FusedResNet:
                          c2.W_range.desc, ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg2 + 4 * numel))
             aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
         keep.append(aA1)
-        if not (fuse and self.fuse_wgrad):
+        if not (fuse and self.fuse_wgrad) and not fb2:
             bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), sp2, ns2,
                                        k="conv_wgrad_kernel", nb=nb_wg2)))
         rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), self._qd(c2.X_range),
@@ -709,7 +772,10 @@ class FusedResNet:
         aB1 = self._chain_bwd_b(b.n1, Gn1, f["qn1"], sums1, shp, C, gq1, c1.grad_range, gcol1)
         if self.sync_bn:
             bwd.append(self._allreduce(sums1))
-        bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB1), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB1)))
+        if not fb1:
+            self._flush_pending(bwd, L)
+            bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB1), k="chain_bwd_b_kernel",
+                         nb=ops._chain_bwd_b_bytes(aB1)))
         keep.append(aB1)
         add = gm
         if cs is not None:
@@ -724,7 +790,9 @@ class FusedResNet:
         gin = None
         sp1, ns1, slab1 = ops.wgrad_slab(self._c, k + "slab1", d1, self.ctx)
         nb_wg1 = f["xa"].numel() + gq1.numel() + 4 * slab1.numel()
-        if fuse:
+        if fb1:  # pass B (bn1) + dgrad (+ residual gradient) + the consumer's pass A, wgrad deferred
+            self._conv_bwd(aB1, c1, d1, add, consumer["a"], bwd, L, self._wjob(f["xa"], gq1, d1, slab1, sp1, ns1))
+        elif fuse:
             nb = ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], add is not None)
             if self.fuse_wgrad:  # conv-1 wgrad in the same launch
                 bwd.append(L(self._fn(c1, "lbt_conv_dgrad_chain_wgrad_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1,
@@ -739,7 +807,7 @@ class FusedResNet:
             gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
             bwd.append(L(self._fn(c1, "lbt_conv_dgrad_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1, self._qd(c1.grad_range),
                          c1.W_range.desc, ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg1))
-        if not (fuse and self.fuse_wgrad):
+        if not (fuse and self.fuse_wgrad) and not fb1:
             bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), sp1, ns1,
                                        k="conv_wgrad_kernel", nb=nb_wg1)))
         rjobs.append(RJob(slab1.data_ptr(), ns1, 9 * Cin, C, 1, gcol1.data_ptr(), self._qd(c1.X_range),

@@ -723,3 +723,36 @@ def test_head_kernel_equals_launch_sequence(N, HW, C, K, table):
                          counts=ctx.counts_view()[:3].sum(1))
     for k, v in out["seq"].items():
         assert torch.equal(v, out["head"][k]), k
+
+
+@pytest.mark.parametrize("B,w4", [(32, False), (128, False), (32, True)])
+def test_fused_conv_backward_equals_launch_pair(B, w4):
+    """lbt_conv_bwd_fused_i8 (pass B + dgrad + pass A in one launch per stride-1 3x3 conv, each
+    conv's wgrad deferred into the next such launch) == the chain_bwd_b / dgrad_wgrad launches it
+    replaces: gradients, momentum, weights, exponents and BN running statistics bit-identical after
+    two optimiser steps (eager, then graph replay)."""
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.trainer import Trainer
+    outs = []
+    for fb in (False, True):
+        ctx = DfxpContext(seed=4)
+        m = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, weight_bits=4 if w4 else None))
+        m.fuse_bwd = fb
+        tr = Trainer(m, lr=1e-2, momentum=0.9, batch_size=B, use_graph=fb)
+        for i in range(2):
+            x, y = synthetic_batch(B, seed=30 + i)
+            tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+        torch.cuda.synchronize()
+        nf = sum(1 for f in m._bwd if getattr(f, "kname", "") == "conv_bwd_kernel")
+        assert nf == (16 if fb else 0), nf
+        bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
+        outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,
+                     m.loss.item()))
+    a, b = outs
+    for i in range(3):
+        assert np.array_equal(a[i], b[i]), i
+    assert a[3] == b[3]
+    for u, v in zip(a[4], b[4]):
+        assert np.array_equal(u, v)
+    assert a[5] == b[5]
