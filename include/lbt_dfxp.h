@@ -399,6 +399,26 @@ typedef struct lbt_conv_bwd {
 } lbt_conv_bwd;
 int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* p, void* stream);
 
+/* One stride-1 3x3 Conv2d_q's forward in ONE launch, with the BN element chain that produces its
+ * input (ResidualBlock_q :858-863 / BatchNorm_q :584-616,677-683 -> Conv2d_q.forward :287-291):
+ *   X  = chain c (exactly lbt_bn_chain_fwd; c.o1 = this conv's input codes, LBT_OUT_U8OFF, stored:
+ *        they are the weight gradient's operand; c.o2 must be NULL)
+ *   y  = conv(X, wf)  (as lbt_conv_fwd_i8 with x_u8off = 1, qx = c.qo1, qw)
+ *   yq = Q(y, qout) with the channel sums of yq into ychsum (the quantising epilogue of
+ *        lbt_conv_fwd_i8: the next Normalization_q's input quantiser)
+ * Each workgroup owns 4 image rows and recomputes the chain over its rows plus a one-pixel halo
+ * into LDS; the chain's stored outputs (R codes, y, X codes), counters and the BN running-average
+ * update (workgroup 0) come from the owning workgroup only: every output is bit-identical to
+ * lbt_bn_chain_fwd followed by lbt_conv_fwd_i8. Shapes as lbt_conv_bwd_fused_i8; chains: int8
+ * Normalization_q inputs, Rescale_q codes stored, ReLU, stochastic noise tables, 1 or 2 branches,
+ * optional residual and y; w4: wf is the packed 4-bit image. Else LBT_EINVAL.                    */
+typedef struct lbt_conv_fwd {
+  lbt_chain_fwd c;
+  const int8_t* wf; int32_t ksf; int32_t w4; const int32_t* wcolsum; lbt_conv_desc d; lbt_qdesc qw;
+  int8_t* yq; lbt_qdesc qout; int64_t* ychsum;
+} lbt_conv_fwd;
+int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* p, void* stream);
+
 /* BN backward passes A and B for 9..16-bit gradient quantisers (config 4): the arithmetic of
  * lbt_bn_chain_bwd_a / _b (one branch, no mask) with int16 grad codes and int64 channel sums.
  * Rows here are pixels: g / R / qn / gout / dout / dx are [rows][C]; inner = the per-sample

@@ -681,7 +681,7 @@ extern "C" int lbt_diag_occupancy(int32_t* out, int32_t n) {
 
 // ============================================================================ fused conv backward
 // lbt_conv_bwd_fused_i8: one stride-1 3x3 conv's backward with both neighbouring BN passes in ONE
-// launch. A dgrad workgroup owns kBTH image rows of one sample:
+// launch. A dgrad workgroup owns tile_rows(CS) image rows of one sample:
 //   phase 1  pass B of the BN after the conv (bn.hip chain_bwd_b_kernel's arithmetic) over the rows
 //            plus a one-pixel halo -> int8 gq codes in LDS; owned pixels also store gq (the weight
 //            gradient's operand), count overflows and add the gq channel sums
@@ -693,10 +693,15 @@ extern "C" int lbt_diag_occupancy(int32_t* out, int32_t n) {
 // conv of the previous launch.
 namespace {
 
-constexpr int kBTH = 4;    // image rows per dgrad workgroup
 constexpr int kBNW = 8;    // waves per workgroup
 constexpr int kBThreads = kBNW * 64;
-constexpr int kBIt = 2;    // phase-1 groups per thread (host: (kBTH+2)(W+2)C/4 <= 1024)
+// image rows per workgroup: 8 for the 16-channel stage (1024 4-row tiles would take two rounds of
+// two 512-thread workgroups per CU), 4 otherwise (W * C == 512: a 4-row tile is 8 MFMA tiles)
+__host__ __device__ constexpr int tile_rows(int CS) { return CS == 1 ? 8 : 4; }
+// phase-1 (halo) channel-quad groups per thread
+__host__ __device__ constexpr int halo_iters(int CS) {
+  return ((tile_rows(CS) + 2) * (512 / (CS * 16) + 2) * CS * 4 + kBThreads - 1) / kBThreads;
+}
 
 struct ConvBwdArgs {
   lbt_chain_bwd_b b;
@@ -708,10 +713,10 @@ struct ConvBwdArgs {
   lbt_chain_bwd_a a;
 };
 
-template <int C>
+template <int C, int TH>
 struct BwdShared {
-  int8_t gq[(kBTH + 2) * (512 / C + 2) * C];   // halo image [(kBTH+2)][(W+2)][C], W*C == 512
-  float tile[kBTH * (512 / C) * (C + 4)];       // dgrad outputs [kBTH*W][C+4] (padded rows)
+  int8_t gq[(TH + 2) * (512 / C + 2) * C];   // halo image [(TH+2)][(W+2)][C], W*C == 512
+  float tile[TH * (512 / C) * (C + 4)];       // dgrad outputs [TH*W][C+4] (padded rows)
   float pb[2 * C];                               // pass-B constants mg, mgx per channel
   int part[kBNW][(2 * 4 + 2) * C];               // per wave: pass-A sums per branch, gq sums
   int cnt[kBNW * 2 * 5];                         // counters: 5 quantisers x waves
@@ -757,8 +762,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   constexpr int C = CS * 16, C4 = C / 4, NT = CS;
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   constexpr int WC = WCS ? WCS : 1;
+  constexpr int TH = tile_rows(CS), kBIt = halo_iters(CS), J = TH / 4;  // J: phase-3 groups per thread
   union Smem {
-    BwdShared<C> b;
+    BwdShared<C, TH> b;
     WgradShared<WC, kBNW> w;
   };
   __shared__ __attribute__((aligned(16))) Smem sm;
@@ -766,15 +772,15 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     conv_wgrad_body<WC, kBNW>(wa, blockIdx.x, sm.w);
     return;
   }
-  BwdShared<C>& sh = sm.b;
+  BwdShared<C, TH>& sh = sm.b;
   LBT_TS(0);
   const lbt_chain_bwd_b& B = p.b;
   const lbt_chain_bwd_a& A = p.a;
   const uint32_t bid = blockIdx.x - nwg;
   constexpr int W = 512 / C, Wp = W + 2;  // W * C == 512 (host check)
   const int H = p.H;
-  const int tpi = H / kBTH;
-  const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * kBTH;
+  const int tpi = H / TH;
+  const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * TH;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4;  // this thread's channel quad (512 % C4 == 0: fixed over its groups)
@@ -782,7 +788,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
 
   // ---------------- every load that does not depend on the sums goes out first
   // phase-1 operands: G / q codes and the output quantiser's noise over the halo rows
-  const int ngrp = (kBTH + 2) * Wp * C4;
+  const int ngrp = (TH + 2) * Wp * C4;
   int Gv[kBIt], Qv[kBIt];
   float4 Uv[kBIt];
 #pragma unroll
@@ -796,8 +802,8 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     Qv[it] = ld4i8(B.qn_codes, img + off);
     Uv[it] = ld4f(B.qo.noise, off);
   }
-  // phase-2 B operands (dgrad weights) of this wave's (m-tile, n-tile) pair (pair = wave, the 8
-  // pairs of a 4-row tile: W*C == 512); ks == 4 * kMaxKS (host check)
+  // phase-2 B operands (dgrad weights) of this wave's (m-tile, n-tile) pairs wave + 8i (one n-tile:
+  // NT | 8; a 4-row tile is 8 pairs, W*C == 512); ks == 4 * kMaxKS (host check)
   v4i bf[kMaxKS];
   {
     const int col = (wave % NT) * 16 + r;
@@ -809,7 +815,6 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
         bf[kk] = *reinterpret_cast<const v4i*>(p.wd + ((int64_t)col * (4 * kMaxKS) + kk * 4 + kg) * 16);
     }
   }
-  constexpr int J = 1;  // phase-3 groups per thread (kBTH*W*C/4 == 512 == kBThreads)
   float mu[4], sg[4], gam[2][4], bet[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -873,7 +878,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     const int y = row0 - 1 + hy, x = hx - 1;
     const bool valid = g < ngrp;
     const bool in = valid && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-    const bool own = in && hy >= 1 && hy <= kBTH;
+    const bool own = in && hy >= 1 && hy <= TH;
     int G[4], q[4], c[4];
     unpack4(Gv[it], G);
     unpack4(Qv[it], q);
@@ -924,8 +929,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   }
 
   // ---------------- phase 2: dgrad from the LDS image, two (m-tile, n-tile) pairs per wave
-  {
-    const int pr = wave;
+#pragma unroll
+  for (int pi = 0; pi < TH / 4; ++pi) {
+    const int pr = wave + 8 * pi;
     const int mt = pr / NT, nt = pr - mt * NT;
     const int m = mt * 16 + r;
     const int ly = m / W, px = m - ly * W;
@@ -1075,7 +1081,7 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   const int C = d.Cin;
   if (!desc_ok(d) || d.KH != 3 || d.KW != 3 || d.SH != 1 || d.SW != 1 || d.PT != 1 || d.PB != 1 || d.PL != 1 ||
       d.PR != 1 || d.Ho != d.H || d.Wo != d.W || d.Cout != C || (C != 16 && C != 32 && C != 64) ||
-      d.H % kBTH || d.W * C != 512)
+      d.H % tile_rows(C / 16) || d.W * C != 512)
     return LBT_EINVAL;
   const int CS = C / 16;
   const int64_t inner = (int64_t)d.H * d.W * C;
@@ -1093,7 +1099,6 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   }
   if (q->ksd != 4 * ((9 * CS + 3) / 4) || !q->wd) return LBT_EINVAL;
   if (q->w4 && q->qw.bits > 4) return LBT_EINVAL;
-  if ((int64_t)(kBTH + 2) * (d.W + 2) * C / 4 > kBIt * kBThreads) return LBT_EINVAL;
   WgradArgs wa{};
   uint32_t wblocks = 0;
   int wcs = 0;
@@ -1105,7 +1110,7 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   ConvBwdArgs p;
   p.b = b; p.wd = q->wd; p.ks = q->ksd; p.nslices = 9 * CS; p.w4 = q->w4; p.qw = q->qw;
   p.H = d.H; p.W = d.W; p.add_src = q->add_src; p.a = a;
-  const int64_t tiles = (int64_t)d.N * (d.H / kBTH);
+  const int64_t tiles = (int64_t)d.N * (d.H / tile_rows(CS));
   if (tiles + wblocks > 0x7fffffff) return LBT_EINVAL;
   const dim3 grid((unsigned)(tiles + wblocks));
   hipStream_t st = (hipStream_t)stream;
@@ -1126,10 +1131,345 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   LBT_BW(CS_, kAFused | kAYMask | kAGmask, 1, CS_)              \
   LBT_BW(CS_, kAFused | kAYMask, 2, CS_)                        \
   LBT_BW(CS_, kAFused | kAYMask, 1, CS_)
-  LBT_BW_CS(1)
+  LBT_BW(1, kAFused | kAMaskR, 1, 0)
+  LBT_BW(1, kAFused | kAMaskR, 1, 1)
+  LBT_BW(1, kAFused | kAYMask | kAGmask, 1, 1)
+  LBT_BW(1, kAFused | kAYMask, 1, 1)
   LBT_BW_CS(2)
   LBT_BW_CS(4)
 #undef LBT_BW_CS
 #undef LBT_BW
+  return LBT_EINVAL;
+}
+
+// ============================================================================ fused conv forward
+// lbt_conv_fwd_fused_i8: the BN element chain that produces a stride-1 3x3 conv's input (bn.hip
+// chain_fwd_kernel's arithmetic) runs as the conv's operand staging. A workgroup owns TH image
+// rows: phase 1 evaluates the chain over the rows plus a one-pixel halo into an LDS image of the
+// conv's input codes (owned pixels also store R codes / y / X codes and count overflows), phase 2
+// runs the MFMAs from LDS into an fp32 LDS tile, phase 3 quantises the tile for the next BN (one
+// channel quad per thread) and adds its channel sums.
+namespace {
+
+struct ConvFwdArgs {
+  lbt_chain_fwd c;
+  const int8_t* wf;
+  const int32_t* wcolsum;
+  lbt_qdesc qw;
+  int H;
+  int8_t* yq;
+  lbt_qdesc qout;
+  int64_t* ychsum;
+};
+
+template <int C, int TH>
+struct FwdShared {
+  int8_t x[(TH + 2) * (512 / C + 2) * C];   // the conv's input codes, halo image (q - 128)
+  float tile[TH * (512 / C) * (C + 4)];      // conv outputs [TH*W][C+4]
+  float cst[2][2][C];                          // per branch: mu, sigma
+  int part[kBNW][2 * C];                       // per wave: S1, S2 of the output codes
+  int cnt[kBNW * 2 * 4];                       // counters: R (2 branches), X, output
+};
+
+template <int CS, int NB, int F, bool W4>
+__global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_kernel(ConvFwdArgs p) {
+  constexpr int C = CS * 16, C4 = C / 4, NT = CS, W = 512 / C, Wp = W + 2;
+  constexpr int kMaxKS = (9 * CS + 3) / 4;
+  constexpr int TH = tile_rows(CS), kBIt = halo_iters(CS), J = TH / 4;
+  __shared__ __attribute__((aligned(16))) FwdShared<C, TH> sh;
+  LBT_TS(0);
+  const lbt_chain_fwd& a = p.c;
+  const int H = p.H;
+  const uint32_t bid = blockIdx.x;
+  const int tpi = H / TH;
+  const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * TH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int cq = (tid % C4) * 4;
+  const int64_t img = (int64_t)n * H * W * C;
+  constexpr bool RES = (F & kFRes) != 0, YST = (F & kFY) != 0;
+
+  // ---------------- loads that do not depend on the moments
+  const int ngrp = (TH + 2) * Wp * C4;
+  int qv[NB][kBIt];
+  float4 rv[kBIt], nrv[NB][kBIt], nov[kBIt];
+#pragma unroll
+  for (int it = 0; it < kBIt; ++it) {
+    const int g = tid + it * kBThreads;
+    const int pix = g / C4, hy = pix / Wp, hx = pix - hy * Wp;
+    const int y = row0 - 1 + hy, x = hx - 1;
+    const bool in = g < ngrp && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const uint32_t off = in ? (uint32_t)((y * W + x) * C + cq) : 0u;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_chain_branch& Bb = b == 0 ? a.b1 : a.b2;
+      qv[b][it] = ld4i8(Bb.nrm.q, img + off);
+      nrv[b][it] = ld4f(Bb.qr.noise, off);
+    }
+    if constexpr (RES) rv[it] = ld4f(a.res, img + off);
+    nov[it] = ld4f(a.qo1.noise, off);
+  }
+  // the B operands (this wave's n-tile of the forward weight image): loaded up front, or -- in the
+  // variants whose phase 1 holds the most registers -- right after phase 1
+  constexpr bool kLateB = NB == 2 || RES;
+  v4i bf[kMaxKS];
+  const int bcol = (wave % NT) * 16 + r;
+  auto load_b = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < kMaxKS; ++kk) {
+      if constexpr (W4)
+        bf[kk] = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wf + ((int64_t)bcol * (4 * kMaxKS) + kk * 4 + kg) * 8));
+      else
+        bf[kk] = *reinterpret_cast<const v4i*>(p.wf + ((int64_t)bcol * (4 * kMaxKS) + kk * 4 + kg) * 16);
+    }
+  };
+  if constexpr (!kLateB) load_b();
+  const int corr = 128 * p.wcolsum[bcol];  // the unsigned-9-bit offset encoding undone: + 128 * sum_k W[k][col]
+  float gam[NB][4], bet[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      gam[b][k] = (b == 0 ? a.b1 : a.b2).gb[cq + k];
+      bet[b][k] = (b == 0 ? a.b1 : a.b2).gb[C + cq + k];
+    }
+  QState qr[2];
+  float sn[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    qr[b] = qstate((b == 0 ? a.b1 : a.b2).qr);
+    sn[b] = qscale((b == 0 ? a.b1 : a.b2).nrm.qn);
+  }
+  const QState so1 = qstate(a.qo1), sq = qstate(p.qout);
+  const float scale = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw)));
+
+  // ---------------- Normalization_q moments (bn.hip bn_moments): threads c < C of each branch
+  if (tid < NB * C) {
+    const int b = tid / C, c = tid - b * C;
+    const lbt_bn_norm& nb = b == 0 ? a.b1.nrm : a.b2.nrm;
+    long long v[2][LBT_NSHARD];
+#pragma unroll
+    for (int k = 0; k < LBT_NSHARD; ++k) {
+      v[0][k] = nb.chsum[(int64_t)k * 2 * C + c];
+      v[1][k] = nb.chsum[(int64_t)k * 2 * C + C + c];
+    }
+    long long S1 = 0, S2 = 0;
+#pragma unroll
+    for (int k = 0; k < LBT_NSHARD; ++k) {
+      S1 += v[0][k];
+      S2 += v[1][k];
+    }
+    const double s = ldexp(1.0, -frac_exp(nb.qn));
+    const double mean_d = (double)S1 * s / (double)nb.n;
+    const double var_d = (double)S2 * (s * s) / (double)nb.n - mean_d * mean_d;
+    const float m = (float)mean_d, vv = (float)var_d;
+    const float sigma = sqrtf(vv + nb.eps);
+    sh.cst[b][0][c] = m;
+    sh.cst[b][1][c] = sigma;
+    if (bid == 0) {  // one writer: ms for the backward, the running averages (:601-612)
+      if (nb.ms) { nb.ms[c] = m; nb.ms[C + c] = sigma; }
+      if (nb.run_mean) {
+        nb.run_mean[c] = nb.momentum * nb.run_mean[c] + nb.one_minus_momentum * m;
+        nb.run_var[c] = nb.momentum * nb.run_var[c] + nb.one_minus_momentum * vv;
+      }
+    }
+  }
+  __syncthreads();
+  LBT_TS(1);
+  float pm[NB][4];
+  Recip ps[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pm[b][k] = sh.cst[b][0][cq + k];
+      ps[b][k] = recip(sh.cst[b][1][cq + k]);
+    }
+
+  // ---------------- phase 1: the chain over the rows + halo -> LDS input codes
+  int ovr[2][2] = {{0, 0}, {0, 0}}, ovx1 = 0, ovx2 = 0;
+#pragma unroll
+  for (int it = 0; it < kBIt; ++it) {
+    if (it * kBThreads >= ngrp) break;  // uniform
+    const int g = tid + it * kBThreads;
+    const int pix = g / C4, hy = pix / Wp, hx = pix - hy * Wp;
+    const int y = row0 - 1 + hy, x = hx - 1;
+    const bool valid = g < ngrp;
+    const bool in = valid && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const bool own = in && hy >= 1 && hy <= TH;
+    const uint32_t e = (uint32_t)((y * W + x) * C + cq);
+    float v[4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_chain_branch& Bb = b == 0 ? a.b1 : a.b2;
+      int q[4], R[4];
+      unpack4(qv[b][it], q);
+      const float u[4] = {nrv[b][it].x, nrv[b][it].y, nrv[b][it].z, nrv[b][it].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x1 = (float)q[k] * sn[b];
+        const float x2 = x1 - pm[b][k];
+        const float t = div_by(x2, ps[b][k]);
+        R[k] = quant_sc(qr[b], t, u[k], own, ovr[b][0], ovr[b][1]);
+        const float xr = (float)R[k] * qr[b].inv_m;
+        const float m1 = xr * gam[b][k];
+        const float tt = m1 + bet[b][k];
+        v[k] = b ? v[k] + tt : tt;
+      }
+      if (own) *reinterpret_cast<int*>(Bb.rout + img + e) = pack4(R);
+    }
+    if constexpr (RES) {
+      v[0] = v[0] + rv[it].x; v[1] = v[1] + rv[it].y; v[2] = v[2] + rv[it].z; v[3] = v[3] + rv[it].w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+    if (YST && own) *reinterpret_cast<float4*>(a.y + img + e) = make_float4(v[0], v[1], v[2], v[3]);
+    const float uo[4] = {nov[it].x, nov[it].y, nov[it].z, nov[it].w};
+    int c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cc = quant_sc(so1, v[k], uo[k], own, ovx1, ovx2);
+      c[k] = in ? (cc < 0 ? 0 : cc) - 128 : -128;  // LBT_OUT_U8OFF; outside the image: the code of 0
+    }
+    if (valid) *reinterpret_cast<int*>(sh.x + pix * C + cq) = pack4(c);
+    if (own) *reinterpret_cast<int*>((int8_t*)a.o1 + img + e) = pack4(c);
+  }
+  if constexpr (kLateB) load_b();
+  __syncthreads();
+  LBT_TS(2);
+  // phase-3 noise (the output quantiser), issued under the MFMAs
+  float4 u3[J];  // J channel quads per thread: TH*W*C/4 == J * kBThreads
+#pragma unroll
+  for (int j = 0; j < J; ++j) u3[j] = ld4f(p.qout.noise, (uint32_t)(row0 * W * C + ((tid + j * kBThreads) / C4) * C + cq));
+
+  // ---------------- phase 2: the conv from the LDS image (pair = wave)
+#pragma unroll
+  for (int pi = 0; pi < TH / 4; ++pi) {
+    const int pr = wave + 8 * pi;
+    const int mt = pr / NT, nt = pr - mt * NT;
+    const int m = mt * 16 + r;
+    const int ly = m / W, px = m - ly * W;
+    const int8_t* base = sh.x + (ly * Wp + px) * C;
+    v4i acc = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < kMaxKS; ++kk) {
+      const int s = kk * 4 + kg;
+      const int tap = s / CS, cs = s - tap * CS;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      v4i av = *reinterpret_cast<const v4i*>(base + (kh * Wp + kw) * C + cs * 16);
+      if (s >= 9 * CS) av = v4i{0, 0, 0, 0};  // k padding (its weights are zero too)
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bf[kk], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      sh.tile[(mt * 16 + 4 * kg + i) * (C + 4) + nt * 16 + r] = (float)(acc[i] + corr) * scale;
+  }
+  __syncthreads();
+  LBT_TS(3);
+
+  // ---------------- phase 3: the next BN's input quantiser + its channel sums
+  int ovq1 = 0, ovq2 = 0;
+  int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pix3 = (tid + j * kBThreads) / C4;
+    const float4 t = *reinterpret_cast<const float4*>(sh.tile + pix3 * (C + 4) + cq);
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+    const float u[4] = {u3[j].x, u3[j].y, u3[j].z, u3[j].w};
+    int c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c[k] = quant_w<1>(sq, 1, tv[k], u[k], ovq1, ovq2);
+      s1[k] += c[k];
+      s2[k] += c[k] * c[k];
+    }
+    *reinterpret_cast<int*>(p.yq + img + (uint32_t)(row0 * W * C + pix3 * C + cq)) = pack4(c);
+  }
+  {
+    const bool own = lane < C4;
+    int v1[4], v2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v1[k] = chan_reduce<C4>(s1[k]);
+      v2[k] = chan_reduce<C4>(s2[k]);
+    }
+    if (own) {
+      *reinterpret_cast<int4*>(sh.part[wave] + cq) = make_int4(v1[0], v1[1], v1[2], v1[3]);
+      *reinterpret_cast<int4*>(sh.part[wave] + C + cq) = make_int4(v2[0], v2[1], v2[2], v2[3]);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) counts_stage_w(b, 4, ovr[b][0], ovr[b][1], sh.cnt);
+  counts_stage_w(2, 4, ovx1, ovx2, sh.cnt);
+  counts_stage_w(3, 4, ovq1, ovq2, sh.cnt);
+  __syncthreads();
+  LBT_TS(4);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) counts_publish(b, 4, (b == 0 ? a.b1 : a.b2).qr, sh.cnt);
+  counts_publish(2, 4, a.qo1, sh.cnt);
+  counts_publish(3, 4, p.qout, sh.cnt);
+  if (p.ychsum && tid < 2 * C) {
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kBNW; ++w) t += sh.part[w][tid];
+    if (t) LBT_GADD((unsigned long long*)&p.ychsum[(int64_t)shard_id() * 2 * C + tid], (unsigned long long)t);
+  }
+  LBT_TS(5);
+}
+
+}  // namespace
+
+extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
+  if (!q) return LBT_EINVAL;
+  const lbt_conv_desc& d = q->d;
+  const int C = d.Cin;
+  if (!desc_ok(d) || d.KH != 3 || d.KW != 3 || d.SH != 1 || d.SW != 1 || d.PT != 1 || d.PB != 1 || d.PL != 1 ||
+      d.PR != 1 || d.Ho != d.H || d.Wo != d.W || d.Cout != C || (C != 16 && C != 32 && C != 64) ||
+      d.H % tile_rows(C / 16) || d.W * C != 512)
+    return LBT_EINVAL;
+  const int CS = C / 16;
+  const lbt_chain_fwd& a = q->c;
+  const int64_t inner = (int64_t)d.H * d.W * C;
+  if (a.C != C || a.rows != d.N || a.inner != inner || a.o2 || !a.o1 || a.o1_kind != LBT_OUT_U8OFF) return LBT_EINVAL;
+  const int f = fwd_flags(a);
+  constexpr int kNeed = kFQ | kFRout | kFRelu | kFO1 | kFStoch | kFU8;
+  if ((f & kRt) || (f & kNeed) != kNeed || (f & (kFO2 | kFNoR))) return LBT_EINVAL;
+  if (!noise_ok(a.qo1)) return LBT_EINVAL;
+  for (int br = 0; br < (a.has_b2 ? 2 : 1); ++br) {
+    const lbt_chain_branch& Bb = br ? a.b2 : a.b1;
+    if (!noise_ok(Bb.qr) || !Bb.gb || !Bb.nrm.chsum || Bb.nrm.frozen) return LBT_EINVAL;
+  }
+  if (!q->yq || !noise_ok(q->qout) || !q->wcolsum || !q->wf) return LBT_EINVAL;
+  if (q->ksf != 4 * ((9 * CS + 3) / 4)) return LBT_EINVAL;
+  if (q->w4 && q->qw.bits > 4) return LBT_EINVAL;
+  ConvFwdArgs p;
+  p.c = a; p.wf = q->wf; p.wcolsum = q->wcolsum; p.qw = q->qw; p.H = d.H;
+  p.yq = q->yq; p.qout = q->qout; p.ychsum = q->ychsum;
+  const int64_t tiles = (int64_t)d.N * (d.H / tile_rows(CS));
+  if (tiles > 0x7fffffff) return LBT_EINVAL;
+  const dim3 grid((unsigned)tiles);
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = a.has_b2 ? 2 : 1;
+  const int fl = f & ~kFU8 & ~kFStoch;  // variant key: Y / residual present
+#define LBT_FW(CS_, NB_, FL_)                                                                            \
+  if (CS == CS_ && nb == NB_ && fl == ((FL_) & ~kFU8 & ~kFStoch)) {                                      \
+    if (q->w4)                                                                                           \
+      hipLaunchKernelGGL((conv_fwd_fused_kernel<CS_, NB_, FL_, true>), grid, dim3(kBThreads), 0, st, p);   \
+    else                                                                                                 \
+      hipLaunchKernelGGL((conv_fwd_fused_kernel<CS_, NB_, FL_, false>), grid, dim3(kBThreads), 0, st, p);  \
+    return (int)hipGetLastError();                                                                       \
+  }
+  // c2 (bn1 chain), c1 after an identity / projection block, block 0's c1 (the stem's chain)
+#define LBT_FW_CS(CS_)                                  \
+  LBT_FW(CS_, 1, kNeed)                                 \
+  LBT_FW(CS_, 1, kNeed | kFRes | kFY)                   \
+  LBT_FW(CS_, 2, kNeed | kFY)
+  LBT_FW(1, 1, kNeed)
+  LBT_FW(1, 1, kNeed | kFRes | kFY)
+  LBT_FW(1, 1, kNeed | kFY)
+  LBT_FW_CS(2)
+  LBT_FW_CS(4)
+#undef LBT_FW_CS
+#undef LBT_FW
   return LBT_EINVAL;
 }

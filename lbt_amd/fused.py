@@ -26,7 +26,7 @@ import torch
 
 from . import _lib
 from ._lib import NO_Q, OUT_I8, OUT_I16, OUT_U8OFF, BnNorm, BwdBranch, ChainBwdA, ChainBwdB, ChainFwd, ConvBwd, \
-    NJob, PJob, QJob, RJob, WgradJob, WJob, call, ptr
+    ConvFwd, NJob, PJob, QJob, RJob, WgradJob, WJob, call, ptr
 from .dfxp import ops
 from .dfxp.layers import _Cache
 
@@ -91,6 +91,9 @@ class FusedResNet:
         # conv's wgrad deferred into the next such launch (1 = default)
         self.fuse_bwd = (os.environ.get("LBT_FUSE_BWD", "1") == "1" and self.fuse_dgrad_chain and self.fuse_wgrad)
         self._pending = None  # the deferred wgrad job (lbt_wgrad_job) of the last fused backward launch
+        # stride-1 3x3 convs: the BN chain producing the input runs in the conv launch (lbt_conv_fwd_fused_i8)
+        self.fuse_fwd = os.environ.get("LBT_FUSE_FWD", "1") == "1"
+        self._chain_pending = None  # a forward chain not launched yet (the next conv may absorb it)
         self._side = None
 
     # ------------------------------------------------------------------ Trainer interface
@@ -339,8 +342,8 @@ class FusedResNet:
                             o1=xa, q1=b0.c1.X_range, o2=xs, q2=b0.cs.X_range if xs is not None else None)
         if self.sync_bn:
             fwd.append(self._allreduce(chs0))
-        fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a)))
         self._keep = [a]
+        self._chain_pending = a
 
         # ---- residual blocks
         Xin = X0
@@ -350,6 +353,7 @@ class FusedResNet:
             Xin, xa, xs, info = self._block_fwd(i, b, nxt, Xin, xa, xs, fwd, L, obs)
             saved.append(info)
         Ylast = Xin
+        self._flush_chain(fwd, L)
 
         # ---- head: avg pool, dense, loss -- as separate launches (forward / compute_loss /
         # backward called one by one) and as ONE fused launch (train_fwd_bwd, the training step)
@@ -566,9 +570,7 @@ class FusedResNet:
         qn1 = self._buf(k + "qn1", shp, torch.int8)
         chs1 = self._sums(k + "chs1", ops.NSHARD * 2 * C)
         obs(b.n1.X_range, numel)
-        fwd.append(L(self._fn(c1, "lbt_conv_fwd_i8"), ptr(xa), 1, self._wf(c1), c1.ksf, ptr(c1.wcolsum), d1, self._qd(c1.X_range),
-                     c1.W_range.desc, None, ptr(qn1), self._qd(b.n1.X_range), ptr(chs1), k="conv_gemm_kernel<0> (fwd)",
-                     nb=xa.numel() + c1.wf.numel() + qn1.numel()))
+        self._conv_fwd(fwd, L, c1, d1, xa, qn1, b.n1.X_range, chs1)
         R1 = self._buf(k + "R1", shp, torch.int8)
         xb = self._buf(k + "xb", shp, torch.int8)
         obs(b.r1.X_range, numel)
@@ -577,13 +579,12 @@ class FusedResNet:
                              q1=c2.X_range)
         if self.sync_bn:
             fwd.append(self._allreduce(chs1))
-        fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a1), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a1)))
+        self._flush_chain(fwd, L)
+        self._chain_pending = a1
         qn2 = self._buf(k + "qn2", shp, torch.int8)
         chs2 = self._sums(k + "chs2", ops.NSHARD * 2 * C)
         obs(b.n2.X_range, numel)
-        fwd.append(L(self._fn(c2, "lbt_conv_fwd_i8"), ptr(xb), 1, self._wf(c2), c2.ksf, ptr(c2.wcolsum), d2, self._qd(c2.X_range),
-                     c2.W_range.desc, None, ptr(qn2), self._qd(b.n2.X_range), ptr(chs2), k="conv_gemm_kernel<0> (fwd)",
-                     nb=xb.numel() + c2.wf.numel() + qn2.numel()))
+        self._conv_fwd(fwd, L, c2, d2, xb, qn2, b.n2.X_range, chs2)
         ds = qns = chss = Rs = None
         if cs is not None:
             ds = ops.conv_desc(N, H, W, Cin, C, 1, 1, s, s, cs.padding)
@@ -591,9 +592,7 @@ class FusedResNet:
             qns = self._buf(k + "qns", shp, torch.int8)
             chss = self._sums(k + "chss", ops.NSHARD * 2 * C)
             obs(b.ns.X_range, numel)
-            fwd.append(L(self._fn(cs, "lbt_conv_fwd_i8"), ptr(xs), 1, self._wf(cs), cs.ksf, ptr(cs.wcolsum), ds, self._qd(cs.X_range),
-                         cs.W_range.desc, None, ptr(qns), self._qd(b.ns.X_range), ptr(chss), k="conv_gemm_kernel<0> (fwd)",
-                         nb=xs.numel() + cs.wf.numel() + qns.numel()))
+            self._conv_fwd(fwd, L, cs, ds, xs, qns, b.ns.X_range, chss)
             Rs = self._buf(k + "Rs", shp, torch.int8)
             obs(b.rs.X_range, numel)
         R2 = self._buf(k + "R2", shp, torch.int8)
@@ -614,7 +613,8 @@ class FusedResNet:
             fwd.append(self._allreduce(chs2))
             if chss is not None:
                 fwd.append(self._allreduce(chss))
-        fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a2), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a2)))
+        self._flush_chain(fwd, L)
+        self._chain_pending = a2
         self._keep += [a1, a2]
         info = dict(Xin=Xin, xa=xa, xs=xs, d1=d1, d2=d2, ds=ds, qn1=qn1, R1=R1, xb=xb, qn2=qn2, R2=R2, qns=qns,
                     Rs=Rs, Y=Y, shp=shp, C=C, Cin=Cin)
@@ -644,11 +644,49 @@ class FusedResNet:
         self._keep.append(a)
         return dict(a=a, Gn2=Gn2, sums2=sums2, gm=gm, Gns=Gns, sumss=sumss)
 
-    def _fusable_bwd(self, c, d):
-        """lbt_conv_bwd_fused_i8 takes this conv: stride-1 3x3 SAME, Cin = Cout, W*C = 512."""
-        return (self.fuse_bwd and c.mfma and d.KH == 3 and d.KW == 3 and d.SH == 1 and d.SW == 1 and d.PT == 1
+    def _flush_chain(self, fwd, L):
+        """Launch the pending forward chain on its own (the next launch does not absorb it)."""
+        a = self._chain_pending
+        if a is None:
+            return
+        self._chain_pending = None
+        fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a)))
+
+    def _conv_fwd(self, fwd, L, c, d, xq, yq, qout, chs):
+        """Append conv c's forward (quantising epilogue yq / qout / chs): one lbt_conv_fwd_fused_i8 with
+        the pending chain when that chain produces exactly this conv's input, else the chain's own
+        launch (if any) and lbt_conv_fwd_i8."""
+        a = self._chain_pending
+        if (a is not None and self.fuse_fwd and self._fusable_bwd(c, d, flag=True) and a.o1 == xq.data_ptr()
+                and not a.o2):
+            cf = ConvFwd()
+            cf.c = a
+            cf.wf = self._wf(c).value
+            cf.ksf = c.ksf
+            cf.w4 = 1 if getattr(c, "w4", False) else 0
+            cf.wcolsum = c.wcolsum.data_ptr()
+            cf.d = d
+            cf.qw = c.W_range.desc
+            cf.yq = yq.data_ptr()
+            cf.qout = self._qd(qout)
+            cf.ychsum = chs.data_ptr()
+            nq = (2 if a.has_b2 else 1) + 2  # noise tables: R quantiser(s), X, output
+            nb = ops._chain_fwd_bytes(a) + c.wf.numel() + yq.numel() + 4 * nq * a.inner
+            fwd.append(L("lbt_conv_fwd_fused_i8", ctypes.byref(cf), k="conv_fwd_kernel", nb=nb))
+            self._keep.append(cf)
+            self._chain_pending = None
+            return
+        self._flush_chain(fwd, L)
+        fwd.append(L(self._fn(c, "lbt_conv_fwd_i8"), ptr(xq), 1, self._wf(c), c.ksf, ptr(c.wcolsum), d, self._qd(c.X_range),
+                     c.W_range.desc, None, ptr(yq), self._qd(qout), ptr(chs), k="conv_gemm_kernel<0> (fwd)",
+                     nb=xq.numel() + c.wf.numel() + yq.numel()))
+
+    def _fusable_bwd(self, c, d, flag=None):
+        """lbt_conv_bwd_fused_i8 / lbt_conv_fwd_fused_i8 take this conv: stride-1 3x3 SAME, Cin = Cout,
+        W*C = 512 (flag: the switch to honour, default fuse_bwd)."""
+        return ((self.fuse_bwd if flag is None else flag) and c.mfma and d.KH == 3 and d.KW == 3 and d.SH == 1 and d.SW == 1 and d.PT == 1
                 and d.PB == 1 and d.PL == 1 and d.PR == 1 and d.Cin == d.Cout and d.Cin in (16, 32, 64)
-                and d.H % 4 == 0 and d.W * d.Cin == 512)
+                and d.H % (8 if d.Cin == 16 else 4) == 0 and d.W * d.Cin == 512)
 
     def _flush_pending(self, bwd, L):
         """Run the deferred wgrad job on its own (the next launch is not a fused conv backward)."""

@@ -728,9 +728,10 @@ def test_head_kernel_equals_launch_sequence(N, HW, C, K, table):
 @pytest.mark.parametrize("B,w4", [(32, False), (128, False), (32, True)])
 def test_fused_conv_backward_equals_launch_pair(B, w4):
     """lbt_conv_bwd_fused_i8 (pass B + dgrad + pass A in one launch per stride-1 3x3 conv, each
-    conv's wgrad deferred into the next such launch) == the chain_bwd_b / dgrad_wgrad launches it
-    replaces: gradients, momentum, weights, exponents and BN running statistics bit-identical after
-    two optimiser steps (eager, then graph replay)."""
+    conv's wgrad deferred into the next such launch) and lbt_conv_fwd_fused_i8 (the BN chain that
+    produces a conv's input run inside the conv launch) == the chain_bwd_b / dgrad_wgrad and
+    chain_fwd / conv_fwd launches they replace: gradients, momentum, weights, exponents and BN running
+    statistics bit-identical after two optimiser steps (eager, then graph replay)."""
     from lbt_amd.fused import FusedResNet
     from lbt_amd.models import CIFAR10_Resnet20
     from lbt_amd.trainer import Trainer
@@ -738,13 +739,15 @@ def test_fused_conv_backward_equals_launch_pair(B, w4):
     for fb in (False, True):
         ctx = DfxpContext(seed=4)
         m = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, weight_bits=4 if w4 else None))
-        m.fuse_bwd = fb
+        m.fuse_bwd = m.fuse_fwd = fb
         tr = Trainer(m, lr=1e-2, momentum=0.9, batch_size=B, use_graph=fb)
         for i in range(2):
             x, y = synthetic_batch(B, seed=30 + i)
             tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
         torch.cuda.synchronize()
         nf = sum(1 for f in m._bwd if getattr(f, "kname", "") == "conv_bwd_kernel")
+        assert nf == (16 if fb else 0), nf
+        nf = sum(1 for f in m._fwd if getattr(f, "kname", "") == "conv_fwd_kernel")
         assert nf == (16 if fb else 0), nf
         bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
         outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,
