@@ -229,6 +229,11 @@ def main():
         tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                           "pmc_traffic_resnet50.json" if r50 else "pmc_traffic.json")
         out["roofline"] = measure_dominant(trainer, xs[0], ys[0], traffic_file=tf)
+        sb = out["roofline"].get("step_algorithmic_bytes")
+        if sb:  # the whole step against the same roofline: algorithmic bytes per step / step time
+            gbs = sb / (el / args.steps) / 1e9
+            out["roofline"]["step"] = {"achieved": round(gbs, 1), "frac": round(gbs / out["roofline"]["peak"], 4),
+                                       "algorithmic_bytes": sb, "ms_per_step": out["ms_per_step"]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_r50(args.cpu_seconds) if r50 else cpu_baseline(args.cpu_seconds, args.batch)
     if rank == 0:

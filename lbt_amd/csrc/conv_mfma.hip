@@ -1125,18 +1125,22 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
       hipLaunchKernelGGL((conv_bwd_kernel<CS_, CF_, NB_, false, WCS_>), grid, dim3(kBThreads), 0, st, p, wa, wblocks); \
     return (int)hipGetLastError();                                                                 \
   }
+  // (WCS = 0 everywhere: the plan's LBT_SIDE_WGRAD mode runs each wgrad as a parallel branch)
 #define LBT_BW_CS(CS_)                                          \
   LBT_BW(CS_, kAFused | kAMaskR, 1, 0)                          \
   LBT_BW(CS_, kAFused | kAMaskR, 1, CS_)                        \
+  LBT_BW(CS_, kAFused | kAYMask | kAGmask, 1, 0)                \
   LBT_BW(CS_, kAFused | kAYMask | kAGmask, 1, CS_)              \
-  LBT_BW(CS_, kAFused | kAYMask, 2, CS_)                        \
-  LBT_BW(CS_, kAFused | kAYMask, 1, CS_)
-  LBT_BW(1, kAFused | kAMaskR, 1, 0)
-  LBT_BW(1, kAFused | kAMaskR, 1, 1)
-  LBT_BW(1, kAFused | kAYMask | kAGmask, 1, 1)
-  LBT_BW(1, kAFused | kAYMask, 1, 1)
+  LBT_BW(CS_, kAFused | kAYMask, 2, 0)                          \
+  LBT_BW(CS_, kAFused | kAYMask, 2, CS_)
+  LBT_BW_CS(1)
   LBT_BW_CS(2)
   LBT_BW_CS(4)
+  LBT_BW(1, kAFused | kAYMask, 1, 0)
+  LBT_BW(1, kAFused | kAYMask, 1, 1)
+  // a stage's last c2 carrying the wgrad of the next stage's c2 (across the projection block)
+  LBT_BW(1, kAFused | kAMaskR, 1, 2)
+  LBT_BW(2, kAFused | kAMaskR, 1, 4)
 #undef LBT_BW_CS
 #undef LBT_BW
   return LBT_EINVAL;

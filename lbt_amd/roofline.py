@@ -138,7 +138,11 @@ def measure_dominant_graph(trainer, traffic_file=None):
         r[1] += t
         r[2] += f.nbytes
     stats = {k: (n, t / n, b / n, t) for k, (n, t, b) in fam.items()}
-    return _dominant(stats, traffic_file, "graph replay, each launch captured 20x in isolation")
+    out = _dominant(stats, traffic_file, "graph replay, each launch captured 20x in isolation")
+    out["step_algorithmic_bytes"] = int(sum(f.nbytes for f in launches))
+    out["step_launches"] = len(launches)
+    out["step_kernel_us_isolated"] = round(sum(us), 1)
+    return out
 
 
 def measure_dominant(trainer, x, y, traffic_file=None):

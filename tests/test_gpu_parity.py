@@ -747,7 +747,7 @@ def test_fused_conv_backward_equals_launch_pair(B, w4):
         torch.cuda.synchronize()
         nf = sum(1 for f in m._bwd if getattr(f, "kname", "") == "conv_bwd_kernel")
         assert nf == (16 if fb else 0), nf
-        nf = sum(1 for f in m._fwd if getattr(f, "kname", "") == "conv_fwd_kernel")
+        nf = sum(1 for f in m._fwd if getattr(f, "kname", "") == "conv_fwd_fused_kernel")
         assert nf == (16 if fb else 0), nf
         bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
         outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,

@@ -47,6 +47,15 @@ def main():
         tot += us
         print("%3d %8.2f  %s" % (i, us, f.kname))
     print("sum %.1f us over %d launches" % (tot, len(launches)))
+    # the whole step, graph-replayed back to back (what bench.py times)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        tr.step(xs[0], ys[0])
+    e1.record()
+    e1.synchronize()
+    print("step %.1f us (graph replay, 50 steps)" % (1000.0 * e0.elapsed_time(e1) / 50))
 
 
 if __name__ == "__main__":
