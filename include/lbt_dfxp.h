@@ -374,6 +374,13 @@ typedef struct lbt_wgrad_job {
   int32_t* slab; int32_t nsplit, nshard;
 } lbt_wgrad_job;
 
+/* lbt_conv_wgrad_i8 for njobs convs in ONE launch (Conv2d_q.backward's dW pass 1,
+ * dynamic_fixed_point.py:302, of every conv of a step): jobs is a HOST array, each entry exactly
+ * the arguments of one lbt_conv_wgrad_i8 call (Cin = 16, 32 or 64; slab != NULL); the results are
+ * those of the njobs calls (integer atomics into each job's slab). Every job is checked before
+ * anything is queued.                                                                          */
+int lbt_conv_wgrad_many_i8(const lbt_wgrad_job* jobs, int32_t njobs, void* stream);
+
 /* One stride-1 3x3 Conv2d_q's backward in ONE launch, with the BN backward passes on either side
  * (Conv2d_q.backward dynamic_fixed_point.py:299-305 between Normalization_q.backward :620-623 of
  * the BN it feeds and the BN it consumes):

@@ -167,6 +167,7 @@ _SIGS = {
     "lbt_conv_dgrad_chain_wgrad_i8w4": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int32, _P, c_int32,
                                         c_int32, _P],
     "lbt_conv_wgrad_i8": [_P, c_int32, _P, ConvDesc, _P, c_int32, c_int32, _P],
+    "lbt_conv_wgrad_many_i8": [_P, c_int32, _P],
     "lbt_conv_wgrad_reduce": [_P, c_int32, c_int32, c_int32, c_int32, _P, QDesc, QDesc, _P, c_float, _P, _P],
     "lbt_conv_fwd_generic": [_P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_conv_dgrad_generic": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, _P],

@@ -653,6 +653,221 @@ extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t
   return (int)hipGetLastError();
 }
 
+// ---- many convs' weight gradients in ONE launch (lbt_conv_wgrad_many_i8): the jobs travel in the
+// kernel arguments; job j owns blocks [start[j], start[j+1]) (multiples of 8: each job keeps its
+// XCD-aware unit order). 3x3 / stride-1 / SAME jobs whose image rows tile 64-pixel chunks run
+// wgrad_s1_body, the others conv_wgrad_body (one unit = pixel split x tap x co slice).
+//
+// wgrad_s1_body: workgroup = (pixel split, ci slice, co slice) of kFW waves. A wave takes 64
+// consecutive output pixels at a time (whole image rows: 64 % W == 0, H % (64 / W) == 0), stages the
+// X slices of those rows plus a one-pixel halo ([64/W + 2][W + 2][16 B], the fill code outside the
+// image) and the 64 G slices in its own LDS region, and runs all 9 taps' MFMAs from there with
+// per-lane transposed reads: X and G leave L2 once per (ci, co) slice pair instead of once per tap,
+// and the next chunk's loads are in flight during the MFMAs. The waves' partials are summed in
+// LDS and added into the job's slab (shard = split % nshard) with one integer atomic per output.
+namespace {
+constexpr int kMaxWJobs = 24;
+constexpr int kFW = 8;        // waves per workgroup of the batched launch
+constexpr int kHaloMax = 3;   // halo slices per lane: (64/W + 2) * (W + 2) <= 192 (W | 64, 2 <= W <= 32)
+struct WgradMany {
+  WgradArgs j[kMaxWJobs];
+  uint32_t start[kMaxWJobs + 1];
+  int32_t fast[kMaxWJobs];
+  int n;
+};
+union WgradManyShared {
+  WgradShared<1, kFW> s1;
+  WgradShared<2, kFW> s2;
+  int8_t stage[kFW][5 * 1024];               // wgrad_s1_body: per wave X halo | G (at +4096)
+  int red[kFW][9 * 256];                      // wgrad_s1_body: per wave partials [tap][kg][r][4]
+};
+
+bool wgrad_s1_ok(const lbt_conv_desc& d, int nsplit) {
+  if (d.KH != 3 || d.KW != 3 || d.SH != 1 || d.SW != 1 || d.PT != 1 || d.PB != 1 || d.PL != 1 || d.PR != 1 ||
+      d.Ho != d.H || d.Wo != d.W || d.W > 64 || 64 % d.W || d.H % (64 / d.W) ||
+      (64 / d.W + 2) * (d.W + 2) > 64 * kHaloMax)
+    return false;
+  const int64_t chunks = (int64_t)d.N * d.H * d.W / 64;
+  return nsplit > 0 && chunks % nsplit == 0;
+}
+
+LBT_DEV v4i tr_frag_at(const int8_t* img, int oa, int ob) {
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(img + oa));
+  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(img + ob));
+  return v4i{lo.x, lo.y, hi.x, hi.y};
+}
+
+__device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid, WgradManyShared& sm) {
+  const lbt_conv_desc& d = wa.d;
+  const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
+  const int ncs = Cin >> 4, ncos = Cout >> 4, nsplit = wa.nsplit;
+  const int total = nsplit * ncs * ncos;
+  const int xchunk = (total + 7) >> 3;
+  const int u = (int)(bid & 7) * xchunk + (int)(bid >> 3);  // XCD-aware: a split's slices share an L2
+  if (u >= total) return;
+  const int split = u / (ncs * ncos), urem = u - split * (ncs * ncos);
+  const int cis = urem / ncos, cos = urem - cis * ncos;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 15, kg = lane >> 4;
+  const int RB = 64 / W, Wp = W + 2, nhalo = (RB + 2) * Wp;
+  const int64_t cps = (int64_t)d.N * H * W / 64 / nsplit;  // chunks per split (exact: host check)
+  const int64_t c0 = (int64_t)split * cps;
+  const int nmine = cps > wave ? (int)((cps - wave + kFW - 1) / kFW) : 0;
+  const int HW = H * W;
+  const int fill = wa.x_fill;
+  int8_t* st = sm.stage[wave];
+  int8_t* gs = st + 4096;
+  // per-lane transposed-read offsets (chunk-invariant): pixels pa = 16kg + j/2 and pa + 8
+  const int pa = 16 * kg + (j >> 1), pb = pa + 8;
+  const int oxa = ((pa / W) * Wp + pa % W) * 16 + 8 * (j & 1);
+  const int oxb = ((pb / W) * Wp + pb % W) * 16 + 8 * (j & 1);
+  const int oga = pa * 16 + 8 * (j & 1), ogb = pb * 16 + 8 * (j & 1);
+
+  // two register buffers: chunk s + 2's loads are issued while chunk s is computed (s + 1's are
+  // already in flight), so a wave waits on a load issued two chunks earlier
+  struct Buf {
+    v4i x[kHaloMax], g;
+    uint32_t valid;
+  };
+  auto load = [&](Buf& b, int64_t c) {
+    const int64_t p0 = c * 64;
+    const int n = (int)(p0 / HW), row0 = (int)(p0 - (int64_t)n * HW) / W;
+    const int8_t* xim = wa.xq + (int64_t)n * HW * Cin + cis * 16;
+    b.valid = 0;
+#pragma unroll
+    for (int i = 0; i < kHaloMax; ++i) {
+      const int t = lane + 64 * i;
+      const int hy = t / Wp, hx = t - hy * Wp;
+      const int y = row0 - 1 + hy, x = hx - 1;
+      const bool v = t < nhalo && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      b.valid |= (uint32_t)v << i;
+      b.x[i] = *reinterpret_cast<const v4i*>(xim + (v ? (int64_t)(y * W + x) * Cin : 0));
+    }
+    b.g = *reinterpret_cast<const v4i*>(wa.gq + (p0 + lane) * Cout + cos * 16);
+  };
+  v4i acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = v4i{0, 0, 0, 0};
+  // chunk s of this wave: stage b into LDS, refill b with chunk s + 2, MFMAs of all 9 taps
+  auto step = [&](Buf& b, int s) {
+#pragma unroll
+    for (int i = 0; i < kHaloMax; ++i) {
+      const int t = lane + 64 * i;
+      const v4i v = (b.valid >> i) & 1 ? b.x[i] : v4i{fill, fill, fill, fill};
+      if (t < nhalo) *reinterpret_cast<v4i*>(st + t * 16) = v;
+    }
+    *reinterpret_cast<v4i*>(gs + lane * 16) = b.g;
+    // the images are read by other lanes of the same wave only
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (s + 2 < nmine) load(b, c0 + wave + (int64_t)(s + 2) * kFW);
+    const v4i bfrag = tr_frag_at(gs, oga, ogb);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = ((t / 3) * Wp + t % 3) * 16;
+      const v4i afrag = tr_frag_at(st, oxa + toff, oxb + toff);
+      acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag, bfrag, acc[t], 0, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  LBT_TS(0);
+  Buf b0, b1;
+  if (nmine > 0) load(b0, c0 + wave);
+  if (nmine > 1) load(b1, c0 + wave + kFW);
+  for (int s = 0; s < nmine; s += 2) {
+    step(b0, s);
+    if (s + 1 < nmine) step(b1, s + 1);
+  }
+  LBT_TS(1);
+  __syncthreads();  // the partials overwrite the staging regions
+  // acc[t] element i: ci = 4kg + i, co = j (16x16 C/D map)
+#pragma unroll
+  for (int t = 0; t < 9; ++t) *reinterpret_cast<v4i*>(&sm.red[wave][(t * 64 + lane) * 4]) = acc[t];
+  __syncthreads();
+  LBT_TS(2);
+  int32_t* dst = wa.slab + (int64_t)(split % wa.nshard) * 9 * Cin * Cout + (int64_t)cis * 16 * Cout + cos * 16;
+  for (int i = threadIdx.x; i < 9 * 256; i += kFW * 64) {
+    int v = 0;
+#pragma unroll
+    for (int w = 0; w < kFW; ++w) v += sm.red[w][i];
+    const int t = i >> 8, l = (i >> 2) & 63, ii = i & 3;
+    const int ci = 4 * (l >> 4) + ii, co = l & 15;
+    if (v) LBT_GADD(&dst[((int64_t)t * Cin + ci) * Cout + co], v);  // integer atomics: exact, order-independent
+  }
+  LBT_TS(3);
+}
+
+__global__ __launch_bounds__(kFW * 64, 4) void conv_wgrad_many_kernel(const WgradMany m) {
+  __shared__ __attribute__((aligned(16))) WgradManyShared sm;
+  const uint32_t b = blockIdx.x;
+  int j = 0;
+#pragma unroll 1
+  while (j + 1 < m.n && b >= m.start[j + 1]) ++j;
+  const WgradArgs& wa = m.j[j];
+  const uint32_t rb = b - m.start[j];
+#ifdef LBT_TRACE
+  if (threadIdx.x == 0 && lbt_trace_buf) lbt_trace_buf[(size_t)blockIdx.x * 8 + 6] = (unsigned long long)(j + 1);
+#endif
+  if (m.fast[j]) {
+    wgrad_s1_body(wa, rb, sm);
+    return;
+  }
+  switch (wa.d.Cin >> 4) {
+    case 1: conv_wgrad_body<1, kFW>(wa, rb, sm.s1); break;
+    default: conv_wgrad_body<2, kFW>(wa, rb, sm.s2); break;
+  }
+}
+static_assert(sizeof(WgradMany) <= 4096, "kernel arguments");
+
+// WgradArgs + block count of one job of the batched launch
+int wgrad_many_setup(const lbt_wgrad_job& w, WgradArgs& wa, uint32_t& blocks, int32_t& fast) {
+  if (!w.slab || !w.xq || !w.gq) return LBT_EINVAL;
+  const int e = wgrad_setup(w.xq, w.x_u8off, w.gq, w.d, w.slab, w.nsplit, w.nshard, wa, blocks);
+  if (e) return e;
+  fast = wgrad_s1_ok(w.d, w.nsplit) ? 1 : 0;
+  if (fast) {
+    const int64_t units = (int64_t)w.nsplit * (w.d.Cin / 16) * (w.d.Cout / 16);
+    blocks = (uint32_t)((units + 7) / 8 * 8);
+  } else if (w.d.Cin != 16 && w.d.Cin != 32) {
+    return LBT_EINVAL;  // conv_wgrad_body<CSI, kFW> instances: CSI 1, 2
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" int lbt_conv_wgrad_many_i8(const lbt_wgrad_job* jobs, int32_t njobs, void* stream) {
+  if (njobs < 0 || (njobs > 0 && !jobs)) return LBT_EINVAL;
+  for (int i = 0; i < njobs; ++i) {  // every job checked before anything is queued
+    WgradArgs wa;
+    uint32_t blocks = 0;
+    int32_t fast = 0;
+    const int e = wgrad_many_setup(jobs[i], wa, blocks, fast);
+    if (e) return e;
+  }
+  for (int base = 0; base < njobs; base += kMaxWJobs) {
+    WgradMany m{};
+    const int n = njobs - base < kMaxWJobs ? njobs - base : kMaxWJobs;
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) {
+      uint32_t blocks = 0;
+      wgrad_many_setup(jobs[base + i], m.j[i], blocks, m.fast[i]);
+      m.start[i] = (uint32_t)total;
+      total += blocks;
+    }
+    if (total >= 0x7fffffffull) return LBT_EINVAL;
+    m.start[n] = (uint32_t)total;
+    m.n = n;
+    hipLaunchKernelGGL(conv_wgrad_many_kernel, dim3((unsigned)total), dim3(kFW * 64), 0, (hipStream_t)stream, m);
+    const int rc = (int)hipGetLastError();
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 extern "C" int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int32_t x_u8off,
                                      const int64_t* gcolsum, lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2,
                                      float* dw, void* stream) {

@@ -1,6 +1,7 @@
 """Typed wrappers over the C-ABI (include/lbt_dfxp.h). Tensors in, kernels launched on the
 current torch stream, nothing synchronised. All shape logic of the HIP path lives here."""
 import math
+import os
 
 import torch
 
@@ -195,6 +196,33 @@ def wgrad_nsplit(d, generic=False):
     return max(lo, min(want, max(1, P // 512)))
 
 
+def wgrad_s1_ok(d):
+    """lbt_conv_wgrad_many_i8's staged 3x3 / stride-1 body takes this conv (64-pixel chunks of
+    whole image rows); mirrors wgrad_s1_ok in conv_mfma.hip."""
+    return (d.KH == 3 and d.KW == 3 and d.SH == 1 and d.SW == 1 and d.PT == 1 and d.PB == 1 and d.PL == 1
+            and d.PR == 1 and d.Ho == d.H and d.Wo == d.W and d.W <= 64 and 64 % d.W == 0
+            and d.H % (64 // d.W) == 0 and (64 // d.W + 2) * (d.W + 2) <= 192)
+
+
+WGRAD_CPW = int(os.environ.get("LBT_WGRAD_CPW", "8"))  # batched staged wgrad: 64-pixel chunks per wave
+WGRAD_UNITS = int(os.environ.get("LBT_WGRAD_UNITS", "128"))  # batched per-tap wgrad: workgroups per conv
+
+
+def wgrad_nsplit_batched(d, chunks_per_wave=None):
+    """Pixel splits of a conv's wgrad inside the batched launch (8-wave workgroups). Staged 3x3
+    body: each split = 8 waves x `chunks_per_wave` 64-pixel chunks, a divisor of the chunk count.
+    Other convs: ~128 workgroups (split x tap x co slice) per conv."""
+    P = d.N * d.Ho * d.Wo
+    if wgrad_s1_ok(d):
+        chunks = P // 64
+        ns = max(1, chunks // (8 * (chunks_per_wave or WGRAD_CPW)))
+        while chunks % ns:
+            ns -= 1
+        return ns
+    lo = -(-P // 65536)
+    return max(lo, min(max(1, WGRAD_UNITS // (d.KH * d.KW * (d.Cout // 16))), max(1, P // 512)))
+
+
 def wgrad_nshard(d, nsplit):
     """Shards of the MFMA wgrad slab: each covers <= 65536 pixels (int32-exact partial sums)."""
     P = d.N * d.Ho * d.Wo
@@ -202,9 +230,10 @@ def wgrad_nshard(d, nsplit):
     return -(-nsplit // max(1, 65536 // per))
 
 
-def wgrad_slab(cache, key, d, ctx):
-    """(nsplit, nshard, zeroed int32 slab [nshard, K, Cout]) carved from the context's sums arena."""
-    ns = wgrad_nsplit(d)
+def wgrad_slab(cache, key, d, ctx, batched=False):
+    """(nsplit, nshard, zeroed int32 slab [nshard, K, Cout]) carved from the context's sums arena
+    (batched: the split of the conv's job in lbt_conv_wgrad_many_i8)."""
+    ns = wgrad_nsplit_batched(d) if batched else wgrad_nsplit(d)
     nh = wgrad_nshard(d, ns)
     n = nh * d.KH * d.KW * d.Cin * d.Cout
     slab = cache.sums(key, (n + 1) // 2, ctx).view(torch.int32)[:n].view(nh, d.KH * d.KW * d.Cin, d.Cout)

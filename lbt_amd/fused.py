@@ -99,6 +99,13 @@ class FusedResNet:
         # (measured a loss: 0.78 -> 1.02 ms per step -- graph branches do not overlap here)
         self.side_wgrad = os.environ.get("LBT_SIDE_WGRAD", "0") == "1"
         self._side = None
+        # every conv's weight gradient of the step in ONE launch at the end of the backward
+        # (lbt_conv_wgrad_many_i8) instead of inside the dgrad launches: a dgrad launch's tiles fill
+        # every workgroup slot of the chip, so wgrad workgroups in the same grid ran as extra rounds
+        # ahead of them (measured per-workgroup: +6..10 us on each of 14 launches)
+        self.batch_wgrad = (os.environ.get("LBT_BATCH_WGRAD", "1") == "1" and not self.overlap_wgrad
+                            and not self.side_wgrad)
+        self._wbatch = []  # the batched launch's jobs (lbt_wgrad_job), in backward order
 
     # ------------------------------------------------------------------ Trainer interface
     def param_slots(self):
@@ -423,6 +430,7 @@ class FusedResNet:
 
         # ---- stem backward (d loss / d image is never needed)
         self._flush_pending(bwd, L)
+        self._flush_wbatch(bwd, L)
         if gY is not None:  # pass A not fused into block 0's dgrad
             aA.g = gY.data_ptr()
             bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
@@ -692,6 +700,26 @@ class FusedResNet:
                 and d.PB == 1 and d.PL == 1 and d.PR == 1 and d.Cin == d.Cout and d.Cin in (16, 32, 64)
                 and d.H % (8 if d.Cin == 16 else 4) == 0 and d.W * d.Cin == 512)
 
+    def _wgrad(self, bwd, L, xq, gq, d, slab, nsplit, nshard, nb):
+        """One conv's weight gradient (pass 1 into its slab): a job of the end-of-backward batched
+        launch, or its own lbt_conv_wgrad_i8 launch (on the side stream in overlap mode)."""
+        if self.batch_wgrad:
+            w = self._wjob(xq, gq, d, slab, nsplit, nshard)
+            w._nb = nb
+            self._wbatch.append(w)
+            return
+        bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(xq), 1, ptr(gq), d, ptr(slab), nsplit, nshard,
+                                   k="conv_wgrad_kernel", nb=nb)))
+
+    def _flush_wbatch(self, bwd, L):
+        """The batched weight-gradient launch of every job collected so far."""
+        jobs, self._wbatch = self._wbatch, []
+        if not jobs:
+            return
+        arr = (WgradJob * len(jobs))(*jobs)
+        self._keep.append(arr)
+        bwd.append(L("lbt_conv_wgrad_many_i8", arr, len(jobs), k="conv_wgrad_many_kernel", nb=sum(w._nb for w in jobs)))
+
     def _flush_pending(self, bwd, L):
         """Run the deferred wgrad job on its own (the next launch is not a fused conv backward)."""
         w = self._pending
@@ -714,6 +742,13 @@ class FusedResNet:
         cb.add_src = add.data_ptr() if add is not None else None
         cb.a = aA
         nbw = 0
+        if self.batch_wgrad:  # this conv's wgrad joins the end-of-backward batch
+            nb = (ops._chain_bwd_b_bytes(aB) + 4 * aB.inner
+                  + ops._dgrad_chain_bytes(0, c.wd.numel(), aA, add is not None))
+            bwd.append(L("lbt_conv_bwd_fused_i8", ctypes.byref(cb), k="conv_bwd_kernel", nb=nb))
+            self._keep.append(cb)
+            self._wbatch.append(wjob)
+            return
         if self.side_wgrad:  # this conv's wgrad as a parallel branch: nothing deferred
             nb = (ops._chain_bwd_b_bytes(aB) + 4 * aB.inner
                   + ops._dgrad_chain_bytes(0, c.wd.numel(), aA, add is not None))
@@ -785,7 +820,7 @@ class FusedResNet:
         Gn1 = self._buf(k + "Gn1", shp, torch.int8)
         sums1 = self._sums(k + "sums1", ops.NSHARD * 4 * C)
         nb_dg2 = gq2.numel() + c2.wd.numel()
-        sp2, ns2, slab2 = ops.wgrad_slab(self._c, k + "slab2", d2, self.ctx)
+        sp2, ns2, slab2 = ops.wgrad_slab(self._c, k + "slab2", d2, self.ctx, batched=self.batch_wgrad)
         nb_wg2 = f["xb"].numel() + gq2.numel() + 4 * slab2.numel()
         if fb2:  # pass B (bn2) + dgrad + pass A (bn1) in one launch, conv-2 wgrad deferred
             if cs is not None:  # the shortcut BN's pass B (its conv is not fused) goes first
@@ -796,7 +831,7 @@ class FusedResNet:
         elif fuse:
             aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
             nb = ops._dgrad_chain_bytes(gq2.numel(), c2.wd.numel(), aA1, False)
-            if self.fuse_wgrad:  # conv-2 wgrad in the same launch
+            if self.fuse_wgrad and not self.batch_wgrad:  # conv-2 wgrad in the same launch
                 bwd.append(L(self._fn(c2, "lbt_conv_dgrad_chain_wgrad_i8"), ptr(gq2), self._wd(c2), c2.ksd, d2,
                              self._qd(c2.grad_range), c2.W_range.desc, None, ctypes.byref(aA1), ptr(f["xb"]), 1,
                              ptr(slab2), sp2, ns2, k="dgrad_wgrad_kernel", nb=nb + nb_wg2 - gq2.numel()))
@@ -810,9 +845,8 @@ class FusedResNet:
                          c2.W_range.desc, ptr(d1g), None, k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg2 + 4 * numel))
             aA1 = self._chain_bwd_a(d1g, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
         keep.append(aA1)
-        if not (fuse and self.fuse_wgrad) and not fb2:
-            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xb"]), 1, ptr(gq2), d2, ptr(slab2), sp2, ns2,
-                                       k="conv_wgrad_kernel", nb=nb_wg2)))
+        if not (fuse and self.fuse_wgrad and not self.batch_wgrad) and not fb2:
+            self._wgrad(bwd, L, f["xb"], gq2, d2, slab2, sp2, ns2, nb_wg2)
         rjobs.append(RJob(slab2.data_ptr(), ns2, 9 * C, C, 1, gcol2.data_ptr(), self._qd(c2.X_range),
                           self._qd(c2.grad_range), c2.W.data_ptr(), ops.f32(2 * c2.weight_decay), c2.dW.data_ptr()))
         if not fuse:
@@ -837,13 +871,13 @@ class FusedResNet:
         nin = math.prod(f["Xin"].shape)
         nb_dg1 = gq1.numel() + c1.wd.numel() + 8 * nin
         gin = None
-        sp1, ns1, slab1 = ops.wgrad_slab(self._c, k + "slab1", d1, self.ctx)
+        sp1, ns1, slab1 = ops.wgrad_slab(self._c, k + "slab1", d1, self.ctx, batched=self.batch_wgrad)
         nb_wg1 = f["xa"].numel() + gq1.numel() + 4 * slab1.numel()
         if fb1:  # pass B (bn1) + dgrad (+ residual gradient) + the consumer's pass A, wgrad deferred
             self._conv_bwd(aB1, c1, d1, add, consumer["a"], bwd, L, self._wjob(f["xa"], gq1, d1, slab1, sp1, ns1))
         elif fuse:
             nb = ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], add is not None)
-            if self.fuse_wgrad:  # conv-1 wgrad in the same launch
+            if self.fuse_wgrad and not self.batch_wgrad:  # conv-1 wgrad in the same launch
                 bwd.append(L(self._fn(c1, "lbt_conv_dgrad_chain_wgrad_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1,
                              self._qd(c1.grad_range), c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]),
                              ptr(f["xa"]), 1, ptr(slab1), sp1, ns1, k="dgrad_wgrad_kernel",
@@ -856,15 +890,13 @@ class FusedResNet:
             gin = self._buf(k + "gin", f["Xin"].shape, torch.float32)
             bwd.append(L(self._fn(c1, "lbt_conv_dgrad_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1, self._qd(c1.grad_range),
                          c1.W_range.desc, ptr(gin), ptr(add), k="conv_gemm_kernel<1> (dgrad)", nb=nb_dg1))
-        if not (fuse and self.fuse_wgrad) and not fb1:
-            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xa"]), 1, ptr(gq1), d1, ptr(slab1), sp1, ns1,
-                                       k="conv_wgrad_kernel", nb=nb_wg1)))
+        if not (fuse and self.fuse_wgrad and not self.batch_wgrad) and not fb1:
+            self._wgrad(bwd, L, f["xa"], gq1, d1, slab1, sp1, ns1, nb_wg1)
         rjobs.append(RJob(slab1.data_ptr(), ns1, 9 * Cin, C, 1, gcol1.data_ptr(), self._qd(c1.X_range),
                           self._qd(c1.grad_range), c1.W.data_ptr(), ops.f32(2 * c1.weight_decay), c1.dW.data_ptr()))
         if cs is not None:
-            sps, nss, slabs = ops.wgrad_slab(self._c, k + "slabs", ds, self.ctx)
-            bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(f["xs"]), 1, ptr(gqs), ds, ptr(slabs), sps, nss,
-                                       k="conv_wgrad_kernel", nb=f["xs"].numel() + gqs.numel() + 4 * slabs.numel())))
+            sps, nss, slabs = ops.wgrad_slab(self._c, k + "slabs", ds, self.ctx, batched=self.batch_wgrad)
+            self._wgrad(bwd, L, f["xs"], gqs, ds, slabs, sps, nss, f["xs"].numel() + gqs.numel() + 4 * slabs.numel())
             rjobs.append(RJob(slabs.data_ptr(), nss, Cin, C, 1, gcols.data_ptr(), self._qd(cs.X_range),
                               self._qd(cs.grad_range), cs.W.data_ptr(), ops.f32(2 * cs.weight_decay), cs.dW.data_ptr()))
         for r in (b.r1, b.r2) + ((b.rs,) if cs is not None else ()):

@@ -759,3 +759,65 @@ def test_fused_conv_backward_equals_launch_pair(B, w4):
     for u, v in zip(a[4], b[4]):
         assert np.array_equal(u, v)
     assert a[5] == b[5]
+
+
+# (N, H, W, Cin, Cout, k, s): the staged 3x3 / stride-1 body (W | 64, whole-row chunks) and the
+# per-tap body (strided / 1x1), mixed in one launch
+WGRAD_MANY_CASES = [(8, 32, 32, 16, 16, 3, 1), (8, 16, 16, 32, 32, 3, 1), (8, 8, 8, 64, 64, 3, 1),
+                    (8, 32, 32, 16, 32, 3, 2), (8, 32, 32, 16, 32, 1, 2), (4, 16, 16, 32, 64, 3, 2),
+                    (2, 4, 64, 16, 32, 3, 1), (3, 12, 8, 32, 16, 3, 1), (128, 8, 8, 64, 64, 3, 1)]
+
+
+def _wgrad_ref(x, g, d, fill):
+    """Exact int64 sum_p X_tap (x) G of a TF-SAME conv (x: int8 NHWC codes, out-of-image taps = fill)."""
+    N, H, W, Cin = x.shape
+    _, Ho, Wo, Cout = g.shape
+    xp = np.full((N, H + d.PT + d.PB + d.SH * 2, W + d.PL + d.PR + d.SW * 2, Cin), fill, np.int64)
+    xp[:, d.PT:d.PT + H, d.PL:d.PL + W] = x
+    out = np.zeros((d.KH, d.KW, Cin, Cout), np.int64)
+    gg = g.reshape(-1, Cout).astype(np.int64)
+    for kh in range(d.KH):
+        for kw in range(d.KW):
+            xt = xp[:, kh:kh + d.SH * Ho:d.SH, kw:kw + d.SW * Wo:d.SW][:, :Ho, :Wo].reshape(-1, Cin)
+            out[kh, kw] = xt.T @ gg
+    return out.reshape(-1, Cout)
+
+
+def test_wgrad_many_equals_single_launches():
+    """lbt_conv_wgrad_many_i8 (one launch, staged and per-tap bodies) == one lbt_conv_wgrad_i8 per
+    conv == the exact integer sum, shard totals compared (int32 partials, exact)."""
+    from lbt_amd._lib import WgradJob
+    rng = np.random.default_rng(5)
+    jobs, refs, singles, keep = [], [], [], []
+    for (N, H, W, Cin, Cout, k, s) in WGRAD_MANY_CASES:
+        d = ops.conv_desc(N, H, W, Cin, Cout, k, k, s, s, "SAME")
+        x = rng.integers(-128, 128, size=(N, H, W, Cin), dtype=np.int8)
+        g = rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout), dtype=np.int8)
+        xq, gq = torch.from_numpy(x).to(DEV), torch.from_numpy(g).to(DEV)
+        ns = ops.wgrad_nsplit_batched(d)
+        nh = ops.wgrad_nshard(d, ns)
+        slab = torch.zeros((nh, k * k * Cin, Cout), dtype=torch.int32, device=DEV)
+        keep += [xq, gq, slab]
+        jobs.append(WgradJob(xq.data_ptr(), 1, gq.data_ptr(), d, slab.data_ptr(), ns, nh))
+        refs.append((slab, _wgrad_ref(x, g, d, -128)))
+        ns1 = ops.wgrad_nsplit(d)
+        nh1 = ops.wgrad_nshard(d, ns1)
+        slab1 = torch.zeros((nh1, k * k * Cin, Cout), dtype=torch.int32, device=DEV)
+        ops.conv_wgrad_i8(xq, 1, gq, d, slab1, ns1, nh1)
+        singles.append(slab1)
+    arr = (WgradJob * len(jobs))(*jobs)
+    ops.call("lbt_conv_wgrad_many_i8", arr, len(jobs), ops.stream())
+    # more jobs than one launch carries (24): two launches, same sums
+    for slab, _ in refs:
+        slab.zero_()
+    arr3 = (WgradJob * (3 * len(jobs)))(*(jobs * 3))
+    ops.call("lbt_conv_wgrad_many_i8", arr3, 3 * len(jobs), ops.stream())
+    torch.cuda.synchronize()
+    for (slab, ref), slab1, case in zip(refs, singles, WGRAD_MANY_CASES):
+        got = slab.cpu().numpy().astype(np.int64).sum(0)
+        assert np.array_equal(got, 3 * ref), case
+        assert np.array_equal(slab1.cpu().numpy().astype(np.int64).sum(0), ref), case
+    bad = WgradJob(jobs[0].xq, 1, jobs[0].gq, jobs[0].d, None, jobs[0].nsplit, jobs[0].nshard)
+    arrb = (WgradJob * 2)(jobs[0], bad)
+    with pytest.raises(Exception):
+        ops.call("lbt_conv_wgrad_many_i8", arrb, 2, ops.stream())

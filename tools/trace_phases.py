@@ -100,6 +100,12 @@ def main():
             continue
         T0 = t[:, 0].min()
         groups = [("all", t)]
+        if "wgrad_many" in f.kname:  # slot 6 = job index + 1: one line per job, phases 0..3
+            for jid in sorted(set(t[:, 6].tolist())):
+                tj = t[t[:, 6] == jid].copy()
+                tj[:, 6] = 0
+                report(idx, "%s:job%d" % (f.kname, jid - 1), tj, T0)
+            continue
         has5 = t[:, 5] != 0
         if has5.any() and not has5.all():  # two workgroup roles (e.g. deferred wgrad + dgrad tiles)
             groups = [("A", t[~has5]), ("B", t[has5])]
