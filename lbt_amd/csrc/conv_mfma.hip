@@ -961,15 +961,71 @@ LBT_DEV int chan_reduce(int v) {
   return (int)h[0] + (int)h[1];
 }
 
-// quant_w<1> (stochastic) whose overflow predicates count only where `cnt` (halo lanes compute
-// the same codes as the owning workgroup but must not count them twice)
-LBT_DEV int quant_sc(const QState& s, float x, float u, bool cnt, int& ov1w, int& ov2w) {
+// Stochastic quantiser (quant_w<1>'s arithmetic) with PER-LANE overflow counts, on the VALU only:
+// the asymmetric predicate x >= T or x < -T (T a power of two) is max(x, -x*(1-2^-24)) >= T -- for
+// x < 0 the product rounds to >= T exactly when -x > T (the float after T, T(1+2^-23), gives
+// T(1+2^-24-2^-47), which rounds down to T; -x = T gives T(1-2^-24), representable and < T). A NaN
+// threshold (lanes that must not count: halo pixels, which the owning workgroup counts) compares
+// false. Two compares + two carry-adds per element and no lane masks live in SGPRs (the __ballot
+// form kept one 64-bit mask per predicate live across the unrolled elements and spilled them into
+// VGPR lanes); ov_wave turns the lane counts into wave totals once per kernel.
+LBT_DEV int quant_sl(const QState& s, float x, float u, float T1, float T2, int& c1, int& c2) {
   const float xm = x * s.m;
-  ov1w += __popcll(__ballot(cnt && ((xm >= s.L) | (xm < -s.L))));
-  ov2w += __popcll(__ballot(cnt && ((xm >= s.Lh) | (xm < -s.Lh))));
+  const float a = fmaxf(xm, -xm * 0x1.fffffep-1f);
+  c1 += a >= T1;
+  c2 += a >= T2;
   float v = xm + u;
   v = fminf(fmaxf(v, -s.L), s.Lm1);
   return (int)floorf(v);
+}
+// Keep the counts of a phase computed inside it: otherwise the compiler sinks the compares to
+// the counts' use at the kernel end and keeps every element's operand live across the phases.
+LBT_DEV void pin_counts(int& c1, int& c2) { asm volatile("" : "+v"(c1), "+v"(c2)); }
+LBT_DEV float ov_thr(bool cnt, float T) { return cnt ? T : __builtin_nanf(""); }
+// lane counts (each < 2^16) -> the wave totals, in every lane
+LBT_DEV void ov_wave(int& c1, int& c2) {
+  const int t = wave_sum_i32(c1 | (c2 << 16));
+  c1 = t & 0xffff;
+  c2 = t >> 16;
+}
+
+// ---- channel pairs on packed fp32 (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two lanes' worth of
+// IEEE fp32 per instruction, each half rounded exactly as the scalar op). The element chains of the
+// fused conv kernels are VALU-bound (SQ: VALU busy ~70 % of the kernel), so every multiply / add /
+// fma of a channel quad runs as two packed ops; compares, clamps, floors and conversions stay scalar.
+typedef float f2 __attribute__((ext_vector_type(2)));
+LBT_DEV f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+LBT_DEV f2 mk2(float a, float b) { return f2{a, b}; }
+LBT_DEV f2 cvt2(int a, int b) { return f2{(float)a, (float)b}; }
+// div_by (the compiler's correctly rounded x / y given y's reciprocal refinement) on a pair
+LBT_DEV f2 div_by2(f2 x, f2 y, f2 rc) {
+  const f2 q = x * rc;
+  const f2 r = fma2(-y, q, x);
+  const f2 q1 = fma2(r, rc, q);
+  const f2 r1 = fma2(-y, q1, x);
+  return __builtin_elementwise_copysign(fma2(r1, rc, q1), x);
+}
+// overflow counts of a pair (quant_sl's predicate; NaN thresholds count nothing)
+LBT_DEV void ov_count2(f2 xm, float T1, float T2, int& c1, int& c2) {
+  const f2 n = xm * mk2(-0x1.fffffep-1f, -0x1.fffffep-1f);
+  const float a0 = fmaxf(xm.x, n.x), a1 = fmaxf(xm.y, n.y);
+  c1 += (a0 >= T1) + (a1 >= T1);
+  c2 += (a0 >= T2) + (a1 >= T2);
+}
+// the same for xm >= 0 (inputs after a ReLU): x < -T cannot hold
+LBT_DEV void ov_count2_pos(f2 xm, float T1, float T2, int& c1, int& c2) {
+  c1 += (xm.x >= T1) + (xm.y >= T1);
+  c2 += (xm.x >= T2) + (xm.y >= T2);
+}
+// floor(clip(xm + u, -L, L-1)) of a pair, as floats (the codes, exact); med3 is the clip for
+// non-NaN operands
+LBT_DEV f2 qfloor2(const QState& s, f2 xm, f2 u) {
+  const f2 v = xm + u;
+  return mk2(floorf(__builtin_amdgcn_fmed3f(v.x, -s.L, s.Lm1)), floorf(__builtin_amdgcn_fmed3f(v.y, -s.L, s.Lm1)));
+}
+LBT_DEV int pack4f(f2 a, f2 b) {
+  const int c[4] = {(int)a.x, (int)a.y, (int)b.x, (int)b.y};
+  return pack4(c);
 }
 
 template <int CS, int CF, int NB, bool W4, int WCS>
@@ -1081,6 +1137,15 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     rmgx[k] = sh.pb[C + cq + k];
     rsg[k] = recip(sg[k]);
   }
+  f2 mu2[2], sg2[2], rsc2[2], rmg2[2], rmgx2[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    mu2[h] = mk2(mu[2 * h], mu[2 * h + 1]);
+    sg2[h] = mk2(rsg[2 * h].y, rsg[2 * h + 1].y);
+    rsc2[h] = mk2(rsg[2 * h].rc, rsg[2 * h + 1].rc);
+    rmg2[h] = mk2(rmg[2 * h], rmg[2 * h + 1]);
+    rmgx2[h] = mk2(rmgx[2 * h], rmgx[2 * h + 1]);
+  }
 
   // ---------------- phase 1: pass B over the rows + halo -> LDS gq image
   int ovq1 = 0, ovq2 = 0;
@@ -1094,21 +1159,25 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     const bool valid = g < ngrp;
     const bool in = valid && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
     const bool own = in && hy >= 1 && hy <= TH;
+    const float T1 = ov_thr(own, so.L), T2 = ov_thr(own, so.Lh);
     int G[4], q[4], c[4];
     unpack4(Gv[it], G);
     unpack4(Qv[it], q);
-    const float u[4] = {Uv[it].x, Uv[it].y, Uv[it].z, Uv[it].w};
+    const f2 u[2] = {mk2(Uv[it].x, Uv[it].y), mk2(Uv[it].z, Uv[it].w)};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float x1 = (float)q[k] * sn.inv_m;
-      const float x2 = x1 - mu[k];
-      const float xh = div_by(x2, rsg[k]);
-      const float gh = (float)G[k] * sgq.inv_m;
-      const float t1 = gh - rmg[k];
-      const float t2 = xh * rmgx[k];
-      const float dx = div_by(t1 - t2, rsg[k]);
-      c[k] = quant_sc(so, dx, u[k], own, ovq1, ovq2);
-      if (!in) c[k] = 0;  // the conv's zero padding
+    for (int h = 0; h < 2; ++h) {
+      const f2 x1 = cvt2(q[2 * h], q[2 * h + 1]) * sn.inv_m;
+      const f2 x2 = x1 - mu2[h];
+      const f2 xh = div_by2(x2, sg2[h], rsc2[h]);
+      const f2 gh = cvt2(G[2 * h], G[2 * h + 1]) * sgq.inv_m;
+      const f2 t1 = gh - rmg2[h];
+      const f2 t2 = xh * rmgx2[h];
+      const f2 dx = div_by2(t1 - t2, sg2[h], rsc2[h]);
+      const f2 xm = dx * so.m;
+      ov_count2(xm, T1, T2, ovq1, ovq2);
+      const f2 fl = qfloor2(so, xm, u[h]);
+      c[2 * h] = in ? (int)fl.x : 0;  // outside the image: the conv's zero padding
+      c[2 * h + 1] = in ? (int)fl.y : 0;
     }
     if (valid) *reinterpret_cast<int*>(sh.gq + pix * C + cq) = pack4(c);
     if (own) {
@@ -1120,6 +1189,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
       }
     }
   }
+  pin_counts(ovq1, ovq2);
   __syncthreads();
   LBT_TS(2);
 
@@ -1177,49 +1247,69 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc3[b][s][k] = 0;
   const bool has_add = p.add_src != nullptr;
+  f2 gam2a[NB][2], bet2a[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) gam2a[b][h] = mk2(gam[b][2 * h], gam[b][2 * h + 1]);
+    bet2a[h] = mk2(bet[2 * h], bet[2 * h + 1]);
+  }
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int pix = (tid + j * kBThreads) / C4;
     const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);
     const float4 t = *reinterpret_cast<const float4*>(sh.tile + pix * (C + 4) + cq);
-    float g[4] = {t.x, t.y, t.z, t.w};
+    f2 g[2] = {mk2(t.x, t.y), mk2(t.z, t.w)};
     if (has_add) {
-      g[0] = g[0] + av[j].x; g[1] = g[1] + av[j].y; g[2] = g[2] + av[j].z; g[3] = g[3] + av[j].w;
+      g[0] = g[0] + mk2(av[j].x, av[j].y);
+      g[1] = g[1] + mk2(av[j].z, av[j].w);
     }
     int R1[4];
     unpack4(Rv[0][j], R1);
     if (CF & kAYMask) {
       const float ym[4] = {ymv[j].x, ymv[j].y, ymv[j].z, ymv[j].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) g[k] = ym[k] > 0.f ? g[k] : 0.f;
+      for (int h = 0; h < 2; ++h)
+        g[h] = mk2(ym[2 * h] > 0.f ? g[h].x : 0.f, ym[2 * h + 1] > 0.f ? g[h].y : 0.f);
     } else if (CF & kAMaskR) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float xr = (float)R1[k] * r_inv;
-        const float m1 = xr * gam[0][k];
-        const float yv = m1 + bet[k];
-        g[k] = yv > 0.f ? g[k] : 0.f;
+      for (int h = 0; h < 2; ++h) {
+        const f2 xr = cvt2(R1[2 * h], R1[2 * h + 1]) * r_inv;
+        const f2 m1 = xr * gam2a[0][h];
+        const f2 yv = m1 + bet2a[h];
+        g[h] = mk2(yv.x > 0.f ? g[h].x : 0.f, yv.y > 0.f ? g[h].y : 0.f);
       }
     }
-    if (CF & kAGmask) *reinterpret_cast<float4*>(A.gmask_out + img + off) = make_float4(g[0], g[1], g[2], g[3]);
+    if (CF & kAGmask) *reinterpret_cast<float4*>(A.gmask_out + img + off) = make_float4(g[0].x, g[0].y, g[1].x, g[1].y);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
       int R[4], qn[4], Gc[4];
       unpack4(Rv[b][j], R);
       unpack4(qnv[b][j], qn);
-      const float ur[4] = {urg[b][j].x, urg[b][j].y, urg[b][j].z, urg[b][j].w};
-      const float un[4] = {ung[b][j].x, ung[b][j].y, ung[b][j].z, ung[b][j].w};
+      const f2 ur[2] = {mk2(urg[b][j].x, urg[b][j].y), mk2(urg[b][j].z, urg[b][j].w)};
+      const f2 un[2] = {mk2(ung[b][j].x, ung[b][j].y), mk2(ung[b][j].z, ung[b][j].w)};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int G2 = quant_w<1>(qrg[b], 1, g[k], ur[k], ov[b][0][0], ov[b][0][1]);
-        acc3[b][0][k] += G2 * R[k];
-        acc3[b][1][k] += G2;
-        const float gh = (float)G2 * qrg[b].inv_m;
-        const float d = gh * gam[b][k];
-        Gc[k] = quant_w<1>(qng[b], 1, d, un[k], ov[b][1][0], ov[b][1][1]);
-        acc3[b][2][k] += Gc[k];
-        acc3[b][3][k] += Gc[k] * qn[k];
+      for (int h = 0; h < 2; ++h) {
+        const f2 xm = g[h] * qrg[b].m;
+        ov_count2(xm, qrg[b].L, qrg[b].Lh, ov[b][0][0], ov[b][0][1]);
+        const f2 f1 = qfloor2(qrg[b], xm, ur[h]);  // G2 codes
+        const f2 gh = f1 * qrg[b].inv_m;
+        const f2 d = gh * gam2a[b][h];
+        const f2 dm = d * qng[b].m;
+        ov_count2(dm, qng[b].L, qng[b].Lh, ov[b][1][0], ov[b][1][1]);
+        const f2 f2c = qfloor2(qng[b], dm, un[h]);  // Gc codes
+        const int G2[2] = {(int)f1.x, (int)f1.y};
+        Gc[2 * h] = (int)f2c.x;
+        Gc[2 * h + 1] = (int)f2c.y;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int k = 2 * h + i;
+          acc3[b][0][k] += G2[i] * R[k];
+          acc3[b][1][k] += G2[i];
+          acc3[b][2][k] += Gc[k];
+          acc3[b][3][k] += Gc[k] * qn[k];
+        }
       }
       *reinterpret_cast<int*>(Bb.gout + img + off) = pack4(Gc);
     }
@@ -1249,6 +1339,12 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
       *reinterpret_cast<int4*>(part + 8 * C + cq) = make_int4(v1[0], v1[1], v1[2], v1[3]);
       *reinterpret_cast<int4*>(part + 9 * C + cq) = make_int4(v2[0], v2[1], v2[2], v2[3]);
     }
+  }
+  ov_wave(ovq1, ovq2);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    ov_wave(ov[b][0][0], ov[b][0][1]);
+    ov_wave(ov[b][1][0], ov[b][1][1]);
   }
   counts_stage_w(0, 5, ovq1, ovq2, sh.cnt);  // (counts_publish sums blockDim.x / 64 waves)
 #pragma unroll
@@ -1504,6 +1600,17 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       pm[b][k] = sh.cst[b][0][cq + k];
       ps[b][k] = recip(sh.cst[b][1][cq + k]);
     }
+  f2 pm2[NB][2], psy2[NB][2], psr2[NB][2], gam2[NB][2], bet2[NB][2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pm2[b][h] = mk2(pm[b][2 * h], pm[b][2 * h + 1]);
+      psy2[b][h] = mk2(ps[b][2 * h].y, ps[b][2 * h + 1].y);
+      psr2[b][h] = mk2(ps[b][2 * h].rc, ps[b][2 * h + 1].rc);
+      gam2[b][h] = mk2(gam[b][2 * h], gam[b][2 * h + 1]);
+      bet2[b][h] = mk2(bet[b][2 * h], bet[b][2 * h + 1]);
+    }
 
   // ---------------- phase 1: the chain over the rows + halo -> LDS input codes
   int ovr[2][2] = {{0, 0}, {0, 0}}, ovx1 = 0, ovx2 = 0;
@@ -1517,42 +1624,61 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     const bool in = valid && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
     const bool own = in && hy >= 1 && hy <= TH;
     const uint32_t e = (uint32_t)((y * W + x) * C + cq);
-    float v[4];
+    f2 v[2];  // the channel quad as two packed pairs
+    float T1[2], T2[2];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      T1[b] = ov_thr(own, qr[b].L);
+      T2[b] = ov_thr(own, qr[b].Lh);
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const lbt_chain_branch& Bb = b == 0 ? a.b1 : a.b2;
-      int q[4], R[4];
+      int q[4];
       unpack4(qv[b][it], q);
-      const float u[4] = {nrv[b][it].x, nrv[b][it].y, nrv[b][it].z, nrv[b][it].w};
+      const f2 u[2] = {mk2(nrv[b][it].x, nrv[b][it].y), mk2(nrv[b][it].z, nrv[b][it].w)};
+      f2 fl[2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float x1 = (float)q[k] * sn[b];
-        const float x2 = x1 - pm[b][k];
-        const float t = div_by(x2, ps[b][k]);
-        R[k] = quant_sc(qr[b], t, u[k], own, ovr[b][0], ovr[b][1]);
-        const float xr = (float)R[k] * qr[b].inv_m;
-        const float m1 = xr * gam[b][k];
-        const float tt = m1 + bet[b][k];
-        v[k] = b ? v[k] + tt : tt;
+      for (int h = 0; h < 2; ++h) {
+        const f2 x1 = cvt2(q[2 * h], q[2 * h + 1]) * sn[b];
+        const f2 x2 = x1 - pm2[b][h];
+        const f2 t = div_by2(x2, psy2[b][h], psr2[b][h]);
+        const f2 xm = t * qr[b].m;
+        ov_count2(xm, T1[b], T2[b], ovr[b][0], ovr[b][1]);
+        fl[h] = qfloor2(qr[b], xm, u[h]);  // the R codes
+        const f2 xr = fl[h] * qr[b].inv_m;
+        const f2 m1 = xr * gam2[b][h];
+        const f2 tt = m1 + bet2[b][h];
+        v[h] = b ? v[h] + tt : tt;
       }
-      if (own) *reinterpret_cast<int*>(Bb.rout + img + e) = pack4(R);
+      if (own) *reinterpret_cast<int*>(Bb.rout + img + e) = pack4f(fl[0], fl[1]);
     }
     if constexpr (RES) {
-      v[0] = v[0] + rv[it].x; v[1] = v[1] + rv[it].y; v[2] = v[2] + rv[it].z; v[3] = v[3] + rv[it].w;
+      v[0] = v[0] + mk2(rv[it].x, rv[it].y);
+      v[1] = v[1] + mk2(rv[it].z, rv[it].w);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
-    if (YST && own) *reinterpret_cast<float4*>(a.y + img + e) = make_float4(v[0], v[1], v[2], v[3]);
-    const float uo[4] = {nov[it].x, nov[it].y, nov[it].z, nov[it].w};
-    int c[4];
+    for (int h = 0; h < 2; ++h) v[h] = mk2(v[h].x > 0.f ? v[h].x : 0.f, v[h].y > 0.f ? v[h].y : 0.f);
+    if (YST && own) *reinterpret_cast<float4*>(a.y + img + e) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+    const f2 uo[2] = {mk2(nov[it].x, nov[it].y), mk2(nov[it].z, nov[it].w)};
+    const float X1 = ov_thr(own, so1.L), X2 = ov_thr(own, so1.Lh);
+    f2 co[2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int cc = quant_sc(so1, v[k], uo[k], own, ovx1, ovx2);
-      c[k] = in ? (cc < 0 ? 0 : cc) - 128 : -128;  // LBT_OUT_U8OFF; outside the image: the code of 0
+    for (int h = 0; h < 2; ++h) {
+      // v >= 0 after the ReLU (NaN -> 0): the lower clip and x < -L cannot hold, the codes are >= 0
+      const f2 xm = v[h] * so1.m;
+      ov_count2_pos(xm, X1, X2, ovx1, ovx2);
+      const f2 w = xm + uo[h];
+      co[h] = mk2(floorf(fminf(w.x, so1.Lm1)), floorf(fminf(w.y, so1.Lm1)));
     }
-    if (valid) *reinterpret_cast<int*>(sh.x + pix * C + cq) = pack4(c);
-    if (own) *reinterpret_cast<int*>((int8_t*)a.o1 + img + e) = pack4(c);
+    // LBT_OUT_U8OFF: code - 128 (= code ^ 0x80 for codes in [0, 255]); outside the image: the code of 0
+    const int cw = in ? (pack4f(co[0], co[1]) ^ (int)0x80808080) : (int)0x80808080;
+    if (valid) *reinterpret_cast<int*>(sh.x + pix * C + cq) = cw;
+    if (own) *reinterpret_cast<int*>((int8_t*)a.o1 + img + e) = cw;
   }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) pin_counts(ovr[b][0], ovr[b][1]);
+  pin_counts(ovx1, ovx2);
   if constexpr (kLateB) load_b();
   __syncthreads();
   LBT_TS(2);
@@ -1593,12 +1719,18 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   for (int j = 0; j < J; ++j) {
     const int pix3 = (tid + j * kBThreads) / C4;
     const float4 t = *reinterpret_cast<const float4*>(sh.tile + pix3 * (C + 4) + cq);
-    const float tv[4] = {t.x, t.y, t.z, t.w};
-    const float u[4] = {u3[j].x, u3[j].y, u3[j].z, u3[j].w};
-    int c[4];
+    const f2 tv[2] = {mk2(t.x, t.y), mk2(t.z, t.w)};
+    const f2 u[2] = {mk2(u3[j].x, u3[j].y), mk2(u3[j].z, u3[j].w)};
+    f2 fl[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f2 xm = tv[h] * sq.m;
+      ov_count2(xm, sq.L, sq.Lh, ovq1, ovq2);
+      fl[h] = qfloor2(sq, xm, u[h]);
+    }
+    const int c[4] = {(int)fl[0].x, (int)fl[0].y, (int)fl[1].x, (int)fl[1].y};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      c[k] = quant_w<1>(sq, 1, tv[k], u[k], ovq1, ovq2);
       s1[k] += c[k];
       s2[k] += c[k] * c[k];
     }
@@ -1617,6 +1749,10 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       *reinterpret_cast<int4*>(sh.part[wave] + C + cq) = make_int4(v2[0], v2[1], v2[2], v2[3]);
     }
   }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) ov_wave(ovr[b][0], ovr[b][1]);
+  ov_wave(ovx1, ovx2);
+  ov_wave(ovq1, ovq2);
 #pragma unroll
   for (int b = 0; b < NB; ++b) counts_stage_w(b, 4, ovr[b][0], ovr[b][1], sh.cnt);
   counts_stage_w(2, 4, ovx1, ovx2, sh.cnt);
