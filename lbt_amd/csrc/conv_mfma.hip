@@ -1057,7 +1057,18 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   const int cq = (tid % C4) * 4;  // this thread's channel quad (512 % C4 == 0: fixed over its groups)
   const int64_t img = (int64_t)n * H * W * C;
 
-  // ---------------- every load that does not depend on the sums goes out first
+  // ---------------- the pass-B statistics' shard sums first (they gate the first barrier): 16 groups
+  // of 32 lanes, lane = shard, group g owning channels g*CPG .. g*CPG+CPG-1 (SG, SGQ)
+  static_assert(LBT_NSHARD == 32 && kBThreads == 512 && C % 16 == 0, "statistics layout");
+  constexpr int CPG = C / 16;
+  long long sv[CPG][2];
+#pragma unroll
+  for (int i = 0; i < CPG; ++i) {
+    const int64_t* ps = B.sums + (int64_t)(tid & 31) * 4 * C + (tid >> 5) * CPG + i;
+    sv[i][0] = ps[2 * C];
+    sv[i][1] = ps[3 * C];
+  }
+  // then every load that does not depend on the sums
   // phase-1 operands: G / q codes and the output quantiser's noise over the halo rows
   const int ngrp = (TH + 2) * Wp * C4;
   int Gv[kBIt], Qv[kBIt];
@@ -1105,27 +1116,27 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
   const float scale = ldexpf(1.0f, -(frac_exp(B.qo) + frac_exp(p.qw)));
 
-  // ---------------- pass-B statistics (SG, SGQ of every shard), LDS sums cleared
-  // pass-B constants of channel c (threads c < C): SG, SGQ summed over the shards, then in double
-  // exactly as chain_bwd_b_kernel
-  if (tid < C) {
-    long long v[2][LBT_NSHARD];
+  // ---------------- pass-B statistics: the shard sums (loaded first, above) reduced over 32-lane
+  // groups (lane = shard, group g owns channels g*CPG ..), lane i < CPG of the group finishing
+  // channel g*CPG + i in double exactly as chain_bwd_b_kernel
 #pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) {
-      v[0][k] = B.sums[(int64_t)k * 4 * C + 2 * C + tid];
-      v[1][k] = B.sums[(int64_t)k * 4 * C + 3 * C + tid];
+  for (int i = 0; i < CPG; ++i)
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      sv[i][0] += __shfl_xor(sv[i][0], o, 64);
+      sv[i][1] += __shfl_xor(sv[i][1], o, 64);
     }
+  if ((tid & 31) < CPG) {
     long long SGi = 0, SGQi = 0;
 #pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) {
-      SGi += v[0][k];
-      SGQi += v[1][k];
-    }
+    for (int i = 0; i < CPG; ++i)
+      if ((tid & 31) == i) { SGi = sv[i][0]; SGQi = sv[i][1]; }
+    const int c = (tid >> 5) * CPG + (tid & 31);
     const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, nn = (double)B.n;
     const double SG = (double)SGi, SGQ = (double)SGQi;
-    const float m = B.ms[tid], sig = B.ms[C + tid];
-    sh.pb[tid] = (float)(gsc * SG / nn);
-    sh.pb[C + tid] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
+    const float m = B.ms[c], sig = B.ms[C + c];
+    sh.pb[c] = (float)(gsc * SG / nn);
+    sh.pb[C + c] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
   }
   __syncthreads();
   LBT_TS(1);
@@ -1354,12 +1365,12 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   }
   __syncthreads();
   LBT_TS(4);
-  counts_publish(0, 5, B.qo, sh.cnt);
+  counts_publish_nw<kBNW>(0, 5, B.qo, sh.cnt);
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
-    counts_publish(1 + 2 * b, 5, Bb.qrg, sh.cnt);
-    counts_publish(2 + 2 * b, 5, Bb.qng, sh.cnt);
+    counts_publish_nw<kBNW>(1 + 2 * b, 5, Bb.qrg, sh.cnt);
+    counts_publish_nw<kBNW>(2 + 2 * b, 5, Bb.qng, sh.cnt);
   }
   // slot i of [NB*4C pass-A sums | 2C gq sums]: one thread each, the waves' partials in int64
   const int shard = shard_id();
@@ -1504,7 +1515,18 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   const int64_t img = (int64_t)n * H * W * C;
   constexpr bool RES = (F & kFRes) != 0, YST = (F & kFY) != 0;
 
-  // ---------------- loads that do not depend on the moments
+  // ---------------- the moments' shard sums first (they gate the first barrier), then the loads that
+  // do not depend on the moments
+  static_assert(LBT_NSHARD == 32 && kBThreads == 512 && (NB * C) % 16 == 0, "moments layout");
+  constexpr int CPG = (NB * C) / 16;
+  long long sv[CPG][2];
+#pragma unroll
+  for (int i = 0; i < CPG; ++i) {
+    const int bc = (tid >> 5) * CPG + i, b = bc / C, c = bc - b * C;
+    const int64_t* cs = (b == 0 ? a.b1 : a.b2).nrm.chsum + (int64_t)(tid & 31) * 2 * C + c;
+    sv[i][0] = cs[0];
+    sv[i][1] = cs[C];
+  }
   const int ngrp = (TH + 2) * Wp * C4;
   int qv[NB][kBIt];
   float4 rv[kBIt], nrv[NB][kBIt], nov[kBIt];
@@ -1558,22 +1580,25 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   const QState so1 = qstate(a.qo1), sq = qstate(p.qout);
   const float scale = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw)));
 
-  // ---------------- Normalization_q moments (bn.hip bn_moments): threads c < C of each branch
-  if (tid < NB * C) {
-    const int b = tid / C, c = tid - b * C;
-    const lbt_bn_norm& nb = b == 0 ? a.b1.nrm : a.b2.nrm;
-    long long v[2][LBT_NSHARD];
+  // ---------------- Normalization_q moments (bn.hip bn_moments). The shard sums: 16 groups of 32
+  // lanes, lane = shard, group g owning (branch, channel) pairs g*CPG .. g*CPG+CPG-1; a 32-lane
+  // butterfly leaves the totals in every lane of the group and lane i < CPG finishes pair g*CPG+i.
+  // (Was: threads c < C loading all 2 x 32 shards each -- 64 dependent-issue loads in one wave on
+  // the launch's critical path.)
 #pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) {
-      v[0][k] = nb.chsum[(int64_t)k * 2 * C + c];
-      v[1][k] = nb.chsum[(int64_t)k * 2 * C + C + c];
+  for (int i = 0; i < CPG; ++i)
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      sv[i][0] += __shfl_xor(sv[i][0], o, 64);
+      sv[i][1] += __shfl_xor(sv[i][1], o, 64);
     }
+  if ((tid & 31) < CPG) {
     long long S1 = 0, S2 = 0;
 #pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) {
-      S1 += v[0][k];
-      S2 += v[1][k];
-    }
+    for (int i = 0; i < CPG; ++i)
+      if ((tid & 31) == i) { S1 = sv[i][0]; S2 = sv[i][1]; }
+    const int bc = (tid >> 5) * CPG + (tid & 31), b = bc / C, c = bc - b * C;
+    const lbt_bn_norm& nb = b == 0 ? a.b1.nrm : a.b2.nrm;
     const double s = ldexp(1.0, -frac_exp(nb.qn));
     const double mean_d = (double)S1 * s / (double)nb.n;
     const double var_d = (double)S2 * (s * s) / (double)nb.n - mean_d * mean_d;
@@ -1760,9 +1785,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   __syncthreads();
   LBT_TS(4);
 #pragma unroll
-  for (int b = 0; b < NB; ++b) counts_publish(b, 4, (b == 0 ? a.b1 : a.b2).qr, sh.cnt);
-  counts_publish(2, 4, a.qo1, sh.cnt);
-  counts_publish(3, 4, p.qout, sh.cnt);
+  for (int b = 0; b < NB; ++b) counts_publish_nw<kBNW>(b, 4, (b == 0 ? a.b1 : a.b2).qr, sh.cnt);
+  counts_publish_nw<kBNW>(2, 4, a.qo1, sh.cnt);
+  counts_publish_nw<kBNW>(3, 4, p.qout, sh.cnt);
   if (p.ychsum && tid < 2 * C) {
     long long t = 0;
 #pragma unroll

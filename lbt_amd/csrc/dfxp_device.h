@@ -249,6 +249,19 @@ LBT_DEV void counts_publish(int i, int nq, const lbt_qdesc& q, const int* sh) {
   if (t) LBT_GADD(q.counts + ((int64_t)q.slot * LBT_NSHARD + shard_id()) * LBT_CSTRIDE + j, t);
 }
 
+// counts_publish for a block of NW waves (compile time), counter i published by lanes 0/1 of wave
+// i % NW, so a kernel's counters go out from different waves in parallel (the generic form runs a
+// blockDim-bounded loop in wave 0 for every counter, one after another, at the kernel's tail).
+template <int NW>
+LBT_DEV void counts_publish_nw(int i, int nq, const lbt_qdesc& q, const int* sh) {
+  const int j = (int)threadIdx.x - 64 * (i % NW);
+  if (!q.counts || j < 0 || j > 1) return;
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) t += sh[w * 2 * nq + 2 * i + j];
+  if (t) LBT_GADD(q.counts + ((int64_t)q.slot * LBT_NSHARD + shard_id()) * LBT_CSTRIDE + j, t);
+}
+
 // Single-quantiser flush for kernels with nothing else to publish. EVERY thread of the block
 // must call it (contains barriers). sh must hold 2 ints per wave.
 LBT_DEV void block_flush_counts(const lbt_qdesc& q, int ov1, int ov2, int* sh) {
