@@ -98,6 +98,10 @@ class FusedResNet:
         # deferred into the next conv's launch
         # (measured a loss: 0.78 -> 1.02 ms per step -- graph branches do not overlap here)
         self.side_wgrad = os.environ.get("LBT_SIDE_WGRAD", "0") == "1"
+        # the end-of-backward batched wgrad launch as a parallel graph branch beside the stem's pass B
+        # and weight gradient (independent until the final reduction). Measured a loss: 0.65 -> 0.71
+        # ms/step (a forked HIP graph pays more in inter-stream synchronisation than the overlap wins)
+        self.tail_fork = os.environ.get("LBT_TAIL_FORK", "0") == "1"
         self._side = None
         # every conv's weight gradient of the step in ONE launch at the end of the backward
         # (lbt_conv_wgrad_many_i8) instead of inside the dgrad launches: a dgrad launch's tiles fill
@@ -204,6 +208,7 @@ class FusedResNet:
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
                 run()
+        f.kname, f.nbytes, f.inner = getattr(run, "kname", "side"), getattr(run, "nbytes", 0), run
         return f
 
     def _join_side(self):
@@ -211,6 +216,7 @@ class FusedResNet:
             ev = torch.cuda.Event()
             ev.record(self._side)
             torch.cuda.current_stream().wait_event(ev)
+        f.kname = "join"
         return f
 
     # ------------------------------------------------------------------ plan
@@ -430,7 +436,8 @@ class FusedResNet:
 
         # ---- stem backward (d loss / d image is never needed)
         self._flush_pending(bwd, L)
-        self._flush_wbatch(bwd, L)
+        tail_fork = self.tail_fork and self.batch_wgrad and not (self.overlap_wgrad or self.side_wgrad)
+        self._flush_wbatch(bwd, L, side=tail_fork)
         if gY is not None:  # pass A not fused into block 0's dgrad
             aA.g = gY.data_ptr()
             bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
@@ -456,7 +463,7 @@ class FusedResNet:
         # ---- batched reductions (after the side-stream weight gradients have landed): every
         # split wgrad, every dgamma / dbeta and -- in the training step -- the head's Dense_q dW
         # and loss, one launch (lbt_step_reduce)
-        if self.overlap_wgrad or (self.side_wgrad and self.fuse_bwd):
+        if self.overlap_wgrad or (self.side_wgrad and self.fuse_bwd) or tail_fork:
             bwd.append(self._join_side())
         self._rjobs = _dev_array(rjobs, ctx.device)
         total_blocks = sum((j.K * j.Cout + 255) // 256 for j in rjobs)
@@ -711,14 +718,16 @@ class FusedResNet:
         bwd.append(self._on_side(L("lbt_conv_wgrad_i8", ptr(xq), 1, ptr(gq), d, ptr(slab), nsplit, nshard,
                                    k="conv_wgrad_kernel", nb=nb)))
 
-    def _flush_wbatch(self, bwd, L):
-        """The batched weight-gradient launch of every job collected so far."""
+    def _flush_wbatch(self, bwd, L, side=False):
+        """The batched weight-gradient launch of every job collected so far (side: on the side stream,
+        joined before the final reduction)."""
         jobs, self._wbatch = self._wbatch, []
         if not jobs:
             return
         arr = (WgradJob * len(jobs))(*jobs)
         self._keep.append(arr)
-        bwd.append(L("lbt_conv_wgrad_many_i8", arr, len(jobs), k="conv_wgrad_many_kernel", nb=sum(w._nb for w in jobs)))
+        run = L("lbt_conv_wgrad_many_i8", arr, len(jobs), k="conv_wgrad_many_kernel", nb=sum(w._nb for w in jobs))
+        bwd.append(self._on_side(run, force=True) if side else run)
 
     def _flush_pending(self, bwd, L):
         """Run the deferred wgrad job on its own (the next launch is not a fused conv backward)."""

@@ -125,11 +125,18 @@ def time_launches(trainer, launches, reps=20, replays=5):
     return out
 
 
+def graph_launches(m):
+    """Every kernel launch of a fused plan's step, in order, each callable on its own (side-stream
+    wrappers unwrapped, stream joins dropped)."""
+    return [getattr(f, "inner", f) for f in m._fwd + m._hfused + m._bwd + m._tail_fused if hasattr(f, "nbytes")]
+
+
 def measure_dominant_graph(trainer, traffic_file=None):
     """Fused plans: every launch of the step timed in isolation by graph replay (time_launches);
     the kernel family with the largest per-step total is the dominant one."""
     m = trainer.model
-    launches = [f for f in m._fwd + m._hfused + m._bwd + m._tail_fused if hasattr(f, "nbytes")]
+    # (a launch wrapped onto the side stream is timed as itself: graph_launches unwraps it)
+    launches = graph_launches(m)
     us = time_launches(trainer, launches)
     fam = {}
     for f, t in zip(launches, us):

@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import bench  # noqa: E402
 from lbt_amd.fused import FusedResNet  # noqa: E402
 from lbt_amd.models import CIFAR10_Resnet20  # noqa: E402
-from lbt_amd.roofline import time_launches  # noqa: E402
+from lbt_amd.roofline import graph_launches, time_launches  # noqa: E402
 from lbt_amd.runtime import DfxpContext  # noqa: E402
 from lbt_amd.trainer import Trainer  # noqa: E402
 
@@ -39,8 +39,7 @@ def main():
     for _ in range(3):
         tr.step(xs[0], ys[0])
     torch.cuda.synchronize()
-    launches = [f for f in model._fwd + model._hfused + model._bwd + model._tail_fused
-                if a.filter in getattr(f, "kname", "")]
+    launches = [f for f in graph_launches(model) if a.filter in getattr(f, "kname", "")]
     res = time_launches(tr, launches, reps=a.reps)
     tot = 0.0
     for i, (f, us) in enumerate(zip(launches, res)):

@@ -73,7 +73,8 @@ def main():
         s.argtypes = [ctypes.c_void_p]
     nwg_max = 1 << 15
     buf = torch.zeros(nwg_max * 8, dtype=torch.int64, device=dev)
-    launches = [f for f in model._fwd + model._hfused + model._bwd + model._tail_fused if a.filter in getattr(f, "kname", "")]
+    from lbt_amd.roofline import graph_launches
+    launches = [f for f in graph_launches(model) if a.filter in getattr(f, "kname", "")]
     side = torch.cuda.Stream(device=dev)
     for idx, f in enumerate(launches[:a.max]):
         # the launch replayed from a graph (as in the timed step), twice: the second one is traced
