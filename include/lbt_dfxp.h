@@ -140,6 +140,18 @@ int lbt_conv_fwd_i8(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t
                     const int32_t* wcolsum, lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw,
                     float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream);
 
+/* Two lbt_conv_fwd_i8 calls in ONE launch: a projection ResidualBlock_q's first conv (3x3, stride
+ * 2; dynamic_fixed_point.py:772-795 -> 860) and its shortcut conv (1x1, stride 2; :831-846 -> 861)
+ * read the same input codes and produce same-shaped outputs. Each job is exactly the arguments of
+ * lbt_conv_fwd_i8 (w4: wf is the packed 4-bit image, as lbt_conv_fwd_i8w4); both jobs need equal
+ * Cin, Cout, N*Ho*Wo and w4, with (Cin, Cout) in {(16,32), (32,64)}, else LBT_EINVAL. Results
+ * are bit-identical to the two single calls.                                                    */
+typedef struct lbt_conv_fwd_job {
+  const int8_t* xq; int32_t x_u8off; int32_t w4; const int8_t* wf; int32_t ksf; const int32_t* wcolsum;
+  lbt_conv_desc d; lbt_qdesc qx; lbt_qdesc qw; float* y; int8_t* yq; lbt_qdesc qout; int64_t* ychsum;
+} lbt_conv_fwd_job;
+int lbt_conv_fwd_pair_i8(const lbt_conv_fwd_job* j0, const lbt_conv_fwd_job* j1, void* stream);
+
 /* Conv2d_q backward dX = tf.gradients(y, X, gradq) (dynamic_fixed_point.py:305): int8
  * implicit GEMM over (tap, co) of the quantised grad.  dx (fp32 NHWC [N,H,W,Cin]) =
  * acc * 2^-(eg+ew) (+ add_src[e] if add_src != NULL).  Requires Cin%16 == 0, Cout%16 == 0. */
@@ -366,6 +378,11 @@ typedef struct lbt_chain_bwd_b {
   int64_t rows, inner; int32_t C;
 } lbt_chain_bwd_b;
 int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream);
+/* Two pass-B chains of the same shape (rows, inner, C) and flags in one launch: a projection
+ * block's shortcut-BN and first-BN backward (dynamic_fixed_point.py:620-623 for ns and n1 of
+ * :746-875), both feeding strided convs whose dgrad has no pass-B prologue. Bit-identical to two
+ * lbt_bn_chain_bwd_b calls; mismatched shapes / flags -> LBT_EINVAL.                         */
+int lbt_bn_chain_bwd_b_pair(const lbt_chain_bwd_b* a, const lbt_chain_bwd_b* b, void* stream);
 
 /* The weight gradient of one conv (the arguments of lbt_conv_wgrad_i8), as a job another launch
  * carries out; slab == NULL: no job.                                                        */

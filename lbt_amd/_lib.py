@@ -91,6 +91,12 @@ class ConvFwd(ctypes.Structure):
                 ("d", ConvDesc), ("qw", QDesc), ("yq", c_void_p), ("qout", QDesc), ("ychsum", c_void_p)]
 
 
+class ConvFwdJob(ctypes.Structure):
+    _fields_ = [("xq", c_void_p), ("x_u8off", c_int32), ("w4", c_int32), ("wf", c_void_p), ("ksf", c_int32),
+                ("wcolsum", c_void_p), ("d", ConvDesc), ("qx", QDesc), ("qw", QDesc), ("y", c_void_p),
+                ("yq", c_void_p), ("qout", QDesc), ("ychsum", c_void_p)]
+
+
 class WJob(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("KH", c_int32), ("KW", c_int32), ("Cin", c_int32), ("Cout", c_int32),
                 ("q", QDesc), ("w_hwio", c_void_p), ("wf", c_void_p), ("ksf", c_int32), ("wd", c_void_p),
@@ -192,6 +198,8 @@ _SIGS = {
     "lbt_bn_chain_fwd": [_P, _P],
     "lbt_bn_chain_bwd_a": [_P, _P],
     "lbt_bn_chain_bwd_b": [_P, _P],
+    "lbt_bn_chain_bwd_b_pair": [_P, _P, _P],
+    "lbt_conv_fwd_pair_i8": [_P, _P, _P],
     "lbt_conv_bwd_fused_i8": [_P, _P],
     "lbt_conv_fwd_fused_i8": [_P, _P],
     "lbt_bn_bwd_a_wide": [_P, QDesc, _P, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64, c_int32, _P],

@@ -467,8 +467,9 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
 
 // ============================================================================ backward pass B
 
+// (by: the workgroup's row-block index -- blockIdx.y, or its index within its job of a pair launch)
 template <int F>
-__global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a, int rpt) {
+__device__ __forceinline__ void chain_bwd_b_body(const lbt_chain_bwd_b& a, int rpt, uint32_t by) {
   extern __shared__ float shf[];  // mu, sigma, mg, mgx [C]; then long long tmp[2C], csum[2C]
   __shared__ int sh_cnt[8 * kThreads / 64];
   constexpr int ST = (F & kRt) ? -1 : ((F & kBStoch) ? 1 : 0);
@@ -484,7 +485,7 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
   const bool live = g < groups;
   const int64_t gl = live ? g : 0;
   const int c0 = (int)(((uint32_t)gl << 2) % (uint32_t)C);
-  const int64_t r0 = (int64_t)blockIdx.y * rpt;
+  const int64_t r0 = (int64_t)by * rpt;
   const int64_t rend = r0 + rpt < a.rows ? r0 + rpt : a.rows;
   // ---- first rows + noise before the moment prologue
   int Gv[kRB], qv[kRB];
@@ -583,6 +584,21 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a
   counts_publish(0, 1, a.qo, sh_cnt);
   if (gcol) block_flush_sums(csum, 2 * C, a.gcolsum, 2 * C);
   LBT_TS(3);
+}
+
+template <int F>
+__global__ __launch_bounds__(kThreads) void chain_bwd_b_kernel(lbt_chain_bwd_b a, int rpt) {
+  chain_bwd_b_body<F>(a, rpt, blockIdx.y);
+}
+
+// two same-shaped pass-B chains in one grid: row blocks [0, ny) of job a, then those of job b
+template <int F>
+__global__ __launch_bounds__(kThreads) void chain_bwd_b2_kernel(lbt_chain_bwd_b a, lbt_chain_bwd_b b, int rpt,
+                                                                uint32_t ny) {
+  if (blockIdx.y < ny)
+    chain_bwd_b_body<F>(a, rpt, blockIdx.y);
+  else
+    chain_bwd_b_body<F>(b, rpt, blockIdx.y - ny);
 }
 
 __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
@@ -729,6 +745,28 @@ extern "C" int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream) {
     LBT_LAUNCH((chain_bwd_b_kernel<kBQ | kBStoch>), grid, shm, st, *a, rpt);
   else
     LBT_LAUNCH((chain_bwd_b_kernel<kRt>), grid, shm, st, *a, rpt);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_bn_chain_bwd_b_pair(const lbt_chain_bwd_b* a, const lbt_chain_bwd_b* b, void* stream) {
+  if (!a || !b || !shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;
+  if (a->rows != b->rows || a->inner != b->inner || a->C != b->C) return LBT_EINVAL;
+  const int f = bwd_b_flags(*a);
+  if (f != bwd_b_flags(*b)) return LBT_EINVAL;
+  dim3 grid;
+  int rpt;
+  if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
+  const uint32_t ny = grid.y;
+  if ((uint64_t)ny * 2 > 65535) return LBT_EINVAL;
+  grid.y = 2 * ny;
+  const size_t shm = sizeof(float) * 4 * a->C + sizeof(long long) * 4 * a->C;
+  hipStream_t st = (hipStream_t)stream;
+  if (f == (kBQ | kBStoch | kBGcol))
+    LBT_LAUNCH((chain_bwd_b2_kernel<kBQ | kBStoch | kBGcol>), grid, shm, st, *a, *b, rpt, ny);
+  else if (f == (kBQ | kBStoch))
+    LBT_LAUNCH((chain_bwd_b2_kernel<kBQ | kBStoch>), grid, shm, st, *a, *b, rpt, ny);
+  else
+    LBT_LAUNCH((chain_bwd_b2_kernel<kRt>), grid, shm, st, *a, *b, rpt, ny);
   return (int)hipGetLastError();
 }
 

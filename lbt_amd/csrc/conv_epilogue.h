@@ -109,7 +109,7 @@ LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, 
       long long tot = 0;
 #pragma unroll
       for (int mt = 0; mt < MTB; ++mt) {
-        const int64_t row0 = ((int64_t)blockIdx.x * MTB + mt) * 16;
+        const int64_t row0 = (mtile - wave / WPM + mt) * 16;  // the block's first m-tile from this wave's
         if (row0 < o.M) tot += sh.part[mt * WPM + wcol][which][lc];
       }
       if (tot) LBT_GADD((unsigned long long*)&o.chsum[(int64_t)shard_id() * 2 * o.ncol + t], (unsigned long long)tot);

@@ -258,6 +258,17 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1
   conv_gemm_body<MODE, CS, NT, CF, NB, W4>(p, blockIdx.x);
 }
 
+// Two independent GEMMs of one geometry class (same CS / NT / M) in one grid: workgroups [0, nb0)
+// run p0's tiles, the rest p1's (a projection block's 3x3/2 conv and its 1x1/2 shortcut, which
+// read the same input codes: one launch instead of two).
+template <int MODE, int CS, int NT, bool W4>
+__global__ __launch_bounds__(kThreads) void conv_gemm2_kernel(GemmArgs p0, GemmArgs p1, uint32_t nb0) {
+  if (blockIdx.x < nb0)
+    conv_gemm_body<MODE, CS, NT, 0, 1, W4>(p0, blockIdx.x);
+  else
+    conv_gemm_body<MODE, CS, NT, 0, 1, W4>(p1, blockIdx.x - nb0);
+}
+
 // ----------------------------------------------------------------------------- wgrad
 // dW[tap][ci][co] = sum_p X[p shifted by tap][ci] * G[p][co]: GEMM rows = ci, cols = co, k = pixels.
 // grid (nsplit, taps, Cout/16): workgroup = one tap, one 16-channel co slice, a pixel range; each
@@ -469,13 +480,11 @@ bool desc_ok(const lbt_conv_desc& d) {
 LBT_TRACE_SETTER(conv)
 
 namespace {
-template <bool W4>
-int conv_fwd(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf, const int32_t* wcolsum,
-             lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum,
-             void* stream) {
+int fwd_setup(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf, const int32_t* wcolsum,
+              lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum,
+              GemmArgs& p) {
   if (!desc_ok(d) || d.Cin % 16 || d.Cout % 16 || d.Cout > 128) return LBT_EINVAL;
   const int cs = d.Cin / 16;
-  GemmArgs p;
   p.a = xq; p.b = wf; p.ks = ksf; p.nslices = d.KH * d.KW * cs;
   if (ksf % 4 || ksf < p.nslices) return LBT_EINVAL;
   p.a_fill = x_u8off ? (int)0x80808080u : 0;
@@ -484,7 +493,51 @@ int conv_fwd(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf, c
   if (yq && qout.stochastic && !qout.noise) return LBT_EINVAL;  // quantising epilogue reads the noise table
   p.d = d; p.qa = qx; p.qb = qw; p.y = y; p.add_src = nullptr; p.yq = yq; p.qout = qout; p.ychsum = ychsum;
   p.M = (int64_t)d.N * d.Ho * d.Wo; p.ncol = d.Cout;
-  return launch_gemm<MODE_FWD, W4>(p, cs, (hipStream_t)stream);
+  return 0;
+}
+
+template <bool W4>
+int conv_fwd(const int8_t* xq, int32_t x_u8off, const int8_t* wf, int32_t ksf, const int32_t* wcolsum,
+             lbt_conv_desc d, lbt_qdesc qx, lbt_qdesc qw, float* y, int8_t* yq, lbt_qdesc qout, int64_t* ychsum,
+             void* stream) {
+  GemmArgs p;
+  const int e = fwd_setup(xq, x_u8off, wf, ksf, wcolsum, d, qx, qw, y, yq, qout, ychsum, p);
+  if (e) return e;
+  return launch_gemm<MODE_FWD, W4>(p, d.Cin / 16, (hipStream_t)stream);
+}
+
+template <int CS, int NT, bool W4>
+int launch_fwd_pair(const GemmArgs& p0, const GemmArgs& p1, hipStream_t st) {
+  constexpr int MTB = EpiGeom<NT>::MTB;
+  const int64_t blocks = ((p0.M + 15) / 16 + MTB - 1) / MTB;
+  if (2 * blocks > 0x7fffffff) return LBT_EINVAL;
+  hipLaunchKernelGGL((conv_gemm2_kernel<MODE_FWD, CS, NT, W4>), dim3((unsigned)(2 * blocks)), dim3(kThreads), 0, st,
+                     p0, p1, (uint32_t)blocks);
+  return (int)hipGetLastError();
+}
+
+int conv_fwd_pair(const lbt_conv_fwd_job* j0, const lbt_conv_fwd_job* j1, void* stream) {
+  if (!j0 || !j1 || j0->w4 != j1->w4) return LBT_EINVAL;
+  GemmArgs p[2];
+  const lbt_conv_fwd_job* j[2] = {j0, j1};
+  for (int i = 0; i < 2; ++i) {
+    if (j[i]->w4 && j[i]->qw.bits > 4) return LBT_EINVAL;
+    const int e = fwd_setup(j[i]->xq, j[i]->x_u8off, j[i]->wf, j[i]->ksf, j[i]->wcolsum, j[i]->d, j[i]->qx, j[i]->qw,
+                            j[i]->y, j[i]->yq, j[i]->qout, j[i]->ychsum, p[i]);
+    if (e) return e;
+  }
+  if (p[0].M != p[1].M || p[0].ncol != p[1].ncol || j0->d.Cin != j1->d.Cin) return LBT_EINVAL;
+  if (p[0].M * p[0].ncol >= (int64_t)1 << 31) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int key = ((j0->d.Cin / 16) << 8) | ((p[0].ncol / 16) << 1) | (j0->w4 ? 1 : 0);
+#define LBT_FP(CS_, NT_)                                                                   \
+  if (key == ((CS_ << 8) | (NT_ << 1))) return launch_fwd_pair<CS_, NT_, false>(p[0], p[1], st); \
+  if (key == ((CS_ << 8) | (NT_ << 1) | 1)) return launch_fwd_pair<CS_, NT_, true>(p[0], p[1], st);
+  // ResNet-20 / CIFAR projection blocks: 16 -> 32 and 32 -> 64 channels
+  LBT_FP(1, 2)
+  LBT_FP(2, 4)
+#undef LBT_FP
+  return LBT_EINVAL;
 }
 
 template <bool W4>
@@ -513,6 +566,9 @@ extern "C" int lbt_conv_fwd_i8w4(const int8_t* xq, int32_t x_u8off, const uint8_
                                  int8_t* yq, lbt_qdesc qout, int64_t* ychsum, void* stream) {
   if (qw.bits > 4) return LBT_EINVAL;
   return conv_fwd<true>(xq, x_u8off, (const int8_t*)wf4, ksf, wcolsum, d, qx, qw, y, yq, qout, ychsum, stream);
+}
+extern "C" int lbt_conv_fwd_pair_i8(const lbt_conv_fwd_job* j0, const lbt_conv_fwd_job* j1, void* stream) {
+  return conv_fwd_pair(j0, j1, stream);
 }
 extern "C" int lbt_conv_dgrad_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                                  lbt_qdesc qw, float* dx, const float* add_src, void* stream) {

@@ -102,6 +102,9 @@ class FusedResNet:
         # and weight gradient (independent until the final reduction). Measured a loss: 0.65 -> 0.71
         # ms/step (a forked HIP graph pays more in inter-stream synchronisation than the overlap wins)
         self.tail_fork = os.environ.get("LBT_TAIL_FORK", "0") == "1"
+        # a projection block's two strided convs (3x3/2 + 1x1/2 shortcut) as ONE launch forward, and
+        # its two pass-B chains (shortcut BN, first BN) as ONE launch backward
+        self.pair_launch = os.environ.get("LBT_PAIR", "1") == "1"
         self._side = None
         # every conv's weight gradient of the step in ONE launch at the end of the backward
         # (lbt_conv_wgrad_many_i8) instead of inside the dgrad launches: a dgrad launch's tiles fill
@@ -589,7 +592,24 @@ class FusedResNet:
         qn1 = self._buf(k + "qn1", shp, torch.int8)
         chs1 = self._sums(k + "chs1", ops.NSHARD * 2 * C)
         obs(b.n1.X_range, numel)
-        self._conv_fwd(fwd, L, c1, d1, xa, qn1, b.n1.X_range, chs1)
+        ds = qns = chss = Rs = None
+        if cs is not None:
+            ds = ops.conv_desc(N, H, W, Cin, C, 1, 1, s, s, cs.padding)
+            cs.d = ds
+            qns = self._buf(k + "qns", shp, torch.int8)
+            chss = self._sums(k + "chss", ops.NSHARD * 2 * C)
+            obs(b.ns.X_range, numel)
+        pair = (self.pair_launch and cs is not None and not self._fusable_bwd(c1, d1, flag=True)
+                and (Cin, C) in ((16, 32), (32, 64)))
+        if pair:  # conv-1 and the shortcut conv read the same input codes: one launch
+            self._flush_chain(fwd, L)
+            j0 = self._fwd_job(c1, d1, xa, qn1, b.n1.X_range, chs1)
+            j1 = self._fwd_job(cs, ds, xs, qns, b.ns.X_range, chss)
+            self._keep += [j0, j1]
+            fwd.append(L("lbt_conv_fwd_pair_i8", ctypes.byref(j0), ctypes.byref(j1), k="conv_gemm2_kernel (fwd pair)",
+                         nb=xa.numel() + xs.numel() + c1.wf.numel() + cs.wf.numel() + 2 * qn1.numel()))
+        else:
+            self._conv_fwd(fwd, L, c1, d1, xa, qn1, b.n1.X_range, chs1)
         R1 = self._buf(k + "R1", shp, torch.int8)
         xb = self._buf(k + "xb", shp, torch.int8)
         obs(b.r1.X_range, numel)
@@ -604,14 +624,9 @@ class FusedResNet:
         chs2 = self._sums(k + "chs2", ops.NSHARD * 2 * C)
         obs(b.n2.X_range, numel)
         self._conv_fwd(fwd, L, c2, d2, xb, qn2, b.n2.X_range, chs2)
-        ds = qns = chss = Rs = None
         if cs is not None:
-            ds = ops.conv_desc(N, H, W, Cin, C, 1, 1, s, s, cs.padding)
-            cs.d = ds
-            qns = self._buf(k + "qns", shp, torch.int8)
-            chss = self._sums(k + "chss", ops.NSHARD * 2 * C)
-            obs(b.ns.X_range, numel)
-            self._conv_fwd(fwd, L, cs, ds, xs, qns, b.ns.X_range, chss)
+            if not pair:
+                self._conv_fwd(fwd, L, cs, ds, xs, qns, b.ns.X_range, chss)
             Rs = self._buf(k + "Rs", shp, torch.int8)
             obs(b.rs.X_range, numel)
         R2 = self._buf(k + "R2", shp, torch.int8)
@@ -670,6 +685,12 @@ class FusedResNet:
             return
         self._chain_pending = None
         fwd.append(L("lbt_bn_chain_fwd", ctypes.byref(a), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(a)))
+
+    def _fwd_job(self, c, d, xq, yq, qout, chs):
+        """One lbt_conv_fwd_job: the arguments of conv c's lbt_conv_fwd_i8 (quantising epilogue)."""
+        return _lib.ConvFwdJob(xq.data_ptr(), 1, 1 if getattr(c, "w4", False) else 0, self._wf(c).value, c.ksf,
+                               c.wcolsum.data_ptr(), d, self._qd(c.X_range), c.W_range.desc, None, yq.data_ptr(),
+                               self._qd(qout), chs.data_ptr())
 
     def _conv_fwd(self, fwd, L, c, d, xq, yq, qout, chs):
         """Append conv c's forward (quantising epilogue yq / qout / chs): one lbt_conv_fwd_fused_i8 with
@@ -831,8 +852,10 @@ class FusedResNet:
         nb_dg2 = gq2.numel() + c2.wd.numel()
         sp2, ns2, slab2 = ops.wgrad_slab(self._c, k + "slab2", d2, self.ctx, batched=self.batch_wgrad)
         nb_wg2 = f["xb"].numel() + gq2.numel() + 4 * slab2.numel()
+        # the shortcut BN's pass B shares one launch with bn1's when conv-1 is not fused either
+        bpair = self.pair_launch and cs is not None and fb2 and not fb1
         if fb2:  # pass B (bn2) + dgrad + pass A (bn1) in one launch, conv-2 wgrad deferred
-            if cs is not None:  # the shortcut BN's pass B (its conv is not fused) goes first
+            if cs is not None and not bpair:  # the shortcut BN's pass B (its conv is not fused) goes first
                 bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aBs), k="chain_bwd_b_kernel",
                              nb=ops._chain_bwd_b_bytes(aBs)))
             aA1 = self._chain_bwd_a(None, None, True, None, (b.r1, f["R1"], b.n1, f["qn1"], Gn1, sums1), None, shp, C)
@@ -865,7 +888,10 @@ class FusedResNet:
         aB1 = self._chain_bwd_b(b.n1, Gn1, f["qn1"], sums1, shp, C, gq1, c1.grad_range, gcol1)
         if self.sync_bn:
             bwd.append(self._allreduce(sums1))
-        if not fb1:  # (a pending wgrad stays pending: the next fused launch carries it)
+        if bpair:
+            bwd.append(L("lbt_bn_chain_bwd_b_pair", ctypes.byref(aBs), ctypes.byref(aB1), k="chain_bwd_b2_kernel",
+                         nb=ops._chain_bwd_b_bytes(aBs) + ops._chain_bwd_b_bytes(aB1)))
+        elif not fb1:  # (a pending wgrad stays pending: the next fused launch carries it)
             bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB1), k="chain_bwd_b_kernel",
                          nb=ops._chain_bwd_b_bytes(aB1)))
         keep.append(aB1)

@@ -761,6 +761,40 @@ def test_fused_conv_backward_equals_launch_pair(B, w4):
     assert a[5] == b[5]
 
 
+@pytest.mark.parametrize("w4", [False, True])
+def test_pair_launches_equal_single_launches(w4):
+    """lbt_conv_fwd_pair_i8 (a projection block's 3x3/2 conv and 1x1/2 shortcut in one launch) and
+    lbt_bn_chain_bwd_b_pair (its shortcut-BN and first-BN pass B in one launch) == the single
+    launches they replace: gradients, momentum, weights, exponents, BN running statistics and loss
+    bit-identical after two graph-replayed optimiser steps at B=128."""
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.trainer import Trainer
+    outs = []
+    for pair in (False, True):
+        ctx = DfxpContext(seed=6)
+        m = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, weight_bits=4 if w4 else None))
+        m.pair_launch = pair
+        tr = Trainer(m, lr=1e-2, momentum=0.9, batch_size=128, use_graph=True)
+        for i in range(2):
+            x, y = synthetic_batch(128, seed=40 + i)
+            tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+        torch.cuda.synchronize()
+        nf = sum(1 for f in m._fwd if getattr(f, "kname", "").startswith("conv_gemm2_kernel"))
+        nb = sum(1 for f in m._bwd if getattr(f, "kname", "") == "chain_bwd_b2_kernel")
+        assert (nf, nb) == ((2, 2) if pair else (0, 0)), (nf, nb)
+        bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
+        outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,
+                     m.loss.item()))
+    a, b = outs
+    for i in range(3):
+        assert np.array_equal(a[i], b[i]), i
+    assert a[3] == b[3]
+    for u, v in zip(a[4], b[4]):
+        assert np.array_equal(u, v)
+    assert a[5] == b[5]
+
+
 # (N, H, W, Cin, Cout, k, s): the staged 3x3 / stride-1 body (W | 64, whole-row chunks) and the
 # per-tap body (strided / 1x1), mixed in one launch
 WGRAD_MANY_CASES = [(8, 32, 32, 16, 16, 3, 1), (8, 16, 16, 32, 32, 3, 1), (8, 8, 8, 64, 64, 3, 1),
