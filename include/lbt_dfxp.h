@@ -351,6 +351,17 @@ int lbt_bn_chain_bwd_a(const lbt_chain_bwd_a* a, void* stream);
  * y_mask or from branch-1 R; optional gmask_out.                                          */
 int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                             lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream);
+
+/* A projection ResidualBlock_q's input gradient in one launch: the 3x3/2 conv's dgrad (gq, wd,
+ * d, qg, qw) plus the 1x1/2 shortcut conv's (gq2, wd2, d2, qg2, qw2; dynamic_fixed_point.py:866-869,
+ * each Conv2d_q.backward :305) summed as fp32 dx + dx2, then pass A of a (as
+ * lbt_conv_dgrad_chain_i8). Bit-identical to lbt_conv_dgrad_i8(gq2 ...) into a buffer followed by
+ * lbt_conv_dgrad_chain_i8(gq ..., add_src = that buffer). Both descriptors must share N, H, W, Cin,
+ * Cout, Ho, Wo with Cout = 2 Cin (16 -> 32, 32 -> 64); w4: wd / wd2 are packed 4-bit images. */
+int lbt_conv_dgrad2_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                             lbt_qdesc qw, const int8_t* gq2, const int8_t* wd2, int32_t ksd2,
+                             lbt_conv_desc d2, lbt_qdesc qg2, lbt_qdesc qw2, int32_t w4,
+                             const lbt_chain_bwd_a* a, void* stream);
 /* ... with the 4-bit packed weight image (see lbt_conv_fwd_i8w4). */
 int lbt_conv_dgrad_chain_i8w4(const int8_t* gq, const uint8_t* wd4, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                               lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream);

@@ -200,6 +200,8 @@ _SIGS = {
     "lbt_bn_chain_bwd_b": [_P, _P],
     "lbt_bn_chain_bwd_b_pair": [_P, _P, _P],
     "lbt_conv_fwd_pair_i8": [_P, _P, _P],
+    "lbt_conv_dgrad2_chain_i8": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, c_int32, ConvDesc, QDesc, QDesc,
+                                 c_int32, _P, _P],
     "lbt_conv_bwd_fused_i8": [_P, _P],
     "lbt_conv_fwd_fused_i8": [_P, _P],
     "lbt_bn_bwd_a_wide": [_P, QDesc, _P, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64, c_int32, _P],

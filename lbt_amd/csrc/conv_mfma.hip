@@ -72,8 +72,12 @@ LBT_DEV v4i unpack_i4x16(v2i pk) {
 // k-slice (no int4 MFMA on gfx950 -- unpacked to int8 in registers).
 // One workgroup's tile (bid = its index in the GEMM's grid); the body of conv_gemm_kernel and of
 // the dgrad half of dgrad_wgrad_kernel.
-template <int MODE, int CS, int NT, int CF, int NB, bool W4>
-__device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid) {
+// DUAL (dgrad with pass A only): p2 is a second dgrad GEMM into the same output pixels (a projection
+// block's 1x1/2 shortcut beside its 3x3/2 first conv); its fp32 result float(acc2) * scale2 is the
+// pass-A addend, exactly the value the shortcut's own dgrad launch would have stored and this one
+// re-loaded as add_src.
+template <int MODE, int CS, int NT, int CF, int NB, bool W4, bool DUAL = false>
+__device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid, const GemmArgs* p2 = nullptr) {
   using G = EpiGeom<NT>;
   constexpr int NTW = G::NTW, WPM = G::WPM, MTB = G::MTB;
   __shared__ EpiShared<NT> sh;
@@ -105,12 +109,13 @@ __device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid) 
 
   // A fragment of k-step kk (slice s = 4*kk + kg) for this lane's row: its address, and the
   // value it takes instead when the slice is padding (0) or the tap is outside the image (fill)
-  auto addr_a = [&](int kk, bool& use, int& alt) -> const v4i* {
+  auto addr_aq = [&](const GemmArgs& q, int kk, bool& use, int& alt) -> const v4i* {
+    const lbt_conv_desc& d = q.d;
     const int s = kk * 4 + kg;
     use = false;
     alt = 0;
-    if (s >= p.nslices) return reinterpret_cast<const v4i*>(p.a);
-    alt = MODE == MODE_DGRAD ? 0 : p.a_fill;
+    if (s >= q.nslices) return reinterpret_cast<const v4i*>(q.a);
+    alt = MODE == MODE_DGRAD ? 0 : q.a_fill;
     const int tap = s / CS, cs = s - tap * CS;
     const int kh = tap / d.KW, kw = tap - kh * d.KW;
     int sy, sx;
@@ -126,16 +131,18 @@ __device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid) 
       ok = ny >= 0 && nx >= 0 && sy * d.SH == ny && sx * d.SW == nx && sy < SH && sx < SW;
     }
     use = ok && row_ok;
-    if (!use) return reinterpret_cast<const v4i*>(p.a);
-    return reinterpret_cast<const v4i*>(p.a + (((int64_t)n * SH + sy) * SW + sx) * cred + cs * 16);
+    if (!use) return reinterpret_cast<const v4i*>(q.a);
+    return reinterpret_cast<const v4i*>(q.a + (((int64_t)n * SH + sy) * SW + sx) * cred + cs * 16);
   };
-  auto load_b = [&](int kk, int j) -> v4i {
+  auto addr_a = [&](int kk, bool& use, int& alt) -> const v4i* { return addr_aq(p, kk, use, alt); };
+  auto load_bq = [&](const GemmArgs& q, int kk, int j) -> v4i {
     const int col = (nt0 + j) * 16 + r;
     if constexpr (W4)
-      return unpack_i4x16(*reinterpret_cast<const v2i*>(p.b + ((int64_t)col * p.ks + kk * 4 + kg) * 8));
+      return unpack_i4x16(*reinterpret_cast<const v2i*>(q.b + ((int64_t)col * q.ks + kk * 4 + kg) * 8));
     else
-      return *reinterpret_cast<const v4i*>(p.b + ((int64_t)col * p.ks + kk * 4 + kg) * 16);
+      return *reinterpret_cast<const v4i*>(q.b + ((int64_t)col * q.ks + kk * 4 + kg) * 16);
   };
+  auto load_b = [&](int kk, int j) -> v4i { return load_bq(p, kk, j); };
 
   v4i acc[NTW];
 #pragma unroll
@@ -219,6 +226,28 @@ __device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid) 
         }
     }
   }
+  if constexpr (DUAL) {
+    static_assert(MODE == MODE_DGRAD && CF != 0, "dual GEMM: dgrad + pass A only");
+    const GemmArgs& q = *p2;
+    v4i acc2[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc2[j] = v4i{0, 0, 0, 0};
+    const int nks2 = q.ks >> 2;
+    for (int kk = 0; kk < nks2; ++kk) {
+      bool use;
+      int alt;
+      const v4i* pa = addr_aq(q, kk, use, alt);
+      v4i a = *pa;
+      if (!use) a = v4i{alt, alt, alt, alt};
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc2[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, load_bq(q, kk, j), acc2[j], 0, 0, 0);
+    }
+    const float scale2 = ldexpf(1.0f, -(frac_exp(q.qa) + frac_exp(q.qb)));
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cp.add[j][i] = (float)acc2[j][i] * scale2;
+  }
   LBT_TS(1);
 
   // ---------------- epilogue: lane owns column (nt0+j)*16 + r of rows mtile*16 + 4*kg + i
@@ -230,7 +259,7 @@ __device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid) 
     for (int i = 0; i < 4; ++i) v[j][i] = (float)(acc[j][i] + corr[j]) * scale;
   if constexpr (CF != 0) {
     LBT_TS(2);
-    chain_epi<NT, NB, CF>(p.chain, p.add_src != nullptr, p.M, p.ncol, mtile, nt0, wave, lane, v, cp, csh);
+    chain_epi<NT, NB, CF>(p.chain, DUAL || p.add_src != nullptr, p.M, p.ncol, mtile, nt0, wave, lane, v, cp, csh);
     LBT_TS(3);
     return;
   }
@@ -256,6 +285,14 @@ template <int MODE, int CS, int NT, int CF = 0, int NB = 1, bool W4 = false>
 __global__ __launch_bounds__(kThreads, (CS == 1 && MODE == MODE_DGRAD && NB == 1) ? 8 : 1) void conv_gemm_kernel(
     GemmArgs p) {
   conv_gemm_body<MODE, CS, NT, CF, NB, W4>(p, blockIdx.x);
+}
+
+// dgrad + pass A of a projection block's input gradient: its 3x3/2 conv's dgrad (p) plus the 1x1/2
+// shortcut's (p2) in one launch (was: the shortcut's dgrad to an fp32 buffer, then p with it as
+// add_src)
+template <int CS, int NT, int CF, int NB, bool W4>
+__global__ __launch_bounds__(kThreads) void conv_dgrad2_kernel(GemmArgs p, GemmArgs p2) {
+  conv_gemm_body<MODE_DGRAD, CS, NT, CF, NB, W4, true>(p, blockIdx.x, &p2);
 }
 
 // Two independent GEMMs of one geometry class (same CS / NT / M) in one grid: workgroups [0, nb0)
@@ -654,6 +691,57 @@ int dgrad_chain(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d
   return LBT_EINVAL;
 }
 
+template <int CS, int NT, int CF, int NB, bool W4>
+int launch_dgrad2(const GemmArgs& p, const GemmArgs& p2, hipStream_t st) {
+  constexpr int MTB = EpiGeom<NT>::MTB;
+  const int64_t blocks = ((p.M + 15) / 16 + MTB - 1) / MTB;
+  hipLaunchKernelGGL((conv_dgrad2_kernel<CS, NT, CF, NB, W4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, p, p2);
+  return (int)hipGetLastError();
+}
+
+// dgrad (gq, wd, d) + dgrad (gq2, wd2, d2) + pass A, one launch (see conv_dgrad2_kernel)
+template <bool W4>
+int dgrad2_chain(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
+                 const int8_t* gq2, const int8_t* wd2, int32_t ksd2, lbt_conv_desc d2, lbt_qdesc qg2, lbt_qdesc qw2,
+                 const lbt_chain_bwd_a* a, void* stream) {
+  if (!desc_ok(d) || !desc_ok(d2) || d.Cin % 16 || d.Cout % 16 || d.Cin > 128 || !a) return LBT_EINVAL;
+  // same input-gradient pixels and channels, same gathered-gradient geometry
+  if (d2.N != d.N || d2.H != d.H || d2.W != d.W || d2.Cin != d.Cin || d2.Cout != d.Cout || d2.Ho != d.Ho ||
+      d2.Wo != d.Wo)
+    return LBT_EINVAL;
+  if (a->C != d.Cin || a->rows != d.N || a->inner != (int64_t)d.H * d.W * d.Cin) return LBT_EINVAL;
+  const int f = bwd_a_flags(*a);
+  if ((f & kAFused) != kAFused) return LBT_EINVAL;
+  const lbt_bwd_branch* br[2] = {&a->b1, &a->b2};
+  for (int b = 0; b < (a->has_b2 ? 2 : 1); ++b)
+    if (!br[b]->qrg.noise || !br[b]->qng.noise || !br[b]->gb) return LBT_EINVAL;
+  const int cs = d.Cout / 16;
+  GemmArgs p, p2;
+  p.a = gq; p.b = wd; p.ks = ksd; p.nslices = d.KH * d.KW * cs;
+  p2.a = gq2; p2.b = wd2; p2.ks = ksd2; p2.nslices = d2.KH * d2.KW * cs;
+  if (ksd % 4 || ksd < p.nslices || ksd2 % 4 || ksd2 < p2.nslices) return LBT_EINVAL;
+  p.a_fill = p2.a_fill = 0; p.colsum = p2.colsum = nullptr;
+  p.d = d; p.qa = qg; p.qb = qw; p.y = nullptr; p.add_src = nullptr; p.yq = nullptr; p.qout = lbt_qdesc{};
+  p.ychsum = nullptr;
+  p.M = (int64_t)d.N * d.H * d.W; p.ncol = d.Cin;
+  p.chain = *a;
+  p2.d = d2; p2.qa = qg2; p2.qb = qw2; p2.y = nullptr; p2.add_src = nullptr; p2.yq = nullptr; p2.qout = lbt_qdesc{};
+  p2.ychsum = nullptr; p2.M = p.M; p2.ncol = p.ncol; p2.chain = lbt_chain_bwd_a{};
+  if (p.M * p.ncol >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int nt = d.Cin / 16;
+  const int key = (cs << 8) | (nt << 4) | (a->has_b2 ? 1 : 0);
+#define LBT_D2(CS_, NT_, CF_, NB_)                                                                \
+  if (key == ((CS_ << 8) | (NT_ << 4) | (NB_ == 2)) && f == (CF_))                                  \
+    return launch_dgrad2<CS_, NT_, CF_, NB_, W4>(p, p2, st);
+  // projection blocks (Cout = 2 Cin) whose input gradient feeds an identity block's end chain or
+  // the stem's
+  LBT_D2(2, 1, kAFused | kAYMask | kAGmask, 1) LBT_D2(4, 2, kAFused | kAYMask | kAGmask, 1)
+  LBT_D2(2, 1, kAFused | kAYMask, 1) LBT_D2(4, 2, kAFused | kAYMask, 1)
+#undef LBT_D2
+  return LBT_EINVAL;
+}
+
 template <bool W4>
 int dgrad_chain_wgrad(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg, lbt_qdesc qw,
                       const float* add_src, const lbt_chain_bwd_a* a, const int8_t* xq, int32_t x_u8off,
@@ -667,6 +755,16 @@ int dgrad_chain_wgrad(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_
 
 }  // namespace
 
+extern "C" int lbt_conv_dgrad2_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                                        lbt_qdesc qw, const int8_t* gq2, const int8_t* wd2, int32_t ksd2,
+                                        lbt_conv_desc d2, lbt_qdesc qg2, lbt_qdesc qw2, int32_t w4,
+                                        const lbt_chain_bwd_a* a, void* stream) {
+  if (w4) {
+    if (qw.bits > 4 || qw2.bits > 4) return LBT_EINVAL;
+    return dgrad2_chain<true>(gq, wd, ksd, d, qg, qw, gq2, wd2, ksd2, d2, qg2, qw2, a, stream);
+  }
+  return dgrad2_chain<false>(gq, wd, ksd, d, qg, qw, gq2, wd2, ksd2, d2, qg2, qw2, a, stream);
+}
 extern "C" int lbt_conv_dgrad_chain_i8(const int8_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                                        lbt_qdesc qw, const float* add_src, const lbt_chain_bwd_a* a, void* stream) {
   return dgrad_chain<false>(gq, wd, ksd, d, qg, qw, add_src, a, nullptr, 0, stream);

@@ -896,7 +896,10 @@ class FusedResNet:
                          nb=ops._chain_bwd_b_bytes(aB1)))
         keep.append(aB1)
         add = gm
-        if cs is not None:
+        # conv-1's and the shortcut's dgrads (+ the consumer's pass A) as ONE launch
+        dual = (self.pair_launch and cs is not None and not fb1 and fuse and not (self.fuse_wgrad and not self.batch_wgrad)
+                and (Cin, C) in ((16, 32), (32, 64)) and getattr(c1, "w4", False) == getattr(cs, "w4", False))
+        if cs is not None and not dual:
             dsg = self._buf(k + "dsc", f["Xin"].shape, torch.float32)
             bwd.append(L(self._fn(cs, "lbt_conv_dgrad_i8"), ptr(gqs), self._wd(cs), cs.ksd, ds, self._qd(cs.grad_range),
                          cs.W_range.desc, ptr(dsg), None, k="conv_gemm_kernel<1> (dgrad)",
@@ -917,6 +920,13 @@ class FusedResNet:
                              self._qd(c1.grad_range), c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]),
                              ptr(f["xa"]), 1, ptr(slab1), sp1, ns1, k="dgrad_wgrad_kernel",
                              nb=nb + nb_wg1 - gq1.numel()))
+            elif dual:
+                nb = (ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], False)
+                      + gqs.numel() + cs.wd.numel())
+                bwd.append(L("lbt_conv_dgrad2_chain_i8", ptr(gq1), self._wd(c1), c1.ksd, d1, self._qd(c1.grad_range),
+                             c1.W_range.desc, ptr(gqs), self._wd(cs), cs.ksd, ds, self._qd(cs.grad_range),
+                             cs.W_range.desc, 1 if getattr(c1, "w4", False) else 0, ctypes.byref(consumer["a"]),
+                             k="conv_dgrad2_kernel (dgrad x2 + A)", nb=nb))
             else:
                 bwd.append(L(self._fn(c1, "lbt_conv_dgrad_chain_i8"), ptr(gq1), self._wd(c1), c1.ksd, d1,
                              self._qd(c1.grad_range), c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]),

@@ -763,8 +763,9 @@ def test_fused_conv_backward_equals_launch_pair(B, w4):
 
 @pytest.mark.parametrize("w4", [False, True])
 def test_pair_launches_equal_single_launches(w4):
-    """lbt_conv_fwd_pair_i8 (a projection block's 3x3/2 conv and 1x1/2 shortcut in one launch) and
-    lbt_bn_chain_bwd_b_pair (its shortcut-BN and first-BN pass B in one launch) == the single
+    """lbt_conv_fwd_pair_i8 (a projection block's 3x3/2 conv and 1x1/2 shortcut in one launch),
+    lbt_bn_chain_bwd_b_pair (its shortcut-BN and first-BN pass B in one launch) and
+    lbt_conv_dgrad2_chain_i8 (both convs' dgrads + the consumer's pass A in one launch) == the single
     launches they replace: gradients, momentum, weights, exponents, BN running statistics and loss
     bit-identical after two graph-replayed optimiser steps at B=128."""
     from lbt_amd.fused import FusedResNet
@@ -782,7 +783,8 @@ def test_pair_launches_equal_single_launches(w4):
         torch.cuda.synchronize()
         nf = sum(1 for f in m._fwd if getattr(f, "kname", "").startswith("conv_gemm2_kernel"))
         nb = sum(1 for f in m._bwd if getattr(f, "kname", "") == "chain_bwd_b2_kernel")
-        assert (nf, nb) == ((2, 2) if pair else (0, 0)), (nf, nb)
+        nd = sum(1 for f in m._bwd if getattr(f, "kname", "").startswith("conv_dgrad2_kernel"))
+        assert (nf, nb, nd) == ((2, 2, 2) if pair else (0, 0, 0)), (nf, nb, nd)
         bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
         outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,
                      m.loss.item()))
