@@ -233,8 +233,6 @@ class Conv2d_q(Layer_q):
             return
         # int8 MFMA kernels: 8-bit codes on both GEMM sides (16-bit gradients: generic int64 kernels)
         self.mfma = ops.mfma_ok(Cin, Cout) and bits <= 8 and grad_bits <= 8
-        if grad_bits > 8 and use_bias:
-            raise NotImplementedError("bias with > 8-bit gradient codes")
         # x codes: unsigned 9-bit (offset int8, MFMA) / signed <= 8 bit (int8, MFMA) / int16 (VALU)
         # wide layers (channels beyond the register-resident MFMA kernels, or 16-bit gradients):
         # LDS-tiled MFMA implicit GEMMs (igemm.hip) -- the weight gradient too when the input is a
@@ -387,7 +385,12 @@ class Conv2d_q(Layer_q):
         d = self.d
         dev = grad.device
         K = d.KH * d.KW * d.Cin
-        self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16, dev))
+        # db = sum of the quantised gradient per channel (:303-304): the quantiser's exact channel sums
+        gsum = self._c.sums("gsum", ops.NSHARD * 2 * d.Cout, self.ctx) if self.use_bias else None
+        self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16, dev),
+                                  chsum=gsum, C=d.Cout if self.use_bias else 0)
+        if self.use_bias:
+            ops.bias_grad(gsum, d.Cout, self.grad_range.desc, self.db)
         if self.igemm_w:
             self._wgrad_igemm(1)
         elif self.stem_wide(d):
@@ -560,10 +563,12 @@ class Dense_q(Layer_q):
             dx = _conv_bwd_f32(self, self.gradq, d, dev)
             return dx.view(d.N, self.in_units)
         if self.grad_bits > 8:
-            if self.use_bias:
-                raise NotImplementedError("bias with > 8-bit gradient codes")
+            gsum = self._c.sums("gsum", ops.NSHARD * 2 * self.units, self.ctx) if self.use_bias else None
             self.gradq = ops.quantize(grad, self.grad_range, OUT_I16, out=self._c.get("gq16", grad.shape, torch.int16,
-                                                                                       dev))
+                                                                                       dev),
+                                      chsum=gsum, C=self.units if self.use_bias else 0)
+            if self.use_bias:  # db = the quantised gradient summed per unit (:457)
+                ops.bias_grad(gsum, self.units, self.grad_range.desc, self.db)
             if self.mfma:
                 return self._backward_mfma(dev)
             ns = ops.wgrad_nsplit(d, generic=True)

@@ -192,3 +192,42 @@ def test_resnet20_20bit_step_matches_oracle():
         assert np.abs(a - b).max() <= 1e-4 * np.abs(b).max() + 1e-12, k
     ctx.update_range_op()
     assert ctx.ranges() == octx.new_ranges()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,shape", [("conv", (4, 8, 8, 16, 32, 3, 1)), ("conv", (2, 8, 8, 64, 64, 1, 2)),
+                                        ("dense", (33, 64, 10, 0, 0, 0, 0))])
+def test_bias_with_16bit_gradients_matches_oracle(kind, shape):
+    """Conv2d_q / Dense_q with use_bias=True and 16-bit gradient codes (config 4 with the
+    batch_norm=False blocks of ResidualBlock_q, dynamic_fixed_point.py:778): db = the quantised
+    gradient summed per channel (:303-304, :457) from the quantiser's exact channel sums; dW, db and
+    dX bit-exact against the oracle, exponents identical."""
+    rng = np.random.default_rng(sum(shape))
+    ctx = DfxpContext(seed=17)
+    if kind == "conv":
+        N, H, Cin, Cout, k, s = shape[0], shape[1], shape[3], shape[4], shape[5], shape[6]
+        gl = D.Conv2d_q("c", 8, [k, k, Cin, Cout], [1, s, s, 1], "SAME", use_bias=True, weight_decay=2e-4,
+                        grad_bits=16, ctx=ctx)
+        ol = onn.Conv2dQ("c", 8, [k, k, Cin, Cout], [1, s, s, 1], "SAME", 2e-4, grad_bits=16, use_bias=True)
+        x = rng.uniform(-1.5, 1.5, size=(N, H, H, Cin)).astype(F32)
+    else:
+        N, Cin, Cout = shape[0], shape[1], shape[2]
+        gl = D.Dense_q("fc", 8, Cin, Cout, use_bias=True, weight_decay=2e-4, grad_bits=16, ctx=ctx)
+        ol = onn.DenseQ("fc", 8, Cin, Cout, 2e-4, use_bias=True, grad_bits=16)
+        x = rng.uniform(-2, 2, size=(N, Cin)).astype(F32)
+    ol.W = gl.W.cpu().numpy().copy()
+    b = (0.1 * rng.standard_normal(Cout)).astype(F32)
+    gl.b.copy_(torch.from_numpy(b))
+    ol.b = b.copy()
+    octx = onn.Ctx(ctx.ranges(), 0, 17)
+    y = gl.forward(torch.from_numpy(x).to(DEV))
+    yr = ol.forward(x, octx)
+    assert np.array_equal(y.cpu().numpy(), yr)
+    g = rng.normal(0, 0.01, size=yr.shape).astype(F32)
+    dx = gl.backward(torch.from_numpy(g).to(DEV))
+    dxr = ol.backward(g, octx)
+    assert np.array_equal(gl.dW.cpu().numpy(), ol.dW)
+    assert np.array_equal(gl.db.cpu().numpy(), ol.db)
+    assert np.array_equal(dx.cpu().numpy(), dxr)
+    ctx.update_range_op()
+    assert ctx.ranges() == octx.new_ranges()
