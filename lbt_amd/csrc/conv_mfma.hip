@@ -1106,13 +1106,29 @@ LBT_DEV float4 ld4f(const float* p, int64_t i) { return *reinterpret_cast<const 
 // rotations inside each 16-lane row, then the rows paired by a lane shuffle (xor 16) and the halves
 // by v_permlane32_swap (its two results are the lane's own half and the other half, both ways:
 // their sum is the pair total in every lane). The total lands in every lane.
+// (The row pairing is v_permlane16_swap: its two results hold the lane's own row and the paired
+// row, both ways -- a VALU exchange where __shfl_xor(v, 16) was an LDS ds_bpermute round trip.)
+LBT_DEV int row_pair_sum(int v) {
+  const auto h = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return (int)h[0] + (int)h[1];
+}
+LBT_DEV int half_pair_sum(int v) {
+  const auto h = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (int)h[0] + (int)h[1];
+}
 template <int C4>
 LBT_DEV int chan_reduce(int v) {
   if constexpr (C4 <= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
   if constexpr (C4 <= 4) v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);  // row_ror:4
-  v += __shfl_xor(v, 16, 64);
-  const auto h = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return (int)h[0] + (int)h[1];
+  return half_pair_sum(row_pair_sum(v));
+}
+// the whole wave's total in every lane, on DPP / permlane swaps only (no LDS)
+LBT_DEV int wave_total(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  return half_pair_sum(row_pair_sum(v));
 }
 
 // Stochastic quantiser (quant_w<1>'s arithmetic) with PER-LANE overflow counts, on the VALU only:
@@ -1138,7 +1154,7 @@ LBT_DEV void pin_counts(int& c1, int& c2) { asm volatile("" : "+v"(c1), "+v"(c2)
 LBT_DEV float ov_thr(bool cnt, float T) { return cnt ? T : __builtin_nanf(""); }
 // lane counts (each < 2^16) -> the wave totals, in every lane
 LBT_DEV void ov_wave(int& c1, int& c2) {
-  const int t = wave_sum_i32(c1 | (c2 << 16));
+  const int t = wave_total(c1 | (c2 << 16));
   c1 = t & 0xffff;
   c2 = t >> 16;
 }
