@@ -1116,6 +1116,17 @@ LBT_DEV int half_pair_sum(int v) {
   const auto h = __builtin_amdgcn_permlane32_swap(v, v, false, false);
   return (int)h[0] + (int)h[1];
 }
+// 64-bit sum over the four 16-lane rows of a wave (permlane16 then permlane32 swaps on both halves)
+LBT_DEV long long rows_total64(long long v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)((unsigned long long)v >> 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  v = (long long)(((unsigned long long)b[0] << 32) | a[0]) + (long long)(((unsigned long long)b[1] << 32) | a[1]);
+  const uint32_t lo2 = (uint32_t)v, hi2 = (uint32_t)((unsigned long long)v >> 32);
+  const auto c = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
+  const auto d = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
+  return (long long)(((unsigned long long)d[0] << 32) | c[0]) + (long long)(((unsigned long long)d[1] << 32) | c[1]);
+}
 template <int C4>
 LBT_DEV int chan_reduce(int v) {
   if constexpr (C4 <= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
@@ -1229,14 +1240,19 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
 
   // ---------------- the pass-B statistics' shard sums first (they gate the first barrier): 16 groups
   // of 32 lanes, lane = shard, group g owning channels g*CPG .. g*CPG+CPG-1 (SG, SGQ)
-  static_assert(LBT_NSHARD == 32 && kBThreads == 512 && C % 16 == 0, "statistics layout");
-  constexpr int CPG = C / 16;
-  long long sv[CPG][2];
+  // Waves w < C / 16 each own 16 channels: lane l reads channel w*16 + (l & 15) of shards
+  // 8*(l >> 4) .. +7, so every load instruction covers 4 shards x 16 consecutive channels (128-byte
+  // rows); rows_total64 adds the wave's four lane rows.
+  static_assert(LBT_NSHARD == 32 && kBThreads == 512 && C % 16 == 0 && C / 16 <= kBNW, "statistics layout");
+  constexpr int kSW = C / 16;  // statistics waves
+  long long sv[8][2];
+  if (wave < kSW) {  // uniform per wave
+    const int64_t* ps = B.sums + (int64_t)(8 * (lane >> 4)) * 4 * C + wave * 16 + (lane & 15);
 #pragma unroll
-  for (int i = 0; i < CPG; ++i) {
-    const int64_t* ps = B.sums + (int64_t)(tid & 31) * 4 * C + (tid >> 5) * CPG + i;
-    sv[i][0] = ps[2 * C];
-    sv[i][1] = ps[3 * C];
+    for (int i = 0; i < 8; ++i) {
+      sv[i][0] = ps[(int64_t)i * 4 * C + 2 * C];
+      sv[i][1] = ps[(int64_t)i * 4 * C + 3 * C];
+    }
   }
   // then every load that does not depend on the sums
   // phase-1 operands: G / q codes and the output quantiser's noise over the halo rows
@@ -1286,27 +1302,26 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
   const float scale = ldexpf(1.0f, -(frac_exp(B.qo) + frac_exp(p.qw)));
 
-  // ---------------- pass-B statistics: the shard sums (loaded first, above) reduced over 32-lane
-  // groups (lane = shard, group g owns channels g*CPG ..), lane i < CPG of the group finishing
-  // channel g*CPG + i in double exactly as chain_bwd_b_kernel
-#pragma unroll
-  for (int i = 0; i < CPG; ++i)
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      sv[i][0] += __shfl_xor(sv[i][0], o, 64);
-      sv[i][1] += __shfl_xor(sv[i][1], o, 64);
-    }
-  if ((tid & 31) < CPG) {
+  // ---------------- pass-B statistics: the shard sums (loaded first, above) added per lane, then over
+  // the statistics wave's four lane rows; lanes < 16 finish their channel in double exactly as
+  // chain_bwd_b_kernel
+  if (wave < kSW) {
     long long SGi = 0, SGQi = 0;
 #pragma unroll
-    for (int i = 0; i < CPG; ++i)
-      if ((tid & 31) == i) { SGi = sv[i][0]; SGQi = sv[i][1]; }
-    const int c = (tid >> 5) * CPG + (tid & 31);
+    for (int i = 0; i < 8; ++i) {
+      SGi += sv[i][0];
+      SGQi += sv[i][1];
+    }
+    SGi = rows_total64(SGi);
+    SGQi = rows_total64(SGQi);
+    const int c = wave * 16 + (lane & 15);
+    if (lane < 16) {
     const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, nn = (double)B.n;
     const double SG = (double)SGi, SGQ = (double)SGQi;
     const float m = B.ms[c], sig = B.ms[C + c];
     sh.pb[c] = (float)(gsc * SG / nn);
     sh.pb[C + c] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
+    }
   }
   __syncthreads();
   LBT_TS(1);
@@ -1687,15 +1702,20 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
 
   // ---------------- the moments' shard sums first (they gate the first barrier), then the loads that
   // do not depend on the moments
-  static_assert(LBT_NSHARD == 32 && kBThreads == 512 && (NB * C) % 16 == 0, "moments layout");
-  constexpr int CPG = (NB * C) / 16;
-  long long sv[CPG][2];
+  // waves w < NB*C/16 each own 16 (branch, channel) pairs: lane l reads pair w*16 + (l & 15) of
+  // shards 8*(l >> 4) .. +7 (each load instruction: 4 shards x 16 consecutive channels)
+  static_assert(LBT_NSHARD == 32 && kBThreads == 512 && (NB * C) % 16 == 0 && NB * C / 16 <= kBNW,
+                "moments layout");
+  constexpr int kSW = NB * C / 16;  // statistics waves
+  long long sv[8][2];
+  if (wave < kSW) {  // uniform per wave
+    const int bc = wave * 16 + (lane & 15), b = bc / C, c = bc - b * C;
+    const int64_t* cs = (b == 0 ? a.b1 : a.b2).nrm.chsum + (int64_t)(8 * (lane >> 4)) * 2 * C + c;
 #pragma unroll
-  for (int i = 0; i < CPG; ++i) {
-    const int bc = (tid >> 5) * CPG + i, b = bc / C, c = bc - b * C;
-    const int64_t* cs = (b == 0 ? a.b1 : a.b2).nrm.chsum + (int64_t)(tid & 31) * 2 * C + c;
-    sv[i][0] = cs[0];
-    sv[i][1] = cs[C];
+    for (int i = 0; i < 8; ++i) {
+      sv[i][0] = cs[(int64_t)i * 2 * C];
+      sv[i][1] = cs[(int64_t)i * 2 * C + C];
+    }
   }
   const int ngrp = (TH + 2) * Wp * C4;
   int qv[NB][kBIt];
@@ -1750,24 +1770,21 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   const QState so1 = qstate(a.qo1), sq = qstate(p.qout);
   const float scale = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw)));
 
-  // ---------------- Normalization_q moments (bn.hip bn_moments). The shard sums: 16 groups of 32
-  // lanes, lane = shard, group g owning (branch, channel) pairs g*CPG .. g*CPG+CPG-1; a 32-lane
-  // butterfly leaves the totals in every lane of the group and lane i < CPG finishes pair g*CPG+i.
+  // ---------------- Normalization_q moments (bn.hip bn_moments) from the shard sums loaded above: each
+  // statistics wave adds its 8 shards per lane, then its four lane rows; lanes < 16 finish a pair.
   // (Was: threads c < C loading all 2 x 32 shards each -- 64 dependent-issue loads in one wave on
   // the launch's critical path.)
-#pragma unroll
-  for (int i = 0; i < CPG; ++i)
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      sv[i][0] += __shfl_xor(sv[i][0], o, 64);
-      sv[i][1] += __shfl_xor(sv[i][1], o, 64);
-    }
-  if ((tid & 31) < CPG) {
+  if (wave < kSW) {
     long long S1 = 0, S2 = 0;
 #pragma unroll
-    for (int i = 0; i < CPG; ++i)
-      if ((tid & 31) == i) { S1 = sv[i][0]; S2 = sv[i][1]; }
-    const int bc = (tid >> 5) * CPG + (tid & 31), b = bc / C, c = bc - b * C;
+    for (int i = 0; i < 8; ++i) {
+      S1 += sv[i][0];
+      S2 += sv[i][1];
+    }
+    S1 = rows_total64(S1);
+    S2 = rows_total64(S2);
+    const int bc = wave * 16 + (lane & 15), b = bc / C, c = bc - b * C;
+    if (lane < 16) {
     const lbt_bn_norm& nb = b == 0 ? a.b1.nrm : a.b2.nrm;
     const double s = ldexp(1.0, -frac_exp(nb.qn));
     const double mean_d = (double)S1 * s / (double)nb.n;
@@ -1782,6 +1799,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
         nb.run_mean[c] = nb.momentum * nb.run_mean[c] + nb.one_minus_momentum * m;
         nb.run_var[c] = nb.momentum * nb.run_var[c] + nb.one_minus_momentum * vv;
       }
+    }
     }
   }
   __syncthreads();
