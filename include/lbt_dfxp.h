@@ -549,6 +549,10 @@ typedef struct lbt_head {
   float* gx;
   void* scratch;
   int32_t loss_n;
+  /* optional: pass A of the last block's output BatchNorm chain (one branch, ReLU mask from
+   * y_mask, gmask_out, stochastic quantisers; a.g unused) run per sample on the un-pooled gradient
+   * inside this launch -- then gx is not written. Bit-identical to lbt_bn_chain_bwd_a(a) on gx. */
+  const lbt_chain_bwd_a* pa;
 } lbt_head;
 int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K);  /* = N * (C + 72) */
 int lbt_head_fwd_bwd(const lbt_head* h, void* stream);

@@ -132,7 +132,7 @@ class Head(ctypes.Structure):
                 ("gq", c_void_p), ("qg", QDesc),
                 ("w", c_void_p), ("wd2", c_float), ("dw", c_void_p),
                 ("gx", c_void_p),
-                ("scratch", c_void_p), ("loss_n", c_int32)]
+                ("scratch", c_void_p), ("loss_n", c_int32), ("pa", c_void_p)]
 
 
 class Xchg(ctypes.Structure):

@@ -34,12 +34,92 @@ LBT_DEV float head_noise(const lbt_qdesc& q, const QState& s, int i, int n) {
   return (s.active && q.stochastic) ? (tab ? tv : pv) : 0.f;
 }
 
-__global__ __launch_bounds__(kT) void head_kernel(lbt_head h) {
+// Pass A (bn.hip chain_bwd_a_kernel<1, kAFB | kAStoch | kAYMask | kAGmask>'s arithmetic, element for
+// element) of sample n's gradient g[p][c] = s_dp[c] * (1/HW), the value the un-pool writes: ReLU
+// mask from y_mask, gmask_out, the Rescale_q gradient quantiser (sums G2*R, G2), times gamma_q, the
+// Normalization_q gradient quantiser (codes to gout, sums G, G*q), overflow counters. Thread t owns
+// the channel quad c0 = 4t mod C of quads t, t + 256, ... (C | 1024). Every thread calls it.
+LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const float* s_dp, int* sh_cnt) {
+  __shared__ int s_sum[kT / 64][4 * 256];  // per wave: [sum][channel] (|.| < 2^19)
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const lbt_bwd_branch& B = a.b1;
+  const QState qrg = qstate(B.qrg), qng = qstate(B.qng);
+  const int nq = HW * C / 4, c0 = (4 * t) % C;
+  const int64_t base = (int64_t)n * HW * C;
+  const float inv = 1.0f / (float)HW;
+  float gam[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) gam[k] = B.gb[c0 + k];
+  int ov[2][2] = {{0, 0}, {0, 0}};
+  int acc[4][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[s][k] = 0;
+  for (int q = t; q < nq; q += kT) {  // (C % 4 == 0, so c0 is this thread's quad in every pass)
+    const int64_t e = base + 4 * (int64_t)q;
+    const float4 ym4 = *reinterpret_cast<const float4*>(a.y_mask + e);
+    const int Rw = *reinterpret_cast<const int*>(B.R + e);
+    const int qw = *reinterpret_cast<const int*>(B.qn_codes + e);
+    const Noise4 nrg = (qrg.active && B.qrg.stochastic) ? qnoise4(B.qrg, qrg.step, (uint64_t)q) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+    const Noise4 nng = (qng.active && B.qng.stochastic) ? qnoise4(B.qng, qng.step, (uint64_t)q) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+    const float ym[4] = {ym4.x, ym4.y, ym4.z, ym4.w};
+    float gv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float g = s_dp[c0 + k] * inv;
+      gv[k] = ym[k] > 0.f ? g : 0.f;
+    }
+    if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+    int G[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int R = (int)(int8_t)(Rw >> (8 * k)), qn = (int)(int8_t)(qw >> (8 * k));
+      const int G2 = quant_w<1>(qrg, 1, gv[k], nrg.u[k], ov[0][0], ov[0][1]);
+      acc[0][k] += G2 * R;
+      acc[1][k] += G2;
+      const float gh = (float)G2 * qrg.inv_m;
+      const float d = gh * gam[k];
+      G[k] = quant_w<1>(qng, 1, d, nng.u[k], ov[1][0], ov[1][1]);
+      acc[2][k] += G[k];
+      acc[3][k] += G[k] * qn;
+    }
+    *reinterpret_cast<int*>(B.gout + e) =
+        (int)((uint32_t)(G[0] & 255) | ((uint32_t)(G[1] & 255) << 8) | ((uint32_t)(G[2] & 255) << 16) | ((uint32_t)G[3] << 24));
+  }
+  // channel sums: the lanes sharing a quad (t = c0/4 mod C/4) meet by shuffles within the wave, the
+  // waves in LDS; one int64 atomic per (sum, channel) into this sample's shard
+  const int per = C / 4;  // lanes l, l + per, ... share a quad (per | 64)
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int v = acc[s][k];
+      for (int o = per; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (lane < per) s_sum[wave][s * C + c0 + k] = v;
+    }
+  counts_stage_w(2, 4, ov[0][0], ov[0][1], sh_cnt);
+  counts_stage_w(3, 4, ov[1][0], ov[1][1], sh_cnt);
+  __syncthreads();
+  if (qrg.active) counts_publish(2, 4, B.qrg, sh_cnt);
+  if (qng.active) counts_publish(3, 4, B.qng, sh_cnt);
+  if (B.sums) {
+    int64_t* dst = B.sums + (int64_t)shard_id() * 4 * C;
+    for (int i = t; i < 4 * C; i += kT) {
+      long long v = 0;
+#pragma unroll
+      for (int w = 0; w < kT / 64; ++w) v += s_sum[w][i];
+      if (v) LBT_GADD((unsigned long long*)&dst[i], (unsigned long long)v);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa) {
   __shared__ __attribute__((aligned(16))) float s_x[kXChunk / 4];
   __shared__ __attribute__((aligned(16))) int8_t s_w[kMaxW];
   __shared__ int s_pq[256], s_gq[64], s_part[16][16];
   __shared__ float s_z[64], s_dp[256];
-  __shared__ int sh_cnt[2 * 2 * (kT / 64)];
+  __shared__ int sh_cnt[4 * 2 * (kT / 64)];  // counters: qx, qg (+ pass A's qrg, qng)
   const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int C = h.C, K = h.K, HW = h.HW, N = h.N;
   LBT_TS(0);
@@ -160,11 +240,11 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h) {
       *reinterpret_cast<double*>(rec + C + 64) = term;  // 8-byte aligned: C % 8 == 0
     }
   }
-  counts_stage_w(0, 2, ovx1, ovx2, sh_cnt);
-  counts_stage_w(1, 2, ovg1, ovg2, sh_cnt);
+  counts_stage_w(0, 4, ovx1, ovx2, sh_cnt);
+  counts_stage_w(1, 4, ovg1, ovg2, sh_cnt);
   __syncthreads();
-  counts_publish(0, 2, h.qx, sh_cnt);
-  counts_publish(1, 2, h.qg, sh_cnt);
+  counts_publish(0, 4, h.qx, sh_cnt);
+  counts_publish(1, 4, h.qg, sh_cnt);
 
   // ---- the record's codes: pq[C] | gq[64]
   {
@@ -195,6 +275,11 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h) {
     s_dp[t] = (float)a * ldexpf(1.0f, -(frac_exp(h.qg) + frac_exp(h.qw)));
   }
   __syncthreads();
+  if (h.pa) {  // uniform (the descriptor itself travels by value in pa)
+    head_pass_a(pa, n, HW, C, s_dp, sh_cnt);
+    LBT_TS(2);
+    return;
+  }
   {
     const float inv = 1.0f / (float)HW;
     float4* gx = reinterpret_cast<float4*>(h.gx + (int64_t)n * HW * C);
@@ -221,11 +306,20 @@ extern "C" int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K) {
 
 extern "C" int lbt_head_fwd_bwd(const lbt_head* h, void* stream) {
   if (!h || h->N <= 0 || h->HW <= 0 || h->C <= 0 || h->C > 256 || h->C % 8 || h->K <= 0 || h->K > 64) return LBT_EINVAL;
-  if (!h->x || !h->wq || !h->labels || !h->logits || !h->dz || !h->gx || !h->scratch) return LBT_EINVAL;
+  if (!h->x || !h->wq || !h->labels || !h->logits || !h->dz || (!h->gx && !h->pa) || !h->scratch) return LBT_EINVAL;
+  if (h->pa) {  // the fused pass A: one branch, y mask, stochastic quantisers, C | 1024, C <= 256
+    const lbt_chain_bwd_a& a = *h->pa;
+    if (a.has_b2 || !a.y_mask || a.C != h->C || a.rows != h->N || a.inner != (int64_t)h->HW * h->C ||
+        (1024 % h->C) || !a.b1.R || !a.b1.qn_codes || !a.b1.gout || !a.b1.gb || a.b1.qrg.bits <= 0 ||
+        a.b1.qng.bits <= 0 || !a.b1.qrg.stochastic || !a.b1.qng.stochastic)
+      return LBT_EINVAL;
+  }
   if ((int64_t)h->N * (h->C + kHeadRecPad) >= ((int64_t)1 << 31)) return LBT_EINVAL;
   if ((reinterpret_cast<uintptr_t>(h->wq) & 3) || (reinterpret_cast<uintptr_t>(h->x) & 15) ||
       (reinterpret_cast<uintptr_t>(h->scratch) & 7))
     return LBT_EINVAL;
-  hipLaunchKernelGGL(head_kernel, dim3((unsigned)h->N), dim3(kT), 0, (hipStream_t)stream, *h);
+  lbt_chain_bwd_a pa{};
+  if (h->pa) pa = *h->pa;
+  hipLaunchKernelGGL(head_kernel, dim3((unsigned)h->N), dim3(kT), 0, (hipStream_t)stream, *h, pa);
   return (int)hipGetLastError();
 }

@@ -105,6 +105,8 @@ class FusedResNet:
         # a projection block's two strided convs (3x3/2 + 1x1/2 shortcut) as ONE launch forward, and
         # its two pass-B chains (shortcut BN, first BN) as ONE launch backward
         self.pair_launch = os.environ.get("LBT_PAIR", "1") == "1"
+        # the last block's output BN pass A inside the fused head launch (lbt_head.pa)
+        self.head_pass_a = os.environ.get("LBT_HEAD_PASS_A", "1") == "1"
         self._side = None
         # every conv's weight gradient of the step in ONE launch at the end of the backward
         # (lbt_conv_wgrad_many_i8) instead of inside the dgrad launches: a dgrad launch's tiles fill
@@ -425,6 +427,17 @@ class FusedResNet:
         # as the epilogue of the dgrad that produces its input gradient (lbt_conv_dgrad_chain_i8),
         # except the last block's, which follows the avgpool backward.
         ends = [self._block_end_chain(i, b, saved[i], obs) for i, b in enumerate(self.blocks)]
+        # the last block's output pass A runs inside the fused head (per sample, on the un-pooled
+        # gradient it would have written); the separate head launches run it after avgpool_bwd
+        aL = ends[-1]["a"]
+        head_a = self.head_pass_a and not aL.has_b2 and bool(aL.y_mask) and (1024 % Ch == 0)
+        if head_a:
+            aL.g = gY.data_ptr()
+            hd.pa = ctypes.addressof(aL)
+            hbwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aL), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aL)))
+            # head bytes: x in, weights, and pass A's operands / outputs instead of the fp32 gx
+            hfused[0].nbytes = 4 * Ylast.numel() + d.w_hwio.numel() + ops._chain_bwd_a_bytes(aL) - 4 * Ylast.numel()
+            gY = None
         gq0 = self._buf("gq0", shp0, torch.int8)
         Gn0 = self._buf("Gn0", shp0, torch.int8)
         sums0 = self._sums("sums0", ops.NSHARD * 4 * C0)
