@@ -20,6 +20,8 @@
 //        (integer atomics) for lbt_conv_wgrad_reduce(_many).
 #include "conv_epilogue.h"
 
+#include <cstdlib>
+
 using namespace lbt;
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -113,6 +115,105 @@ __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(StemFwdArgs p) {
   if (want_q) epi_noise<NTW>(p.o, mtile, nt0, lane, u);
 #pragma unroll
   for (int jt = 0; jt < NTW; ++jt) acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[jt], acc[jt], 0, 0, 0);
+  LBT_TS(1);
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qx) + frac_exp(p.qw)));
+  float v[NTW][4];
+#pragma unroll
+  for (int jt = 0; jt < NTW; ++jt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[jt][i] = acc[jt][i] * scale;
+  if (!want_q) {
+#pragma unroll
+    for (int jt = 0; jt < NTW; ++jt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = mtile * 16 + kg * 4 + i;
+        if (row < M) p.y[row * d.Cout + (nt0 + jt) * 16 + r] = v[jt][i];
+      }
+    return;
+  }
+  LBT_TS(2);
+  epi_quant<NT>(p.o, qs, mtile, nt0, wave, lane, v, u, sh);
+  LBT_TS(3);
+}
+
+// The same conv when a block's pixels are whole output rows of one image (3x3, stride 1, SAME, W | the
+// block's MTB*16 pixels, Cin <= 4): the block first stages its input rows plus the one-row / one-column
+// halo ([rows + 2][W + 2][Cin] int16, zeros outside the image) in LDS with one coalesced load per
+// thread, and every lane gathers its 8 patch codes from there -- instead of 8 scattered 2-byte global
+// loads per lane. Same fp16 fragments, same MFMA, same epilogue: bit-identical.
+constexpr int kStemRowsMax = 4, kStemWMax = 64, kStemCinMax = 4;
+template <int NT>
+__global__ __launch_bounds__(kThreads) void stem_fwd_rows_kernel(StemFwdArgs p) {
+  using G = EpiGeom<NT>;
+  constexpr int NTW = G::NTW, WPM = G::WPM, MTB = G::MTB, PB = MTB * 16;
+  __shared__ EpiShared<NT> sh;
+  __shared__ int16_t s_img[kStemRowsMax * (kStemWMax + 2) * kStemCinMax];
+  LBT_TS(0);
+  const lbt_conv_desc& d = p.d;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int mt_local = wave / WPM;
+  const int nt0 = (wave % WPM) * NTW;
+  const int64_t mtile = (int64_t)blockIdx.x * MTB + mt_local;
+  const int r = lane & 15, kg = lane >> 4;
+  const int64_t M = p.o.M;
+  const bool want_q = p.o.yq != nullptr;
+  const QState qs = qstate(p.o.q);
+  const int W = d.W, Cin = d.Cin, HWp = d.H * d.W;
+  const int64_t m0 = (int64_t)blockIdx.x * PB;  // host: HW % PB == 0, PB % W == 0
+  const int n = (int)(m0 / HWp), oy0 = (int)(m0 - (int64_t)n * HWp) / W;
+  const int NR = PB / W + 2, NC = W + 2, E = NR * NC * Cin;
+  // ---- stage: element t = ((row * NC) + col) * Cin + ci of rows oy0-1 .. oy0+PB/W, cols -1 .. W
+  // (two elements per thread: E <= 2 * kThreads, host check; both loads issued before the stores)
+  {
+    int16_t v[2];
+    bool ok[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = (int)threadIdx.x + h * kThreads;
+      const int ci = t % Cin, pc = t / Cin, col = pc % NC, row = pc / NC;
+      const int iy = oy0 - 1 + row, ix = col - 1;
+      ok[h] = t < E && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)W;
+      v[h] = p.x[ok[h] ? (((int64_t)n * d.H + iy) * W + ix) * Cin + ci : 0];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = (int)threadIdx.x + h * kThreads;
+      if (t < E) s_img[t] = ok[h] ? v[h] : (int16_t)0;
+    }
+  }
+  // ---- operands that do not need the image: weights, epilogue noise
+  h8 b[NTW];
+  {
+    int8_t wv[NTW][8];
+#pragma unroll
+    for (int jt = 0; jt < NTW; ++jt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * kg + j;
+        wv[jt][j] = p.w[(int64_t)(k < p.K ? k : 0) * d.Cout + (nt0 + jt) * 16 + r];
+      }
+#pragma unroll
+    for (int jt = 0; jt < NTW; ++jt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[jt][j] = (_Float16)(float)(8 * kg + j < p.K ? (int)wv[jt][j] : 0);
+  }
+  float u[NTW][4];
+  if (want_q) epi_noise<NTW>(p.o, mtile, nt0, lane, u);
+  __syncthreads();
+  // ---- this lane's 8 patch codes from LDS: pixel (oy0 + ly, ox), k = 8kg + j = (tap, ci)
+  const int lm = (int)(mtile * 16 + r - m0), ly = lm / W, ox = lm - ly * W;
+  h8 a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j;
+    const int tap = k / Cin, ci = k - tap * Cin, kh = tap / 3, kw = tap - kh * 3;
+    const int v = k < p.K ? (int)s_img[((ly + kh) * NC + ox + kw) * Cin + ci] : 0;
+    a[j] = (_Float16)(float)v;
+  }
+  f4v acc[NTW];
+#pragma unroll
+  for (int jt = 0; jt < NTW; ++jt) acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[jt], f4v{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
   LBT_TS(1);
   const float scale = ldexpf(1.0f, -(frac_exp(p.qx) + frac_exp(p.qw)));
   float v[NTW][4];
@@ -234,6 +335,21 @@ extern "C" int lbt_conv_stem_fwd(const int16_t* x, const int8_t* w_hwio, lbt_con
   if (M * d.Cout >= (int64_t)1 << 31) return LBT_EINVAL;  // 32-bit element offsets
   hipStream_t st = (hipStream_t)stream;
   const int64_t mtiles = (M + 15) / 16;
+  // whole-row blocks staged in LDS (CIFAR stems): 3x3 / stride 1 / SAME, block pixels = whole rows
+  const int pb = d.Cout == 16 ? 64 : 32;  // EpiGeom<Cout/16>::MTB * 16 of the two row variants
+  if ((d.Cout == 16 || d.Cout == 32) && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
+      d.PL == 1 && d.Ho == d.H && d.Wo == d.W && d.Cin <= kStemCinMax && d.W <= kStemWMax && pb % d.W == 0 &&
+      pb / d.W + 2 <= kStemRowsMax && ((int64_t)d.H * d.W) % pb == 0 &&
+      (pb / d.W + 2) * (d.W + 2) * d.Cin <= 2 * kThreads &&
+      getenv("LBT_STEM_GATHER") == nullptr) {
+    const unsigned blocks = (unsigned)(M / pb);
+    switch (d.Cout / 16) {
+      case 1: hipLaunchKernelGGL(stem_fwd_rows_kernel<1>, dim3(blocks), dim3(kThreads), 0, st, p); break;
+      case 2: hipLaunchKernelGGL(stem_fwd_rows_kernel<2>, dim3(blocks), dim3(kThreads), 0, st, p); break;
+      default: return LBT_EINVAL;
+    }
+    return (int)hipGetLastError();
+  }
   switch (d.Cout / 16) {
     case 1: hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3((unsigned)((mtiles + 3) / 4)), dim3(kThreads), 0, st, p); break;
     case 2: hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3((unsigned)((mtiles + 1) / 2)), dim3(kThreads), 0, st, p); break;
