@@ -317,6 +317,82 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const int16_t* __r
   }
 }
 
+// stem_wgrad_kernel's arithmetic when a block's 256 pixels are whole rows of one image (3x3 / stride
+// 1 / SAME, W | 64, Cin <= 4, Cout == 16): the block stages its 256 // W input rows + halo and its
+// [256][16] gradient codes in LDS (coalesced), and the lanes build the same fp16 fragments from there.
+constexpr int kSWRows = 256 / 8 + 2;  // rows of the staged image for W >= 8
+__global__ __launch_bounds__(kThreads) void stem_wgrad_rows_kernel(const int16_t* __restrict__ x,
+                                                                   const int8_t* __restrict__ gq, lbt_conv_desc d,
+                                                                   int K, int32_t* __restrict__ slab, int nshard) {
+  __shared__ int red[4][32][64];
+  __shared__ int16_t s_img[kSWRows * (kStemWMax + 2) * kStemCinMax > 4096 ? 4096 : kSWRows * (kStemWMax + 2) * kStemCinMax];
+  __shared__ __attribute__((aligned(16))) int8_t s_g[kWgPixels * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, t = threadIdx.x;
+  const int r = lane & 15, kg = lane >> 4;
+  const int nkt = (K + 15) >> 4;
+  const int W = d.W, Cin = d.Cin, HWp = d.H * d.W;
+  const int64_t m0 = (int64_t)blockIdx.x * kWgPixels;  // host: HW % 256 == 0, 256 % W == 0
+  const int n = (int)(m0 / HWp), oy0 = (int)(m0 - (int64_t)n * HWp) / W;
+  const int NC = W + 2, E = (kWgPixels / W + 2) * NC * Cin;  // host: E <= 4096
+  // ---- stage the image rows (up to 16 per thread, all loads before the stores) and the codes
+  {
+    const int4 gv = *reinterpret_cast<const int4*>(gq + m0 * 16 + t * 16);
+    constexpr int kPer = 16;
+    int16_t v[kPer];
+    bool ok[kPer];
+#pragma unroll
+    for (int h = 0; h < kPer; ++h) {
+      const int e = t + h * kThreads;
+      const int ci = e % Cin, pc = e / Cin, col = pc % NC, row = pc / NC;
+      const int iy = oy0 - 1 + row, ix = col - 1;
+      ok[h] = e < E && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)W;
+      v[h] = x[ok[h] ? (((int64_t)n * d.H + iy) * W + ix) * Cin + ci : 0];
+    }
+#pragma unroll
+    for (int h = 0; h < kPer; ++h) {
+      const int e = t + h * kThreads;
+      if (e < E) s_img[e] = ok[h] ? v[h] : (int16_t)0;
+    }
+    *reinterpret_cast<int4*>(s_g + t * 16) = gv;
+  }
+  __syncthreads();
+  f4v acc[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) acc[kt] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    h8 a[2], b;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int k = kt * 16 + r;
+      const int tap = k / Cin, ci = k - tap * Cin, kh = tap / 3, kw = tap - kh * 3;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int lm = wave * 64 + 32 * s + 8 * kg + j, ly = lm / W, ox = lm - ly * W;
+        const int v = (kt < nkt && k < K) ? (int)s_img[((ly + kh) * NC + ox + kw) * Cin + ci] : 0;
+        a[kt][j] = (_Float16)(float)v;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = (_Float16)(float)(int)s_g[(wave * 64 + 32 * s + 8 * kg + j) * 16 + r];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+      if (kt < nkt) acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[kt], b, acc[kt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (kt < nkt) red[wave][kt * 16 + 4 * kg + i][r] = (int)acc[kt][i];
+  __syncthreads();
+  int32_t* out = slab + (int64_t)(blockIdx.x % nshard) * K * 16;
+  for (int i = threadIdx.x; i < K * 16; i += kThreads) {
+    const int k = i / 16, c = i - k * 16;
+    const int v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    if (v) LBT_GADD(&out[i], v);  // integer atomics: exact, order-independent
+  }
+}
+
 }  // namespace
 
 LBT_TRACE_SETTER(stem)
@@ -369,6 +445,14 @@ extern "C" int lbt_conv_stem_wgrad(const int16_t* x, const int8_t* gq, lbt_conv_
   const int64_t blocks = (M + kWgPixels - 1) / kWgPixels;
   // int32 shard totals stay exact: <= ceil(blocks/nshard) * 256 pixels * 2048 * 128 < 2^31
   if ((blocks + nshard - 1) / nshard > 31 || M >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  if (d.Cout == 16 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 && d.PL == 1 && d.Ho == d.H &&
+      d.Wo == d.W && d.Cin <= kStemCinMax && d.W >= 8 && d.W <= kStemWMax && 64 % d.W == 0 &&
+      ((int64_t)d.H * d.W) % kWgPixels == 0 && (kWgPixels / d.W + 2) * (d.W + 2) * d.Cin <= 4096 &&
+      (kWgPixels / d.W + 2) * (d.W + 2) * d.Cin <= 16 * kThreads && getenv("LBT_STEM_GATHER") == nullptr) {
+    hipLaunchKernelGGL(stem_wgrad_rows_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, x, gq, d,
+                       K, slab, (int)nshard);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(stem_wgrad_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, x, gq, d, K, M,
                      slab, (int)nshard);
   return (int)hipGetLastError();
