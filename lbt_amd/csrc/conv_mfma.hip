@@ -1186,6 +1186,17 @@ LBT_DEV f2 div_by2(f2 x, f2 y, f2 rc) {
   const f2 r1 = fma2(-y, q1, x);
   return __builtin_elementwise_copysign(fma2(r1, rc, q1), x);
 }
+// div_by2 for numerators that are never -0 -- the copysign only restores div_fixup's -0 / y = -0;
+// every other quotient already carries x's sign. True of the BN differences it is used on: x1 - mu
+// with x1 = q * 2^-e (an integer code: +0 when q == 0) and t1 - t2 with t1 = G * 2^-e - mg (mg from
+// an integer sum: never -0), since a - b is -0 only when a is -0 and b is +0.
+LBT_DEV f2 div_by2_nz(f2 x, f2 y, f2 rc) {
+  const f2 q = x * rc;
+  const f2 r = fma2(-y, q, x);
+  const f2 q1 = fma2(r, rc, q);
+  const f2 r1 = fma2(-y, q1, x);
+  return fma2(r1, rc, q1);
+}
 // overflow counts of a pair (quant_sl's predicate; NaN thresholds count nothing)
 LBT_DEV void ov_count2(f2 xm, float T1, float T2, int& c1, int& c2) {
   const f2 n = xm * mk2(-0x1.fffffep-1f, -0x1.fffffep-1f);
@@ -1364,11 +1375,11 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     for (int h = 0; h < 2; ++h) {
       const f2 x1 = cvt2(q[2 * h], q[2 * h + 1]) * sn.inv_m;
       const f2 x2 = x1 - mu2[h];
-      const f2 xh = div_by2(x2, sg2[h], rsc2[h]);
+      const f2 xh = div_by2_nz(x2, sg2[h], rsc2[h]);
       const f2 gh = cvt2(G[2 * h], G[2 * h + 1]) * sgq.inv_m;
       const f2 t1 = gh - rmg2[h];
       const f2 t2 = xh * rmgx2[h];
-      const f2 dx = div_by2(t1 - t2, sg2[h], rsc2[h]);
+      const f2 dx = div_by2_nz(t1 - t2, sg2[h], rsc2[h]);
       const f2 xm = dx * so.m;
       ov_count2(xm, T1, T2, ovq1, ovq2);
       const f2 fl = qfloor2(so, xm, u[h]);
@@ -1855,7 +1866,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       for (int h = 0; h < 2; ++h) {
         const f2 x1 = cvt2(q[2 * h], q[2 * h + 1]) * sn[b];
         const f2 x2 = x1 - pm2[b][h];
-        const f2 t = div_by2(x2, psy2[b][h], psr2[b][h]);
+        const f2 t = div_by2_nz(x2, psy2[b][h], psr2[b][h]);
         const f2 xm = t * qr[b].m;
         ov_count2(xm, T1[b], T2[b], ovr[b][0], ovr[b][1]);
         fl[h] = qfloor2(qr[b], xm, u[h]);  // the R codes
