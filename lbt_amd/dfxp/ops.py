@@ -205,7 +205,7 @@ def wgrad_s1_ok(d):
 
 
 WGRAD_CPW = int(os.environ.get("LBT_WGRAD_CPW", "8"))  # batched staged wgrad: 64-pixel chunks per wave
-WGRAD_UNITS = int(os.environ.get("LBT_WGRAD_UNITS", "128"))  # batched per-tap wgrad: workgroups per conv
+WGRAD_UNITS = int(os.environ.get("LBT_WGRAD_UNITS", "64"))  # batched per-tap wgrad: workgroups per conv (sweep: 32 / 48 / 64 / 80 / 96 / 128 -> 49 / 30 / 26 / 29 / 29 / 30 us)
 
 
 def wgrad_nsplit_batched(d, chunks_per_wave=None):
