@@ -437,16 +437,28 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_a_kernel(lbt_chain_bwd_a a
   LBT_TS(2);
   {
     const int per = chan_period(C);
-    const bool own = chan_owner(per);
+    if (chan_scatter_ok(per)) {  // uniform: row lane >> 4 ends with channel c0 + (lane >> 4)
+      const bool own = chan_scatter_owner(per);
+      const int cr = (int)(((uint32_t)g << 2) % (uint32_t)C) + (int)((threadIdx.x & 63) >> 4);  // natural quad (c0 is 0 on dead lanes)
 #pragma unroll
-    for (int b = 0; b < NB; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int v = wave_chan_reduce(acc[b][s][k], per);
-          if (own && v) atomicAdd((unsigned long long*)&S[b * 4 * C + s * C + c0 + k], (unsigned long long)(long long)v);
+        for (int s = 0; s < 4; ++s) {
+          const int v = chan_scatter4(acc[b][s], per);
+          if (own && v) atomicAdd((unsigned long long*)&S[b * 4 * C + s * C + cr], (unsigned long long)(long long)v);
         }
+    } else {
+      const bool own = chan_owner(per);
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int v = wave_chan_reduce(acc[b][s][k], per);
+            if (own && v) atomicAdd((unsigned long long*)&S[b * 4 * C + s * C + c0 + k], (unsigned long long)(long long)v);
+          }
+    }
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -570,12 +582,20 @@ __device__ __forceinline__ void chain_bwd_b_body(const lbt_chain_bwd_b& a, int r
   const bool gcol = LBT_FL(kBGcol, a.gcolsum != nullptr);
   if (want_q && gcol) {
     const int per = chan_period(C);
-    const bool own = chan_owner(per);
+    if (chan_scatter_ok(per)) {  // uniform: row lane >> 4 ends with channel c0 + (lane >> 4)
+      const bool own = chan_scatter_owner(per);
+      const int cr = (int)(((uint32_t)g << 2) % (uint32_t)C) + (int)((threadIdx.x & 63) >> 4);  // natural quad (c0 is 0 on dead lanes)
+      const int v1 = chan_scatter4(s1, per), v2 = chan_scatter4(s2, per);
+      if (own && v1) atomicAdd((unsigned long long*)&csum[cr], (unsigned long long)(long long)v1);
+      if (own && v2) atomicAdd((unsigned long long*)&csum[C + cr], (unsigned long long)(long long)v2);
+    } else {
+      const bool own = chan_owner(per);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int v1 = wave_chan_reduce(s1[k], per), v2 = wave_chan_reduce(s2[k], per);
-      if (own && v1) atomicAdd((unsigned long long*)&csum[c0 + k], (unsigned long long)(long long)v1);
-      if (own && v2) atomicAdd((unsigned long long*)&csum[C + c0 + k], (unsigned long long)(long long)v2);
+      for (int k = 0; k < 4; ++k) {
+        const int v1 = wave_chan_reduce(s1[k], per), v2 = wave_chan_reduce(s2[k], per);
+        if (own && v1) atomicAdd((unsigned long long*)&csum[c0 + k], (unsigned long long)(long long)v1);
+        if (own && v2) atomicAdd((unsigned long long*)&csum[C + c0 + k], (unsigned long long)(long long)v2);
+      }
     }
   }
   if (!want_q) return;

@@ -86,14 +86,9 @@ LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, 
   if (want_sum) {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
-      s1[j] += __shfl_xor(s1[j], 16, 64);
-      s2[j] += __shfl_xor(s2[j], 16, 64);
-      s1[j] += __shfl_xor(s1[j], 32, 64);
-      s2[j] += __shfl_xor(s2[j], 32, 64);
-      if (kg == 0) {
-        sh.part[wave][0][j * 16 + r] = s1[j];
-        sh.part[wave][1][j * 16 + r] = s2[j];
-      }
+      // lanes r, r+16, r+32, r+48 share a column: row 0 ends with s1's total, row 1 with s2's
+      const int t = rows_scatter2(s1[j], s2[j]);
+      if (kg < 2) sh.part[wave][kg][j * 16 + r] = t;
     }
   }
   if (o.q.counts) counts_stage_w(0, 1, ov1, ov2, sh.cnt);  // wave totals (quant_w)
@@ -245,14 +240,10 @@ LBT_DEV void chain_epi(const lbt_chain_bwd_a& c, bool has_add, int64_t M, int nc
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll
-    for (int j = 0; j < NTW; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        int t = acc[b][j][s];
-        t += __shfl_xor(t, 16, 64);
-        t += __shfl_xor(t, 32, 64);
-        if (kg == 0) sh.part[wave][b][s][j * 16 + r] = t;
-      }
+    for (int j = 0; j < NTW; ++j) {
+      // row kg ends with sum kg's column total (rows_scatter4)
+      sh.part[wave][b][kg][j * 16 + r] = rows_scatter4(acc[b][j][0], acc[b][j][1], acc[b][j][2], acc[b][j][3]);
+    }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const lbt_bwd_branch& B = b == 0 ? c.b1 : c.b2;

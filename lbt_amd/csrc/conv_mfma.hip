@@ -1127,12 +1127,6 @@ LBT_DEV long long rows_total64(long long v) {
   const auto d = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
   return (long long)(((unsigned long long)d[0] << 32) | c[0]) + (long long)(((unsigned long long)d[1] << 32) | c[1]);
 }
-template <int C4>
-LBT_DEV int chan_reduce(int v) {
-  if constexpr (C4 <= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
-  if constexpr (C4 <= 4) v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);  // row_ror:4
-  return half_pair_sum(row_pair_sum(v));
-}
 // the whole wave's total in every lane, on DPP / permlane swaps only (no LDS)
 LBT_DEV int wave_total(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
@@ -1525,26 +1519,21 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   // ---------------- channel sums: wave butterfly -> this wave's LDS slots (plain stores, no LDS
   // atomics); counters; one barrier; the waves' slots summed and flushed
   {
-    const bool own = lane < C4;  // lanes l, l + C4, ... hold the same channels (C4 <= 16 divides 64)
-    int* part = sh.part[wave];
+    // lanes l, l + C4, ... hold the same channels (C4 <= 16 divides 64); after chan_scatter4 the
+    // lanes (lane & 15) < C4 of row lane >> 4 hold channel cq + (lane >> 4)
+    const bool own = (lane & 15) < C4;
+    int* part = sh.part[wave] + cq + (lane >> 4);
 #pragma unroll
     for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        int v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = chan_reduce<C4>(acc3[b][s][k]);
-        if (own) *reinterpret_cast<int4*>(part + (b * 4 + s) * C + cq) = make_int4(v[0], v[1], v[2], v[3]);
+        const int t = chan_scatter4(acc3[b][s], C4);
+        if (own) part[(b * 4 + s) * C] = t;
       }
-    int v1[4], v2[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v1[k] = chan_reduce<C4>(s1[k]);
-      v2[k] = chan_reduce<C4>(s2[k]);
-    }
+    const int t1 = chan_scatter4(s1, C4), t2 = chan_scatter4(s2, C4);
     if (own) {
-      *reinterpret_cast<int4*>(part + 8 * C + cq) = make_int4(v1[0], v1[1], v1[2], v1[3]);
-      *reinterpret_cast<int4*>(part + 9 * C + cq) = make_int4(v2[0], v2[1], v2[2], v2[3]);
+      part[8 * C] = t1;
+      part[9 * C] = t2;
     }
   }
   ov_wave(ovq1, ovq2);
@@ -1961,16 +1950,10 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     *reinterpret_cast<int*>(p.yq + img + (uint32_t)(row0 * W * C + pix3 * C + cq)) = pack4(c);
   }
   {
-    const bool own = lane < C4;
-    int v1[4], v2[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v1[k] = chan_reduce<C4>(s1[k]);
-      v2[k] = chan_reduce<C4>(s2[k]);
-    }
-    if (own) {
-      *reinterpret_cast<int4*>(sh.part[wave] + cq) = make_int4(v1[0], v1[1], v1[2], v1[3]);
-      *reinterpret_cast<int4*>(sh.part[wave] + C + cq) = make_int4(v2[0], v2[1], v2[2], v2[3]);
+    const int t1 = chan_scatter4(s1, C4), t2 = chan_scatter4(s2, C4);  // row lane >> 4: channel cq + row
+    if ((lane & 15) < C4) {
+      sh.part[wave][cq + (lane >> 4)] = t1;
+      sh.part[wave][C + cq + (lane >> 4)] = t2;
     }
   }
 #pragma unroll

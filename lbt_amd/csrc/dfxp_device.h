@@ -306,6 +306,41 @@ LBT_DEV int wave_chan_reduce(int v, int period) {
 // true if this lane should publish its (reduced) per-channel partials
 LBT_DEV bool chan_owner(int period) { return period == 0 || (int)(threadIdx.x & 63) < period; }
 
+// ---- reduce-scatter over the wave's four 16-lane rows, on VALU lane swaps (no LDS round trips).
+// v_permlane16_swap(x, y) swaps x's odd rows with y's even rows, so the sum of its two results holds
+// x's row-pair sums (rows 0+1, 2+3) in rows 0 / 2 and y's in rows 1 / 3; v_permlane32_swap(P, Q)
+// swaps P's upper half with Q's lower half, so the sum of its results holds P's half totals in rows
+// 0-1 and Q's in rows 2-3. Integer sums: exact in any order.
+// rows_scatter4: row r (lanes 16r..16r+15) ends with v_r summed over the four rows at its lane
+// position (three swaps for four values; a full butterfly spends two per value).
+LBT_DEV int rows_scatter4(int v0, int v1, int v2, int v3) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v0, v1, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(v2, v3, false, false);
+  const int p01 = (int)a[0] + (int)a[1], p23 = (int)b[0] + (int)b[1];
+  const auto c = __builtin_amdgcn_permlane32_swap(p01, p23, false, false);
+  return (int)c[0] + (int)c[1];
+}
+// rows_scatter2: rows 0 and 2 end with v0's four-row total, rows 1 and 3 with v1's
+LBT_DEV int rows_scatter2(int v0, int v1) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v0, v1, false, false);
+  const int p = (int)a[0] + (int)a[1];
+  const auto c = __builtin_amdgcn_permlane32_swap(p, p, false, false);
+  return (int)c[0] + (int)c[1];
+}
+// Channel-quad partials v[k] (channel c0 + k, lanes l, l + period, ... sharing c0; period a power of
+// two <= 16): the wave total of channel c0 + (lane >> 4) lands in the lanes (lane & 15) < period of
+// row lane >> 4 (chan_scatter_owner). The DPP steps add the row's period-spaced repeats.
+LBT_DEV int chan_scatter4(const int v[4], int period) {
+  int t = rows_scatter4(v[0], v[1], v[2], v[3]);
+  if (period <= 8) t += __builtin_amdgcn_update_dpp(0, t, 0x128, 0xf, 0xf, false);  // row_ror:8
+  if (period <= 4) t += __builtin_amdgcn_update_dpp(0, t, 0x124, 0xf, 0xf, false);  // row_ror:4
+  if (period <= 2) t += __builtin_amdgcn_update_dpp(0, t, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  if (period <= 1) t += __builtin_amdgcn_update_dpp(0, t, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  return t;
+}
+LBT_DEV bool chan_scatter_ok(int period) { return period >= 1 && period <= 16; }
+LBT_DEV bool chan_scatter_owner(int period) { return (int)(threadIdx.x & 15) < period; }
+
 // MomentumOptimizer.apply_gradients (trainer.py:81-82) on element i: a = mu*a + g*gscale; w -= lr*a.
 LBT_DEV void sgd_momentum_elem(float* w, float* a, const float* g, int64_t i, float lr, float mu, float gscale) {
   const float t = mu * a[i];

@@ -90,14 +90,22 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const f
   // channel sums: the lanes sharing a quad (t = c0/4 mod C/4) meet by shuffles within the wave, the
   // waves in LDS; one int64 atomic per (sum, channel) into this sample's shard
   const int per = C / 4;  // lanes l, l + per, ... share a quad (per | 64)
+  if (chan_scatter_ok(per)) {  // uniform: row lane >> 4 ends with channel c0 + (lane >> 4)
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int v = acc[s][k];
-      for (int o = per; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (lane < per) s_sum[wave][s * C + c0 + k] = v;
+    for (int s = 0; s < 4; ++s) {
+      const int v = chan_scatter4(acc[s], per);
+      if (chan_scatter_owner(per)) s_sum[wave][s * C + c0 + (lane >> 4)] = v;
     }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int v = acc[s][k];
+        for (int o = per; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (lane < per) s_sum[wave][s * C + c0 + k] = v;
+      }
+  }
   counts_stage_w(2, 4, ov[0][0], ov[0][1], sh_cnt);
   counts_stage_w(3, 4, ov[1][0], ov[1][1], sh_cnt);
   __syncthreads();

@@ -70,6 +70,14 @@ __global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
   if (chsum) {
     const int per = chan_period(C);
     const int ch = (int)((g << 2) % C);
+    if (chan_scatter_ok(per)) {  // uniform: row lane >> 4 ends with channel ch + (lane >> 4)
+      const int cr = ch + (int)((threadIdx.x & 63) >> 4);
+      const int v1 = chan_scatter4(s1, per), v2 = chan_scatter4(s2, per);
+      if (chan_scatter_owner(per)) {
+        if (v1) atomicAdd((unsigned long long*)&sh_sum[cr], (unsigned long long)(long long)v1);
+        if (v2) atomicAdd((unsigned long long*)&sh_sum[C + cr], (unsigned long long)(long long)v2);
+      }
+    } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) { s1[k] = wave_chan_reduce(s1[k], per); s2[k] = wave_chan_reduce(s2[k], per); }
     if (chan_owner(per)) {
@@ -78,6 +86,7 @@ __global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
         if (s1[k]) atomicAdd((unsigned long long*)&sh_sum[ch + k], (unsigned long long)(long long)s1[k]);
         if (s2[k]) atomicAdd((unsigned long long*)&sh_sum[C + ch + k], (unsigned long long)(long long)s2[k]);
       }
+    }
     }
   }
   if (q.counts) counts_stage(0, 1, ov1, ov2, sh_cnt);
