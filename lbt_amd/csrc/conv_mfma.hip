@@ -1163,6 +1163,24 @@ LBT_DEV void ov_wave(int& c1, int& c2) {
   c1 = t & 0xffff;
   c2 = t >> 16;
 }
+// Four quantisers' packed lane counts (c1 | c2 << 16 each, as ov_wave) -> their wave totals,
+// staged at counts_stage_w's slots i0 .. i0 + 3 (slots >= nq skipped): one rows_scatter4 leaves
+// quantiser r's four-row sums in row r, the DPP steps finish the row (10 VALU exchanges where four
+// ov_wave calls spend 24).
+LBT_DEV int ov_pack(int c1, int c2) { return c1 | (c2 << 16); }
+LBT_DEV void ov_stage4(int i0, int nq, int v0, int v1, int v2, int v3, int* sh) {
+  int t = rows_scatter4(v0, v1, v2, v3);
+  t += __builtin_amdgcn_update_dpp(0, t, 0x128, 0xf, 0xf, false);  // row_ror:8
+  t += __builtin_amdgcn_update_dpp(0, t, 0x124, 0xf, 0xf, false);  // row_ror:4
+  t += __builtin_amdgcn_update_dpp(0, t, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  t += __builtin_amdgcn_update_dpp(0, t, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  const int lane = (int)(threadIdx.x & 63), i = i0 + (lane >> 4);
+  if ((lane & 15) == 0 && i < nq) {
+    int* p = sh + (int)(threadIdx.x >> 6) * 2 * nq + 2 * i;
+    p[0] = t & 0xffff;
+    p[1] = t >> 16;
+  }
+}
 
 // ---- channel pairs on packed fp32 (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two lanes' worth of
 // IEEE fp32 per instruction, each half rounded exactly as the scalar op). The element chains of the
@@ -1536,17 +1554,12 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
       part[9 * C] = t2;
     }
   }
-  ov_wave(ovq1, ovq2);
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    ov_wave(ov[b][0][0], ov[b][0][1]);
-    ov_wave(ov[b][1][0], ov[b][1][1]);
-  }
-  counts_stage_w(0, 5, ovq1, ovq2, sh.cnt);  // (counts_publish sums blockDim.x / 64 waves)
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    counts_stage_w(1 + 2 * b, 5, ov[b][0][0], ov[b][0][1], sh.cnt);
-    counts_stage_w(2 + 2 * b, 5, ov[b][1][0], ov[b][1][1], sh.cnt);
+  // slots [qo | qrg, qng of branch 1 | qrg, qng of branch 2] (counts_publish sums the kBNW waves)
+  ov_stage4(0, 5, ov_pack(ovq1, ovq2), ov_pack(ov[0][0][0], ov[0][0][1]), ov_pack(ov[0][1][0], ov[0][1][1]),
+            NB == 2 ? ov_pack(ov[1][0][0], ov[1][0][1]) : 0, sh.cnt);
+  if constexpr (NB == 2) {
+    ov_wave(ov[1][1][0], ov[1][1][1]);
+    counts_stage_w(4, 5, ov[1][1][0], ov[1][1][1], sh.cnt);
   }
   __syncthreads();
   LBT_TS(4);
@@ -1956,14 +1969,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       sh.part[wave][C + cq + (lane >> 4)] = t2;
     }
   }
-#pragma unroll
-  for (int b = 0; b < NB; ++b) ov_wave(ovr[b][0], ovr[b][1]);
-  ov_wave(ovx1, ovx2);
-  ov_wave(ovq1, ovq2);
-#pragma unroll
-  for (int b = 0; b < NB; ++b) counts_stage_w(b, 4, ovr[b][0], ovr[b][1], sh.cnt);
-  counts_stage_w(2, 4, ovx1, ovx2, sh.cnt);
-  counts_stage_w(3, 4, ovq1, ovq2, sh.cnt);
+  // slots [qr of branch 1 | qr of branch 2 | qo1 | qout]
+  ov_stage4(0, 4, ov_pack(ovr[0][0], ovr[0][1]), NB == 2 ? ov_pack(ovr[NB - 1][0], ovr[NB - 1][1]) : 0,
+            ov_pack(ovx1, ovx2), ov_pack(ovq1, ovq2), sh.cnt);
   __syncthreads();
   LBT_TS(4);
 #pragma unroll
