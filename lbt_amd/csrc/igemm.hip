@@ -153,14 +153,10 @@ LBT_DEV void quant_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i
   int64_t* cs = p.chsum + (int64_t)shard * 2 * ncol;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    int a = cs1[j], b = cs2[j];
-    a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
-    b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
+    // row 0 ends with the column's code sum, row 1 with its sum of squares (rows_scatter2)
+    const int t = rows_scatter2(cs1[j], cs2[j]);
     const int col = cw + j * 16 + r;
-    if (q == 0 && cw + j * 16 < ncol) {
-      if (a) atomicAdd((unsigned long long*)&cs[col], (unsigned long long)(long long)a);
-      if (b) atomicAdd((unsigned long long*)&cs[ncol + col], (unsigned long long)(long long)b);
-    }
+    if (q < 2 && cw + j * 16 < ncol && t) atomicAdd((unsigned long long*)&cs[q * ncol + col], (unsigned long long)(long long)t);
   }
   if ((threadIdx.x & 63) == 0 && p.qout.counts) {
     int32_t* ct = p.qout.counts + ((int64_t)p.qout.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
