@@ -34,12 +34,48 @@ LBT_DEV float head_noise(const lbt_qdesc& q, const QState& s, int i, int n) {
   return (s.active && q.stochastic) ? (tab ? tv : pv) : 0.f;
 }
 
+// lane k's value of v (k wave-uniform)
+LBT_DEV float lane_f(float v, int k) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+}
+
 // Pass A (bn.hip chain_bwd_a_kernel<1, kAFB | kAStoch | kAYMask | kAGmask>'s arithmetic, element for
 // element) of sample n's gradient g[p][c] = s_dp[c] * (1/HW), the value the un-pool writes: ReLU
 // mask from y_mask, gmask_out, the Rescale_q gradient quantiser (sums G2*R, G2), times gamma_q, the
 // Normalization_q gradient quantiser (codes to gout, sums G, G*q), overflow counters. Thread t owns
 // the channel quad c0 = 4t mod C of quads t, t + 256, ... (C | 1024). Every thread calls it.
-LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const float* s_dp, int* sh_cnt) {
+// Sample n's pass-A operands of the first kPaPre quad passes (y mask, R / qn codes, the two noise
+// tables' values when the quantisers have tables), loaded at the top of head_kernel so that their
+// latency hides behind the pooling / logits / softmax instead of following them. Clamped
+// addresses, no branches (the values are selected where they are used).
+constexpr int kPaPre = 4;
+struct HeadPaPre {
+  float4 ym[kPaPre], nr[kPaPre], nn[kPaPre];
+  int R[kPaPre], qn[kPaPre];
+};
+LBT_DEV bool head_pa_prefetchable(int HW, int C) { return HW * C / 4 <= kPaPre * kT; }
+LBT_DEV void head_pa_prefetch(const lbt_chain_bwd_a& a, int n, int HW, int C, HeadPaPre& p) {
+  const lbt_bwd_branch& B = a.b1;
+  const int nq = HW * C / 4, t = threadIdx.x;
+  const int64_t base = (int64_t)n * HW * C;
+  const float* tr = B.qrg.noise ? B.qrg.noise : zf();
+  const float* tn = B.qng.noise ? B.qng.noise : zf();
+  const uint32_t mr = B.qrg.noise ? 0xffffffffu : 0u, mn = B.qng.noise ? 0xffffffffu : 0u;
+#pragma unroll
+  for (int it = 0; it < kPaPre; ++it) {
+    const int q = t + it * kT, qq = q < nq ? q : 0;
+    const int64_t e = base + 4 * (int64_t)qq;
+    p.ym[it] = *reinterpret_cast<const float4*>(a.y_mask + e);
+    p.R[it] = *reinterpret_cast<const int*>(B.R + e);
+    p.qn[it] = *reinterpret_cast<const int*>(B.qn_codes + e);
+    p.nr[it] = *reinterpret_cast<const float4*>(tr + ((4u * (uint32_t)qq) & mr));
+    p.nn[it] = *reinterpret_cast<const float4*>(tn + ((4u * (uint32_t)qq) & mn));
+  }
+}
+
+// use_pre: pre holds head_pa_prefetch's operands (HW * C / 4 <= kPaPre * kT); else loaded here
+LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const float* s_dp, int* sh_cnt,
+                         const HeadPaPre& pre, bool use_pre) {
   __shared__ int s_sum[kT / 64][4 * 256];  // per wave: [sum][channel] (|.| < 2^19)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const lbt_bwd_branch& B = a.b1;
@@ -56,13 +92,10 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const f
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[s][k] = 0;
-  for (int q = t; q < nq; q += kT) {  // (C % 4 == 0, so c0 is this thread's quad in every pass)
+  const bool sr = qrg.active && B.qrg.stochastic, sn = qng.active && B.qng.stochastic;
+  // one quad pass (C % 4 == 0, so c0 is this thread's quad in every pass)
+  auto pass = [&](int q, const float4& ym4, int Rw, int qw, const Noise4& nrg, const Noise4& nng) {
     const int64_t e = base + 4 * (int64_t)q;
-    const float4 ym4 = *reinterpret_cast<const float4*>(a.y_mask + e);
-    const int Rw = *reinterpret_cast<const int*>(B.R + e);
-    const int qw = *reinterpret_cast<const int*>(B.qn_codes + e);
-    const Noise4 nrg = (qrg.active && B.qrg.stochastic) ? qnoise4(B.qrg, qrg.step, (uint64_t)q) : Noise4{{0.f, 0.f, 0.f, 0.f}};
-    const Noise4 nng = (qng.active && B.qng.stochastic) ? qnoise4(B.qng, qng.step, (uint64_t)q) : Noise4{{0.f, 0.f, 0.f, 0.f}};
     const float ym[4] = {ym4.x, ym4.y, ym4.z, ym4.w};
     float gv[4];
 #pragma unroll
@@ -86,6 +119,29 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const f
     }
     *reinterpret_cast<int*>(B.gout + e) =
         (int)((uint32_t)(G[0] & 255) | ((uint32_t)(G[1] & 255) << 8) | ((uint32_t)(G[2] & 255) << 16) | ((uint32_t)G[3] << 24));
+  };
+  const Noise4 z4 = {{0.f, 0.f, 0.f, 0.f}};
+  if (use_pre) {  // uniform
+#pragma unroll
+    for (int it = 0; it < kPaPre; ++it) {
+      const int q = t + it * kT;
+      if (q >= nq) break;
+      const Noise4 nrg = !sr ? z4 : B.qrg.noise ? Noise4{{pre.nr[it].x, pre.nr[it].y, pre.nr[it].z, pre.nr[it].w}}
+                                                : qnoise4(B.qrg, qrg.step, (uint64_t)q);
+      const Noise4 nng = !sn ? z4 : B.qng.noise ? Noise4{{pre.nn[it].x, pre.nn[it].y, pre.nn[it].z, pre.nn[it].w}}
+                                                : qnoise4(B.qng, qng.step, (uint64_t)q);
+      pass(q, pre.ym[it], pre.R[it], pre.qn[it], nrg, nng);
+    }
+  } else {
+    for (int q = t; q < nq; q += kT) {
+      const int64_t e = base + 4 * (int64_t)q;
+      const float4 ym4 = *reinterpret_cast<const float4*>(a.y_mask + e);
+      const int Rw = *reinterpret_cast<const int*>(B.R + e);
+      const int qw = *reinterpret_cast<const int*>(B.qn_codes + e);
+      const Noise4 nrg = sr ? qnoise4(B.qrg, qrg.step, (uint64_t)q) : z4;
+      const Noise4 nng = sn ? qnoise4(B.qng, qng.step, (uint64_t)q) : z4;
+      pass(q, ym4, Rw, qw, nrg, nng);
+    }
   }
   // channel sums: the lanes sharing a quad (t = c0/4 mod C/4) meet by shuffles within the wave, the
   // waves in LDS; one int64 atomic per (sum, channel) into this sample's shard
@@ -159,6 +215,10 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     }                                                                                            \
   } while (0)
   LBT_HEAD_LOAD_CHUNK(0);
+  // the fused pass A's operands, in flight from here
+  HeadPaPre pre;
+  const bool pre_ok = h.pa && head_pa_prefetchable(HW, C);  // uniform
+  if (pre_ok) head_pa_prefetch(pa, n, HW, C, pre);
 
   // ---- AvgPool_q: channel t, the HW pixels summed in order (avgpool_fwd_kernel), from LDS
   float acc = 0.f;
@@ -226,12 +286,17 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   // ---- softmax cross-entropy in wave 0, lane k = class (softmax_xent_kernel's arithmetic:
   // max, then s = sum of expf(z - m) in class order, p = expf(z - m) / s)
   if (wave == 0) {
+    // the class loops read lane k's value with v_readlane (no LDS / ds_bpermute round trip per
+    // class; same values, same order)
     const float zk = lane < K ? s_z[lane] : 0.f;
-    float m = s_z[0];
-    for (int k = 1; k < K; ++k) m = s_z[k] > m ? s_z[k] : m;
+    float m = lane_f(zk, 0);
+    for (int k = 1; k < K; ++k) {
+      const float zc = lane_f(zk, k);
+      m = zc > m ? zc : m;
+    }
     const float e = expf(zk - m);
     float s = 0.f;
-    for (int k = 0; k < K; ++k) s = s + __shfl(e, k, 64);
+    for (int k = 0; k < K; ++k) s = s + lane_f(e, k);
     if (lane < K) {
       const float p = e / s;
       const float dz = (p - (lane == y ? 1.f : 0.f)) / (float)(h.loss_n > 0 ? h.loss_n : N);
@@ -284,7 +349,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   }
   __syncthreads();
   if (h.pa) {  // uniform (the descriptor itself travels by value in pa)
-    head_pass_a(pa, n, HW, C, s_dp, sh_cnt);
+    head_pass_a(pa, n, HW, C, s_dp, sh_cnt, pre, pre_ok);
     LBT_TS(2);
     return;
   }
