@@ -77,6 +77,24 @@ def test_quantize_channel_sums_and_range_update():
     assert int(ctx.counts.abs().sum().item()) == 0
 
 
+@pytest.mark.parametrize("C", [4, 8, 12, 32, 64, 128, 256])
+def test_quantize_channel_sums_every_lane_period(C):
+    """Per-channel sums of the quantiser (quantize.hip: reduce-scatter over the wave's rows for a
+    channel-quad period of 1..16 lanes, butterfly / per-lane atomics otherwise) on a ragged shape
+    (inner = 21 C: the last wave of a row has dead lanes)."""
+    rng = np.random.default_rng(C)
+    x = rng.normal(0, 1.5, size=(5, 3, 7, C)).astype(np.float32)
+    ctx = DfxpContext(seed=4)
+    q = ctx.quantizer("p/X_range", 8, 2)
+    chsum = ops.new_sums(C, 2, DEV)
+    codes = ops.quantize(torch.from_numpy(x).to(DEV), q, OUT_I8, chsum=chsum, C=C)
+    ref = odfxp.quantize_int(x, 8, 2, True, odfxp.noise_for(x.shape, qid_of("p/X_range"), 0, 4))
+    assert np.array_equal(codes.cpu().numpy(), ref)
+    s = chsum.view(NSHARD, 2 * C).sum(0).cpu().numpy()
+    r = ref.reshape(-1, C).astype(np.int64)
+    assert np.array_equal(s[:C], r.sum(0)) and np.array_equal(s[C:], (r * r).sum(0))
+
+
 def test_counts_fold_and_folded_range_update():
     """The data-parallel controller path (fold -> [all-reduce] -> folded update) equals the
     sharded one; large counters survive the fp32 fold exactly."""
@@ -261,7 +279,11 @@ def test_dense_layer_bitexact():
     assert np.array_equal(dx.cpu().numpy(), dxr)
 
 
-@pytest.mark.parametrize("shape", [(16, 32, 32, 16), (16, 8, 8, 64), (128, 16, 16, 32)])
+# channel counts 4 / 8 / 16 / 32 / 64 put 1 / 2 / 4 / 8 / 16 lanes between repeats of a channel quad
+# (every DPP step of chan_scatter4); 128 and 12 take the butterfly fallback; the small ragged shapes
+# leave workgroups with dead lanes
+@pytest.mark.parametrize("shape", [(16, 32, 32, 16), (16, 8, 8, 64), (128, 16, 16, 32), (6, 5, 7, 4), (6, 5, 3, 8),
+                                   (4, 6, 6, 128), (3, 5, 5, 12)])
 def test_batchnorm_bitexact(shape):
     rng = np.random.default_rng(shape[0] + shape[-1])
     C = shape[-1]
