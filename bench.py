@@ -1,19 +1,28 @@
 #!/usr/bin/env python
 """bench.py -- train-step samples/s of ResNet-20 / CIFAR-10, 8-bit DFXP, on 1..8 MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch B [--bn sync|local]]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step is one ``Trainer.step`` (reference trainer.py:157): forward, mean softmax-CE, manual
 backward through all 192 DFXP quantisers, MomentumOptimizer update and the update_range
-collection, on a synthetic CIFAR-shaped batch already resident in HBM. Data parallel runs use
-128 images per GPU (weak scaling) and one RCCL all-reduce of gradients + overflow counters per
-step. Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").
+collection, on a synthetic CIFAR-shaped batch already resident in HBM. Data parallel runs are
+one process per GPU over RCCL: ``--gpus N`` without a torchrun environment starts the N rank
+processes itself (torch.distributed.run as a child process, before this process touches the GPU).
+Default: 128 images per GPU (weak scaling) and one RCCL all-reduce of the exact gradient
+numerators + overflow counters per step, captured in the step's HIP graph. ``--global-batch B``:
+strong scaling, B/N images per GPU; with ``--bn sync`` (its default) every BatchNorm takes the
+whole-batch moments of the reference (dynamic_fixed_point.py:588) through exact all-reduces of the
+integer statistics inside the step, so the N-GPU step computes the 1-GPU step on B images.
+Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
+import sys
 import time
 
 import numpy as np
@@ -120,9 +129,81 @@ def cpu_baseline(seconds=15.0, batch=128):
                       "ResNet-20 B=%d, %.1f s" % (n, batch, el)}
 
 
+def _launch_ranks(n):
+    """``--gpus N`` outside a torchrun environment: run this script under torch.distributed.run with
+    N local ranks as a CHILD process and return its exit status (rank 0's JSON line goes to our
+    stdout). Called before anything initialises the GPU, so no process that touched it execs."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
+    return subprocess.call(cmd, env=env)
+
+
+def _timed_region(step, steps, warmup, world, sync, device):
+    """W untimed steps, then exactly K steps between barrier + synchronize on both sides; the MAX over
+    ranks of the elapsed time."""
+    for i in range(warmup):
+        step(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def _dry_run(args, world, rank, backend, strong):
+    if backend != "gloo":
+        raise SystemExit("--dry-run runs on the gloo backend (CPU)")
+    if world > 1:
+        dist.init_process_group("gloo")
+        world, rank = dist.get_world_size(), dist.get_rank()
+    buf = torch.ones(1024, dtype=torch.int64)
+
+    def step(i):
+        if world > 1:
+            dist.all_reduce(buf)
+            buf.fill_(1)
+    el = _timed_region(step, args.steps, args.warmup, world, lambda: None, "cpu")
+    per = args.global_batch // world if strong else (args.batch or 128)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher plumbing, no measurement)", "value": None, "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000.0 * el / args.steps, 4),
+                          "scaling": "strong" if strong else "weak",
+                          "config": {"global_batch": per * world, "per_gpu_batch": per, "backend": backend,
+                                     "bn": args.bn or ("sync" if strong else "local"),
+                                     }}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (= ranks) of this node; without WORLD_SIZE in the environment the ranks are "
+                         "launched by this script")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: this many images per step over all GPUs (B/N per GPU)")
+    ap.add_argument("--bn", choices=("sync", "local"), default=None,
+                    help="BatchNorm statistics over the whole batch (sync, exact integer all-reduces inside "
+                         "the step: the reference's semantics) or per GPU (local, standard DDP). Default: sync "
+                         "with --global-batch, local otherwise")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=None,
@@ -134,29 +215,57 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group plumbing only (CPU, gloo): each step is one all-reduce of a "
+                         "small CPU tensor; used by the CPU tests, never a measurement")
     ap.add_argument("--workload", choices=("resnet20", "resnet50", "resnet20w4"), default="resnet20",
                     help="resnet50: BASELINE configs[3], ImageNet-shape, 16-bit gradients (layer path); "
                          "resnet20w4: configs[4], 4-bit packed weights")
     args = ap.parse_args()
     r50 = args.workload == "resnet50"
     w4 = args.workload == "resnet20w4"
-    if args.batch is None:
-        args.batch = 256 if r50 else 128
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but the launcher started %d ranks; reporting the ranks that ran"
+              % (args.gpus, world), file=sys.stderr)
+    strong = args.global_batch is not None
+    if strong:
+        if r50:
+            ap.error("--global-batch: ResNet-20 workloads only")
+        if args.global_batch % world:
+            ap.error("--global-batch %d is not divisible by %d ranks" % (args.global_batch, world))
+        args.batch = args.global_batch // world
+    elif args.batch is None:
+        args.batch = 256 if r50 else 128
+    bn_mode = args.bn or ("sync" if strong else "local")
+    if bn_mode == "sync" and r50:
+        ap.error("--bn sync: ResNet-20 workloads only")
     # LBT_DIST_BACKEND=gloo + LBT_SHARE_GPU=1: a rehearsal of the N-rank path with every rank on the
     # box's GPUs round-robin (one-GPU boxes); the measured configuration is RCCL, one GPU per rank
-    backend = os.environ.get("LBT_DIST_BACKEND", "nccl")
+    backend = os.environ.get("LBT_DIST_BACKEND", "gloo" if args.dry_run else "nccl")
+    if args.dry_run:
+        return _dry_run(args, world, rank, backend, strong)
     if os.environ.get("LBT_SHARE_GPU") == "1":
         local = local % max(1, torch.cuda.device_count())
+    elif world > 1 and torch.cuda.device_count() < world:
+        print("bench.py: %d ranks but %d visible GPUs (LBT_SHARE_GPU=1 rehearses on fewer)"
+              % (world, torch.cuda.device_count()), file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -173,29 +282,19 @@ def main():
         model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, weight_bits=4 if w4 else None)
         if not args.layerwise:
             from lbt_amd.fused import FusedResNet
-            model = FusedResNet(model)
-        xs, ys = synthetic_batches(4, args.batch, seed=1000 + rank, device=device)
+            model = FusedResNet(model, sync_bn=bn_mode == "sync")
+        if strong:  # every rank takes its shard of the same global batches
+            gx, gy = synthetic_batches(4, args.global_batch, seed=1000, device="cpu")
+            b = args.batch
+            xs = [x[rank * b:(rank + 1) * b].contiguous().to(device) for x in gx]
+            ys = [y[rank * b:(rank + 1) * b].contiguous().to(device) for y in gy]
+        else:
+            xs, ys = synthetic_batches(4, args.batch, seed=1000 + rank, device=device)
     trainer = Trainer(model, lr=1e-2, momentum=0.9, batch_size=args.batch, use_graph=not args.eager)
     trainer.init_model()
 
-    for i in range(args.warmup):
-        trainer.step(xs[i % 4], ys[i % 4])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        trainer.step(xs[i % 4], ys[i % 4])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = _timed_region(lambda i: trainer.step(xs[i % 4], ys[i % 4]), args.steps, args.warmup, world,
+                       torch.cuda.synchronize, device)
     loss = float(model.loss.item())
 
     out = {
@@ -207,7 +306,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * el / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "int8",
         "data": "synthetic CIFAR-10-shaped batches (uniform uint8 pixels, (p-127.5)/128), random-init weights",
@@ -216,6 +315,11 @@ def main():
                    "parallelism": "dp%d" % world, "hip_graph": not args.eager,
                    "executor": "layerwise" if args.layerwise else "fused", "final_loss": round(loss, 4)},
     }
+    if world > 1 or strong:
+        out["config"]["backend"] = backend if world > 1 else None
+        out["config"]["bn"] = bn_mode if world > 1 else "local"
+        out["config"]["collectives_in_graph"] = bool(getattr(trainer, "capture_comm", False))
+        out["config"]["shared_gpu"] = os.environ.get("LBT_SHARE_GPU") == "1"
     if w4:
         out["config"]["workload"] = "ResNet-20 CIFAR-10, 4-bit DFXP weights (packed, 2 per byte), 8-bit A/G, train step"
     if r50:

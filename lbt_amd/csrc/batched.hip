@@ -491,7 +491,9 @@ __global__ __launch_bounds__(256) void step_finish_kernel(const lbt_fseg* __rest
 __global__ void range_update_x_kernel(int32_t* exps, const int64_t* xbuf, int64_t cnt_off, const int32_t* bits,
                                       const float* target, const float* nelem, int nslots, uint64_t* step) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nslots && nelem[i] > 0.f) {  // update_range (dynamic_fixed_point.py:70-94) on the summed counts
+  // update_range (dynamic_fixed_point.py:70-94) on the summed counts; a 32-bit slot has no range op
+  // (the bits==32 bypass, :22-23), as in range_apply
+  if (i < nslots && nelem[i] > 0.f && bits[i] < 32) {
     const long long c1 = xbuf[cnt_off + 2 * i], c2 = xbuf[cnt_off + 2 * i + 1];
     const float r1 = (float)c1 / nelem[i];
     const float r2 = (float)c2 / nelem[i];

@@ -60,15 +60,18 @@ class _Block:
 class FusedResNet:
     """Drop-in for the Trainer (forward / compute_loss / backward / param_slots / ctx / loss)."""
 
-    def __init__(self, model, sync_bn=False, process_group=None):
+    def __init__(self, model, sync_bn=False, process_group=None, force_sync_bn=False):
         """sync_bn: data-parallel parity mode -- every BatchNorm takes its moments (forward) and its
         pass-A sums (backward) over the GLOBAL batch: the per-rank integer sums are all-reduced
         (exact) before the kernel that consumes them, so N ranks of b samples compute what one
         process computes on the N*b batch (tf.nn.moments over the whole batch,
-        dynamic_fixed_point.py:588). The step then holds blocking collectives: run it eagerly."""
+        dynamic_fixed_point.py:588). The step then holds collectives: the Trainer captures them into
+        its HIP graph (RCCL) or runs the step eagerly (gloo).
+        force_sync_bn: keep the collectives at world size 1 (tests of the captured path: a sum over
+        one rank is the identity, so the step must equal the plain plan bit for bit)."""
         self.model = model
         self.ctx = model.ctx
-        self.sync_bn = bool(sync_bn) and self.ctx.world_size > 1
+        self.sync_bn = bool(sync_bn) and (self.ctx.world_size > 1 or bool(force_sync_bn))
         self.pg = process_group
         self.xchg = None  # data-parallel exchange descriptor (Trainer.set_exchange)
         L = model.layers

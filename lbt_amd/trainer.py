@@ -22,6 +22,8 @@ MI355X-native execution:
   - layer-wise models: dequantised fp32 gradients + counters folded into exact fp32 pairs, one
     fp32 all-reduce (gscale = 1/world).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -57,7 +59,13 @@ class FlatParams:
 class Trainer:
     def __init__(self, model, dataset=None, logger=None, logdir=None, lr=1e-2, lr_decay_factor=0.5,
                  lr_decay_epoch=50, momentum=0.95, n_epoch=5, batch_size=128, use_graph=True,
-                 process_group=None):
+                 process_group=None, exchange=None, capture_comm=None):
+        """exchange: run the data-parallel exchange (default: when the process group has > 1 rank;
+        True at world 1 exercises the same path -- an all-reduce over one rank is the identity).
+        capture_comm: put the step's collectives (the exchange, SyncBN's statistics) INSIDE the
+        captured HIP graph, so a step is one graph launch (default: on for the nccl = RCCL backend,
+        LBT_CAPTURE_COMM=0 turns it off; gloo collectives cannot be captured and run from the host
+        between graph segments / eagerly)."""
         self.model = model
         self.dataset = dataset
         self.logger = logger
@@ -74,8 +82,14 @@ class Trainer:
         # data-parallel exchange: int64 [numerators | counters | loss] (fused plans) or fp32
         # [grads | folded overflow counters] (layer-wise models) -> ONE in-place all-reduce per step
         self.comm = self.xbuf = None
-        exact = self.world > 1 and hasattr(model, "set_exchange")
-        if self.world > 1 and not exact:
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.dp = (self.world > 1) if exchange is None else (bool(exchange) and dist_on)
+        if capture_comm is None:
+            capture_comm = (dist_on and dist.get_backend(process_group) == "nccl"
+                            and os.environ.get("LBT_CAPTURE_COMM", "1") == "1")
+        self.capture_comm = bool(capture_comm) and dist_on
+        exact = self.dp and hasattr(model, "set_exchange")
+        if self.dp and not exact:
             n = sum(getattr(o, v).numel() for o, v, _ in model.param_slots())
             self.comm = D.make_comm_buffer(n, len(self.ctx.quantizers), self.ctx.device)
         self.flat = FlatParams(model, self.comm)
@@ -129,10 +143,15 @@ class Trainer:
         p = self._plans.get(N)
         if p is None:
             from .fused import FusedResNet
-            p = FusedResNet(m.model, sync_bn=m.sync_bn, process_group=m.pg)
+            p = FusedResNet(m.model, sync_bn=m.sync_bn, process_group=m.pg, force_sync_bn=m.sync_bn)
             if self.xbuf is not None:
                 p.set_exchange(self._xchg)
             self._plans[N] = p
+            # graphs captured while this was the only plan hold no per-step element-count copy
+            # (_fwd_bwd adds one only once several plans exist): re-capture them with it, or they
+            # would replay with the new plan's overflow-rate denominators
+            self._gcache = {}
+            self._graphs = None
         return p
 
     def _fwd_bwd(self, X, y):
@@ -177,7 +196,7 @@ class Trainer:
 
     def _eager(self, X, y):
         self._fwd_bwd(X, y)
-        if self.world > 1:
+        if self.dp:
             self._exchange()
         self._update()
 
@@ -190,6 +209,10 @@ class Trainer:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             self._fwd_bwd(X, y)
+            if self.dp and self.capture_comm:
+                # a collective must have run once (communicator set up) before one is captured; the
+                # exchange buffer is rewritten by the next step's backward
+                self._exchange()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.ctx.counts.zero_()
@@ -208,40 +231,40 @@ class Trainer:
         sX.copy_(X)
         sy.copy_(y)
         self._warmup(sX, sy)
+        self._graphs = self._capture_step(sX, sy)
+
+    def _capture_step(self, X, y):
+        """(g1, g2): the step as one graph (no exchange, or captured collectives), else the forward +
+        backward and the update as two graphs with the host-issued exchange between them."""
+        one = not self.dp or self.capture_comm
+        # thread-local capture: the process group's watchdog thread queries events meanwhile
+        mode = "thread_local" if self.capture_comm else "global"
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
-            self._fwd_bwd(sX, sy)
-            if self.world == 1:  # nothing to exchange: the whole step is one graph
+        with torch.cuda.graph(g1, capture_error_mode=mode):
+            self._fwd_bwd(X, y)
+            if one:
+                if self.dp:
+                    self._exchange()
                 self._update()
         g2 = None
-        if self.world > 1:
+        if not one:
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
                 self._update()
-        self._graphs = (g1, g2)
+        return g1, g2
 
     def _capture_bound(self, X, y):
         """Capture the step reading (X, y) in place (models with binds_inputs): one graph per batch
         buffer pair, the first capture after a warm-up that allocates every per-layer buffer."""
         if getattr(self._plan(X.shape[0]), "_shape", 0) is None or not self._gcache:
             self._warmup(X, y)  # every plan's first run allocates its buffers outside a capture
-        g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
-            self._fwd_bwd(X, y)
-            if self.world == 1:
-                self._update()
-        g2 = None
-        if self.world > 1:
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
-                self._update()
-        return g1, g2
+        return self._capture_step(X, y)
 
     def step(self, X, y):
         """One training step on batch (X [B,32,32,3] fp32 NHWC, y [B] int32), device tensors.
-        A SyncBN plan holds collectives inside the step and runs eagerly."""
+        A SyncBN plan holds collectives inside the step: captured with them (RCCL), else eager."""
         self._active = self._plan(X.shape[0])
-        if not self.use_graph or getattr(self.model, "sync_bn", False):
+        if not self.use_graph or (getattr(self.model, "sync_bn", False) and not self.capture_comm):
             self._eager(X, y)
         else:
             key = (X.data_ptr(), y.data_ptr(), tuple(X.shape))
@@ -335,6 +358,10 @@ class Trainer:
             nb += 1
         self.ctx.counts.copy_(saved)
         self.ctx.nelem.copy_(saved_nelem)
+        # the quantisers' cached counts now describe the eval plan, not ctx.nelem: forget them so
+        # the next plan build writes its own (Quantizer.observe skips a write that matches its cache)
+        for q in self.ctx.quantizers:
+            q._nelem = None
         if shared:
             self._graphs = None
         return acc_sum / max(nb, 1), loss_sum / max(nb, 1)
@@ -356,7 +383,7 @@ class Trainer:
         return out
 
     def save_model(self, exp_path):
-        """Checkpoint (trainer.py:194-197, tf.train.Saver): parameters, momentum accumulators, DFXP
+        """Checkpoint (trainer.py:189-192, tf.train.Saver): parameters, momentum accumulators, DFXP
         exponents + noise step, BN running statistics and the trainer's step / lr, as one
         safetensors file exp_path/model.safetensors (no pickled objects)."""
         import json

@@ -102,6 +102,29 @@ def update_range_from_counts(c1, c2, n, target, bits, I):
     return clamp_I(bits, min(int(bits) - 1, int(I) + delta))
 
 
+def overflow_rates_f32(x, bits, I):
+    """``overflow_rate`` as the reference computes it (``:60-67``): fp32 masks, fp32 reduce_mean
+    (pairwise fp32 sum / n). Equal to count / n whenever n < 2**24 (every partial sum of 0/1/2
+    values is then an exact integer)."""
+    x = np.asarray(x, dtype=np.float32).reshape(-1)
+    e = frac_bits(bits, I)
+    m = np.float32(2.0 ** e)
+    L = np.float32(2.0 ** (bits - 1))
+    xm = (x * m).astype(np.float32)
+    m1 = (xm >= L).astype(np.float32) + (xm < -L).astype(np.float32)
+    m2 = (xm >= L / np.float32(2)).astype(np.float32) + (xm < -(L / np.float32(2))).astype(np.float32)
+    n = np.float32(x.size)
+    return (np.add.reduce(m1, dtype=np.float32) / n).astype(np.float32), \
+        (np.add.reduce(m2, dtype=np.float32) / n).astype(np.float32)
+
+
+def update_range_from_rates(r1, r2, target, bits, I):
+    """``update_range`` (``:83-94``) given the two fp32 rates."""
+    t = np.float32(target)
+    delta = 1 if np.float32(r1) > t else (-1 if np.float32(r2) <= t else 0)
+    return clamp_I(bits, min(int(bits) - 1, int(I) + delta))
+
+
 def update_range(x, target, bits, I):
     c1, c2 = overflow_counts(x, bits, I)
     return update_range_from_counts(c1, c2, np.asarray(x).size, target, bits, I)

@@ -28,6 +28,51 @@ from . import dfxp
 
 F32 = np.float32
 
+# Arithmetic mode of the restatement (see oracle/tfarith.py):
+#   "exact" -- the build's contract: integer GEMMs and BN / Rescale reductions summed exactly, finished
+#              in double, rounded once to fp32 (what the HIP kernels compute bit for bit);
+#   "tf32"  -- a model of the REFERENCE's own arithmetic: TF sums the same fake-quantised fp32 values
+#              in fp32 -- tf.nn.conv2d / conv2d_backprop_* / tf.matmul as fp32 GEMMs
+#              (dynamic_fixed_point.py:291,302-305,388,457-460), tf.nn.moments as fp32 reduce_means
+#              (:588), the BN backward as TF's autodiff of (Xq - mean) / (var + eps) ** 0.5 (:616,623),
+#              Rescale's dgamma / dbeta as fp32 reduce_sums (:689-690), overflow rates as fp32
+#              reduce_means of fp32 masks (:63-67).
+ARITH = "exact"
+
+
+#   "tf32seq" -- the same fp32 arithmetic in another legitimate order (sequential reductions, per-tap
+#              conv GEMMs): a control for how far two fp32 implementations of the reference land
+#              from EACH OTHER (TF's CPU and GPU kernels sum in different orders).
+
+
+def _tf32():
+    return ARITH in ("tf32", "tf32seq")
+
+
+def _seq():
+    return ARITH == "tf32seq"
+
+
+def f32_colsum(a):
+    """fp32 sum over the rows of a 2-D array (one value per column): pairwise (numpy's float32
+    reduction along a contiguous axis, the class of Eigen's tree reductions), or row after row
+    (ARITH "tf32seq")."""
+    a = np.asarray(a, F32)
+    if _seq():
+        return np.add.reduce(a, axis=0, dtype=F32)
+    return np.add.reduce(np.ascontiguousarray(a.T), axis=-1, dtype=F32)
+
+
+def _im2col(x, kh, kw, sh, sw, Ho, Wo, pt, pl, dtype):
+    """[N*Ho*Wo, kh*kw*C] patches of x (zero padding), tap-major then channel."""
+    N, H, W, C = x.shape
+    xp = _windows(x.astype(dtype), kh, kw, sh, sw, Ho, Wo, pt, pl).astype(dtype)
+    cols = np.empty((N, Ho, Wo, kh, kw, C), dtype)
+    for i in range(kh):
+        for j in range(kw):
+            cols[:, :, :, i, j, :] = xp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :]
+    return cols.reshape(N * Ho * Wo, kh * kw * C)
+
 
 def tf_same_pads(in_size, k, s):
     """TF 'SAME' padding (before, after) and output size."""
@@ -70,6 +115,18 @@ def conv_fwd_int(xq, wq, strides, padding):
     kh, kw, _, Cout = wq.shape
     sh, sw = strides
     Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    if _seq():  # per-tap fp32 GEMMs accumulated in fp32
+        xp = _windows(xq.astype(F32), kh, kw, sh, sw, Ho, Wo, pt, pl).astype(F32)
+        acc = np.zeros((N * Ho * Wo, Cout), dtype=F32)
+        for i in range(kh):
+            for j in range(kw):
+                xs = xp[:, i:i + (Ho - 1) * sh + 1:sh, j:j + (Wo - 1) * sw + 1:sw, :]
+                acc += xs.reshape(-1, Cin) @ wq[i, j].astype(F32)
+        return acc.astype(np.int64).reshape(N, Ho, Wo, Cout)
+    if _tf32():  # tf.nn.conv2d: one fp32 GEMM over K = kh*kw*Cin (sums of integers stay integers)
+        cols = _im2col(xq, kh, kw, sh, sw, Ho, Wo, pt, pl, F32)
+        acc = cols @ wq.astype(F32).reshape(kh * kw * Cin, Cout)
+        return acc.astype(np.int64).reshape(N, Ho, Wo, Cout)
     xp = _windows(xq.astype(np.float64), kh, kw, sh, sw, Ho, Wo, pt, pl)
     acc = np.zeros((N * Ho * Wo, Cout), dtype=np.float64)
     wf = wq.astype(np.float64)
@@ -88,9 +145,10 @@ def conv_dgrad_int(gq, wq, strides, padding, in_shape):
     Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
     Hp = max(H + pt, (Ho - 1) * sh + kh)
     Wp = max(W + pl, (Wo - 1) * sw + kw)
-    dxp = np.zeros((N, Hp, Wp, Cin), dtype=np.float64)
-    g = gq.astype(np.float64).reshape(-1, Cout)
-    wf = wq.astype(np.float64)
+    dt = F32 if _tf32() else np.float64  # tf32: per-tap fp32 GEMMs over Cout, fp32 col2im adds
+    dxp = np.zeros((N, Hp, Wp, Cin), dtype=dt)
+    g = gq.astype(dt).reshape(-1, Cout)
+    wf = wq.astype(dt)
     for i in range(kh):
         for j in range(kw):
             contrib = (g @ wf[i, j].T).reshape(N, Ho, Wo, Cin)
@@ -105,6 +163,16 @@ def conv_wgrad_int(xq, gq, strides, padding, kshape):
     Cout = gq.shape[-1]
     sh, sw = strides
     Ho, Wo, pt, pb, pl, pr = conv_geometry(H, W, kh, kw, sh, sw, padding)
+    if _tf32():  # conv2d_backprop_filter: one fp32 GEMM contracting the N*Ho*Wo pixels
+        cols = _im2col(xq, kh, kw, sh, sw, Ho, Wo, pt, pl, F32)
+        g2 = gq.astype(F32).reshape(-1, Cout)
+        if _seq():  # pixel chunks of 4096 accumulated in fp32
+            dw = np.zeros((cols.shape[1], Cout), F32)
+            for p0 in range(0, cols.shape[0], 4096):
+                dw += cols[p0:p0 + 4096].T @ g2[p0:p0 + 4096]
+        else:
+            dw = cols.T @ g2
+        return dw.astype(np.int64).reshape(kh, kw, Cin, Cout)
     xp = _windows(xq.astype(np.float64), kh, kw, sh, sw, Ho, Wo, pt, pl)
     g = gq.astype(np.float64).reshape(-1, Cout)
     dw = np.zeros((kh, kw, Cin, Cout), dtype=np.float64)
@@ -179,6 +247,7 @@ class Ctx:
         self.seed = int(seed)
         self.target = target
         self.counts = {}           # name -> (c1, c2, n, bits)
+        self.rates = {}            # name -> (rate, rate_2x) as fp32 means (ARITH "tf32" only)
         self.record = {}           # name -> int codes (for parity tests)
 
     def fq(self, name, x, bits, stochastic=True):
@@ -197,13 +266,19 @@ class Ctx:
         q = dfxp.quantize_int(x, bits, I, stochastic, noise)
         c1, c2 = dfxp.overflow_counts(x, bits, I)
         self.counts[name] = (c1, c2, x.size, bits)
+        if _tf32():  # the reference's rates: fp32 reduce_mean of fp32 masks (:63-67)
+            self.rates[name] = dfxp.overflow_rates_f32(x, bits, I)
         self.record[name] = q
         return q, dfxp.frac_bits(bits, I)
 
     def new_ranges(self):
         out = dict(self.I)
         for name, (c1, c2, n, bits) in self.counts.items():
-            out[name] = dfxp.update_range_from_counts(c1, c2, n, self.target, bits, self.I[name])
+            if name in self.rates:
+                r1, r2 = self.rates[name]
+                out[name] = dfxp.update_range_from_rates(r1, r2, self.target, bits, self.I[name])
+            else:
+                out[name] = dfxp.update_range_from_counts(c1, c2, n, self.target, bits, self.I[name])
         return out
 
 
@@ -298,6 +373,12 @@ class Conv2dQ(LayerQ):
         return scale_int(acc_x, eg + self.ew)
 
 
+def _mm(a, b):
+    """Integer-code GEMM: exact (float64, partial sums < 2**53), or tf.matmul's fp32 (ARITH tf32)."""
+    dt = F32 if _tf32() else np.float64
+    return np.asarray(a).astype(dt) @ np.asarray(b).astype(dt)
+
+
 class DenseQ(LayerQ):
     def __init__(self, name, bits, in_units, units, weight_decay=0.0, grad_bits=None, weight_bits=None,
                  use_bias=False):
@@ -326,7 +407,7 @@ class DenseQ(LayerQ):
             return y
         self.xq, self.ex = ctx.q(self.name + "/X_range", X, self.bits)
         self.wq, self.ew = ctx.q(self.name + "/W_range", self.W, self.weight_bits)
-        acc = np.rint(self.xq.astype(np.float64) @ self.wq.astype(np.float64)).astype(np.int64)
+        acc = np.rint(_mm(self.xq, self.wq)).astype(np.int64)
         y = scale_int(acc, self.ex + self.ew)
         return _bias_fwd(self, y, ctx) if self.use_bias else y
 
@@ -340,13 +421,13 @@ class DenseQ(LayerQ):
             return (gf @ self.wf.astype(np.float64).T).astype(F32)
         gq, eg = ctx.q(self.name + "/grad_range", g, self.grad_bits)
         self.gq = gq
-        acc_w = np.rint(self.xq.astype(np.float64).T @ gq.astype(np.float64)).astype(np.int64)
+        acc_w = np.rint(_mm(self.xq.T, gq)).astype(np.int64)
         self.acc_w, self.ew_grad = acc_w, self.ex + eg
         if self.use_bias:
             _bias_bwd(self, gq, eg)
         c = F32(2 * self.wd)
         self.dW = (scale_int(acc_w, self.ex + eg) + (c * self.W).astype(F32)).astype(F32)
-        acc_x = np.rint(gq.astype(np.float64) @ self.wq.astype(np.float64).T).astype(np.int64)
+        acc_x = np.rint(_mm(gq, self.wq.T)).astype(np.int64)
         return scale_int(acc_x, eg + self.ew)
 
 
@@ -400,14 +481,24 @@ class NormQ(LayerQ):
             return xhat
         qf = q.reshape(-1, C).astype(np.int64)
         n = qf.shape[0]
-        S1 = qf.sum(0)
-        S2 = (qf * qf).sum(0)
-        mean_d = S1.astype(np.float64) * s / n
-        var_d = S2.astype(np.float64) * (s * s) / n - mean_d * mean_d
-        mu = mean_d.astype(F32)
-        var = var_d.astype(F32)
-        sigma = np.sqrt((var + F32(self.eps)).astype(F32)).astype(F32)
-        xhat = (((q.astype(F32) * F32(s)).astype(F32) - mu).astype(F32) / sigma).astype(F32)
+        if _tf32():  # tf.nn.moments: fp32 reduce_mean, then reduce_mean of squared_difference (:588)
+            xq = (q.astype(F32) * F32(s)).astype(F32)
+            x2 = xq.reshape(-1, C)
+            mu = (f32_colsum(x2) / F32(n)).astype(F32)
+            dd = (x2 - mu).astype(F32)
+            var = (f32_colsum((dd * dd).astype(F32)) / F32(n)).astype(F32)
+            sigma = np.power((var + F32(self.eps)).astype(F32), F32(0.5)).astype(F32)  # (:616) ** 0.5
+            xhat = ((xq - mu).astype(F32) / sigma).astype(F32)
+            self.var_tf = var
+        else:
+            S1 = qf.sum(0)
+            S2 = (qf * qf).sum(0)
+            mean_d = S1.astype(np.float64) * s / n
+            var_d = S2.astype(np.float64) * (s * s) / n - mean_d * mean_d
+            mu = mean_d.astype(F32)
+            var = var_d.astype(F32)
+            sigma = np.sqrt((var + F32(self.eps)).astype(F32)).astype(F32)
+            xhat = (((q.astype(F32) * F32(s)).astype(F32) - mu).astype(F32) / sigma).astype(F32)
         m = F32(self.momentum)
         self.mean_running = ((m * self.mean_running).astype(F32) + (F32(1 - self.momentum) * mu).astype(F32)).astype(F32)
         self.var_running = ((m * self.var_running).astype(F32) + (F32(1 - self.momentum) * var).astype(F32)).astype(F32)
@@ -435,6 +526,8 @@ class NormQ(LayerQ):
         C = g.shape[-1]
         if not self.train:
             return ((G.astype(F32) * F32(sg)).astype(F32) / self.sigma).astype(F32)
+        if _tf32():
+            return self._backward_tf32(G, sg, s, C)
         Gf = G.reshape(-1, C).astype(np.int64)
         qf = self.q.reshape(-1, C).astype(np.int64)
         SG = Gf.sum(0)
@@ -448,6 +541,28 @@ class NormQ(LayerQ):
         a = (ghat - mg).astype(F32)
         b = (self.xhat * mgx).astype(F32)
         return ((a - b).astype(F32) / self.sigma).astype(F32)
+
+
+    def _backward_tf32(self, G, sg, s, C):
+        """tf.gradients of y = (Xq - mean) / (var + eps) ** 0.5 with (mean, var) = tf.nn.moments(Xq)
+        (:588,616,623) in fp32, term by term as TF's gradient functions build it: RealDiv (g / s and
+        -sum(g * (-d / s) / s)), Pow (grad * 0.5 * pow(v, -0.5)), Mean (/ n), SquaredDifference
+        (2 * grad * (x - mean), mean under stop_gradient), Sub (-sum), the three contributions to
+        Xq added in that order."""
+        g = (G.astype(F32) * F32(sg)).astype(F32).reshape(-1, C)
+        x = (self.q.astype(F32) * F32(s)).astype(F32).reshape(-1, C)
+        n = F32(self.n)
+        d = (x - self.mu).astype(F32)
+        sig = self.sigma
+        g_d = (g / sig).astype(F32)
+        g_s = f32_colsum((g * (((-d) / sig).astype(F32) / sig).astype(F32)).astype(F32))
+        v = (self.var_tf + F32(self.eps)).astype(F32)
+        g_v = ((g_s * F32(0.5)).astype(F32) * np.power(v, F32(-0.5)).astype(F32)).astype(F32)
+        g_sq = (g_v / n).astype(F32)
+        t_sq = ((F32(2.0) * g_sq).astype(F32) * d).astype(F32)
+        g_mean = ((-f32_colsum(g_d)).astype(F32) / n).astype(F32)
+        dx = ((g_d + t_sq).astype(F32) + g_mean).astype(F32)
+        return dx.reshape(G.shape)
 
 
 class RescaleQ(LayerQ):
@@ -496,6 +611,12 @@ class RescaleQ(LayerQ):
         sg = 2.0 ** -eg
         sr = 2.0 ** -self.er
         c = F32(2 * self.wd)
+        if _tf32():  # Mul / Add gradients: fp32 reduce_sums over the broadcast axes (:689-691)
+            ghat = (G.astype(F32) * F32(sg)).astype(F32).reshape(-1, C)
+            xr = (self.R.astype(F32) * F32(sr)).astype(F32).reshape(-1, C)
+            self.dgamma = (f32_colsum((ghat * xr).astype(F32)) + (c * self.gamma).astype(F32)).astype(F32)
+            self.dbeta = f32_colsum(ghat)
+            return (ghat * self.gq_f).astype(F32).reshape(G.shape)
         # integer numerators of dgamma / dbeta and their scales, for the data-parallel oracle
         self.sgr, self.sg, self.eg, self.sgsr = (Gf * Rf).sum(0), Gf.sum(0), sg, sg * sr
         self.dgamma = ((Gf * Rf).sum(0).astype(np.float64) * (sg * sr)).astype(F32)

@@ -62,26 +62,31 @@ def _batches(B):
     return xs, ys
 
 
-def _make(world, sync, B):
+def _make(world, sync, B, force=False, exchange=None):
     from lbt_amd.fused import FusedResNet
     from lbt_amd.models import CIFAR10_Resnet20
     from lbt_amd.runtime import DfxpContext
     from lbt_amd.trainer import Trainer
     ctx = DfxpContext(device="cuda:0", seed=0, world_size=world)
-    m = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx), sync_bn=sync)
-    return ctx, m, Trainer(m, lr=1e-2, momentum=0.9, batch_size=B // world, use_graph=True)
+    m = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx), sync_bn=sync, force_sync_bn=force)
+    return ctx, m, Trainer(m, lr=1e-2, momentum=0.9, batch_size=B // world, use_graph=True, exchange=exchange)
 
 
-def _worker(rank, world, port, sync, B, out_q):
+def _worker(rank, world, port, sync, B, out_q, backend="gloo", force=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
-        ctx, m, tr = _make(world, sync, B)
+        ctx, m, tr = _make(world, sync, B, force=force, exchange=True if force else None)
+        if force:  # the captured-collective path must be the one that ran
+            assert tr.dp and tr.capture_comm and m.sync_bn == sync, (tr.dp, tr.capture_comm, m.sync_bn)
         xs, ys = _batches(B)
         b = B // world
         xr = [x[rank * b:(rank + 1) * b].contiguous().cuda() for x in xs]  # kept alive: graphs read them
@@ -91,6 +96,8 @@ def _worker(rank, world, port, sync, B, out_q):
             tr.step(xr[i], yr[i])
             torch.cuda.synchronize()
             rec.append(_state(tr, ctx, m))
+        if force:  # one graph per step: the exchange (and SyncBN's sums) captured inside it
+            assert tr._graphs is not None and tr._graphs[1] is None
         out_q.put((rank, rec))
     except Exception as e:  # pragma: no cover - surfaced by the parent
         out_q.put((rank, repr(e)))
@@ -99,11 +106,11 @@ def _worker(rank, world, port, sync, B, out_q):
         dist.destroy_process_group()
 
 
-def _run_ranks(sync, B, world=2):
+def _run_ranks(sync, B, world=2, backend="gloo", force=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, sync, B, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sync, B, q, backend, force)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
@@ -178,3 +185,29 @@ def test_dp_two_ranks_syncbn_equals_single_process_batch():
                 assert np.array_equal(ma, mb) and np.array_equal(va, vb), i
         # each rank's dz rows are the single process's rows of the same global-batch gradient
         assert np.array_equal(np.concatenate([r0[i]["dz"], r1[i]["dz"]]), ref["dz"]), i
+
+
+@pytest.mark.parametrize("sync", [False, True])
+def test_captured_rccl_collectives_world1_equal_plain_step(sync):
+    """The nccl (= RCCL) path with its collectives CAPTURED in the step's HIP graph (Trainer
+    capture_comm): one rank, so every all-reduce is the identity and the step -- exchange buffer,
+    lbt_step_finish, range update from the exchanged counters, and with SyncBN the 42 statistics
+    all-reduces inside the graph -- must equal the plain single-process step bit for bit. (Two RCCL
+    ranks cannot share one GPU; the N-rank sums themselves are covered by the gloo tests above.)"""
+    B = 32
+    (r0,) = _run_ranks(sync, B, world=1, backend="nccl", force=True)
+    ctx, m, tr = _make(1, False, B)
+    xs, ys = _batches(B)
+    xg = [x.cuda() for x in xs]
+    yg = [y.cuda() for y in ys]
+    for i in range(STEPS):
+        tr.step(xg[i], yg[i])
+        torch.cuda.synchronize()
+        ref = _state(tr, ctx, m)
+        s = r0[i]
+        assert np.array_equal(s["w"], ref["w"]), i
+        assert np.array_equal(s["g"], ref["g"]), i
+        assert s["ranges"] == ref["ranges"], i
+        assert abs(s["loss"] - ref["loss"]) <= 1e-6 * abs(ref["loss"]), i  # 2^-32 fixed-point loss sum
+        for (ma, va), (mb, vb) in zip(s["bn"], ref["bn"]):
+            assert np.array_equal(ma, mb) and np.array_equal(va, vb), i

@@ -163,12 +163,16 @@ def _params_of(gm):
 
 
 @pytest.mark.gpu
-def test_partial_final_batch_steps_match_oracle():
+@pytest.mark.parametrize("target", [0.0, 0.01])
+def test_partial_final_batch_steps_match_oracle(target):
     """An epoch of 40 images at batch 16 ends with a batch of 8 (trainer.py:98 keeps it): the fused
     trainer runs it on a second plan over the same parameters and quantisers (graph-captured), and
     all three steps -- 16, 16, 8 -- are bit-identical to the oracle's (dz injected; loss 1e-5),
-    including the overflow-rate denominators of the short batch."""
+    including the overflow-rate denominators of the short batch. With target_overflow_rate > 0 the
+    rates are compared with the target (not only with 0), so a graph replaying with the other plan's
+    denominators changes exponents (the epoch-2 replay of the first plan's graph)."""
     ctx, gm, tr = _fused_trainer(21, 16)
+    ctx.target[:len(ctx.quantizers)] = target
     om = oresnet.build_resnet((3, 3, 3), 8, 2e-4)
     p = _params_of(gm)
     state = dict(params=p, accum={k: np.zeros_like(v) for k, v in p.items()}, ranges=oresnet.init_ranges(om), step=0)
@@ -177,12 +181,13 @@ def test_partial_final_batch_steps_match_oracle():
     Y = rng.integers(0, 10, size=40).astype(np.int32)
     xs = [torch.from_numpy(X[b:b + 16]).to(DEV) for b in range(0, 40, 16)]
     ys = [torch.from_numpy(Y[b:b + 16]).to(DEV) for b in range(0, 40, 16)]
-    for epoch in range(2):  # the second epoch replays both plans' graphs
+    for epoch in range(3):  # the later epochs replay both plans' graphs
         for i, (x, y) in enumerate(zip(xs, ys)):
             loss = tr.step(x, y).item()
             torch.cuda.synchronize()
             dz = tr._active.dlogits.cpu().numpy()
-            lref, state, _ = oresnet.train_step(om, state, x.cpu().numpy(), y.cpu().numpy(), seed=21, dz=dz)
+            lref, state, _ = oresnet.train_step(om, state, x.cpu().numpy(), y.cpu().numpy(), seed=21, target=target,
+                                                dz=dz)
             assert abs(loss - lref) <= 1e-5 * abs(lref), (epoch, i)
             gp = _params_of(gm)
             for k in gp:
@@ -240,3 +245,30 @@ def test_evaluate_matches_oracle_test_loop():
         assert np.array_equal(g_.X_mean_running.cpu().numpy(), o.mean_running)
         assert np.array_equal(g_.X_var_running.cpu().numpy(), o.var_running)
     assert torch.equal(counts, ctx.counts) and ctx.ranges() == ranges
+
+
+@pytest.mark.gpu
+def test_evaluate_before_training_keeps_element_counts():
+    """evaluate() at the training batch size BEFORE the first training step: the eval
+    plan's build caches its element counts in the quantisers; the training plan built afterwards must
+    still declare its own (a quantiser left at nelem 0 would never move its exponent). Two training
+    steps after it are bit-identical to the oracle's, exponents included."""
+    ctx, gm, tr = _fused_trainer(24, 16)
+    om = oresnet.build_resnet((3, 3, 3), 8, 2e-4)
+    p = _params_of(gm)
+    state = dict(params=p, accum={k: np.zeros_like(v) for k, v in p.items()}, ranges=oresnet.init_ranges(om), step=0)
+    rng = np.random.default_rng(24)
+    Xte = ((rng.integers(0, 256, size=(16, 32, 32, 3)) - 127.5) / 128).astype(F32)
+    tr.evaluate(Xte, rng.integers(0, 10, size=16).astype(np.int32), batch_size=16)
+    for i in range(2):
+        x = torch.from_numpy(((rng.integers(0, 256, size=(16, 32, 32, 3)) - 127.5) / 128).astype(F32)).to(DEV)
+        y = torch.from_numpy(rng.integers(0, 10, size=16).astype(np.int32)).to(DEV)
+        loss = tr.step(x, y).item()
+        torch.cuda.synchronize()
+        dz = tr._active.dlogits.cpu().numpy()
+        lref, state, _ = oresnet.train_step(om, state, x.cpu().numpy(), y.cpu().numpy(), seed=24, dz=dz)
+        assert abs(loss - lref) <= 1e-5 * abs(lref), i
+        gp = _params_of(gm)
+        for k in gp:
+            assert np.array_equal(gp[k], state["params"][k]), (i, k)
+        assert ctx.ranges() == state["ranges"], i
