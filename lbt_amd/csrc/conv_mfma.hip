@@ -821,6 +821,13 @@ extern "C" int lbt_conv_wgrad_i8(const int8_t* xq, int32_t x_u8off, const int8_t
 // LDS and added into the job's slab (shard = split % nshard) with one integer atomic per output.
 namespace {
 constexpr int kMaxWJobs = 24;
+#ifndef LBT_WGM_OCC
+#define LBT_WGM_OCC 4  // waves per SIMD the batched launch's registers are budgeted for
+#endif
+#ifndef LBT_WGM_BUFS
+#define LBT_WGM_BUFS 2
+#endif
+constexpr int kWgmBufs = LBT_WGM_BUFS;  // chunks of loads in flight per wave (register buffers)
 constexpr int kFW = 8;        // waves per workgroup of the batched launch
 constexpr int kHaloMax = 3;   // halo slices per lane: (64/W + 2) * (W + 2) <= 192 (W | 64, 2 <= W <= 32)
 struct WgradMany {
@@ -833,7 +840,9 @@ union WgradManyShared {
   WgradShared<1, kFW> s1;
   WgradShared<2, kFW> s2;
   int8_t stage[kFW][5 * 1024];               // wgrad_s1_body: per wave X halo | G (at +4096)
-  int red[kFW][9 * 256];                      // wgrad_s1_body: per wave partials [tap][kg][r][4]
+  // wgrad_s1_body: partials [tap][kg][r][4] of wave pair (w, w + kFW/2), summed in place (the LDS of
+  // three workgroups per CU: the batched launch fits one round)
+  int red[kFW / 2][9 * 256];
 };
 
 bool wgrad_s1_ok(const lbt_conv_desc& d, int nsplit) {
@@ -916,7 +925,7 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (s + 2 < nmine) load(b, c0 + wave + (int64_t)(s + 2) * kFW);
+    if (s + kWgmBufs < nmine) load(b, c0 + wave + (int64_t)(s + kWgmBufs) * kFW);
     const v4i bfrag = tr_frag_at(gs, oga, ogb);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -929,25 +938,42 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
   LBT_TS(0);
-  Buf b0, b1;
-  if (nmine > 0) load(b0, c0 + wave);
-  if (nmine > 1) load(b1, c0 + wave + kFW);
-  for (int s = 0; s < nmine; s += 2) {
-    step(b0, s);
-    if (s + 1 < nmine) step(b1, s + 1);
+  if constexpr (kWgmBufs == 2) {
+    Buf b0, b1;
+    if (nmine > 0) load(b0, c0 + wave);
+    if (nmine > 1) load(b1, c0 + wave + kFW);
+    for (int s = 0; s < nmine; s += 2) {
+      step(b0, s);
+      if (s + 1 < nmine) step(b1, s + 1);
+    }
+  } else {  // one register buffer: chunk s + 1's loads in flight during chunk s's MFMAs
+    Buf b0;
+    if (nmine > 0) load(b0, c0 + wave);
+    for (int s = 0; s < nmine; ++s) step(b0, s);
   }
   LBT_TS(1);
   __syncthreads();  // the partials overwrite the staging regions
-  // acc[t] element i: ci = 4kg + i, co = j (16x16 C/D map)
+  // acc[t] element i: ci = 4kg + i, co = j (16x16 C/D map); waves w and w + kFW/2 share slot w
+  constexpr int kHalf = kFW / 2;
+  if (wave < kHalf) {
 #pragma unroll
-  for (int t = 0; t < 9; ++t) *reinterpret_cast<v4i*>(&sm.red[wave][(t * 64 + lane) * 4]) = acc[t];
+    for (int t = 0; t < 9; ++t) *reinterpret_cast<v4i*>(&sm.red[wave][(t * 64 + lane) * 4]) = acc[t];
+  }
+  __syncthreads();
+  if (wave >= kHalf) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      v4i* q = reinterpret_cast<v4i*>(&sm.red[wave - kHalf][(t * 64 + lane) * 4]);
+      *q = *q + acc[t];
+    }
+  }
   __syncthreads();
   LBT_TS(2);
   int32_t* dst = wa.slab + (int64_t)(split % wa.nshard) * 9 * Cin * Cout + (int64_t)cis * 16 * Cout + cos * 16;
   for (int i = threadIdx.x; i < 9 * 256; i += kFW * 64) {
     int v = 0;
 #pragma unroll
-    for (int w = 0; w < kFW; ++w) v += sm.red[w][i];
+    for (int w = 0; w < kHalf; ++w) v += sm.red[w][i];
     const int t = i >> 8, l = (i >> 2) & 63, ii = i & 3;
     const int ci = 4 * (l >> 4) + ii, co = l & 15;
     if (v) LBT_GADD(&dst[((int64_t)t * Cin + ci) * Cout + co], v);  // integer atomics: exact, order-independent
@@ -955,7 +981,7 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
   LBT_TS(3);
 }
 
-__global__ __launch_bounds__(kFW * 64, 4) void conv_wgrad_many_kernel(const WgradMany m) {
+__global__ __launch_bounds__(kFW * 64, LBT_WGM_OCC) void conv_wgrad_many_kernel(const WgradMany m) {
   __shared__ __attribute__((aligned(16))) WgradManyShared sm;
   const uint32_t b = blockIdx.x;
   int j = 0;
