@@ -389,6 +389,14 @@ typedef struct lbt_chain_bwd_b {
   int64_t rows, inner; int32_t C;
 } lbt_chain_bwd_b;
 int lbt_bn_chain_bwd_b(const lbt_chain_bwd_b* a, void* stream);
+/* The stem's whole backward in one launch (replaces lbt_bn_chain_bwd_b + lbt_conv_stem_wgrad of the
+ * fused plan; dynamic_fixed_point.py:620-623 pass B of the stem BN, :299-302 conv1's quantised
+ * gradient and dW): pass B of b (C = 16, 8-bit qo, no dx / gcolsum; b->gq optional -- the codes are
+ * only written when it is non-NULL) evaluated straight into the weight gradient's operand, then
+ * lbt_conv_stem_wgrad's exact partials into slab[nshard][K][16]. Shapes: 3x3 / stride 1 / SAME,
+ * Cout 16, W in {8,16,32,64}, (H*W) % LBT_STEM_WG_PIXELS == 0. Bit-identical to the two launches. */
+int lbt_conv_stem_bwd(const lbt_chain_bwd_b* b, const int16_t* x, lbt_conv_desc d, int32_t* slab, int32_t nshard,
+                      void* stream);
 /* Two pass-B chains of the same shape (rows, inner, C) and flags in one launch: a projection
  * block's shortcut-BN and first-BN backward (dynamic_fixed_point.py:620-623 for ns and n1 of
  * :746-875), both feeding strided convs whose dgrad has no pass-B prologue. Bit-identical to two

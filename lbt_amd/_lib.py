@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -183,6 +183,7 @@ _SIGS = {
     "lbt_conv_wgrad_reduce64": [_P, c_int32, c_int32, c_int32, QDesc, QDesc, _P, c_float, _P, _P],
     "lbt_conv_stem_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
     "lbt_conv_stem_wgrad": [_P, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_stem_bwd": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_stem_wide_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_stem_wide_nsplit": [ConvDesc],
     "lbt_conv_stem_wide_wgrad": [_P, c_int32, _P, c_int32, ConvDesc, _P, c_int32, _P],

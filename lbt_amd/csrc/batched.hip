@@ -183,20 +183,28 @@ __global__ __launch_bounds__(256) void step_reduce_kernel(const lbt_rjob* __rest
                                                           lbt_head head, int has_head, lbt_xchg x) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLds];
   const int b = blockIdx.x;
+  LBT_TS(0);
   if (b < r_blocks) {
+    LBT_TROLE(1);
     rjob_block(rjobs, nr, b, lds, x);
+    LBT_TS(1);
     return;
   }
   const int b2 = b - r_blocks;
   if (b2 < np * pblk) {
+    LBT_TROLE(2);
     pjob_channel(pjobs[b2 / pblk], (b2 % pblk) * 256 + threadIdx.x, x);
+    LBT_TS(1);
     return;
   }
   const int b3 = b2 - np * pblk;
   if (has_head && b3 == 0) {
+    LBT_TROLE(3);
     head_reduce(head, x, lds);
+    LBT_TS(1);
     return;
   }
+  LBT_TROLE(4);
   const int i = (b3 - has_head) * 4 + (int)(threadIdx.x >> 6);
   if (x.buf && i < x.nslots) fold_slot_x(x, i);
 }
@@ -279,6 +287,8 @@ __global__ __launch_bounds__(kThreads) void step_prologue_kernel(Prologue a) {
 }
 
 }  // namespace
+
+LBT_TRACE_SETTER(batched)
 
 extern "C" int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t max_n, int64_t* zero, int64_t nzero,
                                    void* stream) {

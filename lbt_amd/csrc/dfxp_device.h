@@ -36,6 +36,12 @@ static __device__ unsigned long long* lbt_trace_buf;
       }                                                                                                 \
     }                                                                                                   \
   } while (0)
+// slot 6 = a role tag (workgroups of one launch doing different work: tools/trace_phases.py groups by it)
+#define LBT_TROLE(v)                                                                                    \
+  do {                                                                                                  \
+    if (threadIdx.x == 0 && lbt_trace_buf)                                                              \
+      lbt_trace_buf[((size_t)blockIdx.x + (size_t)blockIdx.y * gridDim.x) * 8 + 6] = (v);               \
+  } while (0)
 #define LBT_TRACE_SETTER(tu)                                                                            \
   extern "C" int lbt_trace_set_##tu(void* p) {                                                          \
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(lbt_trace_buf), &p, sizeof(p));                            \
@@ -43,6 +49,9 @@ static __device__ unsigned long long* lbt_trace_buf;
 #else
 #define LBT_TS(i) \
   do {            \
+  } while (0)
+#define LBT_TROLE(v) \
+  do {               \
   } while (0)
 #define LBT_TRACE_SETTER(tu)
 #endif

@@ -54,16 +54,16 @@ struct HeadPaPre {
   int R[kPaPre], qn[kPaPre];
 };
 LBT_DEV bool head_pa_prefetchable(int HW, int C) { return HW * C / 4 <= kPaPre * kT; }
-LBT_DEV void head_pa_prefetch(const lbt_chain_bwd_a& a, int n, int HW, int C, HeadPaPre& p) {
+LBT_DEV void head_pa_prefetch(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0, int q1, HeadPaPre& p) {
   const lbt_bwd_branch& B = a.b1;
-  const int nq = HW * C / 4, t = threadIdx.x;
+  const int t = threadIdx.x;
   const int64_t base = (int64_t)n * HW * C;
   const float* tr = B.qrg.noise ? B.qrg.noise : zf();
   const float* tn = B.qng.noise ? B.qng.noise : zf();
   const uint32_t mr = B.qrg.noise ? 0xffffffffu : 0u, mn = B.qng.noise ? 0xffffffffu : 0u;
 #pragma unroll
   for (int it = 0; it < kPaPre; ++it) {
-    const int q = t + it * kT, qq = q < nq ? q : 0;
+    const int q = q0 + t + it * kT, qq = q < q1 ? q : q0;
     const int64_t e = base + 4 * (int64_t)qq;
     p.ym[it] = *reinterpret_cast<const float4*>(a.y_mask + e);
     p.R[it] = *reinterpret_cast<const int*>(B.R + e);
@@ -74,13 +74,14 @@ LBT_DEV void head_pa_prefetch(const lbt_chain_bwd_a& a, int n, int HW, int C, He
 }
 
 // use_pre: pre holds head_pa_prefetch's operands (HW * C / 4 <= kPaPre * kT); else loaded here
-LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const float* s_dp, int* sh_cnt,
-                         const HeadPaPre& pre, bool use_pre) {
+// (quads [q0, q1) of the sample: the workgroup's share, q0 % (C / 4) == 0)
+LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0, int q1, const float* s_dp,
+                         int* sh_cnt, const HeadPaPre& pre, bool use_pre) {
   __shared__ int s_sum[kT / 64][4 * 256];  // per wave: [sum][channel] (|.| < 2^19)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const lbt_bwd_branch& B = a.b1;
   const QState qrg = qstate(B.qrg), qng = qstate(B.qng);
-  const int nq = HW * C / 4, c0 = (4 * t) % C;
+  const int c0 = (4 * t) % C;
   const int64_t base = (int64_t)n * HW * C;
   const float inv = 1.0f / (float)HW;
   float gam[4];
@@ -124,8 +125,8 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const f
   if (use_pre) {  // uniform
 #pragma unroll
     for (int it = 0; it < kPaPre; ++it) {
-      const int q = t + it * kT;
-      if (q >= nq) break;
+      const int q = q0 + t + it * kT;
+      if (q >= q1) break;
       const Noise4 nrg = !sr ? z4 : B.qrg.noise ? Noise4{{pre.nr[it].x, pre.nr[it].y, pre.nr[it].z, pre.nr[it].w}}
                                                 : qnoise4(B.qrg, qrg.step, (uint64_t)q);
       const Noise4 nng = !sn ? z4 : B.qng.noise ? Noise4{{pre.nn[it].x, pre.nn[it].y, pre.nn[it].z, pre.nn[it].w}}
@@ -133,7 +134,7 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const f
       pass(q, pre.ym[it], pre.R[it], pre.qn[it], nrg, nng);
     }
   } else {
-    for (int q = t; q < nq; q += kT) {
+    for (int q = q0 + t; q < q1; q += kT) {
       const int64_t e = base + 4 * (int64_t)q;
       const float4 ym4 = *reinterpret_cast<const float4*>(a.y_mask + e);
       const int Rw = *reinterpret_cast<const int*>(B.R + e);
@@ -178,14 +179,20 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, const f
   }
 }
 
-__global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa) {
+// S workgroups per sample (grid N * S): each one pools, quantises, takes the logits, softmax and
+// dgrad of its sample (the same operations on the same operands: identical values, a few KB from
+// L2), and runs pass A / the un-pool over its 1/S of the sample's pixels; workgroup s == 0 alone
+// writes the sample's outputs and counts its Dense_q quantisers.
+__global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa, int S) {
   __shared__ __attribute__((aligned(16))) float s_x[kXChunk / 4];
   __shared__ __attribute__((aligned(16))) int8_t s_w[kMaxW];
   __shared__ int s_pq[256], s_gq[64], s_part[16][16];
   __shared__ float s_z[64], s_dp[256];
   __shared__ int sh_cnt[4 * 2 * (kT / 64)];  // counters: qx, qg (+ pass A's qrg, qng)
-  const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = (int)blockIdx.x / S, split = (int)blockIdx.x - n * S, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bool lead = split == 0;
   const int C = h.C, K = h.K, HW = h.HW, N = h.N;
+  const int q0 = split * (HW / S) * C / 4, q1 = q0 + (HW / S) * C / 4;  // host: HW % S == 0
   LBT_TS(0);
   const QState sx = qstate(h.qx), sg = qstate(h.qg);
   int ovx1 = 0, ovx2 = 0, ovg1 = 0, ovg2 = 0;  // wave totals (quant_w)
@@ -217,8 +224,8 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   LBT_HEAD_LOAD_CHUNK(0);
   // the fused pass A's operands, in flight from here
   HeadPaPre pre;
-  const bool pre_ok = h.pa && head_pa_prefetchable(HW, C);  // uniform
-  if (pre_ok) head_pa_prefetch(pa, n, HW, C, pre);
+  const bool pre_ok = h.pa && head_pa_prefetchable(HW / S, C);  // uniform
+  if (pre_ok) head_pa_prefetch(pa, n, HW, C, q0, q1, pre);
 
   // ---- AvgPool_q: channel t, the HW pixels summed in order (avgpool_fwd_kernel), from LDS
   float acc = 0.f;
@@ -252,11 +259,11 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   LBT_TS(1);
   if (t < C) {
     const float pooled = acc * (1.0f / (float)HW);
-    if (h.pooled) h.pooled[(int64_t)n * C + t] = pooled;
+    if (h.pooled && lead) h.pooled[(int64_t)n * C + t] = pooled;
     // Dense_q X quantiser (:385 stochastic_identity), noise index = channel (X.shape[1:] = [C])
     const int q = sx.active ? quant_w<-1>(sx, h.qx.stochastic, pooled, ux, ovx1, ovx2) : 0;
     s_pq[t] = q;
-    if (h.pq) h.pq[(int64_t)n * C + t] = (int8_t)q;
+    if (h.pq && lead) h.pq[(int64_t)n * C + t] = (int8_t)q;
   }
   __syncthreads();
 
@@ -278,11 +285,12 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
       for (int gg = 0; gg < 16; ++gg) z += s_part[gg][t];
       const float zf_ = (float)z * sxw;
       s_z[kb + t] = zf_;
-      h.logits[(int64_t)n * K + kb + t] = zf_;
+      if (lead) h.logits[(int64_t)n * K + kb + t] = zf_;
     }
     __syncthreads();
   }
 
+  LBT_TS(2);
   // ---- softmax cross-entropy in wave 0, lane k = class (softmax_xent_kernel's arithmetic:
   // max, then s = sum of expf(z - m) in class order, p = expf(z - m) / s)
   if (wave == 0) {
@@ -300,13 +308,13 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     if (lane < K) {
       const float p = e / s;
       const float dz = (p - (lane == y ? 1.f : 0.f)) / (float)(h.loss_n > 0 ? h.loss_n : N);
-      h.dz[(int64_t)n * K + lane] = dz;
+      if (lead) h.dz[(int64_t)n * K + lane] = dz;
       // Dense_q grad quantiser (:454), noise index = class
       const int q = sg.active ? quant_w<-1>(sg, h.qg.stochastic, dz, ug, ovg1, ovg2) : 0;
       s_gq[lane] = q;
-      if (h.gq) h.gq[(int64_t)n * K + lane] = (int8_t)q;
+      if (h.gq && lead) h.gq[(int64_t)n * K + lane] = (int8_t)q;
     }
-    if (lane == 0) {
+    if (lane == 0 && lead) {
       const float lse = logf(s) + m;
       const double term = (double)(lse - s_z[y]);
       uint8_t* rec = reinterpret_cast<uint8_t*>(h.scratch) + (int64_t)n * (C + kHeadRecPad);
@@ -316,11 +324,14 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   counts_stage_w(0, 4, ovx1, ovx2, sh_cnt);
   counts_stage_w(1, 4, ovg1, ovg2, sh_cnt);
   __syncthreads();
-  counts_publish(0, 4, h.qx, sh_cnt);
-  counts_publish(1, 4, h.qg, sh_cnt);
+  if (lead) {
+    counts_publish(0, 4, h.qx, sh_cnt);
+    counts_publish(1, 4, h.qg, sh_cnt);
+  }
 
+  LBT_TS(3);
   // ---- the record's codes: pq[C] | gq[64]
-  {
+  if (lead) {
     uint32_t* rec = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(h.scratch) + (int64_t)n * (C + kHeadRecPad));
     if (t < C / 4) {
       uint32_t w = 0;
@@ -348,21 +359,21 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     s_dp[t] = (float)a * ldexpf(1.0f, -(frac_exp(h.qg) + frac_exp(h.qw)));
   }
   __syncthreads();
+  LBT_TS(4);
   if (h.pa) {  // uniform (the descriptor itself travels by value in pa)
-    head_pass_a(pa, n, HW, C, s_dp, sh_cnt, pre, pre_ok);
-    LBT_TS(2);
+    head_pass_a(pa, n, HW, C, q0, q1, s_dp, sh_cnt, pre, pre_ok);
+    LBT_TS(5);
     return;
   }
   {
     const float inv = 1.0f / (float)HW;
     float4* gx = reinterpret_cast<float4*>(h.gx + (int64_t)n * HW * C);
-    const int nq = HW * C / 4;  // C % 4 == 0
-    for (int i = t; i < nq; i += kT) {
+    for (int i = q0 + t; i < q1; i += kT) {  // C % 4 == 0
       const int c = (4 * i) % C;
       gx[i] = make_float4(s_dp[c] * inv, s_dp[c + 1] * inv, s_dp[c + 2] * inv, s_dp[c + 3] * inv);
     }
   }
-  LBT_TS(2);
+  LBT_TS(5);
 }
 
 }  // namespace
@@ -393,6 +404,14 @@ extern "C" int lbt_head_fwd_bwd(const lbt_head* h, void* stream) {
     return LBT_EINVAL;
   lbt_chain_bwd_a pa{};
   if (h->pa) pa = *h->pa;
-  hipLaunchKernelGGL(head_kernel, dim3((unsigned)h->N), dim3(kT), 0, (hipStream_t)stream, *h, pa);
+  // workgroups per sample: the pass A / un-pool split over up to LBT_HEAD_SPLIT (default 2) pixel ranges
+  static const int smax = [] {
+    const char* e = getenv("LBT_HEAD_SPLIT");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : v;
+  }();
+  int S = smax;
+  while (S > 1 && (h->HW % S || (int64_t)h->N * S > 0x7fffffff)) --S;
+  hipLaunchKernelGGL(head_kernel, dim3((unsigned)(h->N * S)), dim3(kT), 0, (hipStream_t)stream, *h, pa, S);
   return (int)hipGetLastError();
 }

@@ -463,9 +463,22 @@ class FusedResNet:
         aB = self._chain_bwd_b(n0, Gn0, qn0, sums0, shp0, C0, gq0, c.grad_range, None)
         if self.sync_bn:
             bwd.append(self._allreduce(sums0))
-        bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB)))
+        # the stem's pass B evaluated inside its weight-gradient launch (lbt_conv_stem_bwd): one launch,
+        # and the gradient codes (read by nothing else: d loss / d image is not needed) stay in LDS
+        stem_bwd = (self._stem and os.environ.get("LBT_STEM_BWD", "1") == "1" and C0 == 16 and Cin0 <= 4
+                    and (dc.KH, dc.KW, dc.SH, dc.SW, dc.PT, dc.PL) == (3, 3, 1, 1, 1, 1) and dc.Ho == H and dc.Wo == W
+                    and W in (8, 16, 32, 64) and (H * W) % 256 == 0)
         self._keep += [aA, aB]
-        if self._stem:
+        if stem_bwd:
+            aB.gq = None
+            ns0, slab0 = ops.stem_slab(self._c, "slab0", dc, ctx)
+            bwd.append(L("lbt_conv_stem_bwd", ctypes.byref(aB), ptr(ximg), dc, ptr(slab0), ns0, k="stem_bwd_kernel",
+                         nb=ops._chain_bwd_b_bytes(aB) + 2 * ximg.numel() + 4 * slab0.numel()))
+        else:
+            bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB), k="chain_bwd_b_kernel", nb=ops._chain_bwd_b_bytes(aB)))
+        if stem_bwd:
+            pass  # (the weight gradient ran above)
+        elif self._stem:
             ns0, slab0 = ops.stem_slab(self._c, "slab0", dc, ctx)
             bwd.append(L("lbt_conv_stem_wgrad", ptr(ximg), ptr(gq0), dc, ptr(slab0), ns0, k="stem_wgrad_kernel",
                          nb=2 * ximg.numel() + gq0.numel() + 4 * slab0.numel()))

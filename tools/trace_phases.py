@@ -68,7 +68,7 @@ def main():
         tr.step(xs[0], ys[0])
     torch.cuda.synchronize()
     lib = _lib.load()
-    setters = [getattr(lib, "lbt_trace_set_" + t) for t in ("conv", "bn", "head", "stem") if hasattr(lib, "lbt_trace_set_" + t)]
+    setters = [getattr(lib, "lbt_trace_set_" + t) for t in ("conv", "bn", "head", "stem", "batched") if hasattr(lib, "lbt_trace_set_" + t)]
     for s in setters:
         s.argtypes = [ctypes.c_void_p]
     nwg_max = 1 << 15
@@ -101,7 +101,7 @@ def main():
             continue
         T0 = t[:, 0].min()
         groups = [("all", t)]
-        if "wgrad_many" in f.kname:  # slot 6 = job index + 1: one line per job, phases 0..3
+        if (t[:, 6] != 0).any():  # slot 6 = job index / role + 1: one line per job, phases 0..3
             for jid in sorted(set(t[:, 6].tolist())):
                 tj = t[t[:, 6] == jid].copy()
                 tj[:, 6] = 0
