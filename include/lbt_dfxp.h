@@ -741,6 +741,28 @@ int lbt_affine_f32(const float* x, const float* gb, int64_t n, int32_t C, int32_
 int lbt_affine_grads_f32(const double* part, int32_t nsplit, int32_t C, const float* gamma, float wd2, float* dgamma,
                          float* dbeta, void* stream);
 
+/* ---- The exact data-parallel exchange of the layer-wise models (ResNet-50, configs[3] at N GPUs;
+ * SURVEY 8(e)). Each of these writes the INTEGER numerator of a gradient where its dequantising twin
+ * (same name without _x) writes dW = (float)S * 2^-(ex+eg) + wd2 * W (dynamic_fixed_point.py:302,
+ * :457-460) or dgamma / dbeta (:689-691): num[i] = S (int64, exact). The trainer points num into
+ * the int64 exchange buffer at the gradient's offset in the flat gradient buffer, all-reduces it
+ * (RCCL, SUM: exact and order-independent) and dequantises once with lbt_step_finish -- so a step
+ * on N ranks equals the oracle's N-shard step (oracle/resnet.py dp_train_step) bit for bit.
+ * lbt_softmax_xent_n: lbt_softmax_xent(_wide) with the mean over `norm` >= N rows (the GLOBAL
+ * batch of a shard) and, if loss_fx != NULL, the ordered double sum of the loss terms in 2^-32 fixed
+ * point (the exchange's loss slot). */
+int lbt_conv_wgrad_reduce_x(const int32_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int32_t x_u8off,
+                            const int64_t* gcolsum, int64_t* num, void* stream);
+int lbt_conv_wgrad_reduce64_x(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int64_t* num,
+                              void* stream);
+int lbt_dense_wgrad_x(const int8_t* xq, const void* g, int32_t g16, int32_t N, int32_t in_units, int32_t units,
+                      int64_t* num, void* stream);
+int lbt_bn_param_grads_x(const int64_t* sums, int32_t C, int64_t* num_g, int64_t* num_b, void* stream);
+int lbt_softmax_xent_n(const float* z, const int32_t* labels, int32_t N, int32_t K, int32_t norm, float* loss,
+                       float* dz, int64_t* loss_fx, void* stream);
+int lbt_softmax_xent_wide_n(const float* z, const int32_t* labels, int32_t N, int32_t K, int32_t norm, float* loss,
+                            float* dz, int64_t* loss_fx, void* stream);
+
 /* ABI version for the Python loader. */
 int lbt_abi_version(void);
 

@@ -184,6 +184,12 @@ _SIGS = {
     "lbt_conv_stem_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
     "lbt_conv_stem_wgrad": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_stem_bwd": [_P, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_wgrad_reduce_x": [_P, c_int32, c_int32, c_int32, c_int32, _P, _P, _P],
+    "lbt_conv_wgrad_reduce64_x": [_P, c_int32, c_int32, c_int32, _P, _P],
+    "lbt_dense_wgrad_x": [_P, _P, c_int32, c_int32, c_int32, c_int32, _P, _P],
+    "lbt_bn_param_grads_x": [_P, c_int32, _P, _P, _P],
+    "lbt_softmax_xent_n": [_P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P],
+    "lbt_softmax_xent_wide_n": [_P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P],
     "lbt_conv_stem_wide_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_stem_wide_nsplit": [ConvDesc],
     "lbt_conv_stem_wide_wgrad": [_P, c_int32, _P, c_int32, ConvDesc, _P, c_int32, _P],

@@ -176,37 +176,42 @@ LBT_DEV void fold_slot_x(const lbt_xchg& x, int i) {
   }
 }
 
-// lbt_step_reduce(_x): [r_blocks wgrad-reduce blocks][np * pblk param-grad blocks][1 head block]
-// [exchange only: ceil(nslots / 4) counter-fold blocks]
+// lbt_step_reduce(_x): [1 head block][np * pblk param-grad blocks][exchange only: ceil(nslots / 4)
+// counter-fold blocks][r_blocks wgrad-reduce blocks]. The head block (a serial chain of ~7 us: the
+// records, the Dense_q dW, the ordered loss sum) is dispatched first: placed last, it started only
+// after the ~1 000 wgrad-reduce blocks had been dispatched (~5 us) and ended the launch.
 __global__ __launch_bounds__(256) void step_reduce_kernel(const lbt_rjob* __restrict__ rjobs, int nr, int r_blocks,
                                                           const lbt_pjob* __restrict__ pjobs, int np, int pblk,
-                                                          lbt_head head, int has_head, lbt_xchg x) {
+                                                          lbt_head head, int has_head, lbt_xchg x, int fold) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLds];
-  const int b = blockIdx.x;
+  int b = blockIdx.x;
   LBT_TS(0);
-  if (b < r_blocks) {
-    LBT_TROLE(1);
-    rjob_block(rjobs, nr, b, lds, x);
-    LBT_TS(1);
-    return;
+  if (has_head) {
+    if (b == 0) {
+      LBT_TROLE(3);
+      head_reduce(head, x, lds);
+      LBT_TS(1);
+      return;
+    }
+    --b;
   }
-  const int b2 = b - r_blocks;
-  if (b2 < np * pblk) {
+  if (b < np * pblk) {
     LBT_TROLE(2);
-    pjob_channel(pjobs[b2 / pblk], (b2 % pblk) * 256 + threadIdx.x, x);
+    pjob_channel(pjobs[b / pblk], (b % pblk) * 256 + threadIdx.x, x);
     LBT_TS(1);
     return;
   }
-  const int b3 = b2 - np * pblk;
-  if (has_head && b3 == 0) {
-    LBT_TROLE(3);
-    head_reduce(head, x, lds);
-    LBT_TS(1);
+  b -= np * pblk;
+  if (b < fold) {
+    LBT_TROLE(4);
+    const int i = b * 4 + (int)(threadIdx.x >> 6);
+    if (x.buf && i < x.nslots) fold_slot_x(x, i);
     return;
   }
-  LBT_TROLE(4);
-  const int i = (b3 - has_head) * 4 + (int)(threadIdx.x >> 6);
-  if (x.buf && i < x.nslots) fold_slot_x(x, i);
+  b -= fold;
+  LBT_TROLE(1);
+  rjob_block(rjobs, nr, b, lds, x);
+  LBT_TS(1);
 }
 
 // grid (blocks, njobs): thread -> noise block b (4 values, one Philox call)
@@ -428,7 +433,7 @@ int step_reduce_launch(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, cons
   const int64_t blocks = (int64_t)r_blocks + (int64_t)np * pblk + (head ? 1 : 0) + fold;
   if (blocks <= 0) return LBT_OK;
   hipLaunchKernelGGL(step_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rjobs, nr, r_blocks,
-                     pjobs, np, pblk, h, head ? 1 : 0, x);
+                     pjobs, np, pblk, h, head ? 1 : 0, x, fold);
   return (int)hipGetLastError();
 }
 }  // namespace

@@ -621,14 +621,20 @@ __global__ __launch_bounds__(kThreads) void chain_bwd_b2_kernel(lbt_chain_bwd_b 
     chain_bwd_b_body<F>(b, rpt, blockIdx.y - ny);
 }
 
+// num_g / num_b (the exact exchange): the integer sums instead, dequantised after the all-reduce
 __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
-                                   float wd2, float* dgamma, float* dbeta) {
+                                   float wd2, float* dgamma, float* dbeta, long long* num_g, long long* num_b) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   long long sgr = 0, sg = 0;
   for (int k = 0; k < LBT_NSHARD; ++k) {
     sgr += sums[(int64_t)k * 4 * C + c];
     sg += sums[(int64_t)k * 4 * C + C + c];
+  }
+  if (num_g) {
+    num_g[c] = sgr;
+    num_b[c] = sg;
+    return;
   }
   const double g2 = ldexp(1.0, -frac_exp(qrg)), r = ldexp(1.0, -frac_exp(qr));
   const float a = (float)((double)sgr * (g2 * r));
@@ -793,6 +799,12 @@ extern "C" int lbt_bn_chain_bwd_b_pair(const lbt_chain_bwd_b* a, const lbt_chain
 extern "C" int lbt_bn_param_grads(const int64_t* sums, int32_t C, lbt_qdesc qrg, lbt_qdesc qr, const float* gamma,
                                   float wd2, float* dgamma, float* dbeta, void* stream) {
   hipLaunchKernelGGL(param_grads_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, C, qrg, qr,
-                     gamma, wd2, dgamma, dbeta);
+                     gamma, wd2, dgamma, dbeta, nullptr, nullptr);
+  return (int)hipGetLastError();
+}
+extern "C" int lbt_bn_param_grads_x(const int64_t* sums, int32_t C, int64_t* num_g, int64_t* num_b, void* stream) {
+  if (!num_g || !num_b || C <= 0) return LBT_EINVAL;
+  hipLaunchKernelGGL(param_grads_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, C, lbt_qdesc{},
+                     lbt_qdesc{}, nullptr, 0.f, nullptr, nullptr, (long long*)num_g, (long long*)num_b);
   return (int)hipGetLastError();
 }

@@ -217,11 +217,16 @@ bool wgrad_geom(const lbt_conv_desc& d, int nsplit, dim3& grid, int& chunk, size
 template <typename TACC>
 __global__ __launch_bounds__(256) void wgrad_reduce_generic_kernel(const TACC* __restrict__ slab, int nsplit, int64_t total,
                                                                   lbt_qdesc qx, lbt_qdesc qg, const float* __restrict__ w,
-                                                                  float wd2, float* __restrict__ dw) {
+                                                                  float wd2, float* __restrict__ dw,
+                                                                  long long* __restrict__ num) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   long long s = 0;
   for (int b = 0; b < nsplit; ++b) s += (long long)slab[(int64_t)b * total + i];
+  if (num) {  // the exact exchange: the numerator, dequantised after the all-reduce
+    num[i] = s;
+    return;
+  }
   const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qg)));
   const float a = (float)s * scale;
   const float b = wd2 * w[i];
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_generic_kernel(const TACC* _
 __global__ __launch_bounds__(256) void wgrad_reduce64_split_kernel(const long long* __restrict__ slab, int nsplit,
                                                                    int64_t total, lbt_qdesc qx, lbt_qdesc qg,
                                                                    const float* __restrict__ w, float wd2,
-                                                                   float* __restrict__ dw) {
+                                                                   float* __restrict__ dw, long long* __restrict__ num) {
   __shared__ long long red[4][64];
   const int lo = threadIdx.x & 63, sg = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + lo;
@@ -246,6 +251,10 @@ __global__ __launch_bounds__(256) void wgrad_reduce64_split_kernel(const long lo
   __syncthreads();
   if (sg != 0 || i >= total) return;
   s = red[0][lo] + red[1][lo] + red[2][lo] + red[3][lo];
+  if (num) {
+    num[i] = s;
+    return;
+  }
   const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qg)));
   const float a = (float)s * scale;
   const float b = wd2 * w[i];
@@ -289,15 +298,24 @@ extern "C" int lbt_conv_wgrad_generic16(const void* xq, int32_t x_i16, const int
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_conv_wgrad_reduce64(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, lbt_qdesc qx,
-                                       lbt_qdesc qg, const float* w, float wd2, float* dw, void* stream) {
+static int reduce64_launch(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, lbt_qdesc qx, lbt_qdesc qg,
+                           const float* w, float wd2, float* dw, int64_t* num, void* stream) {
   if (nsplit <= 0 || K <= 0 || Cout <= 0) return LBT_EINVAL;
   const int64_t total = (int64_t)K * Cout;
   if (nsplit > 8)
     hipLaunchKernelGGL(wgrad_reduce64_split_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0,
-                       (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw);
+                       (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw, (long long*)num);
   else
     hipLaunchKernelGGL((wgrad_reduce_generic_kernel<long long>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw);
+                       (hipStream_t)stream, (const long long*)slab, nsplit, total, qx, qg, w, wd2, dw, (long long*)num);
   return (int)hipGetLastError();
+}
+extern "C" int lbt_conv_wgrad_reduce64(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, lbt_qdesc qx,
+                                       lbt_qdesc qg, const float* w, float wd2, float* dw, void* stream) {
+  return reduce64_launch(slab, nsplit, K, Cout, qx, qg, w, wd2, dw, nullptr, stream);
+}
+extern "C" int lbt_conv_wgrad_reduce64_x(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int64_t* num,
+                                         void* stream) {
+  if (!num) return LBT_EINVAL;
+  return reduce64_launch(slab, nsplit, K, Cout, lbt_qdesc{}, lbt_qdesc{}, nullptr, 0.f, nullptr, num, stream);
 }

@@ -453,7 +453,8 @@ __global__ __launch_bounds__(kThreads, (CS == 1 && NB == 1) ? 8 : 1) void dgrad_
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const int32_t* __restrict__ slab, int nsplit, int K,
                                                            int Cout, int x_u8off, const int64_t* __restrict__ gcolsum,
                                                            lbt_qdesc qx, lbt_qdesc qg, const float* __restrict__ w,
-                                                           float wd2, float* __restrict__ dw) {
+                                                           float wd2, float* __restrict__ dw,
+                                                           long long* __restrict__ num) {
   __shared__ long long red[8][32];
   const int lo = threadIdx.x & 31, sg = threadIdx.x >> 5;
   const int64_t total = (int64_t)K * Cout;
@@ -472,6 +473,10 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const int32_t* __rest
     long long cs = 0;
     for (int k = 0; k < LBT_NSHARD; ++k) cs += gcolsum[(int64_t)k * 2 * Cout + co];
     s += 128ll * cs;
+  }
+  if (num) {  // the exact exchange: the numerator, dequantised after the all-reduce
+    num[i] = s;
+    return;
   }
   const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qg)));
   const float a = (float)s * scale;
@@ -1054,7 +1059,15 @@ extern "C" int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_
   const int64_t total = (int64_t)K * Cout;
   const int64_t blocks = (total + 31) / 32;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, slab, nsplit, K,
-                     Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw);
+                     Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw, nullptr);
+  return (int)hipGetLastError();
+}
+extern "C" int lbt_conv_wgrad_reduce_x(const int32_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int32_t x_u8off,
+                                       const int64_t* gcolsum, int64_t* num, void* stream) {
+  if (!num || nsplit <= 0 || K <= 0 || Cout <= 0) return LBT_EINVAL;
+  const int64_t blocks = ((int64_t)K * Cout + 31) / 32;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, slab, nsplit, K,
+                     Cout, x_u8off, gcolsum, lbt_qdesc{}, lbt_qdesc{}, nullptr, 0.f, nullptr, (long long*)num);
   return (int)hipGetLastError();
 }
 

@@ -139,7 +139,7 @@ template <typename TG>
 __global__ __launch_bounds__(kThreads) void dense_wgrad_kernel(const int8_t* __restrict__ x, const TG* __restrict__ g,
                                                                int N, int IN, int OUT, lbt_qdesc qx, lbt_qdesc qg,
                                                                const float* __restrict__ w, float wd2,
-                                                               float* __restrict__ dw) {
+                                                               float* __restrict__ dw, long long* __restrict__ num) {
   const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const int uq = OUT / 4;
   if (t >= (int64_t)IN * uq) return;
@@ -156,6 +156,11 @@ __global__ __launch_bounds__(kThreads) void dense_wgrad_kernel(const int8_t* __r
   const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qg)));
   const int64_t o = (int64_t)k * OUT + u;
   const long long sv[4] = {s0, s1, s2, s3};
+  if (num) {  // the exact exchange: the numerators, dequantised after the all-reduce (lbt_step_finish)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) num[o + j] = sv[j];
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float av = (float)sv[j] * scale;
@@ -169,7 +174,8 @@ __global__ __launch_bounds__(kThreads) void dense_wgrad_kernel(const int8_t* __r
 // fixed order. Same per-element formulas as softmax_xent_kernel (misc.hip).
 __global__ __launch_bounds__(1024) void softmax_xent_wide_kernel(const float* __restrict__ z,
                                                                  const int32_t* __restrict__ labels, int N, int K,
-                                                                 float* __restrict__ loss, float* __restrict__ dz) {
+                                                                 float* __restrict__ loss, float* __restrict__ dz,
+                                                                 int norm, long long* loss_fx) {
   __shared__ double part[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double acc = 0.0;
@@ -186,7 +192,7 @@ __global__ __launch_bounds__(1024) void softmax_xent_wide_kernel(const float* __
     const int y = labels[rr];
     for (int k = lane; k < K; k += 64) {
       const float p = expf(zr[k] - m) / s;
-      dz[(int64_t)rr * K + k] = (p - (k == y ? 1.f : 0.f)) / (float)N;
+      dz[(int64_t)rr * K + k] = (p - (k == y ? 1.f : 0.f)) / (float)norm;
     }
     if (lane == 0) {
       const float lse = logf(s) + m;
@@ -198,7 +204,8 @@ __global__ __launch_bounds__(1024) void softmax_xent_wide_kernel(const float* __
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int w = 0; w < 16; ++w) t += part[w];
-    loss[0] = (float)(t / (double)N);
+    loss[0] = (float)(t / (double)norm);
+    if (loss_fx) *loss_fx = (long long)llrint(t * 4294967296.0);
   }
 }
 
@@ -228,25 +235,46 @@ extern "C" int lbt_dense_gemm(const void* a, int32_t a16, int32_t lda, int32_t k
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_dense_wgrad(const int8_t* xq, const void* g, int32_t g16, int32_t N, int32_t in_units,
-                               int32_t units, lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2, float* dw,
-                               void* stream) {
+static int dense_wgrad_launch(const int8_t* xq, const void* g, int32_t g16, int32_t N, int32_t in_units,
+                              int32_t units, lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2, float* dw,
+                              int64_t* num, void* stream) {
   if (N <= 0 || in_units <= 0 || units <= 0 || units % 4) return LBT_EINVAL;
   const int64_t threads = (int64_t)in_units * (units / 4);
   dim3 grid((unsigned)((threads + kThreads - 1) / kThreads));
   hipStream_t st = (hipStream_t)stream;
   if (g16)
     hipLaunchKernelGGL(dense_wgrad_kernel<int16_t>, grid, dim3(kThreads), 0, st, xq, (const int16_t*)g, N, in_units,
-                       units, qx, qg, w, wd2, dw);
+                       units, qx, qg, w, wd2, dw, (long long*)num);
   else
     hipLaunchKernelGGL(dense_wgrad_kernel<int8_t>, grid, dim3(kThreads), 0, st, xq, (const int8_t*)g, N, in_units,
-                       units, qx, qg, w, wd2, dw);
+                       units, qx, qg, w, wd2, dw, (long long*)num);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lbt_dense_wgrad(const int8_t* xq, const void* g, int32_t g16, int32_t N, int32_t in_units,
+                               int32_t units, lbt_qdesc qx, lbt_qdesc qg, const float* w, float wd2, float* dw,
+                               void* stream) {
+  return dense_wgrad_launch(xq, g, g16, N, in_units, units, qx, qg, w, wd2, dw, nullptr, stream);
+}
+extern "C" int lbt_dense_wgrad_x(const int8_t* xq, const void* g, int32_t g16, int32_t N, int32_t in_units,
+                                 int32_t units, int64_t* num, void* stream) {
+  if (!num) return LBT_EINVAL;
+  return dense_wgrad_launch(xq, g, g16, N, in_units, units, lbt_qdesc{}, lbt_qdesc{}, nullptr, 0.f, nullptr, num,
+                            stream);
+}
+
+extern "C" int lbt_softmax_xent_wide_n(const float* z, const int32_t* labels, int32_t N, int32_t K, int32_t norm,
+                                       float* loss, float* dz, int64_t* loss_fx, void* stream) {
+  if (N <= 0 || K <= 0 || norm < N) return LBT_EINVAL;
+  hipLaunchKernelGGL(softmax_xent_wide_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, z, labels, N, K, loss, dz,
+                     norm, (long long*)loss_fx);
   return (int)hipGetLastError();
 }
 
 extern "C" int lbt_softmax_xent_wide(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss,
                                      float* dz, void* stream) {
   if (N <= 0 || K <= 0) return LBT_EINVAL;
-  hipLaunchKernelGGL(softmax_xent_wide_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, z, labels, N, K, loss, dz);
+  hipLaunchKernelGGL(softmax_xent_wide_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, z, labels, N, K, loss, dz,
+                     N, nullptr);
   return (int)hipGetLastError();
 }

@@ -73,8 +73,10 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ g, float* __restric
 }
 
 // one block; rows strided over threads; loss = mean over rows
+// norm: the batch the mean is over (N; the GLOBAL batch for a data-parallel shard); loss_fx: the
+// ordered double sum of the loss terms in 2^-32 fixed point (the exact exchange's loss slot)
 __global__ void softmax_xent_kernel(const float* __restrict__ z, const int32_t* __restrict__ labels, int N, int K,
-                                    float* __restrict__ loss, float* __restrict__ dz) {
+                                    float* __restrict__ loss, float* __restrict__ dz, int norm, long long* loss_fx) {
   __shared__ double red[256];
   double part = 0.0;
   for (int r = threadIdx.x; r < N; r += blockDim.x) {
@@ -86,7 +88,7 @@ __global__ void softmax_xent_kernel(const float* __restrict__ z, const int32_t* 
     const int y = labels[r];
     for (int k = 0; k < K; ++k) {
       const float p = expf(zr[k] - m) / s;
-      dz[(int64_t)r * K + k] = (p - (k == y ? 1.f : 0.f)) / (float)N;
+      dz[(int64_t)r * K + k] = (p - (k == y ? 1.f : 0.f)) / (float)norm;
     }
     const float lse = logf(s) + m;
     part += (double)(lse - zr[y]);
@@ -97,7 +99,10 @@ __global__ void softmax_xent_kernel(const float* __restrict__ z, const int32_t* 
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) loss[0] = (float)(red[0] / (double)N);
+  if (threadIdx.x == 0) {
+    loss[0] = (float)(red[0] / (double)norm);
+    if (loss_fx) *loss_fx = (long long)llrint(red[0] * 4294967296.0);
+  }
 }
 
 __global__ void sgd_momentum_kernel(float* __restrict__ w, float* __restrict__ a, const float* __restrict__ g,
@@ -164,7 +169,16 @@ extern "C" int lbt_avgpool_bwd(const float* g, float* dx, int32_t N, int32_t HW,
 }
 extern "C" int lbt_softmax_xent(const float* z, const int32_t* labels, int32_t N, int32_t K, float* loss, float* dz,
                                 void* stream) {
-  hipLaunchKernelGGL(softmax_xent_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, z, labels, N, K, loss, dz);
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, z, labels, N, K, loss, dz, N,
+                     nullptr);
+  return (int)hipGetLastError();
+}
+extern "C" int lbt_softmax_xent_n(const float* z, const int32_t* labels, int32_t N, int32_t K, int32_t norm, float* loss,
+                                  float* dz, int64_t* loss_fx, void* stream) {
+  if (N <= 0 || K <= 0 || norm < N) return LBT_EINVAL;
+  if (K > 64) return lbt_softmax_xent_wide_n(z, labels, N, K, norm, loss, dz, loss_fx, stream);
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, z, labels, N, K, loss, dz, norm,
+                     (long long*)loss_fx);
   return (int)hipGetLastError();
 }
 extern "C" int lbt_sgd_momentum(float* w, float* a, const float* g, int64_t n, float lr, float mu, float gscale,

@@ -249,7 +249,38 @@ def _conv_wgrad_i8(xq, x_u8off, gq, d, slab, nsplit, nshard):
     call("lbt_conv_wgrad_i8", ptr(xq), int(x_u8off), ptr(gq), d, ptr(slab), int(nsplit), int(nshard), stream())
 
 
+# ---- the exact data-parallel exchange of the layer-wise models (Trainer, lbt_amd/distributed.py): while a
+# sink is set, every gradient reduction writes the INTEGER numerator of its gradient into the int64
+# exchange buffer at the gradient's offset in the flat gradient buffer (the *_x entry points), and the
+# softmax normalises by the global batch and leaves its loss sum in the buffer's loss slot; the
+# trainer all-reduces the buffer and dequantises once (lbt_step_finish).
+_XSINK = None
+
+
+def set_exchange_sink(gbase=None, n=0, xbuf=None, loss_off=0, world=1):
+    """gbase: the flat gradient buffer (n fp32); xbuf: the int64 exchange buffer. No args: unset."""
+    global _XSINK
+    _XSINK = None if gbase is None else dict(gbase=gbase.data_ptr(), n=int(n), xbuf=xbuf.data_ptr(),
+                                             loss=xbuf.data_ptr() + 8 * int(loss_off), world=int(world))
+
+
+def _num(dw):
+    """The exchange slot of gradient tensor dw (None: no sink)."""
+    s = _XSINK
+    if s is None:
+        return None
+    off = dw.data_ptr() - s["gbase"]
+    if off < 0 or off + 4 * dw.numel() > 4 * s["n"] or off % 4:
+        raise RuntimeError("exact exchange: a gradient outside the flat gradient buffer")
+    return _lib.ctypes.c_void_p(s["xbuf"] + 2 * off)  # int64 index = fp32 index
+
+
 def conv_wgrad_reduce(slab, nsplit, K, Cout, x_u8off, gcolsum, qx, qg, w, wd2, dw):
+    num = _num(dw)
+    if num is not None:
+        call("lbt_conv_wgrad_reduce_x", ptr(slab), int(nsplit), int(K), int(Cout), int(x_u8off), ptr(gcolsum), num,
+             stream())
+        return
     call("lbt_conv_wgrad_reduce", ptr(slab), int(nsplit), int(K), int(Cout), int(x_u8off), ptr(gcolsum), qx, qg,
          ptr(w), float(wd2), ptr(dw), stream())
 
@@ -374,6 +405,10 @@ def chain_bwd_b(desc):
 
 
 def bn_param_grads(sums, C, qrg, qr, gamma, wd2, dgamma, dbeta):
+    ng = _num(dgamma)
+    if ng is not None:
+        call("lbt_bn_param_grads_x", ptr(sums), int(C), ng, _num(dbeta), stream())
+        return
     call("lbt_bn_param_grads", ptr(sums), int(C), qrg, qr, ptr(gamma), float(wd2), ptr(dgamma), ptr(dbeta), stream())
 
 
@@ -410,6 +445,11 @@ def avgpool_gen_bwd(g, dx, d):
 
 def softmax_xent(z, labels, loss, dz):
     N, K = z.shape
+    s = _XSINK
+    if s is not None:  # exact exchange: the mean over the GLOBAL batch, the loss sum into its slot
+        call("lbt_softmax_xent_n", ptr(z), ptr(labels), int(N), int(K), int(N * s["world"]), ptr(loss), ptr(dz),
+             _lib.ctypes.c_void_p(s["loss"]), stream())
+        return
     if K > 64:  # wide heads: one wave per row (the narrow kernel keeps the fused head's order)
         with _Timed("softmax_xent_wide_kernel", 8 * z.numel()):
             call("lbt_softmax_xent_wide", ptr(z), ptr(labels), int(N), int(K), ptr(loss), ptr(dz), stream())
@@ -437,6 +477,11 @@ def dense_gemm(a, b, kvalid, qa, qb, out, kernel="dense_gemm_kernel"):
 
 def dense_wgrad(xq, g, qx, qg, w, wd2, dw):
     N, IN = xq.shape
+    num = _num(dw)
+    if num is not None:
+        call("lbt_dense_wgrad_x", ptr(xq), ptr(g), int(g.dtype == torch.int16), int(N), int(IN), int(g.shape[1]), num,
+             stream())
+        return
     with _Timed("dense_wgrad_kernel", xq.numel() + g.numel() * g.element_size() + 8 * w.numel()):
         call("lbt_dense_wgrad", ptr(xq), ptr(g), int(g.dtype == torch.int16), int(N), int(IN), int(g.shape[1]), qx,
              qg, ptr(w), wd2, ptr(dw), stream())
@@ -525,6 +570,10 @@ def conv_wgrad_generic16(xq, x_i16, gq, d, slab, nsplit):
 
 
 def conv_wgrad_reduce64(slab, nsplit, K, Cout, qx, qg, w, wd2, dw):
+    num = _num(dw)
+    if num is not None:
+        call("lbt_conv_wgrad_reduce64_x", ptr(slab), int(nsplit), int(K), int(Cout), num, stream())
+        return
     call("lbt_conv_wgrad_reduce64", ptr(slab), int(nsplit), int(K), int(Cout), qx, qg, ptr(w), wd2, ptr(dw), stream())
 
 

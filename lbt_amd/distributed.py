@@ -12,7 +12,16 @@ dequant(sum_pixels Xq * Gq) + 2*wd*W, so summing the integer sums over ranks and
 (lbt_step_finish) is EXACT -- the quantised-gradient exchange of SURVEY 8(e) -- and independent of
 the order RCCL adds in. (2.2 MB; latency-bound on xGMI, one flat bucket.)
 
-Layer-wise models exchange dequantised gradients instead, an all-reduce SUM of
+Layer-wise models whose trainable variables are all integer-coded (quantised conv / dense W, BN
+gamma / beta: exact_layerwise_ok -- the ResNet-50 of configs[3]) use the SAME int64 exchange: while
+the Trainer runs their forward / backward, ops.set_exchange_sink points every gradient reduction
+(lbt_conv_wgrad_reduce(64)_x, lbt_dense_wgrad_x, lbt_bn_param_grads_x) at the gradient's slots of the
+buffer, the softmax (lbt_softmax_xent_n) normalises by the global batch and leaves its loss sum in the
+loss slot, and lbt_step_reduce_x's fold blocks add the counters: an N-rank step equals the oracle's
+N-shard step bit for bit (tests/test_dp_resnet50_gpu.py).
+
+Other layer-wise models (fp32-mode layers, biases) exchange dequantised gradients instead, an
+all-reduce SUM of
 
     [ flat fp32 gradients | every quantiser's folded overflow counters ]
 
@@ -81,6 +90,16 @@ def finish_segments(flat, device):
         blocks += (sz + 255) // 256
     raw = bytes((_lib.FSeg * len(segs))(*segs))
     return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device), blocks
+
+
+def exact_layerwise_ok(model):
+    """True when every trainable variable of a layer-wise model gets an INTEGER gradient numerator
+    (quantised conv / dense W, BN gamma / beta; no fp32-mode layer, no bias): the models the exact
+    int64 exchange (ops.set_exchange_sink) takes."""
+    for owner, var, _ in model.param_slots():
+        if var not in ("W", "gamma", "beta") or getattr(owner, "fmode", False):
+            return False
+    return True
 
 
 def allreduce_comm(comm, group=None):

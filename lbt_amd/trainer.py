@@ -89,12 +89,19 @@ class Trainer:
                             and os.environ.get("LBT_CAPTURE_COMM", "1") == "1")
         self.capture_comm = bool(capture_comm) and dist_on
         exact = self.dp and hasattr(model, "set_exchange")
-        if self.dp and not exact:
+        # layer-wise models (ResNet-50, configs[3]): the same exact int64 exchange when every gradient
+        # is an integer numerator (integer-coded W / gamma / beta only; LBT_EXACT_LAYERWISE=0: fp32)
+        self._lw_exact = (self.dp and not exact and D.exact_layerwise_ok(model)
+                          and os.environ.get("LBT_EXACT_LAYERWISE", "1") == "1")
+        if self.dp and not exact and not self._lw_exact:
             n = sum(getattr(o, v).numel() for o, v, _ in model.param_slots())
             self.comm = D.make_comm_buffer(n, len(self.ctx.quantizers), self.ctx.device)
         self.flat = FlatParams(model, self.comm)
+        self._loss_n = 0
         if exact:
             self._setup_exchange()
+        elif self._lw_exact:
+            self._setup_exchange_layerwise()
         self.ctx.sums_managed = True
         self.global_step = 0
         self._graphs = None
@@ -119,6 +126,18 @@ class Trainer:
         x.counts = ctx.counts.data_ptr()
         self._xchg = x
         m.set_exchange(x)
+        self._segs, self._seg_blocks = D.finish_segments(flat, ctx.device)
+
+    def _setup_exchange_layerwise(self):
+        """The exact exchange of a layer-wise model: every gradient reduction writes its integer
+        numerator into the exchange buffer (ops.set_exchange_sink during the step), the counters are
+        folded in by lbt_step_reduce_x's fold blocks; all-reduce, lbt_step_finish, range update."""
+        ctx, flat = self.ctx, self.flat
+        self.xbuf, x = D.make_exchange(flat.n, len(ctx.quantizers), ctx.device)
+        x.gbase = flat.g.data_ptr()
+        x.counts = ctx.counts.data_ptr()
+        x.pjob_scale = 1
+        self._xchg = x
         self._segs, self._seg_blocks = D.finish_segments(flat, ctx.device)
 
     # -- the reference's API ---------------------------------------------------------------
@@ -163,6 +182,18 @@ class Trainer:
             self.ctx.zero_sums()
         if hasattr(m, "train_fwd_bwd"):
             m.train_fwd_bwd(X, y)
+        elif self._lw_exact:
+            x = self._xchg
+            self._loss_n = int(X.shape[0]) * self.world
+            ops.set_exchange_sink(self.flat.g, self.flat.n, self.xbuf, x.loss_off, self.world)
+            try:
+                m.forward(X)
+                m.compute_loss(y)
+                m.backward()
+            finally:
+                ops.set_exchange_sink()
+            # the overflow counters into the buffer (lbt_step_reduce_x with its fold blocks only)
+            _lib.call("lbt_step_reduce_x", None, 0, 0, None, 0, 0, None, _lib.ctypes.byref(x), _lib.stream())
         else:
             m.forward(X)
             m.compute_loss(y)
@@ -184,7 +215,7 @@ class Trainer:
             _lib.call("lbt_step_finish", _lib.ptr(self._segs), len(self._segs) // _lib.ctypes.sizeof(_lib.FSeg),
                       self._seg_blocks, _lib.ptr(self.xbuf), _lib.ptr(f.w), _lib.ptr(f.a), _lib.ptr(f.g),
                       float(self.lr), float(self.momentum), _lib.ptr(self._active.loss), x.loss_off,
-                      int(self._active._head.loss_n), _lib.stream())
+                      self._loss_n if self._lw_exact else int(self._active._head.loss_n), _lib.stream())
             _lib.call("lbt_dfxp_range_update_x", _lib.ptr(ctx.exps), _lib.ptr(self.xbuf), x.cnt_off,
                       _lib.ptr(ctx.bits), _lib.ptr(ctx.target), _lib.ptr(ctx.nelem), len(ctx.quantizers),
                       _lib.ptr(ctx.step), _lib.stream())

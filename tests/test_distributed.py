@@ -173,3 +173,23 @@ def test_exact_int64_exchange_gloo(world):
         assert ok                                   # exact: bit-identical to the oracle's global step
         assert counts == res[0][2]                  # every rank sees the same global counts
         assert abs(loss - want_loss) < 1e-6
+
+
+def test_exchange_sink_slots_follow_the_flat_gradient_layout():
+    """ops.set_exchange_sink: a gradient view of the flat fp32 buffer maps to the int64 slots at the
+    same element offsets (the exact layer-wise exchange); a tensor outside the buffer is refused."""
+    from lbt_amd.dfxp import ops
+    g = torch.zeros(100, dtype=torch.float32)
+    x = torch.zeros(100 + 7, dtype=torch.int64)
+    ops.set_exchange_sink(g, 100, x, loss_off=106, world=4)
+    try:
+        assert ops._num(g[10:30]).value == x.data_ptr() + 8 * 10
+        assert ops._num(g).value == x.data_ptr()
+        assert ops._XSINK["loss"] == x.data_ptr() + 8 * 106 and ops._XSINK["world"] == 4
+        with pytest.raises(RuntimeError):
+            ops._num(torch.zeros(4))
+        with pytest.raises(RuntimeError):
+            ops._num(torch.zeros(200)[:101])
+    finally:
+        ops.set_exchange_sink()
+    assert ops._num(g) is None
