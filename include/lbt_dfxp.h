@@ -442,6 +442,22 @@ typedef struct lbt_conv_bwd {
 } lbt_conv_bwd;
 int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* p, void* stream);
 
+/* A projection block's strided convs' backward in ONE launch (the stage transition of the CIFAR
+ * ResNets: ResidualBlock_q :772-795 / :831-846 backward): pass B of BOTH BNs after the strided
+ * convs (b1: the 3x3/2 conv-1's BN, bs: the 1x1/2 shortcut's; each exactly lbt_bn_chain_bwd_b with
+ * gq required and stored, dx NULL), dx = dgrad(d1, wd1 on b1.gq) + dgrad(ds, wds on bs.gq) summed in
+ * fp32, and pass A of the BN that consumes dx (a) -- bit-identical to lbt_bn_chain_bwd_b_pair(bs, b1)
+ * followed by lbt_conv_dgrad2_chain_i8. Shapes: d1 3x3 stride 2 SAME (pads 0 / 1), ds 1x1 stride 2,
+ * Cin = C in {16, 32}, Cout = 2C, W * C = 512, H % (C == 16 ? 8 : 4) == 0; w4 != 0: packed 4-bit
+ * weight images. Else LBT_EINVAL.                                                              */
+typedef struct lbt_conv_bwd2 {
+  lbt_chain_bwd_b b1, bs;
+  const int8_t* wd1; int32_t ksd1; const int8_t* wds; int32_t ksds; int32_t w4;
+  lbt_conv_desc d1, ds; lbt_qdesc qw1, qws;
+  lbt_chain_bwd_a a;
+} lbt_conv_bwd2;
+int lbt_conv_bwd2_fused_i8(const lbt_conv_bwd2* p, void* stream);
+
 /* One stride-1 3x3 Conv2d_q's forward in ONE launch, with the BN element chain that produces its
  * input (ResidualBlock_q :858-863 / BatchNorm_q :584-616,677-683 -> Conv2d_q.forward :287-291):
  *   X  = chain c (exactly lbt_bn_chain_fwd; c.o1 = this conv's input codes, LBT_OUT_U8OFF, stored:

@@ -86,6 +86,12 @@ class ConvBwd(ctypes.Structure):
                 ("qw", QDesc), ("add_src", c_void_p), ("a", ChainBwdA), ("w", WgradJob)]
 
 
+class ConvBwd2(ctypes.Structure):
+    _fields_ = [("b1", ChainBwdB), ("bs", ChainBwdB), ("wd1", c_void_p), ("ksd1", c_int32), ("wds", c_void_p),
+                ("ksds", c_int32), ("w4", c_int32), ("d1", ConvDesc), ("ds", ConvDesc), ("qw1", QDesc),
+                ("qws", QDesc), ("a", ChainBwdA)]
+
+
 class ConvFwd(ctypes.Structure):
     _fields_ = [("c", ChainFwd), ("wf", c_void_p), ("ksf", c_int32), ("w4", c_int32), ("wcolsum", c_void_p),
                 ("d", ConvDesc), ("qw", QDesc), ("yq", c_void_p), ("qout", QDesc), ("ychsum", c_void_p)]
@@ -184,6 +190,7 @@ _SIGS = {
     "lbt_conv_stem_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
     "lbt_conv_stem_wgrad": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_stem_bwd": [_P, _P, ConvDesc, _P, c_int32, _P],
+    "lbt_conv_bwd2_fused_i8": [_P, _P],
     "lbt_conv_wgrad_reduce_x": [_P, c_int32, c_int32, c_int32, c_int32, _P, _P, _P],
     "lbt_conv_wgrad_reduce64_x": [_P, c_int32, c_int32, c_int32, _P, _P],
     "lbt_dense_wgrad_x": [_P, _P, c_int32, c_int32, c_int32, c_int32, _P, _P],

@@ -1705,6 +1705,479 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   return LBT_EINVAL;
 }
 
+// ============================================================================ fused transition backward
+// lbt_conv_bwd2_fused_i8: a projection block's first-conv / shortcut backward (the stage transition)
+// in ONE launch -- what lbt_bn_chain_bwd_b_pair + lbt_conv_dgrad2_chain_i8 computed in two:
+//   phase 1  pass B of BOTH BNs after the strided convs (conv-1's bn1 and the shortcut BN, at the
+//            low resolution Hq x Wq x Cq, Cq = 2C) over the low-res rows the workgroup's dx rows read
+//            (plus the one-row halo above that the 3x3/2 conv's SAME padding (top 0, bottom 1)
+//            reaches) -> int8 gradient-code images in LDS; owned rows store gq (the weight
+//            gradients' operands), count overflows and add the gq channel sums
+//   phase 2  dx = dgrad(3x3/2, gq1) + dgrad(1x1/2, gqs) from LDS: each lane's dx pixel takes the
+//            taps of its parity (the stride's zero rows read as 0), the two GEMMs in their own
+//            accumulators, summed in fp32 in the order the dual dgrad launch used
+//   phase 3  pass A of the BN that consumes dx (conv_bwd_kernel's phase 3)
+namespace {
+
+struct ConvBwd2Args {
+  lbt_chain_bwd_b b1, bs;
+  const int8_t* wd1;
+  const int8_t* wds;
+  lbt_qdesc qw1, qws;
+  int H;  // dx rows
+  lbt_chain_bwd_a a;
+};
+
+template <int C, int TH>
+struct Bwd2Shared {
+  int8_t g1[(TH / 2 + 1) * 512];   // conv-1's gradient codes, low-res rows q0-1 .. q0+TH/2-1 ([row][Wq][Cq])
+  int8_t gs[(TH / 2) * 512];       // the shortcut's, rows q0 .. q0+TH/2-1
+  float tile[TH * (512 / C) * (C + 4)];
+  float cst[2][5][2 * C];          // per BN (conv-1's, shortcut's): mu, sigma, sigma's rcp refinement, mg, mgx
+  int part[kBNW][(2 * 4 + 8) * C]; // per wave: pass-A sums (<= 2 branches x 4C), gq sums (2 x 2Cq)
+  int cnt[kBNW * 2 * 6];           // counters: qo1, qos, qrg / qng per branch
+};
+
+template <int CS, int CF, int NB, bool W4>
+__global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(ConvBwd2Args p) {
+  constexpr int C = CS * 16, C4 = C / 4, Cq = 2 * C, Cq4 = Cq / 4, CSq = 2 * CS, NT = CS;
+  constexpr int W = 512 / C, Wq = W / 2;  // W * C == Wq * Cq == 512 (host check)
+  constexpr int TH = tile_rows(CS), J = TH / 4;
+  constexpr int kK1 = (9 * CSq + 3) / 4;  // k-steps of the 3x3/2 dgrad
+  constexpr int NG1 = (TH / 2 + 1) * Wq * Cq4, NGS = (TH / 2) * Wq * Cq4;
+  constexpr int kIt = (NG1 + NGS + kBThreads - 1) / kBThreads;
+  static_assert(NG1 % 64 == 0 && CSq <= 4 && LBT_NSHARD == 32 && 2 * Cq / 16 <= kBNW, "layout");
+  __shared__ __attribute__((aligned(16))) Bwd2Shared<C, TH> sh;
+  LBT_TS(0);
+  const lbt_chain_bwd_a& A = p.a;
+  const uint32_t bid = blockIdx.x;
+  const int H = p.H, Hq = H / 2;
+  const int tpi = H / TH;
+  const int n = (int)(bid / (uint32_t)tpi), r0 = (int)(bid - (uint32_t)n * tpi) * TH, q0 = r0 / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int cq = (tid % C4) * 4;     // dx channel quad (phase 3)
+  const int cqq = (tid % Cq4) * 4;   // low-res channel quad (phase 1)
+  const int64_t img = (int64_t)n * H * W * C, imgq = (int64_t)n * Hq * Wq * Cq;
+
+  // ---------------- both BNs' pass-B statistics shard sums first (they gate the first barrier):
+  // wave w < 2 * CSq owns 16 channels of BN w / CSq; lane l reads shards 8 (l >> 4) .. + 7
+  constexpr int kSW = 2 * CSq;
+  long long sv[8][2];
+  if (wave < kSW) {
+    const lbt_chain_bwd_b& Bb = wave < CSq ? p.b1 : p.bs;
+    const int c = (wave % CSq) * 16 + (lane & 15);
+    const int64_t* ps = Bb.sums + (int64_t)(8 * (lane >> 4)) * 4 * Cq + c;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sv[i][0] = ps[(int64_t)i * 4 * Cq + 2 * Cq];
+      sv[i][1] = ps[(int64_t)i * 4 * Cq + 3 * Cq];
+    }
+  }
+  // phase-1 operands: G / q codes and the output quantiser's noise of the low-res groups (region 1:
+  // conv-1's BN over rows q0-1 .. q0+TH/2-1; region 2: the shortcut BN over rows q0 .. q0+TH/2-1)
+  int Gv[kIt], Qv[kIt];
+  float4 Uv[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int g = tid + it * kBThreads;
+    const bool r1 = g < NG1;  // wave-uniform (NG1 % 64 == 0)
+    const int gg = r1 ? g : g - NG1;
+    const int pix = gg / Cq4, hy = pix / Wq, x = pix - hy * Wq;
+    const int y = r1 ? q0 - 1 + hy : q0 + hy;
+    const bool in = (r1 || gg < NGS) && (unsigned)y < (unsigned)Hq;
+    const uint32_t off = in ? (uint32_t)((y * Wq + x) * Cq + cqq) : 0u;
+    const lbt_chain_bwd_b& Bb = r1 ? p.b1 : p.bs;
+    Gv[it] = ld4i8(Bb.G, imgq + off);
+    Qv[it] = ld4i8(Bb.qn_codes, imgq + off);
+    Uv[it] = ld4f(Bb.qo.noise, off);
+  }
+  // phase-2 B operands of this wave's n-tile (NT | 8): the 3x3/2 dgrad image and the 1x1/2 one
+  v4i bf1[kK1], bfs;
+  {
+    const int col = (wave % NT) * 16 + r;
+#pragma unroll
+    for (int kk = 0; kk < kK1; ++kk) {
+      if constexpr (W4)
+        bf1[kk] = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wd1 + ((int64_t)col * (4 * kK1) + kk * 4 + kg) * 8));
+      else
+        bf1[kk] = *reinterpret_cast<const v4i*>(p.wd1 + ((int64_t)col * (4 * kK1) + kk * 4 + kg) * 16);
+    }
+    if constexpr (W4)
+      bfs = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wds + ((int64_t)col * 4 + kg) * 8));
+    else
+      bfs = *reinterpret_cast<const v4i*>(p.wds + ((int64_t)col * 4 + kg) * 16);
+  }
+  float gam[NB][4], bet[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) gam[b][k] = (b == 0 ? A.b1 : A.b2).gb[cq + k];
+    bet[k] = A.b1.gb[C + cq + k];
+  }
+  const QState so1 = qstate(p.b1.qo), sos = qstate(p.bs.qo);
+  QState qrg[2], qng[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    qrg[b] = qstate((b == 0 ? A.b1 : A.b2).qrg);
+    qng[b] = qstate((b == 0 ? A.b1 : A.b2).qng);
+  }
+  const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
+  const float scale1 = ldexpf(1.0f, -(frac_exp(p.b1.qo) + frac_exp(p.qw1)));
+  const float scale2 = ldexpf(1.0f, -(frac_exp(p.bs.qo) + frac_exp(p.qws)));
+
+  // ---------------- pass-B constants of both BNs (chain_bwd_b_kernel's double arithmetic)
+  if (wave < kSW) {
+    long long SGi = 0, SGQi = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      SGi += sv[i][0];
+      SGQi += sv[i][1];
+    }
+    SGi = rows_total64(SGi);
+    SGQi = rows_total64(SGQi);
+    const int bn = wave < CSq ? 0 : 1, c = (wave % CSq) * 16 + (lane & 15);
+    if (lane < 16) {
+      const lbt_chain_bwd_b& Bb = bn == 0 ? p.b1 : p.bs;
+      const double s = (double)qstate(Bb.qn).inv_m, gsc = (double)qstate(Bb.qng).inv_m, nn = (double)Bb.n;
+      const double SG = (double)SGi, SGQ = (double)SGQi;
+      const float m = Bb.ms[c], sig = Bb.ms[Cq + c];
+      const Recip rc = recip(sig);
+      sh.cst[bn][0][c] = m;
+      sh.cst[bn][1][c] = sig;
+      sh.cst[bn][2][c] = rc.rc;
+      sh.cst[bn][3][c] = (float)(gsc * SG / nn);
+      sh.cst[bn][4][c] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
+    }
+  }
+  const QState sn1 = qstate(p.b1.qn), sns = qstate(p.bs.qn), sg1 = qstate(p.b1.qng), sgs = qstate(p.bs.qng);
+  __syncthreads();
+  LBT_TS(1);
+
+  // ---------------- phase 1: both pass-B chains -> LDS gradient-code images
+  int ov1a = 0, ov2a = 0, ov1b = 0, ov2b = 0;
+  int s1a[4] = {0, 0, 0, 0}, s2a[4] = {0, 0, 0, 0}, s1b[4] = {0, 0, 0, 0}, s2b[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    if (it * kBThreads >= NG1 + NGS) break;  // uniform
+    const int g = tid + it * kBThreads;
+    const bool r1 = g < NG1;  // wave-uniform
+    const int gg = r1 ? g : g - NG1;
+    const bool valid = r1 || gg < NGS;
+    const int pix = gg / Cq4, hy = pix / Wq, x = pix - hy * Wq;
+    const int y = r1 ? q0 - 1 + hy : q0 + hy;
+    const bool in = valid && (unsigned)y < (unsigned)Hq;
+    const bool own = in && (!r1 || hy >= 1);
+    const int bn = r1 ? 0 : 1;
+    const QState& so = r1 ? so1 : sos;
+    const QState& sn = r1 ? sn1 : sns;
+    const QState& sgq = r1 ? sg1 : sgs;
+    const float4 mu4 = *reinterpret_cast<const float4*>(&sh.cst[bn][0][cqq]);
+    const float4 sg4 = *reinterpret_cast<const float4*>(&sh.cst[bn][1][cqq]);
+    const float4 rc4 = *reinterpret_cast<const float4*>(&sh.cst[bn][2][cqq]);
+    const float4 mg4 = *reinterpret_cast<const float4*>(&sh.cst[bn][3][cqq]);
+    const float4 mx4 = *reinterpret_cast<const float4*>(&sh.cst[bn][4][cqq]);
+    const f2 mu2[2] = {mk2(mu4.x, mu4.y), mk2(mu4.z, mu4.w)}, sg2[2] = {mk2(sg4.x, sg4.y), mk2(sg4.z, sg4.w)};
+    const f2 rc2[2] = {mk2(rc4.x, rc4.y), mk2(rc4.z, rc4.w)}, mg2[2] = {mk2(mg4.x, mg4.y), mk2(mg4.z, mg4.w)};
+    const f2 mx2[2] = {mk2(mx4.x, mx4.y), mk2(mx4.z, mx4.w)};
+    const float T1 = ov_thr(own, so.L), T2 = ov_thr(own, so.Lh);
+    int G[4], q[4], c[4];
+    unpack4(Gv[it], G);
+    unpack4(Qv[it], q);
+    const f2 u[2] = {mk2(Uv[it].x, Uv[it].y), mk2(Uv[it].z, Uv[it].w)};
+    int o1 = 0, o2 = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f2 x1 = cvt2(q[2 * h], q[2 * h + 1]) * sn.inv_m;
+      const f2 x2 = x1 - mu2[h];
+      const f2 xh = div_by2_nz(x2, sg2[h], rc2[h]);
+      const f2 gh = cvt2(G[2 * h], G[2 * h + 1]) * sgq.inv_m;
+      const f2 t1 = gh - mg2[h];
+      const f2 t2 = xh * mx2[h];
+      const f2 dx = div_by2_nz(t1 - t2, sg2[h], rc2[h]);
+      const f2 xm = dx * so.m;
+      ov_count2(xm, T1, T2, o1, o2);
+      const f2 fl = qfloor2(so, xm, u[h]);
+      c[2 * h] = in ? (int)fl.x : 0;  // outside the image: the conv's zero padding
+      c[2 * h + 1] = in ? (int)fl.y : 0;
+    }
+    const int w = pack4(c);
+    if (r1) {
+      ov1a += o1;
+      ov2a += o2;
+      *reinterpret_cast<int*>(sh.g1 + pix * Cq + cqq) = w;
+      if (own) {
+        *reinterpret_cast<int*>(p.b1.gq + imgq + (uint32_t)((y * Wq + x) * Cq + cqq)) = w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s1a[k] += c[k];
+          s2a[k] += c[k] * c[k];
+        }
+      }
+    } else {
+      ov1b += o1;
+      ov2b += o2;
+      if (valid) *reinterpret_cast<int*>(sh.gs + pix * Cq + cqq) = w;
+      if (own) {
+        *reinterpret_cast<int*>(p.bs.gq + imgq + (uint32_t)((y * Wq + x) * Cq + cqq)) = w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s1b[k] += c[k];
+          s2b[k] += c[k] * c[k];
+        }
+      }
+    }
+  }
+  pin_counts(ov1a, ov2a);
+  pin_counts(ov1b, ov2b);
+  __syncthreads();
+  LBT_TS(2);
+
+  // phase-3 operands, issued now (they land while the MFMAs run)
+  float4 ymv[J], urg[NB][J], ung[NB][J];
+  int Rv[NB][J], qnv[NB][J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pix = (tid + j * kBThreads) / C4;
+    const uint32_t off = (uint32_t)(r0 * W * C + pix * C + cq);
+    if (CF & kAYMask) ymv[j] = ld4f(A.y_mask, img + off);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+      Rv[b][j] = ld4i8(Bb.R, img + off);
+      qnv[b][j] = ld4i8(Bb.qn_codes, img + off);
+      urg[b][j] = ld4f(Bb.qrg.noise, off);
+      ung[b][j] = ld4f(Bb.qng.noise, off);
+    }
+  }
+
+  // ---------------- phase 2: dx = dgrad(3x3/2) + dgrad(1x1/2) from the LDS images
+#pragma unroll
+  for (int pi = 0; pi < TH / 4; ++pi) {
+    const int pr = wave + 8 * pi;
+    const int mt = pr / NT, nt = pr - mt * NT;
+    const int m = mt * 16 + r;
+    const int ly = m / W, px = m - ly * W;
+    v4i acc = v4i{0, 0, 0, 0}, acc2 = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < kK1; ++kk) {
+      const int s = kk * 4 + kg;  // (tap, 16-channel slice of Cq)
+      const int tap = s / CSq, cs = s - tap * CSq;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      // dx row r0 + ly reads gq row (r0 + ly - kh) / 2 = local row (ly - kh) / 2 + 1 when even
+      const bool ok = s < 9 * CSq && ((ly - kh) & 1) == 0 && ((px - kw) & 1) == 0 && px >= kw;
+      const int lr = ((ly - kh) >> 1) + 1, ox = (px - kw) >> 1;
+      v4i a = *reinterpret_cast<const v4i*>(sh.g1 + (ok ? (lr * Wq + ox) * Cq + cs * 16 : 0));
+      if (!ok) a = v4i{0, 0, 0, 0};
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bf1[kk], acc, 0, 0, 0);
+    }
+    {
+      const bool ok = kg < CSq && (ly & 1) == 0 && (px & 1) == 0;
+      v4i a = *reinterpret_cast<const v4i*>(sh.gs + (ok ? ((ly >> 1) * Wq + (px >> 1)) * Cq + kg * 16 : 0));
+      if (!ok) a = v4i{0, 0, 0, 0};
+      acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bfs, acc2, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = (float)acc[i] * scale1, add = (float)acc2[i] * scale2;
+      sh.tile[(mt * 16 + 4 * kg + i) * (C + 4) + nt * 16 + r] = v + add;
+    }
+  }
+  __syncthreads();
+  LBT_TS(3);
+
+  // ---------------- phase 3: pass A over the tile (conv_bwd_kernel's phase 3)
+  int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};
+  int acc3[NB][4][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc3[b][s][k] = 0;
+  f2 gam2a[NB][2], bet2a[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) gam2a[b][h] = mk2(gam[b][2 * h], gam[b][2 * h + 1]);
+    bet2a[h] = mk2(bet[2 * h], bet[2 * h + 1]);
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int pix = (tid + j * kBThreads) / C4;
+    const uint32_t off = (uint32_t)(r0 * W * C + pix * C + cq);
+    const float4 t = *reinterpret_cast<const float4*>(sh.tile + pix * (C + 4) + cq);
+    f2 g[2] = {mk2(t.x, t.y), mk2(t.z, t.w)};
+    int R1[4];
+    unpack4(Rv[0][j], R1);
+    if (CF & kAYMask) {
+      const float ym[4] = {ymv[j].x, ymv[j].y, ymv[j].z, ymv[j].w};
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        g[h] = mk2(ym[2 * h] > 0.f ? g[h].x : 0.f, ym[2 * h + 1] > 0.f ? g[h].y : 0.f);
+    } else if (CF & kAMaskR) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f2 xr = cvt2(R1[2 * h], R1[2 * h + 1]) * r_inv;
+        const f2 m1 = xr * gam2a[0][h];
+        const f2 yv = m1 + bet2a[h];
+        g[h] = mk2(yv.x > 0.f ? g[h].x : 0.f, yv.y > 0.f ? g[h].y : 0.f);
+      }
+    }
+    if (CF & kAGmask) *reinterpret_cast<float4*>(A.gmask_out + img + off) = make_float4(g[0].x, g[0].y, g[1].x, g[1].y);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+      int R[4], qn[4], Gc[4];
+      unpack4(Rv[b][j], R);
+      unpack4(qnv[b][j], qn);
+      const f2 ur[2] = {mk2(urg[b][j].x, urg[b][j].y), mk2(urg[b][j].z, urg[b][j].w)};
+      const f2 un[2] = {mk2(ung[b][j].x, ung[b][j].y), mk2(ung[b][j].z, ung[b][j].w)};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f2 xm = g[h] * qrg[b].m;
+        ov_count2(xm, qrg[b].L, qrg[b].Lh, ov[b][0][0], ov[b][0][1]);
+        const f2 f1 = qfloor2(qrg[b], xm, ur[h]);  // G2 codes
+        const f2 gh = f1 * qrg[b].inv_m;
+        const f2 d = gh * gam2a[b][h];
+        const f2 dm = d * qng[b].m;
+        ov_count2(dm, qng[b].L, qng[b].Lh, ov[b][1][0], ov[b][1][1]);
+        const f2 f2c = qfloor2(qng[b], dm, un[h]);  // Gc codes
+        const int G2[2] = {(int)f1.x, (int)f1.y};
+        Gc[2 * h] = (int)f2c.x;
+        Gc[2 * h + 1] = (int)f2c.y;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int k = 2 * h + i;
+          acc3[b][0][k] += G2[i] * R[k];
+          acc3[b][1][k] += G2[i];
+          acc3[b][2][k] += Gc[k];
+          acc3[b][3][k] += Gc[k] * qn[k];
+        }
+      }
+      *reinterpret_cast<int*>(Bb.gout + img + off) = pack4(Gc);
+    }
+  }
+
+  // ---------------- channel sums and counters (conv_bwd_kernel's publish, plus a second gq sum set)
+  {
+    const bool own = (lane & 15) < C4;
+    int* part = sh.part[wave] + cq + (lane >> 4);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int t = chan_scatter4(acc3[b][s], C4);
+        if (own) part[(b * 4 + s) * C] = t;
+      }
+    const bool ownq = (lane & 15) < Cq4;
+    int* pq = sh.part[wave] + NB * 4 * C + cqq + (lane >> 4);
+    const int t1 = chan_scatter4(s1a, Cq4), t2 = chan_scatter4(s2a, Cq4);
+    const int t3 = chan_scatter4(s1b, Cq4), t4 = chan_scatter4(s2b, Cq4);
+    if (ownq) {
+      pq[0] = t1;
+      pq[Cq] = t2;
+      pq[2 * Cq] = t3;
+      pq[3 * Cq] = t4;
+    }
+  }
+  constexpr int NQ = 2 + 2 * NB;  // [qo1 | qos | qrg, qng of branch 1 | of branch 2]
+  ov_stage4(0, NQ, ov_pack(ov1a, ov2a), ov_pack(ov1b, ov2b), ov_pack(ov[0][0][0], ov[0][0][1]),
+            ov_pack(ov[0][1][0], ov[0][1][1]), sh.cnt);
+  if constexpr (NB == 2) {
+    ov_wave(ov[1][0][0], ov[1][0][1]);
+    counts_stage_w(4, NQ, ov[1][0][0], ov[1][0][1], sh.cnt);
+    ov_wave(ov[1][1][0], ov[1][1][1]);
+    counts_stage_w(5, NQ, ov[1][1][0], ov[1][1][1], sh.cnt);
+  }
+  __syncthreads();
+  LBT_TS(4);
+  counts_publish_nw<kBNW>(0, NQ, p.b1.qo, sh.cnt);
+  counts_publish_nw<kBNW>(1, NQ, p.bs.qo, sh.cnt);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+    counts_publish_nw<kBNW>(2 + 2 * b, NQ, Bb.qrg, sh.cnt);
+    counts_publish_nw<kBNW>(3 + 2 * b, NQ, Bb.qng, sh.cnt);
+  }
+  // slot i of [NB*4C pass-A sums | 2Cq conv-1 gq sums | 2Cq shortcut gq sums]
+  const int shard = shard_id();
+  for (int i = tid; i < NB * 4 * C + 4 * Cq; i += kBThreads) {
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kBNW; ++w) t += sh.part[w][i];
+    if (!t) continue;
+    int64_t* dst;
+    if (i < NB * 4 * C) {
+      const int b = i / (4 * C);
+      dst = (b == 0 ? A.b1 : A.b2).sums + (int64_t)shard * 4 * C + (i - b * 4 * C);
+    } else {
+      const int k = i - NB * 4 * C;
+      const lbt_chain_bwd_b& Bb = k < 2 * Cq ? p.b1 : p.bs;
+      if (!Bb.gcolsum) continue;
+      dst = Bb.gcolsum + (int64_t)shard * 2 * Cq + (k < 2 * Cq ? k : k - 2 * Cq);
+    }
+    LBT_GADD((unsigned long long*)dst, (unsigned long long)t);
+  }
+  LBT_TS(5);
+}
+
+}  // namespace
+
+extern "C" int lbt_conv_bwd2_fused_i8(const lbt_conv_bwd2* q, void* stream) {
+  if (!q) return LBT_EINVAL;
+  const lbt_conv_desc &d1 = q->d1, &ds = q->ds;
+  const int C = d1.Cin, Cq = d1.Cout;
+  // the projection block's 3x3/2 SAME conv (pads: top / left 0, bottom / right 1) and 1x1/2 shortcut
+  if (!desc_ok(d1) || !desc_ok(ds) || d1.KH != 3 || d1.KW != 3 || d1.SH != 2 || d1.SW != 2 || d1.PT != 0 ||
+      d1.PL != 0 || ds.KH != 1 || ds.KW != 1 || ds.SH != 2 || ds.SW != 2 || ds.PT != 0 || ds.PL != 0 ||
+      (C != 16 && C != 32) || Cq != 2 * C || d1.W * C != 512 || d1.H % 2 || d1.W % 2 || d1.Ho * 2 != d1.H ||
+      d1.Wo * 2 != d1.W || d1.H % tile_rows(C / 16) || ds.N != d1.N || ds.H != d1.H || ds.W != d1.W || ds.Cin != C ||
+      ds.Cout != Cq || ds.Ho != d1.Ho || ds.Wo != d1.Wo)
+    return LBT_EINVAL;
+  const int CS = C / 16;
+  const int64_t inq = (int64_t)d1.Ho * d1.Wo * Cq;
+  const lbt_chain_bwd_b* bb[2] = {&q->b1, &q->bs};
+  for (int i = 0; i < 2; ++i) {
+    const lbt_chain_bwd_b& b = *bb[i];
+    if (!b.G || !b.qn_codes || !b.ms || !b.sums || !b.gq || b.dx || !noise_ok(b.qo) || b.C != Cq || b.rows != d1.N ||
+        b.inner != inq)
+      return LBT_EINVAL;
+  }
+  const lbt_chain_bwd_a& a = q->a;
+  if (a.C != C || a.rows != d1.N || a.inner != (int64_t)d1.H * d1.W * C) return LBT_EINVAL;
+  const int f = bwd_a_flags(a);
+  if ((f & kAFused) != kAFused) return LBT_EINVAL;
+  for (int br = 0; br < (a.has_b2 ? 2 : 1); ++br) {
+    const lbt_bwd_branch& Bb = br ? a.b2 : a.b1;
+    if (!noise_ok(Bb.qrg) || !noise_ok(Bb.qng) || !Bb.gb) return LBT_EINVAL;
+  }
+  if (q->ksd1 != 4 * ((9 * 2 * CS + 3) / 4) || q->ksds != 4 || !q->wd1 || !q->wds) return LBT_EINVAL;
+  if (q->w4 && (q->qw1.bits > 4 || q->qws.bits > 4)) return LBT_EINVAL;
+  ConvBwd2Args p;
+  p.b1 = q->b1; p.bs = q->bs; p.wd1 = q->wd1; p.wds = q->wds; p.qw1 = q->qw1; p.qws = q->qws; p.H = d1.H; p.a = a;
+  const int64_t tiles = (int64_t)d1.N * (d1.H / tile_rows(CS));
+  if (tiles > 0x7fffffff || (int64_t)d1.N * d1.H * d1.W * C >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = a.has_b2 ? 2 : 1;
+#define LBT_B2(CS_, CF_, NB_)                                                                              \
+  if (CS == CS_ && f == (CF_) && nb == NB_) {                                                              \
+    if (q->w4)                                                                                             \
+      hipLaunchKernelGGL((conv_bwd2_kernel<CS_, CF_, NB_, true>), dim3((unsigned)tiles), dim3(kBThreads), 0, st, p); \
+    else                                                                                                   \
+      hipLaunchKernelGGL((conv_bwd2_kernel<CS_, CF_, NB_, false>), dim3((unsigned)tiles), dim3(kBThreads), 0, st, p); \
+    return (int)hipGetLastError();                                                                         \
+  }
+  // the consumer is an identity block's end chain (mask from y, masked gradient stored) or the
+  // stem's (y mask only)
+  LBT_B2(1, kAFused | kAYMask | kAGmask, 1)
+  LBT_B2(2, kAFused | kAYMask | kAGmask, 1)
+  LBT_B2(1, kAFused | kAYMask, 1)
+  LBT_B2(2, kAFused | kAYMask, 1)
+#undef LBT_B2
+  return LBT_EINVAL;
+}
+
 // ============================================================================ fused conv forward
 // lbt_conv_fwd_fused_i8: the BN element chain that produces a stride-1 3x3 conv's input (bn.hip
 // chain_fwd_kernel's arithmetic) runs as the conv's operand staging. A workgroup owns TH image

@@ -917,17 +917,21 @@ class FusedResNet:
         aB1 = self._chain_bwd_b(b.n1, Gn1, f["qn1"], sums1, shp, C, gq1, c1.grad_range, gcol1)
         if self.sync_bn:
             bwd.append(self._allreduce(sums1))
+        # conv-1's and the shortcut's dgrads (+ the consumer's pass A) as ONE launch
+        dual = (self.pair_launch and cs is not None and not fb1 and fuse and not (self.fuse_wgrad and not self.batch_wgrad)
+                and (Cin, C) in ((16, 32), (32, 64)) and getattr(c1, "w4", False) == getattr(cs, "w4", False))
+        # ... and with both pass-B chains in the same launch (lbt_conv_bwd2_fused_i8): the whole transition
+        bwd2 = (bpair and dual and os.environ.get("LBT_FUSE_BWD2", "1") == "1" and Cin * f["Xin"].shape[2] == 512
+                and f["Xin"].shape[1] % (8 if Cin == 16 else 4) == 0 and (d1.PT, d1.PL, ds.PT, ds.PL) == (0, 0, 0, 0))
         if bpair:
-            bwd.append(L("lbt_bn_chain_bwd_b_pair", ctypes.byref(aBs), ctypes.byref(aB1), k="chain_bwd_b2_kernel",
-                         nb=ops._chain_bwd_b_bytes(aBs) + ops._chain_bwd_b_bytes(aB1)))
+            if not bwd2:  # (else both pass-B chains run inside the transition launch below)
+                bwd.append(L("lbt_bn_chain_bwd_b_pair", ctypes.byref(aBs), ctypes.byref(aB1), k="chain_bwd_b2_kernel",
+                             nb=ops._chain_bwd_b_bytes(aBs) + ops._chain_bwd_b_bytes(aB1)))
         elif not fb1:  # (a pending wgrad stays pending: the next fused launch carries it)
             bwd.append(L("lbt_bn_chain_bwd_b", ctypes.byref(aB1), k="chain_bwd_b_kernel",
                          nb=ops._chain_bwd_b_bytes(aB1)))
         keep.append(aB1)
         add = gm
-        # conv-1's and the shortcut's dgrads (+ the consumer's pass A) as ONE launch
-        dual = (self.pair_launch and cs is not None and not fb1 and fuse and not (self.fuse_wgrad and not self.batch_wgrad)
-                and (Cin, C) in ((16, 32), (32, 64)) and getattr(c1, "w4", False) == getattr(cs, "w4", False))
         if cs is not None and not dual:
             dsg = self._buf(k + "dsc", f["Xin"].shape, torch.float32)
             bwd.append(L(self._fn(cs, "lbt_conv_dgrad_i8"), ptr(gqs), self._wd(cs), cs.ksd, ds, self._qd(cs.grad_range),
@@ -949,6 +953,17 @@ class FusedResNet:
                              self._qd(c1.grad_range), c1.W_range.desc, ptr(add), ctypes.byref(consumer["a"]),
                              ptr(f["xa"]), 1, ptr(slab1), sp1, ns1, k="dgrad_wgrad_kernel",
                              nb=nb + nb_wg1 - gq1.numel()))
+            elif bwd2:
+                cb2 = _lib.ConvBwd2()
+                cb2.b1, cb2.bs = aB1, aBs
+                cb2.wd1, cb2.ksd1, cb2.wds, cb2.ksds = self._wd(c1).value, c1.ksd, self._wd(cs).value, cs.ksd
+                cb2.w4 = 1 if getattr(c1, "w4", False) else 0
+                cb2.d1, cb2.ds, cb2.qw1, cb2.qws = d1, ds, c1.W_range.desc, cs.W_range.desc
+                cb2.a = consumer["a"]
+                self._keep.append(cb2)
+                nb = (ops._chain_bwd_b_bytes(aBs) + ops._chain_bwd_b_bytes(aB1) + 4 * (aBs.inner + aB1.inner)
+                      + ops._dgrad_chain_bytes(0, c1.wd.numel(), consumer["a"], False) + cs.wd.numel())
+                bwd.append(L("lbt_conv_bwd2_fused_i8", ctypes.byref(cb2), k="conv_bwd2_kernel", nb=nb))
             elif dual:
                 nb = (ops._dgrad_chain_bytes(gq1.numel(), c1.wd.numel(), consumer["a"], False)
                       + gqs.numel() + cs.wd.numel())
