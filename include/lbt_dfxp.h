@@ -779,6 +779,25 @@ int lbt_softmax_xent_n(const float* z, const int32_t* labels, int32_t N, int32_t
 int lbt_softmax_xent_wide_n(const float* z, const int32_t* labels, int32_t N, int32_t K, int32_t norm, float* loss,
                             float* dz, int64_t* loss_fx, void* stream);
 
+/* A stage transition's forward in ONE launch (the last identity block's end chain, ResidualBlock_q
+ * :858-863 with BatchNorm_q :584-616,677-683, feeding a projection block's 3x3/2 conv and 1x1/2
+ * shortcut :772-795 / :831-846): the chain c (exactly lbt_bn_chain_fwd; NB 1, residual, y stored,
+ * o1 = the 3x3/2 conv's input codes and o2 = the shortcut's, both LBT_OUT_U8OFF and stored) evaluated
+ * into LDS, both convs from there (as lbt_conv_fwd_pair_i8: wf1 / wfs, their wcolsum offset
+ * corrections), and each conv's quantising epilogue (yq1 / qout1 / ychsum1, yqs / qouts / ychsums).
+ * Bit-identical to lbt_bn_chain_fwd followed by lbt_conv_fwd_pair_i8. Shapes: d1 3x3 stride 2 SAME
+ * (pads 0 / 1), ds 1x1 stride 2, Cin = C in {16, 32}, Cout = 2C, W * C = 512, Ho % 4 == 0. */
+typedef struct lbt_conv_fwd2 {
+  lbt_chain_fwd c;
+  const int8_t* wf1; int32_t ksf1; const int32_t* wcolsum1;
+  const int8_t* wfs; int32_t ksfs; const int32_t* wcolsums;
+  int32_t w4;
+  lbt_conv_desc d1, ds; lbt_qdesc qw1, qws;
+  int8_t* yq1; lbt_qdesc qout1; int64_t* ychsum1;
+  int8_t* yqs; lbt_qdesc qouts; int64_t* ychsums;
+} lbt_conv_fwd2;
+int lbt_conv_fwd2_fused_i8(const lbt_conv_fwd2* p, void* stream);
+
 /* ABI version for the Python loader. */
 int lbt_abi_version(void);
 

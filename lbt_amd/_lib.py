@@ -97,6 +97,13 @@ class ConvFwd(ctypes.Structure):
                 ("d", ConvDesc), ("qw", QDesc), ("yq", c_void_p), ("qout", QDesc), ("ychsum", c_void_p)]
 
 
+class ConvFwd2(ctypes.Structure):
+    _fields_ = [("c", ChainFwd), ("wf1", c_void_p), ("ksf1", c_int32), ("wcolsum1", c_void_p), ("wfs", c_void_p),
+                ("ksfs", c_int32), ("wcolsums", c_void_p), ("w4", c_int32), ("d1", ConvDesc), ("ds", ConvDesc),
+                ("qw1", QDesc), ("qws", QDesc), ("yq1", c_void_p), ("qout1", QDesc), ("ychsum1", c_void_p),
+                ("yqs", c_void_p), ("qouts", QDesc), ("ychsums", c_void_p)]
+
+
 class ConvFwdJob(ctypes.Structure):
     _fields_ = [("xq", c_void_p), ("x_u8off", c_int32), ("w4", c_int32), ("wf", c_void_p), ("ksf", c_int32),
                 ("wcolsum", c_void_p), ("d", ConvDesc), ("qx", QDesc), ("qw", QDesc), ("y", c_void_p),
@@ -191,6 +198,7 @@ _SIGS = {
     "lbt_conv_stem_wgrad": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_stem_bwd": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_bwd2_fused_i8": [_P, _P],
+    "lbt_conv_fwd2_fused_i8": [_P, _P],
     "lbt_conv_wgrad_reduce_x": [_P, c_int32, c_int32, c_int32, c_int32, _P, _P, _P],
     "lbt_conv_wgrad_reduce64_x": [_P, c_int32, c_int32, c_int32, _P, _P],
     "lbt_dense_wgrad_x": [_P, _P, c_int32, c_int32, c_int32, c_int32, _P, _P],

@@ -2499,6 +2499,320 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   LBT_TS(5);
 }
 
+// ---- lbt_conv_fwd2_fused_i8: a stage transition's forward in ONE launch -- the last identity block's
+// end chain (bn2 + residual + ReLU, its R codes and fp32 y, and BOTH of the projection block's input
+// quantisers: the 3x3/2 conv's and the 1x1/2 shortcut's) evaluated into LDS code images, the two
+// strided convs from LDS, and both BNs' input quantisers + channel sums over the two conv tiles.
+// Bit-identical to lbt_bn_chain_fwd + lbt_conv_fwd_pair_i8. A workgroup owns TH2 output rows, i.e.
+// input rows 2 oy0 .. 2 oy0 + 2 TH2 - 1 (+ the row below: the 3x3/2 SAME padding is bottom / right).
+constexpr int kTH2 = 4;  // output rows per workgroup (2 x 4 m-tiles: one (m, n) pair per wave)
+
+struct ConvFwd2Args {
+  lbt_chain_fwd c;
+  const int8_t* wf1;
+  const int8_t* wfs;
+  const int32_t* wcolsum1;
+  const int32_t* wcolsums;
+  lbt_qdesc qw1, qws;
+  int H;  // input rows
+  int8_t* yq1;
+  int8_t* yqs;
+  lbt_qdesc qout1, qouts;
+  int64_t* ychsum1;
+  int64_t* ychsums;
+};
+
+template <int C>
+struct Fwd2Shared {
+  int8_t xa[(2 * kTH2 + 1) * 512];          // the 3x3/2 conv's input codes (q - 128), rows 2oy0 .. 2oy0+2TH2
+  int8_t xs[kTH2 * 256];                     // the shortcut's, even rows / columns only ([TH2][W/2][C])
+  float tile[2][kTH2 * (256 / C) * (2 * C + 4)];  // the two conv outputs [pixel][Cq + 4]
+  float cst[2][C];                           // bn2: mu, sigma
+  int part[kBNW][2 * 2 * 2 * C];             // per wave: S1, S2 of both output code sets (2Cq each)
+  int cnt[kBNW * 2 * 5];                     // counters: qr, qo1, qo2, qout1, qouts
+};
+
+template <int CS, bool W4>
+__global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(ConvFwd2Args p) {
+  constexpr int C = CS * 16, C4 = C / 4, W = 512 / C, Cq = 2 * C, Cq4 = Cq / 4, Wq = W / 2, NTq = Cq / 16;
+  constexpr int kK1 = (9 * CS + 3) / 4;
+  constexpr int NG = (2 * kTH2 + 1) * W * C4;  // chain groups (rows 2oy0 .. 2oy0 + 2TH2)
+  constexpr int kIt = (NG + kBThreads - 1) / kBThreads;
+  static_assert(kTH2 * Wq * Cq == 2 * 1024 && C / 16 <= kBNW, "layout");
+  __shared__ __attribute__((aligned(16))) Fwd2Shared<C> sh;
+  LBT_TS(0);
+  const lbt_chain_fwd& a = p.c;
+  const int H = p.H, Hq = H / 2;
+  const uint32_t bid = blockIdx.x;
+  const int tpi = Hq / kTH2;
+  const int n = (int)(bid / (uint32_t)tpi), oy0 = (int)(bid - (uint32_t)n * tpi) * kTH2, y0 = 2 * oy0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int cq = (tid % C4) * 4, cqq = (tid % Cq4) * 4;
+  const int64_t img = (int64_t)n * H * W * C, imgq = (int64_t)n * Hq * Wq * Cq;
+
+  // ---------------- bn2's moment shard sums first (waves w < C / 16), then every other load
+  constexpr int kSW = C / 16;
+  long long sv[8][2];
+  if (wave < kSW) {
+    const int c = wave * 16 + (lane & 15);
+    const int64_t* cs = a.b1.nrm.chsum + (int64_t)(8 * (lane >> 4)) * 2 * C + c;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sv[i][0] = cs[(int64_t)i * 2 * C];
+      sv[i][1] = cs[(int64_t)i * 2 * C + C];
+    }
+  }
+  int qv[kIt];
+  float4 rv[kIt], nrv[kIt], no1[kIt], no2[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int g = tid + it * kBThreads;
+    const int pix = g / C4, hy = pix / W, x = pix - hy * W;
+    const int y = y0 + hy;
+    const bool in = g < NG && y < H;
+    const uint32_t off = in ? (uint32_t)((y * W + x) * C + cq) : 0u;
+    qv[it] = ld4i8(a.b1.nrm.q, img + off);
+    nrv[it] = ld4f(a.b1.qr.noise, off);
+    rv[it] = ld4f(a.res, img + off);
+    no1[it] = ld4f(a.qo1.noise, off);
+    no2[it] = ld4f(a.qo2.noise, off);
+  }
+  // the two convs' B operands (forward weight images) of this wave's n-tile; one (m, n) pair per wave
+  const int mt = wave / NTq, nt = wave - mt * NTq;
+  const int bcol = nt * 16 + r;
+  v4i bf1[kK1], bfs;
+#pragma unroll
+  for (int kk = 0; kk < kK1; ++kk) {
+    if constexpr (W4)
+      bf1[kk] = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wf1 + ((int64_t)bcol * (4 * kK1) + kk * 4 + kg) * 8));
+    else
+      bf1[kk] = *reinterpret_cast<const v4i*>(p.wf1 + ((int64_t)bcol * (4 * kK1) + kk * 4 + kg) * 16);
+  }
+  if constexpr (W4)
+    bfs = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wfs + ((int64_t)bcol * 4 + kg) * 8));
+  else
+    bfs = *reinterpret_cast<const v4i*>(p.wfs + ((int64_t)bcol * 4 + kg) * 16);
+  const int corr1 = 128 * p.wcolsum1[bcol], corr2 = 128 * p.wcolsums[bcol];
+  float gam[4], bet[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    gam[k] = a.b1.gb[cq + k];
+    bet[k] = a.b1.gb[C + cq + k];
+  }
+  const QState qr = qstate(a.b1.qr), so1 = qstate(a.qo1), so2 = qstate(a.qo2);
+  const QState sq1 = qstate(p.qout1), sqs = qstate(p.qouts);
+  const float sn = qscale(a.b1.nrm.qn);
+  const float scale1 = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw1)));
+  const float scale2 = ldexpf(1.0f, -(frac_exp(a.qo2) + frac_exp(p.qws)));
+
+  // ---------------- Normalization_q moments (conv_fwd_fused_kernel's arithmetic)
+  if (wave < kSW) {
+    long long S1 = 0, S2 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      S1 += sv[i][0];
+      S2 += sv[i][1];
+    }
+    S1 = rows_total64(S1);
+    S2 = rows_total64(S2);
+    const int c = wave * 16 + (lane & 15);
+    if (lane < 16) {
+      const lbt_bn_norm& nb = a.b1.nrm;
+      const double s = ldexp(1.0, -frac_exp(nb.qn));
+      const double mean_d = (double)S1 * s / (double)nb.n;
+      const double var_d = (double)S2 * (s * s) / (double)nb.n - mean_d * mean_d;
+      const float m = (float)mean_d, vv = (float)var_d;
+      const float sigma = sqrtf(vv + nb.eps);
+      sh.cst[0][c] = m;
+      sh.cst[1][c] = sigma;
+      if (bid == 0) {  // one writer: ms for the backward, the running averages (:601-612)
+        if (nb.ms) { nb.ms[c] = m; nb.ms[C + c] = sigma; }
+        if (nb.run_mean) {
+          nb.run_mean[c] = nb.momentum * nb.run_mean[c] + nb.one_minus_momentum * m;
+          nb.run_var[c] = nb.momentum * nb.run_var[c] + nb.one_minus_momentum * vv;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  LBT_TS(1);
+  f2 pm2[2], psy2[2], psr2[2], gam2[2], bet2[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const Recip r0 = recip(sh.cst[1][cq + 2 * h]), r1 = recip(sh.cst[1][cq + 2 * h + 1]);
+    pm2[h] = mk2(sh.cst[0][cq + 2 * h], sh.cst[0][cq + 2 * h + 1]);
+    psy2[h] = mk2(r0.y, r1.y);
+    psr2[h] = mk2(r0.rc, r1.rc);
+    gam2[h] = mk2(gam[2 * h], gam[2 * h + 1]);
+    bet2[h] = mk2(bet[2 * h], bet[2 * h + 1]);
+  }
+
+  // ---------------- phase 1: the chain over the input rows -> the two LDS code images
+  int ovr1 = 0, ovr2 = 0, ovx1 = 0, ovx2 = 0, ovs1 = 0, ovs2 = 0;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    if (it * kBThreads >= NG) break;  // uniform
+    const int g = tid + it * kBThreads;
+    const int pix = g / C4, hy = pix / W, x = pix - hy * W;
+    const int y = y0 + hy;
+    const bool valid = g < NG;
+    const bool in = valid && y < H;
+    const bool own = in && hy < 2 * kTH2;
+    const uint32_t e = (uint32_t)((y * W + x) * C + cq);
+    int q[4];
+    unpack4(qv[it], q);
+    const f2 u[2] = {mk2(nrv[it].x, nrv[it].y), mk2(nrv[it].z, nrv[it].w)};
+    const float T1 = ov_thr(own, qr.L), T2 = ov_thr(own, qr.Lh);
+    f2 fl[2], v[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f2 x1 = cvt2(q[2 * h], q[2 * h + 1]) * sn;
+      const f2 x2 = x1 - pm2[h];
+      const f2 t = div_by2_nz(x2, psy2[h], psr2[h]);
+      const f2 xm = t * qr.m;
+      ov_count2(xm, T1, T2, ovr1, ovr2);
+      fl[h] = qfloor2(qr, xm, u[h]);  // the R codes
+      const f2 xr = fl[h] * qr.inv_m;
+      const f2 m1 = xr * gam2[h];
+      v[h] = m1 + bet2[h];
+    }
+    if (own) *reinterpret_cast<int*>(a.b1.rout + img + e) = pack4f(fl[0], fl[1]);
+    v[0] = v[0] + mk2(rv[it].x, rv[it].y);
+    v[1] = v[1] + mk2(rv[it].z, rv[it].w);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) v[h] = mk2(v[h].x > 0.f ? v[h].x : 0.f, v[h].y > 0.f ? v[h].y : 0.f);
+    if (own) *reinterpret_cast<float4*>(a.y + img + e) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+    const f2 u1[2] = {mk2(no1[it].x, no1[it].y), mk2(no1[it].z, no1[it].w)};
+    const f2 u2[2] = {mk2(no2[it].x, no2[it].y), mk2(no2[it].z, no2[it].w)};
+    const float X1 = ov_thr(own, so1.L), X2 = ov_thr(own, so1.Lh);
+    const float Z1 = ov_thr(own, so2.L), Z2 = ov_thr(own, so2.Lh);
+    f2 c1[2], c2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // v >= 0 after the ReLU: only the upper clip can act, the codes are >= 0
+      const f2 xm = v[h] * so1.m;
+      ov_count2_pos(xm, X1, X2, ovx1, ovx2);
+      const f2 w1 = xm + u1[h];
+      c1[h] = mk2(floorf(fminf(w1.x, so1.Lm1)), floorf(fminf(w1.y, so1.Lm1)));
+      const f2 zm = v[h] * so2.m;
+      ov_count2_pos(zm, Z1, Z2, ovs1, ovs2);
+      const f2 w2 = zm + u2[h];
+      c2[h] = mk2(floorf(fminf(w2.x, so2.Lm1)), floorf(fminf(w2.y, so2.Lm1)));
+    }
+    // LBT_OUT_U8OFF (code ^ 0x80); below the image: the code of 0
+    const int cw1 = in ? (pack4f(c1[0], c1[1]) ^ (int)0x80808080) : (int)0x80808080;
+    const int cw2 = in ? (pack4f(c2[0], c2[1]) ^ (int)0x80808080) : (int)0x80808080;
+    if (valid) *reinterpret_cast<int*>(sh.xa + pix * C + cq) = cw1;
+    if (own && !(hy & 1) && !(x & 1)) *reinterpret_cast<int*>(sh.xs + ((hy >> 1) * Wq + (x >> 1)) * C + cq) = cw2;
+    if (own) {
+      *reinterpret_cast<int*>((int8_t*)a.o1 + img + e) = cw1;
+      *reinterpret_cast<int*>((int8_t*)a.o2 + img + e) = cw2;
+    }
+  }
+  pin_counts(ovr1, ovr2);
+  pin_counts(ovx1, ovx2);
+  pin_counts(ovs1, ovs2);
+  __syncthreads();
+  LBT_TS(2);
+  // phase-3 noise of both output quantisers (one quad of each tile per thread: TH2*Wq*Cq/4 == 512)
+  const uint32_t off3 = (uint32_t)(oy0 * Wq * Cq + (tid / Cq4) * Cq + cqq);
+  const float4 un1 = ld4f(p.qout1.noise, off3), uns = ld4f(p.qouts.noise, off3);
+
+  // ---------------- phase 2: both strided convs from LDS (output pixel (ly, px) reads input
+  // (2 ly + kh, 2 px + kw); column W is the SAME padding: the code of 0)
+  {
+    const int m = mt * 16 + r;
+    const int ly = m / Wq, px = m - ly * Wq;
+    v4i acc = v4i{0, 0, 0, 0}, acc2 = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < kK1; ++kk) {
+      const int s = kk * 4 + kg;
+      const int tap = s / CS, cs = s - tap * CS;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const int ix = 2 * px + kw;
+      const bool okx = ix < W;
+      v4i av = *reinterpret_cast<const v4i*>(sh.xa + (((2 * ly + kh) * W + (okx ? ix : 0)) * C + cs * 16));
+      if (!okx) av = v4i{(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+      if (s >= 9 * CS) av = v4i{0, 0, 0, 0};  // k padding (its weights are zero too)
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bf1[kk], acc, 0, 0, 0);
+    }
+    {
+      v4i av = *reinterpret_cast<const v4i*>(sh.xs + ((ly * Wq + px) * C + (kg < CS ? kg : 0) * 16));
+      if (kg >= CS) av = v4i{0, 0, 0, 0};
+      acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bfs, acc2, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (mt * 16 + 4 * kg + i) * (Cq + 4) + nt * 16 + r;
+      sh.tile[0][row] = (float)(acc[i] + corr1) * scale1;
+      sh.tile[1][row] = (float)(acc2[i] + corr2) * scale2;
+    }
+  }
+  __syncthreads();
+  LBT_TS(3);
+
+  // ---------------- phase 3: both BNs' input quantisers + channel sums
+  int ovq[2][2] = {{0, 0}, {0, 0}};
+  int s1[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  {
+    const int pix3 = tid / Cq4;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const QState& sq = b ? sqs : sq1;
+      const float4 un = b ? uns : un1;
+      const float4 t = *reinterpret_cast<const float4*>(sh.tile[b] + pix3 * (Cq + 4) + cqq);
+      const f2 tv[2] = {mk2(t.x, t.y), mk2(t.z, t.w)};
+      const f2 u[2] = {mk2(un.x, un.y), mk2(un.z, un.w)};
+      f2 fl[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f2 xm = tv[h] * sq.m;
+        ov_count2(xm, sq.L, sq.Lh, ovq[b][0], ovq[b][1]);
+        fl[h] = qfloor2(sq, xm, u[h]);
+      }
+      const int c[4] = {(int)fl[0].x, (int)fl[0].y, (int)fl[1].x, (int)fl[1].y};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s1[b][k] += c[k];
+        s2[b][k] += c[k] * c[k];
+      }
+      *reinterpret_cast<int*>((b ? p.yqs : p.yq1) + imgq + off3) = pack4(c);
+    }
+  }
+  {
+    const bool ownq = (lane & 15) < Cq4;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int t1 = chan_scatter4(s1[b], Cq4), t2 = chan_scatter4(s2[b], Cq4);
+      if (ownq) {
+        sh.part[wave][b * 2 * Cq + cqq + (lane >> 4)] = t1;
+        sh.part[wave][b * 2 * Cq + Cq + cqq + (lane >> 4)] = t2;
+      }
+    }
+  }
+  // slots [qr | qo1 | qo2 | qout1 | qouts]
+  ov_stage4(0, 5, ov_pack(ovr1, ovr2), ov_pack(ovx1, ovx2), ov_pack(ovs1, ovs2), ov_pack(ovq[0][0], ovq[0][1]),
+            sh.cnt);
+  ov_wave(ovq[1][0], ovq[1][1]);
+  counts_stage_w(4, 5, ovq[1][0], ovq[1][1], sh.cnt);
+  __syncthreads();
+  LBT_TS(4);
+  counts_publish_nw<kBNW>(0, 5, a.b1.qr, sh.cnt);
+  counts_publish_nw<kBNW>(1, 5, a.qo1, sh.cnt);
+  counts_publish_nw<kBNW>(2, 5, a.qo2, sh.cnt);
+  counts_publish_nw<kBNW>(3, 5, p.qout1, sh.cnt);
+  counts_publish_nw<kBNW>(4, 5, p.qouts, sh.cnt);
+  if (tid < 4 * Cq) {
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kBNW; ++w) t += sh.part[w][tid];
+    int64_t* dst = tid < 2 * Cq ? p.ychsum1 : p.ychsums;
+    if (t && dst) LBT_GADD((unsigned long long*)&dst[(int64_t)shard_id() * 2 * Cq + (tid % (2 * Cq))], (unsigned long long)t);
+  }
+  LBT_TS(5);
+}
+
 }  // namespace
 
 extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
@@ -2553,5 +2867,51 @@ extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
   LBT_FW_CS(4)
 #undef LBT_FW_CS
 #undef LBT_FW
+  return LBT_EINVAL;
+}
+
+extern "C" int lbt_conv_fwd2_fused_i8(const lbt_conv_fwd2* q, void* stream) {
+  if (!q) return LBT_EINVAL;
+  const lbt_conv_desc &d1 = q->d1, &ds = q->ds;
+  const int C = d1.Cin, Cq = d1.Cout;
+  if (!desc_ok(d1) || !desc_ok(ds) || d1.KH != 3 || d1.KW != 3 || d1.SH != 2 || d1.SW != 2 || d1.PT != 0 ||
+      d1.PL != 0 || ds.KH != 1 || ds.KW != 1 || ds.SH != 2 || ds.SW != 2 || ds.PT != 0 || ds.PL != 0 ||
+      (C != 16 && C != 32) || Cq != 2 * C || d1.W * C != 512 || d1.H % 2 || d1.W % 2 || d1.Ho * 2 != d1.H ||
+      d1.Wo * 2 != d1.W || d1.Ho % kTH2 || ds.N != d1.N || ds.H != d1.H || ds.W != d1.W || ds.Cin != C ||
+      ds.Cout != Cq || ds.Ho != d1.Ho || ds.Wo != d1.Wo)
+    return LBT_EINVAL;
+  const int CS = C / 16;
+  const lbt_chain_fwd& a = q->c;
+  if (a.C != C || a.rows != d1.N || a.inner != (int64_t)d1.H * d1.W * C || a.has_b2 || !a.o1 || !a.o2 ||
+      a.o1_kind != LBT_OUT_U8OFF || a.o2_kind != LBT_OUT_U8OFF || !a.res || !a.y)
+    return LBT_EINVAL;
+  const int f = fwd_flags(a);
+  constexpr int kNeed = kFQ | kFRout | kFRelu | kFO1 | kFO2 | kFStoch | kFU8 | kFRes | kFY;
+  if (f != kNeed) return LBT_EINVAL;
+  if (!noise_ok(a.qo1) || !noise_ok(a.qo2) || !noise_ok(a.b1.qr) || !a.b1.gb || !a.b1.nrm.chsum || a.b1.nrm.frozen)
+    return LBT_EINVAL;
+  if (!q->yq1 || !q->yqs || !noise_ok(q->qout1) || !noise_ok(q->qouts) || !q->wcolsum1 || !q->wcolsums || !q->wf1 ||
+      !q->wfs)
+    return LBT_EINVAL;
+  if (q->ksf1 != 4 * ((9 * CS + 3) / 4) || q->ksfs != 4) return LBT_EINVAL;
+  if (q->w4 && (q->qw1.bits > 4 || q->qws.bits > 4)) return LBT_EINVAL;
+  ConvFwd2Args p;
+  p.c = a; p.wf1 = q->wf1; p.wfs = q->wfs; p.wcolsum1 = q->wcolsum1; p.wcolsums = q->wcolsums;
+  p.qw1 = q->qw1; p.qws = q->qws; p.H = d1.H; p.yq1 = q->yq1; p.yqs = q->yqs; p.qout1 = q->qout1;
+  p.qouts = q->qouts; p.ychsum1 = q->ychsum1; p.ychsums = q->ychsums;
+  const int64_t tiles = (int64_t)d1.N * (d1.Ho / kTH2);
+  if (tiles > 0x7fffffff || (int64_t)d1.N * d1.H * d1.W * C >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+#define LBT_F2(CS_)                                                                                           \
+  if (CS == CS_) {                                                                                            \
+    if (q->w4)                                                                                                \
+      hipLaunchKernelGGL((conv_fwd2_kernel<CS_, true>), dim3((unsigned)tiles), dim3(kBThreads), 0, st, p);    \
+    else                                                                                                      \
+      hipLaunchKernelGGL((conv_fwd2_kernel<CS_, false>), dim3((unsigned)tiles), dim3(kBThreads), 0, st, p);   \
+    return (int)hipGetLastError();                                                                            \
+  }
+  LBT_F2(1)
+  LBT_F2(2)
+#undef LBT_F2
   return LBT_EINVAL;
 }

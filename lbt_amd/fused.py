@@ -630,7 +630,28 @@ class FusedResNet:
             obs(b.ns.X_range, numel)
         pair = (self.pair_launch and cs is not None and not self._fusable_bwd(c1, d1, flag=True)
                 and (Cin, C) in ((16, 32), (32, 64)))
-        if pair:  # conv-1 and the shortcut conv read the same input codes: one launch
+        a = self._chain_pending
+        # the whole transition (the pending end chain of the previous block + both strided convs and their
+        # quantising epilogues) as ONE launch (lbt_conv_fwd2_fused_i8)
+        fwd2 = (pair and a is not None and os.environ.get("LBT_FUSE_FWD2", "1") == "1" and not a.has_b2
+                and a.o1 == xa.data_ptr() and a.o2 == xs.data_ptr() and bool(a.res) and bool(a.y)
+                and W * Cin == 512 and d1.Ho % 4 == 0 and (d1.PT, d1.PL, ds.PT, ds.PL) == (0, 0, 0, 0)
+                and getattr(c1, "w4", False) == getattr(cs, "w4", False))
+        if fwd2:
+            cf2 = _lib.ConvFwd2()
+            cf2.c = a
+            cf2.wf1, cf2.ksf1, cf2.wcolsum1 = self._wf(c1).value, c1.ksf, c1.wcolsum.data_ptr()
+            cf2.wfs, cf2.ksfs, cf2.wcolsums = self._wf(cs).value, cs.ksf, cs.wcolsum.data_ptr()
+            cf2.w4 = 1 if getattr(c1, "w4", False) else 0
+            cf2.d1, cf2.ds, cf2.qw1, cf2.qws = d1, ds, c1.W_range.desc, cs.W_range.desc
+            cf2.yq1, cf2.qout1, cf2.ychsum1 = qn1.data_ptr(), self._qd(b.n1.X_range), chs1.data_ptr()
+            cf2.yqs, cf2.qouts, cf2.ychsums = qns.data_ptr(), self._qd(b.ns.X_range), chss.data_ptr()
+            self._keep.append(cf2)
+            self._chain_pending = None
+            nb = (ops._chain_fwd_bytes(a) + c1.wf.numel() + cs.wf.numel() + 2 * qn1.numel()
+                  + 4 * (3 * a.inner + 2 * qn1.numel() // N))
+            fwd.append(L("lbt_conv_fwd2_fused_i8", ctypes.byref(cf2), k="conv_fwd2_kernel", nb=nb))
+        elif pair:  # conv-1 and the shortcut conv read the same input codes: one launch
             self._flush_chain(fwd, L)
             j0 = self._fwd_job(c1, d1, xa, qn1, b.n1.X_range, chs1)
             j1 = self._fwd_job(cs, ds, xs, qns, b.ns.X_range, chss)

@@ -789,10 +789,13 @@ def test_pair_launches_equal_single_launches(w4, bwd2, monkeypatch):
     """lbt_conv_fwd_pair_i8 (a projection block's 3x3/2 conv and 1x1/2 shortcut in one launch),
     lbt_bn_chain_bwd_b_pair (its shortcut-BN and first-BN pass B in one launch) and
     lbt_conv_dgrad2_chain_i8 (both convs' dgrads + the consumer's pass A in one launch) -- or, bwd2,
-    lbt_conv_bwd2_fused_i8 (both pass-B chains, both dgrads and the pass A in ONE launch) == the single
-    launches they replace: gradients, momentum, weights, exponents, BN running statistics and loss
-    bit-identical after two graph-replayed optimiser steps at B=128."""
+    lbt_conv_bwd2_fused_i8 (both pass-B chains, both dgrads and the pass A in ONE launch) and
+    lbt_conv_fwd2_fused_i8 (the previous block's end chain, both strided convs and both quantising
+    epilogues in ONE launch) == the single launches they replace: gradients, momentum, weights,
+    exponents, BN running statistics and loss bit-identical after two graph-replayed optimiser steps
+    at B=128."""
     monkeypatch.setenv("LBT_FUSE_BWD2", "1" if bwd2 else "0")
+    monkeypatch.setenv("LBT_FUSE_FWD2", "1" if bwd2 else "0")
     from lbt_amd.fused import FusedResNet
     from lbt_amd.models import CIFAR10_Resnet20
     from lbt_amd.trainer import Trainer
@@ -810,8 +813,9 @@ def test_pair_launches_equal_single_launches(w4, bwd2, monkeypatch):
         nb = sum(1 for f in m._bwd if getattr(f, "kname", "") == "chain_bwd_b2_kernel")
         nd = sum(1 for f in m._bwd if getattr(f, "kname", "").startswith("conv_dgrad2_kernel"))
         n2 = sum(1 for f in m._bwd if getattr(f, "kname", "") == "conv_bwd2_kernel")
-        want = ((2, 0, 0, 2) if bwd2 else (2, 2, 2, 0)) if pair else (0, 0, 0, 0)
-        assert (nf, nb, nd, n2) == want, (nf, nb, nd, n2)
+        nf2 = sum(1 for f in m._fwd if getattr(f, "kname", "") == "conv_fwd2_kernel")
+        want = ((0, 0, 0, 2, 2) if bwd2 else (2, 2, 2, 0, 0)) if pair else (0, 0, 0, 0, 0)
+        assert (nf, nb, nd, n2, nf2) == want, (nf, nb, nd, n2, nf2)
         bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
         outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,
                      m.loss.item()))
