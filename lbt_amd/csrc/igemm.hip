@@ -68,6 +68,7 @@ struct IgArgs {
   // (ih + PT - kh) % SH == 0 reach such a pixel, and for them the source row is yc + oy - th (no
   // zero rows, no division in the loop).
   int nkh, nkw, kh0, kw0, oy, ox, ch, cw, cpy, cpx;
+  int dbg;  // igemm_big_kernel diagnostics (LBT_IGEMM_BIG_DBG; 1: no operand loads after the prologue)
 };
 
 // every tap, rows = every output pixel (fwd, unit-stride dgrad)
@@ -461,6 +462,360 @@ __global__ __launch_bounds__(256) void igemm_splitk_reduce_kernel(IgArgs p) {
   *reinterpret_cast<float4*>(p.y + i4) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// ---------------------------------------------------------------------------- 256-row tiles
+// igemm_big_kernel: the same implicit GEMMs (no split-K, no parity classes) on 256-row x BN-column
+// workgroup tiles of 8 waves (wave tile (256 / WM) x 64, WM x WN = 8, WN = BN / 64), with BOTH operands
+// staged by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no ds_write pass) through an S-stage
+// LDS ring: k-block kb + S - 1 is in flight while kb is multiplied, ordered by a counted vmcnt and a
+// raw s_barrier per k-block (a __syncthreads would drain the DMA ring with vmcnt(0)). The DMA writes
+// each wave-instruction's 1 KiB lane-linearly, so the bank-conflict swizzle is applied on the SOURCE
+// side: 16-byte segment s of row r lands at segment s ^ f(r) (A8 / B: f = (r >> 2) & 3 over 64-byte
+// rows; A16: f = (r >> 1) & 7 over 128-byte rows of raw int16 codes, split into hi / lo' on the
+// fragment read), and the fragment reads apply the same XOR. Out-of-image taps and rows past M read a
+// 16-byte fill block (0, or 0x80 for offset codes).
+constexpr int kBT = 512;
+static __device__ __attribute__((aligned(16))) uint32_t kFill80[4] = {0x80808080u, 0x80808080u, 0x80808080u,
+                                                                      0x80808080u};
+
+template <int N>
+LBT_DEV void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+// Segment swizzles of the LDS images, conflict-free for ds_read_b128's lane groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32): a fragment read by lanes (r = lane & 15, q = lane >> 4)
+// of rows base + r (base % 16 == 0) hits 16 distinct 4-bank quads in every group.
+// 64-byte rows (4 segments; bank quad = (row & 3, segment)): f = {0, 2, 3, 1}[(row >> 2) & 3].
+LBT_DEV int swz64(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+// 128-byte rows (8 segments; quad = (row & 1, segment)), segments 2q ^ f and 2q + 1 ^ f: f = (row >> 1) & 5.
+LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
+
+template <int MODE, bool A16, bool ADD, int BN, int S>
+__global__ __launch_bounds__(kBT, 1) void igemm_big_kernel(IgArgs p) {
+  constexpr int BM = 256, WN = BN / 64, WM = 8 / WN, TR = BM / WM, MI = TR / 16, NJ = 4;
+  constexpr int NA = A16 ? 2 : 1;
+  constexpr int ROWB = A16 ? 128 : 64;                 // bytes of one A row per k-block
+  constexpr int ABYTES = BM * ROWB, BBYTES = BN * 64, STAGE = ABYTES + BBYTES;
+  constexpr int NIA = ABYTES / 1024, NIB = BBYTES / 1024;  // 1-KiB DMA wave-instructions per stage
+  constexpr int GA = NIA / 8;                          // A instructions per wave (2 or 4)
+  constexpr int RPI = A16 ? 8 : 16;                    // A rows per instruction
+  static_assert(NIA % 8 == 0 && (NIB % 8 == 0 || NIB == 4) && (!A16 || BN <= 128), "geometry");
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int r = lane & 15, q = lane >> 4;
+  // XCD-aware bijective tile order: the WN column tiles of one row tile share an XCD's L2
+  const int ntn = p.ncol / BN;
+  const uint32_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const uint32_t tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int64_t m0 = (int64_t)(tile / (uint32_t)ntn) * BM;
+  const int n0 = (int)(tile % (uint32_t)ntn) * BN;
+  const lbt_conv_desc& d = p.d;
+  const int OH = p.ch, OW = p.cw;
+  const int SH = MODE == MODE_FWD ? d.H : d.Ho, SW = MODE == MODE_FWD ? d.W : d.Wo;
+  const int cblocks = p.cred / kBK, nk = p.nkh * p.nkw * cblocks;
+  const int8_t* fill = (!A16 && p.a_u8off) ? reinterpret_cast<const int8_t*>(kFill80)
+                                           : reinterpret_cast<const int8_t*>(zi());
+
+  // ---- this lane's DMA rows: A row (i = wave + 8 g) * RPI + lane / (64 / RPI), segment lane % (64 / RPI)
+  constexpr int SPR = 64 / RPI;  // lanes (16-byte segments) per row: 4 (A8) or 8 (A16)
+  int an[GA], ay[GA], ax[GA], aseg[GA];
+  bool arow[GA];
+#pragma unroll
+  for (int g = 0; g < GA; ++g) {
+    const int row = (wave + 8 * g) * RPI + lane / SPR;
+    const int64_t m = m0 + row;
+    arow[g] = m < p.M;
+    const uint32_t mu = (uint32_t)(arow[g] ? m : 0);
+    ax[g] = (int)(mu % (uint32_t)OW);
+    const uint32_t tt = mu / (uint32_t)OW;
+    ay[g] = (int)(tt % (uint32_t)OH);
+    an[g] = (int)(tt / (uint32_t)OH);
+    const int ps = lane % SPR;  // the LDS segment this lane fills; its source is segment ps ^ f(row)
+    aseg[g] = A16 ? (ps ^ swz128(row)) : (ps ^ swz64(row));
+  }
+  // B: instruction i covers weight-image columns n0 + 16 i .. + 15 (64 bytes of the k-block each)
+  constexpr int GB = NIB >= 8 ? NIB / 8 : 1;
+  const bool bact = NIB >= 8 || wave < NIB;
+  int bcolx[GB], bseg[GB];
+#pragma unroll
+  for (int g = 0; g < GB; ++g) {
+    const int cl = (wave + 8 * g) * 16 + lane / 4;
+    bcolx[g] = n0 + cl;
+    bseg[g] = (lane % 4) ^ swz64(cl);
+  }
+  auto issue = [&](int kb, int st) {
+    const int tap = kb / cblocks, cb = kb - tap * cblocks;
+    const int th = tap / p.nkw, tw = tap - th * p.nkw;
+    const int kh = MODE == MODE_FWD ? th : p.kh0 + d.SH * th, kw = MODE == MODE_FWD ? tw : p.kw0 + d.SW * tw;
+    const int kbw = (kh * d.KW + kw) * cblocks + cb;
+    int8_t* sb = lds + st * STAGE;
+#pragma unroll
+    for (int g = 0; g < GA; ++g) {
+      int sy, sx;
+      if (MODE == MODE_FWD) {
+        sy = ay[g] * d.SH + kh - d.PT;
+        sx = ax[g] * d.SW + kw - d.PL;
+      } else {
+        sy = ay[g] + p.oy - th;
+        sx = ax[g] + p.ox - tw;
+      }
+      const bool ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW && arow[g];
+      const int8_t* src;
+      if (ok) {
+        const uint32_t pix = (uint32_t)((an[g] * SH + sy) * SW + sx);
+        src = reinterpret_cast<const int8_t*>(p.a) +
+              (uint64_t)(pix * (uint32_t)p.cred + (uint32_t)(cb * kBK)) * (A16 ? 2 : 1) + aseg[g] * 16;
+      } else {
+        src = fill;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_vptr)(sb + (wave + 8 * g) * 1024), 16, 0, 0);
+    }
+    if (bact) {
+#pragma unroll
+      for (int g = 0; g < GB; ++g) {
+        const int8_t* src = p.b + ((uint32_t)(bcolx[g] * p.ks + kbw * 4 + bseg[g]) << 4);
+        __builtin_amdgcn_global_load_lds(src, (lds_vptr)(sb + ABYTES + (wave + 8 * g) * 1024), 16, 0, 0);
+      }
+    }
+  };
+  auto wait_landed = [&]() {  // k-block kb's DMA landed: at most S-2 younger groups in flight
+    if constexpr (NIB >= 8) {
+      vm_wait<(S - 2) * (GA + GB)>();
+    } else {
+      if (bact) vm_wait<(S - 2) * (GA + 1)>(); else vm_wait<(S - 2) * GA>();
+    }
+  };
+
+  v4i acc[NA][MI][NJ], accw[NJ];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[a][i][j] = v4i{0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) accw[j] = v4i{0, 0, 0, 0};
+  const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
+  // sum_k W per column (the +128 term of offset / split codes): from the caller's column sums when it
+  // has them, else from MFMAs against ones (16-bit codes; offset codes of lbt_conv_fwd_igemm_q)
+  const bool wmfma = A16 || (p.a_u8off && !p.colsum);  // uniform
+
+  // fragments of one k-block (A16: the raw int16 code pairs, split into hi / lo' at the MFMA)
+  typedef v4i FragA[MI][NA];
+  typedef v4i FragB[NJ];
+  auto read_frags = [&](int st, FragA& fa, FragB& fb) {
+    const int8_t* sb = lds + st * STAGE;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = wn * 64 + j * 16 + r;
+      fb[j] = *reinterpret_cast<const v4i*>(sb + ABYTES + col * 64 + ((q ^ swz64(col)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * TR + i * 16 + r;
+      if constexpr (A16) {
+        const int f = swz128(row);
+        fa[i][0] = *reinterpret_cast<const v4i*>(sb + row * 128 + (((2 * q) ^ f) << 4));
+        fa[i][NA - 1] = *reinterpret_cast<const v4i*>(sb + row * 128 + (((2 * q + 1) ^ f) << 4));
+      } else {
+        fa[i][0] = *reinterpret_cast<const v4i*>(sb + row * 64 + ((q ^ swz64(row)) << 4));
+      }
+    }
+  };
+  auto mma = [&](const FragA& fa, const FragB& fb) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      if constexpr (A16) {
+        // codes (int16) e0 e1 | e2 e3 per dword: hi = high bytes, lo' = low bytes ^ 0x80 (a = 256 hi + lo' + 128)
+        const v4i c0 = fa[i][0], c1 = fa[i][NA - 1];
+        const uint32_t w[8] = {(uint32_t)c0[0], (uint32_t)c0[1], (uint32_t)c0[2], (uint32_t)c0[3],
+                               (uint32_t)c1[0], (uint32_t)c1[1], (uint32_t)c1[2], (uint32_t)c1[3]};
+        v4i hi, lo;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          hi[u] = (int)__builtin_amdgcn_perm(w[2 * u + 1], w[2 * u], 0x07050301u);
+          lo[u] = (int)(__builtin_amdgcn_perm(w[2 * u + 1], w[2 * u], 0x06040200u) ^ 0x80808080u);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          acc[0][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(hi, fb[j], acc[0][i][j], 0, 0, 0);
+          acc[NA - 1][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, fb[j], acc[NA - 1][i][j], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[0][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i][0], fb[j], acc[0][i][j], 0, 0, 0);
+      }
+    }
+    if (wmfma) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) accw[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, fb[j], accw[j], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(s < nk ? s : nk - 1, s);
+  if constexpr (S >= 3) {
+    // Software-pipelined: k-block kb + 1's fragments are read from LDS while kb's MFMAs run. Step kb
+    // waits for DMA group kb + 1 (at most S - 3 younger groups in flight) and the barrier, which also
+    // retires every wave's reads of the stage the new DMA (group kb + S - 1) overwrites (read in step kb - 2).
+    auto wait_next = [&]() {
+      if constexpr (NIB >= 8) {
+        vm_wait<(S - 3) * (GA + GB)>();
+      } else {
+        if (bact) vm_wait<(S - 3) * (GA + 1)>(); else vm_wait<(S - 3) * GA>();
+      }
+    };
+    auto step = [&](int kb, const FragA& ca, const FragB& cb, FragA& na, FragB& nb) {
+      wait_next();
+      __builtin_amdgcn_s_barrier();
+      if (!(p.dbg & 1)) {
+        const int nx = kb + S - 1;
+        issue(nx < nk ? nx : nk - 1, nx % S);
+      }
+      read_frags((kb + 1) % S, na, nb);  // past the last k-block: an unused read of a stale stage
+      mma(ca, cb);
+    };
+    wait_landed();
+    __builtin_amdgcn_s_barrier();
+    FragA fa0, fa1;
+    FragB fb0, fb1;
+    read_frags(0, fa0, fb0);
+    for (int kb = 0; kb < nk; kb += 2) {
+      step(kb, fa0, fb0, fa1, fb1);
+      if (kb + 1 < nk) step(kb + 1, fa1, fb1, fa0, fb0);
+    }
+  } else {
+    for (int kb = 0; kb < nk; ++kb) {
+      wait_landed();
+      __builtin_amdgcn_s_barrier();
+      if (!(p.dbg & 1)) {
+        const int nx = kb + S - 1;
+        issue(nx < nk ? nx : nk - 1, nx % S);  // refills the stage read in iteration kb - 1
+      }
+      FragA fa;
+      FragB fb;
+      read_frags(kb % S, fa, fb);
+      mma(fa, fb);
+    }
+  }
+  vm_wait<0>();  // the ring's trailing (clamped) DMAs: nothing may still write LDS when the block ends
+
+  // ---- epilogue (igemm_kernel's): lane owns column (tile col + r), rows (tile row + 4q + e)
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
+  constexpr bool addv = MODE == MODE_DGRAD && ADD;
+  const int ncol = p.ncol;
+  const int64_t rtile = m0 + wm * TR + q * 4;  // + i * 16 + e
+  const bool full = m0 + BM <= p.M;
+  const int rlim = full ? TR : (int)(p.M - rtile);
+  const int cw = n0 + wn * 64;
+  // the +128 sum_k W term of offset codes: the weight image's column sums (fwd); 16-bit codes: accw
+  if constexpr (!A16) {
+    if (p.a_u8off && p.colsum) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int cs = p.colsum[cw + j * 16 + r];
+        accw[j] = v4i{cs, cs, cs, cs};
+      }
+    }
+  }
+  const int u8 = (!A16 && p.a_u8off) ? 128 : 0;
+  if constexpr (MODE == MODE_FWD && !A16) {
+    if (p.yq) {  // uniform: quantising epilogue
+      quant_epilogue<MI, NJ>(p, acc[0], accw, u8, scale, rtile, rlim, full, cw, r, q);
+      return;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = cw + j * 16 + r;
+    float* yp = p.y + rtile * ncol + col;
+    const float* ap = addv ? p.add_src + rtile * ncol + col : nullptr;
+    float av[MI][4];
+    if constexpr (addv) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) av[i][e] = (i * 16 + e < rlim) ? ap[(i * 16 + e) * ncol] : 0.f;
+    }
+    const int wsum = (A16 || p.a_u8off) ? accw[j][0] : 0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v;
+        if constexpr (A16) {
+          const double hs = (double)acc[0][i][j][e] * 256.0;
+          const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
+          v = (float)(hs + ls) * scale;
+        } else {
+          v = (float)(acc[0][i][j][e] + u8 * wsum) * scale;
+        }
+        if (full || i * 16 + e < rlim) yp[(i * 16 + e) * ncol] = addv ? v + av[i][e] : v;
+      }
+  }
+}
+
+template <int MODE, bool A16, int BN, int S>
+void launch_big_bn(IgArgs p, hipStream_t st) {
+  static const int dbg = getenv_int("LBT_IGEMM_BIG_DBG", 0);
+  p.dbg = dbg;
+  const int64_t tiles = ((p.M + 255) / 256) * (p.ncol / BN);
+  constexpr int BM = 256, ROWB = A16 ? 128 : 64;
+  constexpr size_t shm = (size_t)S * (BM * ROWB + BN * 64);
+  const bool add = MODE == MODE_DGRAD && p.add_src;
+#define LBT_BIG(ADD_)                                                                                     \
+  do {                                                                                                    \
+    static bool attr_ = [] {                                                                              \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, ADD_, BN, S>), \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                   \
+      return true;                                                                                        \
+    }();                                                                                                  \
+    (void)attr_;                                                                                          \
+    hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, ADD_, BN, S>), dim3((unsigned)tiles), dim3(kBT), shm, st, p); \
+  } while (0)
+  if (add) LBT_BIG(true); else LBT_BIG(false);
+#undef LBT_BIG
+}
+
+// The 256-row LDS-DMA kernel takes a GEMM when it is big enough to give every CU about one tile
+// (LBT_IGEMM_BIG_MIN tiles, default 200; LBT_IGEMM_BIG=0: never) and is not split / classed.
+template <int MODE, bool A16>
+bool launch_big(const IgArgs& p, hipStream_t st) {
+  static const int on = getenv_int("LBT_IGEMM_BIG", 1), tmin = getenv_int("LBT_IGEMM_BIG_MIN", 200);
+  if (!on || p.ksplit != 1 || p.ncol % 64 || p.cred % kBK) return false;
+  if ((p.M + 255) / 256 * (p.ncol / 64) > 0x7fffffff) return false;
+  // column tile: the widest that still gives LBT_IGEMM_BIG_MIN tiles (256 only without the quantising
+  // epilogue and on request: its 8 x 4 accumulator tiles per wave spill)
+  const int64_t mt = (p.M + 255) / 256;
+  int bn = 0;
+  if (!A16 && !p.yq && p.ncol % 256 == 0 && getenv_int("LBT_IGEMM_BIG_BN256", 0) && mt * (p.ncol / 256) >= tmin) bn = 256;
+  else if (p.ncol % 128 == 0 && mt * (p.ncol / 128) >= tmin) bn = 128;
+  else if (mt * (p.ncol / 64) >= tmin) bn = 64;
+  if (!bn) return false;
+  // LDS ring depth (LBT_IGEMM_BIG_S): 2 by default -- the probe on the ResNet-50 shapes measured the
+  // occupancy of 2 stages (A8 BN 128: 48 KiB, two workgroups per CU) ahead of the latency hiding of 3-4
+  // (72-96 KiB, one; the software-pipelined loop), except 3x3 dgrad16 at 28x28 / 14x14 (3-5 %)
+  static const int sdep = getenv_int("LBT_IGEMM_BIG_S", 2);
+  const int S = sdep;
+  if (bn == 256) {
+    if constexpr (!A16) launch_big_bn<MODE, A16, 256, 4>(p, st);
+  } else if (bn == 128) {
+    if (S == 2) launch_big_bn<MODE, A16, 128, 2>(p, st);
+    else if (S == 3 || A16) launch_big_bn<MODE, A16, 128, 3>(p, st);
+    else launch_big_bn<MODE, A16, 128, 4>(p, st);
+  } else {
+    if (S == 2) launch_big_bn<MODE, A16, 64, 2>(p, st);
+    else if (S == 3 || A16) launch_big_bn<MODE, A16, 64, 3>(p, st);
+    else launch_big_bn<MODE, A16, 64, 4>(p, st);
+  }
+  return true;
+}
+
 template <int MODE, bool A16, int BM, int BN, bool CLS = false>
 void launch_tile(const IgArgs& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.ncol + BN - 1) / BN), (unsigned)p.ksplit);
@@ -523,6 +878,7 @@ int launch(const IgArgs& p, hipStream_t st) {
     if (bn64) launch_tile<MODE, A16, 64, 64, true>(p, st); else launch_tile<MODE, A16, 64, 128, true>(p, st);
     return (int)hipGetLastError();
   }
+  if (launch_big<MODE, A16>(p, st)) return (int)hipGetLastError();
   const int64_t nb = (p.ncol + (bn64 ? 63 : 127)) / (bn64 ? 64 : 128);
   // ... and always for 16-bit codes when the tile would be 128 x 128: that variant needs 256 VGPRs
   // (one wave per SIMD), which leaves its fp32 epilogue stores unhidden

@@ -17,7 +17,16 @@ shapes = [("l1_c3_fwd", B, 56, 64, 256, 1, 1, "fwd"), ("l1_c1_dgrad16", B, 56, 2
           ("l1_c2_fwd", B, 56, 64, 64, 3, 1, "fwd"), ("l1_c2_dgrad16", B, 56, 64, 64, 3, 1, "dgrad"),
           ("l2_c2_fwd", B, 28, 128, 128, 3, 1, "fwd"), ("l2_c2_dgrad16", B, 28, 128, 128, 3, 1, "dgrad"),
           ("l3_c2_fwd", B, 14, 256, 256, 3, 1, "fwd"), ("l3_c2_dgrad16", B, 14, 256, 256, 3, 1, "dgrad"),
-          ("l4_c2_fwd", B, 7, 512, 512, 3, 1, "fwd"), ("l4_c2_dgrad16", B, 7, 512, 512, 3, 1, "dgrad")]
+          ("l4_c2_fwd", B, 7, 512, 512, 3, 1, "fwd"), ("l4_c2_dgrad16", B, 7, 512, 512, 3, 1, "dgrad"),
+          ("l1_c2_fwdq", B, 56, 64, 64, 3, 1, "fwdq"), ("l2_c2_fwdq", B, 28, 128, 128, 3, 1, "fwdq"),
+          ("l3_c2_fwdq", B, 14, 256, 256, 3, 1, "fwdq"), ("l1_c3_fwdq", B, 56, 64, 256, 1, 1, "fwdq"),
+          ("l3_c3_fwdq", B, 14, 256, 1024, 1, 1, "fwdq")]
+# PROBE_QNOISE: inline (Philox in the epilogue), table (a per-step noise table, lbt_dfxp_noise_fill),
+# none (round-to-nearest quantiser)
+QN = os.environ.get("PROBE_QNOISE", "inline")
+qo = ctx.quantizer("t/Y", 8, 2, stochastic=QN != "none")
+only = os.environ.get("PROBE_ONLY")
+shapes = [sh for sh in shapes if not only or sh[0] in only.split(",")]
 for name, N, H, Cin, Cout, k, s, mode in shapes:
     d = ops.conv_desc(N, H, H, Cin, Cout, k, k, s, s, "SAME")
     W = torch.rand((k, k, Cin, Cout), device=dev) * 2 - 1
@@ -26,7 +35,21 @@ for name, N, H, Cin, Cout, k, s, mode in shapes:
     wd = torch.zeros((Cin, ksd * 16), dtype=torch.int8, device=dev)
     ops.quantize_weight(W, qw, w_hwio=torch.empty((k, k, Cin, Cout), dtype=torch.int8, device=dev),
                         wf=wf, ksf=ksf, wd=wd, ksd=ksd)
-    if mode == "fwd":
+    if mode == "fwdq":
+        x = torch.randint(-128, 128, (N, H, H, Cin), dtype=torch.int8, device=dev)
+        yq = torch.empty((N, d.Ho, d.Wo, Cout), dtype=torch.int8, device=dev)
+        chs = torch.zeros((64, 2 * Cout), dtype=torch.int64, device=dev)
+        if QN == "table":
+            from lbt_amd import _lib
+            from lbt_amd.fused import _dev_array
+            inner = d.Ho * d.Wo * Cout
+            tab = torch.zeros((inner + 3) // 4 * 4, dtype=torch.float32, device=dev)
+            jobs = _dev_array([_lib.NJob(ctx.step.data_ptr(), ctx.seed, qo.qid, 0, inner, tab.data_ptr())], dev)
+            _lib.call("lbt_dfxp_noise_fill", _lib.ptr(jobs), 1, inner, None, 0, _lib.stream())
+            qo.desc.noise = tab.data_ptr()
+        fn = lambda: ops.conv_fwd_igemm_q(x, 1, wf, ksf, d, qx.desc, qw.desc, yq, qo, chs)  # noqa: E731
+        macs = N * d.Ho * d.Wo * Cout * k * k * Cin
+    elif mode == "fwd":
         x = torch.randint(-128, 128, (N, H, H, Cin), dtype=torch.int8, device=dev)
         y = torch.empty((N, d.Ho, d.Wo, Cout), device=dev)
         fn = lambda: ops.conv_fwd_igemm(x, 1, wf, ksf, d, qx.desc, qw.desc, y)  # noqa: E731
