@@ -1231,6 +1231,201 @@ __global__ __launch_bounds__(kT, 1) void wgrad_wide_kernel(const int8_t* __restr
   }
 }
 
+
+// ----------------------------------------------------------------------------- 3x3 wgrad, all taps
+// wgrad3_kernel: a stride-1 SAME 3x3 conv's weight gradient with ALL 9 taps in one workgroup tile, so
+// X and G leave L2 once per (ci block, co block) instead of once per tap (wgrad_wide_kernel's 9x).
+// Workgroup = (pixel split, 64 ci, 64 co) of 8 waves; a chunk is RB = 64 / W whole output rows of one
+// image (RB * W <= 64 pixels = the MFMA k), staged once for all waves: the X halo window
+// [4 ci slices][(RB + 2) x (W + 2) pixels][16 B] (fill code outside the image) and G's 64 pixels x
+// 64 co ([hi | lo'][4 co slices][64 px][16 B]; past the rows / image: g = 0). Wave w owns ci slice
+// w & 3 and co slices 2 (w >> 2) + {0, 1} for all 9 taps; its A fragments are transposed reads of
+// the window at the tap's offset (pixels past the chunk read a duplicate of its last pixel: their
+// g = 0 cancels them exactly, see the identity of wgrad_wide_kernel), its B fragments the G image.
+// The next chunk's loads fly during the MFMAs. Every (split, tap, ci, co) has one writer: STORED
+// into slab[split][9 * Cin][Cout] (int64), reduced by lbt_conv_wgrad_reduce64 over the splits.
+constexpr int kW3Win = 192;  // window pixels per ci slice: (64 / W + 2) * (W + 2) <= 192 (host check)
+
+LBT_DEV v4i tr_frag2(const int8_t* img, int oa, int ob) {
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(img + oa));
+  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(img + ob));
+  return v4i{lo.x, lo.y, hi.x, hi.y};
+}
+
+template <bool G16>
+__global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
+                                                      lbt_conv_desc d, long long* __restrict__ slab, int nsplit) {
+  constexpr int NP = G16 ? 2 : 1;  // G planes: (gh, gl') or g
+  __shared__ __attribute__((aligned(16))) int8_t sx[4 * kW3Win * 16];
+  __shared__ __attribute__((aligned(16))) int8_t sg[NP * 4 * 64 * 16];
+  __shared__ int sax[9 * 64];  // sum_p x' per (tap, ci): waves 0-3 -> all
+  __shared__ int sag[NP * 64];  // sum_p g (planes) per co: waves with ci slice 0 -> all
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 15, q = lane >> 4;
+  const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
+  const int RB = 64 / W, NPX = RB * W, Wp = W + 2, WIN = (RB + 2) * Wp;
+  const int CPI = (H + RB - 1) / RB;
+  const int64_t TC = (int64_t)d.N * CPI;
+  const int nblk = (Cin / 64) * (Cout / 64);
+  const int blk = (int)(blockIdx.x % (uint32_t)nblk), split = (int)(blockIdx.x / (uint32_t)nblk);
+  const int cb = blk / (Cout / 64), ob = blk - cb * (Cout / 64);
+  const int64_t c0 = TC * split / nsplit, c1 = TC * (split + 1) / nsplit;
+  const int ws = wave & 3, wh = wave >> 2;
+  const bool do_ax = G16 && wh == 0, do_ag = ws == 0;
+  // transposed-read offsets: pixels pa = 16q + j/2 and pa + 8 of the chunk (X: clamped to the chunk)
+  const int pa = 16 * q + (j >> 1), pb = pa + 8;
+  const int xa = pa < NPX ? pa : NPX - 1, xb = pb < NPX ? pb : NPX - 1;
+  const int oxa = ((xa / W) * Wp + xa % W) * 16 + 8 * (j & 1);
+  const int oxb = ((xb / W) * Wp + xb % W) * 16 + 8 * (j & 1);
+  const int oga = pa * 16 + 8 * (j & 1), ogb = pb * 16 + 8 * (j & 1);
+  const int fx = (int)0x80808080u;  // x' = -128: x = 0
+
+  // this thread's staging items: X (window pixel, ci slice) t and t + 512; G (pixel, 16-byte segment)
+  v4i xr[2], gr;
+  bool xin[2], xit[2];
+  int xdst[2];
+  auto load = [&](int64_t c) {
+    const int n = (int)(c / CPI), row0 = (int)(c - (int64_t)n * CPI) * RB;
+    const int8_t* xim = xq + (int64_t)n * H * W * Cin + cb * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int it = tid + 512 * i;
+      const int pix = it >> 2, sl = it & 3;
+      const int hy = pix / Wp, hx = pix - hy * Wp;
+      const int y = row0 - 1 + hy, x = hx - 1;
+      xit[i] = pix < WIN;
+      xin[i] = xit[i] && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      xdst[i] = (sl * kW3Win + pix) * 16;
+      xr[i] = *reinterpret_cast<const v4i*>(xim + (xin[i] ? (int64_t)(y * W + x) * Cin + sl * 16 : 0));
+    }
+    if constexpr (G16) {
+      const int pl = tid >> 3, seg = tid & 7;
+      const int oy = row0 + pl / W, ox = pl % W;
+      const bool in = pl < NPX && oy < H;
+      const int16_t* gp = reinterpret_cast<const int16_t*>(gq) + ((int64_t)n * H * W + (in ? oy * W + ox : 0)) * Cout +
+                          ob * 64 + seg * 8;
+      gr = *reinterpret_cast<const v4i*>(gp);
+      if (!in) gr = v4i{0, 0, 0, 0};
+    } else {
+      const int pl = tid >> 2, cs = tid & 3;
+      const int oy = row0 + pl / W, ox = pl % W;
+      const bool in = tid < 256 && pl < NPX && oy < H;
+      const int8_t* gp = reinterpret_cast<const int8_t*>(gq) + ((int64_t)n * H * W + (in ? oy * W + ox : 0)) * Cout +
+                         ob * 64 + cs * 16;
+      gr = *reinterpret_cast<const v4i*>(gp);
+      if (!in) gr = v4i{0, 0, 0, 0};
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const v4i v = xin[i] ? xr[i] : v4i{fx, fx, fx, fx};
+      if (xit[i]) *reinterpret_cast<v4i*>(sx + xdst[i]) = v;
+    }
+    if constexpr (G16) {
+      const int pl = tid >> 3, seg = tid & 7;
+      // 8 codes -> 8 gh bytes and 8 gl' bytes (g = 256 gh + gl' + 128); g = 0 gives gh = 0, gl' = -128
+      int hi[2], lo[2];
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const uint32_t c01 = (uint32_t)gr[2 * w], c23 = (uint32_t)gr[2 * w + 1];
+        hi[w] = (int)__builtin_amdgcn_perm(c23, c01, 0x07050301u);
+        lo[w] = (int)(__builtin_amdgcn_perm(c23, c01, 0x06040200u) ^ 0x80808080u);
+      }
+      const int o = ((seg >> 1) * 64 + pl) * 16 + (seg & 1) * 8;
+      *reinterpret_cast<v2i*>(sg + o) = v2i{hi[0], hi[1]};
+      *reinterpret_cast<v2i*>(sg + 4 * 64 * 16 + o) = v2i{lo[0], lo[1]};
+    } else {
+      if (tid < 256) *reinterpret_cast<v4i*>(sg + ((tid & 3) * 64 + (tid >> 2)) * 16) = gr;
+    }
+  };
+
+  v4i acc[9][2][NP], ax[9], ag[2][NP];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    ax[t] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int h = 0; h < NP; ++h) acc[t][c][h] = v4i{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int h = 0; h < NP; ++h) ag[c][h] = v4i{0, 0, 0, 0};
+  const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
+  const int8_t* xs = sx + ws * kW3Win * 16;
+
+  if (c0 < c1) load(c0);
+  for (int64_t c = c0; c < c1; ++c) {
+    __syncthreads();  // every wave's reads of the previous chunk are done
+    stage();
+    if (c + 1 < c1) load(c + 1);  // in flight during this chunk's MFMAs
+    __syncthreads();
+    v4i bf[2][NP];
+#pragma unroll
+    for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+      for (int h = 0; h < NP; ++h) {
+        bf[cs][h] = tr_frag2(sg + ((h * 4 + 2 * wh + cs) * 64) * 16, oga, ogb);
+        if (do_ag) ag[cs][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[cs][h], ag[cs][h], 0, 0, 0);
+      }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = ((t / 3) * Wp + t % 3) * 16;
+      const v4i af = tr_frag2(xs, oxa + toff, oxb + toff);
+      if (do_ax) ax[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, ones, ax[t], 0, 0, 0);
+#pragma unroll
+      for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+        for (int h = 0; h < NP; ++h) acc[t][cs][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[cs][h], acc[t][cs][h], 0, 0, 0);
+    }
+  }
+  // ---- the row / column sums to every wave, then one exact int64 per output
+  if (do_ax && j == 0) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sax[t * 64 + ws * 16 + 4 * q + i] = ax[t][i];
+  }
+  if (do_ag && q == 0) {
+#pragma unroll
+    for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+      for (int h = 0; h < NP; ++h) sag[h * 64 + (2 * wh + cs) * 16 + j] = ag[cs][h][0];
+  }
+  __syncthreads();
+  const long long npix = (long long)(c1 - c0) * 64;
+  long long* dst = slab + (int64_t)split * 9 * Cin * Cout;
+#pragma unroll
+  for (int cs = 0; cs < 2; ++cs) {
+    const int col = (2 * wh + cs) * 16 + j;
+    const long long sgc = G16 ? 256ll * sag[col] + (long long)sag[64 + col] + 128ll * npix : (long long)sag[col];
+    const int co = ob * 64 + col;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int cl = ws * 16 + 4 * q + i;
+        long long v;
+        if constexpr (G16)
+          v = 256ll * acc[t][cs][0][i] + (long long)acc[t][cs][NP - 1][i] + 128ll * sax[t * 64 + cl] + 128ll * sgc;
+        else
+          v = (long long)acc[t][cs][0][i] + 128ll * sgc;
+        dst[((int64_t)t * Cin + cb * 64 + cl) * Cout + co] = v;
+      }
+  }
+}
+
+bool wgrad3_ok(const lbt_conv_desc& d) {
+  if (d.KH != 3 || d.KW != 3 || d.SH != 1 || d.SW != 1 || d.PT != 1 || d.PB != 1 || d.PL != 1 || d.PR != 1 ||
+      d.Ho != d.H || d.Wo != d.W || d.W > 64 || d.Cin % 64 || d.Cout % 64)
+    return false;
+  const int RB = 64 / d.W;
+  return (RB + 2) * (d.W + 2) <= kW3Win;
+}
+
 }  // namespace
 
 // wide wgrad: x offset int8 codes (q - 128), g int8 (g_i16 = 0) or int16 codes; adds into a
@@ -1261,10 +1456,24 @@ extern "C" int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int3
   const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
   if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
   if ((P + nsplit - 1) / nsplit > 4 * 131072) return LBT_EINVAL;  // int32 MFMA sums of a wave stay exact
+  hipStream_t st = (hipStream_t)stream;
+  static const int w3 = getenv_int("LBT_WGRAD3", 1);
+  if (w3 && wgrad3_ok(d)) {  // 3x3 / stride 1: all taps per workgroup; splits over whole-row chunks
+    const int RB = 64 / d.W;
+    const int64_t chunks = (int64_t)d.N * ((d.H + RB - 1) / RB);
+    const int64_t nblk = (int64_t)(d.Cin / 64) * (d.Cout / 64);
+    // <= 1024 chunks a split: every int32 MFMA sum stays below 2^31 (64 products of |x' g| <= 2^14 a chunk)
+    if (nsplit > chunks || (chunks + nsplit - 1) / nsplit > 1024 || nblk * nsplit > 0x7fffffff) return LBT_EINVAL;
+    const dim3 grid((unsigned)(nblk * nsplit));
+    if (g_i16)
+      hipLaunchKernelGGL((wgrad3_kernel<true>), grid, dim3(512), 0, st, xq, gq, d, (long long*)slab, nsplit);
+    else
+      hipLaunchKernelGGL((wgrad3_kernel<false>), grid, dim3(512), 0, st, xq, gq, d, (long long*)slab, nsplit);
+    return (int)hipGetLastError();
+  }
   const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
   if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
   dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
-  hipStream_t st = (hipStream_t)stream;
   if (g_i16)
     hipLaunchKernelGGL((wgrad_wide_kernel<true, true>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
                        nsplit);

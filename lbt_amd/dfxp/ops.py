@@ -652,8 +652,29 @@ def wgrad_igemm_nsplit(d):
     return max(lo, min(max(1, P // 256), -(-1024 // tiles)))
 
 
+WGRAD3 = os.environ.get("LBT_WGRAD3", "1") != "0"
+
+
+def wgrad3_ok(d):
+    """lbt_conv_wgrad_igemm_store's all-taps 3x3 body takes this conv (wgrad3_ok in igemm.hip)."""
+    if not WGRAD3:
+        return False
+    if (d.KH, d.KW, d.SH, d.SW, d.PT, d.PB, d.PL, d.PR) != (3, 3, 1, 1, 1, 1, 1, 1) or d.Ho != d.H or d.Wo != d.W:
+        return False
+    if d.W > 64 or d.Cin % 64 or d.Cout % 64:
+        return False
+    return (64 // d.W + 2) * (d.W + 2) <= 192
+
+
 def wgrad_store_nsplit(d):
-    """Pixel splits of the storing wide wgrad: >= ~512 workgroups, each split's slab written once."""
+    """Pixel splits of the storing wide wgrad: >= ~512 workgroups, each split's slab written once.
+    All-taps 3x3 body: splits of whole-row chunks, ~256 workgroups (one per CU; each covers all 9
+    taps of a 64 x 64 channel block), <= 1024 chunks a split."""
+    if wgrad3_ok(d):
+        rb = 64 // d.W
+        chunks = d.N * (-(-d.H // rb))
+        nblk = (d.Cin // 64) * (d.Cout // 64)
+        return min(chunks, max(-(-chunks // 1024), -(-256 // nblk)))
     P = d.N * d.Ho * d.Wo
     tiles = d.KH * d.KW * (d.Cin // 64) * (d.Cout // 64)
     lo = -(-P // (4 * 131072))
