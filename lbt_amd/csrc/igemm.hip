@@ -1246,6 +1246,21 @@ __global__ __launch_bounds__(kT, 1) void wgrad_wide_kernel(const int8_t* __restr
 // into slab[split][9 * Cin][Cout] (int64), reduced by lbt_conv_wgrad_reduce64 over the splits.
 constexpr int kW3Win = 192;  // window pixels per ci slice: (64 / W + 2) * (W + 2) <= 192 (host check)
 
+// ds_read_b64_tr_b8 as inline asm: the compiler's waitcnt pass makes every ds_read_tr intrinsic wait
+// for ALL outstanding LDS-DMA (vmcnt(0): it cannot tell the ring's stages apart), which serialises the
+// DMA ring. The asm form is invisible to that pass, so its results are fenced by hand: tr_wait()
+// (s_waitcnt lgkmcnt(0)) takes the fragments as in/out operands, so no use can move above it.
+LBT_DEV v2i tr8_asm(uint32_t addr) {
+  v2i r;
+  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+LBT_DEV v4i tr_frag_asm(uint32_t a, uint32_t b) {
+  const v2i lo = tr8_asm(a), hi = tr8_asm(b);
+  return v4i{lo.x, lo.y, hi.x, hi.y};
+}
+LBT_DEV void tr_wait(v4i& a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)::"memory"); }
+
 LBT_DEV v4i tr_frag2(const int8_t* img, int oa, int ob) {
   typedef __attribute__((address_space(3))) v2i lds_v2i;
   const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(img + oa));
@@ -1253,15 +1268,27 @@ LBT_DEV v4i tr_frag2(const int8_t* img, int oa, int ob) {
   return v4i{lo.x, lo.y, hi.x, hi.y};
 }
 
-template <bool G16>
+// Operands reach LDS by LDS-DMA (global_load_lds_dwordx4, no staging registers) through an S-stage
+// ring of raw chunks -- the X window in its final [slice][pixel][16 B] layout, G as raw codes
+// [pixel][64 co] -- with one barrier per chunk: step c waits for chunk c + 1's DMA, splits its raw G
+// into the hi / lo' planes of plane buffer (c + 1) & 1, issues chunk c + S - 1's DMA into the stage
+// chunk c - 1 left, and runs chunk c's MFMAs. NXW = X DMA instructions per wave per chunk (each wave
+// issues exactly NXW + 1 per chunk -- idle slots write a dummy KiB -- so the vmcnt waits are constants).
+template <bool G16, int NXW, int S>
 __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
-                                                      lbt_conv_desc d, long long* __restrict__ slab, int nsplit) {
-  constexpr int NP = G16 ? 2 : 1;  // G planes: (gh, gl') or g
-  __shared__ __attribute__((aligned(16))) int8_t sx[4 * kW3Win * 16];
-  __shared__ __attribute__((aligned(16))) int8_t sg[NP * 4 * 64 * 16];
+                                                      lbt_conv_desc d, long long* __restrict__ slab, int nsplit,
+                                                      int dbg) {
+  constexpr int NP = G16 ? 2 : 1;                    // G planes: (gh, gl') or g
+  constexpr int XB = 4 * kW3Win * 16;                // X window image (12 KiB)
+  constexpr int GB = 64 * 64 * (G16 ? 2 : 1);        // raw G codes of a chunk (8 / 4 KiB)
+  constexpr int STG = XB + GB;
+  constexpr int PB = NP * 4 * 64 * 16;               // one plane buffer
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  int8_t* const planes = lds + S * STG;              // [2][PB]
+  int8_t* const dummy = planes + 2 * PB;             // 1 KiB sink of the idle DMA slots
   __shared__ int sax[9 * 64];  // sum_p x' per (tap, ci): waves 0-3 -> all
   __shared__ int sag[NP * 64];  // sum_p g (planes) per co: waves with ci slice 0 -> all
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 15, q = lane >> 4;
   const int H = d.H, W = d.W, Cin = d.Cin, Cout = d.Cout;
   const int RB = 64 / W, NPX = RB * W, Wp = W + 2, WIN = (RB + 2) * Wp;
@@ -1271,6 +1298,9 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
   const int blk = (int)(blockIdx.x % (uint32_t)nblk), split = (int)(blockIdx.x / (uint32_t)nblk);
   const int cb = blk / (Cout / 64), ob = blk - cb * (Cout / 64);
   const int64_t c0 = TC * split / nsplit, c1 = TC * (split + 1) / nsplit;
+  const int nc = (int)(c1 - c0);
+  typedef __attribute__((address_space(3))) int8_t lds_i8;
+  const uint32_t lbase = (uint32_t)(uintptr_t)(lds_i8*)lds;  // LDS byte address of the ring
   const int ws = wave & 3, wh = wave >> 2;
   const bool do_ax = G16 && wh == 0, do_ag = ws == 0;
   // transposed-read offsets: pixels pa = 16q + j/2 and pa + 8 of the chunk (X: clamped to the chunk)
@@ -1279,53 +1309,64 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
   const int oxa = ((xa / W) * Wp + xa % W) * 16 + 8 * (j & 1);
   const int oxb = ((xb / W) * Wp + xb % W) * 16 + 8 * (j & 1);
   const int oga = pa * 16 + 8 * (j & 1), ogb = pb * 16 + 8 * (j & 1);
-  const int fx = (int)0x80808080u;  // x' = -128: x = 0
+  const int ngx = (WIN + 63) >> 6;  // 64-pixel groups of the window per slice
 
-  // this thread's staging items: X (window pixel, ci slice) t and t + 512; G (pixel, 16-byte segment)
-  v4i xr[2], gr;
-  bool xin[2], xit[2];
-  int xdst[2];
-  auto load = [&](int64_t c) {
-    const int n = (int)(c / CPI), row0 = (int)(c - (int64_t)n * CPI) * RB;
-    const int8_t* xim = xq + (int64_t)n * H * W * Cin + cb * 64;
+  // DMA of chunk k (clamped to the split's last) into stage st. Everything but the chunk's (image,
+  // first row) is loop-invariant per lane, and issue() is called with k = 0, 1, 2, ... (clamped), so
+  // (n, row0) advance incrementally -- no divisions in the loop.
+  int xhy[NXW], xrel[NXW], xdst[NXW];
+  bool xreal[NXW];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int it = tid + 512 * i;
-      const int pix = it >> 2, sl = it & 3;
-      const int hy = pix / Wp, hx = pix - hy * Wp;
-      const int y = row0 - 1 + hy, x = hx - 1;
-      xit[i] = pix < WIN;
-      xin[i] = xit[i] && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-      xdst[i] = (sl * kW3Win + pix) * 16;
-      xr[i] = *reinterpret_cast<const v4i*>(xim + (xin[i] ? (int64_t)(y * W + x) * Cin + sl * 16 : 0));
+  for (int u = 0; u < NXW; ++u) {
+    const int ins = wave + 8 * u;  // (slice, pixel group) = (ins % 4, ins / 4)
+    const int sl = ins & 3, gp = ins >> 2;
+    const int pix = gp * 64 + lane;
+    const int hy = pix / Wp, hx = pix - hy * Wp;
+    xreal[u] = gp < ngx;
+    // window pixels past WIN and columns outside the image read the fill (hy = -1 marks them)
+    xhy[u] = (pix < WIN && hx >= 1 && hx <= W) ? hy : -1000000;
+    xrel[u] = (hy - 1) * W + (hx - 1);
+    xdst[u] = xreal[u] ? (sl * kW3Win + gp * 64) * 16 : -1;
+  }
+  const int gitem = wave * 64 + lane;
+  const int gpl = G16 ? gitem >> 3 : gitem >> 2, gseg = G16 ? gitem & 7 : gitem & 3;
+  const bool greal = G16 || wave < 4;
+  const int grow = gpl < NPX ? gpl / W : 1000000;  // output row of the pixel within the chunk
+  int in_n = (int)(c0 / CPI), in_row0 = (int)(c0 - (int64_t)in_n * CPI) * RB, in_k = 0;
+  auto issue = [&](int k, int st) {
+    if (k < nc && k != in_k) {  // advance to chunk k (= in_k + 1)
+      in_row0 += RB;
+      if (in_row0 >= H) { in_row0 = 0; ++in_n; }
+      in_k = k;
     }
-    if constexpr (G16) {
-      const int pl = tid >> 3, seg = tid & 7;
-      const int oy = row0 + pl / W, ox = pl % W;
-      const bool in = pl < NPX && oy < H;
-      const int16_t* gp = reinterpret_cast<const int16_t*>(gq) + ((int64_t)n * H * W + (in ? oy * W + ox : 0)) * Cout +
-                          ob * 64 + seg * 8;
-      gr = *reinterpret_cast<const v4i*>(gp);
-      if (!in) gr = v4i{0, 0, 0, 0};
-    } else {
-      const int pl = tid >> 2, cs = tid & 3;
-      const int oy = row0 + pl / W, ox = pl % W;
-      const bool in = tid < 256 && pl < NPX && oy < H;
-      const int8_t* gp = reinterpret_cast<const int8_t*>(gq) + ((int64_t)n * H * W + (in ? oy * W + ox : 0)) * Cout +
-                         ob * 64 + cs * 16;
-      gr = *reinterpret_cast<const v4i*>(gp);
-      if (!in) gr = v4i{0, 0, 0, 0};
+    const int n = in_n, row0 = in_row0;
+    int8_t* sb = lds + st * STG;
+    const int8_t* xim = xq + ((int64_t)n * H * W + (int64_t)row0 * W) * Cin + cb * 64;
+#pragma unroll
+    for (int u = 0; u < NXW; ++u) {
+      const int sl = (wave + 8 * u) & 3;
+      const bool in = (unsigned)(row0 - 1 + xhy[u]) < (unsigned)H;
+      const int8_t* src = in ? xim + (int64_t)xrel[u] * Cin + sl * 16 : reinterpret_cast<const int8_t*>(kFill80);
+      int8_t* dst = xreal[u] ? sb + xdst[u] : dummy;
+      __builtin_amdgcn_global_load_lds(src, (lds_vptr)dst, 16, 0, 0);
+    }
+    {  // G: wave w moves items 64 w .. 64 w + 63 of the chunk's raw codes (G8: waves 4-7 idle)
+      const bool in = greal && row0 + grow < H;
+      const int8_t* src = in ? reinterpret_cast<const int8_t*>(gq) +
+                                   (((int64_t)n * H * W + (int64_t)row0 * W + gpl) * Cout + ob * 64) * (G16 ? 2 : 1) +
+                                   gseg * 16
+                             : reinterpret_cast<const int8_t*>(zi());
+      int8_t* dst = greal ? sb + XB + wave * 1024 : dummy;
+      __builtin_amdgcn_global_load_lds(src, (lds_vptr)dst, 16, 0, 0);
     }
   };
-  auto stage = [&]() {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const v4i v = xin[i] ? xr[i] : v4i{fx, fx, fx, fx};
-      if (xit[i]) *reinterpret_cast<v4i*>(sx + xdst[i]) = v;
-    }
+  // raw G of the chunk in stage st -> plane buffer pbuf (one 16-byte item per thread)
+  auto split_g = [&](int st, int pbuf) {
+    const int8_t* raw = lds + st * STG + XB;
+    int8_t* pl8 = planes + pbuf * PB;
     if constexpr (G16) {
       const int pl = tid >> 3, seg = tid & 7;
-      // 8 codes -> 8 gh bytes and 8 gl' bytes (g = 256 gh + gl' + 128); g = 0 gives gh = 0, gl' = -128
+      const v4i gr = *reinterpret_cast<const v4i*>(raw + tid * 16);
       int hi[2], lo[2];
 #pragma unroll
       for (int w = 0; w < 2; ++w) {
@@ -1334,10 +1375,10 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
         lo[w] = (int)(__builtin_amdgcn_perm(c23, c01, 0x06040200u) ^ 0x80808080u);
       }
       const int o = ((seg >> 1) * 64 + pl) * 16 + (seg & 1) * 8;
-      *reinterpret_cast<v2i*>(sg + o) = v2i{hi[0], hi[1]};
-      *reinterpret_cast<v2i*>(sg + 4 * 64 * 16 + o) = v2i{lo[0], lo[1]};
-    } else {
-      if (tid < 256) *reinterpret_cast<v4i*>(sg + ((tid & 3) * 64 + (tid >> 2)) * 16) = gr;
+      *reinterpret_cast<v2i*>(pl8 + o) = v2i{hi[0], hi[1]};
+      *reinterpret_cast<v2i*>(pl8 + 4 * 64 * 16 + o) = v2i{lo[0], lo[1]};
+    } else if (tid < 256) {
+      *reinterpret_cast<v4i*>(pl8 + ((tid & 3) * 64 + (tid >> 2)) * 16) = *reinterpret_cast<const v4i*>(raw + tid * 16);
     }
   };
 
@@ -1355,32 +1396,66 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
 #pragma unroll
     for (int h = 0; h < NP; ++h) ag[c][h] = v4i{0, 0, 0, 0};
   const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
-  const int8_t* xs = sx + ws * kW3Win * 16;
+  constexpr int G1 = NXW + 1;  // DMA instructions per wave per chunk
 
-  if (c0 < c1) load(c0);
-  for (int64_t c = c0; c < c1; ++c) {
-    __syncthreads();  // every wave's reads of the previous chunk are done
-    stage();
-    if (c + 1 < c1) load(c + 1);  // in flight during this chunk's MFMAs
-    __syncthreads();
+  // chunk k's MFMAs; the A fragment of tap t + 1 is read while tap t's MFMAs run
+  auto mma = [&](int k) {
+    const uint32_t xs = lbase + (uint32_t)((k % S) * STG + ws * kW3Win * 16);
+    const uint32_t gp = lbase + (uint32_t)(S * STG + (k & 1) * PB);
     v4i bf[2][NP];
 #pragma unroll
     for (int cs = 0; cs < 2; ++cs)
 #pragma unroll
       for (int h = 0; h < NP; ++h) {
-        bf[cs][h] = tr_frag2(sg + ((h * 4 + 2 * wh + cs) * 64) * 16, oga, ogb);
-        if (do_ag) ag[cs][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[cs][h], ag[cs][h], 0, 0, 0);
+        const uint32_t b = gp + (uint32_t)(((h * 4 + 2 * wh + cs) * 64) * 16);
+        bf[cs][h] = tr_frag_asm(b + oga, b + ogb);
       }
+    v4i af = tr_frag_asm(xs + oxa, xs + oxb);
+#pragma unroll
+    for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+      for (int h = 0; h < NP; ++h) tr_wait(bf[cs][h]);
+    tr_wait(af);
+    if (do_ag) {
+#pragma unroll
+      for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+        for (int h = 0; h < NP; ++h) ag[cs][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[cs][h], ag[cs][h], 0, 0, 0);
+    }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int toff = ((t / 3) * Wp + t % 3) * 16;
-      const v4i af = tr_frag2(xs, oxa + toff, oxb + toff);
+      v4i an = af;
+      if (t < 8) {
+        const uint32_t toff = (uint32_t)((((t + 1) / 3) * Wp + (t + 1) % 3) * 16);
+        an = tr_frag_asm(xs + oxa + toff, xs + oxb + toff);
+      }
       if (do_ax) ax[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, ones, ax[t], 0, 0, 0);
 #pragma unroll
       for (int cs = 0; cs < 2; ++cs)
 #pragma unroll
         for (int h = 0; h < NP; ++h) acc[t][cs][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[cs][h], acc[t][cs][h], 0, 0, 0);
+      if (t < 8) {
+        tr_wait(an);
+        af = an;
+      }
     }
+  };
+
+  if (nc > 0) {
+#pragma unroll
+    for (int k = 0; k < S - 1; ++k) issue(k, k);
+    vm_wait<(S - 2) * G1>();  // chunk 0 landed
+    __builtin_amdgcn_s_barrier();
+    split_g(0, 0);
+    for (int k = 0; k < nc; ++k) {
+      vm_wait<(S - 3) * G1>();  // chunk k + 1 landed (this wave's part)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's plane writes of chunk k
+      __builtin_amdgcn_s_barrier();  // every wave's DMA of k + 1 and planes of k; chunk k - 1's readers done
+      if (!(dbg & 1)) issue(k + S - 1, (k + S - 1) % S);
+      split_g((k + 1) % S, (k + 1) & 1);  // past the last chunk: a harmless split of a stale stage
+      mma(k);
+    }
+    vm_wait<0>();  // no DMA may still write LDS when the workgroup ends
   }
   // ---- the row / column sums to every wave, then one exact int64 per output
   if (do_ax && j == 0) {
@@ -1396,7 +1471,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
       for (int h = 0; h < NP; ++h) sag[h * 64 + (2 * wh + cs) * 16 + j] = ag[cs][h][0];
   }
   __syncthreads();
-  const long long npix = (long long)(c1 - c0) * 64;
+  const long long npix = (long long)nc * 64;
   long long* dst = slab + (int64_t)split * 9 * Cin * Cout;
 #pragma unroll
   for (int cs = 0; cs < 2; ++cs) {
@@ -1416,6 +1491,21 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
         dst[((int64_t)t * Cin + cb * 64 + cl) * Cout + co] = v;
       }
   }
+}
+
+template <bool G16, int NXW>
+void wgrad3_launch(const int8_t* xq, const void* gq, const lbt_conv_desc& d, long long* slab, int nsplit, dim3 grid,
+                   int dbg, hipStream_t st) {
+  constexpr int S = 4;
+  constexpr int PB = (G16 ? 2 : 1) * 4 * 64 * 16;
+  constexpr size_t shm = (size_t)S * (4 * kW3Win * 16 + 64 * 64 * (G16 ? 2 : 1)) + 2 * PB + 1024;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad3_kernel<G16, NXW, S>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((wgrad3_kernel<G16, NXW, S>), grid, dim3(512), shm, st, xq, gq, d, slab, nsplit, dbg);
 }
 
 bool wgrad3_ok(const lbt_conv_desc& d) {
@@ -1465,10 +1555,17 @@ extern "C" int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int3
     // <= 1024 chunks a split: every int32 MFMA sum stays below 2^31 (64 products of |x' g| <= 2^14 a chunk)
     if (nsplit > chunks || (chunks + nsplit - 1) / nsplit > 1024 || nblk * nsplit > 0x7fffffff) return LBT_EINVAL;
     const dim3 grid((unsigned)(nblk * nsplit));
-    if (g_i16)
-      hipLaunchKernelGGL((wgrad3_kernel<true>), grid, dim3(512), 0, st, xq, gq, d, (long long*)slab, nsplit);
-    else
-      hipLaunchKernelGGL((wgrad3_kernel<false>), grid, dim3(512), 0, st, xq, gq, d, (long long*)slab, nsplit);
+    static const int dbg = getenv_int("LBT_WGRAD3_DBG", 0);  // diagnostics: 1 = no DMA after the prologue
+    const int win = (RB + 2) * (d.W + 2);
+    const bool two = 4 * ((win + 63) / 64) > 8;  // X DMA instructions per wave per chunk: 1 or 2
+    long long* sl = (long long*)slab;
+    if (g_i16) {
+      if (two) wgrad3_launch<true, 2>(xq, gq, d, sl, nsplit, grid, dbg, st);
+      else wgrad3_launch<true, 1>(xq, gq, d, sl, nsplit, grid, dbg, st);
+    } else {
+      if (two) wgrad3_launch<false, 2>(xq, gq, d, sl, nsplit, grid, dbg, st);
+      else wgrad3_launch<false, 1>(xq, gq, d, sl, nsplit, grid, dbg, st);
+    }
     return (int)hipGetLastError();
   }
   const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
