@@ -1097,9 +1097,9 @@ class ResidualBottleneck_q(ResidualBlock_q):
         (int8 codes straight from the MFMA accumulators), else fp32 y + the quantise pass."""
         kh, kw, Cin, Cout = conv.ksize
         d = ops.conv_desc(N, H, W, Cin, Cout, kh, kw, conv.strides[1], conv.strides[2], conv.padding)
-        # the quantising epilogue is exact but measured slower than fp32 y + the quantise pass on
-        # MI355X (its Philox / ballot / byte-store work lands on the GEMM's critical path): opt-in
-        if ops.igemm_workspace_bytes(d, 0, False) or os.environ.get("LBT_FUSE_CONV_QUANT", "0") != "1":
+        # the quantising epilogue (exact): with the 256-row LDS-DMA GEMM it beats fp32 y + the quantise
+        # pass by 0.2-0.5 ms per ResNet-50 step (round 3 A/B; with the round-2 GEMM it lost); LBT_FUSE_CONV_QUANT=0: off
+        if ops.igemm_workspace_bytes(d, 0, False) or os.environ.get("LBT_FUSE_CONV_QUANT", "1") != "1":
             y = conv.fwd_codes(xq, N, H, W)
             ResidualBottleneck_q._norm_in(bn, y, ctx)
             return y
