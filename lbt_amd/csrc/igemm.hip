@@ -1303,8 +1303,11 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
   const uint32_t lbase = (uint32_t)(uintptr_t)(lds_i8*)lds;  // LDS byte address of the ring
   const int ws = wave & 3, wh = wave >> 2;
   const bool do_ax = G16 && wh == 0, do_ag = ws == 0;
-  // transposed-read offsets: pixels pa = 16q + j/2 and pa + 8 of the chunk (X: clamped to the chunk)
-  const int pa = 16 * q + (j >> 1), pb = pa + 8;
+  // transposed-read offsets (X: clamped to the chunk). Lane group q supplies k = pixels 8q .. 8q+7 (first
+  // read) and 32+8q .. 32+8q+7 (second) -- any k order serves, A and B use the same -- so lanes 0-31 of
+  // each ds_read_b64_tr_b8 cover 16 consecutive 16-byte rows (all 64 banks once; pixels 16q + j/2 put
+  // lane groups 0 and 1 on the same 32 banks: 2-way conflicts)
+  const int pa = 8 * q + (j >> 1), pb = pa + 32;
   const int xa = pa < NPX ? pa : NPX - 1, xb = pb < NPX ? pb : NPX - 1;
   const int oxa = ((xa / W) * Wp + xa % W) * 16 + 8 * (j & 1);
   const int oxb = ((xb / W) * Wp + xb % W) * 16 + 8 * (j & 1);
@@ -1452,8 +1455,8 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's plane writes of chunk k
       __builtin_amdgcn_s_barrier();  // every wave's DMA of k + 1 and planes of k; chunk k - 1's readers done
       if (!(dbg & 1)) issue(k + S - 1, (k + S - 1) % S);
-      split_g((k + 1) % S, (k + 1) & 1);  // past the last chunk: a harmless split of a stale stage
       mma(k);
+      split_g((k + 1) % S, (k + 1) & 1);  // in the MFMAs' shadow; past the last chunk: a harmless stale split
     }
     vm_wait<0>();  // no DMA may still write LDS when the workgroup ends
   }
