@@ -306,7 +306,9 @@ typedef struct lbt_chain_branch {
  *   v = b1 (+ b2 if has_b2) (+ res[e] if res) ; if relu: v = max(0, v)
  *   (ResidualBlock_q :858-863: relu(y1 + y2))
  *   y = v (fp32, if y != NULL); o1 = Q(v, qo1) and o2 = Q(v, qo2) in o*_kind if != NULL
- *   (the next layers' input quantisers, e.g. Conv2d_q X at bits+1 in LBT_OUT_U8OFF).        */
+ *   (the next layers' input quantisers, e.g. Conv2d_q X at bits+1 in LBT_OUT_U8OFF).
+ *   ybits (optional, C % 4 == 0): ybits[e / 4] bit k = (v[e + k] > 0) for every channel quad
+ *   e = 4j -- the ReLU mask of y in 1/32 of y's bytes (lbt_bn_bwd_a_wide_masked's y_bits).      */
 typedef struct lbt_chain_fwd {
   lbt_chain_branch b1, b2; int32_t has_b2;
   const float* res; int32_t relu;
@@ -314,6 +316,7 @@ typedef struct lbt_chain_fwd {
   void* o1; int32_t o1_kind; lbt_qdesc qo1;
   void* o2; int32_t o2_kind; lbt_qdesc qo2;
   int64_t rows, inner; int32_t C;
+  uint8_t* ybits;
 } lbt_chain_fwd;
 int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream);
 
@@ -498,8 +501,10 @@ int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* qn, lbt_qde
  * straight into the consuming conv's 9..16-bit gradient quantiser qo (int16 codes gq, overflow
  * counters, noise period inner) instead of storing dx. g2 (optional): the incoming gradient is
  * g + g2 (the block's two branch gradients, ResidualBlock_q.backward :865-869, summed here
- * instead of in their own pass). Bit-identical to the unfused sequence.                      */
-int lbt_bn_bwd_a_wide_masked(const float* g, const float* g2, const float* y_mask, int32_t mask_r, lbt_qdesc qr,
+ * instead of in their own pass). y_bits (instead of y_mask): the mask as lbt_chain_fwd's ybits
+ * (one byte per channel quad). Bit-identical to the unfused sequence.                         */
+int lbt_bn_bwd_a_wide_masked(const float* g, const float* g2, const float* y_mask, const uint8_t* y_bits,
+                             int32_t mask_r, lbt_qdesc qr,
                              const float* gb,
                              float* gmask_out, lbt_qdesc qrg, const int8_t* R, lbt_qdesc qng, const int8_t* qn,
                              int16_t* gout, float* dout, int64_t* sums, int64_t rows, int64_t inner, int32_t C,

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -54,7 +54,7 @@ class ChainFwd(ctypes.Structure):
                 ("res", c_void_p), ("relu", c_int32), ("y", c_void_p),
                 ("o1", c_void_p), ("o1_kind", c_int32), ("qo1", QDesc),
                 ("o2", c_void_p), ("o2_kind", c_int32), ("qo2", QDesc),
-                ("rows", c_int64), ("inner", c_int64), ("C", c_int32)]
+                ("rows", c_int64), ("inner", c_int64), ("C", c_int32), ("ybits", c_void_p)]
 
 
 class BwdBranch(ctypes.Structure):
@@ -211,7 +211,7 @@ _SIGS = {
     "lbt_dense_pack": [_P, c_int32, c_int32, _P, c_int32, _P, c_int32, _P],
     "lbt_flat_weight_blocks": [c_int64],
     "lbt_dfxp_quantize_weights_flat": [_P, _P, c_int32, c_int32, _P],
-    "lbt_bn_bwd_a_wide_masked": [_P, _P, _P, c_int32, QDesc, _P, _P, QDesc, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64,
+    "lbt_bn_bwd_a_wide_masked": [_P, _P, _P, _P, c_int32, QDesc, _P, _P, QDesc, _P, QDesc, _P, _P, _P, _P, c_int64, c_int64,
                                  c_int32, _P],
     "lbt_bn_bwd_b_wide_q": [_P, QDesc, _P, QDesc, _P, _P, c_int64, _P, QDesc, c_int64, c_int64, c_int32, _P],
     "lbt_dense_gemm": [_P, c_int32, c_int32, c_int32, _P, c_int32, c_int32, c_int32, QDesc, QDesc, _P, _P],

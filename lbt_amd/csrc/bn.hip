@@ -259,6 +259,8 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
           for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
         }
         if (ystore) store4_f32(a.y, e, v);
+        if (a.ybits)  // uniform
+          a.ybits[e >> 2] = (uint8_t)((v[0] > 0.f) | ((v[1] > 0.f) << 1) | ((v[2] > 0.f) << 2) | ((v[3] > 0.f) << 3));
         if (o1) {
           int c[4];
 #pragma unroll

@@ -43,6 +43,7 @@ struct WideA {
   float* gmask_out;
   const float* g2;       // optional second summand of the incoming gradient: g + g2 (ResidualBlock_q
                          // .backward's add of the two branch gradients, :865-869, done here)
+  const uint8_t* y_bits; // the y_mask > 0 mask as one byte per channel quad (lbt_chain_fwd.ybits)
 };
 
 // Thread = 4 consecutive channels (one Philox4x32 call covers their 4 noise values) x one pixel.
@@ -79,6 +80,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn
   const float* __restrict__ gp = a.g;
   const float* __restrict__ g2p = YM ? a.g2 : nullptr;
   const float* __restrict__ ymp = YM ? a.y_mask : nullptr;
+  const uint8_t* __restrict__ ybp = YM ? a.y_bits : nullptr;
   const int8_t* __restrict__ Rp = a.R;
   const int8_t* __restrict__ qnp = a.qn;
   const bool needR = a.mask_r || srg.active;
@@ -93,6 +95,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn
     for (int64_t nb = n0; nb < n1; nb += U) {
       float4 gv[U], g2v[YM ? U : 1], ym[YM ? U : 1];
       char4 rv[U], qv[U];
+      uint32_t yb[YM ? U : 1];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t n = nb + u < n1 ? nb + u : nb;
@@ -100,6 +103,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn
         gv[u] = *reinterpret_cast<const float4*>(gp + e);
         if (YM && g2p) g2v[u] = *reinterpret_cast<const float4*>(g2p + e);
         if (YM && ymp) ym[u] = *reinterpret_cast<const float4*>(ymp + e);
+        if (YM && ybp) yb[u] = ybp[e >> 2];
         if (needR) rv[u] = *reinterpret_cast<const char4*>(Rp + e);
         if (sng.active) qv[u] = *reinterpret_cast<const char4*>(qnp + e);
       }
@@ -116,6 +120,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn
           const float m[4] = {ym[u].x, ym[u].y, ym[u].z, ym[u].w};
 #pragma unroll
           for (int k = 0; k < 4; ++k) d[k] = m[k] > 0.f ? d[k] : 0.f;
+        } else if (YM && ybp) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[k] = ((yb[u] >> k) & 1u) ? d[k] : 0.f;
         } else if (a.mask_r) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {  // bn.hip chain_bwd_a's recomputation, op for op
@@ -333,7 +340,7 @@ int launch_a(WideA a, int cb, hipStream_t st) {
   const int64_t zb = (a.samples + a.spb - 1) / a.spb;
   if (yb > 65535 || zb > 65535 || a.spb > kRowsA) return LBT_EINVAL;
   const dim3 grid((unsigned)cb, (unsigned)yb, (unsigned)zb);
-  if (a.y_mask || a.g2)
+  if (a.y_mask || a.y_bits || a.g2)
     hipLaunchKernelGGL(bn_bwd_a_wide_kernel<true>, grid, dim3(kT), 0, st, a);
   else
     hipLaunchKernelGGL(bn_bwd_a_wide_kernel<false>, grid, dim3(kT), 0, st, a);
@@ -348,7 +355,7 @@ extern "C" int lbt_bn_bwd_a_wide(const float* g, lbt_qdesc qrg, const int8_t* R,
   if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gamma_q)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
   WideA a{g, qrg, R, gamma_q, qng, qn, gout, dout, sums, rows, inner, C, 0, 0, 0, nullptr, 0, lbt_qdesc{}, nullptr,
-          nullptr, nullptr};
+          nullptr, nullptr, nullptr};
   return launch_a(a, (C + kCB - 1) / kCB, (hipStream_t)stream);
 }
 
@@ -363,14 +370,17 @@ extern "C" int lbt_bn_bwd_b_wide(const int16_t* G, lbt_qdesc qng, const int8_t* 
 
 // Pass A with the ReLU mask folded in (y_mask, or mask_r: recomputed from R with qr and
 // gb = [gamma_q | beta_q]) and the masked gradient optionally stored (gmask_out).
-extern "C" int lbt_bn_bwd_a_wide_masked(const float* g, const float* g2, const float* y_mask, int32_t mask_r, lbt_qdesc qr,
+extern "C" int lbt_bn_bwd_a_wide_masked(const float* g, const float* g2, const float* y_mask, const uint8_t* y_bits,
+                                        int32_t mask_r, lbt_qdesc qr,
                                         const float* gb, float* gmask_out, lbt_qdesc qrg, const int8_t* R,
                                         lbt_qdesc qng, const int8_t* qn, int16_t* gout, float* dout, int64_t* sums,
                                         int64_t rows, int64_t inner, int32_t C, void* stream) {
   if (rows <= 0 || C <= 0 || C % 4 || inner <= 0 || inner % C) return LBT_EINVAL;
   if ((qrg.bits > 0 && (!R || !gb)) || (qng.bits > 0 && (!qn || !gout))) return LBT_EINVAL;
-  if (mask_r && (y_mask || !R || !gb || qr.bits <= 0)) return LBT_EINVAL;
-  WideA a{g, qrg, R, gb, qng, qn, gout, dout, sums, rows, inner, C, 0, 0, 0, y_mask, mask_r, qr, gb, gmask_out, g2};
+  if (mask_r && (y_mask || y_bits || !R || !gb || qr.bits <= 0)) return LBT_EINVAL;
+  if (y_mask && y_bits) return LBT_EINVAL;
+  WideA a{g, qrg, R, gb, qng, qn, gout, dout, sums, rows, inner, C, 0, 0, 0, y_mask, mask_r, qr, gb, gmask_out, g2,
+          y_bits};
   return launch_a(a, (C + kCB - 1) / kCB, (hipStream_t)stream);
 }
 

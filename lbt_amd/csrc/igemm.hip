@@ -1070,23 +1070,43 @@ constexpr int kWP = 64;
 
 // STORE: the workgroup's partial is STORED into slab[split] (every element of slab[nsplit][K][Cout]
 // has exactly one writer -- no zeroing, no atomics); else atomically added into shard split % nshard.
+// Grid: 1-D over (split, tap x ci block, co block). xmap = 1 (default): XCD-aware order -- the
+// workgroups of one pixel split (every ci / co block, which share that split's X and G chunks) are
+// consecutive on ONE XCD, meant to serve the Cout/64-fold X and Cin/64-fold G re-reads of a 64 x 64 tile
+// from that XCD's L2 (LBT_WGRAD_XMAP=1; measured 0.3 ms per ResNet-50 step SLOWER); xmap = 0 (default):
+// split fastest (the former 3-D grid's order).
 template <bool G16, bool STORE>
 __global__ __launch_bounds__(kT, 1) void wgrad_wide_kernel(const int8_t* __restrict__ xq, const void* __restrict__ gq,
                                                         lbt_conv_desc d, long long* __restrict__ slab, int64_t P,
-                                                        int nsplit, int nshard) {
+                                                        int nsplit, int nshard, int xmap) {
   constexpr int NG = G16 ? 2 : 1;  // G images: (gh, gl') or g
   constexpr int NBS = 4, COW = 16 * NBS;  // output-channel slices per workgroup
   // per wave: X [4 slices][64 px][16 B], G [NG][4 slices][64 px][16 B]; reused as the int64 tile
   __shared__ __attribute__((aligned(16))) int8_t lds[4][(4 + NBS * NG) * kWP * 16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
-  const int cib = d.Cin / 64;
-  const int tap = blockIdx.y / cib, cb = blockIdx.y - tap * cib, ob = blockIdx.z;
+  const int cib = d.Cin / 64, cob = d.Cout / 64;
+  const uint32_t gy = (uint32_t)(d.KH * d.KW * cib), nblk = gy * (uint32_t)cob;
+  uint32_t split, by, ob_;
+  if (xmap) {
+    const uint32_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+    const uint32_t t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+    split = t / nblk;
+    const uint32_t b = t - split * nblk;
+    by = b / (uint32_t)cob;
+    ob_ = b - by * (uint32_t)cob;
+  } else {
+    split = blockIdx.x % (uint32_t)nsplit;
+    const uint32_t b = blockIdx.x / (uint32_t)nsplit;
+    ob_ = b / gy;
+    by = b - ob_ * gy;
+  }
+  const int tap = (int)by / cib, cb = (int)by - tap * cib, ob = (int)ob_;
   const int kh = tap / d.KW, kw = tap - kh * d.KW;
   int8_t* Xi = lds[wave];
   int8_t* Gi = lds[wave] + 4 * kWP * 16;
   const int64_t per = (P + nsplit - 1) / nsplit;
-  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p0 = (int64_t)split * per;
   const int64_t p1 = p0 + per < P ? p0 + per : P;
   const uint32_t HWo = (uint32_t)d.Ho * d.Wo;
   v4i acc[NG][4][NBS], ax[4], ag[NG][NBS];
@@ -1219,7 +1239,7 @@ __global__ __launch_bounds__(kT, 1) void wgrad_wide_kernel(const int8_t* __restr
     }
     __syncthreads();
   }
-  const int64_t shard = STORE ? (int64_t)blockIdx.x : (int64_t)(blockIdx.x % nshard);
+  const int64_t shard = STORE ? (int64_t)split : (int64_t)(split % (uint32_t)nshard);
   long long* dst = slab + (shard * (d.KH * d.KW) + tap) * d.Cin * d.Cout;
   for (int i = threadIdx.x; i < 64 * COW; i += kT) {
     const long long v = tile[i];
@@ -1519,6 +1539,196 @@ bool wgrad3_ok(const lbt_conv_desc& d) {
   return (RB + 2) * (d.W + 2) <= kW3Win;
 }
 
+// ----------------------------------------------------------------------------- 1x1 wgrad, 16-bit G
+// wgrad1_kernel: a 1x1 conv's weight gradient (pad 0, any stride) with 16-bit gradient codes on a
+// workgroup tile of (64 WCI) ci x (32 WCO) co, WCI x WCO = 8 waves of 64 ci x 32 co (wgrad_wide_kernel's
+// 64 x 64 tile re-read X Cout/64 times and G Cin/64 times: ~616 MB of operand loads per ResNet-50 1x1
+// conv against 100-460 MB of data). A chunk = 64 pixels (the MFMA k); every operand image is
+// [64 px][16 B] -- an X slice of 16 ci, or a RAW G group of 8 co as (lo, hi) byte pairs -- moved by
+// LDS-DMA through an S-stage ring with one barrier per chunk. The raw G image needs no split pass:
+// a transposed read gives lane i byte i of each pixel's 16 bytes, i.e. column i = (co i / 2, byte
+// i & 1), so the MFMA runs on 16 "columns" of 8 co x (lo, hi); the lo lanes XOR their bytes with
+// 0x80 (lo' = lo - 128, signed), and the epilogue joins lane pairs:
+//   sum x g = 256 sum x' gh + sum x' gl' + 128 sum x' + 128 (256 sum gh + sum gl' + 128 npix)
+// (x' = x - 128; every processed pixel counts, padding ones carry x' = -128, g = 0, which the
+// identity cancels). Every (split, ci, co) has one writer: STORED into slab[split][Cin][Cout].
+template <int WCI, int S>
+__global__ __launch_bounds__(512, 1) void wgrad1_kernel(const int8_t* __restrict__ xq, const int16_t* __restrict__ gq,
+                                                      lbt_conv_desc d, long long* __restrict__ slab, int nsplit) {
+  constexpr int WCO = 8 / WCI;
+  constexpr int TCI = 64 * WCI, TCO = 32 * WCO;     // workgroup tile
+  constexpr int NXS = TCI / 16, NGG = TCO / 8;       // X slices, G groups (1 KiB images each)
+  constexpr int NXW = (NXS + 7) / 8, NGW = NGG / 8;  // DMA instructions per wave per chunk
+  constexpr int G1 = NXW + NGW;
+  constexpr int STG = (NXS + NGG) * 1024;
+  static_assert(NGG % 8 == 0, "geometry");
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  int8_t* const dummy = lds + S * STG;  // 1 KiB sink of idle X slots
+  __shared__ int sax[TCI];              // sum_p x' per ci
+  __shared__ int sag[2 * TCO];          // sum_p of each raw-G column (co, byte)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 15, q = lane >> 4;
+  const int wci = wave / WCO, wco = wave - wci * WCO;
+  const int Cin = d.Cin, Cout = d.Cout;
+  const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
+  const int64_t TC = (P + 63) / 64;
+  const int cbn = Cin / TCI, obn = Cout / TCO, nblk = cbn * obn;
+  const int blk = (int)(blockIdx.x % (uint32_t)nblk), split = (int)(blockIdx.x / (uint32_t)nblk);
+  const int cb = blk / obn, ob = blk - cb * obn;
+  const int64_t c0 = TC * split / nsplit, c1 = TC * (split + 1) / nsplit;
+  const int nc = (int)(c1 - c0);
+  typedef __attribute__((address_space(3))) int8_t lds_i8;
+  const uint32_t lbase = (uint32_t)(uintptr_t)(lds_i8*)lds;
+  const bool do_ax = wco == 0, do_ag = wci == 0;
+  // transposed-read offsets: lane group q supplies k = pixels 8q .. 8q+7 (first read), 32 + 8q .. (second)
+  const int pa = 8 * q + (j >> 1);
+  const int oa = pa * 16 + 8 * (j & 1), ob2 = oa + 32 * 16;
+  const uint32_t hwo = (uint32_t)d.Ho * d.Wo;
+  const bool unit = d.SH == 1 && d.SW == 1 && d.Ho == d.H && d.Wo == d.W;
+
+  auto issue = [&](int k, int st) {
+    const int64_t p = (c0 + k) * 64 + lane;
+    const bool pv = p < P;
+    const uint32_t pu = (uint32_t)(pv ? p : 0);
+    uint32_t xp = pu;
+    if (!unit) {
+      const uint32_t n = pu / hwo, rem = pu - n * hwo, oh = rem / (uint32_t)d.Wo, ow = rem - oh * (uint32_t)d.Wo;
+      xp = (n * (uint32_t)d.H + oh * (uint32_t)d.SH) * (uint32_t)d.W + ow * (uint32_t)d.SW;
+    }
+    int8_t* sb = lds + st * STG;
+    const int8_t* xs = xq + (int64_t)xp * Cin + cb * TCI;
+#pragma unroll
+    for (int u = 0; u < NXW; ++u) {
+      const int sl = wave + 8 * u;
+      const bool real = sl < NXS;
+      const int8_t* src = (pv && real) ? xs + sl * 16 : reinterpret_cast<const int8_t*>(kFill80);
+      int8_t* dst = real ? sb + sl * 1024 : dummy;
+      __builtin_amdgcn_global_load_lds(src, (lds_vptr)dst, 16, 0, 0);
+    }
+    const int8_t* gs = reinterpret_cast<const int8_t*>(gq + (int64_t)pu * Cout + ob * TCO);
+#pragma unroll
+    for (int u = 0; u < NGW; ++u) {
+      const int g = wave + 8 * u;
+      const int8_t* src = pv ? gs + g * 16 : reinterpret_cast<const int8_t*>(zi());
+      __builtin_amdgcn_global_load_lds(src, (lds_vptr)(sb + (NXS + g) * 1024), 16, 0, 0);
+    }
+  };
+
+  v4i acc[4][4], ax[4], ag[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    ax[a] = v4i{0, 0, 0, 0};
+    ag[a] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
+  }
+  const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
+  const int lox = (j & 1) ? 0 : (int)0x80808080u;  // lo-byte columns: lo' = lo ^ 0x80
+
+  auto mma = [&](int k) {
+    const uint32_t sb = lbase + (uint32_t)((k % S) * STG);
+    v4i af[4], bf[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t g = sb + (uint32_t)((NXS + wco * 4 + b) * 1024);
+      bf[b] = tr_frag_asm(g + oa, g + ob2);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const uint32_t x = sb + (uint32_t)((wci * 4 + a) * 1024);
+      af[a] = tr_frag_asm(x + oa, x + ob2);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      tr_wait(bf[b]);
+      bf[b] = bf[b] ^ v4i{lox, lox, lox, lox};
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) tr_wait(af[a]);
+    if (do_ag) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) ag[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, bf[b], ag[b], 0, 0, 0);
+    }
+    if (do_ax) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) ax[a] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], ones, ax[a], 0, 0, 0);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+  };
+
+  if (nc > 0) {
+#pragma unroll
+    for (int k = 0; k < S - 1; ++k) issue(k < nc ? k : nc - 1, k);
+    for (int k = 0; k < nc; ++k) {
+      vm_wait<(S - 2) * G1>();       // chunk k landed (this wave's part)
+      __builtin_amdgcn_s_barrier();  // every wave's part of chunk k; chunk k - 1's readers done
+      const int nx = k + S - 1;
+      issue(nx < nc ? nx : nc - 1, nx % S);
+      mma(k);
+    }
+    vm_wait<0>();  // no DMA may still write LDS when the workgroup ends
+  }
+  // ---- sums to every wave; lo lanes (even columns) join their hi partner and store
+  if (do_ax && j == 0) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sax[(wci * 4 + a) * 16 + 4 * q + i] = ax[a][i];
+  }
+  if (do_ag && q == 0) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) sag[(wco * 4 + b) * 16 + j] = ag[b][0];
+  }
+  __syncthreads();
+  const long long npix = (long long)nc * 64;
+  long long* dst = slab + (int64_t)split * Cin * Cout;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int colg = (wco * 4 + b) * 16 + (j & ~1);  // this pair's lo column in the tile
+    const long long sgc = 256ll * sag[colg + 1] + (long long)sag[colg] + 128ll * npix;  // sum_p g[co]
+    const int co = ob * TCO + (wco * 4 + b) * 8 + (j >> 1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hi = __shfl_xor(acc[a][b][i], 1, 64);
+        const int cl = (wci * 4 + a) * 16 + 4 * q + i;
+        const long long v = 256ll * hi + (long long)acc[a][b][i] + 128ll * sax[cl] + 128ll * sgc;
+        if (!(j & 1)) dst[(int64_t)(cb * TCI + cl) * Cout + co] = v;
+      }
+  }
+}
+
+// the 1x1 body's tile: 0 = not taken, else WCI (waves along ci; 8 / WCI along co)
+int wgrad1_wci(const lbt_conv_desc& d) {
+  if (d.KH != 1 || d.KW != 1 || d.PT || d.PL || d.PB < 0 || d.PR < 0 || (d.Ho - 1) * d.SH >= d.H ||
+      (d.Wo - 1) * d.SW >= d.W)
+    return 0;
+  if (d.Cin % 128 == 0 && d.Cout % 128 == 0) return 2;
+  if (d.Cin % 64 == 0 && d.Cout % 256 == 0) return 1;
+  if (d.Cin % 256 == 0 && d.Cout % 64 == 0) return 4;
+  return 0;
+}
+
+template <int WCI>
+void wgrad1_launch(const int8_t* xq, const int16_t* gq, const lbt_conv_desc& d, long long* slab, int nsplit,
+                   hipStream_t st) {
+  constexpr int S = 3, WCO = 8 / WCI;
+  constexpr size_t shm = (size_t)S * (4 * WCI + 4 * WCO) * 1024 + 1024;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1_kernel<WCI, S>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    return true;
+  }();
+  (void)attr;
+  const int64_t nblk = (int64_t)(d.Cin / (64 * WCI)) * (d.Cout / (32 * WCO));
+  hipLaunchKernelGGL((wgrad1_kernel<WCI, S>), dim3((unsigned)(nblk * nsplit)), dim3(512), shm, st, xq, gq, d, slab,
+                     nsplit);
+}
+
 }  // namespace
 
 // wide wgrad: x offset int8 codes (q - 128), g int8 (g_i16 = 0) or int16 codes; adds into a
@@ -1528,16 +1738,17 @@ extern "C" int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_
   if (!desc_ok(d) || d.Cin % 64 || d.Cout % 64 || nsplit <= 0 || nshard <= 0 || nshard > nsplit) return LBT_EINVAL;
   const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
   if (P >= ((int64_t)1 << 31)) return LBT_EINVAL;
-  const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
-  if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
-  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
+  const int64_t nwg = (int64_t)d.KH * d.KW * (d.Cin / 64) * (d.Cout / 64) * nsplit;
+  if (nwg > 0x7fffffff) return LBT_EINVAL;
+  const dim3 grid((unsigned)nwg);
+  static const int xmap = getenv_int("LBT_WGRAD_XMAP", 0);
   hipStream_t st = (hipStream_t)stream;
   if (g_i16)
     hipLaunchKernelGGL((wgrad_wide_kernel<true, false>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
-                       nshard);
+                       nshard, xmap);
   else
     hipLaunchKernelGGL((wgrad_wide_kernel<false, false>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
-                       nshard);
+                       nshard, xmap);
   return (int)hipGetLastError();
 }
 
@@ -1571,14 +1782,29 @@ extern "C" int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int3
     }
     return (int)hipGetLastError();
   }
-  const int64_t gy = (int64_t)d.KH * d.KW * (d.Cin / 64);
-  if (gy > 65535 || d.Cout / 64 > 65535) return LBT_EINVAL;
-  dim3 grid((unsigned)nsplit, (unsigned)gy, (unsigned)(d.Cout / 64));
+  static const int w1 = getenv_int("LBT_WGRAD1", 1);
+  if (w1 && g_i16 && wgrad1_wci(d)) {  // 1x1, 16-bit G: (64 WCI) ci x (32 WCO) co workgroup tiles
+    const int wci = wgrad1_wci(d);
+    const int64_t chunks = (P + 63) / 64;
+    const int64_t nblk = (int64_t)(d.Cin / (64 * wci)) * (d.Cout / (256 / wci));
+    // <= 2048 chunks a split: every int32 MFMA sum stays below 2^31 (|x' g| <= 2^14 a pixel)
+    if (nsplit > chunks || (chunks + nsplit - 1) / nsplit > 2048 || nblk * nsplit > 0x7fffffff) return LBT_EINVAL;
+    const int16_t* g16 = reinterpret_cast<const int16_t*>(gq);
+    long long* sl = (long long*)slab;
+    if (wci == 2) wgrad1_launch<2>(xq, g16, d, sl, nsplit, st);
+    else if (wci == 1) wgrad1_launch<1>(xq, g16, d, sl, nsplit, st);
+    else wgrad1_launch<4>(xq, g16, d, sl, nsplit, st);
+    return (int)hipGetLastError();
+  }
+  const int64_t nwg = (int64_t)d.KH * d.KW * (d.Cin / 64) * (d.Cout / 64) * nsplit;
+  if (nwg > 0x7fffffff) return LBT_EINVAL;
+  const dim3 grid((unsigned)nwg);
+  static const int xmap = getenv_int("LBT_WGRAD_XMAP", 0);
   if (g_i16)
     hipLaunchKernelGGL((wgrad_wide_kernel<true, true>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
-                       nsplit);
+                       nsplit, xmap);
   else
     hipLaunchKernelGGL((wgrad_wide_kernel<false, true>), grid, dim3(kT), 0, st, xq, gq, d, (long long*)slab, P, nsplit,
-                       nsplit);
+                       nsplit, xmap);
   return (int)hipGetLastError();
 }

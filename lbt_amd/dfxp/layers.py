@@ -414,7 +414,7 @@ class Conv2d_q(Layer_q):
         """Weight gradient on the wide-layer MFMA kernel (int64 slab, one shard) + its reduce."""
         d = self.d
         K = d.KH * d.KW * d.Cin
-        ns = ops.wgrad_store_nsplit(d)
+        ns = ops.wgrad_store_nsplit(d, g_i16)
         slab = self._c.get("wslab64", (ns, K, d.Cout), torch.int64, self.ctx.device)  # fully written
         ops.conv_wgrad_igemm_store(self.xq, self.gradq, g_i16, d, slab, ns)
         ops.conv_wgrad_reduce64(slab, ns, K, d.Cout, self.X_range.desc, self.grad_range.desc, self.W,
@@ -1063,7 +1063,8 @@ class ResidualBottleneck_q(ResidualBlock_q):
             return self._backward_fused(grad)
 
     @staticmethod
-    def _chain(c, bn, y, relu, res=None, bn2=None, out=None, o1=None, o1_conv=None, o2=None, o2_conv=None):
+    def _chain(c, bn, y, relu, res=None, bn2=None, out=None, o1=None, o1_conv=None, o2=None, o2_conv=None,
+               ybits=None):
         """One forward element chain: bn (norm of its input codes -> rescale quantiser ->
         affine) [+ bn2 | + res] [-> ReLU] -> fp32 out and / or the next convs' X codes."""
         a = ChainFwd()
@@ -1081,6 +1082,7 @@ class ResidualBottleneck_q(ResidualBlock_q):
         a.res = res.data_ptr() if res is not None else None
         a.relu = int(relu)
         a.y = out.data_ptr() if out is not None else None
+        a.ybits = ybits.data_ptr() if ybits is not None else None
         if o1 is not None:
             o1_conv.X_range.observe(y.numel())
             a.o1, a.o1_kind, a.qo1 = o1.data_ptr(), OUT_U8OFF, o1_conv.X_range.desc
@@ -1160,18 +1162,22 @@ class ResidualBottleneck_q(ResidualBlock_q):
             o = dict(o1=nb._c.get("x1", y3.shape, torch.int8, dev), o1_conv=nb.residual.layers[0])
             if nsc:
                 o.update(o2=nb._c.get("xs", y3.shape, torch.int8, dev), o2_conv=nsc[0])
+        # the backward's ReLU mask as one byte per channel quad (pass A reads 1/16 of fp32 y's bytes)
+        ybits = (self._c.get("ybits", (y3.numel() // 4,), torch.uint8, dev)
+                 if os.environ.get("LBT_YBITS", "1") == "1" else None)
+        self.ybits = ybits
         if sc:
             self._conv_norm(sc[0], sc[1], xs, N, H, W, ctx)
-            self._chain(c3, bn3, y3, True, bn2=sc[1], out=out, **o)
+            self._chain(c3, bn3, y3, True, bn2=sc[1], out=out, ybits=ybits, **o)
         else:
-            self._chain(c3, bn3, y3, True, res=X, out=out, **o)
+            self._chain(c3, bn3, y3, True, res=X, out=out, ybits=ybits, **o)
         if nb is not None:
             nb._x_pre = out
         self.y = out
         return out
 
     @staticmethod
-    def _bn_bwd(bn, conv_out, g, ctx, y_mask=None, mask_r=False, gmask_out=None, g2=None):
+    def _bn_bwd(bn, conv_out, g, ctx, y_mask=None, mask_r=False, gmask_out=None, g2=None, y_bits=None):
         """One BN's backward with the ReLU mask in front (pass A: rescale + norm gradient
         quantisers, dgamma / dbeta), then pass B straight into the producing conv's 16-bit
         gradient quantiser: returns that conv's int16 gradient codes."""
@@ -1184,7 +1190,7 @@ class ResidualBottleneck_q(ResidualBlock_q):
         n.grad_range.observe(g.numel())
         G16 = n._c.get("G16", g.shape, torch.int16, dev)
         ops.bn_bwd_a_wide_masked(g, y_mask, mask_r, r.X_range.desc, r.gb, gmask_out, r.grad_range.desc, r.R,
-                                 n.grad_range.desc, n.q, G16, sums, rows, inner, C, g2=g2)
+                                 n.grad_range.desc, n.q, G16, sums, rows, inner, C, g2=g2, y_bits=y_bits)
         with side_work():
             ops.bn_param_grads(sums, C, r.grad_range.desc, r.X_range.desc, r.gamma, ops.f32(2 * r.weight_decay),
                                r.dgamma, r.dbeta)
@@ -1207,8 +1213,9 @@ class ResidualBottleneck_q(ResidualBlock_q):
         dev = gin.device
         # block ReLU mask from the block output; bn3 (and the shortcut bn) see the same masked g
         gmask = None if sc else self._c.get("gmask", gin.shape, torch.float32, dev)
-        g3 = self._bn_bwd(bn3, c3, gin, ctx, y_mask=self.y, gmask_out=gmask, g2=gin2)
-        gs = self._bn_bwd(sc[1], sc[0], gin, ctx, y_mask=self.y, g2=gin2) if sc else None
+        ym = dict(y_bits=self.ybits) if self.ybits is not None else dict(y_mask=self.y)
+        g3 = self._bn_bwd(bn3, c3, gin, ctx, gmask_out=gmask, g2=gin2, **ym)
+        gs = self._bn_bwd(sc[1], sc[0], gin, ctx, g2=gin2, **ym) if sc else None
         d3 = c3.bwd_codes16(g3)
         g2 = self._bn_bwd(bn2, c2, d3, ctx, mask_r=True)
         d2 = c2.bwd_codes16(g2)

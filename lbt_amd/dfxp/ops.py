@@ -362,9 +362,10 @@ def _chain_fwd_bytes(a):
         per += 1 if b.rout else 0
     per += 4 if a.res else 0
     per += 4 if a.y else 0
+    per += 0.25 if a.ybits else 0
     per += _code_bytes(a.o1_kind) if a.o1 else 0
     per += _code_bytes(a.o2_kind) if a.o2 else 0
-    return per * a.rows * a.inner
+    return int(per * a.rows * a.inner)
 
 
 def _chain_bwd_a_bytes(a):
@@ -588,11 +589,15 @@ def bn_bwd_b_wide(G, qng, qn, qn_q, ms, sums, n, dx, rows, C):
 
 
 # ---------------------------------------------------------------- wide layers (igemm.hip)
-def bn_bwd_a_wide_masked(g, y_mask, mask_r, qr, gb, gmask_out, qrg, R, qng, qn, gout, sums, rows, inner, C, g2=None):
+def bn_bwd_a_wide_masked(g, y_mask, mask_r, qr, gb, gmask_out, qrg, R, qng, qn, gout, sums, rows, inner, C, g2=None,
+                         y_bits=None):
+    """y_bits: the ReLU mask as chain_fwd's ybits (one byte per channel quad) instead of fp32 y_mask."""
     with _Timed("bn_bwd_a_wide_kernel", g.numel() * (4 + 1 + 1 + 2) + (4 * g.numel() if y_mask is not None else 0)
+                + (g.numel() // 4 if y_bits is not None else 0)
                 + (4 * g.numel() if gmask_out is not None else 0) + (4 * g.numel() if g2 is not None else 0)):
-        call("lbt_bn_bwd_a_wide_masked", ptr(g), ptr(g2), ptr(y_mask), int(mask_r), qr, ptr(gb), ptr(gmask_out), qrg, ptr(R),
-             qng, ptr(qn), ptr(gout), None, ptr(sums), int(rows), int(inner), int(C), stream())
+        call("lbt_bn_bwd_a_wide_masked", ptr(g), ptr(g2), ptr(y_mask), ptr(y_bits), int(mask_r), qr, ptr(gb),
+             ptr(gmask_out), qrg, ptr(R), qng, ptr(qn), ptr(gout), None, ptr(sums), int(rows), int(inner), int(C),
+             stream())
 
 
 def bn_bwd_b_wide_q(G, qng, qn, qn_q, ms, sums, n, gq, qo, rows, inner, C):
@@ -666,10 +671,35 @@ def wgrad3_ok(d):
     return (64 // d.W + 2) * (d.W + 2) <= 192
 
 
-def wgrad_store_nsplit(d):
+WGRAD1 = os.environ.get("LBT_WGRAD1", "1") != "0"
+
+
+def wgrad1_wci(d):
+    """lbt_conv_wgrad_igemm_store's 1x1 body (16-bit G) takes this conv with (64 wci) x (256 / wci)
+    channel tiles (wgrad1_wci in igemm.hip); 0: not taken."""
+    if not WGRAD1 or (d.KH, d.KW, d.PT, d.PL) != (1, 1, 0, 0) or d.PB < 0 or d.PR < 0:
+        return 0
+    if (d.Ho - 1) * d.SH >= d.H or (d.Wo - 1) * d.SW >= d.W:
+        return 0
+    if d.Cin % 128 == 0 and d.Cout % 128 == 0:
+        return 2
+    if d.Cin % 64 == 0 and d.Cout % 256 == 0:
+        return 1
+    if d.Cin % 256 == 0 and d.Cout % 64 == 0:
+        return 4
+    return 0
+
+
+def wgrad_store_nsplit(d, g_i16=True):
     """Pixel splits of the storing wide wgrad: >= ~512 workgroups, each split's slab written once.
     All-taps 3x3 body: splits of whole-row chunks, ~256 workgroups (one per CU; each covers all 9
-    taps of a 64 x 64 channel block), <= 1024 chunks a split."""
+    taps of a 64 x 64 channel block), <= 1024 chunks a split. 1x1 body (16-bit G): 64-pixel
+    chunks, ~512 workgroups, <= 2048 chunks a split."""
+    wci = wgrad1_wci(d) if g_i16 else 0
+    if wci:
+        chunks = -(-(d.N * d.Ho * d.Wo) // 64)
+        nblk = (d.Cin // (64 * wci)) * (d.Cout // (256 // wci))
+        return min(chunks, max(-(-chunks // 2048), -(-512 // nblk)))
     if wgrad3_ok(d):
         rb = 64 // d.W
         chunks = d.N * (-(-d.H // rb))

@@ -215,7 +215,7 @@ def test_wgrad_igemm_matches_generic(N, H, Cin, Cout, k, s):
             ref = torch.zeros((ns, K, Cout), dtype=torch.int32, device=DEV)
             ops.conv_wgrad_generic(x16, True, g, d, ref, ns)
         assert torch.equal(got, ref.to(torch.int64).sum(0)), g_i16
-        ns2 = ops.wgrad_store_nsplit(d)
+        ns2 = ops.wgrad_store_nsplit(d, g_i16)
         slab2 = torch.full((ns2, K, Cout), 3, dtype=torch.int64, device=DEV)  # every element overwritten
         ops.conv_wgrad_igemm_store(x_off, g, g_i16, d, slab2, ns2)
         assert torch.equal(slab2.sum(0), ref.to(torch.int64).sum(0)), ("store", g_i16)
@@ -370,6 +370,15 @@ def test_resnet50_fused_conv_quant_epilogue_bitexact(monkeypatch):
     the fused bottleneck bit-exact against the oracle."""
     monkeypatch.setenv("LBT_FUSE_CONV_QUANT", "1")
     test_resnet50_layers_bitexact_vs_oracle((1, 1, 1, 1), 64, 32, 16, 16)
+
+
+@pytest.mark.gpu
+def test_resnet50_fp32_ymask_path_bitexact(monkeypatch):
+    """LBT_YBITS=0: the fused bottleneck's last pass A reads the fp32 block output as its ReLU mask
+    instead of the chain's one-byte-per-channel-quad ybits; both forms bit-exact against the oracle
+    (the default run of test_resnet50_layers_bitexact_vs_oracle covers ybits)."""
+    monkeypatch.setenv("LBT_YBITS", "0")
+    test_resnet50_layers_bitexact_vs_oracle((2, 1, 1, 1), 64, 32, 16, 16)
 
 
 @pytest.mark.gpu

@@ -41,3 +41,28 @@ def test_wgrad3_exact(N, H, W, Ci, Co, g16):
     got = slab.sum(0).cpu()
     exp = _expected(x.double(), g.double()).to(torch.int64)
     assert torch.equal(got, exp)
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,s", [(2, 14, 128, 128, 1), (3, 9, 64, 256, 1), (2, 10, 256, 64, 1),
+                                         (2, 15, 128, 256, 2), (3, 7, 256, 128, 1), (4, 56, 64, 256, 1),
+                                         (1, 8, 512, 512, 2)])
+def test_wgrad1_exact(N, H, Ci, Co, s):
+    """The 1x1 16-bit-gradient weight gradient (igemm.hip wgrad1_kernel: raw int16 G images read
+    transposed as (lo, hi) byte columns) against the float64 sum dW[ci, co] = sum_{n,oh,ow}
+    x[n, oh*s, ow*s, ci] * g[n, oh, ow, co]; ragged pixel counts (P % 64 != 0), every tile shape
+    (wci 1 / 2 / 4), strided shortcuts, several splits."""
+    from lbt_amd.dfxp import ops
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device="cpu").manual_seed(N * 1000 + H + Ci + Co + s)
+    d = ops.conv_desc(N, H, H, Ci, Co, 1, 1, s, s, "SAME")
+    assert ops.wgrad1_wci(d)
+    x = torch.randint(0, 256, (N, H, H, Ci), generator=gen)
+    g = torch.randint(-32768, 32768, (N, d.Ho, d.Wo, Co), generator=gen)
+    ns = ops.wgrad_store_nsplit(d, 1)
+    xq = (x - 128).to(torch.int8).to(dev)
+    slab = torch.full((ns, Ci, Co), 7, dtype=torch.int64, device=dev)  # every element must be written
+    ops.conv_wgrad_igemm_store(xq, g.to(torch.int16).to(dev), 1, d, slab, ns)
+    torch.cuda.synchronize()
+    xs = x[:, ::s, ::s, :][:, :d.Ho, :d.Wo, :].reshape(-1, Ci).double()
+    exp = (xs.t() @ g.reshape(-1, Co).double()).to(torch.int64)
+    assert torch.equal(slab.sum(0).cpu(), exp)
