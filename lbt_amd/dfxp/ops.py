@@ -628,12 +628,20 @@ def conv_dgrad_igemm_ws(gq, g_i16, wd, ksd, d, qg, qw, dx, ws, add_src=None):
              ptr(ws), 0 if ws is None else ws.numel() * ws.element_size(), stream())
 
 
+NOISE_TABLES = os.environ.get("LBT_EPI_NOISE_TABLE", "1") == "1"
+
+
 def conv_fwd_igemm_q(xq, a_kind, wf, ksf, d, qx, qw, yq, qout, chsum):
-    """Wide fwd + the Normalization_q input quantiser in its epilogue (int8 codes, sums, counters)."""
+    """Wide fwd + the Normalization_q input quantiser in its epilogue (int8 codes, sums, counters).
+    A stochastic qout reads its noise from the context's per-step table (one Philox call per 4 noise
+    values per step instead of one per 4 outputs of every sample)."""
     M = d.N * d.Ho * d.Wo
     qout.observe(M * d.Cout)
+    qd = qout.desc
+    if NOISE_TABLES and qout.stochastic:
+        qd = qout.ctx.noise_table_desc(qout, d.Ho * d.Wo * d.Cout)
     with _Timed("igemm_kernel<fwd>", xq.numel() * xq.element_size() + wf.numel() + M * d.Cout):
-        call("lbt_conv_fwd_igemm_q", ptr(xq), int(a_kind), ptr(wf), int(ksf), d, qx, qw, ptr(yq), qout.desc,
+        call("lbt_conv_fwd_igemm_q", ptr(xq), int(a_kind), ptr(wf), int(ksf), d, qx, qw, ptr(yq), qd,
              ptr(chsum), stream())
 
 

@@ -103,6 +103,7 @@ class Model:
         self.ctx.params_ready = True
 
     def forward(self, X):
+        self.ctx.fill_noise_tables()  # this step's noise of the quantisers that read tables
         if self.batched_params:
             self._param_prologue()
         try:

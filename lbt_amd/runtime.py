@@ -110,6 +110,41 @@ class DfxpContext:
         self.by_name[name] = q
         return q
 
+    def noise_table_desc(self, q, inner):
+        """A copy of stochastic quantiser q's descriptor whose noise comes from a per-step table of its
+        `inner` noise values (u[i] for i < inner: the same Philox values the kernels draw inline,
+        lbt_dfxp_noise_fill). For consumers that would otherwise recompute each value once per sample
+        (the wide GEMMs' quantising epilogue: a tile's rows are pixels, the noise repeats over the
+        batch). A new table is filled at once; fill_noise_tables (the model's per-step prologue)
+        refills every table for the step that follows."""
+        tabs = self.__dict__.setdefault("_ntab", {})
+        ent = tabs.get(q.slot)
+        if ent is None or ent[1] != inner:
+            n4 = (int(inner) + 3) // 4 * 4
+            tab = torch.empty(n4, dtype=torch.float32, device=self.device)
+            d = QDesc.from_buffer_copy(q.desc)
+            d.noise = tab.data_ptr()
+            job = _lib.NJob(self.step.data_ptr(), self.seed, q.qid, 0, int(inner), tab.data_ptr())
+            ent = (tab, int(inner), d, job)
+            tabs[q.slot] = ent
+            # job arrays uploaded here (eagerly: never inside a graph capture), the new table filled now
+            self._njobs = self._job_array([e[3] for e in tabs.values()], max(e[1] for e in tabs.values()))
+            dev, n, max_n = self._job_array([job], int(inner))
+            _lib.call("lbt_dfxp_noise_fill", _lib.ptr(dev), n, max_n, None, 0, _lib.stream())
+        return ent[2]
+
+    def _job_array(self, jobs, max_n):
+        n = len(jobs)
+        host = torch.frombuffer(bytearray(bytes((_lib.NJob * n)(*jobs))), dtype=torch.uint8)
+        return host.to(self.device), n, int(max_n)
+
+    def fill_noise_tables(self):
+        """Refill every noise_table_desc table for the current step (one launch)."""
+        if getattr(self, "_njobs", None) is None:
+            return
+        dev, n, max_n = self._njobs
+        _lib.call("lbt_dfxp_noise_fill", _lib.ptr(dev), n, int(max_n), None, 0, _lib.stream())
+
     def alloc_sums(self, n):
         """n int64 from the arena. When the first arena is full (wide models: ResNet-50's weight-
         gradient slabs), further buffers come from overflow arenas of at least the same size --
