@@ -89,7 +89,8 @@ def _batch(B, image, classes, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("grad_bits", [8, 16])
 @pytest.mark.parametrize("blocks,width,image,classes", [((1, 1, 1, 1), 8, 32, 10), ((2, 1, 1, 1), 16, 40, 10),
-                                                        ((1, 1, 1, 1), 8, 32, 16), ((2, 1, 1, 1), 64, 32, 16)])
+                                                        ((1, 1, 1, 1), 8, 32, 16), ((2, 1, 1, 1), 64, 32, 16),
+                                                        ((3, 2, 1, 1), 64, 40, 16)])
 def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, classes, grad_bits):
     """classes=16: the fc runs on the int8-MFMA dense kernels (dense.hip), 10: the generic ones.
     width 64 with 16-bit gradients: every bottleneck runs fused (ResidualBottleneck_q._fusable)."""
@@ -379,6 +380,7 @@ def test_resnet50_fp32_ymask_path_bitexact(monkeypatch):
     (the default run of test_resnet50_layers_bitexact_vs_oracle covers ybits)."""
     monkeypatch.setenv("LBT_YBITS", "0")
     test_resnet50_layers_bitexact_vs_oracle((2, 1, 1, 1), 64, 32, 16, 16)
+    test_resnet50_layers_bitexact_vs_oracle((2, 2, 1, 1), 64, 32, 16, 16)
 
 
 @pytest.mark.gpu
