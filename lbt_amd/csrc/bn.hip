@@ -124,6 +124,34 @@ LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long 
 // the fused ResNet plan launches (no per-element branches, constant rounding mode and output
 // encoding); kRt selects the variant that reads everything from the descriptor at run time.
 
+// Channel pairs on packed fp32 (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: each half rounded exactly
+// as the scalar op): the forward chain is VALU-bound on the wide layers (ResNet-50: ~40 VALU ops per
+// element against 3-12 bytes), so its multiplies / adds / fmas run two channels per instruction;
+// compares, clamps, floors and conversions stay scalar.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+LBT_DEV pf2 pk(float a, float b) { return pf2{a, b}; }
+LBT_DEV pf2 pcvt(int a, int b) { return pf2{(float)a, (float)b}; }
+// div_by on a pair (the same operations, so the same bits as '/')
+LBT_DEV pf2 pdiv(pf2 x, pf2 y, pf2 rc) {
+  const pf2 q = x * rc;
+  const pf2 r = __builtin_elementwise_fma(-y, q, x);
+  const pf2 q1 = __builtin_elementwise_fma(r, rc, q);
+  const pf2 r1 = __builtin_elementwise_fma(-y, q1, x);
+  return __builtin_elementwise_copysign(__builtin_elementwise_fma(r1, rc, q1), x);
+}
+// quant_w on a pair: the codes of x.x / x.y into c0 / c1, wave-total overflow counts
+template <int STOCH>
+LBT_DEV void quant_w2(const QState& s, int stochastic, pf2 x, pf2 u, int& ov1w, int& ov2w, int& c0, int& c1) {
+  const pf2 xm = x * pk(s.m, s.m);
+  ov1w += __popcll(__ballot((xm.x >= s.L) | (xm.x < -s.L))) + __popcll(__ballot((xm.y >= s.L) | (xm.y < -s.L)));
+  ov2w += __popcll(__ballot((xm.x >= s.Lh) | (xm.x < -s.Lh))) + __popcll(__ballot((xm.y >= s.Lh) | (xm.y < -s.Lh)));
+  const bool st = STOCH < 0 ? stochastic != 0 : STOCH == 1;
+  const pf2 v = st ? xm + u : xm;
+  const float v0 = fminf(fmaxf(v.x, -s.L), s.Lm1), v1 = fminf(fmaxf(v.y, -s.L), s.Lm1);
+  c0 = (int)(st ? floorf(v0) : rintf(v0));
+  c1 = (int)(st ? floorf(v1) : rintf(v1));
+}
+
 template <int B>
 LBT_DEV const lbt_chain_branch& fbranch(const lbt_chain_fwd& a) { return B == 0 ? a.b1 : a.b2; }
 
@@ -205,6 +233,19 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
       pb[b][k] = P[3 * C + c0 + k];
     }
   }
+  // ... and as channel pairs for the packed math
+  pf2 pmv[NB][2], psy[NB][2], psr[NB][2], pgv[NB][2], pbv[NB][2], nr2[NB][2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pmv[b][h] = pk(pm[b][2 * h], pm[b][2 * h + 1]);
+      psy[b][h] = pk(ps[b][2 * h].y, ps[b][2 * h + 1].y);
+      psr[b][h] = pk(ps[b][2 * h].rc, ps[b][2 * h + 1].rc);
+      pgv[b][h] = pk(pg[b][2 * h], pg[b][2 * h + 1]);
+      pbv[b][h] = pk(pb[b][2 * h], pb[b][2 * h + 1]);
+      nr2[b][h] = pk(nr[b].u[2 * h], nr[b].u[2 * h + 1]);
+    }
   int ovr[2][2] = {{0, 0}, {0, 0}};  // wave totals (quant_w)
   int ovo[2][2] = {{0, 0}, {0, 0}};
   const bool relu = LBT_FL(kFRelu, a.relu != 0), ystore = LBT_FL(kFY, a.y != nullptr);
@@ -217,43 +258,47 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
       for (int j = 0; j < kRB; ++j) {
         if (rb + j >= rend) break;
         const int64_t e = (rb + j) * a.inner + (g << 2);
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        pf2 v2[2] = {pk(0.f, 0.f), pk(0.f, 0.f)};
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
-          float t[4];
+          pf2 t2[2];
           if (q_in[b]) {
             int q[4];
             unpack4_i8(qv[b][j], q);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const float x1 = (float)q[k] * sn[b];
-              const float x2 = x1 - pm[b][k];
-              t[k] = div_by(x2, ps[b][k]);  // == x2 / sigma
+            for (int h = 0; h < 2; ++h) {
+              const pf2 x1 = pcvt(q[2 * h], q[2 * h + 1]) * pk(sn[b], sn[b]);
+              const pf2 x2 = x1 - pmv[b][h];
+              t2[h] = pdiv(x2, psy[b][h], psr[b][h]);  // == x2 / sigma
             }
           } else {
+            float t[4];
             f4(xv[b][j], t);
+            t2[0] = pk(t[0], t[1]);
+            t2[1] = pk(t[2], t[3]);
           }
           if ((F & kRt) ? qr[b].active : !(F & kFNoR)) {
             int R[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              R[k] = quant_w<ST>(qr[b], Bb.qr.stochastic, t[k], nr[b].u[k], ovr[b][0], ovr[b][1]);
-              const float xr = (float)R[k] * qr[b].inv_m;
-              const float m1 = xr * pg[b][k];
-              t[k] = m1 + pb[b][k];
+            for (int h = 0; h < 2; ++h) {
+              quant_w2<ST>(qr[b], Bb.qr.stochastic, t2[h], nr2[b][h], ovr[b][0], ovr[b][1], R[2 * h], R[2 * h + 1]);
+              const pf2 xr = pcvt(R[2 * h], R[2 * h + 1]) * pk(qr[b].inv_m, qr[b].inv_m);
+              const pf2 m1 = xr * pgv[b][h];
+              t2[h] = m1 + pbv[b][h];
             }
             if (LBT_FL(kFRout, Bb.rout != nullptr)) store4_i8(Bb.rout, e, R, 0);
           }
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = b ? v[k] + t[k] : t[k];
+          for (int h = 0; h < 2; ++h) v2[h] = b ? v2[h] + t2[h] : t2[h];
         }
         if (res) {
           float rr[4];
           f4(rv[j], rr);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = v[k] + rr[k];
+          v2[0] = v2[0] + pk(rr[0], rr[1]);
+          v2[1] = v2[1] + pk(rr[2], rr[3]);
         }
+        float v[4] = {v2[0].x, v2[0].y, v2[1].x, v2[1].y};
         if (relu) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
@@ -264,14 +309,18 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
         if (o1) {
           int c[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) c[k] = quant_w<ST>(so1, a.qo1.stochastic, v[k], no1.u[k], ovo[0][0], ovo[0][1]);
+          for (int h = 0; h < 2; ++h)
+            quant_w2<ST>(so1, a.qo1.stochastic, pk(v[2 * h], v[2 * h + 1]), pk(no1.u[2 * h], no1.u[2 * h + 1]),
+                         ovo[0][0], ovo[0][1], c[2 * h], c[2 * h + 1]);
           if (u8) store4_code(a.o1, LBT_OUT_U8OFF, e, c, 0.f);
           else store4_code(a.o1, a.o1_kind, e, c, so1.inv_m);
         }
         if (o2) {
           int c[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) c[k] = quant_w<ST>(so2, a.qo2.stochastic, v[k], no2.u[k], ovo[1][0], ovo[1][1]);
+          for (int h = 0; h < 2; ++h)
+            quant_w2<ST>(so2, a.qo2.stochastic, pk(v[2 * h], v[2 * h + 1]), pk(no2.u[2 * h], no2.u[2 * h + 1]),
+                         ovo[1][0], ovo[1][1], c[2 * h], c[2 * h + 1]);
           if (u8) store4_code(a.o2, LBT_OUT_U8OFF, e, c, 0.f);
           else store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
         }
