@@ -12,6 +12,7 @@
 #include <cstdlib>
 
 #include "chain_flags.h"
+#include "pk2.h"
 
 using namespace lbt;
 
@@ -123,34 +124,6 @@ LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long 
 // Kernel variants: F holds the chain's configuration as compile-time flags for the combinations
 // the fused ResNet plan launches (no per-element branches, constant rounding mode and output
 // encoding); kRt selects the variant that reads everything from the descriptor at run time.
-
-// Channel pairs on packed fp32 (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: each half rounded exactly
-// as the scalar op): the forward chain is VALU-bound on the wide layers (ResNet-50: ~40 VALU ops per
-// element against 3-12 bytes), so its multiplies / adds / fmas run two channels per instruction;
-// compares, clamps, floors and conversions stay scalar.
-typedef float pf2 __attribute__((ext_vector_type(2)));
-LBT_DEV pf2 pk(float a, float b) { return pf2{a, b}; }
-LBT_DEV pf2 pcvt(int a, int b) { return pf2{(float)a, (float)b}; }
-// div_by on a pair (the same operations, so the same bits as '/')
-LBT_DEV pf2 pdiv(pf2 x, pf2 y, pf2 rc) {
-  const pf2 q = x * rc;
-  const pf2 r = __builtin_elementwise_fma(-y, q, x);
-  const pf2 q1 = __builtin_elementwise_fma(r, rc, q);
-  const pf2 r1 = __builtin_elementwise_fma(-y, q1, x);
-  return __builtin_elementwise_copysign(__builtin_elementwise_fma(r1, rc, q1), x);
-}
-// quant_w on a pair: the codes of x.x / x.y into c0 / c1, wave-total overflow counts
-template <int STOCH>
-LBT_DEV void quant_w2(const QState& s, int stochastic, pf2 x, pf2 u, int& ov1w, int& ov2w, int& c0, int& c1) {
-  const pf2 xm = x * pk(s.m, s.m);
-  ov1w += __popcll(__ballot((xm.x >= s.L) | (xm.x < -s.L))) + __popcll(__ballot((xm.y >= s.L) | (xm.y < -s.L)));
-  ov2w += __popcll(__ballot((xm.x >= s.Lh) | (xm.x < -s.Lh))) + __popcll(__ballot((xm.y >= s.Lh) | (xm.y < -s.Lh)));
-  const bool st = STOCH < 0 ? stochastic != 0 : STOCH == 1;
-  const pf2 v = st ? xm + u : xm;
-  const float v0 = fminf(fmaxf(v.x, -s.L), s.Lm1), v1 = fminf(fmaxf(v.y, -s.L), s.Lm1);
-  c0 = (int)(st ? floorf(v0) : rintf(v0));
-  c1 = (int)(st ? floorf(v1) : rintf(v1));
-}
 
 template <int B>
 LBT_DEV const lbt_chain_branch& fbranch(const lbt_chain_fwd& a) { return B == 0 ? a.b1 : a.b2; }

@@ -13,6 +13,7 @@
 // registers, and the 16 pixel lanes meet (shuffles, then LDS) before one atomic per
 // (channel, sum) into a shard.
 #include "dfxp_device.h"
+#include "pk2.h"
 
 namespace {
 
@@ -92,6 +93,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn
     const Noise4 z{{0.f, 0.f, 0.f, 0.f}};
     const Noise4 nz1 = (srg.active && a.qrg.stochastic) ? qnoise4(a.qrg, srg.step, blk) : z;
     const Noise4 nz2 = (sng.active && a.qng.stochastic) ? qnoise4(a.qng, sng.step, blk) : z;
+    // channel pairs for the packed math (pk2.h)
+    const pf2 u1[2] = {pk(nz1.u[0], nz1.u[1]), pk(nz1.u[2], nz1.u[3])};
+    const pf2 u2[2] = {pk(nz2.u[0], nz2.u[1]), pk(nz2.u[2], nz2.u[3])};
+    const pf2 gam2[2] = {pk(gam[0], gam[1]), pk(gam[2], gam[3])};
+    const pf2 bet2[2] = {pk(bet[0], bet[1]), pk(bet[2], bet[3])};
     for (int64_t nb = n0; nb < n1; nb += U) {
       float4 gv[U], g2v[YM ? U : 1], ym[YM ? U : 1];
       char4 rv[U], qv[U];
@@ -111,44 +117,53 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn
       for (int u = 0; u < U; ++u) {
         if (nb + u >= n1) break;
         const int64_t e = (nb + u) * a.inner + pos;
-        float d[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+        pf2 d2[2] = {pk(gv[u].x, gv[u].y), pk(gv[u].z, gv[u].w)};
         if (YM && g2p) {
-          d[0] = d[0] + g2v[u].x; d[1] = d[1] + g2v[u].y; d[2] = d[2] + g2v[u].z; d[3] = d[3] + g2v[u].w;
+          d2[0] = d2[0] + pk(g2v[u].x, g2v[u].y);
+          d2[1] = d2[1] + pk(g2v[u].z, g2v[u].w);
         }
         const int R[4] = {needR ? rv[u].x : 0, needR ? rv[u].y : 0, needR ? rv[u].z : 0, needR ? rv[u].w : 0};
         if (YM && ymp) {
-          const float m[4] = {ym[u].x, ym[u].y, ym[u].z, ym[u].w};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) d[k] = m[k] > 0.f ? d[k] : 0.f;
+          d2[0].x = ym[u].x > 0.f ? d2[0].x : 0.f;
+          d2[0].y = ym[u].y > 0.f ? d2[0].y : 0.f;
+          d2[1].x = ym[u].z > 0.f ? d2[1].x : 0.f;
+          d2[1].y = ym[u].w > 0.f ? d2[1].y : 0.f;
         } else if (YM && ybp) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) d[k] = ((yb[u] >> k) & 1u) ? d[k] : 0.f;
+          d2[0].x = (yb[u] & 1u) ? d2[0].x : 0.f;
+          d2[0].y = (yb[u] & 2u) ? d2[0].y : 0.f;
+          d2[1].x = (yb[u] & 4u) ? d2[1].x : 0.f;
+          d2[1].y = (yb[u] & 8u) ? d2[1].y : 0.f;
         } else if (a.mask_r) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {  // bn.hip chain_bwd_a's recomputation, op for op
-            const float xr = (float)R[k] * sr;
-            const float m1 = xr * gam[k];
-            const float yv = m1 + bet[k];
-            d[k] = yv > 0.f ? d[k] : 0.f;
+          for (int h = 0; h < 2; ++h) {  // bn.hip chain_bwd_a's recomputation, op for op
+            const pf2 xr = pcvt(R[2 * h], R[2 * h + 1]) * pk(sr, sr);
+            const pf2 m1 = xr * gam2[h];
+            const pf2 yv = m1 + bet2[h];
+            d2[h].x = yv.x > 0.f ? d2[h].x : 0.f;
+            d2[h].y = yv.y > 0.f ? d2[h].y : 0.f;
           }
         }
-        if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(d[0], d[1], d[2], d[3]);
+        if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(d2[0].x, d2[0].y, d2[1].x, d2[1].y);
         if (srg.active) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int G2 = quant_w<-1>(srg, a.qrg.stochastic, d[k], nz1.u[k], o1, o2);
-            s0[k] += G2 * R[k];
-            s1[k] += G2;
-            const float gh = (float)G2 * srg.inv_m;
-            d[k] = gh * gam[k];
+          for (int h = 0; h < 2; ++h) {
+            int G2[2];
+            quant_w2<-1>(srg, a.qrg.stochastic, d2[h], u1[h], o1, o2, G2[0], G2[1]);
+            s0[2 * h] += G2[0] * R[2 * h];
+            s0[2 * h + 1] += G2[1] * R[2 * h + 1];
+            s1[2 * h] += G2[0];
+            s1[2 * h + 1] += G2[1];
+            const pf2 gh = pcvt(G2[0], G2[1]) * pk(srg.inv_m, srg.inv_m);
+            d2[h] = gh * gam2[h];
           }
         }
         if (sng.active) {
           const int qn[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
           int G[4];
 #pragma unroll
+          for (int h = 0; h < 2; ++h) quant_w2<-1>(sng, a.qng.stochastic, d2[h], u2[h], p1, p2, G[2 * h], G[2 * h + 1]);
+#pragma unroll
           for (int k = 0; k < 4; ++k) {
-            G[k] = quant_w<-1>(sng, a.qng.stochastic, d[k], nz2.u[k], p1, p2);
             s2[k] += G[k];
             s3[k] += G[k] * qn[k];
           }
@@ -156,7 +171,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn
           o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
           *reinterpret_cast<short4*>(a.gout + e) = o;
         } else if (a.dout) {
-          *reinterpret_cast<float4*>(a.dout + e) = make_float4(d[0], d[1], d[2], d[3]);
+          *reinterpret_cast<float4*>(a.dout + e) = make_float4(d2[0].x, d2[0].y, d2[1].x, d2[1].y);
         }
       }
     }
@@ -257,6 +272,17 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
       mg[k] = s_mg[4 * cq + k];
       mgx[k] = s_mgx[4 * cq + k];
     }
+    // channel pairs (0, 1), (2, 3) for the packed math (pk2.h)
+    pf2 mu2[2], mg2[2], mgx2[2], rsy[2], rsr[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      mu2[h] = pk(mu[2 * h], mu[2 * h + 1]);
+      mg2[h] = pk(mg[2 * h], mg[2 * h + 1]);
+      mgx2[h] = pk(mgx[2 * h], mgx[2 * h + 1]);
+      rsy[h] = pk(rs[2 * h].y, rs[2 * h + 1].y);
+      rsr[h] = pk(rs[2 * h].rc, rs[2 * h + 1].rc);
+    }
+    const pf2 sn2 = pk(sn.inv_m, sn.inv_m), sg2 = pk(sgq.inv_m, sgq.inv_m);
     const int64_t n0 = (int64_t)blockIdx.z * b.spb;
     const int64_t n1 = n0 + b.spb < b.samples ? n0 + b.spb : b.samples;
     const int64_t pos = hw * b.C + c0, inner = b.hw * b.C;
@@ -281,26 +307,27 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
       const char4 qv = qva[u];
       const short4 gv = gva[u];
       const int q[4] = {qv.x, qv.y, qv.z, qv.w}, G[4] = {gv.x, gv.y, gv.z, gv.w};
-      float o[4];
+      pf2 o[2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float x1 = (float)q[k] * sn.inv_m;
-        const float x2 = x1 - mu[k];
-        const float xh = div_by(x2, rs[k]);  // == x2 / sigma
-        const float gh = (float)G[k] * sgq.inv_m;
-        const float t1 = gh - mg[k];
-        const float t2 = xh * mgx[k];
-        o[k] = div_by(t1 - t2, rs[k]);       // == (t1 - t2) / sigma
+      for (int h = 0; h < 2; ++h) {
+        const pf2 x1 = pcvt(q[2 * h], q[2 * h + 1]) * sn2;
+        const pf2 x2 = x1 - mu2[h];
+        const pf2 xh = pdiv(x2, rsy[h], rsr[h]);  // == x2 / sigma
+        const pf2 gh = pcvt(G[2 * h], G[2 * h + 1]) * sg2;
+        const pf2 t1 = gh - mg2[h];
+        const pf2 t2 = xh * mgx2[h];
+        o[h] = pdiv(t1 - t2, rsy[h], rsr[h]);     // == (t1 - t2) / sigma
       }
       if (quant) {
+        int c[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          quant_w2<-1>(so, b.qo.stochastic, o[h], pk(nz.u[2 * h], nz.u[2 * h + 1]), o1, o2, c[2 * h], c[2 * h + 1]);
         short4 v;
-        v.x = (short)quant_w<-1>(so, b.qo.stochastic, o[0], nz.u[0], o1, o2);
-        v.y = (short)quant_w<-1>(so, b.qo.stochastic, o[1], nz.u[1], o1, o2);
-        v.z = (short)quant_w<-1>(so, b.qo.stochastic, o[2], nz.u[2], o1, o2);
-        v.w = (short)quant_w<-1>(so, b.qo.stochastic, o[3], nz.u[3], o1, o2);
+        v.x = (short)c[0]; v.y = (short)c[1]; v.z = (short)c[2]; v.w = (short)c[3];
         *reinterpret_cast<short4*>(b.gq + e) = v;
       } else {
-        *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(b.dx + e) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
       }
       }
     }
