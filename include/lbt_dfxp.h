@@ -419,6 +419,14 @@ typedef struct lbt_wgrad_job {
  * those of the njobs calls (integer atomics into each job's slab). Every job is checked before
  * anything is queued.                                                                          */
 int lbt_conv_wgrad_many_i8(const lbt_wgrad_job* jobs, int32_t njobs, void* stream);
+/* lbt_conv_wgrad_many_i8(jobs, njobs) followed by lbt_conv_stem_bwd(b, x, d, slab, nshard) as ONE
+ * launch (the stem BN's pass B + conv1's dW of dynamic_fixed_point.py:620-623 / :302 need only the
+ * first block's dgrad output, like every batched wgrad job): the stem's 256-pixel row blocks run two
+ * per workgroup as the batched launch's first workgroups (LBT_STEM_FIRST=0: its last). Same arguments, checks and results as the two
+ * calls (integer atomics); a batch of more than 24 jobs or an odd number of stem row blocks is run as
+ * the two calls.                                                                               */
+int lbt_conv_wgrad_many_stem_i8(const lbt_wgrad_job* jobs, int32_t njobs, const lbt_chain_bwd_b* b, const int16_t* x,
+                                lbt_conv_desc d, int32_t* slab, int32_t nshard, void* stream);
 
 /* One stride-1 3x3 Conv2d_q's backward in ONE launch, with the BN backward passes on either side
  * (Conv2d_q.backward dynamic_fixed_point.py:299-305 between Normalization_q.backward :620-623 of

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -187,6 +187,7 @@ _SIGS = {
                                         c_int32, _P],
     "lbt_conv_wgrad_i8": [_P, c_int32, _P, ConvDesc, _P, c_int32, c_int32, _P],
     "lbt_conv_wgrad_many_i8": [_P, c_int32, _P],
+    "lbt_conv_wgrad_many_stem_i8": [_P, c_int32, _P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_wgrad_reduce": [_P, c_int32, c_int32, c_int32, c_int32, _P, QDesc, QDesc, _P, c_float, _P, _P],
     "lbt_conv_fwd_generic": [_P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P],
     "lbt_conv_dgrad_generic": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, _P],

@@ -22,6 +22,7 @@
 #include "conv_epilogue.h"
 #include "chain_flags.h"
 #include "lds_tr.h"
+#include "stem_bwd.h"
 
 using namespace lbt;
 
@@ -986,9 +987,8 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
   LBT_TS(3);
 }
 
-__global__ __launch_bounds__(kFW * 64, LBT_WGM_OCC) void conv_wgrad_many_kernel(const WgradMany m) {
-  __shared__ __attribute__((aligned(16))) WgradManyShared sm;
-  const uint32_t b = blockIdx.x;
+// block b of a batched launch: find its job, run that job's body
+LBT_DEV void wgrad_many_block(const WgradMany& m, uint32_t b, WgradManyShared& sm) {
   int j = 0;
 #pragma unroll 1
   while (j + 1 < m.n && b >= m.start[j + 1]) ++j;
@@ -1006,6 +1006,35 @@ __global__ __launch_bounds__(kFW * 64, LBT_WGM_OCC) void conv_wgrad_many_kernel(
     default: conv_wgrad_body<2, kFW>(wa, rb, sm.s2); break;
   }
 }
+
+__global__ __launch_bounds__(kFW * 64, LBT_WGM_OCC) void conv_wgrad_many_kernel(const WgradMany m) {
+  __shared__ __attribute__((aligned(16))) WgradManyShared sm;
+  wgrad_many_block(m, blockIdx.x, sm);
+}
+
+// The batched weight gradients with the stem's whole backward (stem_bwd.h, two 256-pixel row blocks
+// per 512-thread workgroup) as extra blocks of the same launch: the stem backward reads only the first
+// block's dgrad output, like the batched jobs, so it shares the batched launch's rounds of workgroups
+// instead of running as a launch of its own after it (lbt_conv_wgrad_many_stem_i8; 25.2 + 13.0 us as
+// two launches -> 34.2 us as one).
+union WgradManyStemShared {
+  WgradManyShared w;
+  StemBwdShared<2> s;
+};
+static_assert(kFW * 64 == 2 * 256, "two stem row blocks per workgroup of the batched launch");
+// (stem_first, the default: the stem's workgroups are the launch's FIRST blocks; else its last)
+__global__ __launch_bounds__(kFW * 64, LBT_WGM_OCC) void conv_wgrad_many_stem_kernel(const WgradMany m,
+                                                                                    const StemBwdArgs st,
+                                                                                    uint32_t pairs, int stem_first) {
+  __shared__ __attribute__((aligned(16))) WgradManyStemShared sm;
+  const uint32_t b = blockIdx.x, nw = m.start[m.n];
+  if (stem_first ? b < pairs : b >= nw) {
+    stem_bwd_body<2>(st, stem_first ? b : b - nw, sm.s);
+    return;
+  }
+  wgrad_many_block(m, stem_first ? b - pairs : b, sm.w);
+}
+static_assert(sizeof(WgradMany) + sizeof(StemBwdArgs) + 8 <= 4096, "kernel arguments");
 static_assert(sizeof(WgradMany) <= 4096, "kernel arguments");
 
 // WgradArgs + block count of one job of the batched launch
@@ -1051,6 +1080,46 @@ extern "C" int lbt_conv_wgrad_many_i8(const lbt_wgrad_job* jobs, int32_t njobs, 
     if (rc) return rc;
   }
   return 0;
+}
+
+extern "C" int lbt_conv_stem_bwd(const lbt_chain_bwd_b* b, const int16_t* x, lbt_conv_desc d, int32_t* slab,
+                                 int32_t nshard, void* stream);
+
+// lbt_conv_wgrad_many_i8(jobs) then lbt_conv_stem_bwd(b, x, d, slab, nshard) with the stem's row
+// blocks riding as the batched launch's last workgroups (two per workgroup); the same results (integer
+// atomics). A batch too large for one launch, or an odd number of stem row blocks, runs as the two calls.
+extern "C" int lbt_conv_wgrad_many_stem_i8(const lbt_wgrad_job* jobs, int32_t njobs, const lbt_chain_bwd_b* b,
+                                           const int16_t* x, lbt_conv_desc d, int32_t* slab, int32_t nshard,
+                                           void* stream) {
+  if (njobs < 0 || (njobs > 0 && !jobs) || !b || !x || !slab || nshard <= 0) return LBT_EINVAL;
+  const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
+  if (M <= 0 || !stem_bwd_shape_ok(b, d)) return M <= 0 ? lbt_conv_wgrad_many_i8(jobs, njobs, stream) : LBT_EINVAL;
+  const int64_t rblocks = M / kSbPixels, pairs = rblocks / 2;
+  // int32 shard totals stay exact: <= 31 row blocks per shard (stem.hip lbt_conv_stem_wgrad)
+  if (njobs > kMaxWJobs || rblocks % 2 || (pairs + nshard - 1) / nshard * 2 > 31) {
+    const int e = lbt_conv_wgrad_many_i8(jobs, njobs, stream);
+    return e ? e : lbt_conv_stem_bwd(b, x, d, slab, nshard, stream);
+  }
+  WgradMany m{};
+  uint64_t total = 0;
+  for (int i = 0; i < njobs; ++i) {  // every job checked before anything is queued
+    uint32_t blocks = 0;
+    const int e = wgrad_many_setup(jobs[i], m.j[i], blocks, m.fast[i]);
+    if (e) return e;
+    m.start[i] = (uint32_t)total;
+    total += blocks;
+  }
+  m.start[njobs] = (uint32_t)total;
+  m.n = njobs;
+  if (total + pairs >= 0x7fffffffull) return LBT_EINVAL;
+  StemBwdArgs st;
+  st.b = *b; st.x = x; st.d = d; st.K = d.KH * d.KW * d.Cin; st.slab = slab; st.nshard = nshard;
+  // stem blocks first (A/B on one box, isolated launch: 34.2 / 34.3 us vs 35.0 / 35.2 us placed last);
+  // LBT_STEM_FIRST=0 places them last
+  static const int stem_first = !(getenv("LBT_STEM_FIRST") != nullptr && getenv("LBT_STEM_FIRST")[0] == '0');
+  hipLaunchKernelGGL(conv_wgrad_many_stem_kernel, dim3((unsigned)(total + pairs)), dim3(kFW * 64), 0,
+                     (hipStream_t)stream, m, st, (uint32_t)pairs, stem_first);
+  return (int)hipGetLastError();
 }
 
 extern "C" int lbt_conv_wgrad_reduce(const int32_t* slab, int32_t nsplit, int32_t K, int32_t Cout, int32_t x_u8off,

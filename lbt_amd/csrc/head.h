@@ -96,15 +96,22 @@ LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds) {
       }
     }
   }
+  // the loss terms' tree sum s[t] += s[t + o], o = 128, 64, ..., 1: the two upper levels through LDS,
+  // the six within wave 0 as shuffles (lane t < o adds lane t + o: the same additions in the same
+  // order as the LDS tree, without its six barriers)
+  static_assert(kHeadT == 256, "tree levels");
   s_red[t] = part;
   __syncthreads();
-  for (int o = kHeadT / 2; o > 0; o >>= 1) {
-    if (t < o) s_red[t] += s_red[t + o];
-    __syncthreads();
-  }
-  if (t == 0) {
-    h.loss[0] = (float)(s_red[0] / (double)(h.loss_n > 0 ? h.loss_n : N));
-    if (x.buf) x.buf[x.loss_off] = (long long)llrint(s_red[0] * 4294967296.0);
+  if (t < 128) s_red[t] += s_red[t + 128];
+  __syncthreads();
+  if (t < 64) {
+    double v = s_red[t] + s_red[t + 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if (t == 0) {
+      h.loss[0] = (float)(v / (double)(h.loss_n > 0 ? h.loss_n : N));
+      if (x.buf) x.buf[x.loss_off] = (long long)llrint(v * 4294967296.0);
+    }
   }
 }
 

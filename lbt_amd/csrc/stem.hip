@@ -19,6 +19,7 @@
 //        adds its exact int32 partial into shard (wg % nshard) of a zeroed slab[nshard][K][Cout]
 //        (integer atomics) for lbt_conv_wgrad_reduce(_many).
 #include "conv_epilogue.h"
+#include "stem_bwd.h"
 
 #include <cstdlib>
 
@@ -393,174 +394,13 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_rows_kernel(const int16_t
   }
 }
 
-// ---- the stem's whole backward in one launch (lbt_conv_stem_bwd): pass B of the stem BN
-// (bn.hip chain_bwd_b_body's arithmetic, dynamic_fixed_point.py:620-623) evaluated straight into
-// the wgrad's LDS gradient image, then stem_wgrad_rows_kernel's MFMAs (conv1's dW, :302). d loss /
-// d image is never needed, so the gradient codes have no other reader: they never go to memory
-// (unless b.gq asks for them), and the chain's launch and its 2 MB round trip are gone.
-LBT_DEV Noise4 noise4_for(const lbt_qdesc& q, const QState& s, int64_t g) {
-  Noise4 n = {{0.f, 0.f, 0.f, 0.f}};
-  if (s.active && q.stochastic) n = qnoise4(q, s.step, (uint64_t)g);
-  return n;
-}
-
-struct StemBwdArgs {
-  lbt_chain_bwd_b b;
-  const int16_t* x;
-  lbt_conv_desc d;
-  int K;
-  int32_t* slab;
-  int nshard;
-};
-
+// ---- the stem's whole backward in one launch (lbt_conv_stem_bwd): stem_bwd.h's body over one
+// 256-pixel row block per workgroup (pass B of the stem BN into the wgrad's LDS operand, conv1's dW).
 __global__ __launch_bounds__(kThreads) void stem_bwd_rows_kernel(StemBwdArgs p) {
-  constexpr int C = 16;
-  __shared__ int red[4][32][64];
-  __shared__ int16_t s_img[kSWRows * (kStemWMax + 2) * kStemCinMax > 4096 ? 4096 : kSWRows * (kStemWMax + 2) * kStemCinMax];
-  __shared__ __attribute__((aligned(16))) int8_t s_g[kWgPixels * 16];
-  __shared__ float s_pb[2 * C];
-  __shared__ int sh_cnt[2 * kThreads / 64];
+  __shared__ __attribute__((aligned(16))) StemBwdShared<1> sm;
   LBT_TS(0);
-  const lbt_chain_bwd_b& a = p.b;
-  const lbt_conv_desc& d = p.d;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, t = threadIdx.x;
-  const int r = lane & 15, kg = lane >> 4;
-  const int nkt = (p.K + 15) >> 4;
-  const int W = d.W, Cin = d.Cin, HWp = d.H * d.W;
-  const int64_t m0 = (int64_t)blockIdx.x * kWgPixels;  // host: HW % 256 == 0, 256 % W == 0
-  const int n = (int)(m0 / HWp), oy0 = (int)(m0 - (int64_t)n * HWp) / W;
-  const int NC = W + 2, E = (kWgPixels / W + 2) * NC * Cin;  // host: E <= 4096
-  // ---- loads: the pass-B statistics' 32 shards (threads < 2C), this thread's 4 channel quads of G /
-  // q codes and their noise, and the image rows of the wgrad
-  long long sv[LBT_NSHARD];
-  if (t < 2 * C) {
-#pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) sv[k] = a.sums[(int64_t)k * 4 * C + 2 * C + t];
-  }
-  const int cq = (t & 3) * 4;
-  int Gv[4], Qv[4];
-  Noise4 nz[4];
-  const QState sgq = qstate(a.qng), sn = qstate(a.qn), so = qstate(a.qo);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int lp = (t >> 2) + 64 * j;                     // local pixel
-    const int64_t e = (m0 + lp) * C + cq;                  // element offset (NHWC, C = 16)
-    Gv[j] = *reinterpret_cast<const int*>(a.G + e);
-    Qv[j] = *reinterpret_cast<const int*>(a.qn_codes + e);
-    const int64_t gl = ((m0 - (int64_t)n * HWp + lp) * C + cq) >> 2;  // noise block within the row
-    nz[j] = noise4_for(a.qo, so, gl);
-  }
-  {
-    constexpr int kPer = 16;
-    int16_t v[kPer];
-    bool ok[kPer];
-#pragma unroll
-    for (int h = 0; h < kPer; ++h) {
-      const int e = t + h * kThreads;
-      const int ci = e % Cin, pc = e / Cin, col = pc % NC, row = pc / NC;
-      const int iy = oy0 - 1 + row, ix = col - 1;
-      ok[h] = e < E && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)W;
-      v[h] = p.x[ok[h] ? (((int64_t)n * d.H + iy) * W + ix) * Cin + ci : 0];
-    }
-#pragma unroll
-    for (int h = 0; h < kPer; ++h) {
-      const int e = t + h * kThreads;
-      if (e < E) s_img[e] = ok[h] ? v[h] : (int16_t)0;
-    }
-  }
-  // ---- pass-B constants mg, mgx per channel, in double exactly as chain_bwd_b_body
-  if (t < 2 * C) {
-    long long s = 0;
-#pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) s += sv[k];
-    reinterpret_cast<long long*>(red)[t] = s;  // red is free until the MFMAs
-  }
-  __syncthreads();
-  if (t < C) {
-    const long long* tmp = reinterpret_cast<const long long*>(red);
-    const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, nn = (double)a.n;
-    const float m = a.ms[t], sig = a.ms[C + t];
-    const double SG = (double)tmp[t], SGQ = (double)tmp[C + t];
-    s_pb[t] = (float)(gsc * SG / nn);
-    s_pb[C + t] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
-  }
-  __syncthreads();
-  LBT_TS(1);
-  float rmu[4], rmg[4], rmgx[4];
-  Recip rsg[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    rmu[k] = a.ms[cq + k];
-    rsg[k] = recip(a.ms[C + cq + k]);
-    rmg[k] = s_pb[cq + k];
-    rmgx[k] = s_pb[C + cq + k];
-  }
-  int ov1 = 0, ov2 = 0;  // wave totals
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int G[4], q[4], c[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      G[k] = (int8_t)((Gv[j] >> (8 * k)) & 0xff);
-      q[k] = (int8_t)((Qv[j] >> (8 * k)) & 0xff);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float x1 = (float)q[k] * sn.inv_m;
-      const float x2 = x1 - rmu[k];
-      const float xh = div_by(x2, rsg[k]);  // == x2 / sigma
-      const float gh = (float)G[k] * sgq.inv_m;
-      const float t1 = gh - rmg[k];
-      const float t2 = xh * rmgx[k];
-      const float dx = div_by(t1 - t2, rsg[k]);  // == (t1 - t2) / sigma
-      c[k] = quant_w<-1>(so, a.qo.stochastic, dx, nz[j].u[k], ov1, ov2);
-    }
-    const int lp = (t >> 2) + 64 * j;
-    const int w = (int)((uint32_t)(c[0] & 0xff) | ((uint32_t)(c[1] & 0xff) << 8) | ((uint32_t)(c[2] & 0xff) << 16) |
-                        ((uint32_t)c[3] << 24));
-    *reinterpret_cast<int*>(s_g + lp * 16 + cq) = w;
-    if (a.gq) *reinterpret_cast<int*>(a.gq + (m0 + lp) * C + cq) = w;
-  }
-  if (a.qo.counts) counts_stage_w(0, 1, ov1, ov2, sh_cnt);
-  __syncthreads();
-  LBT_TS(2);
-  f4v acc[2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) acc[kt] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    h8 af[2], b;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const int k = kt * 16 + r;
-      const int tap = k / Cin, ci = k - tap * Cin, kh = tap / 3, kw = tap - kh * 3;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int lm = wave * 64 + 32 * s + 8 * kg + j, ly = lm / W, ox = lm - ly * W;
-        const int v = (kt < nkt && k < p.K) ? (int)s_img[((ly + kh) * NC + ox + kw) * Cin + ci] : 0;
-        af[kt][j] = (_Float16)(float)v;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = (_Float16)(float)(int)s_g[(wave * 64 + 32 * s + 8 * kg + j) * 16 + r];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-      if (kt < nkt) acc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kt], b, acc[kt], 0, 0, 0);
-  }
-  counts_publish(0, 1, a.qo, sh_cnt);
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (kt < nkt) red[wave][kt * 16 + 4 * kg + i][r] = (int)acc[kt][i];
-  __syncthreads();
+  stem_bwd_body<1>(p, blockIdx.x, sm);
   LBT_TS(3);
-  int32_t* out = p.slab + (int64_t)(blockIdx.x % p.nshard) * p.K * 16;
-  for (int i = threadIdx.x; i < p.K * 16; i += kThreads) {
-    const int k = i / 16, c = i - k * 16;
-    const int v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
-    if (v) LBT_GADD(&out[i], v);  // integer atomics: exact, order-independent
-  }
 }
 
 }  // namespace
@@ -636,14 +476,7 @@ extern "C" int lbt_conv_stem_bwd(const lbt_chain_bwd_b* b, const int16_t* x, lbt
   const int K = d.KH * d.KW * d.Cin;
   const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
   if (M <= 0) return LBT_OK;
-  const bool shape = d.Cout == 16 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 && d.PL == 1 &&
-                     d.Ho == d.H && d.Wo == d.W && d.Cin >= 1 && d.Cin <= kStemCinMax && K <= 32 && d.W >= 8 &&
-                     d.W <= kStemWMax && 64 % d.W == 0 && ((int64_t)d.H * d.W) % kWgPixels == 0 &&
-                     (kWgPixels / d.W + 2) * (d.W + 2) * d.Cin <= 4096 &&
-                     (kWgPixels / d.W + 2) * (d.W + 2) * d.Cin <= 16 * kThreads && M < ((int64_t)1 << 31);
-  if (!shape || b->C != 16 || b->rows != d.N || b->inner != (int64_t)d.H * d.W * 16 || !b->G || !b->qn_codes ||
-      !b->ms || !b->sums || b->dx || b->gcolsum || b->qo.bits <= 0 || b->qo.bits > 8)
-    return LBT_EINVAL;
+  if (!stem_bwd_shape_ok(b, d)) return LBT_EINVAL;
   const int64_t blocks = M / kWgPixels;
   if ((blocks + nshard - 1) / nshard > 31) return LBT_EINVAL;  // int32 shard totals stay exact
   StemBwdArgs p;

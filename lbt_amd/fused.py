@@ -456,20 +456,34 @@ class FusedResNet:
         # ---- stem backward (d loss / d image is never needed)
         self._flush_pending(bwd, L)
         tail_fork = self.tail_fork and self.batch_wgrad and not (self.overlap_wgrad or self.side_wgrad)
-        self._flush_wbatch(bwd, L, side=tail_fork)
+        # the stem's pass B evaluated inside its weight-gradient launch (lbt_conv_stem_bwd): one launch,
+        # and the gradient codes (read by nothing else: d loss / d image is not needed) stay in LDS
+        stem_bwd = (self._stem and os.environ.get("LBT_STEM_BWD", "1") == "1" and C0 == 16 and Cin0 <= 4
+                    and (dc.KH, dc.KW, dc.SH, dc.SW, dc.PT, dc.PL) == (3, 3, 1, 1, 1, 1) and dc.Ho == H and dc.Wo == W
+                    and W in (8, 16, 32, 64) and (H * W) % 256 == 0)
+        # ... and that launch's row blocks as the last workgroups of the batched weight-gradient launch
+        # (lbt_conv_wgrad_many_stem_i8): both read only block 0's dgrad output
+        stem_merge = (stem_bwd and not tail_fork and os.environ.get("LBT_STEM_MERGE", "1") == "1"
+                      and len(self._wbatch) > 0)
+        if not stem_merge:
+            self._flush_wbatch(bwd, L, side=tail_fork)
         if gY is not None:  # pass A not fused into block 0's dgrad
             aA.g = gY.data_ptr()
             bwd.append(L("lbt_bn_chain_bwd_a", ctypes.byref(aA), k="chain_bwd_a_kernel", nb=ops._chain_bwd_a_bytes(aA)))
         aB = self._chain_bwd_b(n0, Gn0, qn0, sums0, shp0, C0, gq0, c.grad_range, None)
         if self.sync_bn:
             bwd.append(self._allreduce(sums0))
-        # the stem's pass B evaluated inside its weight-gradient launch (lbt_conv_stem_bwd): one launch,
-        # and the gradient codes (read by nothing else: d loss / d image is not needed) stay in LDS
-        stem_bwd = (self._stem and os.environ.get("LBT_STEM_BWD", "1") == "1" and C0 == 16 and Cin0 <= 4
-                    and (dc.KH, dc.KW, dc.SH, dc.SW, dc.PT, dc.PL) == (3, 3, 1, 1, 1, 1) and dc.Ho == H and dc.Wo == W
-                    and W in (8, 16, 32, 64) and (H * W) % 256 == 0)
         self._keep += [aA, aB]
-        if stem_bwd:
+        if stem_merge:
+            aB.gq = None
+            ns0, slab0 = ops.stem_slab(self._c, "slab0", dc, ctx)
+            jobs, self._wbatch = self._wbatch, []
+            arr = (WgradJob * len(jobs))(*jobs)
+            self._keep.append(arr)
+            bwd.append(L("lbt_conv_wgrad_many_stem_i8", arr, len(jobs), ctypes.byref(aB), ptr(ximg), dc, ptr(slab0),
+                         ns0, k="conv_wgrad_many_stem_kernel",
+                         nb=sum(w._nb for w in jobs) + ops._chain_bwd_b_bytes(aB) + 2 * ximg.numel() + 4 * slab0.numel()))
+        elif stem_bwd:
             aB.gq = None
             ns0, slab0 = ops.stem_slab(self._c, "slab0", dc, ctx)
             bwd.append(L("lbt_conv_stem_bwd", ctypes.byref(aB), ptr(ximg), dc, ptr(slab0), ns0, k="stem_bwd_kernel",

@@ -828,6 +828,42 @@ def test_pair_launches_equal_single_launches(w4, bwd2, monkeypatch):
     assert a[5] == b[5]
 
 
+@pytest.mark.parametrize("B", [128, 32])
+def test_stem_merge_equals_separate_launches(B, monkeypatch):
+    """lbt_conv_wgrad_many_stem_i8 (the batched weight gradients with the stem's whole backward as the
+    launch's last workgroups) == lbt_conv_wgrad_many_i8 followed by lbt_conv_stem_bwd: gradients,
+    momentum, weights, exponents, BN running statistics and loss bit-identical after two
+    graph-replayed optimiser steps (B=128 is the bench workload)."""
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.trainer import Trainer
+    outs = []
+    for merge in ("0", "1"):
+        monkeypatch.setenv("LBT_STEM_MERGE", merge)
+        ctx = DfxpContext(seed=9)
+        m = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx))
+        tr = Trainer(m, lr=1e-2, momentum=0.9, batch_size=B, use_graph=True)
+        for i in range(2):
+            x, y = synthetic_batch(B, seed=60 + i)
+            tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+        torch.cuda.synchronize()
+        names = [getattr(f, "kname", "") for f in m._bwd]
+        want = (1, 0, 0) if merge == "1" else (0, 1, 1)
+        got = (names.count("conv_wgrad_many_stem_kernel"), names.count("conv_wgrad_many_kernel"),
+               names.count("stem_bwd_kernel"))
+        assert got == want, (merge, got)
+        bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
+        outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,
+                     m.loss.item()))
+    a, b = outs
+    for i in range(3):
+        assert np.array_equal(a[i], b[i]), i
+    assert a[3] == b[3]
+    for u, v in zip(a[4], b[4]):
+        assert np.array_equal(u, v)
+    assert a[5] == b[5]
+
+
 # (N, H, W, Cin, Cout, k, s): the staged 3x3 / stride-1 body (W | 64, whole-row chunks) and the
 # per-tap body (strided / 1x1), mixed in one launch
 WGRAD_MANY_CASES = [(8, 32, 32, 16, 16, 3, 1), (8, 16, 16, 32, 32, 3, 1), (8, 8, 8, 64, 64, 3, 1),
