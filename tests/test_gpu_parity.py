@@ -449,6 +449,42 @@ def test_fused_bench_workload_bitexact_vs_oracle():
             assert np.array_equal(g.X_var_running.cpu().numpy(), o.var_running), (i, g.name)
 
 
+@pytest.mark.parametrize("depth,blocks", [(32, (5, 5, 5)), (56, (9, 9, 9))])
+def test_deeper_cifar_resnets_fused_vs_oracle(depth, blocks):
+    """CIFAR10_Resnet32 / 56 (models.py CIFAR10_Resnet32-56, n = 5 / 9 ResidualBlock_q per stage) on the
+    fused plan with HIP-graph replay against the oracle for 2 optimiser steps at B=32: weights, exponents
+    and every BN running mean / variance bit-identical, loss at 1e-5 (d loss / d logits injected). Their
+    30 / 54 block convs exceed one batched weight-gradient launch (24 jobs), so the stem-merged call
+    (lbt_conv_wgrad_many_stem_i8) takes its two-call path here."""
+    from lbt_amd import models
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.trainer import Trainer
+    ctx = DfxpContext(seed=3)
+    gm = getattr(models, "CIFAR10_Resnet%d" % depth)(8, weight_decay=2e-4, ctx=ctx)
+    om = oresnet.build_resnet(blocks, 8, 2e-4)
+    fm = FusedResNet(gm)
+    state = dict(params=gpu_params(gm), accum=None, ranges=oresnet.init_ranges(om), step=0)
+    state["accum"] = {k: np.zeros_like(v) for k, v in state["params"].items()}
+    assert set(state["params"]) == set(oresnet.get_params(om))
+    tr = Trainer(fm, lr=1e-2, momentum=0.9, batch_size=32, use_graph=True)
+    gn, on = _gpu_norms(gm), _oracle_norms(om)
+    assert len(gn) == len(on) == 2 * sum(blocks) + 3
+    for i in range(2):
+        x, y = synthetic_batch(32, seed=70 + i)
+        loss = tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)).item()
+        torch.cuda.synchronize()
+        dz = fm.dlogits.cpu().numpy()
+        lref, state, octx = oresnet.train_step(om, state, x, y, lr=1e-2, momentum=0.9, seed=3, dz=dz)
+        assert abs(loss - lref) <= 1e-5 * abs(lref), (i, loss, lref)
+        gp = gpu_params(gm)
+        for k in gp:
+            assert np.array_equal(gp[k], state["params"][k]), (i, k)
+        assert ctx.ranges() == state["ranges"], i
+        for g, o in zip(gn, on):
+            assert np.array_equal(g.X_mean_running.cpu().numpy(), o.mean_running), (i, g.name)
+            assert np.array_equal(g.X_var_running.cpu().numpy(), o.var_running), (i, g.name)
+
+
 @pytest.mark.parametrize("scale", [1.0, 3.0])
 def test_nonzero_target_overflow_rate_layers(scale):
     """target_overflow_rate = 0.01 (plumbed through every layer, dynamic_fixed_point.py:131,226,321,
