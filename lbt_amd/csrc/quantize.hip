@@ -164,10 +164,25 @@ __global__ __launch_bounds__(256) void step_update_kernel(float* __restrict__ w,
                                                           const float* __restrict__ g, int64_t n, float lr, float mu,
                                                           float gscale, int sgd_blocks, int32_t* exps, int32_t* counts,
                                                           const int32_t* bits, const float* target, const float* nelem,
-                                                          int nslots, uint64_t* step) {
+                                                          int nslots, uint64_t* step, int vec) {
   if ((int)blockIdx.x < sgd_blocks) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) sgd_momentum_elem(w, a, g, i, lr, mu, gscale);
+    // 4 consecutive parameters per thread (16-byte loads / stores when w, a, g are 16-byte aligned:
+    // vec), each through sgd_momentum_elem's arithmetic
+    const int64_t i = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+    if (vec && i + 4 <= n) {
+      float4 wv = *reinterpret_cast<const float4*>(w + i);
+      float4 av = *reinterpret_cast<const float4*>(a + i);
+      const float4 gv = *reinterpret_cast<const float4*>(g + i);
+      float* wp = &wv.x;
+      float* ap = &av.x;
+      const float* gp = &gv.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sgd_momentum_elem(wp, ap, gp, k, lr, mu, gscale);
+      *reinterpret_cast<float4*>(a + i) = av;
+      *reinterpret_cast<float4*>(w + i) = wv;
+    } else {
+      for (int64_t k = i; k < i + 4 && k < n; ++k) sgd_momentum_elem(w, a, g, k, lr, mu, gscale);
+    }
     return;
   }
   const int rb = (int)blockIdx.x - sgd_blocks;
@@ -286,11 +301,12 @@ extern "C" int lbt_step_update(float* w, float* a, const float* g, int64_t n, fl
                                int32_t* exps, int32_t* counts, const int32_t* bits, const float* target,
                                const float* nelem, int32_t nslots, uint64_t* step, void* stream) {
   if (n < 0 || nslots < 0) return LBT_EINVAL;
-  const int64_t sgd_blocks = (n + 255) / 256;
+  const int vec = (((uintptr_t)w | (uintptr_t)a | (uintptr_t)g) & 15) == 0;  // float4 access
+  const int64_t sgd_blocks = (n + 1023) / 1024;
   const int rblocks = nslots > 0 ? (nslots + 3) / 4 : 1;
   if (sgd_blocks + rblocks >= ((int64_t)1 << 31)) return LBT_EINVAL;
   hipLaunchKernelGGL(step_update_kernel, dim3((unsigned)(sgd_blocks + rblocks)), dim3(256), 0, (hipStream_t)stream, w, a,
-                     g, n, lr, mu, gscale, (int)sgd_blocks, exps, counts, bits, target, nelem, nslots, step);
+                     g, n, lr, mu, gscale, (int)sgd_blocks, exps, counts, bits, target, nelem, nslots, step, vec);
   return (int)hipGetLastError();
 }
 
