@@ -634,6 +634,7 @@ typedef struct lbt_rjob {
   const int32_t* slab; int32_t nsplit, K, Cout, x_u8off; const int64_t* gcolsum;
   lbt_qdesc qx, qg; const float* w; float wd2; float* dw;
 } lbt_rjob;
+/* (a job with x_u8off and gcolsum -- the 128 * sum_p g[co] offset correction -- needs Cout <= 256) */
 int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, int32_t total_blocks, void* stream);
 
 /* lbt_bn_param_grads for many Rescale_q layers. */

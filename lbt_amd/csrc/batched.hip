@@ -77,30 +77,58 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
   int* s_job = reinterpret_cast<int*>(lds + 4096);
   int64_t* s_base = reinterpret_cast<int64_t*>(lds + 4104);
   // every job's block count loaded in parallel (a serial scan of device memory would cost one
-  // memory round trip per job), then scanned in LDS
-  for (int j = threadIdx.x; j < njobs; j += 256) nbs[j] = ((int64_t)jobs[j].K * jobs[j].Cout + 255) / 256;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t b = blk;
-    int jj = njobs;  // past the end: nothing to do
-    for (int j = 0; j < njobs; ++j) {
-      if (b < nbs[j]) { jj = j; break; }
-      b -= nbs[j];
+  // memory round trip per job), then scanned: <= 64 jobs as an inclusive scan across wave 0's lanes
+  // (the owning lane is the one whose [start, end) holds blk), more jobs serially in LDS
+  if (njobs <= 64) {
+    if (threadIdx.x < 64) {
+      const int l = (int)threadIdx.x;
+      const int64_t nb = l < njobs ? ((int64_t)jobs[l].K * jobs[l].Cout + 255) / 256 : 0;
+      int64_t end = nb;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t v = __shfl_up(end, o, 64);
+        if (l >= o) end += v;
+      }
+      const bool own = l < njobs && (int64_t)blk < end && (int64_t)blk >= end - nb;
+      const unsigned long long m = __ballot(own);
+      if (l == 0) *s_job = m ? __ffsll((long long)m) - 1 : njobs;
+      if (own) *s_base = ((int64_t)blk - (end - nb)) * 256;
     }
-    *s_job = jj;
-    *s_base = b * 256;
+    __syncthreads();
+  } else {
+    for (int j = threadIdx.x; j < njobs; j += 256) nbs[j] = ((int64_t)jobs[j].K * jobs[j].Cout + 255) / 256;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t b = blk;
+      int jj = njobs;  // past the end: nothing to do
+      for (int j = 0; j < njobs; ++j) {
+        if (b < nbs[j]) { jj = j; break; }
+        b -= nbs[j];
+      }
+      *s_job = jj;
+      *s_base = b * 256;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (*s_job >= njobs) return;
   const lbt_rjob j = jobs[*s_job];
   const int64_t total = (int64_t)j.K * j.Cout;
   const int64_t i = *s_base + threadIdx.x;
   const bool corr = j.x_u8off && j.gcolsum;
-  if (corr) {
-    for (int c = threadIdx.x; c < j.Cout; c += 256) {
-      long long v[LBT_NSHARD];
+  // the column sums' shard loads (threads c < Cout <= 256, colsum's LDS capacity) and the slab loads
+  // are issued back to back, so both arrive in one memory round trip
+  const int c = (int)threadIdx.x;
+  const bool col = corr && c < j.Cout;
+  long long v[LBT_NSHARD];
+  if (col) {
 #pragma unroll
-      for (int k = 0; k < LBT_NSHARD; ++k) v[k] = j.gcolsum[(int64_t)k * 2 * j.Cout + c];
+    for (int k = 0; k < LBT_NSHARD; ++k) v[k] = j.gcolsum[(int64_t)k * 2 * j.Cout + c];
+  }
+  long long s = 0;
+  if (i < total)
+    for (int b = 0; b < j.nsplit; ++b) s += j.slab[(int64_t)b * total + i];
+  if (corr) {
+    if (col) {
       long long t = 0;
 #pragma unroll
       for (int k = 0; k < LBT_NSHARD; ++k) t += v[k];
@@ -109,8 +137,6 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
     __syncthreads();
   }
   if (i >= total) return;
-  long long s = 0;
-  for (int b = 0; b < j.nsplit; ++b) s += j.slab[(int64_t)b * total + i];
   if (corr) s += 128ll * colsum[i % j.Cout];
   if (x.buf) {  // data-parallel exchange: the exact numerator, dequantised after the all-reduce
     x.buf[(j.dw - x.gbase) + i] = s;
