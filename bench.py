@@ -244,7 +244,9 @@ def main():
         args.batch = args.global_batch // world
     elif args.batch is None:
         args.batch = 256 if r50 else 128
-    bn_mode = args.bn or ("sync" if strong else "local")
+    if args.bn == "sync" and args.layerwise:
+        ap.error("--bn sync: the fused plan only (the layer-wise executor takes per-GPU statistics)")
+    bn_mode = args.bn or ("sync" if strong and not args.layerwise else "local")
     if bn_mode == "sync" and r50:
         ap.error("--bn sync: ResNet-20 workloads only")
     # LBT_DIST_BACKEND=gloo + LBT_SHARE_GPU=1: a rehearsal of the N-rank path with every rank on the
@@ -338,6 +340,13 @@ def main():
             gbs = sb / (el / args.steps) / 1e9
             out["roofline"]["step"] = {"achieved": round(gbs, 1), "frac": round(gbs / out["roofline"]["peak"], 4),
                                        "algorithmic_bytes": sb, "ms_per_step": out["ms_per_step"]}
+            if not r50 and args.batch == 128:
+                # the same step time against SURVEY 8(d)'s 1.09 GB model of a configs[1] step (GEMM
+                # operands + every quantiser's fp32 read / code write): a different byte count
+                from lbt_amd.roofline import SURVEY_STEP_BYTES_R20
+                sg = SURVEY_STEP_BYTES_R20 / (el / args.steps) / 1e9
+                out["roofline"]["step"]["frac_survey_model"] = round(sg / out["roofline"]["peak"], 4)
+                out["roofline"]["step"]["survey_model_bytes"] = int(SURVEY_STEP_BYTES_R20)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_r50(args.cpu_seconds) if r50 else cpu_baseline(args.cpu_seconds, args.batch)
     if rank == 0:

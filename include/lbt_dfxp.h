@@ -187,6 +187,20 @@ int lbt_conv_fwd_igemm_ws(const void* xq, int32_t a_kind, const int8_t* wf, int3
 int lbt_conv_dgrad_igemm_ws(const void* gq, int32_t g_i16, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
                             lbt_qdesc qg, lbt_qdesc qw, float* dx, const float* add_src, void* ws, int64_t ws_bytes,
                             void* stream);
+/* Selection of the 256-row x BN-column LDS-DMA GEMM that the fwd / dgrad calls above use for
+ * large GEMMs (8 waves, S-stage global->LDS DMA ring; bit-identical results to the 128-row kernel
+ * and the generic ones). Process-wide, read by every call made after a set (not captured into a
+ * graph already recorded). big: 0 never, 1 when the GEMM has >= min_tiles 256-row tiles at the
+ * chosen width and is not split-K / a strided dgrad parity class; max_bn: widest column tile
+ * (64, 128, or 256 = A8 without the quantising epilogue); stages 2..4 (A16: 2 or 3).
+ * Defaults: {1, 200, 2, 128}, or the LBT_IGEMM_BIG / _MIN / _S / _BN256 environment at first use.
+ * launches (get only; set ignores it): 256-row GEMM launches issued by this process so far.      */
+typedef struct lbt_igemm_tuning {
+  int32_t big, min_tiles, stages, max_bn;
+  int64_t launches;
+} lbt_igemm_tuning;
+int lbt_igemm_get_tuning(lbt_igemm_tuning* out);
+int lbt_igemm_set_tuning(const lbt_igemm_tuning* t);
 int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
                          int32_t nsplit, int32_t nshard, void* stream);
 /* ... storing one partial per pixel split: slab [nsplit][KH*KW*Cin][Cout] is fully WRITTEN (no

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -153,6 +153,11 @@ class Xchg(ctypes.Structure):
                 ("counts", c_void_p), ("cnt_off", c_int64), ("loss_off", c_int64)]
 
 
+class IgemmTuning(ctypes.Structure):
+    _fields_ = [("big", c_int32), ("min_tiles", c_int32), ("stages", c_int32), ("max_bn", c_int32),
+                ("launches", c_int64)]
+
+
 class FSeg(ctypes.Structure):
     _fields_ = [("off", c_int64), ("n", c_int64), ("kind", c_int32), ("qx", QDesc), ("qg", QDesc), ("wd2", c_float)]
 
@@ -175,6 +180,8 @@ _SIGS = {
     "lbt_conv_dgrad_igemm": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_igemm": [_P, _P, c_int32, ConvDesc, _P, c_int32, c_int32, _P],
     "lbt_igemm_workspace_bytes": [ConvDesc, c_int32, c_int32],
+    "lbt_igemm_get_tuning": [_P],
+    "lbt_igemm_set_tuning": [_P],
     "lbt_conv_fwd_igemm_q": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, QDesc, _P, _P],
     "lbt_conv_fwd_igemm_ws": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P, c_int64, _P],
     "lbt_conv_dgrad_igemm_ws": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int64, _P],

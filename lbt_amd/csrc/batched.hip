@@ -115,10 +115,12 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
   const int64_t total = (int64_t)j.K * j.Cout;
   const int64_t i = *s_base + threadIdx.x;
   const bool corr = j.x_u8off && j.gcolsum;
-  // the column sums' shard loads (threads c < Cout <= 256, colsum's LDS capacity) and the slab loads
-  // are issued back to back, so both arrive in one memory round trip
-  const int c = (int)threadIdx.x;
-  const bool col = corr && c < j.Cout;
+  // the column sums' shard loads and the slab loads are issued back to back, so both arrive in one
+  // memory round trip. Cout <= 256 (colsum's LDS capacity): thread c < Cout sums column c once into
+  // LDS; wider jobs: every thread sums its own column's shards (uniform per block)
+  const bool lds_cols = j.Cout <= 256;
+  const int c = lds_cols ? (int)threadIdx.x : (int)(i % j.Cout);
+  const bool col = corr && (lds_cols ? c < j.Cout : i < total);
   long long v[LBT_NSHARD];
   if (col) {
 #pragma unroll
@@ -127,17 +129,17 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
   long long s = 0;
   if (i < total)
     for (int b = 0; b < j.nsplit; ++b) s += j.slab[(int64_t)b * total + i];
-  if (corr) {
-    if (col) {
-      long long t = 0;
+  long long t = 0;
+  if (col) {
 #pragma unroll
-      for (int k = 0; k < LBT_NSHARD; ++k) t += v[k];
-      colsum[c] = t;
-    }
+    for (int k = 0; k < LBT_NSHARD; ++k) t += v[k];
+  }
+  if (corr && lds_cols) {
+    if (col) colsum[c] = t;
     __syncthreads();
   }
   if (i >= total) return;
-  if (corr) s += 128ll * colsum[i % j.Cout];
+  if (corr) s += 128ll * (lds_cols ? colsum[i % j.Cout] : t);
   if (x.buf) {  // data-parallel exchange: the exact numerator, dequantised after the all-reduce
     x.buf[(j.dw - x.gbase) + i] = s;
     return;

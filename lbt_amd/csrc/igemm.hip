@@ -782,37 +782,56 @@ void launch_big_bn(IgArgs p, hipStream_t st) {
 #undef LBT_BIG
 }
 
+// Selection of the 256-row LDS-DMA kernel (lbt_igemm_tuning, include/lbt_dfxp.h): read per call,
+// so a test can force the kernel onto any shape and variant. Defaults from the environment at the
+// first use (LBT_IGEMM_BIG, LBT_IGEMM_BIG_MIN, LBT_IGEMM_BIG_S, LBT_IGEMM_BIG_BN256) -- the measured
+// choice: on, >= 200 tiles, 2 stages, 128-column tiles at most.
+lbt_igemm_tuning& big_tuning() {
+  static lbt_igemm_tuning t = [] {
+    lbt_igemm_tuning v;
+    v.big = getenv_int("LBT_IGEMM_BIG", 1);
+    v.min_tiles = getenv_int("LBT_IGEMM_BIG_MIN", 200);
+    v.stages = getenv_int("LBT_IGEMM_BIG_S", 2);
+    v.max_bn = getenv_int("LBT_IGEMM_BIG_BN256", 0) ? 256 : 128;
+    v.launches = 0;
+    return v;
+  }();
+  return t;
+}
+
 // The 256-row LDS-DMA kernel takes a GEMM when it is big enough to give every CU about one tile
-// (LBT_IGEMM_BIG_MIN tiles, default 200; LBT_IGEMM_BIG=0: never) and is not split / classed.
+// (min_tiles, default 200; big = 0: never) and is not split / classed.
 template <int MODE, bool A16>
 bool launch_big(const IgArgs& p, hipStream_t st) {
-  static const int on = getenv_int("LBT_IGEMM_BIG", 1), tmin = getenv_int("LBT_IGEMM_BIG_MIN", 200);
-  if (!on || p.ksplit != 1 || p.ncol % 64 || p.cred % kBK) return false;
+  const lbt_igemm_tuning tu = big_tuning();
+  const int64_t tmin = tu.min_tiles;
+  if (!tu.big || p.ksplit != 1 || p.ncol % 64 || p.cred % kBK) return false;
   if ((p.M + 255) / 256 * (p.ncol / 64) > 0x7fffffff) return false;
-  // column tile: the widest that still gives LBT_IGEMM_BIG_MIN tiles (256 only without the quantising
-  // epilogue and on request: its 8 x 4 accumulator tiles per wave spill)
+  // column tile: the widest (<= max_bn) that still gives min_tiles tiles (256 only without the
+  // quantising epilogue and on request: its 8 x 4 accumulator tiles per wave spill)
   const int64_t mt = (p.M + 255) / 256;
   int bn = 0;
-  if (!A16 && !p.yq && p.ncol % 256 == 0 && getenv_int("LBT_IGEMM_BIG_BN256", 0) && mt * (p.ncol / 256) >= tmin) bn = 256;
-  else if (p.ncol % 128 == 0 && mt * (p.ncol / 128) >= tmin) bn = 128;
+  if (!A16 && !p.yq && p.ncol % 256 == 0 && tu.max_bn >= 256 && mt * (p.ncol / 256) >= tmin) bn = 256;
+  else if (tu.max_bn >= 128 && p.ncol % 128 == 0 && mt * (p.ncol / 128) >= tmin) bn = 128;
   else if (mt * (p.ncol / 64) >= tmin) bn = 64;
   if (!bn) return false;
-  // LDS ring depth (LBT_IGEMM_BIG_S): 2 by default -- the probe on the ResNet-50 shapes measured the
+  // LDS ring depth (stages): 2 by default -- the probe on the ResNet-50 shapes measured the
   // occupancy of 2 stages (A8 BN 128: 48 KiB, two workgroups per CU) ahead of the latency hiding of 3-4
-  // (72-96 KiB, one; the software-pipelined loop), except 3x3 dgrad16 at 28x28 / 14x14 (3-5 %)
-  static const int sdep = getenv_int("LBT_IGEMM_BIG_S", 2);
-  const int S = sdep;
+  // (72-96 KiB, one; the software-pipelined loop), except 3x3 dgrad16 at 28x28 / 14x14 (3-5 %).
+  // A16 runs 3 stages for any request above 2 (4 stages of 128-byte A rows at BN 128 would take 160 KiB).
+  const int S = tu.stages;
   if (bn == 256) {
     if constexpr (!A16) launch_big_bn<MODE, A16, 256, 4>(p, st);
   } else if (bn == 128) {
-    if (S == 2) launch_big_bn<MODE, A16, 128, 2>(p, st);
+    if (S <= 2) launch_big_bn<MODE, A16, 128, 2>(p, st);
     else if (S == 3 || A16) launch_big_bn<MODE, A16, 128, 3>(p, st);
     else launch_big_bn<MODE, A16, 128, 4>(p, st);
   } else {
-    if (S == 2) launch_big_bn<MODE, A16, 64, 2>(p, st);
+    if (S <= 2) launch_big_bn<MODE, A16, 64, 2>(p, st);
     else if (S == 3 || A16) launch_big_bn<MODE, A16, 64, 3>(p, st);
     else launch_big_bn<MODE, A16, 64, 4>(p, st);
   }
+  ++big_tuning().launches;
   return true;
 }
 
@@ -991,6 +1010,21 @@ extern "C" int64_t lbt_igemm_workspace_bytes(lbt_conv_desc d, int32_t mode, int3
     return splitk_bytes((int64_t)d.N * d.Ho * d.Wo, d.Cout, d.KH * d.KW * (d.Cin / kBK), a16 != 0);
   if (d.SH > 1 || d.SW > 1) return 0;  // strided dgrad: parity classes, never split
   return splitk_bytes((int64_t)d.N * d.H * d.W, d.Cin, d.KH * d.KW * (d.Cout / kBK), a16 != 0);
+}
+
+// lbt_igemm_tuning: the 256-row kernel's selection, read by every wide fwd / dgrad call after this
+extern "C" int lbt_igemm_get_tuning(lbt_igemm_tuning* out) {
+  if (!out) return LBT_EINVAL;
+  *out = big_tuning();
+  return 0;
+}
+
+extern "C" int lbt_igemm_set_tuning(const lbt_igemm_tuning* t) {
+  if (!t || t->min_tiles < 1 || t->stages < 2 || t->stages > 4 || (t->max_bn != 64 && t->max_bn != 128 && t->max_bn != 256))
+    return LBT_EINVAL;
+  lbt_igemm_tuning& cur = big_tuning();
+  cur.big = t->big; cur.min_tiles = t->min_tiles; cur.stages = t->stages; cur.max_bn = t->max_bn;
+  return 0;
 }
 
 // lbt_conv_fwd_igemm with a caller-owned workspace (ws_bytes >= lbt_igemm_workspace_bytes): the
@@ -1787,8 +1821,9 @@ extern "C" int lbt_conv_wgrad_igemm_store(const int8_t* xq, const void* gq, int3
     const int wci = wgrad1_wci(d);
     const int64_t chunks = (P + 63) / 64;
     const int64_t nblk = (int64_t)(d.Cin / (64 * wci)) * (d.Cout / (256 / wci));
-    // <= 2048 chunks a split: every int32 MFMA sum stays below 2^31 (|x' g| <= 2^14 a pixel)
-    if (nsplit > chunks || (chunks + nsplit - 1) / nsplit > 2048 || nblk * nsplit > 0x7fffffff) return LBT_EINVAL;
+    // <= 2047 chunks a split: every int32 MFMA sum stays below 2^31 (|x' g| <= 2^14 a pixel; 2048
+    // chunks of saturated codes, x' = -128 and both G bytes -128, would reach 2^31 exactly)
+    if (nsplit > chunks || (chunks + nsplit - 1) / nsplit > 2047 || nblk * nsplit > 0x7fffffff) return LBT_EINVAL;
     const int16_t* g16 = reinterpret_cast<const int16_t*>(gq);
     long long* sl = (long long*)slab;
     if (wci == 2) wgrad1_launch<2>(xq, g16, d, sl, nsplit, st);

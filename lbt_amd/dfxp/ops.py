@@ -611,6 +611,32 @@ def igemm_ok(c_gather, c_out):
     return c_gather % 64 == 0 and c_out % 16 == 0
 
 
+def igemm_tuning():
+    """The 256-row LDS-DMA GEMM's selection (lbt_igemm_get_tuning): dict big / min_tiles / stages / max_bn,
+    and `launches`, the number of 256-row GEMM launches this process has issued."""
+    t = _lib.IgemmTuning()
+    call("lbt_igemm_get_tuning", _lib.ctypes.byref(t))
+    return {f: getattr(t, f) for f, _ in t._fields_}
+
+
+class igemm_forced:
+    """Context manager: set the 256-row GEMM's selection for the calls made inside (tests force it onto
+    any shape / variant), restore the previous selection on exit."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        self.saved = igemm_tuning()
+        t = _lib.IgemmTuning(**dict(self.saved, **self.kw))
+        call("lbt_igemm_set_tuning", _lib.ctypes.byref(t))
+        return self
+
+    def __exit__(self, *exc):
+        call("lbt_igemm_set_tuning", _lib.ctypes.byref(_lib.IgemmTuning(**self.saved)))
+        return False
+
+
 def igemm_workspace_bytes(d, mode, a16):
     return int(_lib.load().lbt_igemm_workspace_bytes(d, int(mode), int(a16)))
 
@@ -702,12 +728,12 @@ def wgrad_store_nsplit(d, g_i16=True):
     """Pixel splits of the storing wide wgrad: >= ~512 workgroups, each split's slab written once.
     All-taps 3x3 body: splits of whole-row chunks, ~256 workgroups (one per CU; each covers all 9
     taps of a 64 x 64 channel block), <= 1024 chunks a split. 1x1 body (16-bit G): 64-pixel
-    chunks, ~512 workgroups, <= 2048 chunks a split."""
+    chunks, ~512 workgroups, <= 2047 chunks a split (int32 MFMA sums < 2^31)."""
     wci = wgrad1_wci(d) if g_i16 else 0
     if wci:
         chunks = -(-(d.N * d.Ho * d.Wo) // 64)
         nblk = (d.Cin // (64 * wci)) * (d.Cout // (256 // wci))
-        return min(chunks, max(-(-chunks // 2048), -(-512 // nblk)))
+        return min(chunks, max(-(-chunks // 2047), -(-512 // nblk)))
     if wgrad3_ok(d):
         rb = 64 // d.W
         chunks = d.N * (-(-d.H // rb))

@@ -461,8 +461,9 @@ class FusedResNet:
         stem_bwd = (self._stem and os.environ.get("LBT_STEM_BWD", "1") == "1" and C0 == 16 and Cin0 <= 4
                     and (dc.KH, dc.KW, dc.SH, dc.SW, dc.PT, dc.PL) == (3, 3, 1, 1, 1, 1) and dc.Ho == H and dc.Wo == W
                     and W in (8, 16, 32, 64) and (H * W) % 256 == 0)
-        # ... and that launch's row blocks as the last workgroups of the batched weight-gradient launch
-        # (lbt_conv_wgrad_many_stem_i8): both read only block 0's dgrad output
+        # ... and that launch's row blocks as workgroups of the batched weight-gradient launch
+        # (lbt_conv_wgrad_many_stem_i8; its first workgroups by default, its last with LBT_STEM_FIRST=0):
+        # both read only block 0's dgrad output
         stem_merge = (stem_bwd and not tail_fork and os.environ.get("LBT_STEM_MERGE", "1") == "1"
                       and len(self._wbatch) > 0)
         if not stem_merge:

@@ -116,10 +116,16 @@ class DfxpContext:
         lbt_dfxp_noise_fill). For consumers that would otherwise recompute each value once per sample
         (the wide GEMMs' quantising epilogue: a tile's rows are pixels, the noise repeats over the
         batch). A new table is filled at once; fill_noise_tables (the model's per-step prologue)
-        refills every table for the step that follows."""
+        refills every table for the step that follows. A superseded table or job array is kept alive
+        for the context's lifetime: a graph captured before may still launch the fill on it."""
         tabs = self.__dict__.setdefault("_ntab", {})
         ent = tabs.get(q.slot)
         if ent is None or ent[1] != inner:
+            retired = self.__dict__.setdefault("_retired", [])
+            if ent is not None:
+                retired.append(ent)
+            if getattr(self, "_njobs", None) is not None:
+                retired.append(self._njobs)
             n4 = (int(inner) + 3) // 4 * 4
             tab = torch.empty(n4, dtype=torch.float32, device=self.device)
             d = QDesc.from_buffer_copy(q.desc)
@@ -130,6 +136,7 @@ class DfxpContext:
             # job arrays uploaded here (eagerly: never inside a graph capture), the new table filled now
             self._njobs = self._job_array([e[3] for e in tabs.values()], max(e[1] for e in tabs.values()))
             dev, n, max_n = self._job_array([job], int(inner))
+            retired.append(dev)  # read by the fill launched just below (stream-ordered, asynchronous)
             _lib.call("lbt_dfxp_noise_fill", _lib.ptr(dev), n, max_n, None, 0, _lib.stream())
         return ent[2]
 

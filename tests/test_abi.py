@@ -51,7 +51,8 @@ STRUCTS = {"lbt_qdesc": _lib.QDesc, "lbt_conv_desc": _lib.ConvDesc, "lbt_bn_norm
            "lbt_qjob": _lib.QJob, "lbt_rjob": _lib.RJob, "lbt_pjob": _lib.PJob, "lbt_njob": _lib.NJob,
            "lbt_head": _lib.Head, "lbt_xchg": _lib.Xchg, "lbt_fseg": _lib.FSeg,
            "lbt_wgrad_job": _lib.WgradJob, "lbt_conv_bwd": _lib.ConvBwd,
-           "lbt_conv_fwd": _lib.ConvFwd, "lbt_conv_fwd_job": _lib.ConvFwdJob}
+           "lbt_conv_fwd": _lib.ConvFwd, "lbt_conv_fwd_job": _lib.ConvFwdJob,
+           "lbt_igemm_tuning": _lib.IgemmTuning}
 
 
 def test_struct_layouts_match_c():

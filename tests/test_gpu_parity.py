@@ -310,11 +310,11 @@ def test_batchnorm_bitexact(shape):
     assert ctx.ranges() == octx.new_ranges()
 
 
-def _build_pair(batch_seed=0, wd=2e-4, seed=0):
+def _build_pair(batch_seed=0, wd=2e-4, seed=0, weight_bits=None):
     from lbt_amd.models import CIFAR10_Resnet20
     ctx = DfxpContext(seed=seed)
-    gm = CIFAR10_Resnet20(8, weight_decay=wd, ctx=ctx)
-    om = oresnet.build_resnet((3, 3, 3), 8, wd)
+    gm = CIFAR10_Resnet20(8, weight_decay=wd, ctx=ctx, weight_bits=weight_bits)
+    om = oresnet.build_resnet((3, 3, 3), 8, wd, weight_bits=weight_bits)
     return ctx, gm, om
 
 
@@ -415,16 +415,20 @@ def _gpu_norms(gm):
     return [l for l in gm._walk() if isinstance(l, Normalization_q)]
 
 
-def test_fused_bench_workload_bitexact_vs_oracle():
+@pytest.mark.parametrize("weight_bits", [None, 4])
+def test_fused_bench_workload_bitexact_vs_oracle(weight_bits):
     """The EXACT timed configuration (bench.py: FusedResNet, B=128, bench batches, HIP-graph replay)
     against the oracle for 3 optimiser steps. B=128 puts stage 1 at P = 131 072 pixels, so the
     one-launch conv backward (dgrad_wgrad_kernel) takes its >= 2-shard int32 wgrad branch. With the
     GPU's d loss / d logits injected, every weight, the exponents and every BN running mean /
-    variance (dynamic_fixed_point.py:601-612) are bit-identical after each step; loss at 1e-5."""
+    variance (dynamic_fixed_point.py:601-612) are bit-identical after each step; loss at 1e-5.
+    weight_bits=4: configs[4]'s timed plan (bench.py --workload resnet20w4: packed 4-bit weight
+    images, every fused kernel's W4 variant) against the oracle's 4-bit weight quantisers
+    (dynamic_fixed_point.py:21-38 with bits=4)."""
     import bench
     from lbt_amd.fused import FusedResNet
     from lbt_amd.trainer import Trainer
-    ctx, gm, om = _build_pair(seed=0)
+    ctx, gm, om = _build_pair(seed=0, weight_bits=weight_bits)
     fm = FusedResNet(gm)
     state = dict(params=gpu_params(gm), accum=None, ranges=oresnet.init_ranges(om), step=0)
     state["accum"] = {k: np.zeros_like(v) for k, v in state["params"].items()}

@@ -1,0 +1,194 @@
+"""configs[3]'s production GEMM: the 256-row LDS-DMA implicit GEMM (igemm.hip igemm_big_kernel), which
+runs every large ResNet-50 forward and dgrad GEMM at the benched B=256.
+
+The kernel is taken only by GEMMs with >= 200 256-row tiles; ``ops.igemm_forced`` (the C-ABI
+lbt_igemm_set_tuning) lowers that threshold and picks the column tile and ring depth per call, so
+these tests put every variant on small ragged shapes and compare it, bit for bit, with the generic
+VALU kernels (conv_generic.hip), whose integer arithmetic restates tf.nn.conv2d and its input
+gradient on the quantised codes (reference dynamic_fixed_point.py:287-305). The last test runs a
+bottleneck model large enough to take the kernel with the default selection against the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nn as onn
+from oracle import resnet as oresnet
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (stages, max_bn) pairs: every ring depth and column tile of the kernel
+VARIANTS = [(2, 64), (3, 64), (4, 64), (2, 128), (3, 128), (4, 128), (2, 256)]
+
+
+def _setup(N, H, Cin, Cout, k, s, seed):
+    from lbt_amd.dfxp import ops
+    from lbt_amd.runtime import DfxpContext
+    rng = np.random.default_rng(seed)
+    ctx = DfxpContext(seed=seed)
+    qx, qw, qg = ctx.quantizer("t/X", 9, 2), ctx.quantizer("t/W", 8, 0), ctx.quantizer("t/g", 16, -3)
+    d = ops.conv_desc(N, H, H, Cin, Cout, k, k, s, s, "SAME")
+    W = torch.from_numpy(rng.uniform(-1, 1, size=(k, k, Cin, Cout)).astype(np.float32)).to(DEV)
+    w_hwio = torch.empty((k, k, Cin, Cout), dtype=torch.int8, device=DEV)
+    ksf, ksd = ops.packed_slices(k, k, Cin), ops.packed_slices(k, k, Cout)
+    wf = torch.zeros((Cout, ksf * 16), dtype=torch.int8, device=DEV)
+    wd = torch.zeros((Cin, ksd * 16), dtype=torch.int8, device=DEV)
+    colsum = torch.zeros(Cout, dtype=torch.int32, device=DEV)
+    ops.quantize_weight(W, qw, w_hwio=w_hwio, wf=wf, ksf=ksf, wd=wd, ksd=ksd, colsum=colsum)
+    return rng, ctx, (qx, qw, qg), d, w_hwio, (wf, ksf), (wd, ksd), colsum
+
+
+def _launches():
+    from lbt_amd.dfxp import ops
+    return ops.igemm_tuning()["launches"]
+
+
+def test_tuning_roundtrip_and_validation():
+    from lbt_amd import _lib
+    from lbt_amd.dfxp import ops
+    t0 = ops.igemm_tuning()
+    with ops.igemm_forced(min_tiles=1, stages=3, max_bn=64):
+        t = ops.igemm_tuning()
+        assert (t["min_tiles"], t["stages"], t["max_bn"]) == (1, 3, 64)
+    assert {k: v for k, v in ops.igemm_tuning().items() if k != "launches"} == \
+        {k: v for k, v in t0.items() if k != "launches"}
+    for bad in (dict(stages=5), dict(stages=1), dict(max_bn=32), dict(min_tiles=0)):
+        with pytest.raises(_lib.LbtError):
+            with ops.igemm_forced(**bad):
+                pass
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s", [
+    (3, 14, 64, 128, 3, 1),    # M = 588: two full 256-row tiles + 76 rows
+    (2, 15, 128, 256, 1, 1),   # M = 450, 256 columns (the 256-column tile)
+    (2, 15, 64, 64, 3, 2),     # strided fwd, M = 128: one partial tile
+    (1, 9, 192, 128, 3, 1),    # 27 k-blocks (odd: the pipelined loop's tail), M = 81
+])
+@pytest.mark.parametrize("a_kind", [0, 1, 2])
+def test_big_fwd_matches_generic(N, H, Cin, Cout, k, s, a_kind):
+    """fwd, every ring depth / column tile: signed int8, offset int8 (sum_k W from the MFMA against
+    ones, and from the caller's column sums), int16 codes (hi / lo' split)."""
+    from lbt_amd import _lib
+    from lbt_amd.dfxp import ops
+    rng, ctx, (qx, qw, _), d, w_hwio, (wf, ksf), _, colsum = _setup(N, H, Cin, Cout, k, s, N * H + Cin + a_kind)
+    if a_kind == 2:
+        x = torch.from_numpy(rng.integers(-256, 256, size=(N, H, H, Cin)).astype(np.int16)).to(DEV)
+        xg, signed9 = x, True
+    else:
+        x = torch.from_numpy(rng.integers(-128, 128, size=(N, H, H, Cin)).astype(np.int8)).to(DEV)
+        xg, signed9 = (x.to(torch.int16) + 128, True) if a_kind == 1 else (x, False)
+    ref = torch.empty((N, d.Ho, d.Wo, Cout), device=DEV)
+    ops.conv_fwd_generic(xg, signed9, w_hwio, d, qx.desc, qw.desc, ref)
+    for stages, max_bn in VARIANTS:
+        for cs in ((None, colsum) if a_kind == 1 else (None,)):
+            y = torch.full_like(ref, float("nan"))
+            n0 = _launches()
+            with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn):
+                _lib.call("lbt_conv_fwd_igemm", _lib.ptr(x), a_kind, _lib.ptr(wf), ksf, _lib.ptr(cs), d, qx.desc,
+                          qw.desc, _lib.ptr(y), _lib.stream())
+            assert _launches() == n0 + 1, "the 256-row kernel did not run"
+            assert torch.equal(y, ref), (stages, max_bn, cs is not None)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k", [
+    (3, 14, 128, 64, 3),    # 3x3 dgrad, ncol = Cin = 128, M = 588
+    (2, 15, 256, 128, 1),   # 1x1 dgrad, 256 output columns, M = 450
+    (1, 9, 64, 192, 3),     # 27 k-blocks, M = 81
+])
+@pytest.mark.parametrize("g_i16", [0, 1])
+@pytest.mark.parametrize("add", [False, True])
+def test_big_dgrad_matches_generic(N, H, Cin, Cout, k, g_i16, add):
+    """unit-stride dgrad (strided ones run as parity classes on the 128-row kernel), 8- and 16-bit
+    gradient codes, with and without the residual addend, every ring depth / column tile."""
+    from lbt_amd.dfxp import ops
+    rng, ctx, (_, qw, qg), d, w_hwio, _, (wd, ksd), _ = _setup(N, H, Cin, Cout, k, 1, N * H + Cout + g_i16)
+    if g_i16:
+        g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, d.Ho, d.Wo, Cout)).astype(np.int16)).to(DEV)
+    else:
+        g = torch.from_numpy(rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout)).astype(np.int8)).to(DEV)
+    addend = torch.from_numpy(rng.normal(size=(N, H, H, Cin)).astype(np.float32)).to(DEV) if add else None
+    ref = torch.empty((N, H, H, Cin), device=DEV)
+    (ops.conv_dgrad_generic16 if g_i16 else ops.conv_dgrad_generic)(g, w_hwio, d, qg.desc, qw.desc, ref)
+    if add:
+        ref = ref + addend
+    for stages, max_bn in VARIANTS:
+        dx = torch.full_like(ref, float("nan"))
+        n0 = _launches()
+        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn):
+            ops.conv_dgrad_igemm(g, g_i16, wd, ksd, d, qg.desc, qw.desc, dx, add_src=addend)
+        assert _launches() == n0 + 1, "the 256-row kernel did not run"
+        assert torch.equal(dx, ref), (stages, max_bn)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k", [(3, 14, 64, 128, 3), (2, 15, 128, 64, 1)])
+@pytest.mark.parametrize("a_kind", [0, 1])
+@pytest.mark.parametrize("stochastic", [True, False])
+def test_big_quantising_epilogue_matches_fwd_then_quantize(N, H, Cin, Cout, k, a_kind, stochastic):
+    """lbt_conv_fwd_igemm_q on the 256-row kernel (Normalization_q's input quantiser on the MFMA
+    accumulators, noise from the per-step table) == lbt_conv_fwd_igemm -> lbt_dfxp_quantize: the same
+    int8 codes, overflow counters and exact channel sums (reference :291 then :584-588)."""
+    from lbt_amd._lib import NSHARD, OUT_I8
+    from lbt_amd.dfxp import ops
+    rng, ctx, (qx, qw, _), d, w_hwio, (wf, ksf), _, _ = _setup(N, H, Cin, Cout, k, 1, N + H + Cout + a_kind)
+    # a range that puts a few percent of the outputs past the clip (both counters non-zero)
+    qo = ctx.quantizer("t/bnX", 8, 4, stochastic=stochastic)
+    x = torch.from_numpy(rng.integers(-128, 128, size=(N, H, H, Cin)).astype(np.int8)).to(DEV)
+    y = torch.empty((N, d.Ho, d.Wo, Cout), device=DEV)
+    ops.conv_fwd_igemm(x, a_kind, wf, ksf, d, qx.desc, qw.desc, y)
+    cs_ref = torch.zeros(NSHARD * 2 * Cout, dtype=torch.int64, device=DEV)
+    ctx.counts.zero_()
+    q_ref = ops.quantize(y, qo, OUT_I8, chsum=cs_ref, C=Cout)
+    cnt_ref = ctx.counts_view()[qo.slot].sum(0).cpu()
+    assert cnt_ref[0] > 0 and cnt_ref[1] > cnt_ref[0]
+    for stages, max_bn in VARIANTS[:-1]:  # the quantising epilogue never takes the 256-column tile
+        ctx.counts.zero_()
+        cs = torch.zeros_like(cs_ref)
+        yq = torch.full(q_ref.shape, 99, dtype=torch.int8, device=DEV)
+        n0 = _launches()
+        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn):
+            ops.conv_fwd_igemm_q(x, a_kind, wf, ksf, d, qx.desc, qw.desc, yq, qo, cs)
+        assert _launches() == n0 + 1, "the 256-row kernel did not run"
+        assert torch.equal(yq, q_ref), (stages, max_bn)
+        assert torch.equal(ctx.counts_view()[qo.slot].sum(0).cpu(), cnt_ref), (stages, max_bn)
+        assert torch.equal(cs.view(NSHARD, -1).sum(0), cs_ref.view(NSHARD, -1).sum(0)), (stages, max_bn)
+
+
+def test_bottleneck_takes_big_kernel_naturally_bitexact_vs_oracle():
+    """A ResNet-50 configuration (one bottleneck per stage, width 64, 16-bit gradients, 224x224,
+    B=17) whose stage-1 GEMMs have >= 200 256-row tiles, so the DEFAULT selection runs them on the
+    256-row kernel (3x3 fwd with the quantising epilogue, 3x3 and 1x1 dgrad16): forward logits,
+    every gradient and every exponent update bit-exact against the oracle."""
+    from lbt_amd.dfxp import ops
+    from lbt_amd.models import ImageNet_Resnet
+    from lbt_amd.runtime import DfxpContext
+    t = ops.igemm_tuning()
+    assert t["big"] == 1 and t["min_tiles"] == 200, "run with the default selection"
+    B, image, classes = 17, 224, 16
+    ctx = DfxpContext(seed=1)
+    gm = ImageNet_Resnet(8, (1, 1, 1, 1), grad_bits=16, width=64, classes=classes, image=image, ctx=ctx)
+    om = oresnet.build_resnet50((1, 1, 1, 1), 64, classes, 8, 16)
+    params = {}
+    for owner, var, _ in gm.param_slots():
+        params[owner.name + {"W": "/W", "gamma": "/g", "beta": "/b"}[var]] = getattr(owner, var).detach().cpu().numpy()
+    oresnet.set_params(om, params)
+    rng = np.random.default_rng(2)
+    x = ((rng.integers(0, 256, size=(B, image, image, 3)) - 127.5) / 128).astype(np.float32)
+    y = rng.integers(0, classes, size=B).astype(np.int32)
+    octx = onn.Ctx(oresnet.init_ranges(om), 0, ctx.seed)
+    n0 = _launches()
+    logits = gm.forward(torch.from_numpy(x).to(DEV))
+    gm.compute_loss(torch.from_numpy(y).to(DEV))
+    dz = gm.dlogits.cpu().numpy()
+    gm.backward()
+    torch.cuda.synchronize()
+    assert _launches() - n0 >= 3, "the default selection did not take the 256-row kernel"
+    lr = om.forward(x, octx)
+    assert np.array_equal(logits.cpu().numpy(), lr), "forward must be bit-exact"
+    om.backward(dz, octx)
+    og = oresnet.get_grads(om)
+    for owner, var, gname in gm.param_slots():
+        k = owner.name + {"W": "/W", "gamma": "/g", "beta": "/b"}[var]
+        assert np.array_equal(getattr(owner, gname).detach().cpu().numpy(), og[k]), k
+    ctx.update_range_op()
+    assert ctx.ranges() == octx.new_ranges()
