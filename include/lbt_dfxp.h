@@ -662,9 +662,12 @@ int lbt_bn_param_grads_many(const lbt_pjob* jobs, int32_t njobs, int32_t max_c, 
  * step's input images quantised to int16 codes (input->out_kind == LBT_OUT_I16, n and inner
  * multiples of 4, Philox noise inline -- the input quantiser needs no table). Independent parts:
  * nothing here reads another part's output. Job arrays in device memory, *input in host memory. */
+/* snap_n > 0: the launch also copies snap_src[0, snap_n) to snap_dst (the step's exponents, read by
+ * lbt_step_reduce_update's dequantisations while its range-update blocks rewrite the live ones).  */
 int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_n, int64_t* zero, int64_t nzero,
                       const lbt_wjob* wjobs, int32_t nw, int32_t max_cout, const lbt_qjob* qjobs, int32_t nq,
-                      const lbt_qjob* input, void* stream);
+                      const lbt_qjob* input, const int32_t* snap_src, int32_t* snap_dst, int32_t snap_n,
+                      void* stream);
 
 /* The end of a step's backward in ONE launch: lbt_conv_wgrad_reduce_many's jobs (r_blocks =
  * sum of ceil(K*Cout/256)), lbt_bn_param_grads_many's jobs (Cout <= max_c) and, if head is not
@@ -672,6 +675,22 @@ int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_n, int64_t*
  * the loss summed in softmax_xent's order). Job arrays in device memory, *head in host memory.  */
 int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
                     int32_t max_c, const lbt_head* head, void* stream);
+
+/* lbt_step_reduce and lbt_step_update in ONE launch (single process): every block that forms a
+ * gradient element also applies MomentumOptimizer to it (acc = mu*acc + g; w -= lr*acc,
+ * trainer.py:81-82, lbt_sgd_momentum's arithmetic, gscale 1) -- the job's dw / dgamma / dbeta and the
+ * head's dw lie inside the flat gradient buffer g, their parameter and accumulator at the same
+ * offset in w and a -- and (nslots + 3) / 4 more blocks run update_range on every slot and advance
+ * step (lbt_dfxp_range_update). Those rewrite the exponents while other blocks dequantise, so
+ * every job / head descriptor must read its exponents from a copy taken earlier in the step
+ * (lbt_step_prologue's snapshot). Results bit-identical to lbt_step_reduce + lbt_step_update.   */
+typedef struct lbt_update {
+  float* w; float* a; const float* g; float lr, mu;
+  int32_t* exps; int32_t* counts; const int32_t* bits; const float* target; const float* nelem;
+  uint64_t* step; int32_t nslots; int32_t pad;
+} lbt_update;
+int lbt_step_reduce_update(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
+                           int32_t max_c, const lbt_head* head, const lbt_update* u, void* stream);
 
 /* lbt_sgd_momentum and lbt_dfxp_range_update in ONE launch (independent: the optimiser reads no
  * exponent; the range update reads only the step's counters).                              */

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -158,6 +158,12 @@ class IgemmTuning(ctypes.Structure):
                 ("launches", c_int64)]
 
 
+class Update(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("a", c_void_p), ("g", c_void_p), ("lr", c_float), ("mu", c_float),
+                ("exps", c_void_p), ("counts", c_void_p), ("bits", c_void_p), ("target", c_void_p),
+                ("nelem", c_void_p), ("step", c_void_p), ("nslots", c_int32), ("pad", c_int32)]
+
+
 class FSeg(ctypes.Structure):
     _fields_ = [("off", c_int64), ("n", c_int64), ("kind", c_int32), ("qx", QDesc), ("qg", QDesc), ("wd2", c_float)]
 
@@ -269,9 +275,11 @@ _SIGS = {
     "lbt_bn_param_grads_many": [_P, c_int32, c_int32, _P],
     "lbt_head_scratch_bytes": [c_int32, c_int32, c_int32],
     "lbt_head_fwd_bwd": [_P, _P],
-    "lbt_step_prologue": [_P, c_int32, c_int64, _P, c_int64, _P, c_int32, c_int32, _P, c_int32, _P, _P],
+    "lbt_step_prologue": [_P, c_int32, c_int64, _P, c_int64, _P, c_int32, c_int32, _P, c_int32, _P, _P, _P, c_int32,
+                          _P],
     "lbt_step_reduce": [_P, c_int32, c_int32, _P, c_int32, c_int32, _P, _P],
     "lbt_step_reduce_x": [_P, c_int32, c_int32, _P, c_int32, c_int32, _P, _P, _P],
+    "lbt_step_reduce_update": [_P, c_int32, c_int32, _P, c_int32, c_int32, _P, _P, _P],
     "lbt_step_finish": [_P, c_int32, c_int32, _P, _P, _P, _P, c_float, c_float, _P, c_int64, c_int32, _P],
     "lbt_dfxp_range_update_x": [_P, _P, c_int64, _P, _P, _P, c_int32, _P, _P],
     "lbt_grad_buffer_bwd": [_P, c_int64, _P, c_int64, c_int64, QDesc, _P, _P],

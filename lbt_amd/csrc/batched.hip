@@ -68,10 +68,21 @@ __global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob*
   quantize_many_block(jobs, blockIdx.y);
 }
 
+// MomentumOptimizer on one element whose parameter wv and accumulator am were loaded by the caller:
+// sgd_momentum_elem's operations and order (gscale 1: g * 1.0f == g), so bit-identical to lbt_step_update
+LBT_DEV void sgd_update(float wv, float am, float gv, const lbt_update& u, int64_t o) {
+  const float t = u.mu * am;
+  const float an = t + gv;
+  u.a[o] = an;
+  const float step = u.lr * an;
+  u.w[o] = wv - step;
+}
+
 // Blocks are allotted to the jobs in order, ceil(K*Cout/256) each (1-D grid); a block reduces 256
 // consecutive outputs over the slab's shards, with the offset correction 128 * sum_p g[co]
 // (x_u8off) summed once per column into LDS. lds: >= 4 KB.
-LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, uint8_t* lds, const lbt_xchg& x) {
+LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, uint8_t* lds, const lbt_xchg& x,
+                        const lbt_update& u) {
   int64_t* nbs = reinterpret_cast<int64_t*>(lds);                   // [256]
   long long* colsum = reinterpret_cast<long long*>(lds + 2048);      // [256]
   int* s_job = reinterpret_cast<int*>(lds + 4096);
@@ -127,6 +138,13 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
     for (int k = 0; k < LBT_NSHARD; ++k) v[k] = j.gcolsum[(int64_t)k * 2 * j.Cout + c];
   }
   long long s = 0;
+  // the optimiser's operands (lbt_step_reduce_update) in the same round trip as the slab
+  float wv = 0.f, am = 0.f;
+  const int64_t o = u.w ? (j.dw - u.g) + i : 0;
+  if (u.w && i < total) {
+    wv = j.w[i];
+    am = u.a[o];
+  }
   if (i < total)
     for (int b = 0; b < j.nsplit; ++b) s += j.slab[(int64_t)b * total + i];
   long long t = 0;
@@ -145,6 +163,14 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
     return;
   }
   const float scale = ldexpf(1.0f, -(frac_exp(j.qx) + frac_exp(j.qg)));
+  if (u.w) {  // lbt_step_reduce_update: the gradient, then MomentumOptimizer on the same element
+    const float a = (float)s * scale;
+    const float b = j.wd2 * wv;
+    const float gv = a + b;
+    j.dw[i] = gv;
+    sgd_update(wv, am, gv, u, o);
+    return;
+  }
   const float a = (float)s * scale;
   const float b = j.wd2 * j.w[i];
   j.dw[i] = a + b;
@@ -152,11 +178,18 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
 
 __global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs, int njobs) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4112];
-  rjob_block(jobs, njobs, blockIdx.x, lds, lbt_xchg{});
+  rjob_block(jobs, njobs, blockIdx.x, lds, lbt_xchg{}, lbt_update{});
 }
 
-LBT_DEV void pjob_channel(const lbt_pjob& j, int c, const lbt_xchg& x) {
+LBT_DEV void pjob_channel(const lbt_pjob& j, int c, const lbt_xchg& x, const lbt_update& u) {
   if (c >= j.C) return;
+  int64_t og = 0, ob = 0;
+  float wg = 0.f, ag = 0.f, wb = 0.f, ab = 0.f;
+  if (u.w) {  // the optimiser's operands, loaded with the sums
+    og = (j.dgamma - u.g) + c;
+    ob = (j.dbeta - u.g) + c;
+    wg = u.w[og]; ag = u.a[og]; wb = u.w[ob]; ab = u.a[ob];
+  }
   long long vr[LBT_NSHARD], vg[LBT_NSHARD];  // all shard loads in flight at once
 #pragma unroll
   for (int k = 0; k < LBT_NSHARD; ++k) {
@@ -176,13 +209,22 @@ LBT_DEV void pjob_channel(const lbt_pjob& j, int c, const lbt_xchg& x) {
   }
   const double g2 = ldexp(1.0, -frac_exp(j.qrg)), r = ldexp(1.0, -frac_exp(j.qr));
   const float a = (float)((double)sgr * (g2 * r));
+  if (u.w) {
+    const float b = j.wd2 * wg;  // j.gamma[c] == u.w[og]
+    const float dg = a + b, db = (float)((double)sg * g2);
+    j.dgamma[c] = dg;
+    j.dbeta[c] = db;
+    sgd_update(wg, ag, dg, u, og);
+    sgd_update(wb, ab, db, u, ob);
+    return;
+  }
   const float b = j.wd2 * j.gamma[c];
   j.dgamma[c] = a + b;
   j.dbeta[c] = (float)((double)sg * g2);
 }
 
 __global__ void param_grads_many_kernel(const lbt_pjob* __restrict__ jobs) {
-  pjob_channel(jobs[blockIdx.y], blockIdx.x * blockDim.x + threadIdx.x, lbt_xchg{});
+  pjob_channel(jobs[blockIdx.y], blockIdx.x * blockDim.x + threadIdx.x, lbt_xchg{}, lbt_update{});
 }
 
 // One wave per slot: lane k < LBT_NSHARD reads (and zeroes) shard k of the overflow counters.
@@ -204,28 +246,41 @@ LBT_DEV void fold_slot_x(const lbt_xchg& x, int i) {
   }
 }
 
-// lbt_step_reduce(_x): [1 head block][np * pblk param-grad blocks][exchange only: ceil(nslots / 4)
-// counter-fold blocks][r_blocks wgrad-reduce blocks]. The head block (a serial chain of ~7 us: the
-// records, the Dense_q dW, the ordered loss sum) is dispatched first: placed last, it started only
-// after the ~1 000 wgrad-reduce blocks had been dispatched (~5 us) and ended the launch.
+// lbt_step_reduce(_x / _update): [1 head block][update only: ceil(nslots / 4) range-update blocks]
+// [np * pblk param-grad blocks][exchange only: ceil(nslots / 4) counter-fold blocks][r_blocks
+// wgrad-reduce blocks]. The head block (a serial chain of ~7 us: the records, the Dense_q dW, the
+// ordered loss sum) is dispatched first: placed last, it started only after the ~1 000 wgrad-reduce
+// blocks had been dispatched (~5 us) and ended the launch.
 __global__ __launch_bounds__(256) void step_reduce_kernel(const lbt_rjob* __restrict__ rjobs, int nr, int r_blocks,
                                                           const lbt_pjob* __restrict__ pjobs, int np, int pblk,
-                                                          lbt_head head, int has_head, lbt_xchg x, int fold) {
+                                                          lbt_head head, int has_head, lbt_xchg x, int fold,
+                                                          lbt_update u, int ublocks) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLds];
   int b = blockIdx.x;
   LBT_TS(0);
   if (has_head) {
     if (b == 0) {
       LBT_TROLE(3);
-      head_reduce(head, x, lds);
+      head_reduce(head, x, lds, u);
       LBT_TS(1);
       return;
     }
     --b;
   }
+  if (b < ublocks) {  // update_range (dynamic_fixed_point.py:70-94): one wave per slot
+    LBT_TROLE(5);
+    const int i = b * 4 + (int)(threadIdx.x >> 6);
+    if (i < u.nslots && u.nelem[i] > 0.f) {
+      int c1, c2;
+      if (wave_shard_totals(u.counts, i, c1, c2)) range_apply(i, c1, c2, u.exps, u.bits, u.target, u.nelem);
+    }
+    if (b == 0 && threadIdx.x == 0) u.step[0] += 1ull;
+    return;
+  }
+  b -= ublocks;
   if (b < np * pblk) {
     LBT_TROLE(2);
-    pjob_channel(pjobs[b / pblk], (b % pblk) * 256 + threadIdx.x, x);
+    pjob_channel(pjobs[b / pblk], (b % pblk) * 256 + threadIdx.x, x, u);
     LBT_TS(1);
     return;
   }
@@ -238,7 +293,7 @@ __global__ __launch_bounds__(256) void step_reduce_kernel(const lbt_rjob* __rest
   }
   b -= fold;
   LBT_TROLE(1);
-  rjob_block(rjobs, nr, b, lds, x);
+  rjob_block(rjobs, nr, b, lds, x, u);
   LBT_TS(1);
 }
 
@@ -308,6 +363,7 @@ struct Prologue {
   const lbt_wjob* wjobs; int nw, max_cout;
   const lbt_qjob* qjobs; int nq;
   lbt_qjob input; int nin;
+  const int32_t* snap_src; int32_t* snap_dst; int nsnap;
 };
 
 __global__ __launch_bounds__(kThreads) void step_prologue_kernel(Prologue a) {
@@ -335,6 +391,11 @@ __global__ __launch_bounds__(kThreads) void step_prologue_kernel(Prologue a) {
     return;
   }
   b -= a.nq;
+  if (b < (a.nsnap > 0 ? 1 : 0)) {  // the step's exponents, for lbt_step_reduce_update's dequantisations
+    for (int i = threadIdx.x; i < a.nsnap; i += kThreads) a.snap_dst[i] = a.snap_src[i];
+    return;
+  }
+  if (a.nsnap > 0) --b;
   LBT_TROLE(1);
   noise_fill_block(a.njobs, a.zero, a.nzero, b % a.nbx, b / a.nbx, a.nbx, kNoisePer, a.nn);
   LBT_TS(1);
@@ -357,8 +418,10 @@ extern "C" int lbt_dfxp_noise_fill(const lbt_njob* jobs, int32_t njobs, int64_t 
 
 extern "C" int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_n, int64_t* zero, int64_t nzero,
                                  const lbt_wjob* wjobs, int32_t nw, int32_t max_cout, const lbt_qjob* qjobs, int32_t nq,
-                                 const lbt_qjob* input, void* stream) {
+                                 const lbt_qjob* input, const int32_t* snap_src, int32_t* snap_dst, int32_t snap_n,
+                                 void* stream) {
   if (nn < 0 || nw < 0 || nq < 0 || (nn > 0 && max_n <= 0) || (nw > 0 && max_cout <= 0)) return LBT_EINVAL;
+  if (snap_n < 0 || (snap_n > 0 && (!snap_src || !snap_dst))) return LBT_EINVAL;
   if (nzero > 0 && (reinterpret_cast<uintptr_t>(zero) % 16)) return LBT_EINVAL;
   Prologue a{};
   a.njobs = njobs; a.nn = nn; a.zero = zero; a.nzero = nzero > 0 ? nzero : 0;
@@ -372,7 +435,8 @@ extern "C" int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_
       return LBT_EINVAL;
     a.nin = (int)((a.input.n / 4 + kThreads - 1) / kThreads);
   }
-  const int64_t blocks = (int64_t)a.nbx * nn + (int64_t)a.max_cout * nw + nq + a.nin;
+  a.snap_src = snap_src; a.snap_dst = snap_dst; a.nsnap = snap_n;
+  const int64_t blocks = (int64_t)a.nbx * nn + (int64_t)a.max_cout * nw + nq + a.nin + (snap_n > 0 ? 1 : 0);
   if (blocks <= 0) return LBT_OK;
   if (blocks > 0x7fffffff) return LBT_EINVAL;
   hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, a);
@@ -465,7 +529,7 @@ extern "C" int lbt_conv_wgrad_reduce_many(const lbt_rjob* jobs, int32_t njobs, i
 
 namespace {
 int step_reduce_launch(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
-                       int32_t max_c, const lbt_head* head, const lbt_xchg& x, void* stream) {
+                       int32_t max_c, const lbt_head* head, const lbt_xchg& x, const lbt_update& u, void* stream) {
   if (nr < 0 || np < 0 || nr > 256 || r_blocks < 0 || (nr > 0 && r_blocks == 0) || (np > 0 && max_c <= 0))
     return LBT_EINVAL;
   lbt_head h = {};
@@ -477,25 +541,36 @@ int step_reduce_launch(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, cons
   if (x.buf && (!x.gbase || x.nslots < 0 || (x.nslots > 0 && !x.counts) || x.cnt_off < 0 || x.loss_off < 0 ||
                 (x.pjob_scale != 0 && x.pjob_scale != 1)))
     return LBT_EINVAL;
+  if (u.w && (x.buf || !u.a || !u.g || u.nslots < 0 || !u.exps || !u.counts || !u.bits || !u.target || !u.nelem ||
+              !u.step))
+    return LBT_EINVAL;
   const int pblk = np > 0 ? (max_c + 255) / 256 : 0;
   const int fold = x.buf ? (x.nslots + 3) / 4 : 0;
-  const int64_t blocks = (int64_t)r_blocks + (int64_t)np * pblk + (head ? 1 : 0) + fold;
+  const int ublocks = u.w ? (u.nslots > 0 ? (u.nslots + 3) / 4 : 1) : 0;
+  const int64_t blocks = (int64_t)r_blocks + (int64_t)np * pblk + (head ? 1 : 0) + fold + ublocks;
   if (blocks <= 0) return LBT_OK;
   hipLaunchKernelGGL(step_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rjobs, nr, r_blocks,
-                     pjobs, np, pblk, h, head ? 1 : 0, x, fold);
+                     pjobs, np, pblk, h, head ? 1 : 0, x, fold, u, ublocks);
   return (int)hipGetLastError();
 }
 }  // namespace
 
 extern "C" int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
                                int32_t max_c, const lbt_head* head, void* stream) {
-  return step_reduce_launch(rjobs, nr, r_blocks, pjobs, np, max_c, head, lbt_xchg{}, stream);
+  return step_reduce_launch(rjobs, nr, r_blocks, pjobs, np, max_c, head, lbt_xchg{}, lbt_update{}, stream);
 }
 
 extern "C" int lbt_step_reduce_x(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,
                                  int32_t max_c, const lbt_head* head, const lbt_xchg* x, void* stream) {
   if (!x || !x->buf) return LBT_EINVAL;
-  return step_reduce_launch(rjobs, nr, r_blocks, pjobs, np, max_c, head, *x, stream);
+  return step_reduce_launch(rjobs, nr, r_blocks, pjobs, np, max_c, head, *x, lbt_update{}, stream);
+}
+
+extern "C" int lbt_step_reduce_update(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs,
+                                      int32_t np, int32_t max_c, const lbt_head* head, const lbt_update* u,
+                                      void* stream) {
+  if (!u || !u->w) return LBT_EINVAL;
+  return step_reduce_launch(rjobs, nr, r_blocks, pjobs, np, max_c, head, lbt_xchg{}, *u, stream);
 }
 
 namespace {

@@ -351,6 +351,36 @@ LBT_DEV bool chan_scatter_ok(int period) { return period >= 1 && period <= 16; }
 LBT_DEV bool chan_scatter_owner(int period) { return (int)(threadIdx.x & 15) < period; }
 
 // MomentumOptimizer.apply_gradients (trainer.py:81-82) on element i: a = mu*a + g*gscale; w -= lr*a.
+// update_range on one slot from its total counters (dynamic_fixed_point.py:70-94).
+LBT_DEV void range_apply(int i, int c1, int c2, int32_t* exps, const int32_t* bits, const float* target,
+                         const float* nelem) {
+  if (bits[i] >= 32) return;  // the 32-bit bypass adds no update_range op (:22-23)
+  const float r1 = (float)c1 / nelem[i];
+  const float r2 = (float)c2 / nelem[i];
+  const float t = target[i];
+  const int delta = r1 > t ? 1 : (r2 <= t ? -1 : 0);
+  int I = exps[i] + delta;
+  const int hi = bits[i] - 1, lo = bits[i] - 1 - kEMax;
+  I = I > hi ? hi : (I < lo ? lo : I);
+  exps[i] = I;
+}
+
+// One wave per slot: lane k < LBT_NSHARD reads (and zeroes) shard k, a wave sum gives the totals.
+LBT_DEV bool wave_shard_totals(int32_t* counts, int i, int& c1, int& c2) {
+  const int lane = threadIdx.x & 63;
+  int a = 0, b = 0;
+  if (lane < LBT_NSHARD) {
+    int32_t* c = counts + ((int64_t)i * LBT_NSHARD + lane) * LBT_CSTRIDE;
+    a = c[0];
+    b = c[1];
+    c[0] = 0;
+    c[1] = 0;
+  }
+  c1 = wave_sum_i32(a);
+  c2 = wave_sum_i32(b);
+  return lane == 0;
+}
+
 LBT_DEV void sgd_momentum_elem(float* w, float* a, const float* g, int64_t i, float lr, float mu, float gscale) {
   const float t = mu * a[i];
   const float gg = g[i] * gscale;

@@ -17,7 +17,8 @@ constexpr int kHeadLds = kHeadRecBytes + kHeadT * 16 * 4;   // + per-thread part
 // and loss[0] = (float)(sum of the terms in softmax_xent_kernel's order / loss_n). lds: kHeadLds
 // bytes. With an exchange buffer (x.buf, lbt_step_reduce_x) the integer sums go to
 // x.buf[(dw - gbase) + ...] instead, and the loss-term sum, in 2^-32 fixed point, to x.buf[loss_off].
-LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds) {
+// u.w != NULL (lbt_step_reduce_update): MomentumOptimizer on each dw element as it is formed.
+LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds, const lbt_update& u) {
   uint32_t* s_rec = reinterpret_cast<uint32_t*>(lds);
   int(*s_acc)[16] = reinterpret_cast<int(*)[16]>(lds + kHeadRecBytes);
   __shared__ double s_red[kHeadT];
@@ -30,10 +31,14 @@ LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds) {
   double part = 0.0;
   for (int kb = 0; kb < K; kb += 16) {
     float wf[16 * 256 / kHeadT];  // this pass's fp32 weights (decay term), loaded ahead
+    float af[16 * 256 / kHeadT];  // ... and their momentum accumulators (u.w)
+    const int64_t ob = u.w ? h.dw - u.g : 0;
 #pragma unroll
     for (int j = 0; j < 16 * 256 / kHeadT; ++j) {
       const int o = t + j * kHeadT, oc = o >> 4, ok = kb + (o & 15);
-      wf[j] = h.w[(oc < C && ok < K) ? oc * K + ok : 0];
+      const int e = (oc < C && ok < K) ? oc * K + ok : 0;
+      wf[j] = h.w[e];
+      af[j] = u.w ? u.a[ob + e] : 0.f;
     }
     int sacc[16];
 #pragma unroll
@@ -92,7 +97,15 @@ LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds) {
         }
         const float a = (float)(long long)sum * wscale;
         const float b = h.wd2 * wf[j];
-        h.dw[oc * K + ok] = a + b;
+        const float gv = a + b;
+        h.dw[oc * K + ok] = gv;
+        if (u.w) {  // sgd_momentum_elem's arithmetic (gscale 1)
+          const float tm = u.mu * af[j];
+          const float an = tm + gv;
+          u.a[ob + oc * K + ok] = an;
+          const float stp = u.lr * an;
+          u.w[ob + oc * K + ok] = wf[j] - stp;
+        }
       }
     }
   }

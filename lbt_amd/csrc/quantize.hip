@@ -117,36 +117,6 @@ __global__ __launch_bounds__(kThreads) void quantize_generic_kernel(
   block_flush_counts(q, ov1, ov2, sh_cnt);
 }
 
-// update_range on one slot from its total counters (dynamic_fixed_point.py:70-94).
-LBT_DEV void range_apply(int i, int c1, int c2, int32_t* exps, const int32_t* bits, const float* target,
-                         const float* nelem) {
-  if (bits[i] >= 32) return;  // the 32-bit bypass adds no update_range op (:22-23)
-  const float r1 = (float)c1 / nelem[i];
-  const float r2 = (float)c2 / nelem[i];
-  const float t = target[i];
-  const int delta = r1 > t ? 1 : (r2 <= t ? -1 : 0);
-  int I = exps[i] + delta;
-  const int hi = bits[i] - 1, lo = bits[i] - 1 - kEMax;
-  I = I > hi ? hi : (I < lo ? lo : I);
-  exps[i] = I;
-}
-
-// One wave per slot: lane k < LBT_NSHARD reads (and zeroes) shard k, a wave sum gives the totals.
-LBT_DEV bool wave_shard_totals(int32_t* counts, int i, int& c1, int& c2) {
-  const int lane = threadIdx.x & 63;
-  int a = 0, b = 0;
-  if (lane < LBT_NSHARD) {
-    int32_t* c = counts + ((int64_t)i * LBT_NSHARD + lane) * LBT_CSTRIDE;
-    a = c[0];
-    b = c[1];
-    c[0] = 0;
-    c[1] = 0;
-  }
-  c1 = wave_sum_i32(a);
-  c2 = wave_sum_i32(b);
-  return lane == 0;
-}
-
 // grid: one wave per slot (4 slots per 256-thread block)
 __global__ void range_update_kernel(int32_t* exps, int32_t* counts, const int32_t* bits,
                                     const float* target, const float* nelem, int nslots,
@@ -337,4 +307,4 @@ extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, 
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_abi_version(void) { return 16; }
+extern "C" int lbt_abi_version(void) { return 17; }

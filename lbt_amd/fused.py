@@ -118,6 +118,12 @@ class FusedResNet:
         self.batch_wgrad = (os.environ.get("LBT_BATCH_WGRAD", "1") == "1" and not self.overlap_wgrad
                             and not self.side_wgrad)
         self._wbatch = []  # the batched launch's jobs (lbt_wgrad_job), in backward order
+        # the optimiser and the range update inside the step's last launch (lbt_step_reduce_update;
+        # single process): one launch fewer per step. Off until the Trainer hands over its flat
+        # buffers and hyper-parameters (set_optimizer)
+        self.fused_update = os.environ.get("LBT_FUSED_UPDATE", "1") == "1"
+        self._upd = _lib.Update()
+        self._upd_set = False
 
     # ------------------------------------------------------------------ Trainer interface
     def param_slots(self):
@@ -192,14 +198,40 @@ class FusedResNet:
         run.kname = "allreduce"
         return run
 
-    def train_fwd_bwd(self, X, labels):
+    def set_optimizer(self, flat, lr, momentum):
+        """MomentumOptimizer's flat buffers and hyper-parameters (trainer.py:79-84) for the fused update
+        (train_fwd_bwd(update=True)); call again when lr changes, before the step is re-captured."""
+        ctx = self.ctx
+        u = self._upd
+        u.w, u.a, u.g = flat.w.data_ptr(), flat.a.data_ptr(), flat.g.data_ptr()
+        u.lr, u.mu = float(lr), float(momentum)
+        u.exps, u.counts, u.bits = ctx.exps.data_ptr(), ctx.counts.data_ptr(), ctx.bits.data_ptr()
+        u.target, u.nelem, u.step = ctx.target.data_ptr(), ctx.nelem.data_ptr(), ctx.step.data_ptr()
+        u.nslots = len(ctx.quantizers)
+        self._upd_set = True
+
+    def updates_in_step(self):
+        """Whether train_fwd_bwd(update=True) applies the optimiser and the range update itself."""
+        return self.fused_update and self._upd_set and self.xchg is None
+
+    def _flat_params(self):
+        return [getattr(o, v) for o, v, _ in self.model.param_slots()]
+
+    def step_tail(self, update):
+        """The step's last launch: the reductions (+ the optimiser and the range update)."""
+        return self._tail_upd if update and self.updates_in_step() else self._tail_fused
+
+    def train_fwd_bwd(self, X, labels, update=False):
         """forward + compute_loss + backward of one training step, the head as one launch
-        (lbt_head_fwd_bwd): same results bit for bit as the three calls."""
+        (lbt_head_fwd_bwd): same results bit for bit as the three calls. update=True (and
+        updates_in_step()): the last launch also applies SGD-momentum and update_range (the Trainer's
+        optimiser step, bit-identical). Returns whether it did."""
         self._ensure(X)
         self._bind(X, labels)
-        for f in self._fwd + self._hfused + self._bwd + self._tail_fused:
+        tail = self.step_tail(update)
+        for f in self._fwd + self._hfused + self._bwd + tail:
             f()
-        return self.loss
+        return tail is not self._tail_fused
 
     # ------------------------------------------------------------------ streams
     def _on_side(self, run, force=False):
@@ -272,6 +304,7 @@ class FusedResNet:
             return run
 
         self._nd, njobs = {}, []
+        self._exps_snap = self._buf("exps_snap", tuple(ctx.exps.shape), torch.int32)
 
         def obs(q, n, table=True):
             """Declare an activation / gradient quantiser's per-step element count and give it a
@@ -512,6 +545,15 @@ class FusedResNet:
         # and loss, one launch (lbt_step_reduce)
         if self.overlap_wgrad or (self.side_wgrad and self.fuse_bwd) or tail_fork:
             bwd.append(self._join_side())
+        # the tail's dequantisations read the step's exponent snapshot (identical values: taken by the
+        # prologue, and no exponent changes before the tail), so the fused update's range-update blocks
+        # may rewrite the live exponents in the same launch
+        snap = self._exps_snap.data_ptr()
+        for j in rjobs:
+            j.qx.exps = j.qg.exps = snap
+        for j in pjobs:
+            j.qrg.exps = j.qr.exps = snap
+        hd.qx.exps = hd.qg.exps = snap
         self._rjobs = _dev_array(rjobs, ctx.device)
         total_blocks = sum((j.K * j.Cout + 255) // 256 for j in rjobs)
         self._pjobs = _dev_array(pjobs, ctx.device)
@@ -527,6 +569,11 @@ class FusedResNet:
             self._tail_fused = [L("lbt_step_reduce", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs),
                                   len(pjobs), max_c, ctypes.byref(hd), k="step_reduce_kernel",
                                   nb=nb_red + scratch.numel() + 8 * d.W.numel())]
+        # ... + SGD-momentum on every parameter (w, a read and written, g written) + update_range
+        nflat = sum(p.numel() for p in self._flat_params())
+        self._tail_upd = [L("lbt_step_reduce_update", ptr(self._rjobs), len(rjobs), total_blocks, ptr(self._pjobs),
+                            len(pjobs), max_c, ctypes.byref(hd), ctypes.byref(self._upd), k="step_reduce_kernel",
+                            nb=nb_red + scratch.numel() + 8 * d.W.numel() + 16 * nflat)]
         # ---- this step's noise tables: one launch ahead of everything else
         self._njobs = _dev_array(njobs, ctx.device)
         max_n = max(j.n for j in njobs)
@@ -537,7 +584,8 @@ class FusedResNet:
         # (together with every weight / gamma / beta quantiser and the input image: one launch)
         fwd.insert(0, L("lbt_step_prologue", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
                         ptr(self._wjobs), len(wjobs), max_cout, ptr(self._qjobs), len(qjobs),
-                        ctypes.byref(self._input_job), k="step_prologue_kernel",
+                        ctypes.byref(self._input_job), ptr(ctx.exps), ptr(self._exps_snap), len(ctx.quantizers),
+                        k="step_prologue_kernel",
                         nb=4 * sum(j.n for j in njobs) + 8 * nz + 6 * X.numel()))
         if w4:  # the packed weight images need the quantised ones
             fwd.insert(1, self._w4_pack)
@@ -559,6 +607,14 @@ class FusedResNet:
     def _qd(self, q):
         """The plan's descriptor of quantiser q: with its noise table when it has one."""
         return self._nd.get(q, q.desc)
+
+    def _qs(self, q):
+        """_qd(q) reading its exponent from the step's snapshot (lbt_step_prologue copies the exponents
+        at the start of the step): for the step's last launch, whose range-update blocks rewrite the
+        live exponents while its reductions dequantise (lbt_step_reduce_update)."""
+        d = _lib.QDesc.from_buffer_copy(self._qd(q))
+        d.exps = self._exps_snap.data_ptr()
+        return d
 
     # ------------------------------------------------------------------ descriptor builders
     def _gn(self, n):

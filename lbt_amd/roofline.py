@@ -182,7 +182,8 @@ def kernel_durations_in_graph(trainer, x, y, replays=30):
 def graph_launches(m):
     """Every kernel launch of a fused plan's step, in order, each callable on its own (side-stream
     wrappers unwrapped, stream joins dropped)."""
-    return [getattr(f, "inner", f) for f in m._fwd + m._hfused + m._bwd + m._tail_fused if hasattr(f, "nbytes")]
+    tail = m.step_tail(True) if hasattr(m, "step_tail") else m._tail_fused
+    return [getattr(f, "inner", f) for f in m._fwd + m._hfused + m._bwd + tail if hasattr(f, "nbytes")]
 
 
 def measure_dominant_graph(trainer, traffic_file=None):

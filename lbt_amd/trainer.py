@@ -103,6 +103,10 @@ class Trainer:
         elif self._lw_exact:
             self._setup_exchange_layerwise()
         self.ctx.sums_managed = True
+        # single process, fused plan: the optimiser + range update run inside the step's last launch
+        # (FusedResNet.set_optimizer / lbt_step_reduce_update) instead of one more launch after it
+        self._fused_update = hasattr(model, "set_optimizer") and not self.dp
+        self._sync_optimizer()
         self.global_step = 0
         self._graphs = None
         self._static = None
@@ -140,6 +144,13 @@ class Trainer:
         self._xchg = x
         self._segs, self._seg_blocks = D.finish_segments(flat, ctx.device)
 
+    def _sync_optimizer(self):
+        """Hand the current lr / momentum and the flat buffers to every fused plan that applies the
+        update itself (read when a step is captured or run eagerly)."""
+        if self._fused_update:
+            for p in [self.model] + list(getattr(self, "_plans", {}).values()):
+                p.set_optimizer(self.flat, self.lr, self.momentum)
+
     # -- the reference's API ---------------------------------------------------------------
     def init_model(self):
         self.flat.a.zero_()
@@ -149,6 +160,7 @@ class Trainer:
         self.flat.a.zero_()
         self._graphs = None  # lr is baked into the captured optimiser kernel
         self._gcache = {}
+        self._sync_optimizer()
         return self.step
 
     # -- the step ----------------------------------------------------------------------------
@@ -165,6 +177,8 @@ class Trainer:
             p = FusedResNet(m.model, sync_bn=m.sync_bn, process_group=m.pg, force_sync_bn=m.sync_bn)
             if self.xbuf is not None:
                 p.set_exchange(self._xchg)
+            if self._fused_update:
+                p.set_optimizer(self.flat, self.lr, self.momentum)
             self._plans[N] = p
             # graphs captured while this was the only plan hold no per-step element-count copy
             # (_fwd_bwd adds one only once several plans exist): re-capture them with it, or they
@@ -173,15 +187,18 @@ class Trainer:
             self._graphs = None
         return p
 
-    def _fwd_bwd(self, X, y):
+    def _fwd_bwd(self, X, y, update=False):
+        """The step's forward + backward; update=True lets a fused plan apply the optimiser and the range
+        update in its last launch. Returns whether it did (then _update must not run)."""
         m = self._active = self._plan(X.shape[0])
+        did = False
         nel = getattr(m, "_nelem", None)
         if nel is not None and self._plans:  # several plans: this one's per-step element counts
             self.ctx.nelem.copy_(nel)
         if not getattr(m, "zeroes_own_sums", False):
             self.ctx.zero_sums()
         if hasattr(m, "train_fwd_bwd"):
-            m.train_fwd_bwd(X, y)
+            did = bool(m.train_fwd_bwd(X, y, update=update and self._fused_update))
         elif self._lw_exact:
             x = self._xchg
             self._loss_n = int(X.shape[0]) * self.world
@@ -202,6 +219,7 @@ class Trainer:
             m._nelem = self.ctx.nelem.clone()  # what its build declared (Quantizer.observe)
         if self.comm is not None:
             self.ctx.fold_counts(self.comm[self.flat.n:])
+        return did
 
     def _exchange(self):
         """Sum the step's gradients + overflow counters across ranks (one RCCL all-reduce;
@@ -226,10 +244,11 @@ class Trainer:
             self.ctx.update_range_op(sgd=(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0))
 
     def _eager(self, X, y):
-        self._fwd_bwd(X, y)
+        did = self._fwd_bwd(X, y, update=not self.dp)
         if self.dp:
             self._exchange()
-        self._update()
+        if not did:
+            self._update()
 
     def _warmup(self, X, y):
         """One un-captured forward + backward that allocates every per-layer buffer before a capture.
@@ -272,11 +291,12 @@ class Trainer:
         mode = "thread_local" if self.capture_comm else "global"
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, capture_error_mode=mode):
-            self._fwd_bwd(X, y)
+            did = self._fwd_bwd(X, y, update=not self.dp)
             if one:
                 if self.dp:
                     self._exchange()
-                self._update()
+                if not did:
+                    self._update()
         g2 = None
         if not one:
             g2 = torch.cuda.CUDAGraph()
@@ -454,3 +474,5 @@ class Trainer:
         self.lr = float(meta["lr"])
         self.momentum = float(meta["momentum"])
         self._graphs = None  # lr is baked into the captured optimiser
+        self._gcache = {}
+        self._sync_optimizer()
