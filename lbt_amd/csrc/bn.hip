@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "bn_moments.h"
 #include "chain_flags.h"
 #include "pk2.h"
 
@@ -42,9 +43,8 @@ LBT_DEV void load4_f32(const float* p, int64_t i, float v[4]) {
   v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
 }
 LBT_DEV void store4_i8(int8_t* p, int64_t i, const int v[4], int off) {
-  char4 c;
-  c.x = (int8_t)(v[0] - off); c.y = (int8_t)(v[1] - off); c.z = (int8_t)(v[2] - off); c.w = (int8_t)(v[3] - off);
-  *reinterpret_cast<char4*>(p + i) = c;
+  st_out(p + i, (int)((uint32_t)((v[0] - off) & 255) | ((uint32_t)((v[1] - off) & 255) << 8) |
+                      ((uint32_t)((v[2] - off) & 255) << 16) | ((uint32_t)(v[3] - off) << 24)));
 }
 LBT_DEV void store4_f32(float* p, int64_t i, const float v[4]) {
   *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
@@ -72,52 +72,6 @@ LBT_DEV Noise4 noise_for(const lbt_qdesc& q, const QState& s, int64_t g) {
   Noise4 n = {{0.f, 0.f, 0.f, 0.f}};
   if (s.active && q.stochastic) n = qnoise4(q, s.step, (uint64_t)g);
   return n;
-}
-
-// Sum a sharded [LBT_NSHARD][stride] int64 buffer's first n entries into LDS tmp[n].
-LBT_DEV void sum_shards(const int64_t* src, int n, int stride, long long* tmp) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    long long v[LBT_NSHARD];  // every shard's load in flight at once
-#pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) v[k] = src[(int64_t)k * stride + i];
-    long long s = 0;
-#pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) s += v[k];
-    tmp[i] = s;
-  }
-}
-
-// Normalization_q moments from the exact integer sums -> mu / sigma in LDS (and ms / running
-// stats from the first workgroup).
-LBT_DEV void bn_moments(const lbt_bn_norm& b, int C, float* mu, float* sg, long long* tmp) {
-  const bool writer = blockIdx.x == 0 && blockIdx.y == 0;
-  if (b.frozen) {  // testing mode: the running averages, no update
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      const float m = b.run_mean[c], sigma = sqrtf(b.run_var[c] + b.eps);
-      mu[c] = m;
-      sg[c] = sigma;
-      if (writer && b.ms) { b.ms[c] = m; b.ms[C + c] = sigma; }
-    }
-    return;
-  }
-  sum_shards(b.chsum, 2 * C, 2 * C, tmp);
-  __syncthreads();
-  const double s = ldexp(1.0, -frac_exp(b.qn));
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const double mean_d = (double)tmp[c] * s / (double)b.n;
-    const double var_d = (double)tmp[C + c] * (s * s) / (double)b.n - mean_d * mean_d;
-    const float m = (float)mean_d, v = (float)var_d;
-    const float sigma = sqrtf(v + b.eps);
-    mu[c] = m;
-    sg[c] = sigma;
-    if (writer) {
-      if (b.ms) { b.ms[c] = m; b.ms[C + c] = sigma; }
-      if (b.run_mean) {
-        b.run_mean[c] = b.momentum * b.run_mean[c] + b.one_minus_momentum * m;
-        b.run_var[c] = b.momentum * b.run_var[c] + b.one_minus_momentum * v;
-      }
-    }
-  }
 }
 
 // ============================================================================ forward chain

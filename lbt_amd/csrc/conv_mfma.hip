@@ -1508,7 +1508,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     }
     if (valid) *reinterpret_cast<int*>(sh.gq + pix * C + cq) = pack4(c);
     if (own) {
-      *reinterpret_cast<int*>(B.gq + img + (uint32_t)((y * W + x) * C + cq)) = pack4(c);
+      st_out(B.gq + img + (uint32_t)((y * W + x) * C + cq), pack4(c));
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         s1[k] += c[k];
@@ -1607,7 +1607,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
         g[h] = mk2(yv.x > 0.f ? g[h].x : 0.f, yv.y > 0.f ? g[h].y : 0.f);
       }
     }
-    if (CF & kAGmask) *reinterpret_cast<float4*>(A.gmask_out + img + off) = make_float4(g[0].x, g[0].y, g[1].x, g[1].y);
+    if (CF & kAGmask) st_out4(A.gmask_out, (uint32_t)(img + off), make_float4(g[0].x, g[0].y, g[1].x, g[1].y));
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
@@ -1638,7 +1638,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
           acc3[b][3][k] += Gc[k] * qn[k];
         }
       }
-      *reinterpret_cast<int*>(Bb.gout + img + off) = pack4(Gc);
+      st_out(Bb.gout + img + off, pack4(Gc));
     }
   }
 
@@ -1709,8 +1709,8 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   const int C = d.Cin;
   if (!desc_ok(d) || d.KH != 3 || d.KW != 3 || d.SH != 1 || d.SW != 1 || d.PT != 1 || d.PB != 1 || d.PL != 1 ||
       d.PR != 1 || d.Ho != d.H || d.Wo != d.W || d.Cout != C || (C != 16 && C != 32 && C != 64) ||
-      d.H % tile_rows(C / 16) || d.W * C != 512)
-    return LBT_EINVAL;
+      d.H % tile_rows(C / 16) || d.W * C != 512 || (int64_t)d.N * d.H * 512 >= ((int64_t)1 << 29))
+    return LBT_EINVAL;  // (st_out4's 32-bit byte offsets)
   const int CS = C / 16;
   const int64_t inner = (int64_t)d.H * d.W * C;
   const lbt_chain_bwd_b& b = q->b;
@@ -1976,7 +1976,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
       ov2a += o2;
       *reinterpret_cast<int*>(sh.g1 + pix * Cq + cqq) = w;
       if (own) {
-        *reinterpret_cast<int*>(p.b1.gq + imgq + (uint32_t)((y * Wq + x) * Cq + cqq)) = w;
+        st_out(p.b1.gq + imgq + (uint32_t)((y * Wq + x) * Cq + cqq), w);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           s1a[k] += c[k];
@@ -1988,7 +1988,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
       ov2b += o2;
       if (valid) *reinterpret_cast<int*>(sh.gs + pix * Cq + cqq) = w;
       if (own) {
-        *reinterpret_cast<int*>(p.bs.gq + imgq + (uint32_t)((y * Wq + x) * Cq + cqq)) = w;
+        st_out(p.bs.gq + imgq + (uint32_t)((y * Wq + x) * Cq + cqq), w);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           s1b[k] += c[k];
@@ -2093,7 +2093,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
         g[h] = mk2(yv.x > 0.f ? g[h].x : 0.f, yv.y > 0.f ? g[h].y : 0.f);
       }
     }
-    if (CF & kAGmask) *reinterpret_cast<float4*>(A.gmask_out + img + off) = make_float4(g[0].x, g[0].y, g[1].x, g[1].y);
+    if (CF & kAGmask) st_out4(A.gmask_out, (uint32_t)(img + off), make_float4(g[0].x, g[0].y, g[1].x, g[1].y));
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
@@ -2124,7 +2124,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
           acc3[b][3][k] += Gc[k] * qn[k];
         }
       }
-      *reinterpret_cast<int*>(Bb.gout + img + off) = pack4(Gc);
+      st_out(Bb.gout + img + off, pack4(Gc));
     }
   }
 
@@ -2202,7 +2202,7 @@ extern "C" int lbt_conv_bwd2_fused_i8(const lbt_conv_bwd2* q, void* stream) {
       d1.PL != 0 || ds.KH != 1 || ds.KW != 1 || ds.SH != 2 || ds.SW != 2 || ds.PT != 0 || ds.PL != 0 ||
       (C != 16 && C != 32) || Cq != 2 * C || d1.W * C != 512 || d1.H % 2 || d1.W % 2 || d1.Ho * 2 != d1.H ||
       d1.Wo * 2 != d1.W || d1.H % tile_rows(C / 16) || ds.N != d1.N || ds.H != d1.H || ds.W != d1.W || ds.Cin != C ||
-      ds.Cout != Cq || ds.Ho != d1.Ho || ds.Wo != d1.Wo)
+      ds.Cout != Cq || ds.Ho != d1.Ho || ds.Wo != d1.Wo || (int64_t)d1.N * d1.H * 512 >= ((int64_t)1 << 29))
     return LBT_EINVAL;
   const int CS = C / 16;
   const int64_t inq = (int64_t)d1.Ho * d1.Wo * Cq;
@@ -2458,7 +2458,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
         const f2 tt = m1 + bet2[b][h];
         v[h] = b ? v[h] + tt : tt;
       }
-      if (own) *reinterpret_cast<int*>(Bb.rout + img + e) = pack4f(fl[0], fl[1]);
+      if (own) st_out(Bb.rout + img + e, pack4f(fl[0], fl[1]));
     }
     if constexpr (RES) {
       v[0] = v[0] + mk2(rv[it].x, rv[it].y);
@@ -2466,7 +2466,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) v[h] = mk2(v[h].x > 0.f ? v[h].x : 0.f, v[h].y > 0.f ? v[h].y : 0.f);
-    if (YST && own) *reinterpret_cast<float4*>(a.y + img + e) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+    if (YST && own) st_out4(a.y, (uint32_t)(img + e), make_float4(v[0].x, v[0].y, v[1].x, v[1].y));
     const f2 uo[2] = {mk2(nov[it].x, nov[it].y), mk2(nov[it].z, nov[it].w)};
     const float X1 = ov_thr(own, so1.L), X2 = ov_thr(own, so1.Lh);
     f2 co[2];
@@ -2481,7 +2481,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     // LBT_OUT_U8OFF: code - 128 (= code ^ 0x80 for codes in [0, 255]); outside the image: the code of 0
     const int cw = in ? (pack4f(co[0], co[1]) ^ (int)0x80808080) : (int)0x80808080;
     if (valid) *reinterpret_cast<int*>(sh.x + pix * C + cq) = cw;
-    if (own) *reinterpret_cast<int*>((int8_t*)a.o1 + img + e) = cw;
+    if (own) st_out((int8_t*)a.o1 + img + e, cw);
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) pin_counts(ovr[b][0], ovr[b][1]);
@@ -2541,7 +2541,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       s1[k] += c[k];
       s2[k] += c[k] * c[k];
     }
-    *reinterpret_cast<int*>(p.yq + img + (uint32_t)(row0 * W * C + pix3 * C + cq)) = pack4(c);
+    st_out(p.yq + img + (uint32_t)(row0 * W * C + pix3 * C + cq), pack4(c));
   }
   {
     const int t1 = chan_scatter4(s1, C4), t2 = chan_scatter4(s2, C4);  // row lane >> 4: channel cq + row
@@ -2746,12 +2746,12 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
       const f2 m1 = xr * gam2[h];
       v[h] = m1 + bet2[h];
     }
-    if (own) *reinterpret_cast<int*>(a.b1.rout + img + e) = pack4f(fl[0], fl[1]);
+    if (own) st_out(a.b1.rout + img + e, pack4f(fl[0], fl[1]));
     v[0] = v[0] + mk2(rv[it].x, rv[it].y);
     v[1] = v[1] + mk2(rv[it].z, rv[it].w);
 #pragma unroll
     for (int h = 0; h < 2; ++h) v[h] = mk2(v[h].x > 0.f ? v[h].x : 0.f, v[h].y > 0.f ? v[h].y : 0.f);
-    if (own) *reinterpret_cast<float4*>(a.y + img + e) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+    if (own) st_out4(a.y, (uint32_t)(img + e), make_float4(v[0].x, v[0].y, v[1].x, v[1].y));
     const f2 u1[2] = {mk2(no1[it].x, no1[it].y), mk2(no1[it].z, no1[it].w)};
     const f2 u2[2] = {mk2(no2[it].x, no2[it].y), mk2(no2[it].z, no2[it].w)};
     const float X1 = ov_thr(own, so1.L), X2 = ov_thr(own, so1.Lh);
@@ -2775,8 +2775,8 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
     if (valid) *reinterpret_cast<int*>(sh.xa + pix * C + cq) = cw1;
     if (own && !(hy & 1) && !(x & 1)) *reinterpret_cast<int*>(sh.xs + ((hy >> 1) * Wq + (x >> 1)) * C + cq) = cw2;
     if (own) {
-      *reinterpret_cast<int*>((int8_t*)a.o1 + img + e) = cw1;
-      *reinterpret_cast<int*>((int8_t*)a.o2 + img + e) = cw2;
+      st_out((int8_t*)a.o1 + img + e, cw1);
+      st_out((int8_t*)a.o2 + img + e, cw2);
     }
   }
   pin_counts(ovr1, ovr2);
@@ -2846,7 +2846,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
         s1[b][k] += c[k];
         s2[b][k] += c[k] * c[k];
       }
-      *reinterpret_cast<int*>((b ? p.yqs : p.yq1) + imgq + off3) = pack4(c);
+      st_out((b ? p.yqs : p.yq1) + imgq + off3, pack4(c));
     }
   }
   {
@@ -2890,8 +2890,8 @@ extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
   const int C = d.Cin;
   if (!desc_ok(d) || d.KH != 3 || d.KW != 3 || d.SH != 1 || d.SW != 1 || d.PT != 1 || d.PB != 1 || d.PL != 1 ||
       d.PR != 1 || d.Ho != d.H || d.Wo != d.W || d.Cout != C || (C != 16 && C != 32 && C != 64) ||
-      d.H % tile_rows(C / 16) || d.W * C != 512)
-    return LBT_EINVAL;
+      d.H % tile_rows(C / 16) || d.W * C != 512 || (int64_t)d.N * d.H * 512 >= ((int64_t)1 << 29))
+    return LBT_EINVAL;  // (st_out4's 32-bit byte offsets)
   const int CS = C / 16;
   const lbt_chain_fwd& a = q->c;
   const int64_t inner = (int64_t)d.H * d.W * C;
@@ -2947,7 +2947,7 @@ extern "C" int lbt_conv_fwd2_fused_i8(const lbt_conv_fwd2* q, void* stream) {
       d1.PL != 0 || ds.KH != 1 || ds.KW != 1 || ds.SH != 2 || ds.SW != 2 || ds.PT != 0 || ds.PL != 0 ||
       (C != 16 && C != 32) || Cq != 2 * C || d1.W * C != 512 || d1.H % 2 || d1.W % 2 || d1.Ho * 2 != d1.H ||
       d1.Wo * 2 != d1.W || d1.Ho % kTH2 || ds.N != d1.N || ds.H != d1.H || ds.W != d1.W || ds.Cin != C ||
-      ds.Cout != Cq || ds.Ho != d1.Ho || ds.Wo != d1.Wo)
+      ds.Cout != Cq || ds.Ho != d1.Ho || ds.Wo != d1.Wo || (int64_t)d1.N * d1.H * 512 >= ((int64_t)1 << 29))
     return LBT_EINVAL;
   const int CS = C / 16;
   const lbt_chain_fwd& a = q->c;

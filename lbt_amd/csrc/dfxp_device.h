@@ -58,6 +58,33 @@ static __device__ unsigned long long* lbt_trace_buf;
 
 namespace lbt {
 
+// Outputs that a LATER launch reads (codes, block outputs, masked gradients of the fused conv
+// kernels): written through to memory (`global_store ... sc1`) instead of staying dirty in this
+// XCD's L2 until the end-of-launch write-back, which the next dependent launch waits for (MI355X_
+// MICROARCH "boundary": + B / 6 TB/s for B dirty bytes; tools/wt_probe.hip: a 4 / 12 MB writer + its
+// reader 4.36 -> 4.09 / 6.38 -> 6.16 us with 16-B stores, 6.07 -> 5.27 us with 4-B stores). Seven in
+// eight readers sit on another XCD, whose L2 never held the line. 4- and 8-byte: a relaxed agent-
+// scope atomic store (the compiler's own sc1 store); 16-byte: a raw buffer store with the sc1 bit.
+// -DLBT_PLAIN_OUT (scratch A/B builds): plain stores.
+#ifdef LBT_PLAIN_OUT
+LBT_DEV void st_out(int* p, int v) { *p = v; }
+#else
+LBT_DEV void st_out(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+#endif
+// 16-byte: base[i .. i+3] (i < 2^29, base uniform) by buffer_store_dwordx4 ... sc1 (a compiler-
+// scheduled store: inline asm stores escaped its store-data hazard checks and corrupted results)
+#if defined(LBT_PLAIN_OUT) || defined(LBT_PLAIN_OUT4)
+LBT_DEV void st_out4(float* base, uint32_t i, float4 v) { *reinterpret_cast<float4*>(base + i) = v; }
+#else
+LBT_DEV void st_out4(float* base, uint32_t i, float4 v) {
+  typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  const v4u_ x = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)(i * 4u), 0, 16 /* sc1 */);
+}
+#endif
+LBT_DEV void st_out(int8_t* p, int v) { st_out(reinterpret_cast<int*>(p), v); }
+
 constexpr int kEMax = 30;  // reference computes 2**e in int32: defined for 0 <= e <= 30
 
 // ------------------------------------------------------------------ Philox4x32-10

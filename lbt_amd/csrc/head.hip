@@ -118,8 +118,8 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0,
       acc[2][k] += G[k];
       acc[3][k] += G[k] * qn;
     }
-    *reinterpret_cast<int*>(B.gout + e) =
-        (int)((uint32_t)(G[0] & 255) | ((uint32_t)(G[1] & 255) << 8) | ((uint32_t)(G[2] & 255) << 16) | ((uint32_t)G[3] << 24));
+    st_out(B.gout + e,
+           (int)((uint32_t)(G[0] & 255) | ((uint32_t)(G[1] & 255) << 8) | ((uint32_t)(G[2] & 255) << 16) | ((uint32_t)G[3] << 24)));
   };
   const Noise4 z4 = {{0.f, 0.f, 0.f, 0.f}};
   if (use_pre) {  // uniform
