@@ -604,6 +604,13 @@ typedef struct lbt_head {
    * y_mask, gmask_out, stochastic quantisers; a.g unused) run per sample on the un-pooled gradient
    * inside this launch -- then gx is not written. Bit-identical to lbt_bn_chain_bwd_a(a) on gx. */
   const lbt_chain_bwd_a* pa;
+  /* optional (with pa): the last block's END CHAIN (lbt_bn_chain_fwd of a one-branch chain with int8
+   * Normalization_q codes in, stochastic Rescale_q with its noise table, residual add and ReLU, no
+   * output quantisers; C == this C, HW * C == 4096) evaluated per sample inside this launch: the
+   * block output the head pools and pass A's ReLU mask / R codes come from registers, so x is not
+   * read and the chain's y / R / ybits are not written (its ms and running statistics are, by
+   * workgroup 0). Bit-identical to lbt_bn_chain_fwd(chain) followed by this head on x = chain.y.    */
+  const lbt_chain_fwd* chain;
 } lbt_head;
 int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K);  /* = N * (C + 72) */
 int lbt_head_fwd_bwd(const lbt_head* h, void* stream);

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -145,7 +145,7 @@ class Head(ctypes.Structure):
                 ("gq", c_void_p), ("qg", QDesc),
                 ("w", c_void_p), ("wd2", c_float), ("dw", c_void_p),
                 ("gx", c_void_p),
-                ("scratch", c_void_p), ("loss_n", c_int32), ("pa", c_void_p)]
+                ("scratch", c_void_p), ("loss_n", c_int32), ("pa", c_void_p), ("chain", c_void_p)]
 
 
 class Xchg(ctypes.Structure):

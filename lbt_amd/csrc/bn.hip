@@ -43,8 +43,9 @@ LBT_DEV void load4_f32(const float* p, int64_t i, float v[4]) {
   v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
 }
 LBT_DEV void store4_i8(int8_t* p, int64_t i, const int v[4], int off) {
-  st_out(p + i, (int)((uint32_t)((v[0] - off) & 255) | ((uint32_t)((v[1] - off) & 255) << 8) |
-                      ((uint32_t)((v[2] - off) & 255) << 16) | ((uint32_t)(v[3] - off) << 24)));
+  char4 c;
+  c.x = (int8_t)(v[0] - off); c.y = (int8_t)(v[1] - off); c.z = (int8_t)(v[2] - off); c.w = (int8_t)(v[3] - off);
+  *reinterpret_cast<char4*>(p + i) = c;
 }
 LBT_DEV void store4_f32(float* p, int64_t i, const float v[4]) {
   *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);

@@ -58,12 +58,15 @@ static __device__ unsigned long long* lbt_trace_buf;
 
 namespace lbt {
 
-// Outputs that a LATER launch reads (codes, block outputs, masked gradients of the fused conv
-// kernels): written through to memory (`global_store ... sc1`) instead of staying dirty in this
+// Outputs that a LATER launch reads in the latency-bound ResNet-20 step (codes, block outputs,
+// masked gradients of the fused conv kernels, the head, the step's prologue and tail): written
+// through to memory (`global_store ... sc1`) instead of staying dirty in this
 // XCD's L2 until the end-of-launch write-back, which the next dependent launch waits for (MI355X_
 // MICROARCH "boundary": + B / 6 TB/s for B dirty bytes; tools/wt_probe.hip: a 4 / 12 MB writer + its
 // reader 4.36 -> 4.09 / 6.38 -> 6.16 us with 16-B stores, 6.07 -> 5.27 us with 4-B stores). Seven in
-// eight readers sit on another XCD, whose L2 never held the line. 4- and 8-byte: a relaxed agent-
+// eight readers sit on another XCD, whose L2 never held the line. NOT for the streaming wide-layer
+// kernels (ResNet-50: tens to hundreds of MB per launch): there the same stores cost 42.2 -> 47.9 ms
+// per step (bn.hip, bn_wide.hip, igemm.hip, quantize.hip keep plain stores). 4- and 8-byte: a relaxed agent-
 // scope atomic store (the compiler's own sc1 store); 16-byte: a raw buffer store with the sc1 bit.
 // -DLBT_PLAIN_OUT (scratch A/B builds): plain stores.
 #ifdef LBT_PLAIN_OUT
@@ -84,6 +87,19 @@ LBT_DEV void st_out4(float* base, uint32_t i, float4 v) {
 }
 #endif
 LBT_DEV void st_out(int8_t* p, int v) { st_out(reinterpret_cast<int*>(p), v); }
+LBT_DEV void st_out(float* p, float v) { st_out(reinterpret_cast<int*>(p), __float_as_int(v)); }
+#ifdef LBT_PLAIN_OUT
+LBT_DEV void st_out8(void* p, long long v) { *reinterpret_cast<long long*>(p) = v; }
+#else
+LBT_DEV void st_out8(void* p, long long v) {
+  __hip_atomic_store(reinterpret_cast<long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
+// 16 bytes at any 64-bit address (two 8-byte write-through stores)
+LBT_DEV void st_out16(float* p, float4 v) {
+  st_out8(p, (long long)(((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x)));
+  st_out8(p + 2, (long long)(((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z)));
+}
 
 constexpr int kEMax = 30;  // reference computes 2**e in int32: defined for 0 <= e <= 30
 

@@ -15,7 +15,9 @@
 //
 // Reference: AvgPool_q dynamic_fixed_point.py:1009-1022, Dense_q :319-395 / :441-466,
 // loss models.py:30-32.
+#include "bn_moments.h"
 #include "head.h"
+#include "pk2.h"
 
 namespace lbt {
 namespace {
@@ -54,7 +56,8 @@ struct HeadPaPre {
   int R[kPaPre], qn[kPaPre];
 };
 LBT_DEV bool head_pa_prefetchable(int HW, int C) { return HW * C / 4 <= kPaPre * kT; }
-LBT_DEV void head_pa_prefetch(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0, int q1, HeadPaPre& p) {
+LBT_DEV void head_pa_prefetch(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0, int q1, HeadPaPre& p,
+                              bool operands = true) {
   const lbt_bwd_branch& B = a.b1;
   const int t = threadIdx.x;
   const int64_t base = (int64_t)n * HW * C;
@@ -65,9 +68,11 @@ LBT_DEV void head_pa_prefetch(const lbt_chain_bwd_a& a, int n, int HW, int C, in
   for (int it = 0; it < kPaPre; ++it) {
     const int q = q0 + t + it * kT, qq = q < q1 ? q : q0;
     const int64_t e = base + 4 * (int64_t)qq;
-    p.ym[it] = *reinterpret_cast<const float4*>(a.y_mask + e);
-    p.R[it] = *reinterpret_cast<const int*>(B.R + e);
-    p.qn[it] = *reinterpret_cast<const int*>(B.qn_codes + e);
+    if (operands) {  // else the caller's end chain supplies them (lbt_head.chain)
+      p.ym[it] = *reinterpret_cast<const float4*>(a.y_mask + e);
+      p.R[it] = *reinterpret_cast<const int*>(B.R + e);
+      p.qn[it] = *reinterpret_cast<const int*>(B.qn_codes + e);
+    }
     p.nr[it] = *reinterpret_cast<const float4*>(tr + ((4u * (uint32_t)qq) & mr));
     p.nn[it] = *reinterpret_cast<const float4*>(tn + ((4u * (uint32_t)qq) & mn));
   }
@@ -104,7 +109,7 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0,
       const float g = s_dp[c0 + k] * inv;
       gv[k] = ym[k] > 0.f ? g : 0.f;
     }
-    if (a.gmask_out) *reinterpret_cast<float4*>(a.gmask_out + e) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+    if (a.gmask_out) st_out16(a.gmask_out + e, make_float4(gv[0], gv[1], gv[2], gv[3]));
     int G[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -163,11 +168,11 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0,
         if (lane < per) s_sum[wave][s * C + c0 + k] = v;
       }
   }
-  counts_stage_w(2, 4, ov[0][0], ov[0][1], sh_cnt);
-  counts_stage_w(3, 4, ov[1][0], ov[1][1], sh_cnt);
+  counts_stage_w(2, 5, ov[0][0], ov[0][1], sh_cnt);
+  counts_stage_w(3, 5, ov[1][0], ov[1][1], sh_cnt);
   __syncthreads();
-  if (qrg.active) counts_publish(2, 4, B.qrg, sh_cnt);
-  if (qng.active) counts_publish(3, 4, B.qng, sh_cnt);
+  if (qrg.active) counts_publish(2, 5, B.qrg, sh_cnt);
+  if (qng.active) counts_publish(3, 5, B.qng, sh_cnt);
   if (B.sums) {
     int64_t* dst = B.sums + (int64_t)shard_id() * 4 * C;
     for (int i = t; i < 4 * C; i += kT) {
@@ -179,16 +184,99 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0,
   }
 }
 
+// ---- the last block's end chain inside the head (lbt_head.chain): bn.hip chain_fwd_kernel<1, kFQ |
+// kFRes | kFRelu | kFStoch>'s arithmetic, element for element, over the whole sample (kChainSlots
+// channel quads per thread; the pooling needs every pixel). Slot j < own covers this workgroup's pass-A
+// quads q0 + t + j * kT (the only ones whose Rescale_q overflows it counts), the rest the sample's other
+// quads in order, so pass A finds its y mask / R / qn codes in slots 0 .. own - 1.
+constexpr int kChainSlots = 4;  // HW * C == 4 * kT * 4 (host check)
+struct ChainIn {
+  int q[kChainSlots];
+  float4 r[kChainSlots], u[kChainSlots];
+};
+struct ChainOut {
+  float4 y[kChainSlots];
+  int R[kChainSlots];
+};
+LBT_DEV int chain_quad(int j, int own, int q0, int Q, int t) {
+  return j < own ? q0 + t + j * kT : (q0 + Q / kChainSlots * own + t + (j - own) * kT) % Q;
+}
+LBT_DEV void chain_load(const lbt_chain_fwd& a, int n, int q0, int own, ChainIn& in) {
+  const lbt_chain_branch& B = a.b1;
+  const int t = threadIdx.x, Q = (int)(a.inner >> 2);
+  const int64_t base = (int64_t)n * a.inner;
+#pragma unroll
+  for (int j = 0; j < kChainSlots; ++j) {
+    const int qd = chain_quad(j, own, q0, Q, t);
+    in.q[j] = *reinterpret_cast<const int*>(B.nrm.q + base + 4 * (int64_t)qd);
+    in.r[j] = *reinterpret_cast<const float4*>(a.res + base + 4 * (int64_t)qd);
+    in.u[j] = *reinterpret_cast<const float4*>(B.qr.noise + 4 * qd);
+  }
+}
+// mu / sigma / gamma_q / beta_q per channel into P[4C] (LDS), then the chain; own slots count qr's
+// overflows into ov1 / ov2 (wave totals, quant_w2)
+LBT_DEV void chain_eval(const lbt_chain_fwd& a, int own, const ChainIn& in, float* P, long long* tmp, ChainOut& out,
+                        int& ov1, int& ov2) {
+  const lbt_chain_branch& B = a.b1;
+  const int C = a.C, t = threadIdx.x;
+  bn_moments(B.nrm, C, P, P + C, tmp);
+  for (int c = t; c < C; c += kT) { P[2 * C + c] = B.gb[c]; P[3 * C + c] = B.gb[C + c]; }
+  __syncthreads();
+  const int c0 = (4 * t) % C;
+  const QState qr = qstate(B.qr);
+  const float sn = qscale(B.nrm.qn);
+  pf2 pm[2], psy[2], psr[2], pg[2], pb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const Recip r0 = recip(P[C + c0 + 2 * h]), r1 = recip(P[C + c0 + 2 * h + 1]);
+    pm[h] = pk(P[c0 + 2 * h], P[c0 + 2 * h + 1]);
+    psy[h] = pk(r0.y, r1.y);
+    psr[h] = pk(r0.rc, r1.rc);
+    pg[h] = pk(P[2 * C + c0 + 2 * h], P[2 * C + c0 + 2 * h + 1]);
+    pb[h] = pk(P[3 * C + c0 + 2 * h], P[3 * C + c0 + 2 * h + 1]);
+  }
+#pragma unroll
+  for (int j = 0; j < kChainSlots; ++j) {
+    int z1 = 0, z2 = 0;  // the other workgroups' quads: their owner counts them
+    const int q[4] = {(int)(int8_t)(in.q[j] & 255), (int)(int8_t)((in.q[j] >> 8) & 255),
+                      (int)(int8_t)((in.q[j] >> 16) & 255), (int)(int8_t)(in.q[j] >> 24)};
+    const float uu[4] = {in.u[j].x, in.u[j].y, in.u[j].z, in.u[j].w};
+    const float rr[4] = {in.r[j].x, in.r[j].y, in.r[j].z, in.r[j].w};
+    int R[4];
+    float v[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const pf2 x1 = pcvt(q[2 * h], q[2 * h + 1]) * pk(sn, sn);
+      const pf2 x2 = x1 - pm[h];
+      const pf2 tt = pdiv(x2, psy[h], psr[h]);  // == x2 / sigma
+      if (j < own) quant_w2<1>(qr, 1, tt, pk(uu[2 * h], uu[2 * h + 1]), ov1, ov2, R[2 * h], R[2 * h + 1]);
+      else quant_w2<1>(qr, 1, tt, pk(uu[2 * h], uu[2 * h + 1]), z1, z2, R[2 * h], R[2 * h + 1]);
+      const pf2 xr = pcvt(R[2 * h], R[2 * h + 1]) * pk(qr.inv_m, qr.inv_m);
+      const pf2 m1 = xr * pg[h];
+      const pf2 t2 = m1 + pb[h];
+      const pf2 y2 = t2 + pk(rr[2 * h], rr[2 * h + 1]);
+      v[2 * h] = y2.x;
+      v[2 * h + 1] = y2.y;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+    out.y[j] = make_float4(v[0], v[1], v[2], v[3]);
+    out.R[j] = (int)((uint32_t)(R[0] & 255) | ((uint32_t)(R[1] & 255) << 8) | ((uint32_t)(R[2] & 255) << 16) |
+                     ((uint32_t)R[3] << 24));
+  }
+}
+
 // S workgroups per sample (grid N * S): each one pools, quantises, takes the logits, softmax and
 // dgrad of its sample (the same operations on the same operands: identical values, a few KB from
 // L2), and runs pass A / the un-pool over its 1/S of the sample's pixels; workgroup s == 0 alone
 // writes the sample's outputs and counts its Dense_q quantisers.
-__global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa, int S) {
+template <bool CHAIN>
+__global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa, lbt_chain_fwd ch, int S) {
   __shared__ __attribute__((aligned(16))) float s_x[kXChunk / 4];
   __shared__ __attribute__((aligned(16))) int8_t s_w[kMaxW];
   __shared__ int s_pq[256], s_gq[64], s_part[16][16];
   __shared__ float s_z[64], s_dp[256];
-  __shared__ int sh_cnt[4 * 2 * (kT / 64)];  // counters: qx, qg (+ pass A's qrg, qng)
+  __shared__ int sh_cnt[5 * 2 * (kT / 64)];  // counters: qx, qg (+ pass A's qrg, qng) (+ the chain's qr)
   const int n = (int)blockIdx.x / S, split = (int)blockIdx.x - n * S, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const bool lead = split == 0;
   const int C = h.C, K = h.K, HW = h.HW, N = h.N;
@@ -221,18 +309,43 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
       v[j] = src_[i_ < nq_ ? i_ : 0];                                                            \
     }                                                                                            \
   } while (0)
-  LBT_HEAD_LOAD_CHUNK(0);
+  // chain mode: the end chain's operands instead of the block output (the whole sample in one chunk)
+  ChainIn cin;
+  const int own = kChainSlots / S;
+  if constexpr (CHAIN) chain_load(ch, n, q0, own, cin);
+  else LBT_HEAD_LOAD_CHUNK(0);
   // the fused pass A's operands, in flight from here
   HeadPaPre pre;
   const bool pre_ok = h.pa && head_pa_prefetchable(HW / S, C);  // uniform
-  if (pre_ok) head_pa_prefetch(pa, n, HW, C, q0, q1, pre);
+  if (pre_ok) head_pa_prefetch(pa, n, HW, C, q0, q1, pre, !CHAIN);
+  int ovr1 = 0, ovr2 = 0;
+  if constexpr (CHAIN) {
+    // the chain's block output into s_x (pooling) and, for this workgroup's quads, pass A's operands
+    // (y mask, R codes, and the qn codes: the chain's input)
+    __shared__ float s_P[4 * 256];
+    __shared__ long long s_t[2 * 256];
+    ChainOut co;
+    chain_eval(ch, own, cin, s_P, s_t, co, ovr1, ovr2);
+    const int Q = HW * C / 4;
+#pragma unroll
+    for (int j = 0; j < kChainSlots; ++j) reinterpret_cast<float4*>(s_x)[chain_quad(j, own, q0, Q, t)] = co.y[j];
+#pragma unroll
+    for (int j = 0; j < kPaPre; ++j)
+      if (j < own) {
+        pre.ym[j] = co.y[j];
+        pre.R[j] = co.R[j];
+        pre.qn[j] = cin.q[j];
+      }
+  }
 
   // ---- AvgPool_q: channel t, the HW pixels summed in order (avgpool_fwd_kernel), from LDS
   float acc = 0.f;
   for (int p0 = 0;;) {
     // unconditional: slots past the chunk receive a harmless copy (loads stay un-predicated)
+    if constexpr (!CHAIN) {
 #pragma unroll
-    for (int j = 0; j < kV; ++j) reinterpret_cast<float4*>(s_x)[t + j * kT] = v[j];
+      for (int j = 0; j < kV; ++j) reinterpret_cast<float4*>(s_x)[t + j * kT] = v[j];
+    }
     if (p0 == 0) {
 #pragma unroll
       for (int j = 0; j < kMaxW / 4 / kT; ++j) reinterpret_cast<uint32_t*>(s_w)[t + j * kT] = wv[j];
@@ -253,7 +366,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     p0 += P;
     if (p0 >= HW) break;
     __syncthreads();
-    LBT_HEAD_LOAD_CHUNK(p0);
+    if constexpr (!CHAIN) LBT_HEAD_LOAD_CHUNK(p0);
   }
 #undef LBT_HEAD_LOAD_CHUNK
   LBT_TS(1);
@@ -321,13 +434,15 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
       *reinterpret_cast<double*>(rec + C + 64) = term;  // 8-byte aligned: C % 8 == 0
     }
   }
-  counts_stage_w(0, 4, ovx1, ovx2, sh_cnt);
-  counts_stage_w(1, 4, ovg1, ovg2, sh_cnt);
+  counts_stage_w(0, 5, ovx1, ovx2, sh_cnt);
+  counts_stage_w(1, 5, ovg1, ovg2, sh_cnt);
+  if constexpr (CHAIN) counts_stage_w(4, 5, ovr1, ovr2, sh_cnt);
   __syncthreads();
   if (lead) {
-    counts_publish(0, 4, h.qx, sh_cnt);
-    counts_publish(1, 4, h.qg, sh_cnt);
+    counts_publish(0, 5, h.qx, sh_cnt);
+    counts_publish(1, 5, h.qg, sh_cnt);
   }
+  if constexpr (CHAIN) counts_publish(4, 5, ch.b1.qr, sh_cnt);
 
   LBT_TS(3);
   // ---- the record's codes: pq[C] | gq[64]
@@ -390,7 +505,19 @@ extern "C" int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K) {
 
 extern "C" int lbt_head_fwd_bwd(const lbt_head* h, void* stream) {
   if (!h || h->N <= 0 || h->HW <= 0 || h->C <= 0 || h->C > 256 || h->C % 8 || h->K <= 0 || h->K > 64) return LBT_EINVAL;
-  if (!h->x || !h->wq || !h->labels || !h->logits || !h->dz || (!h->gx && !h->pa) || !h->scratch) return LBT_EINVAL;
+  if ((!h->x && !h->chain) || !h->wq || !h->labels || !h->logits || !h->dz || (!h->gx && !h->pa) || !h->scratch)
+    return LBT_EINVAL;
+  lbt_chain_fwd ch{};
+  if (h->chain) {  // the end chain's configuration (see the header); it rides on the fused pass A
+    ch = *h->chain;
+    const lbt_chain_branch& B = ch.b1;
+    if (!h->pa || ch.has_b2 || ch.C != h->C || ch.rows != h->N || ch.inner != (int64_t)h->HW * h->C ||
+        ch.inner != 4 * kT * kChainSlots || !B.nrm.q || B.nrm.frozen || !B.nrm.chsum || !B.gb || B.qr.bits <= 0 ||
+        !B.qr.stochastic || !B.qr.noise || !ch.res || !ch.relu || (ch.o1 && ch.qo1.bits > 0) ||
+        (ch.o2 && ch.qo2.bits > 0) || (reinterpret_cast<uintptr_t>(ch.res) & 15) ||
+        (reinterpret_cast<uintptr_t>(B.qr.noise) & 15))
+      return LBT_EINVAL;
+  }
   if (h->pa) {  // the fused pass A: one branch, y mask, stochastic quantisers, C | 1024, C <= 256
     const lbt_chain_bwd_a& a = *h->pa;
     if (a.has_b2 || !a.y_mask || a.C != h->C || a.rows != h->N || a.inner != (int64_t)h->HW * h->C ||
@@ -411,7 +538,10 @@ extern "C" int lbt_head_fwd_bwd(const lbt_head* h, void* stream) {
     return v < 1 ? 1 : v;
   }();
   int S = smax;
-  while (S > 1 && (h->HW % S || (int64_t)h->N * S > 0x7fffffff)) --S;
-  hipLaunchKernelGGL(head_kernel, dim3((unsigned)(h->N * S)), dim3(kT), 0, (hipStream_t)stream, *h, pa, S);
+  while (S > 1 && (h->HW % S || (int64_t)h->N * S > 0x7fffffff || (h->chain && kChainSlots % S))) --S;
+  if (h->chain)
+    hipLaunchKernelGGL(head_kernel<true>, dim3((unsigned)(h->N * S)), dim3(kT), 0, (hipStream_t)stream, *h, pa, ch, S);
+  else
+    hipLaunchKernelGGL(head_kernel<false>, dim3((unsigned)(h->N * S)), dim3(kT), 0, (hipStream_t)stream, *h, pa, ch, S);
   return (int)hipGetLastError();
 }

@@ -47,11 +47,12 @@ __global__ __launch_bounds__(kThreads) void quantize_rows_kernel(
       c[3] = quant1(s, q.stochastic, v.w, n.u[3], ov1, ov2);
       if (out_kind == LBT_OUT_I8 || out_kind == LBT_OUT_U8OFF) {
         const int off = out_kind == LBT_OUT_U8OFF ? 128 : 0;
-        uint32_t o = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          o |= (uint32_t)(((out_kind == LBT_OUT_U8OFF && c[k] < 0 ? 0 : c[k]) - off) & 255) << (8 * k);
-        st_out((int8_t*)out + base, (int)o);
+        char4 o;
+        o.x = (int8_t)((out_kind == LBT_OUT_U8OFF && c[0] < 0 ? 0 : c[0]) - off);
+        o.y = (int8_t)((out_kind == LBT_OUT_U8OFF && c[1] < 0 ? 0 : c[1]) - off);
+        o.z = (int8_t)((out_kind == LBT_OUT_U8OFF && c[2] < 0 ? 0 : c[2]) - off);
+        o.w = (int8_t)((out_kind == LBT_OUT_U8OFF && c[3] < 0 ? 0 : c[3]) - off);
+        *reinterpret_cast<char4*>((int8_t*)out + base) = o;
       } else if (out_kind == LBT_OUT_I16) {
         short4 o;
         o.x = (short)c[0]; o.y = (short)c[1]; o.z = (short)c[2]; o.w = (short)c[3];
@@ -306,4 +307,4 @@ extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, 
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_abi_version(void) { return 17; }
+extern "C" int lbt_abi_version(void) { return 18; }

@@ -110,6 +110,9 @@ class FusedResNet:
         self.pair_launch = os.environ.get("LBT_PAIR", "1") == "1"
         # the last block's output BN pass A inside the fused head launch (lbt_head.pa)
         self.head_pass_a = os.environ.get("LBT_HEAD_PASS_A", "1") == "1"
+        # ... and that block's end chain (BN + Rescale_q + residual + ReLU) too (lbt_head.chain): the head
+        # pools the block output from registers, one launch fewer per training step
+        self.head_chain = os.environ.get("LBT_HEAD_CHAIN", "1") == "1"
         self._side = None
         # every conv's weight gradient of the step in ONE launch at the end of the backward
         # (lbt_conv_wgrad_many_i8) instead of inside the dgrad launches: a dgrad launch's tiles fill
@@ -411,13 +414,21 @@ class FusedResNet:
             Xin, xa, xs, info = self._block_fwd(i, b, nxt, Xin, xa, xs, fwd, L, obs)
             saved.append(info)
         Ylast = Xin
-        self._flush_chain(fwd, L)
+        # the last block's end chain: launched here, or (the training step's fused head) evaluated inside
+        # the head launch; the separate head launches (forward / compute_loss / backward) run it first
+        last = self._chain_pending
+        self._chain_pending = None
+        last_launch = None
+        if last is not None:
+            last_launch = L("lbt_bn_chain_fwd", ctypes.byref(last), k="chain_fwd_kernel", nb=ops._chain_fwd_bytes(last))
 
         # ---- head: avg pool, dense, loss -- as separate launches (forward / compute_loss /
         # backward called one by one) and as ONE fused launch (train_fwd_bwd, the training step)
         Nb, Hh, Wh, Ch = Ylast.shape
         pooled = self._buf("pool", (Nb, Ch), torch.float32)
         hfwd, hloss, hbwd = [], [], []
+        if last_launch is not None:
+            hfwd.append(last_launch)
         hfwd.append(L("lbt_avgpool_fwd", ptr(Ylast), ptr(pooled), Nb, Hh * Wh, Ch))
         dd = _lib.ConvDesc(Nb, 1, 1, d.in_units, d.units, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
         d.d = dd
@@ -474,6 +485,17 @@ class FusedResNet:
             # head bytes: x in, weights, and pass A's operands / outputs instead of the fp32 gx
             hfused[0].nbytes = 4 * Ylast.numel() + d.w_hwio.numel() + ops._chain_bwd_a_bytes(aL) - 4 * Ylast.numel()
             gY = None
+        qr_last = last.b1.qr if last is not None else None
+        head_chain = (self.head_chain and head_a and last is not None and not last.has_b2 and bool(last.b1.nrm.q)
+                      and bool(last.res) and bool(last.relu) and not last.o1 and not last.o2 and last.C == Ch
+                      and Hh * Wh * Ch == 4096 and qr_last.bits > 0 and qr_last.stochastic and bool(qr_last.noise))
+        if head_chain:
+            hd.chain = ctypes.addressof(last)
+            # per element the chain's operands (q codes 1 B, residual 4 B) replace the block output (4 B) and
+            # pass A's y mask / R / qn reads (6 B), which come from registers; y and R are not written
+            hfused[0].nbytes += (5 - 4 - 6) * Ylast.numel()
+        elif last_launch is not None:
+            fwd.append(last_launch)
         gq0 = self._buf("gq0", shp0, torch.int8)
         Gn0 = self._buf("Gn0", shp0, torch.int8)
         sums0 = self._sums("sums0", ops.NSHARD * 4 * C0)
