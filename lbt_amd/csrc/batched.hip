@@ -73,9 +73,9 @@ __global__ __launch_bounds__(kThreads) void quantize_many_kernel(const lbt_qjob*
 LBT_DEV void sgd_update(float wv, float am, float gv, const lbt_update& u, int64_t o) {
   const float t = u.mu * am;
   const float an = t + gv;
-  st_out(u.a + o, an);
+  LBT_ST_TAIL(u.a + o, an);
   const float step = u.lr * an;
-  st_out(u.w + o, wv - step);
+  LBT_ST_TAIL(u.w + o, wv - step);
 }
 
 // Blocks are allotted to the jobs in order, ceil(K*Cout/256) each (1-D grid); a block reduces 256
@@ -167,7 +167,7 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
     const float a = (float)s * scale;
     const float b = j.wd2 * wv;
     const float gv = a + b;
-    st_out(j.dw + i, gv);
+    LBT_ST_TAIL(j.dw + i, gv);
     sgd_update(wv, am, gv, u, o);
     return;
   }
@@ -212,8 +212,8 @@ LBT_DEV void pjob_channel(const lbt_pjob& j, int c, const lbt_xchg& x, const lbt
   if (u.w) {
     const float b = j.wd2 * wg;  // j.gamma[c] == u.w[og]
     const float dg = a + b, db = (float)((double)sg * g2);
-    st_out(j.dgamma + c, dg);
-    st_out(j.dbeta + c, db);
+    LBT_ST_TAIL(j.dgamma + c, dg);
+    LBT_ST_TAIL(j.dbeta + c, db);
     sgd_update(wg, ag, dg, u, og);
     sgd_update(wb, ab, db, u, ob);
     return;
@@ -309,10 +309,15 @@ LBT_DEV void noise_fill_block(const lbt_njob* __restrict__ jobs, int64_t* zero, 
     const int64_t zs = 4 * (int64_t)gx * kThreads * (per == 1 ? 1 : gy);
     for (int64_t z = 4 * zb; z < nzero; z += zs) {
       if (z + 4 <= nzero) {
+#ifdef LBT_PLAIN_PRO
+        *reinterpret_cast<longlong2*>(zero + z) = make_longlong2(0, 0);
+        *reinterpret_cast<longlong2*>(zero + z + 2) = make_longlong2(0, 0);
+#else
         st_out8(zero + z, 0);
         st_out8(zero + z + 1, 0);
         st_out8(zero + z + 2, 0);
         st_out8(zero + z + 3, 0);
+#endif
       } else {
         for (int64_t t = z; t < nzero; ++t) zero[t] = 0;
       }
@@ -325,7 +330,11 @@ LBT_DEV void noise_fill_block(const lbt_njob* __restrict__ jobs, int64_t* zero, 
     const int64_t bb = b + (int64_t)i * gx * kThreads;
     if (4 * bb >= j.n) break;
     const Noise4 n = noise4((uint64_t)bb, j.qid, step, j.seed);
+#ifdef LBT_PLAIN_PRO
+    *reinterpret_cast<float4*>(j.out + 4 * bb) = make_float4(n.u[0], n.u[1], n.u[2], n.u[3]);
+#else
     st_out4(j.out, (uint32_t)(4 * bb), make_float4(n.u[0], n.u[1], n.u[2], n.u[3]));  // tables < 2^29 floats
+#endif
   }
 }
 
@@ -351,7 +360,11 @@ LBT_DEV void quantize_input_block(const lbt_qjob& j, int bx) {
     const int c3 = quant1(s, j.q.stochastic, v.w, nz.u[3], ov1, ov2);
     short4 o;
     o.x = (short)c0; o.y = (short)c1; o.z = (short)c2; o.w = (short)c3;
+#ifdef LBT_PLAIN_PRO
+    *reinterpret_cast<short4*>((int16_t*)j.out + e0) = o;
+#else
     st_out8((int16_t*)j.out + e0, *reinterpret_cast<const long long*>(&o));
+#endif
   }
   block_flush_counts(j.q, ov1, ov2, sh_cnt);
 }

@@ -95,6 +95,14 @@ LBT_DEV void st_out8(void* p, long long v) {
   __hip_atomic_store(reinterpret_cast<long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #endif
+// The step's tail (the optimiser's w / a / g) keeps plain stores: written through they cost 9 us per step
+// (A/B, profiles/r04l_ab: the next step's prologue then reads the weights from memory, not L2).
+// LBT_WT_TAIL (scratch A/B builds): write-through there too.
+#ifdef LBT_WT_TAIL
+#define LBT_ST_TAIL(p, v) st_out((p), (v))
+#else
+#define LBT_ST_TAIL(p, v) (void)(*(p) = (v))
+#endif
 // 16 bytes at any 64-bit address (two 8-byte write-through stores)
 LBT_DEV void st_out16(float* p, float4 v) {
   st_out8(p, (long long)(((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x)));

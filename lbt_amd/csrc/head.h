@@ -102,9 +102,9 @@ LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds, con
         if (u.w) {  // sgd_momentum_elem's arithmetic (gscale 1)
           const float tm = u.mu * af[j];
           const float an = tm + gv;
-          st_out(u.a + ob + oc * K + ok, an);
+          LBT_ST_TAIL(u.a + ob + oc * K + ok, an);
           const float stp = u.lr * an;
-          st_out(u.w + ob + oc * K + ok, wf[j] - stp);
+          LBT_ST_TAIL(u.w + ob + oc * K + ok, wf[j] - stp);
         }
       }
     }

@@ -493,8 +493,15 @@ LBT_DEV int swz64(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
 // 128-byte rows (8 segments; quad = (row & 1, segment)), segments 2q ^ f and 2q + 1 ^ f: f = (row >> 1) & 5.
 LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 
+// waves per SIMD the register allocation must leave room for (4: two 512-thread workgroups per CU).
+// 16-bit codes at BN 64: 142 -> 128 VGPRs (20 bytes of spill), two workgroups per CU: l1_c2 dgrad16
+// 170.6 -> 155.6 us, the other shapes unchanged (profiles/r04l_ab probe_*.txt); A8 BN 128 at 3-4 stages
+// would spill 200+ bytes.
+#ifndef LBT_BIG_OCC
+#define LBT_BIG_OCC(A16, BN, S) ((A16 && BN == 64) ? 4 : 1)
+#endif
 template <int MODE, bool A16, bool ADD, int BN, int S>
-__global__ __launch_bounds__(kBT, 1) void igemm_big_kernel(IgArgs p) {
+__global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel(IgArgs p) {
   constexpr int BM = 256, WN = BN / 64, WM = 8 / WN, TR = BM / WM, MI = TR / 16, NJ = 4;
   constexpr int NA = A16 ? 2 : 1;
   constexpr int ROWB = A16 ? 128 : 64;                 // bytes of one A row per k-block

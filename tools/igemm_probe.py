@@ -20,7 +20,8 @@ shapes = [("l1_c3_fwd", B, 56, 64, 256, 1, 1, "fwd"), ("l1_c1_dgrad16", B, 56, 2
           ("l4_c2_fwd", B, 7, 512, 512, 3, 1, "fwd"), ("l4_c2_dgrad16", B, 7, 512, 512, 3, 1, "dgrad"),
           ("l1_c2_fwdq", B, 56, 64, 64, 3, 1, "fwdq"), ("l2_c2_fwdq", B, 28, 128, 128, 3, 1, "fwdq"),
           ("l3_c2_fwdq", B, 14, 256, 256, 3, 1, "fwdq"), ("l1_c3_fwdq", B, 56, 64, 256, 1, 1, "fwdq"),
-          ("l3_c3_fwdq", B, 14, 256, 1024, 1, 1, "fwdq")]
+          ("l3_c3_fwdq", B, 14, 256, 1024, 1, 1, "fwdq"), ("l1_c3_dgrad16", B, 56, 64, 256, 1, 1, "dgrad"),
+          ("l2_c3_dgrad16", B, 28, 128, 512, 1, 1, "dgrad")]
 # PROBE_QNOISE: inline (Philox in the epilogue), table (a per-step noise table, lbt_dfxp_noise_fill),
 # none (round-to-nearest quantiser)
 QN = os.environ.get("PROBE_QNOISE", "inline")
