@@ -57,8 +57,11 @@ constexpr int kRL4 = kT / kCQ; // 16 pixel lanes
 // and its shortcut BN); the mask_r and plain forms carry no registers for them.
 constexpr int kRowsA = 256;
 
+#ifndef LBT_BNA_WPE
+#define LBT_BNA_WPE 4  // waves per SIMD the register allocation targets
+#endif
 template <bool YM>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) void bn_bwd_a_wide_kernel(WideA a) {
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(LBT_BNA_WPE))) void bn_bwd_a_wide_kernel(WideA a) {
   __shared__ long long red[kT / 64][4][kCB];
   __shared__ int sh_cnt[2 * 2 * (kT / 64)];
   const int cq = threadIdx.x % kCQ, pl = threadIdx.x / kCQ;

@@ -71,16 +71,23 @@ LBT_DEV void epi_quant(const QOut& o, const QState& qs, int64_t mtile, int nt0, 
     s1[j] = 0;
     s2[j] = 0;
     const int col = (nt0 + j) * 16 + r;
+    int cc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t row = mtile * 16 + 4 * kg + i;
+      cc[i] = 0;
       if (row < o.M) {
         const int c = quant_w<-1>(qs, o.q.stochastic, v[j][i], u[j][i], ov1, ov2);
-        o.yq[(uint32_t)row * (uint32_t)o.ncol + col] = (int8_t)c;  // M * ncol < 2^31 (launchers)
+        cc[i] = c;
         s1[j] += c;
         s2[j] += c * c;
       }
     }
+    // the 4 lanes of a column quad swap codes so lane r stores row 4 kg + (r & 3)'s 4 columns as one
+    // write-through dword (the next launch reads them) instead of 4 scattered byte stores
+    const uint32_t packed = quad_pack_codes(cc, r & 3);
+    const int64_t rowp = mtile * 16 + 4 * kg + (r & 3);
+    if (rowp < o.M) st_out(o.yq + (uint32_t)rowp * (uint32_t)o.ncol + (col & ~3), (int)packed);  // M * ncol < 2^31
   }
   const bool want_sum = o.chsum != nullptr;
   if (want_sum) {

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/lbt_dfxp.h"
 
 #define LBT_DEV __device__ __forceinline__
@@ -267,6 +269,35 @@ LBT_DEV void counts_stage_w(int i, int nq, int ov1w, int ov2w, int* sh) {
     p[0] = ov1w;
     p[1] = ov2w;
   }
+}
+
+// Lane (jj + K) & 3's v, jj = this lane's slot in its 4-lane group (K = 0..3, compile time): a DPP quad
+// permutation (a VALU move; __shfl would be an LDS ds_bpermute round trip)
+template <int K>
+LBT_DEV int quad_from(int v) {
+  if constexpr (K == 0) return v;
+  else if constexpr (K == 1) return __builtin_amdgcn_mov_dpp(v, 0x39, 0xf, 0xf, false);  // quad_perm [1,2,3,0]
+  else if constexpr (K == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  else return __builtin_amdgcn_mov_dpp(v, 0x93, 0xf, 0xf, false);                        // quad_perm [3,0,1,2]
+}
+template <int K>
+LBT_DEV float quad_from(float v) { return __int_as_float(quad_from<K>(__float_as_int(v))); }
+// 4 lanes x 4 byte codes transposed: lane jj of a 4-lane group holding c[i] (its column, rows i < 4)
+// returns row jj's codes of the group's 4 columns packed into a dword (column g*4 + b in byte b)
+LBT_DEV uint32_t quad_pack_codes(const int (&c)[4], int jj) {
+  uint32_t packed = 0;
+  auto step = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int sc = (jj - k) & 3;
+    const int send = sc == 0 ? c[0] : sc == 1 ? c[1] : sc == 2 ? c[2] : c[3];
+    const int got = quad_from<k>(send);
+    packed |= ((uint32_t)got & 0xFFu) << (8 * ((jj + k) & 3));
+  };
+  step(std::integral_constant<int, 0>{});
+  step(std::integral_constant<int, 1>{});
+  step(std::integral_constant<int, 2>{});
+  step(std::integral_constant<int, 3>{});
+  return packed;
 }
 
 // ------------------------------------------------------------------ reductions

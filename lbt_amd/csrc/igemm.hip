@@ -21,6 +21,7 @@
 #include "lds_tr.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -91,7 +92,7 @@ LBT_DEV void quant_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i
                             int64_t rtile, int rlim, bool full, int cw, int r, int q) {
   const QState qs = qstate(p.qout);
   const int ncol = p.ncol;
-  const int jj = r & 3, gbase = (int)(threadIdx.x & 63) & ~3;  // this lane's slot and its group's first lane
+  const int jj = r & 3;  // this lane's slot in its 4-lane group
   int ov1w = 0, ov2w = 0;
   int cs1[NJ], cs2[NJ];
 #pragma unroll
@@ -108,21 +109,24 @@ LBT_DEV void quant_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i
       const uint64_t blk = ((uint64_t)pix * (uint32_t)ncol + (uint32_t)(col & ~3)) >> 2;
       Noise4 mine = {{0.f, 0.f, 0.f, 0.f}};
       if (p.qout.stochastic) mine = qnoise4(p.qout, qs.step, blk);
-      float u[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        // step k: lane jj sends its block's value for column (jj - k) & 3 of the group and
-        // receives, from lane (jj + k) & 3, the value of this lane's column for row (jj + k) & 3
+      float u[4] = {0.f, 0.f, 0.f, 0.f};
+      // step k: lane jj sends its block's value for column (jj - k) & 3 of the group and
+      // receives, from lane (jj + k) & 3, the value of this lane's column for row (jj + k) & 3
+      auto noise_step = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
         const int sc = (jj - k) & 3;
         const float send = sc == 0 ? mine.u[0] : sc == 1 ? mine.u[1] : sc == 2 ? mine.u[2] : mine.u[3];
-        const float got = __shfl(send, gbase + ((jj + k) & 3), 64);
+        const float got = quad_from<k>(send);
         const int re = (jj + k) & 3;
-        if (k == 0) u[0] = u[1] = u[2] = u[3] = 0.f;
         u[0] = re == 0 ? got : u[0];
         u[1] = re == 1 ? got : u[1];
         u[2] = re == 2 ? got : u[2];
         u[3] = re == 3 ? got : u[3];
-      }
+      };
+      noise_step(std::integral_constant<int, 0>{});
+      noise_step(std::integral_constant<int, 1>{});
+      noise_step(std::integral_constant<int, 2>{});
+      noise_step(std::integral_constant<int, 3>{});
       const int wsum = accw[j][0];
       int cc[4];
 #pragma unroll
@@ -136,14 +140,7 @@ LBT_DEV void quant_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i
       }
       // the same 4-lane transpose on the codes: lane jj collects row jj's codes of the group's 4
       // columns and stores them as one dword
-      uint32_t packed = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int sc = (jj - k) & 3;
-        const int send = sc == 0 ? cc[0] : sc == 1 ? cc[1] : sc == 2 ? cc[2] : cc[3];
-        const int got = __shfl(send, gbase + ((jj + k) & 3), 64);
-        packed |= ((uint32_t)got & 0xFFu) << (8 * ((jj + k) & 3));
-      }
+      const uint32_t packed = quad_pack_codes(cc, jj);
       if (full || i * 16 + jj < rlim)
         *reinterpret_cast<uint32_t*>(p.yq + (rtile + i * 16 + jj) * ncol + (col & ~3)) = packed;
     }

@@ -904,6 +904,46 @@ def test_stem_merge_equals_separate_launches(B, monkeypatch):
     assert a[5] == b[5]
 
 
+@pytest.mark.parametrize("B", [128, 32])
+def test_fused_update_and_head_chain_equal_separate_launches(B, monkeypatch):
+    """The round-4 launch merges against the launches they replace, two graph-replayed optimiser steps
+    then one eager one: the optimiser + update_range inside the step's last launch
+    (lbt_step_reduce_update, LBT_FUSED_UPDATE) vs lbt_step_reduce + lbt_step_update, and the last
+    block's end chain inside the fused head (lbt_head.chain, LBT_HEAD_CHAIN) vs lbt_bn_chain_fwd +
+    the head on its output. Gradients, momentum, weights, exponents, noise step, BN running statistics
+    and loss bit-identical."""
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.models import CIFAR10_Resnet20
+    from lbt_amd.trainer import Trainer
+    outs = []
+    for upd, chain in (("1", "1"), ("0", "0"), ("1", "0"), ("0", "1")):
+        monkeypatch.setenv("LBT_FUSED_UPDATE", upd)
+        monkeypatch.setenv("LBT_HEAD_CHAIN", chain)
+        ctx = DfxpContext(seed=11)
+        m = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx))
+        tr = Trainer(m, lr=1e-2, momentum=0.9, batch_size=B, use_graph=True)
+        for i in range(3):
+            if i == 2:
+                tr.use_graph = False
+            x, y = synthetic_batch(B, seed=80 + i)
+            tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+        torch.cuda.synchronize()
+        names = [getattr(f, "kname", "") for f in m._fwd]
+        assert ("chain_fwd_kernel" in names) == (chain == "0"), (upd, chain)
+        assert m.updates_in_step() == (upd == "1")
+        bn = [t.cpu().numpy() for l in tr._bn_layers() for t in (l.X_mean_running, l.X_var_running)]
+        outs.append((tr.flat.g.cpu().numpy(), tr.flat.a.cpu().numpy(), tr.flat.w.cpu().numpy(), ctx.ranges(), bn,
+                     m.loss.item(), int(ctx.step.item())))
+    ref = outs[0]
+    for o in outs[1:]:
+        for i in range(3):
+            assert np.array_equal(ref[i], o[i]), i
+        assert ref[3] == o[3]
+        for u, v in zip(ref[4], o[4]):
+            assert np.array_equal(u, v)
+        assert ref[5] == o[5] and ref[6] == o[6] == 3
+
+
 # (N, H, W, Cin, Cout, k, s): the staged 3x3 / stride-1 body (W | 64, whole-row chunks) and the
 # per-tap body (strided / 1x1), mixed in one launch
 WGRAD_MANY_CASES = [(8, 32, 32, 16, 16, 3, 1), (8, 16, 16, 32, 32, 3, 1), (8, 8, 8, 64, 64, 3, 1),
