@@ -201,6 +201,28 @@ typedef struct lbt_igemm_tuning {
 } lbt_igemm_tuning;
 int lbt_igemm_get_tuning(lbt_igemm_tuning* out);
 int lbt_igemm_set_tuning(const lbt_igemm_tuning* t);
+/* A 16-bit-gradient dgrad (lbt_conv_dgrad_igemm_ws, g_i16 = 1, no add_src) whose dx is the incoming
+ * gradient of a ReLU_q + BN (Rescale_q :686-691, Normalization_q :620-623): ResidualBottleneck_q's bn1 /
+ * bn2 behind conv-2 / conv-3. Produces what lbt_bn_bwd_a_wide_masked(dx, mask_r = 1, ...) would from
+ * that dx -- the G codes, the four channel sums, both quantisers' overflow counters -- and, when the
+ * 256-row GEMM takes the dgrad (unit stride, enough tiles) and each stochastic quantiser carries its
+ * noise table (lbt_qdesc.noise over inner = H*W*Cin), evaluates it in the GEMM epilogue: no fp32 dx
+ * is stored or read. Otherwise dx (scratch, N*H*W*Cin floats, required) is stored and pass A runs
+ * after. Bit-identical either way. bna.sums accumulates (zero it per step); qrg / qng <= 16 bits.
+ * Reference: Conv2d_q.backward :299-310 followed by ReLU_q / Rescale_q / Normalization_q backward.   */
+typedef struct lbt_dgrad_bna {
+  lbt_qdesc qr;          /* Rescale_q input quantiser: the ReLU mask ((float)R * s_qr) * gb[c] + gb[C+c] > 0 */
+  const int8_t* R;       /* Rescale_q input codes [rows][Cin]                                     */
+  const float* gb;       /* [gamma_q | beta_q] dequantised (2 Cin); gamma_q also scales the rescale  */
+  lbt_qdesc qrg;         /* Rescale_q gradient quantiser                                           */
+  lbt_qdesc qng;         /* Normalization_q gradient quantiser                                      */
+  const int8_t* qn;      /* Normalization_q input codes [rows][Cin]                                */
+  int16_t* gout;         /* G codes out [rows][Cin]                                                */
+  int64_t* sums;         /* [LBT_NSHARD][4 Cin]: S(G2 R), S(G2), S(G), S(G qn) added in          */
+} lbt_dgrad_bna;
+int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                             lbt_qdesc qw, const lbt_dgrad_bna* bna, float* dx, void* ws, int64_t ws_bytes,
+                             void* stream);
 int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
                          int32_t nsplit, int32_t nshard, void* stream);
 /* ... storing one partial per pixel split: slab [nsplit][KH*KW*Cin][Cout] is fully WRITTEN (no

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -164,6 +164,11 @@ class Update(ctypes.Structure):
                 ("nelem", c_void_p), ("step", c_void_p), ("nslots", c_int32), ("pad", c_int32)]
 
 
+class DgradBna(ctypes.Structure):
+    _fields_ = [("qr", QDesc), ("R", c_void_p), ("gb", c_void_p), ("qrg", QDesc), ("qng", QDesc), ("qn", c_void_p),
+                ("gout", c_void_p), ("sums", c_void_p)]
+
+
 class FSeg(ctypes.Structure):
     _fields_ = [("off", c_int64), ("n", c_int64), ("kind", c_int32), ("qx", QDesc), ("qg", QDesc), ("wd2", c_float)]
 
@@ -191,6 +196,8 @@ _SIGS = {
     "lbt_conv_fwd_igemm_q": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, QDesc, _P, _P],
     "lbt_conv_fwd_igemm_ws": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P, c_int64, _P],
     "lbt_conv_dgrad_igemm_ws": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int64, _P],
+    "lbt_conv_dgrad_igemm_bna": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, ctypes.POINTER(DgradBna), _P, _P, c_int64,
+                                 _P],
     "lbt_conv_wgrad_igemm_store": [_P, _P, c_int32, ConvDesc, _P, c_int32, _P],
     "lbt_conv_dgrad_chain_i8w4": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_dgrad_chain_i8": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],

@@ -69,6 +69,10 @@ struct IgArgs {
   // (ih + PT - kh) % SH == 0 reach such a pixel, and for them the source row is yc + oy - th (no
   // zero rows, no division in the loop).
   int nkh, nkw, kh0, kw0, oy, ox, ch, cw, cpy, cpx;
+  // dgrad, A16, 256-row kernel only (has_bna): the BN pass A this dx feeds (lbt_dgrad_bna), run in the
+  // epilogue instead of storing dx (bna_epilogue)
+  int has_bna;
+  lbt_dgrad_bna bna;
   int dbg;  // igemm_big_kernel diagnostics (LBT_IGEMM_BIG_DBG; 1: no operand loads after the prologue)
 };
 
@@ -497,7 +501,155 @@ LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 #ifndef LBT_BIG_OCC
 #define LBT_BIG_OCC(A16, BN, S) ((A16 && BN == 64) ? 4 : 1)
 #endif
-template <int MODE, bool A16, bool ADD, int BN, int S>
+// bn_bwd_a_wide_kernel's mask_r pass (bn_wide.hip) on the dgrad accumulators, element for element:
+// dx (the value the plain epilogue stores) -> ReLU mask from R -> G2 = Q_rg -> gamma-scaled rescale
+// gradient -> G = Q_ng (stored) + the four channel sums + both quantisers' counters. Lane (r, q)
+// holds column cw + 16 j + r of rows rtile + 16 i + e (e < 4): the int8 operands, the two noise
+// tables and the int16 G codes move through 4-lane DPP transposes, so each lane loads / stores one
+// row's 4 consecutive channels (R and qn one dword each, noise a float4, G 8 bytes). Rows past M
+// evaluate 0 (code 0, no overflow, no sums) and store nothing. Channel sums: the 4 q-lanes of a
+// column (rows_scatter2), the WM waves of the tile in LDS (int32: 256 rows x 2^22), one int64 atomic
+// per (column, sum) into shard tile % NSHARD. Noise index = (row % (H*W)) * C + column (the period
+// over shape[1:], dynamic_fixed_point.py:32-38).
+template <int MI, int NJ, int WM, int BN>
+LBT_DEV void bna_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4i (&accw)[NJ], float scale,
+                          int64_t rtile, int rlim, bool full, int n0, int cw, int r, int q, int wm, uint32_t tile,
+                          int8_t* lds) {
+  const lbt_dgrad_bna& b = p.bna;
+  const int C = p.ncol;
+  const QState srg = qstate(b.qrg), sng = qstate(b.qng);
+  const float sr = qstate(b.qr).inv_m;
+  const int srs = b.qrg.stochastic, sns = b.qng.stochastic;
+  const int jj = r & 3, g4 = r & ~3;
+  const uint32_t hw = (uint32_t)(p.ch * p.cw);
+  uint32_t pixl[MI];  // the noise pixel of the row this lane loads / stores, per i
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const bool okl = full || i * 16 + jj < rlim;
+    pixl[i] = (uint32_t)(okl ? rtile + i * 16 + jj : 0) % hw;
+  }
+  int o1 = 0, o2 = 0, p1 = 0, p2 = 0;
+  int* red = reinterpret_cast<int*>(lds);  // [WM][4][BN] per-wave column sums
+  __syncthreads();  // every wave's last fragment reads of the LDS ring are done
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = cw + j * 16 + r;
+    const float gam = b.gb[col], bet = b.gb[C + col];
+    const int wsum = accw[j][0];
+    const int cg = cw + j * 16 + g4;  // the 4-lane group's first column
+    int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t rowl = rtile + i * 16 + jj;  // the row this lane loads / stores
+      const bool okl = full || i * 16 + jj < rlim;
+      const int64_t off = rowl * C + cg;
+      uint32_t rw = 0, qw = 0;
+      if (okl) {
+        rw = *reinterpret_cast<const uint32_t*>(b.R + off);
+        qw = *reinterpret_cast<const uint32_t*>(b.qn + off);
+      }
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const uint32_t noff = pixl[i] * (uint32_t)C + cg;
+      const float4 n1 = srs ? *reinterpret_cast<const float4*>(b.qrg.noise + noff) : z4;
+      const float4 n2 = sns ? *reinterpret_cast<const float4*>(b.qng.noise + noff) : z4;
+      // step k: lane jj sends its row's value of column (jj - k) & 3 and receives, from lane (jj + k) & 3,
+      // row (jj + k) & 3's value of its own column
+      int Rv[4] = {0, 0, 0, 0}, Qv[4] = {0, 0, 0, 0};
+      float u1[4] = {0.f, 0.f, 0.f, 0.f}, u2[4] = {0.f, 0.f, 0.f, 0.f};
+      auto tstep = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const int sc = (jj - k) & 3, re = (jj + k) & 3;
+        const uint32_t sh = 8u * (uint32_t)sc;
+        const int srq = (int)(((rw >> sh) & 0xFFu) | (((qw >> sh) & 0xFFu) << 16));
+        const int grq = quad_from<k>(srq);
+        const float gu1 = quad_from<k>(sc == 0 ? n1.x : sc == 1 ? n1.y : sc == 2 ? n1.z : n1.w);
+        const float gu2 = quad_from<k>(sc == 0 ? n2.x : sc == 1 ? n2.y : sc == 2 ? n2.z : n2.w);
+        const int rv = (int)(int8_t)(grq & 0xFF), qv = (int)(int8_t)((grq >> 16) & 0xFF);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          Rv[e] = re == e ? rv : Rv[e];
+          Qv[e] = re == e ? qv : Qv[e];
+          u1[e] = re == e ? gu1 : u1[e];
+          u2[e] = re == e ? gu2 : u2[e];
+        }
+      };
+      tstep(std::integral_constant<int, 0>{});
+      tstep(std::integral_constant<int, 1>{});
+      tstep(std::integral_constant<int, 2>{});
+      tstep(std::integral_constant<int, 3>{});
+      int cc[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = full || i * 16 + e < rlim;
+        const double hs = (double)acc[0][i][j][e] * 256.0;
+        const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
+        const float v = ok ? (float)(hs + ls) * scale : 0.f;
+        // bn.hip chain_bwd_a's mask recomputation and the two quantisers, op for op (bn_wide.hip :139-175)
+        const float xr = (float)Rv[e] * sr;
+        const float m1 = xr * gam;
+        const float yv = m1 + bet;
+        float dd = yv > 0.f ? v : 0.f;
+        const int G2 = quant1(srg, srs, dd, u1[e], o1, o2);
+        s0 += G2 * Rv[e];
+        s1 += G2;
+        const float gh = (float)G2 * srg.inv_m;
+        dd = gh * gam;
+        const int G = quant1(sng, sns, dd, u2[e], p1, p2);
+        s2 += G;
+        s3 += G * Qv[e];
+        cc[e] = G;
+      }
+      // the transpose back: lane jj collects row jj's 4 codes (columns cg .. cg + 3)
+      uint32_t lo = 0, hi = 0;
+      auto pstep = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const int sc = (jj - k) & 3, ce = (jj + k) & 3;
+        const int got = quad_from<k>(sc == 0 ? cc[0] : sc == 1 ? cc[1] : sc == 2 ? cc[2] : cc[3]);
+        const uint32_t h = ((uint32_t)got & 0xFFFFu) << (16 * (ce & 1));
+        lo |= ce < 2 ? h : 0u;
+        hi |= ce < 2 ? 0u : h;
+      };
+      pstep(std::integral_constant<int, 0>{});
+      pstep(std::integral_constant<int, 1>{});
+      pstep(std::integral_constant<int, 2>{});
+      pstep(std::integral_constant<int, 3>{});
+      if (okl) *reinterpret_cast<uint2*>(b.gout + off) = make_uint2(lo, hi);
+    }
+    // the column's 4 q-lanes meet (rows_scatter2); each (wave, sum, column) slot has one writer
+    const int t01 = rows_scatter2(s0, s1), t23 = rows_scatter2(s2, s3);
+    const int cl = cw - n0 + j * 16 + r;
+    if (q < 2) {
+      red[(wm * 4 + q) * BN + cl] = t01;
+      red[(wm * 4 + 2 + q) * BN + cl] = t23;
+    }
+  }
+  const int shard = (int)(tile % LBT_NSHARD);
+  // per-lane overflow counts (quant1: VALU, no per-element ballot masks held in SGPRs) -> wave totals
+  o1 = wave_sum_i32(o1); o2 = wave_sum_i32(o2); p1 = wave_sum_i32(p1); p2 = wave_sum_i32(p2);
+  if ((threadIdx.x & 63) == 0) {
+    if (b.qrg.counts) {
+      int32_t* ct = b.qrg.counts + ((int64_t)b.qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (o1) atomicAdd(ct, o1);
+      if (o2) atomicAdd(ct + 1, o2);
+    }
+    if (b.qng.counts) {
+      int32_t* ct = b.qng.counts + ((int64_t)b.qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (p1) atomicAdd(ct, p1);
+      if (p2) atomicAdd(ct + 1, p2);
+    }
+  }
+  __syncthreads();
+  static_assert(4 * BN <= kBT, "one sum per thread");
+  if ((int)threadIdx.x < 4 * BN) {
+    const int sidx = threadIdx.x / BN, cl = threadIdx.x % BN;
+    long long v = 0;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) v += red[(w * 4 + sidx) * BN + cl];
+    if (v) atomicAdd((unsigned long long*)&b.sums[(int64_t)shard * 4 * C + sidx * C + n0 + cl], (unsigned long long)v);
+  }
+}
+
+template <int MODE, bool A16, bool ADD, int BN, int S, bool BNA = false>
 __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel(IgArgs p) {
   constexpr int BM = 256, WN = BN / 64, WM = 8 / WN, TR = BM / WM, MI = TR / 16, NJ = 4;
   constexpr int NA = A16 ? 2 : 1;
@@ -603,10 +755,14 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
       for (int j = 0; j < NJ; ++j) acc[a][i][j] = v4i{0, 0, 0, 0};
 #pragma unroll
   for (int j = 0; j < NJ; ++j) accw[j] = v4i{0, 0, 0, 0};
-  const v4i ones = v4i{0x01010101, 0x01010101, 0x01010101, 0x01010101};
   // sum_k W per column (the +128 term of offset / split codes): from the caller's column sums when it
-  // has them, else from MFMAs against ones (16-bit codes; offset codes of lbt_conv_fwd_igemm_q)
+  // has them, else summed from the B fragments on the VALU (16-bit codes; offset codes of
+  // lbt_conv_fwd_igemm_q) -- 4 v_dot4 per fragment instead of an MFMA against ones (an extra 4 of
+  // the 16 (A8) / 32 (A16) MFMAs per k-block of a 64 x 64 wave tile)
   const bool wmfma = A16 || (p.a_u8off && !p.colsum);  // uniform
+  int csw[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) csw[j] = 0;
 
   // fragments of one k-block (A16: the raw int16 code pairs, split into hi / lo' at the MFMA)
   typedef v4i FragA[MI][NA];
@@ -655,9 +811,11 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
           acc[0][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i][0], fb[j], acc[0][i][j], 0, 0, 0);
       }
     }
-    if (wmfma) {
+    if (wmfma) {  // sum_k W of the column: the lane's 16 k-bytes on the VALU (dot4 with ones), beside the MFMAs
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) accw[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ones, fb[j], accw[j], 0, 0, 0);
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) csw[j] = __builtin_amdgcn_sdot4(fb[j][u], 0x01010101, csw[j], false);
     }
   };
 
@@ -708,6 +866,16 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
     }
   }
   vm_wait<0>();  // the ring's trailing (clamped) DMAs: nothing may still write LDS when the block ends
+  if (wmfma) {  // the column totals: lanes r, r + 16, r + 32, r + 48 hold a quarter of column r's k each
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const auto h = __builtin_amdgcn_permlane32_swap(csw[j], csw[j], false, false);
+      const int t1 = (int)h[0] + (int)h[1];
+      const auto g = __builtin_amdgcn_permlane16_swap(t1, t1, false, false);
+      const int t = (int)g[0] + (int)g[1];
+      accw[j] = v4i{t, t, t, t};
+    }
+  }
 
   // ---- epilogue (igemm_kernel's): lane owns column (tile col + r), rows (tile row + 4q + e)
   const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
@@ -733,6 +901,10 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
       quant_epilogue<MI, NJ>(p, acc[0], accw, u8, scale, rtile, rlim, full, cw, r, q);
       return;
     }
+  }
+  if constexpr (BNA) {
+    bna_epilogue<MI, NJ, WM, BN>(p, acc, accw, scale, rtile, rlim, full, n0, cw, r, q, wm, tile, lds);
+    return;
   }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -782,6 +954,19 @@ void launch_big_bn(IgArgs p, hipStream_t st) {
     (void)attr_;                                                                                          \
     hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, ADD_, BN, S>), dim3((unsigned)tiles), dim3(kBT), shm, st, p); \
   } while (0)
+  if constexpr (MODE == MODE_DGRAD && A16) {
+    if (p.has_bna) {
+      static bool attr_ = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, false, BN, S, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        return true;
+      }();
+      (void)attr_;
+      hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, false, BN, S, true>), dim3((unsigned)tiles), dim3(kBT), shm, st,
+                         p);
+      return;
+    }
+  }
   if (add) LBT_BIG(true); else LBT_BIG(false);
 #undef LBT_BIG
 }
@@ -1090,6 +1275,39 @@ extern "C" int lbt_conv_dgrad_igemm_ws(const void* gq, int32_t g_i16, const int8
   hipStream_t st = (hipStream_t)stream;
   if (d.SH > 1 || d.SW > 1) return g_i16 ? dgrad_classes<true>(p, st) : dgrad_classes<false>(p, st);
   return g_i16 ? launch<MODE_DGRAD, true>(p, st) : launch<MODE_DGRAD, false>(p, st);
+}
+
+// The dgrad with the mask_r BN pass A it feeds (include/lbt_dfxp.h lbt_dgrad_bna): in the 256-row
+// kernel's epilogue when that kernel takes the GEMM, else dgrad into dx + lbt_bn_bwd_a_wide_masked.
+// LBT_DGRAD_BNA=0: always the second form (A/B).
+extern "C" int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                                        lbt_qdesc qg, lbt_qdesc qw, const lbt_dgrad_bna* bna, float* dx, void* ws,
+                                        int64_t ws_bytes, void* stream) {
+  if (!bna || !dx || !desc_ok(d)) return LBT_EINVAL;
+  const lbt_dgrad_bna& b = *bna;
+  if (!b.R || !b.gb || !b.qn || !b.gout || !b.sums || b.qr.bits <= 0) return LBT_EINVAL;
+  if (b.qrg.bits <= 0 || b.qrg.bits > 16 || b.qng.bits <= 0 || b.qng.bits > 16 || d.Cin % 4) return LBT_EINVAL;
+  const int64_t rows = (int64_t)d.N * d.H * d.W, inner = (int64_t)d.H * d.W * d.Cin;
+  hipStream_t st = (hipStream_t)stream;
+  static const int fuse = getenv_int("LBT_DGRAD_BNA", 1);
+  const bool tables = (!b.qrg.stochastic || b.qrg.noise) && (!b.qng.stochastic || b.qng.noise);
+  if (fuse && tables && d.SH == 1 && d.SW == 1 && d.Cout % kBK == 0 && d.Cin % 64 == 0 &&
+      (int64_t)d.KH * d.KW * d.Cout * 255 * 128 < ((int64_t)1 << 31) &&
+      (int64_t)d.N * d.Ho * d.Wo * d.Cout < ((int64_t)1 << 31) && (int64_t)ksd * 16 * d.Cin < ((int64_t)1 << 31) &&
+      ksd * 16 >= d.KH * d.KW * d.Cout && rows * d.Cin < ((int64_t)1 << 31) && lbt_igemm_workspace_bytes(d, 1, 1) == 0) {
+    IgArgs p{};
+    p.a = gq; p.b = wd; p.ks = ksd; p.cred = d.Cout; p.a_u8off = 0; p.d = d; p.qa = qg; p.qb = qw;
+    p.colsum = nullptr; p.y = nullptr; p.add_src = nullptr; p.M = rows; p.ncol = d.Cin;
+    p.ksplit = 1;
+    all_taps(p, MODE_DGRAD);
+    p.has_bna = 1;
+    p.bna = b;
+    if (launch_big<MODE_DGRAD, true>(p, st)) return (int)hipGetLastError();
+  }
+  int rc = lbt_conv_dgrad_igemm_ws(gq, 1, wd, ksd, d, qg, qw, dx, nullptr, ws, ws_bytes, stream);
+  if (rc) return rc;
+  return lbt_bn_bwd_a_wide_masked(dx, nullptr, nullptr, nullptr, 1, b.qr, b.gb, nullptr, b.qrg, b.R, b.qng, b.qn,
+                                  b.gout, nullptr, b.sums, rows, inner, d.Cin, stream);
 }
 
 namespace {

@@ -67,6 +67,10 @@ class _Cache:
 # SIDE_STREAM is read once from LBT_SIDE_STREAM (0 = one stream); assign the attribute to change
 # it (a HIP graph captured earlier keeps the schedule it was captured with).
 SIDE_STREAM = os.environ.get("LBT_SIDE_STREAM", "1") != "0"
+# ResidualBottleneck_q: bn1 / bn2's pass A inside conv-2 / conv-3's dgrad (ops.conv_dgrad_igemm_bna);
+# LBT_DGRAD_BNA_PY=0: the separate dgrad + pass A launches (A/B, and the C-side LBT_DGRAD_BNA=0 keeps
+# the entry point but never fuses)
+DGRAD_BNA = os.environ.get("LBT_DGRAD_BNA_PY", "1") != "0"
 _SIDE = {}
 _PENDING = {}
 _DEPTH = [0]
@@ -1191,11 +1195,46 @@ class ResidualBottleneck_q(ResidualBlock_q):
         G16 = n._c.get("G16", g.shape, torch.int16, dev)
         ops.bn_bwd_a_wide_masked(g, y_mask, mask_r, r.X_range.desc, r.gb, gmask_out, r.grad_range.desc, r.R,
                                  n.grad_range.desc, n.q, G16, sums, rows, inner, C, g2=g2, y_bits=y_bits)
+        return ResidualBottleneck_q._bn_bwd_b(bn, conv_out, G16, sums, g.numel(), rows, inner, C)
+
+    @staticmethod
+    def _dgrad_bn_bwd(conv, gq16, bn, conv_out, ctx):
+        """_bn_bwd(bn, conv_out, conv.bwd_codes16(gq16), mask_r=True) with bn's pass A evaluated on
+        conv's dgrad (ops.conv_dgrad_igemm_bna): in the 256-row GEMM's epilogue, no fp32 dx, when that
+        kernel takes the dgrad. bn is the BN in front of conv's input (bn2 behind conv-3, bn1 behind
+        conv-2); returns conv_out's int16 gradient codes."""
+        if not DGRAD_BNA:
+            return ResidualBottleneck_q._bn_bwd(bn, conv_out, conv.bwd_codes16(gq16), ctx, mask_r=True)
+        n, r = bn.layers
+        conv.gradq = gq16
+        with backward_scope():
+            with side_work():  # dW: read only by the optimizer
+                conv._wgrad_igemm(1)
+            d = conv.d
+            C = d.Cin
+            shape = (d.N, d.H, d.W, C)
+            numel = d.N * d.H * d.W * C
+            rows, inner = numel // C, numel // d.N
+            dev = gq16.device
+            sums = r._c.sums("fsums", ops.NSHARD * 4 * C, ctx)
+            r.grad_range.observe(numel)
+            n.grad_range.observe(numel)
+            G16 = n._c.get("G16", shape, torch.int16, dev)
+            dx = conv._c.get("dx", shape, torch.float32, dev)  # used only when the dgrad cannot fuse
+            ops.conv_dgrad_igemm_bna(gq16, conv.wd, conv.ksd, d, conv.grad_range.desc, conv.W_range.desc,
+                                     r.X_range.desc, r.R, r.gb, r.grad_range, n.grad_range, n.q, G16, sums, dx,
+                                     conv._ws(d, 1, True))
+            return ResidualBottleneck_q._bn_bwd_b(bn, conv_out, G16, sums, numel, rows, inner, C)
+
+    @staticmethod
+    def _bn_bwd_b(bn, conv_out, G16, sums, numel, rows, inner, C):
+        """dgamma / dbeta (side stream) and pass B into conv_out's 16-bit gradient quantiser."""
+        n, r = bn.layers
         with side_work():
             ops.bn_param_grads(sums, C, r.grad_range.desc, r.X_range.desc, r.gamma, ops.f32(2 * r.weight_decay),
                                r.dgamma, r.dbeta)
-        conv_out.grad_range.observe(g.numel())
-        gq = conv_out._c.get("gq16", g.shape, torch.int16, dev)
+        conv_out.grad_range.observe(numel)
+        gq = conv_out._c.get("gq16", G16.shape, torch.int16, G16.device)
         ops.bn_bwd_b_wide_q(G16, n.grad_range.desc, n.q, n.X_range.desc, n.ms, sums, n.n, gq,
                             conv_out.grad_range.desc, rows, inner, C)
         return gq
@@ -1216,10 +1255,8 @@ class ResidualBottleneck_q(ResidualBlock_q):
         ym = dict(y_bits=self.ybits) if self.ybits is not None else dict(y_mask=self.y)
         g3 = self._bn_bwd(bn3, c3, gin, ctx, gmask_out=gmask, g2=gin2, **ym)
         gs = self._bn_bwd(sc[1], sc[0], gin, ctx, g2=gin2, **ym) if sc else None
-        d3 = c3.bwd_codes16(g3)
-        g2 = self._bn_bwd(bn2, c2, d3, ctx, mask_r=True)
-        d2 = c2.bwd_codes16(g2)
-        g1 = self._bn_bwd(bn1, c1, d2, ctx, mask_r=True)
+        g2 = self._dgrad_bn_bwd(c3, g3, bn2, c2, ctx)
+        g1 = self._dgrad_bn_bwd(c2, g2, bn1, c1, ctx)
         other = sc[0].bwd_codes16(gs) if sc else gmask
         pb = self.prev_block
         if pb is not None and pb._fusable():

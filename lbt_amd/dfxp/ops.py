@@ -1,5 +1,6 @@
 """Typed wrappers over the C-ABI (include/lbt_dfxp.h). Tensors in, kernels launched on the
 current torch stream, nothing synchronised. All shape logic of the HIP path lives here."""
+import ctypes
 import math
 import os
 
@@ -655,6 +656,23 @@ def conv_dgrad_igemm_ws(gq, g_i16, wd, ksd, d, qg, qw, dx, ws, add_src=None):
 
 
 NOISE_TABLES = os.environ.get("LBT_EPI_NOISE_TABLE", "1") == "1"
+
+
+def conv_dgrad_igemm_bna(gq16, wd, ksd, d, qg, qw, qr, R, gb, qrg, qng, qn, gout, sums, dx, ws):
+    """16-bit-gradient dgrad whose dx is the incoming gradient of a ReLU_q + BN pass A (mask from the
+    Rescale_q codes R, lbt_conv_dgrad_igemm_bna): G codes `gout` + the channel sums + both quantisers'
+    counters, in the 256-row GEMM's epilogue when that kernel takes the GEMM (no fp32 dx), else through
+    dx (scratch) and bn_bwd_a_wide_masked. qrg / qng: Quantizer objects (stochastic ones read this
+    step's noise tables over H*W*Cin); qr: the R codes' descriptor."""
+    inner = d.H * d.W * d.Cin
+    descs = []
+    for q in (qrg, qng):
+        descs.append(q.ctx.noise_table_desc(q, inner) if (NOISE_TABLES and q.stochastic) else q.desc)
+    b = _lib.DgradBna(qr, ptr(R), ptr(gb), descs[0], descs[1], ptr(qn), ptr(gout), ptr(sums))
+    n = d.N * inner
+    with _Timed("igemm_kernel<dgrad+bn_a>", gq16.numel() * 2 + wd.numel() + 4 * n):
+        call("lbt_conv_dgrad_igemm_bna", ptr(gq16), ptr(wd), int(ksd), d, qg, qw, ctypes.byref(b), ptr(dx), ptr(ws),
+             0 if ws is None else ws.numel() * ws.element_size(), stream())
 
 
 def conv_fwd_igemm_q(xq, a_kind, wf, ksf, d, qx, qw, yq, qout, chsum):

@@ -52,7 +52,8 @@ STRUCTS = {"lbt_qdesc": _lib.QDesc, "lbt_conv_desc": _lib.ConvDesc, "lbt_bn_norm
            "lbt_head": _lib.Head, "lbt_xchg": _lib.Xchg, "lbt_fseg": _lib.FSeg,
            "lbt_wgrad_job": _lib.WgradJob, "lbt_conv_bwd": _lib.ConvBwd,
            "lbt_conv_fwd": _lib.ConvFwd, "lbt_conv_fwd_job": _lib.ConvFwdJob,
-           "lbt_igemm_tuning": _lib.IgemmTuning, "lbt_update": _lib.Update}
+           "lbt_igemm_tuning": _lib.IgemmTuning, "lbt_update": _lib.Update,
+           "lbt_dgrad_bna": _lib.DgradBna}
 
 
 def test_struct_layouts_match_c():

@@ -154,6 +154,63 @@ def test_big_quantising_epilogue_matches_fwd_then_quantize(N, H, Cin, Cout, k, a
         assert torch.equal(cs.view(NSHARD, -1).sum(0), cs_ref.view(NSHARD, -1).sum(0)), (stages, max_bn)
 
 
+@pytest.mark.parametrize("N,H,Cin,Cout,k", [
+    (3, 14, 128, 64, 3),    # conv-2's dgrad shape (3x3), ncol = 128, M = 588 (ragged last tile)
+    (2, 15, 64, 256, 1),    # conv-3's dgrad shape (1x1, K = 256), ncol = 64, M = 450
+])
+@pytest.mark.parametrize("stochastic", [True, False])
+def test_big_dgrad_bna_matches_dgrad_then_pass_a(N, H, Cin, Cout, k, stochastic):
+    """lbt_conv_dgrad_igemm_bna (ResidualBottleneck_q bn1 / bn2 pass A in the dgrad16 epilogue: ReLU mask
+    from R, Rescale_q and Normalization_q gradient quantisers, noise from the per-step tables) ==
+    lbt_conv_dgrad_igemm_ws -> lbt_bn_bwd_a_wide_masked(mask_r): the same G codes, channel sums and
+    overflow counters, on every ring depth / column tile, and through the entry's own unfused fallback
+    (reference Conv2d_q.backward :299-310, then ReLU_q, Rescale_q :686-691, Normalization_q :620-623)."""
+    from lbt_amd._lib import NSHARD
+    from lbt_amd.dfxp import ops
+    rng, ctx, (_, qw, qg), d, _, _, (wd, ksd), _ = _setup(N, H, Cin, Cout, k, 1, N * H + Cin + int(stochastic))
+    g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, d.Ho, d.Wo, Cout)).astype(np.int16)).to(DEV)
+    dx = torch.empty((N, H, H, Cin), device=DEV)
+    ops.conv_dgrad_igemm(g, 1, wd, ksd, d, qg.desc, qw.desc, dx)
+    # ranges that clip a few percent of both quantisers' inputs (every counter non-zero)
+    top = int(np.ceil(np.log2(float(dx.abs().max())))) - 1
+    qr = ctx.quantizer("t/rX", 8, 2)
+    qrg = ctx.quantizer("t/rg", 16, top, stochastic=stochastic)
+    qng = ctx.quantizer("t/ng", 16, top, stochastic=stochastic)
+    R = torch.from_numpy(rng.integers(-128, 128, size=dx.shape).astype(np.int8)).to(DEV)
+    qn = torch.from_numpy(rng.integers(-128, 128, size=dx.shape).astype(np.int8)).to(DEV)
+    gb = torch.from_numpy(np.concatenate([rng.uniform(-2, 2, Cin), rng.uniform(-1, 1, Cin)]).astype(np.float32)).to(DEV)
+    rows, inner = N * H * H, H * H * Cin
+
+    def counts():
+        v = ctx.counts_view()
+        return torch.stack([v[qrg.slot].sum(0), v[qng.slot].sum(0)]).cpu()
+
+    ctx.counts.zero_()
+    G_ref = torch.empty(dx.shape, dtype=torch.int16, device=DEV)
+    s_ref = torch.zeros(NSHARD * 4 * Cin, dtype=torch.int64, device=DEV)
+    ops.bn_bwd_a_wide_masked(dx, None, True, qr.desc, gb, None, qrg.desc, R, qng.desc, qn, G_ref, s_ref, rows, inner,
+                             Cin)
+    c_ref = counts()
+    assert (c_ref > 0).all(), c_ref
+    s_ref = s_ref.view(NSHARD, -1).sum(0)
+    variants = [(b, s, m) for b, s, m in [(1, st, mb) for st, mb in VARIANTS if mb <= 128] + [(0, 2, 128)]]
+    for big, stages, max_bn in variants:
+        ctx.counts.zero_()
+        G = torch.full_like(G_ref, 12345)
+        sums = torch.zeros(NSHARD * 4 * Cin, dtype=torch.int64, device=DEV)
+        scratch = torch.full_like(dx, float("nan"))
+        n0 = _launches()
+        with ops.igemm_forced(big=big, min_tiles=1, stages=stages, max_bn=max_bn):
+            ops.conv_dgrad_igemm_bna(g, wd, ksd, d, qg.desc, qw.desc, qr.desc, R, gb, qrg, qng, qn, G, sums, scratch,
+                                     None)
+        assert _launches() == n0 + big, "the 256-row kernel did not run"
+        if big:
+            assert torch.isnan(scratch).all(), "the fused path must not store dx"
+        assert torch.equal(G, G_ref), (big, stages, max_bn)
+        assert torch.equal(sums.view(NSHARD, -1).sum(0), s_ref), (big, stages, max_bn)
+        assert torch.equal(counts(), c_ref), (big, stages, max_bn)
+
+
 def test_bottleneck_takes_big_kernel_naturally_bitexact_vs_oracle():
     """A ResNet-50 configuration (one bottleneck per stage, width 64, 16-bit gradients, 224x224,
     B=17) whose stage-1 GEMMs have >= 200 256-row tiles, so the DEFAULT selection runs them on the
