@@ -223,6 +223,27 @@ typedef struct lbt_dgrad_bna {
 int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
                              lbt_qdesc qw, const lbt_dgrad_bna* bna, float* dx, void* ws, int64_t ws_bytes,
                              void* stream);
+/* The same for the gradient ENTERING a bottleneck block from the next one (ResidualBlock_q.backward
+ * :865-869 + ReLU_q): dx of the next block's conv-1 plus g2 (the next block's other branch),
+ * masked by y_bits (lbt_chain_fwd.ybits of this block's output), optionally stored (gmask_out: the
+ * identity shortcut's gradient), then pass A of each BN it feeds -- bn3, and the projection
+ * shortcut's BN when nbn = 2 -- as lbt_bn_bwd_a_wide_masked(dx, g2, y_bits, gmask_out, ...) per BN.
+ * Fused into the dgrad epilogue on the same conditions as lbt_conv_dgrad_igemm_bna; else through dx.  */
+typedef struct lbt_bna_bn {
+  lbt_qdesc qrg; const int8_t* R; const float* gamma_q;   /* Rescale_q: grad quantiser, X codes, gamma_q */
+  lbt_qdesc qng; const int8_t* qn;                        /* Normalization_q: grad quantiser, X codes    */
+  int16_t* gout; int64_t* sums;                           /* G codes, [LBT_NSHARD][4 Cin] sums          */
+} lbt_bna_bn;
+typedef struct lbt_dgrad_bn3 {
+  const float* g2;        /* [rows][Cin] second summand (required)                 */
+  const uint8_t* y_bits;  /* [rows * Cin / 4] ReLU mask, bit k of byte e/4 = channel quad k */
+  float* gmask_out;       /* optional [rows][Cin]                                   */
+  int32_t nbn, pad;       /* 1 or 2                                                 */
+  lbt_bna_bn bn[2];
+} lbt_dgrad_bn3;
+int lbt_conv_dgrad_igemm_bn3(const int16_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d, lbt_qdesc qg,
+                             lbt_qdesc qw, const lbt_dgrad_bn3* b, float* dx, void* ws, int64_t ws_bytes,
+                             void* stream);
 int lbt_conv_wgrad_igemm(const int8_t* xq, const void* gq, int32_t g_i16, lbt_conv_desc d, int64_t* slab,
                          int32_t nsplit, int32_t nshard, void* stream);
 /* ... storing one partial per pixel split: slab [nsplit][KH*KW*Cin][Cout] is fully WRITTEN (no

@@ -169,6 +169,16 @@ class DgradBna(ctypes.Structure):
                 ("gout", c_void_p), ("sums", c_void_p)]
 
 
+class BnaBn(ctypes.Structure):
+    _fields_ = [("qrg", QDesc), ("R", c_void_p), ("gamma_q", c_void_p), ("qng", QDesc), ("qn", c_void_p),
+                ("gout", c_void_p), ("sums", c_void_p)]
+
+
+class DgradBn3(ctypes.Structure):
+    _fields_ = [("g2", c_void_p), ("y_bits", c_void_p), ("gmask_out", c_void_p), ("nbn", c_int32), ("pad", c_int32),
+                ("bn", BnaBn * 2)]
+
+
 class FSeg(ctypes.Structure):
     _fields_ = [("off", c_int64), ("n", c_int64), ("kind", c_int32), ("qx", QDesc), ("qg", QDesc), ("wd2", c_float)]
 
@@ -197,6 +207,8 @@ _SIGS = {
     "lbt_conv_fwd_igemm_ws": [_P, c_int32, _P, c_int32, _P, ConvDesc, QDesc, QDesc, _P, _P, c_int64, _P],
     "lbt_conv_dgrad_igemm_ws": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int64, _P],
     "lbt_conv_dgrad_igemm_bna": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, ctypes.POINTER(DgradBna), _P, _P, c_int64,
+                                 _P],
+    "lbt_conv_dgrad_igemm_bn3": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, ctypes.POINTER(DgradBn3), _P, _P, c_int64,
                                  _P],
     "lbt_conv_wgrad_igemm_store": [_P, _P, c_int32, ConvDesc, _P, c_int32, _P],
     "lbt_conv_dgrad_chain_i8w4": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P],

@@ -71,8 +71,9 @@ struct IgArgs {
   int nkh, nkw, kh0, kw0, oy, ox, ch, cw, cpy, cpx;
   // dgrad, A16, 256-row kernel only (has_bna): the BN pass A this dx feeds (lbt_dgrad_bna), run in the
   // epilogue instead of storing dx (bna_epilogue)
-  int has_bna;
+  int has_bna;  // 1: bna (mask_r), 2: bn3 (g2 + y_bits, bn3.nbn BNs)
   lbt_dgrad_bna bna;
+  lbt_dgrad_bn3 bn3;
   int dbg;  // igemm_big_kernel diagnostics (LBT_IGEMM_BIG_DBG; 1: no operand loads after the prologue)
 };
 
@@ -649,7 +650,210 @@ LBT_DEV void bna_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4
   }
 }
 
-template <int MODE, bool A16, bool ADD, int BN, int S, bool BNA = false>
+// lbt_dgrad_bn3 in the epilogue: d = dx + g2, masked by y_bits (bn_bwd_a_wide_kernel<true>'s YM form,
+// bn_wide.hip :123-138), optionally stored, then NB BN passes A (bn3, the projection shortcut's BN) on
+// the same d -- each as bna_epilogue's rescale / norm quantisers (no mask_r). The same 4-lane
+// transposes: g2 a float4 per lane row, y_bits one byte per (row, channel quad) riding with R's byte.
+template <int MI, int NJ, int WM, int BN, int NB>
+LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4i (&accw)[NJ], float scale,
+                          int64_t rtile, int rlim, bool full, int n0, int cw, int r, int q, int wm, uint32_t tile,
+                          int8_t* lds) {
+  const lbt_dgrad_bn3& b = p.bn3;
+  const int C = p.ncol;
+  QState srg[NB], sng[NB];
+  int srs[NB], sns[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    srg[k] = qstate(b.bn[k].qrg);
+    sng[k] = qstate(b.bn[k].qng);
+    srs[k] = b.bn[k].qrg.stochastic;
+    sns[k] = b.bn[k].qng.stochastic;
+  }
+  const int jj = r & 3, g4 = r & ~3;
+  const uint32_t hw = (uint32_t)(p.ch * p.cw);
+  uint32_t pixl[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const bool okl = full || i * 16 + jj < rlim;
+    pixl[i] = (uint32_t)(okl ? rtile + i * 16 + jj : 0) % hw;
+  }
+  int ov[NB][4];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) ov[k][0] = ov[k][1] = ov[k][2] = ov[k][3] = 0;
+  int* red = reinterpret_cast<int*>(lds);  // [NB][WM][4][BN]
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = cw + j * 16 + r;
+    float gam[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) gam[k] = b.bn[k].gamma_q[col];
+    const int wsum = accw[j][0];
+    const int cg = cw + j * 16 + g4;
+    int sm[NB][4];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) sm[k][0] = sm[k][1] = sm[k][2] = sm[k][3] = 0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t rowl = rtile + i * 16 + jj;
+      const bool okl = full || i * 16 + jj < rlim;
+      const int64_t off = rowl * C + cg;
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 g2v = z4;
+      uint32_t yb = 0, rw[NB], qw[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) rw[k] = qw[k] = 0;
+      if (okl) {
+        g2v = *reinterpret_cast<const float4*>(b.g2 + off);
+        yb = b.y_bits[off >> 2];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          rw[k] = *reinterpret_cast<const uint32_t*>(b.bn[k].R + off);
+          qw[k] = *reinterpret_cast<const uint32_t*>(b.bn[k].qn + off);
+        }
+      }
+      const uint32_t noff = pixl[i] * (uint32_t)C + cg;
+      float4 n1[NB], n2[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        n1[k] = srs[k] ? *reinterpret_cast<const float4*>(b.bn[k].qrg.noise + noff) : z4;
+        n2[k] = sns[k] ? *reinterpret_cast<const float4*>(b.bn[k].qng.noise + noff) : z4;
+      }
+      int Rv[NB][4], Qv[NB][4], Yv[4] = {0, 0, 0, 0};
+      float u1[NB][4], u2[NB][4], G2v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { Rv[k][e] = Qv[k][e] = 0; u1[k][e] = u2[k][e] = 0.f; }
+      auto pick = [](const float4& v, int sc) { return sc == 0 ? v.x : sc == 1 ? v.y : sc == 2 ? v.z : v.w; };
+      auto tstep = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const int sc = (jj - k) & 3, re = (jj + k) & 3;
+        const uint32_t sh = 8u * (uint32_t)sc;
+        const float gg = quad_from<k>(pick(g2v, sc));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) G2v[e] = re == e ? gg : G2v[e];
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          // R byte, the mask bit (with BN 0), qn byte
+          const int srq = (int)(((rw[t] >> sh) & 0xFFu) | (t == 0 ? ((yb >> sc) & 1u) << 8 : 0u) |
+                                (((qw[t] >> sh) & 0xFFu) << 16));
+          const int grq = quad_from<k>(srq);
+          const float gu1 = quad_from<k>(pick(n1[t], sc)), gu2 = quad_from<k>(pick(n2[t], sc));
+          const int rv = (int)(int8_t)(grq & 0xFF), qv = (int)(int8_t)((grq >> 16) & 0xFF);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            Rv[t][e] = re == e ? rv : Rv[t][e];
+            Qv[t][e] = re == e ? qv : Qv[t][e];
+            u1[t][e] = re == e ? gu1 : u1[t][e];
+            u2[t][e] = re == e ? gu2 : u2[t][e];
+            if (t == 0) Yv[e] = re == e ? (grq >> 8) & 1 : Yv[e];
+          }
+        }
+      };
+      tstep(std::integral_constant<int, 0>{});
+      tstep(std::integral_constant<int, 1>{});
+      tstep(std::integral_constant<int, 2>{});
+      tstep(std::integral_constant<int, 3>{});
+      float dm[4];
+      int cc[NB][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = full || i * 16 + e < rlim;
+        const double hs = (double)acc[0][i][j][e] * 256.0;
+        const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
+        const float v = ok ? (float)(hs + ls) * scale : 0.f;
+        const float g = v + G2v[e];
+        const float d = Yv[e] ? g : 0.f;
+        dm[e] = d;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const int G2 = quant1(srg[t], srs[t], d, u1[t][e], ov[t][0], ov[t][1]);
+          sm[t][0] += G2 * Rv[t][e];
+          sm[t][1] += G2;
+          const float gh = (float)G2 * srg[t].inv_m;
+          const float dd = gh * gam[t];
+          const int G = quant1(sng[t], sns[t], dd, u2[t][e], ov[t][2], ov[t][3]);
+          sm[t][2] += G;
+          sm[t][3] += G * Qv[t][e];
+          cc[t][e] = G;
+        }
+      }
+      if (b.gmask_out) {  // uniform: lane jj stores row jj's 4 masked gradients
+        float4 o = z4;
+        auto fstep = [&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          const int sc = (jj - k) & 3, ce = (jj + k) & 3;
+          const float got = quad_from<k>(sc == 0 ? dm[0] : sc == 1 ? dm[1] : sc == 2 ? dm[2] : dm[3]);
+          o.x = ce == 0 ? got : o.x;
+          o.y = ce == 1 ? got : o.y;
+          o.z = ce == 2 ? got : o.z;
+          o.w = ce == 3 ? got : o.w;
+        };
+        fstep(std::integral_constant<int, 0>{});
+        fstep(std::integral_constant<int, 1>{});
+        fstep(std::integral_constant<int, 2>{});
+        fstep(std::integral_constant<int, 3>{});
+        if (okl) *reinterpret_cast<float4*>(b.gmask_out + off) = o;
+      }
+#pragma unroll
+      for (int t = 0; t < NB; ++t) {
+        uint32_t lo = 0, hi = 0;
+        auto pstep = [&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          const int sc = (jj - k) & 3, ce = (jj + k) & 3;
+          const int got = quad_from<k>(sc == 0 ? cc[t][0] : sc == 1 ? cc[t][1] : sc == 2 ? cc[t][2] : cc[t][3]);
+          const uint32_t h = ((uint32_t)got & 0xFFFFu) << (16 * (ce & 1));
+          lo |= ce < 2 ? h : 0u;
+          hi |= ce < 2 ? 0u : h;
+        };
+        pstep(std::integral_constant<int, 0>{});
+        pstep(std::integral_constant<int, 1>{});
+        pstep(std::integral_constant<int, 2>{});
+        pstep(std::integral_constant<int, 3>{});
+        if (okl) *reinterpret_cast<uint2*>(b.bn[t].gout + off) = make_uint2(lo, hi);
+      }
+    }
+    const int cl = cw - n0 + j * 16 + r;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const int t01 = rows_scatter2(sm[t][0], sm[t][1]), t23 = rows_scatter2(sm[t][2], sm[t][3]);
+      if (q < 2) {
+        red[((t * WM + wm) * 4 + q) * BN + cl] = t01;
+        red[((t * WM + wm) * 4 + 2 + q) * BN + cl] = t23;
+      }
+    }
+  }
+  const int shard = (int)(tile % LBT_NSHARD);
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {
+    const int a0 = wave_sum_i32(ov[t][0]), a1 = wave_sum_i32(ov[t][1]);
+    const int c0 = wave_sum_i32(ov[t][2]), c1 = wave_sum_i32(ov[t][3]);
+    if ((threadIdx.x & 63) == 0) {
+      if (b.bn[t].qrg.counts) {
+        int32_t* ct = b.bn[t].qrg.counts + ((int64_t)b.bn[t].qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+        if (a0) atomicAdd(ct, a0);
+        if (a1) atomicAdd(ct + 1, a1);
+      }
+      if (b.bn[t].qng.counts) {
+        int32_t* ct = b.bn[t].qng.counts + ((int64_t)b.bn[t].qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+        if (c0) atomicAdd(ct, c0);
+        if (c1) atomicAdd(ct + 1, c1);
+      }
+    }
+  }
+  __syncthreads();
+  for (int x = threadIdx.x; x < NB * 4 * BN; x += kBT) {
+    const int t = x / (4 * BN), sidx = (x / BN) & 3, cl = x % BN;
+    long long v = 0;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) v += red[((t * WM + w) * 4 + sidx) * BN + cl];
+    if (v)
+      atomicAdd((unsigned long long*)&b.bn[t].sums[(int64_t)shard * 4 * C + sidx * C + n0 + cl], (unsigned long long)v);
+  }
+}
+
+template <int MODE, bool A16, bool ADD, int BN, int S, int BNA = 0>
 __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel(IgArgs p) {
   constexpr int BM = 256, WN = BN / 64, WM = 8 / WN, TR = BM / WM, MI = TR / 16, NJ = 4;
   constexpr int NA = A16 ? 2 : 1;
@@ -902,8 +1106,11 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
       return;
     }
   }
-  if constexpr (BNA) {
+  if constexpr (BNA == 1) {
     bna_epilogue<MI, NJ, WM, BN>(p, acc, accw, scale, rtile, rlim, full, n0, cw, r, q, wm, tile, lds);
+    return;
+  } else if constexpr (BNA >= 2) {
+    bn3_epilogue<MI, NJ, WM, BN, BNA - 1>(p, acc, accw, scale, rtile, rlim, full, n0, cw, r, q, wm, tile, lds);
     return;
   }
 #pragma unroll
@@ -956,14 +1163,20 @@ void launch_big_bn(IgArgs p, hipStream_t st) {
   } while (0)
   if constexpr (MODE == MODE_DGRAD && A16) {
     if (p.has_bna) {
-      static bool attr_ = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, false, BN, S, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        return true;
-      }();
-      (void)attr_;
-      hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, false, BN, S, true>), dim3((unsigned)tiles), dim3(kBT), shm, st,
-                         p);
+#define LBT_BIG_BNA(E)                                                                                          \
+  do {                                                                                                          \
+    static bool attr_ = [] {                                                                                    \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, false, BN, S, E>),   \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                         \
+      return true;                                                                                              \
+    }();                                                                                                        \
+    (void)attr_;                                                                                                \
+    hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, false, BN, S, E>), dim3((unsigned)tiles), dim3(kBT), shm, st, p); \
+  } while (0)
+      if (p.has_bna == 1) LBT_BIG_BNA(1);
+      else if (p.bn3.nbn == 1) LBT_BIG_BNA(2);
+      else LBT_BIG_BNA(3);
+#undef LBT_BIG_BNA
       return;
     }
   }
@@ -1308,6 +1521,44 @@ extern "C" int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int
   if (rc) return rc;
   return lbt_bn_bwd_a_wide_masked(dx, nullptr, nullptr, nullptr, 1, b.qr, b.gb, nullptr, b.qrg, b.R, b.qng, b.qn,
                                   b.gout, nullptr, b.sums, rows, inner, d.Cin, stream);
+}
+
+extern "C" int lbt_conv_dgrad_igemm_bn3(const int16_t* gq, const int8_t* wd, int32_t ksd, lbt_conv_desc d,
+                                        lbt_qdesc qg, lbt_qdesc qw, const lbt_dgrad_bn3* bn3, float* dx, void* ws,
+                                        int64_t ws_bytes, void* stream) {
+  if (!bn3 || !dx || !desc_ok(d)) return LBT_EINVAL;
+  const lbt_dgrad_bn3& b = *bn3;
+  if (!b.g2 || !b.y_bits || b.nbn < 1 || b.nbn > 2 || d.Cin % 4) return LBT_EINVAL;
+  bool tables = true;
+  for (int k = 0; k < b.nbn; ++k) {
+    const lbt_bna_bn& n = b.bn[k];
+    if (!n.R || !n.gamma_q || !n.qn || !n.gout || !n.sums) return LBT_EINVAL;
+    if (n.qrg.bits <= 0 || n.qrg.bits > 16 || n.qng.bits <= 0 || n.qng.bits > 16) return LBT_EINVAL;
+    tables = tables && (!n.qrg.stochastic || n.qrg.noise) && (!n.qng.stochastic || n.qng.noise);
+  }
+  const int64_t rows = (int64_t)d.N * d.H * d.W, inner = (int64_t)d.H * d.W * d.Cin;
+  hipStream_t st = (hipStream_t)stream;
+  static const int fuse = getenv_int("LBT_DGRAD_BN3", 1);
+  if (fuse && tables && d.SH == 1 && d.SW == 1 && d.Cout % kBK == 0 && d.Cin % 64 == 0 &&
+      (int64_t)d.KH * d.KW * d.Cout * 255 * 128 < ((int64_t)1 << 31) &&
+      (int64_t)d.N * d.Ho * d.Wo * d.Cout < ((int64_t)1 << 31) && (int64_t)ksd * 16 * d.Cin < ((int64_t)1 << 31) &&
+      ksd * 16 >= d.KH * d.KW * d.Cout && rows * d.Cin < ((int64_t)1 << 31) && lbt_igemm_workspace_bytes(d, 1, 1) == 0) {
+    IgArgs p{};
+    p.a = gq; p.b = wd; p.ks = ksd; p.cred = d.Cout; p.a_u8off = 0; p.d = d; p.qa = qg; p.qb = qw;
+    p.colsum = nullptr; p.y = nullptr; p.add_src = nullptr; p.M = rows; p.ncol = d.Cin;
+    p.ksplit = 1;
+    all_taps(p, MODE_DGRAD);
+    p.has_bna = 2;
+    p.bn3 = b;
+    if (launch_big<MODE_DGRAD, true>(p, st)) return (int)hipGetLastError();
+  }
+  int rc = lbt_conv_dgrad_igemm_ws(gq, 1, wd, ksd, d, qg, qw, dx, nullptr, ws, ws_bytes, stream);
+  for (int k = 0; k < b.nbn && !rc; ++k) {
+    const lbt_bna_bn& n = b.bn[k];
+    rc = lbt_bn_bwd_a_wide_masked(dx, b.g2, nullptr, b.y_bits, 0, lbt_qdesc{}, n.gamma_q, k == 0 ? b.gmask_out : nullptr,
+                                  n.qrg, n.R, n.qng, n.qn, n.gout, nullptr, n.sums, rows, inner, d.Cin, stream);
+  }
+  return rc;
 }
 
 namespace {

@@ -71,6 +71,18 @@ SIDE_STREAM = os.environ.get("LBT_SIDE_STREAM", "1") != "0"
 # LBT_DGRAD_BNA_PY=0: the separate dgrad + pass A launches (A/B, and the C-side LBT_DGRAD_BNA=0 keeps
 # the entry point but never fuses)
 DGRAD_BNA = os.environ.get("LBT_DGRAD_BNA_PY", "1") != "0"
+# ... and bn3 (+ the projection shortcut's BN) pass A inside the NEXT block's conv-1 dgrad
+# (ops.conv_dgrad_igemm_bn3): the next block hands back _DgradIn instead of its conv-1 dx
+DGRAD_BN3 = os.environ.get("LBT_DGRAD_BN3_PY", "1") != "0"
+
+
+class _DgradIn:
+    """A fused bottleneck's input gradient, not yet formed: conv's dgrad of the int16 codes gq (its
+    conv-1) plus `other` (its shortcut branch's gradient). The previous fused block evaluates it with
+    its own entry pass A in the dgrad's epilogue (ResidualBottleneck_q._entry_from_dgrad)."""
+
+    def __init__(self, conv, gq, other):
+        self.conv, self.gq, self.other = conv, gq, other
 _SIDE = {}
 _PENDING = {}
 _DEPTH = [0]
@@ -1248,20 +1260,60 @@ class ResidualBottleneck_q(ResidualBlock_q):
         c1, bn1, c2, bn2, c3, bn3 = r[0], r[1], r[3], r[4], r[6], r[7]
         sc = self.shortcut.layers
         ctx = c1.ctx
-        gin, gin2 = grad if isinstance(grad, tuple) else (grad, None)
-        dev = gin.device
-        # block ReLU mask from the block output; bn3 (and the shortcut bn) see the same masked g
-        gmask = None if sc else self._c.get("gmask", gin.shape, torch.float32, dev)
-        ym = dict(y_bits=self.ybits) if self.ybits is not None else dict(y_mask=self.y)
-        g3 = self._bn_bwd(bn3, c3, gin, ctx, gmask_out=gmask, g2=gin2, **ym)
-        gs = self._bn_bwd(sc[1], sc[0], gin, ctx, g2=gin2, **ym) if sc else None
+        if isinstance(grad, _DgradIn):
+            g3, gs, gmask = self._entry_from_dgrad(grad, ctx)
+        else:
+            gin, gin2 = grad if isinstance(grad, tuple) else (grad, None)
+            dev = gin.device
+            # block ReLU mask from the block output; bn3 (and the shortcut bn) see the same masked g
+            gmask = None if sc else self._c.get("gmask", gin.shape, torch.float32, dev)
+            ym = dict(y_bits=self.ybits) if self.ybits is not None else dict(y_mask=self.y)
+            g3 = self._bn_bwd(bn3, c3, gin, ctx, gmask_out=gmask, g2=gin2, **ym)
+            gs = self._bn_bwd(sc[1], sc[0], gin, ctx, g2=gin2, **ym) if sc else None
         g2 = self._dgrad_bn_bwd(c3, g3, bn2, c2, ctx)
         g1 = self._dgrad_bn_bwd(c2, g2, bn1, c1, ctx)
         other = sc[0].bwd_codes16(gs) if sc else gmask
         pb = self.prev_block
         if pb is not None and pb._fusable():
+            if DGRAD_BN3 and pb.ybits is not None:
+                return _DgradIn(c1, g1, other)
             return (c1.bwd_codes16(g1), other)
         return c1.bwd_codes16(g1, add_src=other)
+
+    def _entry_from_dgrad(self, din, ctx):
+        """This block's entry passes A (ReLU mask y_bits on dx + other; bn3, and the projection
+        shortcut's BN) in the epilogue of the next block's conv-1 dgrad (ops.conv_dgrad_igemm_bn3), then
+        each BN's pass B: returns (conv-3's gradient codes, the shortcut conv's or None, gmask)."""
+        r = self.residual.layers
+        c3, bn3 = r[6], r[7]
+        sc = self.shortcut.layers
+        conv = din.conv
+        conv.gradq = din.gq
+        with backward_scope():
+            with side_work():  # dW of the next block's conv-1: read only by the optimizer
+                conv._wgrad_igemm(1)
+            d = conv.d
+            C = d.Cin
+            shape = (d.N, d.H, d.W, C)
+            numel = d.N * d.H * d.W * C
+            rows, inner = numel // C, numel // d.N
+            dev = din.gq.device
+            gmask = None if sc else self._c.get("gmask", shape, torch.float32, dev)
+            pairs = [(bn3, c3)] + ([(sc[1], sc[0])] if sc else [])
+            bns = []
+            for bn, _ in pairs:
+                n, rs = bn.layers
+                sums = rs._c.sums("fsums", ops.NSHARD * 4 * C, ctx)
+                rs.grad_range.observe(numel)
+                n.grad_range.observe(numel)
+                G16 = n._c.get("G16", shape, torch.int16, dev)
+                bns.append((rs.R, rs.gb, rs.grad_range, n.grad_range, n.q, G16, sums))
+            dx = conv._c.get("dx", shape, torch.float32, dev)  # used only when the dgrad cannot fuse
+            ops.conv_dgrad_igemm_bn3(din.gq, conv.wd, conv.ksd, d, conv.grad_range.desc, conv.W_range.desc, din.other,
+                                     self.ybits, gmask, bns, dx, conv._ws(d, 1, True))
+            gq = [self._bn_bwd_b(bn, conv_out, b[5], b[6], numel, rows, inner, C)
+                  for (bn, conv_out), b in zip(pairs, bns)]
+        return gq[0], (gq[1] if sc else None), gmask
 
 
 class MaxPool_q(Layer_q):

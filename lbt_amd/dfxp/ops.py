@@ -675,6 +675,24 @@ def conv_dgrad_igemm_bna(gq16, wd, ksd, d, qg, qw, qr, R, gb, qrg, qng, qn, gout
              0 if ws is None else ws.numel() * ws.element_size(), stream())
 
 
+def conv_dgrad_igemm_bn3(gq16, wd, ksd, d, qg, qw, g2, y_bits, gmask_out, bns, dx, ws):
+    """16-bit-gradient dgrad whose dx, plus g2 and masked by y_bits, is the gradient entering a
+    bottleneck block (lbt_conv_dgrad_igemm_bn3): the masked sum optionally out (gmask_out), then pass A
+    of each BN in `bns` -- tuples (R, gamma_q, qrg, qng, qn, gout, sums), qrg / qng Quantizer objects --
+    in the 256-row GEMM's epilogue when that kernel takes the GEMM, else through dx (scratch)."""
+    inner = d.H * d.W * d.Cin
+    b = _lib.DgradBn3()
+    b.g2, b.y_bits, b.gmask_out, b.nbn = ptr(g2), ptr(y_bits), ptr(gmask_out), len(bns)
+    for k, (R, gamma_q, qrg, qng, qn, gout, sums) in enumerate(bns):
+        dr, dn = [q.ctx.noise_table_desc(q, inner) if (NOISE_TABLES and q.stochastic) else q.desc for q in (qrg, qng)]
+        b.bn[k] = _lib.BnaBn(dr, ptr(R), ptr(gamma_q), dn, ptr(qn), ptr(gout), ptr(sums))
+    n = d.N * inner
+    nb = gq16.numel() * 2 + wd.numel() + n * (4 + 0.25 + (4 if gmask_out is not None else 0) + 4 * len(bns))
+    with _Timed("igemm_kernel<dgrad+bn3_a>", int(nb)):
+        call("lbt_conv_dgrad_igemm_bn3", ptr(gq16), ptr(wd), int(ksd), d, qg, qw, ctypes.byref(b), ptr(dx), ptr(ws),
+             0 if ws is None else ws.numel() * ws.element_size(), stream())
+
+
 def conv_fwd_igemm_q(xq, a_kind, wf, ksf, d, qx, qw, yq, qout, chsum):
     """Wide fwd + the Normalization_q input quantiser in its epilogue (int8 codes, sums, counters).
     A stochastic qout reads its noise from the context's per-step table (one Philox call per 4 noise

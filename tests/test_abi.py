@@ -53,7 +53,7 @@ STRUCTS = {"lbt_qdesc": _lib.QDesc, "lbt_conv_desc": _lib.ConvDesc, "lbt_bn_norm
            "lbt_wgrad_job": _lib.WgradJob, "lbt_conv_bwd": _lib.ConvBwd,
            "lbt_conv_fwd": _lib.ConvFwd, "lbt_conv_fwd_job": _lib.ConvFwdJob,
            "lbt_igemm_tuning": _lib.IgemmTuning, "lbt_update": _lib.Update,
-           "lbt_dgrad_bna": _lib.DgradBna}
+           "lbt_dgrad_bna": _lib.DgradBna, "lbt_bna_bn": _lib.BnaBn, "lbt_dgrad_bn3": _lib.DgradBn3}
 
 
 def test_struct_layouts_match_c():

@@ -211,6 +211,77 @@ def test_big_dgrad_bna_matches_dgrad_then_pass_a(N, H, Cin, Cout, k, stochastic)
         assert torch.equal(counts(), c_ref), (big, stages, max_bn)
 
 
+@pytest.mark.parametrize("N,H,Cin,Cout", [
+    (3, 14, 256, 64),    # the next block's conv-1 (1x1, K = 64) into this block's 256-channel output, M = 588
+    (2, 9, 128, 128),    # K = 128, ncol = 128, M = 162 (one partial tile)
+])
+@pytest.mark.parametrize("nbn,gmask", [(1, True), (2, False), (2, True)])
+@pytest.mark.parametrize("stochastic", [True, False])
+def test_big_dgrad_bn3_matches_dgrad_then_pass_a(N, H, Cin, Cout, nbn, gmask, stochastic):
+    """lbt_conv_dgrad_igemm_bn3 (a bottleneck's entry: dx + g2, ReLU mask y_bits, the masked gradient
+    optionally out, then pass A of bn3 and of the projection shortcut's BN in the dgrad16 epilogue) ==
+    lbt_conv_dgrad_igemm_ws -> lbt_bn_bwd_a_wide_masked(g2, y_bits) per BN: the same G codes, masked
+    gradient, channel sums and counters, on every ring depth / column tile and through the fallback
+    (reference ResidualBlock_q.backward :865-869, ReLU_q, Rescale_q :686-691, Normalization_q :620-623)."""
+    from lbt_amd._lib import NSHARD
+    from lbt_amd.dfxp import ops
+    rng, ctx, (_, qw, qg), d, _, _, (wd, ksd), _ = _setup(N, H, Cin, Cout, 1, 1,
+                                                          N * H + Cin + nbn + 2 * int(gmask) + 4 * int(stochastic))
+    g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, H, H, Cout)).astype(np.int16)).to(DEV)
+    shape = (N, H, H, Cin)
+    dx = torch.empty(shape, device=DEV)
+    ops.conv_dgrad_igemm(g, 1, wd, ksd, d, qg.desc, qw.desc, dx)
+    g2 = torch.from_numpy(rng.normal(size=shape).astype(np.float32)).to(DEV) * dx.abs().mean()
+    ybits = torch.from_numpy(rng.integers(0, 16, size=N * H * H * Cin // 4).astype(np.uint8)).to(DEV)
+    top = int(np.ceil(np.log2(float((dx + g2).abs().max())))) - 1
+    rows, inner = N * H * H, H * H * Cin
+    bns = []
+    for k in range(nbn):
+        qrg = ctx.quantizer("t/rg%d" % k, 16, top - k, stochastic=stochastic)
+        qng = ctx.quantizer("t/ng%d" % k, 16, top - k, stochastic=stochastic)
+        R = torch.from_numpy(rng.integers(-128, 128, size=shape).astype(np.int8)).to(DEV)
+        qn = torch.from_numpy(rng.integers(-128, 128, size=shape).astype(np.int8)).to(DEV)
+        gam = torch.from_numpy(rng.uniform(-2, 2, 2 * Cin).astype(np.float32)).to(DEV)
+        bns.append((R, gam, qrg, qng, qn))
+
+    def counts():
+        v = ctx.counts_view()
+        return torch.stack([v[q.slot].sum(0) for b in bns for q in b[2:4]]).cpu()
+
+    ctx.counts.zero_()
+    ref_G, ref_s = [], []
+    ref_m = torch.empty(shape, device=DEV) if gmask else None
+    for k, (R, gam, qrg, qng, qn) in enumerate(bns):
+        G = torch.empty(shape, dtype=torch.int16, device=DEV)
+        sm = torch.zeros(NSHARD * 4 * Cin, dtype=torch.int64, device=DEV)
+        ops.bn_bwd_a_wide_masked(dx, None, False, qrg.desc, gam, ref_m if k == 0 else None, qrg.desc, R, qng.desc, qn,
+                                 G, sm, rows, inner, Cin, g2=g2, y_bits=ybits)
+        ref_G.append(G)
+        ref_s.append(sm.view(NSHARD, -1).sum(0))
+    c_ref = counts()
+    assert (c_ref > 0).all(), c_ref
+    variants = [(1, st, mb) for st, mb in VARIANTS if mb <= 128] + [(0, 2, 128)]
+    for big, stages, max_bn in variants:
+        ctx.counts.zero_()
+        outs = [(torch.full(shape, 12345, dtype=torch.int16, device=DEV),
+                 torch.zeros(NSHARD * 4 * Cin, dtype=torch.int64, device=DEV)) for _ in bns]
+        m = torch.full(shape, float("nan"), device=DEV) if gmask else None
+        scratch = torch.full(shape, float("nan"), device=DEV)
+        n0 = _launches()
+        with ops.igemm_forced(big=big, min_tiles=1, stages=stages, max_bn=max_bn):
+            ops.conv_dgrad_igemm_bn3(g, wd, ksd, d, qg.desc, qw.desc, g2, ybits, m,
+                                     [b[:2] + b[2:4] + (b[4],) + o for b, o in zip(bns, outs)], scratch, None)
+        assert _launches() == n0 + big, "the 256-row kernel did not run"
+        if big:
+            assert torch.isnan(scratch).all(), "the fused path must not store dx"
+        for k in range(nbn):
+            assert torch.equal(outs[k][0], ref_G[k]), (k, big, stages, max_bn)
+            assert torch.equal(outs[k][1].view(NSHARD, -1).sum(0), ref_s[k]), (k, big, stages, max_bn)
+        if gmask:
+            assert torch.equal(m, ref_m), (big, stages, max_bn)
+        assert torch.equal(counts(), c_ref), (big, stages, max_bn)
+
+
 def test_bottleneck_takes_big_kernel_naturally_bitexact_vs_oracle():
     """A ResNet-50 configuration (one bottleneck per stage, width 64, 16-bit gradients, 224x224,
     B=17) whose stage-1 GEMMs have >= 200 256-row tiles, so the DEFAULT selection runs them on the
