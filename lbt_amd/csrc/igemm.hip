@@ -500,7 +500,7 @@ LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 // 170.6 -> 155.6 us, the other shapes unchanged (profiles/r04l_ab probe_*.txt); A8 BN 128 at 3-4 stages
 // would spill 200+ bytes.
 #ifndef LBT_BIG_OCC
-#define LBT_BIG_OCC(A16, BN, S) ((A16 && BN == 64) ? 4 : 1)
+#define LBT_BIG_OCC(A16, BN, S, HALO) ((A16 && BN == 64 && !HALO) ? 4 : 1)
 #endif
 // bn_bwd_a_wide_kernel's mask_r pass (bn_wide.hip) on the dgrad accumulators, element for element:
 // dx (the value the plain epilogue stores) -> ReLU mask from R -> G2 = Q_rg -> gamma-scaled rescale
@@ -853,8 +853,15 @@ LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4
   }
 }
 
-template <int MODE, bool A16, bool ADD, int BN, int S, int BNA = 0>
-__global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel(IgArgs p) {
+// HALO (3x3, stride 1, pad 1: fwd, and the unit-stride dgrad of such a conv): the k loop runs
+// channel-block-major, and per channel block ONE window of A is staged -- the tile's 256 pixels plus
+// W + 1 on either side in the same row-major pixel order, 256 + 2W + 2 <= 384 rows -- instead of one
+// 256-row A block per tap: the 9 taps read the window shifted by dy * W + dx (invalid taps -- outside
+// the image -- read the fill value in registers). A leaves L2 ~1.4x instead of 9x per channel block.
+// Window: two buffers, the next block's window DMA'd one instruction per wave per tap step while the
+// current block's 9 taps run; B: a 3-stage ring, two taps ahead.
+template <int MODE, bool A16, bool ADD, int BN, int S, int BNA = 0, bool HALO = false>
+__global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO)) void igemm_big_kernel(IgArgs p) {
   constexpr int BM = 256, WN = BN / 64, WM = 8 / WN, TR = BM / WM, MI = TR / 16, NJ = 4;
   constexpr int NA = A16 ? 2 : 1;
   constexpr int ROWB = A16 ? 128 : 64;                 // bytes of one A row per k-block
@@ -1023,6 +1030,113 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
     }
   };
 
+  if constexpr (HALO) {
+    constexpr int GW = A16 ? 6 : 3;        // window DMA instructions per wave: 8 * GW * RPI = 384 rows
+    constexpr int NWR = 8 * GW * RPI, WINB = NWR * ROWB, BST = BN * 64;
+    constexpr int GBI = NIB >= 8 ? NIB / 8 : 1;  // B instructions per issuing wave per tap
+    int8_t* win = lds;                     // [2][NWR][ROWB]
+    int8_t* bring = lds + 2 * WINB;        // [3][BN][64]
+    const int Wd = OW, Hd = OH;
+    const int nwin = 256 + 2 * Wd + 2;     // window rows that can be read
+    const int64_t wbase = m0 - (Wd + 1);
+    uint32_t soff[GW];
+    bool sv[GW];
+#pragma unroll
+    for (int g = 0; g < GW; ++g) {
+      const int wr = (wave + 8 * g) * RPI + lane / SPR;
+      const int64_t px = wbase + wr;
+      sv[g] = wr < nwin && px >= 0 && px < p.M;
+      const int ps = lane % SPR;
+      const int sg = A16 ? (ps ^ swz128(wr)) : (ps ^ swz64(wr));
+      soff[g] = sv[g] ? (uint32_t)px * (uint32_t)p.cred * (A16 ? 2u : 1u) + (uint32_t)sg * 16u : 0u;
+    }
+    auto issue_win = [&](int cb, int buf, int g) {
+      const int8_t* src = sv[g] ? reinterpret_cast<const int8_t*>(p.a) + soff[g] + (uint32_t)cb * (A16 ? 128u : 64u)
+                                : fill;
+      __builtin_amdgcn_global_load_lds(src, (lds_vptr)(win + buf * WINB + (wave + 8 * g) * 1024), 16, 0, 0);
+    };
+    auto issue_b = [&](int k, int st) {
+      const int cb = k / 9, tp = k - cb * 9;
+      const int kbw = tp * cblocks + cb;  // (kh * 3 + kw) * cblocks + cb
+      if (bact) {
+#pragma unroll
+        for (int g = 0; g < GB; ++g) {
+          const int8_t* src = p.b + ((uint32_t)(bcolx[g] * p.ks + kbw * 4 + bseg[g]) << 4);
+          __builtin_amdgcn_global_load_lds(src, (lds_vptr)(bring + st * BST + (wave + 8 * g) * 1024), 16, 0, 0);
+        }
+      }
+    };
+    // this lane's fragment rows: pixel (x, y) within its image, and whether the row exists
+    int fx[MI], fy[MI];
+    bool fok[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * TR + i * 16 + r;
+      fok[i] = m < p.M;
+      const uint32_t mu = (uint32_t)(fok[i] ? m : 0);
+      fx[i] = (int)(mu % (uint32_t)Wd);
+      fy[i] = (int)((mu / (uint32_t)Wd) % (uint32_t)Hd);
+    }
+    const int afill = (!A16 && p.a_u8off) ? (int)0x80808080u : 0;
+#pragma unroll
+    for (int g = 0; g < GW; ++g) issue_win(0, 0, g);
+    issue_b(0, 0);
+    issue_b(nk > 1 ? 1 : 0, 1);
+    for (int cb = 0; cb < cblocks; ++cb) {
+      const bool more = cb + 1 < cblocks;
+      const int8_t* wsb = win + (cb & 1) * WINB;
+      auto tap_step = [&](auto tc) {
+        constexpr int tp = decltype(tc)::value;
+        constexpr int th = tp / 3, tw = tp % 3;
+        constexpr int dy = MODE == MODE_FWD ? th - 1 : 1 - th, dx = MODE == MODE_FWD ? tw - 1 : 1 - tw;
+        // B(k) landed: younger are B(k + 1) and the window pieces of steps k - 2, k - 1
+        constexpr int P = (tp >= 2 && tp - 2 < GW ? 1 : 0) + (tp >= 1 && tp - 1 < GW ? 1 : 0);
+        if (bact) {
+          if (more) vm_wait<GBI + P>(); else vm_wait<GBI>();
+        } else {
+          if (more) vm_wait<P>(); else vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        const int k = cb * 9 + tp;
+        issue_b(k + 2 < nk ? k + 2 : nk - 1, (tp + 2) % 3);
+        if (tp < GW && more) issue_win(cb + 1, (cb + 1) & 1, tp);
+        FragA fa;
+        FragB fb;
+        const int8_t* bsb = bring + (tp % 3) * BST;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int col = wn * 64 + j * 16 + r;
+          fb[j] = *reinterpret_cast<const v4i*>(bsb + col * 64 + ((q ^ swz64(col)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int wr = wm * TR + i * 16 + r + (dy + 1) * Wd + dx + 1;
+          const bool v = fok[i] && (unsigned)(fx[i] + dx) < (unsigned)Wd && (unsigned)(fy[i] + dy) < (unsigned)Hd;
+          if constexpr (A16) {
+            const int f = swz128(wr);
+            const v4i c0 = *reinterpret_cast<const v4i*>(wsb + wr * 128 + (((2 * q) ^ f) << 4));
+            const v4i c1 = *reinterpret_cast<const v4i*>(wsb + wr * 128 + (((2 * q + 1) ^ f) << 4));
+            const v4i z = v4i{0, 0, 0, 0};
+            fa[i][0] = v ? c0 : z;
+            fa[i][NA - 1] = v ? c1 : z;
+          } else {
+            const v4i c0 = *reinterpret_cast<const v4i*>(wsb + wr * 64 + ((q ^ swz64(wr)) << 4));
+            fa[i][0] = v ? c0 : v4i{afill, afill, afill, afill};
+          }
+        }
+        mma(fa, fb);
+      };
+      tap_step(std::integral_constant<int, 0>{});
+      tap_step(std::integral_constant<int, 1>{});
+      tap_step(std::integral_constant<int, 2>{});
+      tap_step(std::integral_constant<int, 3>{});
+      tap_step(std::integral_constant<int, 4>{});
+      tap_step(std::integral_constant<int, 5>{});
+      tap_step(std::integral_constant<int, 6>{});
+      tap_step(std::integral_constant<int, 7>{});
+      tap_step(std::integral_constant<int, 8>{});
+    }
+  } else {
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) issue(s < nk ? s : nk - 1, s);
   if constexpr (S >= 3) {
@@ -1068,6 +1182,7 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
       read_frags(kb % S, fa, fb);
       mma(fa, fb);
     }
+  }
   }
   vm_wait<0>();  // the ring's trailing (clamped) DMAs: nothing may still write LDS when the block ends
   if (wmfma) {  // the column totals: lanes r, r + 16, r + 32, r + 48 hold a quarter of column r's k each
@@ -1143,45 +1258,34 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S)) void igemm_big_kernel
   }
 }
 
-template <int MODE, bool A16, int BN, int S>
+// one igemm_big_kernel instantiation: dynamic LDS = the S-stage ring, or (HALO) two A windows of 384
+// rows + a 3-stage B ring
+template <int MODE, bool A16, bool ADD, int BN, int S, int BNA, bool HALO>
+void big_go(const IgArgs& p, int64_t tiles, hipStream_t st) {
+  constexpr int BM = 256, ROWB = A16 ? 128 : 64;
+  constexpr size_t shm = HALO ? (size_t)2 * 384 * ROWB + (size_t)3 * BN * 64 : (size_t)S * (BM * ROWB + BN * 64);
+  static bool attr_ = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, ADD, BN, S, BNA, HALO>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    return true;
+  }();
+  (void)attr_;
+  hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, ADD, BN, S, BNA, HALO>), dim3((unsigned)tiles), dim3(kBT), shm, st,
+                     p);
+}
+
+template <int MODE, bool A16, int BN, int S, bool HALO = false>
 void launch_big_bn(IgArgs p, hipStream_t st) {
   static const int dbg = getenv_int("LBT_IGEMM_BIG_DBG", 0);
   p.dbg = dbg;
   const int64_t tiles = ((p.M + 255) / 256) * (p.ncol / BN);
-  constexpr int BM = 256, ROWB = A16 ? 128 : 64;
-  constexpr size_t shm = (size_t)S * (BM * ROWB + BN * 64);
-  const bool add = MODE == MODE_DGRAD && p.add_src;
-#define LBT_BIG(ADD_)                                                                                     \
-  do {                                                                                                    \
-    static bool attr_ = [] {                                                                              \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, ADD_, BN, S>), \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                   \
-      return true;                                                                                        \
-    }();                                                                                                  \
-    (void)attr_;                                                                                          \
-    hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, ADD_, BN, S>), dim3((unsigned)tiles), dim3(kBT), shm, st, p); \
-  } while (0)
   if constexpr (MODE == MODE_DGRAD && A16) {
-    if (p.has_bna) {
-#define LBT_BIG_BNA(E)                                                                                          \
-  do {                                                                                                          \
-    static bool attr_ = [] {                                                                                    \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, false, BN, S, E>),   \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);                         \
-      return true;                                                                                              \
-    }();                                                                                                        \
-    (void)attr_;                                                                                                \
-    hipLaunchKernelGGL((igemm_big_kernel<MODE, A16, false, BN, S, E>), dim3((unsigned)tiles), dim3(kBT), shm, st, p); \
-  } while (0)
-      if (p.has_bna == 1) LBT_BIG_BNA(1);
-      else if (p.bn3.nbn == 1) LBT_BIG_BNA(2);
-      else LBT_BIG_BNA(3);
-#undef LBT_BIG_BNA
-      return;
-    }
+    if (p.has_bna == 1) return big_go<MODE, A16, false, BN, S, 1, HALO>(p, tiles, st);
+    if (p.has_bna == 2 && p.bn3.nbn == 1) return big_go<MODE, A16, false, BN, S, 2, HALO>(p, tiles, st);
+    if (p.has_bna == 2) return big_go<MODE, A16, false, BN, S, 3, HALO>(p, tiles, st);
   }
-  if (add) LBT_BIG(true); else LBT_BIG(false);
-#undef LBT_BIG
+  if (MODE == MODE_DGRAD && p.add_src) big_go<MODE, A16, MODE == MODE_DGRAD, BN, S, 0, HALO>(p, tiles, st);
+  else big_go<MODE, A16, false, BN, S, 0, HALO>(p, tiles, st);
 }
 
 // Selection of the 256-row LDS-DMA kernel (lbt_igemm_tuning, include/lbt_dfxp.h): read per call,
@@ -1195,6 +1299,8 @@ lbt_igemm_tuning& big_tuning() {
     v.min_tiles = getenv_int("LBT_IGEMM_BIG_MIN", 200);
     v.stages = getenv_int("LBT_IGEMM_BIG_S", 2);
     v.max_bn = getenv_int("LBT_IGEMM_BIG_BN256", 0) ? 256 : 128;
+    v.halo = getenv_int("LBT_IGEMM_HALO", 1);
+    v.pad = 0;
     v.launches = 0;
     return v;
   }();
@@ -1222,7 +1328,20 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
   // (72-96 KiB, one; the software-pipelined loop), except 3x3 dgrad16 at 28x28 / 14x14 (3-5 %).
   // A16 runs 3 stages for any request above 2 (4 stages of 128-byte A rows at BN 128 would take 160 KiB).
   const int S = tu.stages;
-  if (bn == 256) {
+  // 3x3 / stride 1 / pad 1 with every tap (fwd, unit-stride dgrad) and W <= 63: the A window per
+  // channel block (HALO), 64- and 128-column tiles
+  const lbt_conv_desc& d = p.d;
+  const bool halo = tu.halo && bn <= 128 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
+                    d.PL == 1 && d.Ho == d.H && d.Wo == d.W && p.nkh == 3 && p.nkw == 3 && p.kh0 == 0 &&
+                    p.kw0 == 0 && p.cw == d.W && p.ch == d.H && d.W <= 63;
+  if (halo) {  // 16-bit codes: 64-column tiles (one workgroup per CU: the two 48 KiB windows)
+    if constexpr (A16) {
+      launch_big_bn<MODE, A16, 64, 2, true>(p, st);
+    } else {
+      if (bn == 128) launch_big_bn<MODE, A16, 128, 2, true>(p, st);
+      else launch_big_bn<MODE, A16, 64, 2, true>(p, st);
+    }
+  } else if (bn == 256) {
     if constexpr (!A16) launch_big_bn<MODE, A16, 256, 4>(p, st);
   } else if (bn == 128) {
     if (S <= 2) launch_big_bn<MODE, A16, 128, 2>(p, st);
@@ -1426,6 +1545,7 @@ extern "C" int lbt_igemm_set_tuning(const lbt_igemm_tuning* t) {
     return LBT_EINVAL;
   lbt_igemm_tuning& cur = big_tuning();
   cur.big = t->big; cur.min_tiles = t->min_tiles; cur.stages = t->stages; cur.max_bn = t->max_bn;
+  cur.halo = t->halo;
   return 0;
 }
 

@@ -80,15 +80,15 @@ def test_big_fwd_matches_generic(N, H, Cin, Cout, k, s, a_kind):
         xg, signed9 = (x.to(torch.int16) + 128, True) if a_kind == 1 else (x, False)
     ref = torch.empty((N, d.Ho, d.Wo, Cout), device=DEV)
     ops.conv_fwd_generic(xg, signed9, w_hwio, d, qx.desc, qw.desc, ref)
-    for stages, max_bn in VARIANTS:
+    for (stages, max_bn), halo in [(v, h) for v in VARIANTS for h in (0, 1)]:
         for cs in ((None, colsum) if a_kind == 1 else (None,)):
             y = torch.full_like(ref, float("nan"))
             n0 = _launches()
-            with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn):
+            with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo):
                 _lib.call("lbt_conv_fwd_igemm", _lib.ptr(x), a_kind, _lib.ptr(wf), ksf, _lib.ptr(cs), d, qx.desc,
                           qw.desc, _lib.ptr(y), _lib.stream())
             assert _launches() == n0 + 1, "the 256-row kernel did not run"
-            assert torch.equal(y, ref), (stages, max_bn, cs is not None)
+            assert torch.equal(y, ref), (stages, max_bn, halo, cs is not None)
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k", [
@@ -112,13 +112,13 @@ def test_big_dgrad_matches_generic(N, H, Cin, Cout, k, g_i16, add):
     (ops.conv_dgrad_generic16 if g_i16 else ops.conv_dgrad_generic)(g, w_hwio, d, qg.desc, qw.desc, ref)
     if add:
         ref = ref + addend
-    for stages, max_bn in VARIANTS:
+    for (stages, max_bn), halo in [(v, h) for v in VARIANTS for h in (0, 1)]:
         dx = torch.full_like(ref, float("nan"))
         n0 = _launches()
-        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn):
+        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo):
             ops.conv_dgrad_igemm(g, g_i16, wd, ksd, d, qg.desc, qw.desc, dx, add_src=addend)
         assert _launches() == n0 + 1, "the 256-row kernel did not run"
-        assert torch.equal(dx, ref), (stages, max_bn)
+        assert torch.equal(dx, ref), (stages, max_bn, halo)
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k", [(3, 14, 64, 128, 3), (2, 15, 128, 64, 1)])
@@ -141,17 +141,18 @@ def test_big_quantising_epilogue_matches_fwd_then_quantize(N, H, Cin, Cout, k, a
     q_ref = ops.quantize(y, qo, OUT_I8, chsum=cs_ref, C=Cout)
     cnt_ref = ctx.counts_view()[qo.slot].sum(0).cpu()
     assert cnt_ref[0] > 0 and cnt_ref[1] > cnt_ref[0]
-    for stages, max_bn in VARIANTS[:-1]:  # the quantising epilogue never takes the 256-column tile
+    # the quantising epilogue never takes the 256-column tile
+    for (stages, max_bn), halo in [(v, h) for v in VARIANTS[:-1] for h in (0, 1)]:
         ctx.counts.zero_()
         cs = torch.zeros_like(cs_ref)
         yq = torch.full(q_ref.shape, 99, dtype=torch.int8, device=DEV)
         n0 = _launches()
-        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn):
+        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo):
             ops.conv_fwd_igemm_q(x, a_kind, wf, ksf, d, qx.desc, qw.desc, yq, qo, cs)
         assert _launches() == n0 + 1, "the 256-row kernel did not run"
-        assert torch.equal(yq, q_ref), (stages, max_bn)
-        assert torch.equal(ctx.counts_view()[qo.slot].sum(0).cpu(), cnt_ref), (stages, max_bn)
-        assert torch.equal(cs.view(NSHARD, -1).sum(0), cs_ref.view(NSHARD, -1).sum(0)), (stages, max_bn)
+        assert torch.equal(yq, q_ref), (stages, max_bn, halo)
+        assert torch.equal(ctx.counts_view()[qo.slot].sum(0).cpu(), cnt_ref), (stages, max_bn, halo)
+        assert torch.equal(cs.view(NSHARD, -1).sum(0), cs_ref.view(NSHARD, -1).sum(0)), (stages, max_bn, halo)
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k", [
@@ -193,22 +194,22 @@ def test_big_dgrad_bna_matches_dgrad_then_pass_a(N, H, Cin, Cout, k, stochastic)
     c_ref = counts()
     assert (c_ref > 0).all(), c_ref
     s_ref = s_ref.view(NSHARD, -1).sum(0)
-    variants = [(b, s, m) for b, s, m in [(1, st, mb) for st, mb in VARIANTS if mb <= 128] + [(0, 2, 128)]]
-    for big, stages, max_bn in variants:
+    variants = [(1, st, mb, h) for st, mb in VARIANTS if mb <= 128 for h in (0, 1)] + [(0, 2, 128, 0)]
+    for big, stages, max_bn, halo in variants:
         ctx.counts.zero_()
         G = torch.full_like(G_ref, 12345)
         sums = torch.zeros(NSHARD * 4 * Cin, dtype=torch.int64, device=DEV)
         scratch = torch.full_like(dx, float("nan"))
         n0 = _launches()
-        with ops.igemm_forced(big=big, min_tiles=1, stages=stages, max_bn=max_bn):
+        with ops.igemm_forced(big=big, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo):
             ops.conv_dgrad_igemm_bna(g, wd, ksd, d, qg.desc, qw.desc, qr.desc, R, gb, qrg, qng, qn, G, sums, scratch,
                                      None)
         assert _launches() == n0 + big, "the 256-row kernel did not run"
         if big:
             assert torch.isnan(scratch).all(), "the fused path must not store dx"
-        assert torch.equal(G, G_ref), (big, stages, max_bn)
-        assert torch.equal(sums.view(NSHARD, -1).sum(0), s_ref), (big, stages, max_bn)
-        assert torch.equal(counts(), c_ref), (big, stages, max_bn)
+        assert torch.equal(G, G_ref), (big, stages, max_bn, halo)
+        assert torch.equal(sums.view(NSHARD, -1).sum(0), s_ref), (big, stages, max_bn, halo)
+        assert torch.equal(counts(), c_ref), (big, stages, max_bn, halo)
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout", [
