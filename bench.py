@@ -19,6 +19,7 @@ Rank 0 prints ONE JSON line (see DESIGN.md "Measurement").
 """
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -330,6 +331,10 @@ def main():
                          "global_batch": args.batch * world, "per_gpu_batch": args.batch, "image": [224, 224, 3],
                          "classes": 1000, "parallelism": "dp%d" % world, "hip_graph": not args.eager,
                          "executor": "layerwise", "final_loss": round(loss, 4)}
+    # the timed run trains on 4 synthetic batches from random init with the reference's default ranges;
+    # it can diverge (identically in the oracle) without changing the work per step: flagged here
+    ncls = 1000 if r50 else 10
+    out["config"]["loss_diverged"] = bool(not math.isfinite(loss) or loss > 10 * math.log(ncls))
     if rank == 0 and world == 1 and not args.no_roofline:
         from lbt_amd.roofline import measure_dominant
         tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",

@@ -195,7 +195,7 @@ int lbt_conv_dgrad_igemm_ws(const void* gq, int32_t g_i16, const int8_t* wd, int
  * (64, 128, or 256 = A8 without the quantising epilogue); stages 2..4 (A16: 2 or 3).
  * Defaults: {1, 200, 2, 128}, or the LBT_IGEMM_BIG / _MIN / _S / _BN256 environment at first use.
  * halo: 3x3 / stride-1 / pad-1 GEMMs (fwd, unit-stride dgrad, W <= 63) stage one A window per
- * 64-channel block for all 9 taps (default 1, LBT_IGEMM_HALO).
+ * 64-channel block for all 9 taps; bit 0: int8 codes, bit 1: 16-bit codes (default 1, LBT_IGEMM_HALO).
  * launches (get only; set ignores it): 256-row GEMM launches issued by this process so far.      */
 typedef struct lbt_igemm_tuning {
   int32_t big, min_tiles, stages, max_bn, halo, pad;

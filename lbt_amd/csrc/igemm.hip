@@ -71,7 +71,8 @@ struct IgArgs {
   int nkh, nkw, kh0, kw0, oy, ox, ch, cw, cpy, cpx;
   // dgrad, A16, 256-row kernel only (has_bna): the BN pass A this dx feeds (lbt_dgrad_bna), run in the
   // epilogue instead of storing dx (bna_epilogue)
-  int has_bna;  // 1: bna (mask_r), 2: bn3 (g2 + y_bits, bn3.nbn BNs)
+  int has_bna;  // 1: bna (mask_r), 2: bn3 (g2 + y_bits, bn3.nbn BNs); sample-blocked row tiles (PERM)
+  int npb;      // PERM: 16-pixel blocks per sample
   lbt_dgrad_bna bna;
   lbt_dgrad_bn3 bn3;
   int dbg;  // igemm_big_kernel diagnostics (LBT_IGEMM_BIG_DBG; 1: no operand loads after the prologue)
@@ -500,254 +501,137 @@ LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 // 170.6 -> 155.6 us, the other shapes unchanged (profiles/r04l_ab probe_*.txt); A8 BN 128 at 3-4 stages
 // would spill 200+ bytes.
 #ifndef LBT_BIG_OCC
-#define LBT_BIG_OCC(A16, BN, S, HALO) ((A16 && BN == 64 && !HALO) ? 4 : 1)
+#define LBT_BIG_OCC(A16, BN, S, HALO, BNA) (((A16 && BN == 64 && !HALO && !BNA) || (!A16 && HALO && BN == 64)) ? 4 : 1)
 #endif
-// bn_bwd_a_wide_kernel's mask_r pass (bn_wide.hip) on the dgrad accumulators, element for element:
-// dx (the value the plain epilogue stores) -> ReLU mask from R -> G2 = Q_rg -> gamma-scaled rescale
-// gradient -> G = Q_ng (stored) + the four channel sums + both quantisers' counters. Lane (r, q)
-// holds column cw + 16 j + r of rows rtile + 16 i + e (e < 4): the int8 operands, the two noise
-// tables and the int16 G codes move through 4-lane DPP transposes, so each lane loads / stores one
-// row's 4 consecutive channels (R and qn one dword each, noise a float4, G 8 bytes). Rows past M
-// evaluate 0 (code 0, no overflow, no sums) and store nothing. Channel sums: the 4 q-lanes of a
-// column (rows_scatter2), the WM waves of the tile in LDS (int32: 256 rows x 2^22), one int64 atomic
-// per (column, sum) into shard tile % NSHARD. Noise index = (row % (H*W)) * C + column (the period
-// over shape[1:], dynamic_fixed_point.py:32-38).
-template <int MI, int NJ, int WM, int BN>
-LBT_DEV void bna_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4i (&accw)[NJ], float scale,
-                          int64_t rtile, int rlim, bool full, int n0, int cw, int r, int q, int wm, uint32_t tile,
-                          int8_t* lds) {
-  const lbt_dgrad_bna& b = p.bna;
-  const int C = p.ncol;
-  const QState srg = qstate(b.qrg), sng = qstate(b.qng);
-  const float sr = qstate(b.qr).inv_m;
-  const int srs = b.qrg.stochastic, sns = b.qng.stochastic;
-  const int jj = r & 3, g4 = r & ~3;
-  const uint32_t hw = (uint32_t)(p.ch * p.cw);
-  uint32_t pixl[MI];  // the noise pixel of the row this lane loads / stores, per i
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const bool okl = full || i * 16 + jj < rlim;
-    pixl[i] = (uint32_t)(okl ? rtile + i * 16 + jj : 0) % hw;
-  }
-  int o1 = 0, o2 = 0, p1 = 0, p2 = 0;
-  int* red = reinterpret_cast<int*>(lds);  // [WM][4][BN] per-wave column sums
-  __syncthreads();  // every wave's last fragment reads of the LDS ring are done
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = cw + j * 16 + r;
-    const float gam = b.gb[col], bet = b.gb[C + col];
-    const int wsum = accw[j][0];
-    const int cg = cw + j * 16 + g4;  // the 4-lane group's first column
-    int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int64_t rowl = rtile + i * 16 + jj;  // the row this lane loads / stores
-      const bool okl = full || i * 16 + jj < rlim;
-      const int64_t off = rowl * C + cg;
-      uint32_t rw = 0, qw = 0;
-      if (okl) {
-        rw = *reinterpret_cast<const uint32_t*>(b.R + off);
-        qw = *reinterpret_cast<const uint32_t*>(b.qn + off);
-      }
-      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      const uint32_t noff = pixl[i] * (uint32_t)C + cg;
-      const float4 n1 = srs ? *reinterpret_cast<const float4*>(b.qrg.noise + noff) : z4;
-      const float4 n2 = sns ? *reinterpret_cast<const float4*>(b.qng.noise + noff) : z4;
-      // step k: lane jj sends its row's value of column (jj - k) & 3 and receives, from lane (jj + k) & 3,
-      // row (jj + k) & 3's value of its own column
-      int Rv[4] = {0, 0, 0, 0}, Qv[4] = {0, 0, 0, 0};
-      float u1[4] = {0.f, 0.f, 0.f, 0.f}, u2[4] = {0.f, 0.f, 0.f, 0.f};
-      auto tstep = [&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        const int sc = (jj - k) & 3, re = (jj + k) & 3;
-        const uint32_t sh = 8u * (uint32_t)sc;
-        const int srq = (int)(((rw >> sh) & 0xFFu) | (((qw >> sh) & 0xFFu) << 16));
-        const int grq = quad_from<k>(srq);
-        const float gu1 = quad_from<k>(sc == 0 ? n1.x : sc == 1 ? n1.y : sc == 2 ? n1.z : n1.w);
-        const float gu2 = quad_from<k>(sc == 0 ? n2.x : sc == 1 ? n2.y : sc == 2 ? n2.z : n2.w);
-        const int rv = (int)(int8_t)(grq & 0xFF), qv = (int)(int8_t)((grq >> 16) & 0xFF);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          Rv[e] = re == e ? rv : Rv[e];
-          Qv[e] = re == e ? qv : Qv[e];
-          u1[e] = re == e ? gu1 : u1[e];
-          u2[e] = re == e ? gu2 : u2[e];
-        }
-      };
-      tstep(std::integral_constant<int, 0>{});
-      tstep(std::integral_constant<int, 1>{});
-      tstep(std::integral_constant<int, 2>{});
-      tstep(std::integral_constant<int, 3>{});
-      int cc[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool ok = full || i * 16 + e < rlim;
-        const double hs = (double)acc[0][i][j][e] * 256.0;
-        const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
-        const float v = ok ? (float)(hs + ls) * scale : 0.f;
-        // bn.hip chain_bwd_a's mask recomputation and the two quantisers, op for op (bn_wide.hip :139-175)
-        const float xr = (float)Rv[e] * sr;
-        const float m1 = xr * gam;
-        const float yv = m1 + bet;
-        float dd = yv > 0.f ? v : 0.f;
-        const int G2 = quant1(srg, srs, dd, u1[e], o1, o2);
-        s0 += G2 * Rv[e];
-        s1 += G2;
-        const float gh = (float)G2 * srg.inv_m;
-        dd = gh * gam;
-        const int G = quant1(sng, sns, dd, u2[e], p1, p2);
-        s2 += G;
-        s3 += G * Qv[e];
-        cc[e] = G;
-      }
-      // the transpose back: lane jj collects row jj's 4 codes (columns cg .. cg + 3)
-      uint32_t lo = 0, hi = 0;
-      auto pstep = [&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        const int sc = (jj - k) & 3, ce = (jj + k) & 3;
-        const int got = quad_from<k>(sc == 0 ? cc[0] : sc == 1 ? cc[1] : sc == 2 ? cc[2] : cc[3]);
-        const uint32_t h = ((uint32_t)got & 0xFFFFu) << (16 * (ce & 1));
-        lo |= ce < 2 ? h : 0u;
-        hi |= ce < 2 ? 0u : h;
-      };
-      pstep(std::integral_constant<int, 0>{});
-      pstep(std::integral_constant<int, 1>{});
-      pstep(std::integral_constant<int, 2>{});
-      pstep(std::integral_constant<int, 3>{});
-      if (okl) *reinterpret_cast<uint2*>(b.gout + off) = make_uint2(lo, hi);
-    }
-    // the column's 4 q-lanes meet (rows_scatter2); each (wave, sum, column) slot has one writer
-    const int t01 = rows_scatter2(s0, s1), t23 = rows_scatter2(s2, s3);
-    const int cl = cw - n0 + j * 16 + r;
-    if (q < 2) {
-      red[(wm * 4 + q) * BN + cl] = t01;
-      red[(wm * 4 + 2 + q) * BN + cl] = t23;
-    }
-  }
-  const int shard = (int)(tile % LBT_NSHARD);
-  // per-lane overflow counts (quant1: VALU, no per-element ballot masks held in SGPRs) -> wave totals
-  o1 = wave_sum_i32(o1); o2 = wave_sum_i32(o2); p1 = wave_sum_i32(p1); p2 = wave_sum_i32(p2);
-  if ((threadIdx.x & 63) == 0) {
-    if (b.qrg.counts) {
-      int32_t* ct = b.qrg.counts + ((int64_t)b.qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
-      if (o1) atomicAdd(ct, o1);
-      if (o2) atomicAdd(ct + 1, o2);
-    }
-    if (b.qng.counts) {
-      int32_t* ct = b.qng.counts + ((int64_t)b.qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
-      if (p1) atomicAdd(ct, p1);
-      if (p2) atomicAdd(ct + 1, p2);
-    }
-  }
-  __syncthreads();
-  static_assert(4 * BN <= kBT, "one sum per thread");
-  if ((int)threadIdx.x < 4 * BN) {
-    const int sidx = threadIdx.x / BN, cl = threadIdx.x % BN;
-    long long v = 0;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) v += red[(w * 4 + sidx) * BN + cl];
-    if (v) atomicAdd((unsigned long long*)&b.sums[(int64_t)shard * 4 * C + sidx * C + n0 + cl], (unsigned long long)v);
+// BN pass A (bn_wide.hip bn_bwd_a_wide_kernel) on the dgrad accumulators, element for element.
+// MA = 1 (lbt_dgrad_bna): dx -> ReLU mask recomputed from R -> the BN's two quantisers. MA = 2, 3
+// (lbt_dgrad_bn3): d = dx + g2 masked by y_bits (optionally stored) -> MA - 1 BNs' quantisers. Per BN:
+// G2 = Q_rg(d) -> gamma-scaled rescale gradient -> G = Q_ng (stored) + the four channel sums + the
+// counters. These launches tile the rows SAMPLE-blocked (igemm_big_kernel PERM): a 256-row tile is
+// 16 pixels x 16 samples, MFMA row block i = one pixel, its 16 rows = the 16 samples -- so a lane's 4
+// rows share the pixel's stochastic-rounding noise (over shape[1:], dynamic_fixed_point.py:32-38: one
+// table value per lane per column block, 1/16 of a row-major tile's noise reads). Lane (r, q) holds
+// column cw + 16 j + r of samples 16 sb + 4 q + e (e < 4) at pixel 16 pb + MI wm + i; the int8
+// operands, g2 and the int16 codes move through 4-lane DPP transposes (a lane loads / stores one
+// row's 4 consecutive channels). Rows outside (sample >= N, pixel >= H*W) evaluate 0 and store
+// nothing. Channel sums: the 4 q-lanes of a column (rows_scatter2), the WM waves in LDS (int32: 256
+// rows x 2^22), one int64 atomic per (BN, column, sum) into shard tile % NSHARD.
+struct BnaBn {
+  lbt_qdesc qrg, qng;
+  const int8_t *R, *qn;
+  const float* gamma;
+  int16_t* gout;
+  int64_t* sums;
+};
+template <int MA, int k>
+LBT_DEV BnaBn bna_bn(const IgArgs& p) {
+  if constexpr (MA == 1) {
+    const lbt_dgrad_bna& b = p.bna;
+    return BnaBn{b.qrg, b.qng, b.R, b.qn, b.gb, b.gout, b.sums};
+  } else {
+    const lbt_bna_bn& b = p.bn3.bn[k];
+    return BnaBn{b.qrg, b.qng, b.R, b.qn, b.gamma_q, b.gout, b.sums};
   }
 }
 
-// lbt_dgrad_bn3 in the epilogue: d = dx + g2, masked by y_bits (bn_bwd_a_wide_kernel<true>'s YM form,
-// bn_wide.hip :123-138), optionally stored, then NB BN passes A (bn3, the projection shortcut's BN) on
-// the same d -- each as bna_epilogue's rescale / norm quantisers (no mask_r). The same 4-lane
-// transposes: g2 a float4 per lane row, y_bits one byte per (row, channel quad) riding with R's byte.
-template <int MI, int NJ, int WM, int BN, int NB>
-LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4i (&accw)[NJ], float scale,
-                          int64_t rtile, int rlim, bool full, int n0, int cw, int r, int q, int wm, uint32_t tile,
-                          int8_t* lds) {
-  const lbt_dgrad_bn3& b = p.bn3;
+template <int MI, int NJ, int WM, int BN, int MA>
+LBT_DEV void passa_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4i (&accw)[NJ], float scale,
+                            int sb, int pb, int n0, int cw, int r, int q, int wm, uint32_t tile, int8_t* lds) {
+  constexpr int NB = MA == 3 ? 2 : 1;
   const int C = p.ncol;
+  const int N = p.d.N;
+  const int hw = p.ch * p.cw;
+  BnaBn bn[NB];
+  bn[0] = bna_bn<MA, 0>(p);
+  if constexpr (NB == 2) bn[1] = bna_bn<MA, 1>(p);
   QState srg[NB], sng[NB];
   int srs[NB], sns[NB];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    srg[k] = qstate(b.bn[k].qrg);
-    sng[k] = qstate(b.bn[k].qng);
-    srs[k] = b.bn[k].qrg.stochastic;
-    sns[k] = b.bn[k].qng.stochastic;
+  for (int t = 0; t < NB; ++t) {
+    srg[t] = qstate(bn[t].qrg);
+    sng[t] = qstate(bn[t].qng);
+    srs[t] = bn[t].qrg.stochastic;
+    sns[t] = bn[t].qng.stochastic;
   }
+  const float sr = MA == 1 ? qstate(p.bna.qr).inv_m : 0.f;
   const int jj = r & 3, g4 = r & ~3;
-  const uint32_t hw = (uint32_t)(p.ch * p.cw);
-  uint32_t pixl[MI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const bool okl = full || i * 16 + jj < rlim;
-    pixl[i] = (uint32_t)(okl ? rtile + i * 16 + jj : 0) % hw;
-  }
+  const int s0 = sb * 16 + 4 * q;  // this lane's first sample
   int ov[NB][4];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) ov[k][0] = ov[k][1] = ov[k][2] = ov[k][3] = 0;
+  for (int t = 0; t < NB; ++t) ov[t][0] = ov[t][1] = ov[t][2] = ov[t][3] = 0;
   int* red = reinterpret_cast<int*>(lds);  // [NB][WM][4][BN]
-  __syncthreads();
+  __syncthreads();                         // every wave's last fragment reads of the LDS ring are done
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = cw + j * 16 + r;
     float gam[NB];
 #pragma unroll
-    for (int k = 0; k < NB; ++k) gam[k] = b.bn[k].gamma_q[col];
+    for (int t = 0; t < NB; ++t) gam[t] = bn[t].gamma[col];
+    const float bet = MA == 1 ? p.bna.gb[C + col] : 0.f;
     const int wsum = accw[j][0];
     const int cg = cw + j * 16 + g4;
     int sm[NB][4];
 #pragma unroll
-    for (int k = 0; k < NB; ++k) sm[k][0] = sm[k][1] = sm[k][2] = sm[k][3] = 0;
+    for (int t = 0; t < NB; ++t) sm[t][0] = sm[t][1] = sm[t][2] = sm[t][3] = 0;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const int64_t rowl = rtile + i * 16 + jj;
-      const bool okl = full || i * 16 + jj < rlim;
-      const int64_t off = rowl * C + cg;
+      const int pi = pb * 16 + wm * MI + i;  // this row block's pixel (wave-uniform)
+      const bool pv = pi < hw;
+      const int pic = pv ? pi : 0;
+      const bool okl = pv && s0 + jj < N;  // the row this lane loads / stores: sample s0 + jj
+      const int64_t off = ((int64_t)(okl ? s0 + jj : 0) * hw + pic) * C + cg;
       const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
       float4 g2v = z4;
       uint32_t yb = 0, rw[NB], qw[NB];
 #pragma unroll
-      for (int k = 0; k < NB; ++k) rw[k] = qw[k] = 0;
+      for (int t = 0; t < NB; ++t) rw[t] = qw[t] = 0;
       if (okl) {
-        g2v = *reinterpret_cast<const float4*>(b.g2 + off);
-        yb = b.y_bits[off >> 2];
+        if constexpr (MA >= 2) {
+          g2v = *reinterpret_cast<const float4*>(p.bn3.g2 + off);
+          yb = p.bn3.y_bits[off >> 2];
+        }
 #pragma unroll
-        for (int k = 0; k < NB; ++k) {
-          rw[k] = *reinterpret_cast<const uint32_t*>(b.bn[k].R + off);
-          qw[k] = *reinterpret_cast<const uint32_t*>(b.bn[k].qn + off);
+        for (int t = 0; t < NB; ++t) {
+          rw[t] = *reinterpret_cast<const uint32_t*>(bn[t].R + off);
+          qw[t] = *reinterpret_cast<const uint32_t*>(bn[t].qn + off);
         }
       }
-      const uint32_t noff = pixl[i] * (uint32_t)C + cg;
-      float4 n1[NB], n2[NB];
+      // the pixel's noise, shared by the lane's 4 samples
+      float u1[NB], u2[NB];
 #pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        n1[k] = srs[k] ? *reinterpret_cast<const float4*>(b.bn[k].qrg.noise + noff) : z4;
-        n2[k] = sns[k] ? *reinterpret_cast<const float4*>(b.bn[k].qng.noise + noff) : z4;
+      for (int t = 0; t < NB; ++t) {
+        u1[t] = srs[t] ? bn[t].qrg.noise[pic * C + col] : 0.f;
+        u2[t] = sns[t] ? bn[t].qng.noise[pic * C + col] : 0.f;
       }
+      // step k: lane jj sends its row's value of column (jj - k) & 3 and receives, from lane (jj + k) & 3,
+      // row (jj + k) & 3's value of its own column
       int Rv[NB][4], Qv[NB][4], Yv[4] = {0, 0, 0, 0};
-      float u1[NB][4], u2[NB][4], G2v[4] = {0.f, 0.f, 0.f, 0.f};
+      float G2v[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < NB; ++k)
+      for (int t = 0; t < NB; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { Rv[k][e] = Qv[k][e] = 0; u1[k][e] = u2[k][e] = 0.f; }
-      auto pick = [](const float4& v, int sc) { return sc == 0 ? v.x : sc == 1 ? v.y : sc == 2 ? v.z : v.w; };
+        for (int e = 0; e < 4; ++e) Rv[t][e] = Qv[t][e] = 0;
       auto tstep = [&](auto kc) {
         constexpr int k = decltype(kc)::value;
         const int sc = (jj - k) & 3, re = (jj + k) & 3;
         const uint32_t sh = 8u * (uint32_t)sc;
-        const float gg = quad_from<k>(pick(g2v, sc));
+        if constexpr (MA >= 2) {
+          const float gg = quad_from<k>(sc == 0 ? g2v.x : sc == 1 ? g2v.y : sc == 2 ? g2v.z : g2v.w);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) G2v[e] = re == e ? gg : G2v[e];
+          for (int e = 0; e < 4; ++e) G2v[e] = re == e ? gg : G2v[e];
+        }
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
-          // R byte, the mask bit (with BN 0), qn byte
-          const int srq = (int)(((rw[t] >> sh) & 0xFFu) | (t == 0 ? ((yb >> sc) & 1u) << 8 : 0u) |
-                                (((qw[t] >> sh) & 0xFFu) << 16));
+          // R byte, the y_bits mask bit (with BN 0), qn byte
+          const uint32_t yv = (MA >= 2 && t == 0) ? ((yb >> sc) & 1u) << 8 : 0u;
+          const int srq = (int)(((rw[t] >> sh) & 0xFFu) | yv | (((qw[t] >> sh) & 0xFFu) << 16));
           const int grq = quad_from<k>(srq);
-          const float gu1 = quad_from<k>(pick(n1[t], sc)), gu2 = quad_from<k>(pick(n2[t], sc));
           const int rv = (int)(int8_t)(grq & 0xFF), qv = (int)(int8_t)((grq >> 16) & 0xFF);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             Rv[t][e] = re == e ? rv : Rv[t][e];
             Qv[t][e] = re == e ? qv : Qv[t][e];
-            u1[t][e] = re == e ? gu1 : u1[t][e];
-            u2[t][e] = re == e ? gu2 : u2[t][e];
-            if (t == 0) Yv[e] = re == e ? (grq >> 8) & 1 : Yv[e];
+            if (MA >= 2 && t == 0) Yv[e] = re == e ? (grq >> 8) & 1 : Yv[e];
           }
         }
       };
@@ -759,45 +643,55 @@ LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4
       int cc[NB][4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const bool ok = full || i * 16 + e < rlim;
+        const bool ok = pv && s0 + e < N;
         const double hs = (double)acc[0][i][j][e] * 256.0;
         const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
         const float v = ok ? (float)(hs + ls) * scale : 0.f;
-        const float g = v + G2v[e];
-        const float d = Yv[e] ? g : 0.f;
+        float d;
+        if constexpr (MA == 1) {  // bn.hip chain_bwd_a's mask recomputation, op for op (bn_wide.hip :139-147)
+          const float xr = (float)Rv[0][e] * sr;
+          const float m1 = xr * gam[0];
+          const float yv = m1 + bet;
+          d = yv > 0.f ? v : 0.f;
+        } else {  // bn_wide.hip :123-138
+          const float g = v + G2v[e];
+          d = Yv[e] ? g : 0.f;
+        }
         dm[e] = d;
 #pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          const int G2 = quant1(srg[t], srs[t], d, u1[t][e], ov[t][0], ov[t][1]);
+        for (int t = 0; t < NB; ++t) {  // bn_wide.hip :150-172
+          const int G2 = quant1(srg[t], srs[t], d, u1[t], ov[t][0], ov[t][1]);
           sm[t][0] += G2 * Rv[t][e];
           sm[t][1] += G2;
           const float gh = (float)G2 * srg[t].inv_m;
           const float dd = gh * gam[t];
-          const int G = quant1(sng[t], sns[t], dd, u2[t][e], ov[t][2], ov[t][3]);
+          const int G = quant1(sng[t], sns[t], dd, u2[t], ov[t][2], ov[t][3]);
           sm[t][2] += G;
           sm[t][3] += G * Qv[t][e];
           cc[t][e] = G;
         }
       }
-      if (b.gmask_out) {  // uniform: lane jj stores row jj's 4 masked gradients
-        float4 o = z4;
-        auto fstep = [&](auto kc) {
-          constexpr int k = decltype(kc)::value;
-          const int sc = (jj - k) & 3, ce = (jj + k) & 3;
-          const float got = quad_from<k>(sc == 0 ? dm[0] : sc == 1 ? dm[1] : sc == 2 ? dm[2] : dm[3]);
-          o.x = ce == 0 ? got : o.x;
-          o.y = ce == 1 ? got : o.y;
-          o.z = ce == 2 ? got : o.z;
-          o.w = ce == 3 ? got : o.w;
-        };
-        fstep(std::integral_constant<int, 0>{});
-        fstep(std::integral_constant<int, 1>{});
-        fstep(std::integral_constant<int, 2>{});
-        fstep(std::integral_constant<int, 3>{});
-        if (okl) *reinterpret_cast<float4*>(b.gmask_out + off) = o;
+      if constexpr (MA >= 2) {
+        if (p.bn3.gmask_out) {  // uniform: lane jj stores row jj's 4 masked gradients
+          float4 o = z4;
+          auto fstep = [&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int sc = (jj - k) & 3, ce = (jj + k) & 3;
+            const float got = quad_from<k>(sc == 0 ? dm[0] : sc == 1 ? dm[1] : sc == 2 ? dm[2] : dm[3]);
+            o.x = ce == 0 ? got : o.x;
+            o.y = ce == 1 ? got : o.y;
+            o.z = ce == 2 ? got : o.z;
+            o.w = ce == 3 ? got : o.w;
+          };
+          fstep(std::integral_constant<int, 0>{});
+          fstep(std::integral_constant<int, 1>{});
+          fstep(std::integral_constant<int, 2>{});
+          fstep(std::integral_constant<int, 3>{});
+          if (okl) *reinterpret_cast<float4*>(p.bn3.gmask_out + off) = o;
+        }
       }
 #pragma unroll
-      for (int t = 0; t < NB; ++t) {
+      for (int t = 0; t < NB; ++t) {  // the transpose back: lane jj stores row jj's 4 codes
         uint32_t lo = 0, hi = 0;
         auto pstep = [&](auto kc) {
           constexpr int k = decltype(kc)::value;
@@ -811,9 +705,10 @@ LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4
         pstep(std::integral_constant<int, 1>{});
         pstep(std::integral_constant<int, 2>{});
         pstep(std::integral_constant<int, 3>{});
-        if (okl) *reinterpret_cast<uint2*>(b.bn[t].gout + off) = make_uint2(lo, hi);
+        if (okl) *reinterpret_cast<uint2*>(bn[t].gout + off) = make_uint2(lo, hi);
       }
     }
+    // the column's 4 q-lanes meet (rows_scatter2); each (BN, wave, sum, column) slot has one writer
     const int cl = cw - n0 + j * 16 + r;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
@@ -825,18 +720,19 @@ LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4
     }
   }
   const int shard = (int)(tile % LBT_NSHARD);
+  // per-lane overflow counts (quant1: VALU, no per-element ballot masks held in SGPRs) -> wave totals
 #pragma unroll
   for (int t = 0; t < NB; ++t) {
     const int a0 = wave_sum_i32(ov[t][0]), a1 = wave_sum_i32(ov[t][1]);
     const int c0 = wave_sum_i32(ov[t][2]), c1 = wave_sum_i32(ov[t][3]);
     if ((threadIdx.x & 63) == 0) {
-      if (b.bn[t].qrg.counts) {
-        int32_t* ct = b.bn[t].qrg.counts + ((int64_t)b.bn[t].qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (bn[t].qrg.counts) {
+        int32_t* ct = bn[t].qrg.counts + ((int64_t)bn[t].qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
         if (a0) atomicAdd(ct, a0);
         if (a1) atomicAdd(ct + 1, a1);
       }
-      if (b.bn[t].qng.counts) {
-        int32_t* ct = b.bn[t].qng.counts + ((int64_t)b.bn[t].qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (bn[t].qng.counts) {
+        int32_t* ct = bn[t].qng.counts + ((int64_t)bn[t].qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
         if (c0) atomicAdd(ct, c0);
         if (c1) atomicAdd(ct + 1, c1);
       }
@@ -848,8 +744,8 @@ LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4
     long long v = 0;
 #pragma unroll
     for (int w = 0; w < WM; ++w) v += red[((t * WM + w) * 4 + sidx) * BN + cl];
-    if (v)
-      atomicAdd((unsigned long long*)&b.bn[t].sums[(int64_t)shard * 4 * C + sidx * C + n0 + cl], (unsigned long long)v);
+    int64_t* dst = t == 0 ? bn[0].sums : bn[NB - 1].sums;
+    if (v) atomicAdd((unsigned long long*)&dst[(int64_t)shard * 4 * C + sidx * C + n0 + cl], (unsigned long long)v);
   }
 }
 
@@ -861,7 +757,7 @@ LBT_DEV void bn3_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4
 // Window: two buffers, the next block's window DMA'd one instruction per wave per tap step while the
 // current block's 9 taps run; B: a 3-stage ring, two taps ahead.
 template <int MODE, bool A16, bool ADD, int BN, int S, int BNA = 0, bool HALO = false>
-__global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO)) void igemm_big_kernel(IgArgs p) {
+__global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO, BNA)) void igemm_big_kernel(IgArgs p) {
   constexpr int BM = 256, WN = BN / 64, WM = 8 / WN, TR = BM / WM, MI = TR / 16, NJ = 4;
   constexpr int NA = A16 ? 2 : 1;
   constexpr int ROWB = A16 ? 128 : 64;                 // bytes of one A row per k-block
@@ -878,7 +774,12 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO)) void igemm_big_
   const int ntn = p.ncol / BN;
   const uint32_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
   const uint32_t tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  const int64_t m0 = (int64_t)(tile / (uint32_t)ntn) * BM;
+  // PERM (the pass-A epilogues): row tile rt = (sample block sb, pixel block pb), tile row
+  // (16 px + s) = pixel 16 pb + px of sample 16 sb + s; else rows m0 .. m0 + 255 in pixel order
+  constexpr bool PERM = BNA >= 1;
+  const uint32_t rt = tile / (uint32_t)ntn;
+  const int64_t m0 = PERM ? 0 : (int64_t)rt * BM;
+  const int sb = PERM ? (int)(rt / (uint32_t)p.npb) : 0, pb = PERM ? (int)(rt % (uint32_t)p.npb) : 0;
   const int n0 = (int)(tile % (uint32_t)ntn) * BN;
   const lbt_conv_desc& d = p.d;
   const int OH = p.ch, OW = p.cw;
@@ -894,13 +795,22 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO)) void igemm_big_
 #pragma unroll
   for (int g = 0; g < GA; ++g) {
     const int row = (wave + 8 * g) * RPI + lane / SPR;
-    const int64_t m = m0 + row;
-    arow[g] = m < p.M;
-    const uint32_t mu = (uint32_t)(arow[g] ? m : 0);
-    ax[g] = (int)(mu % (uint32_t)OW);
-    const uint32_t tt = mu / (uint32_t)OW;
-    ay[g] = (int)(tt % (uint32_t)OH);
-    an[g] = (int)(tt / (uint32_t)OH);
+    if constexpr (PERM) {
+      const int sm = sb * 16 + (row & 15), px = pb * 16 + (row >> 4);
+      arow[g] = sm < d.N && px < OH * OW;
+      const uint32_t pu = (uint32_t)(arow[g] ? px : 0);
+      ax[g] = (int)(pu % (uint32_t)OW);
+      ay[g] = (int)(pu / (uint32_t)OW);
+      an[g] = arow[g] ? sm : 0;
+    } else {
+      const int64_t m = m0 + row;
+      arow[g] = m < p.M;
+      const uint32_t mu = (uint32_t)(arow[g] ? m : 0);
+      ax[g] = (int)(mu % (uint32_t)OW);
+      const uint32_t tt = mu / (uint32_t)OW;
+      ay[g] = (int)(tt % (uint32_t)OH);
+      an[g] = (int)(tt / (uint32_t)OH);
+    }
     const int ps = lane % SPR;  // the LDS segment this lane fills; its source is segment ps ^ f(row)
     aseg[g] = A16 ? (ps ^ swz128(row)) : (ps ^ swz64(row));
   }
@@ -1221,11 +1131,8 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO)) void igemm_big_
       return;
     }
   }
-  if constexpr (BNA == 1) {
-    bna_epilogue<MI, NJ, WM, BN>(p, acc, accw, scale, rtile, rlim, full, n0, cw, r, q, wm, tile, lds);
-    return;
-  } else if constexpr (BNA >= 2) {
-    bn3_epilogue<MI, NJ, WM, BN, BNA - 1>(p, acc, accw, scale, rtile, rlim, full, n0, cw, r, q, wm, tile, lds);
+  if constexpr (BNA >= 1) {
+    passa_epilogue<MI, NJ, WM, BN, BNA>(p, acc, accw, scale, sb, pb, n0, cw, r, q, wm, tile, lds);
     return;
   }
 #pragma unroll
@@ -1278,8 +1185,9 @@ template <int MODE, bool A16, int BN, int S, bool HALO = false>
 void launch_big_bn(IgArgs p, hipStream_t st) {
   static const int dbg = getenv_int("LBT_IGEMM_BIG_DBG", 0);
   p.dbg = dbg;
-  const int64_t tiles = ((p.M + 255) / 256) * (p.ncol / BN);
-  if constexpr (MODE == MODE_DGRAD && A16) {
+  const int64_t rtiles = p.has_bna ? (int64_t)((p.d.N + 15) / 16) * p.npb : (p.M + 255) / 256;
+  const int64_t tiles = rtiles * (p.ncol / BN);
+  if constexpr (MODE == MODE_DGRAD && A16 && BN == 64 && !HALO) {
     if (p.has_bna == 1) return big_go<MODE, A16, false, BN, S, 1, HALO>(p, tiles, st);
     if (p.has_bna == 2 && p.bn3.nbn == 1) return big_go<MODE, A16, false, BN, S, 2, HALO>(p, tiles, st);
     if (p.has_bna == 2) return big_go<MODE, A16, false, BN, S, 3, HALO>(p, tiles, st);
@@ -1299,7 +1207,7 @@ lbt_igemm_tuning& big_tuning() {
     v.min_tiles = getenv_int("LBT_IGEMM_BIG_MIN", 200);
     v.stages = getenv_int("LBT_IGEMM_BIG_S", 2);
     v.max_bn = getenv_int("LBT_IGEMM_BIG_BN256", 0) ? 256 : 128;
-    v.halo = getenv_int("LBT_IGEMM_HALO", 1);
+    v.halo = getenv_int("LBT_IGEMM_HALO", 1);  // bit 0: int8 codes (fwd), bit 1: 16-bit codes (dgrad16)
     v.pad = 0;
     v.launches = 0;
     return v;
@@ -1317,12 +1225,13 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
   if ((p.M + 255) / 256 * (p.ncol / 64) > 0x7fffffff) return false;
   // column tile: the widest (<= max_bn) that still gives min_tiles tiles (256 only without the
   // quantising epilogue and on request: its 8 x 4 accumulator tiles per wave spill)
-  const int64_t mt = (p.M + 255) / 256;
+  const int64_t mt = p.has_bna ? (int64_t)((p.d.N + 15) / 16) * p.npb : (p.M + 255) / 256;
   int bn = 0;
   if (!A16 && !p.yq && p.ncol % 256 == 0 && tu.max_bn >= 256 && mt * (p.ncol / 256) >= tmin) bn = 256;
   else if (tu.max_bn >= 128 && p.ncol % 128 == 0 && mt * (p.ncol / 128) >= tmin) bn = 128;
   else if (mt * (p.ncol / 64) >= tmin) bn = 64;
   if (!bn) return false;
+  if (p.has_bna) bn = 64;  // the pass-A epilogues: 64-column tiles, 256 VGPRs (one workgroup per CU)
   // LDS ring depth (stages): 2 by default -- the probe on the ResNet-50 shapes measured the
   // occupancy of 2 stages (A8 BN 128: 48 KiB, two workgroups per CU) ahead of the latency hiding of 3-4
   // (72-96 KiB, one; the software-pipelined loop), except 3x3 dgrad16 at 28x28 / 14x14 (3-5 %).
@@ -1331,16 +1240,11 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
   // 3x3 / stride 1 / pad 1 with every tap (fwd, unit-stride dgrad) and W <= 63: the A window per
   // channel block (HALO), 64- and 128-column tiles
   const lbt_conv_desc& d = p.d;
-  const bool halo = tu.halo && bn <= 128 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
+  const bool halo = (tu.halo & (A16 ? 2 : 1)) && !p.has_bna && bn <= 128 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
                     d.PL == 1 && d.Ho == d.H && d.Wo == d.W && p.nkh == 3 && p.nkw == 3 && p.kh0 == 0 &&
                     p.kw0 == 0 && p.cw == d.W && p.ch == d.H && d.W <= 63;
-  if (halo) {  // 16-bit codes: 64-column tiles (one workgroup per CU: the two 48 KiB windows)
-    if constexpr (A16) {
-      launch_big_bn<MODE, A16, 64, 2, true>(p, st);
-    } else {
-      if (bn == 128) launch_big_bn<MODE, A16, 128, 2, true>(p, st);
-      else launch_big_bn<MODE, A16, 64, 2, true>(p, st);
-    }
+  if (halo) {  // 64-column tiles: int8 codes two workgroups per CU (98 VGPRs, 60 KiB); 16-bit one (2 x 48 KiB windows)
+    launch_big_bn<MODE, A16, 64, 2, true>(p, st);
   } else if (bn == 256) {
     if constexpr (!A16) launch_big_bn<MODE, A16, 256, 4>(p, st);
   } else if (bn == 128) {
@@ -1634,6 +1538,7 @@ extern "C" int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int
     p.ksplit = 1;
     all_taps(p, MODE_DGRAD);
     p.has_bna = 1;
+    p.npb = (d.H * d.W + 15) / 16;
     p.bna = b;
     if (launch_big<MODE_DGRAD, true>(p, st)) return (int)hipGetLastError();
   }
@@ -1669,6 +1574,7 @@ extern "C" int lbt_conv_dgrad_igemm_bn3(const int16_t* gq, const int8_t* wd, int
     p.ksplit = 1;
     all_taps(p, MODE_DGRAD);
     p.has_bna = 2;
+    p.npb = (d.H * d.W + 15) / 16;
     p.bn3 = b;
     if (launch_big<MODE_DGRAD, true>(p, st)) return (int)hipGetLastError();
   }

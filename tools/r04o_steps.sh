@@ -1,7 +1,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/r04o
-timeout -k 10 500 python -u -m pytest tests/test_igemm_big.py tests/test_resnet50.py -m gpu -x -v --timeout 240 \
+timeout -k 10 500 python -u -m pytest tests/test_igemm_big.py tests/test_resnet50.py -m gpu -v --timeout 240 \
   --timeout-method thread > gpurun_out/r04o/first.log 2>&1; rc=$?
 tail -3 gpurun_out/r04o/first.log; [ $rc = 0 ] || exit 1
 S3=l1_c2_fwd,l2_c2_fwd,l3_c2_fwd,l4_c2_fwd,l1_c2_dgrad16,l2_c2_dgrad16,l3_c2_dgrad16,l4_c2_dgrad16,l1_c2_fwdq,l2_c2_fwdq,l3_c2_fwdq
