@@ -499,23 +499,24 @@ LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 // waves per SIMD the register allocation must leave room for (4: two 512-thread workgroups per CU).
 // 16-bit codes at BN 64: 142 -> 128 VGPRs (20 bytes of spill), two workgroups per CU: l1_c2 dgrad16
 // 170.6 -> 155.6 us, the other shapes unchanged (profiles/r04l_ab probe_*.txt); A8 BN 128 at 3-4 stages
-// would spill 200+ bytes.
+// would spill 200+ bytes. HALO int8 at BN 64: 98 VGPRs, two per CU. The pass-A epilogues (BNA) at BN 64
+// fit 128 VGPRs with one BN; with two (BNA 3, the projection blocks) one workgroup per CU.
 #ifndef LBT_BIG_OCC
-#define LBT_BIG_OCC(A16, BN, S, HALO, BNA) (((A16 && BN == 64 && !HALO && !BNA) || (!A16 && HALO && BN == 64)) ? 4 : 1)
+#define LBT_BIG_OCC(A16, BN, S, HALO, BNA) (((A16 && BN == 64 && !HALO && BNA != 3) || (!A16 && HALO && BN == 64)) ? 4 : 1)
 #endif
 // BN pass A (bn_wide.hip bn_bwd_a_wide_kernel) on the dgrad accumulators, element for element.
 // MA = 1 (lbt_dgrad_bna): dx -> ReLU mask recomputed from R -> the BN's two quantisers. MA = 2, 3
 // (lbt_dgrad_bn3): d = dx + g2 masked by y_bits (optionally stored) -> MA - 1 BNs' quantisers. Per BN:
 // G2 = Q_rg(d) -> gamma-scaled rescale gradient -> G = Q_ng (stored) + the four channel sums + the
-// counters. These launches tile the rows SAMPLE-blocked (igemm_big_kernel PERM): a 256-row tile is
-// 16 pixels x 16 samples, MFMA row block i = one pixel, its 16 rows = the 16 samples -- so a lane's 4
-// rows share the pixel's stochastic-rounding noise (over shape[1:], dynamic_fixed_point.py:32-38: one
-// table value per lane per column block, 1/16 of a row-major tile's noise reads). Lane (r, q) holds
-// column cw + 16 j + r of samples 16 sb + 4 q + e (e < 4) at pixel 16 pb + MI wm + i; the int8
-// operands, g2 and the int16 codes move through 4-lane DPP transposes (a lane loads / stores one
-// row's 4 consecutive channels). Rows outside (sample >= N, pixel >= H*W) evaluate 0 and store
-// nothing. Channel sums: the 4 q-lanes of a column (rows_scatter2), the WM waves in LDS (int32: 256
-// rows x 2^22), one int64 atomic per (BN, column, sum) into shard tile % NSHARD.
+// counters. These launches tile the rows SAMPLE-blocked (igemm_big_kernel PERM): a 256-row x 64-column
+// tile is 16 pixels x 16 samples. The dequantised dx tile is staged in LDS ([pixel][sample][column],
+// padded: conflict-free writes from the MFMA layout and reads by quads), then pass A runs with
+// bn_bwd_a_wide_kernel's thread layout: a thread owns one position (pixel, 4 channels) and walks 8
+// samples, so its two Philox calls (or table reads) per BN are made once for 8 samples and a wave's
+// loads / stores are 4 pixels x 64 contiguous channels of one sample (coalesced; the MFMA layout
+// would touch 16 rows x 16 bytes per instruction). Channel sums: lanes of a quad column by shuffles,
+// the 8 waves in LDS (int32: 16 samples x 16 pixels x 2^22), one int64 atomic per (BN, column, sum)
+// into shard tile % NSHARD. Rows outside (sample >= N, pixel >= H*W) are skipped.
 struct BnaBn {
   lbt_qdesc qrg, qng;
   const int8_t *R, *qn;
@@ -533,219 +534,167 @@ LBT_DEV BnaBn bna_bn(const IgArgs& p) {
     return BnaBn{b.qrg, b.qng, b.R, b.qn, b.gamma_q, b.gout, b.sums};
   }
 }
+constexpr int kXRow = 68;                // floats per (pixel, sample) row of the staged dx tile
+constexpr int kXPix = 16 * kXRow + 4;    // floats per pixel: 16 samples + 4 (bank offset per pixel)
+constexpr int kXBytes = 16 * kXPix * 4;  // 69 888 bytes
 
 template <int MI, int NJ, int WM, int BN, int MA>
 LBT_DEV void passa_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const v4i (&accw)[NJ], float scale,
-                            int sb, int pb, int n0, int cw, int r, int q, int wm, uint32_t tile, int8_t* lds) {
+                            int sb, int pb, int n0, int r, int q, int wm, uint32_t tile, int8_t* lds) {
+  static_assert(BN == 64 && WM == 8 && MI == 2, "the pass-A epilogue runs 256 x 64 tiles of 8 waves");
   constexpr int NB = MA == 3 ? 2 : 1;
   const int C = p.ncol;
   const int N = p.d.N;
   const int hw = p.ch * p.cw;
+  float* xs = reinterpret_cast<float*>(lds);
+  // ---- the dequantised dx tile into LDS: lane (r, q) holds column 16 j + r of samples 4 q + e at pixel
+  // MI wm + i
+  __syncthreads();  // every wave's last fragment reads of the LDS ring are done
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int wsum = accw[j][0];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const double hs = (double)acc[0][i][j][e] * 256.0;
+        const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
+        xs[(wm * MI + i) * kXPix + (4 * q + e) * kXRow + j * 16 + r] = (float)(hs + ls) * scale;
+      }
+  }
+  __syncthreads();
+  // ---- pass A: thread = (quad cq, pixel pl, sample half sh)
+  const int t = threadIdx.x;
+  const int cq = t & 15, pl = (t >> 4) & 15, sh = t >> 8;
+  const int c0 = n0 + 4 * cq;
+  const int pix = pb * 16 + pl;
+  const bool pv = pix < hw;
   BnaBn bn[NB];
   bn[0] = bna_bn<MA, 0>(p);
   if constexpr (NB == 2) bn[1] = bna_bn<MA, 1>(p);
+  float gam[NB][4], bet[4] = {0.f, 0.f, 0.f, 0.f};
+  Noise4 u1[NB], u2[NB];
   QState srg[NB], sng[NB];
-  int srs[NB], sns[NB];
+  const uint64_t blk = ((uint64_t)(pv ? pix : 0) * (uint32_t)C + (uint32_t)c0) >> 2;
 #pragma unroll
-  for (int t = 0; t < NB; ++t) {
-    srg[t] = qstate(bn[t].qrg);
-    sng[t] = qstate(bn[t].qng);
-    srs[t] = bn[t].qrg.stochastic;
-    sns[t] = bn[t].qng.stochastic;
+  for (int k = 0; k < NB; ++k) {
+    srg[k] = qstate(bn[k].qrg);
+    sng[k] = qstate(bn[k].qng);
+    const float4 g4 = *reinterpret_cast<const float4*>(bn[k].gamma + c0);
+    gam[k][0] = g4.x; gam[k][1] = g4.y; gam[k][2] = g4.z; gam[k][3] = g4.w;
+    const Noise4 z{{0.f, 0.f, 0.f, 0.f}};
+    u1[k] = bn[k].qrg.stochastic ? qnoise4(bn[k].qrg, srg[k].step, blk) : z;
+    u2[k] = bn[k].qng.stochastic ? qnoise4(bn[k].qng, sng[k].step, blk) : z;
   }
-  const float sr = MA == 1 ? qstate(p.bna.qr).inv_m : 0.f;
-  const int jj = r & 3, g4 = r & ~3;
-  const int s0 = sb * 16 + 4 * q;  // this lane's first sample
+  float sr = 0.f;
+  if constexpr (MA == 1) {
+    const float4 b4 = *reinterpret_cast<const float4*>(p.bna.gb + C + c0);
+    bet[0] = b4.x; bet[1] = b4.y; bet[2] = b4.z; bet[3] = b4.w;
+    sr = qstate(p.bna.qr).inv_m;
+  }
+  int sm[NB][4][4];  // [BN][sum][channel]
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) sm[k][a][0] = sm[k][a][1] = sm[k][a][2] = sm[k][a][3] = 0;
   int ov[NB][4];
 #pragma unroll
-  for (int t = 0; t < NB; ++t) ov[t][0] = ov[t][1] = ov[t][2] = ov[t][3] = 0;
-  int* red = reinterpret_cast<int*>(lds);  // [NB][WM][4][BN]
-  __syncthreads();                         // every wave's last fragment reads of the LDS ring are done
+  for (int k = 0; k < NB; ++k) ov[k][0] = ov[k][1] = ov[k][2] = ov[k][3] = 0;
+  const int sbase = sb * 16 + sh * 8;
+#pragma unroll 2
+  for (int u = 0; u < 8; ++u) {
+    const int sm_ = sbase + u;
+    if (!pv || sm_ >= N) break;  // samples ascend: the rest of this thread's are outside too
+    const int64_t off = ((int64_t)sm_ * hw + pix) * C + c0;
+    const float4 xv = *reinterpret_cast<const float4*>(xs + pl * kXPix + (sh * 8 + u) * kXRow + 4 * cq);
+    float d[4] = {xv.x, xv.y, xv.z, xv.w};
+    char4 rv[NB], qv[NB];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = cw + j * 16 + r;
-    float gam[NB];
+    for (int k = 0; k < NB; ++k) {
+      rv[k] = *reinterpret_cast<const char4*>(bn[k].R + off);
+      qv[k] = *reinterpret_cast<const char4*>(bn[k].qn + off);
+    }
+    if constexpr (MA >= 2) {  // bn_wide.hip :123-138
+      const float4 g2 = *reinterpret_cast<const float4*>(p.bn3.g2 + off);
+      const uint32_t yb = p.bn3.y_bits[off >> 2];
+      d[0] = (yb & 1u) ? d[0] + g2.x : 0.f;
+      d[1] = (yb & 2u) ? d[1] + g2.y : 0.f;
+      d[2] = (yb & 4u) ? d[2] + g2.z : 0.f;
+      d[3] = (yb & 8u) ? d[3] + g2.w : 0.f;
+      if (p.bn3.gmask_out) *reinterpret_cast<float4*>(p.bn3.gmask_out + off) = make_float4(d[0], d[1], d[2], d[3]);
+    } else {  // bn.hip chain_bwd_a's mask recomputation, op for op (bn_wide.hip :139-147)
+      const int R[4] = {rv[0].x, rv[0].y, rv[0].z, rv[0].w};
 #pragma unroll
-    for (int t = 0; t < NB; ++t) gam[t] = bn[t].gamma[col];
-    const float bet = MA == 1 ? p.bna.gb[C + col] : 0.f;
-    const int wsum = accw[j][0];
-    const int cg = cw + j * 16 + g4;
-    int sm[NB][4];
-#pragma unroll
-    for (int t = 0; t < NB; ++t) sm[t][0] = sm[t][1] = sm[t][2] = sm[t][3] = 0;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int pi = pb * 16 + wm * MI + i;  // this row block's pixel (wave-uniform)
-      const bool pv = pi < hw;
-      const int pic = pv ? pi : 0;
-      const bool okl = pv && s0 + jj < N;  // the row this lane loads / stores: sample s0 + jj
-      const int64_t off = ((int64_t)(okl ? s0 + jj : 0) * hw + pic) * C + cg;
-      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      float4 g2v = z4;
-      uint32_t yb = 0, rw[NB], qw[NB];
-#pragma unroll
-      for (int t = 0; t < NB; ++t) rw[t] = qw[t] = 0;
-      if (okl) {
-        if constexpr (MA >= 2) {
-          g2v = *reinterpret_cast<const float4*>(p.bn3.g2 + off);
-          yb = p.bn3.y_bits[off >> 2];
-        }
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          rw[t] = *reinterpret_cast<const uint32_t*>(bn[t].R + off);
-          qw[t] = *reinterpret_cast<const uint32_t*>(bn[t].qn + off);
-        }
-      }
-      // the pixel's noise, shared by the lane's 4 samples
-      float u1[NB], u2[NB];
-#pragma unroll
-      for (int t = 0; t < NB; ++t) {
-        u1[t] = srs[t] ? bn[t].qrg.noise[pic * C + col] : 0.f;
-        u2[t] = sns[t] ? bn[t].qng.noise[pic * C + col] : 0.f;
-      }
-      // step k: lane jj sends its row's value of column (jj - k) & 3 and receives, from lane (jj + k) & 3,
-      // row (jj + k) & 3's value of its own column
-      int Rv[NB][4], Qv[NB][4], Yv[4] = {0, 0, 0, 0};
-      float G2v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < NB; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Rv[t][e] = Qv[t][e] = 0;
-      auto tstep = [&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        const int sc = (jj - k) & 3, re = (jj + k) & 3;
-        const uint32_t sh = 8u * (uint32_t)sc;
-        if constexpr (MA >= 2) {
-          const float gg = quad_from<k>(sc == 0 ? g2v.x : sc == 1 ? g2v.y : sc == 2 ? g2v.z : g2v.w);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) G2v[e] = re == e ? gg : G2v[e];
-        }
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          // R byte, the y_bits mask bit (with BN 0), qn byte
-          const uint32_t yv = (MA >= 2 && t == 0) ? ((yb >> sc) & 1u) << 8 : 0u;
-          const int srq = (int)(((rw[t] >> sh) & 0xFFu) | yv | (((qw[t] >> sh) & 0xFFu) << 16));
-          const int grq = quad_from<k>(srq);
-          const int rv = (int)(int8_t)(grq & 0xFF), qv = (int)(int8_t)((grq >> 16) & 0xFF);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            Rv[t][e] = re == e ? rv : Rv[t][e];
-            Qv[t][e] = re == e ? qv : Qv[t][e];
-            if (MA >= 2 && t == 0) Yv[e] = re == e ? (grq >> 8) & 1 : Yv[e];
-          }
-        }
-      };
-      tstep(std::integral_constant<int, 0>{});
-      tstep(std::integral_constant<int, 1>{});
-      tstep(std::integral_constant<int, 2>{});
-      tstep(std::integral_constant<int, 3>{});
-      float dm[4];
-      int cc[NB][4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool ok = pv && s0 + e < N;
-        const double hs = (double)acc[0][i][j][e] * 256.0;
-        const double ls = (double)(acc[1][i][j][e] + 128 * wsum);
-        const float v = ok ? (float)(hs + ls) * scale : 0.f;
-        float d;
-        if constexpr (MA == 1) {  // bn.hip chain_bwd_a's mask recomputation, op for op (bn_wide.hip :139-147)
-          const float xr = (float)Rv[0][e] * sr;
-          const float m1 = xr * gam[0];
-          const float yv = m1 + bet;
-          d = yv > 0.f ? v : 0.f;
-        } else {  // bn_wide.hip :123-138
-          const float g = v + G2v[e];
-          d = Yv[e] ? g : 0.f;
-        }
-        dm[e] = d;
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {  // bn_wide.hip :150-172
-          const int G2 = quant1(srg[t], srs[t], d, u1[t], ov[t][0], ov[t][1]);
-          sm[t][0] += G2 * Rv[t][e];
-          sm[t][1] += G2;
-          const float gh = (float)G2 * srg[t].inv_m;
-          const float dd = gh * gam[t];
-          const int G = quant1(sng[t], sns[t], dd, u2[t], ov[t][2], ov[t][3]);
-          sm[t][2] += G;
-          sm[t][3] += G * Qv[t][e];
-          cc[t][e] = G;
-        }
-      }
-      if constexpr (MA >= 2) {
-        if (p.bn3.gmask_out) {  // uniform: lane jj stores row jj's 4 masked gradients
-          float4 o = z4;
-          auto fstep = [&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            const int sc = (jj - k) & 3, ce = (jj + k) & 3;
-            const float got = quad_from<k>(sc == 0 ? dm[0] : sc == 1 ? dm[1] : sc == 2 ? dm[2] : dm[3]);
-            o.x = ce == 0 ? got : o.x;
-            o.y = ce == 1 ? got : o.y;
-            o.z = ce == 2 ? got : o.z;
-            o.w = ce == 3 ? got : o.w;
-          };
-          fstep(std::integral_constant<int, 0>{});
-          fstep(std::integral_constant<int, 1>{});
-          fstep(std::integral_constant<int, 2>{});
-          fstep(std::integral_constant<int, 3>{});
-          if (okl) *reinterpret_cast<float4*>(p.bn3.gmask_out + off) = o;
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < NB; ++t) {  // the transpose back: lane jj stores row jj's 4 codes
-        uint32_t lo = 0, hi = 0;
-        auto pstep = [&](auto kc) {
-          constexpr int k = decltype(kc)::value;
-          const int sc = (jj - k) & 3, ce = (jj + k) & 3;
-          const int got = quad_from<k>(sc == 0 ? cc[t][0] : sc == 1 ? cc[t][1] : sc == 2 ? cc[t][2] : cc[t][3]);
-          const uint32_t h = ((uint32_t)got & 0xFFFFu) << (16 * (ce & 1));
-          lo |= ce < 2 ? h : 0u;
-          hi |= ce < 2 ? 0u : h;
-        };
-        pstep(std::integral_constant<int, 0>{});
-        pstep(std::integral_constant<int, 1>{});
-        pstep(std::integral_constant<int, 2>{});
-        pstep(std::integral_constant<int, 3>{});
-        if (okl) *reinterpret_cast<uint2*>(bn[t].gout + off) = make_uint2(lo, hi);
+      for (int c = 0; c < 4; ++c) {
+        const float xr = (float)R[c] * sr;
+        const float m1 = xr * gam[0][c];
+        const float yv = m1 + bet[c];
+        d[c] = yv > 0.f ? d[c] : 0.f;
       }
     }
-    // the column's 4 q-lanes meet (rows_scatter2); each (BN, wave, sum, column) slot has one writer
-    const int cl = cw - n0 + j * 16 + r;
 #pragma unroll
-    for (int t = 0; t < NB; ++t) {
-      const int t01 = rows_scatter2(sm[t][0], sm[t][1]), t23 = rows_scatter2(sm[t][2], sm[t][3]);
-      if (q < 2) {
-        red[((t * WM + wm) * 4 + q) * BN + cl] = t01;
-        red[((t * WM + wm) * 4 + 2 + q) * BN + cl] = t23;
+    for (int k = 0; k < NB; ++k) {  // bn_wide.hip :150-175
+      const int R[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+      const int Q[4] = {qv[k].x, qv[k].y, qv[k].z, qv[k].w};
+      int G[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int G2 = quant1(srg[k], bn[k].qrg.stochastic, d[c], u1[k].u[c], ov[k][0], ov[k][1]);
+        sm[k][0][c] += G2 * R[c];
+        sm[k][1][c] += G2;
+        const float gh = (float)G2 * srg[k].inv_m;
+        const float dd = gh * gam[k][c];
+        G[c] = quant1(sng[k], bn[k].qng.stochastic, dd, u2[k].u[c], ov[k][2], ov[k][3]);
+        sm[k][2][c] += G[c];
+        sm[k][3][c] += G[c] * Q[c];
       }
+      short4 o;
+      o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
+      *reinterpret_cast<short4*>(bn[k].gout + off) = o;
     }
   }
+  // ---- channel sums: the 4 pixel lanes of a wave sharing cq (shuffles), then the 8 waves in LDS
   const int shard = (int)(tile % LBT_NSHARD);
-  // per-lane overflow counts (quant1: VALU, no per-element ballot masks held in SGPRs) -> wave totals
+  const int wv = t >> 6;
+  int* red = reinterpret_cast<int*>(lds);  // [8 waves][NB][4 sums][64 columns]
+  __syncthreads();                         // the staged dx tile is read
 #pragma unroll
-  for (int t = 0; t < NB; ++t) {
-    const int a0 = wave_sum_i32(ov[t][0]), a1 = wave_sum_i32(ov[t][1]);
-    const int c0 = wave_sum_i32(ov[t][2]), c1 = wave_sum_i32(ov[t][3]);
-    if ((threadIdx.x & 63) == 0) {
-      if (bn[t].qrg.counts) {
-        int32_t* ct = bn[t].qrg.counts + ((int64_t)bn[t].qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+  for (int k = 0; k < NB; ++k)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        int v = sm[k][a][c];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if ((t & 63) < 16) red[((wv * NB + k) * 4 + a) * 64 + 4 * cq + c] = v;
+      }
+  // per-lane overflow counts -> wave totals -> lane 0
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int a0 = wave_sum_i32(ov[k][0]), a1 = wave_sum_i32(ov[k][1]);
+    const int b0 = wave_sum_i32(ov[k][2]), b1 = wave_sum_i32(ov[k][3]);
+    if ((t & 63) == 0) {
+      if (bn[k].qrg.counts) {
+        int32_t* ct = bn[k].qrg.counts + ((int64_t)bn[k].qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
         if (a0) atomicAdd(ct, a0);
         if (a1) atomicAdd(ct + 1, a1);
       }
-      if (bn[t].qng.counts) {
-        int32_t* ct = bn[t].qng.counts + ((int64_t)bn[t].qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
-        if (c0) atomicAdd(ct, c0);
-        if (c1) atomicAdd(ct + 1, c1);
+      if (bn[k].qng.counts) {
+        int32_t* ct = bn[k].qng.counts + ((int64_t)bn[k].qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+        if (b0) atomicAdd(ct, b0);
+        if (b1) atomicAdd(ct + 1, b1);
       }
     }
   }
   __syncthreads();
-  for (int x = threadIdx.x; x < NB * 4 * BN; x += kBT) {
-    const int t = x / (4 * BN), sidx = (x / BN) & 3, cl = x % BN;
+  for (int x = t; x < NB * 4 * 64; x += kBT) {
+    const int k = x / 256, a = (x / 64) & 3, cl = x & 63;
     long long v = 0;
 #pragma unroll
-    for (int w = 0; w < WM; ++w) v += red[((t * WM + w) * 4 + sidx) * BN + cl];
-    int64_t* dst = t == 0 ? bn[0].sums : bn[NB - 1].sums;
-    if (v) atomicAdd((unsigned long long*)&dst[(int64_t)shard * 4 * C + sidx * C + n0 + cl], (unsigned long long)v);
+    for (int w = 0; w < 8; ++w) v += red[((w * NB + k) * 4 + a) * 64 + cl];
+    int64_t* dst = k == 0 ? bn[0].sums : bn[NB - 1].sums;
+    if (v) atomicAdd((unsigned long long*)&dst[(int64_t)shard * 4 * C + a * C + n0 + cl], (unsigned long long)v);
   }
 }
 
@@ -1132,7 +1081,7 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO, BNA)) void igemm
     }
   }
   if constexpr (BNA >= 1) {
-    passa_epilogue<MI, NJ, WM, BN, BNA>(p, acc, accw, scale, sb, pb, n0, cw, r, q, wm, tile, lds);
+    if constexpr (BN == 64) passa_epilogue<MI, NJ, WM, BN, BNA>(p, acc, accw, scale, sb, pb, n0, r, q, wm, tile, lds);
     return;
   }
 #pragma unroll
@@ -1170,7 +1119,8 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO, BNA)) void igemm
 template <int MODE, bool A16, bool ADD, int BN, int S, int BNA, bool HALO>
 void big_go(const IgArgs& p, int64_t tiles, hipStream_t st) {
   constexpr int BM = 256, ROWB = A16 ? 128 : 64;
-  constexpr size_t shm = HALO ? (size_t)2 * 384 * ROWB + (size_t)3 * BN * 64 : (size_t)S * (BM * ROWB + BN * 64);
+  constexpr size_t ring = HALO ? (size_t)2 * 384 * ROWB + (size_t)3 * BN * 64 : (size_t)S * (BM * ROWB + BN * 64);
+  constexpr size_t shm = (BNA && ring < (size_t)kXBytes) ? (size_t)kXBytes : ring;  // the staged dx tile
   static bool attr_ = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, ADD, BN, S, BNA, HALO>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
@@ -1242,7 +1192,10 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
   const lbt_conv_desc& d = p.d;
   const bool halo = (tu.halo & (A16 ? 2 : 1)) && !p.has_bna && bn <= 128 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
                     d.PL == 1 && d.Ho == d.H && d.Wo == d.W && p.nkh == 3 && p.nkw == 3 && p.kh0 == 0 &&
-                    p.kw0 == 0 && p.cw == d.W && p.ch == d.H && d.W <= 63;
+                    p.kw0 == 0 && p.cw == d.W && p.ch == d.H && d.W <= 63 &&
+                    // where it measured faster (profiles/r04p): one column tile (the window is not
+                    // re-staged per column tile), or a chip the 128-column tiles would under-fill
+                    (p.ncol == 64 || mt * (p.ncol / bn) < 256);
   if (halo) {  // 64-column tiles: int8 codes two workgroups per CU (98 VGPRs, 60 KiB); 16-bit one (2 x 48 KiB windows)
     launch_big_bn<MODE, A16, 64, 2, true>(p, st);
   } else if (bn == 256) {
