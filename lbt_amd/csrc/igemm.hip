@@ -500,9 +500,9 @@ LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 // 16-bit codes at BN 64: 142 -> 128 VGPRs (20 bytes of spill), two workgroups per CU: l1_c2 dgrad16
 // 170.6 -> 155.6 us, the other shapes unchanged (profiles/r04l_ab probe_*.txt); A8 BN 128 at 3-4 stages
 // would spill 200+ bytes. HALO int8 at BN 64: 98 VGPRs, two per CU. The pass-A epilogues (BNA) at BN 64
-// fit 128 VGPRs with one BN; with two (BNA 3, the projection blocks) one workgroup per CU.
+// fit 128 VGPRs (78 KiB of LDS: two workgroups per CU).
 #ifndef LBT_BIG_OCC
-#define LBT_BIG_OCC(A16, BN, S, HALO, BNA) (((A16 && BN == 64 && !HALO && BNA != 3) || (!A16 && HALO && BN == 64)) ? 4 : 1)
+#define LBT_BIG_OCC(A16, BN, S, HALO, BNA) (((A16 && BN == 64 && !HALO) || (!A16 && HALO && BN == 64)) ? 4 : 1)
 #endif
 // BN pass A (bn_wide.hip bn_bwd_a_wide_kernel) on the dgrad accumulators, element for element.
 // MA = 1 (lbt_dgrad_bna): dx -> ReLU mask recomputed from R -> the BN's two quantisers. MA = 2, 3
@@ -569,133 +569,115 @@ LBT_DEV void passa_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const 
   const int c0 = n0 + 4 * cq;
   const int pix = pb * 16 + pl;
   const bool pv = pix < hw;
-  BnaBn bn[NB];
-  bn[0] = bna_bn<MA, 0>(p);
-  if constexpr (NB == 2) bn[1] = bna_bn<MA, 1>(p);
-  float gam[NB][4], bet[4] = {0.f, 0.f, 0.f, 0.f};
-  Noise4 u1[NB], u2[NB];
-  QState srg[NB], sng[NB];
-  const uint64_t blk = ((uint64_t)(pv ? pix : 0) * (uint32_t)C + (uint32_t)c0) >> 2;
-#pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    srg[k] = qstate(bn[k].qrg);
-    sng[k] = qstate(bn[k].qng);
-    const float4 g4 = *reinterpret_cast<const float4*>(bn[k].gamma + c0);
-    gam[k][0] = g4.x; gam[k][1] = g4.y; gam[k][2] = g4.z; gam[k][3] = g4.w;
-    const Noise4 z{{0.f, 0.f, 0.f, 0.f}};
-    u1[k] = bn[k].qrg.stochastic ? qnoise4(bn[k].qrg, srg[k].step, blk) : z;
-    u2[k] = bn[k].qng.stochastic ? qnoise4(bn[k].qng, sng[k].step, blk) : z;
-  }
+  float bet[4] = {0.f, 0.f, 0.f, 0.f};
   float sr = 0.f;
   if constexpr (MA == 1) {
     const float4 b4 = *reinterpret_cast<const float4*>(p.bna.gb + C + c0);
     bet[0] = b4.x; bet[1] = b4.y; bet[2] = b4.z; bet[3] = b4.w;
     sr = qstate(p.bna.qr).inv_m;
   }
-  int sm[NB][4][4];  // [BN][sum][channel]
-#pragma unroll
-  for (int k = 0; k < NB; ++k)
-#pragma unroll
-    for (int a = 0; a < 4; ++a) sm[k][a][0] = sm[k][a][1] = sm[k][a][2] = sm[k][a][3] = 0;
-  int ov[NB][4];
-#pragma unroll
-  for (int k = 0; k < NB; ++k) ov[k][0] = ov[k][1] = ov[k][2] = ov[k][3] = 0;
+  const uint64_t blk = ((uint64_t)(pv ? pix : 0) * (uint32_t)C + (uint32_t)c0) >> 2;
   const int sbase = sb * 16 + sh * 8;
+  const int shard = (int)(tile % LBT_NSHARD);
+  const int wv = t >> 6;
+  int* red = reinterpret_cast<int*>(lds + kXBytes);  // [8 waves][4 sums][64 columns]
+  // one pass over the thread's samples per BN (the projection blocks' two BNs one after the other: the
+  // same registers)
+  auto bn_pass = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const BnaBn bn = bna_bn<MA, k>(p);
+    const QState srg = qstate(bn.qrg), sng = qstate(bn.qng);
+    const float4 g4 = *reinterpret_cast<const float4*>(bn.gamma + c0);
+    const float gam[4] = {g4.x, g4.y, g4.z, g4.w};
+    const Noise4 z{{0.f, 0.f, 0.f, 0.f}};
+    const Noise4 u1 = bn.qrg.stochastic ? qnoise4(bn.qrg, srg.step, blk) : z;
+    const Noise4 u2 = bn.qng.stochastic ? qnoise4(bn.qng, sng.step, blk) : z;
+    int sm[4][4];  // [sum][channel]
+#pragma unroll
+    for (int a = 0; a < 4; ++a) sm[a][0] = sm[a][1] = sm[a][2] = sm[a][3] = 0;
+    int ov[4] = {0, 0, 0, 0};
 #pragma unroll 2
-  for (int u = 0; u < 8; ++u) {
-    const int sm_ = sbase + u;
-    if (!pv || sm_ >= N) break;  // samples ascend: the rest of this thread's are outside too
-    const int64_t off = ((int64_t)sm_ * hw + pix) * C + c0;
-    const float4 xv = *reinterpret_cast<const float4*>(xs + pl * kXPix + (sh * 8 + u) * kXRow + 4 * cq);
-    float d[4] = {xv.x, xv.y, xv.z, xv.w};
-    char4 rv[NB], qv[NB];
+    for (int u = 0; u < 8; ++u) {
+      const int s_ = sbase + u;
+      if (!pv || s_ >= N) break;  // samples ascend: the rest of this thread's are outside too
+      const int64_t off = ((int64_t)s_ * hw + pix) * C + c0;
+      const float4 xv = *reinterpret_cast<const float4*>(xs + pl * kXPix + (sh * 8 + u) * kXRow + 4 * cq);
+      float d[4] = {xv.x, xv.y, xv.z, xv.w};
+      const char4 rv = *reinterpret_cast<const char4*>(bn.R + off);
+      const char4 qv = *reinterpret_cast<const char4*>(bn.qn + off);
+      const int R[4] = {rv.x, rv.y, rv.z, rv.w};
+      const int Q[4] = {qv.x, qv.y, qv.z, qv.w};
+      if constexpr (MA >= 2) {  // bn_wide.hip :123-138
+        const float4 g2 = *reinterpret_cast<const float4*>(p.bn3.g2 + off);
+        const uint32_t yb = p.bn3.y_bits[off >> 2];
+        d[0] = (yb & 1u) ? d[0] + g2.x : 0.f;
+        d[1] = (yb & 2u) ? d[1] + g2.y : 0.f;
+        d[2] = (yb & 4u) ? d[2] + g2.z : 0.f;
+        d[3] = (yb & 8u) ? d[3] + g2.w : 0.f;
+        if (k == 0 && p.bn3.gmask_out)
+          *reinterpret_cast<float4*>(p.bn3.gmask_out + off) = make_float4(d[0], d[1], d[2], d[3]);
+      } else {  // bn.hip chain_bwd_a's mask recomputation, op for op (bn_wide.hip :139-147)
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      rv[k] = *reinterpret_cast<const char4*>(bn[k].R + off);
-      qv[k] = *reinterpret_cast<const char4*>(bn[k].qn + off);
-    }
-    if constexpr (MA >= 2) {  // bn_wide.hip :123-138
-      const float4 g2 = *reinterpret_cast<const float4*>(p.bn3.g2 + off);
-      const uint32_t yb = p.bn3.y_bits[off >> 2];
-      d[0] = (yb & 1u) ? d[0] + g2.x : 0.f;
-      d[1] = (yb & 2u) ? d[1] + g2.y : 0.f;
-      d[2] = (yb & 4u) ? d[2] + g2.z : 0.f;
-      d[3] = (yb & 8u) ? d[3] + g2.w : 0.f;
-      if (p.bn3.gmask_out) *reinterpret_cast<float4*>(p.bn3.gmask_out + off) = make_float4(d[0], d[1], d[2], d[3]);
-    } else {  // bn.hip chain_bwd_a's mask recomputation, op for op (bn_wide.hip :139-147)
-      const int R[4] = {rv[0].x, rv[0].y, rv[0].z, rv[0].w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float xr = (float)R[c] * sr;
-        const float m1 = xr * gam[0][c];
-        const float yv = m1 + bet[c];
-        d[c] = yv > 0.f ? d[c] : 0.f;
+        for (int c = 0; c < 4; ++c) {
+          const float xr = (float)R[c] * sr;
+          const float m1 = xr * gam[c];
+          const float yv = m1 + bet[c];
+          d[c] = yv > 0.f ? d[c] : 0.f;
+        }
       }
-    }
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {  // bn_wide.hip :150-175
-      const int R[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
-      const int Q[4] = {qv[k].x, qv[k].y, qv[k].z, qv[k].w};
       int G[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int G2 = quant1(srg[k], bn[k].qrg.stochastic, d[c], u1[k].u[c], ov[k][0], ov[k][1]);
-        sm[k][0][c] += G2 * R[c];
-        sm[k][1][c] += G2;
-        const float gh = (float)G2 * srg[k].inv_m;
-        const float dd = gh * gam[k][c];
-        G[c] = quant1(sng[k], bn[k].qng.stochastic, dd, u2[k].u[c], ov[k][2], ov[k][3]);
-        sm[k][2][c] += G[c];
-        sm[k][3][c] += G[c] * Q[c];
+      for (int c = 0; c < 4; ++c) {  // bn_wide.hip :150-175
+        const int G2 = quant1(srg, bn.qrg.stochastic, d[c], u1.u[c], ov[0], ov[1]);
+        sm[0][c] += G2 * R[c];
+        sm[1][c] += G2;
+        const float gh = (float)G2 * srg.inv_m;
+        const float dd = gh * gam[c];
+        G[c] = quant1(sng, bn.qng.stochastic, dd, u2.u[c], ov[2], ov[3]);
+        sm[2][c] += G[c];
+        sm[3][c] += G[c] * Q[c];
       }
       short4 o;
       o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
-      *reinterpret_cast<short4*>(bn[k].gout + off) = o;
+      *reinterpret_cast<short4*>(bn.gout + off) = o;
     }
-  }
-  // ---- channel sums: the 4 pixel lanes of a wave sharing cq (shuffles), then the 8 waves in LDS
-  const int shard = (int)(tile % LBT_NSHARD);
-  const int wv = t >> 6;
-  int* red = reinterpret_cast<int*>(lds);  // [8 waves][NB][4 sums][64 columns]
-  __syncthreads();                         // the staged dx tile is read
-#pragma unroll
-  for (int k = 0; k < NB; ++k)
+    // channel sums: the 4 pixel lanes of a wave sharing cq (shuffles), the 8 waves in LDS
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        int v = sm[k][a][c];
+        int v = sm[a][c];
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        if ((t & 63) < 16) red[((wv * NB + k) * 4 + a) * 64 + 4 * cq + c] = v;
+        if ((t & 63) < 16) red[(wv * 4 + a) * 64 + 4 * cq + c] = v;
       }
-  // per-lane overflow counts -> wave totals -> lane 0
-#pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    const int a0 = wave_sum_i32(ov[k][0]), a1 = wave_sum_i32(ov[k][1]);
-    const int b0 = wave_sum_i32(ov[k][2]), b1 = wave_sum_i32(ov[k][3]);
+    // per-lane overflow counts -> wave totals -> lane 0
+    const int a0 = wave_sum_i32(ov[0]), a1 = wave_sum_i32(ov[1]);
+    const int b0 = wave_sum_i32(ov[2]), b1 = wave_sum_i32(ov[3]);
     if ((t & 63) == 0) {
-      if (bn[k].qrg.counts) {
-        int32_t* ct = bn[k].qrg.counts + ((int64_t)bn[k].qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (bn.qrg.counts) {
+        int32_t* ct = bn.qrg.counts + ((int64_t)bn.qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
         if (a0) atomicAdd(ct, a0);
         if (a1) atomicAdd(ct + 1, a1);
       }
-      if (bn[k].qng.counts) {
-        int32_t* ct = bn[k].qng.counts + ((int64_t)bn[k].qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (bn.qng.counts) {
+        int32_t* ct = bn.qng.counts + ((int64_t)bn.qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
         if (b0) atomicAdd(ct, b0);
         if (b1) atomicAdd(ct + 1, b1);
       }
     }
-  }
-  __syncthreads();
-  for (int x = t; x < NB * 4 * 64; x += kBT) {
-    const int k = x / 256, a = (x / 64) & 3, cl = x & 63;
-    long long v = 0;
+    __syncthreads();
+    if (t < 256) {
+      const int a = t >> 6, cl = t & 63;
+      long long v = 0;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) v += red[((w * NB + k) * 4 + a) * 64 + cl];
-    int64_t* dst = k == 0 ? bn[0].sums : bn[NB - 1].sums;
-    if (v) atomicAdd((unsigned long long*)&dst[(int64_t)shard * 4 * C + a * C + n0 + cl], (unsigned long long)v);
-  }
+      for (int w = 0; w < 8; ++w) v += red[(w * 4 + a) * 64 + cl];
+      if (v) atomicAdd((unsigned long long*)&bn.sums[(int64_t)shard * 4 * C + a * C + n0 + cl], (unsigned long long)v);
+    }
+    if (k + 1 < NB) __syncthreads();  // red is rewritten by the next BN's pass
+  };
+  bn_pass(std::integral_constant<int, 0>{});
+  if constexpr (NB == 2) bn_pass(std::integral_constant<int, 1>{});
 }
 
 // HALO (3x3, stride 1, pad 1: fwd, and the unit-stride dgrad of such a conv): the k loop runs
@@ -1120,7 +1102,8 @@ template <int MODE, bool A16, bool ADD, int BN, int S, int BNA, bool HALO>
 void big_go(const IgArgs& p, int64_t tiles, hipStream_t st) {
   constexpr int BM = 256, ROWB = A16 ? 128 : 64;
   constexpr size_t ring = HALO ? (size_t)2 * 384 * ROWB + (size_t)3 * BN * 64 : (size_t)S * (BM * ROWB + BN * 64);
-  constexpr size_t shm = (BNA && ring < (size_t)kXBytes) ? (size_t)kXBytes : ring;  // the staged dx tile
+  // the staged dx tile + the channel-sum exchange of the pass-A epilogue
+  constexpr size_t shm = (BNA && ring < (size_t)kXBytes + 8192) ? (size_t)kXBytes + 8192 : ring;
   static bool attr_ = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_big_kernel<MODE, A16, ADD, BN, S, BNA, HALO>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
@@ -1480,8 +1463,7 @@ extern "C" int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int
   const int64_t rows = (int64_t)d.N * d.H * d.W, inner = (int64_t)d.H * d.W * d.Cin;
   hipStream_t st = (hipStream_t)stream;
   static const int fuse = getenv_int("LBT_DGRAD_BNA", 1);
-  const bool tables = (!b.qrg.stochastic || b.qrg.noise) && (!b.qng.stochastic || b.qng.noise);
-  if (fuse && tables && d.SH == 1 && d.SW == 1 && d.Cout % kBK == 0 && d.Cin % 64 == 0 &&
+  if (fuse && d.SH == 1 && d.SW == 1 && d.Cout % kBK == 0 && d.Cin % 64 == 0 &&
       (int64_t)d.KH * d.KW * d.Cout * 255 * 128 < ((int64_t)1 << 31) &&
       (int64_t)d.N * d.Ho * d.Wo * d.Cout < ((int64_t)1 << 31) && (int64_t)ksd * 16 * d.Cin < ((int64_t)1 << 31) &&
       ksd * 16 >= d.KH * d.KW * d.Cout && rows * d.Cin < ((int64_t)1 << 31) && lbt_igemm_workspace_bytes(d, 1, 1) == 0) {
@@ -1507,17 +1489,15 @@ extern "C" int lbt_conv_dgrad_igemm_bn3(const int16_t* gq, const int8_t* wd, int
   if (!bn3 || !dx || !desc_ok(d)) return LBT_EINVAL;
   const lbt_dgrad_bn3& b = *bn3;
   if (!b.g2 || !b.y_bits || b.nbn < 1 || b.nbn > 2 || d.Cin % 4) return LBT_EINVAL;
-  bool tables = true;
   for (int k = 0; k < b.nbn; ++k) {
     const lbt_bna_bn& n = b.bn[k];
     if (!n.R || !n.gamma_q || !n.qn || !n.gout || !n.sums) return LBT_EINVAL;
     if (n.qrg.bits <= 0 || n.qrg.bits > 16 || n.qng.bits <= 0 || n.qng.bits > 16) return LBT_EINVAL;
-    tables = tables && (!n.qrg.stochastic || n.qrg.noise) && (!n.qng.stochastic || n.qng.noise);
   }
   const int64_t rows = (int64_t)d.N * d.H * d.W, inner = (int64_t)d.H * d.W * d.Cin;
   hipStream_t st = (hipStream_t)stream;
   static const int fuse = getenv_int("LBT_DGRAD_BN3", 1);
-  if (fuse && tables && d.SH == 1 && d.SW == 1 && d.Cout % kBK == 0 && d.Cin % 64 == 0 &&
+  if (fuse && d.SH == 1 && d.SW == 1 && d.Cout % kBK == 0 && d.Cin % 64 == 0 &&
       (int64_t)d.KH * d.KW * d.Cout * 255 * 128 < ((int64_t)1 << 31) &&
       (int64_t)d.N * d.Ho * d.Wo * d.Cout < ((int64_t)1 << 31) && (int64_t)ksd * 16 * d.Cin < ((int64_t)1 << 31) &&
       ksd * 16 >= d.KH * d.KW * d.Cout && rows * d.Cin < ((int64_t)1 << 31) && lbt_igemm_workspace_bytes(d, 1, 1) == 0) {
