@@ -155,7 +155,7 @@ class Xchg(ctypes.Structure):
 
 class IgemmTuning(ctypes.Structure):
     _fields_ = [("big", c_int32), ("min_tiles", c_int32), ("stages", c_int32), ("max_bn", c_int32),
-                ("halo", c_int32), ("pad", c_int32), ("launches", c_int64)]
+                ("halo", c_int32), ("fwdq_perm", c_int32), ("launches", c_int64)]
 
 
 class Update(ctypes.Structure):

@@ -73,6 +73,7 @@ struct IgArgs {
   // epilogue instead of storing dx (bna_epilogue)
   int has_bna;  // 1: bna (mask_r), 2: bn3 (g2 + y_bits, bn3.nbn BNs); sample-blocked row tiles (PERM)
   int npb;      // PERM: 16-pixel blocks per sample
+  int perm;     // sample-blocked row tiles (the pass-A epilogues, the PERM quantising forward epilogue)
   lbt_dgrad_bna bna;
   lbt_dgrad_bn3 bn3;
   int dbg;  // igemm_big_kernel diagnostics (LBT_IGEMM_BIG_DBG; 1: no operand loads after the prologue)
@@ -502,7 +503,8 @@ LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 // would spill 200+ bytes. HALO int8 at BN 64: 98 VGPRs, two per CU. The pass-A epilogues (BNA) at BN 64
 // fit 128 VGPRs (78 KiB of LDS: two workgroups per CU).
 #ifndef LBT_BIG_OCC
-#define LBT_BIG_OCC(A16, BN, S, HALO, BNA) (((A16 && BN == 64 && !HALO) || (!A16 && HALO && BN == 64)) ? 4 : 1)
+#define LBT_BIG_OCC(A16, BN, S, HALO, BNA) \
+  (((A16 && BN == 64 && !HALO) || (!A16 && HALO && BN == 64) || BNA == 4) ? 4 : 1)
 #endif
 // BN pass A (bn_wide.hip bn_bwd_a_wide_kernel) on the dgrad accumulators, element for element.
 // MA = 1 (lbt_dgrad_bna): dx -> ReLU mask recomputed from R -> the BN's two quantisers. MA = 2, 3
@@ -678,6 +680,97 @@ LBT_DEV void passa_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const 
   };
   bn_pass(std::integral_constant<int, 0>{});
   if constexpr (NB == 2) bn_pass(std::integral_constant<int, 1>{});
+}
+
+// The conv-output quantiser (Normalization_q's input, quant_epilogue's arithmetic) on sample-blocked
+// tiles (BNA 4): per 64-column half, the dequantised tile is staged in LDS as for passa_epilogue, then a
+// thread owns (pixel, 4 channels), draws that position's noise once (table or Philox) and walks 8
+// samples -- int8 codes stored as coalesced char4 runs, exact channel sums (sum q, sum q^2) in
+// registers, one int64 atomic per (column, sum) per workgroup (quant_epilogue: per column per wave).
+template <int MI, int NJ, int WM, int BN>
+LBT_DEV void quantq_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4i (&accw)[NJ], int u8, float scale,
+                             int sb, int pb, int n0, int r, int q, int wm, int wn, uint32_t tile, int8_t* lds) {
+  static_assert((BN == 64 && WM == 8 && MI == 2) || (BN == 128 && WM == 4 && MI == 4), "256 x 64 / 128 tiles");
+  const int C = p.ncol;
+  const int N = p.d.N;
+  const int hw = p.ch * p.cw;
+  const QState qs = qstate(p.qout);
+  const int st = p.qout.stochastic;
+  float* xs = reinterpret_cast<float*>(lds);
+  int* red = reinterpret_cast<int*>(lds + kXBytes);  // [8 waves][2 sums][64 columns]
+  const int t = threadIdx.x;
+  const int cq = t & 15, pl = (t >> 4) & 15, sh = t >> 8, wv = t >> 6;
+  const int pix = pb * 16 + pl;
+  const bool pv = pix < hw;
+  const int sbase = sb * 16 + sh * 8;
+  const int shard = (int)(tile % LBT_NSHARD);
+  int ov1 = 0, ov2 = 0;
+  __syncthreads();  // every wave's last fragment reads of the LDS ring are done
+#pragma unroll
+  for (int h = 0; h < BN / 64; ++h) {
+    if (wn == h) {  // this half's waves stage their rows: pixel MI wm + i, samples 4 q + e, column 16 j + r
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int wsum = accw[j][0];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            xs[(wm * MI + i) * kXPix + (4 * q + e) * kXRow + j * 16 + r] = (float)(acc[i][j][e] + u8 * wsum) * scale;
+      }
+    }
+    __syncthreads();
+    const int c0 = n0 + h * 64 + 4 * cq;
+    const uint64_t blk = ((uint64_t)(pv ? pix : 0) * (uint32_t)C + (uint32_t)c0) >> 2;
+    Noise4 u = {{0.f, 0.f, 0.f, 0.f}};
+    if (st) u = qnoise4(p.qout, qs.step, blk);
+    int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+#pragma unroll 2
+    for (int k = 0; k < 8; ++k) {
+      const int sm = sbase + k;
+      if (!pv || sm >= N) break;  // samples ascend
+      const int64_t off = ((int64_t)sm * hw + pix) * C + c0;
+      const float4 xv = *reinterpret_cast<const float4*>(xs + pl * kXPix + (sh * 8 + k) * kXRow + 4 * cq);
+      const float x[4] = {xv.x, xv.y, xv.z, xv.w};
+      int c[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        c[e] = quant1(qs, st, x[e], u.u[e], ov1, ov2);
+        s1[e] += c[e];
+        s2[e] += c[e] * c[e];
+      }
+      *reinterpret_cast<char4*>(p.yq + off) = make_char4((char)c[0], (char)c[1], (char)c[2], (char)c[3]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      int a = s1[e], b = s2[e];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      if ((t & 63) < 16) {
+        red[(wv * 2 + 0) * 64 + 4 * cq + e] = a;
+        red[(wv * 2 + 1) * 64 + 4 * cq + e] = b;
+      }
+    }
+    __syncthreads();  // xs read and red written: the next half may restage
+    if (t < 128) {
+      const int a = t >> 6, cl = t & 63;
+      long long v = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += red[(w * 2 + a) * 64 + cl];
+      if (v)
+        atomicAdd((unsigned long long*)&p.chsum[(int64_t)shard * 2 * C + a * C + n0 + h * 64 + cl], (unsigned long long)v);
+    }
+    if (h + 1 < BN / 64) __syncthreads();  // red is rewritten by the next half
+  }
+  ov1 = wave_sum_i32(ov1);
+  ov2 = wave_sum_i32(ov2);
+  if ((t & 63) == 0 && p.qout.counts) {
+    int32_t* ct = p.qout.counts + ((int64_t)p.qout.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+    if (ov1) atomicAdd(ct, ov1);
+    if (ov2) atomicAdd(ct + 1, ov2);
+  }
 }
 
 // HALO (3x3, stride 1, pad 1: fwd, and the unit-stride dgrad of such a conv): the k loop runs
@@ -1056,13 +1149,18 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO, BNA)) void igemm
     }
   }
   const int u8 = (!A16 && p.a_u8off) ? 128 : 0;
+  if constexpr (BNA == 4) {
+    if constexpr (MODE == MODE_FWD && !A16)
+      quantq_epilogue<MI, NJ, WM, BN>(p, acc[0], accw, u8, scale, sb, pb, n0, r, q, wm, wn, tile, lds);
+    return;
+  }
   if constexpr (MODE == MODE_FWD && !A16) {
     if (p.yq) {  // uniform: quantising epilogue
       quant_epilogue<MI, NJ>(p, acc[0], accw, u8, scale, rtile, rlim, full, cw, r, q);
       return;
     }
   }
-  if constexpr (BNA >= 1) {
+  if constexpr (BNA >= 1 && BNA <= 3) {
     if constexpr (BN == 64) passa_epilogue<MI, NJ, WM, BN, BNA>(p, acc, accw, scale, sb, pb, n0, r, q, wm, tile, lds);
     return;
   }
@@ -1118,12 +1216,19 @@ template <int MODE, bool A16, int BN, int S, bool HALO = false>
 void launch_big_bn(IgArgs p, hipStream_t st) {
   static const int dbg = getenv_int("LBT_IGEMM_BIG_DBG", 0);
   p.dbg = dbg;
-  const int64_t rtiles = p.has_bna ? (int64_t)((p.d.N + 15) / 16) * p.npb : (p.M + 255) / 256;
+  // sample-blocked tiles only for the instantiations that decode them (the kernel's PERM)
+  const bool qperm = MODE == MODE_FWD && !A16 && BN <= 128 && S == 2 && !HALO && p.perm && p.yq;
+  const bool bna = MODE == MODE_DGRAD && A16 && BN == 64 && !HALO && p.has_bna;
+  if (!qperm && !bna) p.perm = 0;
+  const int64_t rtiles = p.perm ? (int64_t)((p.d.N + 15) / 16) * p.npb : (p.M + 255) / 256;
   const int64_t tiles = rtiles * (p.ncol / BN);
   if constexpr (MODE == MODE_DGRAD && A16 && BN == 64 && !HALO) {
     if (p.has_bna == 1) return big_go<MODE, A16, false, BN, S, 1, HALO>(p, tiles, st);
     if (p.has_bna == 2 && p.bn3.nbn == 1) return big_go<MODE, A16, false, BN, S, 2, HALO>(p, tiles, st);
     if (p.has_bna == 2) return big_go<MODE, A16, false, BN, S, 3, HALO>(p, tiles, st);
+  }
+  if constexpr (MODE == MODE_FWD && !A16 && BN <= 128 && S == 2 && !HALO) {
+    if (qperm) return big_go<MODE, A16, false, BN, S, 4, HALO>(p, tiles, st);
   }
   if (MODE == MODE_DGRAD && p.add_src) big_go<MODE, A16, MODE == MODE_DGRAD, BN, S, 0, HALO>(p, tiles, st);
   else big_go<MODE, A16, false, BN, S, 0, HALO>(p, tiles, st);
@@ -1141,7 +1246,7 @@ lbt_igemm_tuning& big_tuning() {
     v.stages = getenv_int("LBT_IGEMM_BIG_S", 2);
     v.max_bn = getenv_int("LBT_IGEMM_BIG_BN256", 0) ? 256 : 128;
     v.halo = getenv_int("LBT_IGEMM_HALO", 1);  // bit 0: int8 codes (fwd), bit 1: 16-bit codes (dgrad16)
-    v.pad = 0;
+    v.fwdq_perm = getenv_int("LBT_FWDQ_PERM", 1);
     v.launches = 0;
     return v;
   }();
@@ -1158,7 +1263,7 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
   if ((p.M + 255) / 256 * (p.ncol / 64) > 0x7fffffff) return false;
   // column tile: the widest (<= max_bn) that still gives min_tiles tiles (256 only without the
   // quantising epilogue and on request: its 8 x 4 accumulator tiles per wave spill)
-  const int64_t mt = p.has_bna ? (int64_t)((p.d.N + 15) / 16) * p.npb : (p.M + 255) / 256;
+  const int64_t mt = p.perm ? (int64_t)((p.d.N + 15) / 16) * p.npb : (p.M + 255) / 256;
   int bn = 0;
   if (!A16 && !p.yq && p.ncol % 256 == 0 && tu.max_bn >= 256 && mt * (p.ncol / 256) >= tmin) bn = 256;
   else if (tu.max_bn >= 128 && p.ncol % 128 == 0 && mt * (p.ncol / 128) >= tmin) bn = 128;
@@ -1173,7 +1278,7 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
   // 3x3 / stride 1 / pad 1 with every tap (fwd, unit-stride dgrad) and W <= 63: the A window per
   // channel block (HALO), 64- and 128-column tiles
   const lbt_conv_desc& d = p.d;
-  const bool halo = (tu.halo & (A16 ? 2 : 1)) && !p.has_bna && bn <= 128 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
+  const bool halo = (tu.halo & (A16 ? 2 : 1)) && !p.perm && bn <= 128 && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
                     d.PL == 1 && d.Ho == d.H && d.Wo == d.W && p.nkh == 3 && p.nkw == 3 && p.kh0 == 0 &&
                     p.kw0 == 0 && p.cw == d.W && p.ch == d.H && d.W <= 63 &&
                     // where it measured faster (profiles/r04p): one column tile (the window is not
@@ -1361,6 +1466,9 @@ extern "C" int lbt_conv_fwd_igemm_q(const void* xq, int32_t a_kind, const int8_t
   p.ksplit = 1;
   all_taps(p, MODE_FWD);
   p.yq = yq; p.qout = qout; p.chsum = chsum; p.hw = d.Ho * d.Wo;
+  // the 256-row kernel's quantising epilogue on sample-blocked tiles (quantq_epilogue)
+  p.perm = big_tuning().fwdq_perm ? 1 : 0;
+  p.npb = (d.Ho * d.Wo + 15) / 16;
   return launch<MODE_FWD, false>(p, (hipStream_t)stream);
 }
 
@@ -1386,6 +1494,7 @@ extern "C" int lbt_igemm_set_tuning(const lbt_igemm_tuning* t) {
   lbt_igemm_tuning& cur = big_tuning();
   cur.big = t->big; cur.min_tiles = t->min_tiles; cur.stages = t->stages; cur.max_bn = t->max_bn;
   cur.halo = t->halo;
+  cur.fwdq_perm = t->fwdq_perm;
   return 0;
 }
 
@@ -1473,6 +1582,7 @@ extern "C" int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int
     p.ksplit = 1;
     all_taps(p, MODE_DGRAD);
     p.has_bna = 1;
+    p.perm = 1;
     p.npb = (d.H * d.W + 15) / 16;
     p.bna = b;
     if (launch_big<MODE_DGRAD, true>(p, st)) return (int)hipGetLastError();
@@ -1507,6 +1617,7 @@ extern "C" int lbt_conv_dgrad_igemm_bn3(const int16_t* gq, const int8_t* wd, int
     p.ksplit = 1;
     all_taps(p, MODE_DGRAD);
     p.has_bna = 2;
+    p.perm = 1;
     p.npb = (d.H * d.W + 15) / 16;
     p.bn3 = b;
     if (launch_big<MODE_DGRAD, true>(p, st)) return (int)hipGetLastError();

@@ -141,18 +141,20 @@ def test_big_quantising_epilogue_matches_fwd_then_quantize(N, H, Cin, Cout, k, a
     q_ref = ops.quantize(y, qo, OUT_I8, chsum=cs_ref, C=Cout)
     cnt_ref = ctx.counts_view()[qo.slot].sum(0).cpu()
     assert cnt_ref[0] > 0 and cnt_ref[1] > cnt_ref[0]
-    # the quantising epilogue never takes the 256-column tile
-    for (stages, max_bn), halo in [(v, h) for v in VARIANTS[:-1] for h in (0, 3)]:
+    # the quantising epilogue never takes the 256-column tile; fwdq_perm: the sample-blocked, LDS-staged
+    # form (2 stages), else quant_epilogue on row-major tiles (every ring depth, halo on and off)
+    cases = [(v, h, 0) for v in VARIANTS[:-1] for h in (0, 3)] + [((2, mb), 0, 1) for mb in (64, 128)]
+    for (stages, max_bn), halo, perm in cases:
         ctx.counts.zero_()
         cs = torch.zeros_like(cs_ref)
         yq = torch.full(q_ref.shape, 99, dtype=torch.int8, device=DEV)
         n0 = _launches()
-        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo):
+        with ops.igemm_forced(big=1, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo, fwdq_perm=perm):
             ops.conv_fwd_igemm_q(x, a_kind, wf, ksf, d, qx.desc, qw.desc, yq, qo, cs)
         assert _launches() == n0 + 1, "the 256-row kernel did not run"
-        assert torch.equal(yq, q_ref), (stages, max_bn, halo)
-        assert torch.equal(ctx.counts_view()[qo.slot].sum(0).cpu(), cnt_ref), (stages, max_bn, halo)
-        assert torch.equal(cs.view(NSHARD, -1).sum(0), cs_ref.view(NSHARD, -1).sum(0)), (stages, max_bn, halo)
+        assert torch.equal(yq, q_ref), (stages, max_bn, halo, perm)
+        assert torch.equal(ctx.counts_view()[qo.slot].sum(0).cpu(), cnt_ref), (stages, max_bn, halo, perm)
+        assert torch.equal(cs.view(NSHARD, -1).sum(0), cs_ref.view(NSHARD, -1).sum(0)), (stages, max_bn, halo, perm)
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k", [
