@@ -242,18 +242,35 @@ struct WideB {
 
 __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
   __shared__ float s_mg[kCB], s_mgx[kCB];
+  __shared__ long long s_part[2][kT / kCB][kCB];
   __shared__ int sh_cnt[2 * (kT / 64)];
   const int cq = threadIdx.x % kCQ;
   const int c0 = blockIdx.x * kCB + 4 * cq;
   const QState sgq = qstate(b.qng), sn = qstate(b.qn_q), so = qstate(b.qo);
   const bool quant = b.gq != nullptr;
+  {  // the pass-A shard sums of this workgroup's channels: every thread folds 32 / (kT / kCB) shards
+    constexpr int kParts = kT / kCB, kPer = LBT_NSHARD / kParts;
+    const int cl = threadIdx.x % kCB, part = threadIdx.x / kCB, c = blockIdx.x * kCB + cl;
+    long long SG = 0, SGQ = 0;
+    if (c < b.C) {
+#pragma unroll
+      for (int k = part * kPer; k < (part + 1) * kPer; ++k) {
+        SG += b.sums[(int64_t)k * 4 * b.C + 2 * b.C + c];
+        SGQ += b.sums[(int64_t)k * 4 * b.C + 3 * b.C + c];
+      }
+    }
+    s_part[0][part][cl] = SG;
+    s_part[1][part][cl] = SGQ;
+  }
+  __syncthreads();
   if (threadIdx.x < kCB && blockIdx.x * kCB + (int)threadIdx.x < b.C) {
     // bn.hip chain_bwd_b's moment prologue, for this workgroup's channels
     const int c = blockIdx.x * kCB + threadIdx.x;
     long long SG = 0, SGQ = 0;
-    for (int k = 0; k < LBT_NSHARD; ++k) {
-      SG += b.sums[(int64_t)k * 4 * b.C + 2 * b.C + c];
-      SGQ += b.sums[(int64_t)k * 4 * b.C + 3 * b.C + c];
+#pragma unroll
+    for (int k = 0; k < kT / kCB; ++k) {
+      SG += s_part[0][k][threadIdx.x];
+      SGQ += s_part[1][k][threadIdx.x];
     }
     const double s = (double)sn.inv_m, gsc = (double)sgq.inv_m, n = (double)b.n;
     const float m = b.ms[c], sig = b.ms[b.C + c];

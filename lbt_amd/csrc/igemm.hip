@@ -536,6 +536,9 @@ LBT_DEV BnaBn bna_bn(const IgArgs& p) {
     return BnaBn{b.qrg, b.qng, b.R, b.qn, b.gamma_q, b.gout, b.sums};
   }
 }
+#ifndef LBT_EPI_UNROLL
+#define LBT_EPI_UNROLL 2  // samples a thread of the staged epilogues has in flight
+#endif
 constexpr int kXRow = 68;                // floats per (pixel, sample) row of the staged dx tile
 constexpr int kXPix = 16 * kXRow + 4;    // floats per pixel: 16 samples + 4 (bank offset per pixel)
 constexpr int kXBytes = 16 * kXPix * 4;  // 69 888 bytes
@@ -598,7 +601,7 @@ LBT_DEV void passa_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const 
 #pragma unroll
     for (int a = 0; a < 4; ++a) sm[a][0] = sm[a][1] = sm[a][2] = sm[a][3] = 0;
     int ov[4] = {0, 0, 0, 0};
-#pragma unroll 2
+#pragma unroll LBT_EPI_UNROLL
     for (int u = 0; u < 8; ++u) {
       const int s_ = sbase + u;
       if (!pv || s_ >= N) break;  // samples ascend: the rest of this thread's are outside too
@@ -725,7 +728,7 @@ LBT_DEV void quantq_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4
     Noise4 u = {{0.f, 0.f, 0.f, 0.f}};
     if (st) u = qnoise4(p.qout, qs.step, blk);
     int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-#pragma unroll 2
+#pragma unroll LBT_EPI_UNROLL
     for (int k = 0; k < 8; ++k) {
       const int sm = sbase + k;
       if (!pv || sm >= N) break;  // samples ascend
