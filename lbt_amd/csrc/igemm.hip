@@ -537,7 +537,7 @@ LBT_DEV BnaBn bna_bn(const IgArgs& p) {
   }
 }
 #ifndef LBT_EPI_UNROLL
-#define LBT_EPI_UNROLL 2  // samples a thread of the staged epilogues has in flight
+#define LBT_EPI_UNROLL 8  // samples a thread of the staged epilogues has in flight (2: 1.1x slower, 4: spills; profiles/r04u)
 #endif
 constexpr int kXRow = 68;                // floats per (pixel, sample) row of the staged dx tile
 constexpr int kXPix = 16 * kXRow + 4;    // floats per pixel: 16 samples + 4 (bank offset per pixel)
