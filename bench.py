@@ -295,6 +295,8 @@ def main():
             xs, ys = synthetic_batches(4, args.batch, seed=1000 + rank, device=device)
     trainer = Trainer(model, lr=1e-2, momentum=0.9, batch_size=args.batch, use_graph=not args.eager)
     trainer.init_model()
+    for x_, y_ in zip(xs, ys):  # every batch buffer's graph captured before the warm-up and timed steps
+        trainer.prepare(x_, y_)
 
     el = _timed_region(lambda i: trainer.step(xs[i % 4], ys[i % 4]), args.steps, args.warmup, world,
                        torch.cuda.synchronize, device)

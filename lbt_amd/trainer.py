@@ -311,6 +311,20 @@ class Trainer:
             self._warmup(X, y)  # every plan's first run allocates its buffers outside a capture
         return self._capture_step(X, y)
 
+    def prepare(self, X, y):
+        """Build (capture) the step's graph for this batch buffer pair without running a step -- setup
+        before a timed loop, so that no capture lands inside it whatever the warm-up count (a loader's
+        ring of batch buffers gets one graph per buffer, on its first step otherwise)."""
+        self._active = self._plan(X.shape[0])
+        if not self.use_graph or (getattr(self.model, "sync_bn", False) and not self.capture_comm):
+            return
+        key = (X.data_ptr(), y.data_ptr(), tuple(X.shape))
+        if getattr(self.model, "binds_inputs", False):
+            if key not in self._gcache and len(self._gcache) < 8:
+                self._gcache[key] = self._capture_bound(X, y)
+        elif self._graphs is None or self._static is None or self._static[0].shape != X.shape:
+            self._capture(X, y)
+
     def step(self, X, y):
         """One training step on batch (X [B,32,32,3] fp32 NHWC, y [B] int32), device tensors.
         A SyncBN plan holds collectives inside the step: captured with them (RCCL), else eager."""

@@ -272,3 +272,29 @@ def test_evaluate_before_training_keeps_element_counts():
         for k in gp:
             assert np.array_equal(gp[k], state["params"][k]), (i, k)
         assert ctx.ranges() == state["ranges"], i
+
+
+@pytest.mark.gpu
+def test_prepare_captures_every_batch_graph_and_changes_nothing():
+    """Trainer.prepare (bench.py's setup: no graph capture may land in a timed loop, whatever the
+    warm-up count) captures one graph per batch buffer up front; the steps that follow replay them
+    (no further capture) and are bit-identical to a trainer that captured on the fly."""
+    rng = np.random.default_rng(5)
+    xs = [torch.from_numpy(((rng.integers(0, 256, size=(16, 32, 32, 3)) - 127.5) / 128).astype(F32)).to(DEV)
+          for _ in range(3)]
+    ys = [torch.from_numpy(rng.integers(0, 10, size=16).astype(np.int32)).to(DEV) for _ in range(3)]
+    ctx_a, gm_a, tr_a = _fused_trainer(5, 16)
+    ctx_b, gm_b, tr_b = _fused_trainer(5, 16)
+    for x, y in zip(xs, ys):
+        tr_a.prepare(x, y)
+    n_graphs = len(tr_a._gcache)
+    assert n_graphs == 3
+    for i in range(5):
+        la = tr_a.step(xs[i % 3], ys[i % 3]).item()
+        lb = tr_b.step(xs[i % 3], ys[i % 3]).item()
+        assert la == lb, i
+    assert len(tr_a._gcache) == n_graphs
+    pa, pb = _params_of(gm_a), _params_of(gm_b)
+    for k in pa:
+        assert np.array_equal(pa[k], pb[k]), k
+    assert ctx_a.ranges() == ctx_b.ranges()
