@@ -346,13 +346,19 @@ int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const void* g, in
  * if run_mean != NULL, the running averages avg = momentum*avg + one_minus_momentum*x
  * (:601-612).
  * frozen != 0: the testing branch of the tf.cond (:590-600, set_testing, models.py:15): mu and
- * var are the running averages (chsum unused), sigma = sqrtf(run_var + eps), nothing updated.  */
+ * var are the running averages (chsum unused), sigma = sqrtf(run_var + eps), nothing updated.
+ * ms_in != 0 (lbt_bn_chain_fwd only): ms already holds this step's [mu | sigma] (lbt_bn_moments ran
+ * on this descriptor): the chain reads its channels' two floats instead of reducing the sums in
+ * every workgroup, and updates nothing.                                                          */
 typedef struct lbt_bn_norm {
   const int8_t* q; lbt_qdesc qn; const int64_t* chsum; int64_t n;
   float eps, momentum, one_minus_momentum;
   float* ms; float* run_mean; float* run_var;
-  int32_t frozen;
+  int32_t frozen, ms_in;
 } lbt_bn_norm;
+/* The moments above, once: ms = [mu | sigma] and the running averages (the first-workgroup writes of
+ * the chains), one thread per channel. Bit-identical to what the chains compute.                  */
+int lbt_bn_moments(const lbt_bn_norm* nrm, int32_t C, void* stream);
 
 /* One branch of the forward element chain:
  *   v = xin[e]                          if nrm.q == NULL

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -42,7 +42,8 @@ class ConvDesc(ctypes.Structure):
 class BnNorm(ctypes.Structure):
     _fields_ = [("q", c_void_p), ("qn", QDesc), ("chsum", c_void_p), ("n", c_int64),
                 ("eps", c_float), ("momentum", c_float), ("one_minus_momentum", c_float),
-                ("ms", c_void_p), ("run_mean", c_void_p), ("run_var", c_void_p), ("frozen", c_int32)]
+                ("ms", c_void_p), ("run_mean", c_void_p), ("run_var", c_void_p), ("frozen", c_int32),
+                ("ms_in", c_int32)]
 
 
 class ChainBranch(ctypes.Structure):
@@ -208,6 +209,7 @@ _SIGS = {
     "lbt_conv_dgrad_igemm_ws": [_P, c_int32, _P, c_int32, ConvDesc, QDesc, QDesc, _P, _P, _P, c_int64, _P],
     "lbt_conv_dgrad_igemm_bna": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, ctypes.POINTER(DgradBna), _P, _P, c_int64,
                                  _P],
+    "lbt_bn_moments": [ctypes.POINTER(BnNorm), c_int32, _P],
     "lbt_conv_dgrad_igemm_bn3": [_P, _P, c_int32, ConvDesc, QDesc, QDesc, ctypes.POINTER(DgradBn3), _P, _P, c_int64,
                                  _P],
     "lbt_conv_wgrad_igemm_store": [_P, _P, c_int32, ConvDesc, _P, c_int32, _P],

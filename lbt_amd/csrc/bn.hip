@@ -131,6 +131,13 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
   const Noise4 no1 = noise_for(a.qo1, so1, gl);
   const Noise4 no2 = noise_for(a.qo2, so2, gl);
 
+  // ms_in (lbt_bn_moments ran): every branch's [mu | sigma] is in nrm.ms -- no LDS, no moment prologue
+  bool msall = true;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
+    msall = msall && (!q_in[b] || Bb.nrm.ms_in);
+  }
   float sn[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -139,26 +146,36 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
     sn[b] = 0.f;
     if (q_in[b]) {
       sn[b] = qscale(Bb.nrm.qn);
-      bn_moments(Bb.nrm, C, P, P + C, tmp);
-      __syncthreads();
+      if (!msall) {
+        bn_moments(Bb.nrm, C, P, P + C, tmp);
+        __syncthreads();
+      }
     }
-    if (qr[b].active)
+    if (qr[b].active && !msall)
       for (int c = threadIdx.x; c < C; c += kThreads) { P[2 * C + c] = Bb.gb[c]; P[3 * C + c] = Bb.gb[C + c]; }
   }
-  __syncthreads();
+  if (!msall) __syncthreads();
   LBT_TS(1);
   // this thread's channel quad is fixed: its per-channel constants live in registers
   float pm[NB][4], pg[NB][4], pb[NB][4];
   Recip ps[NB][4];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
+    const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
     const float* P = shf + 4 * C * b;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      pm[b][k] = P[c0 + k];
-      ps[b][k] = recip(P[C + c0 + k]);
-      pg[b][k] = P[2 * C + c0 + k];
-      pb[b][k] = P[3 * C + c0 + k];
+      if (msall) {
+        pm[b][k] = q_in[b] ? Bb.nrm.ms[c0 + k] : 0.f;
+        ps[b][k] = recip(q_in[b] ? Bb.nrm.ms[C + c0 + k] : 1.f);
+        pg[b][k] = qr[b].active ? Bb.gb[c0 + k] : 0.f;
+        pb[b][k] = qr[b].active ? Bb.gb[C + c0 + k] : 0.f;
+      } else {
+        pm[b][k] = P[c0 + k];
+        ps[b][k] = recip(P[C + c0 + k]);
+        pg[b][k] = P[2 * C + c0 + k];
+        pb[b][k] = P[3 * C + c0 + k];
+      }
     }
   }
   // ... and as channel pairs for the packed math
@@ -667,6 +684,50 @@ void allow_shm(K kernel, size_t shm) {
 
 }  // namespace
 
+namespace {
+// lbt_bn_moments: bn_moments' arithmetic (bn_moments.h), one thread per channel
+__global__ __launch_bounds__(256) void bn_moments_kernel(lbt_bn_norm b, int C) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  if (b.frozen) {
+    const float m = b.run_mean[c], sigma = sqrtf(b.run_var[c] + b.eps);
+    b.ms[c] = m;
+    b.ms[C + c] = sigma;
+    return;
+  }
+  long long v1[LBT_NSHARD], v2[LBT_NSHARD];
+#pragma unroll
+  for (int k = 0; k < LBT_NSHARD; ++k) {
+    v1[k] = b.chsum[(int64_t)k * 2 * C + c];
+    v2[k] = b.chsum[(int64_t)k * 2 * C + C + c];
+  }
+  long long s1 = 0, s2 = 0;
+#pragma unroll
+  for (int k = 0; k < LBT_NSHARD; ++k) {
+    s1 += v1[k];
+    s2 += v2[k];
+  }
+  const double s = ldexp(1.0, -frac_exp(b.qn));
+  const double mean_d = (double)s1 * s / (double)b.n;
+  const double var_d = (double)s2 * (s * s) / (double)b.n - mean_d * mean_d;
+  const float m = (float)mean_d, v = (float)var_d;
+  const float sigma = sqrtf(v + b.eps);
+  b.ms[c] = m;
+  b.ms[C + c] = sigma;
+  if (b.run_mean) {
+    b.run_mean[c] = b.momentum * b.run_mean[c] + b.one_minus_momentum * m;
+    b.run_var[c] = b.momentum * b.run_var[c] + b.one_minus_momentum * v;
+  }
+}
+}  // namespace
+
+extern "C" int lbt_bn_moments(const lbt_bn_norm* nrm, int32_t C, void* stream) {
+  if (!nrm || C <= 0 || !nrm->ms || (nrm->frozen ? (!nrm->run_mean || !nrm->run_var) : !nrm->chsum)) return LBT_EINVAL;
+  hipLaunchKernelGGL(bn_moments_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *nrm,
+                     (int)C);
+  return (int)hipGetLastError();
+}
+
 LBT_TRACE_SETTER(bn)
 
 // ---- host-side variant selection (flag words: chain_flags.h)
@@ -681,7 +742,11 @@ extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   dim3 grid;
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
-  const size_t shm = sizeof(float) * 8 * a->C + sizeof(long long) * 2 * a->C;
+  // moments precomputed (nrm.ms_in) on every normalising branch: no dynamic LDS (the 48 C bytes of the
+  // in-kernel reduction held wide layers to 1-3 workgroups per CU)
+  const bool msall = (!a->b1.nrm.q || a->b1.nrm.ms_in) && (!a->has_b2 || !a->b2.nrm.q || a->b2.nrm.ms_in);
+  if ((a->b1.nrm.ms_in && !a->b1.nrm.ms) || (a->has_b2 && a->b2.nrm.ms_in && !a->b2.nrm.ms)) return LBT_EINVAL;
+  const size_t shm = msall ? 0 : sizeof(float) * 8 * a->C + sizeof(long long) * 2 * a->C;
   hipStream_t st = (hipStream_t)stream;
   const int f = fwd_flags(*a);
 #define LBT_CF(NB, FL)                                                                            \

@@ -74,6 +74,8 @@ DGRAD_BNA = os.environ.get("LBT_DGRAD_BNA_PY", "1") != "0"
 # ... and bn3 (+ the projection shortcut's BN) pass A inside the NEXT block's conv-1 dgrad
 # (ops.conv_dgrad_igemm_bn3): the next block hands back _DgradIn instead of its conv-1 dx
 DGRAD_BN3 = os.environ.get("LBT_DGRAD_BN3_PY", "1") != "0"
+# ... and the forward chains read their BN's moments from one lbt_bn_moments launch (nrm.ms_in)
+CHAIN_MS = os.environ.get("LBT_CHAIN_MS", "1") != "0"
 
 
 class _DgradIn:
@@ -1091,6 +1093,9 @@ class ResidualBottleneck_q(ResidualBlock_q):
             r.quantize_params()
             r.X_range.observe(y.numel())
             br.nrm = n.norm_desc(n.q, n._chsum, n.n)
+            if CHAIN_MS:  # the BN's moments once (one thread per channel), not in every chain workgroup
+                ops.bn_moments(br.nrm, y.shape[-1])
+                br.nrm.ms_in = 1
             br.qr = r.X_range.desc
             br.rout = r.R.data_ptr()
             br.gb = r.gb.data_ptr()

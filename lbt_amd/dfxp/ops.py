@@ -391,6 +391,12 @@ def _chain_bwd_b_bytes(a):
     return (2 + (4 if a.dx else 0) + (1 if a.gq else 0)) * a.rows * a.inner
 
 
+def bn_moments(nrm, C):
+    """Normalization_q's batch moments once (lbt_bn_moments): nrm.ms = [mu | sigma], running averages."""
+    with _Timed("bn_moments_kernel", 2 * NSHARD * 2 * C * 8 + 8 * C):
+        call("lbt_bn_moments", _lib.ctypes.byref(nrm), int(C), stream())
+
+
 def chain_fwd(desc):
     with _Timed("chain_fwd_kernel", _chain_fwd_bytes(desc)):
         call("lbt_bn_chain_fwd", _lib.ctypes.byref(desc), stream())
