@@ -19,6 +19,8 @@
 // B[k = 8*(l>>4) + j][col l&15], j = 0..7; C/D: col = l&15, row = 4*(l>>4) + reg.
 #include "dfxp_device.h"
 
+#include <cstdlib>
+
 using namespace lbt;
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -256,6 +258,163 @@ __global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t
   }
 }
 
+// Weight gradient on output-row chunks (round 4): a chunk is 64 consecutive output pixels of ONE output
+// row (n, oy, 64 xc ..); its input window (KH rows x (63 SW + KW) columns x Cin) is staged in LDS as fp16
+// once and every patch element -- all K, one 16-row k-tile per wave, up to kRwMaxKT waves -- reads its A
+// fragment from it (stem_wide_wgrad_kernel gathers every patch element of every pixel from global
+// memory, 64 addresses per load instruction, and re-reads the gradient rows once per 64-row k-block of
+// grid.y). Always kRwMaxKT waves: they all stage the window (the k-tiles past K multiply zeros). The next chunk's window and gradient rows are loaded into registers while the current chunk's
+// MFMAs run. Same exact arithmetic: fp16 operands, fp32 partial sums flushed to int32 every kFlush
+// steps, 256 hi + lo into int64 per split.
+constexpr int kRwMaxKT = 10;   // k-tiles (K <= 160)
+constexpr int kRwMaxKH = 7;    // window rows
+constexpr int kRwMaxWC = 136;  // window columns 63 SW + KW
+constexpr int kRwMaxCin = 4;
+constexpr int kRwWin = kRwMaxKH * kRwMaxWC * kRwMaxCin;
+constexpr int kRwWpt = (kRwWin + 64 * kRwMaxKT - 1) / (64 * kRwMaxKT);  // window elements a thread stages (at 10 waves)
+
+template <bool G16, int NCT>
+__global__ __launch_bounds__(64 * kRwMaxKT) void stem_wgrad_rows_kernel(const int16_t* __restrict__ x,
+                                                                        const void* __restrict__ g_, lbt_conv_desc d,
+                                                                        int K, int64_t cper, int64_t nchunks, int xc,
+                                                                        int64_t* __restrict__ slab) {
+  constexpr int NH = G16 ? 2 : 1;
+  constexpr int GV = NCT * 2;  // 16-byte (G16) / 8-byte gradient pieces per pixel (8 channels each)
+  __shared__ __attribute__((aligned(16))) _Float16 sG[NH][NCT * 16][kWgChunk + 8];
+  __shared__ _Float16 sW[kRwWin];
+  const int nthr = blockDim.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int k = wave * 16 + r;
+  const int code = k < K ? patch_code(d, k) : -1;
+  const int dy = code >> 20, dx = (code >> 10) & 1023, ci = code & 1023;
+  const int WC = 63 * d.SW + d.KW, wsz = d.KH * WC * d.Cin;
+  const int aoff = code >= 0 ? (dy * WC + dx) * d.Cin + ci : 0;  // + px * SW * Cin
+  const int astep = d.SW * d.Cin;
+  f4v facc[NH][NCT];
+  int iacc[NH][NCT][4];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      facc[h][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) iacc[h][ct][i] = 0;
+    }
+  const int64_t cb = (int64_t)blockIdx.x * cper;
+  const int64_t ce = cb + cper < nchunks ? cb + cper : nchunks;
+  // one chunk's operands in registers: window elements threadIdx.x + j * nthr, gradient piece threadIdx.x
+  int wv[kRwWpt];
+  int gw[4];
+  auto load = [&](int64_t c) {
+    const int xcc = (int)(c % xc);
+    const int64_t t = c / xc;
+    const int oy = (int)(t % d.Ho), n = (int)(t / d.Ho);
+    const int iy0 = oy * d.SH - d.PT, ix0 = xcc * 64 * d.SW - d.PL;
+#pragma unroll
+    for (int j = 0; j < kRwWpt; ++j) {
+      const int e = threadIdx.x + j * nthr;
+      int v = 0;
+      if (e < wsz) {
+        const int cc = e % d.Cin, t2 = e / d.Cin, col = t2 % WC, row = t2 / WC;
+        const int iy = iy0 + row, ix = ix0 + col;
+        if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W)
+          v = x[((int64_t)(n * d.H + iy) * d.W + ix) * d.Cin + cc];
+      }
+      wv[j] = v;
+    }
+    gw[0] = gw[1] = gw[2] = gw[3] = 0;
+    if ((int)threadIdx.x < 64 * GV) {
+      const int px = threadIdx.x / GV, col = (threadIdx.x % GV) * 8;
+      const int ox = xcc * 64 + px;
+      if (ox < d.Wo && col < d.Cout) {
+        const int64_t p = ((int64_t)n * d.Ho + oy) * d.Wo + ox;
+        if constexpr (G16) {
+          const int4 w4 = *reinterpret_cast<const int4*>(reinterpret_cast<const int16_t*>(g_) + p * d.Cout + col);
+          gw[0] = w4.x; gw[1] = w4.y; gw[2] = w4.z; gw[3] = w4.w;
+        } else {
+          const int2 w2 = *reinterpret_cast<const int2*>(reinterpret_cast<const int8_t*>(g_) + p * d.Cout + col);
+          gw[0] = w2.x; gw[1] = w2.y;
+        }
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < kRwWpt; ++j) {
+      const int e = threadIdx.x + j * nthr;
+      if (e < wsz) sW[e] = (_Float16)(float)wv[j];
+    }
+    if ((int)threadIdx.x < 64 * GV) {
+      const int px = threadIdx.x / GV, col = (threadIdx.x % GV) * 8;
+      int v[8];
+      if constexpr (G16) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[2 * j] = (int)(int16_t)(gw[j] & 0xFFFF); v[2 * j + 1] = gw[j] >> 16; }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] = (int)(int8_t)(gw[0] >> (8 * j)); v[4 + j] = (int)(int8_t)(gw[1] >> (8 * j)); }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (G16) {
+          sG[0][col + j][px] = (_Float16)(float)(v[j] >> 8);        // hi, arithmetic shift: [-128, 127]
+          sG[NH - 1][col + j][px] = (_Float16)(float)(v[j] & 255);  // lo: [0, 255]
+        } else {
+          sG[0][col + j][px] = (_Float16)(float)v[j];
+        }
+      }
+    }
+  };
+  int steps = 0;
+  if (cb < ce) load(cb);
+  for (int64_t c = cb; c < ce; ++c) {
+    __syncthreads();  // the previous chunk's LDS reads are done
+    store();
+    __syncthreads();
+    if (c + 1 < ce) load(c + 1);  // in flight during this chunk's MFMAs
+#pragma unroll
+    for (int s = 0; s < kWgChunk / 32; ++s) {
+      h8 a;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int px = s * 32 + 8 * kg + j;
+        a[j] = code >= 0 ? sW[aoff + px * astep] : (_Float16)0.f;
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const h8 b = *reinterpret_cast<const h8*>(&sG[h][ct * 16 + r][s * 32 + 8 * kg]);
+          facc[h][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, facc[h][ct], 0, 0, 0);
+        }
+      if (++steps == kFlush) {
+        steps = 0;
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) iacc[h][ct][i] += (int)facc[h][ct][i];
+            facc[h][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+    }
+  }
+  int64_t* out = slab + (int64_t)blockIdx.x * K * d.Cout;
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int c = ct * 16 + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = wave * 16 + 4 * kg + i;
+      int64_t v = (int64_t)(iacc[0][ct][i] + (int)facc[0][ct][i]);
+      if constexpr (G16) v = 256 * v + (int64_t)(iacc[1][ct][i] + (int)facc[1][ct][i]);
+      if (kk < K && c < d.Cout) out[(int64_t)kk * d.Cout + c] = v;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int lbt_conv_stem_wide_fwd(const int16_t* x, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qx,
@@ -307,8 +466,38 @@ extern "C" int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const 
   const int64_t per = (M + nsplit - 1) / nsplit;
   if (per > kMaxWgPixels) return LBT_EINVAL;
   const int nct = d.Cout >= 64 ? 4 : d.Cout / 16;
-  dim3 grid((unsigned)nsplit, (unsigned)((K + 63) / 64), (unsigned)((d.Cout + 63) / 64));
   hipStream_t st = (hipStream_t)stream;
+  // the row-chunk kernel where its LDS window fits (LBT_STEM_ROWS=0 at call time: never)
+  {
+    const char* e = getenv("LBT_STEM_ROWS");
+    const int xc = (d.Wo + 63) / 64;
+    const int64_t nchunks = (int64_t)d.N * d.Ho * xc;
+    const int64_t cper = (nchunks + nsplit - 1) / nsplit;
+    if ((!e || atoi(e) != 0) && K <= 16 * kRwMaxKT && d.Cin <= kRwMaxCin && d.KH <= kRwMaxKH &&
+        63 * d.SW + d.KW <= kRwMaxWC && d.Cout <= 64 && cper * 64 <= kMaxWgPixels) {
+#define LBT_STEM_R(G, N)                                                                                  \
+  hipLaunchKernelGGL((stem_wgrad_rows_kernel<G, N>), dim3((unsigned)nsplit), dim3(64 * kRwMaxKT), 0, st, x, g, d, K, \
+                     cper, nchunks, xc, slab)
+      if (g16) {
+        switch (nct) {
+          case 1: LBT_STEM_R(true, 1); break;
+          case 2: LBT_STEM_R(true, 2); break;
+          case 3: LBT_STEM_R(true, 3); break;
+          default: LBT_STEM_R(true, 4); break;
+        }
+      } else {
+        switch (nct) {
+          case 1: LBT_STEM_R(false, 1); break;
+          case 2: LBT_STEM_R(false, 2); break;
+          case 3: LBT_STEM_R(false, 3); break;
+          default: LBT_STEM_R(false, 4); break;
+        }
+      }
+#undef LBT_STEM_R
+      return (int)hipGetLastError();
+    }
+  }
+  dim3 grid((unsigned)nsplit, (unsigned)((K + 63) / 64), (unsigned)((d.Cout + 63) / 64));
 #define LBT_STEM_W(G, N) \
   hipLaunchKernelGGL((stem_wide_wgrad_kernel<G, N>), grid, dim3(kThreads), 0, st, x, g, d, K, per, slab)
   if (g16) {

@@ -6,6 +6,8 @@ GPU: the HIP layer path against the oracle, bit-exact (forward logits, every gra
 same d loss / d logits, every exponent update), on reduced widths / depths so the numpy oracle
 finishes in seconds; the full-size model through a training step (shape and finiteness checks).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -251,9 +253,6 @@ def test_stem_wide_matches_generic(N, H, Cout, k, s):
             g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, d.Ho, d.Wo, Cout)).astype(np.int16)).to(DEV)
         else:
             g = torch.from_numpy(rng.integers(-128, 128, size=(N, d.Ho, d.Wo, Cout)).astype(np.int8)).to(DEV)
-        ns = ops.stem_wide_nsplit(d)
-        slab = torch.full((ns, K, Cout), 7, dtype=torch.int64, device=DEV)  # fully overwritten
-        ops.conv_stem_wide_wgrad(x, 9, g, d, slab, ns)
         nr = ops.wgrad_nsplit(d, generic=True)
         if g_i16:
             ref = torch.zeros((nr, K, Cout), dtype=torch.int64, device=DEV)
@@ -261,7 +260,20 @@ def test_stem_wide_matches_generic(N, H, Cout, k, s):
         else:
             ref = torch.zeros((nr, K, Cout), dtype=torch.int32, device=DEV)
             ops.conv_wgrad_generic(x, True, g, d, ref, nr)
-        assert torch.equal(slab.sum(0), ref.to(torch.int64).sum(0)), g_i16
+        ns = ops.stem_wide_nsplit(d)
+        # the row-chunk kernel (LDS window, default) and the per-element gather kernel (LBT_STEM_ROWS=0)
+        for rows in ("1", "0"):
+            old = os.environ.get("LBT_STEM_ROWS")
+            os.environ["LBT_STEM_ROWS"] = rows
+            try:
+                slab = torch.full((ns, K, Cout), 7, dtype=torch.int64, device=DEV)  # fully overwritten
+                ops.conv_stem_wide_wgrad(x, 9, g, d, slab, ns)
+            finally:
+                if old is None:
+                    del os.environ["LBT_STEM_ROWS"]
+                else:
+                    os.environ["LBT_STEM_ROWS"] = old
+            assert torch.equal(slab.sum(0), ref.to(torch.int64).sum(0)), (g_i16, rows)
 
 
 @pytest.mark.gpu
