@@ -274,7 +274,7 @@ constexpr int kRwWin = kRwMaxKH * kRwMaxWC * kRwMaxCin;
 constexpr int kRwWpt = (kRwWin + 64 * kRwMaxKT - 1) / (64 * kRwMaxKT);  // window elements a thread stages (at 10 waves)
 
 template <bool G16, int NCT>
-__global__ __launch_bounds__(64 * kRwMaxKT) void stem_wgrad_rows_kernel(const int16_t* __restrict__ x,
+__global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_rows_kernel(const int16_t* __restrict__ x,
                                                                         const void* __restrict__ g_, lbt_conv_desc d,
                                                                         int K, int64_t cper, int64_t nchunks, int xc,
                                                                         int64_t* __restrict__ slab) {
@@ -301,6 +301,7 @@ __global__ __launch_bounds__(64 * kRwMaxKT) void stem_wgrad_rows_kernel(const in
 #pragma unroll
       for (int i = 0; i < 4; ++i) iacc[h][ct][i] = 0;
     }
+  const int cg0 = blockIdx.y * NCT * 16;  // this workgroup's output channels cg0 .. cg0 + 16 NCT - 1
   const int64_t cb = (int64_t)blockIdx.x * cper;
   const int64_t ce = cb + cper < nchunks ? cb + cper : nchunks;
   // one chunk's operands in registers: window elements threadIdx.x + j * nthr, gradient piece threadIdx.x
@@ -325,7 +326,7 @@ __global__ __launch_bounds__(64 * kRwMaxKT) void stem_wgrad_rows_kernel(const in
     }
     gw[0] = gw[1] = gw[2] = gw[3] = 0;
     if ((int)threadIdx.x < 64 * GV) {
-      const int px = threadIdx.x / GV, col = (threadIdx.x % GV) * 8;
+      const int px = threadIdx.x / GV, col = cg0 + (threadIdx.x % GV) * 8;
       const int ox = xcc * 64 + px;
       if (ox < d.Wo && col < d.Cout) {
         const int64_t p = ((int64_t)n * d.Ho + oy) * d.Wo + ox;
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(64 * kRwMaxKT) void stem_wgrad_rows_kernel(const in
   int64_t* out = slab + (int64_t)blockIdx.x * K * d.Cout;
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {
-    const int c = ct * 16 + r;
+    const int c = cg0 + ct * 16 + r;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kk = wave * 16 + 4 * kg + i;
@@ -475,18 +476,23 @@ extern "C" int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const 
     const int64_t cper = (nchunks + nsplit - 1) / nsplit;
     if ((!e || atoi(e) != 0) && K <= 16 * kRwMaxKT && d.Cin <= kRwMaxCin && d.KH <= kRwMaxKH &&
         63 * d.SW + d.KW <= kRwMaxWC && d.Cout <= 64 && cper * 64 <= kMaxWgPixels) {
+      // 32-channel groups (grid.y) where Cout allows: half the accumulators, two 10-wave workgroups per CU
+      // (waves per SIMD 5 for NCT <= 2, else 3); LBT_STEM_CG=64 at call time: one group of up to 64
+      const char* cgv = getenv("LBT_STEM_CG");
+      const int ncg = (d.Cout % 32 == 0 && !(cgv && atoi(cgv) == 64)) ? d.Cout / 32 : 1;
+      const int rn = ncg > 1 ? 2 : nct;
 #define LBT_STEM_R(G, N)                                                                                  \
-  hipLaunchKernelGGL((stem_wgrad_rows_kernel<G, N>), dim3((unsigned)nsplit), dim3(64 * kRwMaxKT), 0, st, x, g, d, K, \
-                     cper, nchunks, xc, slab)
+  hipLaunchKernelGGL((stem_wgrad_rows_kernel<G, N>), dim3((unsigned)nsplit, (unsigned)ncg), dim3(64 * kRwMaxKT), 0, st, \
+                     x, g, d, K, cper, nchunks, xc, slab)
       if (g16) {
-        switch (nct) {
+        switch (rn) {
           case 1: LBT_STEM_R(true, 1); break;
           case 2: LBT_STEM_R(true, 2); break;
           case 3: LBT_STEM_R(true, 3); break;
           default: LBT_STEM_R(true, 4); break;
         }
       } else {
-        switch (nct) {
+        switch (rn) {
           case 1: LBT_STEM_R(false, 1); break;
           case 2: LBT_STEM_R(false, 2); break;
           case 3: LBT_STEM_R(false, 3); break;

@@ -16,8 +16,8 @@ g = torch.randint(-32768, 32768, (B, d.Ho, d.Wo, 64), dtype=torch.int16, device=
 ns = ops.stem_wide_nsplit(d)
 slab = torch.empty((ns, 147, 64), dtype=torch.int64, device=dev)
 res = {}
-for rows in ("1", "0"):
-    os.environ["LBT_STEM_ROWS"] = rows
+for rows, cg in (("1", "32"), ("1", "64"), ("0", "64")):
+    os.environ["LBT_STEM_ROWS"], os.environ["LBT_STEM_CG"] = rows, cg
     for _ in range(2):
         ops.conv_stem_wide_wgrad(x, 9, g, d, slab, ns)
     torch.cuda.synchronize()
@@ -27,7 +27,7 @@ for rows in ("1", "0"):
         ops.conv_stem_wide_wgrad(x, 9, g, d, slab, ns)
     e1.record()
     torch.cuda.synchronize()
-    res[rows] = slab.sum(0).clone()
-    print("stem wgrad rows=%s: %.1f us" % (rows, e0.elapsed_time(e1) / 10 * 1000), flush=True)
-assert torch.equal(res["1"], res["0"])
+    res[rows + cg] = slab.sum(0).clone()
+    print("stem wgrad rows=%s cg=%s: %.1f us" % (rows, cg, e0.elapsed_time(e1) / 10 * 1000), flush=True)
+assert torch.equal(res["132"], res["064"]) and torch.equal(res["164"], res["064"])
 print("equal")
