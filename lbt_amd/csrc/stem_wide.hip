@@ -476,10 +476,11 @@ extern "C" int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const 
     const int64_t cper = (nchunks + nsplit - 1) / nsplit;
     if ((!e || atoi(e) != 0) && K <= 16 * kRwMaxKT && d.Cin <= kRwMaxCin && d.KH <= kRwMaxKH &&
         63 * d.SW + d.KW <= kRwMaxWC && d.Cout <= 64 && cper * 64 <= kMaxWgPixels) {
-      // 32-channel groups (grid.y) where Cout allows: half the accumulators, two 10-wave workgroups per CU
-      // (waves per SIMD 5 for NCT <= 2, else 3); LBT_STEM_CG=64 at call time: one group of up to 64
+      // one group of up to 64 channels; LBT_STEM_CG=32 at call time: 32-channel groups on grid.y (half the
+      // accumulators, two 10-wave workgroups per CU, but the window staged twice and 12 spilled registers:
+      // 1296 vs 762 us at B=256, profiles/r05/stem_probe.txt)
       const char* cgv = getenv("LBT_STEM_CG");
-      const int ncg = (d.Cout % 32 == 0 && !(cgv && atoi(cgv) == 64)) ? d.Cout / 32 : 1;
+      const int ncg = (d.Cout % 32 == 0 && cgv && atoi(cgv) == 32) ? d.Cout / 32 : 1;
       const int rn = ncg > 1 ? 2 : nct;
 #define LBT_STEM_R(G, N)                                                                                  \
   hipLaunchKernelGGL((stem_wgrad_rows_kernel<G, N>), dim3((unsigned)nsplit, (unsigned)ncg), dim3(64 * kRwMaxKT), 0, st, \
