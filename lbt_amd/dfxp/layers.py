@@ -1121,8 +1121,10 @@ class ResidualBottleneck_q(ResidualBlock_q):
         kh, kw, Cin, Cout = conv.ksize
         d = ops.conv_desc(N, H, W, Cin, Cout, kh, kw, conv.strides[1], conv.strides[2], conv.padding)
         # the quantising epilogue (exact): with the 256-row LDS-DMA GEMM it beats fp32 y + the quantise
-        # pass by 0.2-0.5 ms per ResNet-50 step (round 3 A/B; with the round-2 GEMM it lost); LBT_FUSE_CONV_QUANT=0: off
-        if ops.igemm_workspace_bytes(d, 0, False) or os.environ.get("LBT_FUSE_CONV_QUANT", "1") != "1":
+        # pass by 0.2-0.5 ms per ResNet-50 step (round 3 A/B; with the round-2 GEMM it lost); LBT_FUSE_CONV_QUANT=0: off,
+        # 2: also the GEMMs that would split K (the unsplit quantising kernel instead of split-K + the quantise pass)
+        mode = os.environ.get("LBT_FUSE_CONV_QUANT", "1")
+        if mode == "0" or (mode != "2" and ops.igemm_workspace_bytes(d, 0, False)):
             y = conv.fwd_codes(xq, N, H, W)
             ResidualBottleneck_q._norm_in(bn, y, ctx)
             return y
