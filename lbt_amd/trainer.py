@@ -23,6 +23,7 @@ MI355X-native execution:
     fp32 all-reduce (gscale = 1/world).
 """
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -285,7 +286,21 @@ class Trainer:
 
     def _capture_step(self, X, y):
         """(g1, g2): the step as one graph (no exchange, or captured collectives), else the forward +
-        backward and the update as two graphs with the host-issued exchange between them."""
+        backward and the update as two graphs with the host-issued exchange between them. A failed
+        capture of the exchange (an RCCL / runtime without graph-capture support for it) falls back to
+        the host-issued exchange, loudly, instead of ending the run (not for SyncBN plans, whose
+        statistics collectives sit inside the forward)."""
+        if self.dp and self.capture_comm and not getattr(self.model, "sync_bn", False):
+            try:
+                return self._capture_step_once(X, y)
+            except RuntimeError as e:
+                print("trainer: capturing the step's collectives failed (%s); the exchange runs from the host "
+                      "between two graphs" % str(e).splitlines()[0], file=sys.stderr)
+                torch.cuda.synchronize()
+                self.capture_comm = False
+        return self._capture_step_once(X, y)
+
+    def _capture_step_once(self, X, y):
         one = not self.dp or self.capture_comm
         # thread-local capture: the process group's watchdog thread queries events meanwhile
         mode = "thread_local" if self.capture_comm else "global"
