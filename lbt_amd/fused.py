@@ -113,6 +113,10 @@ class FusedResNet:
         # ... and that block's end chain (BN + Rescale_q + residual + ReLU) too (lbt_head.chain): the head
         # pools the block output from registers, one launch fewer per training step
         self.head_chain = os.environ.get("LBT_HEAD_CHAIN", "1") == "1"
+        # the step prologue in two launches: noise tables + sums + input + conv1's weights ahead of the
+        # stem, the other weight / gamma / beta quantisers on the side stream underneath it. Measured a
+        # loss: 0.4288 -> 0.5060 ms/step (profiles/r10_prologue_split.txt; the forked graph again)
+        self.prologue_split = os.environ.get("LBT_PROLOGUE_SPLIT", "0") == "1"
         self._side = None
         # every conv's weight gradient of the step in ONE launch at the end of the backward
         # (lbt_conv_wgrad_many_i8) instead of inside the dgrad launches: a dgrad launch's tiles fill
@@ -604,11 +608,28 @@ class FusedResNet:
         if ctx._extra_arenas:  # the prologue clears the first arena only
             raise RuntimeError("FusedResNet: the sums arena overflowed (raise DfxpContext sums_capacity)")
         # (together with every weight / gamma / beta quantiser and the input image: one launch)
-        fwd.insert(0, L("lbt_step_prologue", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
-                        ptr(self._wjobs), len(wjobs), max_cout, ptr(self._qjobs), len(qjobs),
-                        ctypes.byref(self._input_job), ptr(ctx.exps), ptr(self._exps_snap), len(ctx.quantizers),
-                        k="step_prologue_kernel",
-                        nb=4 * sum(j.n for j in njobs) + 8 * nz + 6 * X.numel()))
+        split = self._stem and not w4 and self.convs[0] is self.conv1 and self.prologue_split
+        if split:
+            # the stem needs only the noise tables, the cleared sums, the input image and conv1's
+            # weights: the other layers' weight / gamma / beta quantisers run on the side stream
+            # underneath it and join before the first block's conv
+            self._wjobs_rest = _dev_array(wjobs[1:], ctx.device)
+            fwd.insert(0, L("lbt_step_prologue", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
+                            ptr(self._wjobs), 1, wjobs[0].Cout, None, 0,
+                            ctypes.byref(self._input_job), ptr(ctx.exps), ptr(self._exps_snap), len(ctx.quantizers),
+                            k="step_prologue_kernel",
+                            nb=4 * sum(j.n for j in njobs) + 8 * nz + 6 * X.numel()))
+            fwd.insert(1, self._on_side(L("lbt_step_prologue", None, 0, 0, None, 0,
+                                          ptr(self._wjobs_rest), len(wjobs) - 1, max(j.Cout for j in wjobs[1:]),
+                                          ptr(self._qjobs), len(qjobs), None, None, None, 0,
+                                          k="step_prologue_kernel"), force=True))
+            fwd.insert(3, self._join_side())  # [P1, P2 (side), stem, join, ...]
+        else:
+            fwd.insert(0, L("lbt_step_prologue", ptr(self._njobs), len(njobs), max_n, ptr(ctx.sums_arena), nz,
+                            ptr(self._wjobs), len(wjobs), max_cout, ptr(self._qjobs), len(qjobs),
+                            ctypes.byref(self._input_job), ptr(ctx.exps), ptr(self._exps_snap), len(ctx.quantizers),
+                            k="step_prologue_kernel",
+                            nb=4 * sum(j.n for j in njobs) + 8 * nz + 6 * X.numel()))
         if w4:  # the packed weight images need the quantised ones
             fwd.insert(1, self._w4_pack)
         self._fwd, self._bwd = fwd, bwd
