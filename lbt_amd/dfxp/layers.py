@@ -65,8 +65,10 @@ class _Cache:
 # finds finished gradients on its stream. Side streams and pending joins are keyed by the main
 # stream that forked them: one model's join never waits on, or clears, another stream's work.
 # SIDE_STREAM is read once from LBT_SIDE_STREAM (0 = one stream); assign the attribute to change
-# it (a HIP graph captured earlier keeps the schedule it was captured with).
-SIDE_STREAM = os.environ.get("LBT_SIDE_STREAM", "1") != "0"
+# it (a HIP graph captured earlier keeps the schedule it was captured with). Off by default since
+# round 4's fused epilogues: the forked graph measured 36.23 ms/step against 35.84 on one stream
+# (ResNet-50, B=256, profiles/r10_side_stream_r50.txt); LBT_SIDE_STREAM=1 turns it back on.
+SIDE_STREAM = os.environ.get("LBT_SIDE_STREAM", "0") == "1"
 # ResidualBottleneck_q: bn1 / bn2's pass A inside conv-2 / conv-3's dgrad (ops.conv_dgrad_igemm_bna);
 # LBT_DGRAD_BNA_PY=0: the separate dgrad + pass A launches (A/B, and the C-side LBT_DGRAD_BNA=0 keeps
 # the entry point but never fuses)
