@@ -349,7 +349,8 @@ int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const void* g, in
  * var are the running averages (chsum unused), sigma = sqrtf(run_var + eps), nothing updated.
  * ms_in != 0 (lbt_bn_chain_fwd only): ms already holds this step's [mu | sigma] (lbt_bn_moments ran
  * on this descriptor): the chain reads its channels' two floats instead of reducing the sums in
- * every workgroup, and updates nothing.                                                          */
+ * every workgroup, and updates nothing. Either every normalising branch of a chain sets ms_in or
+ * none does (a mixed two-branch chain returns LBT_EINVAL).                                        */
 typedef struct lbt_bn_norm {
   const int8_t* q; lbt_qdesc qn; const int64_t* chsum; int64_t n;
   float eps, momentum, one_minus_momentum;

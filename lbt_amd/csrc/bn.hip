@@ -746,6 +746,9 @@ extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   // in-kernel reduction held wide layers to 1-3 workgroups per CU)
   const bool msall = (!a->b1.nrm.q || a->b1.nrm.ms_in) && (!a->has_b2 || !a->b2.nrm.q || a->b2.nrm.ms_in);
   if ((a->b1.nrm.ms_in && !a->b1.nrm.ms) || (a->has_b2 && a->b2.nrm.ms_in && !a->b2.nrm.ms)) return LBT_EINVAL;
+  // all or none: a mixed chain would re-run the moments (and the running-average update) of its ms_in branch
+  const bool msany = (a->b1.nrm.q && a->b1.nrm.ms_in) || (a->has_b2 && a->b2.nrm.q && a->b2.nrm.ms_in);
+  if (msany && !msall) return LBT_EINVAL;
   const size_t shm = msall ? 0 : sizeof(float) * 8 * a->C + sizeof(long long) * 2 * a->C;
   hipStream_t st = (hipStream_t)stream;
   const int f = fwd_flags(*a);

@@ -430,9 +430,7 @@ class FusedResNet:
         # backward called one by one) and as ONE fused launch (train_fwd_bwd, the training step)
         Nb, Hh, Wh, Ch = Ylast.shape
         pooled = self._buf("pool", (Nb, Ch), torch.float32)
-        hfwd, hloss, hbwd = [], [], []
-        if last_launch is not None:
-            hfwd.append(last_launch)
+        hfwd, hloss, hbwd = [], [], []  # (the end chain joins hfwd or fwd once head_chain is decided, below)
         hfwd.append(L("lbt_avgpool_fwd", ptr(Ylast), ptr(pooled), Nb, Hh * Wh, Ch))
         dd = _lib.ConvDesc(Nb, 1, 1, d.in_units, d.units, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1)
         d.d = dd
@@ -495,6 +493,10 @@ class FusedResNet:
                       and Hh * Wh * Ch == 4096 and qr_last.bits > 0 and qr_last.stochastic and bool(qr_last.noise))
         if head_chain:
             hd.chain = ctypes.addressof(last)
+            # the training step's fused head evaluates the chain itself; the separate head launches
+            # (forward / compute_loss / backward) run it first -- in exactly one of the two lists, since
+            # forward() runs _fwd + _hfwd
+            hfwd.insert(0, last_launch)
             # per element the chain's operands (q codes 1 B, residual 4 B) replace the block output (4 B) and
             # pass A's y mask / R / qn reads (6 B), which come from registers; y and R are not written
             hfused[0].nbytes += (5 - 4 - 6) * Ylast.numel()

@@ -245,6 +245,7 @@ class Trainer:
             self.ctx.update_range_op(sgd=(self.flat.w, self.flat.a, self.flat.g, self.lr, self.momentum, 1.0))
 
     def _eager(self, X, y):
+        self._sync_optimizer()  # an assignment to self.lr / self.momentum takes effect on the fused update too
         did = self._fwd_bwd(X, y, update=not self.dp)
         if self.dp:
             self._exchange()
@@ -294,6 +295,9 @@ class Trainer:
             try:
                 return self._capture_step_once(X, y)
             except RuntimeError as e:
+                msg = str(e).lower()
+                if not any(k in msg for k in ("nccl", "rccl", "collective", "capture", "not permitted", "process group")):
+                    raise  # not the collective's capture (OOM, a kernel launch error ...): no silent fallback
                 print("trainer: capturing the step's collectives failed (%s); the exchange runs from the host "
                       "between two graphs" % str(e).splitlines()[0], file=sys.stderr)
                 torch.cuda.synchronize()

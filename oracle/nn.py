@@ -40,6 +40,14 @@ F32 = np.float32
 ARITH = "exact"
 
 
+# SyncBN (data-parallel parity mode): when set, a callable SYNC(a, b, n) -> (a, b, n) that sums
+# a Normalization_q's exact integer statistics over the ranks -- forward (S1 = sum q, S2 = sum q^2, the
+# per-channel element count n) and backward (SG = sum G, SGQ = sum G*q) -- so every shard takes the
+# WHOLE-batch moments of tf.nn.moments (dynamic_fixed_point.py:588) and their gradient (:616-623): what
+# the build's FusedResNet(sync_bn=True) all-reduces inside its step. None: per-shard statistics.
+SYNC = None
+
+
 #   "tf32seq" -- the same fp32 arithmetic in another legitimate order (sequential reductions, per-tap
 #              conv GEMMs): a control for how far two fp32 implementations of the reference land
 #              from EACH OTHER (TF's CPU and GPU kernels sum in different orders).
@@ -493,6 +501,8 @@ class NormQ(LayerQ):
         else:
             S1 = qf.sum(0)
             S2 = (qf * qf).sum(0)
+            if SYNC is not None:
+                S1, S2, n = SYNC(S1, S2, n)
             mean_d = S1.astype(np.float64) * s / n
             var_d = S2.astype(np.float64) * (s * s) / n - mean_d * mean_d
             mu = mean_d.astype(F32)
@@ -532,7 +542,9 @@ class NormQ(LayerQ):
         qf = self.q.reshape(-1, C).astype(np.int64)
         SG = Gf.sum(0)
         SGQ = (Gf * qf).sum(0)
-        n = self.n
+        n = self.n  # (the global count under SYNC: set by the forward)
+        if SYNC is not None:
+            SG, SGQ, _ = SYNC(SG, SGQ, 0)
         mu_d = self.mu.astype(np.float64)
         sig_d = self.sigma.astype(np.float64)
         mg = (sg * SG.astype(np.float64) / n).astype(F32)

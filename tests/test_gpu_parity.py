@@ -6,6 +6,8 @@ BIT-EXACT. The only op that is not bit-exact is the softmax (expf/logf): loss an
 logits are compared with rtol 1e-5; the model backward is then checked bit-exact by feeding
 the GPU's d loss / d logits into the oracle backward.
 """
+import types
+
 import numpy as np
 import pytest
 import torch
@@ -716,6 +718,46 @@ def test_fused_executor_bitidentical_to_layerwise():
     torch.cuda.synchronize()
     assert np.array_equal(tA.flat.w.cpu().numpy(), tB.flat.w.cpu().numpy())
     assert ctxA.ranges() == ctxB.ranges()
+
+
+@pytest.mark.parametrize("chain", ["1", "0"])
+def test_fused_separate_calls_bn_state_equals_layerwise(chain, monkeypatch):
+    """forward() / compute_loss() / backward() of the fused plan (the separate head launches) run the
+    last block's end chain exactly once, with and without the head chain (it ran twice
+    when LBT_HEAD_CHAIN=0, moving the BN running averages twice and double-counting the Rescale_q
+    overflows): BN running statistics, gradients and the updated exponents equal the layer-wise model."""
+    from lbt_amd.fused import FusedResNet
+    from lbt_amd.models import CIFAR10_Resnet20
+    monkeypatch.setenv("LBT_HEAD_CHAIN", chain)
+    x, y = synthetic_batch(24, seed=15)
+    xt, yt = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    ctxA, ctxB = DfxpContext(seed=16), DfxpContext(seed=16)
+    A = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctxA)
+    B = FusedResNet(CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctxB))
+    assert np.array_equal(A.forward(xt).cpu().numpy(), B.forward(xt).cpu().numpy())
+    assert A.compute_loss(yt).item() == B.compute_loss(yt).item()
+    A.backward()
+    B.backward()
+    names = [getattr(f, "kname", "") for f in B._fwd + B._hfwd]
+    assert names.count("chain_fwd_kernel") == sum(1 for f in B._fwd if getattr(f, "kname", "") == "chain_fwd_kernel") \
+        + (1 if chain == "1" else 0)
+    ga, gb = gpu_grads(A), gpu_grads(B.model)
+    for k in ga:
+        assert np.array_equal(ga[k], gb[k]), k
+    ra = [t.cpu().numpy() for t in _bn_running(A)]
+    rb = [t.cpu().numpy() for t in _bn_running(B.model)]
+    assert len(ra) == len(rb) > 0
+    for u, v in zip(ra, rb):
+        assert np.array_equal(u, v)
+    ctxA.update_range_op()
+    ctxB.update_range_op()
+    assert ctxA.ranges() == ctxB.ranges()
+
+
+def _bn_running(model):
+    """Every Normalization_q's running mean / variance tensors, in model order."""
+    from lbt_amd.trainer import Trainer
+    return [t for l in Trainer._bn_layers(types.SimpleNamespace(model=model)) for t in (l.X_mean_running, l.X_var_running)]
 
 
 @pytest.mark.parametrize("N,HW,C,K,table", [(128, 64, 64, 10, True), (300, 16, 32, 7, False), (5, 3, 256, 64, True), (700, 4, 8, 3, True)])
