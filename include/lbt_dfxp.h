@@ -667,7 +667,9 @@ typedef struct lbt_head {
    * workgroup 0). Bit-identical to lbt_bn_chain_fwd(chain) followed by this head on x = chain.y.    */
   const lbt_chain_fwd* chain;
 } lbt_head;
-int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K);  /* = N * (C + 72) */
+/* scratch: the records transposed, NP = N rounded up to 16: pqT [C][NP] int8 | gqT [64][NP] int8 |
+ * loss terms [N] double (lbt_step_reduce sums them 4 samples per v_dot4)                         */
+int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K);  /* = (C + 64) * NP + 8 * N */
 int lbt_head_fwd_bwd(const lbt_head* h, void* stream);
 
 /* MomentumOptimizer.apply_gradients (trainer.py:81-82): a = mu*a + g*gscale; w -= lr*a. */
@@ -705,7 +707,8 @@ typedef struct lbt_qjob {
 int lbt_dfxp_quantize_many(const lbt_qjob* jobs, int32_t njobs, void* stream);
 
 /* lbt_conv_wgrad_reduce for many layers: one 1-D launch of total_blocks = sum over the jobs of
- * ceil(K*Cout / 256) workgroups (jobs[] in device memory, Cout <= 256).                    */
+ * lbt_rjob_blocks(K*Cout) workgroups (jobs[] in device memory).                            */
+int lbt_rjob_blocks(int64_t n);  /* workgroups of one reduce job of n = K*Cout outputs (1024 each) */
 typedef struct lbt_rjob {
   const int32_t* slab; int32_t nsplit, K, Cout, x_u8off; const int64_t* gcolsum;
   lbt_qdesc qx, qg; const float* w; float wd2; float* dw;
@@ -732,7 +735,7 @@ int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_n, int64_t*
                       void* stream);
 
 /* The end of a step's backward in ONE launch: lbt_conv_wgrad_reduce_many's jobs (r_blocks =
- * sum of ceil(K*Cout/256)), lbt_bn_param_grads_many's jobs (Cout <= max_c) and, if head is not
+ * sum of lbt_rjob_blocks(K*Cout)), lbt_bn_param_grads_many's jobs (Cout <= max_c) and, if head is not
  * NULL, the head's batch reductions (Dense_q dw and loss[0], from lbt_head_fwd_bwd's records:
  * the loss summed in softmax_xent's order). Job arrays in device memory, *head in host memory.  */
 int lbt_step_reduce(const lbt_rjob* rjobs, int32_t nr, int32_t r_blocks, const lbt_pjob* pjobs, int32_t np,

@@ -19,7 +19,7 @@ NSHARD = 32
 STEM_WG_PIXELS = 256  # LBT_STEM_WG_PIXELS
 CSTRIDE = 32  # int32 stride between overflow-counter shards (LBT_CSTRIDE)
 OUT_I8, OUT_U8OFF, OUT_I16, OUT_F32 = 0, 1, 2, 3
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 c_void_p, c_int32, c_int64, c_uint32, c_uint64, c_float = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float)
@@ -295,6 +295,7 @@ _SIGS = {
     "lbt_conv_wgrad_reduce_many": [_P, c_int32, c_int32, _P],
     "lbt_bn_param_grads_many": [_P, c_int32, c_int32, _P],
     "lbt_head_scratch_bytes": [c_int32, c_int32, c_int32],
+    "lbt_rjob_blocks": [c_int64],
     "lbt_head_fwd_bwd": [_P, _P],
     "lbt_step_prologue": [_P, c_int32, c_int64, _P, c_int64, _P, c_int32, c_int32, _P, c_int32, _P, _P, _P, c_int32,
                           _P],

@@ -47,6 +47,79 @@ LBT_DEV void quantize_weights_block(const lbt_wjob* __restrict__ jobs, int bx, i
   }
 }
 
+// The step prologue's weight quantiser: block bx of job `by` quantises output channels 4 bx .. 4 bx + 3
+// for every k (float4 loads of a W row's 4 channels, one Philox call per 4 noise indices: idx % 4 == 0,
+// inner % 4 == 0), every row's load issued before the arithmetic; the codes go out as char4 stores to
+// w_hwio and the dgrad image (4 consecutive channels of one 16-channel group) and as bytes to the fwd
+// image. quantize_weights_block took one channel per block (1 408 blocks, a Philox call and a
+// Cout-strided 4-byte load per weight: ~5.6 us per block, the prologue's critical path). Jobs that are
+// not 4-channel aligned (the Dense_q W of 10 classes) go channel by channel: bx, bx + nb, ... Same codes,
+// counters and column sums.
+LBT_DEV void quantize_weights_block4(const lbt_wjob* __restrict__ jobs, int bx, int by, int nb) {
+  __shared__ int red4[4][kThreads / 64];
+  __shared__ int sh_cnt4[2 * kThreads / 64];
+  const lbt_wjob j = jobs[by];
+  const bool quad = j.Cout % 4 == 0 && !(reinterpret_cast<uintptr_t>(j.w) & 15) &&
+                    !(reinterpret_cast<uintptr_t>(j.w_hwio) & 3) && !(reinterpret_cast<uintptr_t>(j.wd) & 3);
+  if (!quad) {  // uniform per block
+    for (int co = bx; co < j.Cout; co += nb) quantize_weights_block(jobs, co, by);
+    return;
+  }
+  const int co = 4 * bx;
+  if (co >= j.Cout) return;  // uniform per block
+  const QState s = qstate(j.q);
+  const int st = j.q.stochastic;
+  const int K = j.KH * j.KW * j.Cin;
+  const int64_t inner = (int64_t)j.KW * j.Cin * j.Cout;
+  const int csi = (j.Cin + 15) / 16, cso = (j.Cout + 15) / 16;
+  int ov1 = 0, ov2 = 0, cs[4] = {0, 0, 0, 0};
+  constexpr int kRows = 4;  // k rows per thread per pass: every load in flight before the Philox calls
+  for (int k0 = 0; k0 < K; k0 += kRows * kThreads) {
+    float4 wv[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const int k = k0 + (int)threadIdx.x + r * kThreads;
+      wv[r] = *reinterpret_cast<const float4*>(j.w + (int64_t)(k < K ? k : 0) * j.Cout + co);
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const int k = k0 + (int)threadIdx.x + r * kThreads;
+      if (k >= K) break;
+      const int64_t idx = (int64_t)k * j.Cout + co;
+      const Noise4 nz = st ? qnoise4(j.q, s.step, (uint64_t)((idx % inner) >> 2)) : Noise4{{0.f, 0.f, 0.f, 0.f}};
+      const float w4[4] = {wv[r].x, wv[r].y, wv[r].z, wv[r].w};
+      int c[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        c[e] = quant1(s, st, w4[e], nz.u[e], ov1, ov2);
+        cs[e] += c[e];
+      }
+      const char4 cv = make_char4((char)c[0], (char)c[1], (char)c[2], (char)c[3]);
+      const int tap = k / j.Cin, ci = k - tap * j.Cin;
+      if (j.w_hwio) *reinterpret_cast<char4*>(j.w_hwio + idx) = cv;
+      if (j.wf) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) j.wf[((int64_t)(co + e) * j.ksf + tap * csi + ci / 16) * 16 + (ci & 15)] = (int8_t)c[e];
+      }
+      if (j.wd) *reinterpret_cast<char4*>(j.wd + ((int64_t)ci * j.ksd + tap * cso + co / 16) * 16 + (co & 15)) = cv;
+    }
+  }
+  block_flush_counts(j.q, ov1, ov2, sh_cnt4);
+  if (j.colsum) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int v = wave_sum_i32(cs[e]);
+      if ((threadIdx.x & 63) == 0) red4[e][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      int t = 0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red4[threadIdx.x][i];
+      j.colsum[co + threadIdx.x] = t;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void quantize_weights_kernel(const lbt_wjob* __restrict__ jobs) {
   quantize_weights_block(jobs, blockIdx.x, blockIdx.y);
 }
@@ -78,9 +151,16 @@ LBT_DEV void sgd_update(float wv, float am, float gv, const lbt_update& u, int64
   LBT_ST_TAIL(u.w + o, wv - step);
 }
 
-// Blocks are allotted to the jobs in order, ceil(K*Cout/256) each (1-D grid); a block reduces 256
-// consecutive outputs over the slab's shards, with the offset correction 128 * sum_p g[co]
-// (x_u8off) summed once per column into LDS. lds: >= 4 KB.
+// Blocks are allotted to the jobs in order, lbt_rjob_blocks(K*Cout) = ceil(K*Cout / kRBlock) each (1-D
+// grid); a block reduces kRBlock consecutive outputs (kRPer per thread, 256 apart: coalesced) over the
+// slab's shards, with the offset correction 128 * sum_p g[co] (x_u8off) summed once per column into LDS.
+// (256 outputs per block made ~1 060 blocks of a ResNet-20 step: dispatched over ~7 us, the launch's
+// critical path. lds: >= 4 KB.)
+#ifndef LBT_RPER
+#define LBT_RPER 4
+#endif
+constexpr int kRPer = LBT_RPER;
+constexpr int kRBlock = 256 * kRPer;
 LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, uint8_t* lds, const lbt_xchg& x,
                         const lbt_update& u) {
   int64_t* nbs = reinterpret_cast<int64_t*>(lds);                   // [256]
@@ -93,7 +173,7 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
   if (njobs <= 64) {
     if (threadIdx.x < 64) {
       const int l = (int)threadIdx.x;
-      const int64_t nb = l < njobs ? ((int64_t)jobs[l].K * jobs[l].Cout + 255) / 256 : 0;
+      const int64_t nb = l < njobs ? ((int64_t)jobs[l].K * jobs[l].Cout + kRBlock - 1) / kRBlock : 0;
       int64_t end = nb;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -103,11 +183,11 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
       const bool own = l < njobs && (int64_t)blk < end && (int64_t)blk >= end - nb;
       const unsigned long long m = __ballot(own);
       if (l == 0) *s_job = m ? __ffsll((long long)m) - 1 : njobs;
-      if (own) *s_base = ((int64_t)blk - (end - nb)) * 256;
+      if (own) *s_base = ((int64_t)blk - (end - nb)) * kRBlock;
     }
     __syncthreads();
   } else {
-    for (int j = threadIdx.x; j < njobs; j += 256) nbs[j] = ((int64_t)jobs[j].K * jobs[j].Cout + 255) / 256;
+    for (int j = threadIdx.x; j < njobs; j += 256) nbs[j] = ((int64_t)jobs[j].K * jobs[j].Cout + kRBlock - 1) / kRBlock;
     __syncthreads();
     if (threadIdx.x == 0) {
       int64_t b = blk;
@@ -117,63 +197,106 @@ LBT_DEV void rjob_block(const lbt_rjob* __restrict__ jobs, int njobs, int blk, u
         b -= nbs[j];
       }
       *s_job = jj;
-      *s_base = b * 256;
+      *s_base = b * kRBlock;
     }
     __syncthreads();
   }
   if (*s_job >= njobs) return;
   const lbt_rjob j = jobs[*s_job];
   const int64_t total = (int64_t)j.K * j.Cout;
-  const int64_t i = *s_base + threadIdx.x;
+  const int64_t i0 = *s_base + threadIdx.x;  // this thread's outputs: i0 + 256 e, e < kRPer
   const bool corr = j.x_u8off && j.gcolsum;
-  // the column sums' shard loads and the slab loads are issued back to back, so both arrive in one
-  // memory round trip. Cout <= 256 (colsum's LDS capacity): thread c < Cout sums column c once into
-  // LDS; wider jobs: every thread sums its own column's shards (uniform per block)
+  // the column sums' shard loads, the slab loads and the optimiser's operands are issued back to back,
+  // so all arrive in one memory round trip. Cout <= 256 (colsum's LDS capacity): thread c < Cout sums
+  // column c once into LDS; wider jobs: each output's column summed by its own thread (below)
   const bool lds_cols = j.Cout <= 256;
-  const int c = lds_cols ? (int)threadIdx.x : (int)(i % j.Cout);
-  const bool col = corr && (lds_cols ? c < j.Cout : i < total);
+  const int c = (int)threadIdx.x;
+  const bool col = corr && lds_cols && c < j.Cout;
   long long v[LBT_NSHARD];
   if (col) {
 #pragma unroll
     for (int k = 0; k < LBT_NSHARD; ++k) v[k] = j.gcolsum[(int64_t)k * 2 * j.Cout + c];
   }
-  long long s = 0;
-  // the optimiser's operands (lbt_step_reduce_update) in the same round trip as the slab
-  float wv = 0.f, am = 0.f;
-  const int64_t o = u.w ? (j.dw - u.g) + i : 0;
-  if (u.w && i < total) {
-    wv = j.w[i];
-    am = u.a[o];
-  }
-  if (i < total)
-    for (int b = 0; b < j.nsplit; ++b) s += j.slab[(int64_t)b * total + i];
-  long long t = 0;
-  if (col) {
+  long long s[kRPer];
+  float wv[kRPer], am[kRPer];
+  const int64_t ob = u.w ? (j.dw - u.g) : 0;
 #pragma unroll
-    for (int k = 0; k < LBT_NSHARD; ++k) t += v[k];
+  for (int e = 0; e < kRPer; ++e) {
+    const int64_t i = i0 + 256 * e;
+    s[e] = 0;
+    wv[e] = 0.f;
+    am[e] = 0.f;
+    if (i < total && !x.buf) {
+      wv[e] = j.w[i];
+      if (u.w) am[e] = u.a[ob + i];
+    }
+  }
+  // the slab's shards (1-2 for the block convs, 32 for the stem's): 8 at a time, every load of a group
+  // in flight before its adds (a plain loop waited on each load in turn: 32 round trips for the stem)
+  int b = 0;
+  for (; b + 8 <= j.nsplit; b += 8) {
+    int sv[8][kRPer];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int e = 0; e < kRPer; ++e) {
+        const int64_t i = i0 + 256 * e;
+        sv[q][e] = j.slab[(int64_t)(b + q) * total + (i < total ? i : 0)];
+      }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int e = 0; e < kRPer; ++e) s[e] += sv[q][e];
+  }
+  for (; b < j.nsplit; ++b) {
+    int sv[kRPer];
+#pragma unroll
+    for (int e = 0; e < kRPer; ++e) {
+      const int64_t i = i0 + 256 * e;
+      sv[e] = j.slab[(int64_t)b * total + (i < total ? i : 0)];
+    }
+#pragma unroll
+    for (int e = 0; e < kRPer; ++e) s[e] += sv[e];
   }
   if (corr && lds_cols) {
-    if (col) colsum[c] = t;
+    if (col) {
+      long long t = 0;
+#pragma unroll
+      for (int k = 0; k < LBT_NSHARD; ++k) t += v[k];
+      colsum[c] = t;
+    }
     __syncthreads();
   }
-  if (i >= total) return;
-  if (corr) s += 128ll * (lds_cols ? colsum[i % j.Cout] : t);
-  if (x.buf) {  // data-parallel exchange: the exact numerator, dequantised after the all-reduce
-    x.buf[(j.dw - x.gbase) + i] = s;
-    return;
-  }
   const float scale = ldexpf(1.0f, -(frac_exp(j.qx) + frac_exp(j.qg)));
-  if (u.w) {  // lbt_step_reduce_update: the gradient, then MomentumOptimizer on the same element
-    const float a = (float)s * scale;
-    const float b = j.wd2 * wv;
+#pragma unroll
+  for (int e = 0; e < kRPer; ++e) {
+    const int64_t i = i0 + 256 * e;
+    if (i >= total) break;
+    if (corr) {
+      long long t;
+      if (lds_cols) {
+        t = colsum[i % j.Cout];
+      } else {
+        const int ce = (int)(i % j.Cout);
+        t = 0;
+        for (int k = 0; k < LBT_NSHARD; ++k) t += j.gcolsum[(int64_t)k * 2 * j.Cout + ce];
+      }
+      s[e] += 128ll * t;
+    }
+    if (x.buf) {  // data-parallel exchange: the exact numerator, dequantised after the all-reduce
+      x.buf[(j.dw - x.gbase) + i] = s[e];
+      continue;
+    }
+    const float a = (float)s[e] * scale;
+    const float b = j.wd2 * wv[e];
     const float gv = a + b;
-    LBT_ST_TAIL(j.dw + i, gv);
-    sgd_update(wv, am, gv, u, o);
-    return;
+    if (u.w) {  // lbt_step_reduce_update: the gradient, then MomentumOptimizer on the same element
+      LBT_ST_TAIL(j.dw + i, gv);
+      sgd_update(wv[e], am[e], gv, u, ob + i);
+      continue;
+    }
+    j.dw[i] = gv;
   }
-  const float a = (float)s * scale;
-  const float b = j.wd2 * j.w[i];
-  j.dw[i] = a + b;
 }
 
 __global__ __launch_bounds__(256) void wgrad_reduce_many_kernel(const lbt_rjob* __restrict__ jobs, int njobs) {
@@ -384,10 +507,11 @@ struct Prologue {
 __global__ __launch_bounds__(kThreads) void step_prologue_kernel(Prologue a) {
   int b = blockIdx.x;
   LBT_TS(0);
-  const int n2 = a.max_cout * a.nw;
+  const int nbw = (a.max_cout + 3) / 4;  // weight blocks per job (4 output channels each)
+  const int n2 = nbw * a.nw;
   if (b < n2) {
     LBT_TROLE(2);
-    quantize_weights_block(a.wjobs, b % a.max_cout, b / a.max_cout);
+    quantize_weights_block4(a.wjobs, b % nbw, b / nbw, nbw);
     LBT_TS(1);
     return;
   }
@@ -453,7 +577,7 @@ extern "C" int lbt_step_prologue(const lbt_njob* njobs, int32_t nn, int64_t max_
     a.nin = (int)((a.input.n / 4 + kThreads - 1) / kThreads);
   }
   a.snap_src = snap_src; a.snap_dst = snap_dst; a.nsnap = snap_n;
-  const int64_t blocks = (int64_t)a.nbx * nn + (int64_t)a.max_cout * nw + nq + a.nin + (snap_n > 0 ? 1 : 0);
+  const int64_t blocks = (int64_t)a.nbx * nn + (int64_t)((a.max_cout + 3) / 4) * nw + nq + a.nin + (snap_n > 0 ? 1 : 0);
   if (blocks <= 0) return LBT_OK;
   if (blocks > 0x7fffffff) return LBT_EINVAL;
   hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, a);
@@ -512,6 +636,8 @@ __global__ __launch_bounds__(kThreads) void quantize_weights_flat_kernel(const l
 }
 
 }  // namespace
+
+extern "C" int lbt_rjob_blocks(int64_t n) { return (int)((n + kRBlock - 1) / kRBlock); }
 
 extern "C" int lbt_flat_weight_blocks(int64_t n) { return (int)((n + kFlatPerBlock - 1) / kFlatPerBlock); }
 

@@ -1170,6 +1170,16 @@ extern "C" int lbt_diag_occupancy(int32_t* out, int32_t n) {
 // conv of the previous launch.
 namespace {
 
+// Phase stamps of conv_bwd_kernel (scratch -DLBT_TRACE builds); -DLBT_P1STUDY moves them into its load
+// phase: slots 1-3 = statistics loads issued / all loads issued / statistics finished, 4 / 5 = the ends of
+// the load phase and of phase 1 (tools/trace_phases.py)
+#ifdef LBT_P1STUDY
+#define LBT_TSS(i) LBT_TS(i)
+#define LBT_TSB(i) do { if ((i) == 1) LBT_TS(4); else if ((i) == 2) LBT_TS(5); } while (0)
+#else
+#define LBT_TSS(i) do { } while (0)
+#define LBT_TSB(i) LBT_TS(i)
+#endif
 constexpr int kBNW = 8;    // waves per workgroup
 constexpr int kBThreads = kBNW * 64;
 // image rows per workgroup: 8 for the 16-channel stage (1024 4-row tiles would take two rounds of
@@ -1179,6 +1189,47 @@ __host__ __device__ constexpr int tile_rows(int CS) { return CS == 1 ? 8 : 4; }
 __host__ __device__ constexpr int halo_iters(int CS) {
   return ((tile_rows(CS) + 2) * (512 / (CS * 16) + 2) * CS * 4 + kBThreads - 1) / kBThreads;
 }
+
+// The conv's weight image shared through LDS by the fused conv kernels: [C columns][KS k-slices] of 16
+// bytes (W4: 8-byte packed slices), loaded once per workgroup with coalesced 16-byte loads (in the
+// launch's first load wave), written to LDS at the end of phase 1 (no extra wait: the loads have long
+// landed) and read per fragment in phase 2. Each wave used to load its n-tile's fragments itself: 2
+// (C = 64), 4 (32) or 8 (16) waves per n-tile, i.e. 72 KB of weight loads per stage-3 workgroup where the
+// image is 36 KB -- through one CU's load path, in the load phase that dominates these launches. LDS
+// column stride padded by 16 bytes: the 16 lanes r of a fragment read conflict-free.
+template <int C, int KS, bool W4>
+struct WImg {
+  static constexpr int kBpf = W4 ? 8 : 16;       // bytes per (column, k-slice) fragment
+  static constexpr int kColB = KS * kBpf;         // bytes per column in the global image
+  static constexpr int kStride = kColB + 16;      // ... in LDS
+  static constexpr int kBytes = C * kStride;
+  static constexpr int kChunks = C * kColB / 16;  // 16-byte chunks of the global image
+  static constexpr int kIt = (kChunks + kBThreads - 1) / kBThreads;
+  static_assert(kColB % 16 == 0, "16-byte chunks within a column");
+  LBT_DEV static void load(const int8_t* src, v4i (&v)[kIt]) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = (int)threadIdx.x + it * kBThreads;
+      v[it] = *reinterpret_cast<const v4i*>(src + (int64_t)(i < kChunks ? i : 0) * 16);
+    }
+  }
+  LBT_DEV static void store(int8_t* lds, const v4i (&v)[kIt]) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = (int)threadIdx.x + it * kBThreads;
+      if (i < kChunks) {
+        const int g = i * 16, col = g / kColB;
+        *reinterpret_cast<v4i*>(lds + col * kStride + (g - col * kColB)) = v[it];
+      }
+    }
+  }
+  LBT_DEV static v4i frag(const int8_t* lds, int col, int slice) {
+    if constexpr (W4)
+      return unpack_i4x16(*reinterpret_cast<const v2i*>(lds + col * kStride + slice * 8));
+    else
+      return *reinterpret_cast<const v4i*>(lds + col * kStride + slice * 16);
+  }
+};
 
 struct ConvBwdArgs {
   lbt_chain_bwd_b b;
@@ -1190,8 +1241,9 @@ struct ConvBwdArgs {
   lbt_chain_bwd_a a;
 };
 
-template <int C, int TH>
+template <int C, int TH, int WB>
 struct BwdShared {
+  int8_t w[WB];                                  // the dgrad weight image (WImg)
   int8_t gq[(TH + 2) * (512 / C + 2) * C];   // halo image [(TH+2)][(W+2)][C], W*C == 512
   float tile[TH * (512 / C) * (C + 4)];       // dgrad outputs [TH*W][C+4] (padded rows)
   float pb[2 * C];                               // pass-B constants mg, mgx per channel
@@ -1346,8 +1398,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   constexpr int WC = WCS ? WCS : 1;
   constexpr int TH = tile_rows(CS), kBIt = halo_iters(CS), J = TH / 4;  // J: phase-3 groups per thread
+  using WI = WImg<C, 4 * kMaxKS, W4>;
   union Smem {
-    BwdShared<C, TH> b;
+    BwdShared<C, TH, WI::kBytes> b;
     WgradShared<WC, kBNW> w;
   };
   __shared__ __attribute__((aligned(16))) Smem sm;
@@ -1355,7 +1408,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     conv_wgrad_body<WC, kBNW>(wa, blockIdx.x, sm.w);
     return;
   }
-  BwdShared<C, TH>& sh = sm.b;
+  BwdShared<C, TH, WI::kBytes>& sh = sm.b;
   LBT_TS(0);
   const lbt_chain_bwd_b& B = p.b;
   const lbt_chain_bwd_a& A = p.a;
@@ -1385,6 +1438,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
       sv[i][1] = ps[(int64_t)i * 4 * C + 3 * C];
     }
   }
+  LBT_TSS(1);  // the statistics loads issued
   // then every load that does not depend on the sums
   // phase-1 operands: G / q codes and the output quantiser's noise over the halo rows
   const int ngrp = (TH + 2) * Wp * C4;
@@ -1401,19 +1455,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     Qv[it] = ld4i8(B.qn_codes, img + off);
     Uv[it] = ld4f(B.qo.noise, off);
   }
-  // phase-2 B operands (dgrad weights) of this wave's (m-tile, n-tile) pairs wave + 8i (one n-tile:
-  // NT | 8; a 4-row tile is 8 pairs, W*C == 512); ks == 4 * kMaxKS (host check)
-  v4i bf[kMaxKS];
-  {
-    const int col = (wave % NT) * 16 + r;
-#pragma unroll
-    for (int kk = 0; kk < kMaxKS; ++kk) {
-      if constexpr (W4)
-        bf[kk] = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wd + ((int64_t)col * (4 * kMaxKS) + kk * 4 + kg) * 8));
-      else
-        bf[kk] = *reinterpret_cast<const v4i*>(p.wd + ((int64_t)col * (4 * kMaxKS) + kk * 4 + kg) * 16);
-    }
-  }
+  // the phase-2 B operands (the dgrad weight image, ks == 4 * kMaxKS: host check), for LDS (WImg)
+  v4i wimg[WI::kIt];
+  WI::load(p.wd, wimg);
   float mu[4], sg[4], gam[2][4], bet[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -1432,6 +1476,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   }
   const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
   const float scale = ldexpf(1.0f, -(frac_exp(B.qo) + frac_exp(p.qw)));
+  LBT_TSS(2);  // every other load issued, the descriptors read
 
   // ---------------- pass-B statistics: the shard sums (loaded first, above) added per lane, then over
   // the statistics wave's four lane rows; lanes < 16 finish their channel in double exactly as
@@ -1454,8 +1499,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     sh.pb[C + c] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
     }
   }
+  LBT_TSS(3);  // the statistics finished
   __syncthreads();
-  LBT_TS(1);
+  LBT_TSB(1);
   float rmg[4], rmgx[4];
   Recip rsg[4];
 #pragma unroll
@@ -1517,8 +1563,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     }
   }
   pin_counts(ovq1, ovq2);
+  WI::store(sh.w, wimg);
   __syncthreads();
-  LBT_TS(2);
+  LBT_TSB(2);
 
   // phase-3 operands (addend, mask source, R / qn codes and both quantisers' noise per branch),
   // issued now: they land while the MFMAs run, and phase 1's registers are free
@@ -1549,6 +1596,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     const int ly = m / W, px = m - ly * W;
     const int8_t* base = sh.gq + ((ly + 2) * Wp + px + 2) * C;
     v4i acc = v4i{0, 0, 0, 0};
+    const int col = nt * 16 + r;
 #pragma unroll
     for (int kk = 0; kk < kMaxKS; ++kk) {
       const int s = kk * 4 + kg;  // the k-slice this lane group supplies: (tap, 16-channel slice)
@@ -1556,13 +1604,13 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
       const int kh = tap / 3, kw = tap - kh * 3;
       v4i a = *reinterpret_cast<const v4i*>(base - (kh * Wp + kw) * C + cs * 16);
       if (s >= 9 * CS) a = v4i{0, 0, 0, 0};  // zero padding of the k dimension
-      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bf[kk], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, WI::frag(sh.w, col, s), acc, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) sh.tile[(mt * 16 + 4 * kg + i) * (C + 4) + nt * 16 + r] = (float)acc[i] * scale;
   }
   __syncthreads();
-  LBT_TS(3);
+  LBT_TSB(3);
 
   // ---------------- phase 3: pass A over the tile
   int ov[2][2][2] = {{{0, 0}, {0, 0}}, {{0, 0}, {0, 0}}};
@@ -1670,7 +1718,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     counts_stage_w(4, 5, ov[1][1][0], ov[1][1][1], sh.cnt);
   }
   __syncthreads();
-  LBT_TS(4);
+  LBT_TSB(4);
   counts_publish_nw<kBNW>(0, 5, B.qo, sh.cnt);
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -1696,7 +1744,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     }
     LBT_GADD((unsigned long long*)dst, (unsigned long long)t);
   }
-  LBT_TS(5);
+  LBT_TSB(5);
 }
 
 bool noise_ok(const lbt_qdesc& q) { return q.bits > 0 && q.stochastic && q.noise; }
@@ -2267,8 +2315,9 @@ struct ConvFwdArgs {
   int64_t* ychsum;
 };
 
-template <int C, int TH>
+template <int C, int TH, int WB>
 struct FwdShared {
+  int8_t w[WB];                               // the forward weight image (WImg)
   int8_t x[(TH + 2) * (512 / C + 2) * C];   // the conv's input codes, halo image (q - 128)
   float tile[TH * (512 / C) * (C + 4)];      // conv outputs [TH*W][C+4]
   float cst[2][2][C];                          // per branch: mu, sigma
@@ -2281,7 +2330,8 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   constexpr int C = CS * 16, C4 = C / 4, NT = CS, W = 512 / C, Wp = W + 2;
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   constexpr int TH = tile_rows(CS), kBIt = halo_iters(CS), J = TH / 4;
-  __shared__ __attribute__((aligned(16))) FwdShared<C, TH> sh;
+  using WI = WImg<C, 4 * kMaxKS, W4>;
+  __shared__ __attribute__((aligned(16))) FwdShared<C, TH, WI::kBytes> sh;
   LBT_TS(0);
   const lbt_chain_fwd& a = p.c;
   const int H = p.H;
@@ -2330,21 +2380,11 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     if constexpr (RES) rv[it] = ld4f(a.res, img + off);
     nov[it] = ld4f(a.qo1.noise, off);
   }
-  // the B operands (this wave's n-tile of the forward weight image): loaded up front, or -- in the
-  // variants whose phase 1 holds the most registers -- right after phase 1
-  constexpr bool kLateB = NB == 2 || RES;
-  v4i bf[kMaxKS];
+  // the B operands (the forward weight image, for LDS: WImg): loaded in this first load wave, stored
+  // to LDS at the end of phase 1
+  v4i wimg[WI::kIt];
+  WI::load(p.wf, wimg);
   const int bcol = (wave % NT) * 16 + r;
-  auto load_b = [&]() {
-#pragma unroll
-    for (int kk = 0; kk < kMaxKS; ++kk) {
-      if constexpr (W4)
-        bf[kk] = unpack_i4x16(*reinterpret_cast<const v2i*>(p.wf + ((int64_t)bcol * (4 * kMaxKS) + kk * 4 + kg) * 8));
-      else
-        bf[kk] = *reinterpret_cast<const v4i*>(p.wf + ((int64_t)bcol * (4 * kMaxKS) + kk * 4 + kg) * 16);
-    }
-  };
-  if constexpr (!kLateB) load_b();
   const int corr = 128 * p.wcolsum[bcol];  // the unsigned-9-bit offset encoding undone: + 128 * sum_k W[k][col]
   float gam[NB][4], bet[NB][4];
 #pragma unroll
@@ -2486,7 +2526,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
 #pragma unroll
   for (int b = 0; b < NB; ++b) pin_counts(ovr[b][0], ovr[b][1]);
   pin_counts(ovx1, ovx2);
-  if constexpr (kLateB) load_b();
+  WI::store(sh.w, wimg);
   __syncthreads();
   LBT_TS(2);
   // phase-3 noise (the output quantiser), issued under the MFMAs
@@ -2510,7 +2550,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       const int kh = tap / 3, kw = tap - kh * 3;
       v4i av = *reinterpret_cast<const v4i*>(base + (kh * Wp + kw) * C + cs * 16);
       if (s >= 9 * CS) av = v4i{0, 0, 0, 0};  // k padding (its weights are zero too)
-      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bf[kk], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, WI::frag(sh.w, nt * 16 + r, s), acc, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)

@@ -1,111 +1,92 @@
 // head.h -- per-sample records of the classifier head (head.hip) and their batch reduction
 // (run inside lbt_step_reduce, batched.hip).
-//
-// Record of sample n at scratch + n * (C + kHeadRecPad) bytes:
-//   pq[C] (Dense_q X codes) | gq[64] (Dense_q grad codes, K used) | loss term (double)
 #pragma once
 #include "dfxp_device.h"
 
+#define LBT_HD __host__ __device__ inline
+
 namespace lbt {
 
-constexpr int kHeadRecPad = 72;
+// Records of the N samples in scratch, TRANSPOSED so the batch reduction takes four samples per
+// v_dot4 (NP = N rounded up to 16 bytes; bytes of samples >= N are never read as data: masked):
+//   pqT[C][NP] int8 (Dense_q X codes) | gqT[64][NP] int8 (Dense_q grad codes, rows < K used) |
+//   term[N] double (each sample's loss term)
+LBT_HD int head_np(int N) { return (N + 15) & ~15; }
+LBT_HD int64_t head_gq_off(int N, int C) { return (int64_t)C * head_np(N); }
+LBT_HD int64_t head_term_off(int N, int C) { return (int64_t)(C + 64) * head_np(N); }
+LBT_HD int64_t head_scratch_bytes(int N, int C) { return head_term_off(N, C) + 8 * (int64_t)N; }
+
 constexpr int kHeadT = 256;
-constexpr int kHeadRecBytes = 24576;                        // records staged per pass
-constexpr int kHeadLds = kHeadRecBytes + kHeadT * 16 * 4;   // + per-thread partials
+constexpr int kHeadLds = 4112;  // the step_reduce workgroup's LDS (rjob_block's 4112 B; head_reduce uses its own)
 
 // One 256-thread workgroup: dw = dequant(sum_n pq[n]^T gq[n]) + wd2 * w (wgrad_reduce's formula)
-// and loss[0] = (float)(sum of the terms in softmax_xent_kernel's order / loss_n). lds: kHeadLds
-// bytes. With an exchange buffer (x.buf, lbt_step_reduce_x) the integer sums go to
-// x.buf[(dw - gbase) + ...] instead, and the loss-term sum, in 2^-32 fixed point, to x.buf[loss_off].
-// u.w != NULL (lbt_step_reduce_update): MomentumOptimizer on each dw element as it is formed.
+// and loss[0] = (float)(sum of the terms in softmax_xent_kernel's order / loss_n). Thread (c, kq) owns
+// channel c's outputs k = kq * kpt .. + kpt - 1 and sums them over the samples 4 at a time (v_dot4 on
+// the transposed records, 16 samples per load): exact integers, so the order is free. With an exchange
+// buffer (x.buf, lbt_step_reduce_x) the integer sums go to x.buf[(dw - gbase) + ...] instead, and the
+// loss-term sum, in 2^-32 fixed point, to x.buf[loss_off]. u.w != NULL (lbt_step_reduce_update):
+// MomentumOptimizer on each dw element as it is formed.
 LBT_DEV void head_reduce(const lbt_head& h, const lbt_xchg& x, uint8_t* lds, const lbt_update& u) {
-  uint32_t* s_rec = reinterpret_cast<uint32_t*>(lds);
-  int(*s_acc)[16] = reinterpret_cast<int(*)[16]>(lds + kHeadRecBytes);
+  (void)lds;
   __shared__ double s_red[kHeadT];
-  const int t = threadIdx.x, C = h.C, K = h.K, N = h.N;
-  const int rs = C + kHeadRecPad, words = rs / 4;
-  const int chunk = (kHeadRecBytes / 4) / words;  // samples per pass
-  const int G = kHeadT / C, c = t % C, g = t / C;  // thread (c, g): channel c, samples g, g+G, ...
+  const int t = threadIdx.x, C = h.C, K = h.K, N = h.N, NP = head_np(N);
+  const int G = kHeadT / C, c = t % C, kq = t / C;  // threads t >= G * C idle (C <= 256)
+  const int kpt = (K + G - 1) / G, k0 = kq * kpt;
+  const int nk = kq < G ? (K - k0 < kpt ? (K - k0 > 0 ? K - k0 : 0) : kpt) : 0;
   const uint8_t* scr = reinterpret_cast<const uint8_t*>(h.scratch);
+  const uint4* pr = reinterpret_cast<const uint4*>(scr + (int64_t)c * NP);
+  const uint8_t* gbase = scr + head_gq_off(N, C);
+  const double* term = reinterpret_cast<const double*>(scr + head_term_off(N, C));
   const float wscale = ldexpf(1.0f, -(frac_exp(h.qx) + frac_exp(h.qg)));
+  // the loss terms: thread t sums rows t, t + 256, ... in order (softmax_xent_kernel's order), issued first
   double part = 0.0;
-  for (int kb = 0; kb < K; kb += 16) {
-    float wf[16 * 256 / kHeadT];  // this pass's fp32 weights (decay term), loaded ahead
-    float af[16 * 256 / kHeadT];  // ... and their momentum accumulators (u.w)
-    const int64_t ob = u.w ? h.dw - u.g : 0;
+  for (int r = t; r < N; r += kHeadT) part += term[r];
+  const int64_t ob = u.w ? h.dw - u.g : 0;
+  for (int kb = k0; kb < k0 + nk; kb += 4) {  // 4 outputs per pass, in registers
+    const int n4 = k0 + nk - kb < 4 ? k0 + nk - kb : 4;
+    int acc[4] = {0, 0, 0, 0};
+    for (int m = 0; m < NP / 16; ++m) {
+      uint4 a = pr[m];
+      const int valid = N - 16 * m;  // samples of this 16-byte group that exist
+      if (valid < 16) {              // the last group: bytes of samples >= N masked (pads are not written)
+        uint32_t w[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
-    for (int j = 0; j < 16 * 256 / kHeadT; ++j) {
-      const int o = t + j * kHeadT, oc = o >> 4, ok = kb + (o & 15);
-      const int e = (oc < C && ok < K) ? oc * K + ok : 0;
-      wf[j] = h.w[e];
-      af[j] = u.w ? u.a[ob + e] : 0.f;
-    }
-    int sacc[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) sacc[j] = 0;
-    for (int n0 = 0; n0 < N; n0 += chunk) {
-      const int nn = N - n0 < chunk ? N - n0 : chunk;
-      __syncthreads();
-      {  // every load in flight before the first LDS write (clamped addresses, no branches)
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(scr + (int64_t)n0 * rs);
-        const int lim = nn * words;
-        uint32_t v[kHeadRecBytes / 4 / kHeadT];
-#pragma unroll
-        for (int j = 0; j < kHeadRecBytes / 4 / kHeadT; ++j) {
-          const int i = t + j * kHeadT;
-          v[j] = src[i < lim ? i : 0];
+        for (int q = 0; q < 4; ++q) {
+          const int nv = valid - 4 * q;
+          w[q] = nv >= 4 ? w[q] : (nv <= 0 ? 0u : w[q] & ((1u << (8 * nv)) - 1u));
         }
-#pragma unroll
-        for (int j = 0; j < kHeadRecBytes / 4 / kHeadT; ++j) s_rec[t + j * kHeadT] = v[j];
+        a = make_uint4(w[0], w[1], w[2], w[3]);
       }
-      __syncthreads();
-      const uint8_t* r8 = reinterpret_cast<const uint8_t*>(s_rec);
-      if (g < G) {
-#pragma unroll 4
-        for (int r = g; r < nn; r += G) {
-          const int x = (int)(int8_t)r8[r * rs + c];
-          const uint32_t* gw = s_rec + r * words + C / 4 + kb / 4;  // 4-byte aligned only
-          const uint32_t gv[4] = {gw[0], gw[1], gw[2], gw[3]};
 #pragma unroll
-          for (int w4 = 0; w4 < 4; ++w4)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) sacc[4 * w4 + b] += x * (int)(int8_t)(gv[w4] >> (8 * b));
-        }
-      }
-      if (kb == 0) {  // loss terms: thread t sums rows t, t + 256, ... in order (softmax_xent_kernel)
-        for (int r = (t - n0 % kHeadT + kHeadT) % kHeadT; r < nn; r += kHeadT) {
-          const uint32_t* tw = s_rec + r * words + C / 4 + 16;
-          part += __longlong_as_double((long long)((uint64_t)tw[0] | ((uint64_t)tw[1] << 32)));
-        }
+      for (int i = 0; i < 4; ++i) {
+        if (i >= n4) break;
+        const uint4 g = reinterpret_cast<const uint4*>(gbase + (int64_t)(kb + i) * NP)[m];
+        int v = acc[i];
+        v = __builtin_amdgcn_sdot4((int)a.x, (int)g.x, v, false);
+        v = __builtin_amdgcn_sdot4((int)a.y, (int)g.y, v, false);
+        v = __builtin_amdgcn_sdot4((int)a.z, (int)g.z, v, false);
+        v = __builtin_amdgcn_sdot4((int)a.w, (int)g.w, v, false);
+        acc[i] = v;
       }
     }
-    __syncthreads();
-    if (g < G) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) s_acc[g * C + c][j] = sacc[j];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 16 * 256 / kHeadT; ++j) {
-      const int o = t + j * kHeadT, oc = o >> 4, ok = kb + (o & 15);
-      if (oc < C && ok < K) {
-        int sum = 0;
-        for (int gg = 0; gg < G; ++gg) sum += s_acc[gg * C + oc][o & 15];
-        if (x.buf) {
-          x.buf[(h.dw - x.gbase) + oc * K + ok] = (long long)sum;
-          continue;
-        }
-        const float a = (float)(long long)sum * wscale;
-        const float b = h.wd2 * wf[j];
-        const float gv = a + b;
-        h.dw[oc * K + ok] = gv;
-        if (u.w) {  // sgd_momentum_elem's arithmetic (gscale 1)
-          const float tm = u.mu * af[j];
-          const float an = tm + gv;
-          LBT_ST_TAIL(u.a + ob + oc * K + ok, an);
-          const float stp = u.lr * an;
-          LBT_ST_TAIL(u.w + ob + oc * K + ok, wf[j] - stp);
-        }
+    for (int i = 0; i < 4; ++i) {
+      if (i >= n4) break;
+      const int e = c * K + kb + i;
+      if (x.buf) {
+        x.buf[(h.dw - x.gbase) + e] = (long long)acc[i];
+        continue;
+      }
+      const float a = (float)(long long)acc[i] * wscale;
+      const float b = h.wd2 * h.w[e];
+      const float gv = a + b;
+      h.dw[e] = gv;
+      if (u.w) {  // sgd_momentum_elem's arithmetic (gscale 1)
+        const float tm = u.mu * u.a[ob + e];
+        const float an = tm + gv;
+        LBT_ST_TAIL(u.a + ob + e, an);
+        const float stp = u.lr * an;
+        LBT_ST_TAIL(u.w + ob + e, h.w[e] - stp);
       }
     }
   }

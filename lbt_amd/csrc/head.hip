@@ -184,6 +184,65 @@ LBT_DEV void head_pass_a(const lbt_chain_bwd_a& a, int n, int HW, int C, int q0,
   }
 }
 
+// 64-bit sum over the four 16-lane rows of a wave (v_permlane16 / 32 swaps on both halves)
+LBT_DEV long long head_rows_total64(long long v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)((unsigned long long)v >> 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  v = (long long)(((unsigned long long)b[0] << 32) | a[0]) + (long long)(((unsigned long long)b[1] << 32) | a[1]);
+  const uint32_t lo2 = (uint32_t)v, hi2 = (uint32_t)((unsigned long long)v >> 32);
+  const auto c = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
+  const auto d = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
+  return (long long)(((unsigned long long)d[0] << 32) | c[0]) + (long long)(((unsigned long long)d[1] << 32) | c[1]);
+}
+
+// The end chain's Normalization_q moment sums (the chain's sharded [32][2C] channel sums), issued as
+// the launch's FIRST loads: wave w owns channels 16 w .. 16 w + 15 (C <= 64), lane l channel
+// 16 w + (l & 15) of shards 8 (l >> 4) .. + 7 -- each load instruction covers 4 shards x 16 channels.
+// (bn_moments had threads c < 2C issue all 32 shard loads each behind the launch's other loads.)
+struct HeadStat {
+  long long v[8][2];
+};
+LBT_DEV void head_stat_load(const lbt_bn_norm& b, int C, HeadStat& hs) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = wave * 16 + (lane & 15);
+  const int64_t* cs = b.chsum + (int64_t)(8 * (lane >> 4)) * 2 * C + (c < C ? c : 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    hs.v[i][0] = cs[(int64_t)i * 2 * C];
+    hs.v[i][1] = cs[(int64_t)i * 2 * C + C];
+  }
+}
+// bn_moments' arithmetic on the loaded sums -> mu / sigma in LDS (and ms / running stats from workgroup 0)
+LBT_DEV void head_stat_finish(const lbt_bn_norm& b, int C, const HeadStat& hs, float* mu, float* sg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  long long S1 = 0, S2 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    S1 += hs.v[i][0];
+    S2 += hs.v[i][1];
+  }
+  S1 = head_rows_total64(S1);
+  S2 = head_rows_total64(S2);
+  const int c = wave * 16 + (lane & 15);
+  if (lane < 16 && c < C) {
+    const double s = ldexp(1.0, -frac_exp(b.qn));
+    const double mean_d = (double)S1 * s / (double)b.n;
+    const double var_d = (double)S2 * (s * s) / (double)b.n - mean_d * mean_d;
+    const float m = (float)mean_d, v = (float)var_d;
+    const float sigma = sqrtf(v + b.eps);
+    mu[c] = m;
+    sg[c] = sigma;
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      if (b.ms) { b.ms[c] = m; b.ms[C + c] = sigma; }
+      if (b.run_mean) {
+        b.run_mean[c] = b.momentum * b.run_mean[c] + b.one_minus_momentum * m;
+        b.run_var[c] = b.momentum * b.run_var[c] + b.one_minus_momentum * v;
+      }
+    }
+  }
+}
+
 // ---- the last block's end chain inside the head (lbt_head.chain): bn.hip chain_fwd_kernel<1, kFQ |
 // kFRes | kFRelu | kFStoch>'s arithmetic, element for element, over the whole sample (kChainSlots
 // channel quads per thread; the pooling needs every pixel). Slot j < own covers this workgroup's pass-A
@@ -216,10 +275,13 @@ LBT_DEV void chain_load(const lbt_chain_fwd& a, int n, int q0, int own, ChainIn&
 // mu / sigma / gamma_q / beta_q per channel into P[4C] (LDS), then the chain; own slots count qr's
 // overflows into ov1 / ov2 (wave totals, quant_w2)
 LBT_DEV void chain_eval(const lbt_chain_fwd& a, int own, const ChainIn& in, float* P, long long* tmp, ChainOut& out,
-                        int& ov1, int& ov2) {
+                        int& ov1, int& ov2, const HeadStat& hs, bool hstat) {
   const lbt_chain_branch& B = a.b1;
   const int C = a.C, t = threadIdx.x;
-  bn_moments(B.nrm, C, P, P + C, tmp);
+  if (hstat)  // uniform: the sums loaded at the top of the launch
+    head_stat_finish(B.nrm, C, hs, P, P + C);
+  else
+    bn_moments(B.nrm, C, P, P + C, tmp);
   for (int c = t; c < C; c += kT) { P[2 * C + c] = B.gb[c]; P[3 * C + c] = B.gb[C + c]; }
   __syncthreads();
   const int c0 = (4 * t) % C;
@@ -282,6 +344,10 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   const int C = h.C, K = h.K, HW = h.HW, N = h.N;
   const int q0 = split * (HW / S) * C / 4, q1 = q0 + (HW / S) * C / 4;  // host: HW % S == 0
   LBT_TS(0);
+  // the end chain's moment sums before anything else (they gate the chain)
+  HeadStat hs;
+  const bool hstat = CHAIN && ch.C <= 4 * 16;  // uniform: one 16-channel group per wave
+  if (hstat) head_stat_load(ch.b1.nrm, ch.C, hs);
   const QState sx = qstate(h.qx), sg = qstate(h.qg);
   int ovx1 = 0, ovx2 = 0, ovg1 = 0, ovg2 = 0;  // wave totals (quant_w)
 
@@ -325,7 +391,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     __shared__ float s_P[4 * 256];
     __shared__ long long s_t[2 * 256];
     ChainOut co;
-    chain_eval(ch, own, cin, s_P, s_t, co, ovr1, ovr2);
+    chain_eval(ch, own, cin, s_P, s_t, co, ovr1, ovr2, hs, hstat);
     const int Q = HW * C / 4;
 #pragma unroll
     for (int j = 0; j < kChainSlots; ++j) reinterpret_cast<float4*>(s_x)[chain_quad(j, own, q0, Q, t)] = co.y[j];
@@ -430,8 +496,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     if (lane == 0 && lead) {
       const float lse = logf(s) + m;
       const double term = (double)(lse - s_z[y]);
-      uint8_t* rec = reinterpret_cast<uint8_t*>(h.scratch) + (int64_t)n * (C + kHeadRecPad);
-      *reinterpret_cast<double*>(rec + C + 64) = term;  // 8-byte aligned: C % 8 == 0
+      reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(h.scratch) + head_term_off(N, C))[n] = term;
     }
   }
   counts_stage_w(0, 5, ovx1, ovx2, sh_cnt);
@@ -445,21 +510,12 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   if constexpr (CHAIN) counts_publish(4, 5, ch.b1.qr, sh_cnt);
 
   LBT_TS(3);
-  // ---- the record's codes: pq[C] | gq[64]
+  // ---- the sample's column of the transposed records (head.h): pqT[c][n], gqT[k][n]
   if (lead) {
-    uint32_t* rec = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(h.scratch) + (int64_t)n * (C + kHeadRecPad));
-    if (t < C / 4) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) w |= (uint32_t)(s_pq[4 * t + b] & 255) << (8 * b);
-      rec[t] = w;
-    } else if (t >= 64 && t < 80) {
-      const int j = t - 64;
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) w |= (uint32_t)((4 * j + b < K ? s_gq[4 * j + b] : 0) & 255) << (8 * b);
-      rec[C / 4 + j] = w;
-    }
+    uint8_t* scr = reinterpret_cast<uint8_t*>(h.scratch);
+    const int NP = head_np(N);
+    if (t < C) scr[(int64_t)t * NP + n] = (uint8_t)s_pq[t];
+    if (t < K) scr[head_gq_off(N, C) + (int64_t)t * NP + n] = (uint8_t)s_gq[t];
   }
 
   // ---- Dense_q dgrad + AvgPool_q backward: gx[n][p][c] = ((float)(sum_k gq[k] wq[c][k]) * s) * (1/HW)
@@ -500,7 +556,7 @@ LBT_TRACE_SETTER(head)
 
 extern "C" int lbt_head_scratch_bytes(int32_t N, int32_t C, int32_t K) {
   (void)K;
-  return N * (C + kHeadRecPad);
+  return (int)head_scratch_bytes(N, C);
 }
 
 extern "C" int lbt_head_fwd_bwd(const lbt_head* h, void* stream) {
@@ -525,7 +581,7 @@ extern "C" int lbt_head_fwd_bwd(const lbt_head* h, void* stream) {
         a.b1.qng.bits <= 0 || !a.b1.qrg.stochastic || !a.b1.qng.stochastic)
       return LBT_EINVAL;
   }
-  if ((int64_t)h->N * (h->C + kHeadRecPad) >= ((int64_t)1 << 31)) return LBT_EINVAL;
+  if (head_scratch_bytes(h->N, h->C) >= ((int64_t)1 << 31)) return LBT_EINVAL;
   if ((reinterpret_cast<uintptr_t>(h->wq) & 3) || (reinterpret_cast<uintptr_t>(h->x) & 15) ||
       (reinterpret_cast<uintptr_t>(h->scratch) & 7))
     return LBT_EINVAL;

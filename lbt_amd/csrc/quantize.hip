@@ -307,4 +307,4 @@ extern "C" int lbt_dfxp_quantize_weight(const float* w, int32_t KH, int32_t KW, 
   return (int)hipGetLastError();
 }
 
-extern "C" int lbt_abi_version(void) { return 20; }
+extern "C" int lbt_abi_version(void) { return 21; }

@@ -206,6 +206,7 @@ def wgrad_s1_ok(d):
 
 
 WGRAD_CPW = int(os.environ.get("LBT_WGRAD_CPW", "8"))  # batched staged wgrad: 64-pixel chunks per wave
+WGRAD_MIN_UNITS = int(os.environ.get("LBT_WGRAD_MIN_UNITS", "32"))  # batched staged wgrad: workgroups per job, at least
 WGRAD_UNITS = int(os.environ.get("LBT_WGRAD_UNITS", "64"))  # batched per-tap wgrad: workgroups per conv (sweep: 32 / 48 / 64 / 80 / 96 / 128 -> 49 / 30 / 26 / 29 / 29 / 30 us)
 
 
@@ -217,6 +218,13 @@ def wgrad_nsplit_batched(d, chunks_per_wave=None):
     if wgrad_s1_ok(d):
         chunks = P // 64
         ns = max(1, chunks // (8 * (chunks_per_wave or WGRAD_CPW)))
+        if chunks_per_wave is None:
+            # small batches: more, shorter splits (down to one chunk per wave) until the job has
+            # WGRAD_MIN_UNITS workgroups -- a job takes as long as one workgroup's serial chunk loop, so
+            # at 16 images per GPU 8 chunks per wave left the launch at 8-16 workgroups (B=128: unchanged)
+            units = (d.Cin // 16) * (d.Cout // 16)
+            while ns * units < WGRAD_MIN_UNITS and 2 * ns * 8 <= chunks:
+                ns *= 2
         while chunks % ns:
             ns -= 1
         return ns

@@ -583,7 +583,7 @@ class FusedResNet:
             j.qrg.exps = j.qr.exps = snap
         hd.qx.exps = hd.qg.exps = snap
         self._rjobs = _dev_array(rjobs, ctx.device)
-        total_blocks = sum((j.K * j.Cout + 255) // 256 for j in rjobs)
+        total_blocks = sum(lib.lbt_rjob_blocks(j.K * j.Cout) for j in rjobs)
         self._pjobs = _dev_array(pjobs, ctx.device)
         max_c = max(j.C for j in pjobs)
         nb_red = sum(4 * j.nsplit * j.K * j.Cout + 8 * j.K * j.Cout for j in rjobs)

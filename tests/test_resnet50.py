@@ -92,10 +92,14 @@ def _batch(B, image, classes, seed):
 @pytest.mark.parametrize("grad_bits", [8, 16])
 @pytest.mark.parametrize("blocks,width,image,classes", [((1, 1, 1, 1), 8, 32, 10), ((2, 1, 1, 1), 16, 40, 10),
                                                         ((1, 1, 1, 1), 8, 32, 16), ((2, 1, 1, 1), 64, 32, 16),
-                                                        ((3, 2, 1, 1), 64, 40, 16)])
+                                                        ((3, 2, 1, 1), 64, 40, 16), ((3, 4, 6, 3), 64, 56, 16),
+                                                        ((3, 4, 6, 3), 64, 224, 1000)])
 def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, classes, grad_bits):
     """classes=16: the fc runs on the int8-MFMA dense kernels (dense.hip), 10: the generic ones.
-    width 64 with 16-bit gradients: every bottleneck runs fused (ResidualBottleneck_q._fusable)."""
+    width 64 with 16-bit gradients: every bottleneck runs fused (ResidualBottleneck_q._fusable).
+    (3, 4, 6, 3) at width 64: the benched ResNet-50's depth and widths (stage 3's six-block chain, the
+    2048-channel last stage), at 56x56 and at the benched 224x224 / 1000 classes (configs[3] itself, at
+    B=4 instead of 256: the oracle takes seconds per image)."""
     from lbt_amd.dfxp.layers import ResidualBottleneck_q
     ctx, gm, om = _pair(blocks, width, classes, image, grad_bits, seed=1)
     assert gm.layers[-1].mfma == (classes % 8 == 0)

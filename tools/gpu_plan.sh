@@ -7,7 +7,7 @@
 # Steps (each under its own time limit; the chain stops at the first failure, so nothing more runs
 # on the GPU after a fault, an abort or a time-out):
 #   tests            the whole -m gpu suite
-#   tests:<file|-k>  a subset: tests:tests/test_gpu_parity.py  or  tests:-k=fused
+#   tests:<path>[:<k>]  a subset: tests:tests/test_gpu_parity.py  or  tests:tests:fused or golden
 #   smoke            __graft_entry__.smoke()
 #   bench[:args]     bench.py (default arguments, or the ':'-separated extra ones, e.g. bench:--batch:16)
 #   r50              bench.py --workload resnet50 --steps 20 --warmup 5
@@ -32,10 +32,16 @@ for step in "$@"; do
   log="$OUT/$(printf %02d $n)_${name}"
   case "$name" in
     tests)
-      sel="tests"
-      [ -n "$rest" ] && sel=${args//=/ }
-      timeout -k 10 900 python -u -m pytest $sel -m gpu -x -q --timeout 240 --timeout-method thread \
-        > "$log.log" 2>&1; rc=$?
+      # tests[:<path>[:<-k expression>]]
+      sel="tests"; kx=""
+      if [ -n "$rest" ]; then sel=${rest%%:*}; [ "$rest" != "$sel" ] && kx=${rest#*:}; fi
+      if [ -n "$kx" ]; then
+        timeout -k 10 900 python -u -m pytest $sel -m gpu -x -q --timeout 240 --timeout-method thread -k "$kx" \
+          > "$log.log" 2>&1; rc=$?
+      else
+        timeout -k 10 900 python -u -m pytest $sel -m gpu -x -q --timeout 240 --timeout-method thread \
+          > "$log.log" 2>&1; rc=$?
+      fi
       tail -3 "$log.log" ;;
     smoke)
       timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$log.log" 2>&1; rc=$?

@@ -46,10 +46,11 @@ def main():
     ap.add_argument("--filter", default="conv_bwd_kernel")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--max", type=int, default=40)
+    ap.add_argument("--lib", default=None, help="another -DLBT_TRACE build (tools/build_variant.py)")
     a = ap.parse_args()
     if a.build:
         return build()
-    os.environ["LBT_LIBRARY"] = TRACE_LIB
+    os.environ["LBT_LIBRARY"] = a.lib or TRACE_LIB
     sys.path.insert(0, ROOT)
     import torch
     import bench
