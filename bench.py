@@ -219,6 +219,10 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group plumbing only (CPU, gloo): each step is one all-reduce of a "
                          "small CPU tensor; used by the CPU tests, never a measurement")
+    ap.add_argument("--grad-range", type=int, default=-6,
+                    help="ResNet-20: the gradient quantisers' initial exponent I (the layers' grad_range argument, "
+                         "dynamic_fixed_point.py:225,321,541,628). -6 (default): a run that trains; 2: the reference's "
+                         "default, with which this random-label run diverges (DESIGN 4). The work per step is the same")
     ap.add_argument("--workload", choices=("resnet20", "resnet50", "resnet20w4"), default="resnet20",
                     help="resnet50: BASELINE configs[3], ImageNet-shape, 16-bit gradients (layer path); "
                          "resnet20w4: configs[4], 4-bit packed weights")
@@ -282,7 +286,8 @@ def main():
         model = ImageNet_Resnet50(8, grad_bits=16, weight_decay=1e-4, ctx=ctx)
         xs, ys = synthetic_imagenet(4, args.batch, 1000 + rank, device)
     else:
-        model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, weight_bits=4 if w4 else None)
+        model = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, weight_bits=4 if w4 else None,
+                                 grad_range=args.grad_range)
         if not args.layerwise:
             from lbt_amd.fused import FusedResNet
             model = FusedResNet(model, sync_bn=bn_mode == "sync")
@@ -318,7 +323,8 @@ def main():
         "config": {"workload": "ResNet-20 CIFAR-10 8-bit DFXP W/A/G train step (fwd+bwd+SGD-momentum+range update)",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch, "image": [32, 32, 3],
                    "parallelism": "dp%d" % world, "hip_graph": not args.eager,
-                   "executor": "layerwise" if args.layerwise else "fused", "final_loss": round(loss, 4)},
+                   "executor": "layerwise" if args.layerwise else "fused", "final_loss": round(loss, 4),
+                   "grad_range": args.grad_range},
     }
     if world > 1 or strong:
         out["config"]["backend"] = backend if world > 1 else None

@@ -1186,8 +1186,22 @@ constexpr int kBThreads = kBNW * 64;
 // two 512-thread workgroups per CU), 4 otherwise (W * C == 512: a 4-row tile is 8 MFMA tiles)
 __host__ __device__ constexpr int tile_rows(int CS) { return CS == 1 ? 8 : 4; }
 // phase-1 (halo) channel-quad groups per thread
-__host__ __device__ constexpr int halo_iters(int CS) {
-  return ((tile_rows(CS) + 2) * (512 / (CS * 16) + 2) * CS * 4 + kBThreads - 1) / kBThreads;
+__host__ __device__ constexpr int halo_iters(int CS, int TH) {
+  return ((TH + 2) * (512 / (CS * 16) + 2) * CS * 4 + kBThreads - 1) / kBThreads;
+}
+__host__ __device__ constexpr int halo_iters(int CS) { return halo_iters(CS, tile_rows(CS)); }
+// Batch-adaptive tile rows of the fused conv kernels: the 16-channel stage takes 4-row tiles when its
+// 8-row tiles leave the launch with fewer workgroups than CUs (N * H / 8 < 256: per-GPU batches below
+// 64 -- the strong-scaling shards of configs[2]): twice the workgroups, each with two thirds of the halo
+// rows of phase 1, half the phase-3 groups and MFMA pairs per wave. LBT_TILE_ROWS1=8|4 forces one.
+inline int tile_rows_for(int CS, int64_t N, int H) {
+  if (CS != 1) return tile_rows(CS);
+  static const int force = [] {
+    const char* e = getenv("LBT_TILE_ROWS1");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 4 || force == 8) return H % force ? 8 : force;
+  return (N * H / 8 < 256 && H % 4 == 0) ? 4 : 8;
 }
 
 // The conv's weight image shared through LDS by the fused conv kernels: [C columns][KS k-slices] of 16
@@ -1392,12 +1406,13 @@ LBT_DEV int pack4f(f2 a, f2 b) {
   return pack4(c);
 }
 
-template <int CS, int CF, int NB, bool W4, int WCS>
+template <int CS, int CF, int NB, bool W4, int WCS, int TH = tile_rows(CS)>
 __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(ConvBwdArgs p, WgradArgs wa, uint32_t nwg) {
   constexpr int C = CS * 16, C4 = C / 4, NT = CS;
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   constexpr int WC = WCS ? WCS : 1;
-  constexpr int TH = tile_rows(CS), kBIt = halo_iters(CS), J = TH / 4;  // J: phase-3 groups per thread
+  constexpr int kBIt = halo_iters(CS, TH), J = TH / 4;  // J: phase-3 groups per thread
+  static_assert(TH % 4 == 0, "a tile is whole groups of 4 rows (8 MFMA pairs, one per wave)");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   union Smem {
     BwdShared<C, TH, WI::kBytes> b;
@@ -1786,19 +1801,26 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   ConvBwdArgs p;
   p.b = b; p.wd = q->wd; p.ks = q->ksd; p.nslices = 9 * CS; p.w4 = q->w4; p.qw = q->qw;
   p.H = d.H; p.W = d.W; p.add_src = q->add_src; p.a = a;
-  const int64_t tiles = (int64_t)d.N * (d.H / tile_rows(CS));
+  const int th = tile_rows_for(CS, d.N, d.H);
+  const int64_t tiles = (int64_t)d.N * (d.H / th);
   if (tiles + wblocks > 0x7fffffff) return LBT_EINVAL;
   const dim3 grid((unsigned)(tiles + wblocks));
   hipStream_t st = (hipStream_t)stream;
   const int nb = a.has_b2 ? 2 : 1;
   // the combinations the fused ResNet plan runs (c2: mask from R1, deferred wgrad of the next
   // block's c1 or none; c1: its consumer's chain, deferred wgrad of the same block's c2)
+#define LBT_BW_TH(CS_, CF_, NB_, WCS_, TH_)                                                                 \
+  if (q->w4)                                                                                                \
+    hipLaunchKernelGGL((conv_bwd_kernel<CS_, CF_, NB_, true, WCS_, TH_>), grid, dim3(kBThreads), 0, st, p, wa, wblocks); \
+  else                                                                                                      \
+    hipLaunchKernelGGL((conv_bwd_kernel<CS_, CF_, NB_, false, WCS_, TH_>), grid, dim3(kBThreads), 0, st, p, wa, wblocks);
 #define LBT_BW(CS_, CF_, NB_, WCS_)                                                                  \
   if (CS == CS_ && f == (CF_) && nb == NB_ && wcs == WCS_) {                                       \
-    if (q->w4)                                                                                     \
-      hipLaunchKernelGGL((conv_bwd_kernel<CS_, CF_, NB_, true, WCS_>), grid, dim3(kBThreads), 0, st, p, wa, wblocks); \
-    else                                                                                           \
-      hipLaunchKernelGGL((conv_bwd_kernel<CS_, CF_, NB_, false, WCS_>), grid, dim3(kBThreads), 0, st, p, wa, wblocks); \
+    if (CS_ == 1 && th == 4) {                                                                     \
+      LBT_BW_TH(CS_, CF_, NB_, WCS_, 4)                                                            \
+    } else {                                                                                       \
+      LBT_BW_TH(CS_, CF_, NB_, WCS_, tile_rows(CS_))                                               \
+    }                                                                                              \
     return (int)hipGetLastError();                                                                 \
   }
   // (WCS = 0 everywhere: the plan's LBT_SIDE_WGRAD mode runs each wgrad as a parallel branch)
@@ -1819,6 +1841,7 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   LBT_BW(2, kAFused | kAMaskR, 1, 4)
 #undef LBT_BW_CS
 #undef LBT_BW
+#undef LBT_BW_TH
   return LBT_EINVAL;
 }
 
@@ -2325,11 +2348,12 @@ struct FwdShared {
   int cnt[kBNW * 2 * 4];                       // counters: R (2 branches), X, output
 };
 
-template <int CS, int NB, int F, bool W4>
+template <int CS, int NB, int F, bool W4, int TH = tile_rows(CS)>
 __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_kernel(ConvFwdArgs p) {
   constexpr int C = CS * 16, C4 = C / 4, NT = CS, W = 512 / C, Wp = W + 2;
   constexpr int kMaxKS = (9 * CS + 3) / 4;
-  constexpr int TH = tile_rows(CS), kBIt = halo_iters(CS), J = TH / 4;
+  constexpr int kBIt = halo_iters(CS, TH), J = TH / 4;
+  static_assert(TH % 4 == 0, "a tile is whole groups of 4 rows (8 MFMA pairs, one per wave)");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   __shared__ __attribute__((aligned(16))) FwdShared<C, TH, WI::kBytes> sh;
   LBT_TS(0);
@@ -2950,18 +2974,25 @@ extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
   ConvFwdArgs p;
   p.c = a; p.wf = q->wf; p.wcolsum = q->wcolsum; p.qw = q->qw; p.H = d.H;
   p.yq = q->yq; p.qout = q->qout; p.ychsum = q->ychsum;
-  const int64_t tiles = (int64_t)d.N * (d.H / tile_rows(CS));
+  const int th = tile_rows_for(CS, d.N, d.H);
+  const int64_t tiles = (int64_t)d.N * (d.H / th);
   if (tiles > 0x7fffffff) return LBT_EINVAL;
   const dim3 grid((unsigned)tiles);
   hipStream_t st = (hipStream_t)stream;
   const int nb = a.has_b2 ? 2 : 1;
   const int fl = f & ~kFU8 & ~kFStoch;  // variant key: Y / residual present
+#define LBT_FW_TH(CS_, NB_, FL_, TH_)                                                                        \
+  if (q->w4)                                                                                                 \
+    hipLaunchKernelGGL((conv_fwd_fused_kernel<CS_, NB_, FL_, true, TH_>), grid, dim3(kBThreads), 0, st, p);    \
+  else                                                                                                       \
+    hipLaunchKernelGGL((conv_fwd_fused_kernel<CS_, NB_, FL_, false, TH_>), grid, dim3(kBThreads), 0, st, p);
 #define LBT_FW(CS_, NB_, FL_)                                                                            \
   if (CS == CS_ && nb == NB_ && fl == ((FL_) & ~kFU8 & ~kFStoch)) {                                      \
-    if (q->w4)                                                                                           \
-      hipLaunchKernelGGL((conv_fwd_fused_kernel<CS_, NB_, FL_, true>), grid, dim3(kBThreads), 0, st, p);   \
-    else                                                                                                 \
-      hipLaunchKernelGGL((conv_fwd_fused_kernel<CS_, NB_, FL_, false>), grid, dim3(kBThreads), 0, st, p);  \
+    if (CS_ == 1 && th == 4) {                                                                           \
+      LBT_FW_TH(CS_, NB_, FL_, 4)                                                                        \
+    } else {                                                                                             \
+      LBT_FW_TH(CS_, NB_, FL_, tile_rows(CS_))                                                           \
+    }                                                                                                    \
     return (int)hipGetLastError();                                                                       \
   }
   // c2 (bn1 chain), c1 after an identity / projection block, block 0's c1 (the stem's chain)
@@ -2976,6 +3007,7 @@ extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
   LBT_FW_CS(4)
 #undef LBT_FW_CS
 #undef LBT_FW
+#undef LBT_FW_TH
   return LBT_EINVAL;
 }
 

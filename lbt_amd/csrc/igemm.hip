@@ -19,6 +19,7 @@
 // A8: int8 codes, either signed (fill 0) or offset-by-128 ("u8off", fill -128, + 128 sum_k w).
 #include "dfxp_device.h"
 #include "lds_tr.h"
+#include "pk2.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -601,51 +602,80 @@ LBT_DEV void passa_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const 
 #pragma unroll
     for (int a = 0; a < 4; ++a) sm[a][0] = sm[a][1] = sm[a][2] = sm[a][3] = 0;
     int ov[4] = {0, 0, 0, 0};
+    // PK: both gradient quantisers stochastic (the models' configuration): quant4_w on packed pairs, the
+    // counts as wave totals (lane 0 is active whenever a lane of its wave is: the inactive lanes of a sample
+    // step are the wave's highest, past the image's last pixel); else quant1 per element, per-lane counts
+    auto samples = [&](auto pkc) {
+      constexpr bool PK = decltype(pkc)::value;
 #pragma unroll LBT_EPI_UNROLL
-    for (int u = 0; u < 8; ++u) {
-      const int s_ = sbase + u;
-      if (!pv || s_ >= N) break;  // samples ascend: the rest of this thread's are outside too
-      const int64_t off = ((int64_t)s_ * hw + pix) * C + c0;
-      const float4 xv = *reinterpret_cast<const float4*>(xs + pl * kXPix + (sh * 8 + u) * kXRow + 4 * cq);
-      float d[4] = {xv.x, xv.y, xv.z, xv.w};
-      const char4 rv = *reinterpret_cast<const char4*>(bn.R + off);
-      const char4 qv = *reinterpret_cast<const char4*>(bn.qn + off);
-      const int R[4] = {rv.x, rv.y, rv.z, rv.w};
-      const int Q[4] = {qv.x, qv.y, qv.z, qv.w};
-      if constexpr (MA >= 2) {  // bn_wide.hip :123-138
-        const float4 g2 = *reinterpret_cast<const float4*>(p.bn3.g2 + off);
-        const uint32_t yb = p.bn3.y_bits[off >> 2];
-        d[0] = (yb & 1u) ? d[0] + g2.x : 0.f;
-        d[1] = (yb & 2u) ? d[1] + g2.y : 0.f;
-        d[2] = (yb & 4u) ? d[2] + g2.z : 0.f;
-        d[3] = (yb & 8u) ? d[3] + g2.w : 0.f;
-        if (k == 0 && p.bn3.gmask_out)
-          *reinterpret_cast<float4*>(p.bn3.gmask_out + off) = make_float4(d[0], d[1], d[2], d[3]);
-      } else {  // bn.hip chain_bwd_a's mask recomputation, op for op (bn_wide.hip :139-147)
+      for (int u = 0; u < 8; ++u) {
+        const int s_ = sbase + u;
+        if (!pv || s_ >= N) break;  // samples ascend: the rest of this thread's are outside too
+        const int64_t off = ((int64_t)s_ * hw + pix) * C + c0;
+        const float4 xv = *reinterpret_cast<const float4*>(xs + pl * kXPix + (sh * 8 + u) * kXRow + 4 * cq);
+        float d[4] = {xv.x, xv.y, xv.z, xv.w};
+        const char4 rv = *reinterpret_cast<const char4*>(bn.R + off);
+        const char4 qv = *reinterpret_cast<const char4*>(bn.qn + off);
+        const int R[4] = {rv.x, rv.y, rv.z, rv.w};
+        const int Q[4] = {qv.x, qv.y, qv.z, qv.w};
+        if constexpr (MA >= 2) {  // bn_wide.hip :123-138
+          const float4 g2 = *reinterpret_cast<const float4*>(p.bn3.g2 + off);
+          const uint32_t yb = p.bn3.y_bits[off >> 2];
+          d[0] = (yb & 1u) ? d[0] + g2.x : 0.f;
+          d[1] = (yb & 2u) ? d[1] + g2.y : 0.f;
+          d[2] = (yb & 4u) ? d[2] + g2.z : 0.f;
+          d[3] = (yb & 8u) ? d[3] + g2.w : 0.f;
+          if (k == 0 && p.bn3.gmask_out)
+            *reinterpret_cast<float4*>(p.bn3.gmask_out + off) = make_float4(d[0], d[1], d[2], d[3]);
+        } else {  // bn.hip chain_bwd_a's mask recomputation, op for op (bn_wide.hip :139-147)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float xr = (float)R[c] * sr;
-          const float m1 = xr * gam[c];
-          const float yv = m1 + bet[c];
-          d[c] = yv > 0.f ? d[c] : 0.f;
+          for (int c = 0; c < 4; ++c) {
+            const float xr = (float)R[c] * sr;
+            const float m1 = xr * gam[c];
+            const float yv = m1 + bet[c];
+            d[c] = yv > 0.f ? d[c] : 0.f;
+          }
         }
-      }
-      int G[4];
+        int G[4];
+        if constexpr (PK) {  // bn_wide.hip :150-175 on packed pairs
+          int G2[4];
+          quant4_w<true>(srg, make_float4(d[0], d[1], d[2], d[3]), make_float4(u1.u[0], u1.u[1], u1.u[2], u1.u[3]), G2,
+                         ov[0], ov[1]);
+          const pf2 im = pk(srg.inv_m, srg.inv_m);
+          const pf2 gh0 = pcvt(G2[0], G2[1]) * im, gh1 = pcvt(G2[2], G2[3]) * im;
+          const pf2 dd0 = gh0 * pk(gam[0], gam[1]), dd1 = gh1 * pk(gam[2], gam[3]);
+          quant4_w<true>(sng, make_float4(dd0.x, dd0.y, dd1.x, dd1.y), make_float4(u2.u[0], u2.u[1], u2.u[2], u2.u[3]),
+                         G, ov[2], ov[3]);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {  // bn_wide.hip :150-175
-        const int G2 = quant1(srg, bn.qrg.stochastic, d[c], u1.u[c], ov[0], ov[1]);
-        sm[0][c] += G2 * R[c];
-        sm[1][c] += G2;
-        const float gh = (float)G2 * srg.inv_m;
-        const float dd = gh * gam[c];
-        G[c] = quant1(sng, bn.qng.stochastic, dd, u2.u[c], ov[2], ov[3]);
-        sm[2][c] += G[c];
-        sm[3][c] += G[c] * Q[c];
+          for (int c = 0; c < 4; ++c) {
+            sm[0][c] += G2[c] * R[c];
+            sm[1][c] += G2[c];
+            sm[2][c] += G[c];
+            sm[3][c] += G[c] * Q[c];
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {  // bn_wide.hip :150-175
+            const int G2 = quant1(srg, bn.qrg.stochastic, d[c], u1.u[c], ov[0], ov[1]);
+            sm[0][c] += G2 * R[c];
+            sm[1][c] += G2;
+            const float gh = (float)G2 * srg.inv_m;
+            const float dd = gh * gam[c];
+            G[c] = quant1(sng, bn.qng.stochastic, dd, u2.u[c], ov[2], ov[3]);
+            sm[2][c] += G[c];
+            sm[3][c] += G[c] * Q[c];
+          }
+        }
+        short4 o;
+        o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
+        *reinterpret_cast<short4*>(bn.gout + off) = o;
       }
-      short4 o;
-      o.x = (short)G[0]; o.y = (short)G[1]; o.z = (short)G[2]; o.w = (short)G[3];
-      *reinterpret_cast<short4*>(bn.gout + off) = o;
-    }
+    };
+    const bool pkq = bn.qrg.stochastic && bn.qng.stochastic;  // uniform
+    if (pkq)
+      samples(std::true_type{});
+    else
+      samples(std::false_type{});
     // channel sums: the 4 pixel lanes of a wave sharing cq (shuffles), the 8 waves in LDS
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -656,9 +686,12 @@ LBT_DEV void passa_epilogue(const IgArgs& p, const v4i (&acc)[2][MI][NJ], const 
         v += __shfl_xor(v, 32, 64);
         if ((t & 63) < 16) red[(wv * 4 + a) * 64 + 4 * cq + c] = v;
       }
-    // per-lane overflow counts -> wave totals -> lane 0
-    const int a0 = wave_sum_i32(ov[0]), a1 = wave_sum_i32(ov[1]);
-    const int b0 = wave_sum_i32(ov[2]), b1 = wave_sum_i32(ov[3]);
+    // overflow counts -> wave totals in lane 0 (already wave totals on the packed path)
+    int a0 = ov[0], a1 = ov[1], b0 = ov[2], b1 = ov[3];
+    if (!pkq) {
+      a0 = wave_sum_i32(a0); a1 = wave_sum_i32(a1);
+      b0 = wave_sum_i32(b0); b1 = wave_sum_i32(b1);
+    }
     if ((t & 63) == 0) {
       if (bn.qrg.counts) {
         int32_t* ct = bn.qrg.counts + ((int64_t)bn.qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
@@ -727,23 +760,35 @@ LBT_DEV void quantq_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4
     const uint64_t blk = ((uint64_t)(pv ? pix : 0) * (uint32_t)C + (uint32_t)c0) >> 2;
     Noise4 u = {{0.f, 0.f, 0.f, 0.f}};
     if (st) u = qnoise4(p.qout, qs.step, blk);
+    const float4 u4 = make_float4(u.u[0], u.u[1], u.u[2], u.u[3]);
     int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+    // this lane's samples sbase .. sbase + nsm - 1 (uniform per wave but for the pixel check): the
+    // output pointer and the LDS row advance by one sample per step (no per-sample 64-bit offsets)
+    const int nsm = pv ? (N - sbase < 8 ? (N - sbase > 0 ? N - sbase : 0) : 8) : 0;
+    int8_t* yp = p.yq + ((int64_t)sbase * hw + pix) * C + c0;
+    const int64_t ystep = (int64_t)hw * C;
+    const float* xp = xs + pl * kXPix + (sh * 8) * kXRow + 4 * cq;
+    auto samples = [&](auto stc) {
+      constexpr bool ST = decltype(stc)::value;
 #pragma unroll LBT_EPI_UNROLL
-    for (int k = 0; k < 8; ++k) {
-      const int sm = sbase + k;
-      if (!pv || sm >= N) break;  // samples ascend
-      const int64_t off = ((int64_t)sm * hw + pix) * C + c0;
-      const float4 xv = *reinterpret_cast<const float4*>(xs + pl * kXPix + (sh * 8 + k) * kXRow + 4 * cq);
-      const float x[4] = {xv.x, xv.y, xv.z, xv.w};
-      int c[4];
+      for (int k = 0; k < 8; ++k) {
+        if (k >= nsm) break;  // samples ascend
+        const float4 xv = *reinterpret_cast<const float4*>(xp + k * kXRow);
+        int c[4];
+        quant4_w<ST>(qs, xv, u4, c, ov1, ov2);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        c[e] = quant1(qs, st, x[e], u.u[e], ov1, ov2);
-        s1[e] += c[e];
-        s2[e] += c[e] * c[e];
+        for (int e = 0; e < 4; ++e) {
+          s1[e] += c[e];
+          s2[e] += c[e] * c[e];
+        }
+        *reinterpret_cast<char4*>(yp) = make_char4((char)c[0], (char)c[1], (char)c[2], (char)c[3]);
+        yp += ystep;
       }
-      *reinterpret_cast<char4*>(p.yq + off) = make_char4((char)c[0], (char)c[1], (char)c[2], (char)c[3]);
-    }
+    };
+    if (st)
+      samples(std::true_type{});
+    else
+      samples(std::false_type{});
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       int a = s1[e], b = s2[e];
@@ -767,8 +812,8 @@ LBT_DEV void quantq_epilogue(const IgArgs& p, const v4i (&acc)[MI][NJ], const v4
     }
     if (h + 1 < BN / 64) __syncthreads();  // red is rewritten by the next half
   }
-  ov1 = wave_sum_i32(ov1);
-  ov2 = wave_sum_i32(ov2);
+  // (wave totals, quant4_w: lane 0 was active whenever a lane of its wave was -- the inactive lanes of a
+  // sample step are the ones past the image's last pixel, the wave's highest)
   if ((t & 63) == 0 && p.qout.counts) {
     int32_t* ct = p.qout.counts + ((int64_t)p.qout.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
     if (ov1) atomicAdd(ct, ov1);

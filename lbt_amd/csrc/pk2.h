@@ -32,4 +32,36 @@ LBT_DEV void quant_w2(const QState& s, int stochastic, pf2 x, pf2 u, int& ov1w, 
   c1 = (int)(st ? floorf(v1) : rintf(v1));
 }
 
+// Four consecutive elements (one float4) through a stochastic (ST) or round-to-nearest quantiser: codes
+// c[0..3] and the overflow counts as WAVE totals added to ov1w / ov2w in every active lane (quant_w's
+// convention). One v_cmp per element and predicate: the asymmetric x*m >= T or x*m < -T (T a power of two)
+// equals max(x*m, -x*m (1 - 2^-24)) >= T (x*m < 0: the product rounds to >= T exactly when -x*m > T; NaN
+// compares false either way); the multiplies / adds run on packed pairs, each half rounded as the scalar
+// op, and the stochastic / nearest choice is compile time -- bit-identical to quant1 / quant_w per element
+// at about half their VALU count.
+template <bool ST>
+LBT_DEV void quant4_w(const QState& s, const float4& x, const float4& u, int (&c)[4], int& ov1w, int& ov2w) {
+  const pf2 m2 = pk(s.m, s.m), k2 = pk(-0x1.fffffep-1f, -0x1.fffffep-1f);
+  const pf2 xm[2] = {pk(x.x, x.y) * m2, pk(x.z, x.w) * m2};
+  const pf2 ng[2] = {xm[0] * k2, xm[1] * k2};
+  const float a[4] = {fmaxf(xm[0].x, ng[0].x), fmaxf(xm[0].y, ng[0].y), fmaxf(xm[1].x, ng[1].x),
+                      fmaxf(xm[1].y, ng[1].y)};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ov1w += __popcll(__ballot(a[e] >= s.L));
+    ov2w += __popcll(__ballot(a[e] >= s.Lh));
+  }
+  pf2 v[2] = {xm[0], xm[1]};
+  if constexpr (ST) {
+    v[0] = v[0] + pk(u.x, u.y);
+    v[1] = v[1] + pk(u.z, u.w);
+  }
+  const float w[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float vv = fminf(fmaxf(w[e], -s.L), s.Lm1);
+    c[e] = (int)(ST ? floorf(vv) : rintf(vv));
+  }
+}
+
 }  // namespace lbt

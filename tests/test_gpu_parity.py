@@ -417,8 +417,8 @@ def _gpu_norms(gm):
     return [l for l in gm._walk() if isinstance(l, Normalization_q)]
 
 
-@pytest.mark.parametrize("weight_bits", [None, 4])
-def test_fused_bench_workload_bitexact_vs_oracle(weight_bits):
+@pytest.mark.parametrize("weight_bits,B", [(None, 128), (4, 128), (None, 16), (None, 32)])
+def test_fused_bench_workload_bitexact_vs_oracle(weight_bits, B):
     """The EXACT timed configuration (bench.py: FusedResNet, B=128, bench batches, HIP-graph replay)
     against the oracle for 3 optimiser steps. B=128 puts stage 1 at P = 131 072 pixels, so the
     one-launch conv backward (dgrad_wgrad_kernel) takes its >= 2-shard int32 wgrad branch. With the
@@ -426,7 +426,8 @@ def test_fused_bench_workload_bitexact_vs_oracle(weight_bits):
     variance (dynamic_fixed_point.py:601-612) are bit-identical after each step; loss at 1e-5.
     weight_bits=4: configs[4]'s timed plan (bench.py --workload resnet20w4: packed 4-bit weight
     images, every fused kernel's W4 variant) against the oracle's 4-bit weight quantisers
-    (dynamic_fixed_point.py:21-38 with bits=4)."""
+    (dynamic_fixed_point.py:21-38 with bits=4). B=16 / 32: configs[2]'s per-GPU shards (global batch
+    128 / 256 over 8 GPUs): the small-batch tile geometry (4-row stage-1 tiles) and wgrad splits."""
     import bench
     from lbt_amd.fused import FusedResNet
     from lbt_amd.trainer import Trainer
@@ -434,8 +435,8 @@ def test_fused_bench_workload_bitexact_vs_oracle(weight_bits):
     fm = FusedResNet(gm)
     state = dict(params=gpu_params(gm), accum=None, ranges=oresnet.init_ranges(om), step=0)
     state["accum"] = {k: np.zeros_like(v) for k, v in state["params"].items()}
-    tr = Trainer(fm, lr=1e-2, momentum=0.9, batch_size=128, use_graph=True)
-    xs, ys = bench.synthetic_batches(4, 128, 1000, DEV)
+    tr = Trainer(fm, lr=1e-2, momentum=0.9, batch_size=B, use_graph=True)
+    xs, ys = bench.synthetic_batches(4, B, 1000, DEV)
     gn, on = _gpu_norms(gm), _oracle_norms(om)
     assert len(gn) == len(on) == 21
     for i in range(3):
