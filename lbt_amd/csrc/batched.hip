@@ -73,7 +73,7 @@ LBT_DEV void quantize_weights_block4(const lbt_wjob* __restrict__ jobs, int bx, 
   const int64_t inner = (int64_t)j.KW * j.Cin * j.Cout;
   const int csi = (j.Cin + 15) / 16, cso = (j.Cout + 15) / 16;
   int ov1 = 0, ov2 = 0, cs[4] = {0, 0, 0, 0};
-  constexpr int kRows = 4;  // k rows per thread per pass: every load in flight before the Philox calls
+  constexpr int kRows = 2;  // k rows per thread per pass: every load in flight before the Philox calls (2: the prologue stays at <= 64 VGPRs, 8 waves per SIMD -- one round for its ~1 300 workgroups)
   for (int k0 = 0; k0 < K; k0 += kRows * kThreads) {
     float4 wv[kRows];
 #pragma unroll
@@ -504,7 +504,7 @@ struct Prologue {
   const int32_t* snap_src; int32_t* snap_dst; int nsnap;
 };
 
-__global__ __launch_bounds__(kThreads) void step_prologue_kernel(Prologue a) {
+__global__ __launch_bounds__(kThreads, 8) void step_prologue_kernel(Prologue a) {
   int b = blockIdx.x;
   LBT_TS(0);
   const int nbw = (a.max_cout + 3) / 4;  // weight blocks per job (4 output channels each)

@@ -23,6 +23,15 @@ namespace lbt {
 namespace {
 
 constexpr int kT = kHeadT;
+// Phase stamps (scratch -DLBT_TRACE builds); -DLBT_HEADSTUDY: 1 = loads issued, 2 = end chain done, 3 = pool,
+// 4 = logits, 5 = softmax + counters
+#ifdef LBT_HEADSTUDY
+#define LBT_HSS(i) LBT_TS(i)
+#define LBT_HTS(i) do { if ((i) == 1) LBT_TS(3); else if ((i) == 2) LBT_TS(4); else if ((i) == 3) LBT_TS(5); } while (0)
+#else
+#define LBT_HSS(i) do { } while (0)
+#define LBT_HTS(i) LBT_TS(i)
+#endif
 constexpr int kXChunk = 16384;   // bytes of x staged per pass (pixels x C floats)
 constexpr int kMaxW = 256 * 64;  // Dense_q weight codes C x K
 
@@ -332,8 +341,13 @@ LBT_DEV void chain_eval(const lbt_chain_fwd& a, int own, const ChainIn& in, floa
 // dgrad of its sample (the same operations on the same operands: identical values, a few KB from
 // L2), and runs pass A / the un-pool over its 1/S of the sample's pixels; workgroup s == 0 alone
 // writes the sample's outputs and counts its Dense_q quantisers.
-template <bool CHAIN>
+// FAST (CHAIN, Dense_q weights <= 1 KB, noise tables for both Dense_q quantisers -- the ResNet-20 step): one
+// weight word per thread instead of the kMaxW-sized clamped sweep, the tables read without the branch-free
+// Philox twin, and the loads the dense layer needs issued AFTER the end chain's operands (vmcnt waits are
+// in issue order: the chain no longer waits for the weights)
+template <bool CHAIN, bool FAST = false>
 __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa, lbt_chain_fwd ch, int S) {
+  static_assert(!FAST || CHAIN, "the fast head is the chain head");
   __shared__ __attribute__((aligned(16))) float s_x[kXChunk / 4];
   __shared__ __attribute__((aligned(16))) int8_t s_w[kMaxW];
   __shared__ int s_pq[256], s_gq[64], s_part[16][16];
@@ -353,15 +367,26 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
 
   // ---- every global load, issued together: Dense_q weight codes, label, noise, first x chunk
   const int nw = C * K / 4;
-  uint32_t wv[kMaxW / 4 / kT];
+  constexpr int kWv = FAST ? 1 : kMaxW / 4 / kT;
+  uint32_t wv[kWv];
+  int y;
+  float ux, ug;
+  auto load_dense = [&]() {
 #pragma unroll
-  for (int j = 0; j < kMaxW / 4 / kT; ++j) {
-    const int i = t + j * kT;
-    wv[j] = reinterpret_cast<const uint32_t*>(h.wq)[i < nw ? i : 0];
-  }
-  const int y = h.labels[n];
-  const float ux = head_noise(h.qx, sx, t, C);
-  const float ug = head_noise(h.qg, sg, lane, K);
+    for (int j = 0; j < kWv; ++j) {
+      const int i = t + j * kT;
+      wv[j] = reinterpret_cast<const uint32_t*>(h.wq)[i < nw ? i : 0];
+    }
+    y = h.labels[n];
+    if constexpr (FAST) {  // both quantisers stochastic with tables (host check)
+      ux = h.qx.noise[t < C ? t : C - 1];
+      ug = h.qg.noise[lane < K ? lane : K - 1];
+    } else {
+      ux = head_noise(h.qx, sx, t, C);
+      ug = head_noise(h.qg, sg, lane, K);
+    }
+  };
+  if constexpr (!FAST) load_dense();
   const int P = (kXChunk / 4) / C;  // pixels per chunk
   constexpr int kV = kXChunk / 16 / kT;
   float4 v[kV];
@@ -384,6 +409,8 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   HeadPaPre pre;
   const bool pre_ok = h.pa && head_pa_prefetchable(HW / S, C);  // uniform
   if (pre_ok) head_pa_prefetch(pa, n, HW, C, q0, q1, pre, !CHAIN);
+  if constexpr (FAST) load_dense();
+  LBT_HSS(1);  // every load of the top issued
   int ovr1 = 0, ovr2 = 0;
   if constexpr (CHAIN) {
     // the chain's block output into s_x (pooling) and, for this workgroup's quads, pass A's operands
@@ -392,6 +419,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     __shared__ long long s_t[2 * 256];
     ChainOut co;
     chain_eval(ch, own, cin, s_P, s_t, co, ovr1, ovr2, hs, hstat);
+    LBT_HSS(2);  // moments + the end chain done
     const int Q = HW * C / 4;
 #pragma unroll
     for (int j = 0; j < kChainSlots; ++j) reinterpret_cast<float4*>(s_x)[chain_quad(j, own, q0, Q, t)] = co.y[j];
@@ -414,7 +442,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     }
     if (p0 == 0) {
 #pragma unroll
-      for (int j = 0; j < kMaxW / 4 / kT; ++j) reinterpret_cast<uint32_t*>(s_w)[t + j * kT] = wv[j];
+      for (int j = 0; j < kWv; ++j) reinterpret_cast<uint32_t*>(s_w)[t + j * kT] = wv[j];
     }
     __syncthreads();
     const int np = HW - p0 < P ? HW - p0 : P;
@@ -435,7 +463,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     if constexpr (!CHAIN) LBT_HEAD_LOAD_CHUNK(p0);
   }
 #undef LBT_HEAD_LOAD_CHUNK
-  LBT_TS(1);
+  LBT_HTS(1);
   if (t < C) {
     const float pooled = acc * (1.0f / (float)HW);
     if (h.pooled && lead) h.pooled[(int64_t)n * C + t] = pooled;
@@ -469,7 +497,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     __syncthreads();
   }
 
-  LBT_TS(2);
+  LBT_HTS(2);
   // ---- softmax cross-entropy in wave 0, lane k = class (softmax_xent_kernel's arithmetic:
   // max, then s = sum of expf(z - m) in class order, p = expf(z - m) / s)
   if (wave == 0) {
@@ -509,7 +537,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
   }
   if constexpr (CHAIN) counts_publish(4, 5, ch.b1.qr, sh_cnt);
 
-  LBT_TS(3);
+  LBT_HTS(3);
   // ---- the sample's column of the transposed records (head.h): pqT[c][n], gqT[k][n]
   if (lead) {
     uint8_t* scr = reinterpret_cast<uint8_t*>(h.scratch);
@@ -530,10 +558,10 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
     s_dp[t] = (float)a * ldexpf(1.0f, -(frac_exp(h.qg) + frac_exp(h.qw)));
   }
   __syncthreads();
-  LBT_TS(4);
+  LBT_HTS(4);
   if (h.pa) {  // uniform (the descriptor itself travels by value in pa)
     head_pass_a(pa, n, HW, C, q0, q1, s_dp, sh_cnt, pre, pre_ok);
-    LBT_TS(5);
+    LBT_HTS(5);
     return;
   }
   {
@@ -544,7 +572,7 @@ __global__ __launch_bounds__(kT) void head_kernel(lbt_head h, lbt_chain_bwd_a pa
       gx[i] = make_float4(s_dp[c] * inv, s_dp[c + 1] * inv, s_dp[c + 2] * inv, s_dp[c + 3] * inv);
     }
   }
-  LBT_TS(5);
+  LBT_HTS(5);
 }
 
 }  // namespace
@@ -595,7 +623,11 @@ extern "C" int lbt_head_fwd_bwd(const lbt_head* h, void* stream) {
   }();
   int S = smax;
   while (S > 1 && (h->HW % S || (int64_t)h->N * S > 0x7fffffff || (h->chain && kChainSlots % S))) --S;
-  if (h->chain)
+  const bool fast = h->chain && h->C * h->K <= 4 * kT && h->qx.noise && h->qg.noise && h->qx.bits > 0 && h->qg.bits > 0 &&
+                    h->qx.stochastic && h->qg.stochastic;
+  if (fast)
+    hipLaunchKernelGGL((head_kernel<true, true>), dim3((unsigned)(h->N * S)), dim3(kT), 0, (hipStream_t)stream, *h, pa, ch, S);
+  else if (h->chain)
     hipLaunchKernelGGL(head_kernel<true>, dim3((unsigned)(h->N * S)), dim3(kT), 0, (hipStream_t)stream, *h, pa, ch, S);
   else
     hipLaunchKernelGGL(head_kernel<false>, dim3((unsigned)(h->N * S)), dim3(kT), 0, (hipStream_t)stream, *h, pa, ch, S);
