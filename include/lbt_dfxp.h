@@ -196,9 +196,14 @@ int lbt_conv_dgrad_igemm_ws(const void* gq, int32_t g_i16, const int8_t* wd, int
  * Defaults: {1, 200, 2, 128}, or the LBT_IGEMM_BIG / _MIN / _S / _BN256 environment at first use.
  * halo: 3x3 / stride-1 / pad-1 GEMMs (fwd, unit-stride dgrad, W <= 63) stage one A window per
  * 64-channel block for all 9 taps; bit 0: int8 codes, bit 1: 16-bit codes (default 1, LBT_IGEMM_HALO).
- * fwdq_perm: lbt_conv_fwd_igemm_q on the 256-row kernel tiles rows 16 pixels x 16 samples and runs
- * its quantiser from an LDS-staged tile, one noise draw per position per 8 samples (default 1,
- * LBT_FWDQ_PERM).
+ * fwdq_perm: lbt_conv_fwd_igemm_q (and lbt_conv_dgrad_igemm_bna) on the 256-row kernels tile rows 16
+ * pixels x 16 samples. 1: the quantiser / pass A runs from an LDS-staged tile, one noise draw per
+ * position per 8 samples; 2 (default, LBT_FWDQ_PERM): the same, except the one-k-block forward GEMMs
+ * (1x1, K = 64), which take a persistent kernel (one workgroup per CU, an LDS-DMA ring across its row
+ * tiles, the quantiser on the accumulators, the tile's noise table DMA'd with its operands; table noise
+ * or nearest rounding, 256 % (Cout / column tile) == 0); > 2: the persistent forward and dgrad + pass A
+ * kernels wherever they apply, on that many workgroups (tests; slower on the longer-K shapes);
+ * 0: row-major tiles. stages 3 / 4 set the persistent ring's depth (2: LBT_FWDQ_S, default 4).
  * launches (get only; set ignores it): 256-row GEMM launches issued by this process so far.      */
 typedef struct lbt_igemm_tuning {
   int32_t big, min_tiles, stages, max_bn, halo, fwdq_perm;

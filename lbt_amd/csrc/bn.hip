@@ -37,6 +37,17 @@ LBT_DEV void f4(const float4& c, float v[4]) { v[0] = c.x; v[1] = c.y; v[2] = c.
 // arithmetic (stores may alias the inputs as far as the compiler knows, so it would not hoist
 // them itself) -- one HBM round trip per batch instead of one per row.
 constexpr int kRB = 4;
+// The forward chains' batch: the 3-byte-per-element chains (int8 codes in, two int8 code sets out) keep
+// 16 rows of 4-byte loads in flight per thread -- at 4 a CU held ~12 KiB of loads in flight and the
+// ResNet-50 c1 / c2 chains ran at ~1.1 TB/s. The ones with an fp32 operand (20 bytes a row) stay at 4: 8
+// rows cost 50+ VGPRs, i.e. half the waves, for the same bytes in flight per SIMD.
+#ifndef LBT_FWD_RB
+#define LBT_FWD_RB 4
+#endif
+template <int F>
+constexpr int fwd_rb() {
+  return ((F & kRt) || (F & kFRes) || !(F & kFQ)) ? 4 : LBT_FWD_RB;
+}
 
 LBT_DEV void load4_f32(const float* p, int64_t i, float v[4]) {
   const float4 c = *reinterpret_cast<const float4*>(p + i);
@@ -88,6 +99,7 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
   extern __shared__ float shf[];  // per branch: mu, sigma, gq, bq [C each]; then long long tmp[2C]
   __shared__ int sh_cnt[8 * kThreads / 64];
   constexpr int ST = (F & kRt) ? -1 : ((F & kFStoch) ? 1 : 0);
+  constexpr int RB = fwd_rb<F>();
   LBT_TS(0);
   const int C = a.C;
   long long* tmp = reinterpret_cast<long long*>(shf + 8 * C);
@@ -102,19 +114,23 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
   const bool res = LBT_FL(kFRes, a.res != nullptr);
 
   // ---- the first rows and the noise go out before the moment prologue (their latency overlaps it)
-  int qv[NB][kRB];
-  float4 xv[NB][kRB], rv[kRB];
+  int qv[NB][RB];
+  float4 xv[NB][RB], rv[RB];
+  // addresses: a uniform 64-bit row-batch base + a 32-bit lane offset (j * inner + 4 g < 2^31, checked on
+  // the host) -- per-row 64-bit addresses of every operand held ~7 VGPRs a row
+  const uint32_t inner32 = (uint32_t)a.inner, lo32 = (uint32_t)(gl << 2);
   auto load_batch = [&](int64_t rb) {
+    const int64_t eb = rb * a.inner;
 #pragma unroll
-    for (int j = 0; j < kRB; ++j) {
-      const int64_t e = (rb + j < rend ? rb + j : r0) * a.inner + (gl << 2);  // clamped: never branch
+    for (int j = 0; j < RB; ++j) {
+      const uint32_t oj = (uint32_t)(rb + j < rend ? j : 0) * inner32 + lo32;  // clamped: never branch
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         const lbt_chain_branch& Bb = b == 0 ? fbranch<0>(a) : fbranch<NB - 1>(a);
-        if (q_in[b]) qv[b][j] = ld_i8x4(Bb.nrm.q, e);
-        else xv[b][j] = ld_f32x4(Bb.xin, e);
+        if (q_in[b]) qv[b][j] = ld_i8x4(Bb.nrm.q + eb, oj);
+        else xv[b][j] = ld_f32x4(Bb.xin + eb, oj);
       }
-      if (res) rv[j] = ld_f32x4(a.res, e);
+      if (res) rv[j] = ld_f32x4(a.res + eb, oj);
     }
   };
   load_batch(r0);
@@ -196,13 +212,13 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
   const bool relu = LBT_FL(kFRelu, a.relu != 0), ystore = LBT_FL(kFY, a.y != nullptr);
   const bool u8 = LBT_FL(kFU8, a.o1_kind == LBT_OUT_U8OFF && (!o2 || a.o2_kind == LBT_OUT_U8OFF));
 
-  for (int64_t rb = r0; rb < rend; rb += kRB) {
+  for (int64_t rb = r0; rb < rend; rb += RB) {
     if (rb != r0) load_batch(rb);
     if (live) {
 #pragma unroll
-      for (int j = 0; j < kRB; ++j) {
+      for (int j = 0; j < RB; ++j) {
         if (rb + j >= rend) break;
-        const int64_t e = (rb + j) * a.inner + (g << 2);
+        const int64_t e = rb * a.inner + (int64_t)((uint32_t)j * inner32 + lo32);
         pf2 v2[2] = {pk(0.f, 0.f), pk(0.f, 0.f)};
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
@@ -269,6 +285,8 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
           if (u8) store4_code(a.o2, LBT_OUT_U8OFF, e, c, 0.f);
           else store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
         }
+        // one row at a time: interleaving the batch's rows (the scheduler's default) doubles the VGPRs
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -739,6 +757,7 @@ constexpr int kFwdBlk = kFQ | kFRout | kFRelu | kFStoch;  // every fused-plan fo
 
 extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   if (!shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;
+  if (a->inner * (LBT_FWD_RB + 1) >= ((int64_t)1 << 31)) return LBT_EINVAL;  // 32-bit lane offsets of a row batch
   dim3 grid;
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;

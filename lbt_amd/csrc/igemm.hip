@@ -490,6 +490,27 @@ LBT_DEV void vm_wait() {
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
+// A 16-byte store that is ALWAYS issued (one vector-memory op on the counter whatever `ok` is): a raw buffer
+// store at byte offset off of base (< 2^31), or at an out-of-range offset -- dropped by the buffer range
+// check -- when !ok. The persistent kernels count their epilogue stores into the ring's vmcnt waits.
+LBT_DEV void st16_always(void* base, uint32_t off, bool ok, uint4 v) {
+  typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  const v4u_ x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, rs, ok ? (int)off : (int)0x80000000u, 0, 0);
+}
+// The ring wait of a persistent kernel at k-step s: DMA group s has landed when at most the younger ops are
+// outstanding -- the S - 2 later groups (CNT each) and the NST stores of each epilogue run in steps
+// s - S + 1 .. s - 1 (ne of them; vector-memory ops complete in issue order).
+template <int S, int CNT, int NST>
+LBT_DEV void ring_wait(int ne) {
+  static_assert(S >= 3 && S <= 4, "ring depth");
+  if (ne <= 0) vm_wait<(S - 2) * CNT>();
+  else if (ne == 1) vm_wait<(S - 2) * CNT + NST>();
+  else if (S == 3 || ne == 2) vm_wait<(S - 2) * CNT + 2 * NST>();
+  else vm_wait<(S - 2) * CNT + (S == 4 ? 3 : 2) * NST>();
+}
+
 // Segment swizzles of the LDS images, conflict-free for ds_read_b128's lane groups
 // ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32): a fragment read by lanes (r = lane & 15, q = lane >> 4)
 // of rows base + r (base % 16 == 0) hits 16 distinct 4-bank quads in every group.
@@ -1242,6 +1263,682 @@ __global__ __launch_bounds__(kBT, LBT_BIG_OCC(A16, BN, S, HALO, BNA)) void igemm
   }
 }
 
+// ------------------------------------------------------------ persistent quantising forward
+// igemm_fwdq_kernel: lbt_conv_fwd_igemm_q on sample-blocked 256-row tiles (16 pixels x 16 samples, as
+// quantq_epilogue) with a stochastic qout that reads a noise table (or a nearest-rounding one), for the
+// short-K GEMMs where igemm_big_kernel's one-tile workgroups spend their life in latency (ResNet-50
+// l1_c3, K = 64: one k-block, then a 64 KiB LDS staging pass; profiles/r05 pmc: waves waiting 44 %).
+//  * one workgroup per CU, each owning ONE column tile and a strided set of row tiles; an S-stage
+//    LDS-DMA ring runs across tile boundaries, so the next tiles' operands are in flight during a
+//    tile's epilogue (every wave issues exactly GA + 2 DMA instructions per k-step -- idle slots write
+//    a dummy KiB -- so the counted vmcnt waits are constants);
+//  * the epilogue quantises straight from the accumulators: the MFMA runs with the operands swapped
+//    (weights as the A operand), and the weight image's columns are loaded into LDS permuted (LDS row
+//    16 j + 4 g + e of a 64-column slice <- channel 16 g + 4 j + e), so lane (r, q) ends with 16
+//    CONSECUTIVE channels (16 q .. 16 q + 15 of its wave's slice) of one row: one 16-byte store per
+//    row, no LDS staging of the tile;
+//  * the tile's noise (16 pixels x BN channels of the table) rides the ring with the operands of the
+//    tile's last k-block; lanes of one pixel read it as LDS broadcasts;
+//  * channel sums (sum q, sum q^2) stay in registers across every tile of the workgroup (its column
+//    tile is fixed) and leave once: 16-lane shuffles, the waves in LDS, one int64 atomic per (column,
+//    sum); overflow counters are wave totals (quant4_w), one atomic each at the end.
+// Rows outside the image or batch hold the fill code, whose dequantised value is exactly 0: code 0, no
+// overflow, nothing added to the sums, and their stores are skipped -- quantq_epilogue's results bit for bit.
+template <int BN, int S, bool ST>
+__global__ __launch_bounds__(kBT, 1) void igemm_fwdq_kernel(IgArgs p, int nrg, int rtiles) {
+  constexpr int BM = 256, WN = BN / 64, WM = 8 / WN, TR = BM / WM, MI = TR / 16, NJ = 4;
+  constexpr int ABYTES = BM * 64, BBYTES = BN * 64, NBYTES = 16 * BN * 4;
+  constexpr int STAGE = ABYTES + BBYTES + NBYTES;
+  constexpr int GA = ABYTES / 1024 / 8;  // A instructions per wave per k-block (2)
+  constexpr int NIB = BBYTES / 1024, NIN = NBYTES / 1024;  // B / noise instructions per k-block (<= 8)
+  constexpr int CNT = GA + 2;
+  constexpr int PARTS = kBT / BN;
+  static_assert(NIB <= 8 && NIN <= 8 && (BN == 64 || BN == 128), "geometry");
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  int8_t* dummy = lds + S * STAGE;                   // 1 KiB sink of the idle DMA slots
+  int* wsl = reinterpret_cast<int*>(dummy + 1024);   // [BN] sum_k W per column (offset codes)
+  int* wpart = wsl + BN;                             // [PARTS][BN]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int r = lane & 15, q = lane >> 4;
+  const int ntn = p.ncol / BN;
+  const uint32_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const uint32_t L = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int cn = (int)(L % (uint32_t)ntn), rg = (int)(L / (uint32_t)ntn);
+  const int n0 = cn * BN;
+  const int T = rg < rtiles ? (rtiles - 1 - rg) / nrg + 1 : 0;
+  if (T == 0) return;  // uniform over the workgroup, before any barrier
+  const lbt_conv_desc& d = p.d;
+  const int C = p.ncol, N = d.N, hw = p.hw, OW = p.cw, npb = p.npb;
+  const int cblocks = p.cred / kBK, nk = p.nkh * p.nkw * cblocks;
+  const int8_t* fill = p.a_u8off ? reinterpret_cast<const int8_t*>(kFill80) : reinterpret_cast<const int8_t*>(zi());
+  const int u8 = p.a_u8off ? 128 : 0;
+
+  // ---- sum_k W of this workgroup's columns (offset codes): from the caller's colsum, else from the image
+  int ws[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) ws[k] = 0;
+  if (u8) {
+    {
+      const int ch = t % BN, part = t / BN;
+      int s = 0;
+      if (p.colsum) {
+        if (part == 0) s = p.colsum[n0 + ch];
+      } else {
+        const int8_t* col = p.b + (int64_t)(n0 + ch) * p.ks * 16;
+        for (int c = part; c < nk * 4; c += PARTS) {
+          const int4 v = *reinterpret_cast<const int4*>(col + c * 16);
+          s = __builtin_amdgcn_sdot4(v.x, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(v.y, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(v.z, 0x01010101, s, false);
+          s = __builtin_amdgcn_sdot4(v.w, 0x01010101, s, false);
+        }
+      }
+      wpart[part * BN + ch] = s;
+    }
+    __syncthreads();
+    if (t < BN) {
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < PARTS; ++k) s += wpart[k * BN + t];
+      wsl[t] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ws[k] = wsl[wn * 64 + 16 * q + k];
+  }
+
+  // ---- DMA geometry. A: instruction g of a wave covers tile rows (wave + 8 g) * 16 .. + 15, 4 lanes a row
+  int aseg[GA];
+#pragma unroll
+  for (int g = 0; g < GA; ++g) {
+    const int row = (wave + 8 * g) * 16 + lane / 4;
+    aseg[g] = (lane % 4) ^ swz64(row);
+  }
+  // B: LDS row cl (16 rows per instruction) <- weight column n0 + perm(cl)
+  const bool bact = wave < NIB;
+  int bcol, bseg;
+  {
+    const int cl = wave * 16 + lane / 4;
+    const int pc = (cl & ~63) | (((cl & 15) >> 2) << 4) | (((cl >> 4) & 3) << 2) | (cl & 3);
+    bcol = n0 + (bact ? pc : 0);
+    bseg = (lane % 4) ^ swz64(cl);
+  }
+  // noise: instruction w covers pixels (1024 / (4 BN)) w .. of the tile, lane-linear [pixel][BN] floats
+  constexpr int NPX = 1024 / (4 * BN), NSEG = BN / 4;  // pixels per instruction, 16-byte segments per pixel
+  const bool nact = ST && wave < NIN;
+  const int npl = wave * NPX + lane / NSEG, nseg = lane % NSEG;
+
+  // issue side: tile it, k-block ikb, and its rows
+  int it = 0, ikb = 0;
+  int an[GA], ay[GA], ax[GA];
+  bool arow[GA];
+  int64_t noff = 0;
+  auto set_rows = [&](int k) {
+    const uint32_t rt = (uint32_t)(rg + k * nrg);
+    const int sb = (int)(rt / (uint32_t)npb), pb = (int)(rt % (uint32_t)npb);
+#pragma unroll
+    for (int g = 0; g < GA; ++g) {
+      const int row = (wave + 8 * g) * 16 + lane / 4;
+      const int sm = sb * 16 + (row & 15), px = pb * 16 + (row >> 4);
+      arow[g] = sm < N && px < hw;
+      const uint32_t pu = (uint32_t)(arow[g] ? px : 0);
+      ax[g] = (int)(pu % (uint32_t)OW);
+      ay[g] = (int)(pu / (uint32_t)OW);
+      an[g] = arow[g] ? sm : 0;
+    }
+    const int px = pb * 16 + npl;
+    noff = (int64_t)(px < hw ? px : 0) * C + n0 + 4 * nseg;
+  };
+  set_rows(0);
+  auto issue = [&](int st) {
+    int8_t* sb = lds + st * STAGE;
+    if (it < T) {
+      const int kb = ikb;
+      const int tap = kb / cblocks, cb = kb - tap * cblocks;
+      const int kh = tap / p.nkw, kw = tap - kh * p.nkw;
+      const int kbw = (kh * d.KW + kw) * cblocks + cb;
+#pragma unroll
+      for (int g = 0; g < GA; ++g) {
+        const int sy = ay[g] * d.SH + kh - d.PT, sx = ax[g] * d.SW + kw - d.PL;
+        const bool ok = (unsigned)sy < (unsigned)d.H && (unsigned)sx < (unsigned)d.W && arow[g];
+        const int8_t* src = fill;
+        if (ok) {
+          const uint32_t pix = (uint32_t)((an[g] * d.H + sy) * d.W + sx);
+          src = reinterpret_cast<const int8_t*>(p.a) + (uint64_t)(pix * (uint32_t)p.cred + (uint32_t)(cb * kBK)) +
+                aseg[g] * 16;
+        }
+        __builtin_amdgcn_global_load_lds(src, (lds_vptr)(sb + (wave + 8 * g) * 1024), 16, 0, 0);
+      }
+      {
+        const int8_t* src = bact ? p.b + ((uint32_t)(bcol * p.ks + kbw * 4 + bseg) << 4) : fill;
+        __builtin_amdgcn_global_load_lds(src, (lds_vptr)(bact ? sb + ABYTES + wave * 1024 : dummy), 16, 0, 0);
+      }
+      {
+        const bool nl = nact && kb == nk - 1;
+        const int8_t* src = nl ? reinterpret_cast<const int8_t*>(p.qout.noise + noff) : fill;
+        __builtin_amdgcn_global_load_lds(src, (lds_vptr)(nl ? sb + ABYTES + BBYTES + wave * 1024 : dummy), 16, 0, 0);
+      }
+      if (++ikb == nk) {
+        ikb = 0;
+        if (++it < T) set_rows(it);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < CNT; ++g) __builtin_amdgcn_global_load_lds(fill, (lds_vptr)dummy, 16, 0, 0);
+    }
+  };
+
+  const QState qs = qstate(p.qout);
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
+  v4i acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  int s1[16], s2[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { s1[k] = 0; s2[k] = 0; }
+  int ov1 = 0, ov2 = 0;
+
+  auto epilogue = [&](int k, const int8_t* sbase) {
+    const uint32_t rt = (uint32_t)(rg + k * nrg);
+    const int sb = (int)(rt / (uint32_t)npb), pb = (int)(rt % (uint32_t)npb);
+    const int sample = sb * 16 + r;
+    const float* nimg = reinterpret_cast<const float*>(sbase + ABYTES + BBYTES);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int pt = wm * MI + i, px = pb * 16 + pt;
+      const bool ok = sample < N && px < hw;
+      uint32_t w4[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float4 xv = make_float4((float)(acc[i][j][0] + u8 * ws[4 * j + 0]) * scale,
+                                      (float)(acc[i][j][1] + u8 * ws[4 * j + 1]) * scale,
+                                      (float)(acc[i][j][2] + u8 * ws[4 * j + 2]) * scale,
+                                      (float)(acc[i][j][3] + u8 * ws[4 * j + 3]) * scale);
+        float4 u4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (ST) u4 = *reinterpret_cast<const float4*>(nimg + pt * BN + wn * 64 + 16 * q + 4 * j);
+        int c[4];
+        quant4_w<ST>(qs, xv, u4, c, ov1, ov2);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[4 * j + e] += c[e];
+          s2[4 * j + e] += c[e] * c[e];
+        }
+        w4[j] = (uint32_t)(c[0] & 0xff) | ((uint32_t)(c[1] & 0xff) << 8) | ((uint32_t)(c[2] & 0xff) << 16) |
+                ((uint32_t)c[3] << 24);
+        // the quad's overflow counts are added here (left to itself, the compiler sinks all 4 MI NJ x 8
+        // ballot masks to the end of the epilogue and spills them)
+        asm volatile("" : "+s"(ov1), "+s"(ov2));
+      }
+      st16_always(p.yq, (uint32_t)(((int64_t)sample * hw + px) * C + n0 + wn * 64 + 16 * q), ok,
+                  make_uint4(w4[0], w4[1], w4[2], w4[3]));
+    }
+  };
+
+  // ---- the ring: k-step s reads stage s % S; step s issues step s + S - 1 into the stage step s - 1 read
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(s);
+  const int nsteps = T * nk;
+  int ct = 0, ckb = 0;
+  uint32_t ehist = 0;  // bit k: an epilogue (MI stores) ran k + 1 steps ago
+  for (int s = 0; s < nsteps; ++s) {
+    ring_wait<S, CNT, MI>(__popc(ehist & ((1u << (S - 1)) - 1u)));
+    __builtin_amdgcn_s_barrier();
+    issue((s + S - 1) % S);
+    const int8_t* sbase = lds + (s % S) * STAGE;
+    ehist <<= 1;
+    v4i fa[MI], fb[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = wn * 64 + j * 16 + r;
+      fb[j] = *reinterpret_cast<const v4i*>(sbase + ABYTES + col * 64 + ((q ^ swz64(col)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * TR + i * 16 + r;
+      fa[i] = *reinterpret_cast<const v4i*>(sbase + row * 64 + ((q ^ swz64(row)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    if (++ckb == nk) {
+      ckb = 0;
+      epilogue(ct, sbase);
+      ehist |= 1u;
+      ++ct;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+    }
+  }
+  vm_wait<0>();  // the trailing dummy DMAs: nothing writes LDS past here
+
+  // ---- channel sums: the 16 rows of a lane group by shuffles, the WM waves of a column slice in LDS
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+      s1[k] += __shfl_xor(s1[k], m, 64);
+      s2[k] += __shfl_xor(s2[k], m, 64);
+    }
+  }
+  __syncthreads();  // every wave's last ring reads are done: the ring is reused as the exchange
+  int* red = reinterpret_cast<int*>(lds);  // [WM][BN][2]
+  if (r == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      red[((wm * BN) + wn * 64 + 16 * q + k) * 2 + 0] = s1[k];
+      red[((wm * BN) + wn * 64 + 16 * q + k) * 2 + 1] = s2[k];
+    }
+  }
+  __syncthreads();
+  const int shard = (int)(L % LBT_NSHARD);
+  if (t < 2 * BN) {
+    const int a = t / BN, cl = t % BN;
+    long long v = 0;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) v += red[(w * BN + cl) * 2 + a];
+    if (v) atomicAdd((unsigned long long*)&p.chsum[(int64_t)shard * 2 * C + a * C + n0 + cl], (unsigned long long)v);
+  }
+  if (lane == 0 && p.qout.counts) {
+    int32_t* ctr = p.qout.counts + ((int64_t)p.qout.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+    if (ov1) atomicAdd(ctr, ov1);
+    if (ov2) atomicAdd(ctr + 1, ov2);
+  }
+}
+
+template <int BN, int S, bool ST>
+void fwdq_go(const IgArgs& p, int nwg, int nrg, int rtiles, hipStream_t st) {
+  constexpr size_t shm = (size_t)S * (256 * 64 + BN * 64 + 16 * BN * 4) + 1024 + (size_t)4 * BN + (size_t)4 * kBT;
+  static bool attr_ = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_fwdq_kernel<BN, S, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    return true;
+  }();
+  (void)attr_;
+  hipLaunchKernelGGL((igemm_fwdq_kernel<BN, S, ST>), dim3((unsigned)nwg), dim3(kBT), shm, st, p, nrg, rtiles);
+}
+
+// The persistent quantising forward (tuning fwdq_perm >= 2) takes a sample-blocked fwdq GEMM when its
+// noise is a table (or rounding is to nearest), its column tiles divide the workgroup count (256: one per
+// CU; fwdq_perm > 2: that many, to put many tiles on each in tests), and the int32 lane sums stay exact
+// (<= 2047 tiles a workgroup). Ring stages: the tuning's 3 or 4, else LBT_FWDQ_S (default 4).
+template <int BN>
+bool launch_fwdq_persist(const IgArgs& p, int tstages, hipStream_t st) {
+  static const int dstages = getenv_int("LBT_FWDQ_S", 4);
+  const int stages = tstages >= 3 ? tstages : dstages;
+  const int wgs = p.perm > 2 ? p.perm : 256;
+  if (p.perm < 2 || !p.yq) return false;
+  // default (2): only the one-k-block GEMMs (1x1, K = 64: ResNet-50 stage 1's conv-3 / shortcut), where it
+  // measured faster (l1_c3 188 -> 147 us); the longer-K ones ran slower than the staged two-workgroup form
+  // (l1_c2 108 -> 117 us; the ResNet-50 step 34.65 vs 36.34 ms with every fwdq GEMM persistent,
+  // profiles/round5/persist_ab.txt). > 2: every sample-blocked fwdq GEMM (tests)
+  if (p.perm == 2 && p.nkh * p.nkw * (p.cred / kBK) != 1) return false;
+  const bool stoch = p.qout.stochastic != 0;
+  if (stoch && !p.qout.noise) return false;
+  const int ntn = p.ncol / BN;
+  if (p.ncol % BN || wgs % ntn) return false;
+  const int rtiles = (p.d.N + 15) / 16 * p.npb;
+  int nrg = wgs / ntn;
+  if (nrg > rtiles) nrg = rtiles;
+  if ((rtiles + nrg - 1) / nrg > 2047) return false;
+  const int nwg = nrg * ntn;
+#define LBT_FQ(S_)                                                      \
+  do {                                                                  \
+    if (stoch) fwdq_go<BN, S_, true>(p, nwg, nrg, rtiles, st);          \
+    else fwdq_go<BN, S_, false>(p, nwg, nrg, rtiles, st);               \
+  } while (0)
+  if (stages <= 3) LBT_FQ(3); else LBT_FQ(4);
+#undef LBT_FQ
+  return true;
+}
+
+// ------------------------------------------------------ persistent 16-bit dgrad + BN pass A (bn1 / bn2)
+// igemm_dgrada_kernel: lbt_conv_dgrad_igemm_bna (unit-stride 16-bit dgrad whose dx feeds ReLU_q +
+// Rescale_q + Normalization_q backward, mask from R) in igemm_fwdq_kernel's form, when both gradient
+// quantisers are stochastic with noise tables (the models' configuration): one workgroup per CU owning a
+// 64-column tile (dx channels) and a strided set of sample-blocked row tiles, an S-stage LDS-DMA ring
+// across tile boundaries carrying A (256 rows x 64 16-bit codes), B (64 weight columns, loaded PERMUTED
+// so a lane's accumulators are 16 consecutive channels of one row) and, with a tile's last k-block, both
+// quantisers' noise for its 16 pixels. The epilogue runs pass A straight from the accumulators
+// (passa_epilogue's arithmetic, element for element): the lane's R and qn codes are one 16-byte load
+// each, its G codes one 32-byte store; the four channel sums stay in registers across the workgroup's
+// tiles (its columns are fixed) and leave once. Rows outside the batch / image carry dx = 0 exactly
+// (a = 0 codes), so they quantise to 0 and add nothing; their loads read row 0 and their stores are skipped.
+template <int S>
+__global__ __launch_bounds__(kBT, 1) void igemm_dgrada_kernel(IgArgs p, int nrg, int rtiles) {
+  constexpr int BN = 64, BM = 256, WM = 8, TR = BM / WM, MI = TR / 16, NJ = 4;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 64, NBYTES = 2 * 16 * BN * 4;
+  constexpr int STAGE = ABYTES + BBYTES + NBYTES;
+  constexpr int GA = ABYTES / 1024 / 8;  // 4: A instructions per wave per k-block (8 rows each)
+  constexpr int CNT = GA + 2;            // + B (waves 0-3, else dummy) + noise (waves 0-3 qrg, 4-7 qng)
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  int8_t* dummy = lds + S * STAGE;
+  int* wsl = reinterpret_cast<int*>(dummy + 1024);            // [64] sum_k W per column
+  float* gbl = reinterpret_cast<float*>(wsl + BN);            // [2][64] gamma_q | beta_q of the columns
+  int* wpart = reinterpret_cast<int*>(gbl + 2 * BN);          // [8][64]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave;
+  const int r = lane & 15, q = lane >> 4;
+  const int ntn = p.ncol / BN;
+  const uint32_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const uint32_t L = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int cn = (int)(L % (uint32_t)ntn), rg = (int)(L / (uint32_t)ntn);
+  const int n0 = cn * BN;
+  const int T = rg < rtiles ? (rtiles - 1 - rg) / nrg + 1 : 0;
+  if (T == 0) return;
+  const lbt_conv_desc& d = p.d;
+  const lbt_dgrad_bna& bn = p.bna;
+  const int C = p.ncol, N = d.N, hw = p.ch * p.cw, OW = p.cw, npb = p.npb;
+  const int SH = d.Ho, SW = d.Wo;  // the gathered image (g) of a unit-stride dgrad
+  const int cblocks = p.cred / kBK, nk = p.nkh * p.nkw * cblocks;
+  const int8_t* fill = reinterpret_cast<const int8_t*>(zi());
+
+  // ---- per-column constants: sum_k W (16-bit codes: the + 128 sum W term), gamma_q, beta_q
+  {
+    const int ch = t % BN, part = t / BN;
+    int s = 0;
+    const int8_t* col = p.b + (int64_t)(n0 + ch) * p.ks * 16;
+    for (int c = part; c < nk * 4; c += 8) {
+      const int4 v = *reinterpret_cast<const int4*>(col + c * 16);
+      s = __builtin_amdgcn_sdot4(v.x, 0x01010101, s, false);
+      s = __builtin_amdgcn_sdot4(v.y, 0x01010101, s, false);
+      s = __builtin_amdgcn_sdot4(v.z, 0x01010101, s, false);
+      s = __builtin_amdgcn_sdot4(v.w, 0x01010101, s, false);
+    }
+    wpart[part * BN + ch] = s;
+    if (t < 2 * BN) gbl[t] = bn.gb[(t / BN) * C + n0 + t % BN];
+  }
+  __syncthreads();
+  if (t < BN) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += wpart[k * BN + t];
+    wsl[t] = s;
+  }
+  __syncthreads();
+
+  // ---- DMA geometry. A (16-bit codes, 128-byte rows): instruction g covers rows (wave + 8 g) * 8 .. + 7
+  int aseg[GA];
+#pragma unroll
+  for (int g = 0; g < GA; ++g) {
+    const int row = (wave + 8 * g) * 8 + lane / 8;
+    aseg[g] = (lane % 8) ^ swz128(row);
+  }
+  const bool bact = wave < 4;
+  int bcol, bseg;
+  {
+    const int cl = (wave & 3) * 16 + lane / 4;
+    const int pc = (((cl & 15) >> 2) << 4) | (((cl >> 4) & 3) << 2) | (cl & 3);
+    bcol = n0 + pc;
+    bseg = (lane % 4) ^ swz64(cl);
+  }
+  // noise: waves 0-3 qrg, 4-7 qng; instruction covers 4 pixels x 64 floats of its quantiser's tile image
+  const float* ntab = wave < 4 ? bn.qrg.noise : bn.qng.noise;
+  const int npl = (wave & 3) * 4 + lane / 16, nseg = lane % 16;
+
+  int it = 0, ikb = 0;
+  int an[GA], ay[GA], ax[GA];
+  bool arow[GA];
+  int64_t noff = 0;
+  auto set_rows = [&](int k) {
+    const uint32_t rt = (uint32_t)(rg + k * nrg);
+    const int sb = (int)(rt / (uint32_t)npb), pb = (int)(rt % (uint32_t)npb);
+#pragma unroll
+    for (int g = 0; g < GA; ++g) {
+      const int row = (wave + 8 * g) * 8 + lane / 8;
+      const int sm = sb * 16 + (row & 15), px = pb * 16 + (row >> 4);
+      arow[g] = sm < N && px < hw;
+      const uint32_t pu = (uint32_t)(arow[g] ? px : 0);
+      ax[g] = (int)(pu % (uint32_t)OW);
+      ay[g] = (int)(pu / (uint32_t)OW);
+      an[g] = arow[g] ? sm : 0;
+    }
+    const int px = pb * 16 + npl;
+    noff = (int64_t)(px < hw ? px : 0) * C + n0 + 4 * nseg;
+  };
+  set_rows(0);
+  auto issue = [&](int st) {
+    int8_t* sb = lds + st * STAGE;
+    if (it < T) {
+      const int kb = ikb;
+      const int tap = kb / cblocks, cb = kb - tap * cblocks;
+      const int th = tap / p.nkw, tw = tap - th * p.nkw;
+      const int kbw = (th * d.KW + tw) * cblocks + cb;  // unit stride: kh = th, kw = tw
+#pragma unroll
+      for (int g = 0; g < GA; ++g) {
+        const int sy = ay[g] + p.oy - th, sx = ax[g] + p.ox - tw;
+        const bool ok = (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW && arow[g];
+        const int8_t* src = fill;
+        if (ok) {
+          const uint32_t pix = (uint32_t)((an[g] * SH + sy) * SW + sx);
+          src = reinterpret_cast<const int8_t*>(p.a) + (uint64_t)(pix * (uint32_t)p.cred + (uint32_t)(cb * kBK)) * 2 +
+                aseg[g] * 16;
+        }
+        __builtin_amdgcn_global_load_lds(src, (lds_vptr)(sb + (wave + 8 * g) * 1024), 16, 0, 0);
+      }
+      {
+        const int8_t* src = bact ? p.b + ((uint32_t)(bcol * p.ks + kbw * 4 + bseg) << 4) : fill;
+        __builtin_amdgcn_global_load_lds(src, (lds_vptr)(bact ? sb + ABYTES + wave * 1024 : dummy), 16, 0, 0);
+      }
+      {
+        const bool nl = kb == nk - 1;
+        const int8_t* src = nl ? reinterpret_cast<const int8_t*>(ntab + noff) : fill;
+        __builtin_amdgcn_global_load_lds(src, (lds_vptr)(nl ? sb + ABYTES + BBYTES + wave * 1024 : dummy), 16, 0, 0);
+      }
+      if (++ikb == nk) {
+        ikb = 0;
+        if (++it < T) set_rows(it);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < CNT; ++g) __builtin_amdgcn_global_load_lds(fill, (lds_vptr)dummy, 16, 0, 0);
+    }
+  };
+
+  const QState srg = qstate(bn.qrg), sng = qstate(bn.qng);
+  const float sr = qstate(bn.qr).inv_m;
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qa) + frac_exp(p.qb)));
+  v4i acc[2][MI][NJ];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[a][i][j] = v4i{0, 0, 0, 0};
+  int sm[4][16];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm[a][k] = 0;
+  int ov0 = 0, ov1 = 0, ov2 = 0, ov3 = 0;
+
+  auto epilogue = [&](int k, const int8_t* sbase) {
+    const uint32_t rt = (uint32_t)(rg + k * nrg);
+    const int sb = (int)(rt / (uint32_t)npb), pb = (int)(rt % (uint32_t)npb);
+    const int sample = sb * 16 + r;
+    const float* n1 = reinterpret_cast<const float*>(sbase + ABYTES + BBYTES);
+    const float* n2 = n1 + 16 * BN;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int pt = wm * MI + i, px = pb * 16 + pt;
+      const bool ok = sample < N && px < hw;
+      const int64_t off = ok ? ((int64_t)sample * hw + px) * C + n0 + 16 * q : 0;
+      const int4 R16 = *reinterpret_cast<const int4*>(bn.R + off);
+      const int4 Q16 = *reinterpret_cast<const int4*>(bn.qn + off);
+      const int Rw[4] = {R16.x, R16.y, R16.z, R16.w}, Qw[4] = {Q16.x, Q16.y, Q16.z, Q16.w};
+      uint32_t gw[8];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int4 ws4 = *reinterpret_cast<const int4*>(wsl + 16 * q + 4 * j);
+        const float4 g4 = *reinterpret_cast<const float4*>(gbl + 16 * q + 4 * j);
+        const float4 b4 = *reinterpret_cast<const float4*>(gbl + BN + 16 * q + 4 * j);
+        const int wsv[4] = {ws4.x, ws4.y, ws4.z, ws4.w};
+        const float gam[4] = {g4.x, g4.y, g4.z, g4.w}, bet[4] = {b4.x, b4.y, b4.z, b4.w};
+        int R[4], Q[4];
+        float dv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          R[e] = (int)(int8_t)(Rw[j] >> (8 * e));
+          Q[e] = (int)(int8_t)(Qw[j] >> (8 * e));
+          const double hs = (double)acc[0][i][j][e] * 256.0;
+          const double ls = (double)(acc[1][i][j][e] + 128 * wsv[e]);
+          const float dx = (float)(hs + ls) * scale;
+          const float xr = (float)R[e] * sr;  // the ReLU mask recomputed from R (bn.hip chain_bwd_a)
+          const float m1 = xr * gam[e];
+          const float yv = m1 + bet[e];
+          dv[e] = yv > 0.f ? dx : 0.f;
+        }
+        const float4 u1 = *reinterpret_cast<const float4*>(n1 + pt * BN + 16 * q + 4 * j);
+        const float4 u2 = *reinterpret_cast<const float4*>(n2 + pt * BN + 16 * q + 4 * j);
+        int G2[4], G[4];
+        quant4_w<true>(srg, make_float4(dv[0], dv[1], dv[2], dv[3]), u1, G2, ov0, ov1);
+        const pf2 im = pk(srg.inv_m, srg.inv_m);
+        const pf2 gh0 = pcvt(G2[0], G2[1]) * im, gh1 = pcvt(G2[2], G2[3]) * im;
+        const pf2 dd0 = gh0 * pk(gam[0], gam[1]), dd1 = gh1 * pk(gam[2], gam[3]);
+        quant4_w<true>(sng, make_float4(dd0.x, dd0.y, dd1.x, dd1.y), u2, G, ov2, ov3);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sm[0][4 * j + e] += G2[e] * R[e];
+          sm[1][4 * j + e] += G2[e];
+          sm[2][4 * j + e] += G[e];
+          sm[3][4 * j + e] += G[e] * Q[e];
+        }
+        gw[2 * j] = (uint32_t)(G[0] & 0xffff) | ((uint32_t)G[1] << 16);
+        gw[2 * j + 1] = (uint32_t)(G[2] & 0xffff) | ((uint32_t)G[3] << 16);
+        asm volatile("" : "+s"(ov0), "+s"(ov1), "+s"(ov2), "+s"(ov3));  // (see igemm_fwdq_kernel)
+      }
+      st16_always(bn.gout, (uint32_t)(off * 2), ok, make_uint4(gw[0], gw[1], gw[2], gw[3]));
+      st16_always(bn.gout, (uint32_t)(off * 2 + 16), ok, make_uint4(gw[4], gw[5], gw[6], gw[7]));
+    }
+  };
+
+  // ---- the ring (igemm_fwdq_kernel's), 16-bit A fragments split into hi / lo' at the MFMA
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(s);
+  const int nsteps = T * nk;
+  int ct = 0, ckb = 0;
+  uint32_t ehist = 0;  // bit k: an epilogue (2 MI stores) ran k + 1 steps ago
+  for (int s = 0; s < nsteps; ++s) {
+    ring_wait<S, CNT, 2 * MI>(__popc(ehist & ((1u << (S - 1)) - 1u)));
+    __builtin_amdgcn_s_barrier();
+    issue((s + S - 1) % S);
+    const int8_t* sbase = lds + (s % S) * STAGE;
+    ehist <<= 1;
+    v4i fb[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = j * 16 + r;
+      fb[j] = *reinterpret_cast<const v4i*>(sbase + ABYTES + col * 64 + ((q ^ swz64(col)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * TR + i * 16 + r;
+      const int f = swz128(row);
+      const v4i c0 = *reinterpret_cast<const v4i*>(sbase + row * 128 + (((2 * q) ^ f) << 4));
+      const v4i c1 = *reinterpret_cast<const v4i*>(sbase + row * 128 + (((2 * q + 1) ^ f) << 4));
+      const uint32_t w[8] = {(uint32_t)c0[0], (uint32_t)c0[1], (uint32_t)c0[2], (uint32_t)c0[3],
+                             (uint32_t)c1[0], (uint32_t)c1[1], (uint32_t)c1[2], (uint32_t)c1[3]};
+      v4i hi, lo;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        hi[u] = (int)__builtin_amdgcn_perm(w[2 * u + 1], w[2 * u], 0x07050301u);
+        lo[u] = (int)(__builtin_amdgcn_perm(w[2 * u + 1], w[2 * u], 0x06040200u) ^ 0x80808080u);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        acc[0][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fb[j], hi, acc[0][i][j], 0, 0, 0);
+        acc[1][i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fb[j], lo, acc[1][i][j], 0, 0, 0);
+      }
+    }
+    if (++ckb == nk) {
+      ckb = 0;
+      epilogue(ct, sbase);
+      ehist |= 1u;
+      ++ct;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[a][i][j] = v4i{0, 0, 0, 0};
+    }
+  }
+  vm_wait<0>();
+
+  // ---- the four channel sums (a lane's int32 partials are exact for <= 255 tiles: 2 T products of
+  // <= 2^22), widened: the 16 rows of a lane group by shuffles, the 8 waves in LDS
+  __syncthreads();
+  long long* red = reinterpret_cast<long long*>(lds);  // [8 waves][4 sums][64 columns]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      long long v = sm[a][k];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
+      if (r == 0) red[(wm * 4 + a) * BN + 16 * q + k] = v;
+    }
+  __syncthreads();
+  const int shard = (int)(L % LBT_NSHARD);
+  if (t < 4 * BN) {
+    const int a = t / BN, cl = t % BN;
+    long long v = 0;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) v += red[(w * 4 + a) * BN + cl];
+    if (v) atomicAdd((unsigned long long*)&bn.sums[(int64_t)shard * 4 * C + a * C + n0 + cl], (unsigned long long)v);
+  }
+  if (lane == 0) {
+    if (bn.qrg.counts) {
+      int32_t* ct2 = bn.qrg.counts + ((int64_t)bn.qrg.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (ov0) atomicAdd(ct2, ov0);
+      if (ov1) atomicAdd(ct2 + 1, ov1);
+    }
+    if (bn.qng.counts) {
+      int32_t* ct2 = bn.qng.counts + ((int64_t)bn.qng.slot * LBT_NSHARD + shard) * LBT_CSTRIDE;
+      if (ov2) atomicAdd(ct2, ov2);
+      if (ov3) atomicAdd(ct2 + 1, ov3);
+    }
+  }
+}
+
+template <int S>
+void dgrada_go(const IgArgs& p, int nwg, int nrg, int rtiles, hipStream_t st) {
+  constexpr size_t shm = (size_t)S * (256 * 128 + 64 * 64 + 2 * 16 * 64 * 4) + 1024 + 64 * 4 + 128 * 4 + 512 * 4;
+  static bool attr_ = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_dgrada_kernel<S>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    return true;
+  }();
+  (void)attr_;
+  hipLaunchKernelGGL((igemm_dgrada_kernel<S>), dim3((unsigned)nwg), dim3(kBT), shm, st, p, nrg, rtiles);
+}
+
+// The persistent dgrad + pass A (tuning fwdq_perm > 2, on that many workgroups): both gradient quantisers
+// stochastic with noise tables, 64-column tiles dividing the workgroups, <= 255 tiles a workgroup; a
+// 3-stage ring (132 KiB).
+bool launch_dgrada_persist(const IgArgs& p, hipStream_t st) {
+  // opt-in (fwdq_perm > 2, on that many workgroups): bit-exact, but slower than the staged form on every
+  // ResNet-50 shape measured (l1_c2 206 -> 247 us, l1_c3 175 -> 199, l3_c2 131 -> 187;
+  // profiles/round5/persist_ab.txt)
+  const int wgs = p.perm;
+  if (p.perm <= 2 || p.has_bna != 1) return false;
+  const lbt_dgrad_bna& b = p.bna;
+  if (!b.qrg.stochastic || !b.qng.stochastic || !b.qrg.noise || !b.qng.noise) return false;
+  const int ntn = p.ncol / 64;
+  if (p.ncol % 64 || wgs % ntn || p.cred % kBK) return false;
+  const int rtiles = (p.d.N + 15) / 16 * p.npb;
+  int nrg = wgs / ntn;
+  if (nrg > rtiles) nrg = rtiles;
+  if ((rtiles + nrg - 1) / nrg > 255) return false;  // int32 lane sums exact (see the kernel)
+  dgrada_go<3>(p, nrg * ntn, nrg, rtiles, st);
+  return true;
+}
+
 // one igemm_big_kernel instantiation: dynamic LDS = the S-stage ring, or (HALO) two A windows of 384
 // rows + a 3-stage B ring
 template <int MODE, bool A16, bool ADD, int BN, int S, int BNA, bool HALO>
@@ -1294,7 +1991,7 @@ lbt_igemm_tuning& big_tuning() {
     v.stages = getenv_int("LBT_IGEMM_BIG_S", 2);
     v.max_bn = getenv_int("LBT_IGEMM_BIG_BN256", 0) ? 256 : 128;
     v.halo = getenv_int("LBT_IGEMM_HALO", 1);  // bit 0: int8 codes (fwd), bit 1: 16-bit codes (dgrad16)
-    v.fwdq_perm = getenv_int("LBT_FWDQ_PERM", 1);
+    v.fwdq_perm = getenv_int("LBT_FWDQ_PERM", 2);
     v.launches = 0;
     return v;
   }();
@@ -1332,6 +2029,19 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
                     // where it measured faster (profiles/r04p): one column tile (the window is not
                     // re-staged per column tile), or a chip the 128-column tiles would under-fill
                     (p.ncol == 64 || mt * (p.ncol / bn) < 256);
+  if constexpr (MODE == MODE_DGRAD && A16) {
+    if (p.has_bna == 1 && p.perm >= 2 && launch_dgrada_persist(p, st)) {
+      ++big_tuning().launches;
+      return true;
+    }
+  }
+  if constexpr (MODE == MODE_FWD && !A16) {
+    if (p.yq && p.perm >= 2 && bn <= 128 &&
+        (bn == 128 ? launch_fwdq_persist<128>(p, S, st) : launch_fwdq_persist<64>(p, S, st))) {
+      ++big_tuning().launches;
+      return true;
+    }
+  }
   if (halo) {  // 64-column tiles: int8 codes two workgroups per CU (98 VGPRs, 60 KiB); 16-bit one (2 x 48 KiB windows)
     launch_big_bn<MODE, A16, 64, 2, true>(p, st);
   } else if (bn == 256) {
@@ -1514,8 +2224,9 @@ extern "C" int lbt_conv_fwd_igemm_q(const void* xq, int32_t a_kind, const int8_t
   p.ksplit = 1;
   all_taps(p, MODE_FWD);
   p.yq = yq; p.qout = qout; p.chsum = chsum; p.hw = d.Ho * d.Wo;
-  // the 256-row kernel's quantising epilogue on sample-blocked tiles (quantq_epilogue)
-  p.perm = big_tuning().fwdq_perm ? 1 : 0;
+  // the 256-row kernels' quantising epilogue on sample-blocked tiles (1: quantq_epilogue, >= 2: the
+  // persistent igemm_fwdq_kernel where it applies)
+  p.perm = big_tuning().fwdq_perm > 0 ? big_tuning().fwdq_perm : 0;
   p.npb = (d.Ho * d.Wo + 15) / 16;
   return launch<MODE_FWD, false>(p, (hipStream_t)stream);
 }
@@ -1537,7 +2248,8 @@ extern "C" int lbt_igemm_get_tuning(lbt_igemm_tuning* out) {
 }
 
 extern "C" int lbt_igemm_set_tuning(const lbt_igemm_tuning* t) {
-  if (!t || t->min_tiles < 1 || t->stages < 2 || t->stages > 4 || (t->max_bn != 64 && t->max_bn != 128 && t->max_bn != 256))
+  if (!t || t->min_tiles < 1 || t->stages < 2 || t->stages > 4 || (t->max_bn != 64 && t->max_bn != 128 && t->max_bn != 256) ||
+      t->fwdq_perm < 0 || t->fwdq_perm > 4096)
     return LBT_EINVAL;
   lbt_igemm_tuning& cur = big_tuning();
   cur.big = t->big; cur.min_tiles = t->min_tiles; cur.stages = t->stages; cur.max_bn = t->max_bn;
@@ -1630,7 +2342,7 @@ extern "C" int lbt_conv_dgrad_igemm_bna(const int16_t* gq, const int8_t* wd, int
     p.ksplit = 1;
     all_taps(p, MODE_DGRAD);
     p.has_bna = 1;
-    p.perm = 1;
+    p.perm = big_tuning().fwdq_perm >= 2 ? big_tuning().fwdq_perm : 1;  // >= 2: the persistent form where it applies
     p.npb = (d.H * d.W + 15) / 16;
     p.bna = b;
     if (launch_big<MODE_DGRAD, true>(p, st)) return (int)hipGetLastError();

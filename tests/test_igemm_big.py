@@ -121,7 +121,7 @@ def test_big_dgrad_matches_generic(N, H, Cin, Cout, k, g_i16, add):
         assert torch.equal(dx, ref), (stages, max_bn, halo)
 
 
-@pytest.mark.parametrize("N,H,Cin,Cout,k", [(3, 14, 64, 128, 3), (2, 15, 128, 64, 1)])
+@pytest.mark.parametrize("N,H,Cin,Cout,k", [(3, 14, 64, 128, 3), (2, 15, 128, 64, 1), (3, 14, 64, 256, 1)])
 @pytest.mark.parametrize("a_kind", [0, 1])
 @pytest.mark.parametrize("stochastic", [True, False])
 def test_big_quantising_epilogue_matches_fwd_then_quantize(N, H, Cin, Cout, k, a_kind, stochastic):
@@ -141,9 +141,13 @@ def test_big_quantising_epilogue_matches_fwd_then_quantize(N, H, Cin, Cout, k, a
     q_ref = ops.quantize(y, qo, OUT_I8, chsum=cs_ref, C=Cout)
     cnt_ref = ctx.counts_view()[qo.slot].sum(0).cpu()
     assert cnt_ref[0] > 0 and cnt_ref[1] > cnt_ref[0]
-    # the quantising epilogue never takes the 256-column tile; fwdq_perm: the sample-blocked, LDS-staged
-    # form (2 stages), else quant_epilogue on row-major tiles (every ring depth, halo on and off)
+    # the quantising epilogue never takes the 256-column tile; fwdq_perm 1: the sample-blocked, LDS-staged
+    # form (2 stages); 2 (the default): the same for these K > 64 shapes; 8: the persistent kernel on 8
+    # workgroups, so every workgroup walks many tiles through its ring (3 and 4 stages); 0: quant_epilogue
+    # on row-major tiles (every ring depth, halo on and off). The K = 64 shape (one k-block) takes the
+    # persistent kernel at the default 2 as well.
     cases = [(v, h, 0) for v in VARIANTS[:-1] for h in (0, 3)] + [((2, mb), 0, 1) for mb in (64, 128)]
+    cases += [((st, mb), 0, pp) for mb in (64, 128) for st, pp in ((2, 2), (3, 8), (4, 8))]
     for (stages, max_bn), halo, perm in cases:
         ctx.counts.zero_()
         cs = torch.zeros_like(cs_ref)
@@ -196,22 +200,25 @@ def test_big_dgrad_bna_matches_dgrad_then_pass_a(N, H, Cin, Cout, k, stochastic)
     c_ref = counts()
     assert (c_ref > 0).all(), c_ref
     s_ref = s_ref.view(NSHARD, -1).sum(0)
-    variants = [(1, st, mb, h) for st, mb in VARIANTS if mb <= 128 for h in (0, 3)] + [(0, 2, 128, 0)]
-    for big, stages, max_bn, halo in variants:
+    # fwdq_perm 1 and 2 (the default): the LDS-staged pass-A epilogue; 8: the opt-in persistent kernel
+    # on 8 workgroups (stochastic quantisers with tables; many tiles each)
+    variants = [(1, st, mb, h, 1) for st, mb in VARIANTS if mb <= 128 for h in (0, 3)] + [(0, 2, 128, 0, 1)]
+    variants += [(1, 2, 64, 0, 2), (1, 3, 64, 0, 8)]
+    for big, stages, max_bn, halo, perm in variants:
         ctx.counts.zero_()
         G = torch.full_like(G_ref, 12345)
         sums = torch.zeros(NSHARD * 4 * Cin, dtype=torch.int64, device=DEV)
         scratch = torch.full_like(dx, float("nan"))
         n0 = _launches()
-        with ops.igemm_forced(big=big, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo):
+        with ops.igemm_forced(big=big, min_tiles=1, stages=stages, max_bn=max_bn, halo=halo, fwdq_perm=perm):
             ops.conv_dgrad_igemm_bna(g, wd, ksd, d, qg.desc, qw.desc, qr.desc, R, gb, qrg, qng, qn, G, sums, scratch,
                                      None)
         assert _launches() == n0 + big, "the 256-row kernel did not run"
         if big:
             assert torch.isnan(scratch).all(), "the fused path must not store dx"
-        assert torch.equal(G, G_ref), (big, stages, max_bn, halo)
-        assert torch.equal(sums.view(NSHARD, -1).sum(0), s_ref), (big, stages, max_bn, halo)
-        assert torch.equal(counts(), c_ref), (big, stages, max_bn, halo)
+        assert torch.equal(G, G_ref), (big, stages, max_bn, halo, perm)
+        assert torch.equal(sums.view(NSHARD, -1).sum(0), s_ref), (big, stages, max_bn, halo, perm)
+        assert torch.equal(counts(), c_ref), (big, stages, max_bn, halo, perm)
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout", [

@@ -15,6 +15,7 @@
 #                    per launch position (tools/step_positions.py)
 #   strong           tools/strong_probe.py (per-GPU batch 16/32/64/128 + world-1 RCCL exchange)
 #   py:<script>[:args]  python <script> args
+# Any step may carry environment settings for its own run: VAR=val+VAR2=val@<step>
 # Output: gpurun_out/<tag>/
 set -u
 TAG=${1:?tag}
@@ -23,13 +24,7 @@ cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 n=0
-for step in "$@"; do
-  n=$((n + 1))
-  name=${step%%:*}
-  rest=""
-  [ "$step" != "$name" ] && rest=${step#*:}
-  args=${rest//:/ }
-  log="$OUT/$(printf %02d $n)_${name}"
+run_step() {
   case "$name" in
     tests)
       # tests[:<path>[:<-k expression>]]
@@ -69,8 +64,28 @@ for step in "$@"; do
       timeout -k 10 600 python $args > "$log.log" 2>&1; rc=$?
       tail -5 "$log.log" ;;
     *)
-      echo "unknown step $step"; exit 2 ;;
+      echo "unknown step $step"; rc=2 ;;
   esac
+  return $rc
+}
+for step in "$@"; do
+  n=$((n + 1))
+  envs=()
+  if [[ "$step" == *@* ]]; then
+    # VAR=val+VAR2=val: a '+' piece without '=' belongs to the previous value (e.g. PROBE_ONLY=a+b,c+d)
+    IFS='+' read -ra parts <<< "${step%%@*}"
+    for pc in "${parts[@]}"; do
+      if [[ "$pc" == *=* || ${#envs[@]} -eq 0 ]]; then envs+=("$pc"); else envs[-1]="${envs[-1]}+$pc"; fi
+    done
+    step=${step#*@}
+  fi
+  name=${step%%:*}
+  rest=""
+  [ "$step" != "$name" ] && rest=${step#*:}
+  args=${rest//:/ }
+  log="$OUT/$(printf %02d $n)_${name}"
+  [ ${#envs[@]} -gt 0 ] && printf '%s\n' "${envs[@]}" > "$log.env"
+  ( for ev in "${envs[@]}"; do export "$ev"; done; run_step ); rc=$?
   if [ $rc != 0 ]; then
     echo "step $step failed rc=$rc"; exit 1
   fi
