@@ -208,10 +208,15 @@ LBT_DEV float qscale(const lbt_qdesc& q) { return ldexpf(1.0f, -frac_exp(q)); }
 
 // One element: integer code + overflow predicates (on the UNquantised x, against I_t).
 // stochastic: floor(clip(x*m + u, -L, L-1)); nearest: rint(clip(x*m, -L, L-1)) (half-even).
+// The asymmetric predicate xm >= T or xm < -T (T = L, Lh: powers of two) is ONE compare on
+// a = max(xm, -xm (1 - 2^-24)): for xm < 0 the product rounds to >= T exactly when -xm > T (the float
+// below T is T (1 - 2^-24)); NaN compares false either way. Bit-identical counts, fewer VALU.
+LBT_DEV float ovf_abs(float xm) { return fmaxf(xm, xm * -0x1.fffffep-1f); }
 LBT_DEV int quant1(const QState& s, int stochastic, float x, float u, int& ov1, int& ov2) {
   const float xm = x * s.m;  // exact: m is a power of two
-  ov1 += (xm >= s.L) | (xm < -s.L);
-  ov2 += (xm >= s.Lh) | (xm < -s.Lh);
+  const float a = ovf_abs(xm);
+  ov1 += a >= s.L;
+  ov2 += a >= s.Lh;
   float v = stochastic ? (xm + u) : xm;
   v = fminf(fmaxf(v, -s.L), s.Lm1);
   v = stochastic ? floorf(v) : rintf(v);
@@ -250,8 +255,9 @@ LBT_DEV float div_by(float x, const Recip& d) {
 template <int STOCH>  // 1 stochastic, 0 nearest, -1 from `stochastic`
 LBT_DEV int quant_w(const QState& s, int stochastic, float x, float u, int& ov1w, int& ov2w) {
   const float xm = x * s.m;
-  ov1w += __popcll(__ballot((xm >= s.L) | (xm < -s.L)));
-  ov2w += __popcll(__ballot((xm >= s.Lh) | (xm < -s.Lh)));
+  const float a = ovf_abs(xm);
+  ov1w += __popcll(__ballot(a >= s.L));
+  ov2w += __popcll(__ballot(a >= s.Lh));
   const bool st = STOCH < 0 ? stochastic != 0 : STOCH == 1;
   float v = st ? (xm + u) : xm;
   v = fminf(fmaxf(v, -s.L), s.Lm1);

@@ -19,12 +19,17 @@ LBT_DEV pf2 pdiv(pf2 x, pf2 y, pf2 rc) {
   const pf2 r1 = __builtin_elementwise_fma(-y, q1, x);
   return __builtin_elementwise_copysign(__builtin_elementwise_fma(r1, rc, q1), x);
 }
-// quant_w on a pair: the codes of x.x / x.y into c0 / c1, wave-total overflow counts
+// quant_w on a pair: the codes of x.x / x.y into c0 / c1, wave-total overflow counts. The predicates
+// x m >= T or x m < -T (T = L, Lh: powers of two) as ONE compare each on max(x m, -x m (1 - 2^-24)) (see
+// quant4_w below): one packed multiply and two max for the pair instead of a second compare and an OR per
+// element and threshold -- the ResNet-50 forward chains are VALU-bound (profiles/round5/chain_pmc.txt).
 template <int STOCH>
 LBT_DEV void quant_w2(const QState& s, int stochastic, pf2 x, pf2 u, int& ov1w, int& ov2w, int& c0, int& c1) {
   const pf2 xm = x * pk(s.m, s.m);
-  ov1w += __popcll(__ballot((xm.x >= s.L) | (xm.x < -s.L))) + __popcll(__ballot((xm.y >= s.L) | (xm.y < -s.L)));
-  ov2w += __popcll(__ballot((xm.x >= s.Lh) | (xm.x < -s.Lh))) + __popcll(__ballot((xm.y >= s.Lh) | (xm.y < -s.Lh)));
+  const pf2 ng = xm * pk(-0x1.fffffep-1f, -0x1.fffffep-1f);
+  const float a0 = fmaxf(xm.x, ng.x), a1 = fmaxf(xm.y, ng.y);
+  ov1w += __popcll(__ballot(a0 >= s.L)) + __popcll(__ballot(a1 >= s.L));
+  ov2w += __popcll(__ballot(a0 >= s.Lh)) + __popcll(__ballot(a1 >= s.Lh));
   const bool st = STOCH < 0 ? stochastic != 0 : STOCH == 1;
   const pf2 v = st ? xm + u : xm;
   const float v0 = fminf(fmaxf(v.x, -s.L), s.Lm1), v1 = fminf(fmaxf(v.y, -s.L), s.Lm1);
