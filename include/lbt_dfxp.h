@@ -381,8 +381,9 @@ typedef struct lbt_chain_branch {
  *   (ResidualBlock_q :858-863: relu(y1 + y2))
  *   y = v (fp32, if y != NULL); o1 = Q(v, qo1) and o2 = Q(v, qo2) in o*_kind if != NULL
  *   (the next layers' input quantisers, e.g. Conv2d_q X at bits+1 in LBT_OUT_U8OFF).
- *   ybits (optional, C % 4 == 0): ybits[e / 4] bit k = (v[e + k] > 0) for every channel quad
- *   e = 4j -- the ReLU mask of y in 1/32 of y's bytes (lbt_bn_bwd_a_wide_masked's y_bits).      */
+ *   ybits (optional, C % 4 == 0, only together with y -- else LBT_EINVAL): ybits[e / 4] bit k =
+ *   (v[e + k] > 0) for every channel quad e = 4j -- the ReLU mask of y in 1/32 of y's bytes
+ *   (lbt_bn_bwd_a_wide_masked's y_bits).                                                          */
 typedef struct lbt_chain_fwd {
   lbt_chain_branch b1, b2; int32_t has_b2;
   const float* res; int32_t relu;

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
           for (int k = 0; k < 4; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
         }
         if (ystore) store4_f32(a.y, e, v);
-        if (a.ybits)  // uniform
+        if (ystore && a.ybits)  // uniform; ybits travels with y (host check), so y-less variants compile it out
           a.ybits[e >> 2] = (uint8_t)((v[0] > 0.f) | ((v[1] > 0.f) << 1) | ((v[2] > 0.f) << 2) | ((v[3] > 0.f) << 3));
         if (o1) {
           int c[4];
@@ -758,6 +758,7 @@ constexpr int kFwdBlk = kFQ | kFRout | kFRelu | kFStoch;  // every fused-plan fo
 extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   if (!shape_ok(a->rows, a->inner, a->C)) return LBT_EINVAL;
   if (a->inner * (LBT_FWD_RB + 1) >= ((int64_t)1 << 31)) return LBT_EINVAL;  // 32-bit lane offsets of a row batch
+  if (a->ybits && !a->y) return LBT_EINVAL;  // the ReLU mask bytes are written beside the fp32 block output
   dim3 grid;
   int rpt;
   if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;

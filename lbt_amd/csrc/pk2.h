@@ -4,6 +4,17 @@
 
 namespace lbt {
 
+// The quantisers' last steps for an ACTIVE quantiser (L >= 1) and a non-NaN operand -- every caller of the
+// packed helpers below: the clip is one v_med3_f32 (fminf(fmaxf(v, -L), L - 1) needs two; the fused conv
+// kernels' qfloor2 already clips this way), and floor + conversion is one v_cvt_flr_i32_f32 (exact: |v|
+// <= 2^15). The element chains are VALU-bound (profiles/round5/chain_pmc.txt).
+LBT_DEV float clip_q(const QState& s, float v) { return __builtin_amdgcn_fmed3f(v, -s.L, s.Lm1); }
+LBT_DEV int floor_i(float v) {
+  int r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
 // v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: each half rounded exactly as the scalar op. The element
 // chains are VALU-heavy on the wide layers (ResNet-50: ~30-40 VALU ops per element against 3-12 bytes),
 // so their multiplies / adds / fmas run two channels per instruction; compares, clamps, floors and
@@ -32,9 +43,14 @@ LBT_DEV void quant_w2(const QState& s, int stochastic, pf2 x, pf2 u, int& ov1w, 
   ov2w += __popcll(__ballot(a0 >= s.Lh)) + __popcll(__ballot(a1 >= s.Lh));
   const bool st = STOCH < 0 ? stochastic != 0 : STOCH == 1;
   const pf2 v = st ? xm + u : xm;
-  const float v0 = fminf(fmaxf(v.x, -s.L), s.Lm1), v1 = fminf(fmaxf(v.y, -s.L), s.Lm1);
-  c0 = (int)(st ? floorf(v0) : rintf(v0));
-  c1 = (int)(st ? floorf(v1) : rintf(v1));
+  const float v0 = clip_q(s, v.x), v1 = clip_q(s, v.y);
+  if (STOCH == 1) {
+    c0 = floor_i(v0);
+    c1 = floor_i(v1);
+  } else {
+    c0 = (int)(st ? floorf(v0) : rintf(v0));
+    c1 = (int)(st ? floorf(v1) : rintf(v1));
+  }
 }
 
 // Four consecutive elements (one float4) through a stochastic (ST) or round-to-nearest quantiser: codes
@@ -64,8 +80,8 @@ LBT_DEV void quant4_w(const QState& s, const float4& x, const float4& u, int (&c
   const float w[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const float vv = fminf(fmaxf(w[e], -s.L), s.Lm1);
-    c[e] = (int)(ST ? floorf(vv) : rintf(vv));
+    const float vv = clip_q(s, w[e]);
+    c[e] = ST ? floor_i(vv) : (int)rintf(vv);
   }
 }
 
