@@ -273,7 +273,8 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
           for (int h = 0; h < 2; ++h)
             quant_w2<ST>(so1, a.qo1.stochastic, pk(v[2 * h], v[2 * h + 1]), pk(no1.u[2 * h], no1.u[2 * h + 1]),
                          ovo[0][0], ovo[0][1], c[2 * h], c[2 * h + 1]);
-          if (u8) store4_code(a.o1, LBT_OUT_U8OFF, e, c, 0.f);
+          if (u8 && relu) store4_i8((int8_t*)a.o1, e, c, 128);  // after the ReLU every code is >= 0
+          else if (u8) store4_code(a.o1, LBT_OUT_U8OFF, e, c, 0.f);
           else store4_code(a.o1, a.o1_kind, e, c, so1.inv_m);
         }
         if (o2) {
@@ -282,7 +283,8 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
           for (int h = 0; h < 2; ++h)
             quant_w2<ST>(so2, a.qo2.stochastic, pk(v[2 * h], v[2 * h + 1]), pk(no2.u[2 * h], no2.u[2 * h + 1]),
                          ovo[1][0], ovo[1][1], c[2 * h], c[2 * h + 1]);
-          if (u8) store4_code(a.o2, LBT_OUT_U8OFF, e, c, 0.f);
+          if (u8 && relu) store4_i8((int8_t*)a.o2, e, c, 128);
+          else if (u8) store4_code(a.o2, LBT_OUT_U8OFF, e, c, 0.f);
           else store4_code(a.o2, a.o2_kind, e, c, so2.inv_m);
         }
         // one row at a time: interleaving the batch's rows (the scheduler's default) doubles the VGPRs
