@@ -2533,17 +2533,18 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     if (YST && own) st_out4(a.y, (uint32_t)(img + e), make_float4(v[0].x, v[0].y, v[1].x, v[1].y));
     const f2 uo[2] = {mk2(nov[it].x, nov[it].y), mk2(nov[it].z, nov[it].w)};
     const float X1 = ov_thr(own, so1.L), X2 = ov_thr(own, so1.Lh);
-    f2 co[2];
+    int co[4];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       // v >= 0 after the ReLU (NaN -> 0): the lower clip and x < -L cannot hold, the codes are >= 0
       const f2 xm = v[h] * so1.m;
       ov_count2_pos(xm, X1, X2, ovx1, ovx2);
       const f2 w = xm + uo[h];
-      co[h] = mk2(floorf(fminf(w.x, so1.Lm1)), floorf(fminf(w.y, so1.Lm1)));
+      co[2 * h] = floor_i(fminf(w.x, so1.Lm1));
+      co[2 * h + 1] = floor_i(fminf(w.y, so1.Lm1));
     }
     // LBT_OUT_U8OFF: code - 128 (= code ^ 0x80 for codes in [0, 255]); outside the image: the code of 0
-    const int cw = in ? (pack4f(co[0], co[1]) ^ (int)0x80808080) : (int)0x80808080;
+    const int cw = in ? (pack4(co) ^ (int)0x80808080) : (int)0x80808080;
     if (valid) *reinterpret_cast<int*>(sh.x + pix * C + cq) = cw;
     if (own) st_out((int8_t*)a.o1 + img + e, cw);
   }
@@ -2820,22 +2821,24 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
     const f2 u2[2] = {mk2(no2[it].x, no2[it].y), mk2(no2[it].z, no2[it].w)};
     const float X1 = ov_thr(own, so1.L), X2 = ov_thr(own, so1.Lh);
     const float Z1 = ov_thr(own, so2.L), Z2 = ov_thr(own, so2.Lh);
-    f2 c1[2], c2[2];
+    int c1[4], c2[4];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       // v >= 0 after the ReLU: only the upper clip can act, the codes are >= 0
       const f2 xm = v[h] * so1.m;
       ov_count2_pos(xm, X1, X2, ovx1, ovx2);
       const f2 w1 = xm + u1[h];
-      c1[h] = mk2(floorf(fminf(w1.x, so1.Lm1)), floorf(fminf(w1.y, so1.Lm1)));
+      c1[2 * h] = floor_i(fminf(w1.x, so1.Lm1));
+      c1[2 * h + 1] = floor_i(fminf(w1.y, so1.Lm1));
       const f2 zm = v[h] * so2.m;
       ov_count2_pos(zm, Z1, Z2, ovs1, ovs2);
       const f2 w2 = zm + u2[h];
-      c2[h] = mk2(floorf(fminf(w2.x, so2.Lm1)), floorf(fminf(w2.y, so2.Lm1)));
+      c2[2 * h] = floor_i(fminf(w2.x, so2.Lm1));
+      c2[2 * h + 1] = floor_i(fminf(w2.y, so2.Lm1));
     }
     // LBT_OUT_U8OFF (code ^ 0x80); below the image: the code of 0
-    const int cw1 = in ? (pack4f(c1[0], c1[1]) ^ (int)0x80808080) : (int)0x80808080;
-    const int cw2 = in ? (pack4f(c2[0], c2[1]) ^ (int)0x80808080) : (int)0x80808080;
+    const int cw1 = in ? (pack4(c1) ^ (int)0x80808080) : (int)0x80808080;
+    const int cw2 = in ? (pack4(c2) ^ (int)0x80808080) : (int)0x80808080;
     if (valid) *reinterpret_cast<int*>(sh.xa + pix * C + cq) = cw1;
     if (own && !(hy & 1) && !(x & 1)) *reinterpret_cast<int*>(sh.xs + ((hy >> 1) * Wq + (x >> 1)) * C + cq) = cw2;
     if (own) {

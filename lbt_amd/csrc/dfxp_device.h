@@ -212,6 +212,12 @@ LBT_DEV float qscale(const lbt_qdesc& q) { return ldexpf(1.0f, -frac_exp(q)); }
 // a = max(xm, -xm (1 - 2^-24)): for xm < 0 the product rounds to >= T exactly when -xm > T (the float
 // below T is T (1 - 2^-24)); NaN compares false either way. Bit-identical counts, fewer VALU.
 LBT_DEV float ovf_abs(float xm) { return fmaxf(xm, xm * -0x1.fffffep-1f); }
+// (int)floorf(v) as one v_cvt_flr_i32_f32 (|v| < 2^31, not NaN: the quantisers' clipped operands)
+LBT_DEV int floor_i(float v) {
+  int r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
 LBT_DEV int quant1(const QState& s, int stochastic, float x, float u, int& ov1, int& ov2) {
   const float xm = x * s.m;  // exact: m is a power of two
   const float a = ovf_abs(xm);

@@ -9,11 +9,6 @@ namespace lbt {
 // kernels' qfloor2 already clips this way), and floor + conversion is one v_cvt_flr_i32_f32 (exact: |v|
 // <= 2^15). The element chains are VALU-bound (profiles/round5/chain_pmc.txt).
 LBT_DEV float clip_q(const QState& s, float v) { return __builtin_amdgcn_fmed3f(v, -s.L, s.Lm1); }
-LBT_DEV int floor_i(float v) {
-  int r;
-  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
-  return r;
-}
 
 // v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: each half rounded exactly as the scalar op. The element
 // chains are VALU-heavy on the wide layers (ResNet-50: ~30-40 VALU ops per element against 3-12 bytes),

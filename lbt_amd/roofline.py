@@ -57,9 +57,25 @@ def family(kernel_name):
     n = kernel_name.replace("(anonymous namespace)::", "").replace("void ", "").strip()
     if n.startswith("igemm_kernel<"):
         args = n[len("igemm_kernel<"):].split(">")[0]
-        if args in ("fwd", "dgrad"):  # already a family label
+        if args in ("fwd", "dgrad", "dgrad+bn_a", "dgrad+bn3_a"):  # already a family label
             return n
         return "igemm_kernel<fwd>" if args.split(",")[0].strip() == "0" else "igemm_kernel<dgrad>"
+    # the 256-row / persistent GEMMs under the labels lbt_amd.dfxp.ops times them with:
+    # igemm_big_kernel<MODE, A16, ADD, BN, S, BNA, HALO>
+    if n.startswith("igemm_big_kernel<"):
+        args = [a.strip() for a in n[len("igemm_big_kernel<"):].split(">")[0].split(",")]
+        if args[0] == "0":
+            return "igemm_kernel<fwd>"
+        bna = int(args[5]) if len(args) > 5 and args[5].lstrip("-").isdigit() else 0
+        return {1: "igemm_kernel<dgrad+bn_a>", 2: "igemm_kernel<dgrad+bn3_a>",
+                3: "igemm_kernel<dgrad+bn3_a>"}.get(bna, "igemm_kernel<dgrad>")
+    if n.startswith("igemm_fwdq_kernel"):
+        return "igemm_kernel<fwd>"
+    if n.startswith("igemm_dgrada_kernel"):
+        return "igemm_kernel<dgrad+bn_a>"
+    # the storing wide weight gradient (lbt_conv_wgrad_igemm_store) runs one of three bodies
+    if n.startswith(("wgrad1_kernel", "wgrad3_kernel", "wgrad_wide_kernel")):
+        return "wgrad_wide_kernel"
     if n.startswith("conv_gemm_kernel<"):
         args = [a.strip() for a in n[len("conv_gemm_kernel<"):].split(">")[0].split(",")]
         if len(args) < 3:  # already a family label, e.g. "conv_gemm_kernel<1> (dgrad+A)"
