@@ -490,6 +490,13 @@ LBT_DEV void vm_wait() {
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
+// XCD-contiguous logical id of workgroup b of n: the hardware deals workgroups round-robin over the 8
+// XCDs, so logical ids [start_x, start_x + count_x) all run on XCD x, in dispatch order (bijective)
+LBT_DEV uint32_t xcd_logical(uint32_t b, uint32_t n) {
+  const uint32_t x = b % 8, q = n / 8, r = n % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 // A 16-byte store that is ALWAYS issued (one vector-memory op on the counter whatever `ok` is): a raw buffer
 // store at byte offset off of base (< 2^31), or at an out-of-range offset -- dropped by the buffer range
 // check -- when !ok. The persistent kernels count their epilogue stores into the ring's vmcnt waits.
@@ -2652,7 +2659,10 @@ __global__ __launch_bounds__(512, 2) void wgrad3_kernel(const int8_t* __restrict
   const int CPI = (H + RB - 1) / RB;
   const int64_t TC = (int64_t)d.N * CPI;
   const int nblk = (Cin / 64) * (Cout / 64);
-  const int blk = (int)(blockIdx.x % (uint32_t)nblk), split = (int)(blockIdx.x / (uint32_t)nblk);
+  // dbg bit 1: XCD-aware order (a pixel split's channel blocks, which read the same X / G chunks, on one
+  // XCD's L2)
+  const uint32_t bid = (dbg & 2) ? xcd_logical(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int blk = (int)(bid % (uint32_t)nblk), split = (int)(bid / (uint32_t)nblk);
   const int cb = blk / (Cout / 64), ob = blk - cb * (Cout / 64);
   const int64_t c0 = TC * split / nsplit, c1 = TC * (split + 1) / nsplit;
   const int nc = (int)(c1 - c0);
@@ -2865,7 +2875,9 @@ void wgrad3_launch(const int8_t* xq, const void* gq, const lbt_conv_desc& d, lon
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL((wgrad3_kernel<G16, NXW, S>), grid, dim3(512), shm, st, xq, gq, d, slab, nsplit, dbg);
+  // LBT_WGRAD_XCD bit 1: the XCD-aware order for the 3x3 body (dbg bit 1)
+  static const int xmap = getenv_int("LBT_WGRAD_XCD", 1) & 2;
+  hipLaunchKernelGGL((wgrad3_kernel<G16, NXW, S>), grid, dim3(512), shm, st, xq, gq, d, slab, nsplit, dbg | xmap);
 }
 
 bool wgrad3_ok(const lbt_conv_desc& d) {
@@ -2891,7 +2903,8 @@ bool wgrad3_ok(const lbt_conv_desc& d) {
 // identity cancels). Every (split, ci, co) has one writer: STORED into slab[split][Cin][Cout].
 template <int WCI, int S>
 __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const int8_t* __restrict__ xq, const int16_t* __restrict__ gq,
-                                                      lbt_conv_desc d, long long* __restrict__ slab, int nsplit) {
+                                                      lbt_conv_desc d, long long* __restrict__ slab, int nsplit,
+                                                      int xmap) {
   constexpr int WCO = 8 / WCI;
   constexpr int TCI = 64 * WCI, TCO = 32 * WCO;     // workgroup tile
   constexpr int NXS = TCI / 16, NGG = TCO / 8;       // X slices, G groups (1 KiB images each)
@@ -2910,7 +2923,9 @@ __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const int8_t* __restrict
   const int64_t P = (int64_t)d.N * d.Ho * d.Wo;
   const int64_t TC = (P + 63) / 64;
   const int cbn = Cin / TCI, obn = Cout / TCO, nblk = cbn * obn;
-  const int blk = (int)(blockIdx.x % (uint32_t)nblk), split = (int)(blockIdx.x / (uint32_t)nblk);
+  // xmap: XCD-aware order (a pixel split's channel tiles, which read the same X / G chunks, on one XCD)
+  const uint32_t bid = xmap ? xcd_logical(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int blk = (int)(bid % (uint32_t)nblk), split = (int)(bid / (uint32_t)nblk);
   const int cb = blk / obn, ob = blk - cb * obn;
   const int64_t c0 = TC * split / nsplit, c1 = TC * (split + 1) / nsplit;
   const int nc = (int)(c1 - c0);
@@ -3062,8 +3077,12 @@ void wgrad1_launch(const int8_t* xq, const int16_t* gq, const lbt_conv_desc& d, 
   }();
   (void)attr;
   const int64_t nblk = (int64_t)(d.Cin / (64 * WCI)) * (d.Cout / (32 * WCO));
+  // LBT_WGRAD_XCD (default 1): bit 0 the XCD-aware order for this 1x1 body -- its pixel split's channel
+  // tiles share one XCD's L2 for their X / G chunks (ResNet-50 weight gradients 5.33 -> 5.19 ms per step;
+  // bit 1, the same for the 3x3 body, measured no change: profiles/round5/wgrad_xcd_ab.txt)
+  static const int xmap = getenv_int("LBT_WGRAD_XCD", 1) & 1;
   hipLaunchKernelGGL((wgrad1_kernel<WCI, S>), dim3((unsigned)(nblk * nsplit)), dim3(512), shm, st, xq, gq, d, slab,
-                     nsplit);
+                     nsplit, xmap);
 }
 
 }  // namespace
