@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kThreads) void chain_fwd_kernel(lbt_chain_fwd a, in
             for (int h = 0; h < 2; ++h) {
               const pf2 x1 = pcvt(q[2 * h], q[2 * h + 1]) * pk(sn[b], sn[b]);
               const pf2 x2 = x1 - pmv[b][h];
-              t2[h] = pdiv(x2, psy[b][h], psr[b][h]);  // == x2 / sigma
+              t2[h] = pdiv_nz(x2, psy[b][h], psr[b][h]);  // == x2 / sigma (x2 is never -0: see pdiv_nz)
             }
           } else {
             float t[4];

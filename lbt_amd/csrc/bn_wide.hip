@@ -338,11 +338,11 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
       for (int h = 0; h < 2; ++h) {
         const pf2 x1 = pcvt(q[2 * h], q[2 * h + 1]) * sn2;
         const pf2 x2 = x1 - mu2[h];
-        const pf2 xh = pdiv(x2, rsy[h], rsr[h]);  // == x2 / sigma
+        const pf2 xh = pdiv_nz(x2, rsy[h], rsr[h]);  // == x2 / sigma (never -0: pk2.h pdiv_nz)
         const pf2 gh = pcvt(G[2 * h], G[2 * h + 1]) * sg2;
         const pf2 t1 = gh - mg2[h];
         const pf2 t2 = xh * mgx2[h];
-        o[h] = pdiv(t1 - t2, rsy[h], rsr[h]);     // == (t1 - t2) / sigma
+        o[h] = pdiv_nz(t1 - t2, rsy[h], rsr[h]);  // == (t1 - t2) / sigma (t1 = G s - mg is never -0, so neither is t1 - t2)
       }
       if (quant) {
         int c[4];

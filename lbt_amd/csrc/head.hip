@@ -319,7 +319,7 @@ LBT_DEV void chain_eval(const lbt_chain_fwd& a, int own, const ChainIn& in, floa
     for (int h = 0; h < 2; ++h) {
       const pf2 x1 = pcvt(q[2 * h], q[2 * h + 1]) * pk(sn, sn);
       const pf2 x2 = x1 - pm[h];
-      const pf2 tt = pdiv(x2, psy[h], psr[h]);  // == x2 / sigma
+      const pf2 tt = pdiv_nz(x2, psy[h], psr[h]);  // == x2 / sigma (never -0: pk2.h pdiv_nz)
       if (j < own) quant_w2<1>(qr, 1, tt, pk(uu[2 * h], uu[2 * h + 1]), ov1, ov2, R[2 * h], R[2 * h + 1]);
       else quant_w2<1>(qr, 1, tt, pk(uu[2 * h], uu[2 * h + 1]), z1, z2, R[2 * h], R[2 * h + 1]);
       const pf2 xr = pcvt(R[2 * h], R[2 * h + 1]) * pk(qr.inv_m, qr.inv_m);

@@ -25,6 +25,15 @@ LBT_DEV pf2 pdiv(pf2 x, pf2 y, pf2 rc) {
   const pf2 r1 = __builtin_elementwise_fma(-y, q1, x);
   return __builtin_elementwise_copysign(__builtin_elementwise_fma(r1, rc, q1), x);
 }
+// pdiv for dividends that are never -0 (the copysign only restores x = -0; the BN normalisation's
+// q s - mu is q s for q = 0, i.e. +0, or a difference of two equal values, +0): one VALU fewer per element
+LBT_DEV pf2 pdiv_nz(pf2 x, pf2 y, pf2 rc) {
+  const pf2 q = x * rc;
+  const pf2 r = __builtin_elementwise_fma(-y, q, x);
+  const pf2 q1 = __builtin_elementwise_fma(r, rc, q);
+  const pf2 r1 = __builtin_elementwise_fma(-y, q1, x);
+  return __builtin_elementwise_fma(r1, rc, q1);
+}
 // quant_w on a pair: the codes of x.x / x.y into c0 / c1, wave-total overflow counts. The predicates
 // x m >= T or x m < -T (T = L, Lh: powers of two) as ONE compare each on max(x m, -x m (1 - 2^-24)) (see
 // quant4_w below): one packed multiply and two max for the pair instead of a second compare and an OR per
