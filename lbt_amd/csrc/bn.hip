@@ -660,13 +660,17 @@ __global__ void param_grads_kernel(const int64_t* sums, int C, lbt_qdesc qrg, lb
 }
 
 // grid over [groups, rows/rpt] with >= ~2048 workgroups
-bool grid_for(int64_t rows, int64_t inner, dim3& grid, int& rpt) {
+// target: the workgroup count aimed for (LBT_CHAIN_BLOCKS overrides every chain's). The forward chain
+// aims at 2048 (ResNet-50: 5.40 -> 5.16 ms per step against 512, 1024: 5.22, 4096: 5.33;
+// profiles/round5/chain_blocks_ab.txt), the backward chains keep 512.
+bool grid_for(int64_t rows, int64_t inner, dim3& grid, int& rpt, int64_t dflt = 512) {
   const int64_t groups = inner / 4;
   const int64_t gblocks = (groups + kThreads - 1) / kThreads;
-  static const int64_t target = [] {
+  static const int64_t env_target = [] {
     const char* e = getenv("LBT_CHAIN_BLOCKS");
-    return (int64_t)(e ? atoi(e) : 512);
+    return (int64_t)(e ? atoi(e) : 0);
   }();
+  const int64_t target = env_target > 0 ? env_target : dflt;
   // a workgroup's fixed costs (moment prologue, counter / channel-sum flush) must amortise over
   // enough rows: at least min_rpt per thread even if that leaves fewer than `target` workgroups
   static const int64_t min_rpt = [] {
@@ -763,7 +767,7 @@ extern "C" int lbt_bn_chain_fwd(const lbt_chain_fwd* a, void* stream) {
   if (a->ybits && !a->y) return LBT_EINVAL;  // the ReLU mask bytes are written beside the fp32 block output
   dim3 grid;
   int rpt;
-  if (!grid_for(a->rows, a->inner, grid, rpt)) return LBT_EINVAL;
+  if (!grid_for(a->rows, a->inner, grid, rpt, 2048)) return LBT_EINVAL;
   // moments precomputed (nrm.ms_in) on every normalising branch: no dynamic LDS (the 48 C bytes of the
   // in-kernel reduction held wide layers to 1-3 workgroups per CU)
   const bool msall = (!a->b1.nrm.q || a->b1.nrm.ms_in) && (!a->has_b2 || !a->b2.nrm.q || a->b2.nrm.ms_in);

@@ -12,6 +12,7 @@
 // 4 pixels x 64 consecutive channels of one sample (coalesced), keeps its channel sums in
 // registers, and the 16 pixel lanes meet (shuffles, then LDS) before one atomic per
 // (channel, sum) into a shard.
+#include <cstdlib>
 #include "dfxp_device.h"
 #include "pk2.h"
 
@@ -365,7 +366,12 @@ __global__ __launch_bounds__(kT) void bn_bwd_b_wide_kernel(WideB b) {
 // Samples per workgroup: up to 16 (one noise call per 16 elements of a thread's position) while
 // the grid keeps ~1024+ workgroups.
 int samples_per_block(int64_t xy, int64_t samples) {
-  int64_t s = samples * xy / 1024;
+  static const int64_t target = [] {  // workgroups aimed for (LBT_BWD_WGS; default 1024)
+    const char* e = getenv("LBT_BWD_WGS");
+    const int v = e ? atoi(e) : 0;
+    return (int64_t)(v > 0 ? v : 1024);
+  }();
+  int64_t s = samples * xy / target;
   if (s > 16) s = 16;
   if (s < 1) s = 1;
   if ((samples + s - 1) / s > 65535) s = (samples + 65534) / 65535;  // grid.z limit
