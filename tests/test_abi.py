@@ -73,3 +73,27 @@ def test_struct_layouts_match_c():
         assert int(out[cname]) == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert int(out["%s.%s" % (cname, f)]) == getattr(py, f).offset, (cname, f)
+
+
+def test_host_side_argument_checks_return_einval():
+    """Entry points reject unsupported argument combinations on the host, before any HIP call (so this
+    runs without a GPU): lbt_bn_chain_fwd's ReLU-mask bytes without the fp32 output they travel with,
+    and lbt_igemm_set_tuning's range checks (the accepted selection is restored)."""
+    lib = _lib.load()
+    a = _lib.ChainFwd()
+    a.rows, a.inner, a.C = 2, 64, 16
+    a.ybits = ctypes.c_void_p(0x1000)  # never dereferenced: rejected first
+    a.y = None
+    assert lib.lbt_bn_chain_fwd(ctypes.byref(a), None) == 1001
+    saved = _lib.IgemmTuning()
+    assert lib.lbt_igemm_get_tuning(ctypes.byref(saved)) == 0
+    assert saved.fwdq_perm == 2  # the default: staged, persistent for one-k-block forward GEMMs
+    for field, bad in (("fwdq_perm", -1), ("stages", 5), ("max_bn", 96), ("min_tiles", 0)):
+        t = _lib.IgemmTuning()
+        ctypes.memmove(ctypes.byref(t), ctypes.byref(saved), ctypes.sizeof(t))
+        setattr(t, field, bad)
+        assert lib.lbt_igemm_set_tuning(ctypes.byref(t)) == 1001, field
+    cur = _lib.IgemmTuning()
+    lib.lbt_igemm_get_tuning(ctypes.byref(cur))
+    assert (cur.fwdq_perm, cur.stages, cur.max_bn, cur.min_tiles) == \
+        (saved.fwdq_perm, saved.stages, saved.max_bn, saved.min_tiles)
