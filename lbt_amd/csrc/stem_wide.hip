@@ -130,6 +130,133 @@ __global__ __launch_bounds__(kThreads) void stem_wide_fwd_kernel(const int16_t* 
     }
 }
 
+// Row-tile forward (the default where it applies: Cin <= 4, KW <= 8, Wo <= 256). A workgroup owns TR
+// whole output rows of one image (TR * Wo <= 256 pixels: 8 waves x 2 m-tiles) and loops over such
+// tiles. The image rows under a tile are staged ONCE into LDS as fp16 [R][Wimg][4] (zero padding
+// and a zero 4th channel written in), so a patch row of 8 taps x 4 channels is 32 consecutive
+// halves: one MFMA k-step per kernel row, and a lane's 8 k-elements (2 taps x 4 channels) are one
+// 16-byte LDS read at a per-lane offset fixed for the tile -- no per-element gather or decode. The
+// weights (zeros at tap 7 / channel 3) are staged once per workgroup, [col][ky*32 + kx*4 + ci].
+// Operands are swapped (A = weights, B = pixels) so a lane's accumulator is 4 consecutive output
+// channels of one pixel: one 16-byte store each. The next tile's image codes are loaded into registers
+// while this tile computes. ResNet-50 conv1 at B=256: 748 us (gather kernel) -> 254 us, one eager launch.
+constexpr int kTileThreads = 512;
+constexpr int kTileWaves = kTileThreads / 64;
+constexpr int kTilePixels = kTileWaves * 2 * 16;  // 2 m-tiles per wave
+constexpr int kTilePre = 5;                        // image pixels per thread (R * Wimg <= 2560)
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+template <int NCT>
+__global__ __launch_bounds__(kTileThreads) void stem_wide_fwd_tiles_kernel(const int16_t* __restrict__ x,
+                                                                           const int8_t* __restrict__ w,
+                                                                           lbt_conv_desc d, int TR, int R, int Wimg,
+                                                                           int KS, int ntiles, lbt_qdesc qx,
+                                                                           lbt_qdesc qw, float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  _Float16* sW = reinterpret_cast<_Float16*>(smem);  // [NCT*16][KS], KS = KH*32 + 8
+  _Float16* sX = sW + NCT * 16 * KS;                 // [R][Wimg][4]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, kg = lane >> 4;
+  const int c0 = blockIdx.y * 64;
+  const int KH = d.KH, KW = d.KW, Cin = d.Cin, Cout = d.Cout, Wo = d.Wo;
+  for (int i = threadIdx.x; i < NCT * 16 * KS; i += kTileThreads) {
+    const int col = i / KS, k = i - col * KS;
+    const int ky = k >> 5, kx = (k >> 2) & 7, ci = k & 3, c = c0 + col;
+    const int v = (ky < KH && kx < KW && ci < Cin && c < Cout) ? (int)w[((ky * KW + kx) * Cin + ci) * Cout + c] : 0;
+    sW[i] = (_Float16)(float)v;
+  }
+  const int tpi = (d.Ho + TR - 1) / TR;
+  const int npx = TR * Wo, nmt = (npx + 15) >> 4;
+  const int nimg = R * Wimg;
+  const float scale = ldexpf(1.0f, -(frac_exp(qx) + frac_exp(qw)));
+  // the tile's image pixels e = t + 512 j (j < kTilePre; host: R * Wimg <= 512 kTilePre) travel through
+  // registers: the next tile's loads are issued before this tile's MFMAs and stores
+  int raw[kTilePre][2];
+  auto load_img = [&](int tile) {
+    const int n = tile / tpi, iy0 = (tile - n * tpi) * TR * d.SH - d.PT;
+#pragma unroll
+    for (int j = 0; j < kTilePre; ++j) {
+      const int e = threadIdx.x + j * kTileThreads;
+      const int row = e / Wimg, col = e - row * Wimg;
+      const int iy = iy0 + row, ix = col - d.PL;
+      const bool ok = e < nimg && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      const int16_t* p = x + (ok ? ((n * d.H + iy) * d.W + ix) * Cin : 0);  // host: N*H*W*Cin < 2^31
+      int v[4];
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci) v[ci] = (ok && ci < Cin) ? (int)p[ci] : 0;
+      raw[j][0] = (v[0] & 0xffff) | (v[1] << 16);  // two int16 codes per register
+      raw[j][1] = (v[2] & 0xffff) | (v[3] << 16);
+    }
+  };
+  if (blockIdx.x < ntiles) load_img(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tpi, oy0 = (tile - n * tpi) * TR;
+    __syncthreads();  // the previous tile's image reads are done (first pass: nothing to wait for)
+#pragma unroll
+    for (int j = 0; j < kTilePre; ++j) {
+      const int e = threadIdx.x + j * kTileThreads;
+      if (e < nimg)
+        *reinterpret_cast<h4*>(sX + e * 4) =
+            h4{(_Float16)(float)(int16_t)raw[j][0], (_Float16)(float)(raw[j][0] >> 16),
+               (_Float16)(float)(int16_t)raw[j][1], (_Float16)(float)(raw[j][1] >> 16)};
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) load_img(tile + gridDim.x);
+    // this lane's pixel in each of its m-tiles (m-tile wave + 8*mt of the tile)
+    int xo[2];
+    int64_t orow[2];
+    bool pv[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int q = (wave + kTileWaves * mt) * 16 + r;
+      const int tr = q / Wo, ox = q - tr * Wo;
+      pv[mt] = q < npx && oy0 + tr < d.Ho;
+      xo[mt] = pv[mt] ? ((tr * d.SH) * Wimg + ox * d.SW) * 4 + kg * 8 : 0;
+      orow[mt] = ((int64_t)n * d.Ho + oy0 + tr) * Wo + ox;
+    }
+    const bool m1 = wave + kTileWaves < nmt;  // uniform: this wave's second m-tile exists
+    if (wave < nmt) {
+      f4v acc[2][NCT];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[mt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int ky = 0; ky < KH; ++ky) {
+        h8 a[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) a[ct] = *reinterpret_cast<const h8*>(sW + (ct * 16 + r) * KS + ky * 32 + kg * 8);
+        const int yo = ky * Wimg * 4;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          if (mt == 1 && !m1) break;
+          // two 8-byte reads: the pixel pair is 8-byte aligned only
+          const h4 lo = *reinterpret_cast<const h4*>(sX + xo[mt] + yo);
+          const h4 hi = *reinterpret_cast<const h4*>(sX + xo[mt] + yo + 4);
+          const h8 b = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct)
+            acc[mt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ct], b, acc[mt][ct], 0, 0, 0);
+        }
+      }
+      // D[row = channel 4kg + i][col = pixel r]: 4 consecutive channels per lane
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        if (mt == 1 && !m1) break;
+        if (!pv[mt]) continue;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const int c = c0 + ct * 16 + 4 * kg;
+          if (c < Cout) {  // Cout % 16 == 0: all four channels
+            const f4v o = acc[mt][ct] * scale;  // exact integer * 2^-e
+            // streamed out (the output is ~800 MB at B=256, read once by the next kernel): 266 -> 254 us
+            __builtin_nontemporal_store(o, reinterpret_cast<f4v*>(y + orow[mt] * Cout + c));
+          }
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
 // grid (nsplit, ceil(K / 64), ceil(Cout / 64)): workgroup = one pixel range, 4 k-tiles (one per
 // wave: 16 patch elements), 64 output channels. Per 64-pixel pass the gradient rows are staged
@@ -421,18 +548,52 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
 extern "C" int lbt_conv_stem_wide_fwd(const int16_t* x, const int8_t* w_hwio, lbt_conv_desc d, lbt_qdesc qx,
                                       lbt_qdesc qw, float* y, void* stream) {
   const int K = d.KH * d.KW * d.Cin;
-  if (K <= 0 || K > kMaxK || d.Cout <= 0 || d.Cout % 16 || qx.bits > 16 || qw.bits > 8) return LBT_EINVAL;
+  // |x| <= 2^11: every image code exact in fp16
+  if (K <= 0 || K > kMaxK || d.Cout <= 0 || d.Cout % 16 || qx.bits > 12 || qw.bits > 8) return LBT_EINVAL;
   // exact fp32 accumulation: K * max|x| * max|w| <= 2^24
   if ((double)K * ldexp(1.0, qx.bits - 1) * ldexp(1.0, qw.bits - 1) > 16777216.0) return LBT_EINVAL;
   if (d.KH >= 1024 || d.KW >= 1024 || d.Cin >= 1024 || d.PT >= 1024 || d.PL >= 1024) return LBT_EINVAL;
   const int64_t M = (int64_t)d.N * d.Ho * d.Wo;
   if (M <= 0) return LBT_OK;
   if ((int64_t)d.N * d.H * d.W * d.Cin >= ((int64_t)1 << 31) || M * d.Cout >= ((int64_t)1 << 40)) return LBT_EINVAL;
-  const int KP = (K + 31) / 32 * 32;
   const int nct = d.Cout >= 64 ? 4 : d.Cout / 16;
+  hipStream_t st = (hipStream_t)stream;
+  // row tiles (default; LBT_STEM_WIDE_TILES=0 keeps the gather kernel below)
+  const char* tenv = getenv("LBT_STEM_WIDE_TILES");
+  const int tiles_env = tenv ? atoi(tenv) : 1;
+  if (tiles_env && d.Cin <= 4 && d.KW <= 8 && d.KH <= 15 && d.Wo <= kTilePixels && d.SH <= 16 && d.SW <= 16 &&
+      !(reinterpret_cast<uintptr_t>(y) & 15)) {
+    const int TR = d.Ho < kTilePixels / d.Wo ? d.Ho : kTilePixels / d.Wo;
+    const int R = (TR - 1) * d.SH + d.KH, Wimg = (d.Wo - 1) * d.SW + 8, KS = d.KH * 32 + 8;
+    const size_t shm = (size_t)nct * 16 * KS * 2 + (size_t)R * Wimg * 8;
+    const int64_t ntiles = (int64_t)d.N * ((d.Ho + TR - 1) / TR);
+    if (shm <= 65536 && R * Wimg <= kTilePre * kTileThreads && ntiles < 0x7fffffff) {
+      // one round of resident workgroups (102 VGPRs: 2 per CU x 256 CUs), every one the same number
+      // of tiles (ResNet-50 conv1, B=256: 512 -> 254 us, 768 -> 282, 1024 -> 257, 14336 -> ~590)
+      static const int64_t wgs = [] {
+        const char* e = getenv("LBT_STEM_WIDE_WGS");
+        return (int64_t)(e && atoi(e) > 0 ? atoi(e) : 512);
+      }();
+      const int64_t per = (ntiles + wgs - 1) / wgs;
+      dim3 grid((unsigned)((ntiles + per - 1) / per), (unsigned)((d.Cout + 63) / 64));
+      switch (nct) {
+#define LBT_STEM_TILES(n_)                                                                                       \
+  case n_:                                                                                                     \
+    hipLaunchKernelGGL(stem_wide_fwd_tiles_kernel<n_>, grid, dim3(kTileThreads), shm, st, x, w_hwio, d, TR, R, \
+                       Wimg, KS, (int)ntiles, qx, qw, y);                                                      \
+    break;
+        LBT_STEM_TILES(1)
+        LBT_STEM_TILES(2)
+        LBT_STEM_TILES(3)
+        default: LBT_STEM_TILES(4)
+#undef LBT_STEM_TILES
+      }
+      return (int)hipGetLastError();
+    }
+  }
+  const int KP = (K + 31) / 32 * 32;
   const size_t shm = (size_t)nct * 16 * KP * 2 + (size_t)KP * 4;
   dim3 grid((unsigned)((M + kFwdRows - 1) / kFwdRows), (unsigned)((d.Cout + 63) / 64));
-  hipStream_t st = (hipStream_t)stream;
   switch (nct) {
     case 1: hipLaunchKernelGGL(stem_wide_fwd_kernel<1>, grid, dim3(kThreads), shm, st, x, w_hwio, d, K, KP, qx, qw, y); break;
     case 2: hipLaunchKernelGGL(stem_wide_fwd_kernel<2>, grid, dim3(kThreads), shm, st, x, w_hwio, d, K, KP, qx, qw, y); break;

@@ -76,6 +76,9 @@ def family(kernel_name):
     # the storing wide weight gradient (lbt_conv_wgrad_igemm_store) runs one of three bodies
     if n.startswith(("wgrad1_kernel", "wgrad3_kernel", "wgrad_wide_kernel")):
         return "wgrad_wide_kernel"
+    # conv1's forward: the row-tile kernel or the gather kernel (lbt_conv_stem_wide_fwd)
+    if n.startswith("stem_wide_fwd_tiles_kernel"):
+        return "stem_wide_fwd_kernel"
     if n.startswith("conv_gemm_kernel<"):
         args = [a.strip() for a in n[len("conv_gemm_kernel<"):].split(">")[0].split(",")]
         if len(args) < 3:  # already a family label, e.g. "conv_gemm_kernel<1> (dgrad+A)"

@@ -6,6 +6,7 @@ GPU: the HIP layer path against the oracle, bit-exact (forward logits, every gra
 same d loss / d logits, every exponent update), on reduced widths / depths so the numpy oracle
 finishes in seconds; the full-size model through a training step (shape and finiteness checks).
 """
+import contextlib
 import os
 
 import numpy as np
@@ -17,6 +18,20 @@ from oracle import resnet as oresnet
 
 DEV = "cuda"
 F32 = np.float32
+
+
+@contextlib.contextmanager
+def _env(name, value):
+    """Set one environment variable for the block (launchers that read it per call)."""
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        yield
+    finally:
+        if old is None:
+            del os.environ[name]
+        else:
+            os.environ[name] = old
 
 
 def _maxpool_loops(x, k, s, padding):
@@ -230,7 +245,7 @@ def test_wgrad_igemm_matches_generic(N, H, Cin, Cout, k, s):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,H,Cout,k,s", [(2, 32, 64, 7, 2), (1, 40, 16, 7, 2), (2, 23, 48, 5, 1), (1, 224, 64, 7, 2),
-                                          (3, 17, 32, 3, 2)])
+                                          (3, 17, 32, 3, 2), (1, 230, 64, 7, 2), (1, 36, 128, 7, 2)])
 def test_stem_wide_matches_generic(N, H, Cout, k, s):
     """The ImageNet conv1 on fp16 MFMA (stem_wide.hip: signed 9-bit image codes, K = k*k*3 patch
     elements; 8- and 16-bit gradient codes split hi/lo) == the generic VALU kernels' exact integer
@@ -249,9 +264,13 @@ def test_stem_wide_matches_generic(N, H, Cout, k, s):
     x = torch.from_numpy(rng.integers(-256, 256, size=(N, H, H, 3)).astype(np.int16)).to(DEV)
     y1 = torch.empty((N, d.Ho, d.Wo, Cout), device=DEV)
     y2 = torch.empty_like(y1)
-    ops.conv_stem_wide_fwd(x, w_hwio, d, qx.desc, qw.desc, y1)
     ops.conv_fwd_generic(x, True, w_hwio, d, qx.desc, qw.desc, y2)
-    assert torch.equal(y1, y2)
+    # the row-tile forward (LDS image rows, default) and the per-element gather kernel
+    for tiles in ("1", "0"):
+        with _env("LBT_STEM_WIDE_TILES", tiles):
+            y1.fill_(float("nan"))
+            ops.conv_stem_wide_fwd(x, w_hwio, d, qx.desc, qw.desc, y1)
+        assert torch.equal(y1, y2), tiles
     for g_i16 in (0, 1):
         if g_i16:
             g = torch.from_numpy(rng.integers(-32768, 32768, size=(N, d.Ho, d.Wo, Cout)).astype(np.int16)).to(DEV)
