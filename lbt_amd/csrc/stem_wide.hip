@@ -385,8 +385,9 @@ __global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t
   }
 }
 
-// Weight gradient on output-row chunks (round 4): a chunk is 64 consecutive output pixels of ONE output
-// row (n, oy, 64 xc ..); its input window (KH rows x (63 SW + KW) columns x Cin) is staged in LDS as fp16
+// Weight gradient on output-row chunks (round 4): a chunk is kRwPx (128 since round 5, was 64: twice the
+// MFMA work per chunk behind the same load latency) consecutive output pixels of ONE output row (n, oy,
+// kRwPx xc ..); its input window (KH rows x ((kRwPx-1) SW + KW) columns x Cin) is staged in LDS as fp16
 // once and every patch element -- all K, one 16-row k-tile per wave, up to kRwMaxKT waves -- reads its A
 // fragment from it (stem_wide_wgrad_kernel gathers every patch element of every pixel from global
 // memory, 64 addresses per load instruction, and re-reads the gradient rows once per 64-row k-block of
@@ -395,10 +396,14 @@ __global__ __launch_bounds__(kThreads) void stem_wide_wgrad_kernel(const int16_t
 // steps, 256 hi + lo into int64 per split.
 constexpr int kRwMaxKT = 10;   // k-tiles (K <= 160)
 constexpr int kRwMaxKH = 7;    // window rows
-constexpr int kRwMaxWC = 136;  // window columns 63 SW + KW
+#ifndef LBT_RW_UNROLL
+#define LBT_RW_UNROLL 1
+#endif
+constexpr int kRwPx = 128;     // output pixels per chunk (4 MFMA k-steps)
+constexpr int kRwMaxWC = 264;  // window columns (kRwPx - 1) SW + KW
 constexpr int kRwMaxCin = 4;
 constexpr int kRwWin = kRwMaxKH * kRwMaxWC * kRwMaxCin;
-constexpr int kRwWpt = (kRwWin + 64 * kRwMaxKT - 1) / (64 * kRwMaxKT);  // window elements a thread stages (at 10 waves)
+constexpr int kRwWpt = 8;  // window elements a thread stages (host: KH * WC * Cin <= kRwWpt * 64 * kRwMaxKT)
 
 template <bool G16, int NCT>
 __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_rows_kernel(const int16_t* __restrict__ x,
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
                                                                         int64_t* __restrict__ slab) {
   constexpr int NH = G16 ? 2 : 1;
   constexpr int GV = NCT * 2;  // 16-byte (G16) / 8-byte gradient pieces per pixel (8 channels each)
-  __shared__ __attribute__((aligned(16))) _Float16 sG[NH][NCT * 16][kWgChunk + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 sG[NH][NCT * 16][kRwPx + 8];
   __shared__ _Float16 sW[kRwWin];
   const int nthr = blockDim.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -415,7 +420,7 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
   const int k = wave * 16 + r;
   const int code = k < K ? patch_code(d, k) : -1;
   const int dy = code >> 20, dx = (code >> 10) & 1023, ci = code & 1023;
-  const int WC = 63 * d.SW + d.KW, wsz = d.KH * WC * d.Cin;
+  const int WC = ((d.Wo < kRwPx ? d.Wo : kRwPx) - 1) * d.SW + d.KW, wsz = d.KH * WC * d.Cin;
   const int aoff = code >= 0 ? (dy * WC + dx) * d.Cin + ci : 0;  // + px * SW * Cin
   const int astep = d.SW * d.Cin;
   f4v facc[NH][NCT];
@@ -432,13 +437,14 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
   const int64_t cb = (int64_t)blockIdx.x * cper;
   const int64_t ce = cb + cper < nchunks ? cb + cper : nchunks;
   // one chunk's operands in registers: window elements threadIdx.x + j * nthr, gradient piece threadIdx.x
-  int wv[kRwWpt];
-  int gw[4];
+  int wv[(kRwWpt + 1) / 2];  // two int16 window codes per register
+  constexpr int kGp = (kRwPx * GV + 64 * kRwMaxKT - 1) / (64 * kRwMaxKT);  // gradient pieces a thread stages
+  int gw[kGp][4];
   auto load = [&](int64_t c) {
     const int xcc = (int)(c % xc);
     const int64_t t = c / xc;
     const int oy = (int)(t % d.Ho), n = (int)(t / d.Ho);
-    const int iy0 = oy * d.SH - d.PT, ix0 = xcc * 64 * d.SW - d.PL;
+    const int iy0 = oy * d.SH - d.PT, ix0 = xcc * kRwPx * d.SW - d.PL;
 #pragma unroll
     for (int j = 0; j < kRwWpt; ++j) {
       const int e = threadIdx.x + j * nthr;
@@ -449,20 +455,25 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
         if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W)
           v = x[((int64_t)(n * d.H + iy) * d.W + ix) * d.Cin + cc];
       }
-      wv[j] = v;
+      if (j & 1) wv[j >> 1] |= v << 16;
+      else wv[j >> 1] = v & 0xFFFF;
     }
-    gw[0] = gw[1] = gw[2] = gw[3] = 0;
-    if ((int)threadIdx.x < 64 * GV) {
-      const int px = threadIdx.x / GV, col = cg0 + (threadIdx.x % GV) * 8;
-      const int ox = xcc * 64 + px;
-      if (ox < d.Wo && col < d.Cout) {
-        const int64_t p = ((int64_t)n * d.Ho + oy) * d.Wo + ox;
-        if constexpr (G16) {
-          const int4 w4 = *reinterpret_cast<const int4*>(reinterpret_cast<const int16_t*>(g_) + p * d.Cout + col);
-          gw[0] = w4.x; gw[1] = w4.y; gw[2] = w4.z; gw[3] = w4.w;
-        } else {
-          const int2 w2 = *reinterpret_cast<const int2*>(reinterpret_cast<const int8_t*>(g_) + p * d.Cout + col);
-          gw[0] = w2.x; gw[1] = w2.y;
+#pragma unroll
+    for (int q = 0; q < kGp; ++q) {
+      gw[q][0] = gw[q][1] = gw[q][2] = gw[q][3] = 0;
+      const int idx = threadIdx.x + q * nthr;
+      if (idx < kRwPx * GV) {
+        const int px = idx / GV, col = cg0 + (idx % GV) * 8;
+        const int ox = xcc * kRwPx + px;
+        if (ox < d.Wo && col < d.Cout) {
+          const int64_t p = ((int64_t)n * d.Ho + oy) * d.Wo + ox;
+          if constexpr (G16) {
+            const int4 w4 = *reinterpret_cast<const int4*>(reinterpret_cast<const int16_t*>(g_) + p * d.Cout + col);
+            gw[q][0] = w4.x; gw[q][1] = w4.y; gw[q][2] = w4.z; gw[q][3] = w4.w;
+          } else {
+            const int2 w2 = *reinterpret_cast<const int2*>(reinterpret_cast<const int8_t*>(g_) + p * d.Cout + col);
+            gw[q][0] = w2.x; gw[q][1] = w2.y;
+          }
         }
       }
     }
@@ -471,17 +482,23 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
 #pragma unroll
     for (int j = 0; j < kRwWpt; ++j) {
       const int e = threadIdx.x + j * nthr;
-      if (e < wsz) sW[e] = (_Float16)(float)wv[j];
+      if (e < wsz) sW[e] = (_Float16)(float)((j & 1) ? (wv[j >> 1] >> 16) : (int)(int16_t)wv[j >> 1]);
     }
-    if ((int)threadIdx.x < 64 * GV) {
-      const int px = threadIdx.x / GV, col = (threadIdx.x % GV) * 8;
+#pragma unroll
+    for (int q = 0; q < kGp; ++q) {
+      const int idx = threadIdx.x + q * nthr;
+      if (idx >= kRwPx * GV) break;
+      const int px = idx / GV, col = (idx % GV) * 8;
       int v[8];
       if constexpr (G16) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { v[2 * j] = (int)(int16_t)(gw[j] & 0xFFFF); v[2 * j + 1] = gw[j] >> 16; }
+        for (int j = 0; j < 4; ++j) { v[2 * j] = (int)(int16_t)(gw[q][j] & 0xFFFF); v[2 * j + 1] = gw[q][j] >> 16; }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { v[j] = (int)(int8_t)(gw[0] >> (8 * j)); v[4 + j] = (int)(int8_t)(gw[1] >> (8 * j)); }
+        for (int j = 0; j < 4; ++j) {
+          v[j] = (int)(int8_t)(gw[q][0] >> (8 * j));
+          v[4 + j] = (int)(int8_t)(gw[q][1] >> (8 * j));
+        }
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -494,15 +511,18 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
       }
     }
   };
-  int steps = 0;
+  static_assert(kRwPx / 32 == kFlush, "one fp32 -> int32 flush per chunk");
+  // a window narrower than kRwPx pixels (Wo < kRwPx): the A reads of the pixels past Wo land past wsz
+  // (their gradients are zero) -- zeros there, never NaN patterns of stale LDS (0 * NaN)
+  for (int e = wsz + threadIdx.x; e < kRwWin; e += nthr) sW[e] = (_Float16)0.f;
   if (cb < ce) load(cb);
   for (int64_t c = cb; c < ce; ++c) {
     __syncthreads();  // the previous chunk's LDS reads are done
     store();
     __syncthreads();
     if (c + 1 < ce) load(c + 1);  // in flight during this chunk's MFMAs
-#pragma unroll
-    for (int s = 0; s < kWgChunk / 32; ++s) {
+#pragma unroll LBT_RW_UNROLL
+    for (int s = 0; s < kRwPx / 32; ++s) {
       h8 a;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -516,18 +536,15 @@ __global__ __launch_bounds__(64 * kRwMaxKT, NCT <= 2 ? 5 : 3) void stem_wgrad_ro
           const h8 b = *reinterpret_cast<const h8*>(&sG[h][ct * 16 + r][s * 32 + 8 * kg]);
           facc[h][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, facc[h][ct], 0, 0, 0);
         }
-      if (++steps == kFlush) {
-        steps = 0;
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-#pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) iacc[h][ct][i] += (int)facc[h][ct][i];
-            facc[h][ct] = f4v{0.f, 0.f, 0.f, 0.f};
-          }
-      }
     }
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) iacc[h][ct][i] += (int)facc[h][ct][i];
+        facc[h][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+      }
   }
   int64_t* out = slab + (int64_t)blockIdx.x * K * d.Cout;
 #pragma unroll
@@ -632,11 +649,12 @@ extern "C" int lbt_conv_stem_wide_wgrad(const int16_t* x, int32_t x_bits, const 
   // the row-chunk kernel where its LDS window fits (LBT_STEM_ROWS=0 at call time: never)
   {
     const char* e = getenv("LBT_STEM_ROWS");
-    const int xc = (d.Wo + 63) / 64;
+    const int xc = (d.Wo + kRwPx - 1) / kRwPx;
     const int64_t nchunks = (int64_t)d.N * d.Ho * xc;
     const int64_t cper = (nchunks + nsplit - 1) / nsplit;
     if ((!e || atoi(e) != 0) && K <= 16 * kRwMaxKT && d.Cin <= kRwMaxCin && d.KH <= kRwMaxKH &&
-        63 * d.SW + d.KW <= kRwMaxWC && d.Cout <= 64 && cper * 64 <= kMaxWgPixels) {
+        (kRwPx - 1) * d.SW + d.KW <= kRwMaxWC && d.Cout <= 64 && cper * kRwPx <= kMaxWgPixels &&
+        d.KH * (((d.Wo < kRwPx ? d.Wo : kRwPx) - 1) * d.SW + d.KW) * d.Cin <= kRwWpt * 64 * kRwMaxKT) {
       // one group of up to 64 channels; LBT_STEM_CG=32 at call time: 32-channel groups on grid.y (half the
       // accumulators, two 10-wave workgroups per CU, but the window staged twice and 12 spilled registers:
       // 1296 vs 762 us at B=256, profiles/r05/stem_probe.txt)
