@@ -78,7 +78,8 @@ def test_struct_layouts_match_c():
 def test_host_side_argument_checks_return_einval():
     """Entry points reject unsupported argument combinations on the host, before any HIP call (so this
     runs without a GPU): lbt_bn_chain_fwd's ReLU-mask bytes without the fp32 output they travel with,
-    and lbt_igemm_set_tuning's range checks (the accepted selection is restored)."""
+    lbt_igemm_set_tuning's range checks (the accepted selection is restored), and the conv1 forward's
+    fp16-exactness bound on the image codes."""
     lib = _lib.load()
     a = _lib.ChainFwd()
     a.rows, a.inner, a.C = 2, 64, 16
@@ -97,3 +98,8 @@ def test_host_side_argument_checks_return_einval():
     lib.lbt_igemm_get_tuning(ctypes.byref(cur))
     assert (cur.fwdq_perm, cur.stages, cur.max_bn, cur.min_tiles) == \
         (saved.fwdq_perm, saved.stages, saved.max_bn, saved.min_tiles)
+    # conv1 on fp16 MFMA: image codes wider than 12 bits are not exact in fp16 (|x| <= 2^11)
+    d = _lib.ConvDesc(2, 224, 224, 3, 64, 7, 7, 2, 2, 3, 3, 3, 3, 112, 112)
+    qx, qw = _lib.QDesc(), _lib.QDesc()
+    qx.bits, qw.bits = 13, 2
+    assert lib.lbt_conv_stem_wide_fwd(None, None, d, qx, qw, None, None) == 1001
