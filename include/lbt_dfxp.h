@@ -627,8 +627,8 @@ int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, lbt_conv_des
  * (the pool input is the ReLU output, so an input that receives gradient has x > 0 <=> y[o] > 0);
  * dx = relu_bwd(maxpool_bwd(g)) bit for bit, in one pass. C % 4 == 0.                           */
 /* ... and its forward: y = maxpool(relu(x)) from the ReLU's input x (relu(max) = max(relu)); amax
- * may differ from lbt_maxpool_fwd's where the window max is <= 0, where the fused backward routes
- * nothing. C % 4 == 0.                                                                          */
+ * differs from lbt_maxpool_fwd's where the window max is <= 0: there it is 255 (route nothing),
+ * so lbt_maxpool_relu_bwd may be given y = NULL for this amax. C % 4 == 0, KH*KW <= 255.         */
 int lbt_maxpool_relu_fwd(const float* x, float* y, uint8_t* amax, lbt_conv_desc d, void* stream);
 int lbt_maxpool_relu_bwd(const float* g, const uint8_t* amax, const float* y, float* dx, lbt_conv_desc d,
                          void* stream);

@@ -70,12 +70,15 @@ __global__ __launch_bounds__(kT) void maxpool_bwd_kernel(const float* __restrict
   dx[e] = s;
 }
 
+constexpr int kNoRoute = 255;  // argmax code of a relu pool window that routes no gradient
+
 // maxpool_fwd_kernel for 4 channels per thread (C % 4 == 0): the same scan and strict '>' per
 // channel, 16-byte loads, one 4-byte argmax store.
 // relu != 0: the pool of the preceding ReLU_q's output computed from its INPUT: max(relu(a), ...) =
 // relu(max(a, ...)), so y is bit-identical. The argmax differs only where the window's max is <= 0
-// (the reference's first zero vs the first raw maximum), and there y = 0 makes the fused backward
-// (maxpool_relu_bwd) route nothing either way.
+// (the reference's first zero vs the first raw maximum): there y = 0, the fused backward
+// (maxpool_relu_bwd) routes nothing, and the code is kNoRoute -- the ReLU mask travels in the argmax,
+// so the backward need not read y.
 __global__ __launch_bounds__(kT) void maxpool_fwd4_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                           uint8_t* __restrict__ amax, lbt_conv_desc d, int relu) {
   const int64_t e4 = ((int64_t)blockIdx.x * kT + threadIdx.x) * 4;
@@ -107,7 +110,12 @@ __global__ __launch_bounds__(kT) void maxpool_fwd4_kernel(const float* __restric
   }
   if (relu) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) best[j] = best[j] > 0.f ? best[j] : 0.f;
+    for (int j = 0; j < 4; ++j) {
+      // the ReLU mask rides in the argmax: a window whose max is <= 0 (y = 0) routes no gradient, so
+      // its code is kNoRoute, which no window position equals (KH*KW <= 255, launcher)
+      if (!(best[j] > 0.f)) bi[j] = kNoRoute;
+      best[j] = best[j] > 0.f ? best[j] : 0.f;
+    }
   }
   *reinterpret_cast<float4*>(y + e4) = make_float4(best[0], best[1], best[2], best[3]);
   *reinterpret_cast<uchar4*>(amax + e4) = make_uchar4((uint8_t)bi[0], (uint8_t)bi[1], (uint8_t)bi[2], (uint8_t)bi[3]);
@@ -193,7 +201,7 @@ extern "C" int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, l
 // ReLU_q (forward) of the pool's input folded into the pool: x = the ReLU's input, y = pool(relu(x)).
 // Only for use with lbt_maxpool_relu_bwd (see maxpool_fwd4_kernel). C % 4 == 0.
 extern "C" int lbt_maxpool_relu_fwd(const float* x, float* y, uint8_t* amax, lbt_conv_desc d, void* stream) {
-  if (!pool_desc_ok(d) || d.Cin % 4 || d.KH * d.KW > 256) return LBT_EINVAL;
+  if (!pool_desc_ok(d) || d.Cin % 4 || d.KH * d.KW > kNoRoute) return LBT_EINVAL;
   const int64_t n = (int64_t)d.N * d.Ho * d.Wo * d.Cin;
   hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
                      x, y, amax, d, 1);
@@ -201,10 +209,11 @@ extern "C" int lbt_maxpool_relu_fwd(const float* x, float* y, uint8_t* amax, lbt
 }
 
 // ReLU_q backward of the pool's input folded into the pool backward (y = this pool's forward
-// output): dx = relu_bwd(maxpool_bwd(g)) in one pass. C % 4 == 0.
+// output): dx = relu_bwd(maxpool_bwd(g)) in one pass. C % 4 == 0. y == NULL: amax comes from
+// lbt_maxpool_relu_fwd and carries the mask (kNoRoute), so y is not read (16 of 36 bytes per window).
 extern "C" int lbt_maxpool_relu_bwd(const float* g, const uint8_t* amax, const float* y, float* dx, lbt_conv_desc d,
                                     void* stream) {
-  if (!pool_desc_ok(d) || d.Cin % 4 || !y) return LBT_EINVAL;
+  if (!pool_desc_ok(d) || d.Cin % 4) return LBT_EINVAL;
   const int64_t n = (int64_t)d.N * d.H * d.W * d.Cin;
   hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
                      g, amax, y, dx, d);

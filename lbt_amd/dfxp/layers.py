@@ -1339,8 +1339,9 @@ class MaxPool_q(Layer_q):
                                    self.padding)
         y = self._c.get("y", (N, d.Ho, d.Wo, C), torch.float32, X.device)
         self.amax = self._c.get("amax", (N, d.Ho, d.Wo, C), torch.uint8, X.device)
-        if self.pool_relu is not None and self.pool_relu.act_in_pool and C % 4 == 0:
-            ops.maxpool_relu_fwd(X, y, self.amax, d)  # X is the ReLU's input
+        self.amax_masked = self.pool_relu is not None and self.pool_relu.act_in_pool and C % 4 == 0
+        if self.amax_masked:
+            ops.maxpool_relu_fwd(X, y, self.amax, d)  # X is the ReLU's input; amax carries the ReLU mask
         else:
             ops.maxpool_fwd(X, y, self.amax, d)
         self.y = y
@@ -1349,6 +1350,7 @@ class MaxPool_q(Layer_q):
     # the ReLU_q in front of this pool whose backward this one performs (its input > 0 mask): set
     # by the model builder, see ops.maxpool_relu_bwd
     pool_relu = None
+    amax_masked = False  # amax from maxpool_relu_fwd: the ReLU mask is in the codes (forward)
 
     def backward(self, grad, stochastic=True):
         dx = self._c.get("dx", self.X.shape, torch.float32, grad.device)
@@ -1356,7 +1358,7 @@ class MaxPool_q(Layer_q):
         if self.pool_relu is not None:
             self.pool_relu.mask_in_pool = fuse
         if fuse:
-            ops.maxpool_relu_bwd(grad.contiguous(), self.amax, self.y, dx, self.d)
+            ops.maxpool_relu_bwd(grad.contiguous(), self.amax, None if self.amax_masked else self.y, dx, self.d)
         else:
             ops.maxpool_bwd(grad.contiguous(), self.amax, dx, self.d)
         return dx

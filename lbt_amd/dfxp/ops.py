@@ -569,8 +569,9 @@ def maxpool_bwd(g, amax, dx, d):
 
 
 def maxpool_relu_bwd(g, amax, y, dx, d):
-    """MaxPool_q backward with the preceding ReLU_q's backward folded in (y: the pool's output)."""
-    with _Timed("maxpool_bwd_kernel", 9 * g.numel() + 4 * dx.numel()):
+    """MaxPool_q backward with the preceding ReLU_q's backward folded in (y: the pool's output; None when
+    amax comes from maxpool_relu_fwd, whose codes carry the mask)."""
+    with _Timed("maxpool_bwd_kernel", (9 if y is not None else 5) * g.numel() + 4 * dx.numel()):
         call("lbt_maxpool_relu_bwd", ptr(g), ptr(amax), ptr(y), ptr(dx), d, stream())
 
 

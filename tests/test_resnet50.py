@@ -300,6 +300,39 @@ def test_stem_wide_matches_generic(N, H, Cout, k, s):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,H,C", [(2, 112, 64), (3, 17, 8)])
+def test_maxpool_relu_mask_in_argmax(N, H, C):
+    """lbt_maxpool_relu_fwd's argmax codes carry the ReLU mask (255: route nothing), so
+    lbt_maxpool_relu_bwd without y == with y == relu_bwd(maxpool_bwd(g)) of the torch reference
+    (3x3 / 2 SAME, a third of the inputs <= 0 and whole windows <= 0), bit for bit."""
+    from lbt_amd.dfxp import ops
+    rng = np.random.default_rng(N * H + C)
+    d = ops.conv_desc(N, H, H, C, C, 3, 3, 2, 2, "SAME")
+    xn = rng.standard_normal((N, H, H, C)).astype(np.float32) - 0.5
+    xn[:, : H // 3] = -np.abs(xn[:, : H // 3])  # whole windows with max <= 0
+    x = torch.from_numpy(xn).to(DEV).requires_grad_(True)
+    y = torch.empty((N, d.Ho, d.Wo, C), device=DEV)
+    amax = torch.empty((N, d.Ho, d.Wo, C), dtype=torch.uint8, device=DEV)
+    ops.maxpool_relu_fwd(x.detach(), y, amax, d)
+    assert int((amax == 255).sum()) > 0
+    g = torch.from_numpy(rng.standard_normal((N, d.Ho, d.Wo, C)).astype(np.float32)).to(DEV)
+    dx1, dx2 = torch.empty_like(x), torch.empty_like(x)
+    ops.maxpool_relu_bwd(g, amax, y, dx1, d)
+    ops.maxpool_relu_bwd(g, amax, None, dx2, d)
+    assert torch.equal(dx1, dx2)
+    # torch: relu then max pool (SAME 3x3/2 on even H pads bottom/right only; -inf padding)
+    xr = torch.relu(x).permute(0, 3, 1, 2)
+    pt, pb, pl, pr = d.PT, d.PB, d.PL, d.PR
+    yr = torch.nn.functional.max_pool2d(torch.nn.functional.pad(xr, (pl, pr, pt, pb), value=-float("inf")), 3, 2)
+    assert torch.equal(yr.permute(0, 2, 3, 1).detach(), y)
+    # gradient routing against torch's relu + max-pool backward (fp32; an element that is the maximum of
+    # several windows sums their gradients, possibly in another order: 1e-6)
+    (yr.permute(0, 2, 3, 1) * g).sum().backward()
+    assert torch.allclose(dx1, x.grad, rtol=1e-6, atol=1e-6)
+    assert torch.all(dx1[x.detach() <= 0] == 0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N,IN,OUT", [(32, 2048, 1000), (3, 128, 40), (17, 64, 8)])
 def test_dense_mfma_matches_generic(N, IN, OUT):
     """Dense_q on int8 MFMA (fwd; dgrad with int8 and hi/lo-split int16 gradient codes) and the
