@@ -169,6 +169,38 @@ def _timed_region(step, steps, warmup, world, sync, device):
     return el
 
 
+def _exchange_report(trainer, model, world, reps=20):
+    """The N>1 line's audit fields: the process group's size and backend, whether the
+    collectives ran inside the step's graph, the exchange buffer's bytes, the collectives per step, and
+    the exchange all-reduce timed EAGERLY, once, after the timed loop (reps back to back between a
+    barrier and a synchronize, max over ranks) -- a cost estimate for the in-graph collective, which
+    the timed steps include. The buffer is rewritten by the next step's backward, so summing it here
+    changes nothing."""
+    buf = trainer.xbuf if trainer.xbuf is not None else trainer.comm
+    nsync = 0
+    if getattr(model, "sync_bn", False):
+        nsync = sum(1 for ops_ in (getattr(model, "_fwd", None), getattr(model, "_bwd", None)) if ops_
+                    for op in ops_ if getattr(op, "kname", "") == "allreduce")
+    rep = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+           "collectives_in_graph": bool(getattr(trainer, "capture_comm", False)),
+           "bytes": int(buf.numel() * buf.element_size()) if buf is not None else 0,
+           "dtype": str(buf.dtype).replace("torch.", "") if buf is not None else None,
+           "collectives_per_step": 1 + nsync, "syncbn_collectives_per_step": nsync}
+    if buf is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            trainer._exchange()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device=buf.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rep["eager_allreduce_us"] = round(float(t.item()) / reps * 1e6, 2)
+        rep["eager_reps"] = reps
+    return rep
+
+
 def _dry_run(args, world, rank, backend, strong):
     if backend != "gloo":
         raise SystemExit("--dry-run runs on the gloo backend (CPU)")
@@ -331,6 +363,8 @@ def main():
         out["config"]["bn"] = bn_mode if world > 1 else "local"
         out["config"]["collectives_in_graph"] = bool(getattr(trainer, "capture_comm", False))
         out["config"]["shared_gpu"] = os.environ.get("LBT_SHARE_GPU") == "1"
+    if world > 1:
+        out["config"]["exchange"] = _exchange_report(trainer, model, world)
     if w4:
         out["config"]["workload"] = "ResNet-20 CIFAR-10, 4-bit DFXP weights (packed, 2 per byte), 8-bit A/G, train step"
     if r50:

@@ -628,7 +628,11 @@ int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, lbt_conv_des
  * dx = relu_bwd(maxpool_bwd(g)) bit for bit, in one pass. C % 4 == 0.                           */
 /* ... and its forward: y = maxpool(relu(x)) from the ReLU's input x (relu(max) = max(relu)); amax
  * differs from lbt_maxpool_fwd's where the window max is <= 0: there it is 255 (route nothing),
- * so lbt_maxpool_relu_bwd may be given y = NULL for this amax. C % 4 == 0, KH*KW <= 255.         */
+ * so lbt_maxpool_relu_bwd may be given y = NULL for this amax. C % 4 == 0, KH*KW <= 255.
+ * HARD PRECONDITION of y == NULL: amax must come from lbt_maxpool_relu_fwd (masked codes). The
+ * library cannot tell the two amax encodings apart; an amax from plain lbt_maxpool_fwd with
+ * y == NULL routes gradient to windows whose max is <= 0 -- silently wrong. With amax from
+ * lbt_maxpool_fwd always pass that pool's y.                                                       */
 int lbt_maxpool_relu_fwd(const float* x, float* y, uint8_t* amax, lbt_conv_desc d, void* stream);
 int lbt_maxpool_relu_bwd(const float* g, const uint8_t* amax, const float* y, float* dx, lbt_conv_desc d,
                          void* stream);

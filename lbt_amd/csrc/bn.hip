@@ -37,10 +37,11 @@ LBT_DEV void f4(const float4& c, float v[4]) { v[0] = c.x; v[1] = c.y; v[2] = c.
 // arithmetic (stores may alias the inputs as far as the compiler knows, so it would not hoist
 // them itself) -- one HBM round trip per batch instead of one per row.
 constexpr int kRB = 4;
-// The forward chains' batch: the 3-byte-per-element chains (int8 codes in, two int8 code sets out) keep
-// 16 rows of 4-byte loads in flight per thread -- at 4 a CU held ~12 KiB of loads in flight and the
-// ResNet-50 c1 / c2 chains ran at ~1.1 TB/s. The ones with an fp32 operand (20 bytes a row) stay at 4: 8
-// rows cost 50+ VGPRs, i.e. half the waves, for the same bytes in flight per SIMD.
+// The forward chains' batch: 4 rows per thread by default for every chain. The 3-byte-per-element chains
+// (int8 codes in, two int8 code sets out) can take LBT_FWD_RB rows instead, a build-time option: 16 / 8
+// were measured against 4 and gained nothing -- those chains are VALU-bound, not bound by the loads in
+// flight (profiles/round5/elem_batch_ab.txt). The ones with an fp32 operand (20 bytes a row) always stay
+// at 4: 8 rows cost 50+ VGPRs, i.e. half the waves. The host guard inner * (LBT_FWD_RB + 1) follows it.
 #ifndef LBT_FWD_RB
 #define LBT_FWD_RB 4
 #endif

@@ -500,6 +500,9 @@ LBT_DEV uint32_t xcd_logical(uint32_t b, uint32_t n) {
 // A 16-byte store that is ALWAYS issued (one vector-memory op on the counter whatever `ok` is): a raw buffer
 // store at byte offset off of base (< 2^31), or at an out-of-range offset -- dropped by the buffer range
 // check -- when !ok. The persistent kernels count their epilogue stores into the ring's vmcnt waits.
+// PRECONDITION (host side): every byte the caller may store lies below 2^31 - 16; an offset past it is
+// dropped like a masked one. launch_fwdq_persist checks M * ncol < 2^31 (int8 yq), launch_dgrada_persist
+// 2 * rows * Cin < 2^31 (16-bit G); a new caller must check its own bound the same way.
 LBT_DEV void st16_always(void* base, uint32_t off, bool ok, uint4 v) {
   typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
@@ -1589,6 +1592,7 @@ bool launch_fwdq_persist(const IgArgs& p, int tstages, hipStream_t st) {
   if (stoch && !p.qout.noise) return false;
   const int ntn = p.ncol / BN;
   if (p.ncol % BN || wgs % ntn) return false;
+  if ((int64_t)p.d.N * p.d.Ho * p.d.Wo * p.ncol >= ((int64_t)1 << 31)) return false;  // st16_always bound
   const int rtiles = (p.d.N + 15) / 16 * p.npb;
   int nrg = wgs / ntn;
   if (nrg > rtiles) nrg = rtiles;
@@ -1938,6 +1942,9 @@ bool launch_dgrada_persist(const IgArgs& p, hipStream_t st) {
   if (!b.qrg.stochastic || !b.qng.stochastic || !b.qrg.noise || !b.qng.noise) return false;
   const int ntn = p.ncol / 64;
   if (p.ncol % 64 || wgs % ntn || p.cred % kBK) return false;
+  // the 16-bit G codes leave through st16_always at byte offset off * 2 of a buffer resource whose
+  // num_records is 2^31 - 1: a larger image would wrap or be dropped silently, so it takes the staged form
+  if ((int64_t)p.d.N * p.d.H * p.d.W * p.d.Cin * 2 >= ((int64_t)1 << 31)) return false;
   const int rtiles = (p.d.N + 15) / 16 * p.npb;
   int nrg = wgs / ntn;
   if (nrg > rtiles) nrg = rtiles;

@@ -13,8 +13,17 @@ Tensors use torch's logical NCHW shapes; internally they are NHWC (channels_last
 that is the layout the kernels stream. Weight decay belongs to the torch optimiser here.
 Call :func:`update_range_op` after each optimiser step (the reference's ``'update_range'``
 collection).
+
+Module reuse. A Layer_q keeps what its backward needs (input codes, BN moments, Rescale codes) on
+the layer itself, in buffers the next forward overwrites -- the reference's TF ``Layer_q`` has the
+same single-use assumption (``dynamic_fixed_point.py:97-126``). PyTorch users expect a module to be
+callable several times per graph, so each call holds a token; when a call's state is about to be
+overwritten while its autograd graph is still alive, the state is snapshotted into that call's token,
+and restored into the layer before that call's backward (in whatever order autograd runs them).
+Single-use modules never snapshot (no copies on the common path).
 """
 import itertools
+import weakref
 
 import torch
 from torch import nn
@@ -24,14 +33,79 @@ from . import layers as L
 
 _ids = itertools.count()
 
+# what each Layer_q's backward reads from its own forward (beyond parameters and quantisers,
+# which do not change within a step): X is the caller's tensor (kept by reference), the rest are
+# layer-owned buffers a later forward rewrites
+_STATE = {
+    L.Conv2d_q: ("X", "xq", "wq", "d"),
+    L.Dense_q: ("X", "xq", "wq", "d"),
+    L.Normalization_q: ("X", "q", "n", "ms"),
+    L.Rescale_q: ("X", "R", "xr"),
+}
+
 
 def update_range_op(ctx=None):
     (ctx or default_context()).update_range_op()
 
 
+class _Call:
+    """One forward call of a module: the layers' state it produced once a later call displaced it."""
+    __slots__ = ("snap", "__weakref__")
+
+    def __init__(self):
+        self.snap = None
+
+
+def _snapshot(layers):
+    out = []
+    for layer in layers:
+        s = {}
+        for a in _STATE[type(layer)]:
+            if hasattr(layer, a):
+                v = getattr(layer, a)
+                s[a] = v.clone() if (torch.is_tensor(v) and a != "X") else v
+        out.append(s)
+    return out
+
+
+def _restore(layers, snap):
+    for layer, s in zip(layers, snap):
+        for a, v in s.items():
+            cur = getattr(layer, a, None)
+            if (a != "X" and torch.is_tensor(v) and torch.is_tensor(cur) and cur.shape == v.shape
+                    and cur.dtype == v.dtype and cur.device == v.device):
+                cur.copy_(v)  # the layer's own buffer (descriptors may hold its address)
+            else:
+                setattr(layer, a, v)
+
+
+def _begin_forward(mod):
+    """Called before a forward overwrites the layers' state: a still-live earlier call keeps a copy."""
+    prev = mod._owner() if mod._owner is not None else None
+    if prev is not None and prev.snap is None:
+        prev.snap = _snapshot(mod._layers())
+    call = _Call()
+    mod._owner = weakref.ref(call)
+    return call
+
+
+def _begin_backward(mod, call):
+    """Called before a backward reads the layers' state: make it this call's."""
+    cur = mod._owner() if mod._owner is not None else None
+    if cur is call:
+        return
+    if call.snap is None:  # pragma: no cover - every displaced live call was snapshotted
+        raise RuntimeError("%s: the forward state of this call was lost" % type(mod).__name__)
+    if cur is not None and cur.snap is None:
+        cur.snap = _snapshot(mod._layers())
+    _restore(mod._layers(), call.snap)
+    mod._owner = weakref.ref(call)
+
+
 class _LayerFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, x, weight, bias, mod):
+        fctx.call = _begin_forward(mod)
         mod._load_params(weight, bias)
         y = mod.layer.forward(x.contiguous())
         fctx.mod = mod
@@ -40,12 +114,20 @@ class _LayerFn(torch.autograd.Function):
     @staticmethod
     def backward(fctx, gy):
         mod = fctx.mod
+        _begin_backward(mod, fctx.call)
         dx = mod.layer.backward(gy.contiguous(), True).clone()
         dw, db = mod._param_grads()
         return dx, dw, db, None
 
 
-class Conv2d_q(nn.Module):
+class _Reusable(nn.Module):
+    _owner = None
+
+    def _layers(self):
+        return (self.layer,)
+
+
+class Conv2d_q(_Reusable):
     def __init__(self, bits, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=False, ctx=None,
                  name=None, input_nonnegative=False):
         super().__init__()
@@ -73,7 +155,7 @@ class Conv2d_q(nn.Module):
         return y.permute(0, 3, 1, 2)
 
 
-class Linear_q(nn.Module):
+class Linear_q(_Reusable):
     def __init__(self, bits, in_features, out_features, bias=True, ctx=None, name=None):
         super().__init__()
         self.layer = L.Dense_q(name or "Linear_q_%d" % next(_ids), bits, in_features, out_features, use_bias=bias,
@@ -96,6 +178,7 @@ class Linear_q(nn.Module):
 class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, x, gamma, beta, mod):
+        fctx.call = _begin_forward(mod)
         mod.rescale.gamma.copy_(gamma.detach())
         mod.rescale.beta.copy_(beta.detach())
         y = mod.rescale.forward(mod.norm.forward(x.contiguous()))
@@ -105,12 +188,16 @@ class _BNFn(torch.autograd.Function):
     @staticmethod
     def backward(fctx, gy):
         mod = fctx.mod
+        _begin_backward(mod, fctx.call)
         g = mod.rescale.backward(gy.contiguous(), True)
         dx = mod.norm.backward(g, True).clone()
         return dx, mod.rescale.dgamma.clone(), mod.rescale.dbeta.clone(), None
 
 
-class BatchNorm2d_q(nn.Module):
+class BatchNorm2d_q(_Reusable):
+    def _layers(self):
+        return (self.norm, self.rescale)
+
     def __init__(self, bits, num_features, momentum=0.999, eps=1e-5, ctx=None, name=None):
         super().__init__()
         name = name or "BatchNorm2d_q_%d" % next(_ids)

@@ -285,22 +285,33 @@ class Trainer:
         self._warmup(sX, sy)
         self._graphs = self._capture_step(sX, sy)
 
+    def _comm_capturable(self):
+        """Capture the exchange ALONE into a throwaway graph (never replayed) once: whether this RCCL /
+        runtime supports the collective inside a HIP graph. Only this probe may fail over to the
+        host-issued exchange; any error while capturing the step itself is raised as it is."""
+        if getattr(self, "_comm_probe", None) is None:
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    self._exchange()
+                self._comm_probe = True
+            except RuntimeError:
+                import traceback
+                print("trainer: the collective cannot be captured in a HIP graph; the exchange runs from the "
+                      "host between two graphs. The capture failed with:\n" + traceback.format_exc(),
+                      file=sys.stderr)
+                self._comm_probe = False
+            del g
+            torch.cuda.synchronize()
+        return self._comm_probe
+
     def _capture_step(self, X, y):
         """(g1, g2): the step as one graph (no exchange, or captured collectives), else the forward +
-        backward and the update as two graphs with the host-issued exchange between them. A failed
-        capture of the exchange (an RCCL / runtime without graph-capture support for it) falls back to
-        the host-issued exchange, loudly, instead of ending the run (not for SyncBN plans, whose
-        statistics collectives sit inside the forward)."""
+        backward and the update as two graphs with the host-issued exchange between them. When the
+        exchange cannot be captured (``_comm_capturable``) it runs from the host, loudly (not for SyncBN
+        plans, whose statistics collectives sit inside the forward)."""
         if self.dp and self.capture_comm and not getattr(self.model, "sync_bn", False):
-            try:
-                return self._capture_step_once(X, y)
-            except RuntimeError as e:
-                msg = str(e).lower()
-                if not any(k in msg for k in ("nccl", "rccl", "collective", "capture", "not permitted", "process group")):
-                    raise  # not the collective's capture (OOM, a kernel launch error ...): no silent fallback
-                print("trainer: capturing the step's collectives failed (%s); the exchange runs from the host "
-                      "between two graphs" % str(e).splitlines()[0], file=sys.stderr)
-                torch.cuda.synchronize()
+            if not self._comm_capturable():
                 self.capture_comm = False
         return self._capture_step_once(X, y)
 

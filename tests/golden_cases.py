@@ -61,6 +61,19 @@ def digest(a):
 STEP_B = 128
 PARAM_SEED = 0
 TRAJ_STEPS = 20
+BENCH_GRAD_RANGE = -6  # bench.py --grad-range default: the timed configuration (resnet20_b128_gr6.npz)
+B16 = 16  # one rank's images in configs[2]'s 8 x 16 partition of B = 128
+
+
+def init_ranges(model, grad_range=None):
+    """Initial exponents of an oracle model: every *_range at I = 2 (the reference's defaults,
+    dynamic_fixed_point.py:225,321,541,628), the gradient quantisers at grad_range when given (the
+    layers' grad_range argument, CIFAR10_Resnet20(..., grad_range=-6) on the build side)."""
+    from oracle import resnet as R
+    r = R.init_ranges(model)
+    if grad_range is not None:
+        r = {k: (grad_range if k.endswith("grad_range") else v) for k, v in r.items()}
+    return r
 
 
 def init_params(model):

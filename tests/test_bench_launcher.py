@@ -24,7 +24,7 @@ def _run(*args, timeout=180):
     return p.returncode, lines, p.stderr
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_gpus_n_launches_n_ranks(n):
     rc, lines, err = _run("--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1")
     assert rc == 0, err[-2000:]

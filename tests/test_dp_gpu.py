@@ -1,16 +1,17 @@
 """The Trainer's data-parallel path on the MI355X (VERDICT r1 "next" 1 and 5).
 
-Two ranks are spawned as fresh processes; both use the gloo backend and share cuda:0 (a one-GPU
-rehearsal of the RCCL path: the same Trainer code -- captured graphs, lbt_step_reduce_x, the
-int64 all-reduce, lbt_step_finish, lbt_dfxp_range_update_x -- only the collective's transport
-differs). Every rank takes its half of a global batch of B = 2b images.
+Two or eight ranks are spawned as fresh processes; all use the gloo backend and share cuda:0 (a
+one-GPU rehearsal of the RCCL path: the same Trainer code -- captured graphs, lbt_step_reduce_x,
+the int64 all-reduce, lbt_step_finish, lbt_dfxp_range_update_x -- only the collective's transport
+differs). Every rank takes 16 images of a global batch of B = 16 * world images; world 8 at B = 128
+is BASELINE configs[2]'s partition of the bench batch.
 
 * per-rank BatchNorm (standard DDP, the bench's mode), graph-captured: after every step the weights,
-  the dequantised gradients and the exponents equal the ORACLE's two-shard step
+  the dequantised gradients and the exponents equal the ORACLE's world-shard step
   (oracle.resnet.dp_train_step: per-shard forward / backward with the global-batch loss, integer
   numerators and overflow counts summed, one dequantisation) BIT FOR BIT, given each rank's
   d loss / d logits (the softmax is the one op that is not bit-exact; the loss is compared at 1e-5).
-* SyncBN (FusedResNet(sync_bn=True)): the two ranks' weights, exponents and BN running statistics
+* SyncBN (FusedResNet(sync_bn=True)): every rank's weights, exponents and BN running statistics
   equal a SINGLE process training on the whole batch B bit for bit.
 """
 import os
@@ -137,38 +138,50 @@ def _flat_to_dict(m, flat_vals, offsets):
     return out
 
 
-def test_dp_two_ranks_local_bn_matches_oracle_two_shard_step():
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_ranks_local_bn_match_oracle_shard_step(world):
+    """world 2 (B = 32) and world 8 (B = 128, configs[2]'s partition: 16 images per rank of the bench's
+    batches): every rank's weights / gradients / exponents after every step equal the oracle's
+    world-shard step bit for bit."""
     from oracle import resnet as oresnet
-    B = 32
-    r0, r1 = _run_ranks(False, B)
-    for s0, s1 in zip(r0, r1):  # identical model on both ranks
-        assert np.array_equal(s0["w"], s1["w"]) and s0["ranges"] == s1["ranges"]
-        assert np.array_equal(s0["g"], s1["g"])
-    # the oracle's two-shard step, fed each rank's d loss / d logits
+    B = 16 * world
+    recs = _run_ranks(False, B, world=world)
+    for s in zip(*recs):  # identical model on every rank
+        for o in s[1:]:
+            assert np.array_equal(s[0]["w"], o["w"]) and s[0]["ranges"] == o["ranges"]
+            assert np.array_equal(s[0]["g"], o["g"])
+    # the oracle's shard step, fed each rank's d loss / d logits
     _, m, tr = _make(1, False, B)  # same seed -> same initial parameters, and the flat layout
     om = oresnet.build_resnet((3, 3, 3), 8, 2e-4)
     params = _gpu_params(m)
     state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()},
                  ranges=oresnet.init_ranges(om), step=0)
     xs, ys = _batches(B)
-    b = B // 2
+    b = B // world
     for i in range(STEPS):
-        shards = [(xs[i][r * b:(r + 1) * b].numpy(), ys[i][r * b:(r + 1) * b].numpy()) for r in range(2)]
-        loss, new_state, ctxs = oresnet.dp_train_step(om, state, shards, seed=0, dzs=[r0[i]["dz"], r1[i]["dz"]])
+        shards = [(xs[i][r * b:(r + 1) * b].numpy(), ys[i][r * b:(r + 1) * b].numpy()) for r in range(world)]
+        loss, new_state, ctxs = oresnet.dp_train_step(om, state, shards, seed=0, dzs=[rec[i]["dz"] for rec in recs])
         # each rank's dz is its rows of the global-batch softmax gradient (rtol: expf / logf)
         for r, c in enumerate(ctxs):
-            np.testing.assert_allclose((r0, r1)[r][i]["dz"], c.dz, rtol=1e-5, atol=1e-9)
-        assert abs(r0[i]["loss"] - loss) <= 1e-5 * abs(loss), (i, r0[i]["loss"], loss)
-        got_w = _flat_to_dict(m, r0[i]["w"], tr.flat.offsets)
+            np.testing.assert_allclose(recs[r][i]["dz"], c.dz, rtol=1e-5, atol=1e-9)
+        assert abs(recs[0][i]["loss"] - loss) <= 1e-5 * abs(loss), (i, recs[0][i]["loss"], loss)
+        got_w = _flat_to_dict(m, recs[0][i]["w"], tr.flat.offsets)
         for k in new_state["params"]:
             assert np.array_equal(got_w[k], new_state["params"][k]), (i, k)
-        assert r0[i]["ranges"] == new_state["ranges"], i
+        assert recs[0][i]["ranges"] == new_state["ranges"], i
         state = new_state
 
 
-def test_dp_two_ranks_syncbn_equals_single_process_batch():
-    B = 32
-    r0, r1 = _run_ranks(True, B)
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_ranks_syncbn_equal_single_process_batch(world):
+    """SyncBN over world ranks of 16 images == ONE process on the whole batch (world 8: configs[2]'s
+    8 x 16 partition of the reference's B = 128 step, trainer.py:34,144-162, with the whole-batch
+    moments of dynamic_fixed_point.py:588): weights, gradients, exponents, BN running statistics
+    bit for bit after every step, and each rank's dz rows are the single process's."""
+    B = 16 * world
+    recs = _run_ranks(True, B, world=world)
     ctx, m, tr = _make(1, False, B)
     xs, ys = _batches(B)
     xg = [x.cuda() for x in xs]
@@ -177,14 +190,13 @@ def test_dp_two_ranks_syncbn_equals_single_process_batch():
         tr.step(xg[i], yg[i])
         torch.cuda.synchronize()
         ref = _state(tr, ctx, m)
-        for s in (r0[i], r1[i]):
+        for s in (rec[i] for rec in recs):
             assert np.array_equal(s["w"], ref["w"]), i
             assert np.array_equal(s["g"], ref["g"]), i
             assert s["ranges"] == ref["ranges"], i
             for (ma, va), (mb, vb) in zip(s["bn"], ref["bn"]):
                 assert np.array_equal(ma, mb) and np.array_equal(va, vb), i
-        # each rank's dz rows are the single process's rows of the same global-batch gradient
-        assert np.array_equal(np.concatenate([r0[i]["dz"], r1[i]["dz"]]), ref["dz"]), i
+        assert np.array_equal(np.concatenate([rec[i]["dz"] for rec in recs]), ref["dz"]), i
 
 
 @pytest.mark.parametrize("sync", [False, True])

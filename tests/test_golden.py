@@ -74,3 +74,45 @@ def test_oracle_bench_step_matches_fixture(step):
     loss2, state, _ = R.train_step(model, state, xs[1], ys[1], lr=1e-2, momentum=0.9, seed=0)
     assert loss2 == float(step["traj_loss"][1])
     assert [state["ranges"][k] for k in rnames] == step["traj_ranges"][1].tolist()
+
+
+@pytest.fixture(scope="module")
+def step_gr6():
+    return np.load(os.path.join(GOLD, "resnet20_b128_gr6.npz"))
+
+
+def test_oracle_timed_config_matches_fixture(step_gr6):
+    """The timed configuration (bench.py --grad-range -6: gradient quantisers from I = -6): step 1 in
+    full, step 2's loss and exponents; and the B = 16 step 1 (one rank's share of configs[2])."""
+    f = step_gr6
+    model = R.build_resnet((3, 3, 3), 8, 2e-4)
+    params = G.init_params(model)
+    names = [str(k) for k in f["param_names"]]
+    rnames = [str(k) for k in f["range_names"]]
+    assert [G.digest(params[k]) for k in names] == [str(s) for s in f["init_params_sha"]]
+    ranges0 = G.init_ranges(model, G.BENCH_GRAD_RANGE)
+    assert [ranges0[k] for k in rnames] == f["init_ranges"].tolist()
+    assert sum(k.endswith("grad_range") for k in rnames) == int((f["init_ranges"] == -6).sum()) > 0
+    xs, ys = G.bench_batches()
+    assert [G.digest(x) for x in xs] == [str(s) for s in f["batch_x_sha"]], "bench batch generator drifted"
+    state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()}, ranges=dict(ranges0), step=0)
+    loss, state, ctx = R.train_step(model, state, xs[0], ys[0], lr=1e-2, momentum=0.9, seed=0)
+    assert np.array_equal(ctx.logits, f["step1_logits"]) and np.array_equal(ctx.dz, f["step1_dz"])
+    assert loss == float(f["step1_loss"])
+    grads = R.get_grads(model)
+    assert [G.digest(grads[k]) for k in names] == [str(s) for s in f["step1_grad_sha"]]
+    assert [G.digest(state["params"][k]) for k in names] == [str(s) for s in f["step1_params_sha"]]
+    cn = [str(k) for k in f["step1_codes_names"]]
+    assert [G.digest(ctx.record[k]) for k in cn] == [str(s) for s in f["step1_codes_sha"]]
+    assert [state["ranges"][k] for k in rnames] == f["traj_ranges"][0].tolist()
+    loss2, state, _ = R.train_step(model, state, xs[1], ys[1], lr=1e-2, momentum=0.9, seed=0)
+    assert loss2 == float(f["traj_loss"][1])
+    assert [state["ranges"][k] for k in rnames] == f["traj_ranges"][1].tolist()
+    # B = 16
+    params = G.init_params(model)
+    state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()}, ranges=dict(ranges0), step=0)
+    loss, state, ctx = R.train_step(model, state, xs[0][:G.B16], ys[0][:G.B16], lr=1e-2, momentum=0.9, seed=0)
+    assert np.array_equal(ctx.logits, f["b16_logits"]) and loss == float(f["b16_loss"])
+    grads = R.get_grads(model)
+    assert [G.digest(grads[k]) for k in names] == [str(s) for s in f["b16_grad_sha"]]
+    assert [state["ranges"][k] for k in rnames] == f["b16_ranges"].tolist()

@@ -15,6 +15,7 @@ import torch
 import golden_cases as G
 from lbt_amd._lib import OUT_F32, OUT_I8, OUT_I16, OUT_U8OFF
 from lbt_amd.dfxp import ops
+from lbt_amd.models import CIFAR10_Resnet20
 from lbt_amd.runtime import DfxpContext
 
 pytestmark = pytest.mark.gpu
@@ -28,9 +29,22 @@ def quant():
     return np.load(os.path.join(GOLD, "dfxp_quant.npz"))
 
 
-@pytest.fixture(scope="module")
-def step():
-    return np.load(os.path.join(GOLD, "resnet20_b128.npz"))
+@pytest.fixture(scope="module", params=["resnet20_b128", "resnet20_b128_gr6"])
+def step(request):
+    """The bench workload's frozen trajectory with the reference's default ranges, and in the timed
+    configuration (gradient quantisers from I = -6, bench.py --grad-range's default)."""
+    return np.load(os.path.join(GOLD, request.param + ".npz"))
+
+
+def _model(ctx, step):
+    kw = {}
+    if "init_ranges" in step.files:
+        kw["grad_range"] = G.BENCH_GRAD_RANGE
+    gm = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx, **kw)
+    if "init_ranges" in step.files:
+        r = ctx.ranges()
+        assert [r[str(k)] for k in step["range_names"]] == step["init_ranges"].tolist()
+    return gm
 
 
 @pytest.mark.parametrize("i", range(len(G.QUANT_CASES)))
@@ -104,10 +118,9 @@ def test_bench_step_matches_fixture(step, fused):
     """Step 1 of the bench workload (B=128) on the layer-wise model and on the fused plan (its separate
     forward / compute_loss / backward launches): logits bit-exact, loss / dz at 1e-5, then with the
     fixture's dz injected every gradient, the updated exponents and the BN running averages bit-exact."""
-    from lbt_amd.models import CIFAR10_Resnet20
     xs, ys = G.bench_batches()
     ctx = DfxpContext(seed=0)
-    gm = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+    gm = _model(ctx, step)
     names = _load_params(gm, step)
     m = gm
     if fused:
@@ -139,11 +152,10 @@ def test_fused_plan_20_step_trajectory_matches_fixture(step, monkeypatch):
     every step at 1e-5 -- along a trajectory whose loss runs from 2.6 to 8 000 (the reference's default
     ranges)."""
     from lbt_amd.fused import FusedResNet
-    from lbt_amd.models import CIFAR10_Resnet20
     from lbt_amd.trainer import Trainer
     xs, ys = G.bench_batches()
     ctx = DfxpContext(seed=0)
-    gm = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+    gm = _model(ctx, step)
     names = _load_params(gm, step)
     fm = FusedResNet(gm)
     cur = {"i": 0}
@@ -180,11 +192,10 @@ def test_timed_plan_trajectory_exponents_match_fixture(step):
     trajectory's; the loss at 1e-4 relative (the softmax's last-ulp differences are carried through
     the stochastic rounding of the gradient codes from step 1 on)."""
     from lbt_amd.fused import FusedResNet
-    from lbt_amd.models import CIFAR10_Resnet20
     from lbt_amd.trainer import Trainer
     xs, ys = G.bench_batches()
     ctx = DfxpContext(seed=0)
-    gm = CIFAR10_Resnet20(8, weight_decay=2e-4, ctx=ctx)
+    gm = _model(ctx, step)
     _load_params(gm, step)
     tr = Trainer(FusedResNet(gm), lr=1e-2, momentum=0.9, batch_size=G.STEP_B, use_graph=True)
     tr.init_model()
@@ -199,3 +210,34 @@ def test_timed_plan_trajectory_exponents_match_fixture(step):
         want = float(step["traj_loss"][i])
         assert abs(loss - want) <= 1e-4 * abs(want), (i, loss, want, mism)
     assert sum(mism) == 0, mism
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_b16_step_matches_fixture(fused):
+    """Step 1 at B = 16 (one rank's images of configs[2]'s 8 x 16 partition, as a batch of its own) in
+    the timed configuration, on the batch-adaptive geometry (4-row stage-1 tiles, doubled weight-
+    gradient splits, the 4-way head split): logits bit-exact, loss / dz at 1e-5, then with the
+    fixture's dz injected every gradient, the updated weights and exponents bit-exact."""
+    step = np.load(os.path.join(GOLD, "resnet20_b128_gr6.npz"))
+    xs, ys = G.bench_batches()
+    ctx = DfxpContext(seed=0)
+    gm = _model(ctx, step)
+    names = _load_params(gm, step)
+    m = gm
+    if fused:
+        from lbt_amd.fused import FusedResNet
+        m = FusedResNet(gm)
+    x = torch.from_numpy(xs[0][:G.B16]).to(DEV)
+    y = torch.from_numpy(ys[0][:G.B16]).to(torch.int32).to(DEV)
+    assert np.array_equal(m.forward(x).cpu().numpy(), step["b16_logits"])
+    loss = m.compute_loss(y).item()
+    assert abs(loss - float(step["b16_loss"])) <= 1e-5 * abs(float(step["b16_loss"]))
+    np.testing.assert_allclose(m.dlogits.cpu().numpy(), step["b16_dz"], rtol=1e-5, atol=1e-9)
+    m.dlogits.copy_(torch.from_numpy(step["b16_dz"]).to(DEV))
+    m.backward()
+    torch.cuda.synchronize()
+    g = _grads(gm)
+    assert [G.digest(g[k]) for k in names] == [str(s) for s in step["b16_grad_sha"]]
+    ctx.update_range_op()
+    r = ctx.ranges()
+    assert [r[str(k)] for k in step["range_names"]] == step["b16_ranges"].tolist()

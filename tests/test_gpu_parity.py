@@ -547,6 +547,61 @@ def test_torch_face_conv_matches_layer():
     assert np.array_equal(m.weight.grad.permute(2, 3, 1, 0).cpu().numpy(), ref.dW)
 
 
+@pytest.mark.parametrize("shape", ["chain", "parallel"])
+def test_torch_face_module_reuse_matches_oracle(shape):
+    """One Conv2d_q called twice in a forward: chain ``conv(relu(conv(x)))`` or
+    parallel ``conv(x1) + conv(x2)``. Each call's backward must read its own input codes although the
+    second forward rewrote the layer's buffers (modules.py snapshots a displaced call's state). The
+    oracle side is two Conv2dQ instances with the same name (same quantiser noise key) and weights;
+    the outputs, the input gradients and the summed weight gradient are bit-identical. (The range
+    update is not compared: the oracle keeps the last call's overflow counts per range name, the
+    device adds every call's.)"""
+    import torch.nn.functional as F
+    from lbt_amd.dfxp import Conv2d_q
+    ctx = DfxpContext(seed=9)
+    m = Conv2d_q(8, 16, 16, kernel_size=3, stride=1, padding=1, bias=False, ctx=ctx, name="tr",
+                 input_nonnegative=True)
+    W = m.weight.detach().permute(2, 3, 1, 0).cpu().numpy().copy()
+    refs = []
+    for _ in range(2):
+        o = onn.Conv2dQ("tr", 8, [3, 3, 16, 16], [1, 1, 1, 1], "SAME", 0.0)
+        o.W = W.copy()
+        refs.append(o)
+    rng = np.random.default_rng(9)
+    x1 = rng.uniform(0, 2, size=(4, 16, 10, 10)).astype(np.float32)
+    x2 = rng.uniform(0, 1, size=(4, 16, 10, 10)).astype(np.float32)
+    g = rng.normal(0, 0.05, size=(4, 16, 10, 10)).astype(np.float32)
+    nhwc = lambda a: a.transpose(0, 2, 3, 1).copy()  # noqa: E731
+    octx = onn.Ctx({r: 2 for r in refs[0].range_names()}, 0, 9)
+    t1 = torch.from_numpy(x1).to(DEV).requires_grad_(True)
+    if shape == "chain":
+        h = m(t1)
+        y = m(F.relu(h))
+        y.backward(torch.from_numpy(g).to(DEV))
+        zr = refs[0].forward(nhwc(x1), octx)
+        ar = np.maximum(zr, 0).astype(np.float32)
+        yr = refs[1].forward(ar, octx)
+        gh = refs[1].backward(nhwc(g), octx)
+        gh = np.where(zr > 0, gh, 0).astype(np.float32)
+        dx1 = refs[0].backward(gh, octx)
+        grads = [(t1, dx1)]
+    else:
+        t2 = torch.from_numpy(x2).to(DEV).requires_grad_(True)
+        y = m(t1) + m(t2)
+        y.backward(torch.from_numpy(g).to(DEV))
+        ya = refs[0].forward(nhwc(x1), octx)
+        yb = refs[1].forward(nhwc(x2), octx)
+        yr = (ya + yb).astype(np.float32)
+        dxb = refs[1].backward(nhwc(g), octx)
+        dxa = refs[0].backward(nhwc(g), octx)
+        grads = [(t1, dxa), (t2, dxb)]
+    assert np.array_equal(y.detach().permute(0, 2, 3, 1).cpu().numpy(), yr)
+    for t, ref in grads:
+        assert np.array_equal(t.grad.permute(0, 2, 3, 1).cpu().numpy(), ref)
+    dw = (refs[0].dW + refs[1].dW).astype(np.float32)
+    assert np.array_equal(m.weight.grad.permute(2, 3, 1, 0).cpu().numpy(), dw)
+
+
 def test_torch_face_custom_py_network_matches_oracle():
     """custom.py's own network (custom.py:10-12,15-50) on the torch face: conv5x5(1 -> 6, padding=1) ->
     ReLU -> MaxPool2d(2) -> conv5x5(6 -> 16) -> ReLU -> MaxPool2d(2) -> conv5x5(16 -> 120) -> ReLU ->

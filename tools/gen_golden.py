@@ -1,12 +1,14 @@
 """Freeze the oracle: write tests/golden/dfxp_quant.npz and tests/golden/resnet20_b128.npz.
 
-    python tools/gen_golden.py            (about a minute on 8 cores)
+    python tools/gen_golden.py [quant] [b128] [gr6]     (about a minute each on 8 cores)
 
 Test infrastructure. The reference (TensorFlow 1.x) cannot run here
 and holds no fixtures, so these are the oracle's outputs frozen at a reviewed commit: the quantiser
 codes / overflow counters / range updates of every ResNet-20 tensor class (dynamic_fixed_point.py:4-94),
 and one full B=128 ResNet-20 step plus a 20-step trajectory of the bench workload (models.py:7-54,
-371-455, trainer.py:79-84,144-162). tests/test_golden.py pins the oracle to them on the CPU;
+371-455, trainer.py:79-84,144-162), once with the reference's default ranges and once in the timed
+configuration (gradient quantisers from I = -6, bench.py --grad-range; plus a B = 16 step 1).
+tests/test_golden.py pins the oracle to them on the CPU;
 tests/test_gpu_golden.py checks the HIP path against them directly on the MI355X.
 """
 import os
@@ -47,7 +49,9 @@ def bn_state(model):
     return [(l.mean_running.copy(), l.var_running.copy()) for l in R._walk(model) if isinstance(l, onn.NormQ)]
 
 
-def step_fixtures():
+def step_fixtures(grad_range=None):
+    """grad_range None: the reference's default ranges (every *_range at I = 2); an int: the gradient
+    quantisers start there (bench.py's timed configuration: --grad-range -6, G.init_ranges)."""
     model = R.build_resnet((3, 3, 3), 8, 2e-4)
     params = G.init_params(model)
     names = sorted(params)
@@ -56,8 +60,12 @@ def step_fixtures():
     out = {"param_names": np.array(names), "range_names": np.array(rnames),
            "init_params_sha": np.array([G.digest(params[k]) for k in names]),
            "batch_x_sha": np.array([G.digest(x) for x in xs]), "batch_y_sha": np.array([G.digest(y) for y in ys])}
+    ranges0 = G.init_ranges(model, grad_range)
+    out["init_ranges"] = np.array([ranges0[k] for k in rnames], np.int32)
+    if grad_range is not None:
+        out.update(b16_fixtures(model, names, rnames, ranges0, xs, ys))
     state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()},
-                 ranges=R.init_ranges(model), step=0)
+                 ranges=dict(ranges0), step=0)
     losses, ranges, dzs = [], [], []
     for i in range(G.TRAJ_STEPS):
         loss, state, ctx = R.train_step(model, state, xs[i % 4], ys[i % 4], lr=1e-2, momentum=0.9, seed=0)
@@ -85,10 +93,31 @@ def step_fixtures():
     return out
 
 
+def b16_fixtures(model, names, rnames, ranges0, xs, ys):
+    """Step 1 on the first G.B16 images of the first bench batch (one rank's share of configs[2]'s
+    8 x 16 partition, run as its own batch): logits, loss, dz, every gradient, the new exponents."""
+    params = G.init_params(model)
+    state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()}, ranges=dict(ranges0),
+                 step=0)
+    loss, state, ctx = R.train_step(model, state, xs[0][:G.B16], ys[0][:G.B16], lr=1e-2, momentum=0.9, seed=0)
+    grads = R.get_grads(model)
+    print("b16 step 1 loss %.6f" % loss, flush=True)
+    return {"b16_logits": ctx.logits.astype(np.float32), "b16_dz": ctx.dz.astype(np.float32),
+            "b16_loss": np.array(loss, np.float64),
+            "b16_grad_sha": np.array([G.digest(grads[k]) for k in names]),
+            "b16_params_sha": np.array([G.digest(state["params"][k]) for k in names]),
+            "b16_ranges": np.array([state["ranges"][k] for k in rnames], np.int32)}
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    np.savez_compressed(os.path.join(OUT, "dfxp_quant.npz"), **quant_fixtures())
-    np.savez_compressed(os.path.join(OUT, "resnet20_b128.npz"), **step_fixtures())
+    which = sys.argv[1:] or ["quant", "b128", "gr6"]
+    if "quant" in which:
+        np.savez_compressed(os.path.join(OUT, "dfxp_quant.npz"), **quant_fixtures())
+    if "b128" in which:
+        np.savez_compressed(os.path.join(OUT, "resnet20_b128.npz"), **step_fixtures())
+    if "gr6" in which:  # the timed configuration (bench.py --grad-range -6, its default)
+        np.savez_compressed(os.path.join(OUT, "resnet20_b128_gr6.npz"), **step_fixtures(G.BENCH_GRAD_RANGE))
 
 
 if __name__ == "__main__":
