@@ -105,10 +105,13 @@ def test_oracle_timed_config_matches_fixture(step_gr6):
     cn = [str(k) for k in f["step1_codes_names"]]
     assert [G.digest(ctx.record[k]) for k in cn] == [str(s) for s in f["step1_codes_sha"]]
     assert [state["ranges"][k] for k in rnames] == f["traj_ranges"][0].tolist()
+    bn = [G.digest(np.concatenate([l.mean_running, l.var_running])) for l in R._walk(model) if isinstance(l, onn.NormQ)]
+    assert bn == [str(s) for s in f["step1_bn_sha"]]
     loss2, state, _ = R.train_step(model, state, xs[1], ys[1], lr=1e-2, momentum=0.9, seed=0)
     assert loss2 == float(f["traj_loss"][1])
     assert [state["ranges"][k] for k in rnames] == f["traj_ranges"][1].tolist()
-    # B = 16
+    # B = 16, a fresh model (its own BN running averages)
+    model = R.build_resnet((3, 3, 3), 8, 2e-4)
     params = G.init_params(model)
     state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()}, ranges=dict(ranges0), step=0)
     loss, state, ctx = R.train_step(model, state, xs[0][:G.B16], ys[0][:G.B16], lr=1e-2, momentum=0.9, seed=0)

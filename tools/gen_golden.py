@@ -96,6 +96,7 @@ def step_fixtures(grad_range=None):
 def b16_fixtures(model, names, rnames, ranges0, xs, ys):
     """Step 1 on the first G.B16 images of the first bench batch (one rank's share of configs[2]'s
     8 x 16 partition, run as its own batch): logits, loss, dz, every gradient, the new exponents."""
+    model = R.build_resnet((3, 3, 3), 8, 2e-4)  # its own BN running averages
     params = G.init_params(model)
     state = dict(params=params, accum={k: np.zeros_like(v) for k, v in params.items()}, ranges=dict(ranges0),
                  step=0)
