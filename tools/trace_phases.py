@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--max", type=int, default=40)
     ap.add_argument("--lib", default=None, help="another -DLBT_TRACE build (tools/build_variant.py)")
+    ap.add_argument("--cold", action="store_true",
+                    help="write 512 MB inside the replayed graph before the launch, so its loads miss L2 and the "
+                         "256 MB last-level cache as they do in the step (isolated replays re-read warm caches)")
     a = ap.parse_args()
     if a.build:
         return build()
@@ -77,12 +80,15 @@ def main():
     from lbt_amd.roofline import graph_launches
     launches = [f for f in graph_launches(model) if a.filter in getattr(f, "kname", "")]
     side = torch.cuda.Stream(device=dev)
+    flush = torch.empty(1 << 27, dtype=torch.float32, device=dev) if a.cold else None
     for idx, f in enumerate(launches[:a.max]):
         # the launch replayed from a graph (as in the timed step), twice: the second one is traced
         g = torch.cuda.CUDAGraph()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             with torch.cuda.graph(g, stream=side):
+                if flush is not None:
+                    flush.fill_(float(idx))
                 f()
         torch.cuda.current_stream().wait_stream(side)
         g.replay()
