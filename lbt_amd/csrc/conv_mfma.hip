@@ -85,7 +85,7 @@ __device__ __forceinline__ void conv_gemm_body(const GemmArgs& p, uint32_t bid, 
   __shared__ ChainShared<NT, (CF ? NB : 1)> csh;
   ChainPre<NT, NB, CF> cp;
   LBT_TS(0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int mt_local = wave / WPM;
   const int nt0 = (wave % WPM) * NTW;
   const int64_t mtile = (int64_t)bid * MTB + mt_local;
@@ -350,7 +350,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bi
   auto& lds = sm.lds;
   auto& red = sm.red;
   LBT_TS(0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int r = lane & 15, kg = lane >> 4;
   // XCD-aware unit order: workgroups are dealt round-robin over the 8 XCDs, so unit u of the
   // split-major order (split, tap, co-slice) goes to linear block (u % chunk) * 8 + u / chunk:
@@ -374,42 +374,75 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& wa, uint32_t bi
 #pragma unroll
   for (int a = 0; a < CSI; ++a) acc[a] = v4i{0, 0, 0, 0};
 
-  // chunks are interleaved across the NW waves of the block
-  for (int64_t c0 = p0 + (int64_t)wave * kWP; c0 < p1; c0 += NW * kWP) {
+  // chunks are interleaved across the NW waves of the block, two in flight per wave: chunk k + 2's
+  // loads are issued while chunk k is computed. Every load is unconditional (a chunk past the end has
+  // no valid pixel: clamped addresses, zero gradient), so the compiler's vmcnt waits count exactly the
+  // loads issued since instead of waiting for all of them (each chunk then paid a memory round trip:
+  // the strided jobs' 32 chunks per wave took ~23 us of the batched launch, profiles/round6/budget)
+  struct Chunk {
+    v4i xs[CSI], g;
+    bool xv, pv;
+  };
+  // whole-row chunks (the ResNet shapes: 64-pixel chunks of whole output rows of one image, aligned
+  // splits): the lane's row / column within a chunk are chunk-invariant and the chunk's image and first
+  // row wave-uniform -- no per-lane divisions per chunk
+  const bool rows64 = 64 % d.Wo == 0 && HWo % 64 == 0 && per % 64 == 0 && p0 % 64 == 0;
+  const int lrow = rows64 ? lane / d.Wo : 0, lcol = rows64 ? lane - lrow * d.Wo : 0;
+  auto fetch = [&](int64_t c0, Chunk& b) {
     const int64_t p = c0 + lane;
     const bool pv = p < p1;
     const uint32_t pu = (uint32_t)(pv ? p : p0);  // P < 2^31 (launcher)
-    const uint32_t n = pu / HWo, rem = pu - n * HWo;
-    const int oh = (int)(rem / (uint32_t)d.Wo), ow = (int)(rem - (uint32_t)oh * (uint32_t)d.Wo);
+    uint32_t n;
+    int oh, ow;
+    if (rows64) {  // wave-uniform branch
+      const uint32_t cu = (uint32_t)(c0 < p1 ? c0 : p0);
+      n = cu / HWo;
+      oh = (int)((cu - n * HWo) / (uint32_t)d.Wo) + lrow;
+      ow = lcol;
+    } else {
+      n = pu / HWo;
+      const uint32_t rem = pu - n * HWo;
+      oh = (int)(rem / (uint32_t)d.Wo);
+      ow = (int)(rem - (uint32_t)oh * (uint32_t)d.Wo);
+    }
     const int ih = oh * d.SH + kh - d.PT, iw = ow * d.SW + kw - d.PL;
     const bool xv = pv && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
     // all loads first (clamped addresses, no branches), fills selected afterwards
     const int8_t* xp = xq + (xv ? ((((int64_t)n * d.H + ih) * d.W + iw) * CI) : 0);
-    v4i xs[CSI];
 #pragma unroll
-    for (int cs = 0; cs < CSI; ++cs) xs[cs] = *reinterpret_cast<const v4i*>(xp + cs * 16);
-    v4i g = *reinterpret_cast<const v4i*>(gq + (int64_t)pu * d.Cout + cso * 16);
-    const int xf = pv ? x_fill : 0;
+    for (int cs = 0; cs < CSI; ++cs) b.xs[cs] = *reinterpret_cast<const v4i*>(xp + cs * 16);
+    b.g = *reinterpret_cast<const v4i*>(gq + (int64_t)pu * d.Cout + cso * 16);
+    b.xv = xv;
+    b.pv = pv;
+  };
+  auto consume = [&](Chunk& b, int64_t cnext) {
+    const int xf = b.pv ? x_fill : 0;
 #pragma unroll
-    for (int cs = 0; cs < CSI; ++cs) {
-      if (!xv) xs[cs] = v4i{xf, xf, xf, xf};
-      *reinterpret_cast<v4i*>(Xi + (cs * kWP + lane) * 16) = xs[cs];
-    }
-    if (!pv) g = v4i{0, 0, 0, 0};
-    *reinterpret_cast<v4i*>(Gi + lane * 16) = g;
-    // the images are read by other lanes of the same wave only
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int cs = 0; cs < CSI; ++cs)
+      *reinterpret_cast<v4i*>(Xi + (cs * kWP + lane) * 16) = b.xv ? b.xs[cs] : v4i{xf, xf, xf, xf};
+    *reinterpret_cast<v4i*>(Gi + lane * 16) = b.pv ? b.g : v4i{0, 0, 0, 0};
+    // the images are read by other lanes of the same wave only: a wave's LDS instructions execute in
+    // issue order, so only the compiler must keep the reads after the writes
+    asm volatile("" ::: "memory");
+    fetch(cnext, b);
     const v4i bfrag = tr_frag(Gi, 16 * kg, lane);
 #pragma unroll
     for (int a = 0; a < CSI; ++a) {
       const v4i afrag = tr_frag(Xi + a * kWP * 16, 16 * kg, lane);
       acc[a] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag, bfrag, acc[a], 0, 0, 0);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    asm volatile("" ::: "memory");  // the next chunk's stores after these reads (in-order LDS)
+  };
+  const int64_t cw = p0 + (int64_t)wave * kWP, cstep = (int64_t)NW * kWP;
+  const int64_t nch = p1 > cw ? (p1 - cw + cstep - 1) / cstep : 0;  // this wave's chunks
+  if (nch > 0) {
+    Chunk b0, b1;
+    fetch(cw, b0);
+    fetch(cw + cstep, b1);
+    for (int64_t k = 0; k < nch; k += 2) {
+      consume(b0, cw + (k + 2) * cstep);
+      consume(b1, cw + (k + 3) * cstep);
+    }
   }
   LBT_TS(1);
   // acc[a] element i: row = a*16 + 4*kg + i (ci), col = r (co within the slice)
@@ -877,7 +910,7 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
   if (u >= total) return;
   const int split = u / (ncs * ncos), urem = u - split * (ncs * ncos);
   const int cis = urem / ncos, cos = urem - cis * ncos;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int j = lane & 15, kg = lane >> 4;
   const int RB = 64 / W, Wp = W + 2, nhalo = (RB + 2) * Wp;
   const int64_t cps = (int64_t)d.N * H * W / 64 / nsplit;  // chunks per split (exact: host check)
@@ -892,6 +925,22 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
   const int oxa = ((pa / W) * Wp + pa % W) * 16 + 8 * (j & 1);
   const int oxb = ((pb / W) * Wp + pb % W) * 16 + 8 * (j & 1);
   const int oga = pa * 16 + 8 * (j & 1), ogb = pb * 16 + 8 * (j & 1);
+  // chunk-invariant geometry of this lane's halo slices t = lane + 64 i of the [RB + 2][W + 2] window:
+  // the offset from the chunk's first pixel, whether it is a real column inside the window, whether it
+  // lies in the window's top / bottom row (outside the image at the first / last row block). The
+  // per-chunk part is then wave-uniform (scalar): the per-lane divisions by W + 2 of every chunk were
+  // most of the loop's VALU instructions
+  int hoff[kHaloMax];
+  uint32_t hin = 0, htop = 0, hbot = 0;
+#pragma unroll
+  for (int i = 0; i < kHaloMax; ++i) {
+    const int t = lane + 64 * i;
+    const int hy = t / Wp, hx = t - hy * Wp;
+    hoff[i] = ((hy - 1) * W + hx - 1) * Cin;
+    hin |= (uint32_t)(t < nhalo && hx >= 1 && hx <= W) << i;
+    htop |= (uint32_t)(hy == 0) << i;
+    hbot |= (uint32_t)(hy == RB + 1) << i;
+  }
 
   // two register buffers: chunk s + 2's loads are issued while chunk s is computed (s + 1's are
   // already in flight), so a wave waits on a load issued two chunks earlier
@@ -900,25 +949,25 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
     uint32_t valid;
   };
   auto load = [&](Buf& b, int64_t c) {
-    const int64_t p0 = c * 64;
+    const int64_t p0 = c * 64;  // wave-uniform: the chunk's first pixel, RB whole rows of image n
     const int n = (int)(p0 / HW), row0 = (int)(p0 - (int64_t)n * HW) / W;
-    const int8_t* xim = wa.xq + (int64_t)n * HW * Cin + cis * 16;
-    b.valid = 0;
+    const int8_t* xim = wa.xq + (p0 * Cin + cis * 16);  // = pixel (n, row0, 0)
+    b.valid = hin & ~(row0 == 0 ? htop : 0u) & ~(row0 + RB == H ? hbot : 0u);
 #pragma unroll
-    for (int i = 0; i < kHaloMax; ++i) {
-      const int t = lane + 64 * i;
-      const int hy = t / Wp, hx = t - hy * Wp;
-      const int y = row0 - 1 + hy, x = hx - 1;
-      const bool v = t < nhalo && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-      b.valid |= (uint32_t)v << i;
-      b.x[i] = *reinterpret_cast<const v4i*>(xim + (v ? (int64_t)(y * W + x) * Cin : 0));
-    }
+    for (int i = 0; i < kHaloMax; ++i)
+      b.x[i] = *reinterpret_cast<const v4i*>(xim + ((b.valid >> i) & 1 ? hoff[i] : 0));
     b.g = *reinterpret_cast<const v4i*>(wa.gq + (p0 + lane) * Cout + cos * 16);
   };
   v4i acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = v4i{0, 0, 0, 0};
-  // chunk s of this wave: stage b into LDS, refill b with chunk s + 2, MFMAs of all 9 taps
+  // this wave's chunk s, clamped to its last one: the refills past the end reload it and every load
+  // is UNCONDITIONAL, so the compiler's vmcnt waits count exactly the loads issued since (a load
+  // under a branch made it wait for vmcnt(0) -- every chunk then paid a whole memory round trip:
+  // 8 chunks ~ 12 us per stage-1 job, tools/trace_phases.py, profiles/round6/budget)
+  auto cidx = [&](int s) { return c0 + wave + (int64_t)(s < nmine ? s : nmine - 1) * kFW; };
+  // chunk s of this wave: stage b into LDS, refill b with chunk s + kWgmBufs, MFMAs of all 9 taps
+  // (a step past the end, s >= nmine, adds a zero gradient fragment)
   auto step = [&](Buf& b, int s) {
 #pragma unroll
     for (int i = 0; i < kHaloMax; ++i) {
@@ -926,12 +975,12 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
       const v4i v = (b.valid >> i) & 1 ? b.x[i] : v4i{fill, fill, fill, fill};
       if (t < nhalo) *reinterpret_cast<v4i*>(st + t * 16) = v;
     }
-    *reinterpret_cast<v4i*>(gs + lane * 16) = b.g;
-    // the images are read by other lanes of the same wave only
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (s + kWgmBufs < nmine) load(b, c0 + wave + (int64_t)(s + kWgmBufs) * kFW);
+    *reinterpret_cast<v4i*>(gs + lane * 16) = s < nmine ? b.g : v4i{0, 0, 0, 0};
+    // the images are read by other lanes of the same wave only: a wave's LDS instructions execute in
+    // issue order, so only the compiler must keep the reads after the writes (no fence: a workgroup
+    // release fence would also wait for the refills in flight)
+    asm volatile("" ::: "memory");
+    load(b, cidx(s + kWgmBufs));
     const v4i bfrag = tr_frag_at(gs, oga, ogb);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -939,23 +988,23 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
       const v4i afrag = tr_frag_at(st, oxa + toff, oxb + toff);
       acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag, bfrag, acc[t], 0, 0, 0);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    asm volatile("" ::: "memory");  // the next chunk's stores after these reads (in-order LDS)
   };
   LBT_TS(0);
-  if constexpr (kWgmBufs == 2) {
-    Buf b0, b1;
-    if (nmine > 0) load(b0, c0 + wave);
-    if (nmine > 1) load(b1, c0 + wave + kFW);
-    for (int s = 0; s < nmine; s += 2) {
-      step(b0, s);
-      if (s + 1 < nmine) step(b1, s + 1);
+  if (nmine > 0) {
+    if constexpr (kWgmBufs == 2) {
+      Buf b0, b1;
+      load(b0, cidx(0));
+      load(b1, cidx(1));
+      for (int s = 0; s < nmine; s += 2) {
+        step(b0, s);
+        step(b1, s + 1);
+      }
+    } else {  // one register buffer: chunk s + 1's loads in flight during chunk s's MFMAs
+      Buf b0;
+      load(b0, cidx(0));
+      for (int s = 0; s < nmine; ++s) step(b0, s);
     }
-  } else {  // one register buffer: chunk s + 1's loads in flight during chunk s's MFMAs
-    Buf b0;
-    if (nmine > 0) load(b0, c0 + wave);
-    for (int s = 0; s < nmine; ++s) step(b0, s);
   }
   LBT_TS(1);
   __syncthreads();  // the partials overwrite the staging regions
@@ -1179,6 +1228,9 @@ namespace {
 #else
 #define LBT_TSS(i) do { } while (0)
 #define LBT_TSB(i) LBT_TS(i)
+#endif
+#ifndef LBT_EARLY3
+#define LBT_EARLY3 1
 #endif
 constexpr int kBNW = 8;    // waves per workgroup
 constexpr int kBThreads = kBNW * 64;
@@ -1412,6 +1464,8 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   constexpr int WC = WCS ? WCS : 1;
   constexpr int kBIt = halo_iters(CS, TH), J = TH / 4;  // J: phase-3 groups per thread
+  // phase-3 groups whose operands load with phase 1's (VGPR budget: 128 at CS < 4)
+  constexpr int JE = LBT_EARLY3 ? (CS == 4 || J == 1 ? J : 1) : 0;
   static_assert(TH % 4 == 0, "a tile is whole groups of 4 rows (8 MFMA pairs, one per wave)");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   union Smem {
@@ -1432,7 +1486,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   const int H = p.H;
   const int tpi = H / TH;
   const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * TH;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4;  // this thread's channel quad (512 % C4 == 0: fixed over its groups)
   const int64_t img = (int64_t)n * H * W * C;
@@ -1473,6 +1527,27 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   // the phase-2 B operands (the dgrad weight image, ks == 4 * kMaxKS: host check), for LDS (WImg)
   v4i wimg[WI::kIt];
   WI::load(p.wd, wimg);
+  // phase-3 operands (addend, mask source, R / qn codes and both quantisers' noise per branch): the
+  // first JE groups issued in this first load wave too, so their latency is off the critical path
+  // (the stage-3 workgroup's whole chain, J = 1); the others after phase 1, where its registers are free
+  float4 av[J], ymv[J], urg[NB][J], ung[NB][J];
+  int Rv[NB][J], qnv[NB][J];
+  auto load3 = [&](int j) {
+    const int pix = (tid + j * kBThreads) / C4;
+    const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);  // tile rows are consecutive pixels
+    av[j] = p.add_src ? ld4f(p.add_src, img + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (CF & kAYMask) ymv[j] = ld4f(A.y_mask, img + off);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+      Rv[b][j] = ld4i8(Bb.R, img + off);
+      qnv[b][j] = ld4i8(Bb.qn_codes, img + off);
+      urg[b][j] = ld4f(Bb.qrg.noise, off);
+      ung[b][j] = ld4f(Bb.qng.noise, off);
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < JE; ++j) load3(j);
   float mu[4], sg[4], gam[2][4], bet[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -1482,15 +1557,25 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     for (int b = 0; b < NB; ++b) gam[b][k] = (b == 0 ? A.b1 : A.b2).gb[cq + k];
     bet[k] = A.b1.gb[C + cq + k];
   }
-  const QState sgq = qstate(B.qng), sn = qstate(B.qn), so = qstate(B.qo);
+  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
+  const int I_gq = qexp_load(B.qng), I_n = qexp_load(B.qn), I_o = qexp_load(B.qo), I_w = qexp_load(p.qw);
+  int I_rg[2], I_ng[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    I_rg[b] = qexp_load((b == 0 ? A.b1 : A.b2).qrg);
+    I_ng[b] = qexp_load((b == 0 ? A.b1 : A.b2).qng);
+  }
+  const int I_r = (CF & kAMaskR) ? qexp_load(A.b1.qr) : 0;
+  LBT_ISSUE_FENCE();
+  const QState sgq = qstate_from(B.qng, I_gq), sn = qstate_from(B.qn, I_n), so = qstate_from(B.qo, I_o);
   QState qrg[2], qng[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    qrg[b] = qstate((b == 0 ? A.b1 : A.b2).qrg);
-    qng[b] = qstate((b == 0 ? A.b1 : A.b2).qng);
+    qrg[b] = qstate_from((b == 0 ? A.b1 : A.b2).qrg, I_rg[b]);
+    qng[b] = qstate_from((b == 0 ? A.b1 : A.b2).qng, I_ng[b]);
   }
-  const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
-  const float scale = ldexpf(1.0f, -(frac_exp(B.qo) + frac_exp(p.qw)));
+  const float r_inv = (CF & kAMaskR) ? qstate_from(A.b1.qr, I_r).inv_m : 0.f;
+  const float scale = ldexpf(1.0f, -(frac_exp_from(B.qo, I_o) + frac_exp_from(p.qw, I_w)));
   LBT_TSS(2);  // every other load issued, the descriptors read
 
   // ---------------- pass-B statistics: the shard sums (loaded first, above) added per lane, then over
@@ -1582,25 +1667,9 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   __syncthreads();
   LBT_TSB(2);
 
-  // phase-3 operands (addend, mask source, R / qn codes and both quantisers' noise per branch),
-  // issued now: they land while the MFMAs run, and phase 1's registers are free
-  float4 av[J], ymv[J], urg[NB][J], ung[NB][J];
-  int Rv[NB][J], qnv[NB][J];
+  // the rest of the phase-3 operands, issued now: they land while the MFMAs run
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int pix = (tid + j * kBThreads) / C4;
-    const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);  // tile rows are consecutive pixels
-    av[j] = p.add_src ? ld4f(p.add_src, img + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (CF & kAYMask) ymv[j] = ld4f(A.y_mask, img + off);
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
-      Rv[b][j] = ld4i8(Bb.R, img + off);
-      qnv[b][j] = ld4i8(Bb.qn_codes, img + off);
-      urg[b][j] = ld4f(Bb.qrg.noise, off);
-      ung[b][j] = ld4f(Bb.qng.noise, off);
-    }
-  }
+  for (int j = JE; j < J; ++j) load3(j);
 
   // ---------------- phase 2: dgrad from the LDS image, two (m-tile, n-tile) pairs per wave
 #pragma unroll
@@ -1894,7 +1963,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
   const int H = p.H, Hq = H / 2;
   const int tpi = H / TH;
   const int n = (int)(bid / (uint32_t)tpi), r0 = (int)(bid - (uint32_t)n * tpi) * TH, q0 = r0 / 2;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4;     // dx channel quad (phase 3)
   const int cqq = (tid % Cq4) * 4;   // low-res channel quad (phase 1)
@@ -1955,16 +2024,30 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
     for (int b = 0; b < NB; ++b) gam[b][k] = (b == 0 ? A.b1 : A.b2).gb[cq + k];
     bet[k] = A.b1.gb[C + cq + k];
   }
-  const QState so1 = qstate(p.b1.qo), sos = qstate(p.bs.qo);
+  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
+  const int I_o1 = qexp_load(p.b1.qo), I_os = qexp_load(p.bs.qo), I_w1 = qexp_load(p.qw1), I_ws = qexp_load(p.qws);
+  const int I_n1 = qexp_load(p.b1.qn), I_ns = qexp_load(p.bs.qn), I_g1 = qexp_load(p.b1.qng),
+            I_gs = qexp_load(p.bs.qng);
+  int I_rg[2], I_ng[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    I_rg[b] = qexp_load((b == 0 ? A.b1 : A.b2).qrg);
+    I_ng[b] = qexp_load((b == 0 ? A.b1 : A.b2).qng);
+  }
+  const int I_r = (CF & kAMaskR) ? qexp_load(A.b1.qr) : 0;
+  LBT_ISSUE_FENCE();
+  const QState so1 = qstate_from(p.b1.qo, I_o1), sos = qstate_from(p.bs.qo, I_os);
   QState qrg[2], qng[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    qrg[b] = qstate((b == 0 ? A.b1 : A.b2).qrg);
-    qng[b] = qstate((b == 0 ? A.b1 : A.b2).qng);
+    qrg[b] = qstate_from((b == 0 ? A.b1 : A.b2).qrg, I_rg[b]);
+    qng[b] = qstate_from((b == 0 ? A.b1 : A.b2).qng, I_ng[b]);
   }
-  const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
-  const float scale1 = ldexpf(1.0f, -(frac_exp(p.b1.qo) + frac_exp(p.qw1)));
-  const float scale2 = ldexpf(1.0f, -(frac_exp(p.bs.qo) + frac_exp(p.qws)));
+  const float r_inv = (CF & kAMaskR) ? qstate_from(A.b1.qr, I_r).inv_m : 0.f;
+  const float scale1 = ldexpf(1.0f, -(frac_exp_from(p.b1.qo, I_o1) + frac_exp_from(p.qw1, I_w1)));
+  const float scale2 = ldexpf(1.0f, -(frac_exp_from(p.bs.qo, I_os) + frac_exp_from(p.qws, I_ws)));
+  const QState sn1 = qstate_from(p.b1.qn, I_n1), sns = qstate_from(p.bs.qn, I_ns), sg1 = qstate_from(p.b1.qng, I_g1),
+               sgs = qstate_from(p.bs.qng, I_gs);
 
   // ---------------- pass-B constants of both BNs (chain_bwd_b_kernel's double arithmetic)
   if (wave < kSW) {
@@ -1979,7 +2062,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
     const int bn = wave < CSq ? 0 : 1, c = (wave % CSq) * 16 + (lane & 15);
     if (lane < 16) {
       const lbt_chain_bwd_b& Bb = bn == 0 ? p.b1 : p.bs;
-      const double s = (double)qstate(Bb.qn).inv_m, gsc = (double)qstate(Bb.qng).inv_m, nn = (double)Bb.n;
+      const double s = (double)(bn == 0 ? sn1 : sns).inv_m, gsc = (double)(bn == 0 ? sg1 : sgs).inv_m, nn = (double)Bb.n;
       const double SG = (double)SGi, SGQ = (double)SGQi;
       const float m = Bb.ms[c], sig = Bb.ms[Cq + c];
       const Recip rc = recip(sig);
@@ -1990,7 +2073,6 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
       sh.cst[bn][4][c] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
     }
   }
-  const QState sn1 = qstate(p.b1.qn), sns = qstate(p.bs.qn), sg1 = qstate(p.b1.qng), sgs = qstate(p.bs.qng);
   __syncthreads();
   LBT_TS(1);
 
@@ -2362,7 +2444,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   const uint32_t bid = blockIdx.x;
   const int tpi = H / TH;
   const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * TH;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4;
   const int64_t img = (int64_t)n * H * W * C;
@@ -2418,15 +2500,26 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       gam[b][k] = (b == 0 ? a.b1 : a.b2).gb[cq + k];
       bet[b][k] = (b == 0 ? a.b1 : a.b2).gb[C + cq + k];
     }
-  QState qr[2];
-  float sn[2];
+  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
+  int I_r[2], I_n[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    qr[b] = qstate((b == 0 ? a.b1 : a.b2).qr);
-    sn[b] = qscale((b == 0 ? a.b1 : a.b2).nrm.qn);
+    I_r[b] = qexp_load((b == 0 ? a.b1 : a.b2).qr);
+    I_n[b] = qexp_load((b == 0 ? a.b1 : a.b2).nrm.qn);
   }
-  const QState so1 = qstate(a.qo1), sq = qstate(p.qout);
-  const float scale = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw)));
+  const int I_o1 = qexp_load(a.qo1), I_q = qexp_load(p.qout), I_w = qexp_load(p.qw);
+  LBT_ISSUE_FENCE();
+  QState qr[2];
+  float sn[2];
+  int en[2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    qr[b] = qstate_from((b == 0 ? a.b1 : a.b2).qr, I_r[b]);
+    en[b] = frac_exp_from((b == 0 ? a.b1 : a.b2).nrm.qn, I_n[b]);
+    sn[b] = ldexpf(1.0f, -en[b]);
+  }
+  const QState so1 = qstate_from(a.qo1, I_o1), sq = qstate_from(p.qout, I_q);
+  const float scale = ldexpf(1.0f, -(frac_exp_from(a.qo1, I_o1) + frac_exp_from(p.qw, I_w)));
 
   // ---------------- Normalization_q moments (bn.hip bn_moments) from the shard sums loaded above: each
   // statistics wave adds its 8 shards per lane, then its four lane rows; lanes < 16 finish a pair.
@@ -2444,7 +2537,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     const int bc = wave * 16 + (lane & 15), b = bc / C, c = bc - b * C;
     if (lane < 16) {
     const lbt_bn_norm& nb = b == 0 ? a.b1.nrm : a.b2.nrm;
-    const double s = ldexp(1.0, -frac_exp(nb.qn));
+    const double s = ldexp(1.0, -(b == 0 ? en[0] : en[NB - 1]));
     const double mean_d = (double)S1 * s / (double)nb.n;
     const double var_d = (double)S2 * (s * s) / (double)nb.n - mean_d * mean_d;
     const float m = (float)mean_d, vv = (float)var_d;
@@ -2680,7 +2773,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
   const uint32_t bid = blockIdx.x;
   const int tpi = Hq / kTH2;
   const int n = (int)(bid / (uint32_t)tpi), oy0 = (int)(bid - (uint32_t)n * tpi) * kTH2, y0 = 2 * oy0;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4, cqq = (tid % Cq4) * 4;
   const int64_t img = (int64_t)n * H * W * C, imgq = (int64_t)n * Hq * Wq * Cq;
@@ -2734,11 +2827,16 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
     gam[k] = a.b1.gb[cq + k];
     bet[k] = a.b1.gb[C + cq + k];
   }
-  const QState qr = qstate(a.b1.qr), so1 = qstate(a.qo1), so2 = qstate(a.qo2);
-  const QState sq1 = qstate(p.qout1), sqs = qstate(p.qouts);
-  const float sn = qscale(a.b1.nrm.qn);
-  const float scale1 = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw1)));
-  const float scale2 = ldexpf(1.0f, -(frac_exp(a.qo2) + frac_exp(p.qws)));
+  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
+  const int I_r = qexp_load(a.b1.qr), I_o1 = qexp_load(a.qo1), I_o2 = qexp_load(a.qo2), I_q1 = qexp_load(p.qout1),
+            I_qs = qexp_load(p.qouts), I_n = qexp_load(a.b1.nrm.qn), I_w1 = qexp_load(p.qw1), I_ws = qexp_load(p.qws);
+  LBT_ISSUE_FENCE();
+  const QState qr = qstate_from(a.b1.qr, I_r), so1 = qstate_from(a.qo1, I_o1), so2 = qstate_from(a.qo2, I_o2);
+  const QState sq1 = qstate_from(p.qout1, I_q1), sqs = qstate_from(p.qouts, I_qs);
+  const int en = frac_exp_from(a.b1.nrm.qn, I_n);
+  const float sn = ldexpf(1.0f, -en);
+  const float scale1 = ldexpf(1.0f, -(frac_exp_from(a.qo1, I_o1) + frac_exp_from(p.qw1, I_w1)));
+  const float scale2 = ldexpf(1.0f, -(frac_exp_from(a.qo2, I_o2) + frac_exp_from(p.qws, I_ws)));
 
   // ---------------- Normalization_q moments (conv_fwd_fused_kernel's arithmetic)
   if (wave < kSW) {
@@ -2753,7 +2851,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
     const int c = wave * 16 + (lane & 15);
     if (lane < 16) {
       const lbt_bn_norm& nb = a.b1.nrm;
-      const double s = ldexp(1.0, -frac_exp(nb.qn));
+      const double s = ldexp(1.0, -en);
       const double mean_d = (double)S1 * s / (double)nb.n;
       const double var_d = (double)S2 * (s * s) / (double)nb.n - mean_d * mean_d;
       const float m = (float)mean_d, vv = (float)var_d;
