@@ -866,6 +866,9 @@ constexpr int kMaxWJobs = 24;
 #ifndef LBT_WGM_BUFS
 #define LBT_WGM_BUFS 2
 #endif
+#ifndef LBT_WGX
+#define LBT_WGX 0
+#endif
 constexpr int kWgmBufs = LBT_WGM_BUFS;  // chunks of loads in flight per wave (register buffers)
 constexpr int kFW = 8;        // waves per workgroup of the batched launch
 constexpr int kHaloMax = 3;   // halo slices per lane: (64/W + 2) * (W + 2) <= 192 (W | 64, 2 <= W <= 32)
@@ -968,42 +971,43 @@ __device__ __forceinline__ void wgrad_s1_body(const WgradArgs& wa, uint32_t bid,
   auto cidx = [&](int s) { return c0 + wave + (int64_t)(s < nmine ? s : nmine - 1) * kFW; };
   // chunk s of this wave: stage b into LDS, refill b with chunk s + kWgmBufs, MFMAs of all 9 taps
   // (a step past the end, s >= nmine, adds a zero gradient fragment)
+  // LBT_WGX (scratch timing builds only, wrong results): 1 no refill loads, 2 no LDS staging stores,
+  // 4 no transposed LDS reads (register operands), 8 no MFMAs (integer adds)
   auto step = [&](Buf& b, int s) {
+    if constexpr (!(LBT_WGX & 2)) {
 #pragma unroll
-    for (int i = 0; i < kHaloMax; ++i) {
-      const int t = lane + 64 * i;
-      const v4i v = (b.valid >> i) & 1 ? b.x[i] : v4i{fill, fill, fill, fill};
-      if (t < nhalo) *reinterpret_cast<v4i*>(st + t * 16) = v;
+      for (int i = 0; i < kHaloMax; ++i) {
+        const int t = lane + 64 * i;
+        const v4i v = (b.valid >> i) & 1 ? b.x[i] : v4i{fill, fill, fill, fill};
+        if (t < nhalo) *reinterpret_cast<v4i*>(st + t * 16) = v;
+      }
+      *reinterpret_cast<v4i*>(gs + lane * 16) = s < nmine ? b.g : v4i{0, 0, 0, 0};
     }
-    *reinterpret_cast<v4i*>(gs + lane * 16) = s < nmine ? b.g : v4i{0, 0, 0, 0};
     // the images are read by other lanes of the same wave only: a wave's LDS instructions execute in
     // issue order, so only the compiler must keep the reads after the writes (no fence: a workgroup
     // release fence would also wait for the refills in flight)
     asm volatile("" ::: "memory");
-    load(b, cidx(s + kWgmBufs));
-    const v4i bfrag = tr_frag_at(gs, oga, ogb);
+    if constexpr (!(LBT_WGX & 1)) load(b, cidx(s + kWgmBufs));
+    const v4i bfrag = (LBT_WGX & 4) ? b.g : tr_frag_at(gs, oga, ogb);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int toff = ((t / 3) * Wp + t % 3) * 16;
-      const v4i afrag = tr_frag_at(st, oxa + toff, oxb + toff);
-      acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag, bfrag, acc[t], 0, 0, 0);
+      const v4i afrag = (LBT_WGX & 4) ? b.x[t % kHaloMax] : tr_frag_at(st, oxa + toff, oxb + toff);
+      if constexpr (LBT_WGX & 8)
+        acc[t] = acc[t] + afrag + bfrag;
+      else
+        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afrag, bfrag, acc[t], 0, 0, 0);
     }
     asm volatile("" ::: "memory");  // the next chunk's stores after these reads (in-order LDS)
   };
   LBT_TS(0);
-  if (nmine > 0) {
-    if constexpr (kWgmBufs == 2) {
-      Buf b0, b1;
-      load(b0, cidx(0));
-      load(b1, cidx(1));
-      for (int s = 0; s < nmine; s += 2) {
-        step(b0, s);
-        step(b1, s + 1);
-      }
-    } else {  // one register buffer: chunk s + 1's loads in flight during chunk s's MFMAs
-      Buf b0;
-      load(b0, cidx(0));
-      for (int s = 0; s < nmine; ++s) step(b0, s);
+  if (nmine > 0) {  // kWgmBufs register buffers: chunk s + kWgmBufs's loads issued during chunk s
+    Buf bf[kWgmBufs];
+#pragma unroll
+    for (int k = 0; k < kWgmBufs; ++k) load(bf[k], cidx(k));
+    for (int s = 0; s < nmine; s += kWgmBufs) {
+#pragma unroll
+      for (int k = 0; k < kWgmBufs; ++k) step(bf[k], s + k);
     }
   }
   LBT_TS(1);
@@ -1228,9 +1232,6 @@ namespace {
 #else
 #define LBT_TSS(i) do { } while (0)
 #define LBT_TSB(i) LBT_TS(i)
-#endif
-#ifndef LBT_EARLY3
-#define LBT_EARLY3 1
 #endif
 constexpr int kBNW = 8;    // waves per workgroup
 constexpr int kBThreads = kBNW * 64;
@@ -1464,8 +1465,6 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   constexpr int WC = WCS ? WCS : 1;
   constexpr int kBIt = halo_iters(CS, TH), J = TH / 4;  // J: phase-3 groups per thread
-  // phase-3 groups whose operands load with phase 1's (VGPR budget: 128 at CS < 4)
-  constexpr int JE = LBT_EARLY3 ? (CS == 4 || J == 1 ? J : 1) : 0;
   static_assert(TH % 4 == 0, "a tile is whole groups of 4 rows (8 MFMA pairs, one per wave)");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   union Smem {
@@ -1486,7 +1485,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   const int H = p.H;
   const int tpi = H / TH;
   const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * TH;
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4;  // this thread's channel quad (512 % C4 == 0: fixed over its groups)
   const int64_t img = (int64_t)n * H * W * C;
@@ -1527,27 +1526,6 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   // the phase-2 B operands (the dgrad weight image, ks == 4 * kMaxKS: host check), for LDS (WImg)
   v4i wimg[WI::kIt];
   WI::load(p.wd, wimg);
-  // phase-3 operands (addend, mask source, R / qn codes and both quantisers' noise per branch): the
-  // first JE groups issued in this first load wave too, so their latency is off the critical path
-  // (the stage-3 workgroup's whole chain, J = 1); the others after phase 1, where its registers are free
-  float4 av[J], ymv[J], urg[NB][J], ung[NB][J];
-  int Rv[NB][J], qnv[NB][J];
-  auto load3 = [&](int j) {
-    const int pix = (tid + j * kBThreads) / C4;
-    const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);  // tile rows are consecutive pixels
-    av[j] = p.add_src ? ld4f(p.add_src, img + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (CF & kAYMask) ymv[j] = ld4f(A.y_mask, img + off);
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
-      Rv[b][j] = ld4i8(Bb.R, img + off);
-      qnv[b][j] = ld4i8(Bb.qn_codes, img + off);
-      urg[b][j] = ld4f(Bb.qrg.noise, off);
-      ung[b][j] = ld4f(Bb.qng.noise, off);
-    }
-  };
-#pragma unroll
-  for (int j = 0; j < JE; ++j) load3(j);
   float mu[4], sg[4], gam[2][4], bet[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -1557,25 +1535,15 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     for (int b = 0; b < NB; ++b) gam[b][k] = (b == 0 ? A.b1 : A.b2).gb[cq + k];
     bet[k] = A.b1.gb[C + cq + k];
   }
-  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
-  const int I_gq = qexp_load(B.qng), I_n = qexp_load(B.qn), I_o = qexp_load(B.qo), I_w = qexp_load(p.qw);
-  int I_rg[2], I_ng[2];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    I_rg[b] = qexp_load((b == 0 ? A.b1 : A.b2).qrg);
-    I_ng[b] = qexp_load((b == 0 ? A.b1 : A.b2).qng);
-  }
-  const int I_r = (CF & kAMaskR) ? qexp_load(A.b1.qr) : 0;
-  LBT_ISSUE_FENCE();
-  const QState sgq = qstate_from(B.qng, I_gq), sn = qstate_from(B.qn, I_n), so = qstate_from(B.qo, I_o);
+  const QState sgq = qstate(B.qng), sn = qstate(B.qn), so = qstate(B.qo);
   QState qrg[2], qng[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    qrg[b] = qstate_from((b == 0 ? A.b1 : A.b2).qrg, I_rg[b]);
-    qng[b] = qstate_from((b == 0 ? A.b1 : A.b2).qng, I_ng[b]);
+    qrg[b] = qstate((b == 0 ? A.b1 : A.b2).qrg);
+    qng[b] = qstate((b == 0 ? A.b1 : A.b2).qng);
   }
-  const float r_inv = (CF & kAMaskR) ? qstate_from(A.b1.qr, I_r).inv_m : 0.f;
-  const float scale = ldexpf(1.0f, -(frac_exp_from(B.qo, I_o) + frac_exp_from(p.qw, I_w)));
+  const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
+  const float scale = ldexpf(1.0f, -(frac_exp(B.qo) + frac_exp(p.qw)));
   LBT_TSS(2);  // every other load issued, the descriptors read
 
   // ---------------- pass-B statistics: the shard sums (loaded first, above) added per lane, then over
@@ -1667,9 +1635,25 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   __syncthreads();
   LBT_TSB(2);
 
-  // the rest of the phase-3 operands, issued now: they land while the MFMAs run
+  // phase-3 operands (addend, mask source, R / qn codes and both quantisers' noise per branch),
+  // issued now: they land while the MFMAs run, and phase 1's registers are free
+  float4 av[J], ymv[J], urg[NB][J], ung[NB][J];
+  int Rv[NB][J], qnv[NB][J];
 #pragma unroll
-  for (int j = JE; j < J; ++j) load3(j);
+  for (int j = 0; j < J; ++j) {
+    const int pix = (tid + j * kBThreads) / C4;
+    const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);  // tile rows are consecutive pixels
+    av[j] = p.add_src ? ld4f(p.add_src, img + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (CF & kAYMask) ymv[j] = ld4f(A.y_mask, img + off);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const lbt_bwd_branch& Bb = b == 0 ? A.b1 : A.b2;
+      Rv[b][j] = ld4i8(Bb.R, img + off);
+      qnv[b][j] = ld4i8(Bb.qn_codes, img + off);
+      urg[b][j] = ld4f(Bb.qrg.noise, off);
+      ung[b][j] = ld4f(Bb.qng.noise, off);
+    }
+  }
 
   // ---------------- phase 2: dgrad from the LDS image, two (m-tile, n-tile) pairs per wave
 #pragma unroll
@@ -1963,7 +1947,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
   const int H = p.H, Hq = H / 2;
   const int tpi = H / TH;
   const int n = (int)(bid / (uint32_t)tpi), r0 = (int)(bid - (uint32_t)n * tpi) * TH, q0 = r0 / 2;
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4;     // dx channel quad (phase 3)
   const int cqq = (tid % Cq4) * 4;   // low-res channel quad (phase 1)
@@ -2024,30 +2008,16 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
     for (int b = 0; b < NB; ++b) gam[b][k] = (b == 0 ? A.b1 : A.b2).gb[cq + k];
     bet[k] = A.b1.gb[C + cq + k];
   }
-  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
-  const int I_o1 = qexp_load(p.b1.qo), I_os = qexp_load(p.bs.qo), I_w1 = qexp_load(p.qw1), I_ws = qexp_load(p.qws);
-  const int I_n1 = qexp_load(p.b1.qn), I_ns = qexp_load(p.bs.qn), I_g1 = qexp_load(p.b1.qng),
-            I_gs = qexp_load(p.bs.qng);
-  int I_rg[2], I_ng[2];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    I_rg[b] = qexp_load((b == 0 ? A.b1 : A.b2).qrg);
-    I_ng[b] = qexp_load((b == 0 ? A.b1 : A.b2).qng);
-  }
-  const int I_r = (CF & kAMaskR) ? qexp_load(A.b1.qr) : 0;
-  LBT_ISSUE_FENCE();
-  const QState so1 = qstate_from(p.b1.qo, I_o1), sos = qstate_from(p.bs.qo, I_os);
+  const QState so1 = qstate(p.b1.qo), sos = qstate(p.bs.qo);
   QState qrg[2], qng[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    qrg[b] = qstate_from((b == 0 ? A.b1 : A.b2).qrg, I_rg[b]);
-    qng[b] = qstate_from((b == 0 ? A.b1 : A.b2).qng, I_ng[b]);
+    qrg[b] = qstate((b == 0 ? A.b1 : A.b2).qrg);
+    qng[b] = qstate((b == 0 ? A.b1 : A.b2).qng);
   }
-  const float r_inv = (CF & kAMaskR) ? qstate_from(A.b1.qr, I_r).inv_m : 0.f;
-  const float scale1 = ldexpf(1.0f, -(frac_exp_from(p.b1.qo, I_o1) + frac_exp_from(p.qw1, I_w1)));
-  const float scale2 = ldexpf(1.0f, -(frac_exp_from(p.bs.qo, I_os) + frac_exp_from(p.qws, I_ws)));
-  const QState sn1 = qstate_from(p.b1.qn, I_n1), sns = qstate_from(p.bs.qn, I_ns), sg1 = qstate_from(p.b1.qng, I_g1),
-               sgs = qstate_from(p.bs.qng, I_gs);
+  const float r_inv = (CF & kAMaskR) ? qstate(A.b1.qr).inv_m : 0.f;
+  const float scale1 = ldexpf(1.0f, -(frac_exp(p.b1.qo) + frac_exp(p.qw1)));
+  const float scale2 = ldexpf(1.0f, -(frac_exp(p.bs.qo) + frac_exp(p.qws)));
 
   // ---------------- pass-B constants of both BNs (chain_bwd_b_kernel's double arithmetic)
   if (wave < kSW) {
@@ -2062,7 +2032,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
     const int bn = wave < CSq ? 0 : 1, c = (wave % CSq) * 16 + (lane & 15);
     if (lane < 16) {
       const lbt_chain_bwd_b& Bb = bn == 0 ? p.b1 : p.bs;
-      const double s = (double)(bn == 0 ? sn1 : sns).inv_m, gsc = (double)(bn == 0 ? sg1 : sgs).inv_m, nn = (double)Bb.n;
+      const double s = (double)qstate(Bb.qn).inv_m, gsc = (double)qstate(Bb.qng).inv_m, nn = (double)Bb.n;
       const double SG = (double)SGi, SGQ = (double)SGQi;
       const float m = Bb.ms[c], sig = Bb.ms[Cq + c];
       const Recip rc = recip(sig);
@@ -2073,6 +2043,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_bwd2_kernel(C
       sh.cst[bn][4][c] = (float)(gsc * (s * SGQ - (double)m * SG) / (nn * (double)sig));
     }
   }
+  const QState sn1 = qstate(p.b1.qn), sns = qstate(p.bs.qn), sg1 = qstate(p.b1.qng), sgs = qstate(p.bs.qng);
   __syncthreads();
   LBT_TS(1);
 
@@ -2444,7 +2415,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   const uint32_t bid = blockIdx.x;
   const int tpi = H / TH;
   const int n = (int)(bid / (uint32_t)tpi), row0 = (int)(bid - (uint32_t)n * tpi) * TH;
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4;
   const int64_t img = (int64_t)n * H * W * C;
@@ -2500,26 +2471,15 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
       gam[b][k] = (b == 0 ? a.b1 : a.b2).gb[cq + k];
       bet[b][k] = (b == 0 ? a.b1 : a.b2).gb[C + cq + k];
     }
-  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
-  int I_r[2], I_n[2];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    I_r[b] = qexp_load((b == 0 ? a.b1 : a.b2).qr);
-    I_n[b] = qexp_load((b == 0 ? a.b1 : a.b2).nrm.qn);
-  }
-  const int I_o1 = qexp_load(a.qo1), I_q = qexp_load(p.qout), I_w = qexp_load(p.qw);
-  LBT_ISSUE_FENCE();
   QState qr[2];
   float sn[2];
-  int en[2];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    qr[b] = qstate_from((b == 0 ? a.b1 : a.b2).qr, I_r[b]);
-    en[b] = frac_exp_from((b == 0 ? a.b1 : a.b2).nrm.qn, I_n[b]);
-    sn[b] = ldexpf(1.0f, -en[b]);
+    qr[b] = qstate((b == 0 ? a.b1 : a.b2).qr);
+    sn[b] = qscale((b == 0 ? a.b1 : a.b2).nrm.qn);
   }
-  const QState so1 = qstate_from(a.qo1, I_o1), sq = qstate_from(p.qout, I_q);
-  const float scale = ldexpf(1.0f, -(frac_exp_from(a.qo1, I_o1) + frac_exp_from(p.qw, I_w)));
+  const QState so1 = qstate(a.qo1), sq = qstate(p.qout);
+  const float scale = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw)));
 
   // ---------------- Normalization_q moments (bn.hip bn_moments) from the shard sums loaded above: each
   // statistics wave adds its 8 shards per lane, then its four lane rows; lanes < 16 finish a pair.
@@ -2537,7 +2497,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
     const int bc = wave * 16 + (lane & 15), b = bc / C, c = bc - b * C;
     if (lane < 16) {
     const lbt_bn_norm& nb = b == 0 ? a.b1.nrm : a.b2.nrm;
-    const double s = ldexp(1.0, -(b == 0 ? en[0] : en[NB - 1]));
+    const double s = ldexp(1.0, -frac_exp(nb.qn));
     const double mean_d = (double)S1 * s / (double)nb.n;
     const double var_d = (double)S2 * (s * s) / (double)nb.n - mean_d * mean_d;
     const float m = (float)mean_d, vv = (float)var_d;
@@ -2773,7 +2733,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
   const uint32_t bid = blockIdx.x;
   const int tpi = Hq / kTH2;
   const int n = (int)(bid / (uint32_t)tpi), oy0 = (int)(bid - (uint32_t)n * tpi) * kTH2, y0 = 2 * oy0;
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, kg = lane >> 4;
   const int cq = (tid % C4) * 4, cqq = (tid % Cq4) * 4;
   const int64_t img = (int64_t)n * H * W * C, imgq = (int64_t)n * Hq * Wq * Cq;
@@ -2827,16 +2787,11 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
     gam[k] = a.b1.gb[cq + k];
     bet[k] = a.b1.gb[C + cq + k];
   }
-  // every quantiser's exponent load, issued together after the vector loads (qexp_load)
-  const int I_r = qexp_load(a.b1.qr), I_o1 = qexp_load(a.qo1), I_o2 = qexp_load(a.qo2), I_q1 = qexp_load(p.qout1),
-            I_qs = qexp_load(p.qouts), I_n = qexp_load(a.b1.nrm.qn), I_w1 = qexp_load(p.qw1), I_ws = qexp_load(p.qws);
-  LBT_ISSUE_FENCE();
-  const QState qr = qstate_from(a.b1.qr, I_r), so1 = qstate_from(a.qo1, I_o1), so2 = qstate_from(a.qo2, I_o2);
-  const QState sq1 = qstate_from(p.qout1, I_q1), sqs = qstate_from(p.qouts, I_qs);
-  const int en = frac_exp_from(a.b1.nrm.qn, I_n);
-  const float sn = ldexpf(1.0f, -en);
-  const float scale1 = ldexpf(1.0f, -(frac_exp_from(a.qo1, I_o1) + frac_exp_from(p.qw1, I_w1)));
-  const float scale2 = ldexpf(1.0f, -(frac_exp_from(a.qo2, I_o2) + frac_exp_from(p.qws, I_ws)));
+  const QState qr = qstate(a.b1.qr), so1 = qstate(a.qo1), so2 = qstate(a.qo2);
+  const QState sq1 = qstate(p.qout1), sqs = qstate(p.qouts);
+  const float sn = qscale(a.b1.nrm.qn);
+  const float scale1 = ldexpf(1.0f, -(frac_exp(a.qo1) + frac_exp(p.qw1)));
+  const float scale2 = ldexpf(1.0f, -(frac_exp(a.qo2) + frac_exp(p.qws)));
 
   // ---------------- Normalization_q moments (conv_fwd_fused_kernel's arithmetic)
   if (wave < kSW) {
@@ -2851,7 +2806,7 @@ __global__ __launch_bounds__(kBThreads, CS == 1 ? 4 : 2) void conv_fwd2_kernel(C
     const int c = wave * 16 + (lane & 15);
     if (lane < 16) {
       const lbt_bn_norm& nb = a.b1.nrm;
-      const double s = ldexp(1.0, -en);
+      const double s = ldexp(1.0, -frac_exp(nb.qn));
       const double mean_d = (double)S1 * s / (double)nb.n;
       const double var_d = (double)S2 * (s * s) / (double)nb.n - mean_d * mean_d;
       const float m = (float)mean_d, vv = (float)var_d;

@@ -206,38 +206,10 @@ LBT_DEV QState qstate(const lbt_qdesc& q) {
 // dequant scale 2^-e of a quantiser (the exponent the codes were produced with)
 LBT_DEV float qscale(const lbt_qdesc& q) { return ldexpf(1.0f, -frac_exp(q)); }
 
-// ---- split form for the latency-bound fused kernels: qexp_load ISSUES a quantiser's exponent load,
-// qstate_from / frac_exp_from finish it. A kernel issues every exponent load first, then its other
-// loads, then LBT_ISSUE_FENCE, and only then uses the values: one scalar-memory round trip for all of
-// them, overlapped with the vector loads. With qstate() the compiler placed each load next to its use
-// and waited for it (s_waitcnt lgkmcnt(0)) before issuing the next quantiser's -- one dependent round
-// trip per quantiser, ~1.6 us of the stage-3 fused conv backward's 3.2 us load phase (caches cold,
-// tools/trace_phases.py on a -DLBT_P1STUDY build, profiles/round6/budget). No step counter: the
-// kernels that use these draw their noise from per-step tables.
-LBT_DEV int qexp_load(const lbt_qdesc& q) { return *(q.bits > 0 ? q.exps + q.slot : zi()); }
-LBT_DEV int frac_exp_from(const lbt_qdesc& q, int I) {
-  const int e = q.bits - I - 1;
-  return e < 0 ? 0 : (e > kEMax ? kEMax : e);
-}
-LBT_DEV QState qstate_from(const lbt_qdesc& q, int I) {
-  QState s;
-  s.active = q.bits > 0;
-  const int e = frac_exp_from(q, I);
-  s.e = s.active ? e : 0;
-  s.m = s.active ? ldexpf(1.0f, e) : 0.f;
-  s.inv_m = s.active ? ldexpf(1.0f, -e) : 0.f;
-  s.L = s.active ? ldexpf(1.0f, q.bits - 1) : 0.f;
-  s.Lm1 = s.active ? s.L - 1.0f : 0.f;
-  s.Lh = s.active ? ldexpf(1.0f, q.bits - 2) : 0.f;
-  s.step = 0;
-  return s;
-}
 // the wave's index in its workgroup as a wave-uniform (scalar) value: threadIdx.x >> 6 is a per-lane
 // VGPR value to the compiler, so everything derived from it -- chunk / tile indices, addresses, the
 // branches on it -- was computed per lane on the VALU (divisions included)
 LBT_DEV int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
-// nothing moves across it: the loads above are issued before the uses below
-#define LBT_ISSUE_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // One element: integer code + overflow predicates (on the UNquantised x, against I_t).
 // stochastic: floor(clip(x*m + u, -L, L-1)); nearest: rint(clip(x*m, -L, L-1)) (half-even).
