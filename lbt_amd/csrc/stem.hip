@@ -403,6 +403,115 @@ __global__ __launch_bounds__(kThreads) void stem_bwd_rows_kernel(StemBwdArgs p) 
   LBT_TS(3);
 }
 
+
+// The CIFAR stem (Cout 16, 3x3 / stride 1 / SAME, W == 32, Cin <= 4, quantising epilogue) on whole row
+// bands: a 512-thread workgroup owns kSbRows output rows of one image (512 pixels = 32 16-row tiles, 4 per
+// wave). The input rows + halo are staged in LDS once, each wave loads the weight fragment once and runs
+// its 4 tiles' MFMAs and quantisers, the channel sums and overflow counters accumulate in registers over
+// the tiles and leave once per workgroup. (stem_fwd_rows_kernel: 64-pixel blocks of 4 waves, 2048
+// workgroups at B = 128, each repeating the weight / noise / descriptor loads and the publish barrier.)
+// Per tile the same fp16 fragments, the same MFMA, the same quantiser and noise as stem_fwd_rows_kernel's
+// epilogue (epi_quant): bit-identical codes; integer channel sums and counts (order-free).
+constexpr int kSbRows = 16, kSbW = 32, kSbThreads = 512, kSbTiles = 4;
+constexpr int kSbElems = (kSbRows + 2) * (kSbW + 2) * kStemCinMax, kSbIt = (kSbElems + kSbThreads - 1) / kSbThreads;
+static_assert(kSbRows * kSbW == 16 * kSbTiles * (kSbThreads / 64), "a band is 4 tiles per wave");
+__global__ __launch_bounds__(kSbThreads) void stem_fwd_band_kernel(StemFwdArgs p) {
+  __shared__ int16_t s_img[kSbElems];
+  __shared__ int s_part[kSbThreads / 64][2][16];
+  __shared__ int s_cnt[2 * (kSbThreads / 64)];
+  LBT_TS(0);
+  const lbt_conv_desc& d = p.d;
+  const int Cin = d.Cin, H = d.H, bands = H / kSbRows;
+  const int n = (int)blockIdx.x / bands, oy0 = ((int)blockIdx.x - n * bands) * kSbRows;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, kg = lane >> 4;
+  constexpr int NC = kSbW + 2;
+  const int E = (kSbRows + 2) * NC * Cin;
+  const int64_t HWo = p.o.HWo, m0 = (int64_t)n * HWo + (int64_t)oy0 * kSbW;  // the band's first pixel
+  // ---- every load first: the band's input rows + halo (zeros outside the image), the weight fragment,
+  // the 4 tiles' epilogue noise
+  int16_t xv[kSbIt];
+  bool xok[kSbIt];
+#pragma unroll
+  for (int h = 0; h < kSbIt; ++h) {
+    const int t = tid + h * kSbThreads;
+    const int ci = t % Cin, pc = t / Cin, col = pc % NC, row = pc / NC;
+    const int iy = oy0 - 1 + row, ix = col - 1;
+    xok[h] = t < E && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)kSbW;
+    xv[h] = p.x[xok[h] ? (((int64_t)n * H + iy) * kSbW + ix) * Cin + ci : 0];
+  }
+  int8_t wv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j;
+    wv[j] = p.w[(int64_t)(k < p.K ? k : 0) * 16 + r];
+  }
+  const bool tab = p.o.q.stochastic && p.o.q.noise;  // else the quantiser ignores u: read zeros
+  const float* nsrc = tab ? p.o.q.noise : zf();
+  const uint32_t nmask = tab ? 0xffffffffu : 0u;
+  float u[kSbTiles][4];
+#pragma unroll
+  for (int tt = 0; tt < kSbTiles; ++tt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t pix = (uint32_t)(oy0 * kSbW + (wave * kSbTiles + tt) * 16 + 4 * kg + i);  // < HWo
+      u[tt][i] = nsrc[(pix * 16u + (uint32_t)r) & nmask];
+    }
+  const QState qs = qstate(p.o.q);
+  const float scale = ldexpf(1.0f, -(frac_exp(p.qx) + frac_exp(p.qw)));
+#pragma unroll
+  for (int h = 0; h < kSbIt; ++h) {
+    const int t = tid + h * kSbThreads;
+    if (t < E) s_img[t] = xok[h] ? xv[h] : (int16_t)0;
+  }
+  h8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (_Float16)(float)(8 * kg + j < p.K ? (int)wv[j] : 0);
+  __syncthreads();
+  LBT_TS(1);
+  // ---- the wave's 4 tiles: 8 patch codes per lane from LDS, one MFMA, the quantiser
+  int ov1 = 0, ov2 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+  for (int tt = 0; tt < kSbTiles; ++tt) {
+    const int mt = wave * kSbTiles + tt;
+    const int lm = mt * 16 + r, ly = lm / kSbW, ox = lm - ly * kSbW;
+    h8 a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * kg + j;
+      const int tap = k / Cin, ci = k - tap * Cin, kh = tap / 3, kw = tap - kh * 3;
+      const int v = k < p.K ? (int)s_img[((ly + kh) * NC + ox + kw) * Cin + ci] : 0;
+      a[j] = (_Float16)(float)v;
+    }
+    const f4v acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, f4v{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    int cc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = quant_w<-1>(qs, p.o.q.stochastic, acc[i] * scale, u[tt][i], ov1, ov2);
+      cc[i] = c;
+      s1 += c;
+      s2 += c * c;
+    }
+    // the 4 lanes of a column quad swap codes so lane r stores row 4 kg + (r & 3)'s 4 columns (epi_quant)
+    const uint32_t packed = quad_pack_codes(cc, r & 3);
+    const int64_t rowp = m0 + mt * 16 + 4 * kg + (r & 3);
+    st_out(p.o.yq + (uint32_t)rowp * 16u + (r & ~3), (int)packed);  // M * 16 < 2^31 (launcher)
+  }
+  LBT_TS(2);
+  // ---- channel sums and counters of the band: one barrier, one atomic per (channel, sum)
+  const int t2 = rows_scatter2(s1, s2);  // row 0: column r's S1, row 1: its S2
+  if (kg < 2) s_part[wave][kg][r] = t2;
+  if (p.o.q.counts) counts_stage_w(0, 1, ov1, ov2, s_cnt);  // wave totals (quant_w)
+  __syncthreads();
+  counts_publish(0, 1, p.o.q, s_cnt);
+  if (p.o.chsum && tid < 32) {
+    const int which = tid >> 4, col = tid & 15;
+    long long tot = 0;
+#pragma unroll
+    for (int w = 0; w < kSbThreads / 64; ++w) tot += s_part[w][which][col];
+    if (tot) LBT_GADD((unsigned long long*)&p.o.chsum[(int64_t)shard_id() * 32 + tid], (unsigned long long)tot);
+  }
+  LBT_TS(3);
+}
 }  // namespace
 
 LBT_TRACE_SETTER(stem)
@@ -421,6 +530,17 @@ extern "C" int lbt_conv_stem_fwd(const int16_t* x, const int8_t* w_hwio, lbt_con
   if (M * d.Cout >= (int64_t)1 << 31) return LBT_EINVAL;  // 32-bit element offsets
   hipStream_t st = (hipStream_t)stream;
   const int64_t mtiles = (M + 15) / 16;
+  // whole-row bands of 16 rows (the CIFAR-10 stem of the fused plan) when they fill the chip: 10.5 vs 11.8 us
+  // at B = 128 (256 bands), but 10.5 vs 5.6 us at B = 16 (32 bands: a band's serial 4-tile chain is the
+  // launch), profiles/round6/stem_band.txt. LBT_STEM_BAND=0 / 1: never / always.
+  static const int band_env = getenv("LBT_STEM_BAND") ? atoi(getenv("LBT_STEM_BAND")) : -1;
+  const int64_t nband = (int64_t)d.N * (d.H / kSbRows);
+  if ((band_env == 1 || (band_env < 0 && nband >= 256)) && yq && d.Cout == 16 && d.KH == 3 && d.KW == 3 &&
+      d.SH == 1 && d.SW == 1 && d.PT == 1 && d.PL == 1 && d.Ho == d.H && d.Wo == d.W && d.W == kSbW &&
+      d.H % kSbRows == 0 && d.Cin <= kStemCinMax) {
+    hipLaunchKernelGGL(stem_fwd_band_kernel, dim3((unsigned)nband), dim3(kSbThreads), 0, st, p);
+    return (int)hipGetLastError();
+  }
   // whole-row blocks staged in LDS (CIFAR stems): 3x3 / stride 1 / SAME, block pixels = whole rows
   const int pb = d.Cout == 16 ? 64 : 32;  // EpiGeom<Cout/16>::MTB * 16 of the two row variants
   if ((d.Cout == 16 || d.Cout == 32) && d.KH == 3 && d.KW == 3 && d.SH == 1 && d.SW == 1 && d.PT == 1 &&
