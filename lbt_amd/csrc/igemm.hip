@@ -536,7 +536,8 @@ LBT_DEV int swz128(int row) { return (row >> 1) & 5; }
 // fit 128 VGPRs (78 KiB of LDS: two workgroups per CU).
 #ifndef LBT_BIG_OCC
 #define LBT_BIG_OCC(A16, BN, S, HALO, BNA) \
-  (((A16 && BN == 64 && !HALO) || (!A16 && HALO && BN == 64) || BNA == 4) ? 4 : 1)
+  (((A16 && BN == 64 && !HALO && S <= 2) || (!A16 && HALO && BN == 64) || BNA == 4) ? 4 \
+   : (A16 && BN == 64 && !HALO) ? 2 : 1)
 #endif
 // BN pass A (bn_wide.hip bn_bwd_a_wide_kernel) on the dgrad accumulators, element for element.
 // MA = 1 (lbt_dgrad_bna): dx -> ReLU mask recomputed from R -> the BN's two quantisers. MA = 2, 3
@@ -2066,7 +2067,7 @@ bool launch_big(const IgArgs& p, hipStream_t st) {
     else launch_big_bn<MODE, A16, 128, 4>(p, st);
   } else {
     if (S <= 2) launch_big_bn<MODE, A16, 64, 2>(p, st);
-    else if (S == 3 || A16) launch_big_bn<MODE, A16, 64, 3>(p, st);
+    else if (S == 3) launch_big_bn<MODE, A16, 64, 3>(p, st);
     else launch_big_bn<MODE, A16, 64, 4>(p, st);
   }
   ++big_tuning().launches;

@@ -125,6 +125,11 @@ class FusedResNet:
         self.batch_wgrad = (os.environ.get("LBT_BATCH_WGRAD", "1") == "1" and not self.overlap_wgrad
                             and not self.side_wgrad)
         self._wbatch = []  # the batched launch's jobs (lbt_wgrad_job), in backward order
+        # with the batch on: a fused conv backward launch whose own tiles leave CU slots empty (fewer
+        # than two workgroups per CU: the 64-channel stage at B = 128, every stage at small batches)
+        # carries the previous such launch's wgrad job in those slots, as the unbatched plan does (the
+        # job keeps the batched split, so a job no launch carries still joins the batch)
+        self.defer_underfilled = os.environ.get("LBT_DEFER_UNDERFILLED", "0") == "1"
         # the optimiser and the range update inside the step's last launch (lbt_step_reduce_update;
         # single process): one launch fewer per step. Off until the Trainer hands over its flat
         # buffers and hyper-parameters (set_optimizer)
@@ -894,6 +899,17 @@ class FusedResNet:
                 and d.PB == 1 and d.PL == 1 and d.PR == 1 and d.Cin == d.Cout and d.Cin in (16, 32, 64)
                 and d.H % (8 if d.Cin == 16 else 4) == 0 and d.W * d.Cin == 512)
 
+    @staticmethod
+    def _bwd_tiles(d):
+        """lbt_conv_bwd_fused_i8's workgroup tiles for conv d (conv_mfma.hip tile_rows_for)."""
+        cs = d.Cin // 16
+        th = 4 if cs != 1 or d.N * (d.H // 8) < 256 else 8
+        return d.N * (d.H // th)
+
+    def _defers(self, d, fusable):
+        """This conv's fused backward launch takes a deferred wgrad job (and defers its own)."""
+        return bool(self.batch_wgrad and self.defer_underfilled and fusable and self._bwd_tiles(d) < 2 * 256)
+
     def _wgrad(self, bwd, L, xq, gq, d, slab, nsplit, nshard, nb):
         """One conv's weight gradient (pass 1 into its slab): a job of the end-of-backward batched
         launch, or its own lbt_conv_wgrad_i8 launch (on the side stream in overlap mode)."""
@@ -917,11 +933,15 @@ class FusedResNet:
         bwd.append(self._on_side(run, force=True) if side else run)
 
     def _flush_pending(self, bwd, L):
-        """Run the deferred wgrad job on its own (the next launch is not a fused conv backward)."""
+        """Run the deferred wgrad job on its own (the next launch is not a fused conv backward), or
+        hand it to the end-of-backward batch."""
         w = self._pending
         if w is None:
             return
         self._pending = None
+        if self.batch_wgrad:
+            self._wbatch.append(w)
+            return
         bwd.append(L("lbt_conv_wgrad_i8", w.xq, w.x_u8off, w.gq, w.d, w.slab, w.nsplit, w.nshard,
                      k="conv_wgrad_kernel", nb=w._nb))
 
@@ -938,7 +958,20 @@ class FusedResNet:
         cb.add_src = add.data_ptr() if add is not None else None
         cb.a = aA
         nbw = 0
+        if self.batch_wgrad and self._defers(d, True):  # carry the pending job, defer this conv's
+            if self._pending is not None and self._pending.d.Cin == d.Cin:
+                cb.w = self._pending
+                nbw = self._pending._nb
+                self._pending = None
+            self._flush_pending(bwd, L)  # (a job of another width: to the batch)
+            nb = (ops._chain_bwd_b_bytes(aB) + 4 * aB.inner
+                  + ops._dgrad_chain_bytes(0, c.wd.numel(), aA, add is not None) + nbw)
+            bwd.append(L("lbt_conv_bwd_fused_i8", ctypes.byref(cb), k="conv_bwd_kernel", nb=nb))
+            self._keep.append(cb)
+            self._pending = wjob
+            return
         if self.batch_wgrad:  # this conv's wgrad joins the end-of-backward batch
+            self._flush_pending(bwd, L)
             nb = (ops._chain_bwd_b_bytes(aB) + 4 * aB.inner
                   + ops._dgrad_chain_bytes(0, c.wd.numel(), aA, add is not None))
             bwd.append(L("lbt_conv_bwd_fused_i8", ctypes.byref(cb), k="conv_bwd_kernel", nb=nb))

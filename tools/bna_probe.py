@@ -87,5 +87,11 @@ for name, H, Cin, Cout, k, mode, nbn, gm in shapes:
                                          qng.desc, qn, G, sums, rows, inner, Cin, g2=g2, y_bits=ybits)
     dg = timed(lambda: ops.conv_dgrad_igemm_ws(g, 1, wd, ksd, d, qg.desc, qw.desc, dx, None))
     uf, fu = timed(unfused), timed(fused)
-    print("%-20s dgrad %7.1f us | dgrad + pass A %7.1f us | fused %7.1f us (%.2fx)" % (name, dg, uf, fu, uf / fu),
-          flush=True)
+    # algorithmic bytes of the fused launch: the 16-bit G codes, the weight image, per BN R + qn in and
+    # the 16-bit G out, and (bn3) g2 in, y_bits in, the optional gmask out
+    nel = rows * Cin
+    ab = rows * Cout * 2 + wd.numel() + nbn * nel * 4
+    if mode == "bn3":
+        ab += nel * 4 + nel // 4 + (nel * 4 if gm else 0)
+    print("%-20s dgrad %7.1f us | dgrad + pass A %7.1f us | fused %7.1f us (%.2fx) | %.1f MB, %.2f TB/s" %
+          (name, dg, uf, fu, uf / fu, ab / 1e6, ab / fu / 1e6), flush=True)
