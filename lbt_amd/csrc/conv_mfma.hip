@@ -1247,8 +1247,21 @@ __host__ __device__ constexpr int halo_iters(int CS) { return halo_iters(CS, til
 // 8-row tiles leave the launch with fewer workgroups than CUs (N * H / 8 < 256: per-GPU batches below
 // 64 -- the strong-scaling shards of configs[2]): twice the workgroups, each with two thirds of the halo
 // rows of phase 1, half the phase-3 groups and MFMA pairs per wave. LBT_TILE_ROWS1=8|4 forces one.
+// The 32- / 64-channel stages take 2-row tiles when 4-row tiles leave CUs without a workgroup
+// (N * H / 4 < 256: per-GPU batches below 64 for the 64-channel stage, below 32 for the 32-channel
+// one): B = 16 0.301 -> 0.291 ms per step, bit-identical. Not at one tile per CU: the 64-channel stage
+// at B = 128 (256 tiles) measured 0.414 -> 0.433 ms with 2-row tiles (two co-resident workgroups per CU,
+// each staging the whole 37 KB weight image and a halo of 2 rows per 2; profiles/round6/tile_rows23_ab.txt).
+// LBT_TILE_ROWS23=4|2 forces one.
 inline int tile_rows_for(int CS, int64_t N, int H) {
-  if (CS != 1) return tile_rows(CS);
+  if (CS != 1) {
+    static const int force23 = [] {
+      const char* e = getenv("LBT_TILE_ROWS23");
+      return e ? atoi(e) : 0;
+    }();
+    if (force23 == 4 || H % 4) return 4;
+    return (force23 == 2 || N * H / 4 < 256) ? 2 : 4;
+  }
   static const int force = [] {
     const char* e = getenv("LBT_TILE_ROWS1");
     return e ? atoi(e) : 0;
@@ -1460,12 +1473,15 @@ LBT_DEV int pack4f(f2 a, f2 b) {
 }
 
 template <int CS, int CF, int NB, bool W4, int WCS, int TH = tile_rows(CS)>
-__global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(ConvBwdArgs p, WgradArgs wa, uint32_t nwg) {
+__global__ __launch_bounds__(kBThreads, (CS == 4 && TH >= 4) ? 2 : 4) void conv_bwd_kernel(ConvBwdArgs p, WgradArgs wa, uint32_t nwg) {
   constexpr int C = CS * 16, C4 = C / 4, NT = CS;
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   constexpr int WC = WCS ? WCS : 1;
-  constexpr int kBIt = halo_iters(CS, TH), J = TH / 4;  // J: phase-3 groups per thread
-  static_assert(TH % 4 == 0, "a tile is whole groups of 4 rows (8 MFMA pairs, one per wave)");
+  // J: phase-3 groups per thread (NQ channel quads per tile: TH x 512 bytes / 4); NPR: (m, n) MFMA
+  // pairs per tile (2 TH: one per wave at TH = 4). Two-row tiles (TH = 2, the under-filled 32- /
+  // 64-channel launches) leave waves 4-7 without a pair and threads >= 256 without a phase-3 group.
+  constexpr int kBIt = halo_iters(CS, TH), NQ = TH * 128, J = (NQ + kBThreads - 1) / kBThreads, NPR = 2 * TH;
+  static_assert(TH % 4 == 0 || (TH == 2 && CS >= 2), "whole groups of 4 rows, or 2-row tiles of the wide stages");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   union Smem {
     BwdShared<C, TH, WI::kBytes> b;
@@ -1641,7 +1657,8 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   int Rv[NB][J], qnv[NB][J];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int pix = (tid + j * kBThreads) / C4;
+    const int q3 = tid + j * kBThreads;
+    const int pix = (q3 < NQ ? q3 : 0) / C4;  // (2-row tiles: the idle threads load the tile's first quad)
     const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);  // tile rows are consecutive pixels
     av[j] = p.add_src ? ld4f(p.add_src, img + off) : make_float4(0.f, 0.f, 0.f, 0.f);
     if (CF & kAYMask) ymv[j] = ld4f(A.y_mask, img + off);
@@ -1655,10 +1672,11 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
     }
   }
 
-  // ---------------- phase 2: dgrad from the LDS image, two (m-tile, n-tile) pairs per wave
+  // ---------------- phase 2: dgrad from the LDS image, (m-tile, n-tile) pair wave + 8 pi
 #pragma unroll
-  for (int pi = 0; pi < TH / 4; ++pi) {
+  for (int pi = 0; pi < (NPR + 7) / 8; ++pi) {
     const int pr = wave + 8 * pi;
+    if (NPR % 8 && pr >= NPR) break;  // uniform per wave
     const int mt = pr / NT, nt = pr - mt * NT;
     const int m = mt * 16 + r;
     const int ly = m / W, px = m - ly * W;
@@ -1699,6 +1717,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_bwd_kernel(Co
   }
 #pragma unroll
   for (int j = 0; j < J; ++j) {
+    if (NQ % kBThreads && tid + j * kBThreads >= NQ) break;  // uniform per wave
     const int pix = (tid + j * kBThreads) / C4;
     const uint32_t off = (uint32_t)(row0 * W * C + pix * C + cq);
     const float4 t = *reinterpret_cast<const float4*>(sh.tile + pix * (C + 4) + cq);
@@ -1871,6 +1890,8 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   if (CS == CS_ && f == (CF_) && nb == NB_ && wcs == WCS_) {                                       \
     if (CS_ == 1 && th == 4) {                                                                     \
       LBT_BW_TH(CS_, CF_, NB_, WCS_, (CS_ == 1 ? 4 : tile_rows(CS_)))                              \
+    } else if (CS_ != 1 && th == 2) {                                                              \
+      LBT_BW_TH(CS_, CF_, NB_, WCS_, (CS_ == 1 ? 4 : 2))                                           \
     } else {                                                                                       \
       LBT_BW_TH(CS_, CF_, NB_, WCS_, tile_rows(CS_))                                               \
     }                                                                                              \
@@ -2402,11 +2423,12 @@ struct FwdShared {
 };
 
 template <int CS, int NB, int F, bool W4, int TH = tile_rows(CS)>
-__global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_kernel(ConvFwdArgs p) {
+__global__ __launch_bounds__(kBThreads, (CS == 4 && TH >= 4) ? 2 : 4) void conv_fwd_fused_kernel(ConvFwdArgs p) {
   constexpr int C = CS * 16, C4 = C / 4, NT = CS, W = 512 / C, Wp = W + 2;
   constexpr int kMaxKS = (9 * CS + 3) / 4;
-  constexpr int kBIt = halo_iters(CS, TH), J = TH / 4;
-  static_assert(TH % 4 == 0, "a tile is whole groups of 4 rows (8 MFMA pairs, one per wave)");
+  // (as conv_bwd_kernel: NQ channel quads and NPR MFMA pairs per tile; 2-row tiles idle half of each)
+  constexpr int kBIt = halo_iters(CS, TH), NQ = TH * 128, J = (NQ + kBThreads - 1) / kBThreads, NPR = 2 * TH;
+  static_assert(TH % 4 == 0 || (TH == 2 && CS >= 2), "whole groups of 4 rows, or 2-row tiles of the wide stages");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   __shared__ __attribute__((aligned(16))) FwdShared<C, TH, WI::kBytes> sh;
   LBT_TS(0);
@@ -2608,14 +2630,18 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   __syncthreads();
   LBT_TS(2);
   // phase-3 noise (the output quantiser), issued under the MFMAs
-  float4 u3[J];  // J channel quads per thread: TH*W*C/4 == J * kBThreads
+  float4 u3[J];  // J channel quads per thread: NQ <= J * kBThreads (the idle threads load the first quad)
 #pragma unroll
-  for (int j = 0; j < J; ++j) u3[j] = ld4f(p.qout.noise, (uint32_t)(row0 * W * C + ((tid + j * kBThreads) / C4) * C + cq));
+  for (int j = 0; j < J; ++j) {
+    const int q3 = tid + j * kBThreads;
+    u3[j] = ld4f(p.qout.noise, (uint32_t)(row0 * W * C + ((q3 < NQ ? q3 : 0) / C4) * C + cq));
+  }
 
-  // ---------------- phase 2: the conv from the LDS image (pair = wave)
+  // ---------------- phase 2: the conv from the LDS image (pair = wave + 8 pi)
 #pragma unroll
-  for (int pi = 0; pi < TH / 4; ++pi) {
+  for (int pi = 0; pi < (NPR + 7) / 8; ++pi) {
     const int pr = wave + 8 * pi;
+    if (NPR % 8 && pr >= NPR) break;  // uniform per wave
     const int mt = pr / NT, nt = pr - mt * NT;
     const int m = mt * 16 + r;
     const int ly = m / W, px = m - ly * W;
@@ -2642,6 +2668,7 @@ __global__ __launch_bounds__(kBThreads, CS == 4 ? 2 : 4) void conv_fwd_fused_ker
   int s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int j = 0; j < J; ++j) {
+    if (NQ % kBThreads && tid + j * kBThreads >= NQ) break;  // uniform per wave
     const int pix3 = (tid + j * kBThreads) / C4;
     const float4 t = *reinterpret_cast<const float4*>(sh.tile + pix3 * (C + 4) + cq);
     const f2 tv[2] = {mk2(t.x, t.y), mk2(t.z, t.w)};
@@ -3046,6 +3073,8 @@ extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
   if (CS == CS_ && nb == NB_ && fl == ((FL_) & ~kFU8 & ~kFStoch)) {                                      \
     if (CS_ == 1 && th == 4) {                                                                           \
       LBT_FW_TH(CS_, NB_, FL_, (CS_ == 1 ? 4 : tile_rows(CS_)))                                          \
+    } else if (CS_ != 1 && th == 2) {                                                                    \
+      LBT_FW_TH(CS_, NB_, FL_, (CS_ == 1 ? 4 : 2))                                                       \
     } else {                                                                                             \
       LBT_FW_TH(CS_, NB_, FL_, tile_rows(CS_))                                                           \
     }                                                                                                    \

@@ -903,7 +903,11 @@ class FusedResNet:
     def _bwd_tiles(d):
         """lbt_conv_bwd_fused_i8's workgroup tiles for conv d (conv_mfma.hip tile_rows_for)."""
         cs = d.Cin // 16
-        th = 4 if cs != 1 or d.N * (d.H // 8) < 256 else 8
+        if cs != 1:
+            f23 = os.environ.get("LBT_TILE_ROWS23")
+            th = 2 if d.H % 4 == 0 and f23 != "4" and (f23 == "2" or d.N * d.H // 4 < 256) else 4
+        else:
+            th = 4 if d.N * (d.H // 8) < 256 else 8
         return d.N * (d.H // th)
 
     def _defers(self, d, fusable):
