@@ -1266,8 +1266,9 @@ inline int tile_rows_for(int CS, int64_t N, int H) {
     const char* e = getenv("LBT_TILE_ROWS1");
     return e ? atoi(e) : 0;
   }();
-  if (force == 4 || force == 8) return H % force ? 8 : force;  // (16-row tiles at B=128: 0.447 vs 0.429 ms)
-  return (N * H / 8 < 256 && H % 4 == 0) ? 4 : 8;
+  if (force == 2 || force == 4 || force == 8) return H % force ? 8 : force;  // (16-row tiles at B=128: 0.447 vs 0.429 ms)
+  if (N * H / 8 >= 256 || H % 4) return 8;
+  return (N * H / 4 < 256 && H % 2 == 0) ? 2 : 4;  // (2-row tiles: B = 16, as the wide stages below)
 }
 
 // The conv's weight image shared through LDS by the fused conv kernels: [C columns][KS k-slices] of 16
@@ -1481,7 +1482,7 @@ __global__ __launch_bounds__(kBThreads, (CS == 4 && TH >= 4) ? 2 : 4) void conv_
   // pairs per tile (2 TH: one per wave at TH = 4). Two-row tiles (TH = 2, the under-filled 32- /
   // 64-channel launches) leave waves 4-7 without a pair and threads >= 256 without a phase-3 group.
   constexpr int kBIt = halo_iters(CS, TH), NQ = TH * 128, J = (NQ + kBThreads - 1) / kBThreads, NPR = 2 * TH;
-  static_assert(TH % 4 == 0 || (TH == 2 && CS >= 2), "whole groups of 4 rows, or 2-row tiles of the wide stages");
+  static_assert(TH % 4 == 0 || TH == 2, "whole groups of 4 rows, or 2-row tiles");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   union Smem {
     BwdShared<C, TH, WI::kBytes> b;
@@ -1890,8 +1891,8 @@ extern "C" int lbt_conv_bwd_fused_i8(const lbt_conv_bwd* q, void* stream) {
   if (CS == CS_ && f == (CF_) && nb == NB_ && wcs == WCS_) {                                       \
     if (CS_ == 1 && th == 4) {                                                                     \
       LBT_BW_TH(CS_, CF_, NB_, WCS_, (CS_ == 1 ? 4 : tile_rows(CS_)))                              \
-    } else if (CS_ != 1 && th == 2) {                                                              \
-      LBT_BW_TH(CS_, CF_, NB_, WCS_, (CS_ == 1 ? 4 : 2))                                           \
+    } else if (th == 2) {                                                                          \
+      LBT_BW_TH(CS_, CF_, NB_, WCS_, 2)                                                            \
     } else {                                                                                       \
       LBT_BW_TH(CS_, CF_, NB_, WCS_, tile_rows(CS_))                                               \
     }                                                                                              \
@@ -2428,7 +2429,7 @@ __global__ __launch_bounds__(kBThreads, (CS == 4 && TH >= 4) ? 2 : 4) void conv_
   constexpr int kMaxKS = (9 * CS + 3) / 4;
   // (as conv_bwd_kernel: NQ channel quads and NPR MFMA pairs per tile; 2-row tiles idle half of each)
   constexpr int kBIt = halo_iters(CS, TH), NQ = TH * 128, J = (NQ + kBThreads - 1) / kBThreads, NPR = 2 * TH;
-  static_assert(TH % 4 == 0 || (TH == 2 && CS >= 2), "whole groups of 4 rows, or 2-row tiles of the wide stages");
+  static_assert(TH % 4 == 0 || TH == 2, "whole groups of 4 rows, or 2-row tiles");
   using WI = WImg<C, 4 * kMaxKS, W4>;
   __shared__ __attribute__((aligned(16))) FwdShared<C, TH, WI::kBytes> sh;
   LBT_TS(0);
@@ -3073,8 +3074,8 @@ extern "C" int lbt_conv_fwd_fused_i8(const lbt_conv_fwd* q, void* stream) {
   if (CS == CS_ && nb == NB_ && fl == ((FL_) & ~kFU8 & ~kFStoch)) {                                      \
     if (CS_ == 1 && th == 4) {                                                                           \
       LBT_FW_TH(CS_, NB_, FL_, (CS_ == 1 ? 4 : tile_rows(CS_)))                                          \
-    } else if (CS_ != 1 && th == 2) {                                                                    \
-      LBT_FW_TH(CS_, NB_, FL_, (CS_ == 1 ? 4 : 2))                                                       \
+    } else if (th == 2) {                                                                                \
+      LBT_FW_TH(CS_, NB_, FL_, 2)                                                                        \
     } else {                                                                                             \
       LBT_FW_TH(CS_, NB_, FL_, tile_rows(CS_))                                                           \
     }                                                                                                    \

@@ -906,8 +906,10 @@ class FusedResNet:
         if cs != 1:
             f23 = os.environ.get("LBT_TILE_ROWS23")
             th = 2 if d.H % 4 == 0 and f23 != "4" and (f23 == "2" or d.N * d.H // 4 < 256) else 4
+        elif d.N * (d.H // 8) >= 256:
+            th = 8
         else:
-            th = 4 if d.N * (d.H // 8) < 256 else 8
+            th = 2 if d.N * d.H // 4 < 256 else 4
         return d.N * (d.H // th)
 
     def _defers(self, d, fusable):
