@@ -420,10 +420,57 @@ def chain_bwd_b(desc):
         call("lbt_bn_chain_bwd_b", _lib.ctypes.byref(desc), stream())
 
 
+# ---- the layer-wise backward's BN parameter gradients in ONE launch (lbt_bn_param_grads_many at the end
+# of deferred_param_grads' scope) instead of one lbt_bn_param_grads per BatchNorm (53 per ResNet-50 step).
+# Nothing reads dgamma / dbeta before the backward ends, and each layer's pass-A sums stay in the arena
+# until the next step's clear, so the deferred launch computes the same values (the same per-channel
+# arithmetic, param_grads_many_kernel). The job array is uploaded once per distinct job list (outside
+# any graph capture: the Trainer's warm-up runs the step eagerly first); LBT_BATCH_PGRADS=0: per layer.
+_PDEFER = None
+_PJOB_DEV = {}
+
+
+class deferred_param_grads:
+    def __enter__(self):
+        global _PDEFER
+        self.own = _PDEFER is None and os.environ.get("LBT_BATCH_PGRADS", "1") == "1"
+        if self.own:
+            _PDEFER = []
+        return self
+
+    def __exit__(self, et, ev, tb):
+        global _PDEFER
+        if not self.own:
+            return False
+        jobs, _PDEFER = _PDEFER, None
+        if et is None and jobs:
+            _flush_param_grads(jobs)
+        return False
+
+
+def _flush_param_grads(jobs):
+    key = b"".join(bytes(j) for j in jobs)
+    arr = _PJOB_DEV.get(key)
+    if arr is None:
+        if torch.cuda.is_current_stream_capturing():  # no upload inside a capture: per-layer launches
+            for j in jobs:
+                call("lbt_bn_param_grads", j.sums, int(j.C), j.qrg, j.qr, j.gamma, float(j.wd2), j.dgamma,
+                     j.dbeta, stream())
+            return
+        buf = (_lib.PJob * len(jobs))(*jobs)
+        arr = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8).to(torch.device("cuda", torch.cuda.current_device()))
+        _PJOB_DEV[key] = arr
+    call("lbt_bn_param_grads_many", ptr(arr), len(jobs), max(int(j.C) for j in jobs), stream())
+
+
 def bn_param_grads(sums, C, qrg, qr, gamma, wd2, dgamma, dbeta):
     ng = _num(dgamma)
     if ng is not None:
         call("lbt_bn_param_grads_x", ptr(sums), int(C), ng, _num(dbeta), stream())
+        return
+    if _PDEFER is not None:
+        _PDEFER.append(_lib.PJob(sums.data_ptr(), int(C), qrg, qr, gamma.data_ptr(), float(wd2), dgamma.data_ptr(),
+                                 dbeta.data_ptr()))
         return
     call("lbt_bn_param_grads", ptr(sums), int(C), qrg, qr, ptr(gamma), float(wd2), ptr(dgamma), ptr(dbeta), stream())
 

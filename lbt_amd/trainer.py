@@ -215,7 +215,8 @@ class Trainer:
         else:
             m.forward(X)
             m.compute_loss(y)
-            m.backward()
+            with ops.deferred_param_grads():  # every BN's dgamma / dbeta in one launch at the end
+                m.backward()
         if nel is None and hasattr(m, "set_exchange"):
             m._nelem = self.ctx.nelem.clone()  # what its build declared (Quantizer.observe)
         if self.comm is not None:

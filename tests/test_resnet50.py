@@ -140,6 +140,32 @@ def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, classes, grad_
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("blocks,width,image,classes,grad_bits", [((1, 1, 1, 1), 8, 32, 10, 8),
+                                                                  ((3, 2, 1, 1), 64, 40, 16, 16)])
+def test_resnet50_deferred_param_grads_bitexact(blocks, width, image, classes, grad_bits):
+    """The Trainer's backward scope (ops.deferred_param_grads): every BN's dgamma / dbeta in one
+    lbt_bn_param_grads_many launch at the end of the backward, equal to the oracle's."""
+    from lbt_amd.dfxp import ops
+    ctx, gm, om = _pair(blocks, width, classes, image, grad_bits, seed=3)
+    oresnet.set_params(om, _params(gm))
+    x, y = _batch(4, image, classes, seed=4)
+    octx = onn.Ctx(oresnet.init_ranges(om), 0, ctx.seed)
+    gm.forward(torch.from_numpy(x).to(DEV))
+    om.forward(x, octx)
+    gm.compute_loss(torch.from_numpy(y).to(DEV))
+    dz = gm.dlogits.cpu().numpy()
+    for owner, _, gname in gm.param_slots():  # stale values must not survive
+        getattr(owner, gname).fill_(float("nan"))
+    with ops.deferred_param_grads() as scope:
+        gm.backward()
+    assert scope.own
+    om.backward(dz, octx)
+    gg, og = _grads(gm), oresnet.get_grads(om)
+    for k in gg:
+        assert np.array_equal(gg[k], og[k]), k
+
+
+@pytest.mark.gpu
 def test_resnet50_full_size_step():
     """The real ResNet-50 (224x224, 1000 classes, [3,4,6,3]) through one graph-captured training
     step with 16-bit gradients: finite loss, every gradient finite, exponents updated."""
