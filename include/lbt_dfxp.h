@@ -308,6 +308,16 @@ int lbt_conv_wgrad_generic16(const void* xq, int32_t x_i16, const int16_t* gq, l
                              int32_t nsplit, void* stream);
 int lbt_conv_wgrad_reduce64(const int64_t* slab, int32_t nsplit, int32_t K, int32_t Cout, lbt_qdesc qx, lbt_qdesc qg,
                             const float* w, float wd2, float* dw, void* stream);
+/* Many lbt_conv_wgrad_reduce64 in ONE launch (dynamic_fixed_point.py:302, each conv's dW = dequant(sum) +
+ * 2 wd W): job k owns the 64-output blocks [first_block, first_block + ceil(K*Cout/64)), jobs in
+ * ascending first_block from 0, nblocks the total. The layer-wise Trainer defers every conv's reduce of
+ * the backward into one such launch at its end (each job's slab is the layer's own). Same int64 totals and
+ * the same fp32 epilogue as the single-job launch: bit-identical. Job array in device memory.            */
+typedef struct lbt_r64job {
+  const int64_t* slab; int32_t nsplit, K, Cout, first_block;
+  lbt_qdesc qx, qg; const float* w; float wd2; float* dw;
+} lbt_r64job;
+int lbt_conv_wgrad_reduce64_many(const lbt_r64job* jobs, int32_t njobs, int32_t nblocks, void* stream);
 
 /* Stem convolution (conv1 of the CIFAR ResNets, models.py:387-391): input = the image's SIGNED
  * (bits+1)-bit codes as int16 (|x| <= 2048), patch K = KH*KW*Cin <= 32, Cout % 16 == 0.

@@ -133,6 +133,11 @@ class RJob(ctypes.Structure):
                 ("dw", c_void_p)]
 
 
+class R64Job(ctypes.Structure):
+    _fields_ = [("slab", c_void_p), ("nsplit", c_int32), ("K", c_int32), ("Cout", c_int32), ("first_block", c_int32),
+                ("qx", QDesc), ("qg", QDesc), ("w", c_void_p), ("wd2", c_float), ("dw", c_void_p)]
+
+
 class PJob(ctypes.Structure):
     _fields_ = [("sums", c_void_p), ("C", c_int32), ("qrg", QDesc), ("qr", QDesc), ("gamma", c_void_p),
                 ("wd2", c_float), ("dgamma", c_void_p), ("dbeta", c_void_p)]
@@ -229,6 +234,7 @@ _SIGS = {
     "lbt_conv_dgrad_generic16": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, _P],
     "lbt_conv_wgrad_generic16": [_P, c_int32, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_wgrad_reduce64": [_P, c_int32, c_int32, c_int32, QDesc, QDesc, _P, c_float, _P, _P],
+    "lbt_conv_wgrad_reduce64_many": [_P, c_int32, c_int32, _P],
     "lbt_conv_stem_fwd": [_P, _P, ConvDesc, QDesc, QDesc, _P, _P, QDesc, _P, _P],
     "lbt_conv_stem_wgrad": [_P, _P, ConvDesc, _P, c_int32, _P],
     "lbt_conv_stem_bwd": [_P, _P, ConvDesc, _P, c_int32, _P],

@@ -261,7 +261,44 @@ __global__ __launch_bounds__(256) void wgrad_reduce64_split_kernel(const long lo
   dw[i] = a + b;
 }
 
+// lbt_conv_wgrad_reduce64_many: wgrad_reduce64_split_kernel's block (64 outputs x 4 split groups) for the
+// job owning the block -- the last job whose first_block <= blockIdx.x (uniform scalar loads of the small
+// job array). The int64 totals are exact in any order, so every output equals the single-job launch's.
+__global__ __launch_bounds__(256) void wgrad_reduce64_many_kernel(const lbt_r64job* __restrict__ jobs, int njobs) {
+  __shared__ long long red[4][64];
+  const int b = (int)blockIdx.x;
+  int jb = 0;
+  for (int k = 1; k < njobs; ++k)
+    if (jobs[k].first_block <= b) jb = k;
+  const lbt_r64job& J = jobs[jb];
+  const int64_t total = (int64_t)J.K * J.Cout;
+  const int lo = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int64_t i = (int64_t)(b - J.first_block) * 64 + lo;
+  const long long* slab = reinterpret_cast<const long long*>(J.slab);
+  long long s = 0;
+  if (i < total) {
+#pragma unroll 4
+    for (int k = sg; k < J.nsplit; k += 4) s += slab[(int64_t)k * total + i];
+  }
+  red[sg][lo] = s;
+  __syncthreads();
+  if (sg != 0 || i >= total) return;
+  s = red[0][lo] + red[1][lo] + red[2][lo] + red[3][lo];
+  const float scale = ldexpf(1.0f, -(frac_exp(J.qx) + frac_exp(J.qg)));
+  const float a = (float)s * scale;
+  const float c = J.wd2 * J.w[i];
+  J.dw[i] = a + c;
+}
+
 }  // namespace
+
+extern "C" int lbt_conv_wgrad_reduce64_many(const lbt_r64job* jobs, int32_t njobs, int32_t nblocks, void* stream) {
+  if (njobs < 0 || nblocks < 0 || (njobs > 0 && (!jobs || nblocks <= 0))) return LBT_EINVAL;
+  if (njobs == 0) return LBT_OK;
+  hipLaunchKernelGGL(wgrad_reduce64_many_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, jobs,
+                     njobs);
+  return (int)hipGetLastError();
+}
 
 extern "C" int lbt_conv_wgrad_generic(const void* xq, int32_t x_i16, const int8_t* gq, lbt_conv_desc d,
                                       int32_t* slab, int32_t nsplit, void* stream) {

@@ -420,47 +420,82 @@ def chain_bwd_b(desc):
         call("lbt_bn_chain_bwd_b", _lib.ctypes.byref(desc), stream())
 
 
-# ---- the layer-wise backward's BN parameter gradients in ONE launch (lbt_bn_param_grads_many at the end
-# of deferred_param_grads' scope) instead of one lbt_bn_param_grads per BatchNorm (53 per ResNet-50 step).
-# Nothing reads dgamma / dbeta before the backward ends, and each layer's pass-A sums stay in the arena
-# until the next step's clear, so the deferred launch computes the same values (the same per-channel
-# arithmetic, param_grads_many_kernel). The job array is uploaded once per distinct job list (outside
-# any graph capture: the Trainer's warm-up runs the step eagerly first); LBT_BATCH_PGRADS=0: per layer.
+# ---- the layer-wise backward's gradient reductions batched: every BN's parameter gradients in ONE
+# lbt_bn_param_grads_many launch (53 lbt_bn_param_grads per ResNet-50 step) and every conv's int64 slab
+# reduce in ONE lbt_conv_wgrad_reduce64_many launch (53 per step), both at the end of the
+# deferred_reductions scope (the Trainer's backward). Nothing reads dW / dgamma / dbeta before the
+# backward ends, each layer's slab and pass-A sums are its own (per-layer caches; the sums arena is
+# cleared at the next step's start), and the batched kernels do each output's arithmetic as the per-layer
+# ones: the same values. Job arrays are uploaded once per distinct job list, outside any graph capture (the
+# Trainer's warm-up runs the step eagerly first). LBT_BATCH_PGRADS=0: per layer. The reduces stay per
+# layer by default (LBT_BATCH_WREDUCE=1 batches them): deferred, the 1.8 GB of int64 slabs a ResNet-50
+# step reduces come back from HBM instead of the cache the wgrad just wrote them through -- 31.9 -> 32.4 ms
+# (profiles/round6/batched_reductions_ab.txt); the parameter gradients alone: 32.11 -> 31.79 ms.
 _PDEFER = None
-_PJOB_DEV = {}
+_RDEFER = None
+_JOBS_DEV = {}
 
 
-class deferred_param_grads:
+class deferred_reductions:
     def __enter__(self):
-        global _PDEFER
-        self.own = _PDEFER is None and os.environ.get("LBT_BATCH_PGRADS", "1") == "1"
-        if self.own:
+        global _PDEFER, _RDEFER
+        self.own_p = _PDEFER is None and os.environ.get("LBT_BATCH_PGRADS", "1") == "1"
+        self.own_r = _RDEFER is None and os.environ.get("LBT_BATCH_WREDUCE", "0") == "1"
+        if self.own_p:
             _PDEFER = []
+        if self.own_r:
+            _RDEFER = []
         return self
 
     def __exit__(self, et, ev, tb):
-        global _PDEFER
-        if not self.own:
-            return False
-        jobs, _PDEFER = _PDEFER, None
-        if et is None and jobs:
-            _flush_param_grads(jobs)
+        global _PDEFER, _RDEFER
+        pj, rj = (_PDEFER if self.own_p else None), (_RDEFER if self.own_r else None)
+        if self.own_p:
+            _PDEFER = None
+        if self.own_r:
+            _RDEFER = None
+        if et is None:
+            if rj:
+                _flush_reduce64(rj)
+            if pj:
+                _flush_param_grads(pj)
         return False
 
 
+def _jobs_dev(jobs, T):
+    """The device copy of a job list (None inside a capture when it was never uploaded)."""
+    key = (T.__name__, b"".join(bytes(j) for j in jobs))
+    arr = _JOBS_DEV.get(key)
+    if arr is None and not torch.cuda.is_current_stream_capturing():
+        buf = (T * len(jobs))(*jobs)
+        arr = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8).to(
+            torch.device("cuda", torch.cuda.current_device()))
+        _JOBS_DEV[key] = arr
+    return arr
+
+
 def _flush_param_grads(jobs):
-    key = b"".join(bytes(j) for j in jobs)
-    arr = _PJOB_DEV.get(key)
-    if arr is None:
-        if torch.cuda.is_current_stream_capturing():  # no upload inside a capture: per-layer launches
-            for j in jobs:
-                call("lbt_bn_param_grads", j.sums, int(j.C), j.qrg, j.qr, j.gamma, float(j.wd2), j.dgamma,
-                     j.dbeta, stream())
-            return
-        buf = (_lib.PJob * len(jobs))(*jobs)
-        arr = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8).to(torch.device("cuda", torch.cuda.current_device()))
-        _PJOB_DEV[key] = arr
+    arr = _jobs_dev(jobs, _lib.PJob)
+    if arr is None:  # per-layer launches
+        for j in jobs:
+            call("lbt_bn_param_grads", j.sums, int(j.C), j.qrg, j.qr, j.gamma, float(j.wd2), j.dgamma, j.dbeta,
+                 stream())
+        return
     call("lbt_bn_param_grads_many", ptr(arr), len(jobs), max(int(j.C) for j in jobs), stream())
+
+
+def _flush_reduce64(jobs):
+    nb = 0
+    for j in jobs:
+        j.first_block = nb
+        nb += (int(j.K) * int(j.Cout) + 63) // 64
+    arr = _jobs_dev(jobs, _lib.R64Job)
+    if arr is None:
+        for j in jobs:
+            call("lbt_conv_wgrad_reduce64", j.slab, int(j.nsplit), int(j.K), int(j.Cout), j.qx, j.qg, j.w,
+                 float(j.wd2), j.dw, stream())
+        return
+    call("lbt_conv_wgrad_reduce64_many", ptr(arr), len(jobs), nb, stream())
 
 
 def bn_param_grads(sums, C, qrg, qr, gamma, wd2, dgamma, dbeta):
@@ -637,6 +672,10 @@ def conv_wgrad_reduce64(slab, nsplit, K, Cout, qx, qg, w, wd2, dw):
     num = _num(dw)
     if num is not None:
         call("lbt_conv_wgrad_reduce64_x", ptr(slab), int(nsplit), int(K), int(Cout), num, stream())
+        return
+    if _RDEFER is not None:
+        _RDEFER.append(_lib.R64Job(slab.data_ptr(), int(nsplit), int(K), int(Cout), 0, qx, qg, w.data_ptr(),
+                                   float(wd2), dw.data_ptr()))
         return
     call("lbt_conv_wgrad_reduce64", ptr(slab), int(nsplit), int(K), int(Cout), qx, qg, ptr(w), wd2, ptr(dw), stream())
 

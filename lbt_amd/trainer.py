@@ -215,7 +215,7 @@ class Trainer:
         else:
             m.forward(X)
             m.compute_loss(y)
-            with ops.deferred_param_grads():  # every BN's dgamma / dbeta in one launch at the end
+            with ops.deferred_reductions():  # the backward's wgrad reduces / BN parameter grads: two launches at the end
                 m.backward()
         if nel is None and hasattr(m, "set_exchange"):
             m._nelem = self.ctx.nelem.clone()  # what its build declared (Quantizer.observe)

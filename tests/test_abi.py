@@ -48,7 +48,7 @@ def _load_fresh(path):
 STRUCTS = {"lbt_qdesc": _lib.QDesc, "lbt_conv_desc": _lib.ConvDesc, "lbt_bn_norm": _lib.BnNorm,
            "lbt_chain_branch": _lib.ChainBranch, "lbt_chain_fwd": _lib.ChainFwd, "lbt_bwd_branch": _lib.BwdBranch,
            "lbt_chain_bwd_a": _lib.ChainBwdA, "lbt_chain_bwd_b": _lib.ChainBwdB, "lbt_wjob": _lib.WJob,
-           "lbt_qjob": _lib.QJob, "lbt_rjob": _lib.RJob, "lbt_pjob": _lib.PJob, "lbt_njob": _lib.NJob,
+           "lbt_qjob": _lib.QJob, "lbt_rjob": _lib.RJob, "lbt_pjob": _lib.PJob, "lbt_r64job": _lib.R64Job, "lbt_njob": _lib.NJob,
            "lbt_head": _lib.Head, "lbt_xchg": _lib.Xchg, "lbt_fseg": _lib.FSeg,
            "lbt_wgrad_job": _lib.WgradJob, "lbt_conv_bwd": _lib.ConvBwd,
            "lbt_conv_fwd": _lib.ConvFwd, "lbt_conv_fwd_job": _lib.ConvFwdJob,

@@ -142,10 +142,12 @@ def test_resnet50_layers_bitexact_vs_oracle(blocks, width, image, classes, grad_
 @pytest.mark.gpu
 @pytest.mark.parametrize("blocks,width,image,classes,grad_bits", [((1, 1, 1, 1), 8, 32, 10, 8),
                                                                   ((3, 2, 1, 1), 64, 40, 16, 16)])
-def test_resnet50_deferred_param_grads_bitexact(blocks, width, image, classes, grad_bits):
-    """The Trainer's backward scope (ops.deferred_param_grads): every BN's dgamma / dbeta in one
-    lbt_bn_param_grads_many launch at the end of the backward, equal to the oracle's."""
+def test_resnet50_deferred_reductions_bitexact(blocks, width, image, classes, grad_bits, monkeypatch):
+    """The Trainer's backward scope (ops.deferred_reductions): every conv's slab reduce in one
+    lbt_conv_wgrad_reduce64_many launch and every BN's dgamma / dbeta in one lbt_bn_param_grads_many
+    launch at the end of the backward, equal to the oracle's."""
     from lbt_amd.dfxp import ops
+    monkeypatch.setenv("LBT_BATCH_WREDUCE", "1")  # (off by default: measured slower, ops.py)
     ctx, gm, om = _pair(blocks, width, classes, image, grad_bits, seed=3)
     oresnet.set_params(om, _params(gm))
     x, y = _batch(4, image, classes, seed=4)
@@ -156,9 +158,9 @@ def test_resnet50_deferred_param_grads_bitexact(blocks, width, image, classes, g
     dz = gm.dlogits.cpu().numpy()
     for owner, _, gname in gm.param_slots():  # stale values must not survive
         getattr(owner, gname).fill_(float("nan"))
-    with ops.deferred_param_grads() as scope:
+    with ops.deferred_reductions() as scope:
         gm.backward()
-    assert scope.own
+    assert scope.own_p and scope.own_r
     om.backward(dz, octx)
     gg, og = _grads(gm), oresnet.get_grads(om)
     for k in gg:
