@@ -407,14 +407,17 @@ def test_dense_mfma_matches_generic(N, IN, OUT):
 
 
 @pytest.mark.gpu
-def test_softmax_xent_wide():
-    """The wide-K softmax-CE (one wave per row) against float64 numpy: loss and d loss / d z."""
+@pytest.mark.parametrize("K", [1000, 1024, 1500])
+def test_softmax_xent_wide(K):
+    """The wide-K softmax-CE (one wave per row) against float64 numpy: loss and d loss / d z (K <= 1024:
+    the row held in registers; 1500: the looped form). Bit-exactness against the oracle's softmax is
+    test_resnet50_layers_bitexact_vs_oracle's 1000-class case."""
     from lbt_amd.dfxp import ops
     rng = np.random.default_rng(5)
-    z = (rng.normal(size=(32, 1000)) * 4).astype(np.float32)
-    y = rng.integers(0, 1000, size=32).astype(np.int32)
+    z = (rng.normal(size=(32, K)) * 4).astype(np.float32)
+    y = rng.integers(0, K, size=32).astype(np.int32)
     loss = torch.empty(1, device=DEV)
-    dz = torch.empty((32, 1000), device=DEV)
+    dz = torch.empty((32, K), device=DEV)
     ops.softmax_xent(torch.from_numpy(z).to(DEV), torch.from_numpy(y).to(DEV), loss, dz)
     zd = z.astype(np.float64)
     m = zd.max(1, keepdims=True)
