@@ -180,19 +180,26 @@ __global__ __launch_bounds__(1024) void softmax_xent_wide_kernel(const float* __
   __shared__ double part[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double acc = 0.0;
+  // the row in registers (ImageNet's 1000 classes: 16 per lane) when K <= 1024, the wave's next row loaded
+  // while this one is reduced (the looped form below made three dependent passes over global memory per row:
+  // 205 us per ResNet-50 step at B = 256); each lane's max / sum run over its k in the same ascending order
+  // and through the same shuffle tree, so every value is the loops' bit for bit
+  const bool regs = K <= 64 * kSxReg;
+  float v[kSxReg];
+  auto load_row = [&](int rr, float (&dst)[kSxReg]) {
+    const float* zr = z + (int64_t)rr * K;
+#pragma unroll
+    for (int i = 0; i < kSxReg; ++i) {
+      const int k = lane + 64 * i;
+      dst[i] = k < K ? zr[k] : -INFINITY;
+    }
+  };
+  if (regs && wave < N) load_row(wave, v);
   for (int rr = wave; rr < N; rr += 16) {
     const float* zr = z + (int64_t)rr * K;
-    if (K <= 64 * kSxReg) {
-      // the row in registers (ImageNet's 1000 classes: 16 per lane), loaded once and all in flight
-      // (the loops below made three dependent passes over global memory per row: 205 us per
-      // ResNet-50 step for B = 256); each lane's max / sum run over its k in the same ascending
-      // order and through the same shuffle tree, so every value is the loops' bit for bit
-      float v[kSxReg];
-#pragma unroll
-      for (int i = 0; i < kSxReg; ++i) {
-        const int k = lane + 64 * i;
-        v[i] = k < K ? zr[k] : -INFINITY;
-      }
+    if (regs) {
+      float vn[kSxReg];
+      if (rr + 16 < N) load_row(rr + 16, vn);
       float m = -INFINITY;
 #pragma unroll
       for (int i = 0; i < kSxReg; ++i) m = fmaxf(m, v[i]);
@@ -217,6 +224,8 @@ __global__ __launch_bounds__(1024) void softmax_xent_wide_kernel(const float* __
         const float lse = logf(s) + m;
         acc += (double)(lse - zr[y]);
       }
+#pragma unroll
+      for (int i = 0; i < kSxReg; ++i) v[i] = vn[i];
       continue;
     }
     float m = -INFINITY;
