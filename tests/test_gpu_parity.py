@@ -417,7 +417,7 @@ def _gpu_norms(gm):
     return [l for l in gm._walk() if isinstance(l, Normalization_q)]
 
 
-@pytest.mark.parametrize("weight_bits,B", [(None, 128), (4, 128), (None, 16), (None, 32)])
+@pytest.mark.parametrize("weight_bits,B", [(None, 128), (4, 128), (None, 16), (None, 32), (None, 64), (4, 16)])
 def test_fused_bench_workload_bitexact_vs_oracle(weight_bits, B):
     """The EXACT timed configuration (bench.py: FusedResNet, B=128, bench batches, HIP-graph replay)
     against the oracle for 3 optimiser steps. B=128 puts stage 1 at P = 131 072 pixels, so the
@@ -427,7 +427,9 @@ def test_fused_bench_workload_bitexact_vs_oracle(weight_bits, B):
     weight_bits=4: configs[4]'s timed plan (bench.py --workload resnet20w4: packed 4-bit weight
     images, every fused kernel's W4 variant) against the oracle's 4-bit weight quantisers
     (dynamic_fixed_point.py:21-38 with bits=4). B=16 / 32: configs[2]'s per-GPU shards (global batch
-    128 / 256 over 8 GPUs): the small-batch tile geometry (4-row stage-1 tiles) and wgrad splits."""
+    128 / 256 over 8 GPUs): the small-batch tile geometry (2-row tiles in every stage at B=16, 4-row
+    stage-1 and 2-row stage-2 / 3 tiles at B=32, 2-row stage-3 tiles only at B=64; conv_mfma.hip
+    tile_rows_for) and wgrad splits; (4, 16): the W4 variants of the 2-row tiles."""
     import bench
     from lbt_amd.fused import FusedResNet
     from lbt_amd.trainer import Trainer
