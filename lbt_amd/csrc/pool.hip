@@ -127,18 +127,23 @@ __global__ __launch_bounds__(kT) void maxpool_fwd4_kernel(const float* __restric
 // it, i.e. where it is that window's maximum, and then relu(x) = y[o] (the pool input is the ReLU
 // output), so x > 0 <=> y[o] > 0 -- the mask costs one 16-byte load per window instead of a pass
 // over the ReLU input, and dx is the exact value relu_bwd(maxpool_bwd(g)) stores (sum or +0).
+// IT: the index type of the element -> (n, ih, iw, c) decomposition -- uint32_t when the tensor has < 2^31
+// elements (ResNet-50's pool: 205 M), whose divisions are a few VALU ops where int64's are a software
+// routine per division (three per thread); the same indices, so the same sums.
+template <typename IT>
 __global__ __launch_bounds__(kT) void maxpool_bwd4_kernel(const float* __restrict__ g, const uint8_t* __restrict__ amax,
                                                           const float* __restrict__ ymask, float* __restrict__ dx,
                                                           lbt_conv_desc d) {
   const int64_t e4 = ((int64_t)blockIdx.x * kT + threadIdx.x) * 4;
   const int64_t total = (int64_t)d.N * d.H * d.W * d.Cin;
   if (e4 >= total) return;
-  const int c = (int)(e4 % d.Cin);
-  int64_t m = e4 / d.Cin;
-  const int iw = (int)(m % d.W);
-  m /= d.W;
-  const int ih = (int)(m % d.H);
-  const int n = (int)(m / d.H);
+  const IT ei = (IT)e4;
+  const int c = (int)(ei % (IT)d.Cin);
+  IT m = ei / (IT)d.Cin;
+  const int iw = (int)(m % (IT)d.W);
+  m /= (IT)d.W;
+  const int ih = (int)(m % (IT)d.H);
+  const int n = (int)(m / (IT)d.H);
   const int ylo = ih + d.PT - d.KH + 1, yhi = ih + d.PT;
   const int xlo = iw + d.PL - d.KW + 1, xhi = iw + d.PL;
   int oh0 = ylo <= 0 ? 0 : (ylo + d.SH - 1) / d.SH, oh1 = yhi < 0 ? -1 : yhi / d.SH;
@@ -160,6 +165,15 @@ __global__ __launch_bounds__(kT) void maxpool_bwd4_kernel(const float* __restric
       if ((int)a.w == pos && yv.w > 0.f) s[3] = s[3] + gv.w;
     }
   *reinterpret_cast<float4*>(dx + e4) = make_float4(s[0], s[1], s[2], s[3]);
+}
+
+void launch_bwd4(const float* g, const uint8_t* amax, const float* y, float* dx, const lbt_conv_desc& d, int64_t n,
+                 hipStream_t st) {
+  const dim3 grid((unsigned)((n / 4 + kT - 1) / kT));
+  if (n < ((int64_t)1 << 31))
+    hipLaunchKernelGGL(maxpool_bwd4_kernel<uint32_t>, grid, dim3(kT), 0, st, g, amax, y, dx, d);
+  else
+    hipLaunchKernelGGL(maxpool_bwd4_kernel<int64_t>, grid, dim3(kT), 0, st, g, amax, y, dx, d);
 }
 
 bool pool_desc_ok(const lbt_conv_desc& d) {
@@ -190,8 +204,7 @@ extern "C" int lbt_maxpool_bwd(const float* g, const uint8_t* amax, float* dx, l
     return LBT_EINVAL;
   const int64_t n = (int64_t)d.N * d.H * d.W * d.Cin;
   if (d.Cin % 4 == 0)
-    hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
-                       g, amax, nullptr, dx, d);
+    launch_bwd4(g, amax, nullptr, dx, d, n, (hipStream_t)stream);
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream, g,
                        amax, dx, d);
@@ -215,8 +228,7 @@ extern "C" int lbt_maxpool_relu_bwd(const float* g, const uint8_t* amax, const f
                                     void* stream) {
   if (!pool_desc_ok(d) || d.Cin % 4) return LBT_EINVAL;
   const int64_t n = (int64_t)d.N * d.H * d.W * d.Cin;
-  hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3((unsigned)((n / 4 + kT - 1) / kT)), dim3(kT), 0, (hipStream_t)stream,
-                     g, amax, y, dx, d);
+  launch_bwd4(g, amax, y, dx, d, n, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
 
